@@ -1,0 +1,259 @@
+"""Generate golden vectors from the REFERENCE implementation (run only in the build container).
+
+The reference scripts cannot be imported (module top level imports mmsdk / tensorboard, reads
+/home/... and starts training -- SURVEY.md F8), so this script parses each script with ``ast``
+and executes only its class / function definitions and UPPERCASE constants, with ``device`` =
+cpu and the constant overrides each case names.  It then runs the reference classes on seeded
+inputs (tests/golden/specs.py) exactly as the reference ``train`` functions do -- forward, loss,
+backward, ``clip_grad_norm_``, ``optim.AdamW`` / ``optim.Adam`` step -- and saves the outputs
+(never the reference source) as ``tests/golden/<case>.npz``.
+
+    python tests/golden/make_golden.py            # all cases
+    python tests/golden/make_golden.py cmu_small  # one case
+
+Fixture layout: ``meta`` (JSON: family, constants, ctor kwargs, batch spec, param shapes),
+``logits``, ``loss``, ``gnorm`` (pre-clip global norm), ``grad/<key>`` (full grads, small cases)
+or ``gradnorm/<key>`` + ``gradhead/<key>`` (first 256 entries, large cases), ``post/<key>`` /
+``posthead/<key>`` (parameters after one optimizer step), ``logits2`` (forward after the step),
+and block cases' ``out``, ``scores`` and input grads.
+"""
+import ast
+import json
+import math
+import os
+import sys
+
+import numpy as np
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+import torch.optim as optim
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+import specs  # noqa: E402
+
+REF = '/root/reference'
+SCRIPTS = {'cmu': 'cmu-mosei/run.py', 'realformer': 'others/realformer.py', 'ren': 'Ren-MME/run.py'}
+
+
+def load_reference(family, overrides):
+    path = os.path.join(REF, SCRIPTS[family])
+    tree = ast.parse(open(path).read())
+    ns = {'torch': torch, 'nn': nn, 'F': F, 'np': np, 'math': math, 'optim': optim,
+          'device': torch.device('cpu')}
+    consts = [n for n in tree.body if isinstance(n, ast.Assign)
+              and all(isinstance(t, ast.Name) and t.id.isupper() for t in n.targets)]
+    defs = [n for n in tree.body if isinstance(n, (ast.ClassDef, ast.FunctionDef))]
+    exec(compile(ast.Module(body=consts, type_ignores=[]), path, 'exec'), ns)
+    ns.update(overrides)
+    exec(compile(ast.Module(body=defs, type_ignores=[]), path, 'exec'), ns)
+    return ns
+
+
+def set_params(model, seed):
+    shapes = {k: list(v.shape) for k, v in model.state_dict().items()}
+    vals = specs.param_values(shapes, seed)
+    model.load_state_dict({k: torch.from_numpy(v) for k, v in vals.items()})
+    return shapes
+
+
+def t(x):
+    return torch.from_numpy(np.ascontiguousarray(x))
+
+
+def dump_params(out, model, prefix, full):
+    for k, p in model.named_parameters():
+        v = p.detach().numpy().reshape(-1)
+        if full:
+            out[prefix + '/' + k] = p.detach().numpy().copy()
+        else:
+            out[prefix + 'head/' + k] = v[:256].copy()
+
+
+def dump_grads(out, model, full):
+    for k, p in model.named_parameters():
+        if p.grad is None:
+            out['nograd/' + k] = np.zeros(0, np.float32)
+            continue
+        g = p.grad.detach().numpy()
+        if full:
+            out['grad/' + k] = g.copy()
+        else:
+            out['gradnorm/' + k] = np.float64(np.linalg.norm(g.astype(np.float64)))
+            out['gradhead/' + k] = g.reshape(-1)[:256].copy()
+
+
+# ----------------------------------------------------------------------------------- cases
+
+def case_model(name, family, consts, ctor, batch, full, seed, opt, steps=1):
+    """Whole-model train step(s) as the reference ``train`` performs them."""
+    ns = load_reference(family, consts)
+    torch.manual_seed(0)
+    if family == 'cmu':
+        model = ns['Concat_Trans'](**ctor)
+    elif family == 'ren':
+        model = ns['Base_model'](**ctor)
+    else:
+        model = ns['State_Transfer'](**ctor)
+    shapes = set_params(model, seed)
+    model.train()
+    if family == 'cmu':
+        l, v, a, lm, vm, am, labels = specs.cmu_batch(**batch)
+        args = [t(x) for x in (l, v, a, lm, vm, am)]
+        labels = t(labels)
+    elif family == 'ren':
+        inputs, labels = specs.ren_batch(**batch)
+        args = [t(x) for x in inputs]
+        labels = t(labels)
+    else:
+        l, v, a, labels, lm, vm, am, um = specs.realformer_batch(**batch)
+        args = [t(x) for x in (l, v, a, lm, vm, am)]
+        labels, um = t(labels), t(um)
+    if opt == 'adamw':
+        optimizer = optim.AdamW(model.parameters(), lr=1e-3)
+    else:
+        optimizer = optim.Adam(model.parameters(), lr=1e-3)
+    out = {}
+    for step in range(steps):
+        optimizer.zero_grad()
+        logits = model(*args)
+        if family == 'cmu':
+            loss = ns['multi_circle_loss'](logits, labels).mean()       # cmu-mosei/run.py:365-366
+        elif family == 'ren':
+            m_loss = ns['multi_loss'](logits, labels)                   # Ren-MME/run.py:331-334
+            kl_0 = F.kl_div(F.logsigmoid(logits[::2]), torch.sigmoid(logits[1::2]), reduction='batchmean')
+            kl_1 = F.kl_div(F.logsigmoid(logits[1::2]), torch.sigmoid(logits[::2]), reduction='batchmean')
+            loss = m_loss + (kl_0 + kl_1) / 2
+        else:
+            loss = (ns['multi_circle_loss'](logits, labels) * um).mean()  # realformer.py:311-312
+        loss.backward()
+        gnorm = nn.utils.clip_grad_norm_(model.parameters(), 1.0)
+        if step == 0:
+            out['logits'] = logits.detach().numpy()
+            out['loss'] = np.float64(loss.item())
+            out['gnorm'] = np.float64(gnorm.item())
+            # grads are post-clip here; store the clip coefficient so tests can undo it
+            out['clipcoef'] = np.float64(min(1.0, 1.0 / (gnorm.item() + 1e-6)))
+            dump_grads(out, model, full)
+        optimizer.step()
+    with torch.no_grad():
+        out['logits2'] = model(*args).numpy()
+    dump_params(out, model, 'post', full)
+    meta = dict(kind='model', family=family, consts=consts, ctor=ctor, batch=batch, seed=seed,
+                opt=opt, steps=steps, full=full, shapes=shapes)
+    return meta, out
+
+
+def case_block(name, family, consts, ctor, B, Tq, Tk, seed, with_prev=True, g_scores=True):
+    """Standalone Attention_Block forward/backward with residual scores and an upstream
+    gradient on both outputs (out, post-mask scores)."""
+    ns = load_reference(family, consts)
+    blk = ns['Attention_Block'](**ctor)
+    shapes = set_params(blk, seed)
+    D, H = ctor['dim'], ctor['n_heads']
+    q, kv, mask, s_prev, g_out = specs.block_inputs(seed + 1, B, Tq, Tk, D, H, with_prev)
+    qt, kvt = t(q).requires_grad_(), t(kv).requires_grad_()
+    sp = t(s_prev).requires_grad_() if with_prev else None
+    y, s = blk(qt, kvt, kvt, t(mask), sp)
+    obj = (y * t(g_out)).sum()
+    rng = np.random.default_rng(seed + 2)
+    g_s = (0.05 * rng.standard_normal(s.shape)).astype(np.float32)
+    if g_scores:
+        obj = obj + (s * t(g_s)).sum()
+    obj.backward()
+    out = {'out': y.detach().numpy(), 'scores': s.detach().numpy(), 'g_scores': g_s,
+           'grad_q': qt.grad.numpy(), 'grad_kv': kvt.grad.numpy()}
+    if with_prev:
+        out['grad_sprev'] = sp.grad.numpy()
+    dump_grads(out, blk, True)
+    meta = dict(kind='block', family=family, consts=consts, ctor=ctor, B=B, Tq=Tq, Tk=Tk,
+                seed=seed, with_prev=with_prev, g_scores=g_scores, shapes=shapes)
+    return meta, out
+
+
+def case_chain(name, consts, ctor, B, T, n_layers, seed):
+    """realformer "text chain" (BASELINE cfg2): Conv1d unify of l + position embedding +
+    ``n_layers`` residual blocks (multimodal_blocks[0..n_layers-1]); objective mean(out * G)."""
+    ns = load_reference('realformer', consts)
+    mc = ns['Multi_class'](**ctor)
+    shapes = set_params(mc, seed)
+    rng = np.random.default_rng(seed + 1)
+    lm = specs.masks_for(rng, (B,), T)
+    x = specs.features(rng, (B, T, consts['L_DIM']), lm)
+    G = rng.standard_normal((B, T, ctor['dim'])).astype(np.float32)
+    xt = t(x)
+    lt = mc.unify_dimension.linguistic(xt.transpose(1, 2)).transpose(1, 2)
+    lt = lt + mc.linguistic_position(lt)
+    h, s = lt, None
+    for i in range(n_layers):
+        h, s = mc.multimodal_blocks[i](h, lt, lt, t(lm), s)
+    obj = (h * t(G)).mean()
+    obj.backward()
+    out = {'out': h.detach().numpy(), 'obj': np.float64(obj.item())}
+    grads = {}
+    for k, p in mc.named_parameters():
+        if p.grad is not None:
+            grads['grad/' + k] = p.grad.numpy().copy()
+    out.update(grads)
+    meta = dict(kind='chain', family='realformer', consts=consts, ctor=ctor, B=B, T=T,
+                n_layers=n_layers, seed=seed, shapes=shapes)
+    return meta, out
+
+
+CMU_C = dict(L_DIM=300, V_DIM=35, A_DIM=74, DROP=0.0)
+REN_C = dict(L_DIM=768, V_DIM=640, A_DIM=205, DROP=0.0)
+
+
+def rf_consts(T, ffn=2):
+    return dict(L_DIM=300, V_DIM=35, A_DIM=74, DROP=0.0, FFN=ffn, L_LEN=T, V_LEN=T, A_LEN=T)
+
+
+def cmu_ctor(dim, heads, layers, T=50):
+    return dict(dim=dim, l_len=T, v_len=T, a_len=T, n_heads=heads, n_layers=layers, ffn=1)
+
+
+CASES = {
+    'cmu_small': lambda: case_model('cmu_small', 'cmu', CMU_C, cmu_ctor(32, 2, 1),
+                                    dict(seed=11, B=5, T=[7, 9, 12]), True, 101, 'adamw', 2),
+    'cmu_small_l2': lambda: case_model('cmu_small_l2', 'cmu', CMU_C, cmu_ctor(32, 2, 2),
+                                       dict(seed=12, B=4, T=[6, 10, 8]), True, 102, 'adamw'),
+    'cmu_cfg1': lambda: case_model('cmu_cfg1', 'cmu', CMU_C, cmu_ctor(96, 6, 1),
+                                   dict(seed=13, B=8, T=50), False, 103, 'adamw'),
+    'ren_small': lambda: case_model('ren_small', 'ren', REN_C, dict(dim=32, l_len=5, v_len=6, a_len=8,
+                                    n_heads=2, n_layers=1, ffn=1),
+                                    dict(seed=14, pairs=3, T=[5, 6, 8]), True, 104, 'adamw'),
+    'ren_full': lambda: case_model('ren_full', 'ren', REN_C, dict(dim=128, l_len=40, v_len=76, a_len=96,
+                                   n_heads=8, n_layers=1, ffn=1),
+                                   dict(seed=15, pairs=2, T=[40, 76, 96]), False, 105, 'adamw'),
+    'rf_state_small': lambda: case_model('rf_state_small', 'realformer', rf_consts(6),
+                                         dict(l_dim=300, v_dim=35, a_dim=74, dim=32, l_len=6, v_len=6,
+                                              a_len=6, n_heads=2, n_layers=2, ffn=2),
+                                         dict(seed=16, B=3, P=3, T=6), True, 106, 'adam'),
+    'block_cmu': lambda: case_block('block_cmu', 'cmu', CMU_C, dict(dim=32, n_heads=2, ffn=1),
+                                    3, 7, 11, 107),
+    'block_cmu_noprev': lambda: case_block('block_cmu_noprev', 'cmu', CMU_C, dict(dim=32, n_heads=2, ffn=1),
+                                           2, 9, 5, 108, with_prev=False, g_scores=False),
+    'block_rf': lambda: case_block('block_rf', 'realformer', rf_consts(8), dict(dim=32, n_heads=2),
+                                   3, 8, 10, 109),
+    'rf_chain_small': lambda: case_chain('rf_chain_small', rf_consts(10),
+                                         dict(l_dim=300, v_dim=35, a_dim=74, dim=32, l_len=10, v_len=10,
+                                              a_len=10, n_heads=2, n_layers=2, ffn=2), 4, 10, 2, 110),
+    'rf_chain_cfg2': lambda: case_chain('rf_chain_cfg2', rf_consts(50),
+                                        dict(l_dim=300, v_dim=35, a_dim=74, dim=96, l_len=50, v_len=50,
+                                             a_len=50, n_heads=6, n_layers=2, ffn=2), 8, 50, 2, 111),
+}
+
+
+def main(names):
+    torch.set_num_threads(min(8, os.cpu_count() or 1))
+    for name in names:
+        meta, out = CASES[name]()
+        out['meta'] = np.array(json.dumps(meta))
+        path = os.path.join(HERE, name + '.npz')
+        np.savez_compressed(path, **out)
+        print('wrote', path, os.path.getsize(path), 'bytes')
+
+
+if __name__ == '__main__':
+    main(sys.argv[1:] or list(CASES))

@@ -1,0 +1,70 @@
+"""Pin the CPU oracle against the golden vectors produced by the reference's own classes
+(tests/golden/make_golden.py).  CPU only."""
+import numpy as np
+import pytest
+import torch
+
+from tests import oracle_runner
+from tests.golden import fixtures
+
+RTOL, ATOL = 2e-5, 2e-6
+
+
+def close(a, b, rtol=RTOL, atol=ATOL):
+    a = a.detach().numpy() if torch.is_tensor(a) else np.asarray(a)
+    np.testing.assert_allclose(a, np.asarray(b), rtol=rtol, atol=atol)
+
+
+@pytest.mark.parametrize('name', fixtures.names('model'))
+def test_model_step(name):
+    meta, gold = fixtures.load(name)
+    out = oracle_runner.run_model_case(meta)
+    close(out['logits'], gold['logits'])
+    close(out['loss'], gold['loss'])
+    close(out['gnorm'], gold['gnorm'], rtol=1e-5)
+    for k, g in out['grads'].items():
+        if 'nograd/' + k in gold:
+            assert g is None, k
+            continue
+        if meta['full']:
+            close(g, gold['grad/' + k], rtol=1e-4, atol=1e-6)
+        else:
+            close(torch.linalg.vector_norm(g.double()), gold['gradnorm/' + k], rtol=1e-4, atol=1e-7)
+            close(g.reshape(-1)[:256], gold['gradhead/' + k], rtol=1e-4, atol=1e-6)
+    for k, p in out['post'].items():
+        ref = gold['post/' + k] if meta['full'] else gold['posthead/' + k]
+        close(p if meta["full"] else p.reshape(-1)[:256], ref, rtol=1e-5, atol=2e-5)  # Adam: |update| <= lr; grads ~eps amplify rounding
+    close(out['logits2'], gold['logits2'], rtol=1e-4, atol=1e-5)
+
+
+@pytest.mark.parametrize('name', fixtures.names('block'))
+def test_block(name):
+    meta, gold = fixtures.load(name)
+    P, (qt, kvt, sp), y, s = oracle_runner.run_block_case(meta)
+    close(y, gold['out'])
+    close(s, gold['scores'], rtol=1e-6, atol=1e-4)
+    _, _, _, _, g_out = fixtures.block_inputs(meta)
+    obj = (y * torch.tensor(g_out)).sum()
+    if meta['g_scores']:
+        obj = obj + (s * torch.tensor(gold['g_scores'])).sum()
+    obj.backward()
+    close(qt.grad, gold['grad_q'], rtol=1e-4, atol=1e-5)
+    close(kvt.grad, gold['grad_kv'], rtol=1e-4, atol=1e-5)
+    if sp is not None:
+        close(sp.grad, gold['grad_sprev'], rtol=1e-4, atol=1e-6)
+    for k, p in P.items():
+        if 'nograd/' + k in gold:
+            assert p.grad is None
+        else:
+            close(p.grad, gold['grad/' + k], rtol=1e-4, atol=1e-5)
+
+
+@pytest.mark.parametrize('name', fixtures.names('chain'))
+def test_chain(name):
+    meta, gold = fixtures.load(name)
+    P, h, obj = oracle_runner.run_chain_case(meta)
+    close(h, gold['out'])
+    close(obj, gold['obj'], rtol=1e-5)
+    for k, p in P.items():
+        if 'grad/' + k in gold:
+            close(p.grad, gold['grad/' + k], rtol=1e-4, atol=1e-6)
