@@ -1,0 +1,269 @@
+/*
+ * mep.h -- C ABI of libmep_hip.so, the MI355X (gfx950) kernels of the tri-modal
+ * residual-attention training path (youngzhou97qz/Multimodal-emotion-processing).
+ *
+ * The reference has no FFI: its hot path is PyTorch ATen called from the model classes in
+ * cmu-mosei/run.py, Ren-MME/run.py and others/realformer.py.  Each entry point below replaces
+ * the ATen ops of one reference function (file:line cited per entry).
+ *
+ * Conventions
+ *   - Every pointer is a DEVICE pointer owned by the caller (PyTorch caching allocator).  The
+ *     library never allocates; workspaces are passed in.  Descriptor arrays live in device
+ *     memory too (built once per plan, so a captured hipGraph replays them unchanged).
+ *   - All arithmetic is fp32 (the reference has no AMP).  Layouts are row-major.
+ *   - Launches are asynchronous on `stream`; no host synchronisation, no allocation, so every
+ *     call may be captured into a hipGraph.
+ *   - Return 0 on success or a negative code (-(int)hipError_t, or MEP_EINVAL); the text of the
+ *     last error of the calling thread is available from mep_last_error().
+ *
+ * Row views ("mep_rows"): a token-indexed 2-D view.  Row `tok` (0 <= tok < B*T) of the view
+ * starts at  ptr + (tok / T) * sB + (tok % T) * sT  (in floats); columns are contiguous.  This
+ * addresses slot-strided inputs ([B,2,T,d] slices), strided concatenation slices and plain
+ * contiguous [B*T, d] buffers with one descriptor.
+ */
+#ifndef MEP_H_
+#define MEP_H_
+
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MEP_EINVAL (-1000)
+#define MEP_ABI_VERSION 1
+
+typedef void* mep_stream_t; /* a hipStream_t */
+
+typedef struct {
+    uint64_t ptr;   /* float* base                                  */
+    int64_t  sB;    /* stride (floats) between consecutive batch rows */
+    int64_t  sT;    /* stride (floats) between consecutive time steps */
+    int32_t  T;     /* time steps per batch row                      */
+    int32_t  _pad;
+} mep_rows;
+
+/* ---------------------------------------------------------------- token GEMM (MFMA f32)
+ * Y[tok, n] = act( alpha * sum_k X[tok, k] * W(n, k) + bias[n] + table[tok % T, n] ) (+ Y if accumulate)
+ * W(n,k) = W[n*ldw + k] when w_nt (nn.Linear weight, used by forward), else W[k*ldw + n]
+ * (backward dX = dY W).  Replaces the bias-free nn.Linear of Unify_Dimension
+ * (cmu-mosei/run.py:210-214, Ren-MME/run.py:161-166), the k=1 Conv1d unify + position
+ * embedding (others/realformer.py:136-152,224-227) and the realformer w_qkv / FFN Linears
+ * (others/realformer.py:157,163-168,188). */
+typedef struct {
+    mep_rows x;        /* A operand rows, K columns                      */
+    mep_rows y;        /* output rows, N columns                         */
+    uint64_t w;        /* weight                                          */
+    uint64_t bias;     /* [N] or 0                                        */
+    uint64_t table;    /* [T, N] row table added by (tok % y.T) or 0      */
+    int32_t  ntok, N, K, ldw;
+    int32_t  w_nt;     /* 1: W[n][k] (Linear weight); 0: W[k][n]          */
+    int32_t  accumulate;
+    int32_t  relu;
+    float    alpha;
+} mep_gemm_desc;
+int mep_gemm(const mep_gemm_desc* descs, int n_desc, int max_tiles, mep_stream_t stream);
+
+/* ---------------------------------------------------------------- weight-gradient GEMM
+ * partial[split, n, k] = sum_{tok in split} A[tok, n] * Bm[tok, k]   (dW = dY^T X)
+ * then out[n*ldo + k] (+)= sum_split partial.  Replaces autograd's weight-gradient mm of every
+ * nn.Linear on the path.  `tok_per_split` tokens per split; partial is a workspace of
+ * n_split*N*K floats. */
+typedef struct {
+    mep_rows a;        /* [ntok, N]  (dY)                 */
+    mep_rows b;        /* [ntok, K]  (X)                  */
+    uint64_t partial;  /* workspace [n_split][N][K]       */
+    uint64_t out;      /* [N][ldo] gradient               */
+    int32_t  ntok, N, K, ldo;
+    int32_t  tok_per_split, n_split;
+    int32_t  accumulate;
+    int32_t  _pad;
+} mep_wgrad_desc;
+int mep_wgrad(const mep_wgrad_desc* descs, int n_desc, int max_tiles, mep_stream_t stream);
+int mep_wgrad_reduce(const mep_wgrad_desc* descs, int n_desc, int max_tiles, mep_stream_t stream);
+
+/* ---------------------------------------------------------------- residual attention core
+ * Per (batch row b, head h, query row i):
+ *   s_ik = (q_i . k_k) / sqrt(hd)  [+ c * S_prev[b,h,i,k]]  - 1e8 * (1 - mask[b,k])
+ *   P = softmax_k(s);  X[b,i,h*hd:(h+1)*hd] = sum_k P_ik v_k
+ * cmu-mosei/run.py:236-256 (== Ren-MME/run.py:188-208, realformer.py:182-204 after w_qkv).
+ * hd = 16.  S_out (post-mask scores, needed by a following residual layer, F7) is optional.
+ * Row statistics rowmax / 1/rowsum are saved for the backward. */
+typedef struct {
+    mep_rows q, k, v;   /* [B*Tq, D], [B*Tk, D], [B*Tk, D]  (k may equal v)   */
+    mep_rows x;         /* out [B*Tq, D]                                        */
+    uint64_t mask;      /* key mask: mask[b*mask_sB + k]                        */
+    int64_t  mask_sB;
+    uint64_t s_prev;    /* [B,H,Tq,Tk] or 0                                     */
+    uint64_t c;         /* residual coefficient (device float*), used iff s_prev */
+    uint64_t s_out;     /* [B,H,Tq,Tk] or 0                                     */
+    uint64_t stats;     /* [B,H,Tq,2]: row max, 1/row sum                       */
+    int32_t  B, H, Tq, Tk;
+} mep_attn_desc;
+int mep_attn_fwd(const mep_attn_desc* descs, int n_desc, int max_tiles, mep_stream_t stream);
+
+/* Backward of the attention core.  Inputs dx (grad of X), the forward's q/k/v/x/stats/s_prev.
+ * Outputs: dq += (written with accumulate semantics onto dq_base), dk, dv (dk==dv pointer ->
+ * summed, for k is v), ds_prev = c * dS (grad of S_prev) and a per-workgroup partial of
+ * dc = sum dS * S_prev.  ds_next: gradient arriving on this layer's S output (c_next * dS_next)
+ * or 0. */
+typedef struct {
+    mep_attn_desc f;
+    mep_rows dx;
+    mep_rows dq;        /* accumulated into                       */
+    mep_rows dk, dv;    /* written (summed when dk.ptr == dv.ptr)  */
+    uint64_t ds_next;   /* [B,H,Tq,Tk] or 0                        */
+    uint64_t ds_prev;   /* [B,H,Tq,Tk] or 0                        */
+    uint64_t dc_partial;/* [B * ceil(Tk/64)] floats or 0           */
+} mep_attn_bwd_desc;
+int mep_attn_bwd(const mep_attn_bwd_desc* descs, int n_desc, int max_tiles, mep_stream_t stream);
+
+/* ---------------------------------------------------------------- cmu / Ren-MME block epilogue
+ * xp = drop(x @ Wp^T);  z = [q | xp] @ Wm^T;  out = drop(LayerNorm(z))
+ * cmu-mosei/run.py:257-261 (proj, cat, minus, norm1), Ren-MME/run.py:209-213 (norm2, dropout).
+ * D in {32, 64, 96, 128}.  Saves xp (post-dropout), z and (mean, rstd) for the backward. */
+typedef struct {
+    mep_rows q, x, xp, z, out;
+    uint64_t wp, wm, ln_w, ln_b;
+    uint64_t stats;      /* [ntok][2] */
+    uint64_t seed;       /* device uint64* dropout seed (0: no dropout) */
+    int32_t  ntok, D;
+    float    drop_p;
+    int32_t  drop_stream;/* distinct per block */
+} mep_epi_desc;
+int mep_block_epi_fwd(const mep_epi_desc* descs, int n_desc, int max_tiles, mep_stream_t stream);
+
+/* Backward: dout -> (dropout) -> LN backward -> dz;  dq_direct = dz Wm[:, :D];
+ * dxp = drop'(dz Wm[:, D:]);  dx = dxp Wp.  Writes dz, dxp, dx, dq and per-tile LayerNorm
+ * parameter-gradient partials ln_partial[tile][2][D]. */
+typedef struct {
+    mep_epi_desc f;
+    mep_rows dout;
+    mep_rows dout2;      /* optional second upstream gradient (ptr 0: none), e.g. the next
+                            layer's dq for residual chains */
+    mep_rows dz, dxp, dx, dq;
+    uint64_t ln_partial;
+    int32_t  dq_accumulate;
+    int32_t  _pad;
+} mep_epi_bwd_desc;
+int mep_block_epi_bwd(const mep_epi_bwd_desc* descs, int n_desc, int max_tiles, mep_stream_t stream);
+
+/* ---------------------------------------------------------------- row LayerNorm (D <= 256)
+ * Ren-MME's shared unify LayerNorm (Ren-MME/run.py:164-166).  fwd: y = LN(x); bwd: dx from dy,
+ * per-tile partial dgamma/dbeta. */
+typedef struct {
+    mep_rows x, y, dy, dx;
+    uint64_t w, b, stats, partial;
+    int32_t  ntok, D;
+    int32_t  dx_accumulate;
+    int32_t  _pad;
+} mep_ln_desc;
+int mep_layernorm_fwd(const mep_ln_desc* descs, int n_desc, int max_tiles, mep_stream_t stream);
+int mep_layernorm_bwd(const mep_ln_desc* descs, int n_desc, int max_tiles, mep_stream_t stream);
+
+/* ---------------------------------------------------------------- reductions
+ * Column sums over tiles: out[c] (+)= sum_t partial[t*ld + c].  Used for LayerNorm / bias /
+ * position-embedding / per-row head gradient partials. */
+typedef struct {
+    uint64_t partial, out;
+    int32_t  n_rows, n_cols, ld, accumulate;
+} mep_colsum_desc;
+int mep_colsum(const mep_colsum_desc* descs, int n_desc, int max_tiles, mep_stream_t stream);
+
+/* out = sum_i src_i (up to 16 sources), elementwise over ntok x D rows. */
+#define MEP_SUM_MAX_SRC 16
+typedef struct {
+    mep_rows src[MEP_SUM_MAX_SRC];
+    mep_rows out;
+    int32_t  n_src, ntok, D, accumulate;
+} mep_sum_desc;
+int mep_sum_rows(const mep_sum_desc* descs, int n_desc, int max_tiles, mep_stream_t stream);
+
+/* ---------------------------------------------------------------- mean+max pooling
+ * pooled[b, 0:C] = mean_t x[b,t,:], pooled[b, C:2C] = max_t x[b,t,:] (first index on ties),
+ * cmu-mosei/run.py:314-318, realformer.py:258-262.  bwd: dx = dmean/T + onehot(argmax)*dmax. */
+typedef struct {
+    uint64_t x, dx;       /* [B, T, C] contiguous          */
+    uint64_t pooled, dpooled; /* [B, 2C]                   */
+    uint64_t argmax;      /* int32 [B, C]                  */
+    int32_t  B, T, C, _pad;
+} mep_pool_desc;
+int mep_pool_fwd(const mep_pool_desc* descs, int n_desc, int max_tiles, mep_stream_t stream);
+int mep_pool_bwd(const mep_pool_desc* descs, int n_desc, int max_tiles, mep_stream_t stream);
+
+/* ---------------------------------------------------------------- fusion head + loss
+ * cmu-mosei Concat_Trans head (cmu-mosei/run.py:319,330-339) / Ren-MME Base_model head
+ * (Ren-MME/run.py:271,283-292), fused with multi_circle_loss (cmu-mosei/run.py:342-351) and its
+ * .mean() (run.py:366) / multi_loss + R-Drop KL (Ren-MME/run.py:295-304,331-334):
+ *   last = Wc0 p0, this = Wc1 p1 (classifier, no bias); y = einsum(this,last,trans);
+ *   logits = Wo [this | LN(y)] + bo;  loss = mean_b circle(logits_b, labels_b) (+ KL).
+ * One workgroup per row (per row pair with R-Drop).  Writes logits, per-row losses, dpooled
+ * (grad of both pooled inputs, scaled for the batch mean) and per-row parameter-gradient
+ * partials (layout in head_partial_layout()).  compute_grad = 0 runs forward + loss only. */
+typedef struct {
+    uint64_t pooled0, pooled1;   /* [B, F]                              */
+    uint64_t dpooled0, dpooled1; /* [B, F]                              */
+    uint64_t wc0, wc1;           /* [NC, F]                             */
+    uint64_t trans;              /* [NC, NC, NC]                        */
+    uint64_t ln_w, ln_b;         /* [NC]                                */
+    uint64_t wo, bo;             /* [NC, 2NC], [NC]                     */
+    uint64_t labels;             /* [B, NC] (int64 or float32)          */
+    uint64_t logits;             /* [B, NC]                             */
+    uint64_t row_loss;           /* [B]                                 */
+    uint64_t partial;            /* [B][head_partial_stride]            */
+    int32_t  B, F, NC;
+    int32_t  labels_are_float;
+    int32_t  rdrop;              /* Ren-MME R-Drop pairs (2i, 2i+1)     */
+    int32_t  compute_grad;
+    float    loss_scale;         /* d(total loss)/d(row loss) = 1/B     */
+    int32_t  _pad;
+    uint64_t ext_dlogits;        /* [B, NC] upstream grad of the logits; when set the fused
+                                    loss is skipped and this gradient is back-propagated */
+} mep_head_desc;
+int mep_head_fwd_bwd(const mep_head_desc* d, mep_stream_t stream);
+/* Reduce the per-row partials into the gradient buffers and the batch-mean loss:
+ * g_trans, g_ln_w, g_ln_b, g_wo, g_bo (each [.] floats), g_wc0/g_wc1 = dlogit^T pooled, loss[1]. */
+int mep_head_reduce(const mep_head_desc* d, uint64_t g_trans, uint64_t g_ln_w, uint64_t g_ln_b,
+                    uint64_t g_wo, uint64_t g_bo, uint64_t g_wc0, uint64_t g_wc1, uint64_t loss,
+                    mep_stream_t stream);
+int mep_head_partial_stride(int NC);
+
+/* multi_circle_loss per row (cmu-mosei/run.py:342-351) as a standalone op for callers that
+ * compute the loss outside the model: row_loss[b] and dunit[b, :] = d row_loss[b] / d logits[b, :].
+ * mep_circle_loss_bwd: dlogits[b, n] = grad_rows[b] * dunit[b, n]. */
+int mep_circle_loss_fwd(const float* logits, const void* labels, int labels_are_float, int B, int NC,
+                        float* row_loss, float* dunit, mep_stream_t stream);
+int mep_circle_loss_bwd(const float* dunit, const float* grad_rows, int B, int NC, float* dlogits,
+                        mep_stream_t stream);
+
+/* ---------------------------------------------------------------- optimizer
+ * clip_grad_norm_(max_norm) (cmu-mosei/run.py:368) + AdamW / Adam step (run.py:369,398;
+ * realformer.py:342) over a flat fp32 parameter buffer.  `segs` (host array, <= 16) lists
+ * [offset, length) ranges of parameters that HAVE a gradient this step; torch skips grad-None
+ * parameters entirely (no decay, no state update) and so does this.  Device-side state so a
+ * captured graph replays correctly: hyper = float[7] {lr, beta1, beta2, eps, weight_decay,
+ * max_norm, grad_scale (0 = 1; 1/world after a SUM all-reduce)}; step = int[1] (incremented by the call, then used as the 1-based step t).
+ * partial: workspace of >= 1024 floats.  decoupled = 1: AdamW; 0: Adam (L2 decay in the grad).
+ * gnorm_out (device float*, may be 0) receives the pre-clip global norm.  Grads are clipped in
+ * place, as clip_grad_norm_ does. */
+typedef struct {
+    int64_t offset, length;
+} mep_seg;
+int mep_clip_adam(float* params, float* grads, float* exp_avg, float* exp_avg_sq,
+                  const mep_seg* segs, int n_seg, int64_t total_len, float* partial,
+                  float* gnorm_out, const float* hyper, int* step, int decoupled,
+                  mep_stream_t stream);
+
+/* advance the device-side dropout seed (graph-replay safe) */
+int mep_seed_advance(uint64_t* seed, mep_stream_t stream);
+
+/* ---------------------------------------------------------------- misc */
+int mep_abi_version(void);
+int mep_last_error(char* buf, size_t len);
+int mep_device_sync(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MEP_H_ */

@@ -1,0 +1,193 @@
+"""ctypes binding of libmep_hip.so (include/mep.h).
+
+The library is the product: there is no CPU or PyTorch fallback.  ``lib()`` raises if the
+shared object is missing or cannot be loaded, and every launcher's return code is checked.
+The ctypes structures below mirror include/mep.h field for field; tests/test_abi.py compiles a
+C probe of the header with gcc and checks sizes and offsets against them.
+"""
+import ctypes
+import os
+
+import torch
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(PKG_DIR, 'libmep_hip.so')
+
+u64, i64, i32, f32 = ctypes.c_uint64, ctypes.c_int64, ctypes.c_int32, ctypes.c_float
+
+
+class Rows(ctypes.Structure):
+    _fields_ = [('ptr', u64), ('sB', i64), ('sT', i64), ('T', i32), ('_pad', i32)]
+
+
+class GemmDesc(ctypes.Structure):
+    _fields_ = [('x', Rows), ('y', Rows), ('w', u64), ('bias', u64), ('table', u64),
+                ('ntok', i32), ('N', i32), ('K', i32), ('ldw', i32), ('w_nt', i32),
+                ('accumulate', i32), ('relu', i32), ('alpha', f32)]
+
+
+class WgradDesc(ctypes.Structure):
+    _fields_ = [('a', Rows), ('b', Rows), ('partial', u64), ('out', u64),
+                ('ntok', i32), ('N', i32), ('K', i32), ('ldo', i32),
+                ('tok_per_split', i32), ('n_split', i32), ('accumulate', i32), ('_pad', i32)]
+
+
+class AttnDesc(ctypes.Structure):
+    _fields_ = [('q', Rows), ('k', Rows), ('v', Rows), ('x', Rows), ('mask', u64), ('mask_sB', i64),
+                ('s_prev', u64), ('c', u64), ('s_out', u64), ('stats', u64),
+                ('B', i32), ('H', i32), ('Tq', i32), ('Tk', i32)]
+
+
+class AttnBwdDesc(ctypes.Structure):
+    _fields_ = [('f', AttnDesc), ('dx', Rows), ('dq', Rows), ('dk', Rows), ('dv', Rows),
+                ('ds_next', u64), ('ds_prev', u64), ('dc_partial', u64)]
+
+
+class EpiDesc(ctypes.Structure):
+    _fields_ = [('q', Rows), ('x', Rows), ('xp', Rows), ('z', Rows), ('out', Rows),
+                ('wp', u64), ('wm', u64), ('ln_w', u64), ('ln_b', u64), ('stats', u64), ('seed', u64),
+                ('ntok', i32), ('D', i32), ('drop_p', f32), ('drop_stream', i32)]
+
+
+class EpiBwdDesc(ctypes.Structure):
+    _fields_ = [('f', EpiDesc), ('dout', Rows), ('dout2', Rows), ('dz', Rows), ('dxp', Rows), ('dx', Rows),
+                ('dq', Rows), ('ln_partial', u64), ('dq_accumulate', i32), ('_pad', i32)]
+
+
+class LnDesc(ctypes.Structure):
+    _fields_ = [('x', Rows), ('y', Rows), ('dy', Rows), ('dx', Rows), ('w', u64), ('b', u64),
+                ('stats', u64), ('partial', u64), ('ntok', i32), ('D', i32), ('dx_accumulate', i32),
+                ('_pad', i32)]
+
+
+class ColsumDesc(ctypes.Structure):
+    _fields_ = [('partial', u64), ('out', u64), ('n_rows', i32), ('n_cols', i32), ('ld', i32),
+                ('accumulate', i32)]
+
+
+SUM_MAX_SRC = 16
+
+
+class SumDesc(ctypes.Structure):
+    _fields_ = [('src', Rows * SUM_MAX_SRC), ('out', Rows), ('n_src', i32), ('ntok', i32), ('D', i32),
+                ('accumulate', i32)]
+
+
+class PoolDesc(ctypes.Structure):
+    _fields_ = [('x', u64), ('dx', u64), ('pooled', u64), ('dpooled', u64), ('argmax', u64),
+                ('B', i32), ('T', i32), ('C', i32), ('_pad', i32)]
+
+
+class HeadDesc(ctypes.Structure):
+    _fields_ = [('pooled0', u64), ('pooled1', u64), ('dpooled0', u64), ('dpooled1', u64), ('wc0', u64),
+                ('wc1', u64), ('trans', u64), ('ln_w', u64), ('ln_b', u64), ('wo', u64), ('bo', u64),
+                ('labels', u64), ('logits', u64), ('row_loss', u64), ('partial', u64),
+                ('B', i32), ('F', i32), ('NC', i32), ('labels_are_float', i32), ('rdrop', i32),
+                ('compute_grad', i32), ('loss_scale', f32), ('_pad', i32), ('ext_dlogits', u64)]
+
+
+class Seg(ctypes.Structure):
+    _fields_ = [('offset', i64), ('length', i64)]
+
+
+STRUCTS = {'mep_rows': Rows, 'mep_gemm_desc': GemmDesc, 'mep_wgrad_desc': WgradDesc,
+           'mep_attn_desc': AttnDesc, 'mep_attn_bwd_desc': AttnBwdDesc, 'mep_epi_desc': EpiDesc,
+           'mep_epi_bwd_desc': EpiBwdDesc, 'mep_ln_desc': LnDesc, 'mep_colsum_desc': ColsumDesc,
+           'mep_sum_desc': SumDesc, 'mep_pool_desc': PoolDesc, 'mep_head_desc': HeadDesc, 'mep_seg': Seg}
+
+P = ctypes.c_void_p
+# name -> argtypes (all return int)
+GROUPED = ['mep_gemm', 'mep_wgrad', 'mep_wgrad_reduce', 'mep_attn_fwd', 'mep_attn_bwd', 'mep_block_epi_fwd',
+           'mep_block_epi_bwd', 'mep_layernorm_fwd', 'mep_layernorm_bwd', 'mep_colsum', 'mep_sum_rows',
+           'mep_pool_fwd', 'mep_pool_bwd']
+SIGNATURES = {name: [P, i32, i32, P] for name in GROUPED}
+HP = ctypes.POINTER(HeadDesc)
+SIGNATURES.update({
+    'mep_head_fwd_bwd': [HP, P],
+    'mep_head_reduce': [HP, u64, u64, u64, u64, u64, u64, u64, u64, P],
+    'mep_head_partial_stride': [i32],
+    'mep_circle_loss_fwd': [P, P, i32, i32, i32, P, P, P],
+    'mep_circle_loss_bwd': [P, P, i32, i32, P, P],
+    'mep_clip_adam': [P, P, P, P, P, i32, i64, P, P, P, P, i32, P],
+    'mep_seed_advance': [P, P],
+    'mep_abi_version': [],
+    'mep_last_error': [ctypes.c_char_p, ctypes.c_size_t],
+    'mep_device_sync': [],
+})
+
+_LIB = None
+
+
+def lib():
+    """Load libmep_hip.so (raises OSError with a build hint if it is missing)."""
+    global _LIB
+    if _LIB is None:
+        if not os.path.exists(LIB_PATH):
+            raise OSError('libmep_hip.so not found at %s -- run __graft_entry__.build() '
+                          '(make -C multimodal-emotion-processing_amd/csrc)' % LIB_PATH)
+        L = ctypes.CDLL(LIB_PATH)
+        for name, args in SIGNATURES.items():
+            fn = getattr(L, name)
+            fn.argtypes = args
+            fn.restype = ctypes.c_int
+        _LIB = L
+    return _LIB
+
+
+def last_error():
+    buf = ctypes.create_string_buffer(512)
+    lib().mep_last_error(buf, 512)
+    return buf.value.decode(errors='replace')
+
+
+def check(rc, what=''):
+    if rc != 0:
+        raise RuntimeError('libmep_hip %s failed (%d): %s' % (what, rc, last_error()))
+
+
+def stream_ptr(stream=None):
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return ctypes.c_void_p(s.cuda_stream)
+
+
+# Optional per-launch timer (bench.py): an object with begin(name) / end(name) that records HIP
+# events on the launching stream.  None in normal operation.
+TIMER = None
+
+
+def call(name, *args, stream=None):
+    fn = getattr(lib(), name)
+    if TIMER is not None:
+        TIMER.begin(name)
+    check(fn(*args, stream_ptr(stream)), name)
+    if TIMER is not None:
+        TIMER.end(name)
+
+
+class DescArray:
+    """A device-resident array of descriptors (kept alive by the plan that owns it)."""
+
+    def __init__(self, struct, items, device):
+        self.n = len(items)
+        self.struct = struct
+        if self.n:
+            arr = (struct * self.n)(*items)
+            host = torch.frombuffer(bytearray(bytes(arr)), dtype=torch.uint8)
+            self.dev = host.to(device)
+        else:
+            self.dev = None
+
+    @property
+    def ptr(self):
+        return ctypes.c_void_p(self.dev.data_ptr() if self.dev is not None else 0)
+
+
+def launch(name, descs, max_tiles, stream=None):
+    if descs.n == 0 or max_tiles <= 0:
+        return
+    fn = getattr(lib(), name)
+    if TIMER is not None:
+        TIMER.begin(name)
+    check(fn(descs.ptr, descs.n, int(max_tiles), stream_ptr(stream)), name)
+    if TIMER is not None:
+        TIMER.end(name)

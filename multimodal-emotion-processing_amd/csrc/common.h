@@ -1,0 +1,139 @@
+// Device helpers shared by the gfx950 kernels of libmep_hip.so.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/mep.h"
+
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+
+#define MEP_DEV __device__ __forceinline__
+
+namespace mep {
+
+constexpr int kWave = 64;
+
+// ------------------------------------------------------------------ row views
+MEP_DEV int64_t row_off(const mep_rows& r, int tok) {
+    int b = tok / r.T;
+    int t = tok - b * r.T;
+    return (int64_t)b * r.sB + (int64_t)t * r.sT;
+}
+MEP_DEV float* row_ptr(const mep_rows& r, int tok) { return reinterpret_cast<float*>(r.ptr) + row_off(r, tok); }
+
+// ------------------------------------------------------------------ exact-rounding scalar ops
+// The residual-score sequence of the reference ((q.k)/sqrt(d) + c*S_prev - 1e8*(1-m)) is
+// evaluated with one rounding per op, no FMA contraction (masked slots sit at ~1e8 where
+// ulp = 8).
+MEP_DEV float add_rn(float a, float b) { return __fadd_rn(a, b); }
+MEP_DEV float sub_rn(float a, float b) { return __fsub_rn(a, b); }
+MEP_DEV float mul_rn(float a, float b) { return __fmul_rn(a, b); }
+
+// ------------------------------------------------------------------ wave reductions (64 lanes)
+MEP_DEV float wave_sum(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+MEP_DEV float wave_max(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+    return v;
+}
+
+// ------------------------------------------------------------------ counter-based dropout
+MEP_DEV uint64_t mix64(uint64_t x) {
+    x ^= x >> 30; x *= 0xBF58476D1CE4E5B9ull;
+    x ^= x >> 27; x *= 0x94D049BB133111EBull;
+    x ^= x >> 31;
+    return x;
+}
+// keep-scale for element `idx` of dropout stream `stream`: 0 (dropped) or 1/(1-p).
+MEP_DEV float drop_scale(uint64_t seed, uint32_t stream, uint64_t idx, float p) {
+    uint64_t h = mix64(seed ^ (0x9E3779B97F4A7C15ull * (uint64_t)(stream + 1)) ^ mix64(idx + 0x632BE59BD9B4E019ull));
+    float u = (float)(h >> 40) * (1.0f / 16777216.0f);
+    return u >= p ? 1.0f / (1.0f - p) : 0.0f;
+}
+
+// ------------------------------------------------------------------ f32 MFMA 32x32x2
+// lane l supplies A[l&31][k], B[k][l&31] with k = l>>5 of the 2-wide step; C/D register r of
+// lane l is C[(r&3) + 8*(r>>2) + 4*(l>>5)][l&31].
+MEP_DEV floatx16 mfma32(float a, float b, floatx16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+}
+MEP_DEV int acc_row(int r, int lane) { return (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5); }
+
+// acc += A_lds[m0 .. m0+31][0 .. kc) * W(n0 .. n0+31, k0 .. k0+kc)
+// A_lds: row-major [64][lda] tile in LDS, zero beyond the valid K range.
+// K is traversed in groups of 8: lane half h covers k = 8g + 4h + j at step 4g + j (the sum
+// over k is order-free; this lets each lane fetch 4 consecutive k with one 16-byte read).
+// W(n,k): NT -> W[n*ldw + k] (nn.Linear weight), else W[k*ldw + n].
+template <bool NT>
+MEP_DEV void mma_tile(floatx16& acc, const float* __restrict__ As, int lda, int m0,
+                      const float* __restrict__ W, int ldw, int n0, int N, int k0, int kc, int K,
+                      bool w_vec) {
+    const int lane = threadIdx.x & 63;
+    const int r = lane & 31;
+    const int h = lane >> 5;
+    const float* arow = As + (m0 + r) * lda + 4 * h;
+    const int n = n0 + r;
+    const bool nval = n < N;
+    for (int kk = 0; kk < kc; kk += 8) {
+        const float4 a = *reinterpret_cast<const float4*>(arow + kk);
+        const int kg = k0 + kk + 4 * h;
+        float b0 = 0.f, b1 = 0.f, b2 = 0.f, b3 = 0.f;
+        if (NT) {
+            const float* wp = W + (int64_t)n * ldw + kg;
+            if (nval && w_vec && kg + 3 < K) {
+                const float4 b = *reinterpret_cast<const float4*>(wp);
+                b0 = b.x; b1 = b.y; b2 = b.z; b3 = b.w;
+            } else if (nval) {
+                if (kg < K) b0 = wp[0];
+                if (kg + 1 < K) b1 = wp[1];
+                if (kg + 2 < K) b2 = wp[2];
+                if (kg + 3 < K) b3 = wp[3];
+            }
+        } else {
+            if (nval) {
+                const float* wp = W + (int64_t)kg * ldw + n;
+                if (kg < K) b0 = wp[0];
+                if (kg + 1 < K) b1 = wp[ldw];
+                if (kg + 2 < K) b2 = wp[2 * ldw];
+                if (kg + 3 < K) b3 = wp[3 * ldw];
+            }
+        }
+        acc = mfma32(a.x, b0, acc);
+        acc = mfma32(a.y, b1, acc);
+        acc = mfma32(a.z, b2, acc);
+        acc = mfma32(a.w, b3, acc);
+    }
+}
+
+MEP_DEV floatx16 zero16() {
+    floatx16 z;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) z[i] = 0.f;
+    return z;
+}
+
+// Cooperative load of rows [tok0, tok0+64) x cols [c0, c0+kc) of a row view into an LDS tile
+// [64][lda]; out-of-range rows/cols are zero.  kc_pad (multiple of 8) columns are written.
+MEP_DEV void load_tile(float* __restrict__ dst, int lda, const mep_rows& src, int tok0, int ntok,
+                       int c0, int kc, int kc_pad, int ncol_total) {
+    const int nth = blockDim.x;
+    for (int idx = threadIdx.x; idx < 64 * kc_pad; idx += nth) {
+        const int row = idx / kc_pad;
+        const int col = idx - row * kc_pad;
+        const int tok = tok0 + row;
+        const int c = c0 + col;
+        float v = 0.f;
+        if (tok < ntok && col < kc && c < ncol_total) v = row_ptr(src, tok)[c];
+        dst[row * lda + col] = v;
+    }
+}
+
+}  // namespace mep
+
+// error plumbing shared by the launchers (api.cpp)
+extern "C" void mep_set_error(const char* msg);
+int mep_check_launch(const char* what);

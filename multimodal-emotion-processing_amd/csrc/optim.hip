@@ -1,0 +1,175 @@
+// Reductions, clip_grad_norm_ + AdamW/Adam over the flat parameter buffer, dropout seed.
+//
+// clip + optimizer: cmu-mosei/run.py:368-369 (clip_grad_norm_(model.parameters(), CLIP),
+// optimizer.step()), AdamW(lr) at run.py:398, Adam(lr) at others/realformer.py:342.
+// Two launches: (1) per-workgroup partial sums of g^2 over the segments that have gradients;
+// (2) every workgroup re-reduces the partials in the same fixed order (deterministic, no
+// grid barrier), forms coef = min(1, max_norm / (||g|| + 1e-6)) and applies the torch update
+//   p *= 1 - lr*wd (AdamW);  m = lerp(m, g, 1-b1);  v = b2 v + (1-b2) g^2;
+//   p -= (lr / (1-b1^t)) * m / (sqrt(v) / sqrt(1-b2^t) + eps)
+// Hyper-parameters and the step counter live in device memory so a captured graph replays
+// with the current values.
+#include "common.h"
+
+using namespace mep;
+
+namespace {
+
+constexpr int NPART = 1024;
+constexpr int OPT_THREADS = 256;
+constexpr int MAX_SEG = 16;
+
+struct Segs {
+    int64_t off[MAX_SEG];
+    int64_t len[MAX_SEG];
+    int n;
+};
+
+__global__ __launch_bounds__(OPT_THREADS) void k_sqnorm(const float* __restrict__ g, Segs segs,
+                                                        float* __restrict__ partial, int* __restrict__ step) {
+    float s = 0.f;
+    const int64_t stride = (int64_t)gridDim.x * OPT_THREADS;
+    for (int si = 0; si < segs.n; ++si) {
+        const float* gs = g + segs.off[si];
+        for (int64_t i = (int64_t)blockIdx.x * OPT_THREADS + threadIdx.x; i < segs.len[si]; i += stride) {
+            const float v = gs[i];
+            s = fmaf(v, v, s);
+        }
+    }
+    __shared__ float red[OPT_THREADS / 64];
+    s = wave_sum(s);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        float t = 0.f;
+        for (int w = 0; w < OPT_THREADS / 64; ++w) t += red[w];
+        partial[blockIdx.x] = t;
+        if (blockIdx.x == 0 && step) step[0] += 1;
+    }
+}
+
+// hyper: [lr, beta1, beta2, eps, weight_decay, max_norm, grad_scale]
+__global__ __launch_bounds__(OPT_THREADS) void k_clip_adam(float* __restrict__ p, float* __restrict__ g,
+                                                           float* __restrict__ m, float* __restrict__ v, Segs segs,
+                                                           const float* __restrict__ partial, int npart,
+                                                           const float* __restrict__ hyper,
+                                                           const int* __restrict__ step, float* gnorm_out,
+                                                           int decoupled) {
+    __shared__ float red[OPT_THREADS];
+    float s = 0.f;
+    for (int i = threadIdx.x; i < npart; i += OPT_THREADS) s += partial[i];
+    red[threadIdx.x] = s;
+    __syncthreads();
+    for (int w = OPT_THREADS / 2; w > 0; w >>= 1) {
+        if (threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+        __syncthreads();
+    }
+    const float gscale = hyper[6] > 0.f ? hyper[6] : 1.0f;   // 1/world after a SUM all-reduce
+    const float total = sqrtf(red[0]) * gscale;
+    const float max_norm = hyper[5];
+    const float coef = fminf(max_norm / (total + 1e-6f), 1.0f);
+    if (blockIdx.x == 0 && threadIdx.x == 0 && gnorm_out) *gnorm_out = total;
+    const int t = step[0];
+    const double lr = hyper[0], b1 = hyper[1], b2 = hyper[2], wd = hyper[4];
+    const float eps = hyper[3];
+    const double bc1 = 1.0 - pow(b1, (double)t), bc2 = 1.0 - pow(b2, (double)t);
+    const float step_size = (float)(lr / bc1);
+    const float bc2_sqrt = (float)sqrt(bc2);
+    const float decay = (float)(1.0 - lr * wd);
+    const float one_m_b1 = (float)(1.0 - b1), fb2 = (float)b2, one_m_b2 = (float)(1.0 - b2);
+    const float fwd = (float)wd;
+    const int64_t stride = (int64_t)gridDim.x * OPT_THREADS;
+    for (int si = 0; si < segs.n; ++si) {
+        const int64_t off = segs.off[si];
+        for (int64_t i = (int64_t)blockIdx.x * OPT_THREADS + threadIdx.x; i < segs.len[si]; i += stride) {
+            const int64_t j = off + i;
+            float gv = g[j] * gscale * coef;
+            g[j] = gv;
+            float pv = p[j];
+            if (decoupled) pv *= decay;
+            else if (fwd != 0.f) gv = gv + pv * fwd;
+            float mv = m[j];
+            mv = mv + (gv - mv) * one_m_b1;
+            float vv = v[j] * fb2 + one_m_b2 * gv * gv;
+            const float denom = sqrtf(vv) / bc2_sqrt + eps;
+            pv = pv - step_size * mv / denom;
+            m[j] = mv;
+            v[j] = vv;
+            p[j] = pv;
+        }
+    }
+}
+
+__global__ void k_seed(uint64_t* seed) { seed[0] = mix64(seed[0] + 0x9E3779B97F4A7C15ull); }
+
+// ---------------------------------------------------------------- colsum / row sums
+__global__ __launch_bounds__(256) void k_colsum(const mep_colsum_desc* __restrict__ descs) {
+    const mep_colsum_desc& d = descs[blockIdx.y];
+    const int c = blockIdx.x * 256 + threadIdx.x;
+    if (c >= d.n_cols) return;
+    const float* p = reinterpret_cast<const float*>(d.partial) + c;
+    float s = 0.f;
+    for (int r = 0; r < d.n_rows; ++r) s += p[(int64_t)r * d.ld];
+    float* o = reinterpret_cast<float*>(d.out) + c;
+    *o = d.accumulate ? *o + s : s;
+}
+
+__global__ __launch_bounds__(256) void k_sum_rows(const mep_sum_desc* __restrict__ descs) {
+    const mep_sum_desc& d = descs[blockIdx.y];
+    const int64_t total = (int64_t)d.ntok * d.D;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+        const int tok = (int)(i / d.D), c = (int)(i - (int64_t)tok * d.D);
+        float s = 0.f;
+        for (int k = 0; k < d.n_src; ++k) s += row_ptr(d.src[k], tok)[c];
+        float* o = row_ptr(d.out, tok) + c;
+        *o = d.accumulate ? *o + s : s;
+    }
+}
+
+}  // namespace
+
+extern "C" int mep_clip_adam(float* params, float* grads, float* exp_avg, float* exp_avg_sq, const mep_seg* segs,
+                             int n_seg, int64_t total_len, float* partial, float* gnorm_out, const float* hyper,
+                             int* step, int decoupled, mep_stream_t stream) {
+    if (n_seg <= 0 || n_seg > MAX_SEG || !partial || !hyper || !step) {
+        mep_set_error("mep_clip_adam: need 1..16 segments, partial, hyper and step buffers");
+        return MEP_EINVAL;
+    }
+    Segs s;
+    s.n = n_seg;
+    int64_t longest = 0;
+    for (int i = 0; i < n_seg; ++i) {
+        s.off[i] = segs[i].offset;
+        s.len[i] = segs[i].length;
+        if (segs[i].offset < 0 || segs[i].offset + segs[i].length > total_len) {
+            mep_set_error("mep_clip_adam: segment out of range");
+            return MEP_EINVAL;
+        }
+        if (segs[i].length > longest) longest = segs[i].length;
+    }
+    int grid = (int)((longest + OPT_THREADS * 4 - 1) / (OPT_THREADS * 4));
+    grid = grid < 1 ? 1 : (grid > NPART ? NPART : grid);
+    hipLaunchKernelGGL(k_sqnorm, dim3(grid), dim3(OPT_THREADS), 0, (hipStream_t)stream, grads, s, partial, step);
+    int rc = mep_check_launch("mep_clip_adam/sqnorm");
+    if (rc) return rc;
+    hipLaunchKernelGGL(k_clip_adam, dim3(grid), dim3(OPT_THREADS), 0, (hipStream_t)stream, params, grads, exp_avg,
+                       exp_avg_sq, s, partial, grid, hyper, step, gnorm_out, decoupled);
+    return mep_check_launch("mep_clip_adam/update");
+}
+
+extern "C" int mep_seed_advance(uint64_t* seed, mep_stream_t stream) {
+    hipLaunchKernelGGL(k_seed, dim3(1), dim3(1), 0, (hipStream_t)stream, seed);
+    return mep_check_launch("mep_seed_advance");
+}
+
+extern "C" int mep_colsum(const mep_colsum_desc* descs, int n_desc, int max_tiles, mep_stream_t stream) {
+    if (n_desc <= 0 || max_tiles <= 0) return 0;
+    hipLaunchKernelGGL(k_colsum, dim3(max_tiles, n_desc), dim3(256), 0, (hipStream_t)stream, descs);
+    return mep_check_launch("mep_colsum");
+}
+
+extern "C" int mep_sum_rows(const mep_sum_desc* descs, int n_desc, int max_tiles, mep_stream_t stream) {
+    if (n_desc <= 0 || max_tiles <= 0) return 0;
+    hipLaunchKernelGGL(k_sum_rows, dim3(max_tiles, n_desc), dim3(256), 0, (hipStream_t)stream, descs);
+    return mep_check_launch("mep_sum_rows");
+}

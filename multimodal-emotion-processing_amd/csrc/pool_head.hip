@@ -1,0 +1,379 @@
+// Mean+max pooling over time and the fused fusion-head + loss (forward and backward).
+//
+// Pool: Multi_ATTN's cat(mean_t, max_t) over the time-concatenated block outputs
+// (cmu-mosei/run.py:314-318; realformer.py:258-262).  Padded time steps are included, as in
+// the reference.  Max keeps the FIRST index on ties (torch.max(dim) semantics), which matters
+// for all-zero "no_name" utterances whose rows are identical.
+//
+// Head: Concat_Trans / Base_model head (cmu-mosei/run.py:319,330-339; Ren-MME/run.py:271,
+// 283-292) fused with multi_circle_loss (cmu-mosei/run.py:342-351), the batch mean (run.py:366)
+// and, for Ren-MME, the R-Drop KL (Ren-MME/run.py:331-334).  These are latency-bound (7x7x7
+// bilinear, 14->7 Linear); one workgroup per row (per row pair with R-Drop) does forward,
+// loss and backward in one launch, writing per-row parameter-gradient partials that
+// mep_head_reduce sums in a fixed order (deterministic).
+#include "common.h"
+
+using namespace mep;
+
+namespace {
+
+__global__ __launch_bounds__(256) void k_pool_fwd(const mep_pool_desc* __restrict__ descs) {
+    const mep_pool_desc& d = descs[blockIdx.y];
+    const int nct = (d.C + 255) / 256;
+    if ((int)blockIdx.x >= d.B * nct) return;
+    const int b = blockIdx.x / nct;
+    const int c = (blockIdx.x - b * nct) * 256 + threadIdx.x;
+    if (c >= d.C) return;
+    const float* x = reinterpret_cast<const float*>(d.x) + (int64_t)b * d.T * d.C + c;
+    float s = 0.f, mx = x[0];
+    int idx = 0;
+    for (int t = 0; t < d.T; ++t) {
+        const float v = x[(int64_t)t * d.C];
+        s += v;
+        if (v > mx) { mx = v; idx = t; }
+    }
+    float* pooled = reinterpret_cast<float*>(d.pooled) + (int64_t)b * 2 * d.C;
+    pooled[c] = s / (float)d.T;
+    pooled[d.C + c] = mx;
+    reinterpret_cast<int*>(d.argmax)[(int64_t)b * d.C + c] = idx;
+}
+
+__global__ __launch_bounds__(256) void k_pool_bwd(const mep_pool_desc* __restrict__ descs) {
+    const mep_pool_desc& d = descs[blockIdx.y];
+    const int nct = (d.C + 255) / 256;
+    if ((int)blockIdx.x >= d.B * nct) return;
+    const int b = blockIdx.x / nct;
+    const int c = (blockIdx.x - b * nct) * 256 + threadIdx.x;
+    if (c >= d.C) return;
+    const float* dp = reinterpret_cast<const float*>(d.dpooled) + (int64_t)b * 2 * d.C;
+    const float dmean = dp[c] / (float)d.T, dmax = dp[d.C + c];
+    const int idx = reinterpret_cast<const int*>(d.argmax)[(int64_t)b * d.C + c];
+    float* dx = reinterpret_cast<float*>(d.dx) + (int64_t)b * d.T * d.C + c;
+    for (int t = 0; t < d.T; ++t) dx[(int64_t)t * d.C] = (t == idx) ? dmean + dmax : dmean;
+}
+
+// ---------------------------------------------------------------- fusion head
+constexpr int NCMAX = 16;
+
+struct HeadOff {
+    int wo, bo, lnw, lnb, trans, dl0, dl1, stride;
+};
+__host__ __device__ inline HeadOff head_off(int NC) {
+    HeadOff o;
+    o.wo = 0;
+    o.bo = o.wo + 2 * NC * NC;
+    o.lnw = o.bo + NC;
+    o.lnb = o.lnw + NC;
+    o.trans = o.lnb + NC;
+    o.dl0 = o.trans + NC * NC * NC;
+    o.dl1 = o.dl0 + NC;
+    o.stride = o.dl1 + NC;
+    return o;
+}
+
+MEP_DEV float label_at(const mep_head_desc& d, int b, int n) {
+    if (d.labels_are_float) return reinterpret_cast<const float*>(d.labels)[b * d.NC + n];
+    return (float)reinterpret_cast<const int64_t*>(d.labels)[b * d.NC + n];
+}
+
+// make LDS writes of this wave visible to its other lanes
+MEP_DEV void wave_sync() {
+    __threadfence_block();
+    __builtin_amdgcn_wave_barrier();
+}
+
+MEP_DEV float log_sigmoid(float x) { return fminf(x, 0.f) - log1pf(__expf(-fabsf(x))); }
+
+__global__ __launch_bounds__(256) void k_head(mep_head_desc d) {
+    const int rows = d.rdrop ? 2 : 1;
+    const int r0 = blockIdx.x * rows;
+    const int NC = d.NC, F = d.F;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    __shared__ float s_last[2][NCMAX], s_this[2][NCMAX], s_logit[2][NCMAX], s_dlog[2][NCMAX];
+    __shared__ float s_temp[2][NCMAX * NCMAX];
+    __shared__ float s_yhat[2][NCMAX], s_cat[2][2 * NCMAX], s_rstd[2];
+    __shared__ float s_dlast[2][NCMAX], s_dthis[2][NCMAX];
+    const float* wc0 = reinterpret_cast<const float*>(d.wc0);
+    const float* wc1 = reinterpret_cast<const float*>(d.wc1);
+    const float* trans = reinterpret_cast<const float*>(d.trans);
+    const float* lnw = reinterpret_cast<const float*>(d.ln_w);
+    const float* lnb = reinterpret_cast<const float*>(d.ln_b);
+    const float* wo = reinterpret_cast<const float*>(d.wo);
+    const float* bo = reinterpret_cast<const float*>(d.bo);
+
+    // classifiers (Multi_ATTN.classifier, no bias): one wave per output, lanes over F
+    for (int rr = 0; rr < rows; ++rr) {
+        const int b = r0 + rr;
+        const float* p0 = reinterpret_cast<const float*>(d.pooled0) + (int64_t)b * F;
+        const float* p1 = reinterpret_cast<const float*>(d.pooled1) + (int64_t)b * F;
+        for (int task = wave; task < 2 * NC; task += 4) {
+            const int e = task / NC, n = task - e * NC;
+            const float* w = (e ? wc1 : wc0) + (int64_t)n * F;
+            const float* p = e ? p1 : p0;
+            float s = 0.f;
+            for (int k = lane; k < F; k += 64) s = fmaf(w[k], p[k], s);
+            s = wave_sum(s);
+            if (lane == 0) { if (e) s_this[rr][n] = s; else s_last[rr][n] = s; }
+        }
+    }
+    __syncthreads();
+    if (wave == 0) {
+        for (int rr = 0; rr < rows; ++rr) {
+            // temp[p][n] = sum_m last[m] trans[p][m][n]   (matmul(last[i], trans), run.py:334)
+            for (int idx = lane; idx < NC * NC; idx += 64) {
+                const int p = idx / NC, n = idx - p * NC;
+                float s = 0.f;
+                for (int m = 0; m < NC; ++m) s = fmaf(s_last[rr][m], trans[(p * NC + m) * NC + n], s);
+                s_temp[rr][idx] = s;
+            }
+            wave_sync();
+            float y = 0.f;
+            if (lane < NC)
+                for (int p = 0; p < NC; ++p) y = fmaf(s_this[rr][p], s_temp[rr][p * NC + lane], y);
+            const float mean = wave_sum(lane < NC ? y : 0.f) / (float)NC;
+            const float dv = lane < NC ? y - mean : 0.f;
+            const float var = wave_sum(dv * dv) / (float)NC;
+            const float rstd = 1.0f / sqrtf(var + 1e-5f);
+            if (lane < NC) {
+                s_yhat[rr][lane] = dv * rstd;
+                s_cat[rr][lane] = s_this[rr][lane];
+                s_cat[rr][NC + lane] = dv * rstd * lnw[lane] + lnb[lane];
+            }
+            if (lane == 0) s_rstd[rr] = rstd;
+            wave_sync();
+            if (lane < NC) {
+                float s = 0.f;
+                for (int j = 0; j < 2 * NC; ++j) s = fmaf(wo[lane * 2 * NC + j], s_cat[rr][j], s);
+                s_logit[rr][lane] = s + bo[lane];
+                reinterpret_cast<float*>(d.logits)[(r0 + rr) * NC + lane] = s + bo[lane];
+            }
+            wave_sync();
+        }
+        // losses: circle per row, then R-Drop KL for the pair
+        float* row_loss = reinterpret_cast<float*>(d.row_loss);
+        const float* ext = reinterpret_cast<const float*>(d.ext_dlogits);
+        if (ext) {
+            for (int rr = 0; rr < rows; ++rr)
+                if (lane < NC) s_dlog[rr][lane] = ext[(r0 + rr) * NC + lane];
+            wave_sync();
+        }
+        for (int rr = 0; rr < rows && !ext; ++rr) {
+            const int b = r0 + rr;
+            const bool ok = lane < NC;
+            const float x = ok ? s_logit[rr][lane] : 0.f;
+            const float t = ok ? label_at(d, b, lane) : 0.f;
+            const bool is_pos = ok && t > 0.5f, is_neg = ok && !(t > 0.5f);
+            const float vn = is_neg ? x : -INFINITY;   // y = (1-2t) p for t = 0
+            const float vp = is_pos ? -x : -INFINITY;  // y = (1-2t) p for t = 1
+            const float mn = fmaxf(wave_max(vn), 0.f), mp = fmaxf(wave_max(vp), 0.f);
+            const float en = is_neg ? __expf(vn - mn) : 0.f, ep = is_pos ? __expf(vp - mp) : 0.f;
+            const float sn = wave_sum(en) + __expf(-mn), sp = wave_sum(ep) + __expf(-mp);
+            const float ln = mn + logf(sn), lp = mp + logf(sp);
+            float g = 0.f;
+            if (is_neg) g = __expf(x - ln);
+            if (is_pos) g = -__expf(-x - lp);
+            if (ok) s_dlog[rr][lane] = g * d.loss_scale;
+            if (lane == 0) row_loss[b] = (ln + lp) * d.loss_scale;
+        }
+        if (d.rdrop && !ext) {
+            const float R = (float)(d.B / 2);
+            const bool ok = lane < NC;
+            const float pv = ok ? s_logit[0][lane] : 0.f, qv = ok ? s_logit[1][lane] : 0.f;
+            const float sp = 1.f / (1.f + __expf(-pv)), sq = 1.f / (1.f + __expf(-qv));
+            const float lsp = log_sigmoid(pv), lsq = log_sigmoid(qv);
+            const float lgp = logf(sp), lgq = logf(sq);
+            float kl0 = (ok && sq > 0.f) ? sq * (lgq - lsp) : 0.f;
+            float kl1 = (ok && sp > 0.f) ? sp * (lgp - lsq) : 0.f;
+            const float kl = wave_sum(kl0 + kl1) / R * 0.5f;
+            if (ok) {
+                const float gp = (-sq * (1.f - sp) + (sp > 0.f ? (lgp + 1.f - lsq) * sp * (1.f - sp) : 0.f)) / R * 0.5f;
+                const float gq = (-sp * (1.f - sq) + (sq > 0.f ? (lgq + 1.f - lsp) * sq * (1.f - sq) : 0.f)) / R * 0.5f;
+                s_dlog[0][lane] += gp;
+                s_dlog[1][lane] += gq;
+            }
+            if (lane == 0) row_loss[r0] += kl;
+        }
+        if (d.compute_grad) {
+            const HeadOff o = head_off(NC);
+            for (int rr = 0; rr < rows; ++rr) {
+                float* part = reinterpret_cast<float*>(d.partial) + (int64_t)(r0 + rr) * o.stride;
+                // out Linear: dWo, dbo, dcat
+                for (int idx = lane; idx < NC * 2 * NC; idx += 64) {
+                    const int n = idx / (2 * NC), j = idx - n * 2 * NC;
+                    part[o.wo + idx] = s_dlog[rr][n] * s_cat[rr][j];
+                }
+                float dcat_this = 0.f, dyn = 0.f;
+                if (lane < NC) {
+                    part[o.bo + lane] = s_dlog[rr][lane];
+                    for (int n = 0; n < NC; ++n) {
+                        dcat_this = fmaf(wo[n * 2 * NC + lane], s_dlog[rr][n], dcat_this);
+                        dyn = fmaf(wo[n * 2 * NC + NC + lane], s_dlog[rr][n], dyn);
+                    }
+                    part[o.lnw + lane] = dyn * s_yhat[rr][lane];
+                    part[o.lnb + lane] = dyn;
+                }
+                // LayerNorm(7) backward
+                const float yh = lane < NC ? s_yhat[rr][lane] : 0.f;
+                const float gsc = lane < NC ? dyn * lnw[lane] : 0.f;
+                const float s1 = wave_sum(gsc) / (float)NC, s2 = wave_sum(gsc * yh) / (float)NC;
+                const float dy = lane < NC ? s_rstd[rr] * (gsc - s1 - yh * s2) : 0.f;
+                // bilinear backward
+                __shared__ float s_dy[NCMAX];
+                if (lane < NC) s_dy[lane] = dy;
+                wave_sync();
+                if (lane < NC) {
+                    float dt = dcat_this;
+                    for (int n = 0; n < NC; ++n) dt = fmaf(s_dy[n], s_temp[rr][lane * NC + n], dt);
+                    s_dthis[rr][lane] = dt;
+                    float dl = 0.f;
+                    for (int p = 0; p < NC; ++p) {
+                        const float tp = s_this[rr][p];
+                        for (int n = 0; n < NC; ++n) dl = fmaf(tp * s_dy[n], trans[(p * NC + lane) * NC + n], dl);
+                    }
+                    s_dlast[rr][lane] = dl;
+                    part[o.dl0 + lane] = dl;
+                    part[o.dl1 + lane] = dt;
+                }
+                for (int idx = lane; idx < NC * NC * NC; idx += 64) {
+                    const int p = idx / (NC * NC), m = (idx / NC) % NC, n = idx % NC;
+                    part[o.trans + idx] = s_last[rr][m] * (s_this[rr][p] * s_dy[n]);
+                }
+                wave_sync();
+            }
+        }
+    }
+    if (!d.compute_grad) return;
+    __syncthreads();
+    // dpooled_e = Wc_e^T dlogit_e
+    for (int rr = 0; rr < rows; ++rr) {
+        const int b = r0 + rr;
+        float* dp0 = reinterpret_cast<float*>(d.dpooled0) + (int64_t)b * F;
+        float* dp1 = reinterpret_cast<float*>(d.dpooled1) + (int64_t)b * F;
+        for (int k = threadIdx.x; k < F; k += 256) {
+            float a0 = 0.f, a1 = 0.f;
+            for (int n = 0; n < NC; ++n) {
+                a0 = fmaf(wc0[(int64_t)n * F + k], s_dlast[rr][n], a0);
+                a1 = fmaf(wc1[(int64_t)n * F + k], s_dthis[rr][n], a1);
+            }
+            dp0[k] = a0;
+            dp1[k] = a1;
+        }
+    }
+}
+
+struct HeadGrads {
+    float *g_trans, *g_lnw, *g_lnb, *g_wo, *g_bo, *g_wc0, *g_wc1, *loss;
+};
+
+__global__ __launch_bounds__(256) void k_head_reduce(mep_head_desc d, HeadGrads g) {
+    const int NC = d.NC, F = d.F;
+    const HeadOff o = head_off(NC);
+    const int nA = o.dl0;                 // everything before the dlogit records
+    const int nB = 2 * NC * F;
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    const float* part = reinterpret_cast<const float*>(d.partial);
+    if (i < nA) {
+        float s = 0.f;
+        for (int b = 0; b < d.B; ++b) s += part[(int64_t)b * o.stride + i];
+        float* dst;
+        if (i < o.bo) dst = g.g_wo + (i - o.wo);
+        else if (i < o.lnw) dst = g.g_bo + (i - o.bo);
+        else if (i < o.lnb) dst = g.g_lnw + (i - o.lnw);
+        else if (i < o.trans) dst = g.g_lnb + (i - o.lnb);
+        else dst = g.g_trans + (i - o.trans);
+        *dst = s;
+    } else if (i < nA + nB) {
+        const int j = i - nA;
+        const int e = j / (NC * F), rem = j - e * NC * F;
+        const int n = rem / F, k = rem - n * F;
+        const float* pooled = reinterpret_cast<const float*>(e ? d.pooled1 : d.pooled0);
+        const int off = e ? o.dl1 : o.dl0;
+        float s = 0.f;
+        for (int b = 0; b < d.B; ++b) s = fmaf(part[(int64_t)b * o.stride + off + n], pooled[(int64_t)b * F + k], s);
+        (e ? g.g_wc1 : g.g_wc0)[rem] = s;
+    } else if (i == nA + nB) {
+        const float* rl = reinterpret_cast<const float*>(d.row_loss);
+        float s = 0.f;
+        for (int b = 0; b < d.B; ++b) s += rl[b];
+        *g.loss = s;
+    }
+}
+
+__global__ __launch_bounds__(64) void k_circle_fwd(const float* __restrict__ logits, const void* labels, int lf,
+                                                   int NC, float* __restrict__ row_loss, float* __restrict__ dunit) {
+    const int b = blockIdx.x, lane = threadIdx.x;
+    const bool ok = lane < NC;
+    const float x = ok ? logits[b * NC + lane] : 0.f;
+    float t = 0.f;
+    if (ok) t = lf ? reinterpret_cast<const float*>(labels)[b * NC + lane]
+                   : (float)reinterpret_cast<const int64_t*>(labels)[b * NC + lane];
+    const bool is_pos = ok && t > 0.5f, is_neg = ok && !(t > 0.5f);
+    const float vn = is_neg ? x : -INFINITY, vp = is_pos ? -x : -INFINITY;
+    const float mn = fmaxf(wave_max(vn), 0.f), mp = fmaxf(wave_max(vp), 0.f);
+    const float sn = wave_sum(is_neg ? __expf(vn - mn) : 0.f) + __expf(-mn);
+    const float sp = wave_sum(is_pos ? __expf(vp - mp) : 0.f) + __expf(-mp);
+    const float ln = mn + logf(sn), lp = mp + logf(sp);
+    if (ok) dunit[b * NC + lane] = is_neg ? __expf(x - ln) : -__expf(-x - lp);
+    if (lane == 0) row_loss[b] = ln + lp;
+}
+
+__global__ void k_circle_bwd(const float* __restrict__ dunit, const float* __restrict__ g, int n, int NC,
+                             float* __restrict__ dl) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) dl[i] = dunit[i] * g[i / NC];
+}
+
+}  // namespace
+
+extern "C" int mep_circle_loss_fwd(const float* logits, const void* labels, int labels_are_float, int B, int NC,
+                                   float* row_loss, float* dunit, mep_stream_t stream) {
+    if (NC > 64 || B <= 0) { mep_set_error("mep_circle_loss_fwd: NC <= 64"); return MEP_EINVAL; }
+    hipLaunchKernelGGL(k_circle_fwd, dim3(B), dim3(64), 0, (hipStream_t)stream, logits, labels, labels_are_float, NC,
+                       row_loss, dunit);
+    return mep_check_launch("mep_circle_loss_fwd");
+}
+
+extern "C" int mep_circle_loss_bwd(const float* dunit, const float* grad_rows, int B, int NC, float* dlogits,
+                                   mep_stream_t stream) {
+    const int n = B * NC;
+    if (n <= 0) return 0;
+    hipLaunchKernelGGL(k_circle_bwd, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, dunit, grad_rows, n,
+                       NC, dlogits);
+    return mep_check_launch("mep_circle_loss_bwd");
+}
+
+extern "C" int mep_pool_fwd(const mep_pool_desc* descs, int n_desc, int max_tiles, mep_stream_t stream) {
+    if (n_desc <= 0 || max_tiles <= 0) return 0;
+    hipLaunchKernelGGL(k_pool_fwd, dim3(max_tiles, n_desc), dim3(256), 0, (hipStream_t)stream, descs);
+    return mep_check_launch("mep_pool_fwd");
+}
+
+extern "C" int mep_pool_bwd(const mep_pool_desc* descs, int n_desc, int max_tiles, mep_stream_t stream) {
+    if (n_desc <= 0 || max_tiles <= 0) return 0;
+    hipLaunchKernelGGL(k_pool_bwd, dim3(max_tiles, n_desc), dim3(256), 0, (hipStream_t)stream, descs);
+    return mep_check_launch("mep_pool_bwd");
+}
+
+extern "C" int mep_head_partial_stride(int NC) { return head_off(NC).stride; }
+
+extern "C" int mep_head_fwd_bwd(const mep_head_desc* d, mep_stream_t stream) {
+    if (!d || d->NC > NCMAX || d->NC <= 0 || d->B <= 0 || (d->rdrop && (d->B % 2))) {
+        mep_set_error("mep_head_fwd_bwd: invalid descriptor (NC <= 16, even B with rdrop)");
+        return MEP_EINVAL;
+    }
+    const int groups = d->rdrop ? d->B / 2 : d->B;
+    hipLaunchKernelGGL(k_head, dim3(groups), dim3(256), 0, (hipStream_t)stream, *d);
+    return mep_check_launch("mep_head_fwd_bwd");
+}
+
+extern "C" int mep_head_reduce(const mep_head_desc* d, uint64_t g_trans, uint64_t g_ln_w, uint64_t g_ln_b,
+                               uint64_t g_wo, uint64_t g_bo, uint64_t g_wc0, uint64_t g_wc1, uint64_t loss,
+                               mep_stream_t stream) {
+    if (!d || d->NC > NCMAX) { mep_set_error("mep_head_reduce: invalid descriptor"); return MEP_EINVAL; }
+    HeadGrads g{(float*)g_trans, (float*)g_ln_w, (float*)g_ln_b, (float*)g_wo, (float*)g_bo,
+                (float*)g_wc0, (float*)g_wc1, (float*)loss};
+    const HeadOff o = head_off(d->NC);
+    const int total = o.dl0 + 2 * d->NC * d->F + 1;
+    hipLaunchKernelGGL(k_head_reduce, dim3((total + 255) / 256), dim3(256), 0, (hipStream_t)stream, *d, g);
+    return mep_check_launch("mep_head_reduce");
+}

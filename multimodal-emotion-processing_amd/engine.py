@@ -1,0 +1,98 @@
+"""Fused training-step engine: forward + loss + backward + [gradient all-reduce] + clip + AdamW
+as a fixed launch sequence, captured once per input shape into a hipGraph and replayed.
+
+Data parallelism (one process per GPU, torch.distributed backend "nccl" = RCCL over xGMI): each
+rank runs the step on its own rows; the flat fp32 gradient buffer (2.35 MB for Concat_Trans)
+is all-reduced (SUM) between the backward graph and the optimizer graph, and the optimizer
+graph divides by the world size before clipping, so every rank applies the identical update of
+the global-batch mean (clip after the reduce = 1-GPU large-batch semantics).
+Ren-MME R-Drop pairs are whole rows of the local batch, so they never straddle ranks.
+"""
+import torch
+import torch.distributed as dist
+
+
+class TrainEngine:
+    def __init__(self, model, optimizer, clip=1.0, rdrop=False, graph=True, process_group=None):
+        self.model = model
+        self.opt = optimizer
+        self.clip = clip
+        self.rdrop = rdrop
+        self.graph = graph
+        self.pg = process_group
+        self.world = dist.get_world_size(process_group) if dist.is_available() and dist.is_initialized() else 1
+        self._graphs = {}
+        self._initial_broadcast = self.world > 1
+
+    def _runner(self, device):
+        return self.model.mep_runner(device)
+
+    def plan(self, B, T, device):
+        return self._runner(device).plan(B, T)
+
+    # ---------------------------------------------------------------- step bodies
+    def _fwd_bwd(self, plan):
+        if plan._drop > 0.0:
+            plan.advance_seed()
+        plan.forward(grad=True, rdrop=self.rdrop)
+        plan.backward()
+
+    def _opt(self):
+        self.opt.fused_step()
+
+    def _sync_params(self, runner):
+        """Rank 0's parameters (and optimizer moments, all zero at start) to every rank."""
+        if self._initial_broadcast:
+            dist.broadcast(runner.flat.buf, 0, group=self.pg)
+            self._initial_broadcast = False
+
+    def step_plan(self, plan):
+        """Run one training step on the data already in ``plan``'s input buffers; returns the
+        (local-batch) loss as a device tensor."""
+        runner = self._runner(plan.device)
+        self.opt._bind()
+        self.opt._sync_hyper(self.clip, 1.0 / self.world)
+        p = runner.spec.drop_p if self.model.training else 0.0
+        plan.set_dropout(p)
+        self._sync_params(runner)
+        key = id(plan)
+        g = self._graphs.get(key)
+        if not self.graph:
+            self._fwd_bwd(plan)
+            self._allreduce(runner)
+            self._opt()
+            return plan.loss
+        if g is None:
+            # first step eagerly (loads every kernel), then capture for the next ones
+            self._fwd_bwd(plan)
+            self._allreduce(runner)
+            self._opt()
+            torch.cuda.synchronize()
+            ga, gb = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+            with torch.cuda.graph(ga):
+                self._fwd_bwd(plan)
+                if self.world == 1:
+                    self._opt()
+            if self.world > 1:
+                with torch.cuda.graph(gb):
+                    self._opt()
+            self._graphs[key] = (ga, gb)
+            return plan.loss
+        ga, gb = g
+        ga.replay()
+        if self.world > 1:
+            self._allreduce(runner)
+            gb.replay()
+        return plan.loss
+
+    def _allreduce(self, runner):
+        if self.world > 1:
+            dist.all_reduce(runner.flat.grad, op=dist.ReduceOp.SUM, group=self.pg)
+
+    def step(self, l, v, a, lm, vm, am, labels):
+        """Reference-shaped batch in, loss out (copies the batch into the plan's resident
+        buffers first)."""
+        runner = self._runner(l.device)
+        plan = runner.plan_for(l, v, a)
+        plan.set_inputs(l, v, a, lm, vm, am, labels)
+        return self.step_plan(plan)

@@ -1,0 +1,66 @@
+"""Algorithmic FLOPs and HBM bytes per launch of a TriModalPlan step.
+
+"Algorithmic" = the minimum the math needs: every input read once, every output written once,
+no recomputation (the attention backward's recomputed S / dP are not counted).  fp32 (4 B).
+Per attention-block instance (batch row b, block j), with n_kv = 1 (k is v):
+  fwd flops = 4*Tq*Tk*D;  bytes = 4*(2*Tq*D + Tk*D) + 4*Tk + 8*H*Tq + 4*H*Tq*Tk*(r_in + r_out)
+  bwd flops = 10*Tq*Tk*D; bytes = 4*(Tq*D*(q, x, dx, dq r+w) + Tk*D*(kv, dkv)) + 4*Tk + 8*H*Tq
+          (+ S_prev, ds_next reads, ds_prev write when chained)
+Peaks (MI355X_MICROARCH.md): HBM 8.0 TB/s; fp32 (vector = f32-MFMA rate) 157.3 TFLOP/s.
+"""
+from .trimodal import MODS
+
+HBM_PEAK = 8.0e12
+F32_PEAK = 157.3e12
+
+
+def launch_costs(plan):
+    """{launch name: (flops, bytes)} for one eager training step of the plan (summed over the
+    layers when a launch repeats)."""
+    sp, B = plan.spec, plan.B
+    D, H = sp.D, sp.H
+    out = {}
+
+    def add(name, f, b):
+        f0, b0 = out.get(name, (0, 0))
+        out[name] = (f0 + f, b0 + b)
+
+    for e in range(2):
+        for m, d in zip(MODS, sp.dims):
+            n = plan.ntok[m]
+            add('mep_gemm', 2 * n * D * d, 4 * (n * d + n * D + D * d))
+    for blk in plan.blocks:
+        Tq, Tk = blk['Tq'], blk['Tk']
+        r_in = 1 if blk['i'] > 0 else 0
+        r_out = 1 if 'S' in blk else 0
+        s_bytes = 4 * H * Tq * Tk
+        add('mep_attn_fwd', B * 4 * Tq * Tk * D,
+            B * (4 * (2 * Tq * D + Tk * D) + 4 * Tk + 8 * H * Tq + s_bytes * (r_in + r_out)))
+        n = B * Tq
+        add('mep_block_epi_fwd', 2 * n * D * 3 * D + 8 * n * D, 4 * n * D * 5 + 8 * n + 4 * 3 * D * D + 8 * D)
+        add('mep_block_epi_bwd', 2 * n * D * 3 * D + 10 * n * D,
+            4 * n * D * 7 + 8 * n + 4 * 3 * D * D + 4 * (n // 64 + 1) * 2 * D)
+        chained = s_bytes * ((1 if r_out else 0) + (1 if r_in else 0) * 2)
+        add('mep_attn_bwd', B * 10 * Tq * Tk * D,
+            B * (4 * (5 * Tq * D + 2 * Tk * D) + 4 * Tk + 8 * H * Tq + chained))
+        add('mep_wgrad', 2 * n * D * 3 * D, 4 * n * D * 5)
+    for e in range(2):
+        for m, d in zip(MODS, sp.dims):
+            n = plan.ntok[m]
+            add('mep_wgrad', 2 * n * D * d, 4 * n * (D + d))
+    for e in range(2):
+        add('mep_pool_fwd', B * plan.Ttot * plan.C, 4 * B * (plan.Ttot * plan.C + 2 * plan.C) + 4 * B * plan.C)
+        add('mep_pool_bwd', B * plan.Ttot * plan.C, 4 * B * (plan.Ttot * plan.C + 2 * plan.C) + 4 * B * plan.C)
+    return out
+
+
+def roofline_entry(name, flops, nbytes, seconds):
+    """The bench's roofline object for one kernel: bound = the larger of the two ideal times."""
+    t_mem, t_cmp = nbytes / HBM_PEAK, flops / F32_PEAK
+    if t_mem >= t_cmp:
+        achieved = nbytes / seconds / 1e9
+        return dict(kernel=name, bound='hbm', achieved=round(achieved, 2), peak=HBM_PEAK / 1e9, unit='GB/s',
+                    frac=round(achieved / (HBM_PEAK / 1e9), 4))
+    achieved = flops / seconds / 1e12
+    return dict(kernel=name, bound='mfma', achieved=round(achieved, 3), peak=F32_PEAK / 1e12, unit='TFLOP/s',
+                frac=round(achieved / (F32_PEAK / 1e12), 4))

@@ -1,0 +1,61 @@
+"""Per-model runtime state: the flat parameter buffer and the shape-keyed plan cache.
+
+``ModelRunner`` is attached lazily to a drop-in model the first time it runs on a GPU.  It
+re-homes the parameters into a ``FlatParams`` buffer, builds one ``TriModalPlan`` per input
+shape (batch, T_l, T_v, T_a) and serves both the autograd path (``run_forward`` /
+``run_backward``) and the fused training engine (engine.py).
+"""
+import torch
+
+from .flat import FlatParams
+from .trimodal import TriModalPlan
+
+
+class ModelRunner:
+    n_inputs = 6
+
+    def __init__(self, model, spec, device, labels_float=False):
+        self.model = model
+        self.spec = spec
+        self.device = torch.device(device)
+        self.labels_float = labels_float
+        self.flat = FlatParams(model, self.device, no_grad=spec.no_grad_params())
+        self.plans = {}
+        self._gen = 0
+        self._live = None
+
+    def plan(self, B, T):
+        key = (int(B),) + tuple(int(t) for t in T)
+        p = self.plans.get(key)
+        if p is None:
+            p = TriModalPlan(self.spec, self.flat, key[0], key[1:], self.device, self.labels_float)
+            self.plans[key] = p
+        return p
+
+    def plan_for(self, l, v, a):
+        return self.plan(l.shape[0], (l.shape[2], v.shape[2], a.shape[2]))
+
+    # ------------------------------------------------------------ autograd path
+    def run_forward(self, inputs):
+        l, v, a, lm, vm, am = inputs
+        plan = self.plan_for(l, v, a)
+        p = self.spec.drop_p if self.model.training else 0.0
+        plan.set_dropout(p)
+        if p > 0.0:
+            plan.advance_seed()
+        plan.set_inputs(l, v, a, lm, vm, am)
+        plan.forward(grad=False)
+        self._gen += 1
+        self._live = (plan, self._gen)
+        self.token = self._gen
+        return plan.logits.clone()
+
+    def run_backward(self, dlogits, token=None):
+        plan, gen = self._live
+        if token is not None and token != gen:
+            raise RuntimeError('mep_amd: backward of an older forward -- this plan keeps the '
+                               'activations of the latest forward only; call backward before the next '
+                               'forward of the same shape')
+        plan.backward(ext_dlogits=dlogits)
+        g = self.flat.grad.clone()
+        return [self.flat.view(g, n) if self.flat.has_grad[n] else None for n in self.flat.names]

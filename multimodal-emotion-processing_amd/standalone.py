@@ -1,0 +1,170 @@
+"""Standalone execution of single reference sub-modules on libmep_hip (not the fused step).
+
+``Attention_Block.forward(q, k, v, mask, scores)`` (cmu-mosei/run.py:258-262) and
+``Unify_Dimension.forward`` (run.py:213-214) called directly by user code run here: the same
+kernels as the fused plan, with one descriptor per launch built per call.  The model-level
+forward (Concat_Trans / Base_model) never comes through this module.
+"""
+import ctypes
+
+import torch
+
+from . import _lib
+from ._lib import (AttnBwdDesc, AttnDesc, ColsumDesc, DescArray, EpiBwdDesc, EpiDesc, GemmDesc, Rows,
+                   WgradDesc, launch)
+from .trimodal import TOK_PER_SPLIT, cdiv, crows
+
+
+def _c(t):
+    return t.contiguous().float()
+
+
+def _wgrad(items, dev):
+    total = sum(cdiv(n, TOK_PER_SPLIT) * N * K for (_, _, n, N, K, _, _) in items)
+    ws = torch.empty(total, dtype=torch.float32, device=dev)
+    descs, off, tmax, rmax = [], 0, 0, 0
+    for (a, b, n, N, K, out, ldo) in items:
+        ns = cdiv(n, TOK_PER_SPLIT)
+        descs.append(WgradDesc(a=a, b=b, partial=ws.data_ptr() + 4 * off, out=out, ntok=n, N=N, K=K, ldo=ldo,
+                               tok_per_split=TOK_PER_SPLIT, n_split=ns, accumulate=0))
+        off += ns * N * K
+        tmax = max(tmax, cdiv(N, 64) * cdiv(K, 64) * ns)
+        rmax = max(rmax, cdiv(N * K, 256))
+    arr = DescArray(WgradDesc, descs, dev)
+    launch('mep_wgrad', arr, tmax)
+    launch('mep_wgrad_reduce', arr, rmax)
+    return ws, arr
+
+
+class _BlockFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, H, drop_p, q, k, v, mask, s_prev, c, wp, wm, lnw, lnb):
+        q, k, v, mask = _c(q), _c(k), _c(v), _c(mask)
+        B, Tq, D = q.shape
+        Tk = k.shape[1]
+        dev = q.device
+        same_kv = k.data_ptr() == v.data_ptr()
+        f = dict(dtype=torch.float32, device=dev)
+        X, XP, Z, out = (torch.empty(B, Tq, D, **f) for _ in range(4))
+        S = torch.empty(B, H, Tq, Tk, **f)
+        astat = torch.empty(B, H, Tq, 2, **f)
+        estat = torch.empty(B * Tq, 2, **f)
+        sp = _c(s_prev) if s_prev is not None else None
+        ad = AttnDesc(q=crows(q, Tq, D), k=crows(k, Tk, D), v=crows(v, Tk, D), x=crows(X, Tq, D),
+                      mask=mask.data_ptr(), mask_sB=Tk, s_prev=sp.data_ptr() if sp is not None else 0,
+                      c=c.data_ptr(), s_out=S.data_ptr(), stats=astat.data_ptr(), B=B, H=H, Tq=Tq, Tk=Tk)
+        ed = EpiDesc(q=crows(q, Tq, D), x=crows(X, Tq, D), xp=crows(XP, Tq, D), z=crows(Z, Tq, D),
+                     out=crows(out, Tq, D), wp=wp.data_ptr(), wm=wm.data_ptr(), ln_w=lnw.data_ptr(),
+                     ln_b=lnb.data_ptr(), stats=estat.data_ptr(), seed=0, ntok=B * Tq, D=D, drop_p=0.0,
+                     drop_stream=0)
+        a_arr, e_arr = DescArray(AttnDesc, [ad], dev), DescArray(EpiDesc, [ed], dev)
+        launch('mep_attn_fwd', a_arr, B * cdiv(Tq, 64))
+        launch('mep_block_epi_fwd', e_arr, cdiv(B * Tq, 64))
+        ctx.save_for_backward(q, k, v, mask, X, XP, Z, S, astat, estat, c, wp, wm, lnw, lnb)
+        ctx.sp = sp
+        ctx.meta = (B, Tq, Tk, D, H, same_kv)
+        ctx.descs = (ad, ed)
+        return out, S
+
+    @staticmethod
+    @torch.autograd.function.once_differentiable
+    def backward(ctx, dout, dS):
+        (q, k, v, mask, X, XP, Z, S, astat, estat, c, wp, wm, lnw, lnb) = ctx.saved_tensors
+        B, Tq, Tk, D, H, same_kv = ctx.meta
+        ad, ed = ctx.descs
+        dev = q.device
+        f = dict(dtype=torch.float32, device=dev)
+        dout = _c(dout) if dout is not None else torch.zeros(B, Tq, D, **f)
+        dS = _c(dS) if dS is not None else None
+        dZ, dXP, dX, dQ = (torch.empty(B, Tq, D, **f) for _ in range(4))
+        dK = torch.empty(B, Tk, D, **f)
+        dV = dK if same_kv else torch.empty(B, Tk, D, **f)
+        ln_part = torch.empty(cdiv(B * Tq, 64), 2, D, **f)
+        has_prev = ctx.sp is not None
+        dSp = torch.empty(B, H, Tq, Tk, **f) if has_prev else None
+        dc_part = torch.empty(B * cdiv(Tk, 64), **f) if has_prev else None
+        eb = EpiBwdDesc(f=ed, dout=crows(dout, Tq, D), dout2=Rows(), dz=crows(dZ, Tq, D), dxp=crows(dXP, Tq, D),
+                        dx=crows(dX, Tq, D), dq=crows(dQ, Tq, D), ln_partial=ln_part.data_ptr(), dq_accumulate=0)
+        ab = AttnBwdDesc(f=ad, dx=crows(dX, Tq, D), dq=crows(dQ, Tq, D), dk=crows(dK, Tk, D), dv=crows(dV, Tk, D),
+                         ds_next=dS.data_ptr() if dS is not None else 0,
+                         ds_prev=dSp.data_ptr() if has_prev else 0,
+                         dc_partial=dc_part.data_ptr() if has_prev else 0)
+        launch('mep_block_epi_bwd', DescArray(EpiBwdDesc, [eb], dev), cdiv(B * Tq, 64))
+        launch('mep_attn_bwd', DescArray(AttnBwdDesc, [ab], dev), B * (cdiv(Tq, 64) + cdiv(Tk, 64)))
+        gwp, gwm = torch.empty_like(wp), torch.empty_like(wm)
+        glw, glb, gc = torch.empty_like(lnw), torch.empty_like(lnb), torch.empty_like(c)
+        n = B * Tq
+        keep = _wgrad([(crows(dXP, Tq, D), crows(X, Tq, D), n, D, D, gwp.data_ptr(), D),
+                       (crows(dZ, Tq, D), crows(q, Tq, D), n, D, D, gwm.data_ptr(), 2 * D),
+                       (crows(dZ, Tq, D), crows(XP, Tq, D), n, D, D, gwm.data_ptr() + 4 * D, 2 * D)], dev)
+        cs = [ColsumDesc(partial=ln_part.data_ptr(), out=glw.data_ptr(), n_rows=ln_part.shape[0], n_cols=D,
+                         ld=2 * D, accumulate=0),
+              ColsumDesc(partial=ln_part.data_ptr() + 4 * D, out=glb.data_ptr(), n_rows=ln_part.shape[0],
+                         n_cols=D, ld=2 * D, accumulate=0)]
+        if has_prev:
+            cs.append(ColsumDesc(partial=dc_part.data_ptr(), out=gc.data_ptr(), n_rows=dc_part.numel(), n_cols=1,
+                                 ld=1, accumulate=0))
+        launch('mep_colsum', DescArray(ColsumDesc, cs, dev), cdiv(D, 256))
+        del keep
+        return (None, None, dQ, dK, None if same_kv else dV, None, dSp, gc if has_prev else None,
+                gwp, gwm, glw, glb)
+
+
+def block_forward(block, q, k, v, mask, scores, norm, drop_p=0.0):
+    from ._autograd import require_cuda
+    require_cuda(q, k, v, mask)
+    if mask is None or mask.dim() != 2:
+        raise NotImplementedError('mep_amd attention takes a [batch, kv_len] key mask (the only form the '
+                                  'reference models pass)')
+    if block.training and drop_p > 0.0:
+        raise NotImplementedError('standalone block dropout: run the block inside its model plan')
+    return _BlockFn.apply(block.n_heads, drop_p, q, k, v, mask, scores, block.c, block.proj.weight,
+                          block.minus.weight, norm.weight, norm.bias)
+
+
+class _UnifyFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w):
+        x = _c(x)
+        lead = x.shape[:-1]
+        K = x.shape[-1]
+        N = w.shape[0]
+        x2 = x.reshape(-1, K)
+        n = x2.shape[0]
+        y = torch.empty(n, N, dtype=torch.float32, device=x.device)
+        d = GemmDesc(x=crows(x2, n, K), y=crows(y, n, N), w=w.data_ptr(), bias=0, table=0, ntok=n, N=N, K=K, ldw=K,
+                     w_nt=1, accumulate=0, relu=0, alpha=1.0)
+        launch('mep_gemm', DescArray(GemmDesc, [d], x.device), cdiv(n, 64))
+        ctx.save_for_backward(x2, w)
+        ctx.x_shape = x.shape
+        return y.reshape(*lead, N)
+
+    @staticmethod
+    @torch.autograd.function.once_differentiable
+    def backward(ctx, gy):
+        x2, w = ctx.saved_tensors
+        n, K = x2.shape
+        N = w.shape[0]
+        gy = _c(gy).reshape(n, N)
+        gw = torch.empty_like(w)
+        keep = _wgrad([(crows(gy, n, N), crows(x2, n, K), n, N, K, gw.data_ptr(), K)], x2.device)
+        gx = None
+        if ctx.needs_input_grad[0]:
+            gx = torch.empty(n, K, dtype=torch.float32, device=x2.device)
+            d = GemmDesc(x=crows(gy, n, N), y=crows(gx, n, K), w=w.data_ptr(), bias=0, table=0, ntok=n, N=K, K=N,
+                         ldw=K, w_nt=0, accumulate=0, relu=0, alpha=1.0)
+            launch('mep_gemm', DescArray(GemmDesc, [d], x2.device), cdiv(n, 64))
+            gx = gx.reshape(ctx.x_shape)
+        del keep
+        return gx, gw
+
+
+def linear_nobias(x, w):
+    from ._autograd import require_cuda
+    require_cuda(x)
+    return _UnifyFn.apply(x, w)
+
+
+def unify_forward(mod, l, v, a):
+    return (linear_nobias(l, mod.linguistic.weight), linear_nobias(v, mod.visual.weight),
+            linear_nobias(a, mod.acoustic.weight))

@@ -1,0 +1,439 @@
+"""Execution plan of the tri-modal encoder pair + fusion head (cmu-mosei Concat_Trans,
+Ren-MME Base_model) on libmep_hip.
+
+A plan is built once per (batch, sequence lengths) shape.  It owns every activation and
+gradient buffer of a training step in HBM and the device-resident descriptor arrays of each
+grouped launch, so a step is a fixed sequence of ~20 launches with no host work -- capturable
+as one hipGraph.
+
+Step anatomy (reference call stack: SURVEY.md section 3A; cmu-mosei/run.py:329-369)
+  forward   unify GEMM (both encoders x 3 modalities in ONE launch)  [+ shared LayerNorm, Ren]
+            per layer: attention core (all 9 chains x 2 encoders in one launch),
+                       block epilogue (proj -> cat -> minus -> LayerNorm, one launch)
+            mean+max pool (one launch) -> fused head + circle loss (+R-Drop) + head backward
+  backward  head reduce, pool backward, per layer (reverse): epilogue backward, attention
+            backward; per-modality gradient sum; all weight gradients in one split-K launch +
+            one reduce; LayerNorm / residual-coefficient column sums.
+Independent work is batched into grouped launches (grid.y = descriptor), never looped in
+Python.  HBM layout: block outputs are written straight into the pooled tensor
+[B, T_l+T_a+T_v, 3*n_layers*D] at their (time, feature) offsets (torch.cat at run.py:314-317 is
+never materialised); inputs stay in the reference's [B, 2, T, d] (prev, cur) layout and are read
+through strided row views.
+"""
+import ctypes
+
+import torch
+
+from . import _lib
+from ._lib import (AttnBwdDesc, AttnDesc, ColsumDesc, DescArray, EpiBwdDesc, EpiDesc, GemmDesc,
+                   HeadDesc, LnDesc, PoolDesc, Rows, SumDesc, WgradDesc, launch)
+
+CHAINS = (('l', 'l'), ('l', 'v'), ('l', 'a'),
+          ('v', 'v'), ('v', 'l'), ('v', 'a'),
+          ('a', 'a'), ('a', 'l'), ('a', 'v'))          # cmu-mosei/run.py:279-313
+MODS = ('l', 'v', 'a')
+TIME_ORDER = ('l', 'a', 'v')                          # cmu-mosei/run.py:317
+UNIFY_NAMES = {'l': 'linguistic', 'v': 'visual', 'a': 'acoustic'}
+TOK_PER_SPLIT = 256
+
+
+def cdiv(a, b):
+    return (a + b - 1) // b
+
+
+def rows(t, T, sB, sT, off=0):
+    return Rows(ptr=t.data_ptr() + 4 * off, sB=sB, sT=sT, T=T)
+
+
+def crows(t, T, D, off=0):
+    """contiguous [B*T, D] view"""
+    return rows(t, T, T * D, D, off)
+
+
+class TriModalSpec:
+    """Static description of one model family instance."""
+
+    def __init__(self, D, H, n_layers, dims, NC, variant='cmu', drop_p=0.0):
+        assert D == 16 * H and D % 32 == 0 and D <= 128, 'kernels need hd = 16 and D in {32,64,96,128}'
+        self.D, self.H, self.nl, self.dims, self.NC = D, H, n_layers, tuple(dims), NC
+        self.variant = variant                      # 'cmu' | 'ren'
+        self.unify_norm = variant == 'ren'          # Ren-MME/run.py:164-166
+        self.block_norm = 'norm2' if variant == 'ren' else 'norm1'
+        self.head_norm = 'norm3' if variant == 'ren' else 'norm1'
+        self.drop_p = float(drop_p)
+        self.prefixes = ('intensity.', 'stimulation.')
+
+    def no_grad_params(self):
+        """c of the first layer of every chain never receives a gradient (scores is None)."""
+        out = []
+        for pre in self.prefixes:
+            for j in range(9):
+                out.append(pre + 'multimodal_blocks.%d.c' % (self.nl * j))
+        return out
+
+
+class TriModalPlan:
+    def __init__(self, spec, flat, B, T, device, labels_float=False):
+        self.spec, self.flat, self.B = spec, flat, B
+        self.T = dict(zip(MODS, T))
+        self.device = torch.device(device)
+        self.labels_float = labels_float
+        self._drop = 0.0
+        sp = spec
+        D, H, nl, NC = sp.D, sp.H, sp.nl, sp.NC
+        dev = self.device
+        f32 = dict(dtype=torch.float32, device=dev)
+        self.Ttot = sum(self.T.values())
+        self.C = 3 * nl * D
+        self.F = 2 * self.C
+        E = 2
+        # ---------------- static input buffers ([B, 2, T, d] prev/cur layout)
+        self.x_in = {m: torch.zeros(B, E, self.T[m], d, **f32) for m, d in zip(MODS, sp.dims)}
+        self.m_in = {m: torch.zeros(B, E, self.T[m], **f32) for m in MODS}
+        self.labels = torch.zeros(B, NC, dtype=torch.float32 if labels_float else torch.int64, device=dev)
+        self.seed = torch.zeros(1, dtype=torch.int64, device=dev)
+        # ---------------- activations
+        ntok = {m: B * self.T[m] for m in MODS}
+        self.ntok = ntok
+        self.U = {(e, m): torch.zeros(ntok[m], D, **f32) for e in range(E) for m in MODS}
+        if sp.unify_norm:
+            self.Y = {(e, m): torch.zeros(ntok[m], D, **f32) for e in range(E) for m in MODS}
+            self.Ystat = {(e, m): torch.zeros(ntok[m], 2, **f32) for e in range(E) for m in MODS}
+        self.Xcat = [torch.zeros(B, self.Ttot, self.C, **f32) for _ in range(E)]
+        self.pooled = [torch.zeros(B, self.F, **f32) for _ in range(E)]
+        self.argmax = [torch.zeros(B, self.C, dtype=torch.int32, device=dev) for _ in range(E)]
+        self.dpooled = [torch.zeros(B, self.F, **f32) for _ in range(E)]
+        self.dXcat = [torch.zeros(B, self.Ttot, self.C, **f32) for _ in range(E)]
+        self.logits = torch.zeros(B, NC, **f32)
+        self.row_loss = torch.zeros(B, **f32)
+        self.loss = torch.zeros(1, **f32)
+        self.head_stride = _lib.lib().mep_head_partial_stride(NC)
+        self.head_partial = torch.zeros(B, self.head_stride, **f32)
+        self.toff = {}
+        t = 0
+        for m in TIME_ORDER:
+            self.toff[m] = t
+            t += self.T[m]
+
+        self.blocks = []
+        for e in range(E):
+            for j, (qm, km) in enumerate(CHAINS):
+                for i in range(nl):
+                    self.blocks.append(self._make_block(e, j, i, qm, km))
+        self._build_descriptors()
+
+    # ------------------------------------------------------------------ buffers per block
+    def _make_block(self, e, j, i, qm, km):
+        sp, B, D, H = self.spec, self.B, self.spec.D, self.spec.H
+        f32 = dict(dtype=torch.float32, device=self.device)
+        Tq, Tk = self.T[qm], self.T[km]
+        nq, nk = B * Tq, B * Tk
+        blk = dict(idx=len(self.blocks), e=e, j=j, i=i, qm=qm, km=km, Tq=Tq, Tk=Tk,
+                   pre=sp.prefixes[e] + 'multimodal_blocks.%d.' % (sp.nl * j + i))
+        for name in ('X', 'XP', 'Z', 'dZ', 'dXP', 'dX', 'dQ'):
+            blk[name] = torch.zeros(nq, D, **f32)
+        blk['estat'] = torch.zeros(nq, 2, **f32)
+        blk['astat'] = torch.zeros(B, H, Tq, 2, **f32)
+        blk['dKV'] = torch.zeros(nk, D, **f32)
+        blk['ln_partial'] = torch.zeros(cdiv(nq, 64), 2, D, **f32)
+        if i < sp.nl - 1:
+            blk['S'] = torch.zeros(B, H, Tq, Tk, **f32)
+        if i >= 1:
+            blk['dSprev'] = torch.zeros(B, H, Tq, Tk, **f32)
+            blk['dc_partial'] = torch.zeros(B * cdiv(Tk, 64), **f32)
+        g = j % 3
+        blk['col'] = (g * sp.nl + i) * D
+        return blk
+
+    def _out_rows(self, blk):
+        e, qm = blk['e'], blk['qm']
+        return rows(self.Xcat[e], blk['Tq'], self.Ttot * self.C, self.C, self.toff[qm] * self.C + blk['col'])
+
+    def _dout_rows(self, blk):
+        e, qm = blk['e'], blk['qm']
+        return rows(self.dXcat[e], blk['Tq'], self.Ttot * self.C, self.C, self.toff[qm] * self.C + blk['col'])
+
+    def _q_rows(self, blk):
+        if blk['i'] == 0:
+            return crows(self.U[(blk['e'], blk['qm'])], blk['Tq'], self.spec.D)
+        return self._out_rows(self._blk(blk['e'], blk['j'], blk['i'] - 1))
+
+    def _blk(self, e, j, i):
+        return self.blocks[(e * 9 + j) * self.spec.nl + i]
+
+    def _in_rows(self, e, m):
+        d = self.spec.dims[MODS.index(m)]
+        T = self.T[m]
+        return rows(self.x_in[m], T, 2 * T * d, d, e * T * d)
+
+    # ------------------------------------------------------------------ descriptors
+    def _build_descriptors(self):
+        sp, fl, B, D, H, nl, NC = self.spec, self.flat, self.B, self.spec.D, self.spec.H, self.spec.nl, self.spec.NC
+        dev = self.device
+        E = 2
+        g = fl.gptr
+        # unify
+        ud = []
+        for e in range(E):
+            pre = sp.prefixes[e] + 'unify_dimension.'
+            for m, d in zip(MODS, sp.dims):
+                out = self.Y[(e, m)] if sp.unify_norm else self.U[(e, m)]
+                ud.append(GemmDesc(x=self._in_rows(e, m), y=crows(out, self.T[m], D),
+                                   w=fl.ptr(pre + UNIFY_NAMES[m] + '.weight'), bias=0, table=0,
+                                   ntok=self.ntok[m], N=D, K=d, ldw=d, w_nt=1, accumulate=0, relu=0, alpha=1.0))
+        self.d_unify = DescArray(GemmDesc, ud, dev)
+        self.t_unify = max(cdiv(self.ntok[m], 64) for m in MODS)
+        if sp.unify_norm:
+            ln = []
+            for e in range(E):
+                pre = sp.prefixes[e] + 'unify_dimension.norm1.'
+                for m in MODS:
+                    T = self.T[m]
+                    ln.append(LnDesc(x=crows(self.Y[(e, m)], T, D), y=crows(self.U[(e, m)], T, D),
+                                     dy=Rows(), dx=Rows(), w=fl.ptr(pre + 'weight'), b=fl.ptr(pre + 'bias'),
+                                     stats=self.Ystat[(e, m)].data_ptr(), partial=0, ntok=self.ntok[m], D=D,
+                                     dx_accumulate=0))
+            self.d_uln = DescArray(LnDesc, ln, dev)
+        # per layer: attention + epilogue forward
+        self.d_attn, self.d_epi, self.t_attn, self.t_epi = [], [], [], []
+        for i in range(nl):
+            ad, ed = [], []
+            for blk in (b for b in self.blocks if b['i'] == i):
+                ad.append(self._attn_desc(blk))
+                ed.append(self._epi_desc(blk))
+            self.d_attn.append(DescArray(AttnDesc, ad, dev))
+            self.d_epi.append(DescArray(EpiDesc, ed, dev))
+            self.t_attn.append(max(B * cdiv(b['Tq'], 64) for b in self.blocks))
+            self.t_epi.append(max(cdiv(B * b['Tq'], 64) for b in self.blocks))
+        # pool
+        pd = [PoolDesc(x=self.Xcat[e].data_ptr(), dx=self.dXcat[e].data_ptr(), pooled=self.pooled[e].data_ptr(),
+                       dpooled=self.dpooled[e].data_ptr(), argmax=self.argmax[e].data_ptr(),
+                       B=B, T=self.Ttot, C=self.C) for e in range(E)]
+        self.d_pool = DescArray(PoolDesc, pd, dev)
+        self.t_pool = B * cdiv(self.C, 256)
+        # head
+        hn = sp.head_norm
+        self.head = HeadDesc(
+            pooled0=self.pooled[0].data_ptr(), pooled1=self.pooled[1].data_ptr(),
+            dpooled0=self.dpooled[0].data_ptr(), dpooled1=self.dpooled[1].data_ptr(),
+            wc0=fl.ptr('intensity.classifier.weight'), wc1=fl.ptr('stimulation.classifier.weight'),
+            trans=fl.ptr('trans'), ln_w=fl.ptr(hn + '.weight'), ln_b=fl.ptr(hn + '.bias'),
+            wo=fl.ptr('out.weight'), bo=fl.ptr('out.bias'), labels=self.labels.data_ptr(),
+            logits=self.logits.data_ptr(), row_loss=self.row_loss.data_ptr(),
+            partial=self.head_partial.data_ptr(), B=B, F=self.F, NC=NC,
+            labels_are_float=int(self.labels_float), rdrop=0, compute_grad=1, loss_scale=1.0 / B, ext_dlogits=0)
+        # backward per layer
+        self.d_epib, self.d_attnb, self.t_attnb = [], [], []
+        for i in range(nl):
+            eb, ab = [], []
+            for blk in (b for b in self.blocks if b['i'] == i):
+                eb.append(self._epi_bwd_desc(blk))
+                ab.append(self._attn_bwd_desc(blk))
+            self.d_epib.append(DescArray(EpiBwdDesc, eb, dev))
+            self.d_attnb.append(DescArray(AttnBwdDesc, ab, dev))
+            self.t_attnb.append(max(B * (cdiv(b['Tq'], 64) + cdiv(b['Tk'], 64)) for b in self.blocks))
+        # per-modality gradient sums
+        sd = []
+        self.dU = {}
+        for e in range(E):
+            for m in MODS:
+                T = self.T[m]
+                self.dU[(e, m)] = torch.zeros(self.ntok[m], D, dtype=torch.float32, device=dev)
+                srcs = [crows(self._blk(e, j, 0)['dQ'], T, D) for j, (qm, km) in enumerate(CHAINS) if qm == m]
+                srcs += [crows(self._blk(e, j, i)['dKV'], T, D) for j, (qm, km) in enumerate(CHAINS) if km == m
+                         for i in range(nl)]
+                assert len(srcs) <= _lib.SUM_MAX_SRC
+                arr = (Rows * _lib.SUM_MAX_SRC)(*srcs)
+                sd.append(SumDesc(src=arr, out=crows(self.dU[(e, m)], T, D), n_src=len(srcs),
+                                  ntok=self.ntok[m], D=D, accumulate=0))
+        self.d_sum = DescArray(SumDesc, sd, dev)
+        self.t_sum = min(1024, max(cdiv(self.ntok[m] * D, 256) for m in MODS))
+        if sp.unify_norm:
+            self.dY = {k: torch.zeros_like(v) for k, v in self.dU.items()}
+            tiles = {m: cdiv(self.ntok[m], 64) for m in MODS}
+            self.uln_partial = [torch.zeros(sum(tiles.values()), 2, D, dtype=torch.float32, device=dev)
+                                for _ in range(E)]
+            lb = []
+            for e in range(E):
+                pre = sp.prefixes[e] + 'unify_dimension.norm1.'
+                r0 = 0
+                for m in MODS:
+                    T = self.T[m]
+                    lb.append(LnDesc(x=crows(self.Y[(e, m)], T, D), y=Rows(), dy=crows(self.dU[(e, m)], T, D),
+                                     dx=crows(self.dY[(e, m)], T, D), w=fl.ptr(pre + 'weight'), b=0,
+                                     stats=self.Ystat[(e, m)].data_ptr(),
+                                     partial=self.uln_partial[e].data_ptr() + 4 * r0 * 2 * D,
+                                     ntok=self.ntok[m], D=D, dx_accumulate=0))
+                    r0 += tiles[m]
+            self.d_ulnb = DescArray(LnDesc, lb, dev)
+        self._build_grad_descriptors()
+
+    def _attn_desc(self, blk):
+        sp, fl, D = self.spec, self.flat, self.spec.D
+        e, km = blk['e'], blk['km']
+        kv = crows(self.U[(e, km)], blk['Tk'], D)
+        Tk = self.T[km]
+        prev = self._blk(e, blk['j'], blk['i'] - 1) if blk['i'] > 0 else None
+        return AttnDesc(q=self._q_rows(blk), k=kv, v=kv, x=crows(blk['X'], blk['Tq'], D),
+                        mask=self.m_in[km].data_ptr() + 4 * e * Tk, mask_sB=2 * Tk,
+                        s_prev=prev['S'].data_ptr() if prev is not None else 0,
+                        c=fl.ptr(blk['pre'] + 'c'), s_out=blk['S'].data_ptr() if 'S' in blk else 0,
+                        stats=blk['astat'].data_ptr(), B=self.B, H=sp.H, Tq=blk['Tq'], Tk=Tk)
+
+    def _epi_desc(self, blk):
+        sp, fl, D = self.spec, self.flat, self.spec.D
+        Tq = blk['Tq']
+        stream_id = blk['idx']
+        return EpiDesc(q=self._q_rows(blk), x=crows(blk['X'], Tq, D), xp=crows(blk['XP'], Tq, D),
+                       z=crows(blk['Z'], Tq, D), out=self._out_rows(blk),
+                       wp=fl.ptr(blk['pre'] + 'proj.weight'), wm=fl.ptr(blk['pre'] + 'minus.weight'),
+                       ln_w=fl.ptr(blk['pre'] + sp.block_norm + '.weight'),
+                       ln_b=fl.ptr(blk['pre'] + sp.block_norm + '.bias'),
+                       stats=blk['estat'].data_ptr(), seed=self.seed.data_ptr(),
+                       ntok=self.B * Tq, D=D, drop_p=self._drop, drop_stream=stream_id)
+
+    def _epi_bwd_desc(self, blk):
+        D, Tq = self.spec.D, blk['Tq']
+        nxt = self._blk(blk['e'], blk['j'], blk['i'] + 1) if blk['i'] < self.spec.nl - 1 else None
+        return EpiBwdDesc(f=self._epi_desc(blk), dout=self._dout_rows(blk),
+                          dout2=crows(nxt['dQ'], Tq, D) if nxt is not None else Rows(),
+                          dz=crows(blk['dZ'], Tq, D), dxp=crows(blk['dXP'], Tq, D), dx=crows(blk['dX'], Tq, D),
+                          dq=crows(blk['dQ'], Tq, D), ln_partial=blk['ln_partial'].data_ptr(), dq_accumulate=0)
+
+    def _attn_bwd_desc(self, blk):
+        D = self.spec.D
+        nxt = self._blk(blk['e'], blk['j'], blk['i'] + 1) if blk['i'] < self.spec.nl - 1 else None
+        dkv = crows(blk['dKV'], blk['Tk'], D)
+        return AttnBwdDesc(f=self._attn_desc(blk), dx=crows(blk['dX'], blk['Tq'], D),
+                           dq=crows(blk['dQ'], blk['Tq'], D), dk=dkv, dv=dkv,
+                           ds_next=nxt['dSprev'].data_ptr() if nxt is not None else 0,
+                           ds_prev=blk['dSprev'].data_ptr() if 'dSprev' in blk else 0,
+                           dc_partial=blk['dc_partial'].data_ptr() if 'dc_partial' in blk else 0)
+
+    def _build_grad_descriptors(self):
+        """Descriptors of the launches that write into the flat gradient buffer."""
+        sp, fl, D = self.spec, self.flat, self.spec.D
+        dev = self.device
+        g = fl.gptr
+        items = []   # (a rows, b rows, ntok, N, K, out ptr, ldo)
+        for blk in self.blocks:
+            Tq, nq, pre = blk['Tq'], self.B * blk['Tq'], blk['pre']
+            items.append((crows(blk['dXP'], Tq, D), crows(blk['X'], Tq, D), nq, D, D, g(pre + 'proj.weight'), D))
+            items.append((crows(blk['dZ'], Tq, D), self._q_rows(blk), nq, D, D, g(pre + 'minus.weight'), 2 * D))
+            items.append((crows(blk['dZ'], Tq, D), crows(blk['XP'], Tq, D), nq, D, D,
+                          g(pre + 'minus.weight') + 4 * D, 2 * D))
+        for e in range(2):
+            pre = sp.prefixes[e] + 'unify_dimension.'
+            for m, d in zip(MODS, sp.dims):
+                src = self.dY[(e, m)] if sp.unify_norm else self.dU[(e, m)]
+                items.append((crows(src, self.T[m], D), self._in_rows(e, m), self.ntok[m], D, d,
+                              g(pre + UNIFY_NAMES[m] + '.weight'), d))
+        total = sum(cdiv(n, TOK_PER_SPLIT) * N * K for (_, _, n, N, K, _, _) in items)
+        self.wg_partial = torch.zeros(total, dtype=torch.float32, device=dev)
+        wd, off, tmax, rmax = [], 0, 0, 0
+        for (a, b, n, N, K, out, ldo) in items:
+            ns = cdiv(n, TOK_PER_SPLIT)
+            wd.append(WgradDesc(a=a, b=b, partial=self.wg_partial.data_ptr() + 4 * off, out=out, ntok=n, N=N, K=K,
+                                ldo=ldo, tok_per_split=TOK_PER_SPLIT, n_split=ns, accumulate=0))
+            off += ns * N * K
+            tmax = max(tmax, cdiv(N, 64) * cdiv(K, 64) * ns)
+            rmax = max(rmax, cdiv(N * K, 256))
+        self.d_wgrad = DescArray(WgradDesc, wd, dev)
+        self.t_wgrad, self.t_wgred = tmax, rmax
+        # column sums: block LayerNorms, residual coefficients, Ren unify LayerNorm
+        cs = []
+        for blk in self.blocks:
+            nt = blk['ln_partial'].shape[0]
+            base = blk['ln_partial'].data_ptr()
+            nm = blk['pre'] + sp.block_norm
+            cs.append(ColsumDesc(partial=base, out=g(nm + '.weight'), n_rows=nt, n_cols=D, ld=2 * D, accumulate=0))
+            cs.append(ColsumDesc(partial=base + 4 * D, out=g(nm + '.bias'), n_rows=nt, n_cols=D, ld=2 * D,
+                                 accumulate=0))
+            if 'dc_partial' in blk:
+                cs.append(ColsumDesc(partial=blk['dc_partial'].data_ptr(), out=g(blk['pre'] + 'c'),
+                                     n_rows=blk['dc_partial'].numel(), n_cols=1, ld=1, accumulate=0))
+        if sp.unify_norm:
+            for e in range(2):
+                pre = sp.prefixes[e] + 'unify_dimension.norm1.'
+                p = self.uln_partial[e]
+                cs.append(ColsumDesc(partial=p.data_ptr(), out=g(pre + 'weight'), n_rows=p.shape[0], n_cols=D,
+                                     ld=2 * D, accumulate=0))
+                cs.append(ColsumDesc(partial=p.data_ptr() + 4 * D, out=g(pre + 'bias'), n_rows=p.shape[0],
+                                     n_cols=D, ld=2 * D, accumulate=0))
+        self.d_colsum = DescArray(ColsumDesc, cs, dev)
+        self.t_colsum = cdiv(D, 256)
+        hn = sp.head_norm
+        self.head_grads = (g('trans'), g(hn + '.weight'), g(hn + '.bias'), g('out.weight'), g('out.bias'),
+                           g('intensity.classifier.weight'), g('stimulation.classifier.weight'),
+                           self.loss.data_ptr())
+        self.d_losssum = DescArray(ColsumDesc, [ColsumDesc(partial=self.row_loss.data_ptr(), out=self.loss.data_ptr(),
+                                                           n_rows=self.B, n_cols=1, ld=1, accumulate=0)], dev)
+
+    # ------------------------------------------------------------------ execution
+    def set_inputs(self, l, v, a, lm, vm, am, labels=None):
+        with torch.no_grad():
+            for m, x, mk in (('l', l, lm), ('v', v, vm), ('a', a, am)):
+                self.x_in[m].copy_(x)
+                self.m_in[m].copy_(mk)
+            if labels is not None:
+                self.labels.copy_(labels)
+
+    def set_dropout(self, p):
+        """Dropout probability of the block epilogues (Ren-MME DROP at train time, 0 in eval).
+        Descriptor bytes are rewritten in place so captured graphs see the new value."""
+        p = float(p)
+        if p == self._drop:
+            return
+        self._drop = p
+        for i in range(self.spec.nl):
+            blks = [b for b in self.blocks if b['i'] == i]
+            for arr, items in ((self.d_epi[i], [self._epi_desc(b) for b in blks]),
+                               (self.d_epib[i], [self._epi_bwd_desc(b) for b in blks])):
+                host = (arr.struct * arr.n)(*items)
+                arr.dev.copy_(torch.frombuffer(bytearray(bytes(host)), dtype=torch.uint8))
+
+    def forward(self, grad=True, rdrop=False, stream=None):
+        """Encoder forward + pool + fused head.  The head always produces logits and the per-row
+        loss (row_loss, already scaled by 1/B); grad=True also runs the head backward
+        (dpooled + head parameter partials) inside the same launch."""
+        sp, nl = self.spec, self.spec.nl
+        launch('mep_gemm', self.d_unify, self.t_unify, stream)
+        if sp.unify_norm:
+            launch('mep_layernorm_fwd', self.d_uln, cdiv(max(self.ntok.values()), 4), stream)
+        for i in range(nl):
+            launch('mep_attn_fwd', self.d_attn[i], self.t_attn[i], stream)
+            launch('mep_block_epi_fwd', self.d_epi[i], self.t_epi[i], stream)
+        launch('mep_pool_fwd', self.d_pool, self.t_pool, stream)
+        self.head.compute_grad = int(grad)
+        self.head.rdrop = int(rdrop)
+        self.head.ext_dlogits = 0
+        _lib.call('mep_head_fwd_bwd', ctypes.byref(self.head), stream=stream)
+
+    def backward(self, ext_dlogits=None, stream=None):
+        """Backward from the fused-loss head partials, or from external dlogits [B, NC].
+        Writes every parameter gradient into the flat gradient buffer (flat.grad) and the batch
+        loss into self.loss."""
+        sp, nl = self.spec, self.spec.nl
+        if ext_dlogits is not None:
+            self.head.compute_grad = 1
+            self.head.ext_dlogits = ext_dlogits.data_ptr()
+            _lib.call('mep_head_fwd_bwd', ctypes.byref(self.head), stream=stream)
+            self.head.ext_dlogits = 0
+        _lib.call('mep_head_reduce', ctypes.byref(self.head), *self.head_grads, stream=stream)
+        launch('mep_pool_bwd', self.d_pool, self.t_pool, stream)
+        for i in reversed(range(nl)):
+            launch('mep_block_epi_bwd', self.d_epib[i], self.t_epi[i], stream)
+            launch('mep_attn_bwd', self.d_attnb[i], self.t_attnb[i], stream)
+        launch('mep_sum_rows', self.d_sum, self.t_sum, stream)
+        if sp.unify_norm:
+            launch('mep_layernorm_bwd', self.d_ulnb, cdiv(max(self.ntok.values()), 64), stream)
+        launch('mep_wgrad', self.d_wgrad, self.t_wgrad, stream)
+        launch('mep_wgrad_reduce', self.d_wgrad, self.t_wgred, stream)
+        launch('mep_colsum', self.d_colsum, self.t_colsum, stream)
+
+    def advance_seed(self, stream=None):
+        _lib.call('mep_seed_advance', ctypes.c_void_p(self.seed.data_ptr()), stream=stream)
+
+    def loss_only(self, stream=None):
+        """Batch loss (sum of the scaled per-row losses) without the backward."""
+        launch('mep_colsum', self.d_losssum, 1, stream)

@@ -1,0 +1,37 @@
+"""Helpers for the GPU parity tests: build drop-in models from golden fixtures."""
+import numpy as np
+import torch
+
+from tests.golden import fixtures, specs
+
+
+def assert_close(got, want, rtol, atol_frac=1e-5, name=''):
+    """Elementwise |got - want| <= atol + rtol*|want| with atol = atol_frac * max|want|: a
+    relative tolerance that does not explode on entries that are ~0 by cancellation."""
+    g = got.detach().double().cpu().numpy() if torch.is_tensor(got) else np.asarray(got, np.float64)
+    w = want.detach().double().cpu().numpy() if torch.is_tensor(want) else np.asarray(want, np.float64)
+    assert g.shape == w.shape, (name, g.shape, w.shape)
+    atol = atol_frac * max(float(np.abs(w).max()) if w.size else 0.0, 1e-30)
+    err = np.abs(g - w)
+    bad = err > atol + rtol * np.abs(w)
+    if bad.any():
+        i = np.unravel_index(np.argmax(err - rtol * np.abs(w)), w.shape)
+        raise AssertionError('%s: %d/%d mismatches; worst at %s got %r want %r (rtol %g, atol %g)'
+                             % (name, int(bad.sum()), bad.size, i, g[i], w[i], rtol, atol))
+
+
+def load_params(model, meta):
+    vals = specs.param_values(meta['shapes'], meta['seed'])
+    model.load_state_dict({k: torch.from_numpy(v) for k, v in vals.items()})
+    return model
+
+
+def cmu_model(meta, device):
+    from mep_amd import cmu_mosei
+    c = meta['ctor']
+    m = cmu_mosei.Concat_Trans(**c)
+    return load_params(m, meta).to(device)
+
+
+def cuda_batch(meta, device):
+    return [t.to(device) for t in fixtures.batch(meta)]

@@ -1,0 +1,101 @@
+"""GPU parity of the cmu-mosei Concat_Trans path (libmep_hip) against the reference golden vectors.
+
+Tolerances (north star: logits within 1e-4 fp32 relative): logits / loss rtol 1e-4; gradients
+rtol 1e-3 with an absolute floor of 1e-5 x max|grad| (fp32 sums of 3200 tokens in a different
+order than MKL); post-AdamW parameters atol 2e-5 (= 2 % of lr: Adam normalises tiny gradients
+to ~lr-sized steps, amplifying rounding on near-zero grads).
+"""
+import pytest
+import torch
+
+from tests.golden import fixtures
+from tests.gpu_util import assert_close, cmu_model, cuda_batch
+
+pytestmark = pytest.mark.gpu
+CMU = [n for n in fixtures.names('model') if fixtures.load(n)[0]['family'] == 'cmu']
+
+
+@pytest.mark.parametrize('name', CMU)
+def test_concat_trans_autograd(name, cuda):
+    from mep_amd import cmu_mosei
+    meta, gold = fixtures.load(name)
+    model = cmu_model(meta, cuda)
+    model.train()
+    l, v, a, lm, vm, am, labels = cuda_batch(meta, cuda)
+    logits = model(l, v, a, lm, vm, am)
+    assert_close(logits, gold['logits'], 1e-4, 1e-6, 'logits')
+    loss = cmu_mosei.multi_circle_loss(logits, labels).mean()
+    assert_close(loss.reshape(()), gold['loss'], 1e-4, 0, 'loss')
+    loss.backward()
+    coef = float(gold['clipcoef'])
+    for k, p in model.named_parameters():
+        if 'nograd/' + k in gold:
+            assert p.grad is None, k
+            continue
+        g = p.grad * coef  # fixture holds post-clip gradients
+        if meta['full']:
+            assert_close(g, gold['grad/' + k], 1e-3, 1e-5, k)
+        else:
+            assert_close(g.reshape(-1)[:256], gold['gradhead/' + k], 1e-3, 1e-5, k)
+            assert_close(torch.linalg.vector_norm(g.double()), gold['gradnorm/' + k], 1e-3, 0, k)
+
+
+@pytest.mark.parametrize('graph', [False, True])
+@pytest.mark.parametrize('name', CMU)
+def test_concat_trans_engine_step(name, graph, cuda):
+    from mep_amd.engine import TrainEngine
+    from mep_amd.optim import FusedAdamW
+    meta, gold = fixtures.load(name)
+    model = cmu_model(meta, cuda)
+    model.train()
+    opt = FusedAdamW(model, lr=1e-3)
+    eng = TrainEngine(model, opt, clip=1.0, graph=graph)
+    batch = cuda_batch(meta, cuda)
+    losses = [float(eng.step(*batch).item()) for _ in range(meta['steps'])]
+    assert_close(losses[0], gold['loss'], 1e-4, 0, 'loss')
+    if meta['steps'] == 1:
+        assert_close(opt.gnorm.reshape(()), gold['gnorm'], 1e-4, 0, 'gnorm')
+    for k, p in model.named_parameters():
+        ref = gold['post/' + k] if meta['full'] else gold['posthead/' + k]
+        got = p.detach() if meta['full'] else p.detach().reshape(-1)[:256]
+        err = (got.double().cpu() - torch.as_tensor(ref).double()).abs().max().item()
+        assert err <= 2e-5, (k, err)
+    model.eval()
+    with torch.no_grad():
+        logits2 = model(*batch[:6])
+    assert_close(logits2, gold['logits2'], 1e-3, 1e-5, 'logits2')
+
+
+@pytest.mark.parametrize('name', fixtures.names('block'))
+def test_attention_block_standalone(name, cuda):
+    import numpy as np
+    from mep_amd import cmu_mosei
+    meta, gold = fixtures.load(name)
+    if meta['family'] != 'cmu':
+        pytest.skip('realformer block covered by test_gpu_realformer')
+    c = meta['ctor']
+    blk = cmu_mosei.Attention_Block(c['dim'], c['n_heads'], c['ffn'])
+    from tests.gpu_util import load_params
+    load_params(blk, meta)
+    blk = blk.to(cuda)
+    q, kv, mask, s_prev, g_out = fixtures.block_inputs(meta)
+    qt = torch.tensor(q, device=cuda, requires_grad=True)
+    kvt = torch.tensor(kv, device=cuda, requires_grad=True)
+    sp = torch.tensor(s_prev, device=cuda, requires_grad=True) if s_prev is not None else None
+    y, s = blk(qt, kvt, kvt, torch.tensor(mask, device=cuda), sp)
+    assert_close(y, gold['out'], 1e-4, 1e-6, 'out')
+    assert_close(s, gold['scores'], 1e-6, 1e-12, 'scores')
+    obj = (y * torch.tensor(g_out, device=cuda)).sum()
+    if meta['g_scores']:
+        obj = obj + (s * torch.tensor(gold['g_scores'], device=cuda)).sum()
+    obj.backward()
+    assert_close(qt.grad, gold['grad_q'], 1e-3, 1e-5, 'grad_q')
+    assert_close(kvt.grad, gold['grad_kv'], 1e-3, 1e-5, 'grad_kv')
+    if sp is not None:
+        assert_close(sp.grad, gold['grad_sprev'], 1e-3, 1e-5, 'grad_sprev')
+    for k, p in blk.named_parameters():
+        if 'nograd/' + k in gold:
+            assert p.grad is None, k
+        else:
+            assert_close(p.grad, gold['grad/' + k], 1e-3, 1e-5, k)
+    assert np.isfinite(y.detach().cpu().numpy()).all()
