@@ -66,19 +66,24 @@ typedef struct {
 int mep_gemm(const mep_gemm_desc* descs, int n_desc, int max_tiles, mep_stream_t stream);
 
 /* ---------------------------------------------------------------- weight-gradient GEMM
- * partial[split, n, k] = sum_{tok in split} A[tok, n] * Bm[tok, k]   (dW = dY^T X)
- * then out[n*ldo + k] (+)= sum_split partial.  Replaces autograd's weight-gradient mm of every
- * nn.Linear on the path.  `tok_per_split` tokens per split; partial is a workspace of
- * n_split*N*K floats. */
+ * dW_i[n, k] (+)= sum_tok A[tok, n] * B_i[tok, k]   for up to 4 operands B_i sharing one A
+ * (dW = dY^T X of every nn.Linear on the path; e.g. minus.weight = dZ^T [q | xp] is one
+ * descriptor with two B operands).  One workgroup owns a token chunk (tok_per_split rows) and a
+ * 256-wide column group of the concatenated K, computes the whole N x 256 partial with f32 MFMA
+ * (each input element read once), and writes partial[split][n][k]; mep_wgrad_reduce sums the
+ * splits in a fixed order into out_i.  N <= 128; partial holds n_split * N * Ktot floats.
+ * Grid: mep_wgrad max_tiles = max(n_split * ceil(Ktot/256)); mep_wgrad_reduce max_tiles =
+ * max(ceil(N*Ktot/256)). */
+#define MEP_WG_MAX_B 4
 typedef struct {
-    mep_rows a;        /* [ntok, N]  (dY)                 */
-    mep_rows b;        /* [ntok, K]  (X)                  */
-    uint64_t partial;  /* workspace [n_split][N][K]       */
-    uint64_t out;      /* [N][ldo] gradient               */
-    int32_t  ntok, N, K, ldo;
-    int32_t  tok_per_split, n_split;
-    int32_t  accumulate;
-    int32_t  _pad;
+    mep_rows a;                  /* [ntok, N]  (dY)                           */
+    mep_rows b[MEP_WG_MAX_B];    /* [ntok, K_i]                               */
+    uint64_t out[MEP_WG_MAX_B];  /* dW_i: [N][ldo_i]                          */
+    int32_t  kb[MEP_WG_MAX_B];   /* K_i                                       */
+    int32_t  ldo[MEP_WG_MAX_B];
+    uint64_t partial;            /* workspace [n_split][N][Ktot]              */
+    int32_t  n_b, ntok, N, Ktot;
+    int32_t  tok_per_split, n_split, accumulate, _pad;
 } mep_wgrad_desc;
 int mep_wgrad(const mep_wgrad_desc* descs, int n_desc, int max_tiles, mep_stream_t stream);
 int mep_wgrad_reduce(const mep_wgrad_desc* descs, int n_desc, int max_tiles, mep_stream_t stream);
@@ -101,7 +106,10 @@ typedef struct {
     uint64_t stats;     /* [B,H,Tq,2]: row max, 1/row sum                       */
     int32_t  B, H, Tq, Tk;
 } mep_attn_desc;
-int mep_attn_fwd(const mep_attn_desc* descs, int n_desc, int max_tiles, mep_stream_t stream);
+/* Launch geometry (the host knows every shape): R = 512 / H rows per workgroup, one lane per
+ * (row, head); threads = 64 * ceil(H * min(T, R) / 64) maximised over descriptors (T = Tq, and
+ * also Tk for the backward); max_tiles = max B * ceil(Tq / R) (+ B * ceil(Tk / R) backward). */
+int mep_attn_fwd(const mep_attn_desc* descs, int n_desc, int max_tiles, int threads, mep_stream_t stream);
 
 /* Backward of the attention core.  Inputs dx (grad of X), the forward's q/k/v/x/stats/s_prev.
  * Outputs: dq += (written with accumulate semantics onto dq_base), dk, dv (dk==dv pointer ->
@@ -117,7 +125,7 @@ typedef struct {
     uint64_t ds_prev;   /* [B,H,Tq,Tk] or 0                        */
     uint64_t dc_partial;/* [B * ceil(Tk/64)] floats or 0           */
 } mep_attn_bwd_desc;
-int mep_attn_bwd(const mep_attn_bwd_desc* descs, int n_desc, int max_tiles, mep_stream_t stream);
+int mep_attn_bwd(const mep_attn_bwd_desc* descs, int n_desc, int max_tiles, int threads, mep_stream_t stream);
 
 /* ---------------------------------------------------------------- cmu / Ren-MME block epilogue
  * xp = drop(x @ Wp^T);  z = [q | xp] @ Wm^T;  out = drop(LayerNorm(z))
@@ -132,7 +140,8 @@ typedef struct {
     float    drop_p;
     int32_t  drop_stream;/* distinct per block */
 } mep_epi_desc;
-int mep_block_epi_fwd(const mep_epi_desc* descs, int n_desc, int max_tiles, mep_stream_t stream);
+/* D (32/64/96/128, shared by every descriptor of the launch) selects the compiled variant. */
+int mep_block_epi_fwd(const mep_epi_desc* descs, int n_desc, int max_tiles, int D, mep_stream_t stream);
 
 /* Backward: dout -> (dropout) -> LN backward -> dz;  dq_direct = dz Wm[:, :D];
  * dxp = drop'(dz Wm[:, D:]);  dx = dxp Wp.  Writes dz, dxp, dx, dq and per-tile LayerNorm
@@ -147,7 +156,7 @@ typedef struct {
     int32_t  dq_accumulate;
     int32_t  _pad;
 } mep_epi_bwd_desc;
-int mep_block_epi_bwd(const mep_epi_bwd_desc* descs, int n_desc, int max_tiles, mep_stream_t stream);
+int mep_block_epi_bwd(const mep_epi_bwd_desc* descs, int n_desc, int max_tiles, int D, mep_stream_t stream);
 
 /* ---------------------------------------------------------------- row LayerNorm (D <= 256)
  * Ren-MME's shared unify LayerNorm (Ren-MME/run.py:164-166).  fwd: y = LN(x); bwd: dx from dy,

@@ -26,9 +26,12 @@ class GemmDesc(ctypes.Structure):
                 ('accumulate', i32), ('relu', i32), ('alpha', f32)]
 
 
+WG_MAX_B = 4
+
+
 class WgradDesc(ctypes.Structure):
-    _fields_ = [('a', Rows), ('b', Rows), ('partial', u64), ('out', u64),
-                ('ntok', i32), ('N', i32), ('K', i32), ('ldo', i32),
+    _fields_ = [('a', Rows), ('b', Rows * WG_MAX_B), ('out', u64 * WG_MAX_B), ('kb', i32 * WG_MAX_B),
+                ('ldo', i32 * WG_MAX_B), ('partial', u64), ('n_b', i32), ('ntok', i32), ('N', i32), ('Ktot', i32),
                 ('tok_per_split', i32), ('n_split', i32), ('accumulate', i32), ('_pad', i32)]
 
 
@@ -97,10 +100,12 @@ STRUCTS = {'mep_rows': Rows, 'mep_gemm_desc': GemmDesc, 'mep_wgrad_desc': WgradD
 
 P = ctypes.c_void_p
 # name -> argtypes (all return int)
-GROUPED = ['mep_gemm', 'mep_wgrad', 'mep_wgrad_reduce', 'mep_attn_fwd', 'mep_attn_bwd', 'mep_block_epi_fwd',
-           'mep_block_epi_bwd', 'mep_layernorm_fwd', 'mep_layernorm_bwd', 'mep_colsum', 'mep_sum_rows',
+GROUPED = ['mep_gemm', 'mep_wgrad', 'mep_wgrad_reduce', 'mep_layernorm_fwd', 'mep_layernorm_bwd', 'mep_colsum', 'mep_sum_rows',
            'mep_pool_fwd', 'mep_pool_bwd']
+GROUPED_T = ['mep_attn_fwd', 'mep_attn_bwd',      # + threads per workgroup
+             'mep_block_epi_fwd', 'mep_block_epi_bwd']  # + D (compiled variant)
 SIGNATURES = {name: [P, i32, i32, P] for name in GROUPED}
+SIGNATURES.update({name: [P, i32, i32, i32, P] for name in GROUPED_T})
 HP = ctypes.POINTER(HeadDesc)
 SIGNATURES.update({
     'mep_head_fwd_bwd': [HP, P],
@@ -182,12 +187,30 @@ class DescArray:
         return ctypes.c_void_p(self.dev.data_ptr() if self.dev is not None else 0)
 
 
-def launch(name, descs, max_tiles, stream=None):
+def launch(name, descs, max_tiles, stream=None, threads=None):
+    """threads: the extra int argument of the GROUPED_T launchers (threads or D)."""
     if descs.n == 0 or max_tiles <= 0:
         return
     fn = getattr(lib(), name)
     if TIMER is not None:
         TIMER.begin(name)
-    check(fn(descs.ptr, descs.n, int(max_tiles), stream_ptr(stream)), name)
+    if threads is None:
+        rc = fn(descs.ptr, descs.n, int(max_tiles), stream_ptr(stream))
+    else:
+        rc = fn(descs.ptr, descs.n, int(max_tiles), int(threads), stream_ptr(stream))
+    check(rc, name)
     if TIMER is not None:
         TIMER.end(name)
+
+
+def attn_geometry(shapes):
+    """shapes: [(B, H, Tq, Tk)] -> (fwd tiles, bwd tiles, fwd threads, bwd threads) following the
+    launch rule of include/mep.h (R = 512 // H rows per workgroup, one lane per (row, head))."""
+    ft = bt = fth = bth = 0
+    for (B, H, Tq, Tk) in shapes:
+        R = 512 // H
+        ft = max(ft, B * -(-Tq // R))
+        bt = max(bt, B * (-(-Tq // R) + -(-Tk // R)))
+        fth = max(fth, 64 * -(-(H * min(Tq, R)) // 64))
+        bth = max(bth, 64 * -(-(H * max(min(Tq, R), min(Tk, R))) // 64))
+    return ft, bt, fth, bth

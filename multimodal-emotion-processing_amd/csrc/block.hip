@@ -2,11 +2,13 @@
 //
 // Forward (cmu-mosei/run.py:257-261; Ren-MME/run.py:209-213 with dropout and norm2):
 //   xp = drop(x Wp^T);  z = [q | xp] Wm^T;  out = drop(LayerNorm(z))
-// One workgroup = 64 tokens x D columns (D <= 128), 8 waves; each wave owns one 32x32 output
-// block of the (2 x D/32) task grid and runs f32 MFMA 32x32x2 over LDS-staged token tiles with
-// the weights read from L2.  The two Linears are chained through LDS (xp never round-trips HBM
-// before it is consumed) and the LayerNorm is a wave-per-row shuffle reduction.  The concat
-// [q | xp] is never materialised: the minus Linear is two accumulating MFMA passes.
+// One workgroup = 64 tokens x D columns (D in {32, 64, 96, 128}, a template parameter so every
+// K loop is fully unrolled and hipcc issues the weight loads of a whole chain ahead of its
+// MFMAs), 8 waves; each wave owns one 32x32 output block of the (2 x D/32) task grid and runs
+// f32 MFMA 32x32x2 over LDS-staged token tiles with the weights read from L2.  The two Linears
+// are chained through LDS (xp is consumed before it ever returns from HBM) and the LayerNorm is
+// a wave-per-row shuffle reduction.  The concat [q | xp] is never materialised: the minus
+// Linear is two accumulating MFMA passes.
 #include "common.h"
 
 using namespace mep;
@@ -14,36 +16,55 @@ using namespace mep;
 namespace {
 
 constexpr int THREADS = 512;
-constexpr int LDMAX = 128 + 4;
 constexpr float LN_EPS = 1e-5f;
 
 MEP_DEV bool vec_ok(uint64_t p, int ld) { return ((p & 15) == 0) && (ld % 4 == 0); }
 
+// stage 64 token rows x D columns of a row view into LDS [64][D+4]
+template <int D>
+MEP_DEV void stage(float* dst, const mep_rows& src, int tok0, int ntok) {
+    constexpr int LD = D + 4;
+    constexpr int V = D / 4;  // float4 per row
+    const bool vec = ((src.ptr & 15) == 0) && (src.sB % 4 == 0) && (src.sT % 4 == 0);
+    for (int idx = threadIdx.x; idx < 64 * V; idx += THREADS) {
+        const int row = idx / V, c4 = idx - row * V;
+        const int tok = tok0 + row;
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (tok < ntok) {
+            const float* p = row_ptr(src, tok) + 4 * c4;
+            if (vec) v = *reinterpret_cast<const float4*>(p);
+            else v = make_float4(p[0], p[1], p[2], p[3]);
+        }
+        *reinterpret_cast<float4*>(dst + row * LD + 4 * c4) = v;
+    }
+}
+
+template <int D>
 __global__ __launch_bounds__(THREADS) void k_epi_fwd(const mep_epi_desc* __restrict__ descs) {
     const mep_epi_desc& d = descs[blockIdx.y];
     const int tok0 = blockIdx.x * 64;
     if (tok0 >= d.ntok) return;
-    const int D = d.D, LD = D + 4;
-    __shared__ __attribute__((aligned(16))) float smem[3 * 64 * LDMAX];
+    constexpr int LD = D + 4;
+    __shared__ __attribute__((aligned(16))) float smem[3 * 64 * LD];
     float* Xs = smem;                 // x, later z
     float* Qs = smem + 64 * LD;
     float* Ps = smem + 2 * 64 * LD;   // xp (post-dropout)
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int ntask = 2 * (D / 32);
+    constexpr int NTASK = 2 * (D / 32);
     const int mh = wave & 1, nblk = wave >> 1;
-    const bool task = wave < ntask;
+    const bool task = wave < NTASK;
     const int col = nblk * 32 + (lane & 31);
     const float* Wp = reinterpret_cast<const float*>(d.wp);
     const float* Wm = reinterpret_cast<const float*>(d.wm);
     const float p = d.drop_p;
     const uint64_t seed = (d.seed && p > 0.f) ? *reinterpret_cast<const uint64_t*>(d.seed) : 0;
 
-    load_tile(Xs, LD, d.x, tok0, d.ntok, 0, D, D, D);
-    load_tile(Qs, LD, d.q, tok0, d.ntok, 0, D, D, D);
+    stage<D>(Xs, d.x, tok0, d.ntok);
+    stage<D>(Qs, d.q, tok0, d.ntok);
     __syncthreads();
     floatx16 acc = zero16();
     if (task) {
-        mma_tile<true>(acc, Xs, LD, mh * 32, Wp, D, nblk * 32, D, 0, D, D, vec_ok(d.wp, D));
+        mma_tile<true, D>(acc, Xs, LD, mh * 32, Wp, D, nblk * 32, D, 0, D, D, vec_ok(d.wp, D));
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
             const int row = mh * 32 + acc_row(r, lane);
@@ -58,8 +79,8 @@ __global__ __launch_bounds__(THREADS) void k_epi_fwd(const mep_epi_desc* __restr
     if (task) {
         acc = zero16();
         const bool wv = vec_ok(d.wm, 2 * D);
-        mma_tile<true>(acc, Qs, LD, mh * 32, Wm, 2 * D, nblk * 32, D, 0, D, D, wv);
-        mma_tile<true>(acc, Ps, LD, mh * 32, Wm + D, 2 * D, nblk * 32, D, 0, D, D, wv);
+        mma_tile<true, D>(acc, Qs, LD, mh * 32, Wm, 2 * D, nblk * 32, D, 0, D, D, wv);
+        mma_tile<true, D>(acc, Ps, LD, mh * 32, Wm + D, 2 * D, nblk * 32, D, 0, D, D, wv);
     }
     __syncthreads();  // everyone done reading Xs (x) before it becomes z
     if (task) {
@@ -76,10 +97,12 @@ __global__ __launch_bounds__(THREADS) void k_epi_fwd(const mep_epi_desc* __restr
     const float* lw = reinterpret_cast<const float*>(d.ln_w);
     const float* lb = reinterpret_cast<const float*>(d.ln_b);
     float* stats = reinterpret_cast<float*>(d.stats);
+    const bool c0 = lane < D, c1 = lane + 64 < D;
+    const float w0 = c0 ? lw[lane] : 0.f, w1 = c1 ? lw[lane + 64] : 0.f;
+    const float b0 = c0 ? lb[lane] : 0.f, b1 = c1 ? lb[lane + 64] : 0.f;
     for (int row = wave; row < 64; row += THREADS / 64) {
         const int tok = tok0 + row;
         if (tok >= d.ntok) break;
-        const bool c0 = lane < D, c1 = lane + 64 < D;
         const float x0 = c0 ? Xs[row * LD + lane] : 0.f;
         const float x1 = c1 ? Xs[row * LD + lane + 64] : 0.f;
         const float mean = wave_sum(x0 + x1) / (float)D;
@@ -88,12 +111,12 @@ __global__ __launch_bounds__(THREADS) void k_epi_fwd(const mep_epi_desc* __restr
         const float rstd = 1.0f / sqrtf(var + LN_EPS);
         float* out = row_ptr(d.out, tok);
         if (c0) {
-            float y = d0 * rstd * lw[lane] + lb[lane];
+            float y = d0 * rstd * w0 + b0;
             if (p > 0.f) y *= drop_scale(seed, 2u * d.drop_stream + 1u, (uint64_t)tok * D + lane, p);
             out[lane] = y;
         }
         if (c1) {
-            float y = d1 * rstd * lw[lane + 64] + lb[lane + 64];
+            float y = d1 * rstd * w1 + b1;
             if (p > 0.f) y *= drop_scale(seed, 2u * d.drop_stream + 1u, (uint64_t)tok * D + lane + 64, p);
             out[lane + 64] = y;
         }
@@ -101,13 +124,14 @@ __global__ __launch_bounds__(THREADS) void k_epi_fwd(const mep_epi_desc* __restr
     }
 }
 
+template <int D>
 __global__ __launch_bounds__(THREADS) void k_epi_bwd(const mep_epi_bwd_desc* __restrict__ descs) {
     const mep_epi_bwd_desc& bd = descs[blockIdx.y];
     const mep_epi_desc& d = bd.f;
     const int tok0 = blockIdx.x * 64;
     if (tok0 >= d.ntok) return;
-    const int D = d.D, LD = D + 4;
-    __shared__ __attribute__((aligned(16))) float smem[2 * 64 * LDMAX + 8 * 2 * 128];
+    constexpr int LD = D + 4;
+    __shared__ __attribute__((aligned(16))) float smem[2 * 64 * LD + 8 * 2 * 128];
     float* Gs = smem;                 // dout -> dz
     float* Ps = smem + 64 * LD;       // dxp
     float* red = smem + 2 * 64 * LD;  // [8 waves][2][128]
@@ -115,15 +139,15 @@ __global__ __launch_bounds__(THREADS) void k_epi_bwd(const mep_epi_bwd_desc* __r
     const float p = d.drop_p;
     const uint64_t seed = (d.seed && p > 0.f) ? *reinterpret_cast<const uint64_t*>(d.seed) : 0;
 
-    for (int idx = threadIdx.x; idx < 64 * D; idx += THREADS) {
-        const int row = idx / D, c = idx - row * D;
-        const int tok = tok0 + row;
-        float v = 0.f;
-        if (tok < d.ntok) {
-            v = row_ptr(bd.dout, tok)[c];
-            if (bd.dout2.ptr) v += row_ptr(bd.dout2, tok)[c];
+    stage<D>(Gs, bd.dout, tok0, d.ntok);
+    if (bd.dout2.ptr) {
+        __syncthreads();
+        stage<D>(Ps, bd.dout2, tok0, d.ntok);
+        __syncthreads();
+        for (int idx = threadIdx.x; idx < 64 * D; idx += THREADS) {
+            const int row = idx / D, c = idx - row * D;
+            Gs[row * LD + c] += Ps[row * LD + c];
         }
-        Gs[row * LD + c] = v;
     }
     __syncthreads();
     // LayerNorm backward, wave per row
@@ -131,6 +155,7 @@ __global__ __launch_bounds__(THREADS) void k_epi_bwd(const mep_epi_bwd_desc* __r
     const float* stats = reinterpret_cast<const float*>(d.stats);
     float pw0 = 0.f, pw1 = 0.f, pb0 = 0.f, pb1 = 0.f;
     const bool c0 = lane < D, c1 = lane + 64 < D;
+    const float w0 = c0 ? lw[lane] : 0.f, w1 = c1 ? lw[lane + 64] : 0.f;
     for (int row = wave; row < 64; row += THREADS / 64) {
         const int tok = tok0 + row;
         if (tok >= d.ntok) {
@@ -148,8 +173,7 @@ __global__ __launch_bounds__(THREADS) void k_epi_bwd(const mep_epi_bwd_desc* __r
         }
         const float xh0 = c0 ? (zr[lane] - mean) * rstd : 0.f;
         const float xh1 = c1 ? (zr[lane + 64] - mean) * rstd : 0.f;
-        const float gw0 = c0 ? g0 * lw[lane] : 0.f;
-        const float gw1 = c1 ? g1 * lw[lane + 64] : 0.f;
+        const float gw0 = g0 * w0, gw1 = g1 * w1;
         const float s1 = wave_sum(gw0 + gw1) / (float)D;
         const float s2 = wave_sum(gw0 * xh0 + gw1 * xh1) / (float)D;
         pw0 += g0 * xh0; pw1 += g1 * xh1; pb0 += g0; pb1 += g1;
@@ -167,21 +191,22 @@ __global__ __launch_bounds__(THREADS) void k_epi_bwd(const mep_epi_bwd_desc* __r
         for (int idx = threadIdx.x; idx < 2 * D; idx += THREADS) {
             const int which = idx / D, c = idx - which * D;
             float s = 0.f;
+#pragma unroll
             for (int w = 0; w < THREADS / 64; ++w) s += red[(w * 2 + which) * 128 + c];
             lp[idx] = s;
         }
     }
     // dq_direct = dz Wm[:, :D];  dxp = drop'(dz Wm[:, D:])
-    const int ntask = 2 * (D / 32);
+    constexpr int NTASK = 2 * (D / 32);
     const int mh = wave & 1, nblk = wave >> 1;
-    const bool task = wave < ntask;
+    const bool task = wave < NTASK;
     const int col = nblk * 32 + (lane & 31);
     const float* Wm = reinterpret_cast<const float*>(d.wm);
     const float* Wp = reinterpret_cast<const float*>(d.wp);
     if (task) {
         floatx16 aq = zero16(), ap = zero16();
-        mma_tile<false>(aq, Gs, LD, mh * 32, Wm, 2 * D, nblk * 32, D, 0, D, D, false);
-        mma_tile<false>(ap, Gs, LD, mh * 32, Wm + D, 2 * D, nblk * 32, D, 0, D, D, false);
+        mma_tile<false, D>(aq, Gs, LD, mh * 32, Wm, 2 * D, nblk * 32, D, 0, D, D, false);
+        mma_tile<false, D>(ap, Gs, LD, mh * 32, Wm + D, 2 * D, nblk * 32, D, 0, D, D, false);
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
             const int row = mh * 32 + acc_row(r, lane);
@@ -199,7 +224,7 @@ __global__ __launch_bounds__(THREADS) void k_epi_bwd(const mep_epi_bwd_desc* __r
     __syncthreads();
     if (task) {
         floatx16 ax = zero16();
-        mma_tile<false>(ax, Ps, LD, mh * 32, Wp, D, nblk * 32, D, 0, D, D, false);
+        mma_tile<false, D>(ax, Ps, LD, mh * 32, Wp, D, nblk * 32, D, 0, D, D, false);
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
             const int tok = tok0 + mh * 32 + acc_row(r, lane);
@@ -288,17 +313,36 @@ __global__ __launch_bounds__(256) void k_ln_bwd(const mep_ln_desc* __restrict__ 
     }
 }
 
+template <typename F>
+int dispatch_D(int D, F&& f) {
+    switch (D) {
+        case 32: f(std::integral_constant<int, 32>{}); return 0;
+        case 64: f(std::integral_constant<int, 64>{}); return 0;
+        case 96: f(std::integral_constant<int, 96>{}); return 0;
+        case 128: f(std::integral_constant<int, 128>{}); return 0;
+        default: return MEP_EINVAL;
+    }
+}
+
 }  // namespace
 
-extern "C" int mep_block_epi_fwd(const mep_epi_desc* descs, int n_desc, int max_tiles, mep_stream_t stream) {
+extern "C" int mep_block_epi_fwd(const mep_epi_desc* descs, int n_desc, int max_tiles, int D, mep_stream_t stream) {
     if (n_desc <= 0 || max_tiles <= 0) return 0;
-    hipLaunchKernelGGL(k_epi_fwd, dim3(max_tiles, n_desc), dim3(THREADS), 0, (hipStream_t)stream, descs);
+    const int rc = dispatch_D(D, [&](auto dc) {
+        hipLaunchKernelGGL(k_epi_fwd<decltype(dc)::value>, dim3(max_tiles, n_desc), dim3(THREADS), 0,
+                           (hipStream_t)stream, descs);
+    });
+    if (rc) { mep_set_error("mep_block_epi_fwd: D must be 32, 64, 96 or 128"); return rc; }
     return mep_check_launch("mep_block_epi_fwd");
 }
 
-extern "C" int mep_block_epi_bwd(const mep_epi_bwd_desc* descs, int n_desc, int max_tiles, mep_stream_t stream) {
+extern "C" int mep_block_epi_bwd(const mep_epi_bwd_desc* descs, int n_desc, int max_tiles, int D, mep_stream_t stream) {
     if (n_desc <= 0 || max_tiles <= 0) return 0;
-    hipLaunchKernelGGL(k_epi_bwd, dim3(max_tiles, n_desc), dim3(THREADS), 0, (hipStream_t)stream, descs);
+    const int rc = dispatch_D(D, [&](auto dc) {
+        hipLaunchKernelGGL(k_epi_bwd<decltype(dc)::value>, dim3(max_tiles, n_desc), dim3(THREADS), 0,
+                           (hipStream_t)stream, descs);
+    });
+    if (rc) { mep_set_error("mep_block_epi_bwd: D must be 32, 64, 96 or 128"); return rc; }
     return mep_check_launch("mep_block_epi_bwd");
 }
 

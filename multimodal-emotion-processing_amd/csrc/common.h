@@ -68,7 +68,40 @@ MEP_DEV int acc_row(int r, int lane) { return (r & 3) + 8 * (r >> 2) + 4 * (lane
 // K is traversed in groups of 8: lane half h covers k = 8g + 4h + j at step 4g + j (the sum
 // over k is order-free; this lets each lane fetch 4 consecutive k with one 16-byte read).
 // W(n,k): NT -> W[n*ldw + k] (nn.Linear weight), else W[k*ldw + n].
+// KC > 0: compile-time chunk width (fully unrolled, so hipcc issues every weight load of the
+// chunk ahead of the MFMA chain); KC == 0: runtime width kc.
 template <bool NT>
+MEP_DEV void mma_step(floatx16& acc, const float* __restrict__ arow, const float* __restrict__ W, int ldw, int n,
+                      bool nval, int kk, int kg, int K, bool w_vec) {
+    const float4 a = *reinterpret_cast<const float4*>(arow + kk);
+    float b0 = 0.f, b1 = 0.f, b2 = 0.f, b3 = 0.f;
+    if (NT) {
+        const float* wp = W + (int64_t)n * ldw + kg;
+        if (nval && w_vec && kg + 3 < K) {
+            const float4 b = *reinterpret_cast<const float4*>(wp);
+            b0 = b.x; b1 = b.y; b2 = b.z; b3 = b.w;
+        } else if (nval) {
+            if (kg < K) b0 = wp[0];
+            if (kg + 1 < K) b1 = wp[1];
+            if (kg + 2 < K) b2 = wp[2];
+            if (kg + 3 < K) b3 = wp[3];
+        }
+    } else {
+        if (nval) {
+            const float* wp = W + (int64_t)kg * ldw + n;
+            if (kg < K) b0 = wp[0];
+            if (kg + 1 < K) b1 = wp[ldw];
+            if (kg + 2 < K) b2 = wp[2 * ldw];
+            if (kg + 3 < K) b3 = wp[3 * ldw];
+        }
+    }
+    acc = mfma32(a.x, b0, acc);
+    acc = mfma32(a.y, b1, acc);
+    acc = mfma32(a.z, b2, acc);
+    acc = mfma32(a.w, b3, acc);
+}
+
+template <bool NT, int KC = 0>
 MEP_DEV void mma_tile(floatx16& acc, const float* __restrict__ As, int lda, int m0,
                       const float* __restrict__ W, int ldw, int n0, int N, int k0, int kc, int K,
                       bool w_vec) {
@@ -78,34 +111,11 @@ MEP_DEV void mma_tile(floatx16& acc, const float* __restrict__ As, int lda, int 
     const float* arow = As + (m0 + r) * lda + 4 * h;
     const int n = n0 + r;
     const bool nval = n < N;
-    for (int kk = 0; kk < kc; kk += 8) {
-        const float4 a = *reinterpret_cast<const float4*>(arow + kk);
-        const int kg = k0 + kk + 4 * h;
-        float b0 = 0.f, b1 = 0.f, b2 = 0.f, b3 = 0.f;
-        if (NT) {
-            const float* wp = W + (int64_t)n * ldw + kg;
-            if (nval && w_vec && kg + 3 < K) {
-                const float4 b = *reinterpret_cast<const float4*>(wp);
-                b0 = b.x; b1 = b.y; b2 = b.z; b3 = b.w;
-            } else if (nval) {
-                if (kg < K) b0 = wp[0];
-                if (kg + 1 < K) b1 = wp[1];
-                if (kg + 2 < K) b2 = wp[2];
-                if (kg + 3 < K) b3 = wp[3];
-            }
-        } else {
-            if (nval) {
-                const float* wp = W + (int64_t)kg * ldw + n;
-                if (kg < K) b0 = wp[0];
-                if (kg + 1 < K) b1 = wp[ldw];
-                if (kg + 2 < K) b2 = wp[2 * ldw];
-                if (kg + 3 < K) b3 = wp[3 * ldw];
-            }
-        }
-        acc = mfma32(a.x, b0, acc);
-        acc = mfma32(a.y, b1, acc);
-        acc = mfma32(a.z, b2, acc);
-        acc = mfma32(a.w, b3, acc);
+    if (KC > 0) {
+#pragma unroll
+        for (int kk = 0; kk < KC; kk += 8) mma_step<NT>(acc, arow, W, ldw, n, nval, kk, k0 + kk + 4 * h, K, w_vec);
+    } else {
+        for (int kk = 0; kk < kc; kk += 8) mma_step<NT>(acc, arow, W, ldw, n, nval, kk, k0 + kk + 4 * h, K, w_vec);
     }
 }
 

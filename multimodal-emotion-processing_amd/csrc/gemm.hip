@@ -6,8 +6,7 @@
 //            L2 with 16-byte loads.  Replaces Unify_Dimension's Linear (cmu-mosei/run.py:210-214),
 //            the Conv1d k=1 unify + position add (others/realformer.py:136-152,224-227) and the
 //            realformer w_qkv / FFN Linears (others/realformer.py:157,163-168).
-// mep_wgrad: partial[split][n][k] = sum_{tok in split} A[tok,n] B[tok,k]; workgroup tile
-//            64 x 64 (4 waves of 32x32), tokens streamed through LDS 32 at a time.
+// mep_wgrad: dW_i = A^T B_i over token chunks (see the kernel comment below).
 #include "common.h"
 
 using namespace mep;
@@ -51,10 +50,16 @@ __global__ __launch_bounds__(GEMM_THREADS) void k_gemm(const mep_gemm_desc* __re
                 const int task = wave + 8 * t;
                 if (task < ntask) {
                     const int mh = task & 1, n0 = cg + (task >> 1) * 32;
-                    if (d.w_nt)
+                    if (kc_pad == GEMM_KC) {   // full chunk: unrolled, weight loads issued up front
+                        if (d.w_nt)
+                            mma_tile<true, GEMM_KC>(acc[t], As, GEMM_LDA, mh * 32, W, d.ldw, n0, d.N, k0, kc_pad, d.K, w_vec);
+                        else
+                            mma_tile<false, GEMM_KC>(acc[t], As, GEMM_LDA, mh * 32, W, d.ldw, n0, d.N, k0, kc_pad, d.K, false);
+                    } else if (d.w_nt) {
                         mma_tile<true>(acc[t], As, GEMM_LDA, mh * 32, W, d.ldw, n0, d.N, k0, kc_pad, d.K, w_vec);
-                    else
+                    } else {
                         mma_tile<false>(acc[t], As, GEMM_LDA, mh * 32, W, d.ldw, n0, d.N, k0, kc_pad, d.K, false);
+                    }
                 }
             }
         }
@@ -83,69 +88,101 @@ __global__ __launch_bounds__(GEMM_THREADS) void k_gemm(const mep_gemm_desc* __re
 }
 
 // ---------------------------------------------------------------- weight gradient
-constexpr int WG_THREADS = 256;
-constexpr int WG_TT = 32;          // tokens per LDS stage
-constexpr int WG_LD = 64 + 4;
+// One workgroup = (token chunk, 256-column group of the concatenated K).  It stages 32 tokens of
+// A [32 x N] and of the B operands [32 x 256] in LDS per step and accumulates the whole
+// N x 256 partial (<= 4 x 8 tiles of 32x32, <= 4 per wave) with f32 MFMA, so every input
+// element is read from HBM once per column group.
+constexpr int WG_THREADS = 512;
+constexpr int WG_TT = 32;
+constexpr int WG_KG = 256;
+constexpr int WG_NMAX = 128;
+constexpr int WG_MAXT = 4;
+
+MEP_DEV int wg_koff(const mep_wgrad_desc& d, int i) {
+    int o = 0;
+    for (int j = 0; j < i; ++j) o += d.kb[j];
+    return o;
+}
 
 __global__ __launch_bounds__(WG_THREADS) void k_wgrad(const mep_wgrad_desc* __restrict__ descs) {
     const mep_wgrad_desc& d = descs[blockIdx.y];
-    const int ntn = (d.N + 63) / 64, ntk = (d.K + 63) / 64;
-    const int tiles = ntn * ntk * d.n_split;
-    if ((int)blockIdx.x >= tiles) return;
-    const int split = blockIdx.x / (ntn * ntk);
-    const int rem = blockIdx.x - split * ntn * ntk;
-    const int tn = rem / ntk, tk = rem - (rem / ntk) * ntk;
-    const int n0 = tn * 64, kq0 = tk * 64;
+    const int nkg = (d.Ktot + WG_KG - 1) / WG_KG;
+    if ((int)blockIdx.x >= d.n_split * nkg) return;
+    const int split = blockIdx.x / nkg, kg = blockIdx.x - (blockIdx.x / nkg) * nkg;
     const int t_begin = split * d.tok_per_split;
     const int t_end = min(d.ntok, t_begin + d.tok_per_split);
+    const int kbase = kg * WG_KG, kcnt = min(WG_KG, d.Ktot - kbase);
+    const int ntn = (d.N + 31) / 32, ntk = (kcnt + 31) / 32, ntask = ntn * ntk;
 
-    __shared__ __attribute__((aligned(16))) float As[WG_TT * WG_LD];
-    __shared__ __attribute__((aligned(16))) float Bs[WG_TT * WG_LD];
+    __shared__ __attribute__((aligned(16))) float As[WG_TT * WG_NMAX];
+    __shared__ __attribute__((aligned(16))) float Bs[WG_TT * WG_KG];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int wm = wave & 1, wn = wave >> 1;
-    floatx16 acc = zero16();
+    const int h = lane >> 5, r = lane & 31;
+    floatx16 acc[WG_MAXT];
+#pragma unroll
+    for (int t = 0; t < WG_MAXT; ++t) acc[t] = zero16();
+
     for (int t0 = t_begin; t0 < t_end; t0 += WG_TT) {
         __syncthreads();
-        for (int idx = threadIdx.x; idx < WG_TT * 64; idx += WG_THREADS) {
-            const int row = idx >> 6, col = idx & 63;
+        for (int idx = threadIdx.x; idx < WG_TT * d.N; idx += WG_THREADS) {
+            const int row = idx / d.N, c = idx - row * d.N;
             const int tok = t0 + row;
-            float av = 0.f, bv = 0.f;
-            if (tok < t_end) {
-                if (n0 + col < d.N) av = row_ptr(d.a, tok)[n0 + col];
-                if (kq0 + col < d.K) bv = row_ptr(d.b, tok)[kq0 + col];
+            As[row * WG_NMAX + c] = tok < t_end ? row_ptr(d.a, tok)[c] : 0.f;
+        }
+        int koff = 0;
+        for (int i = 0; i < d.n_b; ++i) {
+            const int lo = max(koff, kbase), hi = min(koff + d.kb[i], kbase + kcnt);
+            const int len = hi - lo;
+            for (int idx = threadIdx.x; len > 0 && idx < WG_TT * len; idx += WG_THREADS) {
+                const int row = idx / len, c = idx - row * len;
+                const int tok = t0 + row;
+                Bs[row * WG_KG + (lo - kbase) + c] = tok < t_end ? row_ptr(d.b[i], tok)[lo - koff + c] : 0.f;
             }
-            As[row * WG_LD + col] = av;
-            Bs[row * WG_LD + col] = bv;
+            koff += d.kb[i];
         }
         __syncthreads();
-        const int h = lane >> 5, r = lane & 31;
-#pragma unroll 4
-        for (int s = 0; s < WG_TT / 2; ++s) {
-            const int tr = 2 * s + h;
-            acc = mfma32(As[tr * WG_LD + wm * 32 + r], Bs[tr * WG_LD + wn * 32 + r], acc);
+#pragma unroll
+        for (int t = 0; t < WG_MAXT; ++t) {
+            const int task = wave + 8 * t;
+            if (task < ntask) {
+                const int tn = task % ntn, tk = task / ntn;
+                const float* ap = As + tn * 32 + r + h * WG_NMAX;
+                const float* bp = Bs + tk * 32 + r + h * WG_KG;
+#pragma unroll 8
+                for (int st = 0; st < WG_TT / 2; ++st)
+                    acc[t] = mfma32(ap[2 * st * WG_NMAX], bp[2 * st * WG_KG], acc[t]);
+            }
         }
     }
-    float* part = reinterpret_cast<float*>(d.partial) + (int64_t)split * d.N * d.K;
-    const int kcol = kq0 + wn * 32 + (lane & 31);
-    if (kcol < d.K) {
+    float* part = reinterpret_cast<float*>(d.partial) + (int64_t)split * d.N * d.Ktot;
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const int n = n0 + wm * 32 + acc_row(r, lane);
-            if (n < d.N) part[(int64_t)n * d.K + kcol] = acc[r];
+    for (int t = 0; t < WG_MAXT; ++t) {
+        const int task = wave + 8 * t;
+        if (task >= ntask) continue;
+        const int tn = task % ntn, tk = task / ntn;
+        const int kcol = tk * 32 + (lane & 31);
+        if (kcol >= kcnt) continue;
+#pragma unroll
+        for (int rr = 0; rr < 16; ++rr) {
+            const int n = tn * 32 + acc_row(rr, lane);
+            if (n < d.N) part[(int64_t)n * d.Ktot + kbase + kcol] = acc[t][rr];
         }
     }
 }
 
-__global__ void k_wgrad_reduce(const mep_wgrad_desc* __restrict__ descs) {
+__global__ __launch_bounds__(256) void k_wgrad_reduce(const mep_wgrad_desc* __restrict__ descs) {
     const mep_wgrad_desc& d = descs[blockIdx.y];
-    const int64_t nk = (int64_t)d.N * d.K;
+    const int64_t nk = (int64_t)d.N * d.Ktot;
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= nk) return;
     const float* part = reinterpret_cast<const float*>(d.partial);
     float s = 0.f;
     for (int sp = 0; sp < d.n_split; ++sp) s += part[sp * nk + i];
-    const int n = (int)(i / d.K), k = (int)(i - (int64_t)n * d.K);
-    float* o = reinterpret_cast<float*>(d.out) + (int64_t)n * d.ldo + k;
+    const int n = (int)(i / d.Ktot);
+    int k = (int)(i - (int64_t)n * d.Ktot);
+    int j = 0;
+    while (j < d.n_b - 1 && k >= d.kb[j]) { k -= d.kb[j]; ++j; }
+    float* o = reinterpret_cast<float*>(d.out[j]) + (int64_t)n * d.ldo[j] + k;
     *o = d.accumulate ? *o + s : s;
 }
 

@@ -103,26 +103,44 @@ __global__ __launch_bounds__(OPT_THREADS) void k_clip_adam(float* __restrict__ p
 __global__ void k_seed(uint64_t* seed) { seed[0] = mix64(seed[0] + 0x9E3779B97F4A7C15ull); }
 
 // ---------------------------------------------------------------- colsum / row sums
+// workgroup = 32 columns x 8 row groups; fixed-order combine (deterministic)
 __global__ __launch_bounds__(256) void k_colsum(const mep_colsum_desc* __restrict__ descs) {
     const mep_colsum_desc& d = descs[blockIdx.y];
-    const int c = blockIdx.x * 256 + threadIdx.x;
-    if (c >= d.n_cols) return;
-    const float* p = reinterpret_cast<const float*>(d.partial) + c;
+    const int cl = threadIdx.x & 31, g = threadIdx.x >> 5;
+    const int c = blockIdx.x * 32 + cl;
+    if ((int)blockIdx.x * 32 >= d.n_cols) return;
+    __shared__ float red[8][32];
     float s = 0.f;
-    for (int r = 0; r < d.n_rows; ++r) s += p[(int64_t)r * d.ld];
-    float* o = reinterpret_cast<float*>(d.out) + c;
-    *o = d.accumulate ? *o + s : s;
+    if (c < d.n_cols) {
+        const float* p = reinterpret_cast<const float*>(d.partial) + c;
+        for (int r = g; r < d.n_rows; r += 8) s += p[(int64_t)r * d.ld];
+    }
+    red[g][cl] = s;
+    __syncthreads();
+    if (g == 0 && c < d.n_cols) {
+        float t = 0.f;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) t += red[k][cl];
+        float* o = reinterpret_cast<float*>(d.out) + c;
+        *o = d.accumulate ? *o + t : t;
+    }
 }
 
+// out = sum of sources, 4 columns per thread (D % 4 == 0 for every model width)
 __global__ __launch_bounds__(256) void k_sum_rows(const mep_sum_desc* __restrict__ descs) {
     const mep_sum_desc& d = descs[blockIdx.y];
-    const int64_t total = (int64_t)d.ntok * d.D;
+    const int D4 = d.D / 4;
+    const int64_t total = (int64_t)d.ntok * D4;
     for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
-        const int tok = (int)(i / d.D), c = (int)(i - (int64_t)tok * d.D);
-        float s = 0.f;
-        for (int k = 0; k < d.n_src; ++k) s += row_ptr(d.src[k], tok)[c];
-        float* o = row_ptr(d.out, tok) + c;
-        *o = d.accumulate ? *o + s : s;
+        const int tok = (int)(i / D4), c = 4 * (int)(i - (int64_t)tok * D4);
+        float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+        for (int k = 0; k < d.n_src; ++k) {
+            const float4 v = *reinterpret_cast<const float4*>(row_ptr(d.src[k], tok) + c);
+            s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+        }
+        float4* o = reinterpret_cast<float4*>(row_ptr(d.out, tok) + c);
+        if (d.accumulate) { const float4 v = *o; s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w; }
+        *o = s;
     }
 }
 

@@ -17,39 +17,64 @@ using namespace mep;
 
 namespace {
 
+// workgroup = (batch row, 32 columns); 8 time groups of 32 lanes stride the time axis and
+// combine in a fixed order (first index of the maximum wins across groups, as within one)
+constexpr int POOL_COLS = 32, POOL_GROUPS = 8;
+
 __global__ __launch_bounds__(256) void k_pool_fwd(const mep_pool_desc* __restrict__ descs) {
     const mep_pool_desc& d = descs[blockIdx.y];
-    const int nct = (d.C + 255) / 256;
+    const int nct = (d.C + POOL_COLS - 1) / POOL_COLS;
     if ((int)blockIdx.x >= d.B * nct) return;
     const int b = blockIdx.x / nct;
-    const int c = (blockIdx.x - b * nct) * 256 + threadIdx.x;
-    if (c >= d.C) return;
-    const float* x = reinterpret_cast<const float*>(d.x) + (int64_t)b * d.T * d.C + c;
-    float s = 0.f, mx = x[0];
-    int idx = 0;
-    for (int t = 0; t < d.T; ++t) {
-        const float v = x[(int64_t)t * d.C];
-        s += v;
-        if (v > mx) { mx = v; idx = t; }
+    const int cl = threadIdx.x & (POOL_COLS - 1), g = threadIdx.x / POOL_COLS;
+    const int c = (blockIdx.x - b * nct) * POOL_COLS + cl;
+    __shared__ float s_sum[POOL_GROUPS][POOL_COLS], s_max[POOL_GROUPS][POOL_COLS];
+    __shared__ int s_idx[POOL_GROUPS][POOL_COLS];
+    float s = 0.f, mx = -INFINITY;
+    int idx = 0x7fffffff;
+    if (c < d.C) {
+        const float* x = reinterpret_cast<const float*>(d.x) + (int64_t)b * d.T * d.C + c;
+        for (int t = g; t < d.T; t += POOL_GROUPS) {
+            const float v = x[(int64_t)t * d.C];
+            s += v;
+            if (v > mx || idx == 0x7fffffff) { mx = v; idx = t; }   // strict >: first index wins
+        }
     }
-    float* pooled = reinterpret_cast<float*>(d.pooled) + (int64_t)b * 2 * d.C;
-    pooled[c] = s / (float)d.T;
-    pooled[d.C + c] = mx;
-    reinterpret_cast<int*>(d.argmax)[(int64_t)b * d.C + c] = idx;
+    s_sum[g][cl] = s;
+    s_max[g][cl] = mx;
+    s_idx[g][cl] = idx;
+    __syncthreads();
+    if (g == 0 && c < d.C) {
+        float ts = 0.f, tm = s_max[0][cl];
+        int ti = s_idx[0][cl];
+#pragma unroll
+        for (int k = 0; k < POOL_GROUPS; ++k) {
+            ts += s_sum[k][cl];
+            const float m = s_max[k][cl];
+            const int i = s_idx[k][cl];
+            if (i != 0x7fffffff && (m > tm || (m == tm && i < ti))) { tm = m; ti = i; }
+        }
+        float* pooled = reinterpret_cast<float*>(d.pooled) + (int64_t)b * 2 * d.C;
+        pooled[c] = ts / (float)d.T;
+        pooled[d.C + c] = tm;
+        reinterpret_cast<int*>(d.argmax)[(int64_t)b * d.C + c] = ti;
+    }
 }
 
+// elementwise over [B, T, C]: dx = dmean / T + onehot(argmax) * dmax
 __global__ __launch_bounds__(256) void k_pool_bwd(const mep_pool_desc* __restrict__ descs) {
     const mep_pool_desc& d = descs[blockIdx.y];
-    const int nct = (d.C + 255) / 256;
-    if ((int)blockIdx.x >= d.B * nct) return;
-    const int b = blockIdx.x / nct;
-    const int c = (blockIdx.x - b * nct) * 256 + threadIdx.x;
-    if (c >= d.C) return;
-    const float* dp = reinterpret_cast<const float*>(d.dpooled) + (int64_t)b * 2 * d.C;
-    const float dmean = dp[c] / (float)d.T, dmax = dp[d.C + c];
-    const int idx = reinterpret_cast<const int*>(d.argmax)[(int64_t)b * d.C + c];
-    float* dx = reinterpret_cast<float*>(d.dx) + (int64_t)b * d.T * d.C + c;
-    for (int t = 0; t < d.T; ++t) dx[(int64_t)t * d.C] = (t == idx) ? dmean + dmax : dmean;
+    const int64_t total = (int64_t)d.B * d.T * d.C;
+    const float* dp = reinterpret_cast<const float*>(d.dpooled);
+    const int* am = reinterpret_cast<const int*>(d.argmax);
+    float* dx = reinterpret_cast<float*>(d.dx);
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+        const int c = (int)(i % d.C);
+        const int64_t bt = i / d.C;
+        const int t = (int)(bt % d.T), b = (int)(bt / d.T);
+        const float dmean = dp[(int64_t)b * 2 * d.C + c] / (float)d.T;
+        dx[i] = (am[(int64_t)b * d.C + c] == t) ? dmean + dp[(int64_t)b * 2 * d.C + d.C + c] : dmean;
+    }
 }
 
 // ---------------------------------------------------------------- fusion head

@@ -11,8 +11,8 @@ import torch
 
 from . import _lib
 from ._lib import (AttnBwdDesc, AttnDesc, ColsumDesc, DescArray, EpiBwdDesc, EpiDesc, GemmDesc, Rows,
-                   WgradDesc, launch)
-from .trimodal import TOK_PER_SPLIT, cdiv, crows
+                   launch)
+from .trimodal import cdiv, crows, make_wgrad
 
 
 def _c(t):
@@ -20,17 +20,7 @@ def _c(t):
 
 
 def _wgrad(items, dev):
-    total = sum(cdiv(n, TOK_PER_SPLIT) * N * K for (_, _, n, N, K, _, _) in items)
-    ws = torch.empty(total, dtype=torch.float32, device=dev)
-    descs, off, tmax, rmax = [], 0, 0, 0
-    for (a, b, n, N, K, out, ldo) in items:
-        ns = cdiv(n, TOK_PER_SPLIT)
-        descs.append(WgradDesc(a=a, b=b, partial=ws.data_ptr() + 4 * off, out=out, ntok=n, N=N, K=K, ldo=ldo,
-                               tok_per_split=TOK_PER_SPLIT, n_split=ns, accumulate=0))
-        off += ns * N * K
-        tmax = max(tmax, cdiv(N, 64) * cdiv(K, 64) * ns)
-        rmax = max(rmax, cdiv(N * K, 256))
-    arr = DescArray(WgradDesc, descs, dev)
+    ws, arr, tmax, rmax = make_wgrad(items, dev)
     launch('mep_wgrad', arr, tmax)
     launch('mep_wgrad_reduce', arr, rmax)
     return ws, arr
@@ -58,8 +48,9 @@ class _BlockFn(torch.autograd.Function):
                      ln_b=lnb.data_ptr(), stats=estat.data_ptr(), seed=0, ntok=B * Tq, D=D, drop_p=0.0,
                      drop_stream=0)
         a_arr, e_arr = DescArray(AttnDesc, [ad], dev), DescArray(EpiDesc, [ed], dev)
-        launch('mep_attn_fwd', a_arr, B * cdiv(Tq, 64))
-        launch('mep_block_epi_fwd', e_arr, cdiv(B * Tq, 64))
+        geo = _lib.attn_geometry([(B, H, Tq, Tk)])
+        launch('mep_attn_fwd', a_arr, geo[0], threads=geo[2])
+        launch('mep_block_epi_fwd', e_arr, cdiv(B * Tq, 64), threads=D)
         ctx.save_for_backward(q, k, v, mask, X, XP, Z, S, astat, estat, c, wp, wm, lnw, lnb)
         ctx.sp = sp
         ctx.meta = (B, Tq, Tk, D, H, same_kv)
@@ -89,14 +80,15 @@ class _BlockFn(torch.autograd.Function):
                          ds_next=dS.data_ptr() if dS is not None else 0,
                          ds_prev=dSp.data_ptr() if has_prev else 0,
                          dc_partial=dc_part.data_ptr() if has_prev else 0)
-        launch('mep_block_epi_bwd', DescArray(EpiBwdDesc, [eb], dev), cdiv(B * Tq, 64))
-        launch('mep_attn_bwd', DescArray(AttnBwdDesc, [ab], dev), B * (cdiv(Tq, 64) + cdiv(Tk, 64)))
+        launch('mep_block_epi_bwd', DescArray(EpiBwdDesc, [eb], dev), cdiv(B * Tq, 64), threads=D)
+        geo = _lib.attn_geometry([(B, H, Tq, Tk)])
+        launch('mep_attn_bwd', DescArray(AttnBwdDesc, [ab], dev), geo[1], threads=geo[3])
         gwp, gwm = torch.empty_like(wp), torch.empty_like(wm)
         glw, glb, gc = torch.empty_like(lnw), torch.empty_like(lnb), torch.empty_like(c)
         n = B * Tq
-        keep = _wgrad([(crows(dXP, Tq, D), crows(X, Tq, D), n, D, D, gwp.data_ptr(), D),
-                       (crows(dZ, Tq, D), crows(q, Tq, D), n, D, D, gwm.data_ptr(), 2 * D),
-                       (crows(dZ, Tq, D), crows(XP, Tq, D), n, D, D, gwm.data_ptr() + 4 * D, 2 * D)], dev)
+        keep = _wgrad([(crows(dXP, Tq, D), D, n, [(crows(X, Tq, D), D, gwp.data_ptr(), D)]),
+                       (crows(dZ, Tq, D), D, n, [(crows(q, Tq, D), D, gwm.data_ptr(), 2 * D),
+                                                 (crows(XP, Tq, D), D, gwm.data_ptr() + 4 * D, 2 * D)])], dev)
         cs = [ColsumDesc(partial=ln_part.data_ptr(), out=glw.data_ptr(), n_rows=ln_part.shape[0], n_cols=D,
                          ld=2 * D, accumulate=0),
               ColsumDesc(partial=ln_part.data_ptr() + 4 * D, out=glb.data_ptr(), n_rows=ln_part.shape[0],
@@ -104,7 +96,7 @@ class _BlockFn(torch.autograd.Function):
         if has_prev:
             cs.append(ColsumDesc(partial=dc_part.data_ptr(), out=gc.data_ptr(), n_rows=dc_part.numel(), n_cols=1,
                                  ld=1, accumulate=0))
-        launch('mep_colsum', DescArray(ColsumDesc, cs, dev), cdiv(D, 256))
+        launch('mep_colsum', DescArray(ColsumDesc, cs, dev), cdiv(D, 32))
         del keep
         return (None, None, dQ, dK, None if same_kv else dV, None, dSp, gc if has_prev else None,
                 gwp, gwm, glw, glb)
@@ -147,7 +139,7 @@ class _UnifyFn(torch.autograd.Function):
         N = w.shape[0]
         gy = _c(gy).reshape(n, N)
         gw = torch.empty_like(w)
-        keep = _wgrad([(crows(gy, n, N), crows(x2, n, K), n, N, K, gw.data_ptr(), K)], x2.device)
+        keep = _wgrad([(crows(gy, n, N), N, n, [(crows(x2, n, K), K, gw.data_ptr(), K)])], x2.device)
         gx = None
         if ctx.needs_input_grad[0]:
             gx = torch.empty(n, K, dtype=torch.float32, device=x2.device)

@@ -41,6 +41,30 @@ def cdiv(a, b):
     return (a + b - 1) // b
 
 
+def make_wgrad(items, dev, tok_per_split=TOK_PER_SPLIT):
+    """items: [(a_rows, N, ntok, [(b_rows, K, out_ptr, ldo), ...]), ...] -> (workspace, descs,
+    wgrad tiles, reduce tiles).  One descriptor per A operand; its B operands concatenate on K."""
+    total = sum(cdiv(n, tok_per_split) * N * sum(b[1] for b in bs) for (_, N, n, bs) in items)
+    ws = torch.zeros(max(total, 1), dtype=torch.float32, device=dev)
+    descs, off, tmax, rmax = [], 0, 0, 0
+    for (a, N, n, bs) in items:
+        assert N <= 128 and len(bs) <= _lib.WG_MAX_B
+        ktot = sum(b[1] for b in bs)
+        ns = cdiv(n, tok_per_split)
+        pad = [(Rows(), 0, 0, 0)] * (_lib.WG_MAX_B - len(bs))
+        allb = list(bs) + pad
+        descs.append(WgradDesc(a=a, b=(Rows * _lib.WG_MAX_B)(*[b[0] for b in allb]),
+                               out=(ctypes.c_uint64 * _lib.WG_MAX_B)(*[b[2] for b in allb]),
+                               kb=(ctypes.c_int32 * _lib.WG_MAX_B)(*[b[1] for b in allb]),
+                               ldo=(ctypes.c_int32 * _lib.WG_MAX_B)(*[b[3] for b in allb]),
+                               partial=ws.data_ptr() + 4 * off, n_b=len(bs), ntok=n, N=N, Ktot=ktot,
+                               tok_per_split=tok_per_split, n_split=ns, accumulate=0))
+        off += ns * N * ktot
+        tmax = max(tmax, ns * cdiv(ktot, 256))
+        rmax = max(rmax, cdiv(N * ktot, 256))
+    return ws, DescArray(WgradDesc, descs, dev), tmax, rmax
+
+
 def rows(t, T, sB, sT, off=0):
     return Rows(ptr=t.data_ptr() + 4 * off, sB=sB, sT=sT, T=T)
 
@@ -195,7 +219,7 @@ class TriModalPlan:
                                      dx_accumulate=0))
             self.d_uln = DescArray(LnDesc, ln, dev)
         # per layer: attention + epilogue forward
-        self.d_attn, self.d_epi, self.t_attn, self.t_epi = [], [], [], []
+        self.d_attn, self.d_epi, self.t_attn, self.t_epi, self.g_attn = [], [], [], [], []
         for i in range(nl):
             ad, ed = [], []
             for blk in (b for b in self.blocks if b['i'] == i):
@@ -203,14 +227,17 @@ class TriModalPlan:
                 ed.append(self._epi_desc(blk))
             self.d_attn.append(DescArray(AttnDesc, ad, dev))
             self.d_epi.append(DescArray(EpiDesc, ed, dev))
-            self.t_attn.append(max(B * cdiv(b['Tq'], 64) for b in self.blocks))
+            geo = _lib.attn_geometry([(B, H, b['Tq'], b['Tk']) for b in self.blocks if b['i'] == i])
+            self.t_attn.append(geo[0])
+            self.g_attn.append(geo)
             self.t_epi.append(max(cdiv(B * b['Tq'], 64) for b in self.blocks))
         # pool
         pd = [PoolDesc(x=self.Xcat[e].data_ptr(), dx=self.dXcat[e].data_ptr(), pooled=self.pooled[e].data_ptr(),
                        dpooled=self.dpooled[e].data_ptr(), argmax=self.argmax[e].data_ptr(),
                        B=B, T=self.Ttot, C=self.C) for e in range(E)]
         self.d_pool = DescArray(PoolDesc, pd, dev)
-        self.t_pool = B * cdiv(self.C, 256)
+        self.t_pool = B * cdiv(self.C, 32)
+        self.t_poolb = min(2048, cdiv(B * self.Ttot * self.C, 256))
         # head
         hn = sp.head_norm
         self.head = HeadDesc(
@@ -231,7 +258,7 @@ class TriModalPlan:
                 ab.append(self._attn_bwd_desc(blk))
             self.d_epib.append(DescArray(EpiBwdDesc, eb, dev))
             self.d_attnb.append(DescArray(AttnBwdDesc, ab, dev))
-            self.t_attnb.append(max(B * (cdiv(b['Tq'], 64) + cdiv(b['Tk'], 64)) for b in self.blocks))
+            self.t_attnb.append(self.g_attn[i][1])
         # per-modality gradient sums
         sd = []
         self.dU = {}
@@ -247,7 +274,7 @@ class TriModalPlan:
                 sd.append(SumDesc(src=arr, out=crows(self.dU[(e, m)], T, D), n_src=len(srcs),
                                   ntok=self.ntok[m], D=D, accumulate=0))
         self.d_sum = DescArray(SumDesc, sd, dev)
-        self.t_sum = min(1024, max(cdiv(self.ntok[m] * D, 256) for m in MODS))
+        self.t_sum = min(1024, max(cdiv(self.ntok[m] * D // 4, 256) for m in MODS))
         if sp.unify_norm:
             self.dY = {k: torch.zeros_like(v) for k, v in self.dU.items()}
             tiles = {m: cdiv(self.ntok[m], 64) for m in MODS}
@@ -315,31 +342,20 @@ class TriModalPlan:
         sp, fl, D = self.spec, self.flat, self.spec.D
         dev = self.device
         g = fl.gptr
-        items = []   # (a rows, b rows, ntok, N, K, out ptr, ldo)
+        items = []
         for blk in self.blocks:
             Tq, nq, pre = blk['Tq'], self.B * blk['Tq'], blk['pre']
-            items.append((crows(blk['dXP'], Tq, D), crows(blk['X'], Tq, D), nq, D, D, g(pre + 'proj.weight'), D))
-            items.append((crows(blk['dZ'], Tq, D), self._q_rows(blk), nq, D, D, g(pre + 'minus.weight'), 2 * D))
-            items.append((crows(blk['dZ'], Tq, D), crows(blk['XP'], Tq, D), nq, D, D,
-                          g(pre + 'minus.weight') + 4 * D, 2 * D))
+            items.append((crows(blk['dXP'], Tq, D), D, nq, [(crows(blk['X'], Tq, D), D, g(pre + 'proj.weight'), D)]))
+            items.append((crows(blk['dZ'], Tq, D), D, nq, [(self._q_rows(blk), D, g(pre + 'minus.weight'), 2 * D),
+                                                           (crows(blk['XP'], Tq, D), D,
+                                                            g(pre + 'minus.weight') + 4 * D, 2 * D)]))
         for e in range(2):
             pre = sp.prefixes[e] + 'unify_dimension.'
             for m, d in zip(MODS, sp.dims):
                 src = self.dY[(e, m)] if sp.unify_norm else self.dU[(e, m)]
-                items.append((crows(src, self.T[m], D), self._in_rows(e, m), self.ntok[m], D, d,
-                              g(pre + UNIFY_NAMES[m] + '.weight'), d))
-        total = sum(cdiv(n, TOK_PER_SPLIT) * N * K for (_, _, n, N, K, _, _) in items)
-        self.wg_partial = torch.zeros(total, dtype=torch.float32, device=dev)
-        wd, off, tmax, rmax = [], 0, 0, 0
-        for (a, b, n, N, K, out, ldo) in items:
-            ns = cdiv(n, TOK_PER_SPLIT)
-            wd.append(WgradDesc(a=a, b=b, partial=self.wg_partial.data_ptr() + 4 * off, out=out, ntok=n, N=N, K=K,
-                                ldo=ldo, tok_per_split=TOK_PER_SPLIT, n_split=ns, accumulate=0))
-            off += ns * N * K
-            tmax = max(tmax, cdiv(N, 64) * cdiv(K, 64) * ns)
-            rmax = max(rmax, cdiv(N * K, 256))
-        self.d_wgrad = DescArray(WgradDesc, wd, dev)
-        self.t_wgrad, self.t_wgred = tmax, rmax
+                items.append((crows(src, self.T[m], D), D, self.ntok[m],
+                              [(self._in_rows(e, m), d, g(pre + UNIFY_NAMES[m] + '.weight'), d)]))
+        self.wg_partial, self.d_wgrad, self.t_wgrad, self.t_wgred = make_wgrad(items, dev)
         # column sums: block LayerNorms, residual coefficients, Ren unify LayerNorm
         cs = []
         for blk in self.blocks:
@@ -361,7 +377,7 @@ class TriModalPlan:
                 cs.append(ColsumDesc(partial=p.data_ptr() + 4 * D, out=g(pre + 'bias'), n_rows=p.shape[0],
                                      n_cols=D, ld=2 * D, accumulate=0))
         self.d_colsum = DescArray(ColsumDesc, cs, dev)
-        self.t_colsum = cdiv(D, 256)
+        self.t_colsum = cdiv(D, 32)
         hn = sp.head_norm
         self.head_grads = (g('trans'), g(hn + '.weight'), g(hn + '.bias'), g('out.weight'), g('out.bias'),
                            g('intensity.classifier.weight'), g('stimulation.classifier.weight'),
@@ -401,8 +417,8 @@ class TriModalPlan:
         if sp.unify_norm:
             launch('mep_layernorm_fwd', self.d_uln, cdiv(max(self.ntok.values()), 4), stream)
         for i in range(nl):
-            launch('mep_attn_fwd', self.d_attn[i], self.t_attn[i], stream)
-            launch('mep_block_epi_fwd', self.d_epi[i], self.t_epi[i], stream)
+            launch('mep_attn_fwd', self.d_attn[i], self.t_attn[i], stream, threads=self.g_attn[i][2])
+            launch('mep_block_epi_fwd', self.d_epi[i], self.t_epi[i], stream, threads=sp.D)
         launch('mep_pool_fwd', self.d_pool, self.t_pool, stream)
         self.head.compute_grad = int(grad)
         self.head.rdrop = int(rdrop)
@@ -420,10 +436,10 @@ class TriModalPlan:
             _lib.call('mep_head_fwd_bwd', ctypes.byref(self.head), stream=stream)
             self.head.ext_dlogits = 0
         _lib.call('mep_head_reduce', ctypes.byref(self.head), *self.head_grads, stream=stream)
-        launch('mep_pool_bwd', self.d_pool, self.t_pool, stream)
+        launch("mep_pool_bwd", self.d_pool, self.t_poolb, stream)
         for i in reversed(range(nl)):
-            launch('mep_block_epi_bwd', self.d_epib[i], self.t_epi[i], stream)
-            launch('mep_attn_bwd', self.d_attnb[i], self.t_attnb[i], stream)
+            launch('mep_block_epi_bwd', self.d_epib[i], self.t_epi[i], stream, threads=sp.D)
+            launch('mep_attn_bwd', self.d_attnb[i], self.t_attnb[i], stream, threads=self.g_attn[i][3])
         launch('mep_sum_rows', self.d_sum, self.t_sum, stream)
         if sp.unify_norm:
             launch('mep_layernorm_bwd', self.d_ulnb, cdiv(max(self.ntok.values()), 64), stream)
