@@ -205,12 +205,14 @@ def launch(name, descs, max_tiles, stream=None, threads=None):
 
 def attn_geometry(shapes):
     """shapes: [(B, H, Tq, Tk)] -> (fwd tiles, bwd tiles, fwd threads, bwd threads) following the
-    launch rule of include/mep.h (R = 512 // H rows per workgroup, one lane per (row, head))."""
-    ft = bt = fth = bth = 0
+    launch rule of csrc/attn.hip: one wave per (b, h, 64-row chunk), 4 waves per workgroup."""
+    ft = bt = 0
     for (B, H, Tq, Tk) in shapes:
-        R = 512 // H
-        ft = max(ft, B * -(-Tq // R))
-        bt = max(bt, B * (-(-Tq // R) + -(-Tk // R)))
-        fth = max(fth, 64 * -(-(H * min(Tq, R)) // 64))
-        bth = max(bth, 64 * -(-(H * max(min(Tq, R), min(Tk, R))) // 64))
-    return ft, bt, fth, bth
+        ft = max(ft, -(-(B * H * -(-Tq // 64)) // 4))
+        bt = max(bt, -(-(B * H * -(-Tk // 64)) // 4))
+    return ft, bt, 256, 256
+
+
+def attn_dc_slots(B, H, Tk):
+    """floats of the backward's dc_partial (one per wave task)"""
+    return B * H * -(-Tk // 64)

@@ -1,17 +1,22 @@
-// Residual scaled-dot-product attention core, forward and backward (fp32, hd = 16).
+// Residual scaled-dot-product attention core, forward and backward, on f32 MFMA (hd = 16).
 //
 // Reference: Attention_Block.multi_head_attention, cmu-mosei/run.py:236-256 (identical in
 // Ren-MME/run.py:188-208 and, after the w_qkv projections, others/realformer.py:182-204):
 //   S = q k^T / sqrt(hd) [+ c * S_prev];  S -= 1e8 (1 - mask);  X = softmax(S) v
 // The post-mask S is returned to the caller, which feeds it to the next layer of the chain.
 //
-// Mapping (CDNA4): one workgroup = (batch row, tile of R = 512/H rows); each LANE owns one
-// (row, head) pair, lane = row*H + head, so a row's 16-float head slices are contiguous across
-// neighbouring lanes (coalesced q / x / dq traffic) and no lane idles on H = 6.  The softmax row
-// max / sum never cross lanes.  K/V tiles of 64 keys (or, in pass B, Q/dX tiles of 64 queries)
-// are staged in LDS; lanes of one head read the same address (broadcast) and the H heads hit
-// disjoint banks.  hd = 16 operands live in registers; dots are split into 4 independent FMA
-// chains and keys are processed 4-8 at a time so the VALU pipeline has independent work.
+// Mapping (CDNA4): one WAVE = one task (batch row b, head h, chunk of 64 queries [forward] or
+// 64 keys [backward]); 4 independent waves per workgroup, no LDS staging, no barriers.  All
+// products (S, P.V, dP, dV, dK, dQ) are v_mfma_f32_16x16x4_f32 (exact fp32 fma chains), with the
+// operand layouts chosen so an accumulator feeds the next product without moving data:
+//   forward   S^T = K Q^T  -> lane (query c, group g) holds keys 4g..4g+3 of its query, i.e.
+//             exactly the A operand of O = P V.  Online softmax across 16-key tiles; the row
+//             max/sum reduce over 4 registers + 2 lane-group shuffles.
+//   backward  S = Q K^T and dP = dO V^T -> lane (key c, g) holds queries 4g..4g+3: the A operand
+//             of dV += P^T dO and dK += dS^T Q directly; dQ += dS K needs dS with the query on
+//             the lane, done by one 16x16 transpose through 1.3 KB of LDS per wave.
+// Reduction dims are ordered (step s, lane group g) -> dim 4g+s, so every operand fetch is one
+// 16-byte load and the forward and backward S are bitwise identical fma chains.
 // Row statistics (max, 1/sum) are kept instead of log-sum-exp because fully masked rows sit at
 // -1e8 where max + log(sum) would round the log away (ulp(1e8) = 8).
 #include <float.h>
@@ -22,328 +27,315 @@ using namespace mep;
 
 namespace {
 
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+
 constexpr int HD = 16;
-constexpr int MAXT = 512;        // threads per workgroup (upper bound; launch uses <= this)
-constexpr int TILE = 64;         // staged keys (fwd / pass A) or queries (pass B) per LDS tile
-constexpr int DMAX = 128;        // H*HD <= 128
+constexpr int WAVES = 4;
+constexpr int THREADS = 64 * WAVES;
+constexpr int CH = 64;              // queries (forward) / keys (backward) per wave task
 constexpr float INV_SCALE = 0.25f;  // 1/sqrt(16), exact
-constexpr int UA = 2;            // keys per step, backward pass A
-constexpr int UB = 2;            // queries per step, backward pass B
+
+MEP_DEV floatx4 mfma16(float a, float b, floatx4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+MEP_DEV floatx4 zero4() { return floatx4{0.f, 0.f, 0.f, 0.f}; }
 
 struct Score {
     bool has_prev;
     float c;
 };
 
-// q . k with four independent FMA chains (identical in forward and both backward passes, so
-// the recomputed probabilities match the forward bit for bit)
-MEP_DEV float dot16(const float* a, const float* b) {
-    float d0 = 0.f, d1 = 0.f, d2 = 0.f, d3 = 0.f;
-#pragma unroll
-    for (int i = 0; i < HD; i += 4) {
-        d0 = fmaf(a[i], b[i], d0);
-        d1 = fmaf(a[i + 1], b[i + 1], d1);
-        d2 = fmaf(a[i + 2], b[i + 2], d2);
-        d3 = fmaf(a[i + 3], b[i + 3], d3);
-    }
-    return (d0 + d1) + (d2 + d3);
-}
-
-// s = (q.k) * 0.25 [+ c*sp]  - 1e8 * (1 - m)      (op order of cmu-mosei/run.py:244-253)
-MEP_DEV float score(const float* q, const float* k, const Score& sc, float sp, float m) {
-    float s = mul_rn(dot16(q, k), INV_SCALE);
+// s = dot * 0.25 [+ c*sp]  - 1e8 * (1 - m)      (op order of cmu-mosei/run.py:244-253)
+MEP_DEV float score(float dot, const Score& sc, float sp, float m) {
+    float s = mul_rn(dot, INV_SCALE);
     if (sc.has_prev) s = add_rn(s, mul_rn(sc.c, sp));
     return sub_rn(s, mul_rn(1.0e8f, sub_rn(1.0f, m)));
 }
 
-MEP_DEV void load16(float* dst, const float* src) {
-#pragma unroll
-    for (int i = 0; i < HD; ++i) dst[i] = src[i];
+MEP_DEV bool aligned16(const mep_rows& r) {
+    return ((r.ptr & 15) == 0) && (r.sB % 4 == 0) && (r.sT % 4 == 0);
 }
 
-// stage rows [r0, r0+64) of a row view (batch row b) into LDS [64][D]
-MEP_DEV void stage_rows(float* dst, const mep_rows& src, int b, int r0, int nrows, int T, int D) {
-    for (int idx = threadIdx.x; idx < TILE * D; idx += blockDim.x) {
-        const int row = idx / D, col = idx - row * D;
-        const int r = r0 + row;
-        dst[idx] = (r < nrows) ? row_ptr(src, b * T + r)[col] : 0.f;
+// four consecutive floats of row `row` (if < n) at column col
+MEP_DEV void load4(float* dst, const mep_rows& v, int base_row, int row, int n, int col, bool vec) {
+    if (row < n) {
+        const float* p = row_ptr(v, base_row + row) + col;
+        if (vec) {
+            const float4 t = *reinterpret_cast<const float4*>(p);
+            dst[0] = t.x; dst[1] = t.y; dst[2] = t.z; dst[3] = t.w;
+        } else {
+            dst[0] = p[0]; dst[1] = p[1]; dst[2] = p[2]; dst[3] = p[3];
+        }
+    } else {
+        dst[0] = dst[1] = dst[2] = dst[3] = 0.f;
     }
 }
 
-MEP_DEV bool same_rows(const mep_rows& a, const mep_rows& b) {
-    return a.ptr == b.ptr && a.sB == b.sB && a.sT == b.sT && a.T == b.T;
-}
+MEP_DEV float shfl(float v, int src) { return __shfl(v, src, 64); }
 
-MEP_DEV int rows_per_tile(int H) { return MAXT / H; }
-
-__global__ __launch_bounds__(MAXT) void k_attn_fwd(const mep_attn_desc* __restrict__ descs) {
+__global__ __launch_bounds__(THREADS) void k_attn_fwd(const mep_attn_desc* __restrict__ descs) {
     const mep_attn_desc& d = descs[blockIdx.y];
-    const int R = rows_per_tile(d.H);
-    const int nqt = (d.Tq + R - 1) / R;
-    if ((int)blockIdx.x >= d.B * nqt) return;
-    const int b = blockIdx.x / nqt, qt = blockIdx.x - (blockIdx.x / nqt) * nqt;
-    const int D = d.H * HD;
-    const int row = threadIdx.x / d.H, h = threadIdx.x - row * d.H;
-    const int i = qt * R + row;
-    const bool active = (row < R) && (i < d.Tq);
-    const bool kv_same = same_rows(d.k, d.v);
-
-    __shared__ __attribute__((aligned(16))) float Ks[TILE * DMAX];
-    __shared__ __attribute__((aligned(16))) float Vs[TILE * DMAX];
-    __shared__ float Ms[TILE];
-
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int c = lane & 15, g = lane >> 4;
+    const int nqc = (d.Tq + CH - 1) / CH;
+    const int task = blockIdx.x * WAVES + wave;
+    if (task >= d.B * d.H * nqc) return;   // whole wave leaves; no barriers below
+    const int qc = task % nqc, bh = task / nqc;
+    const int h = bh % d.H, b = bh / d.H;
+    const int hc = h * HD;
     const Score sc{d.s_prev != 0, d.s_prev ? *reinterpret_cast<const float*>(d.c) : 0.f};
-    float q[HD], o[HD];
-    float m = -FLT_MAX, l = 0.f;
-#pragma unroll
-    for (int t = 0; t < HD; ++t) o[t] = 0.f;
-    const int64_t srow = (((int64_t)b * d.H + h) * d.Tq + i) * d.Tk;
     const float* sprev = reinterpret_cast<const float*>(d.s_prev);
     float* sout = reinterpret_cast<float*>(d.s_out);
-    if (active) load16(q, row_ptr(d.q, b * d.Tq + i) + h * HD);
     const float* mask = reinterpret_cast<const float*>(d.mask) + (int64_t)b * d.mask_sB;
-    const float* Vsrc = kv_same ? Ks : Vs;
+    const bool qv = aligned16(d.q), kv4 = aligned16(d.k);
+    const int64_t sbase = ((int64_t)b * d.H + h) * d.Tq;
 
-    for (int k0 = 0; k0 < d.Tk; k0 += TILE) {
-        __syncthreads();
-        stage_rows(Ks, d.k, b, k0, d.Tk, d.Tk, D);
-        if (!kv_same) stage_rows(Vs, d.v, b, k0, d.Tk, d.Tk, D);
-        if ((int)threadIdx.x < TILE) Ms[threadIdx.x] = (k0 + (int)threadIdx.x < d.Tk) ? mask[k0 + threadIdx.x] : 0.f;
-        __syncthreads();
-        const int nk = min(TILE, d.Tk - k0);
-        if (!active) continue;
-        for (int kb = 0; kb < nk; kb += 8) {
-            float s[8];
-            float cmax = -INFINITY;
+    // B operand of S^T = K Q^T: lane (query c, group g), dims 4g..4g+3 of 4 query tiles
+    float qf[4][4];
+    const int q_lo = qc * CH;
+    const int nqt = min(4, (d.Tq - q_lo + 15) / 16);
 #pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                const int k = kb + j;
-                if (k < nk) {
-                    s[j] = score(q, Ks + k * D + h * HD, sc, sc.has_prev ? sprev[srow + k0 + k] : 0.f, Ms[k]);
-                    if (sout) sout[srow + k0 + k] = s[j];
+    for (int qt = 0; qt < 4; ++qt) load4(qf[qt], d.q, b * d.Tq, q_lo + qt * 16 + c, d.Tq, hc + 4 * g, qv);
+
+    floatx4 o[4];
+    float m[4], l[4];
+#pragma unroll
+    for (int qt = 0; qt < 4; ++qt) { o[qt] = zero4(); m[qt] = -FLT_MAX; l[qt] = 0.f; }
+
+    const int nkt = (d.Tk + 15) / 16;
+    for (int kt = 0; kt < nkt; ++kt) {
+        const int k0 = kt * 16;
+        float kf[4], vf[4], mk[4];
+        load4(kf, d.k, b * d.Tk, k0 + c, d.Tk, hc + 4 * g, kv4);       // A: K[k0+c][4g+s]
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {                                   // B of P.V: V[k0+4g+s][c]
+            const int kk = k0 + 4 * g + s;
+            vf[s] = kk < d.Tk ? row_ptr(d.v, b * d.Tk + kk)[hc + c] : 0.f;
+            mk[s] = kk < d.Tk ? mask[kk] : 0.f;
+        }
+#pragma unroll
+        for (int qt = 0; qt < 4; ++qt) {
+            if (qt >= nqt) break;
+            floatx4 st = zero4();
+#pragma unroll
+            for (int s = 0; s < 4; ++s) st = mfma16(kf[s], qf[qt][s], st);   // C[key 4g+r][query c]
+            const int q = q_lo + qt * 16 + c;
+            const bool qok = q < d.Tq;
+            float sv[4], mx = -INFINITY;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int kk = k0 + 4 * g + r;
+                if (kk < d.Tk) {
+                    const int64_t si = (sbase + q) * d.Tk + kk;
+                    sv[r] = score(st[r], sc, (sc.has_prev && qok) ? sprev[si] : 0.f, mk[r]);
+                    if (sout && qok) sout[si] = sv[r];
                 } else {
-                    s[j] = -INFINITY;
+                    sv[r] = -INFINITY;
                 }
-                cmax = fmaxf(cmax, s[j]);
+                mx = fmaxf(mx, sv[r]);
             }
-            const float mnew = fmaxf(m, cmax);
-            const float corr = __expf(m - mnew);
-            l *= corr;
+            mx = fmaxf(mx, shfl(mx, lane ^ 16));
+            mx = fmaxf(mx, shfl(mx, lane ^ 32));
+            const float mnew = fmaxf(m[qt], mx);
+            const float corr = __expf(m[qt] - mnew);
+            float p[4];
 #pragma unroll
-            for (int t = 0; t < HD; ++t) o[t] *= corr;
+            for (int r = 0; r < 4; ++r) p[r] = __expf(sv[r] - mnew);
+            l[qt] = l[qt] * corr + ((p[0] + p[1]) + (p[2] + p[3]));
+            m[qt] = mnew;
 #pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                const int k = kb + j;
-                const float p = (k < nk) ? __expf(s[j] - mnew) : 0.f;
-                l += p;
-                const float* vr = Vsrc + min(k, nk - 1) * D + h * HD;
+            for (int r = 0; r < 4; ++r) o[qt][r] *= shfl(corr, 4 * g + r);  // O row 4g+r <- corr of query 4g+r
 #pragma unroll
-                for (int t = 0; t < HD; ++t) o[t] = fmaf(p, vr[t], o[t]);
-            }
-            m = mnew;
+            for (int s = 0; s < 4; ++s) o[qt] = mfma16(p[s], vf[s], o[qt]);  // C[query 4g+r][dim c]
         }
     }
-    if (active) {
-        const float inv = 1.0f / l;
-        float* xp = row_ptr(d.x, b * d.Tq + i) + h * HD;
+    float* stats = reinterpret_cast<float*>(d.stats);
 #pragma unroll
-        for (int t = 0; t < HD; ++t) xp[t] = o[t] * inv;
-        float* st = reinterpret_cast<float*>(d.stats) + 2 * ((((int64_t)b * d.H + h) * d.Tq) + i);
-        st[0] = m;
-        st[1] = inv;
+    for (int qt = 0; qt < 4; ++qt) {
+        if (qt >= nqt) break;
+        float lt = l[qt] + shfl(l[qt], lane ^ 16);
+        lt += shfl(lt, lane ^ 32);
+        const float inv = 1.0f / lt;
+        const int q = q_lo + qt * 16 + c;
+        if (g == 0 && q < d.Tq) {
+            stats[2 * (sbase + q)] = m[qt];
+            stats[2 * (sbase + q) + 1] = inv;
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const float ir = shfl(inv, 4 * g + r);
+            const int qq = q_lo + qt * 16 + 4 * g + r;
+            if (qq < d.Tq) row_ptr(d.x, b * d.Tq + qq)[hc + c] = o[qt][r] * ir;
+        }
     }
 }
 
-__global__ __launch_bounds__(MAXT) void k_attn_bwd(const mep_attn_bwd_desc* __restrict__ descs) {
+MEP_DEV void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__global__ __launch_bounds__(THREADS) void k_attn_bwd(const mep_attn_bwd_desc* __restrict__ descs) {
     const mep_attn_bwd_desc& bd = descs[blockIdx.y];
     const mep_attn_desc& d = bd.f;
-    const int R = rows_per_tile(d.H);
-    const int nqt = (d.Tq + R - 1) / R, nkt = (d.Tk + R - 1) / R;
-    if ((int)blockIdx.x >= d.B * (nqt + nkt)) return;
-    const int D = d.H * HD;
-    const int row = threadIdx.x / d.H, h = threadIdx.x - row * d.H;
-    const bool kv_same = same_rows(d.k, d.v);
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int c = lane & 15, g = lane >> 4;
+    const int nkc = (d.Tk + CH - 1) / CH;
+    const int task = blockIdx.x * WAVES + wave;
+    __shared__ __attribute__((aligned(16))) float Tr[WAVES][16 * 20];
+    if (task >= d.B * d.H * nkc) return;   // whole wave leaves; only wave-private LDS below
+    const int kc = task % nkc, bh = task / nkc;
+    const int h = bh % d.H, b = bh / d.H;
+    const int hc = h * HD;
     const Score sc{d.s_prev != 0, d.s_prev ? *reinterpret_cast<const float*>(d.c) : 0.f};
     const float* sprev = reinterpret_cast<const float*>(d.s_prev);
     const float* dsn = reinterpret_cast<const float*>(bd.ds_next);
-    const float* stats = reinterpret_cast<const float*>(d.stats);
-
-    __shared__ __attribute__((aligned(16))) float S1[TILE * DMAX];
-    __shared__ __attribute__((aligned(16))) float S2[TILE * DMAX];
-    __shared__ float Sm[TILE * 8 * 3];   // pass B: (max, 1/sum, delta) per (row, head); pass A: mask
-    __shared__ float Red[MAXT / 64];
-
-    if ((int)blockIdx.x < d.B * nqt) {
-        // ------------------------------------------------ pass A: lane = (query row, head) -> dQ
-        const int b = blockIdx.x / nqt, qt = blockIdx.x - b * nqt;
-        const int i = qt * R + row;
-        const bool active = (row < R) && (i < d.Tq);
-        float q[HD], dout[HD], dq[HD];
-        float delta = 0.f, m = 0.f, linv = 0.f;
-#pragma unroll
-        for (int t = 0; t < HD; ++t) dq[t] = 0.f;
-        const int64_t srow = (((int64_t)b * d.H + h) * d.Tq + i) * d.Tk;
-        if (active) {
-            load16(q, row_ptr(d.q, b * d.Tq + i) + h * HD);
-            load16(dout, row_ptr(bd.dx, b * d.Tq + i) + h * HD);
-            delta = dot16(dout, row_ptr(d.x, b * d.Tq + i) + h * HD);
-            const float* st = stats + 2 * ((((int64_t)b * d.H + h) * d.Tq) + i);
-            m = st[0];
-            linv = st[1];
-        }
-        const float* mask = reinterpret_cast<const float*>(d.mask) + (int64_t)b * d.mask_sB;
-        float* Ks = S1;
-        float* Vs = kv_same ? S1 : S2;
-        for (int k0 = 0; k0 < d.Tk; k0 += TILE) {
-            __syncthreads();
-            stage_rows(Ks, d.k, b, k0, d.Tk, d.Tk, D);
-            if (!kv_same) stage_rows(Vs, d.v, b, k0, d.Tk, d.Tk, D);
-            if ((int)threadIdx.x < TILE) Sm[threadIdx.x] = (k0 + (int)threadIdx.x < d.Tk) ? mask[k0 + threadIdx.x] : 0.f;
-            __syncthreads();
-            if (!active) continue;
-            const int nk = min(TILE, d.Tk - k0);
-            for (int kb = 0; kb < nk; kb += UA) {
-                float ds[UA];
-#pragma unroll
-                for (int j = 0; j < UA; ++j) {
-                    const int k = min(kb + j, nk - 1);
-                    const float* kr = Ks + k * D + h * HD;
-                    const float* vr = Vs + k * D + h * HD;
-                    const float s = score(q, kr, sc, sc.has_prev ? sprev[srow + k0 + k] : 0.f, Sm[k]);
-                    const float p = __expf(s - m) * linv;
-                    float g = p * (dot16(dout, vr) - delta);
-                    if (dsn) g += dsn[srow + k0 + k];
-                    ds[j] = (kb + j < nk) ? g : 0.f;
-                }
-#pragma unroll
-                for (int j = 0; j < UA; ++j) {
-                    const float* kr = Ks + min(kb + j, nk - 1) * D + h * HD;
-#pragma unroll
-                    for (int t = 0; t < HD; ++t) dq[t] = fmaf(ds[j], kr[t], dq[t]);
-                }
-            }
-        }
-        if (active) {
-            float* dqp = row_ptr(bd.dq, b * d.Tq + i) + h * HD;
-#pragma unroll
-            for (int t = 0; t < HD; ++t) dqp[t] += dq[t] * INV_SCALE;
-        }
-        return;
-    }
-    // ------------------------------------------------ pass B: lane = (key row, head) -> dK, dV, dS_prev, dc
-    const int tb = blockIdx.x - d.B * nqt;
-    const int b = tb / nkt, kt = tb - (tb / nkt) * nkt;
-    const int k = kt * R + row;
-    const bool active = (row < R) && (k < d.Tk);
-    float kk[HD], vv[HD], dk[HD], dv[HD];
-    float maskv = 0.f, dc_acc = 0.f;
-#pragma unroll
-    for (int t = 0; t < HD; ++t) { dk[t] = 0.f; dv[t] = 0.f; }
-    if (active) {
-        load16(kk, row_ptr(d.k, b * d.Tk + k) + h * HD);
-        load16(vv, row_ptr(d.v, b * d.Tk + k) + h * HD);
-        maskv = reinterpret_cast<const float*>(d.mask)[(int64_t)b * d.mask_sB + k];
-    }
     float* dsp = reinterpret_cast<float*>(bd.ds_prev);
-    float* Qs = S1;
-    float* Gs = S2;
-    for (int r0 = 0; r0 < d.Tq; r0 += TILE) {
-        __syncthreads();
-        stage_rows(Qs, d.q, b, r0, d.Tq, d.Tq, D);
-        stage_rows(Gs, bd.dx, b, r0, d.Tq, d.Tq, D);
-        for (int idx = threadIdx.x; idx < TILE * d.H; idx += blockDim.x) {
-            const int rr = idx / d.H, hh = idx - (idx / d.H) * d.H;
-            const int r = r0 + rr;
-            float mm = 0.f, li = 0.f, del = 0.f;
-            if (r < d.Tq) {
-                const float* st = stats + 2 * ((((int64_t)b * d.H + hh) * d.Tq) + r);
-                mm = st[0];
-                li = st[1];
-                del = dot16(row_ptr(bd.dx, b * d.Tq + r) + hh * HD, row_ptr(d.x, b * d.Tq + r) + hh * HD);
-            }
-            Sm[(rr * 8 + hh) * 3 + 0] = mm;
-            Sm[(rr * 8 + hh) * 3 + 1] = li;
-            Sm[(rr * 8 + hh) * 3 + 2] = del;
+    const float* stats = reinterpret_cast<const float*>(d.stats);
+    const float* mask = reinterpret_cast<const float*>(d.mask) + (int64_t)b * d.mask_sB;
+    const int64_t sbase = ((int64_t)b * d.H + h) * d.Tq;
+    const bool qv = aligned16(d.q), kv4 = aligned16(d.k), vv4 = aligned16(d.v), gv = aligned16(bd.dx);
+    float* T = Tr[wave];
+
+    const int k_lo = kc * CH;
+    const int nkt = min(4, (d.Tk - k_lo + 15) / 16);
+    // per key tile: B operands of S (K) and dP (V) with the key on the lane, the key mask, and
+    // the B operand of dQ (K rows 4g+s, dim c); dK / dV accumulators (C[key 4g+r][dim c])
+    float kb[4][4], vb[4][4], kq[4][4], mkey[4];
+    floatx4 dk[4], dv[4];
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt) {
+        const int k0 = k_lo + kt * 16;
+        load4(kb[kt], d.k, b * d.Tk, k0 + c, d.Tk, hc + 4 * g, kv4);
+        load4(vb[kt], d.v, b * d.Tk, k0 + c, d.Tk, hc + 4 * g, vv4);
+        mkey[kt] = (k0 + c < d.Tk) ? mask[k0 + c] : 0.f;
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            const int kk = k0 + 4 * g + s;
+            kq[kt][s] = kk < d.Tk ? row_ptr(d.k, b * d.Tk + kk)[hc + c] : 0.f;
         }
-        __syncthreads();
-        if (!active) continue;
-        const int nq = min(TILE, d.Tq - r0);
-        for (int rb = 0; rb < nq; rb += UB) {
-            float ds[UB], p[UB];
+        dk[kt] = zero4();
+        dv[kt] = zero4();
+    }
+    float dc_acc = 0.f;
+    const int nqt = (d.Tq + 15) / 16;
+    for (int qt = 0; qt < nqt; ++qt) {
+        const int q0 = qt * 16;
+        float qa[4], da[4], db[4], qb[4], mm[4], li[4], del[4];
+        load4(qa, d.q, b * d.Tq, q0 + c, d.Tq, hc + 4 * g, qv);        // A of S: Q[q0+c][4g+s]
+        load4(da, bd.dx, b * d.Tq, q0 + c, d.Tq, hc + 4 * g, gv);      // A of dP: dO[q0+c][4g+s]
 #pragma unroll
-            for (int j = 0; j < UB; ++j) {
-                const int rr = min(rb + j, nq - 1);
-                const int r = r0 + rr;
-                const int64_t sidx = (((int64_t)b * d.H + h) * d.Tq + r) * d.Tk + k;
-                const float* qr = Qs + rr * D + h * HD;
-                const float* gr = Gs + rr * D + h * HD;
-                const float spv = sc.has_prev ? sprev[sidx] : 0.f;
-                const float s = score(qr, kk, sc, spv, maskv);
-                const float* sm = Sm + (rr * 8 + h) * 3;
-                const bool ok = rb + j < nq;
-                const float pj = ok ? __expf(s - sm[0]) * sm[1] : 0.f;
-                float g = pj * (dot16(gr, vv) - sm[2]);
-                if (dsn) g += ok ? dsn[sidx] : 0.f;
-                p[j] = pj;
-                ds[j] = ok ? g : 0.f;
+        for (int s = 0; s < 4; ++s) {                                  // B of dV / dK: rows 4g+s, dim c
+            const int qq = q0 + 4 * g + s;
+            const bool ok = qq < d.Tq;
+            db[s] = ok ? row_ptr(bd.dx, b * d.Tq + qq)[hc + c] : 0.f;
+            qb[s] = ok ? row_ptr(d.q, b * d.Tq + qq)[hc + c] : 0.f;
+            const float ov = ok ? row_ptr(d.x, b * d.Tq + qq)[hc + c] : 0.f;
+            float pr = db[s] * ov;                                     // delta = rowsum(dO * O)
+            pr += shfl(pr, lane ^ 1);
+            pr += shfl(pr, lane ^ 2);
+            pr += shfl(pr, lane ^ 4);
+            pr += shfl(pr, lane ^ 8);
+            del[s] = pr;
+            mm[s] = ok ? stats[2 * (sbase + qq)] : 0.f;
+            li[s] = ok ? stats[2 * (sbase + qq) + 1] : 0.f;
+        }
+        floatx4 dq = zero4();
+#pragma unroll
+        for (int kt = 0; kt < 4; ++kt) {
+            if (kt >= nkt) break;
+            const int kk = k_lo + kt * 16 + c;
+            floatx4 st = zero4(), dp = zero4();
+#pragma unroll
+            for (int s = 0; s < 4; ++s) st = mfma16(qa[s], kb[kt][s], st);   // C[query 4g+r][key c]
+#pragma unroll
+            for (int s = 0; s < 4; ++s) dp = mfma16(da[s], vb[kt][s], dp);
+            float p[4], ds[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int qq = q0 + 4 * g + r;
+                const bool ok = (qq < d.Tq) && (kk < d.Tk);
+                const int64_t si = (sbase + qq) * d.Tk + kk;
+                const float spv = (sc.has_prev && ok) ? sprev[si] : 0.f;
+                const float sv = score(st[r], sc, spv, mkey[kt]);
+                const float pv = ok ? __expf(sv - mm[r]) * li[r] : 0.f;
+                float gsv = pv * (dp[r] - del[r]);
+                if (dsn && ok) gsv += dsn[si];
+                gsv = ok ? gsv : 0.f;
                 if (sc.has_prev && ok) {
-                    if (dsp) dsp[sidx] = sc.c * g;
-                    dc_acc = fmaf(g, spv, dc_acc);
+                    if (dsp) dsp[si] = sc.c * gsv;
+                    dc_acc = fmaf(gsv, spv, dc_acc);
                 }
+                p[r] = pv;
+                ds[r] = gsv;
             }
 #pragma unroll
-            for (int j = 0; j < UB; ++j) {
-                const int rr = min(rb + j, nq - 1);
-                const float* qr = Qs + rr * D + h * HD;
-                const float* gr = Gs + rr * D + h * HD;
+            for (int s = 0; s < 4; ++s) {
+                dv[kt] = mfma16(p[s], db[s], dv[kt]);     // dV[key][dim] += P^T dO
+                dk[kt] = mfma16(ds[s], qb[s], dk[kt]);    // dK[key][dim] += dS^T Q
+            }
+            // dQ += dS K: transpose dS (query 4g+r on lane c=key) to the query-on-lane A layout
 #pragma unroll
-                for (int t = 0; t < HD; ++t) {
-                    dk[t] = fmaf(ds[j], qr[t], dk[t]);
-                    dv[t] = fmaf(p[j], gr[t], dv[t]);
-                }
+            for (int r = 0; r < 4; ++r) T[(4 * g + r) * 20 + c] = ds[r];
+            wave_lds_sync();
+            const float4 t4 = *reinterpret_cast<const float4*>(T + c * 20 + 4 * g);
+            wave_lds_sync();
+            dq = mfma16(t4.x, kq[kt][0], dq);
+            dq = mfma16(t4.y, kq[kt][1], dq);
+            dq = mfma16(t4.z, kq[kt][2], dq);
+            dq = mfma16(t4.w, kq[kt][3], dq);
+        }
+        // dq rows q0+4g+r, dim c (exclusive owner when the keys fit one chunk; else atomics)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int qq = q0 + 4 * g + r;
+            if (qq < d.Tq) {
+                float* dqp = row_ptr(bd.dq, b * d.Tq + qq) + hc + c;
+                if (nkc == 1) *dqp += dq[r] * INV_SCALE;
+                else atomicAdd(dqp, dq[r] * INV_SCALE);
             }
         }
     }
-    if (active) {
-        float* dkp = row_ptr(bd.dk, b * d.Tk + k) + h * HD;
-        if (same_rows(bd.dk, bd.dv)) {
+    const bool same_kv = bd.dk.ptr == bd.dv.ptr && bd.dk.sB == bd.dv.sB && bd.dk.sT == bd.dv.sT;
 #pragma unroll
-            for (int t = 0; t < HD; ++t) dkp[t] = dk[t] * INV_SCALE + dv[t];
-        } else {
-            float* dvp = row_ptr(bd.dv, b * d.Tk + k) + h * HD;
+    for (int kt = 0; kt < 4; ++kt) {
+        if (kt >= nkt) break;
 #pragma unroll
-            for (int t = 0; t < HD; ++t) { dkp[t] = dk[t] * INV_SCALE; dvp[t] = dv[t]; }
+        for (int r = 0; r < 4; ++r) {
+            const int kk = k_lo + kt * 16 + 4 * g + r;
+            if (kk >= d.Tk) continue;
+            float* dkp = row_ptr(bd.dk, b * d.Tk + kk) + hc + c;
+            if (same_kv) {
+                *dkp = dk[kt][r] * INV_SCALE + dv[kt][r];
+            } else {
+                *dkp = dk[kt][r] * INV_SCALE;
+                row_ptr(bd.dv, b * d.Tk + kk)[hc + c] = dv[kt][r];
+            }
         }
     }
     if (bd.dc_partial) {
-        // reduce dc over the lanes of this workgroup (fixed order -> deterministic)
-        const float w = wave_sum(active ? dc_acc : 0.f);
-        if ((threadIdx.x & 63) == 0) Red[threadIdx.x >> 6] = w;
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            float s = 0.f;
-            for (int ww = 0; ww < (int)(blockDim.x >> 6); ++ww) s += Red[ww];
-            reinterpret_cast<float*>(bd.dc_partial)[b * nkt + kt] = s;
-        }
+        const float w = wave_sum(dc_acc);
+        if (lane == 0) reinterpret_cast<float*>(bd.dc_partial)[task] = w;
     }
 }
 
 }  // namespace
 
-// threads: 64 * ceil(H * min(T, 512/H) / 64) of the largest descriptor (the host knows the
-// shapes); max_tiles: max over descriptors of B * ceil(Tq / (512/H))  [+ B * ceil(Tk / (512/H))
-// for the backward].
+// Launch geometry: 256 threads (4 waves, one task each); tasks = B * H * ceil(Tq/64) forward,
+// B * H * ceil(Tk/64) backward; max_tiles = ceil(max tasks / 4).  dc_partial (backward) has one
+// float per task, task = (b*H + h) * ceil(Tk/64) + key chunk.
 extern "C" int mep_attn_fwd(const mep_attn_desc* descs, int n_desc, int max_tiles, int threads, mep_stream_t stream) {
     if (n_desc <= 0 || max_tiles <= 0) return 0;
-    if (threads <= 0 || threads > MAXT || threads % 64) { mep_set_error("mep_attn_fwd: threads"); return MEP_EINVAL; }
-    hipLaunchKernelGGL(k_attn_fwd, dim3(max_tiles, n_desc), dim3(threads), 0, (hipStream_t)stream, descs);
+    if (threads != THREADS) { mep_set_error("mep_attn_fwd: threads must be 256"); return MEP_EINVAL; }
+    hipLaunchKernelGGL(k_attn_fwd, dim3(max_tiles, n_desc), dim3(THREADS), 0, (hipStream_t)stream, descs);
     return mep_check_launch("mep_attn_fwd");
 }
 
 extern "C" int mep_attn_bwd(const mep_attn_bwd_desc* descs, int n_desc, int max_tiles, int threads,
                             mep_stream_t stream) {
     if (n_desc <= 0 || max_tiles <= 0) return 0;
-    if (threads <= 0 || threads > MAXT || threads % 64) { mep_set_error("mep_attn_bwd: threads"); return MEP_EINVAL; }
-    hipLaunchKernelGGL(k_attn_bwd, dim3(max_tiles, n_desc), dim3(threads), 0, (hipStream_t)stream, descs);
+    if (threads != THREADS) { mep_set_error("mep_attn_bwd: threads must be 256"); return MEP_EINVAL; }
+    hipLaunchKernelGGL(k_attn_bwd, dim3(max_tiles, n_desc), dim3(THREADS), 0, (hipStream_t)stream, descs);
     return mep_check_launch("mep_attn_bwd");
 }

@@ -142,6 +142,31 @@ MEP_DEV void load_tile(float* __restrict__ dst, int lda, const mep_rows& src, in
     }
 }
 
+// Stage rows [t0, t0+TT) x columns [c0, c0+nc) of a row view into LDS (row stride ld floats);
+// rows at or beyond t_end are zero.  16-byte loads/stores whenever the view allows it, one
+// row-address computation per 4 columns.
+template <int TT>
+MEP_DEV void stage_cols(float* __restrict__ dst, int ld, const mep_rows& src, int t0, int t_end, int c0, int nc) {
+    const bool vec = (nc % 4 == 0) && (c0 % 4 == 0) && (ld % 4 == 0) && ((src.ptr & 15) == 0) &&
+                     (src.sB % 4 == 0) && (src.sT % 4 == 0) && ((reinterpret_cast<uintptr_t>(dst) & 15) == 0);
+    if (vec) {
+        const int nc4 = nc >> 2;
+        for (int s = threadIdx.x; s < TT * nc4; s += blockDim.x) {
+            const int row = s / nc4, c = 4 * (s - row * nc4);
+            const int tok = t0 + row;
+            float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (tok < t_end) v = *reinterpret_cast<const float4*>(row_ptr(src, tok) + c0 + c);
+            *reinterpret_cast<float4*>(dst + row * ld + c) = v;
+        }
+    } else {
+        for (int s = threadIdx.x; s < TT * nc; s += blockDim.x) {
+            const int row = s / nc, c = s - row * nc;
+            const int tok = t0 + row;
+            dst[row * ld + c] = tok < t_end ? row_ptr(src, tok)[c0 + c] : 0.f;
+        }
+    }
+}
+
 }  // namespace mep
 
 // error plumbing shared by the launchers (api.cpp)

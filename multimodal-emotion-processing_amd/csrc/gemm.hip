@@ -124,20 +124,11 @@ __global__ __launch_bounds__(WG_THREADS) void k_wgrad(const mep_wgrad_desc* __re
 
     for (int t0 = t_begin; t0 < t_end; t0 += WG_TT) {
         __syncthreads();
-        for (int idx = threadIdx.x; idx < WG_TT * d.N; idx += WG_THREADS) {
-            const int row = idx / d.N, c = idx - row * d.N;
-            const int tok = t0 + row;
-            As[row * WG_NMAX + c] = tok < t_end ? row_ptr(d.a, tok)[c] : 0.f;
-        }
+        stage_cols<WG_TT>(As, WG_NMAX, d.a, t0, t_end, 0, d.N);
         int koff = 0;
         for (int i = 0; i < d.n_b; ++i) {
             const int lo = max(koff, kbase), hi = min(koff + d.kb[i], kbase + kcnt);
-            const int len = hi - lo;
-            for (int idx = threadIdx.x; len > 0 && idx < WG_TT * len; idx += WG_THREADS) {
-                const int row = idx / len, c = idx - row * len;
-                const int tok = t0 + row;
-                Bs[row * WG_KG + (lo - kbase) + c] = tok < t_end ? row_ptr(d.b[i], tok)[lo - koff + c] : 0.f;
-            }
+            if (hi > lo) stage_cols<WG_TT>(Bs + (lo - kbase), WG_KG, d.b[i], t0, t_end, lo - koff, hi - lo);
             koff += d.kb[i];
         }
         __syncthreads();

@@ -73,7 +73,7 @@ class _BlockFn(torch.autograd.Function):
         ln_part = torch.empty(cdiv(B * Tq, 64), 2, D, **f)
         has_prev = ctx.sp is not None
         dSp = torch.empty(B, H, Tq, Tk, **f) if has_prev else None
-        dc_part = torch.empty(B * cdiv(Tk, 64), **f) if has_prev else None
+        dc_part = torch.empty(_lib.attn_dc_slots(B, H, Tk), **f) if has_prev else None
         eb = EpiBwdDesc(f=ed, dout=crows(dout, Tq, D), dout2=Rows(), dz=crows(dZ, Tq, D), dxp=crows(dXP, Tq, D),
                         dx=crows(dX, Tq, D), dq=crows(dQ, Tq, D), ln_partial=ln_part.data_ptr(), dq_accumulate=0)
         ab = AttnBwdDesc(f=ad, dx=crows(dX, Tq, D), dq=crows(dQ, Tq, D), dk=crows(dK, Tk, D), dv=crows(dV, Tk, D),

@@ -164,7 +164,7 @@ class TriModalPlan:
             blk['S'] = torch.zeros(B, H, Tq, Tk, **f32)
         if i >= 1:
             blk['dSprev'] = torch.zeros(B, H, Tq, Tk, **f32)
-            blk['dc_partial'] = torch.zeros(B * cdiv(Tk, 64), **f32)
+            blk['dc_partial'] = torch.zeros(_lib.attn_dc_slots(B, H, Tk), **f32)
         g = j % 3
         blk['col'] = (g * sp.nl + i) * D
         return blk
