@@ -56,19 +56,26 @@ MEP_DEV bool aligned16(const mep_rows& r) {
     return ((r.ptr & 15) == 0) && (r.sB % 4 == 0) && (r.sT % 4 == 0);
 }
 
-// four consecutive floats of row `row` (if < n) at column col
-MEP_DEV void load4(float* dst, const mep_rows& v, int base_row, int row, int n, int col, bool vec) {
-    if (row < n) {
-        const float* p = row_ptr(v, base_row + row) + col;
-        if (vec) {
-            const float4 t = *reinterpret_cast<const float4*>(p);
-            dst[0] = t.x; dst[1] = t.y; dst[2] = t.z; dst[3] = t.w;
-        } else {
-            dst[0] = p[0]; dst[1] = p[1]; dst[2] = p[2]; dst[3] = p[3];
-        }
-    } else {
-        dst[0] = dst[1] = dst[2] = dst[3] = 0.f;
-    }
+// element (batch b, time t) of a row view whose T is the attention length: no division
+MEP_DEV gfloat* at(const mep_rows& v, int b, int t) {
+    return G<float>(v.ptr) + (int64_t)b * v.sB + (int64_t)t * v.sT;
+}
+
+// four consecutive floats of row t (clamped into [0, n), zeroed when t >= n) at column col;
+// branch-free so the loads of a whole tile issue back to back
+MEP_DEV void load4(float* dst, const mep_rows& v, int b, int t, int n, int col, bool vec) {
+    const bool ok = t < n;
+    const gfloat* p = at(v, b, ok ? t : n - 1) + col;
+    float4 x;
+    if (vec) x = ldg4(p);
+    else x = make_float4(p[0], p[1], p[2], p[3]);
+    dst[0] = ok ? x.x : 0.f; dst[1] = ok ? x.y : 0.f; dst[2] = ok ? x.z : 0.f; dst[3] = ok ? x.w : 0.f;
+}
+// one float of row t (clamped / zeroed as load4)
+MEP_DEV float load1(const mep_rows& v, int b, int t, int n, int col) {
+    const bool ok = t < n;
+    const float x = at(v, b, ok ? t : n - 1)[col];
+    return ok ? x : 0.f;
 }
 
 MEP_DEV float shfl(float v, int src) { return __shfl(v, src, 64); }
@@ -83,10 +90,10 @@ __global__ __launch_bounds__(THREADS) void k_attn_fwd(const mep_attn_desc* __res
     const int qc = task % nqc, bh = task / nqc;
     const int h = bh % d.H, b = bh / d.H;
     const int hc = h * HD;
-    const Score sc{d.s_prev != 0, d.s_prev ? *reinterpret_cast<const float*>(d.c) : 0.f};
-    const float* sprev = reinterpret_cast<const float*>(d.s_prev);
-    float* sout = reinterpret_cast<float*>(d.s_out);
-    const float* mask = reinterpret_cast<const float*>(d.mask) + (int64_t)b * d.mask_sB;
+    const Score sc{d.s_prev != 0, d.s_prev ? *G<const float>(d.c) : 0.f};
+    const gfloat* sprev = G<const float>(d.s_prev);
+    gfloat* sout = G<float>(d.s_out);
+    const gfloat* mask = G<const float>(d.mask) + (int64_t)b * d.mask_sB;
     const bool qv = aligned16(d.q), kv4 = aligned16(d.k);
     const int64_t sbase = ((int64_t)b * d.H + h) * d.Tq;
 
@@ -95,7 +102,7 @@ __global__ __launch_bounds__(THREADS) void k_attn_fwd(const mep_attn_desc* __res
     const int q_lo = qc * CH;
     const int nqt = min(4, (d.Tq - q_lo + 15) / 16);
 #pragma unroll
-    for (int qt = 0; qt < 4; ++qt) load4(qf[qt], d.q, b * d.Tq, q_lo + qt * 16 + c, d.Tq, hc + 4 * g, qv);
+    for (int qt = 0; qt < 4; ++qt) load4(qf[qt], d.q, b, q_lo + qt * 16 + c, d.Tq, hc + 4 * g, qv);
 
     floatx4 o[4];
     float m[4], l[4];
@@ -106,12 +113,13 @@ __global__ __launch_bounds__(THREADS) void k_attn_fwd(const mep_attn_desc* __res
     for (int kt = 0; kt < nkt; ++kt) {
         const int k0 = kt * 16;
         float kf[4], vf[4], mk[4];
-        load4(kf, d.k, b * d.Tk, k0 + c, d.Tk, hc + 4 * g, kv4);       // A: K[k0+c][4g+s]
+        load4(kf, d.k, b, k0 + c, d.Tk, hc + 4 * g, kv4);               // A: K[k0+c][4g+s]
 #pragma unroll
         for (int s = 0; s < 4; ++s) {                                   // B of P.V: V[k0+4g+s][c]
             const int kk = k0 + 4 * g + s;
-            vf[s] = kk < d.Tk ? row_ptr(d.v, b * d.Tk + kk)[hc + c] : 0.f;
-            mk[s] = kk < d.Tk ? mask[kk] : 0.f;
+            vf[s] = load1(d.v, b, kk, d.Tk, hc + c);
+            const float mv = mask[min(kk, d.Tk - 1)];
+            mk[s] = kk < d.Tk ? mv : 0.f;
         }
 #pragma unroll
         for (int qt = 0; qt < 4; ++qt) {
@@ -149,7 +157,7 @@ __global__ __launch_bounds__(THREADS) void k_attn_fwd(const mep_attn_desc* __res
             for (int s = 0; s < 4; ++s) o[qt] = mfma16(p[s], vf[s], o[qt]);  // C[query 4g+r][dim c]
         }
     }
-    float* stats = reinterpret_cast<float*>(d.stats);
+    gfloat* stats = G<float>(d.stats);
 #pragma unroll
     for (int qt = 0; qt < 4; ++qt) {
         if (qt >= nqt) break;
@@ -165,7 +173,7 @@ __global__ __launch_bounds__(THREADS) void k_attn_fwd(const mep_attn_desc* __res
         for (int r = 0; r < 4; ++r) {
             const float ir = shfl(inv, 4 * g + r);
             const int qq = q_lo + qt * 16 + 4 * g + r;
-            if (qq < d.Tq) row_ptr(d.x, b * d.Tq + qq)[hc + c] = o[qt][r] * ir;
+            if (qq < d.Tq) (at(d.x, b, qq))[hc + c] = o[qt][r] * ir;
         }
     }
 }
@@ -188,12 +196,12 @@ __global__ __launch_bounds__(THREADS) void k_attn_bwd(const mep_attn_bwd_desc* _
     const int kc = task % nkc, bh = task / nkc;
     const int h = bh % d.H, b = bh / d.H;
     const int hc = h * HD;
-    const Score sc{d.s_prev != 0, d.s_prev ? *reinterpret_cast<const float*>(d.c) : 0.f};
-    const float* sprev = reinterpret_cast<const float*>(d.s_prev);
-    const float* dsn = reinterpret_cast<const float*>(bd.ds_next);
-    float* dsp = reinterpret_cast<float*>(bd.ds_prev);
-    const float* stats = reinterpret_cast<const float*>(d.stats);
-    const float* mask = reinterpret_cast<const float*>(d.mask) + (int64_t)b * d.mask_sB;
+    const Score sc{d.s_prev != 0, d.s_prev ? *G<const float>(d.c) : 0.f};
+    const gfloat* sprev = G<const float>(d.s_prev);
+    const gfloat* dsn = G<const float>(bd.ds_next);
+    gfloat* dsp = G<float>(bd.ds_prev);
+    const gfloat* stats = G<const float>(d.stats);
+    const gfloat* mask = G<const float>(d.mask) + (int64_t)b * d.mask_sB;
     const int64_t sbase = ((int64_t)b * d.H + h) * d.Tq;
     const bool qv = aligned16(d.q), kv4 = aligned16(d.k), vv4 = aligned16(d.v), gv = aligned16(bd.dx);
     float* T = Tr[wave];
@@ -207,14 +215,12 @@ __global__ __launch_bounds__(THREADS) void k_attn_bwd(const mep_attn_bwd_desc* _
 #pragma unroll
     for (int kt = 0; kt < 4; ++kt) {
         const int k0 = k_lo + kt * 16;
-        load4(kb[kt], d.k, b * d.Tk, k0 + c, d.Tk, hc + 4 * g, kv4);
-        load4(vb[kt], d.v, b * d.Tk, k0 + c, d.Tk, hc + 4 * g, vv4);
-        mkey[kt] = (k0 + c < d.Tk) ? mask[k0 + c] : 0.f;
+        load4(kb[kt], d.k, b, k0 + c, d.Tk, hc + 4 * g, kv4);
+        load4(vb[kt], d.v, b, k0 + c, d.Tk, hc + 4 * g, vv4);
+        const float mv = mask[min(k0 + c, d.Tk - 1)];
+        mkey[kt] = (k0 + c < d.Tk) ? mv : 0.f;
 #pragma unroll
-        for (int s = 0; s < 4; ++s) {
-            const int kk = k0 + 4 * g + s;
-            kq[kt][s] = kk < d.Tk ? row_ptr(d.k, b * d.Tk + kk)[hc + c] : 0.f;
-        }
+        for (int s = 0; s < 4; ++s) kq[kt][s] = load1(d.k, b, k0 + 4 * g + s, d.Tk, hc + c);
         dk[kt] = zero4();
         dv[kt] = zero4();
     }
@@ -223,23 +229,25 @@ __global__ __launch_bounds__(THREADS) void k_attn_bwd(const mep_attn_bwd_desc* _
     for (int qt = 0; qt < nqt; ++qt) {
         const int q0 = qt * 16;
         float qa[4], da[4], db[4], qb[4], mm[4], li[4], del[4];
-        load4(qa, d.q, b * d.Tq, q0 + c, d.Tq, hc + 4 * g, qv);        // A of S: Q[q0+c][4g+s]
-        load4(da, bd.dx, b * d.Tq, q0 + c, d.Tq, hc + 4 * g, gv);      // A of dP: dO[q0+c][4g+s]
+        load4(qa, d.q, b, q0 + c, d.Tq, hc + 4 * g, qv);                // A of S: Q[q0+c][4g+s]
+        load4(da, bd.dx, b, q0 + c, d.Tq, hc + 4 * g, gv);              // A of dP: dO[q0+c][4g+s]
 #pragma unroll
         for (int s = 0; s < 4; ++s) {                                  // B of dV / dK: rows 4g+s, dim c
             const int qq = q0 + 4 * g + s;
             const bool ok = qq < d.Tq;
-            db[s] = ok ? row_ptr(bd.dx, b * d.Tq + qq)[hc + c] : 0.f;
-            qb[s] = ok ? row_ptr(d.q, b * d.Tq + qq)[hc + c] : 0.f;
-            const float ov = ok ? row_ptr(d.x, b * d.Tq + qq)[hc + c] : 0.f;
+            const int qc2 = ok ? qq : d.Tq - 1;
+            db[s] = load1(bd.dx, b, qq, d.Tq, hc + c);
+            qb[s] = load1(d.q, b, qq, d.Tq, hc + c);
+            const float ov = load1(d.x, b, qq, d.Tq, hc + c);
             float pr = db[s] * ov;                                     // delta = rowsum(dO * O)
             pr += shfl(pr, lane ^ 1);
             pr += shfl(pr, lane ^ 2);
             pr += shfl(pr, lane ^ 4);
             pr += shfl(pr, lane ^ 8);
             del[s] = pr;
-            mm[s] = ok ? stats[2 * (sbase + qq)] : 0.f;
-            li[s] = ok ? stats[2 * (sbase + qq) + 1] : 0.f;
+            const float m0 = stats[2 * (sbase + qc2)], l0 = stats[2 * (sbase + qc2) + 1];
+            mm[s] = ok ? m0 : 0.f;
+            li[s] = ok ? l0 : 0.f;
         }
         floatx4 dq = zero4();
 #pragma unroll
@@ -291,9 +299,9 @@ __global__ __launch_bounds__(THREADS) void k_attn_bwd(const mep_attn_bwd_desc* _
         for (int r = 0; r < 4; ++r) {
             const int qq = q0 + 4 * g + r;
             if (qq < d.Tq) {
-                float* dqp = row_ptr(bd.dq, b * d.Tq + qq) + hc + c;
+                gfloat* dqp = at(bd.dq, b, qq) + hc + c;
                 if (nkc == 1) *dqp += dq[r] * INV_SCALE;
-                else atomicAdd(dqp, dq[r] * INV_SCALE);
+                else atomicAdd(reinterpret_cast<float*>(reinterpret_cast<uintptr_t>(dqp)), dq[r] * INV_SCALE);
             }
         }
     }
@@ -305,18 +313,18 @@ __global__ __launch_bounds__(THREADS) void k_attn_bwd(const mep_attn_bwd_desc* _
         for (int r = 0; r < 4; ++r) {
             const int kk = k_lo + kt * 16 + 4 * g + r;
             if (kk >= d.Tk) continue;
-            float* dkp = row_ptr(bd.dk, b * d.Tk + kk) + hc + c;
+            gfloat* dkp = at(bd.dk, b, kk) + hc + c;
             if (same_kv) {
                 *dkp = dk[kt][r] * INV_SCALE + dv[kt][r];
             } else {
                 *dkp = dk[kt][r] * INV_SCALE;
-                row_ptr(bd.dv, b * d.Tk + kk)[hc + c] = dv[kt][r];
+                (at(bd.dv, b, kk))[hc + c] = dv[kt][r];
             }
         }
     }
     if (bd.dc_partial) {
         const float w = wave_sum(dc_acc);
-        if (lane == 0) reinterpret_cast<float*>(bd.dc_partial)[task] = w;
+        if (lane == 0) G<float>(bd.dc_partial)[task] = w;
     }
 }
 

@@ -31,8 +31,8 @@ MEP_DEV void stage(float* dst, const mep_rows& src, int tok0, int ntok) {
         const int tok = tok0 + row;
         float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
         if (tok < ntok) {
-            const float* p = row_ptr(src, tok) + 4 * c4;
-            if (vec) v = *reinterpret_cast<const float4*>(p);
+            const gfloat* p = row_ptr(src, tok) + 4 * c4;
+            if (vec) v = ldg4(p);
             else v = make_float4(p[0], p[1], p[2], p[3]);
         }
         *reinterpret_cast<float4*>(dst + row * LD + 4 * c4) = v;
@@ -54,10 +54,10 @@ __global__ __launch_bounds__(THREADS) void k_epi_fwd(const mep_epi_desc* __restr
     const int mh = wave & 1, nblk = wave >> 1;
     const bool task = wave < NTASK;
     const int col = nblk * 32 + (lane & 31);
-    const float* Wp = reinterpret_cast<const float*>(d.wp);
-    const float* Wm = reinterpret_cast<const float*>(d.wm);
+    const gfloat* Wp = G<const float>(d.wp);
+    const gfloat* Wm = G<const float>(d.wm);
     const float p = d.drop_p;
-    const uint64_t seed = (d.seed && p > 0.f) ? *reinterpret_cast<const uint64_t*>(d.seed) : 0;
+    const uint64_t seed = (d.seed && p > 0.f) ? *G<const uint64_t>(d.seed) : 0;
 
     stage<D>(Xs, d.x, tok0, d.ntok);
     stage<D>(Qs, d.q, tok0, d.ntok);
@@ -94,9 +94,9 @@ __global__ __launch_bounds__(THREADS) void k_epi_fwd(const mep_epi_desc* __restr
     }
     __syncthreads();
     // LayerNorm: wave per row, lane covers columns lane and lane+64
-    const float* lw = reinterpret_cast<const float*>(d.ln_w);
-    const float* lb = reinterpret_cast<const float*>(d.ln_b);
-    float* stats = reinterpret_cast<float*>(d.stats);
+    const gfloat* lw = G<const float>(d.ln_w);
+    const gfloat* lb = G<const float>(d.ln_b);
+    gfloat* stats = G<float>(d.stats);
     const bool c0 = lane < D, c1 = lane + 64 < D;
     const float w0 = c0 ? lw[lane] : 0.f, w1 = c1 ? lw[lane + 64] : 0.f;
     const float b0 = c0 ? lb[lane] : 0.f, b1 = c1 ? lb[lane + 64] : 0.f;
@@ -109,7 +109,7 @@ __global__ __launch_bounds__(THREADS) void k_epi_fwd(const mep_epi_desc* __restr
         const float d0 = c0 ? x0 - mean : 0.f, d1 = c1 ? x1 - mean : 0.f;
         const float var = wave_sum(d0 * d0 + d1 * d1) / (float)D;
         const float rstd = 1.0f / sqrtf(var + LN_EPS);
-        float* out = row_ptr(d.out, tok);
+        gfloat* out = row_ptr(d.out, tok);
         if (c0) {
             float y = d0 * rstd * w0 + b0;
             if (p > 0.f) y *= drop_scale(seed, 2u * d.drop_stream + 1u, (uint64_t)tok * D + lane, p);
@@ -137,7 +137,7 @@ __global__ __launch_bounds__(THREADS) void k_epi_bwd(const mep_epi_bwd_desc* __r
     float* red = smem + 2 * 64 * LD;  // [8 waves][2][128]
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const float p = d.drop_p;
-    const uint64_t seed = (d.seed && p > 0.f) ? *reinterpret_cast<const uint64_t*>(d.seed) : 0;
+    const uint64_t seed = (d.seed && p > 0.f) ? *G<const uint64_t>(d.seed) : 0;
 
     stage<D>(Gs, bd.dout, tok0, d.ntok);
     if (bd.dout2.ptr) {
@@ -151,8 +151,8 @@ __global__ __launch_bounds__(THREADS) void k_epi_bwd(const mep_epi_bwd_desc* __r
     }
     __syncthreads();
     // LayerNorm backward, wave per row
-    const float* lw = reinterpret_cast<const float*>(d.ln_w);
-    const float* stats = reinterpret_cast<const float*>(d.stats);
+    const gfloat* lw = G<const float>(d.ln_w);
+    const gfloat* stats = G<const float>(d.stats);
     float pw0 = 0.f, pw1 = 0.f, pb0 = 0.f, pb1 = 0.f;
     const bool c0 = lane < D, c1 = lane + 64 < D;
     const float w0 = c0 ? lw[lane] : 0.f, w1 = c1 ? lw[lane + 64] : 0.f;
@@ -164,7 +164,7 @@ __global__ __launch_bounds__(THREADS) void k_epi_bwd(const mep_epi_bwd_desc* __r
             continue;
         }
         const float mean = stats[2 * tok], rstd = stats[2 * tok + 1];
-        const float* zr = row_ptr(d.z, tok);
+        const gfloat* zr = row_ptr(d.z, tok);
         float g0 = c0 ? Gs[row * LD + lane] : 0.f;
         float g1 = c1 ? Gs[row * LD + lane + 64] : 0.f;
         if (p > 0.f) {
@@ -177,7 +177,7 @@ __global__ __launch_bounds__(THREADS) void k_epi_bwd(const mep_epi_bwd_desc* __r
         const float s1 = wave_sum(gw0 + gw1) / (float)D;
         const float s2 = wave_sum(gw0 * xh0 + gw1 * xh1) / (float)D;
         pw0 += g0 * xh0; pw1 += g1 * xh1; pb0 += g0; pb1 += g1;
-        float* dzr = row_ptr(bd.dz, tok);
+        gfloat* dzr = row_ptr(bd.dz, tok);
         if (c0) { const float v = rstd * (gw0 - s1 - xh0 * s2); Gs[row * LD + lane] = v; dzr[lane] = v; }
         if (c1) { const float v = rstd * (gw1 - s1 - xh1 * s2); Gs[row * LD + lane + 64] = v; dzr[lane + 64] = v; }
     }
@@ -187,7 +187,7 @@ __global__ __launch_bounds__(THREADS) void k_epi_bwd(const mep_epi_bwd_desc* __r
     red[(wave * 2 + 1) * 128 + lane + 64] = pb1;
     __syncthreads();
     if (bd.ln_partial) {
-        float* lp = reinterpret_cast<float*>(bd.ln_partial) + (int64_t)blockIdx.x * 2 * D;
+        gfloat* lp = G<float>(bd.ln_partial) + (int64_t)blockIdx.x * 2 * D;
         for (int idx = threadIdx.x; idx < 2 * D; idx += THREADS) {
             const int which = idx / D, c = idx - which * D;
             float s = 0.f;
@@ -201,8 +201,8 @@ __global__ __launch_bounds__(THREADS) void k_epi_bwd(const mep_epi_bwd_desc* __r
     const int mh = wave & 1, nblk = wave >> 1;
     const bool task = wave < NTASK;
     const int col = nblk * 32 + (lane & 31);
-    const float* Wm = reinterpret_cast<const float*>(d.wm);
-    const float* Wp = reinterpret_cast<const float*>(d.wp);
+    const gfloat* Wm = G<const float>(d.wm);
+    const gfloat* Wp = G<const float>(d.wp);
     if (task) {
         floatx16 aq = zero16(), ap = zero16();
         mma_tile<false, D>(aq, Gs, LD, mh * 32, Wm, 2 * D, nblk * 32, D, 0, D, D, false);
@@ -215,7 +215,7 @@ __global__ __launch_bounds__(THREADS) void k_epi_bwd(const mep_epi_bwd_desc* __r
             if (p > 0.f && tok < d.ntok) vp *= drop_scale(seed, 2u * d.drop_stream, (uint64_t)tok * D + col, p);
             Ps[row * LD + col] = (tok < d.ntok) ? vp : 0.f;
             if (tok < d.ntok) {
-                float* q = row_ptr(bd.dq, tok) + col;
+                gfloat* q = row_ptr(bd.dq, tok) + col;
                 *q = bd.dq_accumulate ? *q + aq[r] : aq[r];
                 row_ptr(bd.dxp, tok)[col] = vp;
             }
@@ -239,7 +239,7 @@ __global__ __launch_bounds__(256) void k_ln_fwd(const mep_ln_desc* __restrict__ 
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int tok = blockIdx.x * 4 + wave;
     if (tok >= d.ntok) return;
-    const float* x = row_ptr(d.x, tok);
+    const gfloat* x = row_ptr(d.x, tok);
     float v[4], s = 0.f;
 #pragma unroll
     for (int j = 0; j < 4; ++j) { const int c = lane + 64 * j; v[j] = c < d.D ? x[c] : 0.f; s += v[j]; }
@@ -248,13 +248,13 @@ __global__ __launch_bounds__(256) void k_ln_fwd(const mep_ln_desc* __restrict__ 
 #pragma unroll
     for (int j = 0; j < 4; ++j) { const int c = lane + 64 * j; v[j] = c < d.D ? v[j] - mean : 0.f; q += v[j] * v[j]; }
     const float rstd = 1.0f / sqrtf(wave_sum(q) / (float)d.D + LN_EPS);
-    const float* w = reinterpret_cast<const float*>(d.w);
-    const float* b = reinterpret_cast<const float*>(d.b);
-    float* y = row_ptr(d.y, tok);
+    const gfloat* w = G<const float>(d.w);
+    const gfloat* b = G<const float>(d.b);
+    gfloat* y = row_ptr(d.y, tok);
 #pragma unroll
     for (int j = 0; j < 4; ++j) { const int c = lane + 64 * j; if (c < d.D) y[c] = v[j] * rstd * w[c] + b[c]; }
     if (lane == 0) {
-        float* st = reinterpret_cast<float*>(d.stats);
+        gfloat* st = G<float>(d.stats);
         st[2 * tok] = mean;
         st[2 * tok + 1] = rstd;
     }
@@ -268,14 +268,14 @@ __global__ __launch_bounds__(256) void k_ln_bwd(const mep_ln_desc* __restrict__ 
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     __shared__ float red[4][2][256];
     float pw[4] = {0.f, 0.f, 0.f, 0.f}, pb[4] = {0.f, 0.f, 0.f, 0.f};
-    const float* w = reinterpret_cast<const float*>(d.w);
-    const float* st = reinterpret_cast<const float*>(d.stats);
+    const gfloat* w = G<const float>(d.w);
+    const gfloat* st = G<const float>(d.stats);
     for (int row = wave; row < 64; row += 4) {
         const int tok = tok0 + row;
         if (tok >= d.ntok) break;
         const float mean = st[2 * tok], rstd = st[2 * tok + 1];
-        const float* x = row_ptr(d.x, tok);
-        const float* dy = row_ptr(d.dy, tok);
+        const gfloat* x = row_ptr(d.x, tok);
+        const gfloat* dy = row_ptr(d.dy, tok);
         float xh[4], gw[4], s1 = 0.f, s2 = 0.f;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
@@ -291,7 +291,7 @@ __global__ __launch_bounds__(256) void k_ln_bwd(const mep_ln_desc* __restrict__ 
         }
         s1 = wave_sum(s1) / (float)d.D;
         s2 = wave_sum(s2) / (float)d.D;
-        float* dx = row_ptr(d.dx, tok);
+        gfloat* dx = row_ptr(d.dx, tok);
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             const int c = lane + 64 * j;
@@ -305,7 +305,7 @@ __global__ __launch_bounds__(256) void k_ln_bwd(const mep_ln_desc* __restrict__ 
     for (int j = 0; j < 4; ++j) { red[wave][0][lane + 64 * j] = pw[j]; red[wave][1][lane + 64 * j] = pb[j]; }
     __syncthreads();
     if (d.partial) {
-        float* lp = reinterpret_cast<float*>(d.partial) + (int64_t)blockIdx.x * 2 * d.D;
+        gfloat* lp = G<float>(d.partial) + (int64_t)blockIdx.x * 2 * d.D;
         for (int idx = threadIdx.x; idx < 2 * d.D; idx += 256) {
             const int which = idx / d.D, c = idx - which * d.D;
             lp[idx] = red[0][which][c] + red[1][which][c] + red[2][which][c] + red[3][which][c];

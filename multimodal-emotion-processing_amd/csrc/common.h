@@ -8,8 +8,24 @@
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 
 #define MEP_DEV __device__ __forceinline__
+// Device memory is addressed through the GLOBAL address space explicitly: pointers rebuilt from
+// the 64-bit integers of a descriptor are otherwise generic and every access becomes a FLAT
+// instruction (counted on both vmcnt and lgkmcnt, serialising LDS and VMEM waits).
+#define MEP_G __attribute__((address_space(1)))
 
 namespace mep {
+
+typedef MEP_G float gfloat;
+template <typename T>
+MEP_DEV MEP_G T* G(uint64_t p) { return reinterpret_cast<MEP_G T*>(p); }
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+// 16-byte global load / store (p must be 16-byte aligned)
+MEP_DEV float4 ldg4(const gfloat* p) {
+    const f32x4 v = *reinterpret_cast<const MEP_G f32x4*>(p);
+    return make_float4(v.x, v.y, v.z, v.w);
+}
+MEP_DEV void stg4(gfloat* p, float4 v) { *reinterpret_cast<MEP_G f32x4*>(p) = f32x4{v.x, v.y, v.z, v.w}; }
 
 constexpr int kWave = 64;
 
@@ -19,7 +35,7 @@ MEP_DEV int64_t row_off(const mep_rows& r, int tok) {
     int t = tok - b * r.T;
     return (int64_t)b * r.sB + (int64_t)t * r.sT;
 }
-MEP_DEV float* row_ptr(const mep_rows& r, int tok) { return reinterpret_cast<float*>(r.ptr) + row_off(r, tok); }
+MEP_DEV gfloat* row_ptr(const mep_rows& r, int tok) { return G<float>(r.ptr) + row_off(r, tok); }
 
 // ------------------------------------------------------------------ exact-rounding scalar ops
 // The residual-score sequence of the reference ((q.k)/sqrt(d) + c*S_prev - 1e8*(1-m)) is
@@ -71,14 +87,14 @@ MEP_DEV int acc_row(int r, int lane) { return (r & 3) + 8 * (r >> 2) + 4 * (lane
 // KC > 0: compile-time chunk width (fully unrolled, so hipcc issues every weight load of the
 // chunk ahead of the MFMA chain); KC == 0: runtime width kc.
 template <bool NT>
-MEP_DEV void mma_step(floatx16& acc, const float* __restrict__ arow, const float* __restrict__ W, int ldw, int n,
+MEP_DEV void mma_step(floatx16& acc, const float* __restrict__ arow, const gfloat* __restrict__ W, int ldw, int n,
                       bool nval, int kk, int kg, int K, bool w_vec) {
     const float4 a = *reinterpret_cast<const float4*>(arow + kk);
     float b0 = 0.f, b1 = 0.f, b2 = 0.f, b3 = 0.f;
     if (NT) {
-        const float* wp = W + (int64_t)n * ldw + kg;
+        const gfloat* wp = W + (int64_t)n * ldw + kg;
         if (nval && w_vec && kg + 3 < K) {
-            const float4 b = *reinterpret_cast<const float4*>(wp);
+            const float4 b = ldg4(wp);
             b0 = b.x; b1 = b.y; b2 = b.z; b3 = b.w;
         } else if (nval) {
             if (kg < K) b0 = wp[0];
@@ -88,7 +104,7 @@ MEP_DEV void mma_step(floatx16& acc, const float* __restrict__ arow, const float
         }
     } else {
         if (nval) {
-            const float* wp = W + (int64_t)kg * ldw + n;
+            const gfloat* wp = W + (int64_t)kg * ldw + n;
             if (kg < K) b0 = wp[0];
             if (kg + 1 < K) b1 = wp[ldw];
             if (kg + 2 < K) b2 = wp[2 * ldw];
@@ -103,7 +119,7 @@ MEP_DEV void mma_step(floatx16& acc, const float* __restrict__ arow, const float
 
 template <bool NT, int KC = 0>
 MEP_DEV void mma_tile(floatx16& acc, const float* __restrict__ As, int lda, int m0,
-                      const float* __restrict__ W, int ldw, int n0, int N, int k0, int kc, int K,
+                      const gfloat* __restrict__ W, int ldw, int n0, int N, int k0, int kc, int K,
                       bool w_vec) {
     const int lane = threadIdx.x & 63;
     const int r = lane & 31;
@@ -155,7 +171,7 @@ MEP_DEV void stage_cols(float* __restrict__ dst, int ld, const mep_rows& src, in
             const int row = s / nc4, c = 4 * (s - row * nc4);
             const int tok = t0 + row;
             float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-            if (tok < t_end) v = *reinterpret_cast<const float4*>(row_ptr(src, tok) + c0 + c);
+            if (tok < t_end) v = ldg4(row_ptr(src, tok) + c0 + c);
             *reinterpret_cast<float4*>(dst + row * ld + c) = v;
         }
     } else {

@@ -26,10 +26,10 @@ __global__ __launch_bounds__(GEMM_THREADS) void k_gemm(const mep_gemm_desc* __re
 
     const int wave = threadIdx.x >> 6;
     const int lane = threadIdx.x & 63;
-    const float* W = reinterpret_cast<const float*>(d.w);
+    const gfloat* W = G<const float>(d.w);
     const bool w_vec = d.w_nt && (d.ldw % 4 == 0) && ((d.w & 15) == 0);
-    const float* bias = reinterpret_cast<const float*>(d.bias);
-    const float* table = reinterpret_cast<const float*>(d.table);
+    const gfloat* bias = G<const float>(d.bias);
+    const gfloat* table = G<const float>(d.table);
 
     // column groups of 256 (8 waves x 2 tasks x 32 cols / 2 m-halves); A is re-staged per group
     for (int cg = 0; cg < d.N; cg += 256) {
@@ -79,7 +79,7 @@ __global__ __launch_bounds__(GEMM_THREADS) void k_gemm(const mep_gemm_desc* __re
                 if (bias) v += bcol;
                 if (table) v += table[(tok % d.y.T) * d.N + col];
                 if (d.relu) v = fmaxf(v, 0.f);
-                float* yp = row_ptr(d.y, tok) + col;
+                gfloat* yp = row_ptr(d.y, tok) + col;
                 if (d.accumulate) v += *yp;
                 *yp = v;
             }
@@ -145,7 +145,7 @@ __global__ __launch_bounds__(WG_THREADS) void k_wgrad(const mep_wgrad_desc* __re
             }
         }
     }
-    float* part = reinterpret_cast<float*>(d.partial) + (int64_t)split * d.N * d.Ktot;
+    gfloat* part = G<float>(d.partial) + (int64_t)split * d.N * d.Ktot;
 #pragma unroll
     for (int t = 0; t < WG_MAXT; ++t) {
         const int task = wave + 8 * t;
@@ -166,14 +166,14 @@ __global__ __launch_bounds__(256) void k_wgrad_reduce(const mep_wgrad_desc* __re
     const int64_t nk = (int64_t)d.N * d.Ktot;
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= nk) return;
-    const float* part = reinterpret_cast<const float*>(d.partial);
+    const gfloat* part = G<const float>(d.partial);
     float s = 0.f;
     for (int sp = 0; sp < d.n_split; ++sp) s += part[sp * nk + i];
     const int n = (int)(i / d.Ktot);
     int k = (int)(i - (int64_t)n * d.Ktot);
     int j = 0;
     while (j < d.n_b - 1 && k >= d.kb[j]) { k -= d.kb[j]; ++j; }
-    float* o = reinterpret_cast<float*>(d.out[j]) + (int64_t)n * d.ldo[j] + k;
+    gfloat* o = G<float>(d.out[j]) + (int64_t)n * d.ldo[j] + k;
     *o = d.accumulate ? *o + s : s;
 }
 

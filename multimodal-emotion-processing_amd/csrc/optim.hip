@@ -112,7 +112,7 @@ __global__ __launch_bounds__(256) void k_colsum(const mep_colsum_desc* __restric
     __shared__ float red[8][32];
     float s = 0.f;
     if (c < d.n_cols) {
-        const float* p = reinterpret_cast<const float*>(d.partial) + c;
+        const gfloat* p = G<const float>(d.partial) + c;
         for (int r = g; r < d.n_rows; r += 8) s += p[(int64_t)r * d.ld];
     }
     red[g][cl] = s;
@@ -121,7 +121,7 @@ __global__ __launch_bounds__(256) void k_colsum(const mep_colsum_desc* __restric
         float t = 0.f;
 #pragma unroll
         for (int k = 0; k < 8; ++k) t += red[k][cl];
-        float* o = reinterpret_cast<float*>(d.out) + c;
+        gfloat* o = G<float>(d.out) + c;
         *o = d.accumulate ? *o + t : t;
     }
 }
@@ -135,12 +135,12 @@ __global__ __launch_bounds__(256) void k_sum_rows(const mep_sum_desc* __restrict
         const int tok = (int)(i / D4), c = 4 * (int)(i - (int64_t)tok * D4);
         float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
         for (int k = 0; k < d.n_src; ++k) {
-            const float4 v = *reinterpret_cast<const float4*>(row_ptr(d.src[k], tok) + c);
+            const float4 v = ldg4(row_ptr(d.src[k], tok) + c);
             s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
         }
-        float4* o = reinterpret_cast<float4*>(row_ptr(d.out, tok) + c);
-        if (d.accumulate) { const float4 v = *o; s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w; }
-        *o = s;
+        gfloat* o = row_ptr(d.out, tok) + c;
+        if (d.accumulate) { const float4 v = ldg4(o); s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w; }
+        stg4(o, s);
     }
 }
 

@@ -33,7 +33,7 @@ __global__ __launch_bounds__(256) void k_pool_fwd(const mep_pool_desc* __restric
     float s = 0.f, mx = -INFINITY;
     int idx = 0x7fffffff;
     if (c < d.C) {
-        const float* x = reinterpret_cast<const float*>(d.x) + (int64_t)b * d.T * d.C + c;
+        const gfloat* x = G<const float>(d.x) + (int64_t)b * d.T * d.C + c;
         for (int t = g; t < d.T; t += POOL_GROUPS) {
             const float v = x[(int64_t)t * d.C];
             s += v;
@@ -54,10 +54,10 @@ __global__ __launch_bounds__(256) void k_pool_fwd(const mep_pool_desc* __restric
             const int i = s_idx[k][cl];
             if (i != 0x7fffffff && (m > tm || (m == tm && i < ti))) { tm = m; ti = i; }
         }
-        float* pooled = reinterpret_cast<float*>(d.pooled) + (int64_t)b * 2 * d.C;
+        gfloat* pooled = G<float>(d.pooled) + (int64_t)b * 2 * d.C;
         pooled[c] = ts / (float)d.T;
         pooled[d.C + c] = tm;
-        reinterpret_cast<int*>(d.argmax)[(int64_t)b * d.C + c] = ti;
+        G<int>(d.argmax)[(int64_t)b * d.C + c] = ti;
     }
 }
 
@@ -65,9 +65,9 @@ __global__ __launch_bounds__(256) void k_pool_fwd(const mep_pool_desc* __restric
 __global__ __launch_bounds__(256) void k_pool_bwd(const mep_pool_desc* __restrict__ descs) {
     const mep_pool_desc& d = descs[blockIdx.y];
     const int64_t total = (int64_t)d.B * d.T * d.C;
-    const float* dp = reinterpret_cast<const float*>(d.dpooled);
-    const int* am = reinterpret_cast<const int*>(d.argmax);
-    float* dx = reinterpret_cast<float*>(d.dx);
+    const gfloat* dp = G<const float>(d.dpooled);
+    const MEP_G int* am = G<const int>(d.argmax);
+    gfloat* dx = G<float>(d.dx);
     for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
         const int c = (int)(i % d.C);
         const int64_t bt = i / d.C;
@@ -97,8 +97,8 @@ __host__ __device__ inline HeadOff head_off(int NC) {
 }
 
 MEP_DEV float label_at(const mep_head_desc& d, int b, int n) {
-    if (d.labels_are_float) return reinterpret_cast<const float*>(d.labels)[b * d.NC + n];
-    return (float)reinterpret_cast<const int64_t*>(d.labels)[b * d.NC + n];
+    if (d.labels_are_float) return G<const float>(d.labels)[b * d.NC + n];
+    return (float)G<const int64_t>(d.labels)[b * d.NC + n];
 }
 
 // make LDS writes of this wave visible to its other lanes
@@ -118,23 +118,23 @@ __global__ __launch_bounds__(256) void k_head(mep_head_desc d) {
     __shared__ float s_temp[2][NCMAX * NCMAX];
     __shared__ float s_yhat[2][NCMAX], s_cat[2][2 * NCMAX], s_rstd[2];
     __shared__ float s_dlast[2][NCMAX], s_dthis[2][NCMAX];
-    const float* wc0 = reinterpret_cast<const float*>(d.wc0);
-    const float* wc1 = reinterpret_cast<const float*>(d.wc1);
-    const float* trans = reinterpret_cast<const float*>(d.trans);
-    const float* lnw = reinterpret_cast<const float*>(d.ln_w);
-    const float* lnb = reinterpret_cast<const float*>(d.ln_b);
-    const float* wo = reinterpret_cast<const float*>(d.wo);
-    const float* bo = reinterpret_cast<const float*>(d.bo);
+    const gfloat* wc0 = G<const float>(d.wc0);
+    const gfloat* wc1 = G<const float>(d.wc1);
+    const gfloat* trans = G<const float>(d.trans);
+    const gfloat* lnw = G<const float>(d.ln_w);
+    const gfloat* lnb = G<const float>(d.ln_b);
+    const gfloat* wo = G<const float>(d.wo);
+    const gfloat* bo = G<const float>(d.bo);
 
     // classifiers (Multi_ATTN.classifier, no bias): one wave per output, lanes over F
     for (int rr = 0; rr < rows; ++rr) {
         const int b = r0 + rr;
-        const float* p0 = reinterpret_cast<const float*>(d.pooled0) + (int64_t)b * F;
-        const float* p1 = reinterpret_cast<const float*>(d.pooled1) + (int64_t)b * F;
+        const gfloat* p0 = G<const float>(d.pooled0) + (int64_t)b * F;
+        const gfloat* p1 = G<const float>(d.pooled1) + (int64_t)b * F;
         for (int task = wave; task < 2 * NC; task += 4) {
             const int e = task / NC, n = task - e * NC;
-            const float* w = (e ? wc1 : wc0) + (int64_t)n * F;
-            const float* p = e ? p1 : p0;
+            const gfloat* w = (e ? wc1 : wc0) + (int64_t)n * F;
+            const gfloat* p = e ? p1 : p0;
             float s = 0.f;
             for (int k = lane; k < F; k += 64) s = fmaf(w[k], p[k], s);
             s = wave_sum(s);
@@ -170,13 +170,13 @@ __global__ __launch_bounds__(256) void k_head(mep_head_desc d) {
                 float s = 0.f;
                 for (int j = 0; j < 2 * NC; ++j) s = fmaf(wo[lane * 2 * NC + j], s_cat[rr][j], s);
                 s_logit[rr][lane] = s + bo[lane];
-                reinterpret_cast<float*>(d.logits)[(r0 + rr) * NC + lane] = s + bo[lane];
+                G<float>(d.logits)[(r0 + rr) * NC + lane] = s + bo[lane];
             }
             wave_sync();
         }
         // losses: circle per row, then R-Drop KL for the pair
-        float* row_loss = reinterpret_cast<float*>(d.row_loss);
-        const float* ext = reinterpret_cast<const float*>(d.ext_dlogits);
+        gfloat* row_loss = G<float>(d.row_loss);
+        const gfloat* ext = G<const float>(d.ext_dlogits);
         if (ext) {
             for (int rr = 0; rr < rows; ++rr)
                 if (lane < NC) s_dlog[rr][lane] = ext[(r0 + rr) * NC + lane];
@@ -221,7 +221,7 @@ __global__ __launch_bounds__(256) void k_head(mep_head_desc d) {
         if (d.compute_grad) {
             const HeadOff o = head_off(NC);
             for (int rr = 0; rr < rows; ++rr) {
-                float* part = reinterpret_cast<float*>(d.partial) + (int64_t)(r0 + rr) * o.stride;
+                gfloat* part = G<float>(d.partial) + (int64_t)(r0 + rr) * o.stride;
                 // out Linear: dWo, dbo, dcat
                 for (int idx = lane; idx < NC * 2 * NC; idx += 64) {
                     const int n = idx / (2 * NC), j = idx - n * 2 * NC;
@@ -272,8 +272,8 @@ __global__ __launch_bounds__(256) void k_head(mep_head_desc d) {
     // dpooled_e = Wc_e^T dlogit_e
     for (int rr = 0; rr < rows; ++rr) {
         const int b = r0 + rr;
-        float* dp0 = reinterpret_cast<float*>(d.dpooled0) + (int64_t)b * F;
-        float* dp1 = reinterpret_cast<float*>(d.dpooled1) + (int64_t)b * F;
+        gfloat* dp0 = G<float>(d.dpooled0) + (int64_t)b * F;
+        gfloat* dp1 = G<float>(d.dpooled1) + (int64_t)b * F;
         for (int k = threadIdx.x; k < F; k += 256) {
             float a0 = 0.f, a1 = 0.f;
             for (int n = 0; n < NC; ++n) {
@@ -296,7 +296,7 @@ __global__ __launch_bounds__(256) void k_head_reduce(mep_head_desc d, HeadGrads 
     const int nA = o.dl0;                 // everything before the dlogit records
     const int nB = 2 * NC * F;
     const int i = blockIdx.x * 256 + threadIdx.x;
-    const float* part = reinterpret_cast<const float*>(d.partial);
+    const gfloat* part = G<const float>(d.partial);
     if (i < nA) {
         float s = 0.f;
         for (int b = 0; b < d.B; ++b) s += part[(int64_t)b * o.stride + i];
@@ -317,7 +317,7 @@ __global__ __launch_bounds__(256) void k_head_reduce(mep_head_desc d, HeadGrads 
         for (int b = 0; b < d.B; ++b) s = fmaf(part[(int64_t)b * o.stride + off + n], pooled[(int64_t)b * F + k], s);
         (e ? g.g_wc1 : g.g_wc0)[rem] = s;
     } else if (i == nA + nB) {
-        const float* rl = reinterpret_cast<const float*>(d.row_loss);
+        const gfloat* rl = G<const float>(d.row_loss);
         float s = 0.f;
         for (int b = 0; b < d.B; ++b) s += rl[b];
         *g.loss = s;
