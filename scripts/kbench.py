@@ -1,0 +1,69 @@
+"""Per-kernel micro-benchmark of the bench workload's launches (for profiling one kernel at a time).
+
+    python scripts/kbench.py [--kernel mep_attn_fwd] [--reps 50]
+Builds the cfg3 plan (Concat_Trans D=96 H=6 B=64 T=50), runs one eager step, then replays the
+chosen launch `reps` times and prints the average HIP-event time per launch.
+"""
+import argparse
+import os
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import mep_import  # noqa: E402
+
+mep_import.load()
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--kernel', default='all')
+    ap.add_argument('--reps', type=int, default=50)
+    ap.add_argument('--layers', type=int, default=1)
+    ap.add_argument('--T', type=int, default=50)
+    args = ap.parse_args()
+    from bench import synth_batch
+    from mep_amd import cmu_mosei
+    from mep_amd._lib import launch
+    from mep_amd.engine import TrainEngine
+    from mep_amd.optim import FusedAdamW
+    dev = torch.device('cuda:0')
+    torch.manual_seed(0)
+    T = args.T
+    model = cmu_mosei.Concat_Trans(dim=96, l_len=T, v_len=T, a_len=T, n_heads=6, n_layers=args.layers,
+                                   ffn=1).to(dev).train()
+    opt = FusedAdamW(model, lr=1e-3)
+    eng = TrainEngine(model, opt, graph=False)
+    plan = model.mep_runner(dev).plan(64, (T, T, T))
+    plan.set_inputs(*synth_batch(0, dev)) if T == 50 else None
+    eng.step_plan(plan)
+    torch.cuda.synchronize()
+    p = plan
+    D = p.spec.D
+    table = {
+        'mep_gemm': lambda: launch('mep_gemm', p.d_unify, p.t_unify),
+        'mep_attn_fwd': lambda: launch('mep_attn_fwd', p.d_attn[0], p.t_attn[0], threads=p.g_attn[0][2]),
+        'mep_block_epi_fwd': lambda: launch('mep_block_epi_fwd', p.d_epi[0], p.t_epi[0], threads=D),
+        'mep_block_epi_bwd': lambda: launch('mep_block_epi_bwd', p.d_epib[0], p.t_epi[0], threads=D),
+        'mep_attn_bwd': lambda: launch('mep_attn_bwd', p.d_attnb[0], p.t_attnb[0], threads=p.g_attn[0][3]),
+        'mep_wgrad': lambda: launch('mep_wgrad', p.d_wgrad, p.t_wgrad),
+        'mep_pool_fwd': lambda: launch('mep_pool_fwd', p.d_pool, p.t_pool),
+    }
+    names = list(table) if args.kernel == 'all' else [args.kernel]
+    for name in names:
+        fn = table[name]
+        fn()
+        torch.cuda.synchronize()
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        for _ in range(args.reps):
+            fn()
+        b.record()
+        torch.cuda.synchronize()
+        print('%-20s %8.2f us/launch' % (name, a.elapsed_time(b) / args.reps * 1e3), flush=True)
+
+
+if __name__ == '__main__':
+    main()
