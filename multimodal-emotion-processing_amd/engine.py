@@ -52,8 +52,7 @@ class TrainEngine:
         runner = self._runner(plan.device)
         self.opt._bind()
         self.opt._sync_hyper(self.clip, 1.0 / self.world)
-        p = runner.spec.drop_p if self.model.training else 0.0
-        plan.set_dropout(p)
+        plan.set_dropout(runner.drop_p())
         self._sync_params(runner)
         key = id(plan)
         g = self._graphs.get(key)
@@ -92,7 +91,7 @@ class TrainEngine:
     def step(self, l, v, a, lm, vm, am, labels):
         """Reference-shaped batch in, loss out (copies the batch into the plan's resident
         buffers first)."""
-        runner = self._runner(l.device)
+        runner = self._runner((l[0] if isinstance(l, (tuple, list)) else l).device)
         plan = runner.plan_for(l, v, a)
         plan.set_inputs(l, v, a, lm, vm, am, labels)
         return self.step_plan(plan)

@@ -12,10 +12,12 @@ from .trimodal import TriModalPlan
 
 
 class ModelRunner:
-    n_inputs = 6
-
-    def __init__(self, model, spec, device, labels_float=False):
+    def __init__(self, model, spec, device, labels_float=False, n_inputs=6, pack=None):
+        """``pack`` maps the model's forward arguments (``n_inputs`` tensors) to the plan's
+        (l, v, a, l_mask, v_mask, a_mask); None = they already are in that order."""
         self.model = model
+        self.n_inputs = n_inputs
+        self.pack = pack
         self.spec = spec
         self.device = torch.device(device)
         self.labels_float = labels_float
@@ -33,13 +35,26 @@ class ModelRunner:
         return p
 
     def plan_for(self, l, v, a):
-        return self.plan(l.shape[0], (l.shape[2], v.shape[2], a.shape[2]))
+        """Plan for a batch given either as [B, 2, T, d] (prev, cur) tensors (cmu-mosei) or as
+        (prev, cur) pairs of [B, T, d] tensors (Ren-MME's separate pre_/pro_ arguments)."""
+        def bt(x):
+            x0 = x[0] if isinstance(x, (tuple, list)) else x
+            return x0.shape[0], x0.shape[-2]
+        B = bt(l)[0]
+        return self.plan(B, (bt(l)[1], bt(v)[1], bt(a)[1]))
+
+    def drop_p(self):
+        """Dropout probability of the current mode (the model's live nn.Dropout p in train mode)."""
+        if not self.model.training:
+            return 0.0
+        fn = getattr(self.model, 'mep_drop_p', None)
+        return float(fn()) if fn is not None else self.spec.drop_p
 
     # ------------------------------------------------------------ autograd path
     def run_forward(self, inputs):
-        l, v, a, lm, vm, am = inputs
+        l, v, a, lm, vm, am = self.pack(inputs) if self.pack is not None else inputs
         plan = self.plan_for(l, v, a)
-        p = self.spec.drop_p if self.model.training else 0.0
+        p = self.drop_p()
         plan.set_dropout(p)
         if p > 0.0:
             plan.advance_seed()

@@ -160,3 +160,57 @@ def linear_nobias(x, w):
 def unify_forward(mod, l, v, a):
     return (linear_nobias(l, mod.linguistic.weight), linear_nobias(v, mod.visual.weight),
             linear_nobias(a, mod.acoustic.weight))
+
+
+class _LayerNormFn(torch.autograd.Function):
+    """Row LayerNorm on libmep_hip (Ren-MME's shared unify norm1, Ren-MME/run.py:164-166)."""
+
+    @staticmethod
+    def forward(ctx, x, w, b):
+        shape = x.shape
+        D = shape[-1]
+        x2 = _c(x).reshape(-1, D)
+        ntok = x2.shape[0]
+        dev = x.device
+        y = torch.empty_like(x2)
+        stats = torch.empty(ntok, 2, dtype=torch.float32, device=dev)
+        d = _lib.LnDesc(x=crows(x2, 1, D), y=crows(y, 1, D), dy=Rows(), dx=Rows(), w=w.data_ptr(), b=b.data_ptr(),
+                        stats=stats.data_ptr(), partial=0, ntok=ntok, D=D, dx_accumulate=0)
+        launch('mep_layernorm_fwd', DescArray(_lib.LnDesc, [d], dev), cdiv(ntok, 4))
+        ctx.save_for_backward(x2, w, stats)
+        ctx.shape = shape
+        return y.reshape(shape)
+
+    @staticmethod
+    @torch.autograd.function.once_differentiable
+    def backward(ctx, gy):
+        x2, w, stats = ctx.saved_tensors
+        ntok, D = x2.shape
+        dev = x2.device
+        gy = _c(gy).reshape(-1, D)
+        dx = torch.empty_like(x2)
+        tiles = cdiv(ntok, 64)
+        partial = torch.empty(tiles, 2, D, dtype=torch.float32, device=dev)
+        d = _lib.LnDesc(x=crows(x2, 1, D), y=Rows(), dy=crows(gy, 1, D), dx=crows(dx, 1, D), w=w.data_ptr(), b=0,
+                        stats=stats.data_ptr(), partial=partial.data_ptr(), ntok=ntok, D=D, dx_accumulate=0)
+        launch('mep_layernorm_bwd', DescArray(_lib.LnDesc, [d], dev), tiles)
+        gw = torch.empty(D, dtype=torch.float32, device=dev)
+        gb = torch.empty(D, dtype=torch.float32, device=dev)
+        cs = [ColsumDesc(partial=partial.data_ptr(), out=gw.data_ptr(), n_rows=tiles, n_cols=D, ld=2 * D,
+                         accumulate=0),
+              ColsumDesc(partial=partial.data_ptr() + 4 * D, out=gb.data_ptr(), n_rows=tiles, n_cols=D, ld=2 * D,
+                         accumulate=0)]
+        launch('mep_colsum', DescArray(ColsumDesc, cs, dev), cdiv(D, 32))
+        return dx.reshape(ctx.shape), gw, gb
+
+
+def layer_norm(x, norm):
+    from ._autograd import require_cuda
+    require_cuda(x)
+    assert norm.weight.shape[0] <= 256, 'mep_layernorm supports D <= 256'
+    return _LayerNormFn.apply(x, norm.weight, norm.bias)
+
+
+def unify_norm_forward(mod, l, v, a):
+    """Ren-MME Unify_Dimension.forward (Ren-MME/run.py:167-168): shared norm1 after each projection."""
+    return tuple(layer_norm(y, mod.norm1) for y in unify_forward(mod, l, v, a))

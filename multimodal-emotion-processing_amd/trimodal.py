@@ -389,8 +389,13 @@ class TriModalPlan:
     def set_inputs(self, l, v, a, lm, vm, am, labels=None):
         with torch.no_grad():
             for m, x, mk in (('l', l, lm), ('v', v, vm), ('a', a, am)):
-                self.x_in[m].copy_(x)
-                self.m_in[m].copy_(mk)
+                if isinstance(x, (tuple, list)):      # (prev, cur) pair of [B, T, d]
+                    for e in range(2):
+                        self.x_in[m][:, e].copy_(x[e])
+                        self.m_in[m][:, e].copy_(mk[e])
+                else:                                 # [B, 2, T, d]
+                    self.x_in[m].copy_(x)
+                    self.m_in[m].copy_(mk)
             if labels is not None:
                 self.labels.copy_(labels)
 

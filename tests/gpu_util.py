@@ -35,3 +35,14 @@ def cmu_model(meta, device):
 
 def cuda_batch(meta, device):
     return [t.to(device) for t in fixtures.batch(meta)]
+
+
+def ren_model(meta, device, drop=0.0):
+    """Base_model with the fixture's parameters; every nn.Dropout set to ``drop`` (the fixtures
+    were generated with DROP = 0, tests/golden/make_golden.py REN_C)."""
+    from mep_amd import ren_mme
+    m = ren_mme.Base_model(**meta['ctor'])
+    for mod in m.modules():
+        if isinstance(mod, torch.nn.Dropout):
+            mod.p = drop
+    return load_params(m, meta).to(device)

@@ -1,0 +1,125 @@
+"""GPU parity of the Ren-MME Base_model path (libmep_hip) against the reference golden vectors
+(ren_small: D=32 H=2, full gradients; ren_full: D=128 H=8 T=(40,76,96), gradient norms/heads).
+
+Tolerances as test_gpu_cmu.py: logits / loss rtol 1e-4; gradients rtol 1e-3 (floor 1e-5 x
+max|grad|); post-AdamW parameters atol 2e-5.  The loss is multi_loss + the R-Drop KL of
+Ren-MME/run.py:331-334 (the fixtures ran with DROP = 0, so the duplicated rows agree and the KL
+is evaluated, not sampled).  Dropout itself (DROP > 0) uses a device hash, not torch's RNG, so it
+is tested for its statistics and determinism instead of bit parity.
+"""
+import pytest
+import torch
+
+from tests.golden import fixtures
+from tests.gpu_util import assert_close, ren_model
+
+pytestmark = pytest.mark.gpu
+REN = [n for n in fixtures.names('model') if fixtures.load(n)[0]['family'] == 'ren']
+
+
+def _batch(meta, dev):
+    inputs, labels = fixtures.batch(meta)
+    return [t.to(dev) for t in inputs], labels.to(dev)
+
+
+def _check_grads(model, meta, gold, coef):
+    for k, p in model.named_parameters():
+        if 'nograd/' + k in gold:
+            assert p.grad is None, k
+            continue
+        g = p.grad * coef
+        if meta['full']:
+            assert_close(g, gold['grad/' + k], 1e-3, 1e-5, k)
+        else:
+            assert_close(g.reshape(-1)[:256], gold['gradhead/' + k], 1e-3, 1e-5, k)
+            assert_close(torch.linalg.vector_norm(g.double()), gold['gradnorm/' + k], 1e-3, 0, k)
+
+
+@pytest.mark.parametrize('name', REN)
+def test_base_model_autograd(name, cuda):
+    from mep_amd import ren_mme
+    meta, gold = fixtures.load(name)
+    model = ren_model(meta, cuda)
+    model.train()
+    args, labels = _batch(meta, cuda)
+    logits = model(*args)
+    assert_close(logits, gold['logits'], 1e-4, 1e-6, 'logits')
+    loss = ren_mme.multi_loss(logits, labels) + ren_mme.rdrop_kl(logits)
+    assert_close(loss.reshape(()), gold['loss'], 1e-4, 0, 'loss')
+    loss.backward()
+    _check_grads(model, meta, gold, float(gold['clipcoef']))
+
+
+@pytest.mark.parametrize('graph', [False, True])
+@pytest.mark.parametrize('name', REN)
+def test_base_model_engine_step(name, graph, cuda):
+    from mep_amd import ren_mme
+    from mep_amd.engine import TrainEngine
+    from mep_amd.optim import FusedAdamW
+    meta, gold = fixtures.load(name)
+    model = ren_model(meta, cuda)
+    model.train()
+    opt = FusedAdamW(model, lr=1e-3)
+    eng = TrainEngine(model, opt, clip=1.0, rdrop=True, graph=graph)
+    args, labels = _batch(meta, cuda)
+    l, v, a, lm, vm, am = ren_mme._pack(args)
+    losses = [float(eng.step(l, v, a, lm, vm, am, labels).item()) for _ in range(meta['steps'])]
+    assert_close(losses[0], gold['loss'], 1e-4, 0, 'loss')
+    assert_close(opt.gnorm.reshape(()), gold['gnorm'], 1e-4, 0, 'gnorm')
+    for k, p in model.named_parameters():
+        ref = gold['post/' + k] if meta['full'] else gold['posthead/' + k]
+        got = p.detach() if meta['full'] else p.detach().reshape(-1)[:256]
+        err = (got.double().cpu() - torch.as_tensor(ref).double()).abs().max().item()
+        assert err <= 2e-5, (k, err)
+    model.eval()
+    with torch.no_grad():
+        logits2 = model(*args)
+    assert_close(logits2, gold['logits2'], 1e-3, 1e-5, 'logits2')
+
+
+def test_base_model_dropout(cuda):
+    """DROP = 0.1 in train mode: duplicated rows get different masks (what R-Drop needs), the
+    same seed state reproduces, eval mode is exactly the no-dropout network."""
+    meta, gold = fixtures.load('ren_small')
+    model = ren_model(meta, cuda, drop=0.1)
+    args, labels = _batch(meta, cuda)
+    model.eval()
+    with torch.no_grad():
+        ev = model(*args)
+    assert_close(ev, gold['logits'], 1e-4, 1e-6, 'eval logits')
+    model.train()
+    with torch.no_grad():
+        t1 = model(*args)
+        t2 = model(*args)
+    assert torch.isfinite(t1).all()
+    assert (t1[0::2] - t1[1::2]).abs().max() > 1e-4, 'duplicate rows share a dropout mask'
+    assert (t1 - t2).abs().max() > 1e-4, 'dropout seed does not advance between forwards'
+    assert (t1 - ev).abs().max() > 1e-4
+
+
+def test_unify_dimension_standalone(cuda):
+    """Unify_Dimension.forward standalone (Ren-MME/run.py:167-168) vs a torch fp32 statement."""
+    from mep_amd import ren_mme
+    torch.manual_seed(0)
+    u = ren_mme.Unify_Dimension(64).to(cuda)
+    with torch.no_grad():
+        u.norm1.weight.uniform_(0.5, 1.5)
+        u.norm1.bias.uniform_(-0.2, 0.2)
+    xs = [torch.randn(3, t, d, device=cuda, requires_grad=True)
+          for t, d in ((7, ren_mme.L_DIM), (9, ren_mme.V_DIM), (70, ren_mme.A_DIM))]
+    ys = u(*xs)
+    ref_u = ren_mme.Unify_Dimension(64).to(cuda)
+    ref_u.load_state_dict(u.state_dict())
+    xr = [x.detach().clone().requires_grad_(True) for x in xs]
+    n = ref_u.norm1
+    refs = [torch.nn.functional.layer_norm(torch.nn.functional.linear(x, w), (64,), n.weight, n.bias)
+            for x, w in zip(xr, (ref_u.linguistic.weight, ref_u.visual.weight, ref_u.acoustic.weight))]
+    gs = [torch.randn_like(r) for r in refs]
+    for y, r in zip(ys, refs):
+        assert_close(y, r, 1e-4, 1e-5, 'unify out')
+    sum((y * g).sum() for y, g in zip(ys, gs)).backward()
+    sum((r * g).sum() for r, g in zip(refs, gs)).backward()
+    for x, r in zip(xs, xr):
+        assert_close(x.grad, r.grad, 1e-3, 1e-5, 'dx')
+    for (k, p), (_, q) in zip(u.named_parameters(), ref_u.named_parameters()):
+        assert_close(p.grad, q.grad, 1e-3, 1e-5, k)

@@ -1,0 +1,229 @@
+"""Host-logic check of the execution plans (CPU, no GPU): every device range any descriptor of a
+plan names -- operand rows, weights, workspaces, partials -- lies inside one buffer the plan (or
+its flat parameter store) owns.  A descriptor that points past a buffer would be a GPU memory
+fault; this catches it before any kernel runs.  Plans are built on CPU tensors (descriptor
+building only; nothing is launched)."""
+import ctypes
+
+import pytest
+import torch
+
+from mep_amd import _lib
+from mep_amd._lib import (AttnBwdDesc, AttnDesc, ColsumDesc, EpiBwdDesc, EpiDesc, GemmDesc, HeadDesc, LnDesc,
+                          PoolDesc, SumDesc, WgradDesc)
+from mep_amd.trimodal import cdiv
+
+F = 4
+
+
+def _tensors(obj, out, depth=0):
+    if torch.is_tensor(obj):
+        out.append(obj)
+    elif isinstance(obj, dict):
+        for v in obj.values():
+            _tensors(v, out, depth + 1)
+    elif isinstance(obj, (list, tuple)):
+        for v in obj:
+            _tensors(v, out, depth + 1)
+    elif depth < 2 and hasattr(obj, '__dict__') and not isinstance(obj, type):
+        for v in vars(obj).values():
+            _tensors(v, out, depth + 1)
+    return out
+
+
+class Checker:
+    def __init__(self, plan):
+        ts = _tensors(plan, [])
+        fl = plan.flat
+        ts += [fl.buf, fl.grad]
+        self.allocs = sorted({(t.data_ptr(), t.untyped_storage().nbytes()) for t in ts if t.numel()})
+        self.n = 0
+
+    def inside(self, label, ptr, nbytes):
+        if ptr == 0 or nbytes <= 0:
+            return
+        self.n += 1
+        for base, size in self.allocs:
+            if base <= ptr and ptr + nbytes <= base + size:
+                return
+        raise AssertionError('%s: [%#x, +%d) is outside every plan buffer' % (label, ptr, nbytes))
+
+    def rows(self, label, r, ntok, cols):
+        if r.ptr == 0 or ntok == 0:
+            return
+        assert r.T > 0, label
+        last = (ntok - 1) // r.T * r.sB + (ntok - 1) % r.T * r.sT
+        self.inside(label, r.ptr, (last + cols) * F)
+
+
+def _decode(arr):
+    if arr is None or arr.n == 0:
+        return []
+    raw = bytes(arr.dev.cpu().numpy().tobytes())
+    sz = ctypes.sizeof(arr.struct)
+    return [arr.struct.from_buffer_copy(raw[i * sz:(i + 1) * sz]) for i in range(arr.n)]
+
+
+def _gemm(c, d):
+    c.rows('gemm.x', d.x, d.ntok, d.K)
+    c.rows('gemm.y', d.y, d.ntok, d.N)
+    c.inside('gemm.w', d.w, ((d.N - 1) * d.ldw + d.K if d.w_nt else (d.K - 1) * d.ldw + d.N) * F)
+    c.inside('gemm.bias', d.bias, d.N * F)
+    c.inside('gemm.table', d.table, d.y.T * d.N * F)
+
+
+def _wgrad(c, d):
+    c.rows('wgrad.a', d.a, d.ntok, d.N)
+    for i in range(d.n_b):
+        c.rows('wgrad.b%d' % i, d.b[i], d.ntok, d.kb[i])
+        c.inside('wgrad.out%d' % i, d.out[i], ((d.N - 1) * d.ldo[i] + d.kb[i]) * F)
+    assert sum(d.kb[i] for i in range(d.n_b)) == d.Ktot
+    assert d.n_split == cdiv(d.ntok, d.tok_per_split)
+    c.inside('wgrad.partial', d.partial, d.n_split * d.N * d.Ktot * F)
+
+
+def _attn(c, d, tag='attn'):
+    D = 16 * d.H
+    c.rows(tag + '.q', d.q, d.B * d.Tq, D)
+    c.rows(tag + '.k', d.k, d.B * d.Tk, D)
+    c.rows(tag + '.v', d.v, d.B * d.Tk, D)
+    c.rows(tag + '.x', d.x, d.B * d.Tq, D)
+    c.inside(tag + '.mask', d.mask, ((d.B - 1) * d.mask_sB + d.Tk) * F)
+    S = d.B * d.H * d.Tq * d.Tk * F
+    c.inside(tag + '.s_prev', d.s_prev, S)
+    c.inside(tag + '.s_out', d.s_out, S)
+    c.inside(tag + '.c', d.c, F)
+    c.inside(tag + '.stats', d.stats, d.B * d.H * d.Tq * 2 * F)
+
+
+def _attn_bwd(c, d):
+    f = d.f
+    _attn(c, f, 'attn_bwd')
+    D = 16 * f.H
+    for name in ('dx', 'dq'):
+        c.rows('attn_bwd.' + name, getattr(d, name), f.B * f.Tq, D)
+    for name in ('dk', 'dv'):
+        c.rows('attn_bwd.' + name, getattr(d, name), f.B * f.Tk, D)
+    S = f.B * f.H * f.Tq * f.Tk * F
+    c.inside('attn_bwd.ds_next', d.ds_next, S)
+    c.inside('attn_bwd.ds_prev', d.ds_prev, S)
+    c.inside('attn_bwd.dc_partial', d.dc_partial, _lib.attn_dc_slots(f.B, f.H, f.Tk) * F)
+
+
+def _epi(c, d, tag='epi'):
+    for name in ('q', 'x', 'xp', 'z', 'out'):
+        c.rows(tag + '.' + name, getattr(d, name), d.ntok, d.D)
+    c.inside(tag + '.wp', d.wp, d.D * d.D * F)
+    c.inside(tag + '.wm', d.wm, 2 * d.D * d.D * F)
+    c.inside(tag + '.ln_w', d.ln_w, d.D * F)
+    c.inside(tag + '.ln_b', d.ln_b, d.D * F)
+    c.inside(tag + '.stats', d.stats, d.ntok * 2 * F)
+    c.inside(tag + '.seed', d.seed, 8)
+
+
+def _epi_bwd(c, d):
+    f = d.f
+    _epi(c, f, 'epi_bwd')
+    for name in ('dout', 'dout2', 'dz', 'dxp', 'dx', 'dq'):
+        c.rows('epi_bwd.' + name, getattr(d, name), f.ntok, f.D)
+    c.inside('epi_bwd.ln_partial', d.ln_partial, cdiv(f.ntok, 64) * 2 * f.D * F)
+
+
+def _ln(c, d):
+    for name in ('x', 'y', 'dy', 'dx'):
+        c.rows('ln.' + name, getattr(d, name), d.ntok, d.D)
+    c.inside('ln.w', d.w, d.D * F)
+    c.inside('ln.b', d.b, d.D * F)
+    c.inside('ln.stats', d.stats, d.ntok * 2 * F)
+    c.inside('ln.partial', d.partial, cdiv(d.ntok, 64) * 2 * d.D * F)
+
+
+def _colsum(c, d):
+    c.inside('colsum.partial', d.partial, ((d.n_rows - 1) * d.ld + d.n_cols) * F)
+    c.inside('colsum.out', d.out, d.n_cols * F)
+
+
+def _sum(c, d):
+    assert d.n_src <= _lib.SUM_MAX_SRC
+    for i in range(d.n_src):
+        c.rows('sum.src%d' % i, d.src[i], d.ntok, d.D)
+    c.rows('sum.out', d.out, d.ntok, d.D)
+
+
+def _pool(c, d):
+    for name in ('x', 'dx'):
+        c.inside('pool.' + name, getattr(d, name), d.B * d.T * d.C * F)
+    for name in ('pooled', 'dpooled'):
+        c.inside('pool.' + name, getattr(d, name), d.B * 2 * d.C * F)
+    c.inside('pool.argmax', d.argmax, d.B * d.C * 4)
+
+
+def _head(c, d, stride, grads):
+    B, Fd, NC = d.B, d.F, d.NC
+    for name in ('pooled0', 'pooled1', 'dpooled0', 'dpooled1'):
+        c.inside('head.' + name, getattr(d, name), B * Fd * F)
+    c.inside('head.wc0', d.wc0, NC * Fd * F)
+    c.inside('head.wc1', d.wc1, NC * Fd * F)
+    c.inside('head.trans', d.trans, NC ** 3 * F)
+    c.inside('head.ln_w', d.ln_w, NC * F)
+    c.inside('head.ln_b', d.ln_b, NC * F)
+    c.inside('head.wo', d.wo, NC * 2 * NC * F)
+    c.inside('head.bo', d.bo, NC * F)
+    c.inside('head.labels', d.labels, B * NC * (4 if d.labels_are_float else 8))
+    c.inside('head.logits', d.logits, B * NC * F)
+    c.inside('head.row_loss', d.row_loss, B * F)
+    c.inside('head.partial', d.partial, B * stride * F)
+    sizes = [NC ** 3, NC, NC, 2 * NC * NC, NC, NC * Fd, NC * Fd, 1]   # mep_head_reduce order
+    for i, (gp, n) in enumerate(zip(grads, sizes)):
+        c.inside('head_grad%d' % i, int(gp.value if hasattr(gp, 'value') else gp), n * F)
+
+
+def check_plan(p):
+    c = Checker(p)
+    for d in _decode(p.d_unify):
+        _gemm(c, d)
+    for d in _decode(p.d_wgrad):
+        _wgrad(c, d)
+    for arrs, fn in ((p.d_attn, _attn), (p.d_attnb, _attn_bwd), (p.d_epi, _epi), (p.d_epib, _epi_bwd)):
+        for arr in arrs:
+            for d in _decode(arr):
+                fn(c, d)
+    for name in ('d_uln', 'd_ulnb'):
+        for d in _decode(getattr(p, name, None)):
+            _ln(c, d)
+    for name in ('d_colsum', 'd_losssum'):
+        for d in _decode(getattr(p, name)):
+            _colsum(c, d)
+    for d in _decode(p.d_sum):
+        _sum(c, d)
+    for d in _decode(p.d_pool):
+        _pool(c, d)
+    _head(c, p.head, p.head_stride, p.head_grads)
+    return c.n
+
+
+CASES = [
+    ('cmu', dict(dim=32, n_heads=2, n_layers=1), 5, (7, 9, 12)),
+    ('cmu', dict(dim=32, n_heads=2, n_layers=2), 4, (6, 10, 8)),
+    ('cmu', dict(dim=96, n_heads=6, n_layers=1), 3, (50, 50, 50)),
+    ('cmu', dict(dim=64, n_heads=4, n_layers=3), 2, (1, 65, 130)),
+    ('ren', dict(dim=32, n_heads=2, n_layers=1), 6, (5, 6, 8)),
+    ('ren', dict(dim=128, n_heads=8, n_layers=1), 2, (40, 76, 275)),
+    ('ren', dict(dim=64, n_heads=4, n_layers=2), 4, (3, 70, 9)),
+]
+
+
+@pytest.mark.parametrize('family,kw,B,T', CASES)
+def test_plan_descriptors_in_bounds(family, kw, B, T):
+    from mep_amd import cmu_mosei, ren_mme
+    Tl, Tv, Ta = T
+    if family == 'cmu':
+        m = cmu_mosei.Concat_Trans(kw['dim'], Tl, Tv, Ta, kw['n_heads'], kw['n_layers'], 1)
+    else:
+        m = ren_mme.Base_model(dim=kw['dim'], l_len=Tl, v_len=Tv, a_len=Ta, n_heads=kw['n_heads'],
+                               n_layers=kw['n_layers'])
+    runner = m.mep_runner('cpu')
+    plan = runner.plan(B, T)
+    n = check_plan(plan)
+    assert n > 50
+    assert len(plan.blocks) == 18 * kw['n_layers']

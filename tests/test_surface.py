@@ -1,0 +1,64 @@
+"""CPU checks of the drop-in Python surface: class names, constructor defaults, state_dict keys
+and shapes identical to the reference (the golden fixtures record the reference model's
+state_dict shapes), parameter counts, and that CPU tensors are refused (no CPU fallback)."""
+import pytest
+import torch
+
+from tests.golden import fixtures
+
+
+def _model(meta):
+    from mep_amd import cmu_mosei, ren_mme
+    if meta['family'] == 'cmu':
+        return cmu_mosei.Concat_Trans(**meta['ctor'])
+    return ren_mme.Base_model(**meta['ctor'])
+
+
+@pytest.mark.parametrize('name', [n for n in fixtures.names('model')
+                                  if fixtures.load(n)[0]['family'] in ('cmu', 'ren')])
+def test_state_dict_matches_reference(name):
+    meta, _ = fixtures.load(name)
+    sd = _model(meta).state_dict()
+    assert list(sd.keys()) == list(meta['shapes'].keys())
+    for k, v in sd.items():
+        assert list(v.shape) == meta['shapes'][k], k
+
+
+def test_reference_configs_parameter_count():
+    from mep_amd import cmu_mosei, ren_mme
+    m = cmu_mosei.Concat_Trans(cmu_mosei.DIM, cmu_mosei.L_LEN, cmu_mosei.V_LEN, cmu_mosei.A_LEN,
+                               cmu_mosei.N_HEADS, cmu_mosei.N_LAYERS, cmu_mosei.FFN)
+    assert cmu_mosei.get_parameter_number(m) == {'Total': 588192, 'Trainable': 588192}
+    r = ren_mme.Base_model()
+    n = ren_mme.get_parameter_number(r)['Total']
+    D = ren_mme.DIM
+    per_encoder = (768 + 640 + 205) * D + 2 * D + 9 * (D * D + 2 * D * D + 2 * D + 1) + 6 * D * 9
+    assert n == 2 * per_encoder + 9 ** 3 + 2 * 9 + 18 * 9 + 9
+
+
+def test_cpu_tensors_are_refused():
+    from mep_amd import cmu_mosei, ren_mme
+    m = cmu_mosei.Concat_Trans(32, 5, 5, 5, 2, 1, 1)
+    x = [torch.zeros(2, 2, 5, d) for d in (300, 35, 74)]
+    masks = [torch.ones(2, 2, 5)] * 3
+    with pytest.raises(RuntimeError, match='no CPU fallback'):
+        m(*x, *masks)
+    with pytest.raises(RuntimeError, match='no CPU fallback'):
+        cmu_mosei.multi_circle_loss(torch.zeros(2, 7), torch.zeros(2, 7, dtype=torch.int64))
+    r = ren_mme.Base_model(dim=32, n_heads=2)
+    args = []
+    for d in (768, 640, 205):
+        for _ in range(2):
+            args += [torch.zeros(2, 4, d), torch.ones(2, 4)]
+    with pytest.raises(RuntimeError, match='no CPU fallback'):
+        r(*args)
+    with pytest.raises(RuntimeError, match='no CPU fallback'):
+        ren_mme.Unify_Dimension(32)(torch.zeros(1, 2, 768), torch.zeros(1, 2, 640), torch.zeros(1, 2, 205))
+
+
+def test_ren_pack_order():
+    """Base_model's 12 arguments map to (prev, cur) pairs per modality (Ren-MME/run.py:281-285)."""
+    from mep_amd import ren_mme
+    args = list(range(12))
+    l, v, a, lm, vm, am = ren_mme._pack(args)
+    assert (l, lm, v, vm, a, am) == ((0, 2), (1, 3), (4, 6), (5, 7), (8, 10), (9, 11))
