@@ -83,7 +83,10 @@ typedef struct {
     int32_t  ldo[MEP_WG_MAX_B];
     uint64_t partial;            /* workspace [n_split][N][Ktot]              */
     int32_t  n_b, ntok, N, Ktot;
-    int32_t  tok_per_split, n_split, accumulate, _pad;
+    int32_t  tok_per_split, n_split, accumulate;
+    int32_t  out_trans;          /* 1: write dW_i transposed, out_i[k * ldo_i + n] (for weights
+                                    whose output dim exceeds 128, e.g. realformer ffn.0 /
+                                    [w_qkv.1; w_qkv.2])                                         */
 } mep_wgrad_desc;
 int mep_wgrad(const mep_wgrad_desc* descs, int n_desc, int max_tiles, mep_stream_t stream);
 int mep_wgrad_reduce(const mep_wgrad_desc* descs, int n_desc, int max_tiles, mep_stream_t stream);
@@ -106,9 +109,9 @@ typedef struct {
     uint64_t stats;     /* [B,H,Tq,2]: row max, 1/row sum                       */
     int32_t  B, H, Tq, Tk;
 } mep_attn_desc;
-/* Launch geometry (the host knows every shape): R = 512 / H rows per workgroup, one lane per
- * (row, head); threads = 64 * ceil(H * min(T, R) / 64) maximised over descriptors (T = Tq, and
- * also Tk for the backward); max_tiles = max B * ceil(Tq / R) (+ B * ceil(Tk / R) backward). */
+/* Launch geometry: one wave per (b, h, 64-query chunk) in the forward and per (b, h, 64-key
+ * chunk) in the backward, 4 waves (256 threads) per workgroup; max_tiles =
+ * max ceil(B * H * ceil(T / 64) / 4) over descriptors (T = Tq forward, Tk backward). */
 int mep_attn_fwd(const mep_attn_desc* descs, int n_desc, int max_tiles, int threads, mep_stream_t stream);
 
 /* Backward of the attention core.  Inputs dx (grad of X), the forward's q/k/v/x/stats/s_prev.
@@ -157,6 +160,67 @@ typedef struct {
     int32_t  _pad;
 } mep_epi_bwd_desc;
 int mep_block_epi_bwd(const mep_epi_bwd_desc* descs, int n_desc, int max_tiles, int D, mep_stream_t stream);
+
+/* ---------------------------------------------------------------- realformer block epilogue
+ * others/realformer.py:182-209 after the attention core (x = attention output, q = block input):
+ *   xp = x Wp^T;  h = LN1(q + a*xp);  f1 = relu(h W1^T + b1);  f = f1 W2^T + b2;
+ *   out = LN2(h + b*f)
+ * a, b: the block's ReZero scalars (device float*).  One workgroup = 64 tokens; the three
+ * Linears run on f32 MFMA through LDS.  D in {32, 64, 96, 128}, FD = FFN * D with FFN in {1, 2}.
+ * Saves xp, h, f1, f and (mean1, rstd1, mean2, rstd2) per token for the backward. */
+typedef struct {
+    mep_rows q, x;       /* inputs [ntok, D]                        */
+    mep_rows xp, h, f1, f, out;  /* outputs; f1 is [ntok, FD]        */
+    uint64_t wp, w1, b1, w2, b2;
+    uint64_t ln1_w, ln1_b, ln2_w, ln2_b;
+    uint64_t a, b;       /* device float* scalars                   */
+    uint64_t stats;      /* [ntok][4]                               */
+    int32_t  ntok, D, FD, _pad;
+} mep_rf_epi_desc;
+int mep_rf_epi_fwd(const mep_rf_epi_desc* descs, int n_desc, int max_tiles, int D, int FD, mep_stream_t stream);
+
+/* Backward: dout (+dout2) -> LN2' -> dz2;  df = b dz2;  df1 = relu'(f1) (df W2);
+ * dh = dz2 + df1 W1 -> LN1' -> dz1;  dq (+)= dz1 (residual);  dxp = a dz1;  dx = dxp Wp.
+ * Writes df, df1, dxp (the wgrad operands), dx (the attention core's dO), dq, and per-tile
+ * partial sums partial[tile][5D + FD + 2] = [dLN2.w | dLN2.b | dLN1.w | dLN1.b | db2 | db1 | da | db]. */
+typedef struct {
+    mep_rf_epi_desc f;
+    mep_rows dout, dout2;  /* dout2 optional (ptr 0)                 */
+    mep_rows df, df1, dxp, dx, dq;
+    uint64_t partial;
+    int32_t  dq_accumulate, _pad;
+} mep_rf_epi_bwd_desc;
+int mep_rf_epi_bwd(const mep_rf_epi_bwd_desc* descs, int n_desc, int max_tiles, int D, int FD, mep_stream_t stream);
+#define MEP_RF_PARTIAL_STRIDE(D, FD) (5 * (D) + (FD) + 2)
+
+/* ---------------------------------------------------------------- State_Transfer head
+ * others/realformer.py:257-286 after the fully_connected Linear (run by mep_gemm):
+ * per batch row b and utterance i < P (rows r = b*P + i):
+ *   h = relu(LN(fc[r]));  [o | g] = h Wc^T + bc  (classifier D -> 12, chunk(2));
+ *   i > 0: alpha = sigmoid(g + g_prev);  o = (1 - alpha) o + alpha tanh(out_prev @ trans)
+ * plus multi_circle_loss(out, labels) * umask, mean over B*P (realformer.py:311-312).
+ * compute_grad: also the backward through the whole recurrence, writing d12 [R,12] (grad at the
+ * classifier output), dfc [R,D] (grad at the fc output) and partial[b][2D + 36] =
+ * [dLN.w | dLN.b | dtrans].  ext_dout != 0: upstream grad [B,P,6] instead of the fused loss.
+ * One wave per batch row; P <= 16, D <= 128. */
+typedef struct {
+    uint64_t fc;         /* [R, D]                                 */
+    uint64_t ln_w, ln_b; /* normalization                          */
+    uint64_t wc, bc;     /* classifier [12, D], [12]               */
+    uint64_t trans;      /* [6, 6]                                 */
+    uint64_t labels;     /* int64 [B, P, 6]                        */
+    uint64_t umask;      /* int64 [B, P]                           */
+    uint64_t out;        /* out [B, P, 6]                          */
+    uint64_t h;          /* out [R, D]                             */
+    uint64_t d12, dfc;   /* out [R, 12], [R, D]                    */
+    uint64_t row_loss;   /* out [B] (already scaled)               */
+    uint64_t partial;    /* out [B][2D + 36]                       */
+    uint64_t ext_dout;   /* [B, P, 6] or 0                         */
+    int32_t  B, P, D, compute_grad;
+    float    loss_scale;
+    int32_t  _pad;
+} mep_rf_head_desc;
+int mep_rf_head(const mep_rf_head_desc* d, mep_stream_t stream);
 
 /* ---------------------------------------------------------------- row LayerNorm (D <= 256)
  * Ren-MME's shared unify LayerNorm (Ren-MME/run.py:164-166).  fwd: y = LN(x); bwd: dx from dy,

@@ -32,7 +32,7 @@ WG_MAX_B = 4
 class WgradDesc(ctypes.Structure):
     _fields_ = [('a', Rows), ('b', Rows * WG_MAX_B), ('out', u64 * WG_MAX_B), ('kb', i32 * WG_MAX_B),
                 ('ldo', i32 * WG_MAX_B), ('partial', u64), ('n_b', i32), ('ntok', i32), ('N', i32), ('Ktot', i32),
-                ('tok_per_split', i32), ('n_split', i32), ('accumulate', i32), ('_pad', i32)]
+                ('tok_per_split', i32), ('n_split', i32), ('accumulate', i32), ('out_trans', i32)]
 
 
 class AttnDesc(ctypes.Structure):
@@ -89,6 +89,30 @@ class HeadDesc(ctypes.Structure):
                 ('compute_grad', i32), ('loss_scale', f32), ('_pad', i32), ('ext_dlogits', u64)]
 
 
+class RfEpiDesc(ctypes.Structure):
+    _fields_ = [('q', Rows), ('x', Rows), ('xp', Rows), ('h', Rows), ('f1', Rows), ('f', Rows), ('out', Rows),
+                ('wp', u64), ('w1', u64), ('b1', u64), ('w2', u64), ('b2', u64),
+                ('ln1_w', u64), ('ln1_b', u64), ('ln2_w', u64), ('ln2_b', u64), ('a', u64), ('b', u64),
+                ('stats', u64), ('ntok', i32), ('D', i32), ('FD', i32), ('_pad', i32)]
+
+
+class RfEpiBwdDesc(ctypes.Structure):
+    _fields_ = [('f', RfEpiDesc), ('dout', Rows), ('dout2', Rows), ('df', Rows), ('df1', Rows), ('dxp', Rows),
+                ('dx', Rows), ('dq', Rows), ('partial', u64), ('dq_accumulate', i32), ('_pad', i32)]
+
+
+def rf_partial_stride(D, FD):
+    """MEP_RF_PARTIAL_STRIDE: floats per tile of mep_rf_epi_bwd's partial sums"""
+    return 5 * D + FD + 2
+
+
+class RfHeadDesc(ctypes.Structure):
+    _fields_ = [('fc', u64), ('ln_w', u64), ('ln_b', u64), ('wc', u64), ('bc', u64), ('trans', u64),
+                ('labels', u64), ('umask', u64), ('out', u64), ('h', u64), ('d12', u64), ('dfc', u64),
+                ('row_loss', u64), ('partial', u64), ('ext_dout', u64),
+                ('B', i32), ('P', i32), ('D', i32), ('compute_grad', i32), ('loss_scale', f32), ('_pad', i32)]
+
+
 class Seg(ctypes.Structure):
     _fields_ = [('offset', i64), ('length', i64)]
 
@@ -96,7 +120,8 @@ class Seg(ctypes.Structure):
 STRUCTS = {'mep_rows': Rows, 'mep_gemm_desc': GemmDesc, 'mep_wgrad_desc': WgradDesc,
            'mep_attn_desc': AttnDesc, 'mep_attn_bwd_desc': AttnBwdDesc, 'mep_epi_desc': EpiDesc,
            'mep_epi_bwd_desc': EpiBwdDesc, 'mep_ln_desc': LnDesc, 'mep_colsum_desc': ColsumDesc,
-           'mep_sum_desc': SumDesc, 'mep_pool_desc': PoolDesc, 'mep_head_desc': HeadDesc, 'mep_seg': Seg}
+           'mep_sum_desc': SumDesc, 'mep_pool_desc': PoolDesc, 'mep_head_desc': HeadDesc, 'mep_seg': Seg,
+           'mep_rf_epi_desc': RfEpiDesc, 'mep_rf_epi_bwd_desc': RfEpiBwdDesc, 'mep_rf_head_desc': RfHeadDesc}
 
 P = ctypes.c_void_p
 # name -> argtypes (all return int)
@@ -106,6 +131,8 @@ GROUPED_T = ['mep_attn_fwd', 'mep_attn_bwd',      # + threads per workgroup
              'mep_block_epi_fwd', 'mep_block_epi_bwd']  # + D (compiled variant)
 SIGNATURES = {name: [P, i32, i32, P] for name in GROUPED}
 SIGNATURES.update({name: [P, i32, i32, i32, P] for name in GROUPED_T})
+GROUPED_T2 = ['mep_rf_epi_fwd', 'mep_rf_epi_bwd']   # + D, FD (compiled variant)
+SIGNATURES.update({name: [P, i32, i32, i32, i32, P] for name in GROUPED_T2})
 HP = ctypes.POINTER(HeadDesc)
 SIGNATURES.update({
     'mep_head_fwd_bwd': [HP, P],
@@ -115,6 +142,7 @@ SIGNATURES.update({
     'mep_circle_loss_bwd': [P, P, i32, i32, P, P],
     'mep_clip_adam': [P, P, P, P, P, i32, i64, P, P, P, P, i32, P],
     'mep_seed_advance': [P, P],
+    'mep_rf_head': [ctypes.POINTER(RfHeadDesc), P],
     'mep_abi_version': [],
     'mep_last_error': [ctypes.c_char_p, ctypes.c_size_t],
     'mep_device_sync': [],
@@ -187,17 +215,16 @@ class DescArray:
         return ctypes.c_void_p(self.dev.data_ptr() if self.dev is not None else 0)
 
 
-def launch(name, descs, max_tiles, stream=None, threads=None):
-    """threads: the extra int argument of the GROUPED_T launchers (threads or D)."""
+def launch(name, descs, max_tiles, stream=None, threads=None, extra=()):
+    """threads: the extra int argument of the GROUPED_T launchers (threads or D); extra: the
+    extra ints of the GROUPED_T2 launchers (D, FD)."""
     if descs.n == 0 or max_tiles <= 0:
         return
     fn = getattr(lib(), name)
     if TIMER is not None:
         TIMER.begin(name)
-    if threads is None:
-        rc = fn(descs.ptr, descs.n, int(max_tiles), stream_ptr(stream))
-    else:
-        rc = fn(descs.ptr, descs.n, int(max_tiles), int(threads), stream_ptr(stream))
+    ints = ([] if threads is None else [int(threads)]) + [int(x) for x in extra]
+    rc = fn(descs.ptr, descs.n, int(max_tiles), *ints, stream_ptr(stream))
     check(rc, name)
     if TIMER is not None:
         TIMER.end(name)

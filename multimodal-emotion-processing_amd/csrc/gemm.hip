@@ -173,7 +173,7 @@ __global__ __launch_bounds__(256) void k_wgrad_reduce(const mep_wgrad_desc* __re
     int k = (int)(i - (int64_t)n * d.Ktot);
     int j = 0;
     while (j < d.n_b - 1 && k >= d.kb[j]) { k -= d.kb[j]; ++j; }
-    gfloat* o = G<float>(d.out[j]) + (int64_t)n * d.ldo[j] + k;
+    gfloat* o = G<float>(d.out[j]) + (d.out_trans ? (int64_t)k * d.ldo[j] + n : (int64_t)n * d.ldo[j] + k);
     *o = d.accumulate ? *o + s : s;
 }
 

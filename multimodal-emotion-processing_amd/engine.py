@@ -88,10 +88,10 @@ class TrainEngine:
         if self.world > 1:
             dist.all_reduce(runner.flat.grad, op=dist.ReduceOp.SUM, group=self.pg)
 
-    def step(self, l, v, a, lm, vm, am, labels):
-        """Reference-shaped batch in, loss out (copies the batch into the plan's resident
-        buffers first)."""
-        runner = self._runner((l[0] if isinstance(l, (tuple, list)) else l).device)
-        plan = runner.plan_for(l, v, a)
-        plan.set_inputs(l, v, a, lm, vm, am, labels)
+    def step(self, *batch):
+        """Reference-shaped batch in, loss out: the runner copies the batch into the resident
+        buffers of the plan for its shape (cmu-mosei / Ren-MME: l, v, a, l_mask, v_mask, a_mask,
+        labels; realformer: ... , labels, utterance mask)."""
+        first = batch[0][0] if isinstance(batch[0], (tuple, list)) else batch[0]
+        plan = self._runner(first.device).stage(*batch)
         return self.step_plan(plan)

@@ -1,0 +1,516 @@
+"""Execution plan of the others/realformer.py family on libmep_hip: ``Multi_class`` encoders under
+the ``State_Transfer`` head, and the single-chain "text encoder" of BASELINE cfg2.
+
+The P utterances of a State_Transfer batch share the encoder weights and are independent until
+the gate recurrence (realformer.py:272-286), so the plan encodes all R = B*P utterances as ONE
+batch (one grouped launch per stage instead of P Python iterations), and only the tiny
+sigmoid/tanh recurrence runs per batch row (mep_rf_head).
+
+Step anatomy
+  forward   unify GEMM (+ position-embedding table) -> [w_qkv.1; w_qkv.2] KV projections of every
+            block and the layer-0 Q projections (one grouped GEMM) -> per layer: Q projections
+            (layers > 0), attention core (K != V), RealFormer epilogue (proj, a-residual LN1,
+            FFN, b-residual LN2) -> mean+max pool -> fully_connected GEMM -> fused head
+            (LN, ReLU, classifier, gate recurrence, circle loss, and its backward)
+  backward  dpooled GEMM, pool backward, per layer (reverse): epilogue backward, attention
+            backward, dQ / dKV input-gradient GEMMs; per-modality gradient sums; every weight
+            gradient in one split-K launch; column sums for biases, LayerNorms, a/b/c, position
+            tables and the head.
+HBM layout: K and V projections of a block share one [ntok, 2D] buffer (one GEMM against the
+adjacent [w_qkv.1; w_qkv.2] weights, one [ntok, 2D] gradient); last-layer outputs are written
+straight into the pooled tensor [R, T_l+T_a+T_v, 3D] (torch.cat at realformer.py:258-261).
+"""
+import ctypes
+
+import torch
+
+from . import _lib
+from ._lib import (AttnBwdDesc, AttnDesc, ColsumDesc, DescArray, GemmDesc, PoolDesc, RfEpiBwdDesc, RfEpiDesc,
+                   RfHeadDesc, Rows, SumDesc, launch)
+from .trimodal import CHAINS, MODS, TIME_ORDER, UNIFY_NAMES, cdiv, crows, make_wgrad, rows
+
+NC = 6  # State_Transfer classes (realformer.py:268-269)
+POS_NAMES = {'l': 'linguistic_position', 'v': 'visual_position', 'a': 'acoustic_position'}
+
+
+class RealformerSpec:
+    """Static description of a Multi_class encoder (+ optional State_Transfer head).
+
+    prefix: state_dict prefix of the Multi_class ('feature.' under State_Transfer).
+    chains: the (query, key) modality chains to run (all 9 for Multi_class; [('l', 'l')] for the
+    cfg2 text chain, whose output is the last block's output instead of the pooled head)."""
+
+    def __init__(self, D, H, n_layers, FD, dims, T, prefix='feature.', chains=CHAINS, head=True):
+        assert D == 16 * H and D % 32 == 0 and D <= 128, 'kernels need hd = 16 and D in {32,64,96,128}'
+        assert FD in (D, 2 * D), 'mep_rf_epi is compiled for FFN in {1, 2}'
+        self.D, self.H, self.nl, self.FD = D, H, n_layers, FD
+        self.dims = dict(zip(MODS, dims))
+        self.Tlen = dict(zip(MODS, T))
+        self.prefix = prefix
+        self.chains = tuple(chains)
+        self.head = head
+        self.mods = tuple(m for m in MODS if any(m in c for c in self.chains))
+        assert not head or len(self.chains) == 9
+
+    def block_name(self, j, i):
+        """chain j, layer i -> multimodal_blocks index (realformer.py:232-256)"""
+        return self.prefix + 'multimodal_blocks.%d.' % (self.nl * CHAINS.index(self.chains[j]) + i)
+
+    def no_grad_params(self, all_names):
+        """Parameters that never receive a gradient: c of every chain's first layer (its scores
+        input is None, realformer.py:187-190) and everything outside the chains / head run."""
+        used = set()
+        for m in self.mods:
+            used.add(self.prefix + 'unify_dimension.%s.weight' % UNIFY_NAMES[m])
+            used.add(self.prefix + '%s.position_embeddings.weight' % POS_NAMES[m])
+        blocks = [self.block_name(j, i) for j in range(len(self.chains)) for i in range(self.nl)]
+        heads = [self.prefix + 'fully_connected.', self.prefix + 'normalization.', 'classifier.', 'trans']
+        out = []
+        for n in all_names:
+            if n in used:
+                continue
+            blk = [b for b in blocks if n.startswith(b)]
+            if blk:
+                first = int(blk[0].split('.')[-2]) % self.nl == 0
+                if n == blk[0] + 'c' and first:
+                    out.append(n)
+                continue
+            if self.head and any(n.startswith(h) for h in heads):
+                continue
+            out.append(n)
+        return out
+
+
+class RealformerPlan:
+    def __init__(self, spec, flat, B, P, device):
+        self.spec, self.flat = spec, flat
+        self.B, self.P = B, P
+        self.R = R = B * P
+        self.device = dev = torch.device(device)
+        sp = spec
+        D, H, nl, FD = sp.D, sp.H, sp.nl, sp.FD
+        f32 = dict(dtype=torch.float32, device=dev)
+        self.T = {m: sp.Tlen[m] for m in sp.mods}
+        self.ntok = {m: R * self.T[m] for m in sp.mods}
+        # ---------------- static inputs ([R, T, d] = the reference's [B, P, T, d])
+        self.x_in = {m: torch.zeros(R, self.T[m], sp.dims[m], **f32) for m in sp.mods}
+        self.m_in = {m: torch.zeros(R, self.T[m], **f32) for m in sp.mods}
+        self.U = {m: torch.zeros(self.ntok[m], D, **f32) for m in sp.mods}
+        self.dU = {m: torch.zeros(self.ntok[m], D, **f32) for m in sp.mods}
+        self.loss = torch.zeros(1, **f32)
+        if sp.head:
+            self.labels = torch.zeros(B, P, NC, dtype=torch.int64, device=dev)
+            self.umask = torch.zeros(B, P, dtype=torch.int64, device=dev)
+            self.Ttot = sum(self.T.values())
+            self.C = 3 * D
+            self.Xcat = torch.zeros(R, self.Ttot, self.C, **f32)
+            self.dXcat = torch.zeros_like(self.Xcat)
+            self.pooled = torch.zeros(R, 2 * self.C, **f32)
+            self.dpooled = torch.zeros_like(self.pooled)
+            self.argmax = torch.zeros(R, self.C, dtype=torch.int32, device=dev)
+            self.fc = torch.zeros(R, D, **f32)
+            self.h = torch.zeros(R, D, **f32)
+            self.dfc = torch.zeros(R, D, **f32)
+            self.d12 = torch.zeros(R, 2 * NC, **f32)
+            self.out = torch.zeros(B, P, NC, **f32)
+            self.row_loss = torch.zeros(B, **f32)
+            self.head_partial = torch.zeros(B, 2 * D + NC * NC, **f32)
+            self.toff, t = {}, 0
+            for m in TIME_ORDER:
+                self.toff[m] = t
+                t += self.T[m]
+        self.blocks = []
+        for j, (qm, km) in enumerate(sp.chains):
+            for i in range(nl):
+                self.blocks.append(self._make_block(j, i, qm, km))
+        nq_all = sum(b['nq'] for b in self.blocks)
+        self.dQP_all = torch.zeros(nq_all, D, **f32)   # attention dq accumulates: zeroed per step
+        off = 0
+        for b in self.blocks:
+            b['dQP'] = self.dQP_all[off:off + b['nq']]
+            off += b['nq']
+        if not sp.head:
+            last = self._blk(0, nl - 1)
+            self.out_chain = last['OUT']
+            self.dout_chain = torch.zeros_like(last['OUT'])
+        self._build()
+
+    # ------------------------------------------------------------------ buffers
+    def _make_block(self, j, i, qm, km):
+        sp, R = self.spec, self.R
+        D, H, FD, nl = sp.D, sp.H, sp.FD, sp.nl
+        f32 = dict(dtype=torch.float32, device=self.device)
+        Tq, Tk = self.T[qm], self.T[km]
+        nq, nk = R * Tq, R * Tk
+        blk = dict(idx=len(self.blocks), j=j, i=i, qm=qm, km=km, Tq=Tq, Tk=Tk, nq=nq, nk=nk,
+                   pre=sp.block_name(j, i))
+        for name in ('QP', 'X', 'XP', 'H', 'F', 'dXP', 'dX', 'dF', 'dQin'):
+            blk[name] = torch.zeros(nq, D, **f32)
+        blk['F1'] = torch.zeros(nq, FD, **f32)
+        blk['dF1'] = torch.zeros(nq, FD, **f32)
+        blk['KV'] = torch.zeros(nk, 2 * D, **f32)
+        blk['dKV2'] = torch.zeros(nk, 2 * D, **f32)
+        blk['dKVin'] = torch.zeros(nk, D, **f32)
+        blk['estat'] = torch.zeros(nq, 4, **f32)
+        blk['astat'] = torch.zeros(R, H, Tq, 2, **f32)
+        blk['partial'] = torch.zeros(cdiv(nq, 64), _lib.rf_partial_stride(D, FD), **f32)
+        if i < nl - 1 or not sp.head:
+            blk['OUT'] = torch.zeros(nq, D, **f32)
+        if i < nl - 1:
+            blk['S'] = torch.zeros(R, H, Tq, Tk, **f32)
+        if i >= 1:
+            blk['dSprev'] = torch.zeros(R, H, Tq, Tk, **f32)
+            blk['dc_partial'] = torch.zeros(_lib.attn_dc_slots(R, H, Tk), **f32)
+        blk['col'] = (CHAINS.index(sp.chains[j]) % 3) * D
+        return blk
+
+    def _blk(self, j, i):
+        return self.blocks[j * self.spec.nl + i]
+
+    def _q_rows(self, blk):
+        if blk['i'] == 0:
+            return crows(self.U[blk['qm']], blk['Tq'], self.spec.D)
+        return self._out_rows(self._blk(blk['j'], blk['i'] - 1))
+
+    def _out_rows(self, blk):
+        D = self.spec.D
+        if 'OUT' in blk:
+            return crows(blk['OUT'], blk['Tq'], D)
+        return rows(self.Xcat, blk['Tq'], self.Ttot * self.C, self.C, self.toff[blk['qm']] * self.C + blk['col'])
+
+    def _dout_rows(self, blk):
+        D, sp = self.spec.D, self.spec
+        if blk['i'] < sp.nl - 1:
+            return crows(self._blk(blk['j'], blk['i'] + 1)['dQin'], blk['Tq'], D)
+        if not sp.head:
+            return crows(self.dout_chain, blk['Tq'], D)
+        return rows(self.dXcat, blk['Tq'], self.Ttot * self.C, self.C, self.toff[blk['qm']] * self.C + blk['col'])
+
+    def _in_rows(self, m):
+        d, T = self.spec.dims[m], self.T[m]
+        return rows(self.x_in[m], T, T * d, d)
+
+    def _kv_rows(self, blk, which, t):
+        """K (which=0) or V (which=1) half of a [ntok, 2D] buffer t"""
+        D = self.spec.D
+        return rows(t, blk['Tk'], blk['Tk'] * 2 * D, 2 * D, which * D)
+
+    # ------------------------------------------------------------------ descriptors
+    def _attn_desc(self, blk):
+        sp, fl, D = self.spec, self.flat, self.spec.D
+        prev = self._blk(blk['j'], blk['i'] - 1) if blk['i'] > 0 else None
+        return AttnDesc(q=crows(blk['QP'], blk['Tq'], D), k=self._kv_rows(blk, 0, blk['KV']),
+                        v=self._kv_rows(blk, 1, blk['KV']), x=crows(blk['X'], blk['Tq'], D),
+                        mask=self.m_in[blk['km']].data_ptr(), mask_sB=blk['Tk'],
+                        s_prev=prev['S'].data_ptr() if prev is not None else 0, c=fl.ptr(blk['pre'] + 'c'),
+                        s_out=blk['S'].data_ptr() if 'S' in blk else 0, stats=blk['astat'].data_ptr(),
+                        B=self.R, H=sp.H, Tq=blk['Tq'], Tk=blk['Tk'])
+
+    def _epi_desc(self, blk):
+        sp, fl, D, Tq = self.spec, self.flat, self.spec.D, blk['Tq']
+        p = blk['pre']
+        return RfEpiDesc(q=self._q_rows(blk), x=crows(blk['X'], Tq, D), xp=crows(blk['XP'], Tq, D),
+                         h=crows(blk['H'], Tq, D), f1=crows(blk['F1'], Tq, sp.FD), f=crows(blk['F'], Tq, D),
+                         out=self._out_rows(blk), wp=fl.ptr(p + 'proj.weight'), w1=fl.ptr(p + 'ffn.0.weight'),
+                         b1=fl.ptr(p + 'ffn.0.bias'), w2=fl.ptr(p + 'ffn.2.weight'), b2=fl.ptr(p + 'ffn.2.bias'),
+                         ln1_w=fl.ptr(p + 'norm1.weight'), ln1_b=fl.ptr(p + 'norm1.bias'),
+                         ln2_w=fl.ptr(p + 'norm2.weight'), ln2_b=fl.ptr(p + 'norm2.bias'),
+                         a=fl.ptr(p + 'a'), b=fl.ptr(p + 'b'), stats=blk['estat'].data_ptr(),
+                         ntok=blk['nq'], D=D, FD=sp.FD)
+
+    def _epi_bwd_desc(self, blk):
+        D, Tq, FD = self.spec.D, blk['Tq'], self.spec.FD
+        return RfEpiBwdDesc(f=self._epi_desc(blk), dout=self._dout_rows(blk), dout2=Rows(),
+                            df=crows(blk['dF'], Tq, D), df1=crows(blk['dF1'], Tq, FD),
+                            dxp=crows(blk['dXP'], Tq, D), dx=crows(blk['dX'], Tq, D),
+                            dq=crows(blk['dQin'], Tq, D), partial=blk['partial'].data_ptr(), dq_accumulate=0)
+
+    def _attn_bwd_desc(self, blk):
+        D = self.spec.D
+        nxt = self._blk(blk['j'], blk['i'] + 1) if blk['i'] < self.spec.nl - 1 else None
+        return AttnBwdDesc(f=self._attn_desc(blk), dx=crows(blk['dX'], blk['Tq'], D),
+                           dq=crows(blk['dQP'], blk['Tq'], D), dk=self._kv_rows(blk, 0, blk['dKV2']),
+                           dv=self._kv_rows(blk, 1, blk['dKV2']),
+                           ds_next=nxt['dSprev'].data_ptr() if nxt is not None else 0,
+                           ds_prev=blk['dSprev'].data_ptr() if 'dSprev' in blk else 0,
+                           dc_partial=blk['dc_partial'].data_ptr() if 'dc_partial' in blk else 0)
+
+    def _wkv(self, blk):
+        """[w_qkv.1; w_qkv.2] as one [2D, D] matrix (adjacent in the flat buffer)"""
+        fl, D, p = self.flat, self.spec.D, blk['pre']
+        k, v = fl.offsets[p + 'w_qkv.1.weight'], fl.offsets[p + 'w_qkv.2.weight']
+        assert v == k + D * D, 'w_qkv.1 / w_qkv.2 must be adjacent in the flat buffer'
+        return p + 'w_qkv.1.weight'
+
+    def _build(self):
+        sp, fl, R, D, H, nl, FD = self.spec, self.flat, self.R, self.spec.D, self.spec.H, self.spec.nl, self.spec.FD
+        dev = self.device
+        g = fl.gptr
+        gemm = dict(bias=0, table=0, accumulate=0, relu=0, alpha=1.0)
+        # unify: Conv1d k=1 (== Linear on the feature axis) + position embedding table
+        ud = []
+        for m in sp.mods:
+            d, T = sp.dims[m], self.T[m]
+            ud.append(GemmDesc(x=self._in_rows(m), y=crows(self.U[m], T, D),
+                               w=fl.ptr(sp.prefix + 'unify_dimension.%s.weight' % UNIFY_NAMES[m]),
+                               bias=0, table=fl.ptr(sp.prefix + '%s.position_embeddings.weight' % POS_NAMES[m]),
+                               ntok=self.ntok[m], N=D, K=d, ldw=d, w_nt=1, accumulate=0, relu=0, alpha=1.0))
+        self.d_unify = DescArray(GemmDesc, ud, dev)
+        self.t_unify = max(cdiv(self.ntok[m], 64) for m in sp.mods)
+        # projections: KV of every block + Q of layer 0 (all read U only)
+        pd = []
+        for blk in self.blocks:
+            pd.append(GemmDesc(x=crows(self.U[blk['km']], blk['Tk'], D), y=crows(blk['KV'], blk['Tk'], 2 * D),
+                               w=fl.ptr(self._wkv(blk)), ntok=blk['nk'], N=2 * D, K=D, ldw=D, w_nt=1, **gemm))
+            if blk['i'] == 0:
+                pd.append(GemmDesc(x=self._q_rows(blk), y=crows(blk['QP'], blk['Tq'], D),
+                                   w=fl.ptr(blk['pre'] + 'w_qkv.0.weight'), ntok=blk['nq'], N=D, K=D, ldw=D,
+                                   w_nt=1, **gemm))
+        self.d_proj = DescArray(GemmDesc, pd, dev)
+        self.t_proj = max(cdiv(b['nk'], 64) for b in self.blocks)
+        self.d_q, self.d_attn, self.d_epi, self.t_attn, self.t_epi = [], [], [], [], []
+        self.d_epib, self.d_attnb, self.t_attnb, self.d_ingrad = [], [], [], []
+        for i in range(nl):
+            layer = [b for b in self.blocks if b['i'] == i]
+            self.d_q.append(DescArray(GemmDesc, [
+                GemmDesc(x=self._q_rows(b), y=crows(b['QP'], b['Tq'], D), w=fl.ptr(b['pre'] + 'w_qkv.0.weight'),
+                         ntok=b['nq'], N=D, K=D, ldw=D, w_nt=1, **gemm) for b in layer] if i > 0 else [], dev))
+            self.d_attn.append(DescArray(AttnDesc, [self._attn_desc(b) for b in layer], dev))
+            self.d_epi.append(DescArray(RfEpiDesc, [self._epi_desc(b) for b in layer], dev))
+            geo = _lib.attn_geometry([(R, H, b['Tq'], b['Tk']) for b in layer])
+            self.t_attn.append(geo[0])
+            self.t_attnb.append(geo[1])
+            self.t_epi.append(max(cdiv(b['nq'], 64) for b in layer))
+            self.d_epib.append(DescArray(RfEpiBwdDesc, [self._epi_bwd_desc(b) for b in layer], dev))
+            self.d_attnb.append(DescArray(AttnBwdDesc, [self._attn_bwd_desc(b) for b in layer], dev))
+            ig = []
+            for b in layer:
+                # dq_in += dQP W_q  (onto the residual dz1 the epilogue backward wrote)
+                ig.append(GemmDesc(x=crows(b['dQP'], b['Tq'], D), y=crows(b['dQin'], b['Tq'], D),
+                                   w=fl.ptr(b['pre'] + 'w_qkv.0.weight'), bias=0, table=0, ntok=b['nq'], N=D, K=D,
+                                   ldw=D, w_nt=0, accumulate=1, relu=0, alpha=1.0))
+                # dkv_in = [dK | dV] [W_k; W_v]
+                ig.append(GemmDesc(x=crows(b['dKV2'], b['Tk'], 2 * D), y=crows(b['dKVin'], b['Tk'], D),
+                                   w=fl.ptr(self._wkv(b)), ntok=b['nk'], N=D, K=2 * D, ldw=D, w_nt=0, **gemm))
+            self.d_ingrad.append(DescArray(GemmDesc, ig, dev))
+        self.t_ingrad = max(max(cdiv(b['nq'], 64), cdiv(b['nk'], 64)) for b in self.blocks)
+        # per-modality input-gradient sums
+        sd = []
+        for m in sp.mods:
+            T = self.T[m]
+            srcs = [crows(self._blk(j, 0)['dQin'], T, D) for j, (qm, km) in enumerate(sp.chains) if qm == m]
+            srcs += [crows(self._blk(j, i)['dKVin'], T, D) for j, (qm, km) in enumerate(sp.chains) if km == m
+                     for i in range(nl)]
+            assert len(srcs) <= _lib.SUM_MAX_SRC
+            sd.append(SumDesc(src=(Rows * _lib.SUM_MAX_SRC)(*srcs), out=crows(self.dU[m], T, D), n_src=len(srcs),
+                              ntok=self.ntok[m], D=D, accumulate=0))
+        self.d_sum = DescArray(SumDesc, sd, dev)
+        self.t_sum = min(1024, max(cdiv(self.ntok[m] * D // 4, 256) for m in sp.mods))
+        if sp.head:
+            self._build_head()
+        self._build_grads()
+
+    def _build_head(self):
+        sp, fl, R, D = self.spec, self.flat, self.R, self.spec.D
+        dev = self.device
+        pre = sp.prefix
+        self.d_pool = DescArray(PoolDesc, [PoolDesc(x=self.Xcat.data_ptr(), dx=self.dXcat.data_ptr(),
+                                                    pooled=self.pooled.data_ptr(), dpooled=self.dpooled.data_ptr(),
+                                                    argmax=self.argmax.data_ptr(), B=R, T=self.Ttot, C=self.C)], dev)
+        self.t_pool = R * cdiv(self.C, 32)
+        self.t_poolb = min(2048, cdiv(R * self.Ttot * self.C, 256))
+        F = 2 * self.C
+        self.d_fc = DescArray(GemmDesc, [GemmDesc(
+            x=crows(self.pooled, 1, F), y=crows(self.fc, 1, D), w=fl.ptr(pre + 'fully_connected.weight'),
+            bias=fl.ptr(pre + 'fully_connected.bias'), table=0, ntok=R, N=D, K=F, ldw=F, w_nt=1, accumulate=0,
+            relu=0, alpha=1.0)], dev)
+        self.d_fcb = DescArray(GemmDesc, [GemmDesc(
+            x=crows(self.dfc, 1, D), y=crows(self.dpooled, 1, F), w=fl.ptr(pre + 'fully_connected.weight'),
+            bias=0, table=0, ntok=R, N=F, K=D, ldw=F, w_nt=0, accumulate=0, relu=0, alpha=1.0)], dev)
+        self.t_fc = cdiv(R, 64)
+        self.head = RfHeadDesc(fc=self.fc.data_ptr(), ln_w=fl.ptr(pre + 'normalization.weight'),
+                               ln_b=fl.ptr(pre + 'normalization.bias'), wc=fl.ptr('classifier.weight'),
+                               bc=fl.ptr('classifier.bias'), trans=fl.ptr('trans'), labels=self.labels.data_ptr(),
+                               umask=self.umask.data_ptr(), out=self.out.data_ptr(), h=self.h.data_ptr(),
+                               d12=self.d12.data_ptr(), dfc=self.dfc.data_ptr(), row_loss=self.row_loss.data_ptr(),
+                               partial=self.head_partial.data_ptr(), ext_dout=0, B=self.B, P=self.P, D=D,
+                               compute_grad=1, loss_scale=1.0 / R)
+
+    def _build_grads(self):
+        sp, fl, R, D, FD = self.spec, self.flat, self.R, self.spec.D, self.spec.FD
+        dev = self.device
+        g = fl.gptr
+        items = []
+        for b in self.blocks:
+            Tq, Tk, nq, nk, p = b['Tq'], b['Tk'], b['nq'], b['nk'], b['pre']
+            items.append((crows(b['dQP'], Tq, D), D, nq, [(self._q_rows(b), D, g(p + 'w_qkv.0.weight'), D)]))
+            items.append((crows(self.U[b['km']], Tk, D), D, nk,
+                          [(crows(b['dKV2'], Tk, 2 * D), 2 * D, g(self._wkv(b)), D)], 1))
+            items.append((crows(b['dXP'], Tq, D), D, nq, [(crows(b['X'], Tq, D), D, g(p + 'proj.weight'), D)]))
+            items.append((crows(b['H'], Tq, D), D, nq, [(crows(b['dF1'], Tq, FD), FD, g(p + 'ffn.0.weight'), D)], 1))
+            items.append((crows(b['dF'], Tq, D), D, nq, [(crows(b['F1'], Tq, FD), FD, g(p + 'ffn.2.weight'), FD)]))
+        for m in sp.mods:
+            d = sp.dims[m]
+            items.append((crows(self.dU[m], self.T[m], D), D, self.ntok[m],
+                          [(self._in_rows(m), d, g(sp.prefix + 'unify_dimension.%s.weight' % UNIFY_NAMES[m]), d)]))
+        if sp.head:
+            F = 2 * self.C
+            items.append((crows(self.dfc, 1, D), D, R, [(crows(self.pooled, 1, F), F,
+                                                         g(sp.prefix + 'fully_connected.weight'), F)]))
+            items.append((crows(self.d12, 1, 2 * NC), 2 * NC, R, [(crows(self.h, 1, D), D, g('classifier.weight'), D)]))
+        self.wg_partial, self.d_wgrad, self.t_wgrad, self.t_wgred = make_wgrad(items, dev)
+        cs = []
+
+        def col(partial, out, n_rows, n_cols, ld):
+            cs.append(ColsumDesc(partial=partial, out=out, n_rows=n_rows, n_cols=n_cols, ld=ld, accumulate=0))
+
+        S = _lib.rf_partial_stride(D, FD)
+        for b in self.blocks:
+            base, nt, p = b['partial'].data_ptr(), b['partial'].shape[0], b['pre']
+            for k, (name, n) in enumerate((('norm2.weight', D), ('norm2.bias', D), ('norm1.weight', D),
+                                           ('norm1.bias', D), ('ffn.2.bias', D))):
+                col(base + 4 * k * D, g(p + name), nt, n, S)
+            col(base + 4 * 5 * D, g(p + 'ffn.0.bias'), nt, FD, S)
+            col(base + 4 * (5 * D + FD), g(p + 'a'), nt, 1, S)
+            col(base + 4 * (5 * D + FD + 1), g(p + 'b'), nt, 1, S)
+            if 'dc_partial' in b:
+                col(b['dc_partial'].data_ptr(), g(p + 'c'), b['dc_partial'].numel(), 1, 1)
+        for m in sp.mods:
+            T = self.T[m]
+            col(self.dU[m].data_ptr(), g(sp.prefix + '%s.position_embeddings.weight' % POS_NAMES[m]), R, T * D, T * D)
+        if sp.head:
+            pre = sp.prefix
+            col(self.dfc.data_ptr(), g(pre + 'fully_connected.bias'), R, D, D)
+            col(self.d12.data_ptr(), g('classifier.bias'), R, 2 * NC, 2 * NC)
+            W = 2 * D + NC * NC
+            hp = self.head_partial.data_ptr()
+            col(hp, g(pre + 'normalization.weight'), self.B, D, W)
+            col(hp + 4 * D, g(pre + 'normalization.bias'), self.B, D, W)
+            col(hp + 8 * D, g('trans'), self.B, NC * NC, W)
+            col(self.row_loss.data_ptr(), self.loss.data_ptr(), self.B, 1, 1)
+        self.d_colsum = DescArray(ColsumDesc, cs, dev)
+        self.t_colsum = max(cdiv(c.n_cols, 32) for c in cs)
+
+    # ------------------------------------------------------------------ execution
+    def set_inputs(self, l, v, a, lm, vm, am, labels=None, umask=None):
+        """Reference-shaped [B, P, T, d] features / [B, P, T] masks (or [B, T, d] / [B, T] for the
+        single-utterance chain plan) into the resident buffers."""
+        with torch.no_grad():
+            for m, x, mk in (('l', l, lm), ('v', v, vm), ('a', a, am)):
+                if m not in self.spec.mods:
+                    continue
+                self.x_in[m].copy_(x.reshape(self.x_in[m].shape))
+                self.m_in[m].copy_(mk.reshape(self.m_in[m].shape))
+            if labels is not None:
+                self.labels.copy_(labels)
+            if umask is not None:
+                self.umask.copy_(umask)
+
+    _drop = 0.0
+
+    def set_dropout(self, p):
+        if p != 0.0:
+            raise NotImplementedError('mep_amd realformer path: DROP must be 0 (the reference value, '
+                                      'others/realformer.py:37)')
+
+    def advance_seed(self, stream=None):
+        pass
+
+    def forward(self, grad=True, rdrop=False, stream=None):
+        sp, nl = self.spec, self.spec.nl
+        assert not rdrop
+        ex = (sp.D, sp.FD)
+        launch('mep_gemm', self.d_unify, self.t_unify, stream)
+        launch('mep_gemm', self.d_proj, self.t_proj, stream)
+        for i in range(nl):
+            if i > 0:
+                launch('mep_gemm', self.d_q[i], self.t_epi[i], stream)
+            launch('mep_attn_fwd', self.d_attn[i], self.t_attn[i], stream, threads=256)
+            launch('mep_rf_epi_fwd', self.d_epi[i], self.t_epi[i], stream, extra=ex)
+        if sp.head:
+            launch('mep_pool_fwd', self.d_pool, self.t_pool, stream)
+            launch('mep_gemm', self.d_fc, self.t_fc, stream)
+            self.head.compute_grad = int(grad)
+            self.head.ext_dout = 0
+            _lib.call('mep_rf_head', ctypes.byref(self.head), stream=stream)
+
+    def backward(self, ext_dout=None, stream=None):
+        """Backward from the fused loss (or from ext_dout: [B, P, 6] for the head, the last block's
+        output gradient for the chain plan).  Writes every gradient into flat.grad."""
+        sp, nl = self.spec, self.spec.nl
+        ex = (sp.D, sp.FD)
+        if sp.head:
+            if ext_dout is not None:
+                self.head.compute_grad = 1
+                self.head.ext_dout = ext_dout.data_ptr()
+                _lib.call('mep_rf_head', ctypes.byref(self.head), stream=stream)
+                self.head.ext_dout = 0
+            launch('mep_gemm', self.d_fcb, self.t_fc, stream)
+            launch('mep_pool_bwd', self.d_pool, self.t_poolb, stream)
+        elif ext_dout is not None:
+            self.dout_chain.copy_(ext_dout.reshape(self.dout_chain.shape))
+        self.dQP_all.zero_()
+        for i in reversed(range(nl)):
+            launch('mep_rf_epi_bwd', self.d_epib[i], self.t_epi[i], stream, extra=ex)
+            launch('mep_attn_bwd', self.d_attnb[i], self.t_attnb[i], stream, threads=256)
+            launch('mep_gemm', self.d_ingrad[i], self.t_ingrad, stream)
+        launch('mep_sum_rows', self.d_sum, self.t_sum, stream)
+        launch('mep_wgrad', self.d_wgrad, self.t_wgrad, stream)
+        launch('mep_wgrad_reduce', self.d_wgrad, self.t_wgred, stream)
+        launch('mep_colsum', self.d_colsum, self.t_colsum, stream)
+
+
+class RealformerRunner:
+    """Flat parameters + shape-keyed plans of a State_Transfer model (or a Multi_class text chain)."""
+
+    def __init__(self, model, spec, device):
+        from .flat import FlatParams
+        self.model, self.spec = model, spec
+        self.device = torch.device(device)
+        names = [n for n, _ in model.named_parameters()]
+        self.flat = FlatParams(model, self.device, no_grad=spec.no_grad_params(names))
+        self.plans = {}
+        self._gen = 0
+        self._live = None
+        self.n_inputs = 6
+
+    def plan(self, B, P):
+        key = (int(B), int(P))
+        p = self.plans.get(key)
+        if p is None:
+            p = RealformerPlan(self.spec, self.flat, key[0], key[1], self.device)
+            self.plans[key] = p
+        return p
+
+    def plan_for(self, l):
+        if self.spec.head:
+            return self.plan(l.shape[0], l.shape[1])
+        return self.plan(l.shape[0], 1)
+
+    def stage(self, l, v, a, labels, lm, vm, am, umask):
+        """realformer train batch order (others/realformer.py:306-309)"""
+        plan = self.plan_for(l)
+        plan.set_inputs(l, v, a, lm, vm, am, labels, umask)
+        return plan
+
+    def drop_p(self):
+        return 0.0
+
+    def run_forward(self, inputs):
+        l, v, a, lm, vm, am = inputs
+        plan = self.plan_for(l)
+        plan.set_inputs(l, v, a, lm, vm, am)
+        plan.forward(grad=False)
+        self._gen += 1
+        self._live = (plan, self._gen)
+        self.token = self._gen
+        return (plan.out if self.spec.head else plan.out_chain.view(l.shape[0], l.shape[1], -1)).clone()
+
+    def run_backward(self, dout, token=None):
+        plan, gen = self._live
+        if token is not None and token != gen:
+            raise RuntimeError('mep_amd: backward of an older forward -- call backward before the next '
+                               'forward of the same shape')
+        plan.backward(ext_dout=dout)
+        g = self.flat.grad.clone()
+        return [self.flat.view(g, n) if self.flat.has_grad[n] else None for n in self.flat.names]

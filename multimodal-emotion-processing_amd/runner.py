@@ -43,6 +43,12 @@ class ModelRunner:
         B = bt(l)[0]
         return self.plan(B, (bt(l)[1], bt(v)[1], bt(a)[1]))
 
+    def stage(self, l, v, a, lm, vm, am, labels):
+        """Plan for the batch's shape with the batch copied into its resident buffers."""
+        plan = self.plan_for(l, v, a)
+        plan.set_inputs(l, v, a, lm, vm, am, labels)
+        return plan
+
     def drop_p(self):
         """Dropout probability of the current mode (the model's live nn.Dropout p in train mode)."""
         if not self.model.training:

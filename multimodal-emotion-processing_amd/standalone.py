@@ -214,3 +214,126 @@ def layer_norm(x, norm):
 def unify_norm_forward(mod, l, v, a):
     """Ren-MME Unify_Dimension.forward (Ren-MME/run.py:167-168): shared norm1 after each projection."""
     return tuple(layer_norm(y, mod.norm1) for y in unify_forward(mod, l, v, a))
+
+
+class _RFBlockFn(torch.autograd.Function):
+    """realformer Attention_Block.forward (others/realformer.py:182-209) on libmep_hip:
+    Q/K/V projections (mep_gemm), residual attention core, fused RealFormer epilogue."""
+
+    @staticmethod
+    def forward(ctx, H, q, k, v, mask, s_prev, wq, wk, wv, wp, n1w, n1b, n2w, n2b, w1, b1, w2, b2, a, b, c):
+        q, k, v, mask = _c(q), _c(k), _c(v), _c(mask)
+        B, Tq, D = q.shape
+        Tk = k.shape[1]
+        FD = w1.shape[0]
+        dev = q.device
+        f = dict(dtype=torch.float32, device=dev)
+        QP, X, XP, Hh, F, out = (torch.empty(B, Tq, D, **f) for _ in range(6))
+        KV = torch.empty(B, Tk, 2 * D, **f)
+        F1 = torch.empty(B, Tq, FD, **f)
+        S = torch.empty(B, H, Tq, Tk, **f)
+        astat = torch.empty(B, H, Tq, 2, **f)
+        estat = torch.empty(B * Tq, 4, **f)
+        sp = _c(s_prev) if s_prev is not None else None
+        kv = lambda t, which: _lib.Rows(ptr=t.data_ptr() + 4 * which * D, sB=Tk * 2 * D, sT=2 * D, T=Tk)  # noqa: E731
+        g = dict(bias=0, table=0, accumulate=0, relu=0, alpha=1.0, w_nt=1, K=D, ldw=D, N=D)
+        gd = [GemmDesc(x=crows(q, Tq, D), y=crows(QP, Tq, D), w=wq.data_ptr(), ntok=B * Tq, **g),
+              GemmDesc(x=crows(k, Tk, D), y=kv(KV, 0), w=wk.data_ptr(), ntok=B * Tk, **g),
+              GemmDesc(x=crows(v, Tk, D), y=kv(KV, 1), w=wv.data_ptr(), ntok=B * Tk, **g)]
+        launch('mep_gemm', DescArray(GemmDesc, gd, dev), cdiv(B * max(Tq, Tk), 64))
+        ad = AttnDesc(q=crows(QP, Tq, D), k=kv(KV, 0), v=kv(KV, 1), x=crows(X, Tq, D), mask=mask.data_ptr(),
+                      mask_sB=Tk, s_prev=sp.data_ptr() if sp is not None else 0, c=c.data_ptr(), s_out=S.data_ptr(),
+                      stats=astat.data_ptr(), B=B, H=H, Tq=Tq, Tk=Tk)
+        ed = _lib.RfEpiDesc(q=crows(q, Tq, D), x=crows(X, Tq, D), xp=crows(XP, Tq, D), h=crows(Hh, Tq, D),
+                            f1=crows(F1, Tq, FD), f=crows(F, Tq, D), out=crows(out, Tq, D), wp=wp.data_ptr(),
+                            w1=w1.data_ptr(), b1=b1.data_ptr(), w2=w2.data_ptr(), b2=b2.data_ptr(),
+                            ln1_w=n1w.data_ptr(), ln1_b=n1b.data_ptr(), ln2_w=n2w.data_ptr(), ln2_b=n2b.data_ptr(),
+                            a=a.data_ptr(), b=b.data_ptr(), stats=estat.data_ptr(), ntok=B * Tq, D=D, FD=FD)
+        geo = _lib.attn_geometry([(B, H, Tq, Tk)])
+        launch('mep_attn_fwd', DescArray(AttnDesc, [ad], dev), geo[0], threads=geo[2])
+        launch('mep_rf_epi_fwd', DescArray(_lib.RfEpiDesc, [ed], dev), cdiv(B * Tq, 64), extra=(D, FD))
+        ctx.save_for_backward(q, k, v, mask, QP, KV, X, XP, Hh, F1, F, S, astat, estat,
+                              wq, wk, wv, wp, n1w, n1b, n2w, n2b, w1, b1, w2, b2, a, b, c)
+        ctx.sp = sp
+        ctx.meta = (B, Tq, Tk, D, H, FD)
+        ctx.descs = (ad, ed)
+        return out, S
+
+    @staticmethod
+    @torch.autograd.function.once_differentiable
+    def backward(ctx, dout, dS):
+        (q, k, v, mask, QP, KV, X, XP, Hh, F1, F, S, astat, estat,
+         wq, wk, wv, wp, n1w, n1b, n2w, n2b, w1, b1, w2, b2, a, b, c) = ctx.saved_tensors
+        B, Tq, Tk, D, H, FD = ctx.meta
+        ad, ed = ctx.descs
+        dev = q.device
+        f = dict(dtype=torch.float32, device=dev)
+        dout = _c(dout) if dout is not None else torch.zeros(B, Tq, D, **f)
+        dS = _c(dS) if dS is not None else None
+        dF, dXP, dX, dQin = (torch.empty(B, Tq, D, **f) for _ in range(4))
+        dQP = torch.zeros(B, Tq, D, **f)
+        dF1 = torch.empty(B, Tq, FD, **f)
+        dKV2 = torch.empty(B, Tk, 2 * D, **f)
+        dk_in, dv_in = torch.empty(B, Tk, D, **f), torch.empty(B, Tk, D, **f)
+        nt = cdiv(B * Tq, 64)
+        stride = _lib.rf_partial_stride(D, FD)
+        part = torch.empty(nt, stride, **f)
+        has_prev = ctx.sp is not None
+        dSp = torch.empty(B, H, Tq, Tk, **f) if has_prev else None
+        dc_part = torch.empty(_lib.attn_dc_slots(B, H, Tk), **f) if has_prev else None
+        kv = lambda t, which: _lib.Rows(ptr=t.data_ptr() + 4 * which * D, sB=Tk * 2 * D, sT=2 * D, T=Tk)  # noqa: E731
+        eb = _lib.RfEpiBwdDesc(f=ed, dout=crows(dout, Tq, D), dout2=Rows(), df=crows(dF, Tq, D),
+                               df1=crows(dF1, Tq, FD), dxp=crows(dXP, Tq, D), dx=crows(dX, Tq, D),
+                               dq=crows(dQin, Tq, D), partial=part.data_ptr(), dq_accumulate=0)
+        ab = AttnBwdDesc(f=ad, dx=crows(dX, Tq, D), dq=crows(dQP, Tq, D), dk=kv(dKV2, 0), dv=kv(dKV2, 1),
+                         ds_next=dS.data_ptr() if dS is not None else 0, ds_prev=dSp.data_ptr() if has_prev else 0,
+                         dc_partial=dc_part.data_ptr() if has_prev else 0)
+        launch('mep_rf_epi_bwd', DescArray(_lib.RfEpiBwdDesc, [eb], dev), nt, extra=(D, FD))
+        geo = _lib.attn_geometry([(B, H, Tq, Tk)])
+        launch('mep_attn_bwd', DescArray(AttnBwdDesc, [ab], dev), geo[1], threads=geo[3])
+        g = dict(bias=0, table=0, relu=0, alpha=1.0, w_nt=0, K=D, ldw=D, N=D)
+        gd = [GemmDesc(x=crows(dQP, Tq, D), y=crows(dQin, Tq, D), w=wq.data_ptr(), ntok=B * Tq, accumulate=1, **g),
+              GemmDesc(x=kv(dKV2, 0), y=crows(dk_in, Tk, D), w=wk.data_ptr(), ntok=B * Tk, accumulate=0, **g),
+              GemmDesc(x=kv(dKV2, 1), y=crows(dv_in, Tk, D), w=wv.data_ptr(), ntok=B * Tk, accumulate=0, **g)]
+        launch('mep_gemm', DescArray(GemmDesc, gd, dev), cdiv(B * max(Tq, Tk), 64))
+        grads = {name: torch.empty_like(t) for name, t in (('wq', wq), ('wk', wk), ('wv', wv), ('wp', wp),
+                                                           ('n1w', n1w), ('n1b', n1b), ('n2w', n2w), ('n2b', n2b),
+                                                           ('w1', w1), ('b1', b1), ('w2', w2), ('b2', b2),
+                                                           ('a', a), ('b', b), ('c', c))}
+        nq, nk = B * Tq, B * Tk
+        keep = _wgrad([(crows(dQP, Tq, D), D, nq, [(crows(q, Tq, D), D, grads['wq'].data_ptr(), D)]),
+                       (kv(dKV2, 0), D, nk, [(crows(k, Tk, D), D, grads['wk'].data_ptr(), D)]),
+                       (kv(dKV2, 1), D, nk, [(crows(v, Tk, D), D, grads['wv'].data_ptr(), D)]),
+                       (crows(dXP, Tq, D), D, nq, [(crows(X, Tq, D), D, grads['wp'].data_ptr(), D)]),
+                       (crows(Hh, Tq, D), D, nq, [(crows(dF1, Tq, FD), FD, grads['w1'].data_ptr(), D)], 1),
+                       (crows(dF, Tq, D), D, nq, [(crows(F1, Tq, FD), FD, grads['w2'].data_ptr(), FD)])], dev)
+        cs = []
+        for k_, (name, n) in enumerate((('n2w', D), ('n2b', D), ('n1w', D), ('n1b', D), ('b2', D))):
+            cs.append(ColsumDesc(partial=part.data_ptr() + 4 * k_ * D, out=grads[name].data_ptr(), n_rows=nt,
+                                 n_cols=n, ld=stride, accumulate=0))
+        for name, off, n in (('b1', 5 * D, FD), ('a', 5 * D + FD, 1), ('b', 5 * D + FD + 1, 1)):
+            cs.append(ColsumDesc(partial=part.data_ptr() + 4 * off, out=grads[name].data_ptr(), n_rows=nt, n_cols=n,
+                                 ld=stride, accumulate=0))
+        if has_prev:
+            cs.append(ColsumDesc(partial=dc_part.data_ptr(), out=grads['c'].data_ptr(), n_rows=dc_part.numel(),
+                                 n_cols=1, ld=1, accumulate=0))
+        launch('mep_colsum', DescArray(ColsumDesc, cs, dev), cdiv(max(D, FD), 32))
+        del keep
+        return (None, dQin, dk_in, dv_in, None, dSp, grads['wq'], grads['wk'], grads['wv'], grads['wp'],
+                grads['n1w'], grads['n1b'], grads['n2w'], grads['n2b'], grads['w1'], grads['b1'], grads['w2'],
+                grads['b2'], grads['a'], grads['b'], grads['c'] if has_prev else None)
+
+
+def rf_block_forward(block, q, k, v, mask, scores):
+    from ._autograd import require_cuda
+    require_cuda(q, k, v, mask)
+    if mask is None or mask.dim() != 2:
+        raise NotImplementedError('mep_amd attention takes a [batch, kv_len] key mask (the only form the '
+                                  'reference models pass)')
+    if block.training and block.drop.p > 0.0:
+        raise NotImplementedError('realformer dropout: the reference runs DROP = 0 (others/realformer.py:37)')
+    ffn0, ffn2 = block.ffn[0], block.ffn[2]
+    return _RFBlockFn.apply(block.n_heads, q, k, v, mask, scores, block.w_qkv[0].weight, block.w_qkv[1].weight,
+                            block.w_qkv[2].weight, block.proj.weight, block.norm1.weight, block.norm1.bias,
+                            block.norm2.weight, block.norm2.bias, ffn0.weight, ffn0.bias, ffn2.weight, ffn2.bias,
+                            block.a, block.b, block.c)

@@ -42,12 +42,14 @@ def cdiv(a, b):
 
 
 def make_wgrad(items, dev, tok_per_split=TOK_PER_SPLIT):
-    """items: [(a_rows, N, ntok, [(b_rows, K, out_ptr, ldo), ...]), ...] -> (workspace, descs,
-    wgrad tiles, reduce tiles).  One descriptor per A operand; its B operands concatenate on K."""
-    total = sum(cdiv(n, tok_per_split) * N * sum(b[1] for b in bs) for (_, N, n, bs) in items)
+    """items: [(a_rows, N, ntok, [(b_rows, K, out_ptr, ldo), ...][, out_trans]), ...] ->
+    (workspace, descs, wgrad tiles, reduce tiles).  One descriptor per A operand; its B operands
+    concatenate on K.  out_trans: dW written transposed (out[k * ldo + n])."""
+    items = [tuple(it) + (0,) * (5 - len(it)) for it in items]
+    total = sum(cdiv(n, tok_per_split) * N * sum(b[1] for b in bs) for (_, N, n, bs, _) in items)
     ws = torch.zeros(max(total, 1), dtype=torch.float32, device=dev)
     descs, off, tmax, rmax = [], 0, 0, 0
-    for (a, N, n, bs) in items:
+    for (a, N, n, bs, trans) in items:
         assert N <= 128 and len(bs) <= _lib.WG_MAX_B
         ktot = sum(b[1] for b in bs)
         ns = cdiv(n, tok_per_split)
@@ -58,7 +60,7 @@ def make_wgrad(items, dev, tok_per_split=TOK_PER_SPLIT):
                                kb=(ctypes.c_int32 * _lib.WG_MAX_B)(*[b[1] for b in allb]),
                                ldo=(ctypes.c_int32 * _lib.WG_MAX_B)(*[b[3] for b in allb]),
                                partial=ws.data_ptr() + 4 * off, n_b=len(bs), ntok=n, N=N, Ktot=ktot,
-                               tok_per_split=tok_per_split, n_split=ns, accumulate=0))
+                               tok_per_split=tok_per_split, n_split=ns, accumulate=0, out_trans=int(trans)))
         off += ns * N * ktot
         tmax = max(tmax, ns * cdiv(ktot, 256))
         rmax = max(rmax, cdiv(N * ktot, 256))

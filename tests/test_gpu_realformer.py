@@ -1,0 +1,125 @@
+"""GPU parity of the others/realformer.py path (libmep_hip) against the reference golden vectors:
+the standalone RealFormer Attention_Block (K != V projections, residual scores, a/b ReZero
+scalars, FFN), the BASELINE cfg2 text chain (Conv1d unify + positions + 2 blocks, at the small
+and the full D=96/T=50 shape) and the whole State_Transfer step (P utterances through the shared
+encoder, sigmoid/tanh gate recurrence, masked circle loss, clip, Adam).
+
+Tolerances as test_gpu_cmu.py: outputs rtol 1e-4, gradients rtol 1e-3 (floor 1e-5 x max|grad|),
+post-Adam parameters atol 2e-5.
+"""
+import contextlib
+
+import pytest
+import torch
+
+from tests.golden import fixtures
+from tests.gpu_util import assert_close, load_params
+
+pytestmark = pytest.mark.gpu
+
+
+@contextlib.contextmanager
+def ffn_const(meta):
+    """Attention_Block reads the module constant FFN at construction (realformer.py:163-168)."""
+    from mep_amd import realformer as rf
+    old = rf.FFN
+    rf.FFN = meta['consts']['FFN']
+    try:
+        yield rf
+    finally:
+        rf.FFN = old
+
+
+def test_realformer_block_standalone(cuda):
+    meta, gold = fixtures.load('block_rf')
+    with ffn_const(meta) as rf:
+        blk = rf.Attention_Block(meta['ctor']['dim'], meta['ctor']['n_heads'])
+    load_params(blk, meta)
+    blk = blk.to(cuda).train()
+    q, kv, mask, s_prev, g_out = fixtures.block_inputs(meta)
+    qt = torch.tensor(q, device=cuda, requires_grad=True)
+    kvt = torch.tensor(kv, device=cuda, requires_grad=True)
+    sp = torch.tensor(s_prev, device=cuda, requires_grad=True)
+    y, s = blk(qt, kvt, kvt, torch.tensor(mask, device=cuda), sp)
+    assert_close(y, gold['out'], 1e-4, 1e-6, 'out')
+    assert_close(s, gold['scores'], 1e-5, 1e-7, 'scores')
+    obj = (y * torch.tensor(g_out, device=cuda)).sum() + (s * torch.tensor(gold['g_scores'], device=cuda)).sum()
+    obj.backward()
+    assert_close(qt.grad, gold['grad_q'], 1e-3, 1e-5, 'grad_q')
+    assert_close(kvt.grad, gold['grad_kv'], 1e-3, 1e-5, 'grad_kv')
+    assert_close(sp.grad, gold['grad_sprev'], 1e-3, 1e-5, 'grad_sprev')
+    for k, p in blk.named_parameters():
+        assert_close(p.grad, gold['grad/' + k], 1e-3, 1e-5, k)
+
+
+@pytest.mark.parametrize('name', fixtures.names('chain'))
+def test_text_chain(name, cuda):
+    """BASELINE cfg2: realformer text encoder forward + backward of mean(out * G)."""
+    meta, gold = fixtures.load(name)
+    with ffn_const(meta) as rf:
+        mc = rf.Multi_class(**meta['ctor'])
+    load_params(mc, meta)
+    mc = mc.to(cuda).train()
+    x, lm, G = fixtures.chain_inputs(meta)
+    out = rf.encode_chain(mc, torch.tensor(x, device=cuda), torch.tensor(lm, device=cuda), meta['n_layers'])
+    assert_close(out, gold['out'], 1e-4, 1e-6, 'out')
+    obj = (out * torch.tensor(G, device=cuda)).mean()
+    assert_close(obj.reshape(()), gold['obj'], 1e-4, 1e-6, 'obj')
+    obj.backward()
+    for k, p in mc.named_parameters():
+        if 'grad/' + k in gold:
+            assert_close(p.grad, gold['grad/' + k], 1e-3, 1e-5, k)
+        else:
+            assert p.grad is None or float(p.grad.abs().max()) == 0.0, k
+
+
+def _state(meta, cuda):
+    with ffn_const(meta) as rf:
+        m = rf.State_Transfer(**meta['ctor'])
+    load_params(m, meta)
+    return m.to(cuda).train()
+
+
+def _batch(meta, cuda):
+    l, v, a, labels, lm, vm, am, um = [t.to(cuda) for t in fixtures.batch(meta)]
+    return l, v, a, labels, lm, vm, am, um
+
+
+def test_state_transfer_autograd(cuda):
+    from mep_amd import realformer as rf
+    meta, gold = fixtures.load('rf_state_small')
+    model = _state(meta, cuda)
+    l, v, a, labels, lm, vm, am, um = _batch(meta, cuda)
+    out = model(l, v, a, lm, vm, am)
+    assert_close(out, gold['logits'], 1e-4, 1e-6, 'out')
+    loss = (rf.multi_circle_loss(out, labels) * um).mean()
+    assert_close(loss.reshape(()), gold['loss'], 1e-4, 0, 'loss')
+    loss.backward()
+    coef = float(gold['clipcoef'])
+    for k, p in model.named_parameters():
+        if 'nograd/' + k in gold:
+            assert p.grad is None, k
+            continue
+        assert_close(p.grad * coef, gold['grad/' + k], 1e-3, 1e-5, k)
+
+
+@pytest.mark.parametrize('graph', [False, True])
+def test_state_transfer_engine_step(graph, cuda):
+    from mep_amd.engine import TrainEngine
+    from mep_amd.optim import FusedAdam
+    meta, gold = fixtures.load('rf_state_small')
+    model = _state(meta, cuda)
+    opt = FusedAdam(model, lr=1e-3)
+    eng = TrainEngine(model, opt, clip=1.0, graph=graph)
+    batch = _batch(meta, cuda)
+    loss = float(eng.step(*batch).item())
+    assert_close(loss, gold['loss'], 1e-4, 0, 'loss')
+    assert_close(opt.gnorm.reshape(()), gold['gnorm'], 1e-4, 0, 'gnorm')
+    for k, p in model.named_parameters():
+        err = (p.detach().double().cpu() - torch.as_tensor(gold['post/' + k]).double()).abs().max().item()
+        assert err <= 2e-5, (k, err)
+    l, v, a, labels, lm, vm, am, um = batch
+    model.eval()
+    with torch.no_grad():
+        out2 = model(l, v, a, lm, vm, am)
+    assert_close(out2, gold['logits2'], 1e-3, 1e-5, 'logits2')

