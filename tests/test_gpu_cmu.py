@@ -9,7 +9,7 @@ import pytest
 import torch
 
 from tests.golden import fixtures
-from tests.gpu_util import assert_close, cmu_model, cuda_batch
+from tests.gpu_util import assert_close, check_post_params, cmu_model, cuda_batch
 
 pytestmark = pytest.mark.gpu
 CMU = [n for n in fixtures.names('model') if fixtures.load(n)[0]['family'] == 'cmu']
@@ -55,11 +55,7 @@ def test_concat_trans_engine_step(name, graph, cuda):
     assert_close(losses[0], gold['loss'], 1e-4, 0, 'loss')
     if meta['steps'] == 1:
         assert_close(opt.gnorm.reshape(()), gold['gnorm'], 1e-4, 0, 'gnorm')
-    for k, p in model.named_parameters():
-        ref = gold['post/' + k] if meta['full'] else gold['posthead/' + k]
-        got = p.detach() if meta['full'] else p.detach().reshape(-1)[:256]
-        err = (got.double().cpu() - torch.as_tensor(ref).double()).abs().max().item()
-        assert err <= 2e-5, (k, err)
+    check_post_params(model, meta, gold)
     model.eval()
     with torch.no_grad():
         logits2 = model(*batch[:6])

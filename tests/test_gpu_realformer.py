@@ -5,7 +5,15 @@ and the full D=96/T=50 shape) and the whole State_Transfer step (P utterances th
 encoder, sigmoid/tanh gate recurrence, masked circle loss, clip, Adam).
 
 Tolerances as test_gpu_cmu.py: outputs rtol 1e-4, gradients rtol 1e-3 (floor 1e-5 x max|grad|),
-post-Adam parameters atol 2e-5.
+post-Adam parameters atol 2e-5 (gpu_util.check_post_params).
+
+State_Transfer outputs are compared on the real utterances (utterance mask 1).  The padding
+utterances (mask 0, features and key masks all zero) have every attention row fully masked: the
+reference evaluates softmax(s - 1e8), and s - 1e8 rounds to the fp32 grid of spacing 8 around
+-1e8, so those rows' weights are set by the last ulps of s (a summation-order artefact of the
+projections).  Their outputs are masked out of the loss and never feed a real utterance (the
+gate recurrence runs forward and padding is trailing), so loss, gradients and updates are
+unaffected; for them only finiteness is checked.
 """
 import contextlib
 
@@ -13,7 +21,7 @@ import pytest
 import torch
 
 from tests.golden import fixtures
-from tests.gpu_util import assert_close, load_params
+from tests.gpu_util import assert_close, check_post_params, load_params
 
 pytestmark = pytest.mark.gpu
 
@@ -73,6 +81,12 @@ def test_text_chain(name, cuda):
             assert p.grad is None or float(p.grad.abs().max()) == 0.0, k
 
 
+def _check_out(out, want, um, rtol, atol_frac):
+    real = um.bool().cpu()
+    assert torch.isfinite(out).all()
+    assert_close(out.detach().cpu()[real], torch.as_tensor(want)[real], rtol, atol_frac, 'out')
+
+
 def _state(meta, cuda):
     with ffn_const(meta) as rf:
         m = rf.State_Transfer(**meta['ctor'])
@@ -91,7 +105,7 @@ def test_state_transfer_autograd(cuda):
     model = _state(meta, cuda)
     l, v, a, labels, lm, vm, am, um = _batch(meta, cuda)
     out = model(l, v, a, lm, vm, am)
-    assert_close(out, gold['logits'], 1e-4, 1e-6, 'out')
+    _check_out(out, gold['logits'], um, 1e-4, 1e-6)
     loss = (rf.multi_circle_loss(out, labels) * um).mean()
     assert_close(loss.reshape(()), gold['loss'], 1e-4, 0, 'loss')
     loss.backward()
@@ -115,11 +129,9 @@ def test_state_transfer_engine_step(graph, cuda):
     loss = float(eng.step(*batch).item())
     assert_close(loss, gold['loss'], 1e-4, 0, 'loss')
     assert_close(opt.gnorm.reshape(()), gold['gnorm'], 1e-4, 0, 'gnorm')
-    for k, p in model.named_parameters():
-        err = (p.detach().double().cpu() - torch.as_tensor(gold['post/' + k]).double()).abs().max().item()
-        assert err <= 2e-5, (k, err)
+    check_post_params(model, meta, gold)
     l, v, a, labels, lm, vm, am, um = batch
     model.eval()
     with torch.no_grad():
         out2 = model(l, v, a, lm, vm, am)
-    assert_close(out2, gold['logits2'], 1e-3, 1e-5, 'logits2')
+    _check_out(out2, gold['logits2'], um, 1e-3, 1e-5)
