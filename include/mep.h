@@ -111,8 +111,15 @@ typedef struct {
 } mep_attn_desc;
 /* Launch geometry: one wave per (b, h, 64-query chunk) in the forward and per (b, h, 64-key
  * chunk) in the backward, 4 waves (256 threads) per workgroup; max_tiles =
- * max ceil(B * H * ceil(T / 64) / 4) over descriptors (T = Tq forward, Tk backward). */
-int mep_attn_fwd(const mep_attn_desc* descs, int n_desc, int max_tiles, int threads, mep_stream_t stream);
+ * max ceil(B * H * ceil(T / 64) / 4) over descriptors (T = Tq forward, Tk backward).
+ * flags select the specialised kernels: PREV = every descriptor has s_prev, SOUT = every
+ * descriptor has s_out (backward: ds_next); SHORT / LONG = descriptors with Tk <= 64 / Tk > 64
+ * are present (the forward launches one kernel per class present). */
+#define MEP_ATTN_PREV  1
+#define MEP_ATTN_SOUT  2
+#define MEP_ATTN_SHORT 4
+#define MEP_ATTN_LONG  8
+int mep_attn_fwd(const mep_attn_desc* descs, int n_desc, int max_tiles, int flags, mep_stream_t stream);
 
 /* Backward of the attention core.  Inputs dx (grad of X), the forward's q/k/v/x/stats/s_prev.
  * Outputs: dq += (written with accumulate semantics onto dq_base), dk, dv (dk==dv pointer ->
@@ -128,7 +135,7 @@ typedef struct {
     uint64_t ds_prev;   /* [B,H,Tq,Tk] or 0                        */
     uint64_t dc_partial;/* [B * ceil(Tk/64)] floats or 0           */
 } mep_attn_bwd_desc;
-int mep_attn_bwd(const mep_attn_bwd_desc* descs, int n_desc, int max_tiles, int threads, mep_stream_t stream);
+int mep_attn_bwd(const mep_attn_bwd_desc* descs, int n_desc, int max_tiles, int flags, mep_stream_t stream);
 
 /* ---------------------------------------------------------------- cmu / Ren-MME block epilogue
  * xp = drop(x @ Wp^T);  z = [q | xp] @ Wm^T;  out = drop(LayerNorm(z))

@@ -127,7 +127,7 @@ P = ctypes.c_void_p
 # name -> argtypes (all return int)
 GROUPED = ['mep_gemm', 'mep_wgrad', 'mep_wgrad_reduce', 'mep_layernorm_fwd', 'mep_layernorm_bwd', 'mep_colsum', 'mep_sum_rows',
            'mep_pool_fwd', 'mep_pool_bwd']
-GROUPED_T = ['mep_attn_fwd', 'mep_attn_bwd',      # + threads per workgroup
+GROUPED_T = ['mep_attn_fwd', 'mep_attn_bwd',      # + MEP_ATTN_* variant flags
              'mep_block_epi_fwd', 'mep_block_epi_bwd']  # + D (compiled variant)
 SIGNATURES = {name: [P, i32, i32, P] for name in GROUPED}
 SIGNATURES.update({name: [P, i32, i32, i32, P] for name in GROUPED_T})
@@ -216,8 +216,8 @@ class DescArray:
 
 
 def launch(name, descs, max_tiles, stream=None, threads=None, extra=()):
-    """threads: the extra int argument of the GROUPED_T launchers (threads or D); extra: the
-    extra ints of the GROUPED_T2 launchers (D, FD)."""
+    """threads: the extra int argument of the GROUPED_T launchers (attention variant flags, or the
+    epilogue width D); extra: the extra ints of the GROUPED_T2 launchers (D, FD)."""
     if descs.n == 0 or max_tiles <= 0:
         return
     fn = getattr(lib(), name)
@@ -230,14 +230,32 @@ def launch(name, descs, max_tiles, stream=None, threads=None, extra=()):
         TIMER.end(name)
 
 
-def attn_geometry(shapes):
-    """shapes: [(B, H, Tq, Tk)] -> (fwd tiles, bwd tiles, fwd threads, bwd threads) following the
-    launch rule of csrc/attn.hip: one wave per (b, h, 64-row chunk), 4 waves per workgroup."""
+ATTN_PREV, ATTN_SOUT, ATTN_SHORT, ATTN_LONG = 1, 2, 4, 8   # MEP_ATTN_* (include/mep.h)
+
+
+def _uniform(flags, what):
+    if any(flags) and not all(flags):
+        raise ValueError('mep_attn: %s must be set for every descriptor of a launch or for none' % what)
+    return bool(flags and flags[0])
+
+
+def attn_geometry(descs):
+    """AttnDesc list of one launch -> (fwd tiles, bwd tiles, fwd flags) following csrc/attn.hip:
+    one wave per (b, h, 64-row chunk), 4 waves per workgroup; flags = MEP_ATTN_* of the launch."""
     ft = bt = 0
-    for (B, H, Tq, Tk) in shapes:
-        ft = max(ft, -(-(B * H * -(-Tq // 64)) // 4))
-        bt = max(bt, -(-(B * H * -(-Tk // 64)) // 4))
-    return ft, bt, 256, 256
+    for d in descs:
+        ft = max(ft, -(-(d.B * d.H * -(-d.Tq // 64)) // 4))
+        bt = max(bt, -(-(d.B * d.H * -(-d.Tk // 64)) // 4))
+    flags = (ATTN_PREV if _uniform([d.s_prev != 0 for d in descs], 's_prev') else 0) | \
+            (ATTN_SOUT if _uniform([d.s_out != 0 for d in descs], 's_out') else 0) | \
+            (ATTN_SHORT if any(d.Tk <= 64 for d in descs) else 0) | (ATTN_LONG if any(d.Tk > 64 for d in descs) else 0)
+    return ft, bt, flags
+
+
+def attn_bwd_flags(bdescs):
+    """AttnBwdDesc list of one launch -> MEP_ATTN_PREV | MEP_ATTN_SOUT (= ds_next present)"""
+    return (ATTN_PREV if _uniform([b.f.s_prev != 0 for b in bdescs], 's_prev') else 0) | \
+           (ATTN_SOUT if _uniform([b.ds_next != 0 for b in bdescs], 'ds_next') else 0)
 
 
 def attn_dc_slots(B, H, Tk):

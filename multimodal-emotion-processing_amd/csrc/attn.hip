@@ -44,18 +44,6 @@ MEP_DEV floatx4 mfma16(float a, float b, floatx4 c) {
 }
 MEP_DEV floatx4 zero4() { return floatx4{0.f, 0.f, 0.f, 0.f}; }
 
-struct Score {
-    bool has_prev;
-    float c;
-};
-
-// s = dot * 0.25 [+ c*sp]  - 1e8 * (1 - m)      (op order of cmu-mosei/run.py:244-253)
-MEP_DEV float score(float dot, const Score& sc, float sp, float m) {
-    float s = mul_rn(dot, INV_SCALE);
-    if (sc.has_prev) s = add_rn(s, mul_rn(sc.c, sp));
-    return sub_rn(s, mul_rn(1.0e8f, sub_rn(1.0f, m)));
-}
-
 MEP_DEV bool aligned16(const mep_rows& r) {
     return ((r.ptr & 15) == 0) && (r.sB % 4 == 0) && (r.sT % 4 == 0);
 }
@@ -79,20 +67,32 @@ MEP_DEV float load1(const gfloat* base, int sT, int t, int n, int col) {
     return ok ? x : 0.f;
 }
 
+// per-key mask term of the score: 1e8 * (1 - mask) (cmu-mosei/run.py:253), +inf for padding keys
+// beyond Tk so that s - term = -inf and exp() = 0 without any per-score select
+MEP_DEV float mask_term(const gfloat* mask, int k, int Tk) {
+    const float m = mask[min(k, Tk - 1)];
+    return k < Tk ? mul_rn(1.0e8f, sub_rn(1.0f, m)) : INFINITY;
+}
+
 MEP_DEV float shfl(float v, int src) { return __shfl(v, src, 64); }
 
-__global__ __launch_bounds__(THREADS) void k_attn_fwd(const mep_attn_desc* __restrict__ descs) {
-    const mep_attn_desc& d = descs[blockIdx.y];
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+// s = dot * 0.25 [+ c*sp] - 1e8 * (1 - m)      (op order of cmu-mosei/run.py:244-253)
+template <bool PREV>
+MEP_DEV float score(float dot, float c, float sp, float mt) {
+    float s = mul_rn(dot, INV_SCALE);
+    if (PREV) s = add_rn(s, mul_rn(c, sp));
+    return sub_rn(s, mt);
+}
+
+// One forward task: batch row b, head h, 64 queries.  PREV: residual scores in; SOUT: post-mask
+// scores out; SINGLE: Tk <= 64 (one key chunk: exact two-pass softmax, each query tile is
+// finalised right after its P.V, so no running O/max/sum state stays live).
+template <bool PREV, bool SOUT, bool SINGLE>
+MEP_DEV void attn_fwd_task(const mep_attn_desc& d, int qc, int h, int b, int lane) {
     const int c = lane & 15, g = lane >> 4;
-    const int nqc = (d.Tq + CH - 1) / CH;
-    const int task = blockIdx.x * WAVES + wave;
-    if (task >= d.B * d.H * nqc) return;   // whole wave leaves; no barriers below
-    const int qc = task % nqc, bh = task / nqc;
-    const int h = bh % d.H, b = bh / d.H;
     const int hc = h * HD;
     const int Tq = d.Tq, Tk = d.Tk;
-    const Score sc{d.s_prev != 0, d.s_prev ? *G<const float>(d.c) : 0.f};
+    const float cres = PREV ? *G<const float>(d.c) : 0.f;
     const gfloat* sprev = G<const float>(d.s_prev);
     gfloat* sout = G<float>(d.s_out);
     const gfloat* mask = G<const float>(d.mask) + (int64_t)b * d.mask_sB;
@@ -102,22 +102,38 @@ __global__ __launch_bounds__(THREADS) void k_attn_fwd(const mep_attn_desc* __res
     const int qsT = (int)d.q.sT, ksT = (int)d.k.sT, vsT = (int)d.v.sT;
     const bool qv = aligned16(d.q), kv4 = aligned16(d.k);
     const int sbase = (b * d.H + h) * Tq;        // row of (b, h, query 0) in [B,H,Tq,Tk]
-
-    // B operand of S^T = K Q^T: lane (query c, group g), dims 4g..4g+3 of 4 query tiles
-    float qf[NT][4];
     const int q_lo = qc * CH;
     const int nqt = min(NT, (Tq - q_lo + 15) / 16);
-#pragma unroll
-    for (int qt = 0; qt < NT; ++qt) load4(qf[qt], Qb, qsT, q_lo + qt * 16 + c, Tq, hc + 4 * g, qv);
+    gfloat* stats = G<float>(d.stats);
+    gfloat* Xb = bat(d.x, b);
+    const int xsT = (int)d.x.sT;
 
-    floatx4 o[NT];
-    float m[NT], l[NT];
+    floatx4 o[SINGLE ? 1 : NT];
+    float m[SINGLE ? 1 : NT], l[SINGLE ? 1 : NT];
+    if (!SINGLE) {
 #pragma unroll
-    for (int qt = 0; qt < NT; ++qt) { o[qt] = zero4(); m[qt] = -FLT_MAX; l[qt] = 0.f; }
+        for (int qt = 0; qt < NT; ++qt) { o[qt] = zero4(); m[qt] = -FLT_MAX; l[qt] = 0.f; }
+    }
+    auto finish = [&](int qt, const floatx4& oq, float mq, float lq) {
+        float lt = lq + shfl(lq, lane ^ 16);
+        lt += shfl(lt, lane ^ 32);
+        const float inv = 1.0f / lt;
+        const int q = q_lo + qt * 16 + c;
+        if (g == 0 && q < Tq) {
+            stats[2 * (sbase + q)] = mq;
+            stats[2 * (sbase + q) + 1] = inv;
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const float ir = shfl(inv, 4 * g + r);
+            const int qq = q_lo + qt * 16 + 4 * g + r;
+            if (qq < Tq) Xb[qq * xsT + hc + c] = oq[r] * ir;
+        }
+    };
 
     for (int k_lo = 0; k_lo < Tk; k_lo += CH) {
         // operands of the 4 key tiles of this chunk
-        float kf[NT][4], vf[NT][4], mk[NT][4];
+        float kf[NT][4], vf[NT][4], mt[NT][4];
 #pragma unroll
         for (int kt = 0; kt < NT; ++kt) {
             const int k0 = k_lo + kt * 16;
@@ -126,38 +142,42 @@ __global__ __launch_bounds__(THREADS) void k_attn_fwd(const mep_attn_desc* __res
             for (int s = 0; s < 4; ++s) {                                  // B of P.V: V[k0+4g+s][c]
                 const int kk = k0 + 4 * g + s;
                 vf[kt][s] = load1(Vb, vsT, kk, Tk, hc + c);
-                const float mv = mask[min(kk, Tk - 1)];
-                mk[kt][s] = kk < Tk ? mv : 0.f;
+                mt[kt][s] = mask_term(mask, kk, Tk);
             }
         }
 #pragma unroll
         for (int qt = 0; qt < NT; ++qt) {
             if (qt >= nqt) break;
             const int q = q_lo + qt * 16 + c;
-            const bool qok = q < Tq;
-            const int srow = (sbase + (qok ? q : Tq - 1)) * Tk;
+            float qf[4];                                                   // B of S^T: Q[q][4g+s]
+            load4(qf, Qb, qsT, q, Tq, hc + 4 * g, qv);
+            const int srow = (sbase + min(q, Tq - 1)) * Tk;
             float sv[NT][4];
             float mx = -INFINITY;
 #pragma unroll
             for (int kt = 0; kt < NT; ++kt) {
                 floatx4 st = zero4();
 #pragma unroll
-                for (int s = 0; s < 4; ++s) st = mfma16(kf[kt][s], qf[qt][s], st);   // C[key 4g+r][query c]
+                for (int s = 0; s < 4; ++s) st = mfma16(kf[kt][s], qf[s], st);   // C[key 4g+r][query c]
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
+                    float spv = 0.f;
                     const int kk = k_lo + kt * 16 + 4 * g + r;
-                    const bool ok = kk < Tk;
-                    const int si = srow + (ok ? kk : Tk - 1);
-                    const float spv = sc.has_prev ? sprev[si] : 0.f;
-                    const float v = score(st[r], sc, spv, mk[kt][r]);
-                    if (sout && ok && qok) sout[si] = v;
-                    sv[kt][r] = ok ? v : -INFINITY;
+                    if (PREV || SOUT) {
+                        const int si = srow + min(kk, Tk - 1);
+                        if (PREV) spv = sprev[si];
+                        const float v = score<PREV>(st[r], cres, spv, mt[kt][r]);
+                        if (SOUT && kk < Tk && q < Tq) sout[si] = v;
+                        sv[kt][r] = v;
+                    } else {
+                        sv[kt][r] = score<false>(st[r], 0.f, 0.f, mt[kt][r]);
+                    }
                     mx = fmaxf(mx, sv[kt][r]);
                 }
             }
             mx = fmaxf(mx, shfl(mx, lane ^ 16));
             mx = fmaxf(mx, shfl(mx, lane ^ 32));
-            const float mnew = fmaxf(m[qt], mx);
+            const float mnew = SINGLE ? mx : fmaxf(m[qt], mx);
             float lsum = 0.f;
 #pragma unroll
             for (int kt = 0; kt < NT; ++kt)
@@ -166,41 +186,45 @@ __global__ __launch_bounds__(THREADS) void k_attn_fwd(const mep_attn_desc* __res
                     sv[kt][r] = __expf(sv[kt][r] - mnew);
                     lsum += sv[kt][r];
                 }
-            if (k_lo > 0) {   // rescale the running state (never taken when Tk <= 64)
+            floatx4 oq = SINGLE ? zero4() : o[qt];
+            if (!SINGLE && k_lo > 0) {   // rescale the running state
                 const float corr = __expf(m[qt] - mnew);
                 l[qt] *= corr;
 #pragma unroll
-                for (int r = 0; r < 4; ++r) o[qt][r] *= shfl(corr, 4 * g + r);  // O row 4g+r <- query 4g+r
+                for (int r = 0; r < 4; ++r) oq[r] *= shfl(corr, 4 * g + r);  // O row 4g+r <- query 4g+r
             }
-            l[qt] += lsum;
-            m[qt] = mnew;
 #pragma unroll
             for (int kt = 0; kt < NT; ++kt)
 #pragma unroll
-                for (int s = 0; s < 4; ++s) o[qt] = mfma16(sv[kt][s], vf[kt][s], o[qt]);  // C[query 4g+r][dim c]
+                for (int s = 0; s < 4; ++s) oq = mfma16(sv[kt][s], vf[kt][s], oq);  // C[query 4g+r][dim c]
+            if (SINGLE) {
+                finish(qt, oq, mnew, lsum);
+            } else {
+                o[qt] = oq;
+                l[qt] += lsum;
+                m[qt] = mnew;
+            }
         }
     }
-    gfloat* stats = G<float>(d.stats);
-    gfloat* Xb = bat(d.x, b);
-    const int xsT = (int)d.x.sT;
+    if (!SINGLE) {
 #pragma unroll
-    for (int qt = 0; qt < NT; ++qt) {
-        if (qt >= nqt) break;
-        float lt = l[qt] + shfl(l[qt], lane ^ 16);
-        lt += shfl(lt, lane ^ 32);
-        const float inv = 1.0f / lt;
-        const int q = q_lo + qt * 16 + c;
-        if (g == 0 && q < Tq) {
-            stats[2 * (sbase + q)] = m[qt];
-            stats[2 * (sbase + q) + 1] = inv;
-        }
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const float ir = shfl(inv, 4 * g + r);
-            const int qq = q_lo + qt * 16 + 4 * g + r;
-            if (qq < Tq) Xb[qq * xsT + hc + c] = o[qt][r] * ir;
+        for (int qt = 0; qt < NT; ++qt) {
+            if (qt >= nqt) break;
+            finish(qt, o[qt], m[qt], l[qt]);
         }
     }
+}
+
+template <bool PREV, bool SOUT, bool SINGLE>
+__global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu((SINGLE && !PREV) ? 5 : 1))) void k_attn_fwd(const mep_attn_desc* __restrict__ descs) {
+    const mep_attn_desc& d = descs[blockIdx.y];
+    if ((d.Tk <= CH) != SINGLE) return;    // the other variant's descriptor
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int nqc = (d.Tq + CH - 1) / CH;
+    const int task = blockIdx.x * WAVES + wave;
+    if (task >= d.B * d.H * nqc) return;   // whole wave leaves; no barriers below
+    const int qc = task % nqc, bh = task / nqc;
+    attn_fwd_task<PREV, SOUT, SINGLE>(d, qc, bh % d.H, bh / d.H, lane);
 }
 
 MEP_DEV void wave_lds_sync() {
@@ -209,20 +233,15 @@ MEP_DEV void wave_lds_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-__global__ __launch_bounds__(THREADS) void k_attn_bwd(const mep_attn_bwd_desc* __restrict__ descs) {
-    const mep_attn_bwd_desc& bd = descs[blockIdx.y];
+// One backward task: batch row b, head h, 64 keys.  PREV: residual scores (writes dS_prev and the
+// dc partial); DSN: a gradient arrives on this layer's post-mask S output.
+template <bool PREV, bool DSN>
+MEP_DEV void attn_bwd_task(const mep_attn_bwd_desc& bd, int task, int kc, int nkc, int h, int b, int lane, float* T) {
     const mep_attn_desc& d = bd.f;
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int c = lane & 15, g = lane >> 4;
-    const int nkc = (d.Tk + CH - 1) / CH;
-    const int task = blockIdx.x * WAVES + wave;
-    __shared__ __attribute__((aligned(16))) float Tr[WAVES][16 * TLD];
-    if (task >= d.B * d.H * nkc) return;   // whole wave leaves; only wave-private LDS below
-    const int kc = task % nkc, bh = task / nkc;
-    const int h = bh % d.H, b = bh / d.H;
     const int hc = h * HD;
     const int Tq = d.Tq, Tk = d.Tk;
-    const Score sc{d.s_prev != 0, d.s_prev ? *G<const float>(d.c) : 0.f};
+    const float cres = PREV ? *G<const float>(d.c) : 0.f;
     const gfloat* sprev = G<const float>(d.s_prev);
     const gfloat* dsn = G<const float>(bd.ds_next);
     gfloat* dsp = G<float>(bd.ds_prev);
@@ -236,20 +255,20 @@ __global__ __launch_bounds__(THREADS) void k_attn_bwd(const mep_attn_bwd_desc* _
     const int qsT = (int)d.q.sT, ksT = (int)d.k.sT, vsT = (int)d.v.sT, osT = (int)d.x.sT, gsT = (int)bd.dx.sT;
     const int sbase = (b * d.H + h) * Tq;
     const bool qv = aligned16(d.q), kv4 = aligned16(d.k), vv4 = aligned16(d.v), gv = aligned16(bd.dx);
-    float* T = Tr[wave];
+    gfloat* dQb = bat(bd.dq, b);
+    const int dqsT = (int)bd.dq.sT;
 
     const int k_lo = kc * CH;
-    // per key tile: B operands of S (K) and dP (V) with the key on the lane, the key mask, and
-    // the B operand of dQ (K rows 4g+s, dim c); dK / dV accumulators (C[key 4g+r][dim c])
-    float kb[NT][4], vb[NT][4], kq[NT][4], mkey[NT];
+    // per key tile: B operands of S (K) and dP (V) with the key on the lane, the key's mask term,
+    // and the B operand of dQ (K rows 4g+s, dim c); dK / dV accumulators (C[key 4g+r][dim c])
+    float kb[NT][4], vb[NT][4], kq[NT][4], mtk[NT];
     floatx4 dk[NT], dv[NT];
 #pragma unroll
     for (int kt = 0; kt < NT; ++kt) {
         const int k0 = k_lo + kt * 16;
         load4(kb[kt], Kb, ksT, k0 + c, Tk, hc + 4 * g, kv4);
         load4(vb[kt], Vb, vsT, k0 + c, Tk, hc + 4 * g, vv4);
-        const float mv = mask[min(k0 + c, Tk - 1)];
-        mkey[kt] = (k0 + c < Tk) ? mv : 0.f;
+        mtk[kt] = mask_term(mask, k0 + c, Tk);
 #pragma unroll
         for (int s = 0; s < 4; ++s) kq[kt][s] = load1(Kb, ksT, k0 + 4 * g + s, Tk, hc + c);
         dk[kt] = zero4();
@@ -265,25 +284,25 @@ __global__ __launch_bounds__(THREADS) void k_attn_bwd(const mep_attn_bwd_desc* _
 #pragma unroll
         for (int s = 0; s < 4; ++s) {                           // B of dV / dK: rows 4g+s, dim c
             const int qq = q0 + 4 * g + s;
-            const bool ok = qq < Tq;
-            const int qcl = ok ? qq : Tq - 1;
+            const int qcl = min(qq, Tq - 1);
             db[s] = load1(Gb, gsT, qq, Tq, hc + c);
             qb[s] = load1(Qb, qsT, qq, Tq, hc + c);
-            float pr = db[s] * load1(Ob, osT, qq, Tq, hc + c);  // delta = rowsum(dO * O)
+            float pr = db[s] * Ob[qcl * osT + hc + c];          // delta = rowsum(dO * O)
             pr += shfl(pr, lane ^ 1);
             pr += shfl(pr, lane ^ 2);
             pr += shfl(pr, lane ^ 4);
             pr += shfl(pr, lane ^ 8);
             del[s] = pr;
+            // padded queries: max = +inf, 1/sum = 0 make P = exp(-inf) * 0 = 0 (and with it dS)
+            const bool qok = qq < Tq;
             const float m0 = stats[2 * (sbase + qcl)], l0 = stats[2 * (sbase + qcl) + 1];
-            mm[s] = ok ? m0 : 0.f;
-            li[s] = ok ? l0 : 0.f;
+            mm[s] = qok ? m0 : INFINITY;
+            li[s] = qok ? l0 : 0.f;
         }
         float ds[NT][4];
 #pragma unroll
         for (int kt = 0; kt < NT; ++kt) {
             const int kk = k_lo + kt * 16 + c;
-            const bool kok = kk < Tk;
             floatx4 st = zero4(), dp = zero4();
 #pragma unroll
             for (int s = 0; s < 4; ++s) st = mfma16(qa[s], kb[kt][s], st);   // C[query 4g+r][key c]
@@ -293,17 +312,22 @@ __global__ __launch_bounds__(THREADS) void k_attn_bwd(const mep_attn_bwd_desc* _
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const int qq = q0 + 4 * g + r;
-                const bool ok = (qq < Tq) && kok;
-                const int si = (sbase + (qq < Tq ? qq : Tq - 1)) * Tk + (kok ? kk : Tk - 1);
-                const float spv = sc.has_prev ? sprev[si] : 0.f;
-                const float sv = score(st[r], sc, spv, mkey[kt]);
-                const float pv = ok ? __expf(sv - mm[r]) * li[r] : 0.f;
+                float spv = 0.f;
+                int si = 0;
+                if (PREV || DSN) {
+                    si = (sbase + min(qq, Tq - 1)) * Tk + min(kk, Tk - 1);
+                    if (PREV) spv = sprev[si];
+                }
+                const float sv = score<PREV>(st[r], cres, spv, mtk[kt]);
+                const float pv = __expf(sv - mm[r]) * li[r];
                 float gsv = pv * (dp[r] - del[r]);
-                if (dsn) gsv += dsn[si];
-                gsv = ok ? gsv : 0.f;
-                if (sc.has_prev) {
-                    if (dsp && ok) dsp[si] = sc.c * gsv;
-                    dc_acc = fmaf(gsv, spv, dc_acc);
+                if (DSN || PREV) {
+                    const bool ok = (qq < Tq) && (kk < Tk);
+                    if (DSN) gsv += ok ? dsn[si] : 0.f;
+                    if (PREV) {
+                        if (ok) dsp[si] = cres * gsv;
+                        dc_acc = fmaf(gsv, spv, dc_acc);
+                    }
                 }
                 p[r] = pv;
                 ds[kt][r] = gsv;
@@ -329,8 +353,6 @@ __global__ __launch_bounds__(THREADS) void k_attn_bwd(const mep_attn_bwd_desc* _
         }
         wave_lds_sync();
         // dq rows q0+4g+r, dim c (exclusive owner when the keys fit one chunk; else atomics)
-        gfloat* dQb = bat(bd.dq, b);
-        const int dqsT = (int)bd.dq.sT;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             const int qq = q0 + 4 * g + r;
@@ -359,28 +381,62 @@ __global__ __launch_bounds__(THREADS) void k_attn_bwd(const mep_attn_bwd_desc* _
             }
         }
     }
-    if (bd.dc_partial) {
+    if (PREV && bd.dc_partial) {
         const float w = wave_sum(dc_acc);
         if (lane == 0) G<float>(bd.dc_partial)[task] = w;
     }
+}
+
+template <bool PREV, bool DSN>
+__global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu((PREV || DSN) ? 1 : 3))) void k_attn_bwd(const mep_attn_bwd_desc* __restrict__ descs) {
+    const mep_attn_bwd_desc& bd = descs[blockIdx.y];
+    const mep_attn_desc& d = bd.f;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int nkc = (d.Tk + CH - 1) / CH;
+    const int task = blockIdx.x * WAVES + wave;
+    __shared__ __attribute__((aligned(16))) float Tr[WAVES][16 * TLD];
+    if (task >= d.B * d.H * nkc) return;   // whole wave leaves; only wave-private LDS below
+    const int kc = task % nkc, bh = task / nkc;
+    attn_bwd_task<PREV, DSN>(bd, task, kc, nkc, bh % d.H, bh / d.H, lane, Tr[wave]);
 }
 
 }  // namespace
 
 // Launch geometry: 256 threads (4 waves, one task each); tasks = B * H * ceil(Tq/64) forward,
 // B * H * ceil(Tk/64) backward; max_tiles = ceil(max tasks / 4).  dc_partial (backward) has one
-// float per task, task = (b*H + h) * ceil(Tk/64) + key chunk.
-extern "C" int mep_attn_fwd(const mep_attn_desc* descs, int n_desc, int max_tiles, int threads, mep_stream_t stream) {
+// float per task, task = (b*H + h) * ceil(Tk/64) + key chunk.  `flags` (MEP_ATTN_*) select the
+// compiled variants: PREV / SOUT (DSN) must hold for every descriptor of the launch; SHORT / LONG
+// say whether descriptors with Tk <= 64 / Tk > 64 are present (one kernel launch per class).
+extern "C" int mep_attn_fwd(const mep_attn_desc* descs, int n_desc, int max_tiles, int flags, mep_stream_t stream) {
     if (n_desc <= 0 || max_tiles <= 0) return 0;
-    if (threads != THREADS) { mep_set_error("mep_attn_fwd: threads must be 256"); return MEP_EINVAL; }
-    hipLaunchKernelGGL(k_attn_fwd, dim3(max_tiles, n_desc), dim3(THREADS), 0, (hipStream_t)stream, descs);
+    if (!(flags & (MEP_ATTN_SHORT | MEP_ATTN_LONG))) { mep_set_error("mep_attn_fwd: flags need SHORT and/or LONG"); return MEP_EINVAL; }
+    const bool prev = flags & MEP_ATTN_PREV, sout = flags & MEP_ATTN_SOUT;
+    const dim3 grid(max_tiles, n_desc), block(THREADS);
+    hipStream_t st = (hipStream_t)stream;
+#define MEP_FWD(P, S, SI) hipLaunchKernelGGL((k_attn_fwd<P, S, SI>), grid, block, 0, st, descs)
+    for (int single = 1; single >= 0; --single) {
+        if (!(flags & (single ? MEP_ATTN_SHORT : MEP_ATTN_LONG))) continue;
+        if (single) {
+            if (prev) { if (sout) MEP_FWD(true, true, true); else MEP_FWD(true, false, true); }
+            else      { if (sout) MEP_FWD(false, true, true); else MEP_FWD(false, false, true); }
+        } else {
+            if (prev) { if (sout) MEP_FWD(true, true, false); else MEP_FWD(true, false, false); }
+            else      { if (sout) MEP_FWD(false, true, false); else MEP_FWD(false, false, false); }
+        }
+    }
+#undef MEP_FWD
     return mep_check_launch("mep_attn_fwd");
 }
 
-extern "C" int mep_attn_bwd(const mep_attn_bwd_desc* descs, int n_desc, int max_tiles, int threads,
+extern "C" int mep_attn_bwd(const mep_attn_bwd_desc* descs, int n_desc, int max_tiles, int flags,
                             mep_stream_t stream) {
     if (n_desc <= 0 || max_tiles <= 0) return 0;
-    if (threads != THREADS) { mep_set_error("mep_attn_bwd: threads must be 256"); return MEP_EINVAL; }
-    hipLaunchKernelGGL(k_attn_bwd, dim3(max_tiles, n_desc), dim3(THREADS), 0, (hipStream_t)stream, descs);
+    const bool prev = flags & MEP_ATTN_PREV, dsn = flags & MEP_ATTN_SOUT;
+    const dim3 grid(max_tiles, n_desc), block(THREADS);
+    hipStream_t st = (hipStream_t)stream;
+    if (prev) { if (dsn) hipLaunchKernelGGL((k_attn_bwd<true, true>), grid, block, 0, st, descs);
+                else hipLaunchKernelGGL((k_attn_bwd<true, false>), grid, block, 0, st, descs); }
+    else      { if (dsn) hipLaunchKernelGGL((k_attn_bwd<false, true>), grid, block, 0, st, descs);
+                else hipLaunchKernelGGL((k_attn_bwd<false, false>), grid, block, 0, st, descs); }
     return mep_check_launch("mep_attn_bwd");
 }

@@ -270,19 +270,24 @@ class RealformerPlan:
         self.t_proj = max(cdiv(b['nk'], 64) for b in self.blocks)
         self.d_q, self.d_attn, self.d_epi, self.t_attn, self.t_epi = [], [], [], [], []
         self.d_epib, self.d_attnb, self.t_attnb, self.d_ingrad = [], [], [], []
+        self.f_attn, self.f_attnb = [], []
         for i in range(nl):
             layer = [b for b in self.blocks if b['i'] == i]
             self.d_q.append(DescArray(GemmDesc, [
                 GemmDesc(x=self._q_rows(b), y=crows(b['QP'], b['Tq'], D), w=fl.ptr(b['pre'] + 'w_qkv.0.weight'),
                          ntok=b['nq'], N=D, K=D, ldw=D, w_nt=1, **gemm) for b in layer] if i > 0 else [], dev))
-            self.d_attn.append(DescArray(AttnDesc, [self._attn_desc(b) for b in layer], dev))
+            ad = [self._attn_desc(b) for b in layer]
+            self.d_attn.append(DescArray(AttnDesc, ad, dev))
             self.d_epi.append(DescArray(RfEpiDesc, [self._epi_desc(b) for b in layer], dev))
-            geo = _lib.attn_geometry([(R, H, b['Tq'], b['Tk']) for b in layer])
+            geo = _lib.attn_geometry(ad)
             self.t_attn.append(geo[0])
             self.t_attnb.append(geo[1])
+            self.f_attn.append(geo[2])
             self.t_epi.append(max(cdiv(b['nq'], 64) for b in layer))
             self.d_epib.append(DescArray(RfEpiBwdDesc, [self._epi_bwd_desc(b) for b in layer], dev))
-            self.d_attnb.append(DescArray(AttnBwdDesc, [self._attn_bwd_desc(b) for b in layer], dev))
+            ab = [self._attn_bwd_desc(b) for b in layer]
+            self.d_attnb.append(DescArray(AttnBwdDesc, ab, dev))
+            self.f_attnb.append(_lib.attn_bwd_flags(ab))
             ig = []
             for b in layer:
                 # dq_in += dQP W_q  (onto the residual dz1 the epilogue backward wrote)
@@ -425,7 +430,7 @@ class RealformerPlan:
         for i in range(nl):
             if i > 0:
                 launch('mep_gemm', self.d_q[i], self.t_epi[i], stream)
-            launch('mep_attn_fwd', self.d_attn[i], self.t_attn[i], stream, threads=256)
+            launch('mep_attn_fwd', self.d_attn[i], self.t_attn[i], stream, threads=self.f_attn[i])
             launch('mep_rf_epi_fwd', self.d_epi[i], self.t_epi[i], stream, extra=ex)
         if sp.head:
             launch('mep_pool_fwd', self.d_pool, self.t_pool, stream)
@@ -452,7 +457,7 @@ class RealformerPlan:
         self.dQP_all.zero_()
         for i in reversed(range(nl)):
             launch('mep_rf_epi_bwd', self.d_epib[i], self.t_epi[i], stream, extra=ex)
-            launch('mep_attn_bwd', self.d_attnb[i], self.t_attnb[i], stream, threads=256)
+            launch('mep_attn_bwd', self.d_attnb[i], self.t_attnb[i], stream, threads=self.f_attnb[i])
             launch('mep_gemm', self.d_ingrad[i], self.t_ingrad, stream)
         launch('mep_sum_rows', self.d_sum, self.t_sum, stream)
         launch('mep_wgrad', self.d_wgrad, self.t_wgrad, stream)

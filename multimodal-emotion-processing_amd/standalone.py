@@ -48,7 +48,7 @@ class _BlockFn(torch.autograd.Function):
                      ln_b=lnb.data_ptr(), stats=estat.data_ptr(), seed=0, ntok=B * Tq, D=D, drop_p=0.0,
                      drop_stream=0)
         a_arr, e_arr = DescArray(AttnDesc, [ad], dev), DescArray(EpiDesc, [ed], dev)
-        geo = _lib.attn_geometry([(B, H, Tq, Tk)])
+        geo = _lib.attn_geometry([ad])
         launch('mep_attn_fwd', a_arr, geo[0], threads=geo[2])
         launch('mep_block_epi_fwd', e_arr, cdiv(B * Tq, 64), threads=D)
         ctx.save_for_backward(q, k, v, mask, X, XP, Z, S, astat, estat, c, wp, wm, lnw, lnb)
@@ -81,8 +81,8 @@ class _BlockFn(torch.autograd.Function):
                          ds_prev=dSp.data_ptr() if has_prev else 0,
                          dc_partial=dc_part.data_ptr() if has_prev else 0)
         launch('mep_block_epi_bwd', DescArray(EpiBwdDesc, [eb], dev), cdiv(B * Tq, 64), threads=D)
-        geo = _lib.attn_geometry([(B, H, Tq, Tk)])
-        launch('mep_attn_bwd', DescArray(AttnBwdDesc, [ab], dev), geo[1], threads=geo[3])
+        geo = _lib.attn_geometry([ad])
+        launch('mep_attn_bwd', DescArray(AttnBwdDesc, [ab], dev), geo[1], threads=_lib.attn_bwd_flags([ab]))
         gwp, gwm = torch.empty_like(wp), torch.empty_like(wm)
         glw, glb, gc = torch.empty_like(lnw), torch.empty_like(lnb), torch.empty_like(c)
         n = B * Tq
@@ -249,7 +249,7 @@ class _RFBlockFn(torch.autograd.Function):
                             w1=w1.data_ptr(), b1=b1.data_ptr(), w2=w2.data_ptr(), b2=b2.data_ptr(),
                             ln1_w=n1w.data_ptr(), ln1_b=n1b.data_ptr(), ln2_w=n2w.data_ptr(), ln2_b=n2b.data_ptr(),
                             a=a.data_ptr(), b=b.data_ptr(), stats=estat.data_ptr(), ntok=B * Tq, D=D, FD=FD)
-        geo = _lib.attn_geometry([(B, H, Tq, Tk)])
+        geo = _lib.attn_geometry([ad])
         launch('mep_attn_fwd', DescArray(AttnDesc, [ad], dev), geo[0], threads=geo[2])
         launch('mep_rf_epi_fwd', DescArray(_lib.RfEpiDesc, [ed], dev), cdiv(B * Tq, 64), extra=(D, FD))
         ctx.save_for_backward(q, k, v, mask, QP, KV, X, XP, Hh, F1, F, S, astat, estat,
@@ -289,8 +289,8 @@ class _RFBlockFn(torch.autograd.Function):
                          ds_next=dS.data_ptr() if dS is not None else 0, ds_prev=dSp.data_ptr() if has_prev else 0,
                          dc_partial=dc_part.data_ptr() if has_prev else 0)
         launch('mep_rf_epi_bwd', DescArray(_lib.RfEpiBwdDesc, [eb], dev), nt, extra=(D, FD))
-        geo = _lib.attn_geometry([(B, H, Tq, Tk)])
-        launch('mep_attn_bwd', DescArray(AttnBwdDesc, [ab], dev), geo[1], threads=geo[3])
+        geo = _lib.attn_geometry([ad])
+        launch('mep_attn_bwd', DescArray(AttnBwdDesc, [ab], dev), geo[1], threads=_lib.attn_bwd_flags([ab]))
         g = dict(bias=0, table=0, relu=0, alpha=1.0, w_nt=0, K=D, ldw=D, N=D)
         gd = [GemmDesc(x=crows(dQP, Tq, D), y=crows(dQin, Tq, D), w=wq.data_ptr(), ntok=B * Tq, accumulate=1, **g),
               GemmDesc(x=kv(dKV2, 0), y=crows(dk_in, Tk, D), w=wk.data_ptr(), ntok=B * Tk, accumulate=0, **g),

@@ -229,7 +229,7 @@ class TriModalPlan:
                 ed.append(self._epi_desc(blk))
             self.d_attn.append(DescArray(AttnDesc, ad, dev))
             self.d_epi.append(DescArray(EpiDesc, ed, dev))
-            geo = _lib.attn_geometry([(B, H, b['Tq'], b['Tk']) for b in self.blocks if b['i'] == i])
+            geo = _lib.attn_geometry(ad)
             self.t_attn.append(geo[0])
             self.g_attn.append(geo)
             self.t_epi.append(max(cdiv(B * b['Tq'], 64) for b in self.blocks))
@@ -252,7 +252,7 @@ class TriModalPlan:
             partial=self.head_partial.data_ptr(), B=B, F=self.F, NC=NC,
             labels_are_float=int(self.labels_float), rdrop=0, compute_grad=1, loss_scale=1.0 / B, ext_dlogits=0)
         # backward per layer
-        self.d_epib, self.d_attnb, self.t_attnb = [], [], []
+        self.d_epib, self.d_attnb, self.t_attnb, self.f_attnb = [], [], [], []
         for i in range(nl):
             eb, ab = [], []
             for blk in (b for b in self.blocks if b['i'] == i):
@@ -261,6 +261,7 @@ class TriModalPlan:
             self.d_epib.append(DescArray(EpiBwdDesc, eb, dev))
             self.d_attnb.append(DescArray(AttnBwdDesc, ab, dev))
             self.t_attnb.append(self.g_attn[i][1])
+            self.f_attnb.append(_lib.attn_bwd_flags(ab))
         # per-modality gradient sums
         sd = []
         self.dU = {}
@@ -446,7 +447,7 @@ class TriModalPlan:
         launch("mep_pool_bwd", self.d_pool, self.t_poolb, stream)
         for i in reversed(range(nl)):
             launch('mep_block_epi_bwd', self.d_epib[i], self.t_epi[i], stream, threads=sp.D)
-            launch('mep_attn_bwd', self.d_attnb[i], self.t_attnb[i], stream, threads=self.g_attn[i][3])
+            launch('mep_attn_bwd', self.d_attnb[i], self.t_attnb[i], stream, threads=self.f_attnb[i])
         launch('mep_sum_rows', self.d_sum, self.t_sum, stream)
         if sp.unify_norm:
             launch('mep_layernorm_bwd', self.d_ulnb, cdiv(max(self.ntok.values()), 64), stream)

@@ -47,7 +47,7 @@ def main():
         'mep_attn_fwd': lambda: launch('mep_attn_fwd', p.d_attn[0], p.t_attn[0], threads=p.g_attn[0][2]),
         'mep_block_epi_fwd': lambda: launch('mep_block_epi_fwd', p.d_epi[0], p.t_epi[0], threads=D),
         'mep_block_epi_bwd': lambda: launch('mep_block_epi_bwd', p.d_epib[0], p.t_epi[0], threads=D),
-        'mep_attn_bwd': lambda: launch('mep_attn_bwd', p.d_attnb[0], p.t_attnb[0], threads=p.g_attn[0][3]),
+        'mep_attn_bwd': lambda: launch('mep_attn_bwd', p.d_attnb[0], p.t_attnb[0], threads=p.f_attnb[0]),
         'mep_wgrad': lambda: launch('mep_wgrad', p.d_wgrad, p.t_wgrad),
         'mep_pool_fwd': lambda: launch('mep_pool_fwd', p.d_pool, p.t_pool),
     }
