@@ -52,19 +52,19 @@ MEP_DEV bool aligned16(const mep_rows& r) {
 // 32-bit per-lane offsets t * sT
 MEP_DEV gfloat* bat(const mep_rows& v, int b) { return G<float>(v.ptr) + (int64_t)b * v.sB; }
 
-// four consecutive floats of row t (clamped into [0, n), zeroed when t >= n) at column col
+// four consecutive floats of row min(t, n-1) at column col.  Rows past the end are never
+// zeroed: a padded key's score is -inf (its mask term is +inf), so its P and dS are exactly 0
+// whatever K/V hold there, and padded queries are never stored (forward) or carry P = 0
+// (backward); clamping keeps every load in bounds and every value finite.
 MEP_DEV void load4(float* dst, const gfloat* base, int sT, int t, int n, int col, bool vec) {
-    const bool ok = t < n;
-    const gfloat* p = base + (ok ? t : n - 1) * sT + col;
+    const gfloat* p = base + min(t, n - 1) * sT + col;
     float4 x;
     if (vec) x = ldg4(p);
     else x = make_float4(p[0], p[1], p[2], p[3]);
-    dst[0] = ok ? x.x : 0.f; dst[1] = ok ? x.y : 0.f; dst[2] = ok ? x.z : 0.f; dst[3] = ok ? x.w : 0.f;
+    dst[0] = x.x; dst[1] = x.y; dst[2] = x.z; dst[3] = x.w;
 }
 MEP_DEV float load1(const gfloat* base, int sT, int t, int n, int col) {
-    const bool ok = t < n;
-    const float x = base[(ok ? t : n - 1) * sT + col];
-    return ok ? x : 0.f;
+    return base[min(t, n - 1) * sT + col];
 }
 
 // per-key mask term of the score: 1e8 * (1 - mask) (cmu-mosei/run.py:253), +inf for padding keys
