@@ -30,9 +30,16 @@ MEP_DEV void stg4(gfloat* p, float4 v) { *reinterpret_cast<MEP_G f32x4*>(p) = f3
 constexpr int kWave = 64;
 
 // ------------------------------------------------------------------ row views
+// tok -> (b, t) = (tok / T, tok % T) without an integer division: the quotient from the f32
+// reciprocal (v_rcp_f32, 1 ulp) is off by at most one for tok < 2^22 (relative error of the
+// product <= 2^-22), and one correction step each way makes it exact.  Hosts keep every row view
+// under 2^22 rows (4M tokens).
 MEP_DEV int64_t row_off(const mep_rows& r, int tok) {
-    int b = tok / r.T;
-    int t = tok - b * r.T;
+    const int T = r.T;
+    int b = (int)((float)tok * __builtin_amdgcn_rcpf((float)T));
+    int t = tok - b * T;
+    if (t < 0) { --b; t += T; }
+    if (t >= T) { ++b; t -= T; }
     return (int64_t)b * r.sB + (int64_t)t * r.sT;
 }
 MEP_DEV gfloat* row_ptr(const mep_rows& r, int tok) { return G<float>(r.ptr) + row_off(r, tok); }

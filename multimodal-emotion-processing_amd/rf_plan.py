@@ -92,6 +92,7 @@ class RealformerPlan:
         f32 = dict(dtype=torch.float32, device=dev)
         self.T = {m: sp.Tlen[m] for m in sp.mods}
         self.ntok = {m: R * self.T[m] for m in sp.mods}
+        assert max(self.ntok.values()) < 1 << 22, 'row views are limited to 2^22 rows (csrc/common.h row_off)'
         # ---------------- static inputs ([R, T, d] = the reference's [B, P, T, d])
         self.x_in = {m: torch.zeros(R, self.T[m], sp.dims[m], **f32) for m in sp.mods}
         self.m_in = {m: torch.zeros(R, self.T[m], **f32) for m in sp.mods}

@@ -121,6 +121,7 @@ class TriModalPlan:
         # ---------------- activations
         ntok = {m: B * self.T[m] for m in MODS}
         self.ntok = ntok
+        assert max(ntok.values()) < 1 << 22, 'row views are limited to 2^22 rows (csrc/common.h row_off)'
         self.U = {(e, m): torch.zeros(ntok[m], D, **f32) for e in range(E) for m in MODS}
         if sp.unify_norm:
             self.Y = {(e, m): torch.zeros(ntok[m], D, **f32) for e in range(E) for m in MODS}
