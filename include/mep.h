@@ -154,8 +154,8 @@ typedef struct {
 int mep_block_epi_fwd(const mep_epi_desc* descs, int n_desc, int max_tiles, int D, mep_stream_t stream);
 
 /* Backward: dout -> (dropout) -> LN backward -> dz;  dq_direct = dz Wm[:, :D];
- * dxp = drop'(dz Wm[:, D:]);  dx = dxp Wp.  Writes dz, dxp, dx, dq and per-tile LayerNorm
- * parameter-gradient partials ln_partial[tile][2][D]. */
+ * dxp = drop'(dz Wm[:, D:]);  dx = dxp Wp.  Writes dz, dxp, dx, dq and LayerNorm
+ * parameter-gradient partials ln_partial[ceil(ntok / 16)][2][D] (one row per 16 tokens). */
 typedef struct {
     mep_epi_desc f;
     mep_rows dout;

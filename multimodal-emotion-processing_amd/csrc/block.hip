@@ -39,197 +39,214 @@ MEP_DEV void stage(float* dst, const mep_rows& src, int tok0, int ntok) {
     }
 }
 
+constexpr int EW = 4;               // waves per workgroup of the forward epilogue
+constexpr int ETHREADS = 64 * EW;
+
+// One WAVE = 16 tokens x all D columns, four independent waves per workgroup (no block
+// barriers).  Both Linears are wave-level 16-row GEMMs (wgemm16: v_mfma_f32_16x16x4_f32, the
+// weight fragments of the next k block in flight during the current one); the LayerNorm runs on
+// the accumulators in registers (row sums over the D/16 column blocks a lane holds + a 16-lane
+// shuffle reduction).  LDS holds only this wave's A operands: x (then q) and xp.
 template <int D>
-__global__ __launch_bounds__(THREADS) void k_epi_fwd(const mep_epi_desc* __restrict__ descs) {
+__global__ __launch_bounds__(ETHREADS) void k_epi_fwd(const mep_epi_desc* __restrict__ descs) {
     const mep_epi_desc& d = descs[blockIdx.y];
-    const int tok0 = blockIdx.x * 64;
-    if (tok0 >= d.ntok) return;
-    constexpr int LD = D + 4;
-    __shared__ __attribute__((aligned(16))) float smem[3 * 64 * LD];
-    float* Xs = smem;                 // x, later z
-    float* Qs = smem + 64 * LD;
-    float* Ps = smem + 2 * 64 * LD;   // xp (post-dropout)
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    constexpr int NTASK = 2 * (D / 32);
-    const int mh = wave & 1, nblk = wave >> 1;
-    const bool task = wave < NTASK;
-    const int col = nblk * 32 + (lane & 31);
-    const gfloat* Wp = G<const float>(d.wp);
-    const gfloat* Wm = G<const float>(d.wm);
+    const int c = lane & 15, g = lane >> 4;
+    const int ntok = d.ntok;
+    const int r0 = blockIdx.x * 64 + wave * 16;
+    if (r0 >= ntok) return;   // whole wave; only wave-private LDS below
+    constexpr int LD = D + 4, NJ = D / 16;
+    __shared__ __attribute__((aligned(16))) float smem[EW][2][16 * LD];
+    float* Xs = smem[wave][0];   // x, then q
+    float* Ps = smem[wave][1];   // xp (post-dropout)
     const float p = d.drop_p;
     const uint64_t seed = (d.seed && p > 0.f) ? *G<const uint64_t>(d.seed) : 0;
+    const gfloat* Wp = G<const float>(d.wp);
+    const gfloat* Wm = G<const float>(d.wm);
 
-    stage<D>(Xs, d.x, tok0, d.ntok);
-    stage<D>(Qs, d.q, tok0, d.ntok);
-    __syncthreads();
-    floatx16 acc = zero16();
-    if (task) {
-        mma_tile<true, D>(acc, Xs, LD, mh * 32, Wp, D, nblk * 32, D, 0, D, D, vec_ok(d.wp, D));
+    wave_stage16<D>(Xs, LD, d.x, r0, ntok);
+    wave_lds_fence();
+    f32x4 acc[NJ];
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const int row = mh * 32 + acc_row(r, lane);
-            const int tok = tok0 + row;
-            float v = acc[r];
+    for (int j = 0; j < NJ; ++j) acc[j] = zero_f4();
+    wgemm16<NJ, D, true>(acc, Xs, LD, Wp, D, 0, vec_ok(d.wp, D));
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const int row = 4 * g + r, tok = r0 + row;
+        gfloat* xr = row_ptr(d.xp, min(tok, ntok - 1));
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+            const int col = 16 * j + c;
+            float v = acc[j][r];
             if (p > 0.f) v *= drop_scale(seed, 2u * d.drop_stream, (uint64_t)tok * D + col, p);
             Ps[row * LD + col] = v;
-            if (tok < d.ntok) row_ptr(d.xp, tok)[col] = v;
+            if (tok < ntok) xr[col] = v;
         }
     }
-    __syncthreads();
-    if (task) {
-        acc = zero16();
-        const bool wv = vec_ok(d.wm, 2 * D);
-        mma_tile<true, D>(acc, Qs, LD, mh * 32, Wm, 2 * D, nblk * 32, D, 0, D, D, wv);
-        mma_tile<true, D>(acc, Ps, LD, mh * 32, Wm + D, 2 * D, nblk * 32, D, 0, D, D, wv);
-    }
-    __syncthreads();  // everyone done reading Xs (x) before it becomes z
-    if (task) {
+    wave_lds_fence();
+    wave_stage16<D>(Xs, LD, d.q, r0, ntok);
+    wave_lds_fence();
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const int row = mh * 32 + acc_row(r, lane);
-            const int tok = tok0 + row;
-            Xs[row * LD + col] = acc[r];
-            if (tok < d.ntok) row_ptr(d.z, tok)[col] = acc[r];
-        }
-    }
-    __syncthreads();
-    // LayerNorm: wave per row, lane covers columns lane and lane+64
+    for (int j = 0; j < NJ; ++j) acc[j] = zero_f4();
+    const bool wv = vec_ok(d.wm, 2 * D);
+    wgemm16<NJ, D, true>(acc, Xs, LD, Wm, 2 * D, 0, wv);       // [q | xp] Wm^T: q half
+    wgemm16<NJ, D, true>(acc, Ps, LD, Wm + D, 2 * D, 0, wv);   //                xp half
+    // z -> HBM;  LayerNorm on the accumulators
     const gfloat* lw = G<const float>(d.ln_w);
     const gfloat* lb = G<const float>(d.ln_b);
     gfloat* stats = G<float>(d.stats);
-    const bool c0 = lane < D, c1 = lane + 64 < D;
-    const float w0 = c0 ? lw[lane] : 0.f, w1 = c1 ? lw[lane + 64] : 0.f;
-    const float b0 = c0 ? lb[lane] : 0.f, b1 = c1 ? lb[lane + 64] : 0.f;
-    for (int row = wave; row < 64; row += THREADS / 64) {
-        const int tok = tok0 + row;
-        if (tok >= d.ntok) break;
-        const float x0 = c0 ? Xs[row * LD + lane] : 0.f;
-        const float x1 = c1 ? Xs[row * LD + lane + 64] : 0.f;
-        const float mean = wave_sum(x0 + x1) / (float)D;
-        const float d0 = c0 ? x0 - mean : 0.f, d1 = c1 ? x1 - mean : 0.f;
-        const float var = wave_sum(d0 * d0 + d1 * d1) / (float)D;
-        const float rstd = 1.0f / sqrtf(var + LN_EPS);
-        gfloat* out = row_ptr(d.out, tok);
-        if (c0) {
-            float y = d0 * rstd * w0 + b0;
-            if (p > 0.f) y *= drop_scale(seed, 2u * d.drop_stream + 1u, (uint64_t)tok * D + lane, p);
-            out[lane] = y;
+    float wj[NJ], bj[NJ];
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) { wj[j] = lw[16 * j + c]; bj[j] = lb[16 * j + c]; }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const int tok = r0 + 4 * g + r;
+        float s = 0.f;
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) s += acc[j][r];
+        const float mean = group16_sum(s) / (float)D;
+        float q = 0.f;
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) { const float t = acc[j][r] - mean; q += t * t; }
+        const float rstd = 1.0f / sqrtf(group16_sum(q) / (float)D + LN_EPS);
+        if (tok < ntok) {
+            gfloat* zr = row_ptr(d.z, tok);
+            gfloat* orow = row_ptr(d.out, tok);
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) {
+                const int col = 16 * j + c;
+                zr[col] = acc[j][r];
+                float y = (acc[j][r] - mean) * rstd * wj[j] + bj[j];
+                if (p > 0.f) y *= drop_scale(seed, 2u * d.drop_stream + 1u, (uint64_t)tok * D + col, p);
+                orow[col] = y;
+            }
+            if (c == 0) { stats[2 * tok] = mean; stats[2 * tok + 1] = rstd; }
         }
-        if (c1) {
-            float y = d1 * rstd * w1 + b1;
-            if (p > 0.f) y *= drop_scale(seed, 2u * d.drop_stream + 1u, (uint64_t)tok * D + lane + 64, p);
-            out[lane + 64] = y;
-        }
-        if (lane == 0) { stats[2 * tok] = mean; stats[2 * tok + 1] = rstd; }
     }
 }
 
+// Backward, same mapping (one wave = 16 tokens x D): dout (+dout2) and z are read straight into
+// the accumulator layout, the LayerNorm backward runs in registers, dz is staged once in LDS as
+// the A operand of dq_direct = dz Wm[:, :D] and dxp = drop'(dz Wm[:, D:]), and dxp (LDS) of
+// dx = dxp Wp.  ln_partial gets one [2][D] row per 16-token wave (no block barrier anywhere).
 template <int D>
-__global__ __launch_bounds__(THREADS) void k_epi_bwd(const mep_epi_bwd_desc* __restrict__ descs) {
+__global__ __launch_bounds__(ETHREADS) __attribute__((amdgpu_waves_per_eu(3))) void k_epi_bwd(const mep_epi_bwd_desc* __restrict__ descs) {
     const mep_epi_bwd_desc& bd = descs[blockIdx.y];
     const mep_epi_desc& d = bd.f;
-    const int tok0 = blockIdx.x * 64;
-    if (tok0 >= d.ntok) return;
-    constexpr int LD = D + 4;
-    __shared__ __attribute__((aligned(16))) float smem[2 * 64 * LD + 8 * 2 * 128];
-    float* Gs = smem;                 // dout -> dz
-    float* Ps = smem + 64 * LD;       // dxp
-    float* red = smem + 2 * 64 * LD;  // [8 waves][2][128]
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int c = lane & 15, g = lane >> 4;
+    const int ntok = d.ntok;
+    const int r0 = blockIdx.x * 64 + wave * 16;
+    if (r0 >= ntok) return;
+    constexpr int LD = D + 4, NJ = D / 16;
+    __shared__ __attribute__((aligned(16))) float smem[EW][2][16 * LD];
+    float* Gs = smem[wave][0];   // dz
+    float* Ps = smem[wave][1];   // dxp
     const float p = d.drop_p;
     const uint64_t seed = (d.seed && p > 0.f) ? *G<const uint64_t>(d.seed) : 0;
-
-    stage<D>(Gs, bd.dout, tok0, d.ntok);
-    if (bd.dout2.ptr) {
-        __syncthreads();
-        stage<D>(Ps, bd.dout2, tok0, d.ntok);
-        __syncthreads();
-        for (int idx = threadIdx.x; idx < 64 * D; idx += THREADS) {
-            const int row = idx / D, c = idx - row * D;
-            Gs[row * LD + c] += Ps[row * LD + c];
-        }
-    }
-    __syncthreads();
-    // LayerNorm backward, wave per row
     const gfloat* lw = G<const float>(d.ln_w);
     const gfloat* stats = G<const float>(d.stats);
-    float pw0 = 0.f, pw1 = 0.f, pb0 = 0.f, pb1 = 0.f;
-    const bool c0 = lane < D, c1 = lane + 64 < D;
-    const float w0 = c0 ? lw[lane] : 0.f, w1 = c1 ? lw[lane + 64] : 0.f;
-    for (int row = wave; row < 64; row += THREADS / 64) {
-        const int tok = tok0 + row;
-        if (tok >= d.ntok) {
-            if (c0) Gs[row * LD + lane] = 0.f;
-            if (c1) Gs[row * LD + lane + 64] = 0.f;
-            continue;
-        }
-        const float mean = stats[2 * tok], rstd = stats[2 * tok + 1];
-        const gfloat* zr = row_ptr(d.z, tok);
-        float g0 = c0 ? Gs[row * LD + lane] : 0.f;
-        float g1 = c1 ? Gs[row * LD + lane + 64] : 0.f;
-        if (p > 0.f) {
-            if (c0) g0 *= drop_scale(seed, 2u * d.drop_stream + 1u, (uint64_t)tok * D + lane, p);
-            if (c1) g1 *= drop_scale(seed, 2u * d.drop_stream + 1u, (uint64_t)tok * D + lane + 64, p);
-        }
-        const float xh0 = c0 ? (zr[lane] - mean) * rstd : 0.f;
-        const float xh1 = c1 ? (zr[lane + 64] - mean) * rstd : 0.f;
-        const float gw0 = g0 * w0, gw1 = g1 * w1;
-        const float s1 = wave_sum(gw0 + gw1) / (float)D;
-        const float s2 = wave_sum(gw0 * xh0 + gw1 * xh1) / (float)D;
-        pw0 += g0 * xh0; pw1 += g1 * xh1; pb0 += g0; pb1 += g1;
-        gfloat* dzr = row_ptr(bd.dz, tok);
-        if (c0) { const float v = rstd * (gw0 - s1 - xh0 * s2); Gs[row * LD + lane] = v; dzr[lane] = v; }
-        if (c1) { const float v = rstd * (gw1 - s1 - xh1 * s2); Gs[row * LD + lane + 64] = v; dzr[lane + 64] = v; }
-    }
-    red[(wave * 2 + 0) * 128 + lane] = pw0;
-    red[(wave * 2 + 0) * 128 + lane + 64] = pw1;
-    red[(wave * 2 + 1) * 128 + lane] = pb0;
-    red[(wave * 2 + 1) * 128 + lane + 64] = pb1;
-    __syncthreads();
-    if (bd.ln_partial) {
-        gfloat* lp = G<float>(bd.ln_partial) + (int64_t)blockIdx.x * 2 * D;
-        for (int idx = threadIdx.x; idx < 2 * D; idx += THREADS) {
-            const int which = idx / D, c = idx - which * D;
-            float s = 0.f;
+    float wj[NJ], pw[NJ], pb[NJ];
 #pragma unroll
-            for (int w = 0; w < THREADS / 64; ++w) s += red[(w * 2 + which) * 128 + c];
-            lp[idx] = s;
+    for (int j = 0; j < NJ; ++j) { wj[j] = lw[16 * j + c]; pw[j] = 0.f; pb[j] = 0.f; }
+    // LayerNorm backward per row of this lane (rows 4g + r); not unrolled: bounds live registers
+#pragma unroll 1
+    for (int r = 0; r < 4; ++r) {
+        const int row = 4 * g + r, tok = r0 + row;
+        const bool ok = tok < ntok;
+        const int tc = min(tok, ntok - 1);
+        const gfloat* gr = row_ptr(bd.dout, tc);
+        const gfloat* g2 = bd.dout2.ptr ? row_ptr(bd.dout2, tc) : nullptr;
+        const gfloat* zr = row_ptr(d.z, tc);
+        const float mean = stats[2 * tc], rstd = stats[2 * tc + 1];
+        float gv[NJ], xh[NJ], s1 = 0.f, s2 = 0.f;
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+            const int col = 16 * j + c;
+            float gg = gr[col];
+            if (g2) gg += g2[col];
+            if (p > 0.f) gg *= drop_scale(seed, 2u * d.drop_stream + 1u, (uint64_t)tok * D + col, p);
+            gg = ok ? gg : 0.f;
+            gv[j] = gg;
+            xh[j] = (zr[col] - mean) * rstd;
+            const float gw = gg * wj[j];
+            s1 += gw;
+            s2 += gw * xh[j];
+            pw[j] += gg * xh[j];
+            pb[j] += gg;
+        }
+        s1 = group16_sum(s1) / (float)D;
+        s2 = group16_sum(s2) / (float)D;
+        gfloat* dzr = row_ptr(bd.dz, tc);
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+            const int col = 16 * j + c;
+            const float v = ok ? rstd * (gv[j] * wj[j] - s1 - xh[j] * s2) : 0.f;
+            Gs[row * LD + col] = v;
+            if (ok) dzr[col] = v;
         }
     }
-    // dq_direct = dz Wm[:, :D];  dxp = drop'(dz Wm[:, D:])
-    constexpr int NTASK = 2 * (D / 32);
-    const int mh = wave & 1, nblk = wave >> 1;
-    const bool task = wave < NTASK;
-    const int col = nblk * 32 + (lane & 31);
+    // per-wave LayerNorm parameter partials: reduce the 4 lane groups
+    if (bd.ln_partial) {
+        gfloat* lp = G<float>(bd.ln_partial) + (int64_t)(blockIdx.x * EW + wave) * 2 * D;
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+            float a = pw[j], b = pb[j];
+            a += __shfl_xor(a, 16, 64); a += __shfl_xor(a, 32, 64);
+            b += __shfl_xor(b, 16, 64); b += __shfl_xor(b, 32, 64);
+            if (g == 0) { lp[16 * j + c] = a; lp[D + 16 * j + c] = b; }
+        }
+    }
+    wave_lds_fence();
     const gfloat* Wm = G<const float>(d.wm);
     const gfloat* Wp = G<const float>(d.wp);
-    if (task) {
-        floatx16 aq = zero16(), ap = zero16();
-        mma_tile<false, D>(aq, Gs, LD, mh * 32, Wm, 2 * D, nblk * 32, D, 0, D, D, false);
-        mma_tile<false, D>(ap, Gs, LD, mh * 32, Wm + D, 2 * D, nblk * 32, D, 0, D, D, false);
+    f32x4 acc[NJ];
+    // dq_direct = dz Wm[:, :D]      (Wm[k][n] with k the output unit: NT = false)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const int row = mh * 32 + acc_row(r, lane);
-            const int tok = tok0 + row;
-            float vp = ap[r];
-            if (p > 0.f && tok < d.ntok) vp *= drop_scale(seed, 2u * d.drop_stream, (uint64_t)tok * D + col, p);
-            Ps[row * LD + col] = (tok < d.ntok) ? vp : 0.f;
-            if (tok < d.ntok) {
-                gfloat* q = row_ptr(bd.dq, tok) + col;
-                *q = bd.dq_accumulate ? *q + aq[r] : aq[r];
-                row_ptr(bd.dxp, tok)[col] = vp;
-            }
+    for (int j = 0; j < NJ; ++j) acc[j] = zero_f4();
+    wgemm16<NJ, D, false>(acc, Gs, LD, Wm, 2 * D, 0, false);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const int tok = r0 + 4 * g + r;
+        if (tok >= ntok) continue;
+        gfloat* q = row_ptr(bd.dq, tok);
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+            const int col = 16 * j + c;
+            q[col] = bd.dq_accumulate ? q[col] + acc[j][r] : acc[j][r];
         }
     }
-    __syncthreads();
-    if (task) {
-        floatx16 ax = zero16();
-        mma_tile<false, D>(ax, Ps, LD, mh * 32, Wp, D, nblk * 32, D, 0, D, D, false);
+    // dxp = drop'(dz Wm[:, D:])
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const int tok = tok0 + mh * 32 + acc_row(r, lane);
-            if (tok < d.ntok) row_ptr(bd.dx, tok)[col] = ax[r];
+    for (int j = 0; j < NJ; ++j) acc[j] = zero_f4();
+    wgemm16<NJ, D, false>(acc, Gs, LD, Wm + D, 2 * D, 0, false);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const int row = 4 * g + r, tok = r0 + row;
+        const bool ok = tok < ntok;
+        gfloat* xr = row_ptr(bd.dxp, min(tok, ntok - 1));
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+            const int col = 16 * j + c;
+            float v = acc[j][r];
+            if (p > 0.f) v *= drop_scale(seed, 2u * d.drop_stream, (uint64_t)tok * D + col, p);
+            v = ok ? v : 0.f;
+            Ps[row * LD + col] = v;
+            if (ok) xr[col] = v;
         }
+    }
+    wave_lds_fence();
+    // dx = dxp Wp
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) acc[j] = zero_f4();
+    wgemm16<NJ, D, false>(acc, Ps, LD, Wp, D, 0, false);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const int tok = r0 + 4 * g + r;
+        if (tok >= ntok) continue;
+        gfloat* xr = row_ptr(bd.dx, tok);
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) xr[16 * j + c] = acc[j][r];
     }
 }
 
@@ -329,7 +346,7 @@ int dispatch_D(int D, F&& f) {
 extern "C" int mep_block_epi_fwd(const mep_epi_desc* descs, int n_desc, int max_tiles, int D, mep_stream_t stream) {
     if (n_desc <= 0 || max_tiles <= 0) return 0;
     const int rc = dispatch_D(D, [&](auto dc) {
-        hipLaunchKernelGGL(k_epi_fwd<decltype(dc)::value>, dim3(max_tiles, n_desc), dim3(THREADS), 0,
+        hipLaunchKernelGGL(k_epi_fwd<decltype(dc)::value>, dim3(max_tiles, n_desc), dim3(ETHREADS), 0,
                            (hipStream_t)stream, descs);
     });
     if (rc) { mep_set_error("mep_block_epi_fwd: D must be 32, 64, 96 or 128"); return rc; }
@@ -339,7 +356,7 @@ extern "C" int mep_block_epi_fwd(const mep_epi_desc* descs, int n_desc, int max_
 extern "C" int mep_block_epi_bwd(const mep_epi_bwd_desc* descs, int n_desc, int max_tiles, int D, mep_stream_t stream) {
     if (n_desc <= 0 || max_tiles <= 0) return 0;
     const int rc = dispatch_D(D, [&](auto dc) {
-        hipLaunchKernelGGL(k_epi_bwd<decltype(dc)::value>, dim3(max_tiles, n_desc), dim3(THREADS), 0,
+        hipLaunchKernelGGL(k_epi_bwd<decltype(dc)::value>, dim3(max_tiles, n_desc), dim3(ETHREADS), 0,
                            (hipStream_t)stream, descs);
     });
     if (rc) { mep_set_error("mep_block_epi_bwd: D must be 32, 64, 96 or 128"); return rc; }

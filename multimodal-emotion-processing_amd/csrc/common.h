@@ -142,6 +142,55 @@ MEP_DEV void mma_tile(floatx16& acc, const float* __restrict__ As, int lda, int 
     }
 }
 
+// mma_tile with the weight operand of the whole K range fetched into registers before the first
+// MFMA (KC / 8 x 16 bytes per lane): the L2 latency of the weight reads is paid once per tile
+// instead of once per k-step (hipcc otherwise sinks each load next to its MFMA).
+template <bool NT, int KC>
+MEP_DEV void mma_tile_pf(floatx16& acc, const float* __restrict__ As, int lda, int m0,
+                         const gfloat* __restrict__ W, int ldw, int n0, int N, int k0, int K, bool w_vec) {
+    static_assert(KC % 8 == 0, "KC must be a multiple of 8");
+    constexpr int NS = KC / 8;
+    const int lane = threadIdx.x & 63;
+    const int r = lane & 31;
+    const int h = lane >> 5;
+    const float* arow = As + (m0 + r) * lda + 4 * h;
+    const int n = n0 + r;
+    const bool nval = n < N;
+    float4 b[NS];
+#pragma unroll
+    for (int i = 0; i < NS; ++i) {
+        const int kg = k0 + 8 * i + 4 * h;
+        float b0 = 0.f, b1 = 0.f, b2 = 0.f, b3 = 0.f;
+        if (NT) {
+            const gfloat* wp = W + (int64_t)n * ldw + kg;
+            if (nval && w_vec && kg + 3 < K) {
+                const float4 v = ldg4(wp);
+                b0 = v.x; b1 = v.y; b2 = v.z; b3 = v.w;
+            } else if (nval) {
+                if (kg < K) b0 = wp[0];
+                if (kg + 1 < K) b1 = wp[1];
+                if (kg + 2 < K) b2 = wp[2];
+                if (kg + 3 < K) b3 = wp[3];
+            }
+        } else if (nval) {
+            const gfloat* wp = W + (int64_t)kg * ldw + n;
+            if (kg < K) b0 = wp[0];
+            if (kg + 1 < K) b1 = wp[ldw];
+            if (kg + 2 < K) b2 = wp[2 * ldw];
+            if (kg + 3 < K) b3 = wp[3 * ldw];
+        }
+        b[i] = make_float4(b0, b1, b2, b3);
+    }
+#pragma unroll
+    for (int i = 0; i < NS; ++i) {
+        const float4 a = *reinterpret_cast<const float4*>(arow + 8 * i);
+        acc = mfma32(a.x, b[i].x, acc);
+        acc = mfma32(a.y, b[i].y, acc);
+        acc = mfma32(a.z, b[i].z, acc);
+        acc = mfma32(a.w, b[i].w, acc);
+    }
+}
+
 MEP_DEV floatx16 zero16() {
     floatx16 z;
 #pragma unroll
@@ -187,6 +236,97 @@ MEP_DEV void stage_cols(float* __restrict__ dst, int ld, const mep_rows& src, in
             const int tok = t0 + row;
             dst[row * ld + c] = tok < t_end ? row_ptr(src, tok)[c0 + c] : 0.f;
         }
+    }
+}
+
+// ------------------------------------------------------------------ wave-level 16-row GEMM tiles
+// v_mfma_f32_16x16x4_f32: lane l = (c = l & 15, g = l >> 4) supplies A[c][k] and B[k][c] for the
+// k-slot g of a 4-wide step, and holds C[4g + r][c] (r < 4).  Reduction indices are ordered
+// (step s, slot g) -> 4g + s within each 16-wide k block, so every operand fetch is one 16-byte
+// read of 4 consecutive k.
+MEP_DEV f32x4 mfma16x4(float a, float b, f32x4 c) { return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0); }
+MEP_DEV f32x4 zero_f4() { return f32x4{0.f, 0.f, 0.f, 0.f}; }
+
+// LDS writes of this wave visible to all of its lanes (no other wave involved)
+MEP_DEV void wave_lds_fence() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// weight operand of k block kb for output column block j:
+//   NT: W[n][k] = W[n * ldw + k] (nn.Linear weight, forward);  else W[k][n] = W[k * ldw + n]
+template <bool NT>
+MEP_DEV float4 wfrag(const gfloat* W, int ldw, int n, int k, bool w_vec) {
+    if (NT) {
+        const gfloat* p = W + (int64_t)n * ldw + k;
+        if (w_vec) return ldg4(p);
+        return make_float4(p[0], p[1], p[2], p[3]);
+    }
+    const gfloat* p = W + (int64_t)k * ldw + n;
+    return make_float4(p[0], p[ldw], p[2 * ldw], p[3 * ldw]);
+}
+
+// acc[j] += A[16 x K] . W(cols n0 + 16j .. + 15)   for j < NJ (NJ even).  A: 16 rows in LDS,
+// row c at A + c * lda.  Column blocks are processed in pairs (two interleaved accumulation
+// chains hide the 40-cycle dependent-MFMA latency); the weight fragments of the next k block are
+// in flight while the current block's MFMAs issue, so only 4 float4 of weights are live.
+template <int NJ, int K, bool NT>
+MEP_DEV void wgemm16(f32x4 (&acc)[NJ], const float* A, int lda, const gfloat* W, int ldw, int n0, bool w_vec) {
+    static_assert(K % 16 == 0 && NJ % 2 == 0, "K multiple of 16, NJ even");
+    constexpr int KB = K / 16;
+    const int lane = threadIdx.x & 63;
+    const int c = lane & 15, g = lane >> 4;
+    const float* arow = A + c * lda + 4 * g;
+#pragma unroll
+    for (int jp = 0; jp < NJ; jp += 2) {
+        const int na = n0 + 16 * jp + c, nb = na + 16;
+        float4 b0 = wfrag<NT>(W, ldw, na, 4 * g, w_vec), b1 = wfrag<NT>(W, ldw, nb, 4 * g, w_vec);
+#pragma unroll
+        for (int kb = 0; kb < KB; ++kb) {
+            float4 c0 = b0, c1 = b1;
+            if (kb + 1 < KB) {
+                b0 = wfrag<NT>(W, ldw, na, 16 * (kb + 1) + 4 * g, w_vec);
+                b1 = wfrag<NT>(W, ldw, nb, 16 * (kb + 1) + 4 * g, w_vec);
+            }
+            const float4 a = *reinterpret_cast<const float4*>(arow + 16 * kb);
+            acc[jp] = mfma16x4(a.x, c0.x, acc[jp]);
+            acc[jp + 1] = mfma16x4(a.x, c1.x, acc[jp + 1]);
+            acc[jp] = mfma16x4(a.y, c0.y, acc[jp]);
+            acc[jp + 1] = mfma16x4(a.y, c1.y, acc[jp + 1]);
+            acc[jp] = mfma16x4(a.z, c0.z, acc[jp]);
+            acc[jp + 1] = mfma16x4(a.z, c1.z, acc[jp + 1]);
+            acc[jp] = mfma16x4(a.w, c0.w, acc[jp]);
+            acc[jp + 1] = mfma16x4(a.w, c1.w, acc[jp + 1]);
+        }
+    }
+}
+
+// sum over the 16 lanes of a lane group (lanes sharing g = lane >> 4)
+MEP_DEV float group16_sum(float v) {
+    v += __shfl_xor(v, 1, 64);
+    v += __shfl_xor(v, 2, 64);
+    v += __shfl_xor(v, 4, 64);
+    v += __shfl_xor(v, 8, 64);
+    return v;
+}
+
+// stage rows [r0, r0 + 16) of a row view (D columns) into LDS rows of stride lda, one wave;
+// rows >= ntok are zero
+template <int D>
+MEP_DEV void wave_stage16(float* dst, int lda, const mep_rows& src, int r0, int ntok) {
+    const int lane = threadIdx.x & 63;
+    constexpr int V = D / 4;
+    const bool vec = ((src.ptr & 15) == 0) && (src.sB % 4 == 0) && (src.sT % 4 == 0);
+    for (int idx = lane; idx < 16 * V; idx += 64) {
+        const int row = idx / V, c4 = idx - row * V;
+        const int tok = r0 + row;
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (tok < ntok) {
+            const gfloat* p = row_ptr(src, tok) + 4 * c4;
+            v = vec ? ldg4(p) : make_float4(p[0], p[1], p[2], p[3]);
+        }
+        *reinterpret_cast<float4*>(dst + row * lda + 4 * c4) = v;
     }
 }
 

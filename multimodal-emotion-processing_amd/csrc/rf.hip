@@ -29,7 +29,12 @@ MEP_DEV void tile_gemm(const float* As, int lda, const gfloat* W, int ldw, bool 
     for (int t = wave; t < NTASK; t += NWAVE) {
         const int mh = t & 1, nblk = t >> 1;
         floatx16 acc = zero16();
-        mma_tile<NT, K>(acc, As, lda, mh * 32, W, ldw, nblk * 32, N, 0, K, K, w_vec);
+        if constexpr (K <= 128) {
+            mma_tile_pf<NT, K>(acc, As, lda, mh * 32, W, ldw, nblk * 32, N, 0, K, w_vec);
+        } else {   // two halves: at most 64 prefetch registers per pass
+            mma_tile_pf<NT, K / 2>(acc, As, lda, mh * 32, W, ldw, nblk * 32, N, 0, K, w_vec);
+            mma_tile_pf<NT, K / 2>(acc, As + K / 2, lda, mh * 32, W, ldw, nblk * 32, N, K / 2, K, w_vec);
+        }
         const int col = nblk * 32 + (lane & 31);
         if (col < N) {
 #pragma unroll

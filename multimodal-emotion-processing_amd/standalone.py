@@ -70,7 +70,7 @@ class _BlockFn(torch.autograd.Function):
         dZ, dXP, dX, dQ = (torch.empty(B, Tq, D, **f) for _ in range(4))
         dK = torch.empty(B, Tk, D, **f)
         dV = dK if same_kv else torch.empty(B, Tk, D, **f)
-        ln_part = torch.empty(cdiv(B * Tq, 64), 2, D, **f)
+        ln_part = torch.empty(cdiv(B * Tq, 16), 2, D, **f)
         has_prev = ctx.sp is not None
         dSp = torch.empty(B, H, Tq, Tk, **f) if has_prev else None
         dc_part = torch.empty(_lib.attn_dc_slots(B, H, Tk), **f) if has_prev else None

@@ -162,7 +162,7 @@ class TriModalPlan:
         blk['estat'] = torch.zeros(nq, 2, **f32)
         blk['astat'] = torch.zeros(B, H, Tq, 2, **f32)
         blk['dKV'] = torch.zeros(nk, D, **f32)
-        blk['ln_partial'] = torch.zeros(cdiv(nq, 64), 2, D, **f32)
+        blk['ln_partial'] = torch.zeros(cdiv(nq, 16), 2, D, **f32)   # one row per 16-token wave
         if i < sp.nl - 1:
             blk['S'] = torch.zeros(B, H, Tq, Tk, **f32)
         if i >= 1:

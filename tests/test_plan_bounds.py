@@ -127,7 +127,7 @@ def _epi_bwd(c, d):
     _epi(c, f, 'epi_bwd')
     for name in ('dout', 'dout2', 'dz', 'dxp', 'dx', 'dq'):
         c.rows('epi_bwd.' + name, getattr(d, name), f.ntok, f.D)
-    c.inside('epi_bwd.ln_partial', d.ln_partial, cdiv(f.ntok, 64) * 2 * f.D * F)
+    c.inside('epi_bwd.ln_partial', d.ln_partial, cdiv(f.ntok, 16) * 2 * f.D * F)
 
 
 def _ln(c, d):
