@@ -269,6 +269,7 @@ typedef struct {
     uint64_t argmax;      /* int32 [B, C]                  */
     int32_t  B, T, C, _pad;
 } mep_pool_desc;
+/* Grids: forward max_tiles = B * ceil(C / 32); backward max_tiles = B * ceil(T / 16). */
 int mep_pool_fwd(const mep_pool_desc* descs, int n_desc, int max_tiles, mep_stream_t stream);
 int mep_pool_bwd(const mep_pool_desc* descs, int n_desc, int max_tiles, mep_stream_t stream);
 

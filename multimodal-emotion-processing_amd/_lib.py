@@ -11,7 +11,8 @@ import os
 import torch
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(PKG_DIR, 'libmep_hip.so')
+# MEP_LIB: development override (A/B experiments with variant builds); never set in normal use
+LIB_PATH = os.environ.get('MEP_LIB') or os.path.join(PKG_DIR, 'libmep_hip.so')
 
 u64, i64, i32, f32 = ctypes.c_uint64, ctypes.c_int64, ctypes.c_int32, ctypes.c_float
 

@@ -39,6 +39,8 @@ MEP_DEV void stage(float* dst, const mep_rows& src, int tok0, int ntok) {
     }
 }
 
+// MEP_EXP (development A/B builds only; 0 in the product): 1 = no HBM stores, 2 = no MFMA,
+// 4 = no staging loads, 8 = no LayerNorm math, 16 = no weight loads (common.h wfrag)
 constexpr int EW = 4;               // waves per workgroup of the forward epilogue
 constexpr int ETHREADS = 64 * EW;
 
@@ -46,7 +48,9 @@ constexpr int ETHREADS = 64 * EW;
 // barriers).  Both Linears are wave-level 16-row GEMMs (wgemm16: v_mfma_f32_16x16x4_f32, the
 // weight fragments of the next k block in flight during the current one); the LayerNorm runs on
 // the accumulators in registers (row sums over the D/16 column blocks a lane holds + a 16-lane
-// shuffle reduction).  LDS holds only this wave's A operands: x (then q) and xp.
+// shuffle reduction).  LDS holds this wave's A operands: x (then xp) and q.  Every HBM store is
+// issued after the last weight load: s_waitcnt vmcnt counts loads and stores together in issue
+// order, so a store in flight would delay every later weight fragment.
 template <int D>
 __global__ __launch_bounds__(ETHREADS) void k_epi_fwd(const mep_epi_desc* __restrict__ descs) {
     const mep_epi_desc& d = descs[blockIdx.y];
@@ -57,41 +61,43 @@ __global__ __launch_bounds__(ETHREADS) void k_epi_fwd(const mep_epi_desc* __rest
     if (r0 >= ntok) return;   // whole wave; only wave-private LDS below
     constexpr int LD = D + 4, NJ = D / 16;
     __shared__ __attribute__((aligned(16))) float smem[EW][2][16 * LD];
-    float* Xs = smem[wave][0];   // x, then q
-    float* Ps = smem[wave][1];   // xp (post-dropout)
+    float* As = smem[wave][0];   // x, then xp (post-dropout)
+    float* Qs = smem[wave][1];   // q
     const float p = d.drop_p;
     const uint64_t seed = (d.seed && p > 0.f) ? *G<const uint64_t>(d.seed) : 0;
     const gfloat* Wp = G<const float>(d.wp);
     const gfloat* Wm = G<const float>(d.wm);
 
-    wave_stage16<D>(Xs, LD, d.x, r0, ntok);
+    if (!(MEP_EXP & 4)) {
+        wave_stage16<D>(As, LD, d.x, r0, ntok);
+        wave_stage16<D>(Qs, LD, d.q, r0, ntok);
+    }
     wave_lds_fence();
     f32x4 acc[NJ];
 #pragma unroll
     for (int j = 0; j < NJ; ++j) acc[j] = zero_f4();
-    wgemm16<NJ, D, true>(acc, Xs, LD, Wp, D, 0, vec_ok(d.wp, D));
+    if (!(MEP_EXP & 2)) wgemm16<NJ, D, true>(acc, As, LD, Wp, D, 0, vec_ok(d.wp, D));
+    wave_lds_fence();   // every lane is done reading x
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
         const int row = 4 * g + r, tok = r0 + row;
-        gfloat* xr = row_ptr(d.xp, min(tok, ntok - 1));
 #pragma unroll
         for (int j = 0; j < NJ; ++j) {
             const int col = 16 * j + c;
             float v = acc[j][r];
             if (p > 0.f) v *= drop_scale(seed, 2u * d.drop_stream, (uint64_t)tok * D + col, p);
-            Ps[row * LD + col] = v;
-            if (tok < ntok) xr[col] = v;
+            As[row * LD + col] = v;
         }
     }
-    wave_lds_fence();
-    wave_stage16<D>(Xs, LD, d.q, r0, ntok);
     wave_lds_fence();
 #pragma unroll
     for (int j = 0; j < NJ; ++j) acc[j] = zero_f4();
     const bool wv = vec_ok(d.wm, 2 * D);
-    wgemm16<NJ, D, true>(acc, Xs, LD, Wm, 2 * D, 0, wv);       // [q | xp] Wm^T: q half
-    wgemm16<NJ, D, true>(acc, Ps, LD, Wm + D, 2 * D, 0, wv);   //                xp half
-    // z -> HBM;  LayerNorm on the accumulators
+    if (!(MEP_EXP & 2)) {
+        wgemm16<NJ, D, true>(acc, Qs, LD, Wm, 2 * D, 0, wv);       // [q | xp] Wm^T: q half
+        wgemm16<NJ, D, true>(acc, As, LD, Wm + D, 2 * D, 0, wv);   //                xp half
+    }
+    // LayerNorm on the accumulators; then every store
     const gfloat* lw = G<const float>(d.ln_w);
     const gfloat* lb = G<const float>(d.ln_b);
     gfloat* stats = G<float>(d.stats);
@@ -108,8 +114,8 @@ __global__ __launch_bounds__(ETHREADS) void k_epi_fwd(const mep_epi_desc* __rest
         float q = 0.f;
 #pragma unroll
         for (int j = 0; j < NJ; ++j) { const float t = acc[j][r] - mean; q += t * t; }
-        const float rstd = 1.0f / sqrtf(group16_sum(q) / (float)D + LN_EPS);
-        if (tok < ntok) {
+        const float rstd = (MEP_EXP & 8) ? 1.f : 1.0f / sqrtf(group16_sum(q) / (float)D + LN_EPS);
+        if ((MEP_EXP & 1) ? tok < 0 : tok < ntok) {
             gfloat* zr = row_ptr(d.z, tok);
             gfloat* orow = row_ptr(d.out, tok);
 #pragma unroll
@@ -123,6 +129,7 @@ __global__ __launch_bounds__(ETHREADS) void k_epi_fwd(const mep_epi_desc* __rest
             if (c == 0) { stats[2 * tok] = mean; stats[2 * tok + 1] = rstd; }
         }
     }
+    if (!(MEP_EXP & 1)) wave_store16<D>(As, LD, d.xp, r0, ntok);
 }
 
 // Backward, same mapping (one wave = 16 tokens x D): dout (+dout2) and z are read straight into
@@ -177,16 +184,56 @@ __global__ __launch_bounds__(ETHREADS) __attribute__((amdgpu_waves_per_eu(3))) v
         }
         s1 = group16_sum(s1) / (float)D;
         s2 = group16_sum(s2) / (float)D;
-        gfloat* dzr = row_ptr(bd.dz, tc);
 #pragma unroll
         for (int j = 0; j < NJ; ++j) {
             const int col = 16 * j + c;
-            const float v = ok ? rstd * (gv[j] * wj[j] - s1 - xh[j] * s2) : 0.f;
-            Gs[row * LD + col] = v;
-            if (ok) dzr[col] = v;
+            Gs[row * LD + col] = ok ? rstd * (gv[j] * wj[j] - s1 - xh[j] * s2) : 0.f;
         }
     }
-    // per-wave LayerNorm parameter partials: reduce the 4 lane groups
+    wave_lds_fence();
+    const gfloat* Wm = G<const float>(d.wm);
+    const gfloat* Wp = G<const float>(d.wp);
+    f32x4 acc[NJ], accq[NJ];
+    // dxp = drop'(dz Wm[:, D:])  (Wm[k][n] with k the output unit: NT = false) -> LDS
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) acc[j] = zero_f4();
+    wgemm16<NJ, D, false>(acc, Gs, LD, Wm + D, 2 * D, 0, false);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const int row = 4 * g + r, tok = r0 + row;
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+            const int col = 16 * j + c;
+            float v = acc[j][r];
+            if (p > 0.f) v *= drop_scale(seed, 2u * d.drop_stream, (uint64_t)tok * D + col, p);
+            Ps[row * LD + col] = tok < ntok ? v : 0.f;
+        }
+    }
+    // dq_direct = dz Wm[:, :D]
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) accq[j] = zero_f4();
+    wgemm16<NJ, D, false>(accq, Gs, LD, Wm, 2 * D, 0, false);
+    wave_lds_fence();
+    // dx = dxp Wp
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) acc[j] = zero_f4();
+    wgemm16<NJ, D, false>(acc, Ps, LD, Wp, D, 0, false);
+    // stores, after the last weight load
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const int tok = r0 + 4 * g + r;
+        if (tok >= ntok) continue;
+        gfloat* q = row_ptr(bd.dq, tok);
+        gfloat* xr = row_ptr(bd.dx, tok);
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+            const int col = 16 * j + c;
+            q[col] = bd.dq_accumulate ? q[col] + accq[j][r] : accq[j][r];
+            xr[col] = acc[j][r];
+        }
+    }
+    wave_store16<D>(Gs, LD, bd.dz, r0, ntok);
+    wave_store16<D>(Ps, LD, bd.dxp, r0, ntok);    // per-wave LayerNorm parameter partials: reduce the 4 lane groups
     if (bd.ln_partial) {
         gfloat* lp = G<float>(bd.ln_partial) + (int64_t)(blockIdx.x * EW + wave) * 2 * D;
 #pragma unroll
@@ -196,57 +243,6 @@ __global__ __launch_bounds__(ETHREADS) __attribute__((amdgpu_waves_per_eu(3))) v
             b += __shfl_xor(b, 16, 64); b += __shfl_xor(b, 32, 64);
             if (g == 0) { lp[16 * j + c] = a; lp[D + 16 * j + c] = b; }
         }
-    }
-    wave_lds_fence();
-    const gfloat* Wm = G<const float>(d.wm);
-    const gfloat* Wp = G<const float>(d.wp);
-    f32x4 acc[NJ];
-    // dq_direct = dz Wm[:, :D]      (Wm[k][n] with k the output unit: NT = false)
-#pragma unroll
-    for (int j = 0; j < NJ; ++j) acc[j] = zero_f4();
-    wgemm16<NJ, D, false>(acc, Gs, LD, Wm, 2 * D, 0, false);
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-        const int tok = r0 + 4 * g + r;
-        if (tok >= ntok) continue;
-        gfloat* q = row_ptr(bd.dq, tok);
-#pragma unroll
-        for (int j = 0; j < NJ; ++j) {
-            const int col = 16 * j + c;
-            q[col] = bd.dq_accumulate ? q[col] + acc[j][r] : acc[j][r];
-        }
-    }
-    // dxp = drop'(dz Wm[:, D:])
-#pragma unroll
-    for (int j = 0; j < NJ; ++j) acc[j] = zero_f4();
-    wgemm16<NJ, D, false>(acc, Gs, LD, Wm + D, 2 * D, 0, false);
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-        const int row = 4 * g + r, tok = r0 + row;
-        const bool ok = tok < ntok;
-        gfloat* xr = row_ptr(bd.dxp, min(tok, ntok - 1));
-#pragma unroll
-        for (int j = 0; j < NJ; ++j) {
-            const int col = 16 * j + c;
-            float v = acc[j][r];
-            if (p > 0.f) v *= drop_scale(seed, 2u * d.drop_stream, (uint64_t)tok * D + col, p);
-            v = ok ? v : 0.f;
-            Ps[row * LD + col] = v;
-            if (ok) xr[col] = v;
-        }
-    }
-    wave_lds_fence();
-    // dx = dxp Wp
-#pragma unroll
-    for (int j = 0; j < NJ; ++j) acc[j] = zero_f4();
-    wgemm16<NJ, D, false>(acc, Ps, LD, Wp, D, 0, false);
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-        const int tok = r0 + 4 * g + r;
-        if (tok >= ntok) continue;
-        gfloat* xr = row_ptr(bd.dx, tok);
-#pragma unroll
-        for (int j = 0; j < NJ; ++j) xr[16 * j + c] = acc[j][r];
     }
 }
 

@@ -256,8 +256,12 @@ MEP_DEV void wave_lds_fence() {
 
 // weight operand of k block kb for output column block j:
 //   NT: W[n][k] = W[n * ldw + k] (nn.Linear weight, forward);  else W[k][n] = W[k * ldw + n]
+#ifndef MEP_EXP
+#define MEP_EXP 0
+#endif
 template <bool NT>
 MEP_DEV float4 wfrag(const gfloat* W, int ldw, int n, int k, bool w_vec) {
+    if (MEP_EXP & 16) return make_float4(1e-3f * n, 1e-3f * k, 0.f, 1.f);   // A/B: no weight loads
     if (NT) {
         const gfloat* p = W + (int64_t)n * ldw + k;
         if (w_vec) return ldg4(p);
@@ -267,38 +271,38 @@ MEP_DEV float4 wfrag(const gfloat* W, int ldw, int n, int k, bool w_vec) {
     return make_float4(p[0], p[ldw], p[2 * ldw], p[3 * ldw]);
 }
 
-// acc[j] += A[16 x K] . W(cols n0 + 16j .. + 15)   for j < NJ (NJ even).  A: 16 rows in LDS,
-// row c at A + c * lda.  Column blocks are processed in pairs (two interleaved accumulation
-// chains hide the 40-cycle dependent-MFMA latency); the weight fragments of the next k block are
-// in flight while the current block's MFMAs issue, so only 4 float4 of weights are live.
+// acc[j] += A[16 x K] . W(cols n0 + 16j .. + 15)   for j < NJ.  A: 16 rows in LDS, row c at
+// A + c * lda.  Per 16-wide k block all NJ accumulators are advanced (4 NJ MFMAs, 128 NJ cycles
+// of MFMA issue), and the NJ weight fragments of the NEXT k block are loaded before them, so
+// one k block of MFMA work covers the L2 latency of the next block's weights.
 template <int NJ, int K, bool NT>
 MEP_DEV void wgemm16(f32x4 (&acc)[NJ], const float* A, int lda, const gfloat* W, int ldw, int n0, bool w_vec) {
-    static_assert(K % 16 == 0 && NJ % 2 == 0, "K multiple of 16, NJ even");
+    static_assert(K % 16 == 0, "K must be a multiple of 16");
     constexpr int KB = K / 16;
     const int lane = threadIdx.x & 63;
     const int c = lane & 15, g = lane >> 4;
     const float* arow = A + c * lda + 4 * g;
+    float4 b[NJ];
 #pragma unroll
-    for (int jp = 0; jp < NJ; jp += 2) {
-        const int na = n0 + 16 * jp + c, nb = na + 16;
-        float4 b0 = wfrag<NT>(W, ldw, na, 4 * g, w_vec), b1 = wfrag<NT>(W, ldw, nb, 4 * g, w_vec);
+    for (int j = 0; j < NJ; ++j) b[j] = wfrag<NT>(W, ldw, n0 + 16 * j + c, 4 * g, w_vec);
 #pragma unroll
-        for (int kb = 0; kb < KB; ++kb) {
-            float4 c0 = b0, c1 = b1;
-            if (kb + 1 < KB) {
-                b0 = wfrag<NT>(W, ldw, na, 16 * (kb + 1) + 4 * g, w_vec);
-                b1 = wfrag<NT>(W, ldw, nb, 16 * (kb + 1) + 4 * g, w_vec);
-            }
-            const float4 a = *reinterpret_cast<const float4*>(arow + 16 * kb);
-            acc[jp] = mfma16x4(a.x, c0.x, acc[jp]);
-            acc[jp + 1] = mfma16x4(a.x, c1.x, acc[jp + 1]);
-            acc[jp] = mfma16x4(a.y, c0.y, acc[jp]);
-            acc[jp + 1] = mfma16x4(a.y, c1.y, acc[jp + 1]);
-            acc[jp] = mfma16x4(a.z, c0.z, acc[jp]);
-            acc[jp + 1] = mfma16x4(a.z, c1.z, acc[jp + 1]);
-            acc[jp] = mfma16x4(a.w, c0.w, acc[jp]);
-            acc[jp + 1] = mfma16x4(a.w, c1.w, acc[jp + 1]);
+    for (int kb = 0; kb < KB; ++kb) {
+        float4 cur[NJ];
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) cur[j] = b[j];
+        if (kb + 1 < KB) {
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) b[j] = wfrag<NT>(W, ldw, n0 + 16 * j + c, 16 * (kb + 1) + 4 * g, w_vec);
         }
+        const float4 a = *reinterpret_cast<const float4*>(arow + 16 * kb);
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) acc[j] = mfma16x4(a.x, cur[j].x, acc[j]);
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) acc[j] = mfma16x4(a.y, cur[j].y, acc[j]);
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) acc[j] = mfma16x4(a.z, cur[j].z, acc[j]);
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) acc[j] = mfma16x4(a.w, cur[j].w, acc[j]);
     }
 }
 
@@ -327,6 +331,23 @@ MEP_DEV void wave_stage16(float* dst, int lda, const mep_rows& src, int r0, int 
             v = vec ? ldg4(p) : make_float4(p[0], p[1], p[2], p[3]);
         }
         *reinterpret_cast<float4*>(dst + row * lda + 4 * c4) = v;
+    }
+}
+
+// store rows [r0, r0 + 16) (those < ntok) of an LDS tile to a row view, one wave, 16-byte stores
+template <int D>
+MEP_DEV void wave_store16(const float* src, int lda, const mep_rows& dst, int r0, int ntok) {
+    const int lane = threadIdx.x & 63;
+    constexpr int V = D / 4;
+    const bool vec = ((dst.ptr & 15) == 0) && (dst.sB % 4 == 0) && (dst.sT % 4 == 0);
+    for (int idx = lane; idx < 16 * V; idx += 64) {
+        const int row = idx / V, c4 = idx - row * V;
+        const int tok = r0 + row;
+        if (tok >= ntok) continue;
+        const float4 v = *reinterpret_cast<const float4*>(src + row * lda + 4 * c4);
+        gfloat* p = row_ptr(dst, tok) + 4 * c4;
+        if (vec) stg4(p, v);
+        else { p[0] = v.x; p[1] = v.y; p[2] = v.z; p[3] = v.w; }
     }
 }
 

@@ -61,19 +61,25 @@ __global__ __launch_bounds__(256) void k_pool_fwd(const mep_pool_desc* __restric
     }
 }
 
-// elementwise over [B, T, C]: dx = dmean / T + onehot(argmax) * dmax
+// dx = dmean / T + onehot(argmax) * dmax over [B, T, C].  Workgroup = (batch row b, 16 time
+// steps); each thread keeps the pooled gradients and argmax of its columns in registers and
+// writes its columns of the 16 rows (no index division per element).
+constexpr int POOLB_T = 16;
 __global__ __launch_bounds__(256) void k_pool_bwd(const mep_pool_desc* __restrict__ descs) {
     const mep_pool_desc& d = descs[blockIdx.y];
-    const int64_t total = (int64_t)d.B * d.T * d.C;
-    const gfloat* dp = G<const float>(d.dpooled);
-    const MEP_G int* am = G<const int>(d.argmax);
-    gfloat* dx = G<float>(d.dx);
-    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
-        const int c = (int)(i % d.C);
-        const int64_t bt = i / d.C;
-        const int t = (int)(bt % d.T), b = (int)(bt / d.T);
-        const float dmean = dp[(int64_t)b * 2 * d.C + c] / (float)d.T;
-        dx[i] = (am[(int64_t)b * d.C + c] == t) ? dmean + dp[(int64_t)b * 2 * d.C + d.C + c] : dmean;
+    const int ntc = (d.T + POOLB_T - 1) / POOLB_T;
+    const int b = blockIdx.x / ntc, t0 = (blockIdx.x - b * ntc) * POOLB_T;
+    if (b >= d.B) return;
+    const int C = d.C;
+    const gfloat* dp = G<const float>(d.dpooled) + (int64_t)b * 2 * C;
+    const MEP_G int* am = G<const int>(d.argmax) + (int64_t)b * C;
+    gfloat* dx = G<float>(d.dx) + (int64_t)b * d.T * C;
+    const int t1 = min(d.T, t0 + POOLB_T);
+    for (int c = threadIdx.x; c < C; c += 256) {
+        const float dmean = dp[c] / (float)d.T;
+        const float dmax = dp[C + c];
+        const int ta = am[c];
+        for (int t = t0; t < t1; ++t) dx[(int64_t)t * C + c] = (ta == t) ? dmean + dmax : dmean;
     }
 }
 
@@ -120,11 +126,21 @@ __global__ __launch_bounds__(256) void k_head(mep_head_desc d) {
     __shared__ float s_dlast[2][NCMAX], s_dthis[2][NCMAX];
     const gfloat* wc0 = G<const float>(d.wc0);
     const gfloat* wc1 = G<const float>(d.wc1);
-    const gfloat* trans = G<const float>(d.trans);
-    const gfloat* lnw = G<const float>(d.ln_w);
-    const gfloat* lnb = G<const float>(d.ln_b);
-    const gfloat* wo = G<const float>(d.wo);
-    const gfloat* bo = G<const float>(d.bo);
+    // the small head parameters live in LDS for the whole kernel: the serial phases below read
+    // them in dependent chains, where a global (L2) latency per step would dominate
+    __shared__ float trans[NCMAX * NCMAX * NCMAX], wo[NCMAX * 2 * NCMAX], lnw[NCMAX], lnb[NCMAX], bo[NCMAX];
+    __shared__ float s_part[NCMAX * NCMAX];
+    {
+        const gfloat* g_trans = G<const float>(d.trans);
+        const gfloat* g_wo = G<const float>(d.wo);
+        for (int i = threadIdx.x; i < NC * NC * NC; i += 256) trans[i] = g_trans[i];
+        for (int i = threadIdx.x; i < 2 * NC * NC; i += 256) wo[i] = g_wo[i];
+        if (threadIdx.x < NC) {
+            lnw[threadIdx.x] = G<const float>(d.ln_w)[threadIdx.x];
+            lnb[threadIdx.x] = G<const float>(d.ln_b)[threadIdx.x];
+            bo[threadIdx.x] = G<const float>(d.bo)[threadIdx.x];
+        }
+    }
 
     // classifiers (Multi_ATTN.classifier, no bias): one wave per output, lanes over F
     for (int rr = 0; rr < rows; ++rr) {
@@ -246,15 +262,20 @@ __global__ __launch_bounds__(256) void k_head(mep_head_desc d) {
                 __shared__ float s_dy[NCMAX];
                 if (lane < NC) s_dy[lane] = dy;
                 wave_sync();
+                // dlast[m] = sum_p this[p] sum_n dy[n] trans[p][m][n]: lane (m, p) does the n sum
+                for (int idx = lane; idx < NC * NC; idx += 64) {
+                    const int m = idx / NC, p = idx - m * NC;
+                    float s = 0.f;
+                    for (int n = 0; n < NC; ++n) s = fmaf(s_dy[n], trans[(p * NC + m) * NC + n], s);
+                    s_part[idx] = s_this[rr][p] * s;
+                }
+                wave_sync();
                 if (lane < NC) {
                     float dt = dcat_this;
                     for (int n = 0; n < NC; ++n) dt = fmaf(s_dy[n], s_temp[rr][lane * NC + n], dt);
                     s_dthis[rr][lane] = dt;
                     float dl = 0.f;
-                    for (int p = 0; p < NC; ++p) {
-                        const float tp = s_this[rr][p];
-                        for (int n = 0; n < NC; ++n) dl = fmaf(tp * s_dy[n], trans[(p * NC + lane) * NC + n], dl);
-                    }
+                    for (int p = 0; p < NC; ++p) dl += s_part[lane * NC + p];
                     s_dlast[rr][lane] = dl;
                     part[o.dl0 + lane] = dl;
                     part[o.dl1 + lane] = dt;
@@ -290,37 +311,78 @@ struct HeadGrads {
     float *g_trans, *g_lnw, *g_lnb, *g_wo, *g_bo, *g_wc0, *g_wc1, *loss;
 };
 
+// Sum of the per-row head partials.  Workgroups [0, nA32): 32 columns of the small-parameter
+// records each, 8 row groups per column (+ the batch loss in workgroup 0); workgroups after
+// that: 32 columns k of one classifier e, dWc_e[n][k] = sum_b dlogit_e[b][n] pooled_e[b][k] for
+// every n, rows split over 8 groups.  Fixed summation order (deterministic).
 __global__ __launch_bounds__(256) void k_head_reduce(mep_head_desc d, HeadGrads g) {
-    const int NC = d.NC, F = d.F;
+    const int NC = d.NC, F = d.F, B = d.B;
     const HeadOff o = head_off(NC);
     const int nA = o.dl0;                 // everything before the dlogit records
-    const int nB = 2 * NC * F;
-    const int i = blockIdx.x * 256 + threadIdx.x;
+    const int nA32 = (nA + 31) / 32;
+    const int cl = threadIdx.x & 31, rg = threadIdx.x >> 5;
     const gfloat* part = G<const float>(d.partial);
-    if (i < nA) {
+    __shared__ float red[8][NCMAX][33];
+    if ((int)blockIdx.x < nA32) {
+        const int i = blockIdx.x * 32 + cl;
         float s = 0.f;
-        for (int b = 0; b < d.B; ++b) s += part[(int64_t)b * o.stride + i];
-        float* dst;
-        if (i < o.bo) dst = g.g_wo + (i - o.wo);
-        else if (i < o.lnw) dst = g.g_bo + (i - o.bo);
-        else if (i < o.lnb) dst = g.g_lnw + (i - o.lnw);
-        else if (i < o.trans) dst = g.g_lnb + (i - o.lnb);
-        else dst = g.g_trans + (i - o.trans);
-        *dst = s;
-    } else if (i < nA + nB) {
-        const int j = i - nA;
-        const int e = j / (NC * F), rem = j - e * NC * F;
-        const int n = rem / F, k = rem - n * F;
-        const float* pooled = reinterpret_cast<const float*>(e ? d.pooled1 : d.pooled0);
-        const int off = e ? o.dl1 : o.dl0;
-        float s = 0.f;
-        for (int b = 0; b < d.B; ++b) s = fmaf(part[(int64_t)b * o.stride + off + n], pooled[(int64_t)b * F + k], s);
-        (e ? g.g_wc1 : g.g_wc0)[rem] = s;
-    } else if (i == nA + nB) {
-        const gfloat* rl = G<const float>(d.row_loss);
-        float s = 0.f;
-        for (int b = 0; b < d.B; ++b) s += rl[b];
-        *g.loss = s;
+        if (i < nA)
+            for (int b = rg; b < B; b += 8) s += part[(int64_t)b * o.stride + i];
+        red[rg][0][cl] = s;
+        float ls = 0.f;
+        if (blockIdx.x == 0)
+            for (int b = threadIdx.x; b < B; b += 256) ls += G<const float>(d.row_loss)[b];
+        __syncthreads();
+        if (rg == 0 && i < nA) {
+            float t = 0.f;
+#pragma unroll
+            for (int k = 0; k < 8; ++k) t += red[k][0][cl];
+            float* dst;
+            if (i < o.bo) dst = g.g_wo + (i - o.wo);
+            else if (i < o.lnw) dst = g.g_bo + (i - o.bo);
+            else if (i < o.lnb) dst = g.g_lnw + (i - o.lnw);
+            else if (i < o.trans) dst = g.g_lnb + (i - o.lnb);
+            else dst = g.g_trans + (i - o.trans);
+            *G<float>(reinterpret_cast<uint64_t>(dst)) = t;
+        }
+        if (blockIdx.x == 0) {
+            ls = wave_sum(ls);
+            __syncthreads();
+            if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6][1][0] = ls;
+            __syncthreads();
+            if (threadIdx.x == 0)
+                *G<float>(reinterpret_cast<uint64_t>(g.loss)) = red[0][1][0] + red[1][1][0] + red[2][1][0] + red[3][1][0];
+        }
+        return;
+    }
+    const int wb = blockIdx.x - nA32;
+    const int nkb = (F + 31) / 32;
+    const int e = wb / nkb, k = (wb - e * nkb) * 32 + cl;
+    const float* pooled = reinterpret_cast<const float*>(e ? d.pooled1 : d.pooled0);
+    const int off = e ? o.dl1 : o.dl0;
+    float acc[NCMAX];
+#pragma unroll
+    for (int n = 0; n < NCMAX; ++n) acc[n] = 0.f;
+    if (k < F) {
+        for (int b = rg; b < B; b += 8) {
+            const float pk = pooled[(int64_t)b * F + k];
+            const gfloat* pr = part + (int64_t)b * o.stride + off;
+#pragma unroll
+            for (int n = 0; n < NCMAX; ++n)
+                if (n < NC) acc[n] = fmaf(pr[n], pk, acc[n]);
+        }
+    }
+#pragma unroll
+    for (int n = 0; n < NCMAX; ++n) if (n < NC) red[rg][n][cl] = acc[n];
+    __syncthreads();
+    if (k < F) {
+        float* out = e ? g.g_wc1 : g.g_wc0;
+        for (int n = rg; n < NC; n += 8) {
+            float t = 0.f;
+#pragma unroll
+            for (int q = 0; q < 8; ++q) t += red[q][n][cl];
+            *G<float>(reinterpret_cast<uint64_t>(out + (int64_t)n * F + k)) = t;
+        }
     }
 }
 
@@ -398,7 +460,7 @@ extern "C" int mep_head_reduce(const mep_head_desc* d, uint64_t g_trans, uint64_
     HeadGrads g{(float*)g_trans, (float*)g_ln_w, (float*)g_ln_b, (float*)g_wo, (float*)g_bo,
                 (float*)g_wc0, (float*)g_wc1, (float*)loss};
     const HeadOff o = head_off(d->NC);
-    const int total = o.dl0 + 2 * d->NC * d->F + 1;
-    hipLaunchKernelGGL(k_head_reduce, dim3((total + 255) / 256), dim3(256), 0, (hipStream_t)stream, *d, g);
+    const int blocks = (o.dl0 + 31) / 32 + 2 * ((d->F + 31) / 32);
+    hipLaunchKernelGGL(k_head_reduce, dim3(blocks), dim3(256), 0, (hipStream_t)stream, *d, g);
     return mep_check_launch("mep_head_reduce");
 }

@@ -324,7 +324,7 @@ class RealformerPlan:
                                                     pooled=self.pooled.data_ptr(), dpooled=self.dpooled.data_ptr(),
                                                     argmax=self.argmax.data_ptr(), B=R, T=self.Ttot, C=self.C)], dev)
         self.t_pool = R * cdiv(self.C, 32)
-        self.t_poolb = min(2048, cdiv(R * self.Ttot * self.C, 256))
+        self.t_poolb = R * cdiv(self.Ttot, 16)
         F = 2 * self.C
         self.d_fc = DescArray(GemmDesc, [GemmDesc(
             x=crows(self.pooled, 1, F), y=crows(self.fc, 1, D), w=fl.ptr(pre + 'fully_connected.weight'),

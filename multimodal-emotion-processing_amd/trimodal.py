@@ -240,7 +240,7 @@ class TriModalPlan:
                        B=B, T=self.Ttot, C=self.C) for e in range(E)]
         self.d_pool = DescArray(PoolDesc, pd, dev)
         self.t_pool = B * cdiv(self.C, 32)
-        self.t_poolb = min(2048, cdiv(B * self.Ttot * self.C, 256))
+        self.t_poolb = B * cdiv(self.Ttot, 16)
         # head
         hn = sp.head_norm
         self.head = HeadDesc(

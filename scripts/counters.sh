@@ -7,10 +7,10 @@ OUT=gpurun_out/ctr
 mkdir -p $OUT
 K=${KERNELS:-"mep_attn_fwd mep_attn_bwd"}
 timeout -k 10 120 rocprofv3 -L > $OUT/list.txt 2>&1 || true
+CTR_GROUPS=${CTR_GROUPS:-"SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY;SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_MFMA;SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_MFMA SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VMEM SQ_INST_CYCLES_VMEM SQ_WAIT_INST_LDS"}
 i=0
-for grp in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY" \
-           "SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_MFMA" \
-           "SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_MFMA SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VMEM SQ_INST_CYCLES_VMEM SQ_WAIT_INST_LDS"; do
+IFS=';' read -ra GRPS <<< "$CTR_GROUPS"
+for grp in "${GRPS[@]}"; do
   i=$((i+1))
   for k in $K; do
     timeout -k 10 300 rocprofv3 --pmc $grp --kernel-trace -d $OUT/g${i}_$k -o run --output-format csv -- python3 scripts/kbench.py --kernel $k --reps 5 > $OUT/g${i}_$k.log 2>&1
