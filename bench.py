@@ -33,19 +33,20 @@ DIMS = (300, 35, 74)
 
 
 class LaunchTimer:
-    """HIP events around every libmep launch of an eager step, on the launching stream."""
+    """HIP events around every libmep launch of an eager step, on the launching stream (the
+    backward's side-stream launches included)."""
 
     def __init__(self):
         self.ev = []
 
-    def begin(self, name):
+    def begin(self, name, stream=None):
         e = torch.cuda.Event(enable_timing=True)
-        e.record(torch.cuda.current_stream())
+        e.record(stream if stream is not None else torch.cuda.current_stream())
         self.ev.append([name, e, None])
 
-    def end(self, name):
+    def end(self, name, stream=None):
         e = torch.cuda.Event(enable_timing=True)
-        e.record(torch.cuda.current_stream())
+        e.record(stream if stream is not None else torch.cuda.current_stream())
         self.ev[-1][2] = e
 
     def totals(self):

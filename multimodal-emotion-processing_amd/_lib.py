@@ -184,18 +184,18 @@ def stream_ptr(stream=None):
     return ctypes.c_void_p(s.cuda_stream)
 
 
-# Optional per-launch timer (bench.py): an object with begin(name) / end(name) that records HIP
-# events on the launching stream.  None in normal operation.
+# Optional per-launch timer (bench.py): an object with begin(name, stream) / end(name, stream) that
+# records HIP events on the launching stream.  None in normal operation.
 TIMER = None
 
 
 def call(name, *args, stream=None):
     fn = getattr(lib(), name)
     if TIMER is not None:
-        TIMER.begin(name)
+        TIMER.begin(name, stream)
     check(fn(*args, stream_ptr(stream)), name)
     if TIMER is not None:
-        TIMER.end(name)
+        TIMER.end(name, stream)
 
 
 class DescArray:
@@ -223,12 +223,12 @@ def launch(name, descs, max_tiles, stream=None, threads=None, extra=()):
         return
     fn = getattr(lib(), name)
     if TIMER is not None:
-        TIMER.begin(name)
+        TIMER.begin(name, stream)
     ints = ([] if threads is None else [int(threads)]) + [int(x) for x in extra]
     rc = fn(descs.ptr, descs.n, int(max_tiles), *ints, stream_ptr(stream))
     check(rc, name)
     if TIMER is not None:
-        TIMER.end(name)
+        TIMER.end(name, stream)
 
 
 ATTN_PREV, ATTN_SOUT, ATTN_SHORT, ATTN_LONG = 1, 2, 4, 8   # MEP_ATTN_* (include/mep.h)
