@@ -150,7 +150,10 @@ typedef struct {
     float    drop_p;
     int32_t  drop_stream;/* distinct per block */
 } mep_epi_desc;
-/* D (32/64/96/128, shared by every descriptor of the launch) selects the compiled variant. */
+/* D (32/64/96/128, shared by every descriptor of the launch) selects the compiled variant.
+ * Geometry: max_tiles = workgroups PER DESCRIPTOR; each workgroup (512 threads) stages its block's
+ * weights in LDS once and processes a contiguous range of ceil(ceil(ntok/16) / max_tiles)
+ * 16-token tiles.  Row views must be 16-byte aligned (ptr, sB, sT multiples of 4 floats). */
 int mep_block_epi_fwd(const mep_epi_desc* descs, int n_desc, int max_tiles, int D, mep_stream_t stream);
 
 /* Backward: dout -> (dropout) -> LN backward -> dz;  dq_direct = dz Wm[:, :D];

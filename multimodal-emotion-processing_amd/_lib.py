@@ -259,6 +259,17 @@ def attn_bwd_flags(bdescs):
            (ATTN_SOUT if _uniform([b.ds_next != 0 for b in bdescs], 'ds_next') else 0)
 
 
+N_CU = 256   # MI355X compute units
+
+
+def epi_grid(ntok_max, n_desc):
+    """Workgroups per descriptor of mep_block_epi_fwd / _bwd (csrc/block.hip): each workgroup
+    owns a contiguous range of 16-token tiles of one block and stages that block's weights once,
+    so the grid is sized to one workgroup per CU over all descriptors (never more workgroups than
+    tiles)."""
+    return max(1, min(-(-ntok_max // 16), N_CU // max(1, n_desc)))
+
+
 def attn_dc_slots(B, H, Tk):
     """floats of the backward's dc_partial (one per wave task)"""
     return B * H * -(-Tk // 64)

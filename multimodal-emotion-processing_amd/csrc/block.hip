@@ -2,247 +2,297 @@
 //
 // Forward (cmu-mosei/run.py:257-261; Ren-MME/run.py:209-213 with dropout and norm2):
 //   xp = drop(x Wp^T);  z = [q | xp] Wm^T;  out = drop(LayerNorm(z))
-// One workgroup = 64 tokens x D columns (D in {32, 64, 96, 128}, a template parameter so every
-// K loop is fully unrolled and hipcc issues the weight loads of a whole chain ahead of its
-// MFMAs), 8 waves; each wave owns one 32x32 output block of the (2 x D/32) task grid and runs
-// f32 MFMA 32x32x2 over LDS-staged token tiles with the weights read from L2.  The two Linears
-// are chained through LDS (xp is consumed before it ever returns from HBM) and the LayerNorm is
-// a wave-per-row shuffle reduction.  The concat [q | xp] is never materialised: the minus
-// Linear is two accumulating MFMA passes.
+// Backward: LayerNorm backward, dq_direct = dz Wm[:, :D], dxp = drop'(dz Wm[:, D:]), dx = dxp Wp.
+// Weight-stationary: a workgroup (8 waves) owns a contiguous range of 16-token tiles of ONE
+// block and keeps that block's weights in LDS; each wave runs whole tiles through all products on
+// exact fp32 MFMA in the transposed-tile formulation (common.h), so activations never pass
+// through LDS and the concat [q | xp] is two accumulating passes.
 #include "common.h"
 
 using namespace mep;
 
 namespace {
 
-constexpr int THREADS = 512;
 constexpr float LN_EPS = 1e-5f;
+constexpr int EWAVES = 8;                 // waves per workgroup of the epilogues
+constexpr int ETHREADS = 64 * EWAVES;
 
-MEP_DEV bool vec_ok(uint64_t p, int ld) { return ((p & 15) == 0) && (ld % 4 == 0); }
-
-// stage 64 token rows x D columns of a row view into LDS [64][D+4]
+// LDS geometry: the fp32 weights of one block stay resident in LDS for the whole workgroup:
+// forward Wm (and Wp for D <= 96), backward Wm^T (and Wp^T for D <= 96) -- at most 135 KB; for
+// D = 128 the Wp operand is read from L2.  Rows are padded by 4 floats so the 16 rows of a
+// fragment read (lanes c = 0..15, one float4 each) fall in 16 distinct bank groups.
 template <int D>
-MEP_DEV void stage(float* dst, const mep_rows& src, int tok0, int ntok) {
-    constexpr int LD = D + 4;
-    constexpr int V = D / 4;  // float4 per row
-    const bool vec = ((src.ptr & 15) == 0) && (src.sB % 4 == 0) && (src.sT % 4 == 0);
-    for (int idx = threadIdx.x; idx < 64 * V; idx += THREADS) {
-        const int row = idx / V, c4 = idx - row * V;
-        const int tok = tok0 + row;
-        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (tok < ntok) {
-            const gfloat* p = row_ptr(src, tok) + 4 * c4;
-            if (vec) v = ldg4(p);
-            else v = make_float4(p[0], p[1], p[2], p[3]);
-        }
-        *reinterpret_cast<float4*>(dst + row * LD + 4 * c4) = v;
+struct EpiGeo {
+    static constexpr bool WP_LDS = D <= 96;
+    static constexpr int LP = D + 4;       // D-wide rows
+    static constexpr int LM = 2 * D + 4;   // 2D-wide rows
+    static constexpr int FWD = D * LM + (WP_LDS ? D * LP : 0);
+    static constexpr int BWD = 2 * D * LP + (WP_LDS ? D * LP : 0);
+};
+
+// W [R][C] (row stride C, 16-byte rows) -> LDS rows of stride L
+MEP_DEV void stage_rows(lfloat* dst, int L, const gfloat* src, int R, int C) {
+    const int n4 = C >> 2;
+    for (int idx = threadIdx.x; idx < R * n4; idx += ETHREADS) {
+        const int r = idx / n4, c4 = idx - r * n4;
+        *reinterpret_cast<lf32x4*>(dst + r * L + 4 * c4) = *reinterpret_cast<const MEP_G f32x4*>(src + r * C + 4 * c4);
+    }
+}
+// W [R][C] -> W^T in LDS rows of stride L (row c = column c of W); lanes run along C (coalesced reads)
+MEP_DEV void stage_cols_t(lfloat* dst, int L, const gfloat* src, int R, int C) {
+    for (int idx = threadIdx.x; idx < R * C; idx += ETHREADS) {
+        const int r = idx / C, c = idx - r * C;
+        dst[c * L + r] = src[idx];
     }
 }
 
-// MEP_EXP (development A/B builds only; 0 in the product): 1 = no HBM stores, 2 = no MFMA,
-// 4 = no staging loads, 8 = no LayerNorm math, 16 = no weight loads (common.h wfrag)
-constexpr int EW = 4;               // waves per workgroup of the forward epilogue
-constexpr int ETHREADS = 64 * EW;
+MEP_DEV float4 f4(const f32x4 v) { return make_float4(v[0], v[1], v[2], v[3]); }
 
-// One WAVE = 16 tokens x all D columns, four independent waves per workgroup (no block
-// barriers).  Both Linears are wave-level 16-row GEMMs (wgemm16: v_mfma_f32_16x16x4_f32, the
-// weight fragments of the next k block in flight during the current one); the LayerNorm runs on
-// the accumulators in registers (row sums over the D/16 column blocks a lane holds + a 16-lane
-// shuffle reduction).  LDS holds this wave's A operands: x (then xp) and q.  Every HBM store is
-// issued after the last weight load: s_waitcnt vmcnt counts loads and stores together in issue
-// order, so a store in flight would delay every later weight fragment.
-template <int D>
-__global__ __launch_bounds__(ETHREADS) void k_epi_fwd(const mep_epi_desc* __restrict__ descs) {
-    const mep_epi_desc& d = descs[blockIdx.y];
+// tiles [t_begin, t_end) of 16 tokens owned by this workgroup (contiguous range per workgroup)
+MEP_DEV bool tile_range(int ntok, int& t_begin, int& t_end) {
+    const int ntiles = (ntok + 15) >> 4;
+    const int per = (ntiles + (int)gridDim.x - 1) / (int)gridDim.x;
+    t_begin = blockIdx.x * per;
+    t_end = min(ntiles, t_begin + per);
+    return t_begin < t_end;
+}
+
+// ---------------------------------------------------------------- forward
+// Per tile of 16 tokens (common.h, transposed tiles): xp^T = Wp x^T, then z^T = Wm [q | xp]^T
+// with the xp accumulators as the B operand of the second product; LayerNorm on the
+// accumulators.  x and q rows are read straight from HBM into B fragments (no LDS).
+template <int D, typename AP, typename AM>
+MEP_DEV void epi_fwd_tiles(const mep_epi_desc& d, const AP& wp, const AM& wm, int t_begin, int t_end) {
+    constexpr int NI = D / 16, KB = D / 16;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int c = lane & 15, g = lane >> 4;
     const int ntok = d.ntok;
-    const int r0 = blockIdx.x * 64 + wave * 16;
-    if (r0 >= ntok) return;   // whole wave; only wave-private LDS below
-    constexpr int LD = D + 4, NJ = D / 16;
-    __shared__ __attribute__((aligned(16))) float smem[EW][2][16 * LD];
-    float* As = smem[wave][0];   // x, then xp (post-dropout)
-    float* Qs = smem[wave][1];   // q
     const float p = d.drop_p;
     const uint64_t seed = (d.seed && p > 0.f) ? *G<const uint64_t>(d.seed) : 0;
-    const gfloat* Wp = G<const float>(d.wp);
-    const gfloat* Wm = G<const float>(d.wm);
-
-    if (!(MEP_EXP & 4)) {
-        wave_stage16<D>(As, LD, d.x, r0, ntok);
-        wave_stage16<D>(Qs, LD, d.q, r0, ntok);
-    }
-    wave_lds_fence();
-    f32x4 acc[NJ];
-#pragma unroll
-    for (int j = 0; j < NJ; ++j) acc[j] = zero_f4();
-    if (!(MEP_EXP & 2)) wgemm16<NJ, D, true>(acc, As, LD, Wp, D, 0, vec_ok(d.wp, D));
-    wave_lds_fence();   // every lane is done reading x
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-        const int row = 4 * g + r, tok = r0 + row;
-#pragma unroll
-        for (int j = 0; j < NJ; ++j) {
-            const int col = 16 * j + c;
-            float v = acc[j][r];
-            if (p > 0.f) v *= drop_scale(seed, 2u * d.drop_stream, (uint64_t)tok * D + col, p);
-            As[row * LD + col] = v;
-        }
-    }
-    wave_lds_fence();
-#pragma unroll
-    for (int j = 0; j < NJ; ++j) acc[j] = zero_f4();
-    const bool wv = vec_ok(d.wm, 2 * D);
-    if (!(MEP_EXP & 2)) {
-        wgemm16<NJ, D, true>(acc, Qs, LD, Wm, 2 * D, 0, wv);       // [q | xp] Wm^T: q half
-        wgemm16<NJ, D, true>(acc, As, LD, Wm + D, 2 * D, 0, wv);   //                xp half
-    }
-    // LayerNorm on the accumulators; then every store
-    const gfloat* lw = G<const float>(d.ln_w);
-    const gfloat* lb = G<const float>(d.ln_b);
     gfloat* stats = G<float>(d.stats);
-    float wj[NJ], bj[NJ];
+    AM wm_x = wm;
+    wm_x.pos0 += D;                     // Wm[:, D:], the xp half of the concat
+    for (int tile = t_begin + wave; tile < t_end; tile += EWAVES) {
+        const int tok = tile * 16 + c;
+        const bool ok = tok < ntok;
+        const int tc = min(tok, ntok - 1);
+        const gfloat* xr = row_ptr(d.x, tc) + 4 * g;
+        const gfloat* qr = row_ptr(d.q, tc) + 4 * g;
+        f32x4 xp[NI], z[NI];
 #pragma unroll
-    for (int j = 0; j < NJ; ++j) { wj[j] = lw[16 * j + c]; bj[j] = lb[16 * j + c]; }
+        for (int i = 0; i < NI; ++i) { xp[i] = zero_f4(); z[i] = zero_f4(); }
+        tgemm<NI, KB>(xp, wp, [&](int kb) { return ld4w(xr + 16 * kb); });
+        if (p > 0.f) {
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-        const int tok = r0 + 4 * g + r;
-        float s = 0.f;
+            for (int i = 0; i < NI; ++i)
 #pragma unroll
-        for (int j = 0; j < NJ; ++j) s += acc[j][r];
-        const float mean = group16_sum(s) / (float)D;
-        float q = 0.f;
+                for (int r = 0; r < 4; ++r)
+                    xp[i][r] *= drop_scale(seed, 2u * d.drop_stream, (uint64_t)tok * D + 16 * i + 4 * g + r, p);
+        }
+        tgemm<NI, KB>(z, wm, [&](int kb) { return ld4w(qr + 16 * kb); });   // q half of [q | xp]
+        tgemm<NI, KB>(z, wm_x, [&](int kb) { return xp[kb]; });            // xp half
+        // LayerNorm over the D features of token c: in-lane sum + the 4 lane groups
+        float sum = 0.f;
 #pragma unroll
-        for (int j = 0; j < NJ; ++j) { const float t = acc[j][r] - mean; q += t * t; }
-        const float rstd = (MEP_EXP & 8) ? 1.f : 1.0f / sqrtf(group16_sum(q) / (float)D + LN_EPS);
-        if ((MEP_EXP & 1) ? tok < 0 : tok < ntok) {
+        for (int i = 0; i < NI; ++i) sum += (z[i][0] + z[i][1]) + (z[i][2] + z[i][3]);
+        sum += __shfl_xor(sum, 16, 64);
+        sum += __shfl_xor(sum, 32, 64);
+        const float mean = sum / (float)D;
+        float var = 0.f;
+#pragma unroll
+        for (int i = 0; i < NI; ++i)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) { const float t = z[i][r] - mean; var += t * t; }
+        var += __shfl_xor(var, 16, 64);
+        var += __shfl_xor(var, 32, 64);
+        const float rstd = 1.0f / sqrtf(var / (float)D + LN_EPS);
+        if (ok) {
             gfloat* zr = row_ptr(d.z, tok);
             gfloat* orow = row_ptr(d.out, tok);
+            gfloat* pr = row_ptr(d.xp, tok);
 #pragma unroll
-            for (int j = 0; j < NJ; ++j) {
-                const int col = 16 * j + c;
-                zr[col] = acc[j][r];
-                float y = (acc[j][r] - mean) * rstd * wj[j] + bj[j];
-                if (p > 0.f) y *= drop_scale(seed, 2u * d.drop_stream + 1u, (uint64_t)tok * D + col, p);
-                orow[col] = y;
+            for (int i = 0; i < NI; ++i) {
+                const int col = 16 * i + 4 * g;
+                const f32x4 w = ld4w(G<const float>(d.ln_w) + col), b = ld4w(G<const float>(d.ln_b) + col);
+                f32x4 y;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    y[r] = (z[i][r] - mean) * rstd * w[r] + b[r];
+                    if (p > 0.f) y[r] *= drop_scale(seed, 2u * d.drop_stream + 1u, (uint64_t)tok * D + col + r, p);
+                }
+                stg4(zr + col, f4(z[i]));
+                stg4(orow + col, f4(y));
+                stg4(pr + col, f4(xp[i]));
             }
-            if (c == 0) { stats[2 * tok] = mean; stats[2 * tok + 1] = rstd; }
+            if (g == 0) { stats[2 * tok] = mean; stats[2 * tok + 1] = rstd; }
         }
     }
-    if (!(MEP_EXP & 1)) wave_store16<D>(As, LD, d.xp, r0, ntok);
 }
 
-// Backward, same mapping (one wave = 16 tokens x D): dout (+dout2) and z are read straight into
-// the accumulator layout, the LayerNorm backward runs in registers, dz is staged once in LDS as
-// the A operand of dq_direct = dz Wm[:, :D] and dxp = drop'(dz Wm[:, D:]), and dxp (LDS) of
-// dx = dxp Wp.  ln_partial gets one [2][D] row per 16-token wave (no block barrier anywhere).
 template <int D>
-__global__ __launch_bounds__(ETHREADS) __attribute__((amdgpu_waves_per_eu(3))) void k_epi_bwd(const mep_epi_bwd_desc* __restrict__ descs) {
-    const mep_epi_bwd_desc& bd = descs[blockIdx.y];
+__global__ __launch_bounds__(ETHREADS) void k_epi_fwd(const mep_epi_desc* __restrict__ descs) {
+    using Geo = EpiGeo<D>;
+    const mep_epi_desc& d = descs[blockIdx.y];
+    int t_begin, t_end;
+    if (!tile_range(d.ntok, t_begin, t_end)) return;   // whole workgroup
+    __shared__ __attribute__((aligned(16))) float smem[Geo::FWD];
+    lfloat* wm = (lfloat*)&smem[0];
+    stage_rows(wm, Geo::LM, G<const float>(d.wm), D, 2 * D);
+    const WRows<lfloat> am{wm, Geo::LM, 0, 0};
+    if constexpr (Geo::WP_LDS) {
+        lfloat* wp = wm + D * Geo::LM;
+        stage_rows(wp, Geo::LP, G<const float>(d.wp), D, D);
+        __syncthreads();
+        epi_fwd_tiles<D>(d, WRows<lfloat>{wp, Geo::LP, 0, 0}, am, t_begin, t_end);
+    } else {
+        __syncthreads();
+        epi_fwd_tiles<D>(d, WRows<gfloat>{G<const float>(d.wp), D, 0, 0}, am, t_begin, t_end);
+    }
+}
+
+// ---------------------------------------------------------------- backward
+// Same mapping.  dout (+dout2) and z are read straight into the accumulator layout, the
+// LayerNorm backward runs in registers, and dz^T feeds the three products directly:
+// dxp^T = Wm[:, D:]^T dz^T (rows D.. of Wm^T), dq^T = Wm[:, :D]^T dz^T and dx^T = Wp^T dxp^T.
+// LayerNorm parameter partials: per tile, sums over its 16 tokens (DPP row reductions) into the
+// tile's ln_partial row [2][D].  For D = 128 the dq / dx products run in two halves of output
+// tiles so the live accumulators stay within the register budget.
+template <int NI, int KB, int NH, typename AF, typename BF, typename ST>
+MEP_DEV void tgemm_store(AF afr, BF&& bfr, ST&& store) {
+    constexpr int NS = NI / NH;
+#pragma unroll
+    for (int h = 0; h < NH; ++h) {
+        f32x4 acc[NS];
+#pragma unroll
+        for (int i = 0; i < NS; ++i) acc[i] = zero_f4();
+        AF a = afr;
+        a.row0 += 16 * NS * h;
+        tgemm<NS, KB>(acc, a, bfr);
+#pragma unroll
+        for (int i = 0; i < NS; ++i) store(NS * h + i, acc[i]);
+    }
+}
+
+template <int D, typename AM, typename AP>
+MEP_DEV void epi_bwd_tiles(const mep_epi_bwd_desc& bd, const AM& wmt, const AP& wpt, int t_begin, int t_end) {
+    constexpr int NI = D / 16, KB = D / 16, NH = D > 96 ? 2 : 1;
     const mep_epi_desc& d = bd.f;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int c = lane & 15, g = lane >> 4;
     const int ntok = d.ntok;
-    const int r0 = blockIdx.x * 64 + wave * 16;
-    if (r0 >= ntok) return;
-    constexpr int LD = D + 4, NJ = D / 16;
-    __shared__ __attribute__((aligned(16))) float smem[EW][2][16 * LD];
-    float* Gs = smem[wave][0];   // dz
-    float* Ps = smem[wave][1];   // dxp
     const float p = d.drop_p;
     const uint64_t seed = (d.seed && p > 0.f) ? *G<const uint64_t>(d.seed) : 0;
-    const gfloat* lw = G<const float>(d.ln_w);
+    AM wmt_x = wmt;
+    wmt_x.row0 += D;                    // rows D.. of Wm^T = Wm[:, D:]
     const gfloat* stats = G<const float>(d.stats);
-    float wj[NJ], pw[NJ], pb[NJ];
-#pragma unroll
-    for (int j = 0; j < NJ; ++j) { wj[j] = lw[16 * j + c]; pw[j] = 0.f; pb[j] = 0.f; }
-    // LayerNorm backward per row of this lane (rows 4g + r); not unrolled: bounds live registers
-#pragma unroll 1
-    for (int r = 0; r < 4; ++r) {
-        const int row = 4 * g + r, tok = r0 + row;
+    gfloat* lpart = G<float>(bd.ln_partial);
+    for (int tile = t_begin + wave; tile < t_end; tile += EWAVES) {
+        const int tok = tile * 16 + c;
         const bool ok = tok < ntok;
         const int tc = min(tok, ntok - 1);
         const gfloat* gr = row_ptr(bd.dout, tc);
         const gfloat* g2 = bd.dout2.ptr ? row_ptr(bd.dout2, tc) : nullptr;
         const gfloat* zr = row_ptr(d.z, tc);
         const float mean = stats[2 * tc], rstd = stats[2 * tc + 1];
-        float gv[NJ], xh[NJ], s1 = 0.f, s2 = 0.f;
+        f32x4 dz[NI];                   // g * w first, dz after the row sums
+        float s1 = 0.f, s2 = 0.f;
+        gfloat* lp = lpart ? lpart + (int64_t)tile * 2 * D : nullptr;
 #pragma unroll
-        for (int j = 0; j < NJ; ++j) {
-            const int col = 16 * j + c;
-            float gg = gr[col];
-            if (g2) gg += g2[col];
-            if (p > 0.f) gg *= drop_scale(seed, 2u * d.drop_stream + 1u, (uint64_t)tok * D + col, p);
-            gg = ok ? gg : 0.f;
-            gv[j] = gg;
-            xh[j] = (zr[col] - mean) * rstd;
-            const float gw = gg * wj[j];
-            s1 += gw;
-            s2 += gw * xh[j];
-            pw[j] += gg * xh[j];
-            pb[j] += gg;
-        }
-        s1 = group16_sum(s1) / (float)D;
-        s2 = group16_sum(s2) / (float)D;
+        for (int i = 0; i < NI; ++i) {
+            const int col = 16 * i + 4 * g;
+            f32x4 a = ld4w(gr + col);
+            if (g2) a += ld4w(g2 + col);
+            const f32x4 zz = ld4w(zr + col), w = ld4w(G<const float>(d.ln_w) + col);
+            f32x4 pw, pb;
 #pragma unroll
-        for (int j = 0; j < NJ; ++j) {
-            const int col = 16 * j + c;
-            Gs[row * LD + col] = ok ? rstd * (gv[j] * wj[j] - s1 - xh[j] * s2) : 0.f;
+            for (int r = 0; r < 4; ++r) {
+                float gg = a[r];
+                if (p > 0.f) gg *= drop_scale(seed, 2u * d.drop_stream + 1u, (uint64_t)tok * D + col + r, p);
+                gg = ok ? gg : 0.f;
+                const float x = (zz[r] - mean) * rstd;
+                const float gw = gg * w[r];
+                s1 += gw;
+                s2 += gw * x;
+                pw[r] = row16_sum(gg * x);
+                pb[r] = row16_sum(gg);
+                dz[i][r] = gw;
+            }
+            if (lp && c == 0) {
+                stg4(lp + col, f4(pw));
+                stg4(lp + D + col, f4(pb));
+            }
         }
+        s1 += __shfl_xor(s1, 16, 64);
+        s1 += __shfl_xor(s1, 32, 64);
+        s2 += __shfl_xor(s2, 16, 64);
+        s2 += __shfl_xor(s2, 32, 64);
+        s1 /= (float)D;
+        s2 /= (float)D;
+        // dz = rstd * (g w - s1 - x-hat s2), x-hat recomputed from z (L1-hot) instead of kept live
+#pragma unroll
+        for (int i = 0; i < NI; ++i) {
+            const f32x4 zz = ld4w(zr + 16 * i + 4 * g);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const float x = (zz[r] - mean) * rstd;
+                dz[i][r] = ok ? rstd * (dz[i][r] - s1 - x * s2) : 0.f;
+            }
+        }
+        // dxp^T = Wm[:, D:]^T dz^T, then the xp dropout mask
+        f32x4 dxp[NI];
+#pragma unroll
+        for (int i = 0; i < NI; ++i) dxp[i] = zero_f4();
+        tgemm<NI, KB>(dxp, wmt_x, [&](int kb) { return dz[kb]; });
+        if (p > 0.f) {
+#pragma unroll
+            for (int i = 0; i < NI; ++i)
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                    dxp[i][r] *= drop_scale(seed, 2u * d.drop_stream, (uint64_t)tok * D + 16 * i + 4 * g + r, p);
+        }
+        if (ok) {
+            gfloat* dzr = row_ptr(bd.dz, tok);
+            gfloat* dpr = row_ptr(bd.dxp, tok);
+#pragma unroll
+            for (int i = 0; i < NI; ++i) {
+                stg4(dzr + 16 * i + 4 * g, f4(dz[i]));
+                stg4(dpr + 16 * i + 4 * g, f4(dxp[i]));
+            }
+        }
+        // dq^T (direct part) = Wm[:, :D]^T dz^T
+        gfloat* qrw = row_ptr(bd.dq, tc);
+        tgemm_store<NI, KB, NH>(wmt, [&](int kb) { return dz[kb]; }, [&](int i, f32x4 v) {
+            if (!ok) return;
+            if (bd.dq_accumulate) v += ld4w(qrw + 16 * i + 4 * g);
+            stg4(qrw + 16 * i + 4 * g, f4(v));
+        });
+        // dx^T = Wp^T dxp^T
+        gfloat* xrw = row_ptr(bd.dx, tc);
+        tgemm_store<NI, KB, NH>(wpt, [&](int kb) { return dxp[kb]; }, [&](int i, f32x4 v) {
+            if (ok) stg4(xrw + 16 * i + 4 * g, f4(v));
+        });
     }
-    wave_lds_fence();
-    const gfloat* Wm = G<const float>(d.wm);
-    const gfloat* Wp = G<const float>(d.wp);
-    f32x4 acc[NJ], accq[NJ];
-    // dxp = drop'(dz Wm[:, D:])  (Wm[k][n] with k the output unit: NT = false) -> LDS
-#pragma unroll
-    for (int j = 0; j < NJ; ++j) acc[j] = zero_f4();
-    wgemm16<NJ, D, false>(acc, Gs, LD, Wm + D, 2 * D, 0, false);
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-        const int row = 4 * g + r, tok = r0 + row;
-#pragma unroll
-        for (int j = 0; j < NJ; ++j) {
-            const int col = 16 * j + c;
-            float v = acc[j][r];
-            if (p > 0.f) v *= drop_scale(seed, 2u * d.drop_stream, (uint64_t)tok * D + col, p);
-            Ps[row * LD + col] = tok < ntok ? v : 0.f;
-        }
-    }
-    // dq_direct = dz Wm[:, :D]
-#pragma unroll
-    for (int j = 0; j < NJ; ++j) accq[j] = zero_f4();
-    wgemm16<NJ, D, false>(accq, Gs, LD, Wm, 2 * D, 0, false);
-    wave_lds_fence();
-    // dx = dxp Wp
-#pragma unroll
-    for (int j = 0; j < NJ; ++j) acc[j] = zero_f4();
-    wgemm16<NJ, D, false>(acc, Ps, LD, Wp, D, 0, false);
-    // stores, after the last weight load
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-        const int tok = r0 + 4 * g + r;
-        if (tok >= ntok) continue;
-        gfloat* q = row_ptr(bd.dq, tok);
-        gfloat* xr = row_ptr(bd.dx, tok);
-#pragma unroll
-        for (int j = 0; j < NJ; ++j) {
-            const int col = 16 * j + c;
-            q[col] = bd.dq_accumulate ? q[col] + accq[j][r] : accq[j][r];
-            xr[col] = acc[j][r];
-        }
-    }
-    wave_store16<D>(Gs, LD, bd.dz, r0, ntok);
-    wave_store16<D>(Ps, LD, bd.dxp, r0, ntok);    // per-wave LayerNorm parameter partials: reduce the 4 lane groups
-    if (bd.ln_partial) {
-        gfloat* lp = G<float>(bd.ln_partial) + (int64_t)(blockIdx.x * EW + wave) * 2 * D;
-#pragma unroll
-        for (int j = 0; j < NJ; ++j) {
-            float a = pw[j], b = pb[j];
-            a += __shfl_xor(a, 16, 64); a += __shfl_xor(a, 32, 64);
-            b += __shfl_xor(b, 16, 64); b += __shfl_xor(b, 32, 64);
-            if (g == 0) { lp[16 * j + c] = a; lp[D + 16 * j + c] = b; }
-        }
+}
+
+template <int D>
+__global__ __launch_bounds__(ETHREADS) void k_epi_bwd(const mep_epi_bwd_desc* __restrict__ descs) {
+    using Geo = EpiGeo<D>;
+    const mep_epi_bwd_desc& bd = descs[blockIdx.y];
+    const mep_epi_desc& d = bd.f;
+    int t_begin, t_end;
+    if (!tile_range(d.ntok, t_begin, t_end)) return;
+    __shared__ __attribute__((aligned(16))) float smem[Geo::BWD];
+    lfloat* wmt = (lfloat*)&smem[0];              // Wm^T [2D][LP]
+    stage_cols_t(wmt, Geo::LP, G<const float>(d.wm), D, 2 * D);
+    const WRows<lfloat> am{wmt, Geo::LP, 0, 0};
+    if constexpr (Geo::WP_LDS) {
+        lfloat* wpt = wmt + 2 * D * Geo::LP;      // Wp^T [D][LP]
+        stage_cols_t(wpt, Geo::LP, G<const float>(d.wp), D, D);
+        __syncthreads();
+        epi_bwd_tiles<D>(bd, am, WRows<lfloat>{wpt, Geo::LP, 0, 0}, t_begin, t_end);
+    } else {
+        __syncthreads();
+        epi_bwd_tiles<D>(bd, am, WCols{G<const float>(d.wp), D, 0, 0}, t_begin, t_end);
     }
 }
 

@@ -306,6 +306,75 @@ MEP_DEV void wgemm16(f32x4 (&acc)[NJ], const float* A, int lda, const gfloat* W,
     }
 }
 
+// ------------------------------------------------------------------ transposed 16-token tiles
+// Products over a tile of 16 tokens are formed TRANSPOSED: Y^T = W X^T with the output features
+// on the MFMA rows and the tokens on its columns (v_mfma_f32_16x16x4_f32, exact fp32).  Lane
+// (c = lane & 15, g = lane >> 4) then holds features 16i + 4g .. +3 of token c in accumulator i,
+// which is exactly the B operand of the next product over those features (k block i, k = 4g + s),
+// so chained Linears pass activations in registers; a token's row statistics are an in-lane sum
+// plus two shuffles, and its stores are 16-byte stores.  Weights are the A operand, read as one
+// float4 (4 consecutive k of row 16i + c) per (output tile, k block) from LDS or global memory.
+typedef __attribute__((address_space(3))) float lfloat;
+typedef __attribute__((address_space(3))) f32x4 lf32x4;
+
+MEP_DEV f32x4 ld4w(const lfloat* p) { return *reinterpret_cast<const lf32x4*>(p); }
+MEP_DEV f32x4 ld4w(const gfloat* p) { return *reinterpret_cast<const MEP_G f32x4*>(p); }
+
+// acc[i] (i < NI) += sum over KB k blocks of A_i,kb[c][4g + s] * B_kb[4g + s][c]:
+// afr(i, kb) yields the lane's A values (row 16i + c of the weight operand, k = 16kb + 4g + s),
+// bfr(kb) its B values (token c, k = 16kb + 4g + s).  The NI A fragments of a k block are read
+// before its 4*NI MFMAs, which are issued s-major so consecutive MFMAs never chain on one
+// accumulator.
+template <int NI, int KB, typename AF, typename BF>
+MEP_DEV void tgemm(f32x4 (&acc)[NI], AF&& afr, BF&& bfr) {
+#pragma unroll
+    for (int kb = 0; kb < KB; ++kb) {
+        const f32x4 b = bfr(kb);
+        f32x4 a[NI];
+#pragma unroll
+        for (int i = 0; i < NI; ++i) a[i] = afr(i, kb);
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+#pragma unroll
+            for (int i = 0; i < NI; ++i) acc[i] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i][s], b[s], acc[i], 0, 0, 0);
+        // keep the next block's fragment reads behind this block's MFMAs (a fully hoisted,
+        // fully unrolled product holds 4 * NI * KB fragment VGPRs)
+        __builtin_amdgcn_sched_barrier(0);
+    }
+}
+
+// A accessors of tgemm over a weight W [R][C] (row stride ld):
+//   rows of W     : A row n = W row row0 + n, k = W column pos0 + k        (x W^T)
+//   rows of W^T   : A row n = W column row0 + n, k = W row pos0 + k        (dy W)
+template <typename T>
+struct WRows {
+    const T* w;
+    int ld, row0, pos0;
+    MEP_DEV f32x4 operator()(int i, int kb) const {
+        const int lane = threadIdx.x & 63;
+        return ld4w(w + (row0 + 16 * i + (lane & 15)) * ld + pos0 + 16 * kb + 4 * (lane >> 4));
+    }
+};
+struct WCols {
+    const gfloat* w;
+    int ld, row0, pos0;
+    MEP_DEV f32x4 operator()(int i, int kb) const {
+        const int lane = threadIdx.x & 63;
+        const gfloat* p = w + (pos0 + 16 * kb + 4 * (lane >> 4)) * ld + row0 + 16 * i + (lane & 15);
+        return f32x4{p[0], p[ld], p[2 * ld], p[3 * ld]};
+    }
+};
+
+// sum over the 16 lanes of a DPP row (lanes sharing g = lane >> 4), result in every lane: quad
+// butterflies (xor 1, xor 2), then the half-row and row mirrors pair the quads
+MEP_DEV float row16_sum(float v) {
+    v += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0xB1, 0xF, 0xF, false));
+    v += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x4E, 0xF, 0xF, false));
+    v += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x141, 0xF, 0xF, false));
+    v += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x140, 0xF, 0xF, false));
+    return v;
+}
+
 // sum over the 16 lanes of a lane group (lanes sharing g = lane >> 4)
 MEP_DEV float group16_sum(float v) {
     v += __shfl_xor(v, 1, 64);

@@ -16,7 +16,9 @@ from .trimodal import cdiv, crows, make_wgrad
 
 
 def _c(t):
-    return t.contiguous().float()
+    """contiguous fp32 with a 16-byte aligned base (the kernels read rows with 16-byte loads)"""
+    t = t.contiguous().float()
+    return t if t.data_ptr() % 16 == 0 else t.clone()
 
 
 def _wgrad(items, dev):
@@ -43,6 +45,7 @@ class _BlockFn(torch.autograd.Function):
         ad = AttnDesc(q=crows(q, Tq, D), k=crows(k, Tk, D), v=crows(v, Tk, D), x=crows(X, Tq, D),
                       mask=mask.data_ptr(), mask_sB=Tk, s_prev=sp.data_ptr() if sp is not None else 0,
                       c=c.data_ptr(), s_out=S.data_ptr(), stats=astat.data_ptr(), B=B, H=H, Tq=Tq, Tk=Tk)
+        wp, wm = _c(wp), _c(wm)
         ed = EpiDesc(q=crows(q, Tq, D), x=crows(X, Tq, D), xp=crows(XP, Tq, D), z=crows(Z, Tq, D),
                      out=crows(out, Tq, D), wp=wp.data_ptr(), wm=wm.data_ptr(), ln_w=lnw.data_ptr(),
                      ln_b=lnb.data_ptr(), stats=estat.data_ptr(), seed=0, ntok=B * Tq, D=D, drop_p=0.0,
@@ -50,7 +53,7 @@ class _BlockFn(torch.autograd.Function):
         a_arr, e_arr = DescArray(AttnDesc, [ad], dev), DescArray(EpiDesc, [ed], dev)
         geo = _lib.attn_geometry([ad])
         launch('mep_attn_fwd', a_arr, geo[0], threads=geo[2])
-        launch('mep_block_epi_fwd', e_arr, cdiv(B * Tq, 64), threads=D)
+        launch('mep_block_epi_fwd', e_arr, _lib.epi_grid(B * Tq, 1), threads=D)
         ctx.save_for_backward(q, k, v, mask, X, XP, Z, S, astat, estat, c, wp, wm, lnw, lnb)
         ctx.sp = sp
         ctx.meta = (B, Tq, Tk, D, H, same_kv)
@@ -80,7 +83,7 @@ class _BlockFn(torch.autograd.Function):
                          ds_next=dS.data_ptr() if dS is not None else 0,
                          ds_prev=dSp.data_ptr() if has_prev else 0,
                          dc_partial=dc_part.data_ptr() if has_prev else 0)
-        launch('mep_block_epi_bwd', DescArray(EpiBwdDesc, [eb], dev), cdiv(B * Tq, 64), threads=D)
+        launch('mep_block_epi_bwd', DescArray(EpiBwdDesc, [eb], dev), _lib.epi_grid(B * Tq, 1), threads=D)
         geo = _lib.attn_geometry([ad])
         launch('mep_attn_bwd', DescArray(AttnBwdDesc, [ab], dev), geo[1], threads=_lib.attn_bwd_flags([ab]))
         gwp, gwm = torch.empty_like(wp), torch.empty_like(wm)

@@ -233,7 +233,7 @@ class TriModalPlan:
             geo = _lib.attn_geometry(ad)
             self.t_attn.append(geo[0])
             self.g_attn.append(geo)
-            self.t_epi.append(max(cdiv(B * b['Tq'], 64) for b in self.blocks))
+            self.t_epi.append(_lib.epi_grid(max(B * b['Tq'] for b in self.blocks), len(ed)))
         # pool
         pd = [PoolDesc(x=self.Xcat[e].data_ptr(), dx=self.dXcat[e].data_ptr(), pooled=self.pooled[e].data_ptr(),
                        dpooled=self.dpooled[e].data_ptr(), argmax=self.argmax[e].data_ptr(),

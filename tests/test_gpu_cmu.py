@@ -9,7 +9,7 @@ import pytest
 import torch
 
 from tests.golden import fixtures
-from tests.gpu_util import assert_close, check_post_params, cmu_model, cuda_batch
+from tests.gpu_util import OUT_ATOL_FRAC, assert_close, check_post_params, cmu_model, cuda_batch
 
 pytestmark = pytest.mark.gpu
 CMU = [n for n in fixtures.names('model') if fixtures.load(n)[0]['family'] == 'cmu']
@@ -23,7 +23,7 @@ def test_concat_trans_autograd(name, cuda):
     model.train()
     l, v, a, lm, vm, am, labels = cuda_batch(meta, cuda)
     logits = model(l, v, a, lm, vm, am)
-    assert_close(logits, gold['logits'], 1e-4, 1e-6, 'logits')
+    assert_close(logits, gold['logits'], 1e-4, OUT_ATOL_FRAC, 'logits')
     loss = cmu_mosei.multi_circle_loss(logits, labels).mean()
     assert_close(loss.reshape(()), gold['loss'], 1e-4, 0, 'loss')
     loss.backward()
@@ -79,7 +79,7 @@ def test_attention_block_standalone(name, cuda):
     kvt = torch.tensor(kv, device=cuda, requires_grad=True)
     sp = torch.tensor(s_prev, device=cuda, requires_grad=True) if s_prev is not None else None
     y, s = blk(qt, kvt, kvt, torch.tensor(mask, device=cuda), sp)
-    assert_close(y, gold['out'], 1e-4, 1e-6, 'out')
+    assert_close(y, gold['out'], 1e-4, OUT_ATOL_FRAC, 'out')
     assert_close(s, gold['scores'], 1e-6, 1e-12, 'scores')
     obj = (y * torch.tensor(g_out, device=cuda)).sum()
     if meta['g_scores']:

@@ -14,7 +14,7 @@ import pytest
 import torch
 
 from tests.golden import fixtures
-from tests.gpu_util import assert_close, check_post_params, ren_model
+from tests.gpu_util import OUT_ATOL_FRAC, assert_close, check_post_params, ren_model
 
 pytestmark = pytest.mark.gpu
 REN = [n for n in fixtures.names('model') if fixtures.load(n)[0]['family'] == 'ren']
@@ -46,7 +46,7 @@ def test_base_model_autograd(name, cuda):
     model.train()
     args, labels = _batch(meta, cuda)
     logits = model(*args)
-    assert_close(logits, gold['logits'], 1e-4, 1e-6, 'logits')
+    assert_close(logits, gold['logits'], 1e-4, OUT_ATOL_FRAC, 'logits')
     loss = ren_mme.multi_loss(logits, labels) + ren_mme.rdrop_kl(logits)
     assert_close(loss.reshape(()), gold['loss'], 1e-4, 0, 'loss')
     loss.backward()
