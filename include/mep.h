@@ -68,11 +68,15 @@ int mep_gemm(const mep_gemm_desc* descs, int n_desc, int max_tiles, mep_stream_t
 /* ---------------------------------------------------------------- weight-gradient GEMM
  * dW_i[n, k] (+)= sum_tok A[tok, n] * B_i[tok, k]   for up to 4 operands B_i sharing one A
  * (dW = dY^T X of every nn.Linear on the path; e.g. minus.weight = dZ^T [q | xp] is one
- * descriptor with two B operands).  One workgroup owns a token chunk (tok_per_split rows) and a
- * 256-wide column group of the concatenated K, computes the whole N x 256 partial with f32 MFMA
- * (each input element read once), and writes partial[split][n][k]; mep_wgrad_reduce sums the
- * splits in a fixed order into out_i.  N <= 128; partial holds n_split * N * Ktot floats.
- * Grid: mep_wgrad max_tiles = max(n_split * ceil(Ktot/256)); mep_wgrad_reduce max_tiles =
+ * descriptor with two B operands).  Tiling: MT = ceil(N/32) row tiles of 32 x 32 (f32 MFMA
+ * 32x32x2), column groups of KT tiles (KT = 3, 2, 4, 4 for MT = 3, 4, 2, 1).  One workgroup
+ * (4 waves) owns a token chunk of tok_per_split rows (a multiple of 8) and one column group,
+ * and writes partial[split][n][k]; mep_wgrad_reduce sums the splits in a fixed order into out_i.
+ * N <= 128; partial holds n_split * N * Ktot floats; every row view of a descriptor shares T
+ * and spans < 2^31 floats.
+ * mep_wgrad: `descs` holds the n_desc descriptors FOLLOWED BY max_tiles int32 task entries
+ * (descriptor index << 16 | workgroup index within the descriptor, split-major), one per
+ * workgroup of the flat grid.  mep_wgrad_reduce: grid (max_tiles, n_desc), max_tiles =
  * max(ceil(N*Ktot/256)). */
 #define MEP_WG_MAX_B 4
 typedef struct {

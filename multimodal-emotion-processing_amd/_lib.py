@@ -201,12 +201,14 @@ def call(name, *args, stream=None):
 class DescArray:
     """A device-resident array of descriptors (kept alive by the plan that owns it)."""
 
-    def __init__(self, struct, items, device):
+    def __init__(self, struct, items, device, tail=None):
+        """tail: int32 values stored right after the descriptors (the k_wgrad task map)."""
         self.n = len(items)
         self.struct = struct
         if self.n:
             arr = (struct * self.n)(*items)
-            host = torch.frombuffer(bytearray(bytes(arr)), dtype=torch.uint8)
+            raw = bytes(arr) + (b'' if tail is None else bytes((ctypes.c_int32 * len(tail))(*tail)))
+            host = torch.frombuffer(bytearray(raw), dtype=torch.uint8)
             self.dev = host.to(device)
         else:
             self.dev = None

@@ -133,143 +133,213 @@ __global__ __launch_bounds__(GEMM_THREADS) void k_gemm(const mep_gemm_desc* __re
 }
 
 // ---------------------------------------------------------------- weight gradient
-// dW[n][k] = sum_t A[t][n] B[t][k] on f32 MFMA 16x16x4 with the token axis as the MFMA k.
-// One workgroup = (chunk of tok_per_split tokens, group of <= 256 columns of the concatenated K);
-// its 8 waves form a 2 x 4 grid over the (N/16) x (kcnt/16) output tiles, each wave a rectangle
-// of <= 4 x 4 tiles so A fragments are reused across its k tiles and B fragments across its n
-// tiles.  Per 32-token step both operands are staged TRANSPOSED (feature-major) in LDS,
-// double-buffered, with the next step's global loads in flight during the current step's MFMAs:
-// a thread gathers 8 consecutive tokens of one feature (coalesced across the lanes' features)
-// and writes them as two 16-byte LDS stores; a fragment (4 tokens of one feature) is then one
-// 16-byte LDS read.
-constexpr int WG_THREADS = 512;
-constexpr int WG_TT = 32;                      // tokens per step
-constexpr int WG_KG = 256;                     // max columns per workgroup
-constexpr int WG_NMAX = 128;
-constexpr int WG_LD = WG_TT + 4;               // row stride (floats): 16-row fragment reads conflict-free
-constexpr int WG_ROWS = WG_NMAX + WG_KG;       // A feature rows, then B column rows
-constexpr int WG_STAGE = WG_ROWS * WG_LD;      // floats per stage buffer
-constexpr int WG_IPT = (WG_ROWS * (WG_TT / 8) + WG_THREADS - 1) / WG_THREADS;   // items per thread
+// dW[n][k] = sum_t A[t][n] B[t][k]: a long token reduction into a small (<= 128-row) output.
+// f32 MFMA 32x32x2 with the token axis as the MFMA k: per token pair a lane needs ONE element of
+// each operand column it owns (lane l: column 32 i + (l & 31) of row tile i / column tile j,
+// token 2 s + (l >> 5)), so operands go straight from HBM into registers -- no LDS staging, no
+// block barriers in the main loop.  A wave keeps a whole MT x KT block of 32x32 tiles in
+// accumulators (MT = ceil(N/32) covers every output row; KT = 3, 2, 4, 4 for MT = 3, 4, 2, 1) and
+// WG_P token pairs of loads in flight, so every lane issues MT + KT dword loads per MT * KT MFMAs.
+// One workgroup = 4 waves (one per SIMD) on consecutive quarters of a tok_per_split chunk and
+// one column group; the four accumulator blocks are summed through LDS in a fixed order
+// ((w0 + w2) + (w1 + w3)) and written once as partial[split][n][k]; mep_wgrad_reduce sums the
+// splits.  Row views are addressed with 32-bit offsets (hosts keep every view under 2^31 floats).
+constexpr int WG_WAVES = 4;
+constexpr int WG_THREADS = 64 * WG_WAVES;
+constexpr int WG_P = 6;                        // token pairs in flight per lane
+constexpr int WG_RED = 96 * (96 + 8);          // largest 32MT x (32KT + 8) reduction buffer (MT = KT = 3)
 
-struct WgItem {        // one (feature row, 8-token group) staging item of a thread
-    uint64_t ptr;      // column base (row view ptr + column offset), 0 = none
-    int64_t sB, sT;
-    int T, lrow, tg;
-};
+MEP_DEV int wg_kt(int mt) { return mt == 4 ? 2 : mt == 3 ? 3 : 4; }
 
-MEP_DEV void wg_load(float (&v)[WG_IPT][8], const WgItem (&it)[WG_IPT], int t0, int t_end) {
-#pragma unroll
-    for (int m = 0; m < WG_IPT; ++m) {
-        const mep_rows r{it[m].ptr, it[m].sB, it[m].sT, it[m].T, 0};
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            const int tok = t0 + 8 * it[m].tg + j;
-            v[m][j] = (it[m].ptr && tok < t_end) ? *(G<const float>(r.ptr) + row_off(r, tok)) : 0.f;
-        }
-    }
+// byte extent of a row view's first ntok rows, `width` columns wide (the range the raw buffer
+// loads check; hosts keep it under 2^31)
+MEP_DEV int wg_extent(const mep_rows& r, int T, int ntok, int width) {
+    const int64_t last = (int64_t)((ntok - 1) / T) * r.sB + (int64_t)((ntok - 1) % T) * r.sT + width;
+    return (int)min((int64_t)4 * last, (int64_t)0x7fffffff);
 }
 
-MEP_DEV void wg_store(lfloat* st, const float (&v)[WG_IPT][8], const WgItem (&it)[WG_IPT]) {
-#pragma unroll
-    for (int m = 0; m < WG_IPT; ++m) {
-        if (!it[m].ptr) continue;
-        lfloat* q = st + it[m].lrow * WG_LD + 8 * it[m].tg;
-        *reinterpret_cast<lf32x4*>(q) = f32x4{v[m][0], v[m][1], v[m][2], v[m][3]};
-        *reinterpret_cast<lf32x4*>(q + 4) = f32x4{v[m][4], v[m][5], v[m][6], v[m][7]};
-    }
-}
+constexpr int WG_INV = (int)0x80000000u;   // byte offset past every view: the buffer load returns 0
 
-__global__ __launch_bounds__(WG_THREADS) void k_wgrad(const mep_wgrad_desc* __restrict__ descs) {
-    const mep_wgrad_desc& d = descs[blockIdx.y];
-    const int nkg = (d.Ktot + WG_KG - 1) / WG_KG;
-    if ((int)blockIdx.x >= d.n_split * nkg) return;
-    const int split = blockIdx.x / nkg, kg = blockIdx.x - split * nkg;
+template <int MT, int KT>
+MEP_DEV void wgrad_task(const mep_wgrad_desc& d, int split, int kbase, lfloat* red) {
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int c = lane & 31, g = lane >> 5;
+    const int N = d.N;
     const int t_begin = split * d.tok_per_split;
     const int t_end = min(d.ntok, t_begin + d.tok_per_split);
-    const int kbase = kg * WG_KG, kcnt = min(WG_KG, d.Ktot - kbase);
-    const int N = d.N;
-    __shared__ __attribute__((aligned(16))) float smem[2 * WG_STAGE];
-    lfloat* const stage0 = (lfloat*)&smem[0];   // buffer b at stage0 + b * WG_STAGE
+    const int per_wave = d.tok_per_split / WG_WAVES;           // even (host)
+    const int w0 = t_begin + wave * per_wave;
+    const int w1 = min(t_end, w0 + per_wave);
+    const int npairs = w1 > w0 ? (w1 - w0 + 1) >> 1 : 0;       // an odd last token pairs with a zero
 
-    // staging items of this thread: row f of the (N + kcnt) feature rows, token group tg
-    const int nrows = N + kcnt;
-    WgItem it[WG_IPT];
+    // Every view of the item shares T; a T = 1 view is addressed as T = 2 (sT = sB, sB = 2 sB) so
+    // that one wrap check per 2-token advance suffices.
+    const int T0 = d.a.T;
+    const int T = T0 == 1 ? 2 : T0;
+    auto strides = [&](const mep_rows& r, int& sB, int& sT) {
+        sB = (int)(T0 == 1 ? 2 * r.sB : r.sB);
+        sT = (int)(T0 == 1 ? r.sB : r.sT);
+    };
+    // Operand columns of this lane, clamped in range: a column past N (past Ktot) only feeds
+    // output rows (columns) that are never stored.  Tokens past the wave's range read 0 through
+    // the buffer range check (offset WG_INV), so no select sits between a load and its MFMA.
+    const auto rsA = __builtin_amdgcn_make_buffer_rsrc((void*)d.a.ptr, 0, wg_extent(d.a, T0, d.ntok, N), 0x00020000);
+    int colA[MT];
 #pragma unroll
-    for (int m = 0; m < WG_IPT; ++m) {
-        const int idx = threadIdx.x + WG_THREADS * m;
-        const int tg = idx / nrows, f = idx - tg * nrows;
-        it[m] = WgItem{0, 0, 0, 1, 0, 0};
-        if (tg < WG_TT / 8) {
-            if (f < N) {
-                it[m] = WgItem{d.a.ptr + 4ull * f, d.a.sB, d.a.sT, d.a.T, f, tg};
-            } else {
-                int k = kbase + (f - N), i = 0;
-                while (i < d.n_b - 1 && k >= d.kb[i]) { k -= d.kb[i]; ++i; }
-                const mep_rows& b = d.b[i];
-                it[m] = WgItem{b.ptr + 4ull * k, b.sB, b.sT, b.T, WG_NMAX + (f - N), tg};
-            }
-        }
+    for (int i = 0; i < MT; ++i) colA[i] = 4 * min(32 * i + c, N - 1);
+    int asB, asT;
+    strides(d.a, asB, asT);
+    __amdgpu_buffer_rsrc_t rsB[KT];
+    int colB[KT], bsB[KT], bsT[KT];
+#pragma unroll
+    for (int j = 0; j < KT; ++j) {
+        // the operand of tile j is wave-uniform (hosts keep operand boundaries on 32-column tiles)
+        int k0 = min(kbase + 32 * j, d.Ktot - 1), o = 0;
+        while (o < d.n_b - 1 && k0 >= d.kb[o]) { k0 -= d.kb[o]; ++o; }
+        const mep_rows& b = d.b[o];
+        rsB[j] = __builtin_amdgcn_make_buffer_rsrc((void*)b.ptr, 0, wg_extent(b, T0, d.ntok, d.kb[o]), 0x00020000);
+        colB[j] = 4 * min(k0 + c, d.kb[o] - 1);
+        strides(b, bsB[j], bsT[j]);
     }
 
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int c = lane & 15, g = lane >> 4;
-    const int ntn = (N + 15) >> 4, ntk = (kcnt + 15) >> 4;
-    const int wn = wave >> 2, wk = wave & 3;
-    const int pn = (ntn + 1) >> 1, pk = (ntk + 3) >> 2;          // tiles per wave (<= 4 each)
-    const int tn0 = wn * pn, tk0 = wk * pk;
-    const int nn = max(0, min(pn, ntn - tn0)), nk = max(0, min(pk, ntk - tk0));
-    f32x4 acc[4][4];
+    floatx16 acc[MT][KT];
 #pragma unroll
-    for (int a = 0; a < 4; ++a)
+    for (int i = 0; i < MT; ++i)
 #pragma unroll
-        for (int b = 0; b < 4; ++b) acc[a][b] = zero_f4();
+        for (int j = 0; j < KT; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-    float pre[WG_IPT][8];
-    wg_load(pre, it, t_begin, t_end);
-    wg_store(stage0, pre, it);
+    // load cursor: token tok = (b, t) of this lane and its element offsets offA / offB[j],
+    // advanced by two tokens per pair with one wrap check (T >= 2): no multiplies in the loop
+    int tok = w0 + g, t, offA, offB[KT];
+    {
+        const int tq = min(tok, d.ntok - 1);
+        const int bq = tq / T, tt = tq - bq * T;
+        t = tt;
+        offA = bq * asB + tt * asT;
+#pragma unroll
+        for (int j = 0; j < KT; ++j) offB[j] = bq * bsB[j] + tt * bsT[j];
+    }
+    const int wA = asB - T * asT;
+    int wB[KT];
+#pragma unroll
+    for (int j = 0; j < KT; ++j) wB[j] = bsB[j] - T * bsT[j];
+
+    float ra[WG_P][MT], rb[WG_P][KT];
+    auto load = [&](int p) {
+        const bool ok = tok < w1;
+        const int va = ok ? 4 * offA : WG_INV;
+#pragma unroll
+        for (int i = 0; i < MT; ++i)
+            ra[p][i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsA, va + colA[i], 0, 0));
+#pragma unroll
+        for (int j = 0; j < KT; ++j)
+            rb[p][j] = __builtin_bit_cast(
+                float, __builtin_amdgcn_raw_buffer_load_b32(rsB[j], (ok ? 4 * offB[j] : WG_INV) + colB[j], 0, 0));
+        tok += 2;
+        t += 2;
+        const bool wrap = t >= T;
+        t -= wrap ? T : 0;
+        offA += 2 * asT + (wrap ? wA : 0);
+#pragma unroll
+        for (int j = 0; j < KT; ++j) offB[j] += 2 * bsT[j] + (wrap ? wB[j] : 0);
+    };
+    auto mma = [&](int p) {
+#pragma unroll
+        for (int i = 0; i < MT; ++i)
+#pragma unroll
+            for (int j = 0; j < KT; ++j) acc[i][j] = mfma32(ra[p][i], rb[p][j], acc[i][j]);
+    };
+    if (npairs > 0) {
+        // pairs 0 .. P-2 go to slots 0 .. P-2; step s loads pair s + P - 1 into the slot that
+        // step s - 1 consumed, then runs the MFMAs of pair s.  The two are independent, so the
+        // scheduler interleaves them: one MFMA, a few VALU, one load.
+#pragma unroll
+        for (int p = 0; p < WG_P - 1; ++p) load(p);
+        int s0 = 0;
+        for (; s0 + WG_P <= npairs; s0 += WG_P) {
+#pragma unroll
+            for (int p = 0; p < WG_P; ++p) {
+                load((p + WG_P - 1) % WG_P);
+                mma(p);
+#pragma unroll
+                for (int k = 0; k < MT * KT; ++k) {
+                    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);                    // MFMA
+                    __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);                    // VALU
+                    if (k < MT + KT) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);   // VMEM read
+                }
+            }
+        }
+        const int rem = npairs - s0;     // slots 0 .. rem-1 (rem < P) hold the last pairs
+#pragma unroll
+        for (int p = 0; p < WG_P - 1; ++p)
+            if (p < rem) mma(p);
+    }
+
+    // ((w0 + w2) + (w1 + w3)) through two LDS buffers, then one coalesced partial write
+    constexpr int LDR = 32 * KT + 8;            // == 8 mod 16: lane halves 32 banks apart
+    constexpr int BUF = 32 * MT * LDR;
+    lfloat* mine = red + (wave & 1) * BUF;
+    if (wave >= 2) {
+#pragma unroll
+        for (int i = 0; i < MT; ++i)
+#pragma unroll
+            for (int j = 0; j < KT; ++j)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) mine[(32 * i + acc_row(r, lane)) * LDR + 32 * j + c] = acc[i][j][r];
+    }
     __syncthreads();
-    int cur = 0;
-    for (int t0 = t_begin; t0 < t_end; t0 += WG_TT) {
-        const bool more = t0 + WG_TT < t_end;
-        if (more) wg_load(pre, it, t0 + WG_TT, t_end);
-        const lfloat* st = stage0 + cur * WG_STAGE;
+    if (wave < 2) {
 #pragma unroll
-        for (int kb = 0; kb < WG_TT / 16; ++kb) {
-            f32x4 af[4], bf[4];
+        for (int i = 0; i < MT; ++i)
 #pragma unroll
-            for (int a = 0; a < 4; ++a)
-                if (a < nn) af[a] = ld4w(st + (16 * (tn0 + a) + c) * WG_LD + 16 * kb + 4 * g);
+            for (int j = 0; j < KT; ++j)
 #pragma unroll
-            for (int b = 0; b < 4; ++b)
-                if (b < nk) bf[b] = ld4w(st + (WG_NMAX + 16 * (tk0 + b) + c) * WG_LD + 16 * kb + 4 * g);
-#pragma unroll
-            for (int s = 0; s < 4; ++s)
-#pragma unroll
-                for (int a = 0; a < 4; ++a)
-#pragma unroll
-                    for (int b = 0; b < 4; ++b)
-                        if (a < nn && b < nk)
-                            acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[a][s], bf[b][s], acc[a][b], 0, 0, 0);
-        }
-        if (more) wg_store(stage0 + (cur ^ 1) * WG_STAGE, pre, it);
-        __syncthreads();
-        cur ^= 1;
+                for (int r = 0; r < 16; ++r) {
+                    lfloat* q = mine + (32 * i + acc_row(r, lane)) * LDR + 32 * j + c;
+                    *q = acc[i][j][r] + *q;
+                }
     }
-    // partial[split][n][kbase + k]: lane (c, g) holds rows n = 4g + r, column k = c of each tile
-    gfloat* part = G<float>(d.partial) + (int64_t)split * N * d.Ktot;
-#pragma unroll
-    for (int a = 0; a < 4; ++a)
-#pragma unroll
-        for (int b = 0; b < 4; ++b) {
-            if (a >= nn || b >= nk) continue;
-            const int k = 16 * (tk0 + b) + c;
-            if (k >= kcnt) continue;
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int n = 16 * (tn0 + a) + 4 * g + r;
-                if (n < N) part[(int64_t)n * d.Ktot + kbase + k] = acc[a][b][r];
-            }
-        }
+    __syncthreads();
+    const int kcnt = min(32 * KT, d.Ktot - kbase);
+    gfloat* part = G<float>(d.partial) + (int64_t)split * N * d.Ktot + kbase;
+    for (int idx = threadIdx.x; idx < N * 32 * KT; idx += WG_THREADS) {
+        const int n = idx / (32 * KT), k = idx - n * (32 * KT);
+        if (k < kcnt) part[(int64_t)n * d.Ktot + k] = red[n * LDR + k] + red[BUF + n * LDR + k];
+    }
+}
+
+// Flat grid: workgroup w runs task map[w] = (descriptor << 16 | index within the descriptor);
+// the map is stored right after the n_desc descriptors.
+__global__ __launch_bounds__(WG_THREADS, 2) void k_wgrad(const mep_wgrad_desc* __restrict__ descs, int n_desc) {
+    const int task = reinterpret_cast<const int*>(descs + n_desc)[blockIdx.x];
+    const mep_wgrad_desc& d = descs[task >> 16];
+    const int local = task & 0xffff;
+    const int mt = (d.N + 31) >> 5, ktm = wg_kt(mt);
+    const int ktiles = (d.Ktot + 31) >> 5;
+    const int ncg = (ktiles + ktm - 1) / ktm;
+    const int split = local / ncg, cg = local - split * ncg;
+    const int kt = min(ktm, ktiles - cg * ktm);
+    const int kbase = 32 * ktm * cg;
+    __shared__ __attribute__((aligned(16))) float smem[2 * WG_RED];
+    lfloat* red = (lfloat*)&smem[0];
+    switch (8 * mt + kt) {
+        case 8 * 1 + 1: wgrad_task<1, 1>(d, split, kbase, red); break;
+        case 8 * 1 + 2: wgrad_task<1, 2>(d, split, kbase, red); break;
+        case 8 * 1 + 3: wgrad_task<1, 3>(d, split, kbase, red); break;
+        case 8 * 1 + 4: wgrad_task<1, 4>(d, split, kbase, red); break;
+        case 8 * 2 + 1: wgrad_task<2, 1>(d, split, kbase, red); break;
+        case 8 * 2 + 2: wgrad_task<2, 2>(d, split, kbase, red); break;
+        case 8 * 2 + 3: wgrad_task<2, 3>(d, split, kbase, red); break;
+        case 8 * 2 + 4: wgrad_task<2, 4>(d, split, kbase, red); break;
+        case 8 * 3 + 1: wgrad_task<3, 1>(d, split, kbase, red); break;
+        case 8 * 3 + 2: wgrad_task<3, 2>(d, split, kbase, red); break;
+        case 8 * 3 + 3: wgrad_task<3, 3>(d, split, kbase, red); break;
+        case 8 * 4 + 1: wgrad_task<4, 1>(d, split, kbase, red); break;
+        case 8 * 4 + 2: wgrad_task<4, 2>(d, split, kbase, red); break;
+        default: break;
+    }
 }
 
 __global__ __launch_bounds__(256) void k_wgrad_reduce(const mep_wgrad_desc* __restrict__ descs) {
@@ -298,7 +368,7 @@ extern "C" int mep_gemm(const mep_gemm_desc* descs, int n_desc, int max_tiles, m
 
 extern "C" int mep_wgrad(const mep_wgrad_desc* descs, int n_desc, int max_tiles, mep_stream_t stream) {
     if (n_desc <= 0 || max_tiles <= 0) return 0;
-    hipLaunchKernelGGL(k_wgrad, dim3(max_tiles, n_desc), dim3(WG_THREADS), 0, (hipStream_t)stream, descs);
+    hipLaunchKernelGGL(k_wgrad, dim3(max_tiles), dim3(WG_THREADS), 0, (hipStream_t)stream, descs, n_desc);
     return mep_check_launch("mep_wgrad");
 }
 

@@ -34,24 +34,74 @@ CHAINS = (('l', 'l'), ('l', 'v'), ('l', 'a'),
 MODS = ('l', 'v', 'a')
 TIME_ORDER = ('l', 'a', 'v')                          # cmu-mosei/run.py:317
 UNIFY_NAMES = {'l': 'linguistic', 'v': 'visual', 'a': 'acoustic'}
-TOK_PER_SPLIT = 256
 
 
 def cdiv(a, b):
     return (a + b - 1) // b
 
 
-def make_wgrad(items, dev, tok_per_split=TOK_PER_SPLIT):
+WG_WAVES = 4              # csrc/gemm.hip k_wgrad: waves per workgroup (token quarters of a split)
+WG_TARGET = 2 * _lib.N_CU  # workgroups per launch: two per CU (80 KB of LDS each)
+
+
+def wgrad_geometry(N, ktot):
+    """(row tiles MT, column tiles per group KT, column groups) of k_wgrad's 32x32 tiling of an
+    N x ktot weight gradient (csrc/gemm.hip wg_kt)."""
+    mt = cdiv(N, 32)
+    kt = {4: 2, 3: 3}.get(mt, 4)
+    return mt, kt, cdiv(cdiv(ktot, 32), kt)
+
+
+def wgrad_splits(items, n_wg=WG_TARGET):
+    """Token chunk per item such that the launch holds AT MOST n_wg workgroups, all resident at
+    once (two per CU), and the largest workgroup's MFMA work (32x32 tiles x tokens) is as small
+    as the quantisation allows: the kernel lasts as long as its busiest CU, so a launch of 264
+    workgroups (8 CUs holding two) takes twice as long as one of 256.  Multiples of 8 tokens
+    (four waves, token pairs)."""
+    geo = [wgrad_geometry(N, sum(b[1] for b in bs)) for (_, N, n, bs, _) in items]
+    tiles = [mt * kt for (mt, kt, ncg) in geo]
+    total = sum(n * t * ncg for t, (_, _, ncg), (_, N, n, bs, _) in zip(tiles, geo, items))
+
+    def split(budget):
+        tps = []
+        for t, (_, N, n, bs, _) in zip(tiles, items):
+            ns = max(1, cdiv(n * t, max(1, int(budget))))
+            tps.append(max(8, cdiv(cdiv(n, ns), 8) * 8))
+        wgs = sum(cdiv(n, p) * ncg for p, (_, _, ncg), (_, N, n, bs, _) in zip(tps, geo, items))
+        return tps, wgs
+
+    budget = max(8.0, total / float(n_wg))
+    while True:
+        tps, wgs = split(budget)
+        if wgs <= n_wg:
+            return tps
+        budget *= 1.01
+
+
+def make_wgrad(items, dev, tok_per_split=None):
     """items: [(a_rows, N, ntok, [(b_rows, K, out_ptr, ldo), ...][, out_trans]), ...] ->
-    (workspace, descs, wgrad tiles, reduce tiles).  One descriptor per A operand; its B operands
-    concatenate on K.  out_trans: dW written transposed (out[k * ldo + n])."""
+    (workspace, descs, wgrad workgroups, reduce tiles).  One descriptor per A operand; its B operands
+    concatenate on K.  out_trans: dW written transposed (out[k * ldo + n]).  tok_per_split: None =
+    balanced per item (wgrad_splits), else a fixed token chunk."""
     items = [tuple(it) + (0,) * (5 - len(it)) for it in items]
-    total = sum(cdiv(n, tok_per_split) * N * sum(b[1] for b in bs) for (_, N, n, bs, _) in items)
+    if tok_per_split is None:
+        tps = wgrad_splits(items)
+    elif isinstance(tok_per_split, int):
+        tps = [tok_per_split] * len(items)
+    else:
+        tps = list(tok_per_split)
+    total = sum(cdiv(n, t) * N * sum(b[1] for b in bs) for t, (_, N, n, bs, _) in zip(tps, items))
     ws = torch.zeros(max(total, 1), dtype=torch.float32, device=dev)
-    descs, off, tmax, rmax = [], 0, 0, 0
-    for (a, N, n, bs, trans) in items:
-        assert N <= 128 and len(bs) <= _lib.WG_MAX_B
+    descs, tasks, off, rmax = [], [], 0, 0
+    for tok_per_split, (a, N, n, bs, trans) in zip(tps, items):
+        assert N <= 128 and len(bs) <= _lib.WG_MAX_B and tok_per_split % 8 == 0
+        # k_wgrad: every 32-column tile reads one operand (wave-uniform buffer resource)
+        assert all(b[1] % 32 == 0 for b in bs[:-1]), 'wgrad B operand boundaries must be multiples of 32'
         ktot = sum(b[1] for b in bs)
+        for v, w in [(a, N)] + [(b[0], b[1]) for b in bs]:
+            # k_wgrad: one token -> (b, t) map for every view of the item; 32-bit byte offsets
+            assert v.T == a.T, 'wgrad views of one item must share T'
+            assert 4 * ((cdiv(n, v.T) - 1) * v.sB + (v.T - 1) * v.sT + w) < 2 ** 31
         ns = cdiv(n, tok_per_split)
         pad = [(Rows(), 0, 0, 0)] * (_lib.WG_MAX_B - len(bs))
         allb = list(bs) + pad
@@ -62,9 +112,10 @@ def make_wgrad(items, dev, tok_per_split=TOK_PER_SPLIT):
                                partial=ws.data_ptr() + 4 * off, n_b=len(bs), ntok=n, N=N, Ktot=ktot,
                                tok_per_split=tok_per_split, n_split=ns, accumulate=0, out_trans=int(trans)))
         off += ns * N * ktot
-        tmax = max(tmax, ns * cdiv(ktot, 256))
+        tasks += [(len(descs) - 1) << 16 | w for w in range(ns * wgrad_geometry(N, ktot)[2])]
         rmax = max(rmax, cdiv(N * ktot, 256))
-    return ws, DescArray(WgradDesc, descs, dev), tmax, rmax
+    assert len(tasks) < 2 ** 31 and all((t & 0xffff) < 0xffff for t in tasks)
+    return ws, DescArray(WgradDesc, descs, dev, tail=tasks), len(tasks), rmax
 
 
 def rows(t, T, sB, sT, off=0):
@@ -359,6 +410,7 @@ class TriModalPlan:
                 src = self.dY[(e, m)] if sp.unify_norm else self.dU[(e, m)]
                 items.append((crows(src, self.T[m], D), D, self.ntok[m],
                               [(self._in_rows(e, m), d, g(pre + UNIFY_NAMES[m] + '.weight'), d)]))
+        self._wgrad_items = items
         self.wg_partial, self.d_wgrad, self.t_wgrad, self.t_wgred = make_wgrad(items, dev)
         # column sums: block LayerNorms, residual coefficients, Ren unify LayerNorm
         cs = []
