@@ -358,6 +358,129 @@ __global__ __launch_bounds__(256) void k_wgrad_reduce(const mep_wgrad_desc* __re
     *o = d.accumulate ? *o + s : s;
 }
 
+// ---------------------------------------------------------------- unify projection
+// Y[tok][n] = X[tok][:K] . W[n][:K] (+ table[tok % T][n]) for N = D <= 128 output features:
+// Unify_Dimension's bias-free Linears (cmu-mosei/run.py:210-214, Ren-MME/run.py:161-166).
+// Weight-stationary transposed tiles (common.h): a workgroup of 8 waves stages W [N][Kp] (zero
+// padded to Kp = 16 * KB) in LDS once -- or, when that does not fit, reads 16-byte W fragments
+// from L2 (K % 16 == 0) -- and its waves take (16-token tile, output part) tasks of the
+// workgroup's contiguous tile range.  Per task Y^T = W X^T on f32 MFMA 16x16x4: lane (c, g)
+// holds features 16 i + 4g .. +3 of token c, X fragments (4 consecutive k of token c) come
+// straight from HBM through a range-checked buffer resource (past the view: 0), UN_PF k blocks
+// ahead of their MFMAs.  Flat grid: workgroup w runs map[w] = desc << 20 | n_wg << 10 | index.
+constexpr int UN_WAVES = 8;
+constexpr int UN_THREADS = 64 * UN_WAVES;
+constexpr int UN_LDS = 30720;   // floats (120 KB): W [N][Kp + 4] when N * (Kp + 4) fits
+constexpr int UN_PF = 8;        // X fragments (k blocks) in flight per lane
+
+template <int NIP, bool WL, bool XV>
+MEP_DEV void unify_tasks(const mep_gemm_desc& d, const lfloat* wl, int ldl, int tile_lo, int tile_hi, int np) {
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int c = lane & 15, g = lane >> 4;
+    const int K = d.K, KB = (K + 15) >> 4, ntok = d.ntok;
+    const int T = d.x.T;
+    const auto rsX = __builtin_amdgcn_make_buffer_rsrc((void*)d.x.ptr, 0, wg_extent(d.x, T, ntok, K), 0x00020000);
+    const gfloat* wg = G<const float>(d.w);
+    const gfloat* table = G<const float>(d.table);
+    const int ntask = (tile_hi - tile_lo) * np;
+    for (int task = wave; task < ntask; task += UN_WAVES) {
+        const int tile = tile_lo + task / np, part = task - (task / np) * np;
+        const int tok = tile * 16 + c;
+        const bool ok = tok < ntok;
+        int xo = WG_INV;   // byte offset of the lane's X row (k = 4g within each k block)
+        if (ok) {
+            const int b = tok / T, t = tok - b * T;
+            xo = 4 * ((int)(b * d.x.sB + t * d.x.sT) + 4 * g);
+        }
+        const int n0 = 16 * NIP * part;       // first output feature of this part
+        f32x4 acc[NIP];
+#pragma unroll
+        for (int i = 0; i < NIP; ++i) acc[i] = zero_f4();
+        f32x4 xf[UN_PF];
+        auto load = [&](int p, int kb) {
+            const int o = kb < KB ? xo + 64 * kb : WG_INV;
+            if (XV) {
+                xf[p] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rsX, o, 0, 0));
+            } else {
+#pragma unroll
+                for (int e = 0; e < 4; ++e)
+                    xf[p][e] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsX, o + 4 * e, 0, 0));
+            }
+        };
+        auto mma = [&](int p, int kb) {
+            f32x4 a[NIP];
+#pragma unroll
+            for (int i = 0; i < NIP; ++i) {
+                const int row = n0 + 16 * i + c;
+                if (WL) a[i] = ld4w(wl + row * ldl + 16 * kb + 4 * g);
+                else a[i] = ld4w(wg + (int64_t)row * d.ldw + 16 * kb + 4 * g);
+            }
+#pragma unroll
+            for (int s = 0; s < 4; ++s)
+#pragma unroll
+                for (int i = 0; i < NIP; ++i) acc[i] = mfma16x4(a[i][s], xf[p][s], acc[i]);
+        };
+        // k block kb -> slot kb % PF; step kb loads block kb + PF - 1 into the slot step kb - 1
+        // consumed, then runs block kb's MFMAs
+#pragma unroll
+        for (int p = 0; p < UN_PF - 1; ++p) load(p, p);
+        int k0 = 0;
+        for (; k0 + UN_PF <= KB; k0 += UN_PF) {
+#pragma unroll
+            for (int p = 0; p < UN_PF; ++p) {
+                load((p + UN_PF - 1) % UN_PF, k0 + p + UN_PF - 1);
+                mma(p, k0 + p);
+            }
+        }
+#pragma unroll
+        for (int p = 0; p < UN_PF - 1; ++p)
+            if (k0 + p < KB) mma(p, k0 + p);
+        if (ok) {
+            gfloat* yr = row_ptr(d.y, tok);
+            const gfloat* tr = table ? table + (int64_t)(tok % d.y.T) * d.N : nullptr;
+#pragma unroll
+            for (int i = 0; i < NIP; ++i) {
+                const int col = n0 + 16 * i + 4 * g;
+                f32x4 v = acc[i];
+                if (tr) v += ld4w(tr + col);
+                stg4(yr + col, make_float4(v[0], v[1], v[2], v[3]));
+            }
+        }
+    }
+}
+
+__global__ __launch_bounds__(UN_THREADS) void k_unify(const mep_gemm_desc* __restrict__ descs, int n_desc) {
+    const int task = reinterpret_cast<const int*>(descs + n_desc)[blockIdx.x];
+    const mep_gemm_desc& d = descs[task >> 20];
+    const int n_wg = (task >> 10) & 1023, w = task & 1023;
+    const int ntiles = (d.ntok + 15) >> 4;
+    const int per = (ntiles + n_wg - 1) / n_wg;
+    const int tile_lo = w * per, tile_hi = min(ntiles, tile_lo + per);
+    if (tile_lo >= tile_hi) return;   // whole workgroup
+    __shared__ __attribute__((aligned(16))) float smem[UN_LDS];
+    lfloat* wl = (lfloat*)&smem[0];
+    const int N = d.N, K = d.K, KB = (K + 15) >> 4, ldl = 16 * KB + 4;
+    const bool wlds = N * ldl <= UN_LDS;
+    if (wlds) {   // W [N][K] -> LDS rows of ldl floats, zero past K
+        const gfloat* W = G<const float>(d.w);
+        for (int idx = threadIdx.x; idx < N * 16 * KB; idx += UN_THREADS) {
+            const int n = idx / (16 * KB), k = idx - n * (16 * KB);
+            wl[n * ldl + k] = k < K ? W[(int64_t)n * d.ldw + k] : 0.f;
+        }
+        __syncthreads();
+    }
+    const bool xv = (K % 4 == 0) && ((d.x.ptr & 15) == 0) && (d.x.sB % 4 == 0) && (d.x.sT % 4 == 0);
+    const int np = N >= 64 ? 2 : 1, nip = N / (16 * np);
+#define MEP_UN(NIP)                                                                          \
+    if (nip == NIP) {                                                                        \
+        if (wlds) { if (xv) unify_tasks<NIP, true, true>(d, wl, ldl, tile_lo, tile_hi, np);    \
+                    else unify_tasks<NIP, true, false>(d, wl, ldl, tile_lo, tile_hi, np); }     \
+        else unify_tasks<NIP, false, true>(d, wl, ldl, tile_lo, tile_hi, np);                   \
+    }
+    MEP_UN(1) MEP_UN(2) MEP_UN(3) MEP_UN(4)
+#undef MEP_UN
+}
+
 }  // namespace
 
 extern "C" int mep_gemm(const mep_gemm_desc* descs, int n_desc, int max_tiles, mep_stream_t stream) {
@@ -376,4 +499,10 @@ extern "C" int mep_wgrad_reduce(const mep_wgrad_desc* descs, int n_desc, int max
     if (n_desc <= 0 || max_tiles <= 0) return 0;
     hipLaunchKernelGGL(k_wgrad_reduce, dim3(max_tiles, n_desc), dim3(256), 0, (hipStream_t)stream, descs);
     return mep_check_launch("mep_wgrad_reduce");
+}
+
+extern "C" int mep_unify(const mep_gemm_desc* descs, int n_desc, int n_wg, mep_stream_t stream) {
+    if (n_desc <= 0 || n_wg <= 0) return 0;
+    hipLaunchKernelGGL(k_unify, dim3(n_wg), dim3(UN_THREADS), 0, (hipStream_t)stream, descs, n_desc);
+    return mep_check_launch("mep_unify");
 }

@@ -28,7 +28,7 @@ def launch_costs(plan):
     for e in range(2):
         for m, d in zip(MODS, sp.dims):
             n = plan.ntok[m]
-            add('mep_gemm', 2 * n * D * d, 4 * (n * d + n * D + D * d))
+            add('mep_unify', 2 * n * D * d, 4 * (n * d + n * D + D * d))
     for blk in plan.blocks:
         Tq, Tk = blk['Tq'], blk['Tk']
         r_in = 1 if blk['i'] > 0 else 0

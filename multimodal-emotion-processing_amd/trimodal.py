@@ -78,6 +78,35 @@ def wgrad_splits(items, n_wg=WG_TARGET):
         budget *= 1.01
 
 
+UN_LDS = 30720   # csrc/gemm.hip k_unify: floats of LDS for the staged weight
+
+
+def make_unify(descs, dev, n_wg=_lib.N_CU):
+    """mep_unify launch for bias-free forward projections (GemmDesc, w_nt=1, N in {32,..,128}):
+    -> (descriptor array followed by the task map, workgroups).  Workgroups (one per CU: the
+    staged weight holds 120 KB of LDS) are shared out over the descriptors in proportion to
+    their MFMA work (16-token tiles x 16-wide k blocks)."""
+    ntiles, cost = [], []
+    for d in descs:
+        assert d.w_nt == 1 and d.N in (16, 32, 48, 64, 96, 128) and not d.accumulate and not d.relu
+        assert d.bias == 0 and d.alpha == 1.0 and d.y.ptr % 16 == 0 and d.y.sB % 4 == 0 and d.y.sT % 4 == 0
+        kb = cdiv(d.K, 16)
+        xv = d.K % 4 == 0 and d.x.ptr % 16 == 0 and d.x.sB % 4 == 0 and d.x.sT % 4 == 0
+        if d.N * (16 * kb + 4) > UN_LDS:   # weight read from L2: 16-byte fragments, no k tail
+            assert d.K % 16 == 0 and d.ldw % 4 == 0 and d.w % 16 == 0 and xv, 'mep_unify: unsupported shape'
+        assert 4 * ((cdiv(d.ntok, d.x.T) - 1) * d.x.sB + (d.x.T - 1) * d.x.sT + d.K) < 2 ** 31
+        ntiles.append(cdiv(d.ntok, 16))
+        cost.append(ntiles[-1] * kb)
+    total = float(sum(cost))
+    nw = [max(1, min(cdiv(t * 2, 8), int(round(n_wg * c / total)))) for t, c in zip(ntiles, cost)]
+    while sum(nw) > n_wg:
+        i = max(range(len(nw)), key=lambda j: (nw[j], -cost[j]))
+        nw[i] -= 1
+    assert all(0 < w < 1024 for w in nw) and len(descs) < 2048
+    tasks = [(i << 20) | (w << 10) | k for i, w in enumerate(nw) for k in range(w)]
+    return DescArray(GemmDesc, descs, dev, tail=tasks), len(tasks)
+
+
 def make_wgrad(items, dev, tok_per_split=None):
     """items: [(a_rows, N, ntok, [(b_rows, K, out_ptr, ldo), ...][, out_trans]), ...] ->
     (workspace, descs, wgrad workgroups, reduce tiles).  One descriptor per A operand; its B operands
@@ -259,8 +288,7 @@ class TriModalPlan:
                 ud.append(GemmDesc(x=self._in_rows(e, m), y=crows(out, self.T[m], D),
                                    w=fl.ptr(pre + UNIFY_NAMES[m] + '.weight'), bias=0, table=0,
                                    ntok=self.ntok[m], N=D, K=d, ldw=d, w_nt=1, accumulate=0, relu=0, alpha=1.0))
-        self.d_unify = DescArray(GemmDesc, ud, dev)
-        self.t_unify = max(cdiv(self.ntok[m], 64) for m in MODS)
+        self.d_unify, self.t_unify = make_unify(ud, dev)
         if sp.unify_norm:
             ln = []
             for e in range(E):
@@ -474,7 +502,7 @@ class TriModalPlan:
         loss (row_loss, already scaled by 1/B); grad=True also runs the head backward
         (dpooled + head parameter partials) inside the same launch."""
         sp, nl = self.spec, self.spec.nl
-        launch('mep_gemm', self.d_unify, self.t_unify, stream)
+        launch('mep_unify', self.d_unify, self.t_unify, stream)
         if sp.unify_norm:
             launch('mep_layernorm_fwd', self.d_uln, cdiv(max(self.ntok.values()), 4), stream)
         for i in range(nl):

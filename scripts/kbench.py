@@ -43,7 +43,7 @@ def main():
     p = plan
     D = p.spec.D
     table = {
-        'mep_gemm': lambda: launch('mep_gemm', p.d_unify, p.t_unify),
+        'mep_unify': lambda: launch('mep_unify', p.d_unify, p.t_unify),
         'mep_attn_fwd': lambda: launch('mep_attn_fwd', p.d_attn[0], p.t_attn[0], threads=p.g_attn[0][2]),
         'mep_block_epi_fwd': lambda: launch('mep_block_epi_fwd', p.d_epi[0], p.t_epi[0], threads=D),
         'mep_block_epi_bwd': lambda: launch('mep_block_epi_bwd', p.d_epib[0], p.t_epi[0], threads=D),
