@@ -30,6 +30,7 @@ using namespace mep;
 namespace {
 
 typedef float floatx4 __attribute__((ext_vector_type(4)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 constexpr int HD = 16;
 constexpr int WAVES = 4;
@@ -233,6 +234,48 @@ MEP_DEV void wave_lds_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// One batch row of a row view as a range-checked buffer (csrc/common.h raw buffer ops): row t,
+// column col at byte t * sT + 4 col.  Rows t >= n lie past the range (every view has sT >= its
+// D used columns), so their loads return 0 and their stores are dropped -- no clamps, no
+// branches, 32-bit offsets.  The base is wave-uniform by construction (one (b, h) per wave);
+// readfirstlane makes that provable so the descriptor lives in SGPRs.
+struct BRow {
+    __amdgpu_buffer_rsrc_t rs;
+    int sT4;   // row stride in bytes (wave-uniform)
+    bool vec;  // 16-byte loads allowed
+    // byte offset of (row t, column col); loads / stores take a per-lane part plus a wave-uniform
+    // part (SGPR soffset: whole rows ahead), so row steps cost no vector instructions
+    MEP_DEV int at(int t, int col) const { return t * sT4 + 4 * col; }
+    MEP_DEV float ld1(int voff, int soff = 0) const {
+        return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, voff, soff, 0));
+    }
+    MEP_DEV void ld4(float* dst, int voff) const {
+        if (vec) {
+            const f32x4 v = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, voff, 0, 0));
+            dst[0] = v[0]; dst[1] = v[1]; dst[2] = v[2]; dst[3] = v[3];
+        } else {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) dst[e] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, voff + 4 * e, 0, 0));
+        }
+    }
+    MEP_DEV void st1(int voff, int soff, float v) const {
+        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), rs, voff, soff, 0);
+    }
+};
+
+MEP_DEV __amdgpu_buffer_rsrc_t uniform_rsrc(uint64_t base, int64_t bytes) {
+    const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)base);
+    const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(base >> 32));
+    const int n = __builtin_amdgcn_readfirstlane((int)min(bytes, (int64_t)0x7fffffff));
+    return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), 0, n, 0x00020000);
+}
+
+// rows [0, n) of batch row b of a view whose used columns are [0, D)
+MEP_DEV BRow brow(const mep_rows& v, int b, int n, int D) {
+    return BRow{uniform_rsrc(v.ptr + 4ull * (uint64_t)((int64_t)b * v.sB), 4 * ((int64_t)(n - 1) * v.sT + D)),
+                4 * (int)v.sT, aligned16(v)};
+}
+
 // One backward task: batch row b, head h, 64 keys.  PREV: residual scores (writes dS_prev and the
 // dc partial); DSN: a gradient arrives on this layer's post-mask S output.
 template <bool PREV, bool DSN>
@@ -240,23 +283,16 @@ MEP_DEV void attn_bwd_task(const mep_attn_bwd_desc& bd, int task, int kc, int nk
     const mep_attn_desc& d = bd.f;
     const int c = lane & 15, g = lane >> 4;
     const int hc = h * HD;
-    const int Tq = d.Tq, Tk = d.Tk;
+    const int Tq = d.Tq, Tk = d.Tk, D = d.H * HD;
     const float cres = PREV ? *G<const float>(d.c) : 0.f;
     const gfloat* sprev = G<const float>(d.s_prev);
     const gfloat* dsn = G<const float>(bd.ds_next);
     gfloat* dsp = G<float>(bd.ds_prev);
-    const gfloat* stats = G<const float>(d.stats);
     const gfloat* mask = G<const float>(d.mask) + (int64_t)b * d.mask_sB;
-    const gfloat* Qb = bat(d.q, b);
-    const gfloat* Kb = bat(d.k, b);
-    const gfloat* Vb = bat(d.v, b);
-    const gfloat* Ob = bat(d.x, b);
-    const gfloat* Gb = bat(bd.dx, b);
-    const int qsT = (int)d.q.sT, ksT = (int)d.k.sT, vsT = (int)d.v.sT, osT = (int)d.x.sT, gsT = (int)bd.dx.sT;
+    const BRow Qb = brow(d.q, b, Tq, D), Kb = brow(d.k, b, Tk, D), Vb = brow(d.v, b, Tk, D);
+    const BRow Ob = brow(d.x, b, Tq, D), Gb = brow(bd.dx, b, Tq, D), dQb = brow(bd.dq, b, Tq, D);
     const int sbase = (b * d.H + h) * Tq;
-    const bool qv = aligned16(d.q), kv4 = aligned16(d.k), vv4 = aligned16(d.v), gv = aligned16(bd.dx);
-    gfloat* dQb = bat(bd.dq, b);
-    const int dqsT = (int)bd.dq.sT;
+    const auto rsStat = uniform_rsrc(d.stats + 8ull * (uint64_t)sbase, 8 * (int64_t)Tq);
 
     const int k_lo = kc * CH;
     // per key tile: B operands of S (K) and dP (V) with the key on the lane, the key's mask term,
@@ -266,38 +302,50 @@ MEP_DEV void attn_bwd_task(const mep_attn_bwd_desc& bd, int task, int kc, int nk
 #pragma unroll
     for (int kt = 0; kt < NT; ++kt) {
         const int k0 = k_lo + kt * 16;
-        load4(kb[kt], Kb, ksT, k0 + c, Tk, hc + 4 * g, kv4);
-        load4(vb[kt], Vb, vsT, k0 + c, Tk, hc + 4 * g, vv4);
+        Kb.ld4(kb[kt], Kb.at(k0 + c, hc + 4 * g));
+        Vb.ld4(vb[kt], Vb.at(k0 + c, hc + 4 * g));
         mtk[kt] = mask_term(mask, k0 + c, Tk);
 #pragma unroll
-        for (int s = 0; s < 4; ++s) kq[kt][s] = load1(Kb, ksT, k0 + 4 * g + s, Tk, hc + c);
+        for (int s = 0; s < 4; ++s) kq[kt][s] = Kb.ld1(Kb.at(k0 + 4 * g, hc + c), s * Kb.sT4);
         dk[kt] = zero4();
         dv[kt] = zero4();
     }
     float dc_acc = 0.f;
     const int nqt = (Tq + 15) / 16;
-    for (int qt = 0; qt < nqt; ++qt) {
-        const int q0 = qt * 16;
-        float qa[4], da[4], db[4], qb[4], mm[4], li[4], del[4];
-        load4(qa, Qb, qsT, q0 + c, Tq, hc + 4 * g, qv);         // A of S: Q[q0+c][4g+s]
-        load4(da, Gb, gsT, q0 + c, Tq, hc + 4 * g, gv);         // A of dP: dO[q0+c][4g+s]
+    // Every global load of a 16-query tile (Q and dO in both layouts, O for delta, the row stats
+    // and the dQ rows this tile accumulates onto) is issued one tile ahead, into the other of two
+    // register sets, so only the first tile waits for memory.
+    struct QIn {
+        float qa[4], da[4], db[4], qb[4], ob[4], dqo[4];
+        f32x2 st[4];
+    };
+    auto fetch = [&](QIn& in, int qt) {
+        const int q0 = qt * 16;   // tiles past the end read zeros
+        Qb.ld4(in.qa, Qb.at(q0 + c, hc + 4 * g));   // A of S: Q[q0+c][4g+s]
+        Gb.ld4(in.da, Gb.at(q0 + c, hc + 4 * g));   // A of dP: dO[q0+c][4g+s]
+        const int qg = q0 + 4 * g;                  // B of dV / dK: rows qg + s, dim c
+        const int og = Gb.at(qg, hc + c), oq = Qb.at(qg, hc + c), oo = Ob.at(qg, hc + c), od = dQb.at(qg, hc + c);
 #pragma unroll
-        for (int s = 0; s < 4; ++s) {                           // B of dV / dK: rows 4g+s, dim c
+        for (int s = 0; s < 4; ++s) {
+            in.db[s] = Gb.ld1(og, s * Gb.sT4);
+            in.qb[s] = Qb.ld1(oq, s * Qb.sT4);
+            in.ob[s] = Ob.ld1(oo, s * Ob.sT4);
+            in.st[s] = __builtin_bit_cast(f32x2, __builtin_amdgcn_raw_buffer_load_b64(rsStat, 8 * qg, 8 * s, 0));
+            in.dqo[s] = nkc == 1 ? dQb.ld1(od, s * dQb.sT4) : 0.f;
+        }
+    };
+    auto body = [&](const QIn& in, int qt) {
+        const int q0 = qt * 16;
+        float mm[4], li[4], del[4];
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
             const int qq = q0 + 4 * g + s;
-            const int qcl = min(qq, Tq - 1);
-            db[s] = load1(Gb, gsT, qq, Tq, hc + c);
-            qb[s] = load1(Qb, qsT, qq, Tq, hc + c);
-            float pr = db[s] * Ob[qcl * osT + hc + c];          // delta = rowsum(dO * O)
-            pr += shfl(pr, lane ^ 1);
-            pr += shfl(pr, lane ^ 2);
-            pr += shfl(pr, lane ^ 4);
-            pr += shfl(pr, lane ^ 8);
-            del[s] = pr;
+            // delta = rowsum(dO * O): the 16 dims of query qq sit in one DPP row (lanes c)
+            del[s] = row16_sum(in.db[s] * in.ob[s]);
             // padded queries: max = +inf, 1/sum = 0 make P = exp(-inf) * 0 = 0 (and with it dS)
             const bool qok = qq < Tq;
-            const float m0 = stats[2 * (sbase + qcl)], l0 = stats[2 * (sbase + qcl) + 1];
-            mm[s] = qok ? m0 : INFINITY;
-            li[s] = qok ? l0 : 0.f;
+            mm[s] = qok ? in.st[s][0] : INFINITY;
+            li[s] = qok ? in.st[s][1] : 0.f;
         }
         float ds[NT][4];
 #pragma unroll
@@ -305,9 +353,9 @@ MEP_DEV void attn_bwd_task(const mep_attn_bwd_desc& bd, int task, int kc, int nk
             const int kk = k_lo + kt * 16 + c;
             floatx4 st = zero4(), dp = zero4();
 #pragma unroll
-            for (int s = 0; s < 4; ++s) st = mfma16(qa[s], kb[kt][s], st);   // C[query 4g+r][key c]
+            for (int s = 0; s < 4; ++s) st = mfma16(in.qa[s], kb[kt][s], st);   // C[query 4g+r][key c]
 #pragma unroll
-            for (int s = 0; s < 4; ++s) dp = mfma16(da[s], vb[kt][s], dp);
+            for (int s = 0; s < 4; ++s) dp = mfma16(in.da[s], vb[kt][s], dp);
             float p[4];
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
@@ -334,8 +382,8 @@ MEP_DEV void attn_bwd_task(const mep_attn_bwd_desc& bd, int task, int kc, int nk
             }
 #pragma unroll
             for (int s = 0; s < 4; ++s) {
-                dv[kt] = mfma16(p[s], db[s], dv[kt]);         // dV[key][dim] += P^T dO
-                dk[kt] = mfma16(ds[kt][s], qb[s], dk[kt]);    // dK[key][dim] += dS^T Q
+                dv[kt] = mfma16(p[s], in.db[s], dv[kt]);         // dV[key][dim] += P^T dO
+                dk[kt] = mfma16(ds[kt][s], in.qb[s], dk[kt]);    // dK[key][dim] += dS^T Q
             }
 #pragma unroll
             for (int r = 0; r < 4; ++r) T[(4 * g + r) * TLD + kt * 16 + c] = ds[kt][r];   // T[query][key]
@@ -352,32 +400,42 @@ MEP_DEV void attn_bwd_task(const mep_attn_bwd_desc& bd, int task, int kc, int nk
             dq = mfma16(t4.w, kq[kt][3], dq);
         }
         wave_lds_sync();
-        // dq rows q0+4g+r, dim c (exclusive owner when the keys fit one chunk; else atomics)
+        // dq rows q0+4g+r, dim c (exclusive owner when the keys fit one chunk; else atomics);
+        // rows past Tq are dropped by the range check
+        const int od = dQb.at(q0 + 4 * g, hc + c);
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             const int qq = q0 + 4 * g + r;
-            if (qq < Tq) {
-                gfloat* dqp = dQb + qq * dqsT + hc + c;
-                if (nkc == 1) *dqp += dq[r] * INV_SCALE;
-                else atomicAdd(reinterpret_cast<float*>(reinterpret_cast<uintptr_t>(dqp)), dq[r] * INV_SCALE);
+            if (nkc == 1) {
+                dQb.st1(od, r * dQb.sT4, in.dqo[r] + dq[r] * INV_SCALE);
+            } else if (qq < Tq) {
+                gfloat* dqp = G<float>(bd.dq.ptr) + (int64_t)b * bd.dq.sB + (int64_t)qq * bd.dq.sT + hc + c;
+                atomicAdd(reinterpret_cast<float*>(reinterpret_cast<uintptr_t>(dqp)), dq[r] * INV_SCALE);
             }
+        }
+    };
+    QIn bufA, bufB;
+    fetch(bufA, 0);
+    for (int qt = 0; qt < nqt; qt += 2) {
+        fetch(bufB, qt + 1);
+        body(bufA, qt);
+        if (qt + 1 < nqt) {
+            fetch(bufA, qt + 2);
+            body(bufB, qt + 1);
         }
     }
     const bool same_kv = bd.dk.ptr == bd.dv.ptr && bd.dk.sB == bd.dv.sB && bd.dk.sT == bd.dv.sT;
-    gfloat* dKb = bat(bd.dk, b);
-    gfloat* dVb = bat(bd.dv, b);
-    const int dksT = (int)bd.dk.sT, dvsT = (int)bd.dv.sT;
+    const BRow dKb = brow(bd.dk, b, Tk, D), dVb = brow(bd.dv, b, Tk, D);   // keys past Tk: dropped
+    const int ok_ = dKb.at(k_lo + 4 * g, hc + c), ov_ = dVb.at(k_lo + 4 * g, hc + c);
 #pragma unroll
     for (int kt = 0; kt < NT; ++kt) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-            const int kk = k_lo + kt * 16 + 4 * g + r;
-            if (kk >= Tk) continue;
             if (same_kv) {
-                dKb[kk * dksT + hc + c] = dk[kt][r] * INV_SCALE + dv[kt][r];
+                dKb.st1(ok_, (16 * kt + r) * dKb.sT4, dk[kt][r] * INV_SCALE + dv[kt][r]);
             } else {
-                dKb[kk * dksT + hc + c] = dk[kt][r] * INV_SCALE;
-                dVb[kk * dvsT + hc + c] = dv[kt][r];
+                dKb.st1(ok_, (16 * kt + r) * dKb.sT4, dk[kt][r] * INV_SCALE);
+                dVb.st1(ov_, (16 * kt + r) * dVb.sT4, dv[kt][r]);
             }
         }
     }
@@ -388,7 +446,7 @@ MEP_DEV void attn_bwd_task(const mep_attn_bwd_desc& bd, int task, int kc, int nk
 }
 
 template <bool PREV, bool DSN>
-__global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu((PREV || DSN) ? 1 : 3))) void k_attn_bwd(const mep_attn_bwd_desc* __restrict__ descs) {
+__global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu((PREV || DSN) ? 1 : 2))) void k_attn_bwd(const mep_attn_bwd_desc* __restrict__ descs) {
     const mep_attn_bwd_desc& bd = descs[blockIdx.y];
     const mep_attn_desc& d = bd.f;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
