@@ -85,6 +85,48 @@ MEP_DEV float score(float dot, float c, float sp, float mt) {
     return sub_rn(s, mt);
 }
 
+// One batch row of a row view as a range-checked buffer (csrc/common.h raw buffer ops): row t,
+// column col at byte t * sT + 4 col.  Rows t >= n lie past the range (every view has sT >= its
+// D used columns), so their loads return 0 and their stores are dropped -- no clamps, no
+// branches, 32-bit offsets.  The base is wave-uniform by construction (one (b, h) per wave);
+// readfirstlane makes that provable so the descriptor lives in SGPRs.
+struct BRow {
+    __amdgpu_buffer_rsrc_t rs;
+    int sT4;   // row stride in bytes (wave-uniform)
+    bool vec;  // 16-byte loads allowed
+    // byte offset of (row t, column col); loads / stores take a per-lane part plus a wave-uniform
+    // part (SGPR soffset: whole rows ahead), so row steps cost no vector instructions
+    MEP_DEV int at(int t, int col) const { return t * sT4 + 4 * col; }
+    MEP_DEV float ld1(int voff, int soff = 0) const {
+        return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, voff, soff, 0));
+    }
+    MEP_DEV void ld4(float* dst, int voff) const {
+        if (vec) {
+            const f32x4 v = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, voff, 0, 0));
+            dst[0] = v[0]; dst[1] = v[1]; dst[2] = v[2]; dst[3] = v[3];
+        } else {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) dst[e] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, voff + 4 * e, 0, 0));
+        }
+    }
+    MEP_DEV void st1(int voff, int soff, float v) const {
+        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), rs, voff, soff, 0);
+    }
+};
+
+MEP_DEV __amdgpu_buffer_rsrc_t uniform_rsrc(uint64_t base, int64_t bytes) {
+    const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)base);
+    const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(base >> 32));
+    const int n = __builtin_amdgcn_readfirstlane((int)min(bytes, (int64_t)0x7fffffff));
+    return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), 0, n, 0x00020000);
+}
+
+// rows [0, n) of batch row b of a view whose used columns are [0, D)
+MEP_DEV BRow brow(const mep_rows& v, int b, int n, int D) {
+    return BRow{uniform_rsrc(v.ptr + 4ull * (uint64_t)((int64_t)b * v.sB), 4 * ((int64_t)(n - 1) * v.sT + D)),
+                4 * (int)v.sT, aligned16(v)};
+}
+
 // One forward task: batch row b, head h, 64 queries.  PREV: residual scores in; SOUT: post-mask
 // scores out; SINGLE: Tk <= 64 (one key chunk: exact two-pass softmax, each query tile is
 // finalised right after its P.V, so no running O/max/sum state stays live).
@@ -97,17 +139,12 @@ MEP_DEV void attn_fwd_task(const mep_attn_desc& d, int qc, int h, int b, int lan
     const gfloat* sprev = G<const float>(d.s_prev);
     gfloat* sout = G<float>(d.s_out);
     const gfloat* mask = G<const float>(d.mask) + (int64_t)b * d.mask_sB;
-    const gfloat* Qb = bat(d.q, b);
-    const gfloat* Kb = bat(d.k, b);
-    const gfloat* Vb = bat(d.v, b);
-    const int qsT = (int)d.q.sT, ksT = (int)d.k.sT, vsT = (int)d.v.sT;
-    const bool qv = aligned16(d.q), kv4 = aligned16(d.k);
+    const int D = d.H * HD;
+    const BRow Qb = brow(d.q, b, Tq, D), Kb = brow(d.k, b, Tk, D), Vb = brow(d.v, b, Tk, D), Xb = brow(d.x, b, Tq, D);
     const int sbase = (b * d.H + h) * Tq;        // row of (b, h, query 0) in [B,H,Tq,Tk]
     const int q_lo = qc * CH;
     const int nqt = min(NT, (Tq - q_lo + 15) / 16);
     gfloat* stats = G<float>(d.stats);
-    gfloat* Xb = bat(d.x, b);
-    const int xsT = (int)d.x.sT;
 
     floatx4 o[SINGLE ? 1 : NT];
     float m[SINGLE ? 1 : NT], l[SINGLE ? 1 : NT];
@@ -124,12 +161,9 @@ MEP_DEV void attn_fwd_task(const mep_attn_desc& d, int qc, int h, int b, int lan
             stats[2 * (sbase + q)] = mq;
             stats[2 * (sbase + q) + 1] = inv;
         }
+        const int ox = Xb.at(q_lo + qt * 16 + 4 * g, hc + c);   // rows past Tq: dropped
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const float ir = shfl(inv, 4 * g + r);
-            const int qq = q_lo + qt * 16 + 4 * g + r;
-            if (qq < Tq) Xb[qq * xsT + hc + c] = oq[r] * ir;
-        }
+        for (int r = 0; r < 4; ++r) Xb.st1(ox, r * Xb.sT4, oq[r] * shfl(inv, 4 * g + r));
     };
 
     for (int k_lo = 0; k_lo < Tk; k_lo += CH) {
@@ -138,20 +172,22 @@ MEP_DEV void attn_fwd_task(const mep_attn_desc& d, int qc, int h, int b, int lan
 #pragma unroll
         for (int kt = 0; kt < NT; ++kt) {
             const int k0 = k_lo + kt * 16;
-            load4(kf[kt], Kb, ksT, k0 + c, Tk, hc + 4 * g, kv4);          // A: K[k0+c][4g+s]
+            Kb.ld4(kf[kt], Kb.at(k0 + c, hc + 4 * g));                    // A: K[k0+c][4g+s]
+            const int ov = Vb.at(k0 + 4 * g, hc + c);                       // B of P.V: V[k0+4g+s][c]
 #pragma unroll
-            for (int s = 0; s < 4; ++s) {                                  // B of P.V: V[k0+4g+s][c]
-                const int kk = k0 + 4 * g + s;
-                vf[kt][s] = load1(Vb, vsT, kk, Tk, hc + c);
-                mt[kt][s] = mask_term(mask, kk, Tk);
+            for (int s = 0; s < 4; ++s) {
+                vf[kt][s] = Vb.ld1(ov, s * Vb.sT4);
+                mt[kt][s] = mask_term(mask, k0 + 4 * g + s, Tk);
             }
         }
+        float qfa[NT][4];                                                  // B of S^T: Q[q][4g+s]
+#pragma unroll
+        for (int qt = 0; qt < NT; ++qt) Qb.ld4(qfa[qt], Qb.at(q_lo + qt * 16 + c, hc + 4 * g));   // past Tq: 0
 #pragma unroll
         for (int qt = 0; qt < NT; ++qt) {
             if (qt >= nqt) break;
             const int q = q_lo + qt * 16 + c;
-            float qf[4];                                                   // B of S^T: Q[q][4g+s]
-            load4(qf, Qb, qsT, q, Tq, hc + 4 * g, qv);
+            const float* qf = qfa[qt];
             const int srow = (sbase + min(q, Tq - 1)) * Tk;
             float sv[NT][4];
             float mx = -INFINITY;
@@ -217,7 +253,7 @@ MEP_DEV void attn_fwd_task(const mep_attn_desc& d, int qc, int h, int b, int lan
 }
 
 template <bool PREV, bool SOUT, bool SINGLE>
-__global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu((SINGLE && !PREV) ? 5 : 1))) void k_attn_fwd(const mep_attn_desc* __restrict__ descs) {
+__global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu((SINGLE && !PREV) ? 4 : 1))) void k_attn_fwd(const mep_attn_desc* __restrict__ descs) {
     const mep_attn_desc& d = descs[blockIdx.y];
     if ((d.Tk <= CH) != SINGLE) return;    // the other variant's descriptor
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -232,48 +268,6 @@ MEP_DEV void wave_lds_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-
-// One batch row of a row view as a range-checked buffer (csrc/common.h raw buffer ops): row t,
-// column col at byte t * sT + 4 col.  Rows t >= n lie past the range (every view has sT >= its
-// D used columns), so their loads return 0 and their stores are dropped -- no clamps, no
-// branches, 32-bit offsets.  The base is wave-uniform by construction (one (b, h) per wave);
-// readfirstlane makes that provable so the descriptor lives in SGPRs.
-struct BRow {
-    __amdgpu_buffer_rsrc_t rs;
-    int sT4;   // row stride in bytes (wave-uniform)
-    bool vec;  // 16-byte loads allowed
-    // byte offset of (row t, column col); loads / stores take a per-lane part plus a wave-uniform
-    // part (SGPR soffset: whole rows ahead), so row steps cost no vector instructions
-    MEP_DEV int at(int t, int col) const { return t * sT4 + 4 * col; }
-    MEP_DEV float ld1(int voff, int soff = 0) const {
-        return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, voff, soff, 0));
-    }
-    MEP_DEV void ld4(float* dst, int voff) const {
-        if (vec) {
-            const f32x4 v = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, voff, 0, 0));
-            dst[0] = v[0]; dst[1] = v[1]; dst[2] = v[2]; dst[3] = v[3];
-        } else {
-#pragma unroll
-            for (int e = 0; e < 4; ++e) dst[e] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, voff + 4 * e, 0, 0));
-        }
-    }
-    MEP_DEV void st1(int voff, int soff, float v) const {
-        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), rs, voff, soff, 0);
-    }
-};
-
-MEP_DEV __amdgpu_buffer_rsrc_t uniform_rsrc(uint64_t base, int64_t bytes) {
-    const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)base);
-    const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(base >> 32));
-    const int n = __builtin_amdgcn_readfirstlane((int)min(bytes, (int64_t)0x7fffffff));
-    return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), 0, n, 0x00020000);
-}
-
-// rows [0, n) of batch row b of a view whose used columns are [0, D)
-MEP_DEV BRow brow(const mep_rows& v, int b, int n, int D) {
-    return BRow{uniform_rsrc(v.ptr + 4ull * (uint64_t)((int64_t)b * v.sB), 4 * ((int64_t)(n - 1) * v.sT + D)),
-                4 * (int)v.sT, aligned16(v)};
 }
 
 // One backward task: batch row b, head h, 64 keys.  PREV: residual scores (writes dS_prev and the
