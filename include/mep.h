@@ -325,6 +325,15 @@ int mep_head_fwd_bwd(const mep_head_desc* d, mep_stream_t stream);
 int mep_head_reduce(const mep_head_desc* d, uint64_t g_trans, uint64_t g_ln_w, uint64_t g_ln_b,
                     uint64_t g_wo, uint64_t g_bo, uint64_t g_wc0, uint64_t g_wc1, uint64_t loss,
                     mep_stream_t stream);
+/* Every gradient reduction of a step in one launch (no dependencies between them): the
+ * mep_wgrad_reduce split sums (wgrad_tiles per descriptor, as mep_wgrad_reduce's max_tiles), the
+ * mep_colsum column sums (colsum_tiles per descriptor) and, when head is not NULL, the
+ * mep_head_reduce sums of the fusion head (same arguments).  Results are bitwise identical to the
+ * three separate launches. */
+int mep_reduce_grads(const mep_wgrad_desc* wgrad, int n_wgrad, int wgrad_tiles, const mep_colsum_desc* colsum,
+                     int n_colsum, int colsum_tiles, const mep_head_desc* head, uint64_t g_trans, uint64_t g_ln_w,
+                     uint64_t g_ln_b, uint64_t g_wo, uint64_t g_bo, uint64_t g_wc0, uint64_t g_wc1, uint64_t loss,
+                     mep_stream_t stream);
 int mep_head_partial_stride(int NC);
 
 /* multi_circle_loss per row (cmu-mosei/run.py:342-351) as a standalone op for callers that

@@ -420,6 +420,49 @@ MEP_DEV void wave_store16(const float* src, int lda, const mep_rows& dst, int r0
     }
 }
 
+
+// ------------------------------------------------------------------ gradient reductions
+// Block bodies shared by their own launches and the fused mep_reduce_grads launch (256 threads).
+// Weight-gradient split sum (gemm.hip k_wgrad_reduce): block bx of descriptor d sums the
+// n_split partials of 256 consecutive (n, k) entries in a fixed order.
+MEP_DEV void wgrad_reduce_block(const mep_wgrad_desc& d, int bx) {
+    const int64_t nk = (int64_t)d.N * d.Ktot;
+    const int64_t i = (int64_t)bx * 256 + threadIdx.x;
+    if (i >= nk) return;
+    const gfloat* part = G<const float>(d.partial);
+    float s = 0.f;
+    for (int sp = 0; sp < d.n_split; ++sp) s += part[sp * nk + i];
+    const int n = (int)(i / d.Ktot);
+    int k = (int)(i - (int64_t)n * d.Ktot);
+    int j = 0;
+    while (j < d.n_b - 1 && k >= d.kb[j]) { k -= d.kb[j]; ++j; }
+    gfloat* o = G<float>(d.out[j]) + (d.out_trans ? (int64_t)k * d.ldo[j] + n : (int64_t)n * d.ldo[j] + k);
+    *o = d.accumulate ? *o + s : s;
+}
+
+// Column sums of a partial matrix (optim.hip k_colsum): block bx = 32 columns x 8 row groups,
+// fixed-order combine.
+MEP_DEV void colsum_block(const mep_colsum_desc& d, int bx) {
+    const int cl = threadIdx.x & 31, g = threadIdx.x >> 5;
+    const int c = bx * 32 + cl;
+    if (bx * 32 >= d.n_cols) return;   // whole block
+    __shared__ float red[8][32];
+    float s = 0.f;
+    if (c < d.n_cols) {
+        const gfloat* p = G<const float>(d.partial) + c;
+        for (int r = g; r < d.n_rows; r += 8) s += p[(int64_t)r * d.ld];
+    }
+    red[g][cl] = s;
+    __syncthreads();
+    if (g == 0 && c < d.n_cols) {
+        float t = 0.f;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) t += red[k][cl];
+        gfloat* o = G<float>(d.out) + c;
+        *o = d.accumulate ? *o + t : t;
+    }
+}
+
 }  // namespace mep
 
 // error plumbing shared by the launchers (api.cpp)

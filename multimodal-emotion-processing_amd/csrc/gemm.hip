@@ -343,19 +343,7 @@ __global__ __launch_bounds__(WG_THREADS, 2) void k_wgrad(const mep_wgrad_desc* _
 }
 
 __global__ __launch_bounds__(256) void k_wgrad_reduce(const mep_wgrad_desc* __restrict__ descs) {
-    const mep_wgrad_desc& d = descs[blockIdx.y];
-    const int64_t nk = (int64_t)d.N * d.Ktot;
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= nk) return;
-    const gfloat* part = G<const float>(d.partial);
-    float s = 0.f;
-    for (int sp = 0; sp < d.n_split; ++sp) s += part[sp * nk + i];
-    const int n = (int)(i / d.Ktot);
-    int k = (int)(i - (int64_t)n * d.Ktot);
-    int j = 0;
-    while (j < d.n_b - 1 && k >= d.kb[j]) { k -= d.kb[j]; ++j; }
-    gfloat* o = G<float>(d.out[j]) + (d.out_trans ? (int64_t)k * d.ldo[j] + n : (int64_t)n * d.ldo[j] + k);
-    *o = d.accumulate ? *o + s : s;
+    wgrad_reduce_block(descs[blockIdx.y], blockIdx.x);
 }
 
 // ---------------------------------------------------------------- unify projection

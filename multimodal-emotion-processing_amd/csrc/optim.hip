@@ -105,25 +105,7 @@ __global__ void k_seed(uint64_t* seed) { seed[0] = mix64(seed[0] + 0x9E3779B97F4
 // ---------------------------------------------------------------- colsum / row sums
 // workgroup = 32 columns x 8 row groups; fixed-order combine (deterministic)
 __global__ __launch_bounds__(256) void k_colsum(const mep_colsum_desc* __restrict__ descs) {
-    const mep_colsum_desc& d = descs[blockIdx.y];
-    const int cl = threadIdx.x & 31, g = threadIdx.x >> 5;
-    const int c = blockIdx.x * 32 + cl;
-    if ((int)blockIdx.x * 32 >= d.n_cols) return;
-    __shared__ float red[8][32];
-    float s = 0.f;
-    if (c < d.n_cols) {
-        const gfloat* p = G<const float>(d.partial) + c;
-        for (int r = g; r < d.n_rows; r += 8) s += p[(int64_t)r * d.ld];
-    }
-    red[g][cl] = s;
-    __syncthreads();
-    if (g == 0 && c < d.n_cols) {
-        float t = 0.f;
-#pragma unroll
-        for (int k = 0; k < 8; ++k) t += red[k][cl];
-        gfloat* o = G<float>(d.out) + c;
-        *o = d.accumulate ? *o + t : t;
-    }
+    colsum_block(descs[blockIdx.y], blockIdx.x);
 }
 
 // out = sum of sources, 4 columns per thread (D % 4 == 0 for every model width)

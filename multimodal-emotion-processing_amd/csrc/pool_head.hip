@@ -315,7 +315,7 @@ struct HeadGrads {
 // records each, 8 row groups per column (+ the batch loss in workgroup 0); workgroups after
 // that: 32 columns k of one classifier e, dWc_e[n][k] = sum_b dlogit_e[b][n] pooled_e[b][k] for
 // every n, rows split over 8 groups.  Fixed summation order (deterministic).
-__global__ __launch_bounds__(256) void k_head_reduce(mep_head_desc d, HeadGrads g) {
+MEP_DEV void head_reduce_block(const mep_head_desc& d, const HeadGrads& g, int bx) {
     const int NC = d.NC, F = d.F, B = d.B;
     const HeadOff o = head_off(NC);
     const int nA = o.dl0;                 // everything before the dlogit records
@@ -323,14 +323,14 @@ __global__ __launch_bounds__(256) void k_head_reduce(mep_head_desc d, HeadGrads 
     const int cl = threadIdx.x & 31, rg = threadIdx.x >> 5;
     const gfloat* part = G<const float>(d.partial);
     __shared__ float red[8][NCMAX][33];
-    if ((int)blockIdx.x < nA32) {
-        const int i = blockIdx.x * 32 + cl;
+    if ((int)bx < nA32) {
+        const int i = bx * 32 + cl;
         float s = 0.f;
         if (i < nA)
             for (int b = rg; b < B; b += 8) s += part[(int64_t)b * o.stride + i];
         red[rg][0][cl] = s;
         float ls = 0.f;
-        if (blockIdx.x == 0)
+        if (bx == 0)
             for (int b = threadIdx.x; b < B; b += 256) ls += G<const float>(d.row_loss)[b];
         __syncthreads();
         if (rg == 0 && i < nA) {
@@ -345,7 +345,7 @@ __global__ __launch_bounds__(256) void k_head_reduce(mep_head_desc d, HeadGrads 
             else dst = g.g_trans + (i - o.trans);
             *G<float>(reinterpret_cast<uint64_t>(dst)) = t;
         }
-        if (blockIdx.x == 0) {
+        if (bx == 0) {
             ls = wave_sum(ls);
             __syncthreads();
             if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6][1][0] = ls;
@@ -355,7 +355,7 @@ __global__ __launch_bounds__(256) void k_head_reduce(mep_head_desc d, HeadGrads 
         }
         return;
     }
-    const int wb = blockIdx.x - nA32;
+    const int wb = bx - nA32;
     const int nkb = (F + 31) / 32;
     const int e = wb / nkb, k = (wb - e * nkb) * 32 + cl;
     const float* pooled = reinterpret_cast<const float*>(e ? d.pooled1 : d.pooled0);
@@ -384,6 +384,28 @@ __global__ __launch_bounds__(256) void k_head_reduce(mep_head_desc d, HeadGrads 
             *G<float>(reinterpret_cast<uint64_t>(out + (int64_t)n * F + k)) = t;
         }
     }
+}
+
+__global__ __launch_bounds__(256) void k_head_reduce(mep_head_desc d, HeadGrads g) {
+    head_reduce_block(d, g, blockIdx.x);
+}
+
+__host__ __device__ inline int head_reduce_blocks(const mep_head_desc& d) {
+    return (head_off(d.NC).dl0 + 31) / 32 + 2 * ((d.F + 31) / 32);
+}
+
+// Every gradient reduction of a training step in ONE launch: the head-parameter sums (largest
+// blocks first), the weight-gradient split sums and the column sums, each block taking one job
+// (block bodies in common.h); there are no dependencies between them.
+__global__ __launch_bounds__(256) void k_reduce_grads(const mep_wgrad_desc* __restrict__ wd, int n_wd, int wd_tiles,
+                                                      const mep_colsum_desc* __restrict__ cd, int n_cd, int cd_tiles,
+                                                      mep_head_desc hd, HeadGrads hg, int head_blocks) {
+    int bx = blockIdx.x;
+    if (bx < head_blocks) { head_reduce_block(hd, hg, bx); return; }
+    bx -= head_blocks;
+    if (bx < n_wd * wd_tiles) { wgrad_reduce_block(wd[bx / wd_tiles], bx % wd_tiles); return; }
+    bx -= n_wd * wd_tiles;
+    if (bx < n_cd * cd_tiles) colsum_block(cd[bx / cd_tiles], bx % cd_tiles);
 }
 
 __global__ __launch_bounds__(64) void k_circle_fwd(const float* __restrict__ logits, const void* labels, int lf,
@@ -451,6 +473,31 @@ extern "C" int mep_head_fwd_bwd(const mep_head_desc* d, mep_stream_t stream) {
     const int groups = d->rdrop ? d->B / 2 : d->B;
     hipLaunchKernelGGL(k_head, dim3(groups), dim3(256), 0, (hipStream_t)stream, *d);
     return mep_check_launch("mep_head_fwd_bwd");
+}
+
+extern "C" int mep_reduce_grads(const mep_wgrad_desc* wgrad, int n_wgrad, int wgrad_tiles, const mep_colsum_desc* colsum,
+                                int n_colsum, int colsum_tiles, const mep_head_desc* head, uint64_t g_trans,
+                                uint64_t g_ln_w, uint64_t g_ln_b, uint64_t g_wo, uint64_t g_bo, uint64_t g_wc0,
+                                uint64_t g_wc1, uint64_t loss, mep_stream_t stream) {
+    if (head && head->NC > NCMAX) { mep_set_error("mep_reduce_grads: invalid head descriptor"); return MEP_EINVAL; }
+    if (n_wgrad < 0 || n_colsum < 0 || (n_wgrad && wgrad_tiles <= 0) || (n_colsum && colsum_tiles <= 0)) {
+        mep_set_error("mep_reduce_grads: invalid grid");
+        return MEP_EINVAL;
+    }
+    mep_head_desc hd{};
+    HeadGrads g{};
+    int hb = 0;
+    if (head) {
+        hd = *head;
+        g = HeadGrads{(float*)g_trans, (float*)g_ln_w, (float*)g_ln_b, (float*)g_wo, (float*)g_bo,
+                      (float*)g_wc0, (float*)g_wc1, (float*)loss};
+        hb = head_reduce_blocks(hd);
+    }
+    const int blocks = hb + n_wgrad * wgrad_tiles + n_colsum * colsum_tiles;
+    if (blocks <= 0) return 0;
+    hipLaunchKernelGGL(k_reduce_grads, dim3(blocks), dim3(256), 0, (hipStream_t)stream, wgrad, n_wgrad,
+                       wgrad_tiles, colsum, n_colsum, colsum_tiles, hd, g, hb);
+    return mep_check_launch("mep_reduce_grads");
 }
 
 extern "C" int mep_head_reduce(const mep_head_desc* d, uint64_t g_trans, uint64_t g_ln_w, uint64_t g_ln_b,

@@ -524,7 +524,6 @@ class TriModalPlan:
             self.head.ext_dlogits = ext_dlogits.data_ptr()
             _lib.call('mep_head_fwd_bwd', ctypes.byref(self.head), stream=stream)
             self.head.ext_dlogits = 0
-        _lib.call('mep_head_reduce', ctypes.byref(self.head), *self.head_grads, stream=stream)
         launch("mep_pool_bwd", self.d_pool, self.t_poolb, stream)
         for i in reversed(range(nl)):
             launch('mep_block_epi_bwd', self.d_epib[i], self.t_epi[i], stream, threads=sp.D)
@@ -533,8 +532,10 @@ class TriModalPlan:
         if sp.unify_norm:
             launch('mep_layernorm_bwd', self.d_ulnb, cdiv(max(self.ntok.values()), 64), stream)
         launch('mep_wgrad', self.d_wgrad, self.t_wgrad, stream)
-        launch('mep_wgrad_reduce', self.d_wgrad, self.t_wgred, stream)
-        launch('mep_colsum', self.d_colsum, self.t_colsum, stream)
+        # weight-gradient split sums, LayerNorm / residual-coefficient column sums and the head
+        # parameter sums: one launch
+        _lib.call('mep_reduce_grads', self.d_wgrad.ptr, self.d_wgrad.n, self.t_wgred, self.d_colsum.ptr,
+                  self.d_colsum.n, self.t_colsum, ctypes.byref(self.head), *self.head_grads, stream=stream)
 
     def advance_seed(self, stream=None):
         _lib.call('mep_seed_advance', ctypes.c_void_p(self.seed.data_ptr()), stream=stream)
