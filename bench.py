@@ -12,8 +12,10 @@ Arithmetic: fp32 end to end (the reference has no AMP; fp32 keeps the 1e-4 logit
 Rank 0 prints one JSON line.
 """
 import argparse
+import glob
 import json
 import os
+import re
 import sys
 import time
 
@@ -56,6 +58,28 @@ class LaunchTimer:
             t, n = out.get(name, (0.0, 0))
             out[name] = (t + a.elapsed_time(b) / 1e3, n + 1)
         return out
+
+
+# launch name -> kernel symbol prefix in the rocprofv3 summaries (scripts/parse_prof.py)
+KERNEL_OF = {'mep_attn_bwd': 'k_attn_bwd', 'mep_attn_fwd': 'k_attn_fwd', 'mep_block_epi_fwd': 'k_epi_fwd',
+             'mep_block_epi_bwd': 'k_epi_bwd', 'mep_wgrad': 'k_wgrad', 'mep_unify': 'k_unify',
+             'mep_pool_fwd': 'k_pool_fwd', 'mep_pool_bwd': 'k_pool_bwd'}
+
+
+def pmc_traffic(launch):
+    """(HBM bytes per dispatch, source file) of the kernel behind `launch` from the newest
+    committed PMC pass (profiles/r<round>_v<n>_pmc.json: (2 FETCH_SIZE + WRITE_SIZE) x 1024,
+    the gfx950 correction of MI355X_MICROARCH.md section HBM), or (None, None)."""
+    def key(f):
+        return [int(x) for x in re.findall(r'\d+', os.path.basename(f))]
+    files = sorted(glob.glob(os.path.join(ROOT, 'profiles', 'r*_v*_pmc.json')), key=key)
+    prefix = KERNEL_OF.get(launch)
+    if not files or prefix is None:
+        return None, None
+    for k, v in json.load(open(files[-1])).items():
+        if k.startswith(prefix) and 'hbm_bytes_per_dispatch' in v:
+            return int(v['hbm_bytes_per_dispatch']), os.path.relpath(files[-1], ROOT)
+    return None, None
 
 
 def synth_batch(rank, device):
@@ -160,7 +184,7 @@ def main():
     launches_per_step = n_dom // reps
     flops, nbytes = costs[dom]
     rl = roofline.roofline_entry(dom, flops / launches_per_step, nbytes / launches_per_step, per_launch_s)
-    rl['traffic'] = None
+    rl['traffic'], rl['traffic_source'] = pmc_traffic(dom)
     rl['avg_launch_us'] = round(per_launch_s * 1e6, 2)
 
     out = {
