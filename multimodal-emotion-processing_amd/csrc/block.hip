@@ -78,10 +78,17 @@ MEP_DEV void epi_fwd_tiles(const mep_epi_desc& d, const AP& wp, const AM& wm, in
         const int tc = min(tok, ntok - 1);
         const gfloat* xr = row_ptr(d.x, tc) + 4 * g;
         const gfloat* qr = row_ptr(d.q, tc) + 4 * g;
+        // every B fragment of the tile (x and q rows, 4 consecutive features per lane) is issued
+        // before the first MFMA: one memory latency per tile instead of one per k block
+        f32x4 xb[KB], qb[KB];
+#pragma unroll
+        for (int kb = 0; kb < KB; ++kb) xb[kb] = ld4w(xr + 16 * kb);
+#pragma unroll
+        for (int kb = 0; kb < KB; ++kb) qb[kb] = ld4w(qr + 16 * kb);
         f32x4 xp[NI], z[NI];
 #pragma unroll
         for (int i = 0; i < NI; ++i) { xp[i] = zero_f4(); z[i] = zero_f4(); }
-        tgemm<NI, KB>(xp, wp, [&](int kb) { return ld4w(xr + 16 * kb); });
+        tgemm<NI, KB>(xp, wp, [&](int kb) { return xb[kb]; });
         if (p > 0.f) {
 #pragma unroll
             for (int i = 0; i < NI; ++i)
@@ -89,7 +96,7 @@ MEP_DEV void epi_fwd_tiles(const mep_epi_desc& d, const AP& wp, const AM& wm, in
                 for (int r = 0; r < 4; ++r)
                     xp[i][r] *= drop_scale(seed, 2u * d.drop_stream, (uint64_t)tok * D + 16 * i + 4 * g + r, p);
         }
-        tgemm<NI, KB>(z, wm, [&](int kb) { return ld4w(qr + 16 * kb); });   // q half of [q | xp]
+        tgemm<NI, KB>(z, wm, [&](int kb) { return qb[kb]; });              // q half of [q | xp]
         tgemm<NI, KB>(z, wm_x, [&](int kb) { return xp[kb]; });            // xp half
         // LayerNorm over the D features of token c: in-lane sum + the 4 lane groups
         float sum = 0.f;
