@@ -25,16 +25,25 @@ struct Segs {
     int n;
 };
 
+// Segments whose offset is a multiple of 4 floats run as float4 streams (the flat buffers are
+// 256-byte aligned), the rest of a segment (tail, or a misaligned segment) element by element.
 __global__ __launch_bounds__(OPT_THREADS) void k_sqnorm(const float* __restrict__ g, Segs segs,
                                                         float* __restrict__ partial, int* __restrict__ step) {
     float s = 0.f;
+    const int64_t gid = (int64_t)blockIdx.x * OPT_THREADS + threadIdx.x;
     const int64_t stride = (int64_t)gridDim.x * OPT_THREADS;
     for (int si = 0; si < segs.n; ++si) {
         const float* gs = g + segs.off[si];
-        for (int64_t i = (int64_t)blockIdx.x * OPT_THREADS + threadIdx.x; i < segs.len[si]; i += stride) {
-            const float v = gs[i];
-            s = fmaf(v, v, s);
+        const int64_t n = segs.len[si];
+        const int64_t n4 = (segs.off[si] & 3) == 0 ? n >> 2 : 0;
+        for (int64_t i = gid; i < n4; i += stride) {
+            const float4 v = ldg4(G<const float>(reinterpret_cast<uint64_t>(gs)) + 4 * i);
+            s = fmaf(v.x, v.x, s);
+            s = fmaf(v.y, v.y, s);
+            s = fmaf(v.z, v.z, s);
+            s = fmaf(v.w, v.w, s);
         }
+        for (int64_t i = 4 * n4 + gid; i < n; i += stride) s = fmaf(gs[i], gs[i], s);
     }
     __shared__ float red[OPT_THREADS / 64];
     s = wave_sum(s);
@@ -46,6 +55,22 @@ __global__ __launch_bounds__(OPT_THREADS) void k_sqnorm(const float* __restrict_
         partial[blockIdx.x] = t;
         if (blockIdx.x == 0 && step) step[0] += 1;
     }
+}
+
+struct AdamCoef {
+    float gs, step_size, bc2_sqrt, decay, one_m_b1, b2, one_m_b2, wd, eps;
+    int decoupled;
+};
+
+MEP_DEV void adam_elem(float& pv, float& gv, float& mv, float& vv, const AdamCoef& k) {
+    gv = gv * k.gs;
+    float ge = gv;
+    if (k.decoupled) pv *= k.decay;
+    else if (k.wd != 0.f) ge = ge + pv * k.wd;
+    mv = mv + (ge - mv) * k.one_m_b1;
+    vv = vv * k.b2 + k.one_m_b2 * ge * ge;
+    const float denom = sqrtf(vv) / k.bc2_sqrt + k.eps;
+    pv = pv - k.step_size * mv / denom;
 }
 
 // hyper: [lr, beta1, beta2, eps, weight_decay, max_norm, grad_scale]
@@ -71,31 +96,47 @@ __global__ __launch_bounds__(OPT_THREADS) void k_clip_adam(float* __restrict__ p
     if (blockIdx.x == 0 && threadIdx.x == 0 && gnorm_out) *gnorm_out = total;
     const int t = step[0];
     const double lr = hyper[0], b1 = hyper[1], b2 = hyper[2], wd = hyper[4];
-    const float eps = hyper[3];
     const double bc1 = 1.0 - pow(b1, (double)t), bc2 = 1.0 - pow(b2, (double)t);
-    const float step_size = (float)(lr / bc1);
-    const float bc2_sqrt = (float)sqrt(bc2);
-    const float decay = (float)(1.0 - lr * wd);
-    const float one_m_b1 = (float)(1.0 - b1), fb2 = (float)b2, one_m_b2 = (float)(1.0 - b2);
-    const float fwd = (float)wd;
+    AdamCoef k;
+    k.gs = gscale * coef;
+    k.step_size = (float)(lr / bc1);
+    k.bc2_sqrt = (float)sqrt(bc2);
+    k.decay = (float)(1.0 - lr * wd);
+    k.one_m_b1 = (float)(1.0 - b1);
+    k.b2 = (float)b2;
+    k.one_m_b2 = (float)(1.0 - b2);
+    k.wd = (float)wd;
+    k.eps = hyper[3];
+    k.decoupled = decoupled;
+    const int64_t gid = (int64_t)blockIdx.x * OPT_THREADS + threadIdx.x;
     const int64_t stride = (int64_t)gridDim.x * OPT_THREADS;
     for (int si = 0; si < segs.n; ++si) {
-        const int64_t off = segs.off[si];
-        for (int64_t i = (int64_t)blockIdx.x * OPT_THREADS + threadIdx.x; i < segs.len[si]; i += stride) {
+        const int64_t off = segs.off[si], n = segs.len[si];
+        const int64_t n4 = (off & 3) == 0 ? n >> 2 : 0;
+        for (int64_t i = gid; i < n4; i += stride) {
+            const int64_t j = off + 4 * i;
+            gfloat* pp = G<float>(reinterpret_cast<uint64_t>(p)) + j;
+            gfloat* gp = G<float>(reinterpret_cast<uint64_t>(g)) + j;
+            gfloat* mp = G<float>(reinterpret_cast<uint64_t>(m)) + j;
+            gfloat* vp = G<float>(reinterpret_cast<uint64_t>(v)) + j;
+            float4 P4 = ldg4(pp), G4 = ldg4(gp), M4 = ldg4(mp), V4 = ldg4(vp);
+            adam_elem(P4.x, G4.x, M4.x, V4.x, k);
+            adam_elem(P4.y, G4.y, M4.y, V4.y, k);
+            adam_elem(P4.z, G4.z, M4.z, V4.z, k);
+            adam_elem(P4.w, G4.w, M4.w, V4.w, k);
+            stg4(pp, P4);
+            stg4(gp, G4);
+            stg4(mp, M4);
+            stg4(vp, V4);
+        }
+        for (int64_t i = 4 * n4 + gid; i < n; i += stride) {
             const int64_t j = off + i;
-            float gv = g[j] * gscale * coef;
+            float pv = p[j], gv = g[j], mv = m[j], vv = v[j];
+            adam_elem(pv, gv, mv, vv, k);
+            p[j] = pv;
             g[j] = gv;
-            float pv = p[j];
-            if (decoupled) pv *= decay;
-            else if (fwd != 0.f) gv = gv + pv * fwd;
-            float mv = m[j];
-            mv = mv + (gv - mv) * one_m_b1;
-            float vv = v[j] * fb2 + one_m_b2 * gv * gv;
-            const float denom = sqrtf(vv) / bc2_sqrt + eps;
-            pv = pv - step_size * mv / denom;
             m[j] = mv;
             v[j] = vv;
-            p[j] = pv;
         }
     }
 }
@@ -147,7 +188,8 @@ extern "C" int mep_clip_adam(float* params, float* grads, float* exp_avg, float*
         }
         if (segs[i].length > longest) longest = segs[i].length;
     }
-    int grid = (int)((longest + OPT_THREADS * 4 - 1) / (OPT_THREADS * 4));
+    // 4 float4 per thread per pass: one partial per workgroup for the clip's norm
+    int grid = (int)((longest + OPT_THREADS * 16 - 1) / (OPT_THREADS * 16));
     grid = grid < 1 ? 1 : (grid > NPART ? NPART : grid);
     hipLaunchKernelGGL(k_sqnorm, dim3(grid), dim3(OPT_THREADS), 0, (hipStream_t)stream, grads, s, partial, step);
     int rc = mep_check_launch("mep_clip_adam/sqnorm");
