@@ -30,19 +30,59 @@ struct EpiGeo {
     static constexpr int BWD = 2 * D * LP + (WP_LDS ? D * LP : 0);
 };
 
-// W [R][C] (row stride C, 16-byte rows) -> LDS rows of stride L
-MEP_DEV void stage_rows(lfloat* dst, int L, const gfloat* src, int R, int C) {
-    const int n4 = C >> 2;
-    for (int idx = threadIdx.x; idx < R * n4; idx += ETHREADS) {
-        const int r = idx / n4, c4 = idx - r * n4;
-        *reinterpret_cast<lf32x4*>(dst + r * L + 4 * c4) = *reinterpret_cast<const MEP_G f32x4*>(src + r * C + 4 * c4);
+// W [R][C] (row stride C, 16-byte rows) -> LDS rows of stride L; every 16-byte load of the
+// thread is issued before its first LDS write (one L2 latency for the whole staging)
+template <int R, int C>
+MEP_DEV void stage_rows(lfloat* dst, int L, const gfloat* src) {
+    constexpr int n4 = C / 4, NQ = R * n4;
+    constexpr int PER = (NQ + ETHREADS - 1) / ETHREADS;
+    f32x4 v[PER];
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+        const int idx = threadIdx.x + ETHREADS * k;
+        if (idx < NQ) {
+            const int r = idx / n4, c4 = idx - r * n4;
+            v[k] = ld4w(src + r * C + 4 * c4);
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+        const int idx = threadIdx.x + ETHREADS * k;
+        if (idx < NQ) {
+            const int r = idx / n4, c4 = idx - r * n4;
+            *reinterpret_cast<lf32x4*>(dst + r * L + 4 * c4) = v[k];
+        }
     }
 }
-// W [R][C] -> W^T in LDS rows of stride L (row c = column c of W); lanes run along C (coalesced reads)
-MEP_DEV void stage_cols_t(lfloat* dst, int L, const gfloat* src, int R, int C) {
-    for (int idx = threadIdx.x; idx < R * C; idx += ETHREADS) {
-        const int r = idx / C, c = idx - r * C;
-        dst[c * L + r] = src[idx];
+// W [R][C] -> W^T in LDS rows of stride L (row c = column c of W), in 4 x 4 blocks: a thread
+// loads 4 rows x 4 consecutive columns (16-byte loads, consecutive threads along C: coalesced)
+// and writes 4 transposed 16-byte rows; every load of the thread is issued before the first
+// LDS write, so the staging costs about one L2 latency, not one per element.
+template <int R, int C>
+MEP_DEV void stage_cols_t(lfloat* dst, int L, const gfloat* src) {
+    static_assert(R % 4 == 0 && C % 4 == 0, "4 x 4 blocks");
+    constexpr int CB = C / 4, NB = (R / 4) * CB;
+    constexpr int PER = (NB + ETHREADS - 1) / ETHREADS;
+    f32x4 v[PER][4];
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+        const int b = threadIdx.x + ETHREADS * k;
+        if (b < NB) {
+            const int rb = b / CB, cj = b - rb * CB;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[k][e] = ld4w(src + (4 * rb + e) * C + 4 * cj);
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+        const int b = threadIdx.x + ETHREADS * k;
+        if (b < NB) {
+            const int rb = b / CB, cj = b - rb * CB;
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+                *reinterpret_cast<lf32x4*>(dst + (4 * cj + e) * L + 4 * rb) =
+                    f32x4{v[k][0][e], v[k][1][e], v[k][2][e], v[k][3][e]};
+        }
     }
 }
 
@@ -144,11 +184,11 @@ __global__ __launch_bounds__(ETHREADS) void k_epi_fwd(const mep_epi_desc* __rest
     if (!tile_range(d.ntok, t_begin, t_end)) return;   // whole workgroup
     __shared__ __attribute__((aligned(16))) float smem[Geo::FWD];
     lfloat* wm = (lfloat*)&smem[0];
-    stage_rows(wm, Geo::LM, G<const float>(d.wm), D, 2 * D);
+    stage_rows<D, 2 * D>(wm, Geo::LM, G<const float>(d.wm));
     const WRows<lfloat> am{wm, Geo::LM, 0, 0};
     if constexpr (Geo::WP_LDS) {
         lfloat* wp = wm + D * Geo::LM;
-        stage_rows(wp, Geo::LP, G<const float>(d.wp), D, D);
+        stage_rows<D, D>(wp, Geo::LP, G<const float>(d.wp));
         __syncthreads();
         epi_fwd_tiles<D>(d, WRows<lfloat>{wp, Geo::LP, 0, 0}, am, t_begin, t_end);
     } else {
@@ -290,11 +330,11 @@ __global__ __launch_bounds__(ETHREADS) void k_epi_bwd(const mep_epi_bwd_desc* __
     if (!tile_range(d.ntok, t_begin, t_end)) return;
     __shared__ __attribute__((aligned(16))) float smem[Geo::BWD];
     lfloat* wmt = (lfloat*)&smem[0];              // Wm^T [2D][LP]
-    stage_cols_t(wmt, Geo::LP, G<const float>(d.wm), D, 2 * D);
+    stage_cols_t<D, 2 * D>(wmt, Geo::LP, G<const float>(d.wm));
     const WRows<lfloat> am{wmt, Geo::LP, 0, 0};
     if constexpr (Geo::WP_LDS) {
         lfloat* wpt = wmt + 2 * D * Geo::LP;      // Wp^T [D][LP]
-        stage_cols_t(wpt, Geo::LP, G<const float>(d.wp), D, D);
+        stage_cols_t<D, D>(wpt, Geo::LP, G<const float>(d.wp));
         __syncthreads();
         epi_bwd_tiles<D>(bd, am, WRows<lfloat>{wpt, Geo::LP, 0, 0}, t_begin, t_end);
     } else {
