@@ -450,10 +450,27 @@ __global__ __launch_bounds__(UN_THREADS) void k_unify(const mep_gemm_desc* __res
     const int N = d.N, K = d.K, KB = (K + 15) >> 4, ldl = 16 * KB + 4;
     const bool wlds = N * ldl <= UN_LDS;
     if (wlds) {   // W [N][K] -> LDS rows of ldl floats, zero past K
+        // wave w stages rows w, w + 8, ...; 4 rows x 320 columns of loads in flight per batch
         const gfloat* W = G<const float>(d.w);
-        for (int idx = threadIdx.x; idx < N * 16 * KB; idx += UN_THREADS) {
-            const int n = idx / (16 * KB), k = idx - n * (16 * KB);
-            wl[n * ldl + k] = k < K ? W[(int64_t)n * d.ldw + k] : 0.f;
+        const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, KP = 16 * KB;
+        for (int n0 = wave; n0 < N; n0 += 4 * UN_WAVES) {
+            for (int k0 = 0; k0 < KP; k0 += 320) {
+                float v[4][5];
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+#pragma unroll
+                    for (int j = 0; j < 5; ++j) {
+                        const int n = n0 + UN_WAVES * r, k = k0 + lane + 64 * j;
+                        v[r][j] = (n < N && k < K) ? W[(int64_t)n * d.ldw + k] : 0.f;
+                    }
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+#pragma unroll
+                    for (int j = 0; j < 5; ++j) {
+                        const int n = n0 + UN_WAVES * r, k = k0 + lane + 64 * j;
+                        if (n < N && k < KP) wl[n * ldl + k] = v[r][j];
+                    }
+            }
         }
         __syncthreads();
     }
