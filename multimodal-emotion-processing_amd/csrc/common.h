@@ -431,6 +431,7 @@ MEP_DEV void wgrad_reduce_block(const mep_wgrad_desc& d, int bx) {
     if (i >= nk) return;
     const gfloat* part = G<const float>(d.partial);
     float s = 0.f;
+#pragma unroll 8
     for (int sp = 0; sp < d.n_split; ++sp) s += part[sp * nk + i];
     const int n = (int)(i / d.Ktot);
     int k = (int)(i - (int64_t)n * d.Ktot);
@@ -450,6 +451,7 @@ MEP_DEV void colsum_block(const mep_colsum_desc& d, int bx) {
     float s = 0.f;
     if (c < d.n_cols) {
         const gfloat* p = G<const float>(d.partial) + c;
+#pragma unroll 8
         for (int r = g; r < d.n_rows; r += 8) s += p[(int64_t)r * d.ld];
     }
     red[g][cl] = s;

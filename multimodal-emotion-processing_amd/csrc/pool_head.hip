@@ -34,10 +34,22 @@ __global__ __launch_bounds__(256) void k_pool_fwd(const mep_pool_desc* __restric
     int idx = 0x7fffffff;
     if (c < d.C) {
         const gfloat* x = G<const float>(d.x) + (int64_t)b * d.T * d.C + c;
-        for (int t = g; t < d.T; t += POOL_GROUPS) {
-            const float v = x[(int64_t)t * d.C];
-            s += v;
-            if (v > mx || idx == 0x7fffffff) { mx = v; idx = t; }   // strict >: first index wins
+        // 8 time steps of loads in flight, then consumed in time order (ties: first index wins)
+        for (int t0 = g; t0 < d.T; t0 += 8 * POOL_GROUPS) {
+            float v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int t = t0 + POOL_GROUPS * u;
+                v[u] = t < d.T ? x[(int64_t)t * d.C] : 0.f;
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int t = t0 + POOL_GROUPS * u;
+                if (t < d.T) {
+                    s += v[u];
+                    if (v[u] > mx || idx == 0x7fffffff) { mx = v[u]; idx = t; }   // strict >
+                }
+            }
         }
     }
     s_sum[g][cl] = s;
@@ -326,8 +338,10 @@ MEP_DEV void head_reduce_block(const mep_head_desc& d, const HeadGrads& g, int b
     if ((int)bx < nA32) {
         const int i = bx * 32 + cl;
         float s = 0.f;
-        if (i < nA)
+        if (i < nA) {
+#pragma unroll 8
             for (int b = rg; b < B; b += 8) s += part[(int64_t)b * o.stride + i];
+        }
         red[rg][0][cl] = s;
         float ls = 0.f;
         if (bx == 0)
@@ -364,6 +378,7 @@ MEP_DEV void head_reduce_block(const mep_head_desc& d, const HeadGrads& g, int b
 #pragma unroll
     for (int n = 0; n < NCMAX; ++n) acc[n] = 0.f;
     if (k < F) {
+#pragma unroll 4
         for (int b = rg; b < B; b += 8) {
             const float pk = pooled[(int64_t)b * F + k];
             const gfloat* pr = part + (int64_t)b * o.stride + off;
