@@ -53,15 +53,27 @@ MEP_DEV float sub_rn(float a, float b) { return __fsub_rn(a, b); }
 MEP_DEV float mul_rn(float a, float b) { return __fmul_rn(a, b); }
 
 // ------------------------------------------------------------------ wave reductions (64 lanes)
+// DPP within each row of 16 lanes (quad butterflies xor 1 / xor 2, then the half-row and row
+// mirrors), then the four row results through readlane, combined as (r0 + r1) + (r2 + r3): no
+// LDS round trips (ds_bpermute), result wave-uniform, fixed order.
+template <int CTRL>
+MEP_DEV float dpp_mov(float v) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false));
+}
+MEP_DEV float lane_f(float v, int l) { return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), l)); }
 MEP_DEV float wave_sum(float v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    return v;
+    v += dpp_mov<0xB1>(v);
+    v += dpp_mov<0x4E>(v);
+    v += dpp_mov<0x141>(v);
+    v += dpp_mov<0x140>(v);
+    return (lane_f(v, 0) + lane_f(v, 16)) + (lane_f(v, 32) + lane_f(v, 48));
 }
 MEP_DEV float wave_max(float v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
-    return v;
+    v = fmaxf(v, dpp_mov<0xB1>(v));
+    v = fmaxf(v, dpp_mov<0x4E>(v));
+    v = fmaxf(v, dpp_mov<0x141>(v));
+    v = fmaxf(v, dpp_mov<0x140>(v));
+    return fmaxf(fmaxf(lane_f(v, 0), lane_f(v, 16)), fmaxf(lane_f(v, 32), lane_f(v, 48)));
 }
 
 // ------------------------------------------------------------------ counter-based dropout

@@ -97,6 +97,7 @@ __global__ __launch_bounds__(256) void k_pool_bwd(const mep_pool_desc* __restric
 
 // ---------------------------------------------------------------- fusion head
 constexpr int NCMAX = 16;
+constexpr int HEAD_KU = 3;   // classifier columns per thread per pass
 
 struct HeadOff {
     int wo, bo, lnw, lnb, trans, dl0, dl1, stride;
@@ -120,17 +121,40 @@ MEP_DEV float label_at(const mep_head_desc& d, int b, int n) {
 }
 
 // make LDS writes of this wave visible to its other lanes
+// (wavefront-scope fences: LDS ordering only, no wait on the wave's outstanding global stores)
 MEP_DEV void wave_sync() {
-    __threadfence_block();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
 MEP_DEV float log_sigmoid(float x) { return fminf(x, 0.f) - log1pf(__expf(-fabsf(x))); }
 
+
+#ifdef MEP_HEAD_TRACE   // development only: phase timestamps of block 0 / the last block (printf)
+#define HT(i) do { if (threadIdx.x == 0) ht_clk[i] = wall_clock64(); } while (0)
+#define HT_PRINT() do { if (threadIdx.x == 0 && (blockIdx.x == 0 || blockIdx.x == gridDim.x - 1)) \
+    printf("head blk %d: %lld %lld %lld %lld %lld %lld | %lld %lld %lld (x10ns)\n", (int)blockIdx.x, \
+           ht_clk[1] - ht_clk[0], ht_clk[2] - ht_clk[1], ht_clk[3] - ht_clk[2], ht_clk[4] - ht_clk[3], \
+           ht_clk[5] - ht_clk[4], ht_clk[6] - ht_clk[5], ht_clk[7] - ht_clk[3], ht_clk[8] - ht_clk[7], \
+           ht_clk[9] - ht_clk[8]); } while (0)
+#else
+#define HT(i) do { } while (0)
+#define HT_PRINT() do { } while (0)
+#endif
+// NCT: the class count as a compile-time constant (7 cmu-mosei, 9 Ren-MME; 0 = runtime, <= NCMAX):
+// exact unrolls, constant index arithmetic and a small code footprint (each workgroup runs the
+// kernel body once, so instruction fetch is on the critical path)
+template <int NCT>
 __global__ __launch_bounds__(256) void k_head(mep_head_desc d) {
+    constexpr int NU = NCT ? NCT : NCMAX;
+#ifdef MEP_HEAD_TRACE
+    long long ht_clk[12];
+#endif
+    HT(0);
     const int rows = d.rdrop ? 2 : 1;
     const int r0 = blockIdx.x * rows;
-    const int NC = d.NC, F = d.F;
+    const int NC = NCT ? NCT : d.NC, F = d.F;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     __shared__ float s_last[2][NCMAX], s_this[2][NCMAX], s_logit[2][NCMAX], s_dlog[2][NCMAX];
     __shared__ float s_temp[2][NCMAX * NCMAX];
@@ -142,34 +166,105 @@ __global__ __launch_bounds__(256) void k_head(mep_head_desc d) {
     // them in dependent chains, where a global (L2) latency per step would dominate
     __shared__ float trans[NCMAX * NCMAX * NCMAX], wo[NCMAX * 2 * NCMAX], lnw[NCMAX], lnb[NCMAX], bo[NCMAX];
     __shared__ float s_part[NCMAX * NCMAX];
+    // staged with every load in flight at once (registers first, LDS after the classifier loads
+    // are issued): trans <= 1024 and wo <= 512 elements in one pass, a plain loop beyond
+    const int ntr = NC * NC * NC, nwo = 2 * NC * NC;
+    const gfloat* g_trans = G<const float>(d.trans);
+    const gfloat* g_wo = G<const float>(d.wo);
+    float st_tr[4], st_wo[2], st_ln[3];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) st_tr[j] = g_trans[min((int)threadIdx.x + 256 * j, ntr - 1)];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) st_wo[j] = g_wo[min((int)threadIdx.x + 256 * j, nwo - 1)];
     {
-        const gfloat* g_trans = G<const float>(d.trans);
-        const gfloat* g_wo = G<const float>(d.wo);
-        for (int i = threadIdx.x; i < NC * NC * NC; i += 256) trans[i] = g_trans[i];
-        for (int i = threadIdx.x; i < 2 * NC * NC; i += 256) wo[i] = g_wo[i];
-        if (threadIdx.x < NC) {
-            lnw[threadIdx.x] = G<const float>(d.ln_w)[threadIdx.x];
-            lnb[threadIdx.x] = G<const float>(d.ln_b)[threadIdx.x];
-            bo[threadIdx.x] = G<const float>(d.bo)[threadIdx.x];
+        const int c = min((int)threadIdx.x, NC - 1);
+        st_ln[0] = G<const float>(d.ln_w)[c];
+        st_ln[1] = G<const float>(d.ln_b)[c];
+        st_ln[2] = G<const float>(d.bo)[c];
+    }
+    auto stage_params = [&]() {
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            if ((int)threadIdx.x + 256 * j < ntr) trans[threadIdx.x + 256 * j] = st_tr[j];
+        for (int i = threadIdx.x + 1024; i < ntr; i += 256) trans[i] = g_trans[i];
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+            if ((int)threadIdx.x + 256 * j < nwo) wo[threadIdx.x + 256 * j] = st_wo[j];
+        if ((int)threadIdx.x < NC) {
+            lnw[threadIdx.x] = st_ln[0];
+            lnb[threadIdx.x] = st_ln[1];
+            bo[threadIdx.x] = st_ln[2];
         }
+    };
+
+    // the labels of the loss phase, fetched now so their latency hides behind the classifiers
+    float lab[2] = {0.f, 0.f};
+    if (wave == 0 && lane < NC && !d.ext_dlogits) {
+        lab[0] = label_at(d, r0, lane);
+        if (rows > 1) lab[1] = label_at(d, r0 + 1, lane);
     }
 
-    // classifiers (Multi_ATTN.classifier, no bias): one wave per output, lanes over F
+    // classifiers (Multi_ATTN.classifier, no bias): every thread takes columns k = tid + 256 j
+    // of all 2 NC outputs (all loads of a column issued together), then one block reduction
+    __shared__ float s_red[2][4][2 * NCMAX];
     for (int rr = 0; rr < rows; ++rr) {
         const int b = r0 + rr;
         const gfloat* p0 = G<const float>(d.pooled0) + (int64_t)b * F;
         const gfloat* p1 = G<const float>(d.pooled1) + (int64_t)b * F;
-        for (int task = wave; task < 2 * NC; task += 4) {
-            const int e = task / NC, n = task - e * NC;
-            const gfloat* w = (e ? wc1 : wc0) + (int64_t)n * F;
-            const gfloat* p = e ? p1 : p0;
-            float s = 0.f;
-            for (int k = lane; k < F; k += 64) s = fmaf(w[k], p[k], s);
-            s = wave_sum(s);
-            if (lane == 0) { if (e) s_this[rr][n] = s; else s_last[rr][n] = s; }
+        float acc[2 * NCMAX];
+#pragma unroll
+        for (int n = 0; n < 2 * NCMAX; ++n) acc[n] = 0.f;   // [0, NU): last, [NCMAX, NCMAX + NU): this
+        // HEAD_KU columns per thread per pass (F <= 768 in one pass), every load of the pass
+        // issued before the first FMA: rows clamped to NC - 1, columns past F read column F - 1
+        // and are weighted by 0
+        for (int k0 = 0; k0 < F; k0 += 256 * HEAD_KU) {
+            float x0[HEAD_KU], x1[HEAD_KU], w0[HEAD_KU][NCMAX], w1[HEAD_KU][NCMAX];
+#pragma unroll
+            for (int u = 0; u < HEAD_KU; ++u) {
+                const int k = min(k0 + 256 * u + (int)threadIdx.x, F - 1);
+                x0[u] = p0[k];
+                x1[u] = p1[k];
+#pragma unroll
+                for (int n = 0; n < NU; ++n) {
+                    const int64_t o = (int64_t)min(n, NC - 1) * F + k;
+                    w0[u][n] = wc0[o];
+                    w1[u][n] = wc1[o];
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < HEAD_KU; ++u) {
+                const bool kin = k0 + 256 * u + (int)threadIdx.x < F;
+                const float a = kin ? x0[u] : 0.f, c = kin ? x1[u] : 0.f;
+#pragma unroll
+                for (int n = 0; n < NU; ++n) {
+                    acc[n] = fmaf(w0[u][n], a, acc[n]);
+                    acc[NCMAX + n] = fmaf(w1[u][n], c, acc[NCMAX + n]);
+                }
+            }
+        }
+#pragma unroll
+        for (int n = 0; n < NU; ++n) {
+            if (n < NC) {
+                const float s0 = wave_sum(acc[n]), s1 = wave_sum(acc[NCMAX + n]);
+                if (lane == 0) {
+                    s_red[rr][wave][n] = s0;
+                    s_red[rr][wave][NCMAX + n] = s1;
+                }
+            }
+        }
+    }
+    stage_params();
+    __syncthreads();
+    if (threadIdx.x < 2 * NCMAX * rows) {
+        const int rr = threadIdx.x / (2 * NCMAX), n = threadIdx.x % (2 * NCMAX);
+        const int nn = n & (NCMAX - 1);
+        if (nn < NC) {
+            const float s = (s_red[rr][0][n] + s_red[rr][1][n]) + (s_red[rr][2][n] + s_red[rr][3][n]);
+            if (n < NCMAX) s_last[rr][nn] = s; else s_this[rr][nn] = s;
         }
     }
     __syncthreads();
+    HT(1);
     if (wave == 0) {
         for (int rr = 0; rr < rows; ++rr) {
             // temp[p][n] = sum_m last[m] trans[p][m][n]   (matmul(last[i], trans), run.py:334)
@@ -202,6 +297,7 @@ __global__ __launch_bounds__(256) void k_head(mep_head_desc d) {
             }
             wave_sync();
         }
+        HT(2);
         // losses: circle per row, then R-Drop KL for the pair
         gfloat* row_loss = G<float>(d.row_loss);
         const gfloat* ext = G<const float>(d.ext_dlogits);
@@ -214,7 +310,7 @@ __global__ __launch_bounds__(256) void k_head(mep_head_desc d) {
             const int b = r0 + rr;
             const bool ok = lane < NC;
             const float x = ok ? s_logit[rr][lane] : 0.f;
-            const float t = ok ? label_at(d, b, lane) : 0.f;
+            const float t = ok ? (rr ? lab[1] : lab[0]) : 0.f;
             const bool is_pos = ok && t > 0.5f, is_neg = ok && !(t > 0.5f);
             const float vn = is_neg ? x : -INFINITY;   // y = (1-2t) p for t = 0
             const float vp = is_pos ? -x : -INFINITY;  // y = (1-2t) p for t = 1
@@ -246,6 +342,7 @@ __global__ __launch_bounds__(256) void k_head(mep_head_desc d) {
             }
             if (lane == 0) row_loss[r0] += kl;
         }
+        HT(3);
         if (d.compute_grad) {
             const HeadOff o = head_off(NC);
             for (int rr = 0; rr < rows; ++rr) {
@@ -265,6 +362,7 @@ __global__ __launch_bounds__(256) void k_head(mep_head_desc d) {
                     part[o.lnw + lane] = dyn * s_yhat[rr][lane];
                     part[o.lnb + lane] = dyn;
                 }
+                HT(7);
                 // LayerNorm(7) backward
                 const float yh = lane < NC ? s_yhat[rr][lane] : 0.f;
                 const float gsc = lane < NC ? dyn * lnw[lane] : 0.f;
@@ -274,6 +372,7 @@ __global__ __launch_bounds__(256) void k_head(mep_head_desc d) {
                 __shared__ float s_dy[NCMAX];
                 if (lane < NC) s_dy[lane] = dy;
                 wave_sync();
+                HT(8);
                 // dlast[m] = sum_p this[p] sum_n dy[n] trans[p][m][n]: lane (m, p) does the n sum
                 for (int idx = lane; idx < NC * NC; idx += 64) {
                     const int m = idx / NC, p = idx - m * NC;
@@ -282,6 +381,7 @@ __global__ __launch_bounds__(256) void k_head(mep_head_desc d) {
                     s_part[idx] = s_this[rr][p] * s;
                 }
                 wave_sync();
+                HT(9);
                 if (lane < NC) {
                     float dt = dcat_this;
                     for (int n = 0; n < NC; ++n) dt = fmaf(s_dy[n], s_temp[rr][lane * NC + n], dt);
@@ -301,22 +401,45 @@ __global__ __launch_bounds__(256) void k_head(mep_head_desc d) {
         }
     }
     if (!d.compute_grad) return;
+    HT(4);
     __syncthreads();
+    HT(5);
     // dpooled_e = Wc_e^T dlogit_e
     for (int rr = 0; rr < rows; ++rr) {
         const int b = r0 + rr;
         gfloat* dp0 = G<float>(d.dpooled0) + (int64_t)b * F;
         gfloat* dp1 = G<float>(d.dpooled1) + (int64_t)b * F;
-        for (int k = threadIdx.x; k < F; k += 256) {
-            float a0 = 0.f, a1 = 0.f;
-            for (int n = 0; n < NC; ++n) {
-                a0 = fmaf(wc0[(int64_t)n * F + k], s_dlast[rr][n], a0);
-                a1 = fmaf(wc1[(int64_t)n * F + k], s_dthis[rr][n], a1);
+        for (int k0 = 0; k0 < F; k0 += 256 * HEAD_KU) {
+            float w0[HEAD_KU][NCMAX], w1[HEAD_KU][NCMAX];
+#pragma unroll
+            for (int u = 0; u < HEAD_KU; ++u) {   // all loads of the pass in flight at once
+                const int k = min(k0 + 256 * u + (int)threadIdx.x, F - 1);
+#pragma unroll
+                for (int n = 0; n < NU; ++n) {
+                    const int64_t o = (int64_t)min(n, NC - 1) * F + k;
+                    w0[u][n] = wc0[o];
+                    w1[u][n] = wc1[o];
+                }
             }
-            dp0[k] = a0;
-            dp1[k] = a1;
+#pragma unroll
+            for (int u = 0; u < HEAD_KU; ++u) {
+                const int k = k0 + 256 * u + (int)threadIdx.x;
+                float a0 = 0.f, a1 = 0.f;
+#pragma unroll
+                for (int n = 0; n < NU; ++n) {
+                    if (n < NC) {
+                        a0 = fmaf(w0[u][n], s_dlast[rr][n], a0);
+                        a1 = fmaf(w1[u][n], s_dthis[rr][n], a1);
+                    }
+                }
+                if (k < F) {
+                    dp0[k] = a0;
+                    dp1[k] = a1;
+                }
+            }
         }
     }
+    HT(6); HT_PRINT();
 }
 
 struct HeadGrads {
@@ -486,7 +609,10 @@ extern "C" int mep_head_fwd_bwd(const mep_head_desc* d, mep_stream_t stream) {
         return MEP_EINVAL;
     }
     const int groups = d->rdrop ? d->B / 2 : d->B;
-    hipLaunchKernelGGL(k_head, dim3(groups), dim3(256), 0, (hipStream_t)stream, *d);
+    hipStream_t st = (hipStream_t)stream;
+    if (d->NC == 7) hipLaunchKernelGGL(k_head<7>, dim3(groups), dim3(256), 0, st, *d);
+    else if (d->NC == 9) hipLaunchKernelGGL(k_head<9>, dim3(groups), dim3(256), 0, st, *d);
+    else hipLaunchKernelGGL(k_head<0>, dim3(groups), dim3(256), 0, st, *d);
     return mep_check_launch("mep_head_fwd_bwd");
 }
 
