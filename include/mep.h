@@ -365,6 +365,37 @@ int mep_clip_adam(float* params, float* grads, float* exp_avg, float* exp_avg_sq
 /* advance the device-side dropout seed (graph-replay safe) */
 int mep_seed_advance(uint64_t* seed, mep_stream_t stream);
 
+/* ---------------------------------------------------------------- evaluation
+ * Ensemble combine + threshold sweep.  Replaces the test() loops of others/realformer.py:395-477
+ * (pred = pred_1 * 0.6 + pred_2 * 0.4; pred > threshold for t/200 - 1, t < 400; a full test-set
+ * forward per threshold) and cmu-mosei/run.py:456-498 (mean of 4 models, fixed per-class
+ * thresholds): the logits are computed once and every threshold is counted on the GPU.
+ *   score[n, c] = (((p_0[n,c] * w_0) + p_1[n,c] * w_1) + ...) / post_div   (fp32, each op rounded:
+ *   realformer w = {0.6, 0.4}, post_div 1; cmu-mosei w = 1, post_div = the model count)
+ *   pred = score > thr(t, c)  (fp32 compare, as torch compares an fp32 tensor with a scalar);
+ *   thr(t, c) = thresholds[t] or, with thr_per_class, thresholds[t * C + c] (run.py:478-483)
+ *   counts[t, c, :] += {tp, fp, fn, tn} over the rows n that count.
+ * A row counts when row_mask == 0, or when row_mask[i][0..j] are all 1 for n = i * P + j
+ * (the `if mask == 1 ... else: break` walk of realformer.py:423-437).  Labels are positive iff
+ * != 0.  counts is int32 and accumulated into (the caller zeroes it); exact integer atomics, so
+ * the result does not depend on the launch order.  Launch: ceil(N/256) x ceil(n_thr/64)
+ * workgroups of 256 threads; the rows of a workgroup are staged in LDS once. */
+#define MEP_EVAL_MAX_MODELS 8
+#define MEP_EVAL_MAX_CLASSES 16
+typedef struct {
+    uint64_t preds[MEP_EVAL_MAX_MODELS];   /* model m's scores, [N, C] fp32, row stride ld_pred */
+    float    weights[MEP_EVAL_MAX_MODELS];
+    uint64_t labels;       /* [N, C] int64, row stride ld_label                          */
+    uint64_t row_mask;     /* [N / P, P] int64 utterance mask, or 0 (every row counts)    */
+    uint64_t thresholds;   /* [n_thr] fp32, or [n_thr, C] with thr_per_class              */
+    uint64_t scores;       /* [N, C] fp32 out (combined scores, every row), or 0          */
+    uint64_t counts;       /* [n_thr, C, 4] int32, accumulated: tp, fp, fn, tn            */
+    int32_t  n_models, N, C, n_thr, P, ld_pred, ld_label;
+    float    post_div;
+    int32_t  thr_per_class, _pad;
+} mep_sweep_desc;
+int mep_threshold_sweep(const mep_sweep_desc* d, mep_stream_t stream);
+
 /* ---------------------------------------------------------------- misc */
 int mep_abi_version(void);
 int mep_last_error(char* buf, size_t len);

@@ -114,6 +114,16 @@ class RfHeadDesc(ctypes.Structure):
                 ('B', i32), ('P', i32), ('D', i32), ('compute_grad', i32), ('loss_scale', f32), ('_pad', i32)]
 
 
+EVAL_MAX_MODELS, EVAL_MAX_CLASSES = 8, 16   # MEP_EVAL_MAX_* (include/mep.h)
+
+
+class SweepDesc(ctypes.Structure):
+    _fields_ = [('preds', u64 * EVAL_MAX_MODELS), ('weights', f32 * EVAL_MAX_MODELS), ('labels', u64),
+                ('row_mask', u64), ('thresholds', u64), ('scores', u64), ('counts', u64),
+                ('n_models', i32), ('N', i32), ('C', i32), ('n_thr', i32), ('P', i32), ('ld_pred', i32),
+                ('ld_label', i32), ('post_div', f32), ('thr_per_class', i32), ('_pad', i32)]
+
+
 class Seg(ctypes.Structure):
     _fields_ = [('offset', i64), ('length', i64)]
 
@@ -122,7 +132,8 @@ STRUCTS = {'mep_rows': Rows, 'mep_gemm_desc': GemmDesc, 'mep_wgrad_desc': WgradD
            'mep_attn_desc': AttnDesc, 'mep_attn_bwd_desc': AttnBwdDesc, 'mep_epi_desc': EpiDesc,
            'mep_epi_bwd_desc': EpiBwdDesc, 'mep_ln_desc': LnDesc, 'mep_colsum_desc': ColsumDesc,
            'mep_sum_desc': SumDesc, 'mep_pool_desc': PoolDesc, 'mep_head_desc': HeadDesc, 'mep_seg': Seg,
-           'mep_rf_epi_desc': RfEpiDesc, 'mep_rf_epi_bwd_desc': RfEpiBwdDesc, 'mep_rf_head_desc': RfHeadDesc}
+           'mep_rf_epi_desc': RfEpiDesc, 'mep_rf_epi_bwd_desc': RfEpiBwdDesc, 'mep_rf_head_desc': RfHeadDesc,
+           'mep_sweep_desc': SweepDesc}
 
 P = ctypes.c_void_p
 # name -> argtypes (all return int)
@@ -145,6 +156,7 @@ SIGNATURES.update({
     'mep_clip_adam': [P, P, P, P, P, i32, i64, P, P, P, P, i32, P],
     'mep_seed_advance': [P, P],
     'mep_rf_head': [ctypes.POINTER(RfHeadDesc), P],
+    'mep_threshold_sweep': [ctypes.POINTER(SweepDesc), P],
     'mep_abi_version': [],
     'mep_last_error': [ctypes.c_char_p, ctypes.c_size_t],
     'mep_device_sync': [],
