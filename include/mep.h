@@ -396,6 +396,31 @@ typedef struct {
 } mep_sweep_desc;
 int mep_threshold_sweep(const mep_sweep_desc* d, mep_stream_t stream);
 
+/* ---------------------------------------------------------------- batch assembly
+ * Windowed, masked feature slots gathered from packed, HBM-resident sequences.  Replaces the
+ * host numpy of masking() + data_loader() in cmu-mosei/run.py:104-198 and
+ * others/realformer.py:72-82,94-125, and the torch.cuda.FloatTensor(list) copy of the batch
+ * (cmu-mosei/run.py:362, realformer.py:307-309).  For output slot i of a descriptor:
+ *   seq = sel[i] (-1: an empty 'no_name' slot -> zero features, zero mask)
+ *   summary = 1 (cmu): rows 0..2 = max, min, mean over all L frames of seq (in the source dtype,
+ *     the mean as sum-in-frame-order / L), rows 3.. = frames start, start+1, ... (zero past L);
+ *     mask[t] = 1 for t < 3 + (L - start)
+ *   summary = 0 (realformer): rows 0.. = frames start, ...; mask[t] = 1 for t < L - start
+ *   clean = 1: inf / nan source values read as -71 (cmu audio, every realformer modality)
+ * The host picks each slot's window start (first window 0, last window L - (m_len - 3), realformer
+ * max(0, L - m_len)).  Launch: n_out x n_desc workgroups of 256 threads. */
+#define MEP_WINDOW_MAX_DESC 4
+typedef struct {
+    uint64_t src;      /* packed frames [n_frames, d], fp32 (src_f64 = 0) or fp64 (src_f64 = 1) */
+    uint64_t segs;     /* mep_seg [n_seq]: first frame and frame count of each sequence          */
+    uint64_t sel;      /* int32 [n_out]: sequence of each output slot, -1 = empty slot           */
+    uint64_t start;    /* int32 [n_out]: first frame of the slot's window                        */
+    uint64_t out;      /* fp32 [n_out, m_len, d]                                                 */
+    uint64_t mask;     /* fp32 [n_out, m_len]                                                    */
+    int32_t  n_out, m_len, d, src_f64, summary, clean, n_seq, _pad;
+} mep_window_desc;
+int mep_assemble_windows(const mep_window_desc* descs, int n_desc, mep_stream_t stream);
+
 /* ---------------------------------------------------------------- misc */
 int mep_abi_version(void);
 int mep_last_error(char* buf, size_t len);

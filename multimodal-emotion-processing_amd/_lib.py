@@ -124,6 +124,15 @@ class SweepDesc(ctypes.Structure):
                 ('ld_label', i32), ('post_div', f32), ('thr_per_class', i32), ('_pad', i32)]
 
 
+WINDOW_MAX_DESC = 4   # MEP_WINDOW_MAX_DESC
+
+
+class WindowDesc(ctypes.Structure):
+    _fields_ = [('src', u64), ('segs', u64), ('sel', u64), ('start', u64), ('out', u64), ('mask', u64),
+                ('n_out', i32), ('m_len', i32), ('d', i32), ('src_f64', i32), ('summary', i32), ('clean', i32),
+                ('n_seq', i32), ('_pad', i32)]
+
+
 class Seg(ctypes.Structure):
     _fields_ = [('offset', i64), ('length', i64)]
 
@@ -133,7 +142,7 @@ STRUCTS = {'mep_rows': Rows, 'mep_gemm_desc': GemmDesc, 'mep_wgrad_desc': WgradD
            'mep_epi_bwd_desc': EpiBwdDesc, 'mep_ln_desc': LnDesc, 'mep_colsum_desc': ColsumDesc,
            'mep_sum_desc': SumDesc, 'mep_pool_desc': PoolDesc, 'mep_head_desc': HeadDesc, 'mep_seg': Seg,
            'mep_rf_epi_desc': RfEpiDesc, 'mep_rf_epi_bwd_desc': RfEpiBwdDesc, 'mep_rf_head_desc': RfHeadDesc,
-           'mep_sweep_desc': SweepDesc}
+           'mep_sweep_desc': SweepDesc, 'mep_window_desc': WindowDesc}
 
 P = ctypes.c_void_p
 # name -> argtypes (all return int)
@@ -157,6 +166,7 @@ SIGNATURES.update({
     'mep_seed_advance': [P, P],
     'mep_rf_head': [ctypes.POINTER(RfHeadDesc), P],
     'mep_threshold_sweep': [ctypes.POINTER(SweepDesc), P],
+    'mep_assemble_windows': [ctypes.POINTER(WindowDesc), i32, P],
     'mep_abi_version': [],
     'mep_last_error': [ctypes.c_char_p, ctypes.c_size_t],
     'mep_device_sync': [],

@@ -1,0 +1,153 @@
+"""Device-side batch assembly.
+
+The reference builds every batch on the host: per utterance it windows and masks each modality
+with numpy (``masking``), stacks the slots into Python lists and copies them with
+``torch.cuda.FloatTensor(list)`` (cmu-mosei/run.py:104-198,362; others/realformer.py:72-125,
+307-309).  Here the raw sequences are packed once into one HBM-resident buffer per modality
+(``FeatureStore``), and a batch is one ``mep_assemble_windows`` launch that gathers, windows,
+summarises (max / min / mean rows), cleans (inf / nan -> -71) and masks every slot of every
+modality on the device.  Only the per-batch slot table (sequence ids and window starts, a few
+hundred int32) crosses PCIe.
+
+Row order and windows follow the reference's data loaders exactly (tests/test_batching.py pins
+them against the reference's own output, tests/golden/batch_golden.npz):
+  * cmu_batch:  per (previous, current) pair, a row of last windows when the current text has two
+    windows (L >= L_LEN - 3), then a row of first windows; a 'no_name' previous slot is zeros.
+  * rf_batch:   per list of P_LEN names, the last m_len frames of each ('no_name' -> zeros, mask 0).
+"""
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _lib
+
+MODALITIES = ('linguistic', 'visual', 'acoustic')
+NO_NAME = 'no_name'
+
+
+class FeatureStore:
+    """Packed, device-resident sequences: per modality one [n_frames, d] buffer (fp32, or fp64
+    when the source arrays are fp64 -- the statistics are computed in the source dtype, as numpy
+    does) plus an (offset, length) segment table; names map to sequence ids."""
+
+    def __init__(self, data, device='cuda'):
+        """data: {modality: {name: [L, d] array}} (the mmsdk ``computational_sequences[m].data[name]
+        ["features"]`` arrays)."""
+        self.device = torch.device(device)
+        if self.device.type != 'cuda':
+            raise RuntimeError('FeatureStore: device-side batch assembly needs a CUDA device')
+        self.mods = {}
+        for mod, seqs in data.items():
+            names = list(seqs)
+            arrs = [np.asarray(seqs[n]) for n in names]
+            if not arrs:
+                continue
+            d = arrs[0].shape[1]
+            f64 = any(a.dtype == np.float64 for a in arrs)
+            dt = np.float64 if f64 else np.float32
+            for n, a in zip(names, arrs):
+                if a.ndim != 2 or a.shape[1] != d or a.shape[0] < 1:
+                    raise ValueError('FeatureStore: %s/%s must be [L >= 1, %d]' % (mod, n, d))
+            lens = np.array([a.shape[0] for a in arrs], np.int64)
+            offs = np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.int64)
+            packed = torch.from_numpy(np.concatenate([a.astype(dt, copy=False) for a in arrs], axis=0))
+            segs = torch.from_numpy(np.stack([offs, lens], axis=1).reshape(-1))
+            self.mods[mod] = dict(src=packed.to(self.device), segs=segs.to(self.device), d=d, f64=f64,
+                                  ids={n: i for i, n in enumerate(names)}, lens=lens)
+
+    def length(self, mod, name):
+        m = self.mods[mod]
+        return int(m['lens'][m['ids'][name]])
+
+    def dim(self, mod):
+        return self.mods[mod]['d']
+
+    def assemble(self, slots, stream=None):
+        """slots: list of (modality, names, starts, m_len, summary, clean) with names a list of
+        sequence names (NO_NAME for empty slots) -> list of (feat [n, m_len, d], mask [n, m_len])."""
+        if len(slots) > _lib.WINDOW_MAX_DESC:
+            raise ValueError('assemble: at most %d slot groups per launch' % _lib.WINDOW_MAX_DESC)
+        descs = (_lib.WindowDesc * len(slots))()
+        outs, keep = [], []
+        for k, (mod, names, starts, m_len, summary, clean) in enumerate(slots):
+            m = self.mods[mod]
+            sel = np.array([-1 if n == NO_NAME else m['ids'][n] for n in names], np.int32)
+            st = np.asarray(starts, np.int32)
+            if st.shape != sel.shape:
+                raise ValueError('assemble: one window start per slot')
+            tab = torch.from_numpy(np.concatenate([sel, st])).pin_memory().to(self.device, non_blocking=True)
+            n = len(names)
+            feat = torch.empty(n, m_len, m['d'], dtype=torch.float32, device=self.device)
+            mask = torch.empty(n, m_len, dtype=torch.float32, device=self.device)
+            D = descs[k]
+            D.src, D.segs = m['src'].data_ptr(), m['segs'].data_ptr()
+            D.sel, D.start = tab.data_ptr(), tab.data_ptr() + 4 * n
+            D.out, D.mask = feat.data_ptr(), mask.data_ptr()
+            D.n_out, D.m_len, D.d, D.src_f64 = n, m_len, m['d'], int(m['f64'])
+            D.summary, D.clean, D.n_seq = int(summary), int(clean), len(m['ids'])
+            outs.append((feat, mask))
+            keep.append(tab)
+        _lib.call('mep_assemble_windows', descs, len(slots), stream=stream)
+        self._keep = keep       # the slot tables live until the next launch on this store
+        return outs
+
+
+def cmu_windows(L, m_len):
+    """(first, last) window starts of cmu masking() (run.py:127-140): two windows when
+    L >= m_len - 3, else one (both 0)."""
+    return (0, L - (m_len - 3)) if L >= m_len - 3 else (0, 0)
+
+
+def cmu_batch(store, pairs, label_dict, lens, device=None):
+    """data_loader of cmu-mosei/run.py:154-198 for one batch of (previous, current) name pairs ->
+    (l, v, a, l_mask, v_mask, a_mask, label) device tensors: l [R, 2, L_LEN, d_l], masks [R, 2, *],
+    label [R, 7] int64, with R >= len(pairs) rows in the reference's order."""
+    lens = dict(zip(MODALITIES, lens))
+    names = {m: [] for m in MODALITIES}
+    starts = {m: [] for m in MODALITIES}
+    labels = []
+    for prev, cur in pairs:
+        two = store.length('linguistic', cur) >= lens['linguistic'] - 3
+        for k in ([1, 0] if two else [0]):           # rows: last windows (if any), then first windows
+            for m in MODALITIES:
+                for name in (prev, cur):
+                    if name == NO_NAME:
+                        names[m].append(NO_NAME)
+                        starts[m].append(0)
+                    else:
+                        names[m].append(name)
+                        starts[m].append(cmu_windows(store.length(m, name), lens[m])[k])
+            labels.append(np.asarray(label_dict[cur], np.int64))
+    outs = store.assemble([(m, names[m], starts[m], lens[m], True, m == 'acoustic') for m in MODALITIES])
+    R = len(labels)
+    feats = [f.view(R, 2, lens[m], f.shape[-1]) for (f, _), m in zip(outs, MODALITIES)]
+    masks = [k.view(R, 2, lens[m]) for (_, k), m in zip(outs, MODALITIES)]
+    lab = torch.from_numpy(np.stack(labels)).pin_memory().to(store.device, non_blocking=True)
+    return feats + masks + [lab]
+
+
+def rf_label(l):
+    """label_processing of realformer.py:84-92 (drop entry 0, binarise the next six), as int64."""
+    lab = np.array(l[1:], dtype=np.float64)
+    lab[:6] = (lab[:6] > 0)
+    return lab.astype(np.int64)
+
+
+def rf_batch(store, name_lists, labels, lens):
+    """data_loader of realformer.py:94-125 for one batch of P_LEN-name lists -> (l, v, a, label,
+    l_mask, v_mask, a_mask, mask) device tensors (l [B, P, L_LEN, d_l], label [B, P, 6], mask [B, P])."""
+    lens = dict(zip(MODALITIES, lens))
+    P = len(name_lists[0])
+    flat = [n for names in name_lists for n in names]
+    starts = {m: [0 if n == NO_NAME else max(0, store.length(m, n) - lens[m]) for n in flat] for m in MODALITIES}
+    outs = store.assemble([(m, flat, starts[m], lens[m], False, True) for m in MODALITIES])
+    B = len(name_lists)
+    feats = [f.view(B, P, lens[m], f.shape[-1]) for (f, _), m in zip(outs, MODALITIES)]
+    masks = [k.view(B, P, lens[m]) for (_, k), m in zip(outs, MODALITIES)]
+    lab = np.stack([np.zeros(6, np.int64) if n == NO_NAME else rf_label(labels[n]) for n in flat]).reshape(B, P, 6)
+    um = np.array([0 if n == NO_NAME else 1 for n in flat], np.int64).reshape(B, P)
+    dev = store.device
+    lab_t = torch.from_numpy(lab).pin_memory().to(dev, non_blocking=True)
+    um_t = torch.from_numpy(um).pin_memory().to(dev, non_blocking=True)
+    return feats + [lab_t] + masks + [um_t]
