@@ -81,14 +81,15 @@ __global__ __launch_bounds__(SW_THREADS) void k_sweep(mep_sweep_desc d) {
 
 extern "C" int mep_threshold_sweep(const mep_sweep_desc* d, mep_stream_t stream) {
     if (!d || d->n_models < 1 || d->n_models > MEP_EVAL_MAX_MODELS || d->C < 1 || d->C > MEP_EVAL_MAX_CLASSES ||
-        d->N < 0 || d->n_thr < 0 || d->ld_pred < d->C || d->ld_label < d->C || !d->labels || !d->counts ||
-        (d->n_thr > 0 && !d->thresholds) || (d->row_mask && (d->P < 1 || d->N % d->P))) {
+        d->N < 0 || d->n_thr < 0 || d->ld_pred < d->C || d->ld_label < d->C ||
+        (d->N > 0 && d->n_thr > 0 && (!d->labels || !d->counts || !d->thresholds)) ||
+        (d->row_mask && (d->P < 1 || d->N % d->P))) {
         mep_set_error("mep_threshold_sweep: invalid descriptor");
         return MEP_EINVAL;
     }
+    if (d->N == 0 || d->n_thr == 0) return 0;   // empty inputs carry null data pointers
     for (int m = 0; m < d->n_models; ++m)
         if (!d->preds[m]) { mep_set_error("mep_threshold_sweep: null model scores"); return MEP_EINVAL; }
-    if (d->N == 0 || d->n_thr == 0) return 0;
     const dim3 grid((d->N + SW_ROWS - 1) / SW_ROWS, (d->n_thr + SW_THR - 1) / SW_THR);
     hipLaunchKernelGGL(k_sweep, grid, dim3(SW_THREADS), 0, (hipStream_t)stream, *d);
     return mep_check_launch("mep_threshold_sweep");
