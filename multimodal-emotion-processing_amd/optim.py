@@ -83,6 +83,66 @@ class FusedAdamW(torch.optim.Optimizer):
         for p in self.model.parameters():
             p.grad = None
 
+    # ------------------------------------------------------------------ checkpoint / resume
+    # SURVEY 8(f) row 3.  The reference saves only the model (cmu-mosei/run.py:415); optimizer
+    # state is kept here in torch.optim.AdamW / Adam's own state_dict layout (state keyed by the
+    # index in model.parameters(), 'step' / 'exp_avg' / 'exp_avg_sq' shaped like each parameter;
+    # parameters that never get a gradient carry no state), so a checkpoint round-trips through
+    # torch.save and loads into either optimizer.
+    def _torch_cls(self):
+        return torch.optim.AdamW if self.decoupled else torch.optim.Adam
+
+    def state_dict(self):
+        g = self.param_groups[0]
+        ref = self._torch_cls()([torch.zeros(1)], lr=g['lr'], betas=g['betas'], eps=g['eps'],
+                                weight_decay=g['weight_decay'])
+        group = dict(ref.param_groups[0])
+        names = [n for n, _ in self.model.named_parameters()]
+        group['params'] = list(range(len(names)))
+        state = {}
+        if self._dev is not None:
+            flat = self._flat
+            steps = int(self.step_t.item())
+            if steps > 0:
+                for i, n in enumerate(names):
+                    if flat.has_grad[n]:
+                        state[i] = {'step': torch.tensor(float(steps)),
+                                    'exp_avg': flat.view(self.exp_avg, n).detach().cpu().clone(),
+                                    'exp_avg_sq': flat.view(self.exp_avg_sq, n).detach().cpu().clone()}
+        return {'state': state, 'param_groups': [group]}
+
+    @torch.no_grad()
+    def load_state_dict(self, state_dict):
+        groups = state_dict['param_groups']
+        if len(groups) != 1:
+            raise ValueError('FusedAdamW.load_state_dict: expected one parameter group, got %d' % len(groups))
+        names = [n for n, _ in self.model.named_parameters()]
+        if len(groups[0]['params']) != len(names):
+            raise ValueError('FusedAdamW.load_state_dict: %d parameters in the checkpoint, %d in the model'
+                             % (len(groups[0]['params']), len(names)))
+        for k in ('lr', 'betas', 'eps', 'weight_decay'):
+            if k in groups[0]:
+                self.param_groups[0][k] = groups[0][k]
+        flat = self._bind()
+        state = state_dict['state']
+        idx = {p: i for i, p in enumerate(groups[0]['params'])}
+        steps = set()
+        self.exp_avg.zero_()
+        self.exp_avg_sq.zero_()
+        for i, n in enumerate(names):
+            s = state.get(groups[0]['params'][i], state.get(i)) if idx else None
+            if s is None:
+                continue
+            if not flat.has_grad[n]:
+                raise ValueError('FusedAdamW.load_state_dict: state for %s, which never gets a gradient' % n)
+            flat.view(self.exp_avg, n).copy_(s['exp_avg'])
+            flat.view(self.exp_avg_sq, n).copy_(s['exp_avg_sq'])
+            steps.add(int(float(s['step'])))
+        if len(steps) > 1:
+            raise ValueError('FusedAdamW.load_state_dict: parameters at different step counts %s' % sorted(steps))
+        self.step_t.fill_(steps.pop() if steps else 0)
+        self._host_hyper = None
+
 
 class FusedAdam(FusedAdamW):
     """Adam (L2 weight decay folded into the gradient; default 0) as used by realformer."""
