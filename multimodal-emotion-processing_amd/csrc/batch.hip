@@ -46,30 +46,72 @@ MEP_DEV void copy_frames(const mep_window_desc& D, int64_t off, int start, int a
     const int64_t n_src = (int64_t)min(avail, rows) * d;
     const MEP_G T* src = G<const T>(D.src) + (off + start) * (int64_t)d;
     MEP_G float* dst = out + (int64_t)P0 * d;
-    for (int64_t i = threadIdx.x; i < n; i += BA_THREADS)
-        dst[i] = i < n_src ? (float)clean_val<T>(src[i], D.clean) : 0.f;
+    // 4 elements per lane per pass, every load issued before the first store (dst may alias
+    // nothing, but the compiler cannot know that)
+    constexpr int U = 4;
+    for (int64_t i0 = threadIdx.x; i0 < n; i0 += U * BA_THREADS) {
+        T v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t i = i0 + u * BA_THREADS;
+            v[u] = i < n_src ? src[i] : (T)0;
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t i = i0 + u * BA_THREADS;
+            if (i < n) dst[i] = i < n_src ? (float)clean_val<T>(v[u], D.clean) : 0.f;
+        }
+    }
 }
 
 template <typename T>
 MEP_DEV void summary_rows(const mep_window_desc& D, int64_t off, int L, MEP_G float* out, unsigned char* lds) {
+    // Chunks of ch frames fill the LDS buffer; the next chunk is loaded into registers (E values
+    // per lane, coalesced) while the current one is walked, so the frame-order sums wait on LDS
+    // only, not on HBM latency.
+    constexpr int E = BA_LDS_BYTES / (int)sizeof(T) / BA_THREADS;
     T* buf = reinterpret_cast<T*>(lds);
     const int d = D.d;
-    const int ch = max(1, min(64, BA_LDS_BYTES / (int)(d * sizeof(T))));
+    const int ch = max(1, BA_LDS_BYTES / (int)(d * sizeof(T)));
     T mx[BA_MAX_COLS_PER_LANE], mn[BA_MAX_COLS_PER_LANE], sm[BA_MAX_COLS_PER_LANE];
 #pragma unroll
     for (int k = 0; k < BA_MAX_COLS_PER_LANE; ++k) { mx[k] = -(T)INFINITY; mn[k] = (T)INFINITY; sm[k] = -(T)0; }   // -0 + x == x, signed zeros included
     const MEP_G T* src = G<const T>(D.src) + off * (int64_t)d;
+    T pre[E];
+    {
+        const int n = min(ch, L) * d;
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+            const int i = threadIdx.x + e * BA_THREADS;
+            pre[e] = i < n ? src[i] : (T)0;
+        }
+    }
     for (int f0 = 0; f0 < L; f0 += ch) {
         const int nf = min(ch, L - f0);
         const int n = nf * d;
+        __syncthreads();   // the previous chunk has been walked
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+            const int i = threadIdx.x + e * BA_THREADS;
+            if (i < n) buf[i] = clean_val<T>(pre[e], D.clean);
+        }
         __syncthreads();
-        for (int i = threadIdx.x; i < n; i += BA_THREADS) buf[i] = clean_val<T>(src[(int64_t)f0 * d + i], D.clean);
-        __syncthreads();
+        const int f1 = f0 + ch;
+        if (f1 < L) {
+            const int n1 = min(ch, L - f1) * d;
+            const MEP_G T* s1 = src + (int64_t)f1 * d;
+#pragma unroll
+            for (int e = 0; e < E; ++e) {
+                const int i = threadIdx.x + e * BA_THREADS;
+                pre[e] = i < n1 ? s1[i] : (T)0;
+            }
+        }
 #pragma unroll
         for (int k = 0; k < BA_MAX_COLS_PER_LANE; ++k) {
             const int c = threadIdx.x + k * BA_THREADS;
             if (c < d) {
                 T a = mx[k], b = mn[k], s = sm[k];
+#pragma unroll 8
                 for (int f = 0; f < nf; ++f) {
                     const T v = buf[f * d + c];
                     // numpy maximum / minimum: a NaN operand wins, and stays
