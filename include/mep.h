@@ -392,7 +392,12 @@ typedef struct {
     uint64_t counts;       /* [n_thr, C, 4] int32, accumulated: tp, fp, fn, tn            */
     int32_t  n_models, N, C, n_thr, P, ld_pred, ld_label;
     float    post_div;
-    int32_t  thr_per_class, _pad;
+    int32_t  thr_per_class;
+    int32_t  sorted;       /* 1: thr(t, c) is non-decreasing in t for every c (caller's promise):
+                              histogram + suffix-sum path, O(N C log n_thr); needs hist and
+                              C * (3 n_thr + 2) * 4 <= 65536                                 */
+    uint64_t hist;         /* sorted mode: int32 workspace [C, 2, n_thr + 1], zeroed by the caller
+                              once; every call leaves it zeroed                                */
 } mep_sweep_desc;
 int mep_threshold_sweep(const mep_sweep_desc* d, mep_stream_t stream);
 

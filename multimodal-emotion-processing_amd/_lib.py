@@ -121,7 +121,7 @@ class SweepDesc(ctypes.Structure):
     _fields_ = [('preds', u64 * EVAL_MAX_MODELS), ('weights', f32 * EVAL_MAX_MODELS), ('labels', u64),
                 ('row_mask', u64), ('thresholds', u64), ('scores', u64), ('counts', u64),
                 ('n_models', i32), ('N', i32), ('C', i32), ('n_thr', i32), ('P', i32), ('ld_pred', i32),
-                ('ld_label', i32), ('post_div', f32), ('thr_per_class', i32), ('_pad', i32)]
+                ('ld_label', i32), ('post_div', f32), ('thr_per_class', i32), ('sorted', i32), ('hist', u64)]
 
 
 WINDOW_MAX_DESC = 4   # MEP_WINDOW_MAX_DESC

@@ -29,15 +29,28 @@ CMU_CLASSES = (('happ', 0, 0.1), ('sadn', 1, -0.3), ('ange', 2, -0.5), ('surp', 
                ('disg', 3, -0.3), ('fear', 5, -0.5))        # cmu-mosei/run.py:478-495
 
 
+_HIST = {}   # (device, C, n_thr) -> zeroed int32 workspace of the sorted-threshold path
+
+
+def _hist_workspace(dev, C, n_thr):
+    key = (str(dev), C, n_thr)
+    w = _HIST.get(key)
+    if w is None:
+        w = _HIST[key] = torch.zeros(C, 2, n_thr + 1, dtype=torch.int32, device=dev)
+    return w
+
+
 def threshold_sweep(preds, labels, thresholds, weights=None, post_div=1.0, row_mask=None,
-                    counts=None, scores=None, stream=None):
+                    counts=None, scores=None, stream=None, sorted_path=None):
     """Accumulate {tp, fp, fn, tn} for every (threshold, class) into ``counts`` [n_thr, C, 4] int32.
 
     preds: list of [..., C] fp32 CUDA tensors (one per model, same shape; rows may be strided);
     labels: [..., C] int64 (positive iff != 0); thresholds: [n_thr] or [n_thr, C] fp32 (per-class);
     score = (sum_m preds[m] * weights[m]) / post_div (fp32, each op rounded, in model order);
     row_mask: optional [B, P] int64 utterance mask for preds of shape [B, P, C] (a row counts while
-    its mask prefix is all 1, realformer.py:423-437).  Returns counts (allocated zeroed if None)."""
+    its mask prefix is all 1, realformer.py:423-437).  Returns counts (allocated zeroed if None).
+    sorted_path: None = use the histogram formulation whenever every class's thresholds are
+    non-decreasing (realformer's t/200 - 1 are) and fit its LDS budget; False = direct compares."""
     if not preds or len(preds) > _lib.EVAL_MAX_MODELS:
         raise ValueError('threshold_sweep: 1..%d models' % _lib.EVAL_MAX_MODELS)
     weights = [1.0] * len(preds) if weights is None else list(weights)
@@ -92,6 +105,13 @@ def threshold_sweep(preds, labels, thresholds, weights=None, post_div=1.0, row_m
     d.counts = counts.data_ptr()
     d.n_models, d.N, d.C, d.n_thr, d.P = len(p2), N, C, n_thr, P
     d.ld_pred, d.ld_label, d.post_div, d.thr_per_class = ld_pred, C, float(post_div), int(per_class)
+    fits = C * (3 * n_thr + 2) * 4 <= 65536
+    if sorted_path is None:
+        sorted_path = fits and n_thr > 1 and bool((thr[1:] >= thr[:-1]).all())
+    elif sorted_path and not (fits and bool((thr[1:] >= thr[:-1]).all())):
+        raise ValueError('threshold_sweep: sorted_path needs non-decreasing thresholds within the LDS budget')
+    if sorted_path:
+        d.sorted, d.hist = 1, _hist_workspace(dev, C, n_thr).data_ptr()
     _lib.call('mep_threshold_sweep', ctypes.byref(d), stream=stream)
     return counts
 

@@ -137,6 +137,49 @@ def test_sweep_counts_gpu(cuda, case):
     np.testing.assert_array_equal(scores.cpu().numpy(), want_s)   # bit-exact fp32 combine
 
 
+SORTED_CASES = [
+    # (N, C, n_thr, n_models, P, per_class)
+    (24576, 6, 400, 2, 6, False),     # realformer shape
+    (3000, 7, 1, 4, 0, True),         # cmu: per-class fixed thresholds
+    (513, 16, 300, 3, 0, True),
+    (5000, 1, 2000, 1, 0, False),     # many thresholds: several bins per lane in the suffix pass
+]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('case', SORTED_CASES)
+def test_sweep_sorted_path_gpu(cuda, case):
+    """Histogram + suffix-sum formulation (sorted thresholds, ties, NaN scores, scores equal to a
+    threshold) against the oracle and against the direct-compare kernel."""
+    N, C, n_thr, M, P, per_class = case
+    rng = np.random.default_rng(N + C + n_thr)
+    preds_np = [np.round(rng.standard_normal((N, C)), 2).astype(np.float32) for _ in range(M)]
+    preds_np[0][::97, 0] = np.nan
+    labels = (rng.random((N, C)) < 0.3).astype(np.int64)
+    base = np.sort(np.round(rng.uniform(-2, 2, (n_thr, C) if per_class else n_thr), 2).astype(np.float32), axis=0)
+    if n_thr > 3:
+        base[1] = base[2]                                        # a tie
+    mask = None
+    if P:
+        lens = rng.integers(0, P + 1, N // P)
+        mask = (np.arange(P)[None, :] < lens[:, None]).astype(np.int64)
+    want, want_s = oev.sweep_counts(preds_np, [1.0] * M, labels, base, post_div=float(M), row_mask=mask,
+                                    per_class=per_class)
+    preds = [torch.from_numpy(p).to(cuda) for p in preds_np]
+    lab = torch.from_numpy(labels).to(cuda)
+    thr = torch.from_numpy(base).to(cuda)
+    mk = None if mask is None else torch.from_numpy(mask).to(cuda)
+    scores = torch.empty(N, C, device=cuda)
+    got = evaluate.threshold_sweep(preds, lab, thr, post_div=float(M), row_mask=mk, scores=scores, sorted_path=True)
+    direct = evaluate.threshold_sweep(preds, lab, thr, post_div=float(M), row_mask=mk, sorted_path=False)
+    again = evaluate.threshold_sweep(preds, lab, thr, post_div=float(M), row_mask=mk, sorted_path=True)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(got.cpu().numpy().astype(np.int64), want)
+    np.testing.assert_array_equal(direct.cpu().numpy(), got.cpu().numpy())
+    np.testing.assert_array_equal(again.cpu().numpy(), got.cpu().numpy())   # workspace left zeroed
+    np.testing.assert_array_equal(scores.cpu().numpy(), want_s)
+
+
 @pytest.mark.gpu
 def test_sweep_accumulates_across_calls(cuda):
     rng = np.random.default_rng(11)
