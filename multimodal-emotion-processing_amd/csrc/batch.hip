@@ -22,7 +22,7 @@ using namespace mep;
 namespace {
 
 constexpr int BA_THREADS = 256;
-constexpr int BA_LDS_BYTES = 32768;
+constexpr int BA_LDS_BYTES = 65536;   // 2 workgroups per CU; larger chunks = fewer exposed HBM round trips
 constexpr int BA_MAX_COLS_PER_LANE = 4;   // summary mode: d <= 1024
 
 struct WindowArgs {
@@ -46,9 +46,9 @@ MEP_DEV void copy_frames(const mep_window_desc& D, int64_t off, int start, int a
     const int64_t n_src = (int64_t)min(avail, rows) * d;
     const MEP_G T* src = G<const T>(D.src) + (off + start) * (int64_t)d;
     MEP_G float* dst = out + (int64_t)P0 * d;
-    // 4 elements per lane per pass, every load issued before the first store (dst may alias
+    // 16 elements per lane per pass, every load issued before the first store (dst may alias
     // nothing, but the compiler cannot know that)
-    constexpr int U = 4;
+    constexpr int U = 16;   // a 47 x 300 text window is 55 elements per lane: 4 round trips, not 14
     for (int64_t i0 = threadIdx.x; i0 < n; i0 += U * BA_THREADS) {
         T v[U];
 #pragma unroll
@@ -73,6 +73,7 @@ MEP_DEV void summary_rows(const mep_window_desc& D, int64_t off, int L, MEP_G fl
     T* buf = reinterpret_cast<T*>(lds);
     const int d = D.d;
     const int ch = max(1, BA_LDS_BYTES / (int)(d * sizeof(T)));
+    const bool split = d <= BA_THREADS / 2;
     T mx[BA_MAX_COLS_PER_LANE], mn[BA_MAX_COLS_PER_LANE], sm[BA_MAX_COLS_PER_LANE];
 #pragma unroll
     for (int k = 0; k < BA_MAX_COLS_PER_LANE; ++k) { mx[k] = -(T)INFINITY; mn[k] = (T)INFINITY; sm[k] = -(T)0; }   // -0 + x == x, signed zeros included
@@ -106,22 +107,78 @@ MEP_DEV void summary_rows(const mep_window_desc& D, int64_t off, int L, MEP_G fl
                 pre[e] = i < n1 ? s1[i] : (T)0;
             }
         }
+        if (split) {
+            // d <= 128: waves 0-1 carry the serial frame-order sums, waves 2-3 the order-free
+            // max / min of the same columns, side by side on other SIMDs
+            const int c = threadIdx.x & (BA_THREADS / 2 - 1);
+            if (c < d) {
+                if (threadIdx.x < BA_THREADS / 2) {
+                    T s = sm[0];
+#pragma unroll 8
+                    for (int f = 0; f < nf; ++f) s = s + buf[f * d + c];
+                    sm[0] = s;
+                } else {
+                    T a = mx[0], b = mn[0];
+                    if (D.clean) {
+#pragma unroll 8
+                        for (int f = 0; f < nf; ++f) {
+                            const T v = buf[f * d + c];
+                            a = v > a ? v : a;
+                            b = v < b ? v : b;
+                        }
+                    } else {
+#pragma unroll 8
+                        for (int f = 0; f < nf; ++f) {
+                            const T v = buf[f * d + c];
+                            a = (v > a || v != v) ? v : a;
+                            b = (v < b || v != v) ? v : b;
+                        }
+                    }
+                    mx[0] = a; mn[0] = b;
+                }
+            }
+            continue;
+        }
 #pragma unroll
         for (int k = 0; k < BA_MAX_COLS_PER_LANE; ++k) {
             const int c = threadIdx.x + k * BA_THREADS;
             if (c < d) {
                 T a = mx[k], b = mn[k], s = sm[k];
+                if (D.clean) {
+                    // cleaned values hold no NaN: two selects per frame (ties keep the earlier
+                    // frame, as numpy's reduction does)
 #pragma unroll 8
-                for (int f = 0; f < nf; ++f) {
-                    const T v = buf[f * d + c];
-                    // numpy maximum / minimum: a NaN operand wins, and stays
-                    a = (v > a || v != v) ? v : a;
-                    b = (v < b || v != v) ? v : b;
-                    s = s + v;
+                    for (int f = 0; f < nf; ++f) {
+                        const T v = buf[f * d + c];
+                        a = v > a ? v : a;
+                        b = v < b ? v : b;
+                        s = s + v;
+                    }
+                } else {
+#pragma unroll 8
+                    for (int f = 0; f < nf; ++f) {
+                        const T v = buf[f * d + c];
+                        // numpy maximum / minimum: a NaN operand wins, and stays
+                        a = (v > a || v != v) ? v : a;
+                        b = (v < b || v != v) ? v : b;
+                        s = s + v;
+                    }
                 }
                 mx[k] = a; mn[k] = b; sm[k] = s;
             }
         }
+    }
+    if (split) {
+        const int c = threadIdx.x & (BA_THREADS / 2 - 1);
+        if (c < d) {
+            if (threadIdx.x < BA_THREADS / 2) {
+                out[2 * d + c] = (float)div_rn(sm[0], (T)L);
+            } else {
+                out[c] = (float)mx[0];
+                out[d + c] = (float)mn[0];
+            }
+        }
+        return;
     }
 #pragma unroll
     for (int k = 0; k < BA_MAX_COLS_PER_LANE; ++k) {
