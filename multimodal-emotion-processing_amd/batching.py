@@ -63,67 +63,74 @@ class FeatureStore:
     def dim(self, mod):
         return self.mods[mod]['d']
 
+    def ids(self, mod, names):
+        """Sequence ids of ``names`` (NO_NAME -> -1) as int32."""
+        ids = self.mods[mod]['ids']
+        return np.fromiter((-1 if n == NO_NAME else ids[n] for n in names), np.int32, len(names))
+
     def assemble(self, slots, stream=None):
         """slots: list of (modality, names, starts, m_len, summary, clean) with names a list of
-        sequence names (NO_NAME for empty slots) -> list of (feat [n, m_len, d], mask [n, m_len])."""
+        sequence names (NO_NAME for empty slots) or an int32 array of sequence ids (-1 = empty)
+        -> list of (feat [n, m_len, d], mask [n, m_len]).  Every slot table of the launch goes to
+        the device in one pinned copy."""
         if len(slots) > _lib.WINDOW_MAX_DESC:
             raise ValueError('assemble: at most %d slot groups per launch' % _lib.WINDOW_MAX_DESC)
         descs = (_lib.WindowDesc * len(slots))()
-        outs, keep = [], []
-        for k, (mod, names, starts, m_len, summary, clean) in enumerate(slots):
-            m = self.mods[mod]
-            sel = np.array([-1 if n == NO_NAME else m['ids'][n] for n in names], np.int32)
+        tabs, outs = [], []
+        for mod, names, starts, m_len, summary, clean in slots:
+            sel = names if isinstance(names, np.ndarray) else self.ids(mod, names)
             st = np.asarray(starts, np.int32)
             if st.shape != sel.shape:
                 raise ValueError('assemble: one window start per slot')
-            tab = torch.from_numpy(np.concatenate([sel, st])).pin_memory().to(self.device, non_blocking=True)
+            tabs += [sel.astype(np.int32, copy=False), st]
+        tab = torch.from_numpy(np.concatenate(tabs)).pin_memory().to(self.device, non_blocking=True)
+        off = 0
+        for k, (mod, names, starts, m_len, summary, clean) in enumerate(slots):
+            m = self.mods[mod]
             n = len(names)
             feat = torch.empty(n, m_len, m['d'], dtype=torch.float32, device=self.device)
             mask = torch.empty(n, m_len, dtype=torch.float32, device=self.device)
             D = descs[k]
             D.src, D.segs = m['src'].data_ptr(), m['segs'].data_ptr()
-            D.sel, D.start = tab.data_ptr(), tab.data_ptr() + 4 * n
+            D.sel, D.start = tab.data_ptr() + 4 * off, tab.data_ptr() + 4 * (off + n)
+            off += 2 * n
             D.out, D.mask = feat.data_ptr(), mask.data_ptr()
             D.n_out, D.m_len, D.d, D.src_f64 = n, m_len, m['d'], int(m['f64'])
             D.summary, D.clean, D.n_seq = int(summary), int(clean), len(m['ids'])
             outs.append((feat, mask))
-            keep.append(tab)
         _lib.call('mep_assemble_windows', descs, len(slots), stream=stream)
-        self._keep = keep       # the slot tables live until the next launch on this store
+        self._keep = tab        # the slot tables live until the next launch on this store
         return outs
-
-
-def cmu_windows(L, m_len):
-    """(first, last) window starts of cmu masking() (run.py:127-140): two windows when
-    L >= m_len - 3, else one (both 0)."""
-    return (0, L - (m_len - 3)) if L >= m_len - 3 else (0, 0)
 
 
 def cmu_batch(store, pairs, label_dict, lens, device=None):
     """data_loader of cmu-mosei/run.py:154-198 for one batch of (previous, current) name pairs ->
     (l, v, a, l_mask, v_mask, a_mask, label) device tensors: l [R, 2, L_LEN, d_l], masks [R, 2, *],
-    label [R, 7] int64, with R >= len(pairs) rows in the reference's order."""
-    lens = dict(zip(MODALITIES, lens))
-    names = {m: [] for m in MODALITIES}
-    starts = {m: [] for m in MODALITIES}
-    labels = []
-    for prev, cur in pairs:
-        two = store.length('linguistic', cur) >= lens['linguistic'] - 3
-        for k in ([1, 0] if two else [0]):           # rows: last windows (if any), then first windows
-            for m in MODALITIES:
-                for name in (prev, cur):
-                    if name == NO_NAME:
-                        names[m].append(NO_NAME)
-                        starts[m].append(0)
-                    else:
-                        names[m].append(name)
-                        starts[m].append(cmu_windows(store.length(m, name), lens[m])[k])
-            labels.append(np.asarray(label_dict[cur], np.int64))
-    outs = store.assemble([(m, names[m], starts[m], lens[m], True, m == 'acoustic') for m in MODALITIES])
-    R = len(labels)
-    feats = [f.view(R, 2, lens[m], f.shape[-1]) for (f, _), m in zip(outs, MODALITIES)]
-    masks = [k.view(R, 2, lens[m]) for (_, k), m in zip(outs, MODALITIES)]
-    lab = torch.from_numpy(np.stack(labels)).pin_memory().to(store.device, non_blocking=True)
+    label [R, 7] int64, with R >= len(pairs) rows in the reference's order: per pair a row of last
+    windows when the current text has two windows, then a row of first windows.  The slot tables
+    are built with numpy (the host work per batch is a few dict lookups per pair)."""
+    prevs = [p for p, _ in pairs]
+    curs = [c for _, c in pairs]
+    ids = {m: (store.ids(m, prevs), store.ids(m, curs)) for m in MODALITIES}
+    L_l = store.mods['linguistic']['lens'][ids['linguistic'][1]]
+    two = L_l >= lens[0] - 3
+    reps = 1 + two.astype(np.int64)
+    pair_of_row = np.repeat(np.arange(len(pairs)), reps)
+    first_row = np.repeat(np.cumsum(reps) - reps, reps)
+    last = (np.arange(len(pair_of_row)) == first_row) & two[pair_of_row]   # rows of last windows
+    R = len(pair_of_row)
+    slots = []
+    for m, n in zip(MODALITIES, lens):
+        sel = np.stack([ids[m][0][pair_of_row], ids[m][1][pair_of_row]], axis=1)      # [R, 2]
+        L = np.where(sel >= 0, store.mods[m]['lens'][np.maximum(sel, 0)], 0)
+        start = np.where(last[:, None] & (L >= n - 3), L - (n - 3), 0)
+        slots.append((m, sel.reshape(-1).astype(np.int32), start.reshape(-1).astype(np.int32), n, True,
+                      m == 'acoustic'))
+    outs = store.assemble(slots)
+    feats = [f.view(R, 2, n, f.shape[-1]) for (f, _), n in zip(outs, lens)]
+    masks = [k.view(R, 2, n) for (_, k), n in zip(outs, lens)]
+    lab_rows = np.stack([np.asarray(label_dict[c], np.int64) for c in curs])[pair_of_row]
+    lab = torch.from_numpy(lab_rows).pin_memory().to(store.device, non_blocking=True)
     return feats + masks + [lab]
 
 
@@ -151,3 +158,44 @@ def rf_batch(store, name_lists, labels, lens):
     lab_t = torch.from_numpy(lab).pin_memory().to(dev, non_blocking=True)
     um_t = torch.from_numpy(um).pin_memory().to(dev, non_blocking=True)
     return feats + [lab_t] + masks + [um_t]
+
+
+# ------------------------------------------------------------------ drop-in data_loader
+class DeviceBatch(tuple):
+    """A batch already on the device, in the reference's column order; ``train`` / ``valid`` take
+    it as it is (no zip / np.stack / H2D copy)."""
+
+
+def cmu_data_loader(store, lens, prefetch=True):
+    """-> ``data_loader(name_list, label_dict, batch_size)`` with the signature and row order of
+    cmu-mosei/run.py:154-198 (``random.shuffle`` of ``name_list`` in place, batches of
+    ``batch_size`` (previous, current) pairs), yielding DeviceBatch.  With ``prefetch`` batch i+1 is
+    assembled on a side stream while the caller's step on batch i runs on the current stream."""
+    import random
+
+    def data_loader(name_list, label_dict, batch_size):
+        random.shuffle(name_list)
+        chunks = [name_list[i:i + batch_size] for i in range(0, len(name_list), batch_size)]
+        main = torch.cuda.current_stream(store.device)
+        side = torch.cuda.Stream(store.device) if prefetch else main
+
+        def build(pairs):
+            side.wait_stream(main)          # buffers recycled from the caller's stream are free
+            with torch.cuda.stream(side):
+                out = cmu_batch(store, pairs, label_dict, lens)
+                ev = torch.cuda.Event()
+                ev.record(side)
+            return out, ev
+
+        nxt = build(chunks[0]) if chunks else None
+        for i in range(len(chunks)):
+            out, ev = nxt
+            if i + 1 < len(chunks):
+                nxt = build(chunks[i + 1])
+            main.wait_event(ev)
+            if side is not main:
+                for t in out:
+                    t.record_stream(main)
+            yield DeviceBatch(out)
+
+    return data_loader

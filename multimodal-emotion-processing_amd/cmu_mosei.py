@@ -137,7 +137,11 @@ def multi_circle_loss(y_pred, y_true):
 
 # ---------------------------------------------------------------------------- train / eval
 def _to_device(batch, device):
-    """zip(*batch) + tensor construction of run.py:361-363, via pinned host buffers."""
+    """zip(*batch) + tensor construction of run.py:361-363, via pinned host buffers (batches from
+    ``batching.cmu_data_loader`` are already on the device and pass through)."""
+    from .batching import DeviceBatch
+    if isinstance(batch, DeviceBatch):
+        return list(batch)
     cols = list(zip(*batch))
     out = []
     for i, col in enumerate(cols):
@@ -151,11 +155,11 @@ def train(model, iterator, optimizer, device='cuda'):
     """One epoch (cmu-mosei/run.py:354-372).  With an ``mep_amd.optim.FusedAdamW`` optimizer the
     whole step (forward, loss, backward, clip, AdamW) runs as the fused engine; with any other
     optimizer it follows the reference statement by statement through autograd."""
-    from .engine import TrainEngine
+    from .engine import LossSum, engine_for
     from .optim import FusedAdamW
     model.train()
-    epoch_loss, count = 0.0, 0
-    engine = TrainEngine(model, optimizer, clip=CLIP) if isinstance(optimizer, FusedAdamW) else None
+    acc, count = LossSum(), 0
+    engine = engine_for(model, optimizer, clip=CLIP) if isinstance(optimizer, FusedAdamW) else None
     for batch in iterator:
         count += 1
         l, v, a, lm, vm, am, label = _to_device(batch, device)
@@ -168,8 +172,8 @@ def train(model, iterator, optimizer, device='cuda'):
             loss.backward()
             nn.utils.clip_grad_norm_(model.parameters(), CLIP)
             optimizer.step()
-        epoch_loss += float(loss.item())
-    return epoch_loss / count
+        acc.add(loss)
+    return acc.value() / count
 
 
 def valid(model, iterator, device='cuda'):

@@ -95,3 +95,34 @@ class TrainEngine:
         first = batch[0][0] if isinstance(batch[0], (tuple, list)) else batch[0]
         plan = self._runner(first.device).stage(*batch)
         return self.step_plan(plan)
+
+
+def engine_for(model, optimizer, **kw):
+    """The TrainEngine of (model, optimizer, options), kept on the optimizer so the graphs it
+    captured (one per batch shape) are replayed across epochs instead of re-captured by every
+    train() call."""
+    key = (id(model),) + tuple(sorted(kw.items()))
+    cache = optimizer.__dict__.setdefault('_mep_engines', {})
+    eng = cache.get(key)
+    if eng is None or eng.model is not model:
+        eng = cache[key] = TrainEngine(model, optimizer, **kw)
+    return eng
+
+
+class LossSum:
+    """``epoch_loss += float(loss.item())`` of the reference train/valid loops without a host sync
+    per batch: each fp32 loss is widened and added in float64 on the device, in batch order --
+    the same IEEE double additions Python performs on the host, so the epoch value is identical,
+    while the host runs ahead to stage the next batch."""
+
+    def __init__(self):
+        self.t = None
+
+    def add(self, loss):
+        l = loss.detach().reshape(()).double()
+        if self.t is None:
+            self.t = torch.zeros((), dtype=torch.float64, device=l.device)
+        self.t.add_(l)
+
+    def value(self):
+        return float(self.t.item()) if self.t is not None else 0.0

@@ -203,11 +203,11 @@ def _to_device(batch, device):
 def train(model, iterator, optimizer, device='cuda'):
     """One epoch (realformer.py:300-318).  With ``mep_amd.optim.FusedAdam`` the step (forward,
     masked circle loss, backward, clip, Adam) is the fused graph-captured engine."""
-    from .engine import TrainEngine
+    from .engine import LossSum, engine_for
     from .optim import FusedAdamW
     model.train()
-    epoch_loss, count = 0.0, 0
-    engine = TrainEngine(model, optimizer, clip=CLIP) if isinstance(optimizer, FusedAdamW) else None
+    acc, count = LossSum(), 0
+    engine = engine_for(model, optimizer, clip=CLIP) if isinstance(optimizer, FusedAdamW) else None
     for batch in iterator:
         count += 1
         l, v, a, label, lm, vm, am, mask = _to_device(batch, device)
@@ -220,8 +220,8 @@ def train(model, iterator, optimizer, device='cuda'):
             loss.backward()
             nn.utils.clip_grad_norm_(model.parameters(), CLIP)
             optimizer.step()
-        epoch_loss += float(loss.item())
-    return epoch_loss / count
+        acc.add(loss)
+    return acc.value() / count
 
 
 def valid(model, iterator, device='cuda'):

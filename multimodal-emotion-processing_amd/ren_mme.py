@@ -170,11 +170,11 @@ def train(model, iterator, optimizer, device='cuda'):
     """One epoch (Ren-MME/run.py:307-340).  With ``mep_amd.optim.FusedAdamW`` the step (forward,
     circle loss + R-Drop KL, backward, clip, AdamW) is the fused graph-captured engine; with any
     other optimizer it follows the reference statement by statement through autograd."""
-    from .engine import TrainEngine
+    from .engine import LossSum, engine_for
     from .optim import FusedAdamW
     model.train()
-    epoch_loss, count = 0.0, 0
-    engine = TrainEngine(model, optimizer, clip=CLIP, rdrop=True) if isinstance(optimizer, FusedAdamW) else None
+    acc, count = LossSum(), 0
+    engine = engine_for(model, optimizer, clip=CLIP, rdrop=True) if isinstance(optimizer, FusedAdamW) else None
     for batch in iterator:
         count += 1
         cols = _to_device(batch, device)
@@ -189,8 +189,8 @@ def train(model, iterator, optimizer, device='cuda'):
             loss.backward()
             nn.utils.clip_grad_norm_(model.parameters(), CLIP)
             optimizer.step()
-        epoch_loss += float(loss.item())
-    return epoch_loss / count
+        acc.add(loss)
+    return acc.value() / count
 
 
 def valid(model, iterator, device='cuda'):

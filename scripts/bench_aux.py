@@ -170,6 +170,45 @@ def bench_sweep(args, rng):
                                                        '%d rows (list appends + sklearn), x400' % N}}
 
 
+def bench_train(args, rng):
+    """cmu train() epochs (fused engine, B = 64 pairs, T = 50, D = 96) fed by the device loader vs
+    by the reference-layout host loader (numpy windowing + zip/stack + H2D): utterance rows/s of
+    the whole epoch, data loading included."""
+    import random
+    from mep_amd import cmu_mosei
+    from mep_amd.optim import FusedAdamW
+    data, labels = make_data(rng, n=1500)
+    names = list(data['linguistic'])
+    pairs = [(names[i - 1] if i % 9 else batching.NO_NAME, names[i]) for i in range(1, 1281)]  # 20 batches
+    lens = (50, 50, 50)
+    store = batching.FeatureStore(data, 'cuda')
+    res = {}
+    for kind in ('device', 'host'):
+        torch.manual_seed(0)
+        model = cmu_mosei.Concat_Trans(dim=96, l_len=50, v_len=50, a_len=50, n_heads=6, n_layers=1, ffn=1).cuda()
+        opt = FusedAdamW(model, lr=1e-3)
+        times = []
+        for ep in range(3):                  # epoch 0 captures one graph per distinct row count
+            random.seed(ep)
+            order = list(pairs)
+            if kind == 'device':
+                it = batching.cmu_data_loader(store, lens)(order, labels, 64)
+            else:
+                random.shuffle(order)
+                it = (list(zip(*ob.cmu_batch(data, labels, order[i:i + 64], lens))) for i in range(0, len(order), 64))
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            cmu_mosei.train(model, it, opt)
+            torch.cuda.synchronize()
+            times.append(time.perf_counter() - t0)
+        res[kind] = min(times[1:])
+    rows = sum(2 if store.length('linguistic', c) >= 47 else 1 for _, c in pairs)
+    return {'metric': 'cmu train epoch incl. data loading, utterance rows/s (B=64 pairs, T=50)',
+            'row': 'SURVEY 8(f)1 in the training loop', 'value': round(rows / res['device'], 1), 'unit': 'rows/s',
+            'host_loader_value': round(rows / res['host'], 1), 'rows_per_epoch': rows, 'batches': 20,
+            'note': 'host loader = numpy masking/data_loader restatement (1 core) + zip/stack + pinned H2D'}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--iters', type=int, default=50)
@@ -177,7 +216,7 @@ def main():
     ap.add_argument('--only', default='')
     args = ap.parse_args()
     rng = np.random.default_rng(20261016)
-    for name, fn in (('assembly', bench_assembly), ('sweep', bench_sweep)):
+    for name, fn in (('assembly', bench_assembly), ('sweep', bench_sweep), ('train', bench_train)):
         if args.only and args.only != name:
             continue
         print(json.dumps(fn(args, rng)), flush=True)

@@ -121,3 +121,49 @@ def test_cmu_batch_gpu_long_sequences(cuda, dt):
     want = ob.cmu_batch(data, labels, pairs, lens)
     for i, (x, w) in enumerate(zip(out, want)):
         _eq(x, w, 'col %d' % i)
+
+
+def _train_data(rng, n=40):
+    dims = {'linguistic': 300, 'visual': 35, 'acoustic': 74}
+    data = {m: {} for m in MODS}
+    for i in range(n):
+        for m, d in dims.items():
+            x = rng.standard_normal((int(rng.integers(1, 120)), d)).astype(np.float32)
+            if m == 'acoustic':
+                x[rng.random(x.shape) < 0.01] = -np.inf
+            data[m]['s%d' % i] = x
+    names = list(data['linguistic'])
+    pairs = [('no_name' if i % 5 == 0 else names[i - 1], names[i]) for i in range(n)]
+    labels = {k: rng.integers(0, 2, 7) for k in names}
+    return data, labels, pairs
+
+
+@pytest.mark.gpu
+def test_device_loader_trains_like_host_loader(cuda):
+    """cmu train() fed by batching.cmu_data_loader (device assembly, side-stream prefetch) equals
+    train() fed the reference-layout host batches (lists of per-row numpy tuples) bit for bit."""
+    import random
+    from mep_amd import batching, cmu_mosei
+    from mep_amd.optim import FusedAdamW
+    from tests.gpu_util import cmu_model
+    meta, _ = fixtures.load('cmu_cfg1')
+    data, labels, pairs = _train_data(np.random.default_rng(4))
+    lens = (50, 50, 50)
+    store = batching.FeatureStore(data, cuda)
+
+    m1 = cmu_model(meta, cuda)
+    o1 = FusedAdamW(m1, lr=1e-3)
+    random.seed(3)
+    loss_dev = cmu_mosei.train(m1, batching.cmu_data_loader(store, lens)(list(pairs), labels, 16), o1)
+
+    m2 = cmu_model(meta, cuda)
+    o2 = FusedAdamW(m2, lr=1e-3)
+    random.seed(3)
+    order = list(pairs)
+    random.shuffle(order)
+    host = [list(zip(*ob.cmu_batch(data, labels, order[i:i + 16], lens))) for i in range(0, len(order), 16)]
+    loss_host = cmu_mosei.train(m2, host, o2)
+    torch.cuda.synchronize()
+    assert loss_dev == loss_host
+    for (k, a), (_, b) in zip(m1.state_dict().items(), m2.state_dict().items()):
+        assert torch.equal(a, b), k
