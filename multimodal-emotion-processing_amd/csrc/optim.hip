@@ -188,8 +188,9 @@ extern "C" int mep_clip_adam(float* params, float* grads, float* exp_avg, float*
         }
         if (segs[i].length > longest) longest = segs[i].length;
     }
-    // 4 float4 per thread per pass: one partial per workgroup for the clip's norm
-    int grid = (int)((longest + OPT_THREADS * 16 - 1) / (OPT_THREADS * 16));
+    // one float4 per thread (a single HBM round trip per lane in the update pass; 4 float4 per
+    // thread serialised 4 dependent load -> store trips), one partial per workgroup for the norm
+    int grid = (int)((longest + OPT_THREADS * 4 - 1) / (OPT_THREADS * 4));
     grid = grid < 1 ? 1 : (grid > NPART ? NPART : grid);
     hipLaunchKernelGGL(k_sqnorm, dim3(grid), dim3(OPT_THREADS), 0, (hipStream_t)stream, grads, s, partial, step);
     int rc = mep_check_launch("mep_clip_adam/sqnorm");
