@@ -199,3 +199,39 @@ def cmu_data_loader(store, lens, prefetch=True):
             yield DeviceBatch(out)
 
     return data_loader
+
+
+def rf_data_loader(store, labels, lens, prefetch=True):
+    """-> ``data_loader(data_set, name_list, batch_size)`` with the signature and row order of
+    others/realformer.py:94-125 (``random.shuffle`` in place; ``data_set`` is not read -- the
+    sequences live in ``store``, the label rows in ``labels[name]``), yielding DeviceBatch of
+    (l, v, a, label, l_mask, v_mask, a_mask, mask); batch i+1 is assembled on a side stream
+    while the caller's step on batch i runs."""
+    import random
+
+    def data_loader(data_set, name_list, batch_size):
+        random.shuffle(name_list)
+        chunks = [name_list[i:i + batch_size] for i in range(0, len(name_list), batch_size)]
+        main = torch.cuda.current_stream(store.device)
+        side = torch.cuda.Stream(store.device) if prefetch else main
+
+        def build(lists):
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                out = rf_batch(store, lists, labels, lens)
+                ev = torch.cuda.Event()
+                ev.record(side)
+            return out, ev
+
+        nxt = build(chunks[0]) if chunks else None
+        for i in range(len(chunks)):
+            out, ev = nxt
+            if i + 1 < len(chunks):
+                nxt = build(chunks[i + 1])
+            main.wait_event(ev)
+            if side is not main:
+                for t in out:
+                    t.record_stream(main)
+            yield DeviceBatch(out)
+
+    return data_loader

@@ -191,7 +191,11 @@ def multi_circle_loss(y_pred, y_true):
 
 # ---------------------------------------------------------------------------- train / eval
 def _to_device(batch, device):
-    """zip(*batch) + torch.cuda.FloatTensor / LongTensor of realformer.py:307-309."""
+    """zip(*batch) + torch.cuda.FloatTensor / LongTensor of realformer.py:307-309 (batches from
+    ``batching.rf_data_loader`` are already on the device and pass through)."""
+    from .batching import DeviceBatch
+    if isinstance(batch, DeviceBatch):
+        return list(batch)
     out = []
     for i, col in enumerate(zip(*batch)):
         arr = np.stack([np.asarray(x) for x in col])

@@ -167,3 +167,45 @@ def test_device_loader_trains_like_host_loader(cuda):
     assert loss_dev == loss_host
     for (k, a), (_, b) in zip(m1.state_dict().items(), m2.state_dict().items()):
         assert torch.equal(a, b), k
+
+
+@pytest.mark.gpu
+def test_rf_device_loader_trains_like_host_loader(cuda):
+    """realformer train() fed by batching.rf_data_loader equals train() fed the reference-layout
+    host batches bit for bit (State_Transfer, fused Adam engine)."""
+    import random
+    from mep_amd import batching
+    from mep_amd import realformer as rf
+    from mep_amd.optim import FusedAdam
+    from tests.test_gpu_realformer import _state
+    meta, _ = fixtures.load('rf_state_small')
+    rng = np.random.default_rng(8)
+    dims = {'linguistic': 300, 'visual': 35, 'acoustic': 74}
+    data = {m: {} for m in MODS}
+    for i in range(12):
+        for m, d in dims.items():
+            x = rng.standard_normal((int(rng.integers(1, 12)), d)).astype(np.float32)
+            x[rng.random(x.shape) < 0.02] = np.nan
+            data[m]['u%d' % i] = x
+    labels = {'u%d' % i: rng.standard_normal(7) for i in range(12)}
+    lists = [['u%d' % (3 * k), 'u%d' % (3 * k + 1), 'no_name' if k == 1 else 'u%d' % (3 * k + 2)] for k in range(4)]
+    lens = (6, 6, 6)
+    store = batching.FeatureStore(data, cuda)
+
+    m1 = _state(meta, cuda)
+    o1 = FusedAdam(m1, lr=1e-3)
+    random.seed(2)
+    loss_dev = rf.train(m1, batching.rf_data_loader(store, labels, lens)(None, [list(x) for x in lists], 2), o1)
+
+    m2 = _state(meta, cuda)
+    o2 = FusedAdam(m2, lr=1e-3)
+    random.seed(2)
+    order = [list(x) for x in lists]
+    random.shuffle(order)
+    host = [list(zip(*ob.rf_batch(data, labels, order[i:i + 2], lens, tuple(dims.values()))))
+            for i in range(0, len(order), 2)]
+    loss_host = rf.train(m2, host, o2)
+    torch.cuda.synchronize()
+    assert loss_dev == loss_host
+    for (k, a), (_, b) in zip(m1.state_dict().items(), m2.state_dict().items()):
+        assert torch.equal(a, b), k
