@@ -53,7 +53,8 @@ class StreamTimer:
 
 
 def make_data(rng, n=2000):
-    spec = {'linguistic': (5, 60, 300), 'visual': (20, 400, 35), 'acoustic': (50, 1500, 74)}
+    a_max = int(os.environ.get('AUX_AUDIO_MAX', '1500'))   # longest audio sequence (frames)
+    spec = {'linguistic': (5, 60, 300), 'visual': (20, 400, 35), 'acoustic': (50, a_max, 74)}
     data = {m: {} for m in spec}
     for i in range(n):
         for m, (lo, hi, d) in spec.items():
