@@ -84,7 +84,7 @@ MEP_DEV void summary_rows(const mep_window_desc& D, int64_t off, int L, MEP_G fl
 #pragma unroll
         for (int e = 0; e < E; ++e) {
             const int i = threadIdx.x + e * BA_THREADS;
-            pre[e] = i < n ? src[i] : (T)0;
+            pre[e] = src[min(i, n - 1)];   // clamped, not predicated: the loads issue back to back
         }
     }
     for (int f0 = 0; f0 < L; f0 += ch) {
@@ -104,7 +104,7 @@ MEP_DEV void summary_rows(const mep_window_desc& D, int64_t off, int L, MEP_G fl
 #pragma unroll
             for (int e = 0; e < E; ++e) {
                 const int i = threadIdx.x + e * BA_THREADS;
-                pre[e] = i < n1 ? s1[i] : (T)0;
+                pre[e] = s1[min(i, n1 - 1)];   // lanes past the chunk re-read its last element
             }
         }
         if (split) {
