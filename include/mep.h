@@ -123,23 +123,28 @@ typedef struct {
     uint64_t stats;     /* [B,H,Tq,2]: row max, 1/row sum                       */
     int32_t  B, H, Tq, Tk;
 } mep_attn_desc;
-/* Launch geometry: one wave per (b, h, 64-query chunk) in the forward and per (b, h, 64-key
- * chunk) in the backward, 4 waves (256 threads) per workgroup; max_tiles =
- * max ceil(B * H * ceil(T / 64) / 4) over descriptors (T = Tq forward, Tk backward).
+/* Launch geometry: forward one wave per (b, h, 64-query chunk), 4 waves (256 threads) per
+ * workgroup, max_tiles = max ceil(B * H * ceil(Tq / 64) / 4) over descriptors; backward one
+ * 256-thread workgroup per (b, h), max_tiles = max B * H.
  * flags select the specialised kernels: PREV = every descriptor has s_prev, SOUT = every
  * descriptor has s_out (backward: ds_next); SHORT / LONG = descriptors with Tk <= 64 / Tk > 64
- * are present (the forward launches one kernel per class present). */
+ * are present (the forward launches one kernel per class present); backward:
+ * MEP_ATTN_DQ_TILES(n) = the largest ceil(Tq / 16) among descriptors with Tk > 64 (their dQ
+ * tiles are carried across key chunks in LDS; n <= 127).
+ * Products run on the bf16 matrix cores with fp32 operands split into bf16 parts: 3 parts for
+ * the scores (fp32-level error), 2 parts elsewhere (relative error <= 2^-17 per product). */
 #define MEP_ATTN_PREV  1
 #define MEP_ATTN_SOUT  2
 #define MEP_ATTN_SHORT 4
 #define MEP_ATTN_LONG  8
+#define MEP_ATTN_DQ_TILES(n) ((n) << 8)
 int mep_attn_fwd(const mep_attn_desc* descs, int n_desc, int max_tiles, int flags, mep_stream_t stream);
 
 /* Backward of the attention core.  Inputs dx (grad of X), the forward's q/k/v/x/stats/s_prev.
  * Outputs: dq += (written with accumulate semantics onto dq_base), dk, dv (dk==dv pointer ->
  * summed, for k is v), ds_prev = c * dS (grad of S_prev) and a per-workgroup partial of
  * dc = sum dS * S_prev.  ds_next: gradient arriving on this layer's S output (c_next * dS_next)
- * or 0. */
+ * or 0.  Deterministic: every sum (over query tiles, waves and key chunks) has a fixed order. */
 typedef struct {
     mep_attn_desc f;
     mep_rows dx;
@@ -147,7 +152,7 @@ typedef struct {
     mep_rows dk, dv;    /* written (summed when dk.ptr == dv.ptr)  */
     uint64_t ds_next;   /* [B,H,Tq,Tk] or 0                        */
     uint64_t ds_prev;   /* [B,H,Tq,Tk] or 0                        */
-    uint64_t dc_partial;/* [B * ceil(Tk/64)] floats or 0           */
+    uint64_t dc_partial;/* [B * H * ceil(Tk/64)] floats or 0       */
 } mep_attn_bwd_desc;
 int mep_attn_bwd(const mep_attn_bwd_desc* descs, int n_desc, int max_tiles, int flags, mep_stream_t stream);
 

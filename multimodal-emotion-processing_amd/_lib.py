@@ -257,6 +257,7 @@ def launch(name, descs, max_tiles, stream=None, threads=None, extra=()):
 
 
 ATTN_PREV, ATTN_SOUT, ATTN_SHORT, ATTN_LONG = 1, 2, 4, 8   # MEP_ATTN_* (include/mep.h)
+ATTN_MAX_DQ_TILES = (160 * 1024 // 4 - 2 * 4 * 64 * 16 - 4) // 256   # csrc/attn.hip backward LDS
 
 
 def _uniform(flags, what):
@@ -267,11 +268,12 @@ def _uniform(flags, what):
 
 def attn_geometry(descs):
     """AttnDesc list of one launch -> (fwd tiles, bwd tiles, fwd flags) following csrc/attn.hip:
-    one wave per (b, h, 64-row chunk), 4 waves per workgroup; flags = MEP_ATTN_* of the launch."""
+    forward one wave per (b, h, 64-query chunk), 4 waves per workgroup; backward one workgroup per
+    (b, h); flags = MEP_ATTN_* of the launch."""
     ft = bt = 0
     for d in descs:
         ft = max(ft, -(-(d.B * d.H * -(-d.Tq // 64)) // 4))
-        bt = max(bt, -(-(d.B * d.H * -(-d.Tk // 64)) // 4))
+        bt = max(bt, d.B * d.H)
     flags = (ATTN_PREV if _uniform([d.s_prev != 0 for d in descs], 's_prev') else 0) | \
             (ATTN_SOUT if _uniform([d.s_out != 0 for d in descs], 's_out') else 0) | \
             (ATTN_SHORT if any(d.Tk <= 64 for d in descs) else 0) | (ATTN_LONG if any(d.Tk > 64 for d in descs) else 0)
@@ -279,9 +281,14 @@ def attn_geometry(descs):
 
 
 def attn_bwd_flags(bdescs):
-    """AttnBwdDesc list of one launch -> MEP_ATTN_PREV | MEP_ATTN_SOUT (= ds_next present)"""
+    """AttnBwdDesc list of one launch -> MEP_ATTN_PREV | MEP_ATTN_SOUT (= ds_next present) |
+    MEP_ATTN_DQ_TILES(largest ceil(Tq/16) among descriptors with Tk > 64: the query tiles whose dQ
+    the backward carries across key chunks in LDS)"""
+    dq_tiles = max([-(-b.f.Tq // 16) for b in bdescs if b.f.Tk > 64] or [0])
+    assert dq_tiles <= ATTN_MAX_DQ_TILES, 'mep_attn_bwd: Tq > %d with Tk > 64 exceeds the LDS' % (16 * ATTN_MAX_DQ_TILES)
     return (ATTN_PREV if _uniform([b.f.s_prev != 0 for b in bdescs], 's_prev') else 0) | \
-           (ATTN_SOUT if _uniform([b.ds_next != 0 for b in bdescs], 'ds_next') else 0)
+           (ATTN_SOUT if _uniform([b.ds_next != 0 for b in bdescs], 'ds_next') else 0) | (dq_tiles << 8) | \
+           (ATTN_SHORT if any(b.f.Tk <= 64 for b in bdescs) else 0) | (ATTN_LONG if any(b.f.Tk > 64 for b in bdescs) else 0)
 
 
 N_CU = 256   # MI355X compute units
@@ -296,5 +303,5 @@ def epi_grid(ntok_max, n_desc):
 
 
 def attn_dc_slots(B, H, Tk):
-    """floats of the backward's dc_partial (one per wave task)"""
+    """floats of the backward's dc_partial (one per (b, h, 64-key chunk))"""
     return B * H * -(-Tk // 64)

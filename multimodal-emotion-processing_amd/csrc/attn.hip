@@ -1,24 +1,36 @@
-// Residual scaled-dot-product attention core, forward and backward, on f32 MFMA (hd = 16).
+// Residual scaled-dot-product attention core, forward and backward, hd = 16.
 //
 // Reference: Attention_Block.multi_head_attention, cmu-mosei/run.py:236-256 (identical in
 // Ren-MME/run.py:188-208 and, after the w_qkv projections, others/realformer.py:182-204):
 //   S = q k^T / sqrt(hd) [+ c * S_prev];  S -= 1e8 (1 - mask);  X = softmax(S) v
 // The post-mask S is returned to the caller, which feeds it to the next layer of the chain.
 //
-// Mapping (CDNA4): one WAVE = one task (batch row b, head h, chunk of 64 queries [forward] or
-// 64 keys [backward]); 4 independent waves per workgroup, no barriers.  All products (S, P.V, dP,
-// dV, dK, dQ) are v_mfma_f32_16x16x4_f32 (exact fp32 fma chains), with operand layouts chosen so
-// an accumulator feeds the next product without moving data:
-//   forward   S^T = K Q^T  -> lane (query c, group g) holds keys 4g..4g+3 of each 16-key tile,
-//             i.e. exactly the A operand of O = P V.  Keys are processed in chunks of 64 (4 tiles,
-//             16 scores per lane per query tile): one row max / rescale per chunk, so for the
-//             common T <= 64 the softmax is exact two-pass with no rescaling at all.
-//   backward  S = Q K^T and dP = dO V^T -> lane (key c, g) holds queries 4g..4g+3: the A operand
-//             of dV += P^T dO and dK += dS^T Q directly; dQ += dS K needs dS with the query on
-//             the lane: one 16 x 64 transpose through LDS per query tile.
-// Reduction dims are ordered (step s, lane group g) -> dim 4g+s, so every operand fetch is one
-// 16-byte load and the forward and backward S are bitwise identical fma chains.  Validity
-// (padded rows / keys) is handled with clamped loads and selects, never branches.
+// Arithmetic: fp32 storage, fp32 softmax / score sequence, products on the bf16 matrix cores
+// with every fp32 operand split into bf16 parts (x = x0 + x1 [+ x2], each part the round-to-
+// nearest bf16 of the remainder; products of bf16 parts are exact in the fp32 accumulator):
+//   scores q.k (fwd and bwd)   3-way split, the six products x_i y_j with i + j <= 2:
+//                              relative error ~2^-24 per product (fp32 level)
+//   backward dP, dV, dK, dQ    2-way split, three or four products: relative error <= 2^-16
+//   forward P.V                fp32 MFMA (v_mfma_f32_16x16x4_f32) on the raw P and V: exact
+// v_mfma_f32_16x16x32_bf16 takes 8 k-slots per lane; the slot -> index assignment is free as long
+// as A and B agree, so a lane's 4 consecutive fp32 values of a 16-wide contraction (the index
+// layout (step s, lane group g) -> 4g + s of the fp32 16x16x4 form) fill slots 0-3 with one part
+// and slots 4-7 with another: a 16-deep fp32 contraction costs 2 (or 3) bf16 MFMAs of 16 cycles
+// instead of 4 fp32 MFMAs of 32 cycles, and every operand is still one 16-byte load.  The
+// forward and the backward issue the score products in the same slots, so the recomputed
+// backward scores equal the forward's bit for bit.
+//
+// Mapping (CDNA4)
+//   forward   one WAVE per (b, h, 64 queries); S^T = K Q^T leaves lane (query c, group g)
+//             holding keys 4g..4g+3 of each 16-key tile -- the A operand of O = P V directly.
+//             Keys in chunks of 64 (exact two-pass softmax for T <= 64, online rescale above).
+//   backward  one WORKGROUP (4 waves) per (b, h).  Key chunks of 64 are the outer loop; wave w
+//             takes query tiles w, w+4, ...  S = Q K^T and dP = dO V^T leave lane (key c, g)
+//             holding queries 4g..4g+3: the A operand of dV += P^T dO and dK += dS^T Q; dQ += dS K
+//             needs dS with the query on the lane (one 16 x 64 LDS transpose per query tile).
+//             dK / dV partials of the 4 waves are summed through LDS in wave order; a query
+//             tile's dQ is owned by one wave and carried across key chunks in LDS: every sum
+//             has a fixed order, so the backward is deterministic for every Tk.
 // Row statistics (max, 1/sum) are kept instead of log-sum-exp because fully masked rows sit at
 // -1e8 where max + log(sum) would round the log away (ulp(1e8) = 8).
 #include <float.h>
@@ -31,41 +43,100 @@ namespace {
 
 typedef float floatx4 __attribute__((ext_vector_type(4)));
 typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+#ifndef MEP_FWD_WAVES
+#define MEP_FWD_WAVES 3    // waves per SIMD of the short, non-residual forward
+#endif
 
 constexpr int HD = 16;
 constexpr int WAVES = 4;
 constexpr int THREADS = 64 * WAVES;
-constexpr int CH = 64;              // queries (forward) / keys (backward) per wave task
+constexpr int CH = 64;              // queries (forward) / keys (backward) per chunk
 constexpr int NT = CH / 16;         // 16-row tiles per chunk
 constexpr float INV_SCALE = 0.25f;  // 1/sqrt(16), exact
 constexpr int TLD = CH + 4;         // LDS row stride of the dS transpose
+constexpr int RED = 2 * WAVES * CH * HD;   // floats of the backward's dK / dV partial buffer
 
-MEP_DEV floatx4 mfma16(float a, float b, floatx4 c) {
-    return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
-}
 MEP_DEV floatx4 zero4() { return floatx4{0.f, 0.f, 0.f, 0.f}; }
 
-MEP_DEV bool aligned16(const mep_rows& r) {
-    return ((r.ptr & 15) == 0) && (r.sB % 4 == 0) && (r.sT % 4 == 0);
+// ------------------------------------------------------------------ bf16 operand splitting
+// two fp32 -> one word of two round-to-nearest bf16 (v_cvt_pk_bf16_f32)
+MEP_DEV unsigned pk(float a, float b) { return __builtin_bit_cast(unsigned, __builtin_convertvector(f32x2{a, b}, bf16x2)); }
+MEP_DEV float bf_lo(unsigned p) { return __builtin_bit_cast(float, p << 16); }
+MEP_DEV float bf_hi(unsigned p) { return __builtin_bit_cast(float, p & 0xffff0000u); }
+
+// 4 fp32 -> parts as bf16 words: h = x0 (2 words), l = x1 (2-way split)
+struct S2 { unsigned h0, h1, l0, l1; };
+// 4 fp32 -> parts a = x0, b = x1, c = x2 (3-way split)
+struct S3 { unsigned a0, a1, b0, b1, c0, c1; };
+
+MEP_DEV S2 split2(float x0, float x1, float x2, float x3) {
+    S2 s;
+    s.h0 = pk(x0, x1);
+    s.h1 = pk(x2, x3);
+    s.l0 = pk(x0 - bf_lo(s.h0), x1 - bf_hi(s.h0));   // exact remainders (Sterbenz)
+    s.l1 = pk(x2 - bf_lo(s.h1), x3 - bf_hi(s.h1));
+    return s;
+}
+MEP_DEV S2 split2(const float* x) { return split2(x[0], x[1], x[2], x[3]); }
+MEP_DEV S3 split3(const float* x) {
+    S3 s;
+    s.a0 = pk(x[0], x[1]);
+    s.a1 = pk(x[2], x[3]);
+    const float r0 = x[0] - bf_lo(s.a0), r1 = x[1] - bf_hi(s.a0);
+    const float r2 = x[2] - bf_lo(s.a1), r3 = x[3] - bf_hi(s.a1);
+    s.b0 = pk(r0, r1);
+    s.b1 = pk(r2, r3);
+    s.c0 = pk(r0 - bf_lo(s.b0), r1 - bf_hi(s.b0));
+    s.c1 = pk(r2 - bf_lo(s.b1), r3 - bf_hi(s.b1));
+    return s;
 }
 
-// base of batch row b of a row view (wave-uniform, 64-bit) -- rows are then addressed with
-// 32-bit per-lane offsets t * sT
-MEP_DEV gfloat* bat(const mep_rows& v, int b) { return G<float>(v.ptr) + (int64_t)b * v.sB; }
-
-// four consecutive floats of row min(t, n-1) at column col.  Rows past the end are never
-// zeroed: a padded key's score is -inf (its mask term is +inf), so its P and dS are exactly 0
-// whatever K/V hold there, and padded queries are never stored (forward) or carry P = 0
-// (backward); clamping keeps every load in bounds and every value finite.
-MEP_DEV void load4(float* dst, const gfloat* base, int sT, int t, int n, int col, bool vec) {
-    const gfloat* p = base + min(t, n - 1) * sT + col;
-    float4 x;
-    if (vec) x = ldg4(p);
-    else x = make_float4(p[0], p[1], p[2], p[3]);
-    dst[0] = x.x; dst[1] = x.y; dst[2] = x.z; dst[3] = x.w;
+MEP_DEV bf16x8 op(unsigned w0, unsigned w1, unsigned w2, unsigned w3) {
+    return __builtin_bit_cast(bf16x8, u32x4{w0, w1, w2, w3});
 }
-MEP_DEV float load1(const gfloat* base, int sT, int t, int n, int col) {
-    return base[min(t, n - 1) * sT + col];
+MEP_DEV floatx4 mfma(bf16x8 a, bf16x8 b, floatx4 c) { return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0); }
+
+// Score product over the 16 head dims, 3-way split: P = the "packed" operand, U = the
+// "duplicated" one; slots (g, j < 4) and (g, j >= 4) carry
+//   MFMA 1: p0 u0 | p1 u0     MFMA 2: p0 u1 | p1 u1     MFMA 3: p0 u2 | p2 u0
+// P_IS_A selects which MFMA operand P is (forward: K = A; backward: K = B), the products and
+// slots are the same either way.
+template <bool P_IS_A>
+MEP_DEV floatx4 dot_score(const S3& p, const S3& u, floatx4 acc) {
+    const bf16x8 p01 = op(p.a0, p.a1, p.b0, p.b1), p02 = op(p.a0, p.a1, p.c0, p.c1);
+    const bf16x8 u00 = op(u.a0, u.a1, u.a0, u.a1), u11 = op(u.b0, u.b1, u.b0, u.b1), u20 = op(u.c0, u.c1, u.a0, u.a1);
+    if (P_IS_A) {
+        acc = mfma(p01, u00, acc);
+        acc = mfma(p01, u11, acc);
+        acc = mfma(p02, u20, acc);
+    } else {
+        acc = mfma(u00, p01, acc);
+        acc = mfma(u11, p01, acc);
+        acc = mfma(u20, p02, acc);
+    }
+    return acc;
+}
+
+// 16-deep contraction, 2-way split, all four products: A = [x0 | x1], B = [y0 | y0] then [y1 | y1]
+MEP_DEV floatx4 dot16(const S2& x, const S2& y, floatx4 acc) {
+    const bf16x8 a = op(x.h0, x.h1, x.l0, x.l1);
+    acc = mfma(a, op(y.h0, y.h1, y.h0, y.h1), acc);
+    acc = mfma(a, op(y.l0, y.l1, y.l0, y.l1), acc);
+    return acc;
+}
+
+// 32-deep contraction over two 16-row tiles (slots 0-3: tile 0, 4-7: tile 1), 2-way split,
+// products x0 y0 + x1 y0 + x0 y1
+MEP_DEV floatx4 dot32(const S2& xa, const S2& xb, const S2& ya, const S2& yb, floatx4 acc) {
+    const bf16x8 x0 = op(xa.h0, xa.h1, xb.h0, xb.h1), y0 = op(ya.h0, ya.h1, yb.h0, yb.h1);
+    acc = mfma(x0, y0, acc);
+    acc = mfma(op(xa.l0, xa.l1, xb.l0, xb.l1), y0, acc);
+    acc = mfma(x0, op(ya.l0, ya.l1, yb.l0, yb.l1), acc);
+    return acc;
 }
 
 // per-key mask term of the score: 1e8 * (1 - mask) (cmu-mosei/run.py:253), +inf for padding keys
@@ -85,11 +156,15 @@ MEP_DEV float score(float dot, float c, float sp, float mt) {
     return sub_rn(s, mt);
 }
 
+MEP_DEV bool aligned16(const mep_rows& r) {
+    return ((r.ptr & 15) == 0) && (r.sB % 4 == 0) && (r.sT % 4 == 0);
+}
+
 // One batch row of a row view as a range-checked buffer (csrc/common.h raw buffer ops): row t,
 // column col at byte t * sT + 4 col.  Rows t >= n lie past the range (every view has sT >= its
 // D used columns), so their loads return 0 and their stores are dropped -- no clamps, no
-// branches, 32-bit offsets.  The base is wave-uniform by construction (one (b, h) per wave);
-// readfirstlane makes that provable so the descriptor lives in SGPRs.
+// branches, 32-bit offsets.  The base is wave-uniform by construction (one (b, h) per wave or
+// workgroup); readfirstlane makes that provable so the descriptor lives in SGPRs.
 struct BRow {
     __amdgpu_buffer_rsrc_t rs;
     int sT4;   // row stride in bytes (wave-uniform)
@@ -112,6 +187,14 @@ struct BRow {
     MEP_DEV void st1(int voff, int soff, float v) const {
         __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), rs, voff, soff, 0);
     }
+    MEP_DEV void st4(int voff, f32x4 v) const {
+        if (vec) {
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rs, voff, 0, 0);
+        } else {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) st1(voff + 4 * e, 0, v[e]);
+        }
+    }
 };
 
 MEP_DEV __amdgpu_buffer_rsrc_t uniform_rsrc(uint64_t base, int64_t bytes) {
@@ -127,6 +210,7 @@ MEP_DEV BRow brow(const mep_rows& v, int b, int n, int D) {
                 4 * (int)v.sT, aligned16(v)};
 }
 
+// ================================================================== forward
 // One forward task: batch row b, head h, 64 queries.  PREV: residual scores in; SOUT: post-mask
 // scores out; SINGLE: Tk <= 64 (one key chunk: exact two-pass softmax, each query tile is
 // finalised right after its P.V, so no running O/max/sum state stays live).
@@ -167,18 +251,22 @@ MEP_DEV void attn_fwd_task(const mep_attn_desc& d, int qc, int h, int b, int lan
     };
 
     for (int k_lo = 0; k_lo < Tk; k_lo += CH) {
-        // operands of the 4 key tiles of this chunk
-        float kf[NT][4], vf[NT][4], mt[NT][4];
+        // operands of the 4 key tiles of this chunk: K rows (A of S^T: K[k0+c][4g+s], split) and V
+        // columns (B of P.V: V[k0+4g+s][c]); past Tk they read 0 (P is 0 there)
+        S3 ks[NT];
+        float vf[NT][4], mt[NT][4];
 #pragma unroll
         for (int kt = 0; kt < NT; ++kt) {
             const int k0 = k_lo + kt * 16;
-            Kb.ld4(kf[kt], Kb.at(k0 + c, hc + 4 * g));                    // A: K[k0+c][4g+s]
-            const int ov = Vb.at(k0 + 4 * g, hc + c);                       // B of P.V: V[k0+4g+s][c]
+            float kf[4];
+            Kb.ld4(kf, Kb.at(k0 + c, hc + 4 * g));
+            const int ov = Vb.at(k0 + 4 * g, hc + c);
 #pragma unroll
             for (int s = 0; s < 4; ++s) {
                 vf[kt][s] = Vb.ld1(ov, s * Vb.sT4);
                 mt[kt][s] = mask_term(mask, k0 + 4 * g + s, Tk);
             }
+            ks[kt] = split3(kf);
         }
         float qfa[NT][4];                                                  // B of S^T: Q[q][4g+s]
 #pragma unroll
@@ -187,15 +275,13 @@ MEP_DEV void attn_fwd_task(const mep_attn_desc& d, int qc, int h, int b, int lan
         for (int qt = 0; qt < NT; ++qt) {
             if (qt >= nqt) break;
             const int q = q_lo + qt * 16 + c;
-            const float* qf = qfa[qt];
+            const S3 qs = split3(qfa[qt]);
             const int srow = (sbase + min(q, Tq - 1)) * Tk;
             float sv[NT][4];
             float mx = -INFINITY;
 #pragma unroll
             for (int kt = 0; kt < NT; ++kt) {
-                floatx4 st = zero4();
-#pragma unroll
-                for (int s = 0; s < 4; ++s) st = mfma16(kf[kt][s], qf[s], st);   // C[key 4g+r][query c]
+                const floatx4 st = dot_score<true>(ks[kt], qs, zero4());   // C[key 4g+r][query c]
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     float spv = 0.f;
@@ -230,10 +316,16 @@ MEP_DEV void attn_fwd_task(const mep_attn_desc& d, int qc, int h, int b, int lan
 #pragma unroll
                 for (int r = 0; r < 4; ++r) oq[r] *= shfl(corr, 4 * g + r);  // O row 4g+r <- query 4g+r
             }
+            // O += P V over the chunk's 64 keys: key-tile pairs (slots 0-3 / 4-7)
 #pragma unroll
-            for (int kt = 0; kt < NT; ++kt)
+            for (int kt = 0; kt < NT; kt += 2) {
+                // fp32 MFMA on the raw P and V (exact fp32 fma chain): a bf16 split of P would need
+                // three parts for fp32-level logits, and its VALU cost more than these 8 MFMAs
 #pragma unroll
-                for (int s = 0; s < 4; ++s) oq = mfma16(sv[kt][s], vf[kt][s], oq);  // C[query 4g+r][dim c]
+                for (int k2 = 0; k2 < 2; ++k2)
+#pragma unroll
+                    for (int s = 0; s < 4; ++s) oq = mfma16x4(sv[kt + k2][s], vf[kt + k2][s], oq);
+            }
             if (SINGLE) {
                 finish(qt, oq, mnew, lsum);
             } else {
@@ -253,7 +345,7 @@ MEP_DEV void attn_fwd_task(const mep_attn_desc& d, int qc, int h, int b, int lan
 }
 
 template <bool PREV, bool SOUT, bool SINGLE>
-__global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu((SINGLE && !PREV) ? 4 : 1))) void k_attn_fwd(const mep_attn_desc* __restrict__ descs) {
+__global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu((SINGLE && !PREV) ? MEP_FWD_WAVES : 2))) void k_attn_fwd(const mep_attn_desc* __restrict__ descs) {
     const mep_attn_desc& d = descs[blockIdx.y];
     if ((d.Tk <= CH) != SINGLE) return;    // the other variant's descriptor
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -270,54 +362,86 @@ MEP_DEV void wave_lds_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// One backward task: batch row b, head h, 64 keys.  PREV: residual scores (writes dS_prev and the
-// dc partial); DSN: a gradient arrives on this layer's post-mask S output.
+// ================================================================== backward
+// State of one (descriptor, b, h) backward unit: views, the operands of the current 64-key chunk
+// (B of S = K rows with the key on the lane, B of dP = V rows, B of dQ = K columns rows 4g+s /
+// dim c, the keys' mask terms) and the chunk's dK / dV accumulators (C[key 4g+r][dim c]).
+// PREV: residual scores (writes dS_prev, sums the dc partial); DSN: a gradient arrives on this
+// layer's post-mask S output.
 template <bool PREV, bool DSN>
-MEP_DEV void attn_bwd_task(const mep_attn_bwd_desc& bd, int task, int kc, int nkc, int h, int b, int lane, float* T) {
-    const mep_attn_desc& d = bd.f;
-    const int c = lane & 15, g = lane >> 4;
-    const int hc = h * HD;
-    const int Tq = d.Tq, Tk = d.Tk, D = d.H * HD;
-    const float cres = PREV ? *G<const float>(d.c) : 0.f;
-    const gfloat* sprev = G<const float>(d.s_prev);
-    const gfloat* dsn = G<const float>(bd.ds_next);
-    gfloat* dsp = G<float>(bd.ds_prev);
-    const gfloat* mask = G<const float>(d.mask) + (int64_t)b * d.mask_sB;
-    const BRow Qb = brow(d.q, b, Tq, D), Kb = brow(d.k, b, Tk, D), Vb = brow(d.v, b, Tk, D);
-    const BRow Ob = brow(d.x, b, Tq, D), Gb = brow(bd.dx, b, Tq, D), dQb = brow(bd.dq, b, Tq, D);
-    const int sbase = (b * d.H + h) * Tq;
-    const auto rsStat = uniform_rsrc(d.stats + 8ull * (uint64_t)sbase, 8 * (int64_t)Tq);
-
-    const int k_lo = kc * CH;
-    // per key tile: B operands of S (K) and dP (V) with the key on the lane, the key's mask term,
-    // and the B operand of dQ (K rows 4g+s, dim c); dK / dV accumulators (C[key 4g+r][dim c])
-    float kb[NT][4], vb[NT][4], kq[NT][4], mtk[NT];
-    floatx4 dk[NT], dv[NT];
-#pragma unroll
-    for (int kt = 0; kt < NT; ++kt) {
-        const int k0 = k_lo + kt * 16;
-        Kb.ld4(kb[kt], Kb.at(k0 + c, hc + 4 * g));
-        Vb.ld4(vb[kt], Vb.at(k0 + c, hc + 4 * g));
-        mtk[kt] = mask_term(mask, k0 + c, Tk);
-#pragma unroll
-        for (int s = 0; s < 4; ++s) kq[kt][s] = Kb.ld1(Kb.at(k0 + 4 * g, hc + c), s * Kb.sT4);
-        dk[kt] = zero4();
-        dv[kt] = zero4();
-    }
-    float dc_acc = 0.f;
-    const int nqt = (Tq + 15) / 16;
-    // Every global load of a 16-query tile (Q and dO in both layouts, O for delta, the row stats
-    // and the dQ rows this tile accumulates onto) is issued one tile ahead, into the other of two
-    // register sets, so only the first tile waits for memory.
+struct Bwd {
+    // per query tile: A of S (Q rows), A of dP (dO rows), B of dV / dK (dO / Q columns), O
+    // columns for delta, row stats and the dq rows this tile accumulates onto
     struct QIn {
         float qa[4], da[4], db[4], qb[4], ob[4], dqo[4];
         f32x2 st[4];
     };
-    auto fetch = [&](QIn& in, int qt) {
-        const int q0 = qt * 16;   // tiles past the end read zeros
-        Qb.ld4(in.qa, Qb.at(q0 + c, hc + 4 * g));   // A of S: Q[q0+c][4g+s]
-        Gb.ld4(in.da, Gb.at(q0 + c, hc + 4 * g));   // A of dP: dO[q0+c][4g+s]
-        const int qg = q0 + 4 * g;                  // B of dV / dK: rows qg + s, dim c
+    const mep_attn_bwd_desc& bd;
+    int b, h, lane, c, g, hc, Tq, Tk, sbase;
+    float cres;
+    const gfloat *sprev, *dsn, *mask;
+    gfloat* dsp;
+    BRow Qb, Kb, Vb, Ob, Gb, dQb;
+    __amdgpu_buffer_rsrc_t rsStat;
+    bool same_kv;
+    int k_lo;
+    S3 kb[NT];
+    S2 vb[NT], kq[NT];
+    float mtk[NT];
+    floatx4 dk[NT], dv[NT];
+    float dc_acc;
+
+    MEP_DEV Bwd(const mep_attn_bwd_desc& bd_, int b_, int h_, int lane_) : bd(bd_), b(b_), h(h_), lane(lane_) {
+        const mep_attn_desc& d = bd.f;
+        c = lane & 15;
+        g = lane >> 4;
+        hc = h * HD;
+        Tq = d.Tq;
+        Tk = d.Tk;
+        const int D = d.H * HD;
+        cres = PREV ? *G<const float>(d.c) : 0.f;
+        sprev = G<const float>(d.s_prev);
+        dsn = G<const float>(bd.ds_next);
+        dsp = G<float>(bd.ds_prev);
+        mask = G<const float>(d.mask) + (int64_t)b * d.mask_sB;
+        Qb = brow(d.q, b, Tq, D);
+        Kb = brow(d.k, b, Tk, D);
+        Vb = brow(d.v, b, Tk, D);
+        Ob = brow(d.x, b, Tq, D);
+        Gb = brow(bd.dx, b, Tq, D);
+        dQb = brow(bd.dq, b, Tq, D);
+        same_kv = d.k.ptr == d.v.ptr && d.k.sB == d.v.sB && d.k.sT == d.v.sT;
+        sbase = (b * d.H + h) * Tq;
+        rsStat = uniform_rsrc(d.stats + 8ull * (uint64_t)sbase, 8 * (int64_t)Tq);
+    }
+
+    MEP_DEV void load_chunk(int kc) {
+        k_lo = kc * CH;
+#pragma unroll
+        for (int kt = 0; kt < NT; ++kt) {
+            const int k0 = k_lo + kt * 16;
+            float kf[4], vf[4], kc4[4];
+            Kb.ld4(kf, Kb.at(k0 + c, hc + 4 * g));
+            if (!same_kv) Vb.ld4(vf, Vb.at(k0 + c, hc + 4 * g));
+            mtk[kt] = mask_term(mask, k0 + c, Tk);
+            const int okq = Kb.at(k0 + 4 * g, hc + c);
+#pragma unroll
+            for (int s = 0; s < 4; ++s) kc4[s] = Kb.ld1(okq, s * Kb.sT4);
+            kb[kt] = split3(kf);
+            // k is v (cmu-mosei, Ren-MME): the 2-way split of V is the first two parts of K's
+            vb[kt] = same_kv ? S2{kb[kt].a0, kb[kt].a1, kb[kt].b0, kb[kt].b1} : split2(vf);
+            kq[kt] = split2(kc4);
+            dk[kt] = zero4();
+            dv[kt] = zero4();
+        }
+        dc_acc = 0.f;
+    }
+
+    MEP_DEV void fetch(QIn& in, int qt) const {
+        const int q0 = qt * 16;   // rows past Tq read zeros
+        Qb.ld4(in.qa, Qb.at(q0 + c, hc + 4 * g));
+        Gb.ld4(in.da, Gb.at(q0 + c, hc + 4 * g));
+        const int qg = q0 + 4 * g;
         const int og = Gb.at(qg, hc + c), oq = Qb.at(qg, hc + c), oo = Ob.at(qg, hc + c), od = dQb.at(qg, hc + c);
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
@@ -325,10 +449,14 @@ MEP_DEV void attn_bwd_task(const mep_attn_bwd_desc& bd, int task, int kc, int nk
             in.qb[s] = Qb.ld1(oq, s * Qb.sT4);
             in.ob[s] = Ob.ld1(oo, s * Ob.sT4);
             in.st[s] = __builtin_bit_cast(f32x2, __builtin_amdgcn_raw_buffer_load_b64(rsStat, 8 * qg, 8 * s, 0));
-            in.dqo[s] = nkc == 1 ? dQb.ld1(od, s * dQb.sT4) : 0.f;
+            in.dqo[s] = dQb.ld1(od, s * dQb.sT4);
         }
-    };
-    auto body = [&](const QIn& in, int qt) {
+    }
+
+    // one 16-query tile against the chunk's 64 keys: accumulates dK / dV, returns this chunk's
+    // dQ contribution (C[query 4g+r][dim c], before the 1/sqrt(hd) scale).  Tr: the wave's
+    // 16 x TLD transpose scratch in LDS.
+    MEP_DEV floatx4 tile(const QIn& in, int qt, float* Tr) {
         const int q0 = qt * 16;
         float mm[4], li[4], del[4];
 #pragma unroll
@@ -341,16 +469,14 @@ MEP_DEV void attn_bwd_task(const mep_attn_bwd_desc& bd, int task, int kc, int nk
             mm[s] = qok ? in.st[s][0] : INFINITY;
             li[s] = qok ? in.st[s][1] : 0.f;
         }
-        float ds[NT][4];
+        const S3 qs = split3(in.qa);
+        const S2 do2 = split2(in.da), db2 = split2(in.db), qb2 = split2(in.qb);
 #pragma unroll
         for (int kt = 0; kt < NT; ++kt) {
             const int kk = k_lo + kt * 16 + c;
-            floatx4 st = zero4(), dp = zero4();
-#pragma unroll
-            for (int s = 0; s < 4; ++s) st = mfma16(in.qa[s], kb[kt][s], st);   // C[query 4g+r][key c]
-#pragma unroll
-            for (int s = 0; s < 4; ++s) dp = mfma16(in.da[s], vb[kt][s], dp);
-            float p[4];
+            const floatx4 st = dot_score<false>(kb[kt], qs, zero4());   // C[query 4g+r][key c]
+            const floatx4 dp = dot16(do2, vb[kt], zero4());
+            float p[4], dsv[4];
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const int qq = q0 + 4 * g + r;
@@ -372,93 +498,164 @@ MEP_DEV void attn_bwd_task(const mep_attn_bwd_desc& bd, int task, int kc, int nk
                     }
                 }
                 p[r] = pv;
-                ds[kt][r] = gsv;
+                dsv[r] = gsv;
             }
+            dv[kt] = dot16(split2(p), db2, dv[kt]);      // dV[key][dim] += P^T dO
+            dk[kt] = dot16(split2(dsv), qb2, dk[kt]);    // dK[key][dim] += dS^T Q
 #pragma unroll
-            for (int s = 0; s < 4; ++s) {
-                dv[kt] = mfma16(p[s], in.db[s], dv[kt]);         // dV[key][dim] += P^T dO
-                dk[kt] = mfma16(ds[kt][s], in.qb[s], dk[kt]);    // dK[key][dim] += dS^T Q
-            }
-#pragma unroll
-            for (int r = 0; r < 4; ++r) T[(4 * g + r) * TLD + kt * 16 + c] = ds[kt][r];   // T[query][key]
+            for (int r = 0; r < 4; ++r) Tr[(4 * g + r) * TLD + kt * 16 + c] = dsv[r];   // Tr[query][key]
         }
         // dQ += dS K with the query on the lane: read back the transposed 16 x 64 dS tile
         wave_lds_sync();
-        floatx4 dq = zero4();
+        S2 tq[NT];
 #pragma unroll
         for (int kt = 0; kt < NT; ++kt) {
-            const float4 t4 = *reinterpret_cast<const float4*>(T + c * TLD + kt * 16 + 4 * g);
-            dq = mfma16(t4.x, kq[kt][0], dq);
-            dq = mfma16(t4.y, kq[kt][1], dq);
-            dq = mfma16(t4.z, kq[kt][2], dq);
-            dq = mfma16(t4.w, kq[kt][3], dq);
+            const float4 t4 = *reinterpret_cast<const float4*>(Tr + c * TLD + kt * 16 + 4 * g);
+            tq[kt] = split2(t4.x, t4.y, t4.z, t4.w);
         }
         wave_lds_sync();
-        // dq rows q0+4g+r, dim c (exclusive owner when the keys fit one chunk; else atomics);
-        // rows past Tq are dropped by the range check
-        const int od = dQb.at(q0 + 4 * g, hc + c);
+        floatx4 dq = zero4();
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const int qq = q0 + 4 * g + r;
-            if (nkc == 1) {
-                dQb.st1(od, r * dQb.sT4, in.dqo[r] + dq[r] * INV_SCALE);
-            } else if (qq < Tq) {
-                gfloat* dqp = G<float>(bd.dq.ptr) + (int64_t)b * bd.dq.sB + (int64_t)qq * bd.dq.sT + hc + c;
-                atomicAdd(reinterpret_cast<float*>(reinterpret_cast<uintptr_t>(dqp)), dq[r] * INV_SCALE);
-            }
-        }
-    };
-    QIn bufA, bufB;
-    fetch(bufA, 0);
+        for (int kt = 0; kt < NT; kt += 2) dq = dot32(tq[kt], tq[kt + 1], kq[kt], kq[kt + 1], dq);
+        return dq;
+    }
+
+    // final dq rows of a tile: dq_in + total * 1/sqrt(hd) (rows past Tq dropped)
+    MEP_DEV void store_dq(const QIn& in, int qt, const floatx4& dq) const {
+        const int od = dQb.at(qt * 16 + 4 * g, hc + c);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) dQb.st1(od, r * dQb.sT4, in.dqo[r] + dq[r] * INV_SCALE);
+    }
+};
+
+// SHORT (Tk <= 64): one WAVE per (b, h) -- the single key chunk makes the wave the exclusive owner
+// of every dQ row and of its dK / dV rows, so no cross-wave sums are needed; the query tiles are
+// walked with every load of the next tile issued before this tile's math (two register sets).
+template <bool PREV, bool DSN>
+__global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(2))) void k_attn_bwd_short(const mep_attn_bwd_desc* __restrict__ descs) {
+    __shared__ __attribute__((aligned(16))) float Tr[WAVES][16 * TLD];
+    const mep_attn_bwd_desc& bd = descs[blockIdx.y];
+    if (bd.f.Tk > CH) return;                // a LONG descriptor
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int bh = blockIdx.x * WAVES + wave;
+    if (bh >= bd.f.B * bd.f.H) return;       // whole wave leaves; only wave-private LDS below
+    Bwd<PREV, DSN> u(bd, bh / bd.f.H, bh % bd.f.H, lane);
+    const int nqt = (u.Tq + 15) / 16;
+    u.load_chunk(0);
+    typename Bwd<PREV, DSN>::QIn bufA, bufB;
+    u.fetch(bufA, 0);
     for (int qt = 0; qt < nqt; qt += 2) {
-        fetch(bufB, qt + 1);
-        body(bufA, qt);
+        u.fetch(bufB, qt + 1);               // past the end: range-checked zeros, never used
+        u.store_dq(bufA, qt, u.tile(bufA, qt, Tr[wave]));
         if (qt + 1 < nqt) {
-            fetch(bufA, qt + 2);
-            body(bufB, qt + 1);
+            u.fetch(bufA, qt + 2);
+            u.store_dq(bufB, qt + 1, u.tile(bufB, qt + 1, Tr[wave]));
         }
     }
-    const bool same_kv = bd.dk.ptr == bd.dv.ptr && bd.dk.sB == bd.dv.sB && bd.dk.sT == bd.dv.sT;
-    const BRow dKb = brow(bd.dk, b, Tk, D), dVb = brow(bd.dv, b, Tk, D);   // keys past Tk: dropped
-    const int ok_ = dKb.at(k_lo + 4 * g, hc + c), ov_ = dVb.at(k_lo + 4 * g, hc + c);
+    const BRow dKb = brow(bd.dk, u.b, u.Tk, bd.f.H * HD), dVb = brow(bd.dv, u.b, u.Tk, bd.f.H * HD);
+    const bool same_out = bd.dk.ptr == bd.dv.ptr && bd.dk.sB == bd.dv.sB && bd.dk.sT == bd.dv.sT;
+    const int ok_ = dKb.at(4 * u.g, u.hc + u.c), ov_ = dVb.at(4 * u.g, u.hc + u.c);   // keys past Tk: dropped
 #pragma unroll
-    for (int kt = 0; kt < NT; ++kt) {
+    for (int kt = 0; kt < NT; ++kt)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-            if (same_kv) {
-                dKb.st1(ok_, (16 * kt + r) * dKb.sT4, dk[kt][r] * INV_SCALE + dv[kt][r]);
+            if (same_out) {
+                dKb.st1(ok_, (16 * kt + r) * dKb.sT4, u.dk[kt][r] * INV_SCALE + u.dv[kt][r]);
             } else {
-                dKb.st1(ok_, (16 * kt + r) * dKb.sT4, dk[kt][r] * INV_SCALE);
-                dVb.st1(ov_, (16 * kt + r) * dVb.sT4, dv[kt][r]);
+                dKb.st1(ok_, (16 * kt + r) * dKb.sT4, u.dk[kt][r] * INV_SCALE);
+                dVb.st1(ov_, (16 * kt + r) * dVb.sT4, u.dv[kt][r]);
             }
         }
-    }
     if (PREV && bd.dc_partial) {
-        const float w = wave_sum(dc_acc);
-        if (lane == 0) G<float>(bd.dc_partial)[task] = w;
+        const float w = wave_sum(u.dc_acc);
+        if (lane == 0) G<float>(bd.dc_partial)[bh] = w;
     }
 }
 
+// LONG (Tk > 64): one WORKGROUP per (b, h).  Key chunks are the outer loop; wave w takes query
+// tiles w, w+4, ...; the waves' dK / dV partials of a chunk are summed in wave order through LDS
+// and a tile's dQ is carried across chunks in (wave-private) LDS, so every sum has a fixed order.
+// LDS: [RED] dK/dV partials (aliased by the waves' dS transposes during the query loop), [4] dc
+// partials, [dq_tiles][256] the carried dQ tiles.
 template <bool PREV, bool DSN>
-__global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu((PREV || DSN) ? 1 : 2))) void k_attn_bwd(const mep_attn_bwd_desc* __restrict__ descs) {
+__global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(2))) void k_attn_bwd_long(const mep_attn_bwd_desc* __restrict__ descs) {
+    extern __shared__ __attribute__((aligned(16))) float lds[];
     const mep_attn_bwd_desc& bd = descs[blockIdx.y];
     const mep_attn_desc& d = bd.f;
+    const int bh = blockIdx.x;
+    if (d.Tk <= CH || bh >= d.B * d.H) return;   // a SHORT descriptor / past the end: the whole workgroup
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int nkc = (d.Tk + CH - 1) / CH;
-    const int task = blockIdx.x * WAVES + wave;
-    __shared__ __attribute__((aligned(16))) float Tr[WAVES][16 * TLD];
-    if (task >= d.B * d.H * nkc) return;   // whole wave leaves; only wave-private LDS below
-    const int kc = task % nkc, bh = task / nkc;
-    attn_bwd_task<PREV, DSN>(bd, task, kc, nkc, bh % d.H, bh / d.H, lane, Tr[wave]);
+    Bwd<PREV, DSN> u(bd, bh / d.H, bh % d.H, lane);
+    const int D = d.H * HD;
+    const int nqt = (u.Tq + 15) / 16, nkc = (u.Tk + CH - 1) / CH;
+    const int nw = min(WAVES, nqt);          // waves that own query tiles
+    const BRow dKb = brow(bd.dk, u.b, u.Tk, D), dVb = brow(bd.dv, u.b, u.Tk, D);   // keys past Tk: dropped
+    const bool same_out = bd.dk.ptr == bd.dv.ptr && bd.dk.sB == bd.dv.sB && bd.dk.sT == bd.dv.sT;
+    float* Tr = lds + wave * (16 * TLD);     // inside the R region
+    float* R = lds;
+    float* DC = lds + RED;
+    float* DQ = DC + WAVES;
+    for (int kc = 0; kc < nkc; ++kc) {
+        u.load_chunk(kc);
+        for (int qt = wave; qt < nqt; qt += WAVES) {
+            typename Bwd<PREV, DSN>::QIn in;
+            u.fetch(in, qt);
+            floatx4 dq = u.tile(in, qt, Tr);
+            floatx4* carry = reinterpret_cast<floatx4*>(DQ + qt * 256) + lane;
+            if (kc > 0) dq += *carry;
+            if (kc + 1 < nkc) *carry = dq;
+            else u.store_dq(in, qt, dq);
+        }
+        __syncthreads();                      // every wave is done with its transpose region
+        if (wave < nw) {
+            float* Rw = R + wave * 2 * CH * HD;
+#pragma unroll
+            for (int kt = 0; kt < NT; ++kt)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int e = (kt * 16 + 4 * u.g + r) * HD + u.c;
+                    if (same_out) {
+                        Rw[e] = u.dk[kt][r] * INV_SCALE + u.dv[kt][r];
+                    } else {
+                        Rw[e] = u.dk[kt][r] * INV_SCALE;
+                        Rw[CH * HD + e] = u.dv[kt][r];
+                    }
+                }
+        }
+        if (PREV) {
+            const float w = wave < nw ? wave_sum(u.dc_acc) : 0.f;
+            if (lane == 0) DC[wave] = w;
+        }
+        __syncthreads();
+        {
+            const int t = threadIdx.x;               // key t / 4, dims 4 (t % 4) .. + 3
+            const int key = t >> 2, col = 4 * (t & 3);
+            const int e = key * HD + col;
+            f32x4 sk = *reinterpret_cast<const f32x4*>(R + e);
+            f32x4 sv = *reinterpret_cast<const f32x4*>(R + CH * HD + e);
+            for (int w = 1; w < nw; ++w) {
+                sk += *reinterpret_cast<const f32x4*>(R + w * 2 * CH * HD + e);
+                if (!same_out) sv += *reinterpret_cast<const f32x4*>(R + w * 2 * CH * HD + CH * HD + e);
+            }
+            dKb.st4(dKb.at(kc * CH + key, u.hc + col), sk);
+            if (!same_out) dVb.st4(dVb.at(kc * CH + key, u.hc + col), sv);
+            if (PREV && t == 0 && bd.dc_partial)
+                G<float>(bd.dc_partial)[bh * nkc + kc] = ((DC[0] + DC[1]) + DC[2]) + DC[3];
+        }
+        __syncthreads();                      // R read before the next chunk's transposes
+    }
 }
 
 }  // namespace
 
-// Launch geometry: 256 threads (4 waves, one task each); tasks = B * H * ceil(Tq/64) forward,
-// B * H * ceil(Tk/64) backward; max_tiles = ceil(max tasks / 4).  dc_partial (backward) has one
-// float per task, task = (b*H + h) * ceil(Tk/64) + key chunk.  `flags` (MEP_ATTN_*) select the
-// compiled variants: PREV / SOUT (DSN) must hold for every descriptor of the launch; SHORT / LONG
-// say whether descriptors with Tk <= 64 / Tk > 64 are present (one kernel launch per class).
+// Launch geometry: forward 256 threads (4 waves, one task each), tasks = B * H * ceil(Tq/64),
+// max_tiles = ceil(max tasks / 4); backward max_tiles = max B * H: SHORT descriptors (Tk <= 64)
+// one wave per (b, h) (ceil(max_tiles / 4) workgroups), LONG ones one workgroup per (b, h).
+// dc_partial (backward) has one float per (b, h, key chunk): index (b*H + h) * ceil(Tk/64) +
+// chunk.  `flags` (MEP_ATTN_*) select the compiled variants: PREV / SOUT (DSN) must hold for every
+// descriptor of the launch; SHORT / LONG say whether descriptors with Tk <= 64 / Tk > 64 are
+// present (one kernel launch per class); backward: MEP_ATTN_DQ_TILES(n) in bits 8.. = the
+// largest ceil(Tq/16) among descriptors with Tk > 64 (LDS for the carried dQ).
 extern "C" int mep_attn_fwd(const mep_attn_desc* descs, int n_desc, int max_tiles, int flags, mep_stream_t stream) {
     if (n_desc <= 0 || max_tiles <= 0) return 0;
     if (!(flags & (MEP_ATTN_SHORT | MEP_ATTN_LONG))) { mep_set_error("mep_attn_fwd: flags need SHORT and/or LONG"); return MEP_EINVAL; }
@@ -483,12 +680,34 @@ extern "C" int mep_attn_fwd(const mep_attn_desc* descs, int n_desc, int max_tile
 extern "C" int mep_attn_bwd(const mep_attn_bwd_desc* descs, int n_desc, int max_tiles, int flags,
                             mep_stream_t stream) {
     if (n_desc <= 0 || max_tiles <= 0) return 0;
+    if (!(flags & (MEP_ATTN_SHORT | MEP_ATTN_LONG))) { mep_set_error("mep_attn_bwd: flags need SHORT and/or LONG"); return MEP_EINVAL; }
     const bool prev = flags & MEP_ATTN_PREV, dsn = flags & MEP_ATTN_SOUT;
-    const dim3 grid(max_tiles, n_desc), block(THREADS);
+    const int dq_tiles = flags >> 8;
+    const size_t lds = sizeof(float) * ((size_t)RED + WAVES + 256 * (size_t)dq_tiles);
+    if (lds > 160 * 1024) { mep_set_error("mep_attn_bwd: Tq too large for the LDS-carried dQ (Tk > 64)"); return MEP_EINVAL; }
     hipStream_t st = (hipStream_t)stream;
-    if (prev) { if (dsn) hipLaunchKernelGGL((k_attn_bwd<true, true>), grid, block, 0, st, descs);
-                else hipLaunchKernelGGL((k_attn_bwd<true, false>), grid, block, 0, st, descs); }
-    else      { if (dsn) hipLaunchKernelGGL((k_attn_bwd<false, true>), grid, block, 0, st, descs);
-                else hipLaunchKernelGGL((k_attn_bwd<false, false>), grid, block, 0, st, descs); }
+    if (flags & MEP_ATTN_SHORT) {
+        const dim3 grid((max_tiles + WAVES - 1) / WAVES, n_desc), block(THREADS);
+#define MEP_BS(P, S) hipLaunchKernelGGL((k_attn_bwd_short<P, S>), grid, block, 0, st, descs)
+        if (prev) { if (dsn) MEP_BS(true, true); else MEP_BS(true, false); }
+        else      { if (dsn) MEP_BS(false, true); else MEP_BS(false, false); }
+#undef MEP_BS
+    }
+    if (flags & MEP_ATTN_LONG) {
+        static bool lds_attr = false;   // allow more than 64 KB of dynamic LDS (long Tq)
+        if (!lds_attr) {
+            const int mx = 160 * 1024;
+            (void)hipFuncSetAttribute((const void*)k_attn_bwd_long<true, true>, hipFuncAttributeMaxDynamicSharedMemorySize, mx);
+            (void)hipFuncSetAttribute((const void*)k_attn_bwd_long<true, false>, hipFuncAttributeMaxDynamicSharedMemorySize, mx);
+            (void)hipFuncSetAttribute((const void*)k_attn_bwd_long<false, true>, hipFuncAttributeMaxDynamicSharedMemorySize, mx);
+            (void)hipFuncSetAttribute((const void*)k_attn_bwd_long<false, false>, hipFuncAttributeMaxDynamicSharedMemorySize, mx);
+            lds_attr = true;
+        }
+        const dim3 grid(max_tiles, n_desc), block(THREADS);
+#define MEP_BL(P, S) hipLaunchKernelGGL((k_attn_bwd_long<P, S>), grid, block, lds, st, descs)
+        if (prev) { if (dsn) MEP_BL(true, true); else MEP_BL(true, false); }
+        else      { if (dsn) MEP_BL(false, true); else MEP_BL(false, false); }
+#undef MEP_BL
+    }
     return mep_check_launch("mep_attn_bwd");
 }

@@ -3,14 +3,16 @@
 Model checkpoints are the reference's own state_dict (same keys, shapes and order;
 cmu-mosei/run.py:415,447); optimizer state is torch.optim.AdamW's state_dict layout.  A resumed
 run (save after k steps, load into fresh objects, continue) must equal the uninterrupted run bit
-for bit: every kernel of the step is deterministic."""
+for bit: every kernel of the step is deterministic -- including the attention backward at
+Tk > 64 (ren_ref: audio Tk = 275, five key chunks), whose dQ is summed over key chunks in a fixed
+order (csrc/attn.hip k_attn_bwd_long)."""
 import io
 
 import pytest
 import torch
 
 from tests.golden import fixtures
-from tests.gpu_util import cmu_model, cuda_batch
+from tests.gpu_util import cmu_model, cuda_batch, ren_model
 
 pytestmark = pytest.mark.gpu
 
@@ -18,15 +20,25 @@ pytestmark = pytest.mark.gpu
 def _engine(meta, cuda):
     from mep_amd.engine import TrainEngine
     from mep_amd.optim import FusedAdamW
-    model = cmu_model(meta, cuda)
+    ren = meta['family'] == 'ren'
+    model = ren_model(meta, cuda) if ren else cmu_model(meta, cuda)
     model.train()
     opt = FusedAdamW(model, lr=1e-3)
-    return model, opt, TrainEngine(model, opt, clip=1.0, graph=True)
+    return model, opt, TrainEngine(model, opt, clip=1.0, rdrop=ren, graph=True)
 
 
-def test_resume_is_bit_exact(cuda):
-    meta, _ = fixtures.load('cmu_small')
-    batch = cuda_batch(meta, cuda)
+def _batch(meta, cuda):
+    if meta['family'] != 'ren':
+        return cuda_batch(meta, cuda)
+    from mep_amd import ren_mme
+    inputs, labels = fixtures.batch(meta)
+    return list(ren_mme._pack([t.to(cuda) for t in inputs])) + [labels.to(cuda)]
+
+
+@pytest.mark.parametrize('name', ['cmu_small', 'ren_ref'])
+def test_resume_is_bit_exact(name, cuda):
+    meta, _ = fixtures.load(name)
+    batch = _batch(meta, cuda)
     model, opt, eng = _engine(meta, cuda)
     for _ in range(3):
         eng.step(*batch)
@@ -46,6 +58,23 @@ def test_resume_is_bit_exact(cuda):
     e3.step(*batch)
     for k, v in m3.state_dict().items():
         assert torch.equal(v, want[k]), k
+
+
+def test_long_attention_backward_is_deterministic(cuda):
+    """Two backward passes of the same Ren-MME step at Tk = 275 give bitwise equal gradients."""
+    meta, _ = fixtures.load('ren_ref')
+    batch = _batch(meta, cuda)
+    model, opt, eng = _engine(meta, cuda)
+    runner = model.mep_runner(cuda)
+    plan = runner.stage(*batch)
+    plan.set_dropout(0.0)
+    grads = []
+    for _ in range(2):
+        plan.forward(grad=True, rdrop=True)
+        plan.backward()
+        torch.cuda.synchronize()
+        grads.append(runner.flat.grad.clone())
+    assert torch.equal(grads[0], grads[1])
 
 
 def test_optimizer_state_is_torch_layout(cuda):
