@@ -4,10 +4,23 @@
 //   xp = drop(x Wp^T);  z = [q | xp] Wm^T;  out = drop(LayerNorm(z))
 // Backward: LayerNorm backward, dq_direct = dz Wm[:, :D], dxp = drop'(dz Wm[:, D:]), dx = dxp Wp.
 // Weight-stationary: a workgroup (8 waves) owns a contiguous range of 16-token tiles of ONE
-// block and keeps that block's weights in LDS; each wave runs whole tiles through all products on
-// exact fp32 MFMA in the transposed-tile formulation (common.h), so activations never pass
-// through LDS and the concat [q | xp] is two accumulating passes.
+// block and keeps that block's weights in LDS; each wave runs whole tiles through all products in
+// the transposed-tile formulation (common.h), so activations never pass through LDS and the
+// concat [q | xp] is two accumulating passes.
+// Arithmetic (D <= 96): fp32 operands split into three bf16 parts on the bf16 matrix cores (split.h:
+// six products per k pair, fp32-level error, 2.7x the fp32-MFMA rate).  The weights are staged in
+// LDS already split, once per workgroup.  The split Wp and Wm together would need 184 KB, so a
+// workgroup runs its tiles in two phases, one weight resident per phase: forward (1) xp = Wp x,
+// stored, (2) z = Wm [q | xp] re-reading its own xp rows (L2-hot) + LayerNorm; backward (1) the
+// LayerNorm backward, dxp and dq with Wm^T, (2) dx = Wp^T dxp.  The first tile of each phase is
+// loaded while the weight of that phase is staged.  D = 128 (Ren-MME) runs the exact fp32 MFMA
+// path (its split Wm alone would need 210 KB of LDS).
 #include "common.h"
+#include "split.h"
+
+#ifndef MEP_EPI_SPLIT
+#define MEP_EPI_SPLIT 1   // D <= 96 on split-bf16 MFMA (0: exact fp32 MFMA everywhere)
+#endif
 
 using namespace mep;
 
@@ -176,12 +189,329 @@ MEP_DEV void epi_fwd_tiles(const mep_epi_desc& d, const AP& wp, const AM& wm, in
     }
 }
 
+// stage W [R][C] (fp32, row stride C) split into LDS: unit (n, p, g) = W[n][32p + 4g ..] and
+// W[n][32p + 16 + 4g ..]; every load of the thread is issued before its first LDS write
+template <int R, int C>
+MEP_DEV void stage_split_rows(const SplitW<R, C / 32>& dst, const gfloat* src) {
+    constexpr int NU = R * (C / 32) * 4;
+    constexpr int PER = (NU + ETHREADS - 1) / ETHREADS;
+    f32x4 v[PER][2];
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+        const int u = threadIdx.x + ETHREADS * k;
+        if (u < NU) {
+            const int g = u & 3, pp = (u >> 2) % (C / 32), n = (u >> 2) / (C / 32);
+            v[k][0] = ld4w(src + n * C + 32 * pp + 4 * g);
+            v[k][1] = ld4w(src + n * C + 32 * pp + 16 + 4 * g);
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+        const int u = threadIdx.x + ETHREADS * k;
+        if (u < NU) {
+            const int g = u & 3, pp = (u >> 2) % (C / 32), n = (u >> 2) / (C / 32);
+            dst.put(n, pp, g, v[k][0], v[k][1]);
+        }
+    }
+}
+
+// stage W^T of W [R][C] (fp32, row stride C) split into LDS (rows = the C columns of W, k = the R
+// rows): unit (n, p, g) = W[32p + 4g + j][n] and W[32p + 16 + 4g + j][n], j < 4; consecutive
+// threads take consecutive n (coalesced), loads issued before the LDS writes
+template <int R, int C>
+MEP_DEV void stage_split_cols(const SplitW<C, R / 32>& dst, const gfloat* src) {
+    constexpr int NP = R / 32, NU = C * NP * 4;
+    constexpr int PER = (NU + ETHREADS - 1) / ETHREADS;
+    float v[PER][8];
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+        const int u = threadIdx.x + ETHREADS * k;
+        if (u < NU) {
+            const int n = u % C, pg = u / C, g = pg & 3, pp = pg >> 2;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                v[k][j] = src[(32 * pp + 4 * g + j) * C + n];
+                v[k][4 + j] = src[(32 * pp + 16 + 4 * g + j) * C + n];
+            }
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+        const int u = threadIdx.x + ETHREADS * k;
+        if (u < NU) {
+            const int n = u % C, pg = u / C, g = pg & 3, pp = pg >> 2;
+            dst.put(n, pp, g, f32x4{v[k][0], v[k][1], v[k][2], v[k][3]}, f32x4{v[k][4], v[k][5], v[k][6], v[k][7]});
+        }
+    }
+}
+
+// ---------------------------------------------------------------- split-bf16 epilogues (D <= 96)
+// this workgroup's global stores done and visible to its own later loads (the next phase re-reads
+// rows the other waves stored)
+MEP_DEV void wg_store_barrier() {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+}
+
+template <int D>
+MEP_DEV void epi_fwd_split(const mep_epi_desc& d, unsigned char* sm, int t_begin, int t_end) {
+    constexpr int NI = D / 16, KB = D / 16, NP = D / 32;
+    using WP = SplitW<D, NP>;
+    using WM = SplitW<D, 2 * NP>;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int c = lane & 15, g = lane >> 4;
+    const int ntok = d.ntok;
+    const float p = d.drop_p;
+    const uint64_t seed = (d.seed && p > 0.f) ? *G<const uint64_t>(d.seed) : 0;
+    gfloat* stats = G<float>(d.stats);
+    typedef __attribute__((address_space(3))) unsigned char lbyte;
+    const WP wp{(lbyte*)sm, 0};
+    const WM wm{(lbyte*)sm, 0};
+    f32x4 ab[KB], bb[KB];            // one tile ahead: phase 1 x rows; phase 2 q and xp rows
+    auto rows_of = [&](const mep_rows& v, int tile, f32x4 (&dst)[KB]) {
+        const gfloat* r = row_ptr(v, min(tile * 16 + c, ntok - 1)) + 4 * g;
+#pragma unroll
+        for (int kb = 0; kb < KB; ++kb) dst[kb] = ld4w(r + 16 * kb);
+    };
+    // ---- phase 1: xp = drop(x Wp^T)
+    if (t_begin + wave < t_end) rows_of(d.x, t_begin + wave, ab);
+    stage_split_rows<D, D>(wp, G<const float>(d.wp));
+    __syncthreads();
+    for (int tile = t_begin + wave; tile < t_end; tile += EWAVES) {
+        const int tok = tile * 16 + c;
+        Op3 xs[NP];
+#pragma unroll
+        for (int pp = 0; pp < NP; ++pp) xs[pp] = op3(ab[2 * pp], ab[2 * pp + 1]);
+        if (tile + EWAVES < t_end) rows_of(d.x, tile + EWAVES, ab);
+        f32x4 xp[NI];
+#pragma unroll
+        for (int i = 0; i < NI; ++i) xp[i] = zero_f4();
+        tgemm6<NI, NP>(xp, [&](int i, int pp) { return wp.frag(i, pp); }, [&](int pp) { return xs[pp]; });
+        if (tok < ntok) {
+            gfloat* pr = row_ptr(d.xp, tok);
+#pragma unroll
+            for (int i = 0; i < NI; ++i) {
+                if (p > 0.f) {
+#pragma unroll
+                    for (int r = 0; r < 4; ++r)
+                        xp[i][r] *= drop_scale(seed, 2u * d.drop_stream, (uint64_t)tok * D + 16 * i + 4 * g + r, p);
+                }
+                stg4(pr + 16 * i + 4 * g, f4(xp[i]));
+            }
+        }
+    }
+    // ---- phase 2: z = [q | xp] Wm^T, out = drop(LayerNorm(z))
+    if (t_begin + wave < t_end) rows_of(d.q, t_begin + wave, ab);
+    wg_store_barrier();              // xp rows stored; Wp no longer read
+    if (t_begin + wave < t_end) rows_of(d.xp, t_begin + wave, bb);
+    stage_split_rows<D, 2 * D>(wm, G<const float>(d.wm));
+    __syncthreads();
+    for (int tile = t_begin + wave; tile < t_end; tile += EWAVES) {
+        const int tok = tile * 16 + c;
+        Op3 qs[NP], ps[NP];
+#pragma unroll
+        for (int pp = 0; pp < NP; ++pp) { qs[pp] = op3(ab[2 * pp], ab[2 * pp + 1]); ps[pp] = op3(bb[2 * pp], bb[2 * pp + 1]); }
+        if (tile + EWAVES < t_end) { rows_of(d.q, tile + EWAVES, ab); rows_of(d.xp, tile + EWAVES, bb); }
+        f32x4 z[NI];
+#pragma unroll
+        for (int i = 0; i < NI; ++i) z[i] = zero_f4();
+        tgemm6<NI, NP>(z, [&](int i, int pp) { return wm.frag(i, pp); }, [&](int pp) { return qs[pp]; });
+        tgemm6<NI, NP>(z, [&](int i, int pp) { return wm.frag(i, NP + pp); }, [&](int pp) { return ps[pp]; });
+        float sum = 0.f;
+#pragma unroll
+        for (int i = 0; i < NI; ++i) sum += (z[i][0] + z[i][1]) + (z[i][2] + z[i][3]);
+        sum += __shfl_xor(sum, 16, 64);
+        sum += __shfl_xor(sum, 32, 64);
+        const float mean = sum / (float)D;
+        float var = 0.f;
+#pragma unroll
+        for (int i = 0; i < NI; ++i)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) { const float t = z[i][r] - mean; var += t * t; }
+        var += __shfl_xor(var, 16, 64);
+        var += __shfl_xor(var, 32, 64);
+        const float rstd = 1.0f / sqrtf(var / (float)D + LN_EPS);
+        if (tok < ntok) {
+            gfloat* zr = row_ptr(d.z, tok);
+            gfloat* orow = row_ptr(d.out, tok);
+#pragma unroll
+            for (int i = 0; i < NI; ++i) {
+                const int col = 16 * i + 4 * g;
+                const f32x4 w = ld4w(G<const float>(d.ln_w) + col), b = ld4w(G<const float>(d.ln_b) + col);
+                f32x4 y;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    y[r] = (z[i][r] - mean) * rstd * w[r] + b[r];
+                    if (p > 0.f) y[r] *= drop_scale(seed, 2u * d.drop_stream + 1u, (uint64_t)tok * D + col + r, p);
+                }
+                stg4(zr + col, f4(z[i]));
+                stg4(orow + col, f4(y));
+            }
+            if (g == 0) { stats[2 * tok] = mean; stats[2 * tok + 1] = rstd; }
+        }
+    }
+}
+
+template <int D>
+MEP_DEV void epi_bwd_split(const mep_epi_bwd_desc& bd, unsigned char* sm, int t_begin, int t_end) {
+    constexpr int NI = D / 16, KB = D / 16, NP = D / 32;
+    using WMT = SplitW<2 * D, NP>;
+    using WPT = SplitW<D, NP>;
+    const mep_epi_desc& d = bd.f;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int c = lane & 15, g = lane >> 4;
+    const int ntok = d.ntok;
+    const float p = d.drop_p;
+    const uint64_t seed = (d.seed && p > 0.f) ? *G<const uint64_t>(d.seed) : 0;
+    const gfloat* stats = G<const float>(d.stats);
+    gfloat* lpart = G<float>(bd.ln_partial);
+    typedef __attribute__((address_space(3))) unsigned char lbyte;
+    const WMT wmt{(lbyte*)sm, 0};
+    const WMT wmt_x{(lbyte*)sm, D};
+    const WPT wpt{(lbyte*)sm, 0};
+    f32x4 ga[KB], zb[KB];            // one tile ahead: dout (+ dout2) and z rows
+    float mean = 0.f, rstd = 0.f;
+    auto fetch1 = [&](int tile) {
+        const int tc = min(tile * 16 + c, ntok - 1);
+        const gfloat* gr = row_ptr(bd.dout, tc) + 4 * g;
+        const gfloat* zr = row_ptr(d.z, tc) + 4 * g;
+#pragma unroll
+        for (int kb = 0; kb < KB; ++kb) ga[kb] = ld4w(gr + 16 * kb);
+#pragma unroll
+        for (int kb = 0; kb < KB; ++kb) zb[kb] = ld4w(zr + 16 * kb);
+        mean = stats[2 * tc];
+        rstd = stats[2 * tc + 1];
+    };
+    // ---- phase 1: LayerNorm backward, dxp = drop'(dz Wm[:, D:]), dq (+)= dz Wm[:, :D]
+    if (t_begin + wave < t_end) fetch1(t_begin + wave);
+    stage_split_cols<D, 2 * D>(wmt, G<const float>(d.wm));
+    __syncthreads();
+    for (int tile = t_begin + wave; tile < t_end; tile += EWAVES) {
+        const int tok = tile * 16 + c;
+        const bool ok = tok < ntok;
+        const int tc = min(tok, ntok - 1);
+        f32x4 dz[NI], zz[NI];
+        const float mu = mean, rs = rstd;
+#pragma unroll
+        for (int i = 0; i < NI; ++i) { dz[i] = ga[i]; zz[i] = zb[i]; }
+        if (bd.dout2.ptr) {
+            const gfloat* g2 = row_ptr(bd.dout2, tc) + 4 * g;
+#pragma unroll
+            for (int i = 0; i < NI; ++i) dz[i] += ld4w(g2 + 16 * i);
+        }
+        if (tile + EWAVES < t_end) fetch1(tile + EWAVES);
+        float s1 = 0.f, s2 = 0.f;
+        gfloat* lp = lpart ? lpart + (int64_t)tile * 2 * D : nullptr;
+#pragma unroll
+        for (int i = 0; i < NI; ++i) {
+            const int col = 16 * i + 4 * g;
+            const f32x4 w = ld4w(G<const float>(d.ln_w) + col);
+            f32x4 pw, pb;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                float gg = dz[i][r];
+                if (p > 0.f) gg *= drop_scale(seed, 2u * d.drop_stream + 1u, (uint64_t)tok * D + col + r, p);
+                gg = ok ? gg : 0.f;
+                const float x = (zz[i][r] - mu) * rs;
+                const float gw = gg * w[r];
+                s1 += gw;
+                s2 += gw * x;
+                pw[r] = row16_sum(gg * x);
+                pb[r] = row16_sum(gg);
+                dz[i][r] = gw;
+            }
+            if (lp && c == 0) {
+                stg4(lp + col, f4(pw));
+                stg4(lp + D + col, f4(pb));
+            }
+        }
+        s1 += __shfl_xor(s1, 16, 64);
+        s1 += __shfl_xor(s1, 32, 64);
+        s2 += __shfl_xor(s2, 16, 64);
+        s2 += __shfl_xor(s2, 32, 64);
+        s1 /= (float)D;
+        s2 /= (float)D;
+#pragma unroll
+        for (int i = 0; i < NI; ++i)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const float x = (zz[i][r] - mu) * rs;
+                dz[i][r] = ok ? rs * (dz[i][r] - s1 - x * s2) : 0.f;
+            }
+        Op3 dzb[NP];
+#pragma unroll
+        for (int pp = 0; pp < NP; ++pp) dzb[pp] = op3(dz[2 * pp], dz[2 * pp + 1]);
+        f32x4 acc[NI];
+#pragma unroll
+        for (int i = 0; i < NI; ++i) acc[i] = zero_f4();
+        tgemm6<NI, NP>(acc, [&](int i, int pp) { return wmt_x.frag(i, pp); }, [&](int pp) { return dzb[pp]; });
+        if (ok) {
+            gfloat* dzr = row_ptr(bd.dz, tok);
+            gfloat* dpr = row_ptr(bd.dxp, tok);
+#pragma unroll
+            for (int i = 0; i < NI; ++i) {
+                if (p > 0.f) {
+#pragma unroll
+                    for (int r = 0; r < 4; ++r)
+                        acc[i][r] *= drop_scale(seed, 2u * d.drop_stream, (uint64_t)tok * D + 16 * i + 4 * g + r, p);
+                }
+                stg4(dzr + 16 * i + 4 * g, f4(dz[i]));
+                stg4(dpr + 16 * i + 4 * g, f4(acc[i]));
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < NI; ++i) acc[i] = zero_f4();
+        tgemm6<NI, NP>(acc, [&](int i, int pp) { return wmt.frag(i, pp); }, [&](int pp) { return dzb[pp]; });
+        if (ok) {
+            gfloat* qrw = row_ptr(bd.dq, tok);
+#pragma unroll
+            for (int i = 0; i < NI; ++i) {
+                f32x4 v = acc[i];
+                if (bd.dq_accumulate) v += ld4w(qrw + 16 * i + 4 * g);
+                stg4(qrw + 16 * i + 4 * g, f4(v));
+            }
+        }
+    }
+    // ---- phase 2: dx = dxp Wp (this workgroup's own dxp rows, L2-hot)
+    wg_store_barrier();
+    auto fetch2 = [&](int tile) {
+        const gfloat* r = row_ptr(bd.dxp, min(tile * 16 + c, ntok - 1)) + 4 * g;
+#pragma unroll
+        for (int kb = 0; kb < KB; ++kb) ga[kb] = ld4w(r + 16 * kb);
+    };
+    if (t_begin + wave < t_end) fetch2(t_begin + wave);
+    stage_split_cols<D, D>(wpt, G<const float>(d.wp));
+    __syncthreads();
+    for (int tile = t_begin + wave; tile < t_end; tile += EWAVES) {
+        const int tok = tile * 16 + c;
+        Op3 xs[NP];
+#pragma unroll
+        for (int pp = 0; pp < NP; ++pp) xs[pp] = op3(ga[2 * pp], ga[2 * pp + 1]);
+        if (tile + EWAVES < t_end) fetch2(tile + EWAVES);
+        f32x4 acc[NI];
+#pragma unroll
+        for (int i = 0; i < NI; ++i) acc[i] = zero_f4();
+        tgemm6<NI, NP>(acc, [&](int i, int pp) { return wpt.frag(i, pp); }, [&](int pp) { return xs[pp]; });
+        if (tok < ntok) {
+            gfloat* xrw = row_ptr(bd.dx, tok);
+#pragma unroll
+            for (int i = 0; i < NI; ++i) stg4(xrw + 16 * i + 4 * g, f4(acc[i]));
+        }
+    }
+}
+
 template <int D>
 __global__ __launch_bounds__(ETHREADS) void k_epi_fwd(const mep_epi_desc* __restrict__ descs) {
     using Geo = EpiGeo<D>;
     const mep_epi_desc& d = descs[blockIdx.y];
     int t_begin, t_end;
     if (!tile_range(d.ntok, t_begin, t_end)) return;   // whole workgroup
+    if constexpr (MEP_EPI_SPLIT && D <= 96) {
+        constexpr int BYTES = SplitW<D, D / 16>::BYTES;   // the larger phase (Wm)
+        __shared__ __attribute__((aligned(16))) unsigned char sm6[BYTES];
+        epi_fwd_split<D>(d, sm6, t_begin, t_end);
+        return;
+    }
     __shared__ __attribute__((aligned(16))) float smem[Geo::FWD];
     lfloat* wm = (lfloat*)&smem[0];
     stage_rows<D, 2 * D>(wm, Geo::LM, G<const float>(d.wm));
@@ -328,6 +658,12 @@ __global__ __launch_bounds__(ETHREADS) void k_epi_bwd(const mep_epi_bwd_desc* __
     const mep_epi_desc& d = bd.f;
     int t_begin, t_end;
     if (!tile_range(d.ntok, t_begin, t_end)) return;
+    if constexpr (MEP_EPI_SPLIT && D <= 96) {
+        constexpr int BYTES = SplitW<2 * D, D / 32>::BYTES;   // the larger phase (Wm^T)
+        __shared__ __attribute__((aligned(16))) unsigned char sm6[BYTES];
+        epi_bwd_split<D>(bd, sm6, t_begin, t_end);
+        return;
+    }
     __shared__ __attribute__((aligned(16))) float smem[Geo::BWD];
     lfloat* wmt = (lfloat*)&smem[0];              // Wm^T [2D][LP]
     stage_cols_t<D, 2 * D>(wmt, Geo::LP, G<const float>(d.wm));
