@@ -319,8 +319,10 @@ typedef struct {
     int32_t  labels_are_float;
     int32_t  rdrop;              /* Ren-MME R-Drop pairs (2i, 2i+1)     */
     int32_t  compute_grad;
-    float    loss_scale;         /* d(total loss)/d(row loss) = 1/B     */
-    int32_t  _pad;
+    float    loss_scale;         /* d(total loss)/d(row loss) = 1/B (1/B_global under data
+                                    parallelism: the rank's share of the global-batch mean) */
+    int32_t  rdrop_pairs;        /* R-Drop KL batchmean divisor (pairs of the global batch
+                                    under data parallelism); 0 = B / 2                */
     uint64_t ext_dlogits;        /* [B, NC] upstream grad of the logits; when set the fused
                                     loss is skipped and this gradient is back-propagated */
 } mep_head_desc;

@@ -166,37 +166,68 @@ class DeviceBatch(tuple):
     it as it is (no zip / np.stack / H2D copy)."""
 
 
+def _device_loader(chunks, build, store, prefetch):
+    """Yield build(chunk) for each chunk as DeviceBatch (None -> an empty dp.HostShard), with
+    chunk i+1 assembled on a side stream while the caller's step on chunk i runs."""
+    from . import dp
+    main = torch.cuda.current_stream(store.device)
+    side = torch.cuda.Stream(store.device) if prefetch else main
+
+    def launch(chunk):
+        units, global_rows = chunk
+        if not units:
+            return None, None, global_rows
+        side.wait_stream(main)          # buffers recycled from the caller's stream are free
+        with torch.cuda.stream(side):
+            out = build(units)
+            ev = torch.cuda.Event()
+            ev.record(side)
+        return out, ev, global_rows
+
+    nxt = launch(chunks[0]) if chunks else None
+    for i in range(len(chunks)):
+        out, ev, global_rows = nxt
+        if i + 1 < len(chunks):
+            nxt = launch(chunks[i + 1])
+        if out is None:
+            yield dp.HostShard([], global_rows)
+            continue
+        main.wait_event(ev)
+        if side is not main:
+            for t in out:
+                t.record_stream(main)
+        b = DeviceBatch(out)
+        b.global_rows = global_rows
+        yield b
+
+
+def _cmu_rows(store, pairs, lens):
+    """Batch rows of (previous, current) pairs: two when the current text has two windows."""
+    ids = store.ids('linguistic', [c for _, c in pairs])
+    L = np.where(ids >= 0, store.mods['linguistic']['lens'][np.maximum(ids, 0)], 0)
+    return int(len(pairs) + (L >= lens[0] - 3).sum())
+
+
 def cmu_data_loader(store, lens, prefetch=True):
     """-> ``data_loader(name_list, label_dict, batch_size)`` with the signature and row order of
     cmu-mosei/run.py:154-198 (``random.shuffle`` of ``name_list`` in place, batches of
     ``batch_size`` (previous, current) pairs), yielding DeviceBatch.  With ``prefetch`` batch i+1 is
-    assembled on a side stream while the caller's step on batch i runs on the current stream."""
-    import random
+    assembled on a side stream while the caller's step on batch i runs on the current stream.
+    Under data parallelism (mep_amd.dp) ``batch_size`` is per rank: global batch k holds pairs
+    [k B W, (k+1) B W) of rank 0's shuffled order, rank r assembles pairs [r B, (r+1) B) of it and
+    each DeviceBatch carries ``global_rows`` (rows of the whole global batch) for the loss scale."""
+    from . import dp
 
     def data_loader(name_list, label_dict, batch_size):
-        random.shuffle(name_list)
-        chunks = [name_list[i:i + batch_size] for i in range(0, len(name_list), batch_size)]
-        main = torch.cuda.current_stream(store.device)
-        side = torch.cuda.Stream(store.device) if prefetch else main
-
-        def build(pairs):
-            side.wait_stream(main)          # buffers recycled from the caller's stream are free
-            with torch.cuda.stream(side):
-                out = cmu_batch(store, pairs, label_dict, lens)
-                ev = torch.cuda.Event()
-                ev.record(side)
-            return out, ev
-
-        nxt = build(chunks[0]) if chunks else None
-        for i in range(len(chunks)):
-            out, ev = nxt
-            if i + 1 < len(chunks):
-                nxt = build(chunks[i + 1])
-            main.wait_event(ev)
-            if side is not main:
-                for t in out:
-                    t.record_stream(main)
-            yield DeviceBatch(out)
+        dp.shared_shuffle(name_list)
+        w = dp.world()
+        step = batch_size * w
+        chunks = []
+        for i in range(0, len(name_list), step):
+            g = name_list[i:i + step]
+            lo, hi = dp.rank_range(len(g), batch_size)
+            chunks.append((g[lo:hi], _cmu_rows(store, g, lens) if w > 1 else None))
+        return _device_loader(chunks, lambda pairs: cmu_batch(store, pairs, label_dict, lens), store, prefetch)
 
     return data_loader
 
@@ -206,32 +237,19 @@ def rf_data_loader(store, labels, lens, prefetch=True):
     others/realformer.py:94-125 (``random.shuffle`` in place; ``data_set`` is not read -- the
     sequences live in ``store``, the label rows in ``labels[name]``), yielding DeviceBatch of
     (l, v, a, label, l_mask, v_mask, a_mask, mask); batch i+1 is assembled on a side stream
-    while the caller's step on batch i runs."""
-    import random
+    while the caller's step on batch i runs.  Under data parallelism ``batch_size`` groups per
+    rank, sharded as cmu_data_loader shards pairs."""
+    from . import dp
 
     def data_loader(data_set, name_list, batch_size):
-        random.shuffle(name_list)
-        chunks = [name_list[i:i + batch_size] for i in range(0, len(name_list), batch_size)]
-        main = torch.cuda.current_stream(store.device)
-        side = torch.cuda.Stream(store.device) if prefetch else main
-
-        def build(lists):
-            side.wait_stream(main)
-            with torch.cuda.stream(side):
-                out = rf_batch(store, lists, labels, lens)
-                ev = torch.cuda.Event()
-                ev.record(side)
-            return out, ev
-
-        nxt = build(chunks[0]) if chunks else None
-        for i in range(len(chunks)):
-            out, ev = nxt
-            if i + 1 < len(chunks):
-                nxt = build(chunks[i + 1])
-            main.wait_event(ev)
-            if side is not main:
-                for t in out:
-                    t.record_stream(main)
-            yield DeviceBatch(out)
+        dp.shared_shuffle(name_list)
+        w = dp.world()
+        step = batch_size * w
+        chunks = []
+        for i in range(0, len(name_list), step):
+            g = name_list[i:i + step]
+            lo, hi = dp.rank_range(len(g), batch_size)
+            chunks.append((g[lo:hi], len(g) if w > 1 else None))
+        return _device_loader(chunks, lambda lists: rf_batch(store, lists, labels, lens), store, prefetch)
 
     return data_loader

@@ -154,17 +154,27 @@ def _to_device(batch, device):
 def train(model, iterator, optimizer, device='cuda'):
     """One epoch (cmu-mosei/run.py:354-372).  With an ``mep_amd.optim.FusedAdamW`` optimizer the
     whole step (forward, loss, backward, clip, AdamW) runs as the fused engine; with any other
-    optimizer it follows the reference statement by statement through autograd."""
+    optimizer it follows the reference statement by statement through autograd.  Under data
+    parallelism (mep_amd.dp) the batches are this rank's shares of the global batches and the
+    returned epoch loss is the global one, identical on every rank."""
+    from . import dp
     from .engine import LossSum, engine_for
     from .optim import FusedAdamW
     model.train()
-    acc, count = LossSum(), 0
+    acc, count, sharded = LossSum(), 0, False
     engine = engine_for(model, optimizer, clip=CLIP) if isinstance(optimizer, FusedAdamW) else None
+    if engine is None and dp.world() > 1:
+        raise ValueError('data-parallel training runs on the fused engine (FusedAdamW)')
     for batch in iterator:
         count += 1
+        gr = dp.global_rows_of(batch)
+        sharded = sharded or gr is not None
+        if engine is not None and len(batch) == 0:      # empty share of a ragged global batch
+            acc.add(engine.step_empty(device))
+            continue
         l, v, a, lm, vm, am, label = _to_device(batch, device)
         if engine is not None:
-            loss = engine.step(l, v, a, lm, vm, am, label)
+            loss = engine.step(l, v, a, lm, vm, am, label, global_rows=gr)
         else:
             optimizer.zero_grad()
             logits = model(l, v, a, lm, vm, am)
@@ -173,20 +183,28 @@ def train(model, iterator, optimizer, device='cuda'):
             nn.utils.clip_grad_norm_(model.parameters(), CLIP)
             optimizer.step()
         acc.add(loss)
-    return acc.value() / count
+    return dp.epoch_mean(acc.value(), count, sharded, device)
 
 
 def valid(model, iterator, device='cuda'):
-    """cmu-mosei/run.py:375-390 -> (sum of batch losses, batches, mean)."""
+    """cmu-mosei/run.py:375-390 -> (sum of batch losses, batches, mean); global under data
+    parallelism (each rank adds its share of every global batch's mean)."""
+    from . import dp
     model.eval()
-    epoch_loss, count = 0.0, 0
+    epoch_loss, count, sharded = 0.0, 0, False
     with torch.no_grad():
         for batch in iterator:
             count += 1
+            gr = dp.global_rows_of(batch)
+            sharded = sharded or gr is not None
+            if len(batch) == 0:
+                continue
             l, v, a, lm, vm, am, label = _to_device(batch, device)
             logits = model(l, v, a, lm, vm, am)
-            epoch_loss += float(multi_circle_loss(logits, label).mean().item())
-    return epoch_loss, count, epoch_loss / count
+            rl = multi_circle_loss(logits, label)
+            epoch_loss += float((rl.sum() / gr if gr is not None and dp.world() > 1 else rl.mean()).item())
+    mean = dp.epoch_mean(epoch_loss, count, sharded, device)
+    return mean * count, count, mean
 
 
 def run(model, train_list, valid_list, label_dict, batch_size, learning_rate, epochs, log_name,
@@ -199,23 +217,28 @@ def run(model, train_list, valid_list, label_dict, batch_size, learning_rate, ep
     from .optim import FusedAdamW
     if data_loader is None:
         raise ValueError('run() needs the data_loader generator of the caller')
+    from . import dp
+    lead = dp.rank() == 0                   # data parallelism: one log / checkpoint writer
     log_file = os.path.join(log_dir, log_name + '.txt')
-    with open(log_file, 'w') as f:
-        f.write('epoch, train_loss, valid_loss\n')
+    if lead:
+        with open(log_file, 'w') as f:
+            f.write('epoch, train_loss, valid_loss\n')
     optimizer = FusedAdamW(model, lr=learning_rate)
     scheduler = ReduceLROnPlateau(optimizer, factor=0.1, patience=4)
     stop, losses = 0, []
     for epoch in range(epochs):
         train_loss = train(model, data_loader(train_list, label_dict, batch_size), optimizer, device)
         _, _, valid_loss = valid(model, data_loader(valid_list, label_dict, batch_size), device)
-        scheduler.step(valid_loss)
+        scheduler.step(valid_loss)           # the same global valid loss on every rank
         losses.append(valid_loss)
-        with open(log_file, 'a') as f:
-            f.write('\n{epoch},{train_loss: 2.2f},{valid_loss: 2.2f}\n'.format(
-                epoch=epoch + 1, train_loss=train_loss, valid_loss=valid_loss))
+        if lead:
+            with open(log_file, 'a') as f:
+                f.write('\n{epoch},{train_loss: 2.2f},{valid_loss: 2.2f}\n'.format(
+                    epoch=epoch + 1, train_loss=train_loss, valid_loss=valid_loss))
         if valid_loss == min(losses) and valid_loss > 0.009:
             stop = 0
-            torch.save(model.state_dict(), os.path.join(log_dir, log_name + '_' + str(valid_loss)[:4] + '.pt'))
+            if lead:
+                torch.save(model.state_dict(), os.path.join(log_dir, log_name + '_' + str(valid_loss)[:4] + '.pt'))
         else:
             stop += 1
             if stop >= 9:

@@ -325,7 +325,7 @@ __global__ __launch_bounds__(256) void k_head(mep_head_desc d) {
             if (lane == 0) row_loss[b] = (ln + lp) * d.loss_scale;
         }
         if (d.rdrop && !ext) {
-            const float R = (float)(d.B / 2);
+            const float R = (float)(d.rdrop_pairs > 0 ? d.rdrop_pairs : d.B / 2);   // global pairs under DP
             const bool ok = lane < NC;
             const float pv = ok ? s_logit[0][lane] : 0.f, qv = ok ? s_logit[1][lane] : 0.f;
             const float sp = 1.f / (1.f + __expf(-pv)), sq = 1.f / (1.f + __expf(-qv));

@@ -3,10 +3,17 @@ as a fixed launch sequence, captured once per input shape into a hipGraph and re
 
 Data parallelism (one process per GPU, torch.distributed backend "nccl" = RCCL over xGMI): each
 rank runs the step on its own rows; the flat fp32 gradient buffer (2.35 MB for Concat_Trans)
-is all-reduced (SUM) between the backward graph and the optimizer graph, and the optimizer
-graph divides by the world size before clipping, so every rank applies the identical update of
-the global-batch mean (clip after the reduce = 1-GPU large-batch semantics).
-Ren-MME R-Drop pairs are whole rows of the local batch, so they never straddle ranks.
+is all-reduced (SUM) between the backward graph and the optimizer graph, and the optimizer clips
+after the reduce, so every rank applies the identical update of the global-batch mean (1-GPU
+large-batch semantics).  Two scalings give that mean:
+  * global_rows given (a sharded batch, mep_amd.dp): the rank's loss is scaled by 1/B_global in
+    the head kernel and the optimizer sees the plain SUM -- exact for unequal or empty shares;
+  * global_rows None (every rank holds an equal share, e.g. bench.py): the local mean 1/B and
+    grad_scale 1/world in the optimizer.
+Ren-MME R-Drop pairs are whole units of a shard (mep_amd.dp), so they never straddle ranks.
+All weight gradients materialise in the backward's last two launches (one grouped weight-
+gradient GEMM and one reduction), so there is no earlier gradient bucket an all-reduce could
+overlap with; the 2.35 MB SUM runs between the two graph replays.
 """
 import torch
 import torch.distributed as dist
@@ -46,15 +53,18 @@ class TrainEngine:
             dist.broadcast(runner.flat.buf, 0, group=self.pg)
             self._initial_broadcast = False
 
-    def step_plan(self, plan):
-        """Run one training step on the data already in ``plan``'s input buffers; returns the
-        (local-batch) loss as a device tensor."""
+    def step_plan(self, plan, global_rows=None):
+        """Run one training step on the data already in ``plan``'s input buffers; returns the loss
+        as a device tensor (the local-batch mean, or with ``global_rows`` this rank's share of
+        the global-batch mean)."""
         runner = self._runner(plan.device)
+        sharded = self.world > 1 and global_rows is not None
         self.opt._bind()
-        self.opt._sync_hyper(self.clip, 1.0 / self.world)
+        self.opt._sync_hyper(self.clip, 1.0 if sharded else 1.0 / self.world)
         plan.set_dropout(runner.drop_p())
+        scale_key = plan.set_global_rows(global_rows if sharded else None)
         self._sync_params(runner)
-        key = id(plan)
+        key = (id(plan), scale_key)
         g = self._graphs.get(key)
         if not self.graph:
             self._fwd_bwd(plan)
@@ -88,13 +98,25 @@ class TrainEngine:
         if self.world > 1:
             dist.all_reduce(runner.flat.grad, op=dist.ReduceOp.SUM, group=self.pg)
 
-    def step(self, *batch):
+    def step(self, *batch, global_rows=None):
         """Reference-shaped batch in, loss out: the runner copies the batch into the resident
         buffers of the plan for its shape (cmu-mosei / Ren-MME: l, v, a, l_mask, v_mask, a_mask,
         labels; realformer: ... , labels, utterance mask)."""
         first = batch[0][0] if isinstance(batch[0], (tuple, list)) else batch[0]
         plan = self._runner(first.device).stage(*batch)
-        return self.step_plan(plan)
+        return self.step_plan(plan, global_rows)
+
+    def step_empty(self, device):
+        """A rank whose share of the (ragged, last) global batch is empty: zero gradient into the
+        all-reduce, then the same optimizer step as every other rank."""
+        runner = self._runner(torch.device(device))
+        self.opt._bind()
+        self.opt._sync_hyper(self.clip, 1.0)
+        self._sync_params(runner)
+        runner.flat.grad.zero_()
+        self._allreduce(runner)
+        self._opt()
+        return torch.zeros(1, device=runner.flat.buf.device)
 
 
 def engine_for(model, optimizer, **kw):

@@ -206,17 +206,26 @@ def _to_device(batch, device):
 
 def train(model, iterator, optimizer, device='cuda'):
     """One epoch (realformer.py:300-318).  With ``mep_amd.optim.FusedAdam`` the step (forward,
-    masked circle loss, backward, clip, Adam) is the fused graph-captured engine."""
+    masked circle loss, backward, clip, Adam) is the fused graph-captured engine.  Under data
+    parallelism (mep_amd.dp) the batches are this rank's shares of the global batches."""
+    from . import dp
     from .engine import LossSum, engine_for
     from .optim import FusedAdamW
     model.train()
-    acc, count = LossSum(), 0
+    acc, count, sharded = LossSum(), 0, False
     engine = engine_for(model, optimizer, clip=CLIP) if isinstance(optimizer, FusedAdamW) else None
+    if engine is None and dp.world() > 1:
+        raise ValueError('data-parallel training runs on the fused engine (FusedAdam)')
     for batch in iterator:
         count += 1
+        gr = dp.global_rows_of(batch)
+        sharded = sharded or gr is not None
+        if engine is not None and len(batch) == 0:
+            acc.add(engine.step_empty(device))
+            continue
         l, v, a, label, lm, vm, am, mask = _to_device(batch, device)
         if engine is not None:
-            loss = engine.step(l, v, a, label, lm, vm, am, mask)
+            loss = engine.step(l, v, a, label, lm, vm, am, mask, global_rows=gr)
         else:
             optimizer.zero_grad()
             logits = model(l, v, a, lm, vm, am)
@@ -225,20 +234,31 @@ def train(model, iterator, optimizer, device='cuda'):
             nn.utils.clip_grad_norm_(model.parameters(), CLIP)
             optimizer.step()
         acc.add(loss)
-    return acc.value() / count
+    return dp.epoch_mean(acc.value(), count, sharded, device)
 
 
 def valid(model, iterator, device='cuda'):
-    """realformer.py:320-334 -> (sum of batch losses, batches, mean)."""
+    """realformer.py:320-334 -> (sum of batch losses, batches, mean); global under data
+    parallelism."""
+    from . import dp
     model.eval()
-    epoch_loss, count = 0.0, 0
+    epoch_loss, count, sharded = 0.0, 0, False
     with torch.no_grad():
         for batch in iterator:
             count += 1
+            gr = dp.global_rows_of(batch)
+            sharded = sharded or gr is not None
+            if len(batch) == 0:
+                continue
             l, v, a, label, lm, vm, am, mask = _to_device(batch, device)
             logits = model(l, v, a, lm, vm, am)
-            epoch_loss += float((multi_circle_loss(logits, label) * mask).mean().item())
-    return epoch_loss, count, epoch_loss / count
+            masked = multi_circle_loss(logits, label) * mask
+            if gr is not None and dp.world() > 1:
+                epoch_loss += float((masked.sum() / (gr * masked.shape[1])).item())
+            else:
+                epoch_loss += float(masked.mean().item())
+    mean = dp.epoch_mean(epoch_loss, count, sharded, device)
+    return mean * count, count, mean
 
 
 def run(model, data_set, train_list, valid_list, batch_size, learning_rate, epochs, name, data_loader=None,
@@ -250,9 +270,12 @@ def run(model, data_set, train_list, valid_list, batch_size, learning_rate, epoc
     from .optim import FusedAdam
     if data_loader is None:
         raise ValueError('run() needs the data_loader generator of the caller')
+    from . import dp
+    lead = dp.rank() == 0
     log_file = os.path.join(log_dir, name + '.txt')
-    with open(log_file, 'w') as f:
-        f.write('epoch, train_loss, valid_loss\n')
+    if lead:
+        with open(log_file, 'w') as f:
+            f.write('epoch, train_loss, valid_loss\n')
     optimizer = FusedAdam(model, lr=learning_rate)
     scheduler = ReduceLROnPlateau(optimizer, factor=0.1, patience=2)
     stop, losses = 0, []
@@ -261,12 +284,14 @@ def run(model, data_set, train_list, valid_list, batch_size, learning_rate, epoc
         _, _, valid_loss = valid(model, data_loader(data_set, valid_list, batch_size), device)
         scheduler.step(valid_loss)
         losses.append(valid_loss)
-        with open(log_file, 'a') as f:
-            f.write('\n{epoch},{train_loss: 2.2f},{valid_loss: 2.2f}\n'.format(
-                epoch=epoch + 1, train_loss=train_loss, valid_loss=valid_loss))
+        if lead:
+            with open(log_file, 'a') as f:
+                f.write('\n{epoch},{train_loss: 2.2f},{valid_loss: 2.2f}\n'.format(
+                    epoch=epoch + 1, train_loss=train_loss, valid_loss=valid_loss))
         if valid_loss == min(losses):
             stop = 0
-            torch.save(model.state_dict(), os.path.join(log_dir, name + '_' + str(valid_loss)[:4] + '.pt'))
+            if lead:
+                torch.save(model.state_dict(), os.path.join(log_dir, name + '_' + str(valid_loss)[:4] + '.pt'))
         else:
             stop += 1
             if stop >= 4:

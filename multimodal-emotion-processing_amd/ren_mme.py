@@ -169,19 +169,28 @@ def _to_device(batch, device):
 def train(model, iterator, optimizer, device='cuda'):
     """One epoch (Ren-MME/run.py:307-340).  With ``mep_amd.optim.FusedAdamW`` the step (forward,
     circle loss + R-Drop KL, backward, clip, AdamW) is the fused graph-captured engine; with any
-    other optimizer it follows the reference statement by statement through autograd."""
+    other optimizer it follows the reference statement by statement through autograd.  Under data
+    parallelism the batches are pair-preserving shares (``dp.shard_batches(loader, unit=2)``)."""
+    from . import dp
     from .engine import LossSum, engine_for
     from .optim import FusedAdamW
     model.train()
-    acc, count = LossSum(), 0
+    acc, count, sharded = LossSum(), 0, False
     engine = engine_for(model, optimizer, clip=CLIP, rdrop=True) if isinstance(optimizer, FusedAdamW) else None
+    if engine is None and dp.world() > 1:
+        raise ValueError('data-parallel training runs on the fused engine (FusedAdamW)')
     for batch in iterator:
         count += 1
+        gr = dp.global_rows_of(batch)
+        sharded = sharded or gr is not None
+        if engine is not None and len(batch) == 0:
+            acc.add(engine.step_empty(device))
+            continue
         cols = _to_device(batch, device)
         args, label = cols[:12], cols[12]
         if engine is not None:
             l, v, a, lm, vm, am = _pack(args)
-            loss = engine.step(l, v, a, lm, vm, am, label)
+            loss = engine.step(l, v, a, lm, vm, am, label, global_rows=gr)
         else:
             optimizer.zero_grad()
             logits = model(*args)
@@ -190,20 +199,29 @@ def train(model, iterator, optimizer, device='cuda'):
             nn.utils.clip_grad_norm_(model.parameters(), CLIP)
             optimizer.step()
         acc.add(loss)
-    return acc.value() / count
+    return dp.epoch_mean(acc.value(), count, sharded, device)
 
 
 def valid(model, iterator, device='cuda'):
-    """Ren-MME/run.py:342-368: mean over batches of multi_loss (no R-Drop term)."""
+    """Ren-MME/run.py:342-368: mean over batches of multi_loss (no R-Drop term); global under
+    data parallelism."""
+    from . import dp
     model.eval()
-    epoch_loss, count = 0.0, 0
+    epoch_loss, count, sharded = 0.0, 0, False
     with torch.no_grad():
         for batch in iterator:
             count += 1
+            gr = dp.global_rows_of(batch)
+            sharded = sharded or gr is not None
+            if len(batch) == 0:
+                continue
             cols = _to_device(batch, device)
             logits = model(*cols[:12])
-            epoch_loss += float(multi_loss(logits, cols[12]).item())
-    return epoch_loss / count
+            if gr is not None and dp.world() > 1:
+                epoch_loss += float((_autograd.CircleLossFunction.apply(logits, cols[12]).sum() / gr).item())
+            else:
+                epoch_loss += float(multi_loss(logits, cols[12]).item())
+    return dp.epoch_mean(epoch_loss, count, sharded, device)
 
 
 def run(model, train_list, valid_list, batch_size, learning_rate, epochs, name, data_loader=None,
@@ -216,9 +234,12 @@ def run(model, train_list, valid_list, batch_size, learning_rate, epochs, name, 
     from .optim import FusedAdamW
     if data_loader is None:
         raise ValueError('run() needs the data_loader generator of the caller')
+    from . import dp
+    lead = dp.rank() == 0
     log_file = os.path.join(log_path, name + '.txt')
-    with open(log_file, 'w') as f:
-        f.write('epoch, train_loss, valid_loss\n')
+    if lead:
+        with open(log_file, 'w') as f:
+            f.write('epoch, train_loss, valid_loss\n')
     optimizer = FusedAdamW(model, lr=learning_rate)
     scheduler = ReduceLROnPlateau(optimizer, factor=0.1, patience=1)
     stop, losses = 0, []
@@ -227,12 +248,14 @@ def run(model, train_list, valid_list, batch_size, learning_rate, epochs, name, 
         valid_loss = valid(model, data_loader(valid_list, batch_size), device)
         scheduler.step(valid_loss)
         losses.append(valid_loss)
-        with open(log_file, 'a') as f:
-            f.write('\n{epoch}, {train_loss: 3.3f}, {valid_loss: 3.3f}\n'.format(
-                epoch=epoch + 1, train_loss=train_loss, valid_loss=valid_loss))
+        if lead:
+            with open(log_file, 'a') as f:
+                f.write('\n{epoch}, {train_loss: 3.3f}, {valid_loss: 3.3f}\n'.format(
+                    epoch=epoch + 1, train_loss=train_loss, valid_loss=valid_loss))
         if valid_loss == min(losses) and valid_loss > 0.009:
             stop = 0
-            torch.save(model.state_dict(), os.path.join(log_path, name + '_' + str(valid_loss)[:4] + '.pt'))
+            if lead:
+                torch.save(model.state_dict(), os.path.join(log_path, name + '_' + str(valid_loss)[:4] + '.pt'))
         else:
             stop += 1
             if stop >= 3:

@@ -398,6 +398,13 @@ class RealformerPlan:
         self.t_colsum = max(cdiv(c.n_cols, 32) for c in cs)
 
     # ------------------------------------------------------------------ execution
+    def set_global_rows(self, n):
+        """Data-parallel share (mep_amd.dp): the masked circle-loss mean over B * P utterance slots
+        (others/realformer.py:312) taken over the n global rows (None: the local B)."""
+        rows = self.B if n is None else int(n)
+        self.head.loss_scale = 1.0 / (rows * self.P)
+        return rows
+
     def set_inputs(self, l, v, a, lm, vm, am, labels=None, umask=None):
         """Reference-shaped [B, P, T, d] features / [B, P, T] masks (or [B, T, d] / [B, T] for the
         single-utterance chain plan) into the resident buffers."""

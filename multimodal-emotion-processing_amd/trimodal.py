@@ -483,6 +483,16 @@ class TriModalPlan:
             if labels is not None:
                 self.labels.copy_(labels)
 
+    def set_global_rows(self, n):
+        """Scale the fused loss for a data-parallel share (mep_amd.dp): the circle loss by
+        1/n (the rank's part of the global-batch mean) and the R-Drop KL batchmean by n/2 global
+        pairs; None restores the local mean (1/B, B/2).  Returns the key of the scaling (a
+        captured graph holds the head descriptor by value, so the engine keys graphs by it)."""
+        rows = self.B if n is None else int(n)
+        self.head.loss_scale = 1.0 / rows
+        self.head.rdrop_pairs = 0 if n is None else rows // 2
+        return rows
+
     def set_dropout(self, p):
         """Dropout probability of the block epilogues (Ren-MME DROP at train time, 0 in eval).
         Descriptor bytes are rewritten in place so captured graphs see the new value."""

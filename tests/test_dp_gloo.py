@@ -43,6 +43,9 @@ class _FakePlan:
     def set_dropout(self, p):
         assert p == 0.0
 
+    def set_global_rows(self, n):
+        return n
+
     def forward(self, grad=True, rdrop=False, stream=None):
         pass
 
