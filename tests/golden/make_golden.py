@@ -31,7 +31,9 @@ import torch.optim as optim
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, HERE)
+sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
 import specs  # noqa: E402
+from oracle import dropout as odrop  # noqa: E402
 
 REF = '/root/reference'
 SCRIPTS = {'cmu': 'cmu-mosei/run.py', 'realformer': 'others/realformer.py', 'ren': 'Ren-MME/run.py'}
@@ -86,8 +88,29 @@ def dump_grads(out, model, full):
 
 # ----------------------------------------------------------------------------------- cases
 
-def case_model(name, family, consts, ctor, batch, full, seed, opt, steps=1):
-    """Whole-model train step(s) as the reference ``train`` performs them."""
+class MaskDrop(nn.Module):
+    """Stand-in for one Attention_Block's nn.Dropout (Ren-MME/run.py:173): multiplies by the
+    recorded keep-scale mask of the repo's counter hash (oracle/dropout.py) -- what nn.Dropout
+    computes for that mask.  The block calls it twice per forward: site 0 on proj(x)
+    (run.py:209), site 1 on norm2(minus(.)) (run.py:213)."""
+
+    def __init__(self, block, seed, p):
+        super().__init__()
+        self.block, self.seed, self.p, self.calls = block, seed, p, 0
+
+    def forward(self, x):
+        if not self.training:
+            return x
+        site = self.calls % 2
+        self.calls += 1
+        B, T, D = x.shape
+        return x * torch.from_numpy(odrop.block_mask(self.seed, self.block, site, B, T, D, self.p))
+
+
+def case_model(name, family, consts, ctor, batch, full, seed, opt, steps=1, drop=None):
+    """Whole-model train step(s) as the reference ``train`` performs them.  drop = (p, seed0):
+    the blocks' dropout uses the masks of seed advance(seed0) (the engine advances the seed once
+    before a training forward)."""
     ns = load_reference(family, consts)
     torch.manual_seed(0)
     if family == 'cmu':
@@ -97,6 +120,13 @@ def case_model(name, family, consts, ctor, batch, full, seed, opt, steps=1):
     else:
         model = ns['State_Transfer'](**ctor)
     shapes = set_params(model, seed)
+    if drop is not None:
+        p, seed0 = drop
+        s1 = odrop.seed_advance(seed0)
+        nl = ctor['n_layers']
+        for e, enc in enumerate((model.intensity, model.stimulation)):
+            for m, blk in enumerate(enc.multimodal_blocks):
+                blk.drop = MaskDrop(e * 9 * nl + m, s1, p)
     model.train()
     if family == 'cmu':
         l, v, a, lm, vm, am, labels = specs.cmu_batch(**batch)
@@ -137,11 +167,15 @@ def case_model(name, family, consts, ctor, batch, full, seed, opt, steps=1):
             out['clipcoef'] = np.float64(min(1.0, 1.0 / (gnorm.item() + 1e-6)))
             dump_grads(out, model, full)
         optimizer.step()
+    if drop is not None:
+        model.eval()                       # logits2: the no-dropout network after the step
     with torch.no_grad():
         out['logits2'] = model(*args).numpy()
     dump_params(out, model, 'post', full)
     meta = dict(kind='model', family=family, consts=consts, ctor=ctor, batch=batch, seed=seed,
                 opt=opt, steps=steps, full=full, shapes=shapes)
+    if drop is not None:   # its own kind: the CPU oracle has no per-site masks
+        meta.update(kind='model_drop', drop=dict(p=drop[0], seed0=drop[1], seed=odrop.seed_advance(drop[1])))
     return meta, out
 
 
@@ -226,6 +260,10 @@ CASES = {
     'ren_full': lambda: case_model('ren_full', 'ren', REN_C, dict(dim=128, l_len=40, v_len=76, a_len=96,
                                    n_heads=8, n_layers=1, ffn=1),
                                    dict(seed=15, pairs=2, T=[40, 76, 96]), False, 105, 'adamw'),
+    # Ren-MME's DROP = 0.1 (Ren-MME/run.py:36) with the repo's counter-hash masks
+    'ren_drop': lambda: case_model('ren_drop', 'ren', dict(REN_C, DROP=0.1), dict(dim=32, l_len=5, v_len=6, a_len=8,
+                                   n_heads=2, n_layers=1, ffn=1),
+                                   dict(seed=20, pairs=3, T=[5, 6, 8]), True, 115, 'adamw', drop=(0.1, 20261016)),
     # BASELINE cfg3 shape (B=64, T=50, D=96, H=6) with ragged masks and 'no_name' rows
     'cmu_cfg3': lambda: case_model('cmu_cfg3', 'cmu', CMU_C, cmu_ctor(96, 6, 1),
                                    dict(seed=17, B=64, T=50, no_name_rows=(0, 13, 40)), False, 112, 'adamw'),

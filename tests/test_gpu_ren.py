@@ -96,6 +96,108 @@ def test_base_model_dropout(cuda):
     assert (t1 - ev).abs().max() > 1e-4
 
 
+def _seed_tensor(v):
+    import numpy as np
+    return int(np.array([v], dtype=np.uint64).view(np.int64)[0])
+
+
+def test_base_model_dropout_pinned(cuda):
+    """DROP = 0.1 pinned against the reference (tests/golden/ren_drop.npz): the reference's
+    Base_model ran with each block's nn.Dropout applying the repo's counter-hash masks
+    (oracle/dropout.py) of the fixture's seed, so logits, loss and every gradient must match the
+    HIP path with the same seed -- mask placement (proj output and block output,
+    Ren-MME/run.py:209,213), the 1/(1-p) scale and the gradient routing are all pinned."""
+    from mep_amd import ren_mme
+    meta, gold = fixtures.load('ren_drop')
+    model = ren_model(meta, cuda, drop=meta['drop']['p'])
+    model.train()
+    args, labels = _batch(meta, cuda)
+    l, v, a, lm, vm, am = ren_mme._pack(args)
+    runner = model.mep_runner(cuda)
+    plan = runner.stage(l, v, a, lm, vm, am, labels)
+    plan.set_dropout(meta['drop']['p'])
+    plan.seed.fill_(_seed_tensor(meta['drop']['seed']))
+    plan.forward(grad=True, rdrop=True)
+    plan.backward()
+    torch.cuda.synchronize()
+    assert_close(plan.logits, gold['logits'], 1e-4, OUT_ATOL_FRAC, 'logits')
+    assert_close(plan.loss.reshape(()), gold['loss'], 1e-4, 0, 'loss')
+    coef = float(gold['clipcoef'])
+    for k, _ in model.named_parameters():
+        if 'nograd/' + k in gold:
+            continue
+        assert_close(runner.flat.view(runner.flat.grad, k) * coef, gold['grad/' + k], 1e-3, 1e-5, k)
+
+
+@pytest.mark.parametrize('graph', [False, True])
+def test_base_model_dropout_engine_step(graph, cuda):
+    """The fused engine's training step at DROP = 0.1 (seed advanced once before the forward, as
+    every training step does) against the reference step on the same masks: loss, clip norm and
+    post-AdamW parameters; then the eval-mode forward (no dropout) of the updated model."""
+    from mep_amd import ren_mme
+    from mep_amd.engine import TrainEngine
+    from mep_amd.optim import FusedAdamW
+    meta, gold = fixtures.load('ren_drop')
+    model = ren_model(meta, cuda, drop=meta['drop']['p'])
+    model.train()
+    opt = FusedAdamW(model, lr=1e-3)
+    eng = TrainEngine(model, opt, clip=1.0, rdrop=True, graph=graph)
+    args, labels = _batch(meta, cuda)
+    l, v, a, lm, vm, am = ren_mme._pack(args)
+    plan = model.mep_runner(cuda).plan_for(l, v, a)
+    plan.seed.fill_(_seed_tensor(meta['drop']['seed0']))
+    loss = float(eng.step(l, v, a, lm, vm, am, labels).item())
+    assert_close(loss, gold['loss'], 1e-4, 0, 'loss')
+    assert_close(opt.gnorm.reshape(()), gold['gnorm'], 1e-4, 0, 'gnorm')
+    check_post_params(model, meta, gold)
+    model.eval()
+    with torch.no_grad():
+        logits2 = model(*args)
+    assert_close(logits2, gold['logits2'], 1e-3, 1e-5, 'logits2')
+
+
+def test_dropout_mask_statistics(cuda):
+    """The device masks' statistics at p = 0.1 over the whole ren_ref batch: keep rate 0.9 within
+    5 sigma, every kept element scaled by exactly float32(1) / float32(0.9), masks change with
+    the seed, and the two rows of an R-Drop pair get different masks."""
+    import numpy as np
+    meta, _ = fixtures.load('ren_ref')
+    model = ren_model(meta, cuda, drop=0.1)
+    model.train()
+    from mep_amd import ren_mme
+    args, labels = _batch(meta, cuda)
+    l, v, a, lm, vm, am = ren_mme._pack(args)
+    runner = model.mep_runner(cuda)
+    plan = runner.stage(l, v, a, lm, vm, am, labels)
+    plan.set_dropout(0.1)
+    plan.seed.fill_(12345)
+    plan.forward(grad=False)
+    torch.cuda.synchronize()
+    # site 1 of every block: out = drop(LN(z)) -> recover the mask as out / LN(z)
+    blk = plan.blocks[0]
+    z = blk['Z'].double()
+    mean, rstd = blk['estat'][:, 0:1].double(), blk['estat'][:, 1:2].double()
+    pre = runner.flat.view(runner.flat.buf, blk['pre'] + 'norm2.weight').double()
+    bias = runner.flat.view(runner.flat.buf, blk['pre'] + 'norm2.bias').double()
+    y = (z - mean) * rstd * pre + bias
+    out = plan.Xcat[0][:, plan.toff[blk['qm']]:plan.toff[blk['qm']] + blk['Tq'], blk['col']:blk['col'] + plan.spec.D]
+    out = out.reshape(-1, plan.spec.D).double()
+    keep = (out != 0)
+    big = keep & (y.abs() > 0.05)           # ratio well conditioned (fp32 LN output vs the fp64 restatement)
+    ratio = (out[big] / y[big])
+    assert float((ratio - float(np.float32(1) / np.float32(0.9))).abs().max()) < 2e-5
+    n = keep.numel()
+    rate = float(keep.double().mean())
+    assert abs(rate - 0.9) < 5 * (0.09 / n) ** 0.5, rate
+    rows = keep.reshape(plan.B, blk['Tq'], -1)
+    assert bool((rows[0::2] != rows[1::2]).any()), 'pair rows share a mask'
+    plan.seed.fill_(54321)
+    plan.forward(grad=False)
+    torch.cuda.synchronize()
+    out2 = plan.Xcat[0][:, plan.toff[blk['qm']]:plan.toff[blk['qm']] + blk['Tq'], blk['col']:blk['col'] + plan.spec.D]
+    assert bool(((out2.reshape(-1, plan.spec.D) != 0) != keep).any()), 'mask does not depend on the seed'
+
+
 def test_unify_dimension_standalone(cuda):
     """Unify_Dimension.forward standalone (Ren-MME/run.py:167-168) vs a torch fp32 statement."""
     from mep_amd import ren_mme
