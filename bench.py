@@ -1,20 +1,24 @@
-"""Throughput of the cmu-mosei tri-modal training step on MI355X (BASELINE.json metric).
+"""Throughput of the tri-modal training path on MI355X (BASELINE.json metric and configs).
 
-Workload (BASELINE cfg3 / cfg4): Concat_Trans (D=96, H=6, n_layers=1, 7 classes), B=64 utterance
-pairs per GPU, T=50 for text (d=300), visual (d=35) and audio (d=74); one step = forward of both
-encoders + head + circle loss + backward + clip_grad_norm_(1.0) + AdamW (lr 1e-3) [+ RCCL
-all-reduce of the flat gradient when N > 1].  Synthetic N(0,1) features, all-ones masks,
+Default workload (BASELINE cfg3 / cfg4): cmu-mosei Concat_Trans (D=96, H=6, n_layers=1, 7 classes),
+B=64 utterance pairs per GPU, T=50 for text (d=300), visual (d=35) and audio (d=74); one step =
+forward of both encoders + head + circle loss + backward + clip_grad_norm_(1.0) + AdamW (lr 1e-3)
+[+ RCCL all-reduce of the flat gradient when N > 1].  Synthetic N(0,1) features, all-ones masks,
 Bernoulli(0.3) labels, random-init weights; inputs resident in HBM before the timed region.
-Arithmetic: fp32 end to end (the reference has no AMP; fp32 keeps the 1e-4 logits parity).
+Arithmetic: fp32 storage, softmax, LayerNorm and accumulation; the products run on the matrix
+cores either in fp32 (v_mfma_f32_*) or as fp32 operands split into bf16 parts,
+within the 1e-4 logits parity of the fp32 reference.
 
-    python bench.py [--gpus N --steps K --warmup W]
-    torchrun --nproc-per-node N bench.py --gpus N ...      (one process per GPU, RCCL)
+    python bench.py [--gpus N --steps K --warmup W]                  BASELINE cfg3 (cfg4 with N > 1)
+    python bench.py --config cfg2 | cfg5                            the other BASELINE configs
+    torchrun --nproc-per-node N bench.py --gpus N ...                (one process per GPU, RCCL)
 Rank 0 prints one JSON line.
 """
 import argparse
 import glob
 import json
 import os
+import platform
 import re
 import sys
 import time
@@ -35,8 +39,7 @@ DIMS = (300, 35, 74)
 
 
 class LaunchTimer:
-    """HIP events around every libmep launch of an eager step, on the launching stream (the
-    backward's side-stream launches included)."""
+    """HIP events around every libmep launch of an eager step, on the launching stream."""
 
     def __init__(self):
         self.ev = []
@@ -68,52 +71,295 @@ KERNEL_OF = {'mep_attn_bwd': 'k_attn_bwd', 'mep_attn_fwd': 'k_attn_fwd', 'mep_bl
 
 def pmc_traffic(launch):
     """(HBM bytes per dispatch, source file) of the kernel behind `launch` from the newest
-    committed PMC pass (profiles/r<round>_v<n>_pmc.json: (2 FETCH_SIZE + WRITE_SIZE) x 1024,
-    the gfx950 correction of MI355X_MICROARCH.md section HBM), or (None, None)."""
+    committed PMC pass that measured it (profiles/r<round>_v<n>_pmc.json: (2 FETCH_SIZE +
+    WRITE_SIZE) x 1024, the gfx950 correction of MI355X_MICROARCH.md section HBM), or (None, None)."""
     def key(f):
         return [int(x) for x in re.findall(r'\d+', os.path.basename(f))]
-    files = sorted(glob.glob(os.path.join(ROOT, 'profiles', 'r*_v*_pmc.json')), key=key)
     prefix = KERNEL_OF.get(launch)
-    if not files or prefix is None:
+    if prefix is None:
         return None, None
-    for k, v in json.load(open(files[-1])).items():
-        if k.startswith(prefix) and 'hbm_bytes_per_dispatch' in v:
-            return int(v['hbm_bytes_per_dispatch']), os.path.relpath(files[-1], ROOT)
+    for f in sorted(glob.glob(os.path.join(ROOT, 'profiles', 'r*_v*_pmc.json')), key=key, reverse=True):
+        for k, v in json.load(open(f)).items():
+            if k.startswith(prefix) and 'hbm_bytes_per_dispatch' in v:
+                return int(v['hbm_bytes_per_dispatch']), os.path.relpath(f, ROOT)
     return None, None
 
 
-def synth_batch(rank, device):
-    rng = np.random.default_rng(20261015 + rank)
-    f = lambda d: torch.from_numpy(rng.standard_normal((B, 2, T, d), dtype=np.float32)).to(device)  # noqa: E731
-    l, v, a = (f(d) for d in DIMS)
-    m = torch.ones(B, 2, T, device=device)
-    labels = torch.from_numpy((rng.random((B, 7)) < 0.3).astype(np.int64)).to(device)
-    return l, v, a, m, m.clone(), m.clone(), labels
+def cpu_model():
+    try:
+        for line in open('/proc/cpuinfo'):
+            if line.startswith('model name'):
+                return line.split(':', 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor() or 'unknown'
 
 
-def cpu_baseline(budget_s=12.0):
-    """The CPU oracle (repo restatement of the reference path, fp32 PyTorch CPU) on the same
-    workload: fwd+bwd+clip+AdamW at B=64, T=50, timed for a bounded number of steps."""
-    from oracle import cmu_mosei as ocmu
-    from oracle import common
-    from tests.golden import specs
-    from mep_amd import cmu_mosei
-    m = cmu_mosei.Concat_Trans(dim=D, l_len=T, v_len=T, a_len=T, n_heads=H, n_layers=NL, ffn=1)
-    shapes = {k: list(v.shape) for k, v in m.state_dict().items()}
-    P = {k: torch.tensor(v, requires_grad=True) for k, v in specs.param_values(shapes, 1).items()}
-    opt = common.AdamState(P.values(), lr=1e-3, weight_decay=0.01)
-    batch = [torch.from_numpy(x) for x in specs.cmu_batch(seed=5, B=B, T=T, no_name_rows=(), full_masks=True)]
-    ocmu.train_step(P, opt, batch, H, NL)       # warmup
+def timed_cpu(step, budget_s, max_steps=200):
+    step()                                   # warmup
     n, t0 = 0, time.perf_counter()
     while True:
-        ocmu.train_step(P, opt, batch, H, NL)
+        step()
         n += 1
         el = time.perf_counter() - t0
-        if (n >= 3 and el >= budget_s) or n >= 200:
-            break
-    return dict(value=round(B * n / el, 2), unit='utt/s', cores=torch.get_num_threads(), kind='port',
-                sample='%d steps of B=64,T=50 Concat_Trans fwd+bwd+clip+AdamW (oracle, fp32 CPU, %d threads)'
-                       % (n, torch.get_num_threads()))
+        if (n >= 3 and el >= budget_s) or n >= max_steps:
+            return n, el
+
+
+# ------------------------------------------------------------------------------ workloads
+class Cfg3:
+    """cmu-mosei Concat_Trans training step (BASELINE cfg3 / cfg4)."""
+    name = 'cfg3'
+    metric = METRIC
+    unit = 'utt/s'
+
+    def __init__(self, dev, rank, graph):
+        from mep_amd import cmu_mosei
+        from mep_amd.engine import TrainEngine
+        from mep_amd.optim import FusedAdamW
+        torch.manual_seed(0)
+        self.model = cmu_mosei.Concat_Trans(dim=D, l_len=T, v_len=T, a_len=T, n_heads=H, n_layers=NL,
+                                            ffn=1).to(dev).train()
+        self.opt = FusedAdamW(self.model, lr=1e-3)
+        self.eng = TrainEngine(self.model, self.opt, clip=1.0, graph=graph)
+        self.eng_eager = TrainEngine(self.model, self.opt, clip=1.0, graph=False)
+        rng = np.random.default_rng(20261015 + rank)
+        f = lambda d: torch.from_numpy(rng.standard_normal((B, 2, T, d), dtype=np.float32)).to(dev)  # noqa: E731
+        l, v, a = (f(d) for d in DIMS)
+        m = torch.ones(B, 2, T, device=dev)
+        labels = torch.from_numpy((rng.random((B, 7)) < 0.3).astype(np.int64)).to(dev)
+        self.plan = self.model.mep_runner(dev).plan(B, (T, T, T))
+        self.plan.set_inputs(l, v, a, m, m.clone(), m.clone(), labels)
+        self.rows = B
+
+    def step(self):
+        self.eng.step_plan(self.plan)
+
+    def eager_step(self):
+        self.eng_eager.step_plan(self.plan)
+
+    def loss(self):
+        return float(self.plan.loss.item())
+
+    def config(self, world, graph):
+        return {'workload': 'cmu-mosei Concat_Trans train step (fwd+bwd+clip+AdamW), BASELINE cfg3/cfg4',
+                'global_batch': B * world, 'per_gpu_batch': B, 'seq_len': T, 'dims': list(DIMS), 'D': D,
+                'heads': H, 'n_layers': NL, 'parallelism': 'dp%d' % world, 'graph': graph}
+
+    @staticmethod
+    def cpu_baseline(budget_s):
+        """The CPU oracle (repo restatement of the reference path, fp32 PyTorch CPU): fwd+bwd+clip+
+        AdamW at B=64, T=50."""
+        from oracle import cmu_mosei as ocmu
+        from oracle import common
+        from tests.golden import specs
+        from mep_amd import cmu_mosei
+        m = cmu_mosei.Concat_Trans(dim=D, l_len=T, v_len=T, a_len=T, n_heads=H, n_layers=NL, ffn=1)
+        shapes = {k: list(v.shape) for k, v in m.state_dict().items()}
+        P = {k: torch.tensor(v, requires_grad=True) for k, v in specs.param_values(shapes, 1).items()}
+        opt = common.AdamState(P.values(), lr=1e-3, weight_decay=0.01)
+        batch = [torch.from_numpy(x) for x in specs.cmu_batch(seed=5, B=B, T=T, no_name_rows=(), full_masks=True)]
+        n, el = timed_cpu(lambda: ocmu.train_step(P, opt, batch, H, NL), budget_s)
+        return dict(value=round(B * n / el, 2), unit='utt/s', n=n, rows=B,
+                    sample='%d steps of B=64,T=50 Concat_Trans fwd+bwd+clip+AdamW (oracle, fp32 CPU)' % n)
+
+
+class Cfg5:
+    """Ren-MME Base_model training step at T=300 (BASELINE cfg5): 32 rows = 16 duplicate pairs per
+    GPU, text / video / audio d = 768 / 640 / 205, D=128, H=8, DROP=0.1, circle loss + R-Drop KL,
+    AdamW."""
+    name = 'cfg5'
+    metric = 'rows/sec fwd+bwd, Ren-MME Base_model T=300 (d=768/640/205), 32 rows per MI355X'
+    unit = 'rows/s'
+    R, TT, DIMS5 = 32, 300, (768, 640, 205)
+
+    def __init__(self, dev, rank, graph):
+        from mep_amd import ren_mme
+        from mep_amd.engine import TrainEngine
+        from mep_amd.optim import FusedAdamW
+        torch.manual_seed(0)
+        R, TT = self.R, self.TT
+        self.model = ren_mme.Base_model(dim=128, l_len=TT, v_len=TT, a_len=TT, n_heads=8, n_layers=1,
+                                        ffn=1).to(dev).train()
+        self.opt = FusedAdamW(self.model, lr=1e-3)
+        self.eng = TrainEngine(self.model, self.opt, clip=1.0, rdrop=True, graph=graph)
+        self.eng_eager = TrainEngine(self.model, self.opt, clip=1.0, rdrop=True, graph=False)
+        rng = np.random.default_rng(20261015 + rank)
+        feats = []
+        for d in self.DIMS5:            # (prev, cur) per modality, every sample twice (R-Drop)
+            pair = []
+            for _ in range(2):
+                x = rng.standard_normal((R // 2, TT, d), dtype=np.float32)
+                pair.append(torch.from_numpy(np.repeat(x, 2, 0)).to(dev))
+            feats.append(tuple(pair))
+        m = torch.ones(R, TT, device=dev)
+        labels = torch.from_numpy(np.repeat((rng.random((R // 2, 9)) < 0.3).astype(np.float32), 2, 0)).to(dev)
+        runner = self.model.mep_runner(dev)
+        self.plan = runner.plan(R, (TT, TT, TT))
+        self.plan.set_inputs(*feats, (m, m), (m, m), (m, m), labels)
+        self.rows = R
+
+    def step(self):
+        self.eng.step_plan(self.plan)
+
+    def eager_step(self):
+        self.eng_eager.step_plan(self.plan)
+
+    def loss(self):
+        return float(self.plan.loss.item())
+
+    def config(self, world, graph):
+        return {'workload': 'Ren-MME Base_model train step (fwd+bwd+R-Drop KL+clip+AdamW), BASELINE cfg5',
+                'global_batch': self.R * world, 'per_gpu_batch': self.R, 'seq_len': self.TT,
+                'dims': list(self.DIMS5), 'D': 128, 'heads': 8, 'n_layers': 1, 'dropout': 0.1,
+                'parallelism': 'dp%d' % world, 'graph': graph}
+
+    @classmethod
+    def cpu_baseline(cls, budget_s):
+        """The CPU oracle's Ren-MME step (fp32 CPU) on the same shape."""
+        from oracle import common
+        from oracle import ren_mme as oren
+        from tests.golden import specs
+        from mep_amd import ren_mme
+        m = ren_mme.Base_model(dim=128, l_len=cls.TT, v_len=cls.TT, a_len=cls.TT, n_heads=8, n_layers=1, ffn=1)
+        shapes = {k: list(v.shape) for k, v in m.state_dict().items()}
+        P = {k: torch.tensor(v, requires_grad=True) for k, v in specs.param_values(shapes, 1).items()}
+        opt = common.AdamState(P.values(), lr=1e-3, weight_decay=0.01)
+        inputs, labels = specs.ren_batch(seed=5, pairs=cls.R // 2, T=cls.TT)
+        inputs = [torch.from_numpy(x) for x in inputs]
+        labels = torch.from_numpy(labels)
+        n, el = timed_cpu(lambda: oren.train_step(P, opt, inputs, labels, 8, 1), budget_s, max_steps=50)
+        return dict(value=round(cls.R * n / el, 3), unit='rows/s', n=n, rows=cls.R,
+                    sample='%d steps of 32 rows (16 pairs), T=300, Ren-MME Base_model fwd+bwd+KL+clip+AdamW '
+                           '(oracle, fp32 CPU, no dropout)' % n)
+
+
+class Cfg2:
+    """realformer text encoder (BASELINE cfg2): Conv1d unify + position embedding + the first two
+    residual blocks of the linguistic chain (others/realformer.py:224-233), B=64, T=50, d=300,
+    D=96, H=6, FFN 2; backward of mean(out * G) (G fixed, seeded) + Adam (lr 1e-3)."""
+    name = 'cfg2'
+    metric = 'rows/sec fwd+bwd, realformer text encoder (2 residual blocks) B=64 T=50 d=300'
+    unit = 'rows/s'
+
+    def __init__(self, dev, rank, graph):
+        from mep_amd import realformer as rf
+        torch.manual_seed(0)
+        self.mc = rf.Multi_class(l_dim=300, v_dim=35, a_dim=74, dim=96, l_len=T, v_len=T, a_len=T, n_heads=6,
+                                 n_layers=2, ffn=2).to(dev).train()
+        self.runner = runner = self.mc.mep_chain_runner(2, dev)
+        rng = np.random.default_rng(20261015 + rank)
+        x = torch.from_numpy(rng.standard_normal((B, T, 300), dtype=np.float32)).to(dev)
+        m = torch.ones(B, T, device=dev)
+        G = torch.from_numpy(rng.standard_normal((B, T, 96), dtype=np.float32)).to(dev)
+        self.plan = runner.plan(B, 1)
+        z = torch.zeros(0, device=dev)
+        self.plan.set_inputs(x, z, z, m, z, z)
+        self.plan.dout_chain.copy_((G / G.numel()).reshape(self.plan.dout_chain.shape))   # d mean(out * G) / d out
+        self.opt = _FlatAdam(runner.flat, lr=1e-3)
+        self.graph = graph
+        self.g = None
+        self.rows = B
+
+    def _body(self):
+        self.plan.forward(grad=True)
+        self.plan.backward()
+        self.opt.step()
+
+    def step(self):
+        if not self.graph:
+            self._body()
+            return
+        if self.g is None:
+            self._body()
+            torch.cuda.synchronize()
+            self.g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self.g):
+                self._body()
+        self.g.replay()
+
+    def eager_step(self):
+        self._body()
+
+    def loss(self):
+        return float('nan')
+
+    def config(self, world, graph):
+        return {'workload': 'realformer text encoder fwd+bwd+Adam (Conv1d unify + pos + 2 residual blocks), '
+                            'BASELINE cfg2', 'global_batch': B * world, 'per_gpu_batch': B, 'seq_len': T,
+                'dims': [300], 'D': 96, 'heads': 6, 'n_layers': 2, 'ffn': 2, 'parallelism': 'dp%d' % world,
+                'graph': graph}
+
+    @staticmethod
+    def cpu_baseline(budget_s):
+        """The CPU oracle's realformer chain fwd+bwd + torch Adam (fp32 CPU) on the same shape."""
+        from oracle import common
+        from oracle import realformer as orf
+        from tests.golden import specs
+        from mep_amd import realformer as rf
+        mc = rf.Multi_class(l_dim=300, v_dim=35, a_dim=74, dim=96, l_len=T, v_len=T, a_len=T, n_heads=6,
+                            n_layers=2, ffn=2)
+        shapes = {k: list(v.shape) for k, v in mc.state_dict().items()}
+        P = {k: torch.tensor(v, requires_grad=True) for k, v in specs.param_values(shapes, 1).items()}
+        used = [k for k in P if k.startswith(('unify_dimension.linguistic', 'linguistic_position',
+                                             'multimodal_blocks.0.', 'multimodal_blocks.1.'))]
+        opt = torch.optim.Adam([P[k] for k in used], lr=1e-3)
+        rng = np.random.default_rng(5)
+        x = torch.from_numpy(rng.standard_normal((B, T, 300), dtype=np.float32))
+        lm = torch.ones(B, T)
+        G = torch.from_numpy(rng.standard_normal((B, T, 96), dtype=np.float32))
+
+        def step():
+            opt.zero_grad()
+            w = P['unify_dimension.linguistic.weight'][:, :, 0]
+            h0 = common.linear(x, w) + P['linguistic_position.position_embeddings.weight'][:T].unsqueeze(0)
+            h, _ = orf.encode_chain(P, '', h0, 2, 6, lm)
+            (h * G).mean().backward()
+            opt.step()
+        n, el = timed_cpu(step, budget_s)
+        return dict(value=round(B * n / el, 2), unit='rows/s', n=n, rows=B,
+                    sample='%d steps of B=64,T=50 realformer text chain fwd+bwd+Adam (oracle, fp32 CPU)' % n)
+
+
+class _FlatAdam:
+    """Adam (weight decay 0, no clip: others/realformer.py:342) over a runner's flat buffer with the
+    fused clip+Adam kernel (mep_clip_adam), graph-capturable."""
+
+    def __init__(self, flat, lr):
+        import ctypes
+        from mep_amd import _lib
+        self.flat, self._lib, self.ct = flat, _lib, ctypes
+        dev = flat.buf.device
+        self.exp_avg = torch.zeros_like(flat.buf)
+        self.exp_avg_sq = torch.zeros_like(flat.buf)
+        self.partial = torch.zeros(1024, dtype=torch.float32, device=dev)
+        self.gnorm = torch.zeros(1, dtype=torch.float32, device=dev)
+        self.step_t = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.hyper = torch.tensor([lr, 0.9, 0.999, 1e-8, 0.0, float('inf'), 1.0, 0.0], dtype=torch.float32,
+                                  device=dev)
+
+    def step(self):
+        P = self.ct.c_void_p
+        segs = (self._lib.Seg * 1)(self._lib.Seg(0, self.flat.n_grad))
+        self._lib.call('mep_clip_adam', P(self.flat.buf.data_ptr()), P(self.flat.grad.data_ptr()),
+                       P(self.exp_avg.data_ptr()), P(self.exp_avg_sq.data_ptr()), self.ct.cast(segs, P), 1,
+                       self.flat.total, P(self.partial.data_ptr()), P(self.gnorm.data_ptr()),
+                       P(self.hyper.data_ptr()), P(self.step_t.data_ptr()), 0)
+
+
+CONFIGS = {'cfg3': Cfg3, 'cfg5': Cfg5, 'cfg2': Cfg2}
+
+
+def roofline_of(work, name, tot, reps, costs):
+    from mep_amd import roofline
+    t, n = tot[name]
+    per_launch_s = t / n
+    launches_per_step = max(1, n // reps)
+    flops, nbytes = costs[name]
+    rl = roofline.roofline_entry(name, flops / launches_per_step, nbytes / launches_per_step, per_launch_s)
+    rl['traffic'], rl['traffic_source'] = pmc_traffic(name) if work.name == 'cfg3' else (None, None)
+    rl['avg_launch_us'] = round(per_launch_s * 1e6, 2)
+    return rl
 
 
 def main():
@@ -121,6 +367,7 @@ def main():
     ap.add_argument('--gpus', type=int, default=1)
     ap.add_argument('--steps', type=int, default=200)
     ap.add_argument('--warmup', type=int, default=20)
+    ap.add_argument('--config', default='cfg3', choices=sorted(CONFIGS))
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-graph', action='store_true')
     ap.add_argument('--cpu-budget', type=float, default=12.0)
@@ -134,28 +381,19 @@ def main():
         dist.init_process_group('nccl', device_id=torch.device('cuda', local))
     dev = torch.device('cuda', local)
 
-    from mep_amd import cmu_mosei, roofline
-    from mep_amd import _lib
-    from mep_amd.engine import TrainEngine
-    from mep_amd.optim import FusedAdamW
-
-    torch.manual_seed(0)
-    model = cmu_mosei.Concat_Trans(dim=D, l_len=T, v_len=T, a_len=T, n_heads=H, n_layers=NL, ffn=1).to(dev).train()
-    opt = FusedAdamW(model, lr=1e-3)
-    eng = TrainEngine(model, opt, clip=1.0, graph=not args.no_graph)
-    batch = synth_batch(rank, dev)
-    plan = model.mep_runner(dev).plan(B, (T, T, T))
-    plan.set_inputs(*batch)
+    from mep_amd import _lib, roofline
+    graph = not args.no_graph
+    work = CONFIGS[args.config](dev, rank, graph)
 
     for _ in range(args.warmup):
-        eng.step_plan(plan)
+        work.step()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        eng.step_plan(plan)
+        work.step()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -164,33 +402,25 @@ def main():
         t = torch.tensor([el], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
-    loss = float(plan.loss.item())
+    loss = work.loss()
 
-    # per-launch HIP-event timing of eager steps -> dominant kernel roofline
+    # per-launch HIP-event timing of eager steps -> dominant kernel and attention rooflines
     timer = LaunchTimer()
     reps = 20
-    eng_eager = TrainEngine(model, opt, clip=1.0, graph=False)
     _lib.TIMER = timer
     for _ in range(reps):
-        eng_eager.step_plan(plan)
+        work.eager_step()
     _lib.TIMER = None
     tot = timer.totals()
-    costs = roofline.launch_costs(plan)
+    costs = roofline.launch_costs(work.plan)
     per_kernel = {k: dict(ms_per_step=round(t / reps * 1e3, 4), launches_per_step=n // reps)
                   for k, (t, n) in sorted(tot.items(), key=lambda kv: -kv[1][0])}
     dom = max((k for k in tot if k in costs), key=lambda k: tot[k][0])
-    t_dom, n_dom = tot[dom]
-    per_launch_s = t_dom / n_dom
-    launches_per_step = n_dom // reps
-    flops, nbytes = costs[dom]
-    rl = roofline.roofline_entry(dom, flops / launches_per_step, nbytes / launches_per_step, per_launch_s)
-    rl['traffic'], rl['traffic_source'] = pmc_traffic(dom)
-    rl['avg_launch_us'] = round(per_launch_s * 1e6, 2)
 
     out = {
-        'metric': METRIC,
-        'value': round(B * world * args.steps / el, 2),
-        'unit': 'utt/s',
+        'metric': work.metric,
+        'value': round(work.rows * world * args.steps / el, 2),
+        'unit': work.unit,
         'n_gpus': world,
         'steps': args.steps,
         'warmup': args.warmup,
@@ -200,17 +430,17 @@ def main():
         'vs_baseline': None,
         'dtype': 'fp32',
         'data': 'synthetic N(0,1) features, all-ones masks, Bernoulli(0.3) labels, random-init weights',
-        'config': {'workload': 'cmu-mosei Concat_Trans train step (fwd+bwd+clip+AdamW), BASELINE cfg3/cfg4',
-                   'global_batch': B * world, 'per_gpu_batch': B, 'seq_len': T, 'dims': list(DIMS),
-                   'D': D, 'heads': H, 'n_layers': NL, 'parallelism': 'dp%d' % world,
-                   'graph': not args.no_graph},
+        'config': work.config(world, graph),
         'loss': round(loss, 6),
-        'roofline': rl,
+        'roofline': roofline_of(work, dom, tot, reps, costs),
+        'roofline_attention': roofline_of(work, 'mep_attn_bwd', tot, reps, costs),
         'kernels': per_kernel,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        out['cpu_baseline'] = cpu_baseline(args.cpu_budget)
-        out['gpu_vs_cpu'] = round(out['value'] / out['cpu_baseline']['value'], 1)
+        cb = CONFIGS[args.config].cpu_baseline(args.cpu_budget)
+        cb.update(cores=torch.get_num_threads(), kind='port', cpu_model=cpu_model())
+        out['cpu_baseline'] = cb
+        out['gpu_vs_cpu'] = round(out['value'] / cb['value'], 1)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:
