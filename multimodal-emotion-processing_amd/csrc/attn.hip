@@ -44,9 +44,16 @@ namespace {
 typedef float floatx4 __attribute__((ext_vector_type(4)));
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
 typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
+#ifndef MEP_BWD_DB
+#define MEP_BWD_DB 1       // short backward: next query tile's loads in a second register set
+#endif
+#ifndef MEP_BWD_WAVES
+#define MEP_BWD_WAVES 2    // waves per SIMD of the short backward
+#endif
 #ifndef MEP_FWD_WAVES
 #define MEP_FWD_WAVES 3    // waves per SIMD of the short, non-residual forward
 #endif
@@ -57,7 +64,8 @@ constexpr int THREADS = 64 * WAVES;
 constexpr int CH = 64;              // queries (forward) / keys (backward) per chunk
 constexpr int NT = CH / 16;         // 16-row tiles per chunk
 constexpr float INV_SCALE = 0.25f;  // 1/sqrt(16), exact
-constexpr int TLD = CH + 4;         // LDS row stride of the dS transpose
+constexpr int TLD2 = CH + 8;        // LDS row stride (bf16) of the backward's split dS transpose
+constexpr int TFL = 2 * 16 * TLD2 / 2;   // floats of one wave's transpose region (hi + lo parts)
 constexpr int RED = 2 * WAVES * CH * HD;   // floats of the backward's dK / dV partial buffer
 
 MEP_DEV floatx4 zero4() { return floatx4{0.f, 0.f, 0.f, 0.f}; }
@@ -385,8 +393,7 @@ struct Bwd {
     __amdgpu_buffer_rsrc_t rsStat;
     bool same_kv;
     int k_lo;
-    S3 kb[NT];
-    S2 vb[NT], kq[NT];
+    S2 kb[NT], vb[NT], kq[NT];
     float mtk[NT];
     floatx4 dk[NT], dv[NT];
     float dc_acc;
@@ -427,9 +434,8 @@ struct Bwd {
             const int okq = Kb.at(k0 + 4 * g, hc + c);
 #pragma unroll
             for (int s = 0; s < 4; ++s) kc4[s] = Kb.ld1(okq, s * Kb.sT4);
-            kb[kt] = split3(kf);
-            // k is v (cmu-mosei, Ren-MME): the 2-way split of V is the first two parts of K's
-            vb[kt] = same_kv ? S2{kb[kt].a0, kb[kt].a1, kb[kt].b0, kb[kt].b1} : split2(vf);
+            kb[kt] = split2(kf);
+            vb[kt] = same_kv ? kb[kt] : split2(vf);     // k is v (cmu-mosei, Ren-MME)
             kq[kt] = split2(kc4);
             dk[kt] = zero4();
             dv[kt] = zero4();
@@ -455,26 +461,32 @@ struct Bwd {
 
     // one 16-query tile against the chunk's 64 keys: accumulates dK / dV, returns this chunk's
     // dQ contribution (C[query 4g+r][dim c], before the 1/sqrt(hd) scale).  Tr: the wave's
-    // 16 x TLD transpose scratch in LDS.
+    // transpose scratch in LDS (TFL floats: the bf16 hi and lo parts of dS, 16 x TLD2 each).
     MEP_DEV floatx4 tile(const QIn& in, int qt, float* Tr) {
         const int q0 = qt * 16;
+        constexpr float LOG2E = 1.4426950408889634f;
         float mm[4], li[4], del[4];
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
             const int qq = q0 + 4 * g + s;
             // delta = rowsum(dO * O): the 16 dims of query qq sit in one DPP row (lanes c)
             del[s] = row16_sum(in.db[s] * in.ob[s]);
-            // padded queries: max = +inf, 1/sum = 0 make P = exp(-inf) * 0 = 0 (and with it dS)
+            // padded queries: max = +inf, 1/sum = 0 make P = exp(-inf) * 0 = 0 (and with it dS);
+            // the max is kept pre-scaled by log2(e) for exp2
             const bool qok = qq < Tq;
-            mm[s] = qok ? in.st[s][0] : INFINITY;
+            mm[s] = qok ? in.st[s][0] * LOG2E : INFINITY;
             li[s] = qok ? in.st[s][1] : 0.f;
         }
-        const S3 qs = split3(in.qa);
-        const S2 do2 = split2(in.da), db2 = split2(in.db), qb2 = split2(in.qb);
+        const S2 qs = split2(in.qa), do2 = split2(in.da), db2 = split2(in.db), qb2 = split2(in.qb);
+        typedef __attribute__((address_space(3))) unsigned short lushort;
+        lushort* Th = (lushort*)Tr;                 // [16 queries][TLD2] bf16 parts of dS
+        lushort* Tl = Th + 16 * TLD2;
 #pragma unroll
         for (int kt = 0; kt < NT; ++kt) {
             const int kk = k_lo + kt * 16 + c;
-            const floatx4 st = dot_score<false>(kb[kt], qs, zero4());   // C[query 4g+r][key c]
+            // recomputed scores on the 2-way split (the forward's are 3-way): P differs from the
+            // forward's by <= ~2^-16 relative, far inside the gradient tolerance
+            const floatx4 st = dot16(qs, kb[kt], zero4());               // C[query 4g+r][key c]
             const floatx4 dp = dot16(do2, vb[kt], zero4());
             float p[4], dsv[4];
 #pragma unroll
@@ -487,7 +499,7 @@ struct Bwd {
                     if (PREV) spv = sprev[si];
                 }
                 const float sv = score<PREV>(st[r], cres, spv, mtk[kt]);
-                const float pv = __expf(sv - mm[r]) * li[r];
+                const float pv = __builtin_amdgcn_exp2f(fmaf(sv, LOG2E, -mm[r])) * li[r];
                 float gsv = pv * (dp[r] - del[r]);
                 if (DSN || PREV) {
                     const bool ok = (qq < Tq) && (kk < Tk);
@@ -500,18 +512,28 @@ struct Bwd {
                 p[r] = pv;
                 dsv[r] = gsv;
             }
+            const S2 ds2 = split2(dsv);
             dv[kt] = dot16(split2(p), db2, dv[kt]);      // dV[key][dim] += P^T dO
-            dk[kt] = dot16(split2(dsv), qb2, dk[kt]);    // dK[key][dim] += dS^T Q
+            dk[kt] = dot16(ds2, qb2, dk[kt]);            // dK[key][dim] += dS^T Q
+            // the split dS, element by element, into Th / Tl[query][key] (bf16)
+            const unsigned hw[4] = {ds2.h0, ds2.h0 >> 16, ds2.h1, ds2.h1 >> 16};
+            const unsigned lw[4] = {ds2.l0, ds2.l0 >> 16, ds2.l1, ds2.l1 >> 16};
 #pragma unroll
-            for (int r = 0; r < 4; ++r) Tr[(4 * g + r) * TLD + kt * 16 + c] = dsv[r];   // Tr[query][key]
+            for (int r = 0; r < 4; ++r) {
+                Th[(4 * g + r) * TLD2 + kt * 16 + c] = (unsigned short)hw[r];
+                Tl[(4 * g + r) * TLD2 + kt * 16 + c] = (unsigned short)lw[r];
+            }
         }
-        // dQ += dS K with the query on the lane: read back the transposed 16 x 64 dS tile
+        // dQ += dS K with the query on the lane: the transposed 16 x 64 dS parts, already split,
+        // come back as packed words (keys 4g .. 4g+3 of each key tile, one 8-byte read per part)
         wave_lds_sync();
         S2 tq[NT];
+        typedef __attribute__((address_space(3))) u32x2 lu32x2;
 #pragma unroll
         for (int kt = 0; kt < NT; ++kt) {
-            const float4 t4 = *reinterpret_cast<const float4*>(Tr + c * TLD + kt * 16 + 4 * g);
-            tq[kt] = split2(t4.x, t4.y, t4.z, t4.w);
+            const u32x2 hh = *reinterpret_cast<const lu32x2*>(Th + c * TLD2 + kt * 16 + 4 * g);
+            const u32x2 ll = *reinterpret_cast<const lu32x2*>(Tl + c * TLD2 + kt * 16 + 4 * g);
+            tq[kt] = S2{hh[0], hh[1], ll[0], ll[1]};
         }
         wave_lds_sync();
         floatx4 dq = zero4();
@@ -532,8 +554,8 @@ struct Bwd {
 // of every dQ row and of its dK / dV rows, so no cross-wave sums are needed; the query tiles are
 // walked with every load of the next tile issued before this tile's math (two register sets).
 template <bool PREV, bool DSN>
-__global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(2))) void k_attn_bwd_short(const mep_attn_bwd_desc* __restrict__ descs) {
-    __shared__ __attribute__((aligned(16))) float Tr[WAVES][16 * TLD];
+__global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(MEP_BWD_WAVES))) void k_attn_bwd_short(const mep_attn_bwd_desc* __restrict__ descs) {
+    __shared__ __attribute__((aligned(16))) float Tr[WAVES][TFL];
     const mep_attn_bwd_desc& bd = descs[blockIdx.y];
     if (bd.f.Tk > CH) return;                // a LONG descriptor
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -542,6 +564,7 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(2))) vo
     Bwd<PREV, DSN> u(bd, bh / bd.f.H, bh % bd.f.H, lane);
     const int nqt = (u.Tq + 15) / 16;
     u.load_chunk(0);
+#if MEP_BWD_DB
     typename Bwd<PREV, DSN>::QIn bufA, bufB;
     u.fetch(bufA, 0);
     for (int qt = 0; qt < nqt; qt += 2) {
@@ -552,6 +575,13 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(2))) vo
             u.store_dq(bufB, qt + 1, u.tile(bufB, qt + 1, Tr[wave]));
         }
     }
+#else
+    for (int qt = 0; qt < nqt; ++qt) {
+        typename Bwd<PREV, DSN>::QIn in;
+        u.fetch(in, qt);
+        u.store_dq(in, qt, u.tile(in, qt, Tr[wave]));
+    }
+#endif
     const BRow dKb = brow(bd.dk, u.b, u.Tk, bd.f.H * HD), dVb = brow(bd.dv, u.b, u.Tk, bd.f.H * HD);
     const bool same_out = bd.dk.ptr == bd.dv.ptr && bd.dk.sB == bd.dv.sB && bd.dk.sT == bd.dv.sT;
     const int ok_ = dKb.at(4 * u.g, u.hc + u.c), ov_ = dVb.at(4 * u.g, u.hc + u.c);   // keys past Tk: dropped
@@ -591,7 +621,7 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(2))) vo
     const int nw = min(WAVES, nqt);          // waves that own query tiles
     const BRow dKb = brow(bd.dk, u.b, u.Tk, D), dVb = brow(bd.dv, u.b, u.Tk, D);   // keys past Tk: dropped
     const bool same_out = bd.dk.ptr == bd.dv.ptr && bd.dk.sB == bd.dv.sB && bd.dk.sT == bd.dv.sT;
-    float* Tr = lds + wave * (16 * TLD);     // inside the R region
+    float* Tr = lds + wave * TFL;            // inside the R region
     float* R = lds;
     float* DC = lds + RED;
     float* DQ = DC + WAVES;

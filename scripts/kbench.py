@@ -24,23 +24,14 @@ def main():
     ap.add_argument('--layers', type=int, default=1)
     ap.add_argument('--T', type=int, default=50)
     args = ap.parse_args()
-    from bench import synth_batch
-    from mep_amd import cmu_mosei
+    import bench
     from mep_amd._lib import launch
-    from mep_amd.engine import TrainEngine
-    from mep_amd.optim import FusedAdamW
     dev = torch.device('cuda:0')
-    torch.manual_seed(0)
-    T = args.T
-    model = cmu_mosei.Concat_Trans(dim=96, l_len=T, v_len=T, a_len=T, n_heads=6, n_layers=args.layers,
-                                   ffn=1).to(dev).train()
-    opt = FusedAdamW(model, lr=1e-3)
-    eng = TrainEngine(model, opt, graph=False)
-    plan = model.mep_runner(dev).plan(64, (T, T, T))
-    plan.set_inputs(*synth_batch(0, dev)) if T == 50 else None
-    eng.step_plan(plan)
+    bench.T, bench.NL = args.T, args.layers
+    work = bench.Cfg3(dev, 0, graph=False)
+    work.eager_step()
     torch.cuda.synchronize()
-    p = plan
+    p = work.plan
     D = p.spec.D
     table = {
         'mep_unify': lambda: launch('mep_unify', p.d_unify, p.t_unify),
