@@ -118,8 +118,10 @@ class Multi_class(nn.Module):
         self._chain_runner = None
 
     def forward(self, l, v, a, l_mask, v_mask, a_mask):
-        raise NotImplementedError('mep_amd executes Multi_class inside State_Transfer (one fused plan for all '
-                                  'utterances); encode_chain() runs a single chain')
+        """Standalone entry (the training path runs this encoder inside its model's fused plan):
+        HIP unify + blocks, PyTorch-ROCm concatenation / pooling / FC + LayerNorm + ReLU."""
+        from .standalone import multi_class_forward
+        return multi_class_forward(self, l, v, a, l_mask, v_mask, a_mask)
 
     def mep_chain_runner(self, n_layers, device):
         c = self._mep

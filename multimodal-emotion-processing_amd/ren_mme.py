@@ -89,8 +89,10 @@ class Multi_ATTN(nn.Module):
         self.classifier = nn.Linear(dim * 6 * n_layers, N_CLASSES, bias=False)
 
     def forward(self, l, v, a, l_mask, v_mask, a_mask):
-        raise NotImplementedError('mep_amd executes Multi_ATTN inside Base_model (one fused plan for both '
-                                  'encoders); standalone Multi_ATTN.forward is not a hot-path entry')
+        """Standalone entry (the training path runs this encoder inside its model's fused plan):
+        HIP unify + blocks, PyTorch-ROCm concatenation / pooling / classifier."""
+        from .standalone import multi_attn_forward
+        return multi_attn_forward(self, l, v, a, l_mask, v_mask, a_mask)
 
 
 def _pack(args):

@@ -340,3 +340,63 @@ def rf_block_forward(block, q, k, v, mask, scores):
                             block.w_qkv[2].weight, block.proj.weight, block.norm1.weight, block.norm1.bias,
                             block.norm2.weight, block.norm2.bias, ffn0.weight, ffn0.bias, ffn2.weight, ffn2.bias,
                             block.a, block.b, block.c)
+
+
+# ---------------------------------------------------------------- standalone encoders
+# Multi_ATTN.forward (cmu-mosei/run.py:272-319, Ren-MME/run.py:224-277) and Multi_class.forward
+# (others/realformer.py:223-264) as their own entries: the unify projection and every block run
+# on the HIP kernels above (one grouped launch sequence each, with its own backward); the
+# concatenation of the chain outputs, the mean / max pool over time and the classifier (or
+# FC + LayerNorm + ReLU) are PyTorch-ROCm ops.  The training hot path never comes here:
+# Concat_Trans / Base_model / State_Transfer run both encoders, pool and head as one plan.
+def encoder_features(mod, feats, masks, every_layer):
+    """The nine chains of an encoder over unified features: feats / masks {'l','v','a'} ->
+    [B, T_l + T_a + T_v, 3 * D * (n_layers if every_layer else 1)], chain outputs concatenated
+    per query modality in chain order (every layer's output for cmu-mosei / Ren-MME,
+    cmu-mosei/run.py:279-313; the last layer's for realformer, realformer.py:231-259) and the
+    modalities along time in the order l, a, v (cmu-mosei/run.py:317)."""
+    from .trimodal import CHAINS, TIME_ORDER
+    nl = mod.n_layers
+    rows = {'l': [], 'v': [], 'a': []}
+    for j, (qm, km) in enumerate(CHAINS):
+        x, s = feats[qm], None
+        for i in range(nl):
+            x, s = mod.multimodal_blocks[nl * j + i](x, feats[km], feats[km], masks[km], s)
+            if every_layer:
+                rows[qm].append(x)
+        if not every_layer:
+            rows[qm].append(x)
+    return torch.cat([torch.cat(rows[m], dim=2) for m in TIME_ORDER], dim=1)
+
+
+def mean_max_pool(x):
+    """torch.cat([mean(x, 1), max(x, 1)[0]], 1) (cmu-mosei/run.py:318; padded steps included), with
+    the max's gradient routed to the FIRST maximal step -- the reference's (CPU) tie-break, which
+    the fused pool kernel follows too.  Ties are common: every padded step of a row has zero
+    features and the same block output."""
+    mx = x.detach().amax(1, keepdim=True)
+    steps = torch.arange(x.shape[1], device=x.device).view(1, -1, 1)
+    first = torch.where(x.detach() == mx, steps, x.shape[1]).amin(1, keepdim=True)
+    return torch.cat([x.mean(1), x.gather(1, first).squeeze(1)], dim=1)
+
+
+def multi_attn_forward(mod, l, v, a, l_mask, v_mask, a_mask):
+    """cmu-mosei / Ren-MME Multi_ATTN.forward -> classifier logits."""
+    from ._autograd import require_cuda
+    require_cuda(l, v, a, l_mask, v_mask, a_mask)
+    u = dict(zip('lva', mod.unify_dimension(l, v, a)))
+    x = encoder_features(mod, u, {'l': l_mask, 'v': v_mask, 'a': a_mask}, every_layer=True)
+    return mod.classifier(mean_max_pool(x))
+
+
+def multi_class_forward(mod, l, v, a, l_mask, v_mask, a_mask):
+    """realformer Multi_class.forward -> [B, D] (Conv1d unify + position embedding, nine chains,
+    pool, FC, LayerNorm, ReLU, dropout p = 0)."""
+    from ._autograd import require_cuda
+    require_cuda(l, v, a, l_mask, v_mask, a_mask)
+    ul, uv, ua = mod.unify_dimension(l, v, a)
+    u = {'l': ul + mod.linguistic_position(ul), 'v': uv + mod.visual_position(uv),
+         'a': ua + mod.acoustic_position(ua)}
+    x = encoder_features(mod, u, {'l': l_mask, 'v': v_mask, 'a': a_mask}, every_layer=False)
+    x = torch.relu(mod.normalization(mod.fully_connected(mean_max_pool(x))))
+    return mod.drop(x)
