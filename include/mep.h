@@ -36,6 +36,15 @@ extern "C" {
 
 typedef void* mep_stream_t; /* a hipStream_t */
 
+/* Arithmetic precision.  Default (fp32 path): fp32 storage and every product at fp32 level --
+ * f32 MFMA, or fp32 operands split into bf16 parts on the bf16 matrix cores (3 parts: fp32-level
+ * error).  MEP_PREC_BF16 (bf16 path, BASELINE cfg3/cfg5): the matrix products take plain bf16
+ * operands (round-to-nearest of the fp32 values) with fp32 accumulation -- one MFMA per k block
+ * -- while storage, softmax, LayerNorm, scores and optimizer state stay fp32.  OR-ed into the
+ * `flags` of mep_attn_fwd / mep_attn_bwd and the `D` argument of mep_block_epi_fwd /
+ * mep_block_epi_bwd; the `bf16` field of mep_gemm_desc (mep_unify) and mep_wgrad_desc. */
+#define MEP_PREC_BF16 0x10000
+
 typedef struct {
     uint64_t ptr;   /* float* base                                  */
     int64_t  sB;    /* stride (floats) between consecutive batch rows */
@@ -62,6 +71,8 @@ typedef struct {
     int32_t  accumulate;
     int32_t  relu;
     float    alpha;
+    int32_t  bf16;     /* mep_unify: 1 = bf16 operands (MEP_PREC_BF16); mep_gemm: must be 0 */
+    int32_t  _pad;
 } mep_gemm_desc;
 int mep_gemm(const mep_gemm_desc* descs, int n_desc, int max_tiles, mep_stream_t stream);
 
@@ -101,6 +112,8 @@ typedef struct {
     int32_t  out_trans;          /* 1: write dW_i transposed, out_i[k * ldo_i + n] (for weights
                                     whose output dim exceeds 128, e.g. realformer ffn.0 /
                                     [w_qkv.1; w_qkv.2])                                         */
+    int32_t  bf16;               /* 1: bf16 operands (MEP_PREC_BF16); 0: 3-part split (fp32)   */
+    int32_t  _pad;
 } mep_wgrad_desc;
 int mep_wgrad(const mep_wgrad_desc* descs, int n_desc, int max_tiles, mep_stream_t stream);
 int mep_wgrad_reduce(const mep_wgrad_desc* descs, int n_desc, int max_tiles, mep_stream_t stream);

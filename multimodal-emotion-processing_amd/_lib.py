@@ -24,7 +24,7 @@ class Rows(ctypes.Structure):
 class GemmDesc(ctypes.Structure):
     _fields_ = [('x', Rows), ('y', Rows), ('w', u64), ('bias', u64), ('table', u64),
                 ('ntok', i32), ('N', i32), ('K', i32), ('ldw', i32), ('w_nt', i32),
-                ('accumulate', i32), ('relu', i32), ('alpha', f32)]
+                ('accumulate', i32), ('relu', i32), ('alpha', f32), ('bf16', i32), ('_pad', i32)]
 
 
 WG_MAX_B = 4
@@ -33,7 +33,8 @@ WG_MAX_B = 4
 class WgradDesc(ctypes.Structure):
     _fields_ = [('a', Rows), ('b', Rows * WG_MAX_B), ('out', u64 * WG_MAX_B), ('kb', i32 * WG_MAX_B),
                 ('ldo', i32 * WG_MAX_B), ('partial', u64), ('n_b', i32), ('ntok', i32), ('N', i32), ('Ktot', i32),
-                ('tok_per_split', i32), ('n_split', i32), ('accumulate', i32), ('out_trans', i32)]
+                ('tok_per_split', i32), ('n_split', i32), ('accumulate', i32), ('out_trans', i32),
+                ('bf16', i32), ('_pad', i32)]
 
 
 class AttnDesc(ctypes.Structure):
@@ -257,6 +258,7 @@ def launch(name, descs, max_tiles, stream=None, threads=None, extra=()):
 
 
 ATTN_PREV, ATTN_SOUT, ATTN_SHORT, ATTN_LONG = 1, 2, 4, 8   # MEP_ATTN_* (include/mep.h)
+PREC_BF16 = 0x10000   # MEP_PREC_BF16: bf16-operand products (attention flags, epilogue D argument)
 ATTN_MAX_DQ_TILES = (160 * 1024 // 4 - 2 * 4 * 64 * 16 - 4) // 256   # csrc/attn.hip backward LDS
 
 

@@ -5,13 +5,16 @@
 //   S = q k^T / sqrt(hd) [+ c * S_prev];  S -= 1e8 (1 - mask);  X = softmax(S) v
 // The post-mask S is returned to the caller, which feeds it to the next layer of the chain.
 //
-// Arithmetic: fp32 storage, fp32 softmax / score sequence, products on the bf16 matrix cores
+// Arithmetic (fp32 path): fp32 storage, fp32 softmax / score sequence, products on the bf16 matrix cores
 // with every fp32 operand split into bf16 parts (x = x0 + x1 [+ x2], each part the round-to-
 // nearest bf16 of the remainder; products of bf16 parts are exact in the fp32 accumulator):
 //   scores q.k (fwd and bwd)   3-way split, the six products x_i y_j with i + j <= 2:
 //                              relative error ~2^-24 per product (fp32 level)
 //   backward dP, dV, dK, dQ    2-way split, three or four products: relative error <= 2^-16
 //   forward P.V                fp32 MFMA (v_mfma_f32_16x16x4_f32) on the raw P and V: exact
+// bf16 path (MEP_PREC_BF16): every product takes the bf16 parts only (scores and 16-deep
+// contractions on v_mfma_f32_16x16x16_bf16, P.V and dQ on 16x16x32 with P rounded to bf16), fp32
+// softmax, scores and storage as above.
 // v_mfma_f32_16x16x32_bf16 takes 8 k-slots per lane; the slot -> index assignment is free as long
 // as A and B agree, so a lane's 4 consecutive fp32 values of a 16-wide contraction (the index
 // layout (step s, lane group g) -> 4g + s of the fp32 16x16x4 form) fill slots 0-3 with one part
@@ -107,14 +110,19 @@ MEP_DEV bf16x8 op(unsigned w0, unsigned w1, unsigned w2, unsigned w3) {
     return __builtin_bit_cast(bf16x8, u32x4{w0, w1, w2, w3});
 }
 MEP_DEV floatx4 mfma(bf16x8 a, bf16x8 b, floatx4 c) { return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0); }
+// bf16 path: a 16-deep contraction (4 bf16 per lane, k = 4g .. 4g+3) on v_mfma_f32_16x16x16_bf16
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+MEP_DEV s16x4 op4(unsigned w0, unsigned w1) { return __builtin_bit_cast(s16x4, u32x2{w0, w1}); }
+MEP_DEV floatx4 mfma16(s16x4 a, s16x4 b, floatx4 c) { return __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a, b, c, 0, 0, 0); }
 
 // Score product over the 16 head dims, 3-way split: P = the "packed" operand, U = the
 // "duplicated" one; slots (g, j < 4) and (g, j >= 4) carry
 //   MFMA 1: p0 u0 | p1 u0     MFMA 2: p0 u1 | p1 u1     MFMA 3: p0 u2 | p2 u0
 // P_IS_A selects which MFMA operand P is (forward: K = A; backward: K = B), the products and
-// slots are the same either way.
-template <bool P_IS_A>
+// slots are the same either way.  BF (bf16 path): the one product p0 u0.
+template <bool P_IS_A, bool BF>
 MEP_DEV floatx4 dot_score(const S3& p, const S3& u, floatx4 acc) {
+    if (BF) return P_IS_A ? mfma16(op4(p.a0, p.a1), op4(u.a0, u.a1), acc) : mfma16(op4(u.a0, u.a1), op4(p.a0, p.a1), acc);
     const bf16x8 p01 = op(p.a0, p.a1, p.b0, p.b1), p02 = op(p.a0, p.a1, p.c0, p.c1);
     const bf16x8 u00 = op(u.a0, u.a1, u.a0, u.a1), u11 = op(u.b0, u.b1, u.b0, u.b1), u20 = op(u.c0, u.c1, u.a0, u.a1);
     if (P_IS_A) {
@@ -130,7 +138,10 @@ MEP_DEV floatx4 dot_score(const S3& p, const S3& u, floatx4 acc) {
 }
 
 // 16-deep contraction, 2-way split, all four products: A = [x0 | x1], B = [y0 | y0] then [y1 | y1]
+// (BF: x0 y0)
+template <bool BF>
 MEP_DEV floatx4 dot16(const S2& x, const S2& y, floatx4 acc) {
+    if (BF) return mfma16(op4(x.h0, x.h1), op4(y.h0, y.h1), acc);
     const bf16x8 a = op(x.h0, x.h1, x.l0, x.l1);
     acc = mfma(a, op(y.h0, y.h1, y.h0, y.h1), acc);
     acc = mfma(a, op(y.l0, y.l1, y.l0, y.l1), acc);
@@ -138,10 +149,12 @@ MEP_DEV floatx4 dot16(const S2& x, const S2& y, floatx4 acc) {
 }
 
 // 32-deep contraction over two 16-row tiles (slots 0-3: tile 0, 4-7: tile 1), 2-way split,
-// products x0 y0 + x1 y0 + x0 y1
+// products x0 y0 + x1 y0 + x0 y1 (BF: x0 y0)
+template <bool BF>
 MEP_DEV floatx4 dot32(const S2& xa, const S2& xb, const S2& ya, const S2& yb, floatx4 acc) {
     const bf16x8 x0 = op(xa.h0, xa.h1, xb.h0, xb.h1), y0 = op(ya.h0, ya.h1, yb.h0, yb.h1);
     acc = mfma(x0, y0, acc);
+    if (BF) return acc;
     acc = mfma(op(xa.l0, xa.l1, xb.l0, xb.l1), y0, acc);
     acc = mfma(x0, op(ya.l0, ya.l1, yb.l0, yb.l1), acc);
     return acc;
@@ -221,8 +234,9 @@ MEP_DEV BRow brow(const mep_rows& v, int b, int n, int D) {
 // ================================================================== forward
 // One forward task: batch row b, head h, 64 queries.  PREV: residual scores in; SOUT: post-mask
 // scores out; SINGLE: Tk <= 64 (one key chunk: exact two-pass softmax, each query tile is
-// finalised right after its P.V, so no running O/max/sum state stays live).
-template <bool PREV, bool SOUT, bool SINGLE>
+// finalised right after its P.V, so no running O/max/sum state stays live).  BF: the bf16 path
+// (scores on one bf16 product, P.V on bf16 P and V).
+template <bool PREV, bool SOUT, bool SINGLE, bool BF>
 MEP_DEV void attn_fwd_task(const mep_attn_desc& d, int qc, int h, int b, int lane) {
     const int c = lane & 15, g = lane >> 4;
     const int hc = h * HD;
@@ -263,6 +277,7 @@ MEP_DEV void attn_fwd_task(const mep_attn_desc& d, int qc, int h, int b, int lan
         // columns (B of P.V: V[k0+4g+s][c]); past Tk they read 0 (P is 0 there)
         S3 ks[NT];
         float vf[NT][4], mt[NT][4];
+        bf16x8 vbf[NT / 2];     // BF: V of key-tile pairs (kt, kt+1) in slots 0-3 / 4-7
 #pragma unroll
         for (int kt = 0; kt < NT; ++kt) {
             const int k0 = k_lo + kt * 16;
@@ -275,6 +290,12 @@ MEP_DEV void attn_fwd_task(const mep_attn_desc& d, int qc, int h, int b, int lan
                 mt[kt][s] = mask_term(mask, k0 + 4 * g + s, Tk);
             }
             ks[kt] = split3(kf);
+        }
+        if (BF) {
+#pragma unroll
+            for (int kt = 0; kt < NT; kt += 2)
+                vbf[kt / 2] = op(pk(vf[kt][0], vf[kt][1]), pk(vf[kt][2], vf[kt][3]), pk(vf[kt + 1][0], vf[kt + 1][1]),
+                                 pk(vf[kt + 1][2], vf[kt + 1][3]));
         }
         float qfa[NT][4];                                                  // B of S^T: Q[q][4g+s]
 #pragma unroll
@@ -289,7 +310,7 @@ MEP_DEV void attn_fwd_task(const mep_attn_desc& d, int qc, int h, int b, int lan
             float mx = -INFINITY;
 #pragma unroll
             for (int kt = 0; kt < NT; ++kt) {
-                const floatx4 st = dot_score<true>(ks[kt], qs, zero4());   // C[key 4g+r][query c]
+                const floatx4 st = dot_score<true, BF>(ks[kt], qs, zero4());   // C[key 4g+r][query c]
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     float spv = 0.f;
@@ -327,6 +348,11 @@ MEP_DEV void attn_fwd_task(const mep_attn_desc& d, int qc, int h, int b, int lan
             // O += P V over the chunk's 64 keys: key-tile pairs (slots 0-3 / 4-7)
 #pragma unroll
             for (int kt = 0; kt < NT; kt += 2) {
+                if (BF) {   // bf16 P (slots: keys 4g+s of tiles kt / kt+1) against bf16 V
+                    oq = mfma(op(pk(sv[kt][0], sv[kt][1]), pk(sv[kt][2], sv[kt][3]), pk(sv[kt + 1][0], sv[kt + 1][1]),
+                                 pk(sv[kt + 1][2], sv[kt + 1][3])), vbf[kt / 2], oq);
+                    continue;
+                }
                 // fp32 MFMA on the raw P and V (exact fp32 fma chain): a bf16 split of P would need
                 // three parts for fp32-level logits, and its VALU cost more than these 8 MFMAs
 #pragma unroll
@@ -352,7 +378,7 @@ MEP_DEV void attn_fwd_task(const mep_attn_desc& d, int qc, int h, int b, int lan
     }
 }
 
-template <bool PREV, bool SOUT, bool SINGLE>
+template <bool PREV, bool SOUT, bool SINGLE, bool BF>
 __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu((SINGLE && !PREV) ? MEP_FWD_WAVES : 2))) void k_attn_fwd(const mep_attn_desc* __restrict__ descs) {
     const mep_attn_desc& d = descs[blockIdx.y];
     if ((d.Tk <= CH) != SINGLE) return;    // the other variant's descriptor
@@ -361,7 +387,7 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu((SINGLE
     const int task = blockIdx.x * WAVES + wave;
     if (task >= d.B * d.H * nqc) return;   // whole wave leaves; no barriers below
     const int qc = task % nqc, bh = task / nqc;
-    attn_fwd_task<PREV, SOUT, SINGLE>(d, qc, bh % d.H, bh / d.H, lane);
+    attn_fwd_task<PREV, SOUT, SINGLE, BF>(d, qc, bh % d.H, bh / d.H, lane);
 }
 
 MEP_DEV void wave_lds_sync() {
@@ -375,8 +401,8 @@ MEP_DEV void wave_lds_sync() {
 // (B of S = K rows with the key on the lane, B of dP = V rows, B of dQ = K columns rows 4g+s /
 // dim c, the keys' mask terms) and the chunk's dK / dV accumulators (C[key 4g+r][dim c]).
 // PREV: residual scores (writes dS_prev, sums the dc partial); DSN: a gradient arrives on this
-// layer's post-mask S output.
-template <bool PREV, bool DSN>
+// layer's post-mask S output; BF: the bf16 path (one bf16 product per contraction).
+template <bool PREV, bool DSN, bool BF>
 struct Bwd {
     // per query tile: A of S (Q rows), A of dP (dO rows), B of dV / dK (dO / Q columns), O
     // columns for delta, row stats and the dq rows this tile accumulates onto
@@ -486,8 +512,8 @@ struct Bwd {
             const int kk = k_lo + kt * 16 + c;
             // recomputed scores on the 2-way split (the forward's are 3-way): P differs from the
             // forward's by <= ~2^-16 relative, far inside the gradient tolerance
-            const floatx4 st = dot16(qs, kb[kt], zero4());               // C[query 4g+r][key c]
-            const floatx4 dp = dot16(do2, vb[kt], zero4());
+            const floatx4 st = dot16<BF>(qs, kb[kt], zero4());           // C[query 4g+r][key c]
+            const floatx4 dp = dot16<BF>(do2, vb[kt], zero4());
             float p[4], dsv[4];
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
@@ -513,15 +539,15 @@ struct Bwd {
                 dsv[r] = gsv;
             }
             const S2 ds2 = split2(dsv);
-            dv[kt] = dot16(split2(p), db2, dv[kt]);      // dV[key][dim] += P^T dO
-            dk[kt] = dot16(ds2, qb2, dk[kt]);            // dK[key][dim] += dS^T Q
+            dv[kt] = dot16<BF>(split2(p), db2, dv[kt]);  // dV[key][dim] += P^T dO
+            dk[kt] = dot16<BF>(ds2, qb2, dk[kt]);        // dK[key][dim] += dS^T Q
             // the split dS, element by element, into Th / Tl[query][key] (bf16)
             const unsigned hw[4] = {ds2.h0, ds2.h0 >> 16, ds2.h1, ds2.h1 >> 16};
             const unsigned lw[4] = {ds2.l0, ds2.l0 >> 16, ds2.l1, ds2.l1 >> 16};
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 Th[(4 * g + r) * TLD2 + kt * 16 + c] = (unsigned short)hw[r];
-                Tl[(4 * g + r) * TLD2 + kt * 16 + c] = (unsigned short)lw[r];
+                if (!BF) Tl[(4 * g + r) * TLD2 + kt * 16 + c] = (unsigned short)lw[r];
             }
         }
         // dQ += dS K with the query on the lane: the transposed 16 x 64 dS parts, already split,
@@ -532,13 +558,13 @@ struct Bwd {
 #pragma unroll
         for (int kt = 0; kt < NT; ++kt) {
             const u32x2 hh = *reinterpret_cast<const lu32x2*>(Th + c * TLD2 + kt * 16 + 4 * g);
-            const u32x2 ll = *reinterpret_cast<const lu32x2*>(Tl + c * TLD2 + kt * 16 + 4 * g);
+            const u32x2 ll = BF ? u32x2{0u, 0u} : *reinterpret_cast<const lu32x2*>(Tl + c * TLD2 + kt * 16 + 4 * g);
             tq[kt] = S2{hh[0], hh[1], ll[0], ll[1]};
         }
         wave_lds_sync();
         floatx4 dq = zero4();
 #pragma unroll
-        for (int kt = 0; kt < NT; kt += 2) dq = dot32(tq[kt], tq[kt + 1], kq[kt], kq[kt + 1], dq);
+        for (int kt = 0; kt < NT; kt += 2) dq = dot32<BF>(tq[kt], tq[kt + 1], kq[kt], kq[kt + 1], dq);
         return dq;
     }
 
@@ -553,7 +579,7 @@ struct Bwd {
 // SHORT (Tk <= 64): one WAVE per (b, h) -- the single key chunk makes the wave the exclusive owner
 // of every dQ row and of its dK / dV rows, so no cross-wave sums are needed; the query tiles are
 // walked with every load of the next tile issued before this tile's math (two register sets).
-template <bool PREV, bool DSN>
+template <bool PREV, bool DSN, bool BF>
 __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(MEP_BWD_WAVES))) void k_attn_bwd_short(const mep_attn_bwd_desc* __restrict__ descs) {
     __shared__ __attribute__((aligned(16))) float Tr[WAVES][TFL];
     const mep_attn_bwd_desc& bd = descs[blockIdx.y];
@@ -561,11 +587,11 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(MEP_BWD
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int bh = blockIdx.x * WAVES + wave;
     if (bh >= bd.f.B * bd.f.H) return;       // whole wave leaves; only wave-private LDS below
-    Bwd<PREV, DSN> u(bd, bh / bd.f.H, bh % bd.f.H, lane);
+    Bwd<PREV, DSN, BF> u(bd, bh / bd.f.H, bh % bd.f.H, lane);
     const int nqt = (u.Tq + 15) / 16;
     u.load_chunk(0);
 #if MEP_BWD_DB
-    typename Bwd<PREV, DSN>::QIn bufA, bufB;
+    typename Bwd<PREV, DSN, BF>::QIn bufA, bufB;
     u.fetch(bufA, 0);
     for (int qt = 0; qt < nqt; qt += 2) {
         u.fetch(bufB, qt + 1);               // past the end: range-checked zeros, never used
@@ -577,7 +603,7 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(MEP_BWD
     }
 #else
     for (int qt = 0; qt < nqt; ++qt) {
-        typename Bwd<PREV, DSN>::QIn in;
+        typename Bwd<PREV, DSN, BF>::QIn in;
         u.fetch(in, qt);
         u.store_dq(in, qt, u.tile(in, qt, Tr[wave]));
     }
@@ -607,7 +633,7 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(MEP_BWD
 // and a tile's dQ is carried across chunks in (wave-private) LDS, so every sum has a fixed order.
 // LDS: [RED] dK/dV partials (aliased by the waves' dS transposes during the query loop), [4] dc
 // partials, [dq_tiles][256] the carried dQ tiles.
-template <bool PREV, bool DSN>
+template <bool PREV, bool DSN, bool BF>
 __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(2))) void k_attn_bwd_long(const mep_attn_bwd_desc* __restrict__ descs) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     const mep_attn_bwd_desc& bd = descs[blockIdx.y];
@@ -615,7 +641,7 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(2))) vo
     const int bh = blockIdx.x;
     if (d.Tk <= CH || bh >= d.B * d.H) return;   // a SHORT descriptor / past the end: the whole workgroup
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    Bwd<PREV, DSN> u(bd, bh / d.H, bh % d.H, lane);
+    Bwd<PREV, DSN, BF> u(bd, bh / d.H, bh % d.H, lane);
     const int D = d.H * HD;
     const int nqt = (u.Tq + 15) / 16, nkc = (u.Tk + CH - 1) / CH;
     const int nw = min(WAVES, nqt);          // waves that own query tiles
@@ -628,7 +654,7 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(2))) vo
     for (int kc = 0; kc < nkc; ++kc) {
         u.load_chunk(kc);
         for (int qt = wave; qt < nqt; qt += WAVES) {
-            typename Bwd<PREV, DSN>::QIn in;
+            typename Bwd<PREV, DSN, BF>::QIn in;
             u.fetch(in, qt);
             floatx4 dq = u.tile(in, qt, Tr);
             floatx4* carry = reinterpret_cast<floatx4*>(DQ + qt * 256) + lane;
@@ -689,10 +715,11 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(2))) vo
 extern "C" int mep_attn_fwd(const mep_attn_desc* descs, int n_desc, int max_tiles, int flags, mep_stream_t stream) {
     if (n_desc <= 0 || max_tiles <= 0) return 0;
     if (!(flags & (MEP_ATTN_SHORT | MEP_ATTN_LONG))) { mep_set_error("mep_attn_fwd: flags need SHORT and/or LONG"); return MEP_EINVAL; }
-    const bool prev = flags & MEP_ATTN_PREV, sout = flags & MEP_ATTN_SOUT;
+    const bool prev = flags & MEP_ATTN_PREV, sout = flags & MEP_ATTN_SOUT, bf = flags & MEP_PREC_BF16;
     const dim3 grid(max_tiles, n_desc), block(THREADS);
     hipStream_t st = (hipStream_t)stream;
-#define MEP_FWD(P, S, SI) hipLaunchKernelGGL((k_attn_fwd<P, S, SI>), grid, block, 0, st, descs)
+#define MEP_FWD(P, S, SI) \
+    do { if (bf) hipLaunchKernelGGL((k_attn_fwd<P, S, SI, true>), grid, block, 0, st, descs); else hipLaunchKernelGGL((k_attn_fwd<P, S, SI, false>), grid, block, 0, st, descs); } while (0)
     for (int single = 1; single >= 0; --single) {
         if (!(flags & (single ? MEP_ATTN_SHORT : MEP_ATTN_LONG))) continue;
         if (single) {
@@ -711,14 +738,15 @@ extern "C" int mep_attn_bwd(const mep_attn_bwd_desc* descs, int n_desc, int max_
                             mep_stream_t stream) {
     if (n_desc <= 0 || max_tiles <= 0) return 0;
     if (!(flags & (MEP_ATTN_SHORT | MEP_ATTN_LONG))) { mep_set_error("mep_attn_bwd: flags need SHORT and/or LONG"); return MEP_EINVAL; }
-    const bool prev = flags & MEP_ATTN_PREV, dsn = flags & MEP_ATTN_SOUT;
-    const int dq_tiles = flags >> 8;
+    const bool prev = flags & MEP_ATTN_PREV, dsn = flags & MEP_ATTN_SOUT, bf = flags & MEP_PREC_BF16;
+    const int dq_tiles = (flags >> 8) & 0xff;
     const size_t lds = sizeof(float) * ((size_t)RED + WAVES + 256 * (size_t)dq_tiles);
     if (lds > 160 * 1024) { mep_set_error("mep_attn_bwd: Tq too large for the LDS-carried dQ (Tk > 64)"); return MEP_EINVAL; }
     hipStream_t st = (hipStream_t)stream;
     if (flags & MEP_ATTN_SHORT) {
         const dim3 grid((max_tiles + WAVES - 1) / WAVES, n_desc), block(THREADS);
-#define MEP_BS(P, S) hipLaunchKernelGGL((k_attn_bwd_short<P, S>), grid, block, 0, st, descs)
+#define MEP_BS(P, S) \
+    do { if (bf) hipLaunchKernelGGL((k_attn_bwd_short<P, S, true>), grid, block, 0, st, descs); else hipLaunchKernelGGL((k_attn_bwd_short<P, S, false>), grid, block, 0, st, descs); } while (0)
         if (prev) { if (dsn) MEP_BS(true, true); else MEP_BS(true, false); }
         else      { if (dsn) MEP_BS(false, true); else MEP_BS(false, false); }
 #undef MEP_BS
@@ -727,14 +755,16 @@ extern "C" int mep_attn_bwd(const mep_attn_bwd_desc* descs, int n_desc, int max_
         static bool lds_attr = false;   // allow more than 64 KB of dynamic LDS (long Tq)
         if (!lds_attr) {
             const int mx = 160 * 1024;
-            (void)hipFuncSetAttribute((const void*)k_attn_bwd_long<true, true>, hipFuncAttributeMaxDynamicSharedMemorySize, mx);
-            (void)hipFuncSetAttribute((const void*)k_attn_bwd_long<true, false>, hipFuncAttributeMaxDynamicSharedMemorySize, mx);
-            (void)hipFuncSetAttribute((const void*)k_attn_bwd_long<false, true>, hipFuncAttributeMaxDynamicSharedMemorySize, mx);
-            (void)hipFuncSetAttribute((const void*)k_attn_bwd_long<false, false>, hipFuncAttributeMaxDynamicSharedMemorySize, mx);
+            const void* fns[] = {(const void*)k_attn_bwd_long<true, true, false>, (const void*)k_attn_bwd_long<true, false, false>,
+                                 (const void*)k_attn_bwd_long<false, true, false>, (const void*)k_attn_bwd_long<false, false, false>,
+                                 (const void*)k_attn_bwd_long<true, true, true>, (const void*)k_attn_bwd_long<true, false, true>,
+                                 (const void*)k_attn_bwd_long<false, true, true>, (const void*)k_attn_bwd_long<false, false, true>};
+            for (const void* f : fns) (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, mx);
             lds_attr = true;
         }
         const dim3 grid(max_tiles, n_desc), block(THREADS);
-#define MEP_BL(P, S) hipLaunchKernelGGL((k_attn_bwd_long<P, S>), grid, block, lds, st, descs)
+#define MEP_BL(P, S) \
+    do { if (bf) hipLaunchKernelGGL((k_attn_bwd_long<P, S, true>), grid, block, lds, st, descs); else hipLaunchKernelGGL((k_attn_bwd_long<P, S, false>), grid, block, lds, st, descs); } while (0)
         if (prev) { if (dsn) MEP_BL(true, true); else MEP_BL(true, false); }
         else      { if (dsn) MEP_BL(false, true); else MEP_BL(false, false); }
 #undef MEP_BL

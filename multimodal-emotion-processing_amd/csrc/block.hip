@@ -7,14 +7,16 @@
 // block and keeps that block's weights in LDS; each wave runs whole tiles through all products in
 // the transposed-tile formulation (common.h), so activations never pass through LDS and the
 // concat [q | xp] is two accumulating passes.
-// Arithmetic (D <= 96): fp32 operands split into three bf16 parts on the bf16 matrix cores (split.h:
+// Arithmetic, fp32 path (D <= 96): fp32 operands split into three bf16 parts on the bf16 matrix cores (split.h:
 // six products per k pair, fp32-level error, 2.7x the fp32-MFMA rate).  The weights are staged in
 // LDS already split, once per workgroup.  The split Wp and Wm together would need 184 KB, so a
 // workgroup runs its tiles in two phases, one weight resident per phase: forward (1) xp = Wp x,
 // stored, (2) z = Wm [q | xp] re-reading its own xp rows (L2-hot) + LayerNorm; backward (1) the
 // LayerNorm backward, dxp and dq with Wm^T, (2) dx = Wp^T dxp.  The first tile of each phase is
 // loaded while the weight of that phase is staged.  D = 128 (Ren-MME) runs the exact fp32 MFMA
-// path (its split Wm alone would need 210 KB of LDS).
+// path (its split Wm alone would need 210 KB of LDS).  bf16 path (MEP_PREC_BF16, every D): the
+// same two-phase kernels with one bf16 part per operand -- one MFMA per k pair, fp32 accumulate,
+// LayerNorm and dropout in fp32.
 #include "common.h"
 #include "split.h"
 
@@ -191,8 +193,8 @@ MEP_DEV void epi_fwd_tiles(const mep_epi_desc& d, const AP& wp, const AM& wm, in
 
 // stage W [R][C] (fp32, row stride C) split into LDS: unit (n, p, g) = W[n][32p + 4g ..] and
 // W[n][32p + 16 + 4g ..]; every load of the thread is issued before its first LDS write
-template <int R, int C>
-MEP_DEV void stage_split_rows(const SplitW<R, C / 32>& dst, const gfloat* src) {
+template <int R, int C, int NPART>
+MEP_DEV void stage_split_rows(const SplitW<R, C / 32, NPART>& dst, const gfloat* src) {
     constexpr int NU = R * (C / 32) * 4;
     constexpr int PER = (NU + ETHREADS - 1) / ETHREADS;
     f32x4 v[PER][2];
@@ -218,8 +220,8 @@ MEP_DEV void stage_split_rows(const SplitW<R, C / 32>& dst, const gfloat* src) {
 // stage W^T of W [R][C] (fp32, row stride C) split into LDS (rows = the C columns of W, k = the R
 // rows): unit (n, p, g) = W[32p + 4g + j][n] and W[32p + 16 + 4g + j][n], j < 4; consecutive
 // threads take consecutive n (coalesced), loads issued before the LDS writes
-template <int R, int C>
-MEP_DEV void stage_split_cols(const SplitW<C, R / 32>& dst, const gfloat* src) {
+template <int R, int C, int NPART>
+MEP_DEV void stage_split_cols(const SplitW<C, R / 32, NPART>& dst, const gfloat* src) {
     constexpr int NP = R / 32, NU = C * NP * 4;
     constexpr int PER = (NU + ETHREADS - 1) / ETHREADS;
     float v[PER][8];
@@ -253,11 +255,12 @@ MEP_DEV void wg_store_barrier() {
     __syncthreads();
 }
 
-template <int D>
+template <int D, int NPART>
 MEP_DEV void epi_fwd_split(const mep_epi_desc& d, unsigned char* sm, int t_begin, int t_end) {
     constexpr int NI = D / 16, KB = D / 16, NP = D / 32;
-    using WP = SplitW<D, NP>;
-    using WM = SplitW<D, 2 * NP>;
+    using WP = SplitW<D, NP, NPART>;
+    using WM = SplitW<D, 2 * NP, NPART>;
+    using Op = OpN<NPART>;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int c = lane & 15, g = lane >> 4;
     const int ntok = d.ntok;
@@ -275,18 +278,18 @@ MEP_DEV void epi_fwd_split(const mep_epi_desc& d, unsigned char* sm, int t_begin
     };
     // ---- phase 1: xp = drop(x Wp^T)
     if (t_begin + wave < t_end) rows_of(d.x, t_begin + wave, ab);
-    stage_split_rows<D, D>(wp, G<const float>(d.wp));
+    stage_split_rows<D, D, NPART>(wp, G<const float>(d.wp));
     __syncthreads();
     for (int tile = t_begin + wave; tile < t_end; tile += EWAVES) {
         const int tok = tile * 16 + c;
-        Op3 xs[NP];
+        Op xs[NP];
 #pragma unroll
-        for (int pp = 0; pp < NP; ++pp) xs[pp] = op3(ab[2 * pp], ab[2 * pp + 1]);
+        for (int pp = 0; pp < NP; ++pp) xs[pp] = opn<NPART>(ab[2 * pp], ab[2 * pp + 1]);
         if (tile + EWAVES < t_end) rows_of(d.x, tile + EWAVES, ab);
         f32x4 xp[NI];
 #pragma unroll
         for (int i = 0; i < NI; ++i) xp[i] = zero_f4();
-        tgemm6<NI, NP>(xp, [&](int i, int pp) { return wp.frag(i, pp); }, [&](int pp) { return xs[pp]; });
+        tgemm_n<NI, NP, NPART>(xp, [&](int i, int pp) { return wp.frag(i, pp); }, [&](int pp) { return xs[pp]; });
         if (tok < ntok) {
             gfloat* pr = row_ptr(d.xp, tok);
 #pragma unroll
@@ -304,19 +307,19 @@ MEP_DEV void epi_fwd_split(const mep_epi_desc& d, unsigned char* sm, int t_begin
     if (t_begin + wave < t_end) rows_of(d.q, t_begin + wave, ab);
     wg_store_barrier();              // xp rows stored; Wp no longer read
     if (t_begin + wave < t_end) rows_of(d.xp, t_begin + wave, bb);
-    stage_split_rows<D, 2 * D>(wm, G<const float>(d.wm));
+    stage_split_rows<D, 2 * D, NPART>(wm, G<const float>(d.wm));
     __syncthreads();
     for (int tile = t_begin + wave; tile < t_end; tile += EWAVES) {
         const int tok = tile * 16 + c;
-        Op3 qs[NP], ps[NP];
+        Op qs[NP], ps[NP];
 #pragma unroll
-        for (int pp = 0; pp < NP; ++pp) { qs[pp] = op3(ab[2 * pp], ab[2 * pp + 1]); ps[pp] = op3(bb[2 * pp], bb[2 * pp + 1]); }
+        for (int pp = 0; pp < NP; ++pp) { qs[pp] = opn<NPART>(ab[2 * pp], ab[2 * pp + 1]); ps[pp] = opn<NPART>(bb[2 * pp], bb[2 * pp + 1]); }
         if (tile + EWAVES < t_end) { rows_of(d.q, tile + EWAVES, ab); rows_of(d.xp, tile + EWAVES, bb); }
         f32x4 z[NI];
 #pragma unroll
         for (int i = 0; i < NI; ++i) z[i] = zero_f4();
-        tgemm6<NI, NP>(z, [&](int i, int pp) { return wm.frag(i, pp); }, [&](int pp) { return qs[pp]; });
-        tgemm6<NI, NP>(z, [&](int i, int pp) { return wm.frag(i, NP + pp); }, [&](int pp) { return ps[pp]; });
+        tgemm_n<NI, NP, NPART>(z, [&](int i, int pp) { return wm.frag(i, pp); }, [&](int pp) { return qs[pp]; });
+        tgemm_n<NI, NP, NPART>(z, [&](int i, int pp) { return wm.frag(i, NP + pp); }, [&](int pp) { return ps[pp]; });
         float sum = 0.f;
 #pragma unroll
         for (int i = 0; i < NI; ++i) sum += (z[i][0] + z[i][1]) + (z[i][2] + z[i][3]);
@@ -352,11 +355,12 @@ MEP_DEV void epi_fwd_split(const mep_epi_desc& d, unsigned char* sm, int t_begin
     }
 }
 
-template <int D>
+template <int D, int NPART>
 MEP_DEV void epi_bwd_split(const mep_epi_bwd_desc& bd, unsigned char* sm, int t_begin, int t_end) {
     constexpr int NI = D / 16, KB = D / 16, NP = D / 32;
-    using WMT = SplitW<2 * D, NP>;
-    using WPT = SplitW<D, NP>;
+    using WMT = SplitW<2 * D, NP, NPART>;
+    using WPT = SplitW<D, NP, NPART>;
+    using Op = OpN<NPART>;
     const mep_epi_desc& d = bd.f;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int c = lane & 15, g = lane >> 4;
@@ -384,7 +388,7 @@ MEP_DEV void epi_bwd_split(const mep_epi_bwd_desc& bd, unsigned char* sm, int t_
     };
     // ---- phase 1: LayerNorm backward, dxp = drop'(dz Wm[:, D:]), dq (+)= dz Wm[:, :D]
     if (t_begin + wave < t_end) fetch1(t_begin + wave);
-    stage_split_cols<D, 2 * D>(wmt, G<const float>(d.wm));
+    stage_split_cols<D, 2 * D, NPART>(wmt, G<const float>(d.wm));
     __syncthreads();
     for (int tile = t_begin + wave; tile < t_end; tile += EWAVES) {
         const int tok = tile * 16 + c;
@@ -438,13 +442,13 @@ MEP_DEV void epi_bwd_split(const mep_epi_bwd_desc& bd, unsigned char* sm, int t_
                 const float x = (zz[i][r] - mu) * rs;
                 dz[i][r] = ok ? rs * (dz[i][r] - s1 - x * s2) : 0.f;
             }
-        Op3 dzb[NP];
+        Op dzb[NP];
 #pragma unroll
-        for (int pp = 0; pp < NP; ++pp) dzb[pp] = op3(dz[2 * pp], dz[2 * pp + 1]);
+        for (int pp = 0; pp < NP; ++pp) dzb[pp] = opn<NPART>(dz[2 * pp], dz[2 * pp + 1]);
         f32x4 acc[NI];
 #pragma unroll
         for (int i = 0; i < NI; ++i) acc[i] = zero_f4();
-        tgemm6<NI, NP>(acc, [&](int i, int pp) { return wmt_x.frag(i, pp); }, [&](int pp) { return dzb[pp]; });
+        tgemm_n<NI, NP, NPART>(acc, [&](int i, int pp) { return wmt_x.frag(i, pp); }, [&](int pp) { return dzb[pp]; });
         if (ok) {
             gfloat* dzr = row_ptr(bd.dz, tok);
             gfloat* dpr = row_ptr(bd.dxp, tok);
@@ -461,7 +465,7 @@ MEP_DEV void epi_bwd_split(const mep_epi_bwd_desc& bd, unsigned char* sm, int t_
         }
 #pragma unroll
         for (int i = 0; i < NI; ++i) acc[i] = zero_f4();
-        tgemm6<NI, NP>(acc, [&](int i, int pp) { return wmt.frag(i, pp); }, [&](int pp) { return dzb[pp]; });
+        tgemm_n<NI, NP, NPART>(acc, [&](int i, int pp) { return wmt.frag(i, pp); }, [&](int pp) { return dzb[pp]; });
         if (ok) {
             gfloat* qrw = row_ptr(bd.dq, tok);
 #pragma unroll
@@ -480,18 +484,18 @@ MEP_DEV void epi_bwd_split(const mep_epi_bwd_desc& bd, unsigned char* sm, int t_
         for (int kb = 0; kb < KB; ++kb) ga[kb] = ld4w(r + 16 * kb);
     };
     if (t_begin + wave < t_end) fetch2(t_begin + wave);
-    stage_split_cols<D, D>(wpt, G<const float>(d.wp));
+    stage_split_cols<D, D, NPART>(wpt, G<const float>(d.wp));
     __syncthreads();
     for (int tile = t_begin + wave; tile < t_end; tile += EWAVES) {
         const int tok = tile * 16 + c;
-        Op3 xs[NP];
+        Op xs[NP];
 #pragma unroll
-        for (int pp = 0; pp < NP; ++pp) xs[pp] = op3(ga[2 * pp], ga[2 * pp + 1]);
+        for (int pp = 0; pp < NP; ++pp) xs[pp] = opn<NPART>(ga[2 * pp], ga[2 * pp + 1]);
         if (tile + EWAVES < t_end) fetch2(tile + EWAVES);
         f32x4 acc[NI];
 #pragma unroll
         for (int i = 0; i < NI; ++i) acc[i] = zero_f4();
-        tgemm6<NI, NP>(acc, [&](int i, int pp) { return wpt.frag(i, pp); }, [&](int pp) { return xs[pp]; });
+        tgemm_n<NI, NP, NPART>(acc, [&](int i, int pp) { return wpt.frag(i, pp); }, [&](int pp) { return xs[pp]; });
         if (tok < ntok) {
             gfloat* xrw = row_ptr(bd.dx, tok);
 #pragma unroll
@@ -500,16 +504,19 @@ MEP_DEV void epi_bwd_split(const mep_epi_bwd_desc& bd, unsigned char* sm, int t_
     }
 }
 
-template <int D>
+// BF16: the bf16 path (one part per operand, every D); otherwise D <= 96 runs the 3-part split
+// and D = 128 the fp32 MFMA path
+template <int D, bool BF16>
 __global__ __launch_bounds__(ETHREADS) void k_epi_fwd(const mep_epi_desc* __restrict__ descs) {
     using Geo = EpiGeo<D>;
     const mep_epi_desc& d = descs[blockIdx.y];
     int t_begin, t_end;
     if (!tile_range(d.ntok, t_begin, t_end)) return;   // whole workgroup
-    if constexpr (MEP_EPI_SPLIT && D <= 96) {
-        constexpr int BYTES = SplitW<D, D / 16>::BYTES;   // the larger phase (Wm)
+    if constexpr (BF16 || (MEP_EPI_SPLIT && D <= 96)) {
+        constexpr int NPART = BF16 ? 1 : 3;
+        constexpr int BYTES = SplitW<D, D / 16, NPART>::BYTES;   // the larger phase (Wm)
         __shared__ __attribute__((aligned(16))) unsigned char sm6[BYTES];
-        epi_fwd_split<D>(d, sm6, t_begin, t_end);
+        epi_fwd_split<D, NPART>(d, sm6, t_begin, t_end);
         return;
     }
     __shared__ __attribute__((aligned(16))) float smem[Geo::FWD];
@@ -651,17 +658,18 @@ MEP_DEV void epi_bwd_tiles(const mep_epi_bwd_desc& bd, const AM& wmt, const AP& 
     }
 }
 
-template <int D>
+template <int D, bool BF16>
 __global__ __launch_bounds__(ETHREADS) void k_epi_bwd(const mep_epi_bwd_desc* __restrict__ descs) {
     using Geo = EpiGeo<D>;
     const mep_epi_bwd_desc& bd = descs[blockIdx.y];
     const mep_epi_desc& d = bd.f;
     int t_begin, t_end;
     if (!tile_range(d.ntok, t_begin, t_end)) return;
-    if constexpr (MEP_EPI_SPLIT && D <= 96) {
-        constexpr int BYTES = SplitW<2 * D, D / 32>::BYTES;   // the larger phase (Wm^T)
+    if constexpr (BF16 || (MEP_EPI_SPLIT && D <= 96)) {
+        constexpr int NPART = BF16 ? 1 : 3;
+        constexpr int BYTES = SplitW<2 * D, D / 32, NPART>::BYTES;   // the larger phase (Wm^T)
         __shared__ __attribute__((aligned(16))) unsigned char sm6[BYTES];
-        epi_bwd_split<D>(bd, sm6, t_begin, t_end);
+        epi_bwd_split<D, NPART>(bd, sm6, t_begin, t_end);
         return;
     }
     __shared__ __attribute__((aligned(16))) float smem[Geo::BWD];
@@ -774,9 +782,12 @@ int dispatch_D(int D, F&& f) {
 
 extern "C" int mep_block_epi_fwd(const mep_epi_desc* descs, int n_desc, int max_tiles, int D, mep_stream_t stream) {
     if (n_desc <= 0 || max_tiles <= 0) return 0;
-    const int rc = dispatch_D(D, [&](auto dc) {
-        hipLaunchKernelGGL(k_epi_fwd<decltype(dc)::value>, dim3(max_tiles, n_desc), dim3(ETHREADS), 0,
-                           (hipStream_t)stream, descs);
+    const bool bf16 = D & MEP_PREC_BF16;
+    const int rc = dispatch_D(D & ~MEP_PREC_BF16, [&](auto dc) {
+        if (bf16) hipLaunchKernelGGL((k_epi_fwd<decltype(dc)::value, true>), dim3(max_tiles, n_desc), dim3(ETHREADS), 0,
+                                     (hipStream_t)stream, descs);
+        else hipLaunchKernelGGL((k_epi_fwd<decltype(dc)::value, false>), dim3(max_tiles, n_desc), dim3(ETHREADS), 0,
+                                (hipStream_t)stream, descs);
     });
     if (rc) { mep_set_error("mep_block_epi_fwd: D must be 32, 64, 96 or 128"); return rc; }
     return mep_check_launch("mep_block_epi_fwd");
@@ -784,9 +795,12 @@ extern "C" int mep_block_epi_fwd(const mep_epi_desc* descs, int n_desc, int max_
 
 extern "C" int mep_block_epi_bwd(const mep_epi_bwd_desc* descs, int n_desc, int max_tiles, int D, mep_stream_t stream) {
     if (n_desc <= 0 || max_tiles <= 0) return 0;
-    const int rc = dispatch_D(D, [&](auto dc) {
-        hipLaunchKernelGGL(k_epi_bwd<decltype(dc)::value>, dim3(max_tiles, n_desc), dim3(ETHREADS), 0,
-                           (hipStream_t)stream, descs);
+    const bool bf16 = D & MEP_PREC_BF16;
+    const int rc = dispatch_D(D & ~MEP_PREC_BF16, [&](auto dc) {
+        if (bf16) hipLaunchKernelGGL((k_epi_bwd<decltype(dc)::value, true>), dim3(max_tiles, n_desc), dim3(ETHREADS), 0,
+                                     (hipStream_t)stream, descs);
+        else hipLaunchKernelGGL((k_epi_bwd<decltype(dc)::value, false>), dim3(max_tiles, n_desc), dim3(ETHREADS), 0,
+                                (hipStream_t)stream, descs);
     });
     if (rc) { mep_set_error("mep_block_epi_bwd: D must be 32, 64, 96 or 128"); return rc; }
     return mep_check_launch("mep_block_epi_bwd");

@@ -1,4 +1,5 @@
-// Token GEMM (nn.Linear over token rows) and weight-gradient GEMM, fp32 MFMA 16x16x4.
+// Token GEMM (nn.Linear over token rows, fp32 MFMA 16x16x4) and weight-gradient GEMM (bf16 MFMA
+// 32x32x16 on split or plain bf16 operands).
 //
 // mep_gemm : Y[tok, n] = act(alpha * X[tok,:] . W(n,:) + bias[n] + table[tok % T, n]) (+Y)
 //            one workgroup = 64 tokens x all N columns; 8 waves; task (m-half, 32-col block)
@@ -8,6 +9,7 @@
 //            realformer w_qkv / FFN Linears (others/realformer.py:157,163-168).
 // mep_wgrad: dW_i = A^T B_i over token chunks (see the kernel comment below).
 #include "common.h"
+#include "split.h"
 
 using namespace mep;
 
@@ -133,20 +135,27 @@ __global__ __launch_bounds__(GEMM_THREADS) void k_gemm(const mep_gemm_desc* __re
 }
 
 // ---------------------------------------------------------------- weight gradient
-// dW[n][k] = sum_t A[t][n] B[t][k]: a long token reduction into a small (<= 128-row) output.
-// f32 MFMA 32x32x2 with the token axis as the MFMA k: per token pair a lane needs ONE element of
-// each operand column it owns (lane l: column 32 i + (l & 31) of row tile i / column tile j,
-// token 2 s + (l >> 5)), so operands go straight from HBM into registers -- no LDS staging, no
-// block barriers in the main loop.  A wave keeps a whole MT x KT block of 32x32 tiles in
-// accumulators (MT = ceil(N/32) covers every output row; KT = 3, 2, 4, 4 for MT = 3, 4, 2, 1) and
-// WG_P token pairs of loads in flight, so every lane issues MT + KT dword loads per MT * KT MFMAs.
-// One workgroup = 4 waves (one per SIMD) on consecutive quarters of a tok_per_split chunk and
-// one column group; the four accumulator blocks are summed through LDS in a fixed order
+// dW[n][k] = sum_t A[t][n] B[t][k]: a long token reduction into a small (<= 128-row) output, on
+// v_mfma_f32_32x32x16_bf16 with the token axis as the MFMA k.  Lane l (column c = l & 31, half
+// h = l >> 5) supplies A[row c][k = 8h + j] and B[k = 8h + j][col c], j < 8: eight tokens of ONE
+// operand column, so operands go straight from HBM into registers (dword loads, 32 lanes on 32
+// consecutive floats of a row) -- no LDS staging, no block barriers in the main loop.  The lane
+// halves walk two halves of the wave's token range one token at a time (one wrap check per step,
+// no divisions), eight tokens per MFMA k block.  fp32 path: every 8-token operand is split into
+// three bf16 parts (split.h, six products per k block: fp32-level error, 2.7x the f32-MFMA rate);
+// bf16 path (desc.bf16): one bf16 part, one product.  A wave keeps a whole MT x KT block of 32x32
+// tiles in accumulators (MT = ceil(N/32) covers every output row; KT = 3, 2, 4, 4 for MT = 3, 4,
+// 2, 1) and WG_PF k blocks of loads in flight beyond the one being multiplied.  One workgroup = 4
+// waves (one per SIMD, ~400 VGPRs each) on consecutive quarters of a tok_per_split chunk and one
+// column group; the four accumulator blocks are summed through LDS in a fixed order
 // ((w0 + w2) + (w1 + w3)) and written once as partial[split][n][k]; mep_wgrad_reduce sums the
 // splits.  Row views are addressed with 32-bit offsets (hosts keep every view under 2^31 floats).
+#ifndef MEP_WG_PF
+#define MEP_WG_PF 1   // 2 would need ~300 arch VGPRs (spills): double-buffered operands
+#endif
 constexpr int WG_WAVES = 4;
 constexpr int WG_THREADS = 64 * WG_WAVES;
-constexpr int WG_P = 6;                        // token pairs in flight per lane
+constexpr int WG_SLOTS = MEP_WG_PF + 1;       // k blocks of operand registers
 constexpr int WG_RED = 96 * (96 + 8);          // largest 32MT x (32KT + 8) reduction buffer (MT = KT = 3)
 
 MEP_DEV int wg_kt(int mt) { return mt == 4 ? 2 : mt == 3 ? 3 : 4; }
@@ -160,35 +169,29 @@ MEP_DEV int wg_extent(const mep_rows& r, int T, int ntok, int width) {
 
 constexpr int WG_INV = (int)0x80000000u;   // byte offset past every view: the buffer load returns 0
 
-template <int MT, int KT>
+template <int MT, int KT, int NPART>
 MEP_DEV void wgrad_task(const mep_wgrad_desc& d, int split, int kbase, lfloat* red) {
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int c = lane & 31, g = lane >> 5;
+    const int c = lane & 31, h = lane >> 5;
     const int N = d.N;
     const int t_begin = split * d.tok_per_split;
     const int t_end = min(d.ntok, t_begin + d.tok_per_split);
-    const int per_wave = d.tok_per_split / WG_WAVES;           // even (host)
+    const int per_wave = d.tok_per_split / WG_WAVES;
     const int w0 = t_begin + wave * per_wave;
-    const int w1 = min(t_end, w0 + per_wave);
-    const int npairs = w1 > w0 ? (w1 - w0 + 1) >> 1 : 0;       // an odd last token pairs with a zero
+    const int n = max(0, min(t_end, w0 + per_wave) - w0);
+    const int half = (n + 1) >> 1;                         // tokens of lane half 0 (half 1: n - half)
+    const int nh = h ? n - half : half;
+    const int nblk = (half + 7) >> 3;                      // k blocks (wave-uniform)
 
-    // Every view of the item shares T; a T = 1 view is addressed as T = 2 (sT = sB, sB = 2 sB) so
-    // that one wrap check per 2-token advance suffices.
-    const int T0 = d.a.T;
-    const int T = T0 == 1 ? 2 : T0;
-    auto strides = [&](const mep_rows& r, int& sB, int& sT) {
-        sB = (int)(T0 == 1 ? 2 * r.sB : r.sB);
-        sT = (int)(T0 == 1 ? r.sB : r.sT);
-    };
+    const int T = d.a.T;   // every view of the item shares T
     // Operand columns of this lane, clamped in range: a column past N (past Ktot) only feeds
-    // output rows (columns) that are never stored.  Tokens past the wave's range read 0 through
-    // the buffer range check (offset WG_INV), so no select sits between a load and its MFMA.
-    const auto rsA = __builtin_amdgcn_make_buffer_rsrc((void*)d.a.ptr, 0, wg_extent(d.a, T0, d.ntok, N), 0x00020000);
+    // output rows (columns) that are never stored.  Tokens past the lane half's range read 0
+    // through the buffer range check (offset WG_INV).
+    const auto rsA = __builtin_amdgcn_make_buffer_rsrc((void*)d.a.ptr, 0, wg_extent(d.a, T, d.ntok, N), 0x00020000);
     int colA[MT];
 #pragma unroll
     for (int i = 0; i < MT; ++i) colA[i] = 4 * min(32 * i + c, N - 1);
-    int asB, asT;
-    strides(d.a, asB, asT);
+    const int asB = (int)d.a.sB, asT = (int)d.a.sT;
     __amdgpu_buffer_rsrc_t rsB[KT];
     int colB[KT], bsB[KT], bsT[KT];
 #pragma unroll
@@ -197,9 +200,10 @@ MEP_DEV void wgrad_task(const mep_wgrad_desc& d, int split, int kbase, lfloat* r
         int k0 = min(kbase + 32 * j, d.Ktot - 1), o = 0;
         while (o < d.n_b - 1 && k0 >= d.kb[o]) { k0 -= d.kb[o]; ++o; }
         const mep_rows& b = d.b[o];
-        rsB[j] = __builtin_amdgcn_make_buffer_rsrc((void*)b.ptr, 0, wg_extent(b, T0, d.ntok, d.kb[o]), 0x00020000);
+        rsB[j] = __builtin_amdgcn_make_buffer_rsrc((void*)b.ptr, 0, wg_extent(b, T, d.ntok, d.kb[o]), 0x00020000);
         colB[j] = 4 * min(k0 + c, d.kb[o] - 1);
-        strides(b, bsB[j], bsT[j]);
+        bsB[j] = (int)b.sB;
+        bsT[j] = (int)b.sT;
     }
 
     floatx16 acc[MT][KT];
@@ -210,11 +214,10 @@ MEP_DEV void wgrad_task(const mep_wgrad_desc& d, int split, int kbase, lfloat* r
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-    // load cursor: token tok = (b, t) of this lane and its element offsets offA / offB[j],
-    // advanced by two tokens per pair with one wrap check (T >= 2): no multiplies in the loop
-    int tok = w0 + g, t, offA, offB[KT];
+    // load cursor: this lane's next token (b, t) and its element offsets, one token per step
+    int idx = 0, t, offA, offB[KT];
     {
-        const int tq = min(tok, d.ntok - 1);
+        const int tq = min(w0 + h * half, d.ntok - 1);
         const int bq = tq / T, tt = tq - bq * T;
         t = tt;
         offA = bq * asB + tt * asT;
@@ -226,54 +229,58 @@ MEP_DEV void wgrad_task(const mep_wgrad_desc& d, int split, int kbase, lfloat* r
 #pragma unroll
     for (int j = 0; j < KT; ++j) wB[j] = bsB[j] - T * bsT[j];
 
-    float ra[WG_P][MT], rb[WG_P][KT];
+    float ra[WG_SLOTS][MT][8], rb[WG_SLOTS][KT][8];
     auto load = [&](int p) {
-        const bool ok = tok < w1;
-        const int va = ok ? 4 * offA : WG_INV;
 #pragma unroll
-        for (int i = 0; i < MT; ++i)
-            ra[p][i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsA, va + colA[i], 0, 0));
+        for (int e = 0; e < 8; ++e) {
+            const bool ok = idx < nh;
+            const int va = ok ? 4 * offA : WG_INV;
 #pragma unroll
-        for (int j = 0; j < KT; ++j)
-            rb[p][j] = __builtin_bit_cast(
-                float, __builtin_amdgcn_raw_buffer_load_b32(rsB[j], (ok ? 4 * offB[j] : WG_INV) + colB[j], 0, 0));
-        tok += 2;
-        t += 2;
-        const bool wrap = t >= T;
-        t -= wrap ? T : 0;
-        offA += 2 * asT + (wrap ? wA : 0);
+            for (int i = 0; i < MT; ++i)
+                ra[p][i][e] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsA, va + colA[i], 0, 0));
 #pragma unroll
-        for (int j = 0; j < KT; ++j) offB[j] += 2 * bsT[j] + (wrap ? wB[j] : 0);
+            for (int j = 0; j < KT; ++j)
+                rb[p][j][e] = __builtin_bit_cast(
+                    float, __builtin_amdgcn_raw_buffer_load_b32(rsB[j], (ok ? 4 * offB[j] : WG_INV) + colB[j], 0, 0));
+            ++idx;
+            ++t;
+            const bool wrap = t >= T;
+            t -= wrap ? T : 0;
+            offA += asT + (wrap ? wA : 0);
+#pragma unroll
+            for (int j = 0; j < KT; ++j) offB[j] += bsT[j] + (wrap ? wB[j] : 0);
+        }
     };
     auto mma = [&](int p) {
+        OpN<NPART> bo[KT];
 #pragma unroll
-        for (int i = 0; i < MT; ++i)
+        for (int j = 0; j < KT; ++j)
+            bo[j] = opn<NPART>(f32x4{rb[p][j][0], rb[p][j][1], rb[p][j][2], rb[p][j][3]},
+                               f32x4{rb[p][j][4], rb[p][j][5], rb[p][j][6], rb[p][j][7]});
 #pragma unroll
-            for (int j = 0; j < KT; ++j) acc[i][j] = mfma32(ra[p][i], rb[p][j], acc[i][j]);
+        for (int i = 0; i < MT; ++i) {
+            const OpN<NPART> ao = opn<NPART>(f32x4{ra[p][i][0], ra[p][i][1], ra[p][i][2], ra[p][i][3]},
+                                             f32x4{ra[p][i][4], ra[p][i][5], ra[p][i][6], ra[p][i][7]});
+#pragma unroll
+            for (int j = 0; j < KT; ++j) acc[i][j] = mma_n<NPART>(ao, bo[j], acc[i][j]);
+        }
     };
-    if (npairs > 0) {
-        // pairs 0 .. P-2 go to slots 0 .. P-2; step s loads pair s + P - 1 into the slot that
-        // step s - 1 consumed, then runs the MFMAs of pair s.  The two are independent, so the
-        // scheduler interleaves them: one MFMA, a few VALU, one load.
+    if (nblk > 0) {
+        // blocks 0 .. S-2 go to slots 0 .. S-2; step s loads block s + S - 1 into the slot that
+        // step s - 1 consumed, then runs the MFMAs of block s
 #pragma unroll
-        for (int p = 0; p < WG_P - 1; ++p) load(p);
+        for (int p = 0; p < WG_SLOTS - 1; ++p) load(p);
         int s0 = 0;
-        for (; s0 + WG_P <= npairs; s0 += WG_P) {
+        for (; s0 + WG_SLOTS <= nblk; s0 += WG_SLOTS) {
 #pragma unroll
-            for (int p = 0; p < WG_P; ++p) {
-                load((p + WG_P - 1) % WG_P);
+            for (int p = 0; p < WG_SLOTS; ++p) {
+                load((p + WG_SLOTS - 1) % WG_SLOTS);
                 mma(p);
-#pragma unroll
-                for (int k = 0; k < MT * KT; ++k) {
-                    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);                    // MFMA
-                    __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);                    // VALU
-                    if (k < MT + KT) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);   // VMEM read
-                }
             }
         }
-        const int rem = npairs - s0;     // slots 0 .. rem-1 (rem < P) hold the last pairs
+        const int rem = nblk - s0;     // slots 0 .. rem-1 (rem < S) hold the last blocks
 #pragma unroll
-        for (int p = 0; p < WG_P - 1; ++p)
+        for (int p = 0; p < WG_SLOTS - 1; ++p)
             if (p < rem) mma(p);
     }
 
@@ -304,15 +311,15 @@ MEP_DEV void wgrad_task(const mep_wgrad_desc& d, int split, int kbase, lfloat* r
     __syncthreads();
     const int kcnt = min(32 * KT, d.Ktot - kbase);
     gfloat* part = G<float>(d.partial) + (int64_t)split * N * d.Ktot + kbase;
-    for (int idx = threadIdx.x; idx < N * 32 * KT; idx += WG_THREADS) {
-        const int n = idx / (32 * KT), k = idx - n * (32 * KT);
-        if (k < kcnt) part[(int64_t)n * d.Ktot + k] = red[n * LDR + k] + red[BUF + n * LDR + k];
+    for (int e = threadIdx.x; e < N * 32 * KT; e += WG_THREADS) {
+        const int nn = e / (32 * KT), k = e - nn * (32 * KT);
+        if (k < kcnt) part[(int64_t)nn * d.Ktot + k] = red[nn * LDR + k] + red[BUF + nn * LDR + k];
     }
 }
 
 // Flat grid: workgroup w runs task map[w] = (descriptor << 16 | index within the descriptor);
 // the map is stored right after the n_desc descriptors.
-__global__ __launch_bounds__(WG_THREADS, 2) void k_wgrad(const mep_wgrad_desc* __restrict__ descs, int n_desc) {
+__global__ __launch_bounds__(WG_THREADS, 1) void k_wgrad(const mep_wgrad_desc* __restrict__ descs, int n_desc) {
     const int task = reinterpret_cast<const int*>(descs + n_desc)[blockIdx.x];
     const mep_wgrad_desc& d = descs[task >> 16];
     const int local = task & 0xffff;
@@ -324,22 +331,19 @@ __global__ __launch_bounds__(WG_THREADS, 2) void k_wgrad(const mep_wgrad_desc* _
     const int kbase = 32 * ktm * cg;
     __shared__ __attribute__((aligned(16))) float smem[2 * WG_RED];
     lfloat* red = (lfloat*)&smem[0];
+#define MEP_WGT(M, K)                                                              \
+    case 8 * M + K:                                                                \
+        if (d.bf16) wgrad_task<M, K, 1>(d, split, kbase, red);                     \
+        else wgrad_task<M, K, 3>(d, split, kbase, red);                            \
+        break;
     switch (8 * mt + kt) {
-        case 8 * 1 + 1: wgrad_task<1, 1>(d, split, kbase, red); break;
-        case 8 * 1 + 2: wgrad_task<1, 2>(d, split, kbase, red); break;
-        case 8 * 1 + 3: wgrad_task<1, 3>(d, split, kbase, red); break;
-        case 8 * 1 + 4: wgrad_task<1, 4>(d, split, kbase, red); break;
-        case 8 * 2 + 1: wgrad_task<2, 1>(d, split, kbase, red); break;
-        case 8 * 2 + 2: wgrad_task<2, 2>(d, split, kbase, red); break;
-        case 8 * 2 + 3: wgrad_task<2, 3>(d, split, kbase, red); break;
-        case 8 * 2 + 4: wgrad_task<2, 4>(d, split, kbase, red); break;
-        case 8 * 3 + 1: wgrad_task<3, 1>(d, split, kbase, red); break;
-        case 8 * 3 + 2: wgrad_task<3, 2>(d, split, kbase, red); break;
-        case 8 * 3 + 3: wgrad_task<3, 3>(d, split, kbase, red); break;
-        case 8 * 4 + 1: wgrad_task<4, 1>(d, split, kbase, red); break;
-        case 8 * 4 + 2: wgrad_task<4, 2>(d, split, kbase, red); break;
+        MEP_WGT(1, 1) MEP_WGT(1, 2) MEP_WGT(1, 3) MEP_WGT(1, 4)
+        MEP_WGT(2, 1) MEP_WGT(2, 2) MEP_WGT(2, 3) MEP_WGT(2, 4)
+        MEP_WGT(3, 1) MEP_WGT(3, 2) MEP_WGT(3, 3)
+        MEP_WGT(4, 1) MEP_WGT(4, 2)
         default: break;
     }
+#undef MEP_WGT
 }
 
 __global__ __launch_bounds__(256) void k_wgrad_reduce(const mep_wgrad_desc* __restrict__ descs) {

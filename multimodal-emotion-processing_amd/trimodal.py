@@ -41,7 +41,7 @@ def cdiv(a, b):
 
 
 WG_WAVES = 4              # csrc/gemm.hip k_wgrad: waves per workgroup (token quarters of a split)
-WG_TARGET = 2 * _lib.N_CU  # workgroups per launch: two per CU (80 KB of LDS each)
+WG_TARGET = _lib.N_CU      # workgroups per launch: one per CU (4 waves of ~400 registers)
 
 
 def wgrad_geometry(N, ktot):
@@ -54,10 +54,10 @@ def wgrad_geometry(N, ktot):
 
 def wgrad_splits(items, n_wg=WG_TARGET):
     """Token chunk per item such that the launch holds AT MOST n_wg workgroups, all resident at
-    once (two per CU), and the largest workgroup's MFMA work (32x32 tiles x tokens) is as small
+    once (one per CU), and the largest workgroup's MFMA work (32x32 tiles x tokens) is as small
     as the quantisation allows: the kernel lasts as long as its busiest CU, so a launch of 264
-    workgroups (8 CUs holding two) takes twice as long as one of 256.  Multiples of 8 tokens
-    (four waves, token pairs)."""
+    workgroups (8 CUs running two in turn) takes twice as long as one of 256.  Multiples of 8
+    tokens (four waves)."""
     geo = [wgrad_geometry(N, sum(b[1] for b in bs)) for (_, N, n, bs, _) in items]
     tiles = [mt * kt for (mt, kt, ncg) in geo]
     total = sum(n * t * ncg for t, (_, _, ncg), (_, N, n, bs, _) in zip(tiles, geo, items))
@@ -107,11 +107,12 @@ def make_unify(descs, dev, n_wg=_lib.N_CU):
     return DescArray(GemmDesc, descs, dev, tail=tasks), len(tasks)
 
 
-def make_wgrad(items, dev, tok_per_split=None):
+def make_wgrad(items, dev, tok_per_split=None, bf16=False):
     """items: [(a_rows, N, ntok, [(b_rows, K, out_ptr, ldo), ...][, out_trans]), ...] ->
     (workspace, descs, wgrad workgroups, reduce tiles).  One descriptor per A operand; its B operands
     concatenate on K.  out_trans: dW written transposed (out[k * ldo + n]).  tok_per_split: None =
-    balanced per item (wgrad_splits), else a fixed token chunk."""
+    balanced per item (wgrad_splits), else a fixed token chunk.  bf16: plain bf16 operands (the
+    bf16 path) instead of the 3-part split."""
     items = [tuple(it) + (0,) * (5 - len(it)) for it in items]
     if tok_per_split is None:
         tps = wgrad_splits(items)
@@ -139,7 +140,8 @@ def make_wgrad(items, dev, tok_per_split=None):
                                kb=(ctypes.c_int32 * _lib.WG_MAX_B)(*[b[1] for b in allb]),
                                ldo=(ctypes.c_int32 * _lib.WG_MAX_B)(*[b[3] for b in allb]),
                                partial=ws.data_ptr() + 4 * off, n_b=len(bs), ntok=n, N=N, Ktot=ktot,
-                               tok_per_split=tok_per_split, n_split=ns, accumulate=0, out_trans=int(trans)))
+                               tok_per_split=tok_per_split, n_split=ns, accumulate=0, out_trans=int(trans),
+                               bf16=int(bool(bf16))))
         off += ns * N * ktot
         tasks += [(len(descs) - 1) << 16 | w for w in range(ns * wgrad_geometry(N, ktot)[2])]
         rmax = max(rmax, cdiv(N * ktot, 256))

@@ -16,10 +16,10 @@ def _rows(t, T, sB, sT, off=0):
     return Rows(ptr=t.data_ptr() + 4 * off, sB=sB, sT=sT, T=T)
 
 
-def _run(items, dev, tok_per_split=None):
+def _run(items, dev, tok_per_split=None, bf16=False):
     from mep_amd import trimodal
     from mep_amd._lib import launch
-    ws, arr, n_wg, rmax = trimodal.make_wgrad(items, dev, tok_per_split=tok_per_split)
+    ws, arr, n_wg, rmax = trimodal.make_wgrad(items, dev, tok_per_split=tok_per_split, bf16=bf16)
     launch('mep_wgrad', arr, n_wg)
     launch('mep_wgrad_reduce', arr, rmax)
     torch.cuda.synchronize()
@@ -56,6 +56,27 @@ def test_wgrad_vs_torch(N, Ks, B, T, cuda):
     for b, K, o in zip(Bs, Ks, outs):
         want = a2.t() @ b[:, 1].reshape(n, K).double()
         assert_close(o, want, rtol=1e-5, atol_frac=1e-6, name='N%d K%d' % (N, K))
+    del keep
+
+
+@pytest.mark.parametrize('N,Ks,B,T', [CASES[1], CASES[3], CASES[5], CASES[7], CASES[8]])
+def test_wgrad_bf16_vs_torch(N, Ks, B, T, cuda):
+    """bf16 path: exactly the products of the bf16-rounded operands (each exact in fp32), summed in
+    fp32 -- checked against float64 sums of the rounded operands."""
+    torch.manual_seed(N * 1000 + sum(Ks) + B * 7 + T + 1)
+    n = B * T
+    A = torch.randn(B, T, N, device=cuda)
+    Bs = [torch.randn(B, 2, T, K, device=cuda) for K in Ks]
+    outs = [torch.full((N, K), float('nan'), device=cuda) for K in Ks]
+    item = (_rows(A, T, T * N, N), N, n,
+            [(_rows(b, T, 2 * T * K, K, T * K), K, o.data_ptr(), K) for b, K, o in zip(Bs, Ks, outs)])
+    keep = _run([item], cuda, bf16=True)
+    a2 = A.reshape(n, N).bfloat16().double()
+    for b, K, o in zip(Bs, Ks, outs):
+        want = a2.t() @ b[:, 1].reshape(n, K).bfloat16().double()
+        assert_close(o, want, rtol=1e-5, atol_frac=1e-6, name='bf16 N%d K%d' % (N, K))
+        full = A.reshape(n, N).double().t() @ b[:, 1].reshape(n, K).double()
+        assert float((o.double() - full).abs().max()) > 1e-7 * float(full.abs().max())   # really bf16
     del keep
 
 
