@@ -5,12 +5,15 @@ B=64 utterance pairs per GPU, T=50 for text (d=300), visual (d=35) and audio (d=
 forward of both encoders + head + circle loss + backward + clip_grad_norm_(1.0) + AdamW (lr 1e-3)
 [+ RCCL all-reduce of the flat gradient when N > 1].  Synthetic N(0,1) features, all-ones masks,
 Bernoulli(0.3) labels, random-init weights; inputs resident in HBM before the timed region.
-Arithmetic: fp32 storage, softmax, LayerNorm and accumulation; the products run on the matrix
-cores either in fp32 (v_mfma_f32_*) or as fp32 operands split into bf16 parts,
-within the 1e-4 logits parity of the fp32 reference.
+Arithmetic (--dtype fp32, default): fp32 storage, softmax, LayerNorm and accumulation; the
+products run on the matrix cores either in fp32 (v_mfma_f32_*) or as fp32 operands split into
+bf16 parts, within the 1e-4 logits parity of the fp32 reference.  --dtype bf16
+(BASELINE cfg3 / cfg5 name bf16): the same step with plain bf16 operands on every encoder product
+(fp32 accumulation, storage, softmax, LayerNorm, loss, AdamW; tests/test_gpu_bf16.py).
 
     python bench.py [--gpus N --steps K --warmup W]                  BASELINE cfg3 (cfg4 with N > 1)
     python bench.py --config cfg2 | cfg5                            the other BASELINE configs
+    python bench.py [--config cfg5] --dtype bf16                    the bf16 path
     torchrun --nproc-per-node N bench.py --gpus N ...                (one process per GPU, RCCL)
 Rank 0 prints one JSON line.
 """
@@ -113,13 +116,15 @@ class Cfg3:
     metric = METRIC
     unit = 'utt/s'
 
-    def __init__(self, dev, rank, graph):
+    def __init__(self, dev, rank, graph, bf16=False):
         from mep_amd import cmu_mosei
         from mep_amd.engine import TrainEngine
         from mep_amd.optim import FusedAdamW
         torch.manual_seed(0)
+        self.bf16 = bf16
         self.model = cmu_mosei.Concat_Trans(dim=D, l_len=T, v_len=T, a_len=T, n_heads=H, n_layers=NL,
                                             ffn=1).to(dev).train()
+        self.model.mep_precision = "bf16" if bf16 else "fp32"   # = running under autocast(bfloat16)
         self.opt = FusedAdamW(self.model, lr=1e-3)
         self.eng = TrainEngine(self.model, self.opt, clip=1.0, graph=graph)
         self.eng_eager = TrainEngine(self.model, self.opt, clip=1.0, graph=False)
@@ -173,14 +178,16 @@ class Cfg5:
     unit = 'rows/s'
     R, TT, DIMS5 = 32, 300, (768, 640, 205)
 
-    def __init__(self, dev, rank, graph):
+    def __init__(self, dev, rank, graph, bf16=False):
         from mep_amd import ren_mme
         from mep_amd.engine import TrainEngine
         from mep_amd.optim import FusedAdamW
         torch.manual_seed(0)
         R, TT = self.R, self.TT
+        self.bf16 = bf16
         self.model = ren_mme.Base_model(dim=128, l_len=TT, v_len=TT, a_len=TT, n_heads=8, n_layers=1,
                                         ffn=1).to(dev).train()
+        self.model.mep_precision = "bf16" if bf16 else "fp32"
         self.opt = FusedAdamW(self.model, lr=1e-3)
         self.eng = TrainEngine(self.model, self.opt, clip=1.0, rdrop=True, graph=graph)
         self.eng_eager = TrainEngine(self.model, self.opt, clip=1.0, rdrop=True, graph=False)
@@ -242,8 +249,10 @@ class Cfg2:
     metric = 'rows/sec fwd+bwd, realformer text encoder (2 residual blocks) B=64 T=50 d=300'
     unit = 'rows/s'
 
-    def __init__(self, dev, rank, graph):
+    def __init__(self, dev, rank, graph, bf16=False):
         from mep_amd import realformer as rf
+        assert not bf16, 'cfg2 (realformer text encoder) is an fp32 configuration (BASELINE.json)'
+        self.bf16 = False
         torch.manual_seed(0)
         self.mc = rf.Multi_class(l_dim=300, v_dim=35, a_dim=74, dim=96, l_len=T, v_len=T, a_len=T, n_heads=6,
                                  n_layers=2, ffn=2).to(dev).train()
@@ -356,8 +365,9 @@ def roofline_of(work, name, tot, reps, costs):
     per_launch_s = t / n
     launches_per_step = max(1, n // reps)
     flops, nbytes = costs[name]
-    rl = roofline.roofline_entry(name, flops / launches_per_step, nbytes / launches_per_step, per_launch_s)
-    rl['traffic'], rl['traffic_source'] = pmc_traffic(name) if work.name == 'cfg3' else (None, None)
+    rl = roofline.roofline_entry(name, flops / launches_per_step, nbytes / launches_per_step, per_launch_s,
+                                 bf16=work.bf16)
+    rl['traffic'], rl['traffic_source'] = pmc_traffic(name) if work.name == 'cfg3' and not work.bf16 else (None, None)
     rl['avg_launch_us'] = round(per_launch_s * 1e6, 2)
     return rl
 
@@ -371,6 +381,8 @@ def main():
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-graph', action='store_true')
     ap.add_argument('--cpu-budget', type=float, default=12.0)
+    ap.add_argument('--dtype', default='fp32', choices=('fp32', 'bf16'),
+                    help='fp32: the 1e-4 parity path (default); bf16: bf16-operand products (cfg3 / cfg5)')
     args = ap.parse_args()
 
     world = int(os.environ.get('WORLD_SIZE', '1'))
@@ -383,7 +395,7 @@ def main():
 
     from mep_amd import _lib, roofline
     graph = not args.no_graph
-    work = CONFIGS[args.config](dev, rank, graph)
+    work = CONFIGS[args.config](dev, rank, graph, bf16=args.dtype == 'bf16')
 
     for _ in range(args.warmup):
         work.step()
@@ -428,7 +440,7 @@ def main():
         'higher_is_better': True,
         'scaling': 'weak',
         'vs_baseline': None,
-        'dtype': 'fp32',
+        'dtype': args.dtype,
         'data': 'synthetic N(0,1) features, all-ones masks, Bernoulli(0.3) labels, random-init weights',
         'config': work.config(world, graph),
         'loss': round(loss, 6),

@@ -169,7 +169,14 @@ MEP_DEV int wg_extent(const mep_rows& r, int T, int ntok, int width) {
 
 constexpr int WG_INV = (int)0x80000000u;   // byte offset past every view: the buffer load returns 0
 
-template <int MT, int KT, int NPART>
+// a view whose element offset is linear in the token, tok * step (contiguous rows, or T = 1)
+MEP_DEV bool wg_linear(const mep_rows& r) { return r.T == 1 || r.sB == (int64_t)r.T * r.sT; }
+MEP_DEV int wg_step(const mep_rows& r) { return (int)(r.T == 1 ? r.sB : r.sT); }
+
+// LIN: every view of the item is linear in the token -- a lane's eight tokens of a k block sit at
+// fixed byte distances, so they are ONE per-lane base (VGPR) plus a wave-uniform per-token offset
+// (the load's SGPR soffset) and the column tile an immediate: no address arithmetic per token.
+template <int MT, int KT, int NPART, bool LIN>
 MEP_DEV void wgrad_task(const mep_wgrad_desc& d, int split, int kbase, lfloat* red) {
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int c = lane & 31, h = lane >> 5;
@@ -230,7 +237,43 @@ MEP_DEV void wgrad_task(const mep_wgrad_desc& d, int split, int kbase, lfloat* r
     for (int j = 0; j < KT; ++j) wB[j] = bsB[j] - T * bsT[j];
 
     float ra[WG_SLOTS][MT][8], rb[WG_SLOTS][KT][8];
+    // LIN addressing: half h's tokens start at w0 + h * half; token 8 s + e of the half is at
+    // base + (8 s + e) * step (bytes, soffset); columns unclamped (a column past N / Ktot reads
+    // neighbouring data or 0 and only feeds output entries that are never stored)
+    const int t0 = min(w0 + h * half, d.ntok);
+    const int stA = 4 * (LIN ? wg_step(d.a) : 0);
+    int stB[KT], baseB[KT];
+    const int baseA = LIN ? t0 * stA + 4 * c : 0;
+#pragma unroll
+    for (int j = 0; j < KT; ++j) {
+        int k0 = min(kbase + 32 * j, d.Ktot - 1), o = 0;
+        while (o < d.n_b - 1 && k0 >= d.kb[o]) { k0 -= d.kb[o]; ++o; }
+        stB[j] = LIN ? 4 * wg_step(d.b[o]) : 0;
+        baseB[j] = LIN ? t0 * stB[j] + 4 * (k0 + c) : 0;
+    }
+    int blk = 0;   // LIN: next k block to load
+    auto load_lin = [&](int p, bool checked) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            const int tk = 8 * blk + e;
+            const bool ok = !checked || tk < nh;
+            const int va = ok ? baseA : WG_INV;
+#pragma unroll
+            for (int i = 0; i < MT; ++i)
+                ra[p][i][e] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsA, va + 128 * i, tk * stA, 0));
+#pragma unroll
+            for (int j = 0; j < KT; ++j)
+                rb[p][j][e] = __builtin_bit_cast(
+                    float, __builtin_amdgcn_raw_buffer_load_b32(rsB[j], ok ? baseB[j] : WG_INV, tk * stB[j], 0));
+        }
+        ++blk;
+    };
     auto load = [&](int p) {
+        if constexpr (LIN) {
+            if (8 * blk + 8 <= n - half) load_lin(p, false);   // every token of both halves valid
+            else load_lin(p, true);
+            return;
+        }
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
             const bool ok = idx < nh;
@@ -275,6 +318,9 @@ MEP_DEV void wgrad_task(const mep_wgrad_desc& d, int split, int kbase, lfloat* r
 #pragma unroll
             for (int p = 0; p < WG_SLOTS; ++p) {
                 load((p + WG_SLOTS - 1) % WG_SLOTS);
+                // the next block's loads go out before this block's operand conversion (the
+                // scheduler would otherwise hoist the conversion, whose wait then drains them too)
+                __builtin_amdgcn_sched_barrier(0);
                 mma(p);
             }
         }
@@ -331,10 +377,17 @@ __global__ __launch_bounds__(WG_THREADS, 1) void k_wgrad(const mep_wgrad_desc* _
     const int kbase = 32 * ktm * cg;
     __shared__ __attribute__((aligned(16))) float smem[2 * WG_RED];
     lfloat* red = (lfloat*)&smem[0];
+    bool lin = wg_linear(d.a);
+    for (int o = 0; o < d.n_b; ++o) lin = lin && wg_linear(d.b[o]);
 #define MEP_WGT(M, K)                                                              \
     case 8 * M + K:                                                                \
-        if (d.bf16) wgrad_task<M, K, 1>(d, split, kbase, red);                     \
-        else wgrad_task<M, K, 3>(d, split, kbase, red);                            \
+        if (d.bf16) {                                                              \
+            if (lin) wgrad_task<M, K, 1, true>(d, split, kbase, red);              \
+            else wgrad_task<M, K, 1, false>(d, split, kbase, red);                 \
+        } else {                                                                   \
+            if (lin) wgrad_task<M, K, 3, true>(d, split, kbase, red);              \
+            else wgrad_task<M, K, 3, false>(d, split, kbase, red);                 \
+        }                                                                          \
         break;
     switch (8 * mt + kt) {
         MEP_WGT(1, 1) MEP_WGT(1, 2) MEP_WGT(1, 3) MEP_WGT(1, 4)
@@ -441,6 +494,94 @@ MEP_DEV void unify_tasks(const mep_gemm_desc& d, const lfloat* wl, int ldl, int 
     }
 }
 
+// bf16 path (desc.bf16): the same mapping on v_mfma_f32_16x16x32_bf16 with plain bf16 operands,
+// one MFMA per k pair (two 16-wide k blocks: slots 0-3 / 4-7, split.h).  The weight is staged in
+// LDS already rounded, in 16-byte units (n, pair p, lane group g) at n * RS + (4p + g) * 16,
+// RS = 64 NP + 32 bytes (conflict-free fragment reads, split.h SplitW), zero past K; when it does
+// not fit, fragments are read from L2 and rounded on the fly (K % 16 == 0).
+template <int NIP, bool WL, bool XV>
+MEP_DEV void unify_tasks_bf(const mep_gemm_desc& d, const __attribute__((address_space(3))) unsigned char* wl, int tile_lo, int tile_hi, int np) {
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int c = lane & 15, g = lane >> 4;
+    const int K = d.K, NPK = (K + 31) >> 5, ntok = d.ntok, RS = 64 * NPK + 32;
+    const int T = d.x.T;
+    const auto rsX = __builtin_amdgcn_make_buffer_rsrc((void*)d.x.ptr, 0, wg_extent(d.x, T, ntok, K), 0x00020000);
+    const gfloat* wg = G<const float>(d.w);
+    const gfloat* table = G<const float>(d.table);
+    const int ntask = (tile_hi - tile_lo) * np;
+    constexpr int PP = UN_PF / 2;   // k pairs of X fragments in flight
+    for (int task = wave; task < ntask; task += UN_WAVES) {
+        const int tile = tile_lo + task / np, part = task - (task / np) * np;
+        const int tok = tile * 16 + c;
+        const bool ok = tok < ntok;
+        int xo = WG_INV;
+        if (ok) {
+            const int b = tok / T, t = tok - b * T;
+            xo = 4 * ((int)(b * d.x.sB + t * d.x.sT) + 4 * g);
+        }
+        const int n0 = 16 * NIP * part;
+        f32x4 acc[NIP];
+#pragma unroll
+        for (int i = 0; i < NIP; ++i) acc[i] = zero_f4();
+        f32x4 xf[PP][2];
+        auto ld = [&](int o) {
+            f32x4 v;
+            if (XV) {
+                v = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rsX, o, 0, 0));
+            } else {
+#pragma unroll
+                for (int e = 0; e < 4; ++e) v[e] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsX, o + 4 * e, 0, 0));
+            }
+            return v;
+        };
+        auto load = [&](int s, int pp) {
+            const int o = pp < NPK ? xo + 128 * pp : WG_INV;
+            xf[s][0] = ld(o);
+            xf[s][1] = ld(o == WG_INV || 32 * pp + 16 >= K ? WG_INV : o + 64);
+        };
+        auto mma = [&](int s, int pp) {
+            const OpN<1> xb = opn<1>(xf[s][0], xf[s][1]);
+#pragma unroll
+            for (int i = 0; i < NIP; ++i) {
+                const int row = n0 + 16 * i + c;
+                OpN<1> a;
+                if (WL) {
+                    typedef __attribute__((address_space(3))) u32x4 lu32x4;
+                    a.p[0] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const lu32x4*>(wl + row * RS + (4 * pp + g) * 16));
+                } else {
+                    const gfloat* wr = wg + (int64_t)row * d.ldw + 32 * pp + 4 * g;
+                    a = opn<1>(ld4w(wr), 32 * pp + 16 < K ? ld4w(wr + 16) : zero_f4());
+                }
+                acc[i] = mma_n<1>(a, xb, acc[i]);
+            }
+        };
+#pragma unroll
+        for (int s = 0; s < PP - 1; ++s) load(s, s);
+        int p0 = 0;
+        for (; p0 + PP <= NPK; p0 += PP) {
+#pragma unroll
+            for (int s = 0; s < PP; ++s) {
+                load((s + PP - 1) % PP, p0 + s + PP - 1);
+                mma(s, p0 + s);
+            }
+        }
+#pragma unroll
+        for (int s = 0; s < PP - 1; ++s)
+            if (p0 + s < NPK) mma(s, p0 + s);
+        if (ok) {
+            gfloat* yr = row_ptr(d.y, tok);
+            const gfloat* tr = table ? table + (int64_t)(tok % d.y.T) * d.N : nullptr;
+#pragma unroll
+            for (int i = 0; i < NIP; ++i) {
+                const int col = n0 + 16 * i + 4 * g;
+                f32x4 v = acc[i];
+                if (tr) v += ld4w(tr + col);
+                stg4(yr + col, make_float4(v[0], v[1], v[2], v[3]));
+            }
+        }
+    }
+}
+
 __global__ __launch_bounds__(UN_THREADS) void k_unify(const mep_gemm_desc* __restrict__ descs, int n_desc) {
     const int task = reinterpret_cast<const int*>(descs + n_desc)[blockIdx.x];
     const mep_gemm_desc& d = descs[task >> 20];
@@ -450,6 +591,40 @@ __global__ __launch_bounds__(UN_THREADS) void k_unify(const mep_gemm_desc* __res
     const int tile_lo = w * per, tile_hi = min(ntiles, tile_lo + per);
     if (tile_lo >= tile_hi) return;   // whole workgroup
     __shared__ __attribute__((aligned(16))) float smem[UN_LDS];
+    const bool xv = (d.K % 4 == 0) && ((d.x.ptr & 15) == 0) && (d.x.sB % 4 == 0) && (d.x.sT % 4 == 0);
+    const int np = d.N >= 64 ? 2 : 1, nip = d.N / (16 * np);
+    if (d.bf16) {
+        // W [N][K] -> rounded bf16 units in LDS (zero past K) when N * RS fits
+        const int N = d.N, K = d.K, NPK = (K + 31) >> 5, RS = 64 * NPK + 32;
+        const bool wlds = N * RS <= 4 * UN_LDS;
+        typedef __attribute__((address_space(3))) unsigned char lbyte;
+        lbyte* wl = (lbyte*)&smem[0];
+        if (wlds) {
+            const gfloat* W = G<const float>(d.w);
+            for (int u = threadIdx.x; u < N * NPK * 4; u += UN_THREADS) {
+                const int gg = u & 3, pp = (u >> 2) % NPK, n = (u >> 2) / NPK;
+                float v[8];
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const int k = 32 * pp + (j < 4 ? 0 : 16) + 4 * gg + (j & 3);
+                    v[j] = k < K ? W[(int64_t)n * d.ldw + k] : 0.f;
+                }
+                typedef __attribute__((address_space(3))) u32x4 lu32x4;
+                *reinterpret_cast<lu32x4*>(wl + n * RS + (4 * pp + gg) * 16) =
+                    u32x4{pk_bf16(v[0], v[1]), pk_bf16(v[2], v[3]), pk_bf16(v[4], v[5]), pk_bf16(v[6], v[7])};
+            }
+            __syncthreads();
+        }
+#define MEP_UNB(NIP)                                                                                     \
+        if (nip == NIP) {                                                                                \
+            if (wlds) { if (xv) unify_tasks_bf<NIP, true, true>(d, wl, tile_lo, tile_hi, np);            \
+                        else unify_tasks_bf<NIP, true, false>(d, wl, tile_lo, tile_hi, np); }            \
+            else unify_tasks_bf<NIP, false, true>(d, wl, tile_lo, tile_hi, np);                          \
+        }
+        MEP_UNB(1) MEP_UNB(2) MEP_UNB(3) MEP_UNB(4)
+#undef MEP_UNB
+        return;
+    }
     lfloat* wl = (lfloat*)&smem[0];
     const int N = d.N, K = d.K, KB = (K + 15) >> 4, ldl = 16 * KB + 4;
     const bool wlds = N * ldl <= UN_LDS;
@@ -478,8 +653,6 @@ __global__ __launch_bounds__(UN_THREADS) void k_unify(const mep_gemm_desc* __res
         }
         __syncthreads();
     }
-    const bool xv = (K % 4 == 0) && ((d.x.ptr & 15) == 0) && (d.x.sB % 4 == 0) && (d.x.sT % 4 == 0);
-    const int np = N >= 64 ? 2 : 1, nip = N / (16 * np);
 #define MEP_UN(NIP)                                                                          \
     if (nip == NIP) {                                                                        \
         if (wlds) { if (xv) unify_tasks<NIP, true, true>(d, wl, ldl, tile_lo, tile_hi, np);    \

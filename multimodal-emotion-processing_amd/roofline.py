@@ -8,16 +8,18 @@ Per attention-block instance (batch row b, block j), with n_kv = 1 (k is v):
           (+ S_prev, ds_next reads, ds_prev write when chained)
 Peaks (MI355X_MICROARCH.md): HBM 8.0 TB/s; fp32 MFMA (= vector rate) 157.3 TFLOP/s; bf16 MFMA
 2.5 PFLOP/s dense.  Kernels whose fp32 products run as bf16 parts (split.h) are priced against the
-bf16 peak divided by the bf16 products per fp32 product: the block epilogues (six products) at
-2.5 P / 6 = 417 TFLOP/s of fp32 work.  The attention kernels mix fp32 MFMA (forward P.V) and split
-products and are priced at the fp32 MFMA peak (they are HBM-bound at every benched shape).
+bf16 peak divided by the bf16 products per fp32 product: the block epilogues and the weight
+gradients (six products) at 2.5 P / 6 = 417 TFLOP/s of fp32 work.  The attention kernels mix fp32
+MFMA (forward P.V) and split products and are priced at the fp32 MFMA peak (they are HBM-bound at
+every benched shape).  bf16 path (MEP_PREC_BF16): one bf16 product per product, every matrix
+kernel priced at the bf16 peak; the bytes are the same (fp32 storage).
 """
 from .trimodal import MODS
 
 HBM_PEAK = 8.0e12
 F32_PEAK = 157.3e12
 BF16_PEAK = 2.5e15
-COMPUTE_PEAK = {'mep_block_epi_fwd': BF16_PEAK / 6, 'mep_block_epi_bwd': BF16_PEAK / 6}
+COMPUTE_PEAK = {'mep_block_epi_fwd': BF16_PEAK / 6, 'mep_block_epi_bwd': BF16_PEAK / 6, 'mep_wgrad': BF16_PEAK / 6}
 
 
 def launch_costs(plan):
@@ -85,9 +87,9 @@ def rf_launch_costs(plan):
     return out
 
 
-def roofline_entry(name, flops, nbytes, seconds):
+def roofline_entry(name, flops, nbytes, seconds, bf16=False):
     """The bench's roofline object for one kernel: bound = the larger of the two ideal times."""
-    cpeak = COMPUTE_PEAK.get(name, F32_PEAK)
+    cpeak = BF16_PEAK if bf16 else COMPUTE_PEAK.get(name, F32_PEAK)
     t_mem, t_cmp = nbytes / HBM_PEAK, flops / cpeak
     if t_mem >= t_cmp:
         achieved = nbytes / seconds / 1e9

@@ -26,11 +26,20 @@ class ModelRunner:
         self._gen = 0
         self._live = None
 
-    def plan(self, B, T):
-        key = (int(B),) + tuple(int(t) for t in T)
+    def bf16(self):
+        """The bf16 path (csrc MEP_PREC_BF16) runs when the model is called under
+        ``torch.autocast(device_type='cuda', dtype=torch.bfloat16)`` -- the way reference-side code
+        asks for bf16 -- or when ``model.mep_precision == 'bf16'``; otherwise the fp32 path."""
+        if getattr(self.model, 'mep_precision', 'fp32') == 'bf16':
+            return True
+        return torch.is_autocast_enabled('cuda') and torch.get_autocast_dtype('cuda') == torch.bfloat16
+
+    def plan(self, B, T, bf16=None):
+        bf16 = self.bf16() if bf16 is None else bool(bf16)
+        key = (int(B),) + tuple(int(t) for t in T) + (bf16,)
         p = self.plans.get(key)
         if p is None:
-            p = TriModalPlan(self.spec, self.flat, key[0], key[1:], self.device, self.labels_float)
+            p = TriModalPlan(self.spec, self.flat, key[0], key[1:4], self.device, self.labels_float, bf16=bf16)
             self.plans[key] = p
         return p
 

@@ -181,8 +181,13 @@ class TriModalSpec:
 
 
 class TriModalPlan:
-    def __init__(self, spec, flat, B, T, device, labels_float=False):
+    def __init__(self, spec, flat, B, T, device, labels_float=False, bf16=False):
+        """bf16: the bf16 path (include/mep.h MEP_PREC_BF16) -- unify, attention, block epilogue and
+        weight-gradient products on plain bf16 operands with fp32 accumulation; storage, softmax,
+        LayerNorm, pool, head, loss and AdamW in fp32.  Default: the fp32 path (1e-4 parity)."""
         self.spec, self.flat, self.B = spec, flat, B
+        self.bf16 = bool(bf16)
+        self.prec = _lib.PREC_BF16 if self.bf16 else 0
         self.T = dict(zip(MODS, T))
         self.device = torch.device(device)
         self.labels_float = labels_float
@@ -196,7 +201,9 @@ class TriModalPlan:
         self.F = 2 * self.C
         E = 2
         # ---------------- static input buffers ([B, 2, T, d] prev/cur layout)
-        self.x_in = {m: torch.zeros(B, E, self.T[m], d, **f32) for m, d in zip(MODS, sp.dims)}
+        # encoder-major [E, B, T, d]: each encoder's input rows are contiguous (linear in the token,
+        # the fast addressing of k_wgrad); the masks keep the [B, E, T] prev/cur layout
+        self.x_in = {m: torch.zeros(E, B, self.T[m], d, **f32) for m, d in zip(MODS, sp.dims)}
         self.m_in = {m: torch.zeros(B, E, self.T[m], **f32) for m in MODS}
         self.labels = torch.zeros(B, NC, dtype=torch.float32 if labels_float else torch.int64, device=dev)
         self.seed = torch.zeros(1, dtype=torch.int64, device=dev)
@@ -273,7 +280,7 @@ class TriModalPlan:
     def _in_rows(self, e, m):
         d = self.spec.dims[MODS.index(m)]
         T = self.T[m]
-        return rows(self.x_in[m], T, 2 * T * d, d, e * T * d)
+        return rows(self.x_in[m], T, T * d, d, e * self.B * T * d)
 
     # ------------------------------------------------------------------ descriptors
     def _build_descriptors(self):
@@ -289,7 +296,8 @@ class TriModalPlan:
                 out = self.Y[(e, m)] if sp.unify_norm else self.U[(e, m)]
                 ud.append(GemmDesc(x=self._in_rows(e, m), y=crows(out, self.T[m], D),
                                    w=fl.ptr(pre + UNIFY_NAMES[m] + '.weight'), bias=0, table=0,
-                                   ntok=self.ntok[m], N=D, K=d, ldw=d, w_nt=1, accumulate=0, relu=0, alpha=1.0))
+                                   ntok=self.ntok[m], N=D, K=d, ldw=d, w_nt=1, accumulate=0, relu=0, alpha=1.0,
+                                   bf16=int(self.bf16)))
         self.d_unify, self.t_unify = make_unify(ud, dev)
         if sp.unify_norm:
             ln = []
@@ -441,7 +449,7 @@ class TriModalPlan:
                 items.append((crows(src, self.T[m], D), D, self.ntok[m],
                               [(self._in_rows(e, m), d, g(pre + UNIFY_NAMES[m] + '.weight'), d)]))
         self._wgrad_items = items
-        self.wg_partial, self.d_wgrad, self.t_wgrad, self.t_wgred = make_wgrad(items, dev)
+        self.wg_partial, self.d_wgrad, self.t_wgrad, self.t_wgred = make_wgrad(items, dev, bf16=self.bf16)
         # column sums: block LayerNorms, residual coefficients, Ren unify LayerNorm
         cs = []
         for blk in self.blocks:
@@ -477,10 +485,10 @@ class TriModalPlan:
             for m, x, mk in (('l', l, lm), ('v', v, vm), ('a', a, am)):
                 if isinstance(x, (tuple, list)):      # (prev, cur) pair of [B, T, d]
                     for e in range(2):
-                        self.x_in[m][:, e].copy_(x[e])
+                        self.x_in[m][e].copy_(x[e])
                         self.m_in[m][:, e].copy_(mk[e])
                 else:                                 # [B, 2, T, d]
-                    self.x_in[m].copy_(x)
+                    self.x_in[m].copy_(x.transpose(0, 1))
                     self.m_in[m].copy_(mk)
             if labels is not None:
                 self.labels.copy_(labels)
@@ -518,8 +526,8 @@ class TriModalPlan:
         if sp.unify_norm:
             launch('mep_layernorm_fwd', self.d_uln, cdiv(max(self.ntok.values()), 4), stream)
         for i in range(nl):
-            launch('mep_attn_fwd', self.d_attn[i], self.t_attn[i], stream, threads=self.g_attn[i][2])
-            launch('mep_block_epi_fwd', self.d_epi[i], self.t_epi[i], stream, threads=sp.D)
+            launch('mep_attn_fwd', self.d_attn[i], self.t_attn[i], stream, threads=self.g_attn[i][2] | self.prec)
+            launch('mep_block_epi_fwd', self.d_epi[i], self.t_epi[i], stream, threads=sp.D | self.prec)
         launch('mep_pool_fwd', self.d_pool, self.t_pool, stream)
         self.head.compute_grad = int(grad)
         self.head.rdrop = int(rdrop)
@@ -538,8 +546,8 @@ class TriModalPlan:
             self.head.ext_dlogits = 0
         launch("mep_pool_bwd", self.d_pool, self.t_poolb, stream)
         for i in reversed(range(nl)):
-            launch('mep_block_epi_bwd', self.d_epib[i], self.t_epi[i], stream, threads=sp.D)
-            launch('mep_attn_bwd', self.d_attnb[i], self.t_attnb[i], stream, threads=self.f_attnb[i])
+            launch('mep_block_epi_bwd', self.d_epib[i], self.t_epi[i], stream, threads=sp.D | self.prec)
+            launch('mep_attn_bwd', self.d_attnb[i], self.t_attnb[i], stream, threads=self.f_attnb[i] | self.prec)
         launch('mep_sum_rows', self.d_sum, self.t_sum, stream)
         if sp.unify_norm:
             launch('mep_layernorm_bwd', self.d_ulnb, cdiv(max(self.ntok.values()), 64), stream)

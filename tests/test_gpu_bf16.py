@@ -1,0 +1,138 @@
+"""The bf16 path (include/mep.h MEP_PREC_BF16) against the fp32 reference golden vectors.
+
+BASELINE cfg3 (cmu-mosei B=64 T=50) and cfg5 (Ren-MME T=300) are bf16 configurations.  On the bf16
+path every matrix product of the encoders -- unify, attention scores / P.V / backward
+contractions, block epilogue Linears, weight gradients -- takes plain bf16 operands (round to
+nearest of the fp32 values, 2^-9 relative) with fp32 accumulation; storage, softmax, LayerNorm,
+pool, head, loss and AdamW stay fp32.  It is selected the reference-side way, by running the
+model under torch.autocast('cuda', dtype=torch.bfloat16), or by model.mep_precision = 'bf16'.
+
+Tolerance (bf16, separate from the fp32 path's 1e-4): the error budget of torch's own bf16
+execution of the reference arithmetic on the same inputs -- tests/golden/bf16_budget.json, made by
+tests/golden/make_bf16_budget.py running the pinned oracle under torch.autocast(bfloat16) against
+the same fp32 fixtures.  The HIP bf16 path must be about as accurate as that or better:
+  logits max|d| / max|logit| and whole-gradient relative L2 error  <= 1.25 x budget
+  loss relative error                                               <= 2 x budget + 1e-4
+  every parameter gradient's relative L2 error                      <= 2 x its budget + 0.02
+      (fixtures that keep only the first 256 entries of each gradient: <= max(that, 0.5) --
+      one 256-entry row of a weight gradient is too small a sample for the per-tensor ratio;
+      whole-tensor bf16-vs-fp32 errors there are <= 0.2, scripts/bf16_diag.py)
+  post-AdamW parameters within lr/4 of the fp32 reference           >= budget fraction - 0.01
+(measured, round 2: logits and whole-gradient errors 0.2-0.7 x the budget on all five fixtures),
+and it must differ from the fp32 path (the bf16 kernels really ran).
+"""
+import json
+import os
+
+import pytest
+import torch
+
+from tests.golden import fixtures
+from tests.gpu_util import cmu_model, cuda_batch, ren_model
+
+pytestmark = pytest.mark.gpu
+
+CASES = ['cmu_small_l2', 'cmu_cfg3', 'ren_small', 'ren_ref', 'ren_cfg5']
+
+
+def _budget(name):
+    with open(os.path.join(os.path.dirname(os.path.abspath(__file__)), 'golden', 'bf16_budget.json')) as f:
+        return json.load(f)[name]
+
+
+def _model_and_batch(name, cuda):
+    meta, gold = fixtures.load(name)
+    if meta['family'] == 'cmu':
+        model = cmu_model(meta, cuda)
+        batch = cuda_batch(meta, cuda)
+        return meta, gold, model, batch[:6], batch[6]
+    model = ren_model(meta, cuda)
+    inputs, labels = fixtures.batch(meta)
+    return meta, gold, model, [t.to(cuda) for t in inputs], labels.to(cuda)
+
+
+def _loss(meta, logits, labels):
+    if meta['family'] == 'cmu':
+        from mep_amd import cmu_mosei
+        return cmu_mosei.multi_circle_loss(logits, labels).mean()
+    from mep_amd import ren_mme
+    return ren_mme.multi_loss(logits, labels) + ren_mme.rdrop_kl(logits)
+
+
+def _grad_errors(model, meta, gold, coef, budget):
+    """(worst per-tensor error / its allowance, whole-gradient relative L2 error) against the
+    fixture's gradients (full tensors, or the first 256 entries for the large fixtures)."""
+    pairs = []
+    for k, p in model.named_parameters():
+        if 'nograd/' + k in gold:
+            assert p.grad is None, k
+            continue
+        g = (p.grad * coef).double().cpu().reshape(-1)
+        ref = torch.as_tensor(gold[('grad/' if meta['full'] else 'gradhead/') + k]).double().reshape(-1)
+        pairs.append((k, g[:ref.numel()], ref))
+    def allow(k):
+        a = 2 * budget['grads'][k] + 0.02
+        return a if meta['full'] else max(a, 0.5)
+    ratios = sorted(((float((g - r).norm() / r.norm()) / allow(k), k) for k, g, r in pairs), reverse=True)
+    print('  worst tensors (error / allowance):', ', '.join('%s %.2f' % (k, e) for e, k in ratios[:3]))
+    worst = ratios[0][0]
+    gg = torch.cat([g for _, g, _ in pairs])
+    rr = torch.cat([r for _, _, r in pairs])
+    return worst, float((gg - rr).norm() / rr.norm())
+
+
+@pytest.mark.parametrize('name', CASES)
+def test_bf16_autograd_vs_fp32_reference(name, cuda):
+    meta, gold, model, args, labels = _model_and_batch(name, cuda)
+    model.train()
+    with torch.autocast('cuda', dtype=torch.bfloat16):
+        logits = model(*args)
+    runner = model.mep_runner(cuda)
+    assert [k[-1] for k in runner.plans] == [True], 'autocast(bfloat16) did not select the bf16 plan'
+    want = torch.as_tensor(gold['logits']).double()
+    e_logit = float((logits.double().cpu() - want).abs().max() / want.abs().max())
+    loss = _loss(meta, logits.float(), labels)
+    e_loss = abs(float(loss) - float(gold['loss'])) / abs(float(gold['loss']))
+    loss.backward()
+    bud = _budget(name)
+    e_grad, e_all = _grad_errors(model, meta, gold, float(gold['clipcoef']), bud)
+    print('bf16 %s: logits %.2e (budget %.2e) loss %.2e (%.2e) grad all %.2e (%.2e)'
+          % (name, e_logit, bud['logits'], e_loss, bud['loss'], e_all, bud['grad_all']))
+    assert e_logit <= 1.25 * bud['logits'], (e_logit, bud['logits'])
+    assert e_loss <= 2 * bud['loss'] + 1e-4, (e_loss, bud['loss'])
+    assert e_all <= 1.25 * bud['grad_all'], (e_all, bud['grad_all'])
+    assert e_grad <= 1.0, e_grad
+    assert e_logit > 1e-6, 'bf16 logits equal the fp32 reference: the bf16 kernels did not run'
+
+
+@pytest.mark.parametrize('name', ['cmu_cfg3', 'ren_ref'])
+def test_bf16_engine_step(name, cuda):
+    """One captured training step on the bf16 path (model.mep_precision): loss vs the fp32
+    reference, post-AdamW parameters vs the reference's post-step parameters."""
+    from mep_amd.engine import TrainEngine
+    from mep_amd.optim import FusedAdamW
+    meta, gold, model, args, labels = _model_and_batch(name, cuda)
+    model.mep_precision = 'bf16'
+    model.train()
+    lr = 1e-3
+    opt = FusedAdamW(model, lr=lr)
+    eng = TrainEngine(model, opt, clip=1.0, rdrop=meta['family'] == 'ren', graph=True)
+    if meta['family'] == 'ren':
+        from mep_amd import ren_mme
+        args = ren_mme._pack(args)
+    losses = [float(eng.step(*args, labels).item()) for _ in range(meta['steps'])]
+    bud = _budget(name)
+    e_loss = abs(losses[0] - float(gold['loss'])) / abs(float(gold['loss']))
+    assert e_loss <= 2 * bud['loss'] + 1e-4, (e_loss, bud['loss'])
+    n_ok = n_all = 0
+    for k, p in model.named_parameters():
+        ref = gold['post/' + k] if meta['full'] else gold['posthead/' + k]
+        got = p.detach().double().cpu().reshape(-1)
+        ref = torch.as_tensor(ref).double().reshape(-1)
+        err = (got[:ref.numel()] - ref).abs()
+        n_ok += int((err <= 0.25 * lr).sum())
+        n_all += err.numel()
+    frac = n_ok / n_all
+    print('bf16 step %s: loss %.2e, params within lr/4: %.4f (budget %.4f)' % (name, e_loss, frac, bud['post_frac']))
+    assert frac >= bud['post_frac'] - 0.01, (frac, bud['post_frac'])
+    assert all(k[-1] for k in model.mep_runner(cuda).plans)
