@@ -55,6 +55,7 @@ typedef struct {
 
 /* ---------------------------------------------------------------- token GEMM (MFMA f32)
  * Y[tok, n] = act( alpha * sum_k X[tok, k] * W(n, k) + bias[n] + table[tok % T, n] ) (+ Y if accumulate)
+ * (table row stride ldt, default N; T = y.T)
  * W(n,k) = W[n*ldw + k] when w_nt (nn.Linear weight, used by forward), else W[k*ldw + n]
  * (backward dX = dY W).  Replaces the bias-free nn.Linear of Unify_Dimension
  * (cmu-mosei/run.py:210-214, Ren-MME/run.py:161-166), the k=1 Conv1d unify + position
@@ -72,7 +73,7 @@ typedef struct {
     int32_t  relu;
     float    alpha;
     int32_t  bf16;     /* mep_unify: 1 = bf16 operands (MEP_PREC_BF16); mep_gemm: must be 0 */
-    int32_t  _pad;
+    int32_t  ldt;      /* row stride (floats) of table; 0 = N (a column slice of a wider table) */
 } mep_gemm_desc;
 int mep_gemm(const mep_gemm_desc* descs, int n_desc, int max_tiles, mep_stream_t stream);
 
@@ -123,7 +124,8 @@ int mep_wgrad_reduce(const mep_wgrad_desc* descs, int n_desc, int max_tiles, mep
  *   s_ik = (q_i . k_k) / sqrt(hd)  [+ c * S_prev[b,h,i,k]]  - 1e8 * (1 - mask[b,k])
  *   P = softmax_k(s);  X[b,i,h*hd:(h+1)*hd] = sum_k P_ik v_k
  * cmu-mosei/run.py:236-256 (== Ren-MME/run.py:188-208, realformer.py:182-204 after w_qkv).
- * hd = 16.  S_out (post-mask scores, needed by a following residual layer, F7) is optional.
+ * hd = 16 (hd = 32 with MEP_ATTN_HD32: forward only).  S_out (post-mask scores, needed by a
+ * following residual layer, F7) is optional.
  * Row statistics rowmax / 1/rowsum are saved for the backward. */
 typedef struct {
     mep_rows q, k, v;   /* [B*Tq, D], [B*Tk, D], [B*Tk, D]  (k may equal v)   */
@@ -151,6 +153,7 @@ typedef struct {
 #define MEP_ATTN_SHORT 4
 #define MEP_ATTN_LONG  8
 #define MEP_ATTN_DQ_TILES(n) ((n) << 8)
+#define MEP_ATTN_HD32  0x20000   /* head dim 32 (robot_demo.py, D = 192 / H = 6): forward only, fp32 path */
 int mep_attn_fwd(const mep_attn_desc* descs, int n_desc, int max_tiles, int flags, mep_stream_t stream);
 
 /* Backward of the attention core.  Inputs dx (grad of X), the forward's q/k/v/x/stats/s_prev.

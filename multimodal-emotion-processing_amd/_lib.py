@@ -24,7 +24,7 @@ class Rows(ctypes.Structure):
 class GemmDesc(ctypes.Structure):
     _fields_ = [('x', Rows), ('y', Rows), ('w', u64), ('bias', u64), ('table', u64),
                 ('ntok', i32), ('N', i32), ('K', i32), ('ldw', i32), ('w_nt', i32),
-                ('accumulate', i32), ('relu', i32), ('alpha', f32), ('bf16', i32), ('_pad', i32)]
+                ('accumulate', i32), ('relu', i32), ('alpha', f32), ('bf16', i32), ('ldt', i32)]
 
 
 WG_MAX_B = 4
@@ -259,6 +259,12 @@ def launch(name, descs, max_tiles, stream=None, threads=None, extra=()):
 
 ATTN_PREV, ATTN_SOUT, ATTN_SHORT, ATTN_LONG = 1, 2, 4, 8   # MEP_ATTN_* (include/mep.h)
 PREC_BF16 = 0x10000   # MEP_PREC_BF16: bf16-operand products (attention flags, epilogue D argument)
+ATTN_HD32 = 0x20000   # MEP_ATTN_HD32: head dim 32 attention forward (robot_demo)
+
+
+def rf_epi_rows(D):
+    """token rows per workgroup of mep_rf_epi_fwd (csrc/rf.hip rf_fwd_rows)"""
+    return 32 if D > 128 else 64
 ATTN_MAX_DQ_TILES = (160 * 1024 // 4 - 2 * 4 * 64 * 16 - 4) // 256   # csrc/attn.hip backward LDS
 
 

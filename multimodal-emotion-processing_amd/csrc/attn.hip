@@ -169,10 +169,12 @@ MEP_DEV float mask_term(const gfloat* mask, int k, int Tk) {
 
 MEP_DEV float shfl(float v, int src) { return __shfl(v, src, 64); }
 
-// s = dot * 0.25 [+ c*sp] - 1e8 * (1 - m)      (op order of cmu-mosei/run.py:244-253)
-template <bool PREV>
+// s = dot / sqrt(hd) [+ c*sp] - 1e8 * (1 - m)      (op order of cmu-mosei/run.py:244-253); hd = 16:
+// the exact * 0.25; hd = 32 (robot_demo.py:356): a correctly rounded division by float(sqrt(32)),
+// as torch divides by the Python scalar
+template <bool PREV, int HDIM = HD>
 MEP_DEV float score(float dot, float c, float sp, float mt) {
-    float s = mul_rn(dot, INV_SCALE);
+    float s = HDIM == 16 ? mul_rn(dot, INV_SCALE) : __fdiv_rn(dot, 5.65685424949238f);
     if (PREV) s = add_rn(s, mul_rn(c, sp));
     return sub_rn(s, mt);
 }
@@ -235,30 +237,38 @@ MEP_DEV BRow brow(const mep_rows& v, int b, int n, int D) {
 // One forward task: batch row b, head h, 64 queries.  PREV: residual scores in; SOUT: post-mask
 // scores out; SINGLE: Tk <= 64 (one key chunk: exact two-pass softmax, each query tile is
 // finalised right after its P.V, so no running O/max/sum state stays live).  BF: the bf16 path
-// (scores on one bf16 product, P.V on bf16 P and V).
-template <bool PREV, bool SOUT, bool SINGLE, bool BF>
+// (scores on one bf16 product, P.V on bf16 P and V).  HDIM = 16 or 32 (robot_demo, inference):
+// NHB = HDIM / 16 head blocks of 16 dims -- the score sums NHB 16-deep products, P.V fills NHB
+// output tiles.
+template <bool PREV, bool SOUT, bool SINGLE, bool BF, int HDIM = HD>
 MEP_DEV void attn_fwd_task(const mep_attn_desc& d, int qc, int h, int b, int lane) {
+    constexpr int NHB = HDIM / 16;
     const int c = lane & 15, g = lane >> 4;
-    const int hc = h * HD;
+    const int hc = h * HDIM;
     const int Tq = d.Tq, Tk = d.Tk;
     const float cres = PREV ? *G<const float>(d.c) : 0.f;
     const gfloat* sprev = G<const float>(d.s_prev);
     gfloat* sout = G<float>(d.s_out);
     const gfloat* mask = G<const float>(d.mask) + (int64_t)b * d.mask_sB;
-    const int D = d.H * HD;
+    const int D = d.H * HDIM;
     const BRow Qb = brow(d.q, b, Tq, D), Kb = brow(d.k, b, Tk, D), Vb = brow(d.v, b, Tk, D), Xb = brow(d.x, b, Tq, D);
     const int sbase = (b * d.H + h) * Tq;        // row of (b, h, query 0) in [B,H,Tq,Tk]
     const int q_lo = qc * CH;
     const int nqt = min(NT, (Tq - q_lo + 15) / 16);
     gfloat* stats = G<float>(d.stats);
 
-    floatx4 o[SINGLE ? 1 : NT];
+    floatx4 o[SINGLE ? 1 : NT][NHB];
     float m[SINGLE ? 1 : NT], l[SINGLE ? 1 : NT];
     if (!SINGLE) {
 #pragma unroll
-        for (int qt = 0; qt < NT; ++qt) { o[qt] = zero4(); m[qt] = -FLT_MAX; l[qt] = 0.f; }
+        for (int qt = 0; qt < NT; ++qt) {
+#pragma unroll
+            for (int hb = 0; hb < NHB; ++hb) o[qt][hb] = zero4();
+            m[qt] = -FLT_MAX;
+            l[qt] = 0.f;
+        }
     }
-    auto finish = [&](int qt, const floatx4& oq, float mq, float lq) {
+    auto finish = [&](int qt, const floatx4 (&oq)[NHB], float mq, float lq) {
         float lt = lq + shfl(lq, lane ^ 16);
         lt += shfl(lt, lane ^ 32);
         const float inv = 1.0f / lt;
@@ -267,50 +277,64 @@ MEP_DEV void attn_fwd_task(const mep_attn_desc& d, int qc, int h, int b, int lan
             stats[2 * (sbase + q)] = mq;
             stats[2 * (sbase + q) + 1] = inv;
         }
-        const int ox = Xb.at(q_lo + qt * 16 + 4 * g, hc + c);   // rows past Tq: dropped
 #pragma unroll
-        for (int r = 0; r < 4; ++r) Xb.st1(ox, r * Xb.sT4, oq[r] * shfl(inv, 4 * g + r));
+        for (int hb = 0; hb < NHB; ++hb) {
+            const int ox = Xb.at(q_lo + qt * 16 + 4 * g, hc + 16 * hb + c);   // rows past Tq: dropped
+#pragma unroll
+            for (int r = 0; r < 4; ++r) Xb.st1(ox, r * Xb.sT4, oq[hb][r] * shfl(inv, 4 * g + r));
+        }
     };
 
     for (int k_lo = 0; k_lo < Tk; k_lo += CH) {
         // operands of the 4 key tiles of this chunk: K rows (A of S^T: K[k0+c][4g+s], split) and V
         // columns (B of P.V: V[k0+4g+s][c]); past Tk they read 0 (P is 0 there)
-        S3 ks[NT];
-        float vf[NT][4], mt[NT][4];
-        bf16x8 vbf[NT / 2];     // BF: V of key-tile pairs (kt, kt+1) in slots 0-3 / 4-7
+        S3 ks[NT][NHB];
+        float vf[NT][NHB][4], mt[NT][4];
+        bf16x8 vbf[NT / 2][NHB];     // BF: V of key-tile pairs (kt, kt+1) in slots 0-3 / 4-7
 #pragma unroll
         for (int kt = 0; kt < NT; ++kt) {
             const int k0 = k_lo + kt * 16;
-            float kf[4];
-            Kb.ld4(kf, Kb.at(k0 + c, hc + 4 * g));
-            const int ov = Vb.at(k0 + 4 * g, hc + c);
 #pragma unroll
-            for (int s = 0; s < 4; ++s) {
-                vf[kt][s] = Vb.ld1(ov, s * Vb.sT4);
-                mt[kt][s] = mask_term(mask, k0 + 4 * g + s, Tk);
+            for (int hb = 0; hb < NHB; ++hb) {
+                float kf[4];
+                Kb.ld4(kf, Kb.at(k0 + c, hc + 16 * hb + 4 * g));
+                const int ov = Vb.at(k0 + 4 * g, hc + 16 * hb + c);
+#pragma unroll
+                for (int s = 0; s < 4; ++s) vf[kt][hb][s] = Vb.ld1(ov, s * Vb.sT4);
+                ks[kt][hb] = split3(kf);
             }
-            ks[kt] = split3(kf);
+#pragma unroll
+            for (int s = 0; s < 4; ++s) mt[kt][s] = mask_term(mask, k0 + 4 * g + s, Tk);
         }
         if (BF) {
 #pragma unroll
             for (int kt = 0; kt < NT; kt += 2)
-                vbf[kt / 2] = op(pk(vf[kt][0], vf[kt][1]), pk(vf[kt][2], vf[kt][3]), pk(vf[kt + 1][0], vf[kt + 1][1]),
-                                 pk(vf[kt + 1][2], vf[kt + 1][3]));
-        }
-        float qfa[NT][4];                                                  // B of S^T: Q[q][4g+s]
 #pragma unroll
-        for (int qt = 0; qt < NT; ++qt) Qb.ld4(qfa[qt], Qb.at(q_lo + qt * 16 + c, hc + 4 * g));   // past Tq: 0
+                for (int hb = 0; hb < NHB; ++hb)
+                    vbf[kt / 2][hb] = op(pk(vf[kt][hb][0], vf[kt][hb][1]), pk(vf[kt][hb][2], vf[kt][hb][3]),
+                                         pk(vf[kt + 1][hb][0], vf[kt + 1][hb][1]), pk(vf[kt + 1][hb][2], vf[kt + 1][hb][3]));
+        }
+        float qfa[NT][NHB][4];                                             // B of S^T: Q[q][4g+s]
+#pragma unroll
+        for (int qt = 0; qt < NT; ++qt)
+#pragma unroll
+            for (int hb = 0; hb < NHB; ++hb)
+                Qb.ld4(qfa[qt][hb], Qb.at(q_lo + qt * 16 + c, hc + 16 * hb + 4 * g));   // past Tq: 0
 #pragma unroll
         for (int qt = 0; qt < NT; ++qt) {
             if (qt >= nqt) break;
             const int q = q_lo + qt * 16 + c;
-            const S3 qs = split3(qfa[qt]);
+            S3 qs[NHB];
+#pragma unroll
+            for (int hb = 0; hb < NHB; ++hb) qs[hb] = split3(qfa[qt][hb]);
             const int srow = (sbase + min(q, Tq - 1)) * Tk;
             float sv[NT][4];
             float mx = -INFINITY;
 #pragma unroll
             for (int kt = 0; kt < NT; ++kt) {
-                const floatx4 st = dot_score<true, BF>(ks[kt], qs, zero4());   // C[key 4g+r][query c]
+                floatx4 st = zero4();                                      // C[key 4g+r][query c]
+#pragma unroll
+                for (int hb = 0; hb < NHB; ++hb) st = dot_score<true, BF>(ks[kt][hb], qs[hb], st);
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     float spv = 0.f;
@@ -318,11 +342,11 @@ MEP_DEV void attn_fwd_task(const mep_attn_desc& d, int qc, int h, int b, int lan
                     if (PREV || SOUT) {
                         const int si = srow + min(kk, Tk - 1);
                         if (PREV) spv = sprev[si];
-                        const float v = score<PREV>(st[r], cres, spv, mt[kt][r]);
+                        const float v = score<PREV, HDIM>(st[r], cres, spv, mt[kt][r]);
                         if (SOUT && kk < Tk && q < Tq) sout[si] = v;
                         sv[kt][r] = v;
                     } else {
-                        sv[kt][r] = score<false>(st[r], 0.f, 0.f, mt[kt][r]);
+                        sv[kt][r] = score<false, HDIM>(st[r], 0.f, 0.f, mt[kt][r]);
                     }
                     mx = fmaxf(mx, sv[kt][r]);
                 }
@@ -338,19 +362,27 @@ MEP_DEV void attn_fwd_task(const mep_attn_desc& d, int qc, int h, int b, int lan
                     sv[kt][r] = __expf(sv[kt][r] - mnew);
                     lsum += sv[kt][r];
                 }
-            floatx4 oq = SINGLE ? zero4() : o[qt];
+            floatx4 oq[NHB];
+#pragma unroll
+            for (int hb = 0; hb < NHB; ++hb) oq[hb] = SINGLE ? zero4() : o[qt][hb];
             if (!SINGLE && k_lo > 0) {   // rescale the running state
                 const float corr = __expf(m[qt] - mnew);
                 l[qt] *= corr;
 #pragma unroll
-                for (int r = 0; r < 4; ++r) oq[r] *= shfl(corr, 4 * g + r);  // O row 4g+r <- query 4g+r
+                for (int r = 0; r < 4; ++r) {
+                    const float cr = shfl(corr, 4 * g + r);                  // O row 4g+r <- query 4g+r
+#pragma unroll
+                    for (int hb = 0; hb < NHB; ++hb) oq[hb][r] *= cr;
+                }
             }
             // O += P V over the chunk's 64 keys: key-tile pairs (slots 0-3 / 4-7)
 #pragma unroll
             for (int kt = 0; kt < NT; kt += 2) {
                 if (BF) {   // bf16 P (slots: keys 4g+s of tiles kt / kt+1) against bf16 V
-                    oq = mfma(op(pk(sv[kt][0], sv[kt][1]), pk(sv[kt][2], sv[kt][3]), pk(sv[kt + 1][0], sv[kt + 1][1]),
-                                 pk(sv[kt + 1][2], sv[kt + 1][3])), vbf[kt / 2], oq);
+                    const bf16x8 pb = op(pk(sv[kt][0], sv[kt][1]), pk(sv[kt][2], sv[kt][3]), pk(sv[kt + 1][0], sv[kt + 1][1]),
+                                         pk(sv[kt + 1][2], sv[kt + 1][3]));
+#pragma unroll
+                    for (int hb = 0; hb < NHB; ++hb) oq[hb] = mfma(pb, vbf[kt / 2][hb], oq[hb]);
                     continue;
                 }
                 // fp32 MFMA on the raw P and V (exact fp32 fma chain): a bf16 split of P would need
@@ -358,12 +390,15 @@ MEP_DEV void attn_fwd_task(const mep_attn_desc& d, int qc, int h, int b, int lan
 #pragma unroll
                 for (int k2 = 0; k2 < 2; ++k2)
 #pragma unroll
-                    for (int s = 0; s < 4; ++s) oq = mfma16x4(sv[kt + k2][s], vf[kt + k2][s], oq);
+                    for (int s = 0; s < 4; ++s)
+#pragma unroll
+                        for (int hb = 0; hb < NHB; ++hb) oq[hb] = mfma16x4(sv[kt + k2][s], vf[kt + k2][hb][s], oq[hb]);
             }
             if (SINGLE) {
                 finish(qt, oq, mnew, lsum);
             } else {
-                o[qt] = oq;
+#pragma unroll
+                for (int hb = 0; hb < NHB; ++hb) o[qt][hb] = oq[hb];
                 l[qt] += lsum;
                 m[qt] = mnew;
             }
@@ -378,8 +413,8 @@ MEP_DEV void attn_fwd_task(const mep_attn_desc& d, int qc, int h, int b, int lan
     }
 }
 
-template <bool PREV, bool SOUT, bool SINGLE, bool BF>
-__global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu((SINGLE && !PREV) ? MEP_FWD_WAVES : 2))) void k_attn_fwd(const mep_attn_desc* __restrict__ descs) {
+template <bool PREV, bool SOUT, bool SINGLE, bool BF, int HDIM = HD>
+__global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu((SINGLE && !PREV && HDIM == 16) ? MEP_FWD_WAVES : (HDIM == 32 && !SINGLE) ? 1 : 2))) void k_attn_fwd(const mep_attn_desc* __restrict__ descs) {
     const mep_attn_desc& d = descs[blockIdx.y];
     if ((d.Tk <= CH) != SINGLE) return;    // the other variant's descriptor
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -387,7 +422,7 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu((SINGLE
     const int task = blockIdx.x * WAVES + wave;
     if (task >= d.B * d.H * nqc) return;   // whole wave leaves; no barriers below
     const int qc = task % nqc, bh = task / nqc;
-    attn_fwd_task<PREV, SOUT, SINGLE, BF>(d, qc, bh % d.H, bh / d.H, lane);
+    attn_fwd_task<PREV, SOUT, SINGLE, BF, HDIM>(d, qc, bh % d.H, bh / d.H, lane);
 }
 
 MEP_DEV void wave_lds_sync() {
@@ -718,6 +753,22 @@ extern "C" int mep_attn_fwd(const mep_attn_desc* descs, int n_desc, int max_tile
     const bool prev = flags & MEP_ATTN_PREV, sout = flags & MEP_ATTN_SOUT, bf = flags & MEP_PREC_BF16;
     const dim3 grid(max_tiles, n_desc), block(THREADS);
     hipStream_t st = (hipStream_t)stream;
+    if (flags & MEP_ATTN_HD32) {   // robot_demo (inference, fp32 path)
+        if (bf) { mep_set_error("mep_attn_fwd: hd = 32 runs the fp32 path only"); return MEP_EINVAL; }
+#define MEP_FWD32(P, S, SI) hipLaunchKernelGGL((k_attn_fwd<P, S, SI, false, 32>), grid, block, 0, st, descs)
+        for (int single = 1; single >= 0; --single) {
+            if (!(flags & (single ? MEP_ATTN_SHORT : MEP_ATTN_LONG))) continue;
+            if (single) {
+                if (prev) { if (sout) MEP_FWD32(true, true, true); else MEP_FWD32(true, false, true); }
+                else      { if (sout) MEP_FWD32(false, true, true); else MEP_FWD32(false, false, true); }
+            } else {
+                if (prev) { if (sout) MEP_FWD32(true, true, false); else MEP_FWD32(true, false, false); }
+                else      { if (sout) MEP_FWD32(false, true, false); else MEP_FWD32(false, false, false); }
+            }
+        }
+#undef MEP_FWD32
+        return mep_check_launch("mep_attn_fwd");
+    }
 #define MEP_FWD(P, S, SI) \
     do { if (bf) hipLaunchKernelGGL((k_attn_fwd<P, S, SI, true>), grid, block, 0, st, descs); else hipLaunchKernelGGL((k_attn_fwd<P, S, SI, false>), grid, block, 0, st, descs); } while (0)
     for (int single = 1; single >= 0; --single) {
@@ -740,6 +791,7 @@ extern "C" int mep_attn_bwd(const mep_attn_bwd_desc* descs, int n_desc, int max_
     if (!(flags & (MEP_ATTN_SHORT | MEP_ATTN_LONG))) { mep_set_error("mep_attn_bwd: flags need SHORT and/or LONG"); return MEP_EINVAL; }
     const bool prev = flags & MEP_ATTN_PREV, dsn = flags & MEP_ATTN_SOUT, bf = flags & MEP_PREC_BF16;
     const int dq_tiles = (flags >> 8) & 0xff;
+    if (flags & MEP_ATTN_HD32) { mep_set_error("mep_attn_bwd: hd = 32 is forward-only (robot_demo inference)"); return MEP_EINVAL; }
     const size_t lds = sizeof(float) * ((size_t)RED + WAVES + 256 * (size_t)dq_tiles);
     if (lds > 160 * 1024) { mep_set_error("mep_attn_bwd: Tq too large for the LDS-carried dQ (Tk > 64)"); return MEP_EINVAL; }
     hipStream_t st = (hipStream_t)stream;

@@ -118,7 +118,7 @@ __global__ __launch_bounds__(GEMM_THREADS) void k_gemm(const mep_gemm_desc* __re
             const int tok = r0 + 4 * g + r;
             if (tok >= ntok) continue;
             gfloat* yrow = row_ptr(d.y, tok);
-            const gfloat* trow = table ? table + (int64_t)(tok % d.y.T) * N : nullptr;
+            const gfloat* trow = table ? table + (int64_t)(tok % d.y.T) * (d.ldt ? d.ldt : N) : nullptr;
 #pragma unroll
             for (int j = 0; j < GEMM_NJ; ++j) {
                 const int col = cg + 16 * j + c;
@@ -482,7 +482,7 @@ MEP_DEV void unify_tasks(const mep_gemm_desc& d, const lfloat* wl, int ldl, int 
             if (k0 + p < KB) mma(p, k0 + p);
         if (ok) {
             gfloat* yr = row_ptr(d.y, tok);
-            const gfloat* tr = table ? table + (int64_t)(tok % d.y.T) * d.N : nullptr;
+            const gfloat* tr = table ? table + (int64_t)(tok % d.y.T) * (d.ldt ? d.ldt : d.N) : nullptr;
 #pragma unroll
             for (int i = 0; i < NIP; ++i) {
                 const int col = n0 + 16 * i + 4 * g;
@@ -570,7 +570,7 @@ MEP_DEV void unify_tasks_bf(const mep_gemm_desc& d, const __attribute__((address
             if (p0 + s < NPK) mma(s, p0 + s);
         if (ok) {
             gfloat* yr = row_ptr(d.y, tok);
-            const gfloat* tr = table ? table + (int64_t)(tok % d.y.T) * d.N : nullptr;
+            const gfloat* tr = table ? table + (int64_t)(tok % d.y.T) * (d.ldt ? d.ldt : d.N) : nullptr;
 #pragma unroll
             for (int i = 0; i < NIP; ++i) {
                 const int col = n0 + 16 * i + 4 * g;

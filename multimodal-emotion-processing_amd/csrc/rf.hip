@@ -22,12 +22,12 @@ MEP_DEV bool wvec(uint64_t p, int ld) { return ((p & 15) == 0) && (ld % 4 == 0);
 
 // C[64 x N] = A_lds[64 x K] . W  (NT: W[n*ldw + k], else W[k*ldw + n]); epi(row, col, value)
 // for every element of the tile.  Tasks (m-half, 32-column block) round-robin over the waves.
-template <int N, int K, bool NT, typename Epi>
+template <int N, int K, bool NT, int MH = 2, typename Epi>
 MEP_DEV void tile_gemm(const float* As, int lda, const gfloat* W, int ldw, bool w_vec, Epi&& epi) {
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    constexpr int NTASK = 2 * ((N + 31) / 32);
+    constexpr int NTASK = MH * ((N + 31) / 32);   // MH 32-row halves of the token tile
     for (int t = wave; t < NTASK; t += NWAVE) {
-        const int mh = t & 1, nblk = t >> 1;
+        const int mh = t % MH, nblk = t / MH;
         floatx16 acc = zero16();
         if constexpr (K <= 128) {
             mma_tile_pf<NT, K>(acc, As, lda, mh * 32, W, ldw, nblk * 32, N, 0, K, w_vec);
@@ -43,62 +43,79 @@ MEP_DEV void tile_gemm(const float* As, int lda, const gfloat* W, int ldw, bool 
     }
 }
 
+// Token rows per workgroup of the forward: 64, or 32 for D = 192 (robot_demo.py, inference) so the
+// LDS tiles (x/h, xp/f, f1) stay within 160 KB.
+template <int D>
+constexpr int rf_fwd_rows() { return D > 128 ? 32 : 64; }
+
 template <int D, int FD>
 __global__ __launch_bounds__(THREADS) void k_rf_epi_fwd(const mep_rf_epi_desc* __restrict__ descs) {
+    constexpr int TOK = rf_fwd_rows<D>(), MH = TOK / 32;
+    constexpr int NCL = (D + 63) / 64;   // LayerNorm columns per lane (lane + 64 j)
     const mep_rf_epi_desc& d = descs[blockIdx.y];
-    const int tok0 = blockIdx.x * 64;
+    const int tok0 = blockIdx.x * TOK;
     const int ntok = d.ntok;
     if (tok0 >= ntok) return;
     constexpr int LD = D + 4, LF = FD + 4;
-    __shared__ __attribute__((aligned(16))) float smem[2 * 64 * LD + 64 * LF];
-    float* Xs = smem;                // x, then h
-    float* Ps = smem + 64 * LD;      // xp, then f
-    float* Fs = smem + 2 * 64 * LD;  // f1
+    __shared__ __attribute__((aligned(16))) float smem[2 * TOK * LD + TOK * LF];
+    float* Xs = smem;                 // x, then h
+    float* Ps = smem + TOK * LD;      // xp, then f
+    float* Fs = smem + 2 * TOK * LD;  // f1
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const bool c0 = lane < D, c1 = lane + 64 < D;
+    bool cv[NCL];
+#pragma unroll
+    for (int j = 0; j < NCL; ++j) cv[j] = lane + 64 * j < D;
     const float sa = *G<const float>(d.a), sb = *G<const float>(d.b);
     gfloat* stats = G<float>(d.stats);
 
-    stage_cols<64>(Xs, LD, d.x, tok0, ntok, 0, D);
+    stage_cols<TOK>(Xs, LD, d.x, tok0, ntok, 0, D);
     __syncthreads();
     // xp = x Wp^T
-    tile_gemm<D, D, true>(Xs, LD, G<const float>(d.wp), D, wvec(d.wp, D), [&](int row, int col, float v) {
+    tile_gemm<D, D, true, MH>(Xs, LD, G<const float>(d.wp), D, wvec(d.wp, D), [&](int row, int col, float v) {
         Ps[row * LD + col] = v;
         const int tok = tok0 + row;
         if (tok < ntok) row_ptr(d.xp, tok)[col] = v;
     });
     __syncthreads();
+    // LayerNorm of rows z (per lane columns lane + 64 j) into y = w * (z - mean) * rstd + b
+    auto layer_norm = [&](const gfloat* w, const gfloat* bb, const float (&z)[NCL], float (&y)[NCL], float& mean,
+                          float& rstd) {
+        float s1 = 0.f;
+#pragma unroll
+        for (int j = 0; j < NCL; ++j) s1 += z[j];
+        mean = wave_sum(s1) / (float)D;
+        float dv[NCL], s2 = 0.f;
+#pragma unroll
+        for (int j = 0; j < NCL; ++j) { dv[j] = cv[j] ? z[j] - mean : 0.f; s2 += dv[j] * dv[j]; }
+        rstd = 1.0f / sqrtf(wave_sum(s2) / (float)D + LN_EPS);
+#pragma unroll
+        for (int j = 0; j < NCL; ++j) y[j] = cv[j] ? dv[j] * rstd * w[lane + 64 * j] + bb[lane + 64 * j] : 0.f;
+    };
     // h = LN1(q + a * xp)
-    {
-        const gfloat* w = G<const float>(d.ln1_w);
-        const gfloat* bb = G<const float>(d.ln1_b);
-        const float w0 = c0 ? w[lane] : 0.f, w1 = c1 ? w[lane + 64] : 0.f;
-        const float b0 = c0 ? bb[lane] : 0.f, b1 = c1 ? bb[lane + 64] : 0.f;
-        for (int row = wave; row < 64; row += NWAVE) {
-            const int tok = tok0 + row;
-            float* xr = Xs + row * LD;
-            if (tok >= ntok) {
-                if (c0) xr[lane] = 0.f;
-                if (c1) xr[lane + 64] = 0.f;
-                continue;
-            }
-            const gfloat* qr = row_ptr(d.q, tok);
-            const float z0 = c0 ? add_rn(qr[lane], mul_rn(sa, Ps[row * LD + lane])) : 0.f;
-            const float z1 = c1 ? add_rn(qr[lane + 64], mul_rn(sa, Ps[row * LD + lane + 64])) : 0.f;
-            const float mean = wave_sum(z0 + z1) / (float)D;
-            const float d0 = c0 ? z0 - mean : 0.f, d1 = c1 ? z1 - mean : 0.f;
-            const float rstd = 1.0f / sqrtf(wave_sum(d0 * d0 + d1 * d1) / (float)D + LN_EPS);
-            gfloat* hr = row_ptr(d.h, tok);
-            if (c0) { const float y = d0 * rstd * w0 + b0; xr[lane] = y; hr[lane] = y; }
-            if (c1) { const float y = d1 * rstd * w1 + b1; xr[lane + 64] = y; hr[lane + 64] = y; }
-            if (lane == 0) { stats[4 * tok] = mean; stats[4 * tok + 1] = rstd; }
+    for (int row = wave; row < TOK; row += NWAVE) {
+        const int tok = tok0 + row;
+        float* xr = Xs + row * LD;
+        if (tok >= ntok) {
+#pragma unroll
+            for (int j = 0; j < NCL; ++j) if (cv[j]) xr[lane + 64 * j] = 0.f;
+            continue;
         }
+        const gfloat* qr = row_ptr(d.q, tok);
+        float z[NCL], y[NCL], mean, rstd;
+#pragma unroll
+        for (int j = 0; j < NCL; ++j)
+            z[j] = cv[j] ? add_rn(qr[lane + 64 * j], mul_rn(sa, Ps[row * LD + lane + 64 * j])) : 0.f;
+        layer_norm(G<const float>(d.ln1_w), G<const float>(d.ln1_b), z, y, mean, rstd);
+        gfloat* hr = row_ptr(d.h, tok);
+#pragma unroll
+        for (int j = 0; j < NCL; ++j) if (cv[j]) { xr[lane + 64 * j] = y[j]; hr[lane + 64 * j] = y[j]; }
+        if (lane == 0) { stats[4 * tok] = mean; stats[4 * tok + 1] = rstd; }
     }
     __syncthreads();
     // f1 = relu(h W1^T + b1)
     {
         const gfloat* b1 = G<const float>(d.b1);
-        tile_gemm<FD, D, true>(Xs, LD, G<const float>(d.w1), D, wvec(d.w1, D), [&](int row, int col, float v) {
+        tile_gemm<FD, D, true, MH>(Xs, LD, G<const float>(d.w1), D, wvec(d.w1, D), [&](int row, int col, float v) {
             v = fmaxf(v + b1[col], 0.f);
             Fs[row * LF + col] = v;
             const int tok = tok0 + row;
@@ -109,7 +126,7 @@ __global__ __launch_bounds__(THREADS) void k_rf_epi_fwd(const mep_rf_epi_desc* _
     // f = f1 W2^T + b2
     {
         const gfloat* b2 = G<const float>(d.b2);
-        tile_gemm<D, FD, true>(Fs, LF, G<const float>(d.w2), FD, wvec(d.w2, FD), [&](int row, int col, float v) {
+        tile_gemm<D, FD, true, MH>(Fs, LF, G<const float>(d.w2), FD, wvec(d.w2, FD), [&](int row, int col, float v) {
             v += b2[col];
             Ps[row * LD + col] = v;
             const int tok = tok0 + row;
@@ -118,24 +135,18 @@ __global__ __launch_bounds__(THREADS) void k_rf_epi_fwd(const mep_rf_epi_desc* _
     }
     __syncthreads();
     // out = LN2(h + b * f)
-    {
-        const gfloat* w = G<const float>(d.ln2_w);
-        const gfloat* bb = G<const float>(d.ln2_b);
-        const float w0 = c0 ? w[lane] : 0.f, w1 = c1 ? w[lane + 64] : 0.f;
-        const float b0 = c0 ? bb[lane] : 0.f, b1 = c1 ? bb[lane + 64] : 0.f;
-        for (int row = wave; row < 64; row += NWAVE) {
-            const int tok = tok0 + row;
-            if (tok >= ntok) break;
-            const float z0 = c0 ? add_rn(Xs[row * LD + lane], mul_rn(sb, Ps[row * LD + lane])) : 0.f;
-            const float z1 = c1 ? add_rn(Xs[row * LD + lane + 64], mul_rn(sb, Ps[row * LD + lane + 64])) : 0.f;
-            const float mean = wave_sum(z0 + z1) / (float)D;
-            const float d0 = c0 ? z0 - mean : 0.f, d1 = c1 ? z1 - mean : 0.f;
-            const float rstd = 1.0f / sqrtf(wave_sum(d0 * d0 + d1 * d1) / (float)D + LN_EPS);
-            gfloat* orow = row_ptr(d.out, tok);
-            if (c0) orow[lane] = d0 * rstd * w0 + b0;
-            if (c1) orow[lane + 64] = d1 * rstd * w1 + b1;
-            if (lane == 0) { stats[4 * tok + 2] = mean; stats[4 * tok + 3] = rstd; }
-        }
+    for (int row = wave; row < TOK; row += NWAVE) {
+        const int tok = tok0 + row;
+        if (tok >= ntok) break;
+        float z[NCL], y[NCL], mean, rstd;
+#pragma unroll
+        for (int j = 0; j < NCL; ++j)
+            z[j] = cv[j] ? add_rn(Xs[row * LD + lane + 64 * j], mul_rn(sb, Ps[row * LD + lane + 64 * j])) : 0.f;
+        layer_norm(G<const float>(d.ln2_w), G<const float>(d.ln2_b), z, y, mean, rstd);
+        gfloat* orow = row_ptr(d.out, tok);
+#pragma unroll
+        for (int j = 0; j < NCL; ++j) if (cv[j]) orow[lane + 64 * j] = y[j];
+        if (lane == 0) { stats[4 * tok + 2] = mean; stats[4 * tok + 3] = rstd; }
     }
 }
 
@@ -485,11 +496,16 @@ int dispatch_rf(int D, int FD, F&& f) {
 extern "C" int mep_rf_epi_fwd(const mep_rf_epi_desc* descs, int n_desc, int max_tiles, int D, int FD,
                               mep_stream_t stream) {
     if (n_desc <= 0 || max_tiles <= 0) return 0;
+    if (D == 192 && FD == 384) {   // robot_demo.py (DIM 192, FFN 2): forward only, 32 rows per workgroup
+        hipLaunchKernelGGL((k_rf_epi_fwd<192, 384>), dim3(max_tiles, n_desc), dim3(THREADS), 0, (hipStream_t)stream,
+                           descs);
+        return mep_check_launch("mep_rf_epi_fwd");
+    }
     const int rc = dispatch_rf(D, FD, [&](auto dc, auto fc) {
         hipLaunchKernelGGL((k_rf_epi_fwd<decltype(dc)::value, decltype(fc)::value>), dim3(max_tiles, n_desc),
                            dim3(THREADS), 0, (hipStream_t)stream, descs);
     });
-    if (rc) { mep_set_error("mep_rf_epi_fwd: D in {32,64,96,128} and FD in {D, 2D}"); return rc; }
+    if (rc) { mep_set_error("mep_rf_epi_fwd: D in {32,64,96,128} and FD in {D, 2D}, or D = 192 / FD = 384"); return rc; }
     return mep_check_launch("mep_rf_epi_fwd");
 }
 

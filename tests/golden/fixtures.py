@@ -39,6 +39,8 @@ def batch(meta):
     if fam == 'ren':
         inputs, labels = specs.ren_batch(**spec)
         return tuple(torch.from_numpy(x) for x in inputs), torch.from_numpy(labels)
+    if fam == 'robot':
+        return tuple(torch.from_numpy(x) for x in specs.robot_batch(**spec))
     return tuple(torch.from_numpy(x) for x in specs.realformer_batch(**spec))
 
 

@@ -36,7 +36,8 @@ import specs  # noqa: E402
 from oracle import dropout as odrop  # noqa: E402
 
 REF = '/root/reference'
-SCRIPTS = {'cmu': 'cmu-mosei/run.py', 'realformer': 'others/realformer.py', 'ren': 'Ren-MME/run.py'}
+SCRIPTS = {'cmu': 'cmu-mosei/run.py', 'realformer': 'others/realformer.py', 'ren': 'Ren-MME/run.py',
+           'robot': 'robot_demo.py'}
 
 
 def load_reference(family, overrides):
@@ -235,6 +236,30 @@ def case_chain(name, consts, ctor, B, T, n_layers, seed):
     return meta, out
 
 
+def case_robot(name, ctor, batch, seeds):
+    """robot_demo.py inference (robot_demo.py:597-622): four Multi_class models (parameters from
+    ``seeds``) in eval mode under no_grad on one batch; each model's logits, their ensemble mean
+    (pred_1 + pred_2 + pred_3 + pred_4) / 4 and demo_output's per-emotion probabilities
+    sigmoids(pred[0][c], t_c) for every row."""
+    ns = load_reference('robot', {})
+    models, shapes = [], None
+    for sd in seeds:
+        m = ns['Multi_class'](**ctor)
+        shapes = set_params(m, sd)
+        models.append(m.eval())
+    inputs = [t(x) for x in specs.robot_batch(**batch)]
+    with torch.no_grad():
+        preds = [m(*inputs) for m in models]
+    pred = (preds[0] + preds[1] + preds[2] + preds[3]) / 4
+    thr = (0.1, 0.1, -0.1, 0.0, 0.1, 0.0)     # happ sadn ange disg surp fear (robot_demo.py:609)
+    probs = np.array([[ns['sigmoids'](pred[r][c], thr[c]) for c in range(6)] for r in range(pred.shape[0])])
+    out = {'logits%d' % i: p.numpy() for i, p in enumerate(preds)}
+    out.update(ensemble=pred.numpy(), probs=probs)
+    meta = dict(kind='robot', family='robot', ctor=ctor, batch=batch, seeds=list(seeds), seed=seeds[0],
+                shapes=shapes)
+    return meta, out
+
+
 CMU_C = dict(L_DIM=300, V_DIM=35, A_DIM=74, DROP=0.0)
 REN_C = dict(L_DIM=768, V_DIM=640, A_DIM=205, DROP=0.0)
 
@@ -288,6 +313,11 @@ CASES = {
     'rf_chain_small': lambda: case_chain('rf_chain_small', rf_consts(10),
                                          dict(l_dim=300, v_dim=35, a_dim=74, dim=32, l_len=10, v_len=10,
                                               a_len=10, n_heads=2, n_layers=2, ffn=2), 4, 10, 2, 110),
+    # robot_demo.py's own configuration (DIM 192, N_HEADS 6 -> head dim 32, N_LAYERS 2, FFN 2,
+    # L/V/A_LEN 25/100/100: robot_demo.py:35-43), 4-model ensemble
+    'robot_demo': lambda: case_robot('robot_demo', dict(dim=192, l_len=25, v_len=100, a_len=100, n_heads=6,
+                                                        n_layers=2, ffn=2),
+                                     dict(seed=21, B=3, T=[25, 100, 100]), (121, 122, 123, 124)),
     'rf_chain_cfg2': lambda: case_chain('rf_chain_cfg2', rf_consts(50),
                                         dict(l_dim=300, v_dim=35, a_dim=74, dim=96, l_len=50, v_len=50,
                                              a_len=50, n_heads=6, n_layers=2, ffn=2), 8, 50, 2, 111),

@@ -115,3 +115,15 @@ def block_inputs(seed, B, Tq, Tk, D, H, with_prev=True):
         s_prev = (s_prev - np.float32(1e8) * (np.float32(1.0) - mask[:, None, None, :])).astype(np.float32)
     g_out = rng.standard_normal((B, Tq, D)).astype(np.float32)
     return q, kv, mask, s_prev, g_out
+
+
+def robot_batch(seed, B, T, dims=(768, 256, 512, 1024, 40)):
+    """robot_demo.py Multi_class inputs in its forward order (robot_demo.py:390): l [B,T_l,768],
+    v_256 / v_512 / v_1024 [B,T_v,d], a [B,T_a,40], then the l / v / a masks [B,T_m]."""
+    rng = np.random.default_rng(seed)
+    Tl, Tv, Ta = T
+    lm, vm, am = masks_for(rng, (B,), Tl), masks_for(rng, (B,), Tv), masks_for(rng, (B,), Ta)
+    l = features(rng, (B, Tl, dims[0]), lm)
+    v256, v512, v1024 = (features(rng, (B, Tv, d), vm) for d in dims[1:4])
+    a = features(rng, (B, Ta, dims[4]), am)
+    return l, v256, v512, v1024, a, lm, vm, am

@@ -68,3 +68,22 @@ def test_chain(name):
     for k, p in P.items():
         if 'grad/' + k in gold:
             close(p.grad, gold['grad/' + k], rtol=1e-4, atol=1e-6)
+
+
+def test_robot_demo_inference():
+    """oracle/robot_demo.py against the reference's robot_demo.py classes (4-model ensemble at its
+    own configuration: D=192, 6 heads of 32, 2 layers, FFN 2, T = 25 / 100 / 100)."""
+    from oracle import robot_demo as orb
+    meta, gold = fixtures.load('robot_demo')
+    inputs = fixtures.batch(meta)
+    c = meta['ctor']
+    preds = []
+    for i, sd in enumerate(meta['seeds']):
+        P = fixtures.params(dict(meta, seed=sd), requires_grad=False)
+        with torch.no_grad():
+            preds.append(orb.multi_class(P, *inputs, n_heads=c['n_heads'], n_layers=c['n_layers']))
+        np.testing.assert_allclose(preds[-1].numpy(), gold['logits%d' % i], rtol=1e-4, atol=1e-5)
+    ens = orb.ensemble(preds)
+    np.testing.assert_allclose(ens.numpy(), gold['ensemble'], rtol=1e-4, atol=1e-5)
+    probs = np.array([orb.probabilities(ens[r]) for r in range(ens.shape[0])])
+    np.testing.assert_allclose(probs, gold['probs'], rtol=1e-5)
