@@ -52,10 +52,11 @@ typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
 #ifndef MEP_BWD_DB
-#define MEP_BWD_DB 1       // short backward: next query tile's loads in a second register set
+#define MEP_BWD_DB 0       // short backward: next query tile's loads in a second register set (3 waves
+                           // per SIMD without it beat 2 with it: 46 vs 51 us at cfg3)
 #endif
 #ifndef MEP_BWD_WAVES
-#define MEP_BWD_WAVES 2    // waves per SIMD of the short backward
+#define MEP_BWD_WAVES 3    // waves per SIMD of the short backward
 #endif
 #ifndef MEP_FWD_WAVES
 #define MEP_FWD_WAVES 3    // waves per SIMD of the short, non-residual forward
@@ -137,21 +138,54 @@ MEP_DEV floatx4 dot_score(const S3& p, const S3& u, floatx4 acc) {
     return acc;
 }
 
-// 16-deep contraction, 2-way split, all four products: A = [x0 | x1], B = [y0 | y0] then [y1 | y1]
-// (BF: x0 y0)
+#ifndef MEP_BWD_MF16
+#define MEP_BWD_MF16 1   // backward 2-way products as separate 16x16x16 MFMAs (no operand assembly)
+#endif
+#ifndef MEP_BWD_DVF32
+#define MEP_BWD_DVF32 0  // dV += P^T dO on f32 MFMA from the raw P / dO (no split): 48.6 vs 45.5 us, off
+#endif
+#ifndef MEP_BWD_TR
+#define MEP_BWD_TR 0     // dS transposed as packed [key][query] words + ds_read_b64_tr_b16 (47.6-48.5 vs 45.6 us: off)
+#endif
+#ifndef MEP_BWD_EXP2
+#define MEP_BWD_EXP2 1   // P = exp2(dot * log2e/sqrt(hd) - (mask * log2e + max * log2e)): one fma per score
+#endif
+
+// 16-deep contraction, 2-way split, all four products.  MEP_BWD_MF16: four v_mfma_f32_16x16x16_bf16
+// on the parts as they come out of the split (each a register pair: no operand assembly moves);
+// else two 16x16x32 with A = [x0 | x1], B = [y0 | y0] then [y1 | y1].  (BF: x0 y0.)
 template <bool BF>
 MEP_DEV floatx4 dot16(const S2& x, const S2& y, floatx4 acc) {
     if (BF) return mfma16(op4(x.h0, x.h1), op4(y.h0, y.h1), acc);
+#if MEP_BWD_MF16
+    acc = mfma16(op4(x.h0, x.h1), op4(y.h0, y.h1), acc);
+    acc = mfma16(op4(x.l0, x.l1), op4(y.h0, y.h1), acc);
+    acc = mfma16(op4(x.h0, x.h1), op4(y.l0, y.l1), acc);
+    acc = mfma16(op4(x.l0, x.l1), op4(y.l0, y.l1), acc);
+    return acc;
+#else
     const bf16x8 a = op(x.h0, x.h1, x.l0, x.l1);
     acc = mfma(a, op(y.h0, y.h1, y.h0, y.h1), acc);
     acc = mfma(a, op(y.l0, y.l1, y.l0, y.l1), acc);
     return acc;
+#endif
 }
 
 // 32-deep contraction over two 16-row tiles (slots 0-3: tile 0, 4-7: tile 1), 2-way split,
-// products x0 y0 + x1 y0 + x0 y1 (BF: x0 y0)
+// products x0 y0 + x1 y0 + x0 y1 (BF: x0 y0); MEP_BWD_MF16: per tile on 16x16x16
 template <bool BF>
 MEP_DEV floatx4 dot32(const S2& xa, const S2& xb, const S2& ya, const S2& yb, floatx4 acc) {
+#if MEP_BWD_MF16
+    if (!BF) {
+        acc = mfma16(op4(xa.h0, xa.h1), op4(ya.h0, ya.h1), acc);
+        acc = mfma16(op4(xa.l0, xa.l1), op4(ya.h0, ya.h1), acc);
+        acc = mfma16(op4(xa.h0, xa.h1), op4(ya.l0, ya.l1), acc);
+        acc = mfma16(op4(xb.h0, xb.h1), op4(yb.h0, yb.h1), acc);
+        acc = mfma16(op4(xb.l0, xb.l1), op4(yb.h0, yb.h1), acc);
+        acc = mfma16(op4(xb.h0, xb.h1), op4(yb.l0, yb.l1), acc);
+        return acc;
+    }
+#endif
     const bf16x8 x0 = op(xa.h0, xa.h1, xb.h0, xb.h1), y0 = op(ya.h0, ya.h1, yb.h0, yb.h1);
     acc = mfma(x0, y0, acc);
     if (BF) return acc;
@@ -455,7 +489,7 @@ struct Bwd {
     bool same_kv;
     int k_lo;
     S2 kb[NT], vb[NT], kq[NT];
-    float mtk[NT];
+    float mtk[NT], mtl[NT];   // mask term, and the same times log2(e)
     floatx4 dk[NT], dv[NT];
     float dc_acc;
 
@@ -492,6 +526,7 @@ struct Bwd {
             Kb.ld4(kf, Kb.at(k0 + c, hc + 4 * g));
             if (!same_kv) Vb.ld4(vf, Vb.at(k0 + c, hc + 4 * g));
             mtk[kt] = mask_term(mask, k0 + c, Tk);
+            mtl[kt] = mtk[kt] * 1.4426950408889634f;
             const int okq = Kb.at(k0 + 4 * g, hc + c);
 #pragma unroll
             for (int s = 0; s < 4; ++s) kc4[s] = Kb.ld1(okq, s * Kb.sT4);
@@ -537,8 +572,13 @@ struct Bwd {
             const bool qok = qq < Tq;
             mm[s] = qok ? in.st[s][0] * LOG2E : INFINITY;
             li[s] = qok ? in.st[s][1] : 0.f;
+#if MEP_BWD_EXP2
+            // 1/sum folded into the exponent: P = exp2(.. - (max log2 e - log2(1/sum)))
+            mm[s] = qok ? mm[s] - __builtin_amdgcn_logf(li[s]) : INFINITY;
+#endif
         }
-        const S2 qs = split2(in.qa), do2 = split2(in.da), db2 = split2(in.db), qb2 = split2(in.qb);
+        const S2 qs = split2(in.qa), do2 = split2(in.da), qb2 = split2(in.qb);
+        const S2 db2 = (MEP_BWD_DVF32 && !BF) ? S2{} : split2(in.db);
         typedef __attribute__((address_space(3))) unsigned short lushort;
         lushort* Th = (lushort*)Tr;                 // [16 queries][TLD2] bf16 parts of dS
         lushort* Tl = Th + 16 * TLD2;
@@ -548,7 +588,12 @@ struct Bwd {
             // recomputed scores on the 2-way split (the forward's are 3-way): P differs from the
             // forward's by <= ~2^-16 relative, far inside the gradient tolerance
             const floatx4 st = dot16<BF>(qs, kb[kt], zero4());           // C[query 4g+r][key c]
+#if MEP_BWD_EXP2
+            // dP - delta: the accumulator starts at -delta (query 4g+r)
+            const floatx4 dp = dot16<BF>(do2, vb[kt], floatx4{-del[0], -del[1], -del[2], -del[3]});
+#else
             const floatx4 dp = dot16<BF>(do2, vb[kt], zero4());
+#endif
             float p[4], dsv[4];
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
@@ -559,9 +604,17 @@ struct Bwd {
                     si = (sbase + min(qq, Tq - 1)) * Tk + min(kk, Tk - 1);
                     if (PREV) spv = sprev[si];
                 }
+#if MEP_BWD_EXP2
+                // (dot / 4 [+ c sp] - mask) log2 e - max log2 e with the mask and max terms combined
+                float arg = fmaf(st[r], INV_SCALE * LOG2E, -(mtl[kt] + mm[r]));
+                if (PREV) arg = fmaf(cres * LOG2E, spv, arg);
+                const float pv = __builtin_amdgcn_exp2f(arg);
+                float gsv = pv * dp[r];
+#else
                 const float sv = score<PREV>(st[r], cres, spv, mtk[kt]);
                 const float pv = __builtin_amdgcn_exp2f(fmaf(sv, LOG2E, -mm[r])) * li[r];
                 float gsv = pv * (dp[r] - del[r]);
+#endif
                 if (DSN || PREV) {
                     const bool ok = (qq < Tq) && (kk < Tk);
                     if (DSN) gsv += ok ? dsn[si] : 0.f;
@@ -574,8 +627,24 @@ struct Bwd {
                 dsv[r] = gsv;
             }
             const S2 ds2 = split2(dsv);
-            dv[kt] = dot16<BF>(split2(p), db2, dv[kt]);  // dV[key][dim] += P^T dO
+            if (MEP_BWD_DVF32 && !BF) {                  // dV[key][dim] += P^T dO, exact fp32
+#pragma unroll
+                for (int s = 0; s < 4; ++s) dv[kt] = mfma16x4(p[s], in.db[s], dv[kt]);
+            } else {
+                dv[kt] = dot16<BF>(split2(p), db2, dv[kt]);
+            }
             dk[kt] = dot16<BF>(ds2, qb2, dk[kt]);        // dK[key][dim] += dS^T Q
+#if MEP_BWD_TR
+            // the split dS as packed words into [key][16 queries] images (one 8-byte store per
+            // part: this lane's queries 4g .. 4g+3 of key kt*16 + c)
+            {
+                typedef __attribute__((address_space(3))) u32x2 lu32x2w;
+                lu32x2w* Ih = (lu32x2w*)Tr;
+                const int e = (kt * 16 + c) * 4 + g;       // u32x2 index: row (key) * 4 + column block
+                Ih[e] = u32x2{ds2.h0, ds2.h1};
+                if (!BF) Ih[CH * 4 + e] = u32x2{ds2.l0, ds2.l1};
+            }
+#else
             // the split dS, element by element, into Th / Tl[query][key] (bf16)
             const unsigned hw[4] = {ds2.h0, ds2.h0 >> 16, ds2.h1, ds2.h1 >> 16};
             const unsigned lw[4] = {ds2.l0, ds2.l0 >> 16, ds2.l1, ds2.l1 >> 16};
@@ -584,18 +653,34 @@ struct Bwd {
                 Th[(4 * g + r) * TLD2 + kt * 16 + c] = (unsigned short)hw[r];
                 if (!BF) Tl[(4 * g + r) * TLD2 + kt * 16 + c] = (unsigned short)lw[r];
             }
+#endif
         }
         // dQ += dS K with the query on the lane: the transposed 16 x 64 dS parts, already split,
         // come back as packed words (keys 4g .. 4g+3 of each key tile, one 8-byte read per part)
         wave_lds_sync();
         S2 tq[NT];
         typedef __attribute__((address_space(3))) u32x2 lu32x2;
+#if MEP_BWD_TR
+        // ds_read_b64_tr_b16: lane 4q+p of group g addresses key row kt*16 + 4g + q, queries
+        // 4p .. 4p+3; lane c of the group receives query column c of those 4 key rows -- dS[query
+        // c][keys 4g .. 4g+3], the A operand of dQ += dS K (EXEC is full here: no divergence)
+        typedef __attribute__((address_space(3))) s16x4 ls16x4;
+#pragma unroll
+        for (int kt = 0; kt < NT; ++kt) {
+            const int e = (kt * 16 + 4 * g + (c >> 2)) * 4 + (c & 3);
+            const u32x2 hh = __builtin_bit_cast(u32x2, __builtin_amdgcn_ds_read_tr16_b64_v4i16((ls16x4*)Tr + e));
+            const u32x2 ll = BF ? u32x2{0u, 0u}
+                                : __builtin_bit_cast(u32x2, __builtin_amdgcn_ds_read_tr16_b64_v4i16((ls16x4*)Tr + CH * 4 + e));
+            tq[kt] = S2{hh[0], hh[1], ll[0], ll[1]};
+        }
+#else
 #pragma unroll
         for (int kt = 0; kt < NT; ++kt) {
             const u32x2 hh = *reinterpret_cast<const lu32x2*>(Th + c * TLD2 + kt * 16 + 4 * g);
             const u32x2 ll = BF ? u32x2{0u, 0u} : *reinterpret_cast<const lu32x2*>(Tl + c * TLD2 + kt * 16 + 4 * g);
             tq[kt] = S2{hh[0], hh[1], ll[0], ll[1]};
         }
+#endif
         wave_lds_sync();
         floatx4 dq = zero4();
 #pragma unroll
@@ -615,7 +700,7 @@ struct Bwd {
 // of every dQ row and of its dK / dV rows, so no cross-wave sums are needed; the query tiles are
 // walked with every load of the next tile issued before this tile's math (two register sets).
 template <bool PREV, bool DSN, bool BF>
-__global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(MEP_BWD_WAVES))) void k_attn_bwd_short(const mep_attn_bwd_desc* __restrict__ descs) {
+__global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(PREV ? 2 : MEP_BWD_WAVES))) void k_attn_bwd_short(const mep_attn_bwd_desc* __restrict__ descs) {
     __shared__ __attribute__((aligned(16))) float Tr[WAVES][TFL];
     const mep_attn_bwd_desc& bd = descs[blockIdx.y];
     if (bd.f.Tk > CH) return;                // a LONG descriptor

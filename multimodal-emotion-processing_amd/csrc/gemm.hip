@@ -150,6 +150,9 @@ __global__ __launch_bounds__(GEMM_THREADS) void k_gemm(const mep_gemm_desc* __re
 // column group; the four accumulator blocks are summed through LDS in a fixed order
 // ((w0 + w2) + (w1 + w3)) and written once as partial[split][n][k]; mep_wgrad_reduce sums the
 // splits.  Row views are addressed with 32-bit offsets (hosts keep every view under 2^31 floats).
+#ifndef MEP_WG_PARTS
+#define MEP_WG_PARTS 3   // bf16 parts per fp32 operand on the fp32 path (3: fp32-level)
+#endif
 #ifndef MEP_WG_PF
 #define MEP_WG_PF 1   // 2 would need ~300 arch VGPRs (spills): double-buffered operands
 #endif
@@ -385,8 +388,8 @@ __global__ __launch_bounds__(WG_THREADS, 1) void k_wgrad(const mep_wgrad_desc* _
             if (lin) wgrad_task<M, K, 1, true>(d, split, kbase, red);              \
             else wgrad_task<M, K, 1, false>(d, split, kbase, red);                 \
         } else {                                                                   \
-            if (lin) wgrad_task<M, K, 3, true>(d, split, kbase, red);              \
-            else wgrad_task<M, K, 3, false>(d, split, kbase, red);                 \
+            if (lin) wgrad_task<M, K, MEP_WG_PARTS, true>(d, split, kbase, red);   \
+            else wgrad_task<M, K, MEP_WG_PARTS, false>(d, split, kbase, red);      \
         }                                                                          \
         break;
     switch (8 * mt + kt) {

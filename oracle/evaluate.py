@@ -5,10 +5,11 @@ A line-by-line restatement of the reference's test() loops over precomputed mode
 fp32 torch arithmetic with the reference's own metric calls (sklearn ``accuracy_score`` and
 ``f1_score(average='weighted')``, the third-party code the reference uses; sklearn 1.7.2 here).
 
-Pinning: the reference ships no evaluation fixtures, and its test() functions cannot run as
-written (CUDA tensors, data on ``/home``), so these loops are pinned only by their restatement
-of the reference code and by sklearn itself: parity of the metric arithmetic is sklearn-pinned,
-the loop structure is unpinned by reference outputs.
+Pinning: the reference ships no evaluation fixtures and its test() functions cannot run as
+written (CUDA tensors, data on ``/home``).  tests/golden/make_eval_golden.py therefore runs the
+reference's own test() loops (AST-extracted, CPU tensors for ``torch.cuda.*Tensor``, a data_loader
+and score-returning models over recorded synthetic scores) and records their outputs
+(tests/golden/eval_golden.npz); tests/test_eval.py pins ``rf_test`` and ``cmu_test`` to them.
 
 Deliberately reproduced reference behaviour (others/realformer.py:404-477): the per-class label
 and prediction lists are created once, outside the 400-threshold loop, so the metrics at

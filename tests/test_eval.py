@@ -89,6 +89,39 @@ def test_cmu_counts_path_matches_reference_loop():
         assert abs(acc[0, c] - want[k][0]) < 1e-12 and abs(f1[0, c] - want[k][1]) < 1e-12, k
 
 
+def _eval_golden():
+    import os
+    z = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), 'golden', 'eval_golden.npz'))
+    return {k: z[k] for k in z.files}
+
+
+def test_rf_oracle_pinned_to_reference_test_loop():
+    """oracle/evaluate.rf_test against the reference's own test() (others/realformer.py:395-477,
+    AST-extracted and run on recorded scores by tests/golden/make_eval_golden.py), cumulative lists
+    and strict '>' selection included; then the repo's counts formulation against the same."""
+    g = _eval_golden()
+    batches = [(torch.from_numpy(g['rf_pred1'][k]), torch.from_numpy(g['rf_pred2'][k]),
+                torch.from_numpy(g['rf_label'][k]), torch.from_numpy(g['rf_mask'][k]))
+               for k in range(g['rf_pred1'].shape[0])]
+    want = g['rf_best']
+    got = oev.rf_test(batches, 400)
+    np.testing.assert_allclose(np.array(got, np.float64), want, rtol=0, atol=1e-12)
+    got2 = evaluate.rf_select(_rf_counts_oracle(batches, 400), 400, cumulative=True)
+    np.testing.assert_allclose(np.array(got2, np.float64), want, rtol=0, atol=1e-12)
+
+
+def test_cmu_oracle_pinned_to_reference_test_loop():
+    """oracle/evaluate.cmu_test against the accuracy / F1 lines the reference's test()
+    (cmu-mosei/run.py:456-498) printed for the recorded 4-model scores."""
+    g = _eval_golden()
+    preds, labels = g['cmu_preds'], g['cmu_label']
+    rows = [([torch.from_numpy(preds[m, k]) for m in range(preds.shape[0])], torch.from_numpy(labels[k][None]))
+            for k in range(labels.shape[0])]
+    got = oev.cmu_test(rows)
+    for i, k in enumerate(('happ', 'sadn', 'ange', 'fear', 'disg', 'surp')):
+        np.testing.assert_allclose(got[k], g['cmu_metrics'][i], rtol=0, atol=1e-12, err_msg=k)
+
+
 # ------------------------------------------------------------------------------------------ GPU
 SWEEP_CASES = [
     # (N, C, n_thr, n_models, P, per_class, strided)
