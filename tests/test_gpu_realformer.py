@@ -82,9 +82,10 @@ def test_text_chain(name, cuda):
 
 
 def _check_out(out, want, um, rtol, atol_frac):
-    real = um.bool().cpu()
+    """Every utterance slot, padded ones (um = 0) included: the reference returns outputs for all
+    P slots (others/realformer.py:272-286) and the padded slots match too (3e-7 on rf_state_small)."""
     assert torch.isfinite(out).all()
-    assert_close(out.detach().cpu()[real], torch.as_tensor(want)[real], rtol, atol_frac, 'out')
+    assert_close(out.detach().cpu(), torch.as_tensor(want), rtol, atol_frac, 'out')
 
 
 def _state(meta, cuda):
