@@ -90,16 +90,18 @@ int mep_unify(const mep_gemm_desc* descs, int n_desc, int n_wg, mep_stream_t str
 /* ---------------------------------------------------------------- weight-gradient GEMM
  * dW_i[n, k] (+)= sum_tok A[tok, n] * B_i[tok, k]   for up to 4 operands B_i sharing one A
  * (dW = dY^T X of every nn.Linear on the path; e.g. minus.weight = dZ^T [q | xp] is one
- * descriptor with two B operands).  Tiling: MT = ceil(N/32) row tiles of 32 x 32 (f32 MFMA
- * 32x32x2), column groups of KT tiles (KT = 3, 2, 4, 4 for MT = 3, 4, 2, 1).  One workgroup
- * (4 waves) owns a token chunk of tok_per_split rows (a multiple of 8) and one column group,
- * and writes partial[split][n][k]; mep_wgrad_reduce sums the splits in a fixed order into out_i.
+ * descriptor with two B operands).  Tiling: MT = ceil(N/32) row tiles of 32 x 32
+ * (v_mfma_f32_32x32x16_bf16 on 3-part split operands, or plain bf16 with desc.bf16), column
+ * groups of KT tiles (KT = 3, 2, 4, 4 for MT = 3, 4, 2, 1).  A workgroup (4 waves) runs token
+ * ranges ("segments") of column groups and writes each into a partial slot
+ * partial[slot][n][k]; mep_wgrad_reduce sums the n_split slots in a fixed order into out_i
+ * (slots a column group never writes must hold zeros: hosts zero the workspace once).
  * N <= 128; partial holds n_split * N * Ktot floats; every row view of a descriptor shares T
- * and spans < 2^31 floats.
- * mep_wgrad: `descs` holds the n_desc descriptors FOLLOWED BY max_tiles int32 task entries
- * (descriptor index << 16 | workgroup index within the descriptor, split-major), one per
- * workgroup of the flat grid.  mep_wgrad_reduce: grid (max_tiles, n_desc), max_tiles =
- * max(ceil(N*Ktot/256)). */
+ * and spans < 2^31 floats.  tok_per_split: unused (0).
+ * mep_wgrad: `descs` holds the n_desc descriptors FOLLOWED BY an int32 map: max_tiles + 1 CSR
+ * offsets (workgroup w runs segments off[w] .. off[w+1]-1 in order), then 4 int32 per segment
+ * {descriptor << 8 | column group, t_begin, t_end, slot}.  mep_wgrad_reduce: grid (max_tiles,
+ * n_desc), max_tiles = max(ceil(N*Ktot/256)). */
 #define MEP_WG_MAX_B 4
 typedef struct {
     mep_rows a;                  /* [ntok, N]  (dY)                           */

@@ -180,13 +180,12 @@ MEP_DEV int wg_step(const mep_rows& r) { return (int)(r.T == 1 ? r.sB : r.sT); }
 // fixed byte distances, so they are ONE per-lane base (VGPR) plus a wave-uniform per-token offset
 // (the load's SGPR soffset) and the column tile an immediate: no address arithmetic per token.
 template <int MT, int KT, int NPART, bool LIN>
-MEP_DEV void wgrad_task(const mep_wgrad_desc& d, int split, int kbase, lfloat* red) {
+MEP_DEV void wgrad_task(const mep_wgrad_desc& d, int t_begin, int t_end, int slot, int kbase, lfloat* red) {
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int c = lane & 31, h = lane >> 5;
     const int N = d.N;
-    const int t_begin = split * d.tok_per_split;
-    const int t_end = min(d.ntok, t_begin + d.tok_per_split);
-    const int per_wave = d.tok_per_split / WG_WAVES;
+    t_end = min(d.ntok, t_end);
+    const int per_wave = (max(0, t_end - t_begin) + WG_WAVES - 1) / WG_WAVES;
     const int w0 = t_begin + wave * per_wave;
     const int n = max(0, min(t_end, w0 + per_wave) - w0);
     const int half = (n + 1) >> 1;                         // tokens of lane half 0 (half 1: n - half)
@@ -359,48 +358,81 @@ MEP_DEV void wgrad_task(const mep_wgrad_desc& d, int split, int kbase, lfloat* r
     }
     __syncthreads();
     const int kcnt = min(32 * KT, d.Ktot - kbase);
-    gfloat* part = G<float>(d.partial) + (int64_t)split * N * d.Ktot + kbase;
+    gfloat* part = G<float>(d.partial) + (int64_t)slot * N * d.Ktot + kbase;
     for (int e = threadIdx.x; e < N * 32 * KT; e += WG_THREADS) {
         const int nn = e / (32 * KT), k = e - nn * (32 * KT);
         if (k < kcnt) part[(int64_t)nn * d.Ktot + k] = red[nn * LDR + k] + red[BUF + nn * LDR + k];
     }
 }
 
-// Flat grid: workgroup w runs task map[w] = (descriptor << 16 | index within the descriptor);
-// the map is stored right after the n_desc descriptors.
-__global__ __launch_bounds__(WG_THREADS, 1) void k_wgrad(const mep_wgrad_desc* __restrict__ descs, int n_desc) {
-    const int task = reinterpret_cast<const int*>(descs + n_desc)[blockIdx.x];
-    const mep_wgrad_desc& d = descs[task >> 16];
-    const int local = task & 0xffff;
-    const int mt = (d.N + 31) >> 5, ktm = wg_kt(mt);
-    const int ktiles = (d.Ktot + 31) >> 5;
-    const int ncg = (ktiles + ktm - 1) / ktm;
-    const int split = local / ncg, cg = local - split * ncg;
-    const int kt = min(ktm, ktiles - cg * ktm);
-    const int kbase = 32 * ktm * cg;
+// Flat grid of n_wg workgroups.  The map after the n_desc descriptors: off[n_wg + 1] (CSR), then
+// 4-int segments {desc << 8 | column group, t_begin, t_end, slot}.  Workgroup w runs segments
+// off[w] .. off[w+1]-1 in order: tokens [t_begin, t_end) of one column group of one descriptor,
+// written to partial slot `slot` (slots never written stay zero: hosts zero the workspace once).
+// The host cuts the launch's total MFMA work into n_wg equal contiguous ranges, so a workgroup
+// may finish one descriptor's token range and start another's.
+#ifdef MEP_WG_TRACE
+// development build only: per-workgroup wall-clock stamps and hardware ids
+__device__ unsigned long long* g_wg_trace;
+#endif
+__global__ __launch_bounds__(WG_THREADS, 1) void k_wgrad(const mep_wgrad_desc* __restrict__ descs, int n_desc, int n_wg) {
+#ifdef MEP_WG_TRACE
+    const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
+#endif
+    const int* map = reinterpret_cast<const int*>(descs + n_desc);
+    const int s0 = map[blockIdx.x], s1 = map[blockIdx.x + 1];
+    const int* seg = map + n_wg + 1;
     __shared__ __attribute__((aligned(16))) float smem[2 * WG_RED];
     lfloat* red = (lfloat*)&smem[0];
-    bool lin = wg_linear(d.a);
-    for (int o = 0; o < d.n_b; ++o) lin = lin && wg_linear(d.b[o]);
-#define MEP_WGT(M, K)                                                              \
-    case 8 * M + K:                                                                \
-        if (d.bf16) {                                                              \
-            if (lin) wgrad_task<M, K, 1, true>(d, split, kbase, red);              \
-            else wgrad_task<M, K, 1, false>(d, split, kbase, red);                 \
-        } else {                                                                   \
-            if (lin) wgrad_task<M, K, MEP_WG_PARTS, true>(d, split, kbase, red);   \
-            else wgrad_task<M, K, MEP_WG_PARTS, false>(d, split, kbase, red);      \
-        }                                                                          \
-        break;
-    switch (8 * mt + kt) {
-        MEP_WGT(1, 1) MEP_WGT(1, 2) MEP_WGT(1, 3) MEP_WGT(1, 4)
-        MEP_WGT(2, 1) MEP_WGT(2, 2) MEP_WGT(2, 3) MEP_WGT(2, 4)
-        MEP_WGT(3, 1) MEP_WGT(3, 2) MEP_WGT(3, 3)
-        MEP_WGT(4, 1) MEP_WGT(4, 2)
-        default: break;
-    }
+    for (int si = s0; si < s1; ++si) {
+        const int hdr = seg[4 * si], t_begin = seg[4 * si + 1], t_end = seg[4 * si + 2], slot = seg[4 * si + 3];
+        const mep_wgrad_desc& d = descs[hdr >> 8];
+        const int cg = hdr & 0xff;
+        const int mt = (d.N + 31) >> 5, ktm = wg_kt(mt);
+        const int ktiles = (d.Ktot + 31) >> 5;
+        const int kt = min(ktm, ktiles - cg * ktm);
+        const int kbase = 32 * ktm * cg;
+        if (si > s0) __syncthreads();   // the previous segment's partial write has read `red`
+        bool lin = wg_linear(d.a);
+        for (int o = 0; o < d.n_b; ++o) lin = lin && wg_linear(d.b[o]);
+#define MEP_WGT(M, K)                                                                          \
+        case 8 * M + K:                                                                        \
+            if (d.bf16) {                                                                      \
+                if (lin) wgrad_task<M, K, 1, true>(d, t_begin, t_end, slot, kbase, red);       \
+                else wgrad_task<M, K, 1, false>(d, t_begin, t_end, slot, kbase, red);          \
+            } else {                                                                           \
+                if (lin) wgrad_task<M, K, MEP_WG_PARTS, true>(d, t_begin, t_end, slot, kbase, red);  \
+                else wgrad_task<M, K, MEP_WG_PARTS, false>(d, t_begin, t_end, slot, kbase, red);     \
+            }                                                                                  \
+            break;
+        switch (8 * mt + kt) {
+            MEP_WGT(1, 1) MEP_WGT(1, 2) MEP_WGT(1, 3) MEP_WGT(1, 4)
+            MEP_WGT(2, 1) MEP_WGT(2, 2) MEP_WGT(2, 3) MEP_WGT(2, 4)
+            MEP_WGT(3, 1) MEP_WGT(3, 2) MEP_WGT(3, 3)
+            MEP_WGT(4, 1) MEP_WGT(4, 2)
+            default: break;
+        }
 #undef MEP_WGT
+    }
+#ifdef MEP_WG_TRACE
+    __syncthreads();
+    if (threadIdx.x == 0 && g_wg_trace) {
+        const unsigned long long t_end = __builtin_amdgcn_s_memrealtime();
+        const unsigned hw = __builtin_amdgcn_s_getreg((31 << 11) | 4), xcc = __builtin_amdgcn_s_getreg((31 << 11) | 20);
+        unsigned long long* o = g_wg_trace + 4 * blockIdx.x;
+        o[0] = t_start;
+        o[1] = t_end;
+        o[2] = hw;
+        o[3] = xcc;
+    }
+#endif
 }
+
+#ifdef MEP_WG_TRACE
+extern "C" int mep_wgrad_set_trace(void* p) {
+    return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_wg_trace), &p, sizeof(p));
+}
+#endif
 
 __global__ __launch_bounds__(256) void k_wgrad_reduce(const mep_wgrad_desc* __restrict__ descs) {
     wgrad_reduce_block(descs[blockIdx.y], blockIdx.x);
@@ -676,7 +708,7 @@ extern "C" int mep_gemm(const mep_gemm_desc* descs, int n_desc, int max_tiles, m
 
 extern "C" int mep_wgrad(const mep_wgrad_desc* descs, int n_desc, int max_tiles, mep_stream_t stream) {
     if (n_desc <= 0 || max_tiles <= 0) return 0;
-    hipLaunchKernelGGL(k_wgrad, dim3(max_tiles), dim3(WG_THREADS), 0, (hipStream_t)stream, descs, n_desc);
+    hipLaunchKernelGGL(k_wgrad, dim3(max_tiles), dim3(WG_THREADS), 0, (hipStream_t)stream, descs, n_desc, max_tiles);
     return mep_check_launch("mep_wgrad");
 }
 

@@ -42,6 +42,7 @@ def cdiv(a, b):
 
 WG_WAVES = 4              # csrc/gemm.hip k_wgrad: waves per workgroup (token quarters of a split)
 WG_TARGET = _lib.N_CU      # workgroups per launch: one per CU (4 waves of ~400 registers)
+WG_TARGET_OVERRIDE = None  # development: another workgroup count for wgrad_segments
 
 
 def wgrad_geometry(N, ktot):
@@ -52,30 +53,51 @@ def wgrad_geometry(N, ktot):
     return mt, kt, cdiv(cdiv(ktot, 32), kt)
 
 
-def wgrad_splits(items, n_wg=WG_TARGET):
-    """Token chunk per item such that the launch holds AT MOST n_wg workgroups, all resident at
-    once (one per CU), and the largest workgroup's MFMA work (32x32 tiles x tokens) is as small
-    as the quantisation allows: the kernel lasts as long as its busiest CU, so a launch of 264
-    workgroups (8 CUs running two in turn) takes twice as long as one of 256.  Multiples of 8
-    tokens (four waves)."""
-    geo = [wgrad_geometry(N, sum(b[1] for b in bs)) for (_, N, n, bs, _) in items]
-    tiles = [mt * kt for (mt, kt, ncg) in geo]
-    total = sum(n * t * ncg for t, (_, _, ncg), (_, N, n, bs, _) in zip(tiles, geo, items))
-
-    def split(budget):
-        tps = []
-        for t, (_, N, n, bs, _) in zip(tiles, items):
-            ns = max(1, cdiv(n * t, max(1, int(budget))))
-            tps.append(max(8, cdiv(cdiv(n, ns), 8) * 8))
-        wgs = sum(cdiv(n, p) * ncg for p, (_, _, ncg), (_, N, n, bs, _) in zip(tps, geo, items))
-        return tps, wgs
-
-    budget = max(8.0, total / float(n_wg))
-    while True:
-        tps, wgs = split(budget)
-        if wgs <= n_wg:
-            return tps
-        budget *= 1.01
+def wgrad_segments(items, n_wg=WG_TARGET, tok_per_split=None):
+    """Split every (item, column group) token span into segments, one per workgroup, at most
+    n_wg workgroups (all resident at once, one per CU: the kernel lasts as long as its busiest
+    CU), minimising the largest workgroup's cost.  The cost of a token is its operand loads,
+    MT + KT dwords per lane (a per-workgroup trace, scripts/wgrad_trace.py, shows the kernel
+    load / latency-bound: a 3 x 1-tile column group costs ~0.7x a 3 x 3 one per token, not 1/3).
+    -> (per-workgroup segment lists [(item, cg, t0, t1, slot)], slots per item).  tok_per_split:
+    fixed chunks instead (tests)."""
+    units = []
+    for i, (_, N, n, bs, _) in enumerate(items):
+        mt, kt, ncg = wgrad_geometry(N, sum(b[1] for b in bs))
+        ktiles = cdiv(sum(b[1] for b in bs), 32)
+        for cg in range(ncg):
+            if n > 0:
+                units.append((i, cg, mt + min(kt, ktiles - cg * kt), n))
+    bins = []
+    if tok_per_split is not None:
+        for (i, cg, t, n) in units:
+            tps = tok_per_split[i] if isinstance(tok_per_split, (list, tuple)) else tok_per_split
+            bins += [[(i, cg, t0, min(n, t0 + tps))] for t0 in range(0, n, tps)]
+    else:
+        # water-filling: split the unit whose workgroups carry the most work until n_wg workgroups;
+        # one segment per workgroup (a workgroup running two segments pays the pipeline start and
+        # the reduction twice: ~15 us each, scripts/wgrad_trace.py)
+        ns = [1] * len(units)
+        while sum(ns) < n_wg:
+            u = max(range(len(units)), key=lambda k: (units[k][2] * units[k][3] / ns[k], -k))
+            if units[u][3] < 16 * (ns[u] + 1):
+                break
+            ns[u] += 1
+        for u, (i, cg, t, n) in enumerate(units):
+            cuts = [cdiv(n * k, ns[u] * 8) * 8 for k in range(ns[u])] + [n]
+            bins += [[(i, cg, a, b)] for a, b in zip(cuts[:-1], cuts[1:]) if b > a]
+    slots = [0] * len(items)
+    count = {}
+    segs = []
+    for b in bins:
+        out = []
+        for (i, cg, t0, t1) in b:
+            s = count.get((i, cg), 0)
+            count[(i, cg)] = s + 1
+            slots[i] = max(slots[i], s + 1)
+            out.append((i, cg, t0, t1, s))
+        segs.append(out)
+    return segs, slots
 
 
 UN_LDS = 30720   # csrc/gemm.hip k_unify: floats of LDS for the staged weight
@@ -111,20 +133,15 @@ def make_wgrad(items, dev, tok_per_split=None, bf16=False):
     """items: [(a_rows, N, ntok, [(b_rows, K, out_ptr, ldo), ...][, out_trans]), ...] ->
     (workspace, descs, wgrad workgroups, reduce tiles).  One descriptor per A operand; its B operands
     concatenate on K.  out_trans: dW written transposed (out[k * ldo + n]).  tok_per_split: None =
-    balanced per item (wgrad_splits), else a fixed token chunk.  bf16: plain bf16 operands (the
-    bf16 path) instead of the 3-part split."""
+    the launch's work balanced over one workgroup per CU (wgrad_segments), else fixed token
+    chunks.  bf16: plain bf16 operands (the bf16 path) instead of the 3-part split."""
     items = [tuple(it) + (0,) * (5 - len(it)) for it in items]
-    if tok_per_split is None:
-        tps = wgrad_splits(items)
-    elif isinstance(tok_per_split, int):
-        tps = [tok_per_split] * len(items)
-    else:
-        tps = list(tok_per_split)
-    total = sum(cdiv(n, t) * N * sum(b[1] for b in bs) for t, (_, N, n, bs, _) in zip(tps, items))
-    ws = torch.zeros(max(total, 1), dtype=torch.float32, device=dev)
-    descs, tasks, off, rmax = [], [], 0, 0
-    for tok_per_split, (a, N, n, bs, trans) in zip(tps, items):
-        assert N <= 128 and len(bs) <= _lib.WG_MAX_B and tok_per_split % 8 == 0
+    segs, slots = wgrad_segments(items, n_wg=WG_TARGET_OVERRIDE or WG_TARGET, tok_per_split=tok_per_split)
+    total = sum(max(1, s) * N * sum(b[1] for b in bs) for s, (_, N, n, bs, _) in zip(slots, items))
+    ws = torch.zeros(max(total, 1), dtype=torch.float32, device=dev)   # unwritten slots stay 0
+    descs, off, rmax = [], 0, 0
+    for ns, (a, N, n, bs, trans) in zip(slots, items):
+        assert N <= 128 and len(bs) <= _lib.WG_MAX_B
         # k_wgrad: every 32-column tile reads one operand (wave-uniform buffer resource)
         assert all(b[1] % 32 == 0 for b in bs[:-1]), 'wgrad B operand boundaries must be multiples of 32'
         ktot = sum(b[1] for b in bs)
@@ -132,7 +149,7 @@ def make_wgrad(items, dev, tok_per_split=None, bf16=False):
             # k_wgrad: one token -> (b, t) map for every view of the item; 32-bit byte offsets
             assert v.T == a.T, 'wgrad views of one item must share T'
             assert 4 * ((cdiv(n, v.T) - 1) * v.sB + (v.T - 1) * v.sT + w) < 2 ** 31
-        ns = cdiv(n, tok_per_split)
+        ns = max(1, ns)
         pad = [(Rows(), 0, 0, 0)] * (_lib.WG_MAX_B - len(bs))
         allb = list(bs) + pad
         descs.append(WgradDesc(a=a, b=(Rows * _lib.WG_MAX_B)(*[b[0] for b in allb]),
@@ -140,13 +157,17 @@ def make_wgrad(items, dev, tok_per_split=None, bf16=False):
                                kb=(ctypes.c_int32 * _lib.WG_MAX_B)(*[b[1] for b in allb]),
                                ldo=(ctypes.c_int32 * _lib.WG_MAX_B)(*[b[3] for b in allb]),
                                partial=ws.data_ptr() + 4 * off, n_b=len(bs), ntok=n, N=N, Ktot=ktot,
-                               tok_per_split=tok_per_split, n_split=ns, accumulate=0, out_trans=int(trans),
+                               tok_per_split=0, n_split=ns, accumulate=0, out_trans=int(trans),
                                bf16=int(bool(bf16))))
         off += ns * N * ktot
-        tasks += [(len(descs) - 1) << 16 | w for w in range(ns * wgrad_geometry(N, ktot)[2])]
         rmax = max(rmax, cdiv(N * ktot, 256))
-    assert len(tasks) < 2 ** 31 and all((t & 0xffff) < 0xffff for t in tasks)
-    return ws, DescArray(WgradDesc, descs, dev, tail=tasks), len(tasks), rmax
+    assert len(descs) < 2 ** 23 and all(cg < 256 for b in segs for (_, cg, _, _, _) in b)
+    offs, flat = [0], []
+    for b in segs:
+        for (i, cg, t0, t1, s) in b:
+            flat += [(i << 8) | cg, t0, t1, s]
+        offs.append(offs[-1] + len(b))
+    return ws, DescArray(WgradDesc, descs, dev, tail=offs + flat), len(segs), rmax
 
 
 def rows(t, T, sB, sT, off=0):
