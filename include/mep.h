@@ -156,6 +156,10 @@ typedef struct {
 #define MEP_ATTN_LONG  8
 #define MEP_ATTN_DQ_TILES(n) ((n) << 8)
 #define MEP_ATTN_HD32  0x20000   /* head dim 32 (robot_demo.py, D = 192 / H = 6): forward only, fp32 path */
+#define MEP_ATTN_KV    0x40000   /* backward: every descriptor has k == v and dk == dv (cmu-mosei, Ren-MME:
+                                    cmu-mosei/run.py:241-242 attends with k = v): the short kernel keeps one
+                                    register set for K / V and one dK + dV accumulator (4 waves per SIMD);
+                                    a descriptor that breaks the promise gets NaN dq rows */
 int mep_attn_fwd(const mep_attn_desc* descs, int n_desc, int max_tiles, int flags, mep_stream_t stream);
 
 /* Backward of the attention core.  Inputs dx (grad of X), the forward's q/k/v/x/stats/s_prev.

@@ -260,6 +260,7 @@ def launch(name, descs, max_tiles, stream=None, threads=None, extra=()):
 ATTN_PREV, ATTN_SOUT, ATTN_SHORT, ATTN_LONG = 1, 2, 4, 8   # MEP_ATTN_* (include/mep.h)
 PREC_BF16 = 0x10000   # MEP_PREC_BF16: bf16-operand products (attention flags, epilogue D argument)
 ATTN_HD32 = 0x20000   # MEP_ATTN_HD32: head dim 32 attention forward (robot_demo)
+ATTN_KV = 0x40000     # MEP_ATTN_KV: backward with k == v and dk == dv on every descriptor
 
 
 def rf_epi_rows(D):
@@ -291,12 +292,16 @@ def attn_geometry(descs):
 def attn_bwd_flags(bdescs):
     """AttnBwdDesc list of one launch -> MEP_ATTN_PREV | MEP_ATTN_SOUT (= ds_next present) |
     MEP_ATTN_DQ_TILES(largest ceil(Tq/16) among descriptors with Tk > 64: the query tiles whose dQ
-    the backward carries across key chunks in LDS)"""
+    the backward carries across key chunks in LDS) | MEP_ATTN_KV when every descriptor has k == v
+    and dk == dv (the same row view)"""
+    same = lambda x, y: (x.ptr, x.sB, x.sT) == (y.ptr, y.sB, y.sT)  # noqa: E731
+    kv = bool(bdescs) and all(same(b.f.k, b.f.v) and same(b.dk, b.dv) for b in bdescs)
     dq_tiles = max([-(-b.f.Tq // 16) for b in bdescs if b.f.Tk > 64] or [0])
     assert dq_tiles <= ATTN_MAX_DQ_TILES, 'mep_attn_bwd: Tq > %d with Tk > 64 exceeds the LDS' % (16 * ATTN_MAX_DQ_TILES)
     return (ATTN_PREV if _uniform([b.f.s_prev != 0 for b in bdescs], 's_prev') else 0) | \
            (ATTN_SOUT if _uniform([b.ds_next != 0 for b in bdescs], 'ds_next') else 0) | (dq_tiles << 8) | \
-           (ATTN_SHORT if any(b.f.Tk <= 64 for b in bdescs) else 0) | (ATTN_LONG if any(b.f.Tk > 64 for b in bdescs) else 0)
+           (ATTN_SHORT if any(b.f.Tk <= 64 for b in bdescs) else 0) | (ATTN_LONG if any(b.f.Tk > 64 for b in bdescs) else 0) | \
+           (ATTN_KV if kv else 0)
 
 
 N_CU = 256   # MI355X compute units

@@ -58,6 +58,9 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 #ifndef MEP_BWD_WAVES
 #define MEP_BWD_WAVES 3    // waves per SIMD of the short backward
 #endif
+#ifndef MEP_BWD_WAVES_KV
+#define MEP_BWD_WAVES_KV 4 // waves per SIMD of the short backward with MEP_ATTN_KV (<= 128 registers)
+#endif
 #ifndef MEP_FWD_WAVES
 #define MEP_FWD_WAVES 3    // waves per SIMD of the short, non-residual forward
 #endif
@@ -255,6 +258,9 @@ struct BRow {
 };
 
 MEP_DEV __amdgpu_buffer_rsrc_t uniform_rsrc(uint64_t base, int64_t bytes) {
+#ifdef MEP_ATTN_NOLOAD   // timing-only development build: row / stats loads return 0, stores dropped
+    bytes = 0;
+#endif
     const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)base);
     const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(base >> 32));
     const int n = __builtin_amdgcn_readfirstlane((int)min(bytes, (int64_t)0x7fffffff));
@@ -470,8 +476,10 @@ MEP_DEV void wave_lds_sync() {
 // (B of S = K rows with the key on the lane, B of dP = V rows, B of dQ = K columns rows 4g+s /
 // dim c, the keys' mask terms) and the chunk's dK / dV accumulators (C[key 4g+r][dim c]).
 // PREV: residual scores (writes dS_prev, sums the dc partial); DSN: a gradient arrives on this
-// layer's post-mask S output; BF: the bf16 path (one bf16 product per contraction).
-template <bool PREV, bool DSN, bool BF>
+// layer's post-mask S output; BF: the bf16 path (one bf16 product per contraction); KV: k is v
+// and dk is dv (MEP_ATTN_KV: one register set for the K / V rows and ONE accumulator per key tile
+// for dK + dV, with Q pre-scaled by the exact 1/sqrt(hd) = 1/4 -- about 32 registers fewer).
+template <bool PREV, bool DSN, bool BF, bool KV = false>
 struct Bwd {
     // per query tile: A of S (Q rows), A of dP (dO rows), B of dV / dK (dO / Q columns), O
     // columns for delta, row stats and the dq rows this tile accumulates onto
@@ -524,17 +532,17 @@ struct Bwd {
             const int k0 = k_lo + kt * 16;
             float kf[4], vf[4], kc4[4];
             Kb.ld4(kf, Kb.at(k0 + c, hc + 4 * g));
-            if (!same_kv) Vb.ld4(vf, Vb.at(k0 + c, hc + 4 * g));
+            if (!KV && !same_kv) Vb.ld4(vf, Vb.at(k0 + c, hc + 4 * g));
             mtk[kt] = mask_term(mask, k0 + c, Tk);
             mtl[kt] = mtk[kt] * 1.4426950408889634f;
             const int okq = Kb.at(k0 + 4 * g, hc + c);
 #pragma unroll
             for (int s = 0; s < 4; ++s) kc4[s] = Kb.ld1(okq, s * Kb.sT4);
             kb[kt] = split2(kf);
-            vb[kt] = same_kv ? kb[kt] : split2(vf);     // k is v (cmu-mosei, Ren-MME)
+            if (!KV) vb[kt] = same_kv ? kb[kt] : split2(vf);     // k is v (cmu-mosei, Ren-MME)
             kq[kt] = split2(kc4);
             dk[kt] = zero4();
-            dv[kt] = zero4();
+            if (!KV) dv[kt] = zero4();
         }
         dc_acc = 0.f;
     }
@@ -577,7 +585,16 @@ struct Bwd {
             mm[s] = qok ? mm[s] - __builtin_amdgcn_logf(li[s]) : INFINITY;
 #endif
         }
-        const S2 qs = split2(in.qa), do2 = split2(in.da), qb2 = split2(in.qb);
+        const S2 qs = split2(in.qa), do2 = split2(in.da);
+        S2 qb2;
+        if (KV) {   // dK folded into the dV accumulator: Q columns times the exact 1/sqrt(hd)
+            float q4[4];
+#pragma unroll
+            for (int s = 0; s < 4; ++s) q4[s] = in.qb[s] * INV_SCALE;
+            qb2 = split2(q4);
+        } else {
+            qb2 = split2(in.qb);
+        }
         const S2 db2 = (MEP_BWD_DVF32 && !BF) ? S2{} : split2(in.db);
         typedef __attribute__((address_space(3))) unsigned short lushort;
         lushort* Th = (lushort*)Tr;                 // [16 queries][TLD2] bf16 parts of dS
@@ -590,9 +607,9 @@ struct Bwd {
             const floatx4 st = dot16<BF>(qs, kb[kt], zero4());           // C[query 4g+r][key c]
 #if MEP_BWD_EXP2
             // dP - delta: the accumulator starts at -delta (query 4g+r)
-            const floatx4 dp = dot16<BF>(do2, vb[kt], floatx4{-del[0], -del[1], -del[2], -del[3]});
+            const floatx4 dp = dot16<BF>(do2, KV ? kb[kt] : vb[kt], floatx4{-del[0], -del[1], -del[2], -del[3]});
 #else
-            const floatx4 dp = dot16<BF>(do2, vb[kt], zero4());
+            const floatx4 dp = dot16<BF>(do2, KV ? kb[kt] : vb[kt], zero4());
 #endif
             float p[4], dsv[4];
 #pragma unroll
@@ -627,7 +644,9 @@ struct Bwd {
                 dsv[r] = gsv;
             }
             const S2 ds2 = split2(dsv);
-            if (MEP_BWD_DVF32 && !BF) {                  // dV[key][dim] += P^T dO, exact fp32
+            if (KV) {                                    // dKV[key][dim] += P^T dO + dS^T Q / 4
+                dk[kt] = dot16<BF>(split2(p), db2, dk[kt]);
+            } else if (MEP_BWD_DVF32 && !BF) {           // dV[key][dim] += P^T dO, exact fp32
 #pragma unroll
                 for (int s = 0; s < 4; ++s) dv[kt] = mfma16x4(p[s], in.db[s], dv[kt]);
             } else {
@@ -699,19 +718,33 @@ struct Bwd {
 // SHORT (Tk <= 64): one WAVE per (b, h) -- the single key chunk makes the wave the exclusive owner
 // of every dQ row and of its dK / dV rows, so no cross-wave sums are needed; the query tiles are
 // walked with every load of the next tile issued before this tile's math (two register sets).
-template <bool PREV, bool DSN, bool BF>
-__global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(PREV ? 2 : MEP_BWD_WAVES))) void k_attn_bwd_short(const mep_attn_bwd_desc* __restrict__ descs) {
+// waves per SIMD of the short backward by register need (scripts/resusage.py, fp32 path; the bf16
+// instances need fewer): KV frees the V rows and the dV accumulators
+template <bool PREV, bool DSN, bool KV>
+constexpr int bwd_short_waves() { return PREV ? (KV ? 3 : 2) : (KV && !DSN) ? MEP_BWD_WAVES_KV : MEP_BWD_WAVES; }
+
+template <bool PREV, bool DSN, bool BF, bool KV>
+__global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(bwd_short_waves<PREV, DSN, KV>()))) void k_attn_bwd_short(const mep_attn_bwd_desc* __restrict__ descs) {
     __shared__ __attribute__((aligned(16))) float Tr[WAVES][TFL];
     const mep_attn_bwd_desc& bd = descs[blockIdx.y];
     if (bd.f.Tk > CH) return;                // a LONG descriptor
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int bh = blockIdx.x * WAVES + wave;
     if (bh >= bd.f.B * bd.f.H) return;       // whole wave leaves; only wave-private LDS below
-    Bwd<PREV, DSN, BF> u(bd, bh / bd.f.H, bh % bd.f.H, lane);
+    Bwd<PREV, DSN, BF, KV> u(bd, bh / bd.f.H, bh % bd.f.H, lane);
     const int nqt = (u.Tq + 15) / 16;
+    const bool same_out = bd.dk.ptr == bd.dv.ptr && bd.dk.sB == bd.dv.sB && bd.dk.sT == bd.dv.sT;
+    if (KV && !(u.same_kv && same_out)) {    // broken MEP_ATTN_KV promise: NaN dq rows, loudly
+        for (int qt = 0; qt < nqt; ++qt) {
+            const int od = u.dQb.at(qt * 16 + 4 * u.g, u.hc + u.c);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) u.dQb.st1(od, r * u.dQb.sT4, __builtin_nanf(""));
+        }
+        return;
+    }
     u.load_chunk(0);
 #if MEP_BWD_DB
-    typename Bwd<PREV, DSN, BF>::QIn bufA, bufB;
+    typename Bwd<PREV, DSN, BF, KV>::QIn bufA, bufB;
     u.fetch(bufA, 0);
     for (int qt = 0; qt < nqt; qt += 2) {
         u.fetch(bufB, qt + 1);               // past the end: range-checked zeros, never used
@@ -723,19 +756,20 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(PREV ? 
     }
 #else
     for (int qt = 0; qt < nqt; ++qt) {
-        typename Bwd<PREV, DSN, BF>::QIn in;
+        typename Bwd<PREV, DSN, BF, KV>::QIn in;
         u.fetch(in, qt);
         u.store_dq(in, qt, u.tile(in, qt, Tr[wave]));
     }
 #endif
     const BRow dKb = brow(bd.dk, u.b, u.Tk, bd.f.H * HD), dVb = brow(bd.dv, u.b, u.Tk, bd.f.H * HD);
-    const bool same_out = bd.dk.ptr == bd.dv.ptr && bd.dk.sB == bd.dv.sB && bd.dk.sT == bd.dv.sT;
     const int ok_ = dKb.at(4 * u.g, u.hc + u.c), ov_ = dVb.at(4 * u.g, u.hc + u.c);   // keys past Tk: dropped
 #pragma unroll
     for (int kt = 0; kt < NT; ++kt)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-            if (same_out) {
+            if (KV) {
+                dKb.st1(ok_, (16 * kt + r) * dKb.sT4, u.dk[kt][r]);
+            } else if (same_out) {
                 dKb.st1(ok_, (16 * kt + r) * dKb.sT4, u.dk[kt][r] * INV_SCALE + u.dv[kt][r]);
             } else {
                 dKb.st1(ok_, (16 * kt + r) * dKb.sT4, u.dk[kt][r] * INV_SCALE);
@@ -875,6 +909,7 @@ extern "C" int mep_attn_bwd(const mep_attn_bwd_desc* descs, int n_desc, int max_
     if (n_desc <= 0 || max_tiles <= 0) return 0;
     if (!(flags & (MEP_ATTN_SHORT | MEP_ATTN_LONG))) { mep_set_error("mep_attn_bwd: flags need SHORT and/or LONG"); return MEP_EINVAL; }
     const bool prev = flags & MEP_ATTN_PREV, dsn = flags & MEP_ATTN_SOUT, bf = flags & MEP_PREC_BF16;
+    const bool kv = flags & MEP_ATTN_KV;
     const int dq_tiles = (flags >> 8) & 0xff;
     if (flags & MEP_ATTN_HD32) { mep_set_error("mep_attn_bwd: hd = 32 is forward-only (robot_demo inference)"); return MEP_EINVAL; }
     const size_t lds = sizeof(float) * ((size_t)RED + WAVES + 256 * (size_t)dq_tiles);
@@ -882,11 +917,13 @@ extern "C" int mep_attn_bwd(const mep_attn_bwd_desc* descs, int n_desc, int max_
     hipStream_t st = (hipStream_t)stream;
     if (flags & MEP_ATTN_SHORT) {
         const dim3 grid((max_tiles + WAVES - 1) / WAVES, n_desc), block(THREADS);
-#define MEP_BS(P, S) \
-    do { if (bf) hipLaunchKernelGGL((k_attn_bwd_short<P, S, true>), grid, block, 0, st, descs); else hipLaunchKernelGGL((k_attn_bwd_short<P, S, false>), grid, block, 0, st, descs); } while (0)
+#define MEP_BS2(P, S, K) \
+    do { if (bf) hipLaunchKernelGGL((k_attn_bwd_short<P, S, true, K>), grid, block, 0, st, descs); else hipLaunchKernelGGL((k_attn_bwd_short<P, S, false, K>), grid, block, 0, st, descs); } while (0)
+#define MEP_BS(P, S) do { if (kv) MEP_BS2(P, S, true); else MEP_BS2(P, S, false); } while (0)
         if (prev) { if (dsn) MEP_BS(true, true); else MEP_BS(true, false); }
         else      { if (dsn) MEP_BS(false, true); else MEP_BS(false, false); }
 #undef MEP_BS
+#undef MEP_BS2
     }
     if (flags & MEP_ATTN_LONG) {
         static bool lds_attr = false;   // allow more than 64 KB of dynamic LDS (long Tq)

@@ -166,6 +166,9 @@ MEP_DEV int wg_kt(int mt) { return mt == 4 ? 2 : mt == 3 ? 3 : 4; }
 // byte extent of a row view's first ntok rows, `width` columns wide (the range the raw buffer
 // loads check; hosts keep it under 2^31)
 MEP_DEV int wg_extent(const mep_rows& r, int T, int ntok, int width) {
+#ifdef MEP_WG_NOLOAD   // timing-only development build: every operand load returns 0 (compute time alone)
+    return 0;
+#endif
     const int64_t last = (int64_t)((ntok - 1) / T) * r.sB + (int64_t)((ntok - 1) % T) * r.sT + width;
     return (int)min((int64_t)4 * last, (int64_t)0x7fffffff);
 }
@@ -175,6 +178,19 @@ constexpr int WG_INV = (int)0x80000000u;   // byte offset past every view: the b
 // a view whose element offset is linear in the token, tok * step (contiguous rows, or T = 1)
 MEP_DEV bool wg_linear(const mep_rows& r) { return r.T == 1 || r.sB == (int64_t)r.T * r.sT; }
 MEP_DEV int wg_step(const mep_rows& r) { return (int)(r.T == 1 ? r.sB : r.sT); }
+
+#ifdef MEP_WG_TRACE
+// development build only (scripts/wgrad_trace.py): per-workgroup wall-clock stamps and hardware
+// ids, 8 words per workgroup: start, main loop start, main loop end, partial written, end, HW_ID,
+// XCC_ID, k blocks of wave 0
+__device__ unsigned long long* g_wg_trace;
+MEP_DEV void wg_stamp(int k, unsigned long long v) {
+    if (threadIdx.x == 0 && g_wg_trace) g_wg_trace[8 * blockIdx.x + k] = v;
+}
+#define MEP_WG_STAMP(k) wg_stamp(k, __builtin_amdgcn_s_memrealtime())
+#else
+#define MEP_WG_STAMP(k) ((void)0)
+#endif
 
 // LIN: every view of the item is linear in the token -- a lane's eight tokens of a k block sit at
 // fixed byte distances, so they are ONE per-lane base (VGPR) plus a wave-uniform per-token offset
@@ -260,17 +276,37 @@ MEP_DEV void wgrad_task(const mep_wgrad_desc& d, int t_begin, int t_end, int slo
             const int tk = 8 * blk + e;
             const bool ok = !checked || tk < nh;
             const int va = ok ? baseA : WG_INV;
+            // per-token offsets are wave-uniform: readfirstlane keeps them in SGPRs (a VGPR
+            // soffset would turn every load into a waterfall loop)
 #pragma unroll
             for (int i = 0; i < MT; ++i)
-                ra[p][i][e] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsA, va + 128 * i, tk * stA, 0));
+                ra[p][i][e] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsA, va + 128 * i,
+                                                 __builtin_amdgcn_readfirstlane(tk * stA), 0));
 #pragma unroll
             for (int j = 0; j < KT; ++j)
                 rb[p][j][e] = __builtin_bit_cast(
-                    float, __builtin_amdgcn_raw_buffer_load_b32(rsB[j], ok ? baseB[j] : WG_INV, tk * stB[j], 0));
+                    float, __builtin_amdgcn_raw_buffer_load_b32(rsB[j], ok ? baseB[j] : WG_INV,
+                                                                __builtin_amdgcn_readfirstlane(tk * stB[j]), 0));
         }
         ++blk;
     };
     auto load = [&](int p) {
+#ifdef MEP_WG_NOLD    // timing-only development build: no operand loads (registers hold zeros)
+        if (blk == 0) {
+#pragma unroll
+            for (int q = 0; q < WG_SLOTS; ++q) {
+#pragma unroll
+                for (int e = 0; e < 8; ++e) {
+#pragma unroll
+                    for (int i = 0; i < MT; ++i) ra[q][i][e] = 0.f;
+#pragma unroll
+                    for (int j = 0; j < KT; ++j) rb[q][j][e] = 0.f;
+                }
+            }
+        }
+        ++blk;
+        return;
+#endif
         if constexpr (LIN) {
             if (8 * blk + 8 <= n - half) load_lin(p, false);   // every token of both halves valid
             else load_lin(p, true);
@@ -297,6 +333,16 @@ MEP_DEV void wgrad_task(const mep_wgrad_desc& d, int t_begin, int t_end, int slo
         }
     };
     auto mma = [&](int p) {
+#ifdef MEP_WG_NOMMA   // timing-only development build: loads kept live by one add each, no products
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+#pragma unroll
+            for (int i = 0; i < MT; ++i) acc[i][0][e] += ra[p][i][e];
+#pragma unroll
+            for (int j = 0; j < KT; ++j) acc[0][j][8 + e] += rb[p][j][e];
+        }
+        return;
+#endif
         OpN<NPART> bo[KT];
 #pragma unroll
         for (int j = 0; j < KT; ++j)
@@ -310,12 +356,34 @@ MEP_DEV void wgrad_task(const mep_wgrad_desc& d, int t_begin, int t_end, int slo
             for (int j = 0; j < KT; ++j) acc[i][j] = mma_n<NPART>(ao, bo[j], acc[i][j]);
         }
     };
+    MEP_WG_STAMP(1);
+#ifdef MEP_WG_TRACE
+    wg_stamp(7, nblk);
+#endif
     if (nblk > 0) {
         // blocks 0 .. S-2 go to slots 0 .. S-2; step s loads block s + S - 1 into the slot that
         // step s - 1 consumed, then runs the MFMAs of block s
 #pragma unroll
         for (int p = 0; p < WG_SLOTS - 1; ++p) load(p);
         int s0 = 0;
+        if constexpr (LIN) {
+            // main loop: every block it loads (s0 + S - 1 .. s0 + 2S - 2) is full in both lane
+            // halves -- unchecked loads and a branch-free body, so the wait counts stay exact
+            // (the loads of the next block stay in flight across this block's products)
+            const int nfast = (n - half) >> 3;
+            for (; s0 + WG_SLOTS <= nblk && s0 + 2 * WG_SLOTS - 2 < nfast; s0 += WG_SLOTS) {
+#pragma unroll
+                for (int p = 0; p < WG_SLOTS; ++p) {
+#ifdef MEP_WG_NOLD
+                    load((p + WG_SLOTS - 1) % WG_SLOTS);
+#else
+                    load_lin((p + WG_SLOTS - 1) % WG_SLOTS, false);
+#endif
+                    __builtin_amdgcn_sched_barrier(0);
+                    mma(p);
+                }
+            }
+        }
         for (; s0 + WG_SLOTS <= nblk; s0 += WG_SLOTS) {
 #pragma unroll
             for (int p = 0; p < WG_SLOTS; ++p) {
@@ -332,6 +400,7 @@ MEP_DEV void wgrad_task(const mep_wgrad_desc& d, int t_begin, int t_end, int slo
             if (p < rem) mma(p);
     }
 
+    MEP_WG_STAMP(2);
     // ((w0 + w2) + (w1 + w3)) through two LDS buffers, then one coalesced partial write
     constexpr int LDR = 32 * KT + 8;            // == 8 mod 16: lane halves 32 banks apart
     constexpr int BUF = 32 * MT * LDR;
@@ -363,6 +432,7 @@ MEP_DEV void wgrad_task(const mep_wgrad_desc& d, int t_begin, int t_end, int slo
         const int nn = e / (32 * KT), k = e - nn * (32 * KT);
         if (k < kcnt) part[(int64_t)nn * d.Ktot + k] = red[nn * LDR + k] + red[BUF + nn * LDR + k];
     }
+    MEP_WG_STAMP(3);
 }
 
 // Flat grid of n_wg workgroups.  The map after the n_desc descriptors: off[n_wg + 1] (CSR), then
@@ -371,10 +441,6 @@ MEP_DEV void wgrad_task(const mep_wgrad_desc& d, int t_begin, int t_end, int slo
 // written to partial slot `slot` (slots never written stay zero: hosts zero the workspace once).
 // The host cuts the launch's total MFMA work into n_wg equal contiguous ranges, so a workgroup
 // may finish one descriptor's token range and start another's.
-#ifdef MEP_WG_TRACE
-// development build only: per-workgroup wall-clock stamps and hardware ids
-__device__ unsigned long long* g_wg_trace;
-#endif
 __global__ __launch_bounds__(WG_THREADS, 1) void k_wgrad(const mep_wgrad_desc* __restrict__ descs, int n_desc, int n_wg) {
 #ifdef MEP_WG_TRACE
     const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
@@ -419,11 +485,11 @@ __global__ __launch_bounds__(WG_THREADS, 1) void k_wgrad(const mep_wgrad_desc* _
     if (threadIdx.x == 0 && g_wg_trace) {
         const unsigned long long t_end = __builtin_amdgcn_s_memrealtime();
         const unsigned hw = __builtin_amdgcn_s_getreg((31 << 11) | 4), xcc = __builtin_amdgcn_s_getreg((31 << 11) | 20);
-        unsigned long long* o = g_wg_trace + 4 * blockIdx.x;
+        unsigned long long* o = g_wg_trace + 8 * blockIdx.x;
         o[0] = t_start;
-        o[1] = t_end;
-        o[2] = hw;
-        o[3] = xcc;
+        o[4] = t_end;
+        o[5] = hw;
+        o[6] = xcc;
     }
 #endif
 }

@@ -24,18 +24,21 @@ def main():
     L = _lib.lib()
     for name, kw in (('balanced', {}), ('tps1072', dict(tok_per_split=1072))):
         ws, arr, n_wg, rmax = trimodal.make_wgrad(p._wgrad_items, dev, **kw)
-        tr = torch.zeros(4 * n_wg, dtype=torch.int64, device=dev)
+        tr = torch.zeros(8 * n_wg, dtype=torch.int64, device=dev)
         L.mep_wgrad_set_trace(ctypes.c_void_p(tr.data_ptr()))
         for _ in range(3):
             launch('mep_wgrad', arr, n_wg)
         torch.cuda.synchronize()
-        t = tr.view(n_wg, 4).cpu()
+        t = tr.view(n_wg, 8).cpu()
         t0 = int(t[:, 0].min())
-        dur = (t[:, 1] - t[:, 0]).double() / 100.0     # s_memrealtime: 100 MHz -> us
+        dur = (t[:, 4] - t[:, 0]).double() / 100.0     # s_memrealtime: 100 MHz -> us
         start = (t[:, 0] - t0).double() / 100.0
-        end = (t[:, 1] - t0).double() / 100.0
-        cu = [(int(x) >> 8) & 15 | ((int(x) >> 12) & 1) << 4 | ((int(x) >> 13) & 7) << 5 for x in t[:, 2]]
-        key = [(int(t[i, 3]) & 15, cu[i]) for i in range(n_wg)]
+        end = (t[:, 4] - t0).double() / 100.0
+        ph = [(t[:, k + 1] - t[:, k]).double() / 100.0 for k in range(4)]
+        print('%s phases (median us): setup %.2f  main loop %.2f  reduce+write %.2f  tail %.2f; k blocks (wave 0) median %d'
+              % (name, *[float(x.median()) for x in ph], int(t[:, 7].median())), flush=True)
+        cu = [(int(x) >> 8) & 15 | ((int(x) >> 12) & 1) << 4 | ((int(x) >> 13) & 7) << 5 for x in t[:, 5]]
+        key = [(int(t[i, 6]) & 15, cu[i]) for i in range(n_wg)]
         per = collections.Counter(key)
         print('%s: wgs %d  span %.1f us  dur min %.1f med %.1f max %.1f  start max %.1f  distinct CUs %d  max WGs/CU %d'
               % (name, n_wg, float(end.max()), float(dur.min()), float(dur.median()), float(dur.max()),
