@@ -563,6 +563,49 @@ struct Bwd {
         }
     }
 
+    // ---- staged query tiles (short kernel, MEP_BWD_DMA): the next tile's Q, dO, O and dQ rows
+    // (16 rows x 64 B each: one 1-KiB LDS-DMA wave-instruction per operand, lane L = row L / 4,
+    // 16-byte piece L % 4) and its row statistics go straight from HBM into the wave's LDS
+    // staging area while this tile computes: no VGPRs in flight, 5 load instructions per tile
+    // instead of 22.  Rows past Tq fall outside the row views (no data: the area is zeroed at the
+    // wave's start and later holds finite rows of earlier tiles, whose products are masked).
+    static constexpr int STG = 4 * 256 + 32;   // floats: Q, dO, O, dQ [16][16], stats [16][2]
+    MEP_DEV bool dma_ok() const { return Qb.vec && Gb.vec && Ob.vec && dQb.vec; }
+    MEP_DEV void stage(int qt, float* S) const {
+        typedef __attribute__((address_space(3))) void lvoid;
+        const int row = qt * 16 + (lane >> 2), col = hc + 4 * (lane & 3);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(Qb.rs, (lvoid*)(S), 16, Qb.at(row, col), 0, 0, 0);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(Gb.rs, (lvoid*)(S + 256), 16, Gb.at(row, col), 0, 0, 0);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(Ob.rs, (lvoid*)(S + 512), 16, Ob.at(row, col), 0, 0, 0);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(dQb.rs, (lvoid*)(S + 768), 16, dQb.at(row, col), 0, 0, 0);
+        if (lane < 32)   // dword pieces: the range check drops exactly the rows past Tq
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rsStat, (lvoid*)(S + 1024), 4, 8 * 16 * qt + 4 * lane, 0, 0, 0);
+    }
+    // the staged tile in the operand layouts of fetch()
+    MEP_DEV void read_staged(QIn& in, const float* S) const {
+        typedef __attribute__((address_space(3))) const float lcf;
+        typedef __attribute__((address_space(3))) const f32x4 lcf4;
+        typedef __attribute__((address_space(3))) const f32x2 lcf2;
+        lcf* L = (lcf*)S;
+        const f32x4 qa = *(lcf4*)(L + 16 * c + 4 * g), da = *(lcf4*)(L + 256 + 16 * c + 4 * g);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) { in.qa[e] = qa[e]; in.da[e] = da[e]; }
+#pragma unroll
+        for (int s4 = 0; s4 < 4; ++s4) {
+            const int r = (4 * g + s4) * 16 + c;
+            in.qb[s4] = L[r];
+            in.db[s4] = L[256 + r];
+            in.ob[s4] = L[512 + r];
+            in.dqo[s4] = L[768 + r];
+            in.st[s4] = *(lcf2*)(L + 1024 + 2 * (4 * g + s4));
+        }
+    }
+    MEP_DEV void store_dq_rows(const float (&dqo)[4], int qt, const floatx4& dq) const {
+        const int od = dQb.at(qt * 16 + 4 * g, hc + c);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) dQb.st1(od, r * dQb.sT4, dqo[r] + dq[r] * INV_SCALE);
+    }
+
     // one 16-query tile against the chunk's 64 keys: accumulates dK / dV, returns this chunk's
     // dQ contribution (C[query 4g+r][dim c], before the 1/sqrt(hd) scale).  Tr: the wave's
     // transpose scratch in LDS (TFL floats: the bf16 hi and lo parts of dS, 16 x TLD2 each).
@@ -723,9 +766,16 @@ struct Bwd {
 template <bool PREV, bool DSN, bool KV>
 constexpr int bwd_short_waves() { return PREV ? (KV ? 3 : 2) : (KV && !DSN) ? MEP_BWD_WAVES_KV : MEP_BWD_WAVES; }
 
+#ifndef MEP_BWD_DMA
+#define MEP_BWD_DMA 1   // short backward: query tiles staged one ahead by LDS-DMA (Bwd::stage)
+#endif
+
 template <bool PREV, bool DSN, bool BF, bool KV>
 __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(bwd_short_waves<PREV, DSN, KV>()))) void k_attn_bwd_short(const mep_attn_bwd_desc* __restrict__ descs) {
     __shared__ __attribute__((aligned(16))) float Tr[WAVES][TFL];
+#if MEP_BWD_DMA
+    __shared__ __attribute__((aligned(16))) float Stg[WAVES][Bwd<PREV, DSN, BF, KV>::STG];
+#endif
     const mep_attn_bwd_desc& bd = descs[blockIdx.y];
     if (bd.f.Tk > CH) return;                // a LONG descriptor
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -742,6 +792,31 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(bwd_sho
         }
         return;
     }
+#if MEP_BWD_DMA
+    if (u.dma_ok()) {
+        float* S = Stg[wave];
+        typedef __attribute__((address_space(3))) f32x4 lf4;
+        for (int e = lane; e < Bwd<PREV, DSN, BF, KV>::STG / 4; e += 64) ((lf4*)S)[e] = f32x4{0.f, 0.f, 0.f, 0.f};
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        u.stage(0, S);
+        u.load_chunk(0);   // (K rows staged by LDS-DMA as well measured slower: 42.2-43.7 vs 41.7 us)
+        floatx4 dq_prev = zero4();
+        float dqo_prev[4] = {0.f, 0.f, 0.f, 0.f};
+        for (int qt = 0; qt < nqt; ++qt) {
+            typename Bwd<PREV, DSN, BF, KV>::QIn in;
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // tile qt landed in S
+            u.read_staged(in, S);
+            if (qt > 0) u.store_dq_rows(dqo_prev, qt - 1, dq_prev);   // after the wait: stores stay in flight
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // S read before it is refilled
+            if (qt + 1 < nqt) u.stage(qt + 1, S);
+            dq_prev = u.tile(in, qt, Tr[wave]);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) dqo_prev[r] = in.dqo[r];
+        }
+        if (nqt > 0) u.store_dq_rows(dqo_prev, nqt - 1, dq_prev);
+    } else
+#endif
+    {
     u.load_chunk(0);
 #if MEP_BWD_DB
     typename Bwd<PREV, DSN, BF, KV>::QIn bufA, bufB;
@@ -761,6 +836,7 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(bwd_sho
         u.store_dq(in, qt, u.tile(in, qt, Tr[wave]));
     }
 #endif
+    }
     const BRow dKb = brow(bd.dk, u.b, u.Tk, bd.f.H * HD), dVb = brow(bd.dv, u.b, u.Tk, bd.f.H * HD);
     const int ok_ = dKb.at(4 * u.g, u.hc + u.c), ov_ = dVb.at(4 * u.g, u.hc + u.c);   // keys past Tk: dropped
 #pragma unroll

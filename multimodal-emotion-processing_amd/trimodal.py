@@ -54,38 +54,35 @@ def wgrad_geometry(N, ktot):
 
 
 def wgrad_segments(items, n_wg=WG_TARGET, tok_per_split=None):
-    """Split every (item, column group) token span into segments, one per workgroup, at most
-    n_wg workgroups (all resident at once, one per CU: the kernel lasts as long as its busiest
-    CU), minimising the largest workgroup's cost.  The cost of a token is its operand loads,
-    MT + KT dwords per lane (a per-workgroup trace, scripts/wgrad_trace.py, shows the kernel
-    load / latency-bound: a 3 x 1-tile column group costs ~0.7x a 3 x 3 one per token, not 1/3).
-    -> (per-workgroup segment lists [(item, cg, t0, t1, slot)], slots per item).  tok_per_split:
-    fixed chunks instead (tests)."""
+    """Split every (item, column group) token span into segments of at most tok_per_split tokens,
+    one segment per workgroup; tok_per_split None: the smallest multiple of 8 that keeps the launch
+    within n_wg workgroups (all resident at once, one per CU).  Uniform chunks beat a cost-balanced
+    water-filling over all n_wg CUs (47.3 vs 49.6 us at cfg3, scripts/wgrad_balance.py); a span
+    longer than the chunk is cut into near-equal pieces.  The loop
+    is bound by HBM traffic and the operand-load rate, so more, smaller segments only add setup
+    and partial-reduction work (~10 us per workgroup, scripts/wgrad_trace.py).
+    -> (per-workgroup segment lists [(item, cg, t0, t1, slot)], slots per item)."""
     units = []
     for i, (_, N, n, bs, _) in enumerate(items):
         mt, kt, ncg = wgrad_geometry(N, sum(b[1] for b in bs))
-        ktiles = cdiv(sum(b[1] for b in bs), 32)
         for cg in range(ncg):
             if n > 0:
-                units.append((i, cg, mt + min(kt, ktiles - cg * kt), n))
+                units.append((i, cg, n))
+    if tok_per_split is None:
+        lo, hi = 1, cdiv(max([n for (_, _, n) in units] or [8]), 8)   # in units of 8 tokens
+        while lo < hi:                        # the segment count only falls as the chunk grows
+            mid = (lo + hi) // 2
+            if sum(cdiv(n, 8 * mid) for (_, _, n) in units) <= n_wg:
+                hi = mid
+            else:
+                lo = mid + 1
+        tok_per_split = 8 * lo
     bins = []
-    if tok_per_split is not None:
-        for (i, cg, t, n) in units:
-            tps = tok_per_split[i] if isinstance(tok_per_split, (list, tuple)) else tok_per_split
-            bins += [[(i, cg, t0, min(n, t0 + tps))] for t0 in range(0, n, tps)]
-    else:
-        # water-filling: split the unit whose workgroups carry the most work until n_wg workgroups;
-        # one segment per workgroup (a workgroup running two segments pays the pipeline start and
-        # the reduction twice: ~15 us each, scripts/wgrad_trace.py)
-        ns = [1] * len(units)
-        while sum(ns) < n_wg:
-            u = max(range(len(units)), key=lambda k: (units[k][2] * units[k][3] / ns[k], -k))
-            if units[u][3] < 16 * (ns[u] + 1):
-                break
-            ns[u] += 1
-        for u, (i, cg, t, n) in enumerate(units):
-            cuts = [cdiv(n * k, ns[u] * 8) * 8 for k in range(ns[u])] + [n]
-            bins += [[(i, cg, a, b)] for a, b in zip(cuts[:-1], cuts[1:]) if b > a]
+    for (i, cg, n) in units:
+        tps = tok_per_split[i] if isinstance(tok_per_split, (list, tuple)) else tok_per_split
+        k = cdiv(n, tps)                      # k near-equal chunks, cut at multiples of 8
+        cuts = [min(n, cdiv(n * q, 8 * k) * 8) for q in range(k)] + [n]
+        bins += [[(i, cg, a, b)] for a, b in zip(cuts[:-1], cuts[1:]) if b > a]
     slots = [0] * len(items)
     count = {}
     segs = []
