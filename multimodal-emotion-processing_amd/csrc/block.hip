@@ -255,6 +255,16 @@ MEP_DEV void wg_store_barrier() {
     __syncthreads();
 }
 
+#ifdef MEP_EPI_TRACE
+// development build only (scripts/epi_trace.py): per-workgroup phase stamps, 8 words per workgroup
+// of the launch grid (x + gridDim.x * y): start, weight 1 staged, phase 1 done, weight 2 staged, end
+__device__ unsigned long long* g_epi_trace;
+extern "C" int mep_epi_set_trace(void* p) { return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_epi_trace), &p, sizeof(p)); }
+#define MEP_EPI_STAMP(k) do { if (threadIdx.x == 0 && g_epi_trace) g_epi_trace[8 * (blockIdx.x + gridDim.x * blockIdx.y) + (k)] = __builtin_amdgcn_s_memrealtime(); } while (0)
+#else
+#define MEP_EPI_STAMP(k) ((void)0)
+#endif
+
 template <int D, int NPART>
 MEP_DEV void epi_fwd_split(const mep_epi_desc& d, unsigned char* sm, int t_begin, int t_end) {
     constexpr int NI = D / 16, KB = D / 16, NP = D / 32;
@@ -277,9 +287,11 @@ MEP_DEV void epi_fwd_split(const mep_epi_desc& d, unsigned char* sm, int t_begin
         for (int kb = 0; kb < KB; ++kb) dst[kb] = ld4w(r + 16 * kb);
     };
     // ---- phase 1: xp = drop(x Wp^T)
+    MEP_EPI_STAMP(0);
     if (t_begin + wave < t_end) rows_of(d.x, t_begin + wave, ab);
     stage_split_rows<D, D, NPART>(wp, G<const float>(d.wp));
     __syncthreads();
+    MEP_EPI_STAMP(1);
     for (int tile = t_begin + wave; tile < t_end; tile += EWAVES) {
         const int tok = tile * 16 + c;
         Op xs[NP];
@@ -306,9 +318,11 @@ MEP_DEV void epi_fwd_split(const mep_epi_desc& d, unsigned char* sm, int t_begin
     // ---- phase 2: z = [q | xp] Wm^T, out = drop(LayerNorm(z))
     if (t_begin + wave < t_end) rows_of(d.q, t_begin + wave, ab);
     wg_store_barrier();              // xp rows stored; Wp no longer read
+    MEP_EPI_STAMP(2);
     if (t_begin + wave < t_end) rows_of(d.xp, t_begin + wave, bb);
     stage_split_rows<D, 2 * D, NPART>(wm, G<const float>(d.wm));
     __syncthreads();
+    MEP_EPI_STAMP(3);
     for (int tile = t_begin + wave; tile < t_end; tile += EWAVES) {
         const int tok = tile * 16 + c;
         Op qs[NP], ps[NP];
@@ -353,6 +367,11 @@ MEP_DEV void epi_fwd_split(const mep_epi_desc& d, unsigned char* sm, int t_begin
             if (g == 0) { stats[2 * tok] = mean; stats[2 * tok + 1] = rstd; }
         }
     }
+#ifdef MEP_EPI_TRACE
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    MEP_EPI_STAMP(4);
+#endif
 }
 
 template <int D, int NPART>

@@ -122,6 +122,9 @@ struct SplitW {
 
 // acc[i] (i < NI) += A_i B over NP k pairs: afr(i, p) -> OpN (A fragment of output tile i),
 // bfr(p) -> OpN (B fragment, shared by the NI tiles).
+#ifndef MEP_TG_GROUP
+#define MEP_TG_GROUP 2   // output tiles per scheduling group of tgemm_n
+#endif
 template <int NI, int NP, int NPART, typename AF, typename BF>
 MEP_DEV void tgemm_n(f32x4 (&acc)[NI], AF&& afr, BF&& bfr) {
 #pragma unroll
@@ -132,7 +135,7 @@ MEP_DEV void tgemm_n(f32x4 (&acc)[NI], AF&& afr, BF&& bfr) {
             acc[i] = mma_n<NPART>(afr(i, p), b, acc[i]);
             // keep the next fragment's reads behind these MFMAs (a fully hoisted, fully unrolled
             // product would hold 4 NPART NI NP fragment VGPRs)
-            if (i % 2 == 1) __builtin_amdgcn_sched_barrier(0);
+            if (i % MEP_TG_GROUP == MEP_TG_GROUP - 1) __builtin_amdgcn_sched_barrier(0);
         }
     }
 }
