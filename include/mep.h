@@ -208,7 +208,15 @@ typedef struct {
     mep_rows dz, dxp, dx, dq;
     uint64_t ln_partial;
     int32_t  dq_accumulate;
-    int32_t  _pad;
+    /* pool_T > 0: dout is not read; the upstream gradient is the mean+max pool's backward
+     * (mep_pool_bwd's dx, formed in registers: dmean / pool_T, + dmax at the argmax step) for
+     * this block's slice of the pooled tensor -- token tok = b * pool_Tq + t sits at time
+     * pool_t0 + t and columns pool_col .. pool_col + D - 1 of [B, pool_T, pool_C]
+     * (cmu-mosei/run.py:314-318).  dout2 is still added. */
+    int32_t  pool_T;
+    uint64_t pool_dpooled;   /* [B][2 * pool_C] floats (mean part, then max part) */
+    uint64_t pool_argmax;    /* [B][pool_C] int32 */
+    int32_t  pool_C, pool_Tq, pool_t0, pool_col;
 } mep_epi_bwd_desc;
 int mep_block_epi_bwd(const mep_epi_bwd_desc* descs, int n_desc, int max_tiles, int D, mep_stream_t stream);
 

@@ -56,7 +56,9 @@ class EpiDesc(ctypes.Structure):
 
 class EpiBwdDesc(ctypes.Structure):
     _fields_ = [('f', EpiDesc), ('dout', Rows), ('dout2', Rows), ('dz', Rows), ('dxp', Rows), ('dx', Rows),
-                ('dq', Rows), ('ln_partial', u64), ('dq_accumulate', i32), ('_pad', i32)]
+                ('dq', Rows), ('ln_partial', u64), ('dq_accumulate', i32), ('pool_T', i32),
+                ('pool_dpooled', u64), ('pool_argmax', u64), ('pool_C', i32), ('pool_Tq', i32),
+                ('pool_t0', i32), ('pool_col', i32)]
 
 
 class LnDesc(ctypes.Structure):
@@ -229,6 +231,7 @@ class DescArray:
         """tail: int32 values stored right after the descriptors (the k_wgrad task map)."""
         self.n = len(items)
         self.struct = struct
+        self.items = list(items)
         if self.n:
             arr = (struct * self.n)(*items)
             raw = bytes(arr) + (b'' if tail is None else bytes((ctypes.c_int32 * len(tail))(*tail)))

@@ -112,6 +112,36 @@ MEP_DEV bool tile_range(int ntok, int& t_begin, int& t_end) {
     return t_begin < t_end;
 }
 
+// upstream gradient of token tc (clamped in range), features col .. col+3: the dout row view, or
+// with pool_T > 0 the mean+max pool's backward formed in registers -- exactly k_pool_bwd's dx
+// (pool_head.hip: dmean = dpooled / T, + dmax at the argmax step), so the pooled tensor's gradient
+// [B, T, C] is never written or read (cmu-mosei/run.py:314-318)
+struct Upstream {
+    const gfloat* dp;      // pool: this block's columns of dpooled (mean part; max part at + C)
+    const MEP_G int* am;   // pool: this block's columns of argmax
+    int C, T, Tq, t0;
+    MEP_DEV explicit Upstream(const mep_epi_bwd_desc& bd)
+        : dp(G<const float>(bd.pool_dpooled) + bd.pool_col), am(G<const int>(bd.pool_argmax) + bd.pool_col),
+          C(bd.pool_C), T(bd.pool_T), Tq(bd.pool_Tq), t0(bd.pool_t0) {}
+    MEP_DEV f32x4 at(const mep_epi_bwd_desc& bd, int tc, int col) const {
+        if (T <= 0) return ld4w(row_ptr(bd.dout, tc) + col);
+        const int b = tc / Tq, tg = t0 + (tc - b * Tq);
+        const gfloat* p = dp + (int64_t)b * 2 * C + col;
+        const f32x4 mean = ld4w(p), mx = ld4w(p + C);
+        // the indices as an integer vector: as float bits they would be denormals, which float
+        // moves/selects may flush to zero
+        typedef MEP_G const u32x4 gu32x4;
+        const u32x4 a = *reinterpret_cast<gu32x4*>(am + (int64_t)b * C + col);
+        f32x4 v;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const float dmean = mean[r] / (float)T;
+            v[r] = ((int)a[r] == tg) ? dmean + mx[r] : dmean;
+        }
+        return v;
+    }
+};
+
 // ---------------------------------------------------------------- forward
 // Per tile of 16 tokens (common.h, transposed tiles): xp^T = Wp x^T, then z^T = Wm [q | xp]^T
 // with the xp accumulators as the B operand of the second product; LayerNorm on the
@@ -394,12 +424,12 @@ MEP_DEV void epi_bwd_split(const mep_epi_bwd_desc& bd, unsigned char* sm, int t_
     const WPT wpt{(lbyte*)sm, 0};
     f32x4 ga[KB], zb[KB];            // one tile ahead: dout (+ dout2) and z rows
     float mean = 0.f, rstd = 0.f;
+    const Upstream up(bd);
     auto fetch1 = [&](int tile) {
         const int tc = min(tile * 16 + c, ntok - 1);
-        const gfloat* gr = row_ptr(bd.dout, tc) + 4 * g;
         const gfloat* zr = row_ptr(d.z, tc) + 4 * g;
 #pragma unroll
-        for (int kb = 0; kb < KB; ++kb) ga[kb] = ld4w(gr + 16 * kb);
+        for (int kb = 0; kb < KB; ++kb) ga[kb] = up.at(bd, tc, 16 * kb + 4 * g);
 #pragma unroll
         for (int kb = 0; kb < KB; ++kb) zb[kb] = ld4w(zr + 16 * kb);
         mean = stats[2 * tc];
@@ -589,11 +619,11 @@ MEP_DEV void epi_bwd_tiles(const mep_epi_bwd_desc& bd, const AM& wmt, const AP& 
     wmt_x.row0 += D;                    // rows D.. of Wm^T = Wm[:, D:]
     const gfloat* stats = G<const float>(d.stats);
     gfloat* lpart = G<float>(bd.ln_partial);
+    const Upstream up(bd);
     for (int tile = t_begin + wave; tile < t_end; tile += EWAVES) {
         const int tok = tile * 16 + c;
         const bool ok = tok < ntok;
         const int tc = min(tok, ntok - 1);
-        const gfloat* gr = row_ptr(bd.dout, tc);
         const gfloat* g2 = bd.dout2.ptr ? row_ptr(bd.dout2, tc) : nullptr;
         const gfloat* zr = row_ptr(d.z, tc);
         const float mean = stats[2 * tc], rstd = stats[2 * tc + 1];
@@ -603,7 +633,7 @@ MEP_DEV void epi_bwd_tiles(const mep_epi_bwd_desc& bd, const AM& wmt, const AP& 
 #pragma unroll
         for (int i = 0; i < NI; ++i) {
             const int col = 16 * i + 4 * g;
-            f32x4 a = ld4w(gr + col);
+            f32x4 a = up.at(bd, tc, col);
             if (g2) a += ld4w(g2 + col);
             const f32x4 zz = ld4w(zr + col), w = ld4w(G<const float>(d.ln_w) + col);
             f32x4 pw, pb;

@@ -48,8 +48,10 @@ def launch_costs(plan):
             B * (4 * (2 * Tq * D + Tk * D) + 4 * Tk + 8 * H * Tq + s_bytes * (r_in + r_out)))
         n = B * Tq
         add('mep_block_epi_fwd', 2 * n * D * 3 * D + 8 * n * D, 4 * n * D * 5 + 8 * n + 4 * 3 * D * D + 8 * D)
+        # upstream gradient formed from this block's dpooled / argmax slices (B x 3D), not read
+        # as [n, D] rows (the pool backward is folded into this launch)
         add('mep_block_epi_bwd', 2 * n * D * 3 * D + 10 * n * D,
-            4 * n * D * 7 + 8 * n + 4 * 3 * D * D + 4 * (n // 64 + 1) * 2 * D)
+            4 * n * D * 6 + 8 * n + 4 * 3 * D * D + 4 * (n // 64 + 1) * 2 * D + 4 * B * 3 * D)
         chained = s_bytes * ((1 if r_out else 0) + (1 if r_in else 0) * 2)
         add('mep_attn_bwd', B * 10 * Tq * Tk * D,
             B * (4 * (5 * Tq * D + 2 * Tk * D) + 4 * Tk + 8 * H * Tq + chained))
@@ -60,7 +62,6 @@ def launch_costs(plan):
             add('mep_wgrad', 2 * n * D * d, 4 * n * (D + d))
     for e in range(2):
         add('mep_pool_fwd', B * plan.Ttot * plan.C, 4 * B * (plan.Ttot * plan.C + 2 * plan.C) + 4 * B * plan.C)
-        add('mep_pool_bwd', B * plan.Ttot * plan.C, 4 * B * (plan.Ttot * plan.C + 2 * plan.C) + 4 * B * plan.C)
     return out
 
 

@@ -11,7 +11,7 @@ Step anatomy (reference call stack: SURVEY.md section 3A; cmu-mosei/run.py:329-3
             per layer: attention core (all 9 chains x 2 encoders in one launch),
                        block epilogue (proj -> cat -> minus -> LayerNorm, one launch)
             mean+max pool (one launch) -> fused head + circle loss (+R-Drop) + head backward
-  backward  head reduce, pool backward, per layer (reverse): epilogue backward, attention
+  backward  per layer (reverse): epilogue backward (from the pool's gradient), attention
             backward; per-modality gradient sum; all weight gradients in one split-K launch +
             one reduce; LayerNorm / residual-coefficient column sums.
 Independent work is batched into grouped launches (grid.y = descriptor), never looped in
@@ -21,6 +21,7 @@ never materialised); inputs stay in the reference's [B, 2, T, d] (prev, cur) lay
 through strided row views.
 """
 import ctypes
+import os
 
 import torch
 
@@ -43,6 +44,8 @@ def cdiv(a, b):
 WG_WAVES = 4              # csrc/gemm.hip k_wgrad: waves per workgroup (token quarters of a split)
 WG_TARGET = _lib.N_CU      # workgroups per launch: one per CU (4 waves of ~400 registers)
 WG_TARGET_OVERRIDE = None  # development: another workgroup count for wgrad_segments
+# the pool's backward formed inside the epilogue backward (0: a separate mep_pool_bwd into dXcat)
+POOL_FOLD = os.environ.get('MEP_POOL_FOLD', '1') != '0'
 
 
 def wgrad_geometry(N, ktot):
@@ -234,10 +237,11 @@ class TriModalPlan:
             self.Y = {(e, m): torch.zeros(ntok[m], D, **f32) for e in range(E) for m in MODS}
             self.Ystat = {(e, m): torch.zeros(ntok[m], 2, **f32) for e in range(E) for m in MODS}
         self.Xcat = [torch.zeros(B, self.Ttot, self.C, **f32) for _ in range(E)]
+        self.pool_fold = POOL_FOLD
+        self.dXcat = None if self.pool_fold else [torch.zeros(B, self.Ttot, self.C, **f32) for _ in range(E)]
         self.pooled = [torch.zeros(B, self.F, **f32) for _ in range(E)]
         self.argmax = [torch.zeros(B, self.C, dtype=torch.int32, device=dev) for _ in range(E)]
         self.dpooled = [torch.zeros(B, self.F, **f32) for _ in range(E)]
-        self.dXcat = [torch.zeros(B, self.Ttot, self.C, **f32) for _ in range(E)]
         self.logits = torch.zeros(B, NC, **f32)
         self.row_loss = torch.zeros(B, **f32)
         self.loss = torch.zeros(1, **f32)
@@ -282,10 +286,6 @@ class TriModalPlan:
     def _out_rows(self, blk):
         e, qm = blk['e'], blk['qm']
         return rows(self.Xcat[e], blk['Tq'], self.Ttot * self.C, self.C, self.toff[qm] * self.C + blk['col'])
-
-    def _dout_rows(self, blk):
-        e, qm = blk['e'], blk['qm']
-        return rows(self.dXcat[e], blk['Tq'], self.Ttot * self.C, self.C, self.toff[qm] * self.C + blk['col'])
 
     def _q_rows(self, blk):
         if blk['i'] == 0:
@@ -342,7 +342,9 @@ class TriModalPlan:
             self.g_attn.append(geo)
             self.t_epi.append(_lib.epi_grid(max(B * b['Tq'] for b in self.blocks), len(ed)))
         # pool
-        pd = [PoolDesc(x=self.Xcat[e].data_ptr(), dx=self.dXcat[e].data_ptr(), pooled=self.pooled[e].data_ptr(),
+        # (the pool's backward is formed inside the epilogue backward: no dx tensor, no launch)
+        pd = [PoolDesc(x=self.Xcat[e].data_ptr(), dx=0 if self.pool_fold else self.dXcat[e].data_ptr(),
+                       pooled=self.pooled[e].data_ptr(),
                        dpooled=self.dpooled[e].data_ptr(), argmax=self.argmax[e].data_ptr(),
                        B=B, T=self.Ttot, C=self.C) for e in range(E)]
         self.d_pool = DescArray(PoolDesc, pd, dev)
@@ -433,10 +435,21 @@ class TriModalPlan:
     def _epi_bwd_desc(self, blk):
         D, Tq = self.spec.D, blk['Tq']
         nxt = self._blk(blk['e'], blk['j'], blk['i'] + 1) if blk['i'] < self.spec.nl - 1 else None
-        return EpiBwdDesc(f=self._epi_desc(blk), dout=self._dout_rows(blk),
+        e = blk['e']
+        # upstream gradient: the mean+max pool's backward of this block's slice of Xcat (formed in
+        # the kernel from dpooled / argmax) + the next layer's dq
+        if self.pool_fold:
+            up = dict(dout=Rows(), pool_T=self.Ttot, pool_dpooled=self.dpooled[e].data_ptr(),
+                      pool_argmax=self.argmax[e].data_ptr(), pool_C=self.C, pool_Tq=Tq,
+                      pool_t0=self.toff[blk['qm']], pool_col=blk['col'])
+        else:
+            up = dict(dout=rows(self.dXcat[e], Tq, self.Ttot * self.C, self.C,
+                                self.toff[blk['qm']] * self.C + blk['col']))
+        return EpiBwdDesc(f=self._epi_desc(blk),
                           dout2=crows(nxt['dQ'], Tq, D) if nxt is not None else Rows(),
                           dz=crows(blk['dZ'], Tq, D), dxp=crows(blk['dXP'], Tq, D), dx=crows(blk['dX'], Tq, D),
-                          dq=crows(blk['dQ'], Tq, D), ln_partial=blk['ln_partial'].data_ptr(), dq_accumulate=0)
+                          dq=crows(blk['dQ'], Tq, D), ln_partial=blk['ln_partial'].data_ptr(), dq_accumulate=0,
+                          **up)
 
     def _attn_bwd_desc(self, blk):
         D = self.spec.D
@@ -562,7 +575,8 @@ class TriModalPlan:
             self.head.ext_dlogits = ext_dlogits.data_ptr()
             _lib.call('mep_head_fwd_bwd', ctypes.byref(self.head), stream=stream)
             self.head.ext_dlogits = 0
-        launch("mep_pool_bwd", self.d_pool, self.t_poolb, stream)
+        if not self.pool_fold:
+            launch("mep_pool_bwd", self.d_pool, self.t_poolb, stream)
         for i in reversed(range(nl)):
             launch('mep_block_epi_bwd', self.d_epib[i], self.t_epi[i], stream, threads=sp.D | self.prec)
             launch('mep_attn_bwd', self.d_attnb[i], self.t_attnb[i], stream, threads=self.f_attnb[i] | self.prec)
