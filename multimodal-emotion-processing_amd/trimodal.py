@@ -97,7 +97,45 @@ def wgrad_segments(items, n_wg=WG_TARGET, tok_per_split=None):
             slots[i] = max(slots[i], s + 1)
             out.append((i, cg, t0, t1, s))
         segs.append(out)
+    if WG_XCD_PAIR:
+        segs = _xcd_pairs(segs, n_wg)
     return segs, slots
+
+
+WG_XCD_PAIR = os.environ.get('MEP_WG_XCD', '1') != '0'
+
+
+def _xcd_pairs(segs, n_wg):
+    """Workgroup order that puts the column groups of one token chunk on one XCD: blocks b and
+    b + 8 share an XCD (round-robin dispatch, MI355X_MICROARCH.md section Workgroup dispatch), so
+    member r of chunk group q (same item and tokens, column group r: the same A rows) goes to
+    block 8 r + q of its 8-group block and the A operand is read from HBM once and hit in that
+    XCD's L2 by the other column groups, which stream it at the same time.  Empty workgroups pad
+    a short last block; the plain order is kept when the padding would exceed n_wg."""
+    groups, order = {}, []
+    for seg in segs:
+        (i, cg, t0, t1, s), = seg
+        key = (i, t0, t1)
+        if key not in groups:
+            groups[key] = []
+            order.append(key)
+        groups[key].append(seg)
+    by_m = {}
+    for key in order:
+        by_m.setdefault(len(groups[key]), []).append(groups[key])
+    out = []
+    for m in sorted(by_m):
+        gl = by_m[m]
+        if m == 1:
+            out += [g[0] for g in gl]
+            continue
+        for b0 in range(0, len(gl), 8):
+            blk = gl[b0:b0 + 8]
+            for r in range(m):
+                out += [blk[q][r] if q < len(blk) else [] for q in range(8)]
+    if len(out) > max(n_wg, len(segs)):
+        return segs
+    return out
 
 
 UN_LDS = 30720   # csrc/gemm.hip k_unify: floats of LDS for the staged weight
