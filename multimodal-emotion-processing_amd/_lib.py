@@ -266,9 +266,15 @@ ATTN_HD32 = 0x20000   # MEP_ATTN_HD32: head dim 32 attention forward (robot_demo
 ATTN_KV = 0x40000     # MEP_ATTN_KV: backward with k == v and dk == dv on every descriptor
 
 
+def rf_bwd_rows():
+    """token rows per workgroup of mep_rf_epi_bwd (csrc/rf.hip MEP_RF_BWD_ROWS): one row of its
+    partial buffer per workgroup"""
+    return int(os.environ.get('MEP_RF_BWD_ROWS', '32'))   # env: A/B builds only
+
+
 def rf_epi_rows(D):
     """token rows per workgroup of mep_rf_epi_fwd (csrc/rf.hip rf_fwd_rows)"""
-    return 32 if D > 128 else 64
+    return 32 if D > 128 else int(os.environ.get('MEP_RF_FWD_ROWS', '32'))   # env: A/B builds only
 ATTN_MAX_DQ_TILES = (160 * 1024 // 4 - 2 * 4 * 64 * 16 - 4) // 256   # csrc/attn.hip backward LDS
 
 

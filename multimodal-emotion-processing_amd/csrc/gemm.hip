@@ -15,8 +15,8 @@ using namespace mep;
 
 namespace {
 
-// One WAVE = 16 tokens x (up to 128 columns per pass); 4 independent waves per workgroup of 64
-// tokens, no block barriers.  v_mfma_f32_16x16x4_f32 with the wave's A rows staged in its own LDS
+// One WAVE = 16 tokens x one pass of 16 * GEMM_NJ columns (passes over grid.z, then strided); 4
+// independent waves per workgroup of 64 tokens, no block barriers.  v_mfma_f32_16x16x4_f32 with the wave's A rows staged in its own LDS
 // slice (128-wide K chunks, zero-padded past K and past the last token) and the weight fragments
 // of the next 16-wide k block loaded during the MFMAs of the current one.  Per lane: acc[j] holds
 // rows 4g..4g+3 of column block j (c = lane & 15, g = lane >> 4; common.h wgemm16 layout).
@@ -24,7 +24,14 @@ constexpr int GEMM_WAVES = 4;
 constexpr int GEMM_THREADS = 64 * GEMM_WAVES;
 constexpr int GEMM_KC = 128;
 constexpr int GEMM_LDA = GEMM_KC + 4;
-constexpr int GEMM_NJ = 8;        // 16-column blocks per pass
+#ifndef MEP_GEMM_NJ
+#define MEP_GEMM_NJ 1
+#endif
+constexpr int GEMM_NJ = MEP_GEMM_NJ;   // 16-column blocks per pass
+#ifndef MEP_GEMM_ZP
+#define MEP_GEMM_ZP 32
+#endif
+constexpr int GEMM_ZP = MEP_GEMM_ZP;             // column passes spread over grid.z (more waves in flight)
 
 // weight fragment W(n, k .. k+3) with k clamped into [0, K) and n into [0, N): the clamped
 // values meet zero A columns (k >= K) or are never stored (n >= N), so they only need to be finite
@@ -58,7 +65,7 @@ __global__ __launch_bounds__(GEMM_THREADS) void k_gemm(const mep_gemm_desc* __re
     // per-lane row offsets of the staging pattern (row = idx / 32 for float4 idx = lane + 64 i)
     const float* arow = As + c * GEMM_LDA + 4 * g;
 
-    for (int cg = 0; cg < N; cg += 16 * GEMM_NJ) {
+    for (int cg = 16 * GEMM_NJ * (int)blockIdx.z; cg < N; cg += 16 * GEMM_NJ * (int)gridDim.z) {
         const int nj = min(GEMM_NJ, (N - cg + 15) / 16);
         f32x4 acc[GEMM_NJ];
 #pragma unroll
@@ -768,7 +775,8 @@ __global__ __launch_bounds__(UN_THREADS) void k_unify(const mep_gemm_desc* __res
 
 extern "C" int mep_gemm(const mep_gemm_desc* descs, int n_desc, int max_tiles, mep_stream_t stream) {
     if (n_desc <= 0 || max_tiles <= 0) return 0;
-    hipLaunchKernelGGL(k_gemm, dim3(max_tiles, n_desc), dim3(GEMM_THREADS), 0, (hipStream_t)stream, descs);
+    // grid.z: column passes of 16 * GEMM_NJ (blocks past a descriptor's N leave at once)
+    hipLaunchKernelGGL(k_gemm, dim3(max_tiles, n_desc, GEMM_ZP), dim3(GEMM_THREADS), 0, (hipStream_t)stream, descs);
     return mep_check_launch("mep_gemm");
 }
 

@@ -43,10 +43,14 @@ MEP_DEV void tile_gemm(const float* As, int lda, const gfloat* W, int ldw, bool 
     }
 }
 
-// Token rows per workgroup of the forward: 64, or 32 for D = 192 (robot_demo.py, inference) so the
-// LDS tiles (x/h, xp/f, f1) stay within 160 KB.
+// Token rows per workgroup of the forward: 32 (MEP_RF_FWD_ROWS; 64 halves the workgroup count --
+// 50 per block at cfg2 -- and measured slower), and 32 always for D = 192 (robot_demo.py,
+// inference) so the LDS tiles (x/h, xp/f, f1) stay within 160 KB.
+#ifndef MEP_RF_FWD_ROWS
+#define MEP_RF_FWD_ROWS 32
+#endif
 template <int D>
-constexpr int rf_fwd_rows() { return D > 128 ? 32 : 64; }
+constexpr int rf_fwd_rows() { return D > 128 ? 32 : MEP_RF_FWD_ROWS; }
 
 template <int D, int FD>
 __global__ __launch_bounds__(THREADS) void k_rf_epi_fwd(const mep_rf_epi_desc* __restrict__ descs) {
@@ -150,32 +154,39 @@ __global__ __launch_bounds__(THREADS) void k_rf_epi_fwd(const mep_rf_epi_desc* _
     }
 }
 
+// Token rows per workgroup of the backward (32: twice the workgroups of 64 -- 50 per block at
+// cfg2 -- and half the LDS; hosts size the partial rows with _lib.rf_bwd_rows)
+#ifndef MEP_RF_BWD_ROWS
+#define MEP_RF_BWD_ROWS 32
+#endif
+
 template <int D, int FD>
 __global__ __launch_bounds__(THREADS) void k_rf_epi_bwd(const mep_rf_epi_bwd_desc* __restrict__ descs) {
     const mep_rf_epi_bwd_desc& bd = descs[blockIdx.y];
     const mep_rf_epi_desc& d = bd.f;
-    const int tok0 = blockIdx.x * 64;
+    constexpr int TB = MEP_RF_BWD_ROWS, MH = TB / 32;   // token rows of this workgroup
+    const int tok0 = blockIdx.x * TB;
     const int ntok = d.ntok;
     if (tok0 >= ntok) return;
     constexpr int LD = D + 4, LF = FD + 4;
     constexpr int STRIDE = 5 * D + FD + 2;
-    __shared__ __attribute__((aligned(16))) float smem[2 * 64 * LD + 64 * LF];
+    __shared__ __attribute__((aligned(16))) float smem[2 * TB * LD + TB * LF];
     __shared__ float red[NWAVE][2][128];
     __shared__ float sred[NWAVE][2];
     float* Gs = smem;                // dout -> dz2 -> dh -> dz1
-    float* Ps = smem + 64 * LD;      // df, then dxp
-    float* Fs = smem + 2 * 64 * LD;  // df1
+    float* Ps = smem + TB * LD;      // df, then dxp
+    float* Fs = smem + 2 * TB * LD;  // df1
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const bool c0 = lane < D, c1 = lane + 64 < D;
     const float sa = *G<const float>(d.a), sb = *G<const float>(d.b);
     const gfloat* stats = G<const float>(d.stats);
     gfloat* part = G<float>(bd.partial) + (int64_t)blockIdx.x * STRIDE;
 
-    stage_cols<64>(Gs, LD, bd.dout, tok0, ntok, 0, D);
+    stage_cols<TB>(Gs, LD, bd.dout, tok0, ntok, 0, D);
     if (bd.dout2.ptr) {
-        stage_cols<64>(Ps, LD, bd.dout2, tok0, ntok, 0, D);
+        stage_cols<TB>(Ps, LD, bd.dout2, tok0, ntok, 0, D);
         __syncthreads();
-        for (int idx = threadIdx.x; idx < 64 * D; idx += THREADS) {
+        for (int idx = threadIdx.x; idx < TB * D; idx += THREADS) {
             const int row = idx / D, c = idx - row * D;
             Gs[row * LD + c] += Ps[row * LD + c];
         }
@@ -187,7 +198,7 @@ __global__ __launch_bounds__(THREADS) void k_rf_epi_bwd(const mep_rf_epi_bwd_des
         const gfloat* w = G<const float>(d.ln2_w);
         const float w0 = c0 ? w[lane] : 0.f, w1 = c1 ? w[lane + 64] : 0.f;
         float pw0 = 0.f, pw1 = 0.f, pb0 = 0.f, pb1 = 0.f;
-        for (int row = wave; row < 64; row += NWAVE) {
+        for (int row = wave; row < TB; row += NWAVE) {
             const int tok = tok0 + row;
             float* gr = Gs + row * LD;
             float* pr = Ps + row * LD;
@@ -234,11 +245,11 @@ __global__ __launch_bounds__(THREADS) void k_rf_epi_bwd(const mep_rf_epi_bwd_des
     }
     for (int c = threadIdx.x; c < D; c += THREADS) {
         float s = 0.f;
-        for (int r = 0; r < 64; ++r) s += Ps[r * LD + c];
+        for (int r = 0; r < TB; ++r) s += Ps[r * LD + c];
         part[4 * D + c] = s;  // db2
     }
     // df1 = relu'(f1) * (df W2)      W2: [D][FD] -> element (k = d, n = f) at W2[d * FD + f]
-    tile_gemm<FD, D, false>(Ps, LD, G<const float>(d.w2), FD, false, [&](int row, int col, float v) {
+    tile_gemm<FD, D, false, MH>(Ps, LD, G<const float>(d.w2), FD, false, [&](int row, int col, float v) {
         const int tok = tok0 + row;
         float o = 0.f;
         if (tok < ntok) {
@@ -250,11 +261,11 @@ __global__ __launch_bounds__(THREADS) void k_rf_epi_bwd(const mep_rf_epi_bwd_des
     __syncthreads();
     for (int c = threadIdx.x; c < FD; c += THREADS) {
         float s = 0.f;
-        for (int r = 0; r < 64; ++r) s += Fs[r * LF + c];
+        for (int r = 0; r < TB; ++r) s += Fs[r * LF + c];
         part[5 * D + c] = s;  // db1
     }
     // dh = dz2 + df1 W1              W1: [FD][D] -> element (k = f, n = d) at W1[f * D + d]
-    tile_gemm<D, FD, false>(Fs, LF, G<const float>(d.w1), D, false, [&](int row, int col, float v) {
+    tile_gemm<D, FD, false, MH>(Fs, LF, G<const float>(d.w1), D, false, [&](int row, int col, float v) {
         Gs[row * LD + col] += v;
     });
     __syncthreads();
@@ -264,7 +275,7 @@ __global__ __launch_bounds__(THREADS) void k_rf_epi_bwd(const mep_rf_epi_bwd_des
         const gfloat* w = G<const float>(d.ln1_w);
         const float w0 = c0 ? w[lane] : 0.f, w1 = c1 ? w[lane + 64] : 0.f;
         float pw0 = 0.f, pw1 = 0.f, pb0 = 0.f, pb1 = 0.f;
-        for (int row = wave; row < 64; row += NWAVE) {
+        for (int row = wave; row < TB; row += NWAVE) {
             const int tok = tok0 + row;
             float* gr = Gs + row * LD;
             float* pr = Ps + row * LD;
@@ -320,7 +331,7 @@ __global__ __launch_bounds__(THREADS) void k_rf_epi_bwd(const mep_rf_epi_bwd_des
         part[5 * D + FD + threadIdx.x] = s;  // da, db
     }
     // dx = dxp Wp                   Wp: [D][D] -> element (k = n_out, n = k_in) at Wp[n_out * D + k_in]
-    tile_gemm<D, D, false>(Ps, LD, G<const float>(d.wp), D, false, [&](int row, int col, float v) {
+    tile_gemm<D, D, false, MH>(Ps, LD, G<const float>(d.wp), D, false, [&](int row, int col, float v) {
         const int tok = tok0 + row;
         if (tok < ntok) row_ptr(bd.dx, tok)[col] = v;
     });

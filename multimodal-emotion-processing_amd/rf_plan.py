@@ -154,7 +154,7 @@ class RealformerPlan:
         blk['dKVin'] = torch.zeros(nk, D, **f32)
         blk['estat'] = torch.zeros(nq, 4, **f32)
         blk['astat'] = torch.zeros(R, H, Tq, 2, **f32)
-        blk['partial'] = torch.zeros(cdiv(nq, 64), _lib.rf_partial_stride(D, FD), **f32)
+        blk['partial'] = torch.zeros(cdiv(nq, _lib.rf_bwd_rows()), _lib.rf_partial_stride(D, FD), **f32)
         if i < nl - 1 or not sp.head:
             blk['OUT'] = torch.zeros(nq, D, **f32)
         if i < nl - 1:
@@ -270,6 +270,7 @@ class RealformerPlan:
         self.d_proj = DescArray(GemmDesc, pd, dev)
         self.t_proj = max(cdiv(b['nk'], 64) for b in self.blocks)
         self.d_q, self.d_attn, self.d_epi, self.t_attn, self.t_epi = [], [], [], [], []
+        self.t_epif, self.t_epib = [], []   # mep_rf_epi_fwd / _bwd workgroups (t_epi: 64-token tiles)
         self.d_epib, self.d_attnb, self.t_attnb, self.d_ingrad = [], [], [], []
         self.f_attn, self.f_attnb = [], []
         for i in range(nl):
@@ -285,6 +286,8 @@ class RealformerPlan:
             self.t_attnb.append(geo[1])
             self.f_attn.append(geo[2])
             self.t_epi.append(max(cdiv(b['nq'], 64) for b in layer))
+            self.t_epif.append(max(cdiv(b['nq'], _lib.rf_epi_rows(self.spec.D)) for b in layer))
+            self.t_epib.append(max(cdiv(b['nq'], _lib.rf_bwd_rows()) for b in layer))
             self.d_epib.append(DescArray(RfEpiBwdDesc, [self._epi_bwd_desc(b) for b in layer], dev))
             ab = [self._attn_bwd_desc(b) for b in layer]
             self.d_attnb.append(DescArray(AttnBwdDesc, ab, dev))
@@ -439,7 +442,7 @@ class RealformerPlan:
             if i > 0:
                 launch('mep_gemm', self.d_q[i], self.t_epi[i], stream)
             launch('mep_attn_fwd', self.d_attn[i], self.t_attn[i], stream, threads=self.f_attn[i])
-            launch('mep_rf_epi_fwd', self.d_epi[i], self.t_epi[i], stream, extra=ex)
+            launch('mep_rf_epi_fwd', self.d_epi[i], self.t_epif[i], stream, extra=ex)
         if sp.head:
             launch('mep_pool_fwd', self.d_pool, self.t_pool, stream)
             launch('mep_gemm', self.d_fc, self.t_fc, stream)
@@ -464,7 +467,7 @@ class RealformerPlan:
             self.dout_chain.copy_(ext_dout.reshape(self.dout_chain.shape))
         self.dQP_all.zero_()
         for i in reversed(range(nl)):
-            launch('mep_rf_epi_bwd', self.d_epib[i], self.t_epi[i], stream, extra=ex)
+            launch('mep_rf_epi_bwd', self.d_epib[i], self.t_epib[i], stream, extra=ex)
             launch('mep_attn_bwd', self.d_attnb[i], self.t_attnb[i], stream, threads=self.f_attnb[i])
             launch('mep_gemm', self.d_ingrad[i], self.t_ingrad, stream)
         launch('mep_sum_rows', self.d_sum, self.t_sum, stream)

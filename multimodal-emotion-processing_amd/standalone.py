@@ -254,7 +254,7 @@ class _RFBlockFn(torch.autograd.Function):
                             a=a.data_ptr(), b=b.data_ptr(), stats=estat.data_ptr(), ntok=B * Tq, D=D, FD=FD)
         geo = _lib.attn_geometry([ad])
         launch('mep_attn_fwd', DescArray(AttnDesc, [ad], dev), geo[0], threads=geo[2])
-        launch('mep_rf_epi_fwd', DescArray(_lib.RfEpiDesc, [ed], dev), cdiv(B * Tq, 64), extra=(D, FD))
+        launch('mep_rf_epi_fwd', DescArray(_lib.RfEpiDesc, [ed], dev), cdiv(B * Tq, _lib.rf_epi_rows(D)), extra=(D, FD))
         ctx.save_for_backward(q, k, v, mask, QP, KV, X, XP, Hh, F1, F, S, astat, estat,
                               wq, wk, wv, wp, n1w, n1b, n2w, n2b, w1, b1, w2, b2, a, b, c)
         ctx.sp = sp
@@ -278,7 +278,7 @@ class _RFBlockFn(torch.autograd.Function):
         dF1 = torch.empty(B, Tq, FD, **f)
         dKV2 = torch.empty(B, Tk, 2 * D, **f)
         dk_in, dv_in = torch.empty(B, Tk, D, **f), torch.empty(B, Tk, D, **f)
-        nt = cdiv(B * Tq, 64)
+        nt = cdiv(B * Tq, _lib.rf_bwd_rows())
         stride = _lib.rf_partial_stride(D, FD)
         part = torch.empty(nt, stride, **f)
         has_prev = ctx.sp is not None

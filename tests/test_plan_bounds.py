@@ -206,7 +206,7 @@ def _rf_epi_bwd(c, d):
     for name in ('dout', 'dout2', 'df', 'dxp', 'dx', 'dq'):
         c.rows('rf_epi_bwd.' + name, getattr(d, name), f.ntok, f.D)
     c.rows('rf_epi_bwd.df1', d.df1, f.ntok, f.FD)
-    c.inside('rf_epi_bwd.partial', d.partial, cdiv(f.ntok, 64) * _lib.rf_partial_stride(f.D, f.FD) * F)
+    c.inside('rf_epi_bwd.partial', d.partial, cdiv(f.ntok, _lib.rf_bwd_rows()) * _lib.rf_partial_stride(f.D, f.FD) * F)
 
 
 def _rf_head(c, d):
