@@ -160,6 +160,10 @@ typedef struct {
                                     cmu-mosei/run.py:241-242 attends with k = v): the short kernel keeps one
                                     register set for K / V and one dK + dV accumulator (4 waves per SIMD);
                                     a descriptor that breaks the promise gets NaN dq rows */
+#define MEP_ATTN_SPLITQ 0x80000  /* for launches with few (b, h) units: forward tasks of 16 queries instead
+                                    of 64 (max_tiles = ceil(B H ceil(Tq / 16) / 4)); backward: descriptors
+                                    with Tk <= 64 also run the workgroup-per-(b, h) kernel, its 4 waves on
+                                    separate query tiles (4x the waves of the wave-per-(b, h) kernel) */
 int mep_attn_fwd(const mep_attn_desc* descs, int n_desc, int max_tiles, int flags, mep_stream_t stream);
 
 /* Backward of the attention core.  Inputs dx (grad of X), the forward's q/k/v/x/stats/s_prev.

@@ -264,6 +264,24 @@ ATTN_PREV, ATTN_SOUT, ATTN_SHORT, ATTN_LONG = 1, 2, 4, 8   # MEP_ATTN_* (include
 PREC_BF16 = 0x10000   # MEP_PREC_BF16: bf16-operand products (attention flags, epilogue D argument)
 ATTN_HD32 = 0x20000   # MEP_ATTN_HD32: head dim 32 attention forward (robot_demo)
 ATTN_KV = 0x40000     # MEP_ATTN_KV: backward with k == v and dk == dv on every descriptor
+ATTN_SPLITQ = 0x80000 # MEP_ATTN_SPLITQ: backward, Tk <= 64 descriptors on the workgroup-per-(b, h) kernel
+
+
+def attn_fwd_splitq(descs, min_units=1024):
+    """(MEP_ATTN_SPLITQ, forward max_tiles with 16-query wave tasks) when the launch holds fewer
+    (b, h) units than min_units, else (0, None)"""
+    units = sum(d.B * d.H for d in descs)
+    if not 0 < units < min_units:
+        return 0, None
+    return ATTN_SPLITQ, max(-(-(d.B * d.H * -(-d.Tq // 16)) // 4) for d in descs)
+
+
+def attn_bwd_splitq(bdescs, min_units=1024):
+    """MEP_ATTN_SPLITQ when the launch's Tk <= 64 descriptors hold fewer (b, h) units than
+    min_units (one wave each on the short kernel would leave most of the 1024 SIMDs idle: cfg2's
+    realformer layer has 64 x 6 = 384); 0 otherwise"""
+    units = sum(b.f.B * b.f.H for b in bdescs if b.f.Tk <= 64)
+    return ATTN_SPLITQ if 0 < units < min_units else 0
 
 
 def rf_bwd_rows():

@@ -280,7 +280,7 @@ MEP_DEV BRow brow(const mep_rows& v, int b, int n, int D) {
 // (scores on one bf16 product, P.V on bf16 P and V).  HDIM = 16 or 32 (robot_demo, inference):
 // NHB = HDIM / 16 head blocks of 16 dims -- the score sums NHB 16-deep products, P.V fills NHB
 // output tiles.
-template <bool PREV, bool SOUT, bool SINGLE, bool BF, int HDIM = HD>
+template <bool PREV, bool SOUT, bool SINGLE, bool BF, int HDIM = HD, int qch = CH>
 MEP_DEV void attn_fwd_task(const mep_attn_desc& d, int qc, int h, int b, int lane) {
     constexpr int NHB = HDIM / 16;
     const int c = lane & 15, g = lane >> 4;
@@ -293,8 +293,8 @@ MEP_DEV void attn_fwd_task(const mep_attn_desc& d, int qc, int h, int b, int lan
     const int D = d.H * HDIM;
     const BRow Qb = brow(d.q, b, Tq, D), Kb = brow(d.k, b, Tk, D), Vb = brow(d.v, b, Tk, D), Xb = brow(d.x, b, Tq, D);
     const int sbase = (b * d.H + h) * Tq;        // row of (b, h, query 0) in [B,H,Tq,Tk]
-    const int q_lo = qc * CH;
-    const int nqt = min(NT, (Tq - q_lo + 15) / 16);
+    const int q_lo = qc * qch;                   // qch: queries per task (64, or 16 with MEP_ATTN_SPLITQ)
+    const int nqt = min(qch / 16, (Tq - q_lo + 15) / 16);
     gfloat* stats = G<float>(d.stats);
 
     floatx4 o[SINGLE ? 1 : NT][NHB];
@@ -358,8 +358,10 @@ MEP_DEV void attn_fwd_task(const mep_attn_desc& d, int qc, int h, int b, int lan
 #pragma unroll
         for (int qt = 0; qt < NT; ++qt)
 #pragma unroll
-            for (int hb = 0; hb < NHB; ++hb)
-                Qb.ld4(qfa[qt][hb], Qb.at(q_lo + qt * 16 + c, hc + 16 * hb + 4 * g));   // past Tq: 0
+            for (int hb = 0; hb < NHB; ++hb) {
+                if (qch == CH || qt < nqt) Qb.ld4(qfa[qt][hb], Qb.at(q_lo + qt * 16 + c, hc + 16 * hb + 4 * g));   // past Tq: 0
+                else qfa[qt][hb][0] = qfa[qt][hb][1] = qfa[qt][hb][2] = qfa[qt][hb][3] = 0.f;
+            }
 #pragma unroll
         for (int qt = 0; qt < NT; ++qt) {
             if (qt >= nqt) break;
@@ -454,15 +456,17 @@ MEP_DEV void attn_fwd_task(const mep_attn_desc& d, int qc, int h, int b, int lan
 }
 
 template <bool PREV, bool SOUT, bool SINGLE, bool BF, int HDIM = HD>
-__global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu((SINGLE && !PREV && HDIM == 16) ? MEP_FWD_WAVES : (HDIM == 32 && !SINGLE) ? 1 : 2))) void k_attn_fwd(const mep_attn_desc* __restrict__ descs) {
+__global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu((SINGLE && !PREV && HDIM == 16) ? MEP_FWD_WAVES : (HDIM == 32 && !SINGLE) ? 1 : 2))) void k_attn_fwd(const mep_attn_desc* __restrict__ descs, int qch) {
     const mep_attn_desc& d = descs[blockIdx.y];
     if ((d.Tk <= CH) != SINGLE) return;    // the other variant's descriptor
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int nqc = (d.Tq + CH - 1) / CH;
+    const int nqc = (d.Tq + qch - 1) / qch;
     const int task = blockIdx.x * WAVES + wave;
     if (task >= d.B * d.H * nqc) return;   // whole wave leaves; no barriers below
     const int qc = task % nqc, bh = task / nqc;
-    attn_fwd_task<PREV, SOUT, SINGLE, BF, HDIM>(d, qc, bh % d.H, bh / d.H, lane);
+    // queries per task as a compile-time constant (the 64-query path keeps its constant indexing)
+    if (qch == CH) attn_fwd_task<PREV, SOUT, SINGLE, BF, HDIM, CH>(d, qc, bh % d.H, bh / d.H, lane);
+    else attn_fwd_task<PREV, SOUT, SINGLE, BF, HDIM, 16>(d, qc, bh % d.H, bh / d.H, lane);
 }
 
 MEP_DEV void wave_lds_sync() {
@@ -864,12 +868,12 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(bwd_sho
 // LDS: [RED] dK/dV partials (aliased by the waves' dS transposes during the query loop), [4] dc
 // partials, [dq_tiles][256] the carried dQ tiles.
 template <bool PREV, bool DSN, bool BF>
-__global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(2))) void k_attn_bwd_long(const mep_attn_bwd_desc* __restrict__ descs) {
+__global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(2))) void k_attn_bwd_long(const mep_attn_bwd_desc* __restrict__ descs, int splitq) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     const mep_attn_bwd_desc& bd = descs[blockIdx.y];
     const mep_attn_desc& d = bd.f;
     const int bh = blockIdx.x;
-    if (d.Tk <= CH || bh >= d.B * d.H) return;   // a SHORT descriptor / past the end: the whole workgroup
+    if ((d.Tk <= CH && !splitq) || bh >= d.B * d.H) return;   // a SHORT descriptor / past the end: the whole workgroup
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     Bwd<PREV, DSN, BF> u(bd, bh / d.H, bh % d.H, lane);
     const int D = d.H * HD;
@@ -946,11 +950,12 @@ extern "C" int mep_attn_fwd(const mep_attn_desc* descs, int n_desc, int max_tile
     if (n_desc <= 0 || max_tiles <= 0) return 0;
     if (!(flags & (MEP_ATTN_SHORT | MEP_ATTN_LONG))) { mep_set_error("mep_attn_fwd: flags need SHORT and/or LONG"); return MEP_EINVAL; }
     const bool prev = flags & MEP_ATTN_PREV, sout = flags & MEP_ATTN_SOUT, bf = flags & MEP_PREC_BF16;
+    const int qch = (flags & MEP_ATTN_SPLITQ) ? 16 : CH;   // queries per wave task
     const dim3 grid(max_tiles, n_desc), block(THREADS);
     hipStream_t st = (hipStream_t)stream;
     if (flags & MEP_ATTN_HD32) {   // robot_demo (inference, fp32 path)
         if (bf) { mep_set_error("mep_attn_fwd: hd = 32 runs the fp32 path only"); return MEP_EINVAL; }
-#define MEP_FWD32(P, S, SI) hipLaunchKernelGGL((k_attn_fwd<P, S, SI, false, 32>), grid, block, 0, st, descs)
+#define MEP_FWD32(P, S, SI) hipLaunchKernelGGL((k_attn_fwd<P, S, SI, false, 32>), grid, block, 0, st, descs, qch)
         for (int single = 1; single >= 0; --single) {
             if (!(flags & (single ? MEP_ATTN_SHORT : MEP_ATTN_LONG))) continue;
             if (single) {
@@ -965,7 +970,8 @@ extern "C" int mep_attn_fwd(const mep_attn_desc* descs, int n_desc, int max_tile
         return mep_check_launch("mep_attn_fwd");
     }
 #define MEP_FWD(P, S, SI) \
-    do { if (bf) hipLaunchKernelGGL((k_attn_fwd<P, S, SI, true>), grid, block, 0, st, descs); else hipLaunchKernelGGL((k_attn_fwd<P, S, SI, false>), grid, block, 0, st, descs); } while (0)
+    do { if (bf) hipLaunchKernelGGL((k_attn_fwd<P, S, SI, true>), grid, block, 0, st, descs, qch); \
+         else hipLaunchKernelGGL((k_attn_fwd<P, S, SI, false>), grid, block, 0, st, descs, qch); } while (0)
     for (int single = 1; single >= 0; --single) {
         if (!(flags & (single ? MEP_ATTN_SHORT : MEP_ATTN_LONG))) continue;
         if (single) {
@@ -991,7 +997,8 @@ extern "C" int mep_attn_bwd(const mep_attn_bwd_desc* descs, int n_desc, int max_
     const size_t lds = sizeof(float) * ((size_t)RED + WAVES + 256 * (size_t)dq_tiles);
     if (lds > 160 * 1024) { mep_set_error("mep_attn_bwd: Tq too large for the LDS-carried dQ (Tk > 64)"); return MEP_EINVAL; }
     hipStream_t st = (hipStream_t)stream;
-    if (flags & MEP_ATTN_SHORT) {
+    const bool splitq = flags & MEP_ATTN_SPLITQ;
+    if ((flags & MEP_ATTN_SHORT) && !splitq) {
         const dim3 grid((max_tiles + WAVES - 1) / WAVES, n_desc), block(THREADS);
 #define MEP_BS2(P, S, K) \
     do { if (bf) hipLaunchKernelGGL((k_attn_bwd_short<P, S, true, K>), grid, block, 0, st, descs); else hipLaunchKernelGGL((k_attn_bwd_short<P, S, false, K>), grid, block, 0, st, descs); } while (0)
@@ -1001,7 +1008,7 @@ extern "C" int mep_attn_bwd(const mep_attn_bwd_desc* descs, int n_desc, int max_
 #undef MEP_BS
 #undef MEP_BS2
     }
-    if (flags & MEP_ATTN_LONG) {
+    if ((flags & MEP_ATTN_LONG) || splitq) {
         static bool lds_attr = false;   // allow more than 64 KB of dynamic LDS (long Tq)
         if (!lds_attr) {
             const int mx = 160 * 1024;
@@ -1014,7 +1021,8 @@ extern "C" int mep_attn_bwd(const mep_attn_bwd_desc* descs, int n_desc, int max_
         }
         const dim3 grid(max_tiles, n_desc), block(THREADS);
 #define MEP_BL(P, S) \
-    do { if (bf) hipLaunchKernelGGL((k_attn_bwd_long<P, S, true>), grid, block, lds, st, descs); else hipLaunchKernelGGL((k_attn_bwd_long<P, S, false>), grid, block, lds, st, descs); } while (0)
+    do { if (bf) hipLaunchKernelGGL((k_attn_bwd_long<P, S, true>), grid, block, lds, st, descs, (int)splitq); \
+         else hipLaunchKernelGGL((k_attn_bwd_long<P, S, false>), grid, block, lds, st, descs, (int)splitq); } while (0)
         if (prev) { if (dsn) MEP_BL(true, true); else MEP_BL(true, false); }
         else      { if (dsn) MEP_BL(false, true); else MEP_BL(false, false); }
 #undef MEP_BL

@@ -21,6 +21,7 @@ adjacent [w_qkv.1; w_qkv.2] weights, one [ntok, 2D] gradient); last-layer output
 straight into the pooled tensor [R, T_l+T_a+T_v, 3D] (torch.cat at realformer.py:258-261).
 """
 import ctypes
+import os
 
 import torch
 
@@ -28,6 +29,8 @@ from . import _lib
 from ._lib import (AttnBwdDesc, AttnDesc, ColsumDesc, DescArray, GemmDesc, PoolDesc, RfEpiBwdDesc, RfEpiDesc,
                    RfHeadDesc, Rows, SumDesc, launch)
 from .trimodal import CHAINS, MODS, TIME_ORDER, UNIFY_NAMES, cdiv, crows, make_wgrad, rows
+
+RF_SPLITQ = os.environ.get('MEP_RF_SPLITQ', '1') != '0'   # attention backward: query tiles over 4 waves
 
 NC = 6  # State_Transfer classes (realformer.py:268-269)
 POS_NAMES = {'l': 'linguistic_position', 'v': 'visual_position', 'a': 'acoustic_position'}
@@ -282,16 +285,17 @@ class RealformerPlan:
             self.d_attn.append(DescArray(AttnDesc, ad, dev))
             self.d_epi.append(DescArray(RfEpiDesc, [self._epi_desc(b) for b in layer], dev))
             geo = _lib.attn_geometry(ad)
-            self.t_attn.append(geo[0])
+            sq, sq_tiles = _lib.attn_fwd_splitq(ad) if RF_SPLITQ else (0, None)
+            self.t_attn.append(sq_tiles or geo[0])
             self.t_attnb.append(geo[1])
-            self.f_attn.append(geo[2])
+            self.f_attn.append(geo[2] | sq)
             self.t_epi.append(max(cdiv(b['nq'], 64) for b in layer))
             self.t_epif.append(max(cdiv(b['nq'], _lib.rf_epi_rows(self.spec.D)) for b in layer))
             self.t_epib.append(max(cdiv(b['nq'], _lib.rf_bwd_rows()) for b in layer))
             self.d_epib.append(DescArray(RfEpiBwdDesc, [self._epi_bwd_desc(b) for b in layer], dev))
             ab = [self._attn_bwd_desc(b) for b in layer]
             self.d_attnb.append(DescArray(AttnBwdDesc, ab, dev))
-            self.f_attnb.append(_lib.attn_bwd_flags(ab))
+            self.f_attnb.append(_lib.attn_bwd_flags(ab) | (_lib.attn_bwd_splitq(ab) if RF_SPLITQ else 0))
             ig = []
             for b in layer:
                 # dq_in += dQP W_q  (onto the residual dz1 the epilogue backward wrote)
