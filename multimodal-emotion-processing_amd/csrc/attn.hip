@@ -455,18 +455,16 @@ MEP_DEV void attn_fwd_task(const mep_attn_desc& d, int qc, int h, int b, int lan
     }
 }
 
-template <bool PREV, bool SOUT, bool SINGLE, bool BF, int HDIM = HD>
-__global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu((SINGLE && !PREV && HDIM == 16) ? MEP_FWD_WAVES : (HDIM == 32 && !SINGLE) ? 1 : 2))) void k_attn_fwd(const mep_attn_desc* __restrict__ descs, int qch) {
+template <bool PREV, bool SOUT, bool SINGLE, bool BF, int HDIM = HD, int QCH = CH>
+__global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu((SINGLE && !PREV && HDIM == 16) ? MEP_FWD_WAVES : (HDIM == 32 && !SINGLE) ? 1 : 2))) void k_attn_fwd(const mep_attn_desc* __restrict__ descs) {
     const mep_attn_desc& d = descs[blockIdx.y];
     if ((d.Tk <= CH) != SINGLE) return;    // the other variant's descriptor
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int nqc = (d.Tq + qch - 1) / qch;
+    const int nqc = (d.Tq + QCH - 1) / QCH;   // QCH: queries per wave task (64, or 16 with MEP_ATTN_SPLITQ)
     const int task = blockIdx.x * WAVES + wave;
     if (task >= d.B * d.H * nqc) return;   // whole wave leaves; no barriers below
     const int qc = task % nqc, bh = task / nqc;
-    // queries per task as a compile-time constant (the 64-query path keeps its constant indexing)
-    if (qch == CH) attn_fwd_task<PREV, SOUT, SINGLE, BF, HDIM, CH>(d, qc, bh % d.H, bh / d.H, lane);
-    else attn_fwd_task<PREV, SOUT, SINGLE, BF, HDIM, 16>(d, qc, bh % d.H, bh / d.H, lane);
+    attn_fwd_task<PREV, SOUT, SINGLE, BF, HDIM, QCH>(d, qc, bh % d.H, bh / d.H, lane);
 }
 
 MEP_DEV void wave_lds_sync() {
@@ -950,12 +948,12 @@ extern "C" int mep_attn_fwd(const mep_attn_desc* descs, int n_desc, int max_tile
     if (n_desc <= 0 || max_tiles <= 0) return 0;
     if (!(flags & (MEP_ATTN_SHORT | MEP_ATTN_LONG))) { mep_set_error("mep_attn_fwd: flags need SHORT and/or LONG"); return MEP_EINVAL; }
     const bool prev = flags & MEP_ATTN_PREV, sout = flags & MEP_ATTN_SOUT, bf = flags & MEP_PREC_BF16;
-    const int qch = (flags & MEP_ATTN_SPLITQ) ? 16 : CH;   // queries per wave task
+    const bool splitq = flags & MEP_ATTN_SPLITQ;   // 16 queries per wave task instead of 64
     const dim3 grid(max_tiles, n_desc), block(THREADS);
     hipStream_t st = (hipStream_t)stream;
     if (flags & MEP_ATTN_HD32) {   // robot_demo (inference, fp32 path)
         if (bf) { mep_set_error("mep_attn_fwd: hd = 32 runs the fp32 path only"); return MEP_EINVAL; }
-#define MEP_FWD32(P, S, SI) hipLaunchKernelGGL((k_attn_fwd<P, S, SI, false, 32>), grid, block, 0, st, descs, qch)
+#define MEP_FWD32(P, S, SI) hipLaunchKernelGGL((k_attn_fwd<P, S, SI, false, 32>), grid, block, 0, st, descs)
         for (int single = 1; single >= 0; --single) {
             if (!(flags & (single ? MEP_ATTN_SHORT : MEP_ATTN_LONG))) continue;
             if (single) {
@@ -970,8 +968,10 @@ extern "C" int mep_attn_fwd(const mep_attn_desc* descs, int n_desc, int max_tile
         return mep_check_launch("mep_attn_fwd");
     }
 #define MEP_FWD(P, S, SI) \
-    do { if (bf) hipLaunchKernelGGL((k_attn_fwd<P, S, SI, true>), grid, block, 0, st, descs, qch); \
-         else hipLaunchKernelGGL((k_attn_fwd<P, S, SI, false>), grid, block, 0, st, descs, qch); } while (0)
+    do { if (splitq) { if (bf) hipLaunchKernelGGL((k_attn_fwd<P, S, SI, true, HD, 16>), grid, block, 0, st, descs); \
+                       else hipLaunchKernelGGL((k_attn_fwd<P, S, SI, false, HD, 16>), grid, block, 0, st, descs); } \
+         else if (bf) hipLaunchKernelGGL((k_attn_fwd<P, S, SI, true>), grid, block, 0, st, descs); \
+         else hipLaunchKernelGGL((k_attn_fwd<P, S, SI, false>), grid, block, 0, st, descs); } while (0)
     for (int single = 1; single >= 0; --single) {
         if (!(flags & (single ? MEP_ATTN_SHORT : MEP_ATTN_LONG))) continue;
         if (single) {
