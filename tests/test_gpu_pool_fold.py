@@ -11,12 +11,13 @@ pytestmark = pytest.mark.gpu
 
 
 def _step(model, fold, B, T, dims, dev, NC):
-    trimodal.POOL_FOLD = fold
+    saved, trimodal.POOL_FOLD = trimodal.POOL_FOLD, fold
     try:
         r = model.mep_runner(dev)
         p = trimodal.TriModalPlan(r.spec, r.flat, B, T, dev)
     finally:
-        trimodal.POOL_FOLD = True
+        trimodal.POOL_FOLD = saved
+    assert p.pool_fold == fold
     g = torch.Generator(device='cpu').manual_seed(5)
     x = [torch.randn(B, 2, t, d, generator=g).to(dev) for t, d in zip(T, dims)]
     mk = [torch.ones(B, 2, t).to(dev) for t in T]
