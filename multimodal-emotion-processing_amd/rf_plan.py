@@ -476,8 +476,11 @@ class RealformerPlan:
             launch('mep_gemm', self.d_ingrad[i], self.t_ingrad, stream)
         launch('mep_sum_rows', self.d_sum, self.t_sum, stream)
         launch('mep_wgrad', self.d_wgrad, self.t_wgrad, stream)
-        launch('mep_wgrad_reduce', self.d_wgrad, self.t_wgred, stream)
-        launch('mep_colsum', self.d_colsum, self.t_colsum, stream)
+        # weight-gradient split sums and LayerNorm / ReZero / residual-coefficient column sums: one
+        # launch (no head partials here: the State_Transfer head reduces in mep_rf_head)
+        _lib.call('mep_reduce_grads', self.d_wgrad.ptr, self.d_wgrad.n, self.t_wgred, self.d_colsum.ptr,
+                  self.d_colsum.n, self.t_colsum if self.d_colsum.n else 0, None, 0, 0, 0, 0, 0, 0, 0, 0,
+                  stream=stream)
 
 
 class RealformerRunner:
