@@ -217,7 +217,8 @@ typedef struct {
      * this block's slice of the pooled tensor -- token tok = b * pool_Tq + t sits at time
      * pool_t0 + t and columns pool_col .. pool_col + D - 1 of [B, pool_T, pool_C]
      * (cmu-mosei/run.py:314-318).  dout2 is still added. */
-    int32_t  pool_T;
+    int32_t  pool_T;         /* < 0: the mean half of dpooled already holds dmean / |pool_T|
+                                (mep_head_desc.mean_div) */
     uint64_t pool_dpooled;   /* [B][2 * pool_C] floats (mean part, then max part) */
     uint64_t pool_argmax;    /* [B][pool_C] int32 */
     int32_t  pool_C, pool_Tq, pool_t0, pool_col;
@@ -359,6 +360,10 @@ typedef struct {
                                     under data parallelism); 0 = B / 2                */
     uint64_t ext_dlogits;        /* [B, NC] upstream grad of the logits; when set the fused
                                     loss is skipped and this gradient is back-propagated */
+    int32_t  mean_div;           /* > 0: the mean halves of dpooled0/1 (entries < F/2) are written
+                                    already divided by mean_div (the pool's time length T), i.e.
+                                    as the per-step gradient dmean / T of the mean pool */
+    int32_t  _pad;
 } mep_head_desc;
 int mep_head_fwd_bwd(const mep_head_desc* d, mep_stream_t stream);
 /* Reduce the per-row partials into the gradient buffers and the batch-mean loss:

@@ -90,7 +90,8 @@ class HeadDesc(ctypes.Structure):
                 ('wc1', u64), ('trans', u64), ('ln_w', u64), ('ln_b', u64), ('wo', u64), ('bo', u64),
                 ('labels', u64), ('logits', u64), ('row_loss', u64), ('partial', u64),
                 ('B', i32), ('F', i32), ('NC', i32), ('labels_are_float', i32), ('rdrop', i32),
-                ('compute_grad', i32), ('loss_scale', f32), ('rdrop_pairs', i32), ('ext_dlogits', u64)]
+                ('compute_grad', i32), ('loss_scale', f32), ('rdrop_pairs', i32), ('ext_dlogits', u64),
+                ('mean_div', i32), ('_pad', i32)]
 
 
 class RfEpiDesc(ctypes.Structure):

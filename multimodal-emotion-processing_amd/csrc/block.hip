@@ -113,9 +113,10 @@ MEP_DEV bool tile_range(int ntok, int& t_begin, int& t_end) {
 }
 
 // upstream gradient of token tc (clamped in range), features col .. col+3: the dout row view, or
-// with pool_T > 0 the mean+max pool's backward formed in registers -- exactly k_pool_bwd's dx
+// with pool_T != 0 the mean+max pool's backward formed in registers -- exactly k_pool_bwd's dx
 // (pool_head.hip: dmean = dpooled / T, + dmax at the argmax step), so the pooled tensor's gradient
-// [B, T, C] is never written or read (cmu-mosei/run.py:314-318)
+// [B, T, C] is never written or read (cmu-mosei/run.py:314-318).  pool_T < 0: the head already
+// wrote the mean half of dpooled divided by |pool_T| (the same division, done once per column).
 struct Upstream {
     const gfloat* dp;      // pool: this block's columns of dpooled (mean part; max part at + C)
     const MEP_G int* am;   // pool: this block's columns of argmax
@@ -124,7 +125,7 @@ struct Upstream {
         : dp(G<const float>(bd.pool_dpooled) + bd.pool_col), am(G<const int>(bd.pool_argmax) + bd.pool_col),
           C(bd.pool_C), T(bd.pool_T), Tq(bd.pool_Tq), t0(bd.pool_t0) {}
     MEP_DEV f32x4 at(const mep_epi_bwd_desc& bd, int tc, int col) const {
-        if (T <= 0) return ld4w(row_ptr(bd.dout, tc) + col);
+        if (T == 0) return ld4w(row_ptr(bd.dout, tc) + col);
         const int b = tc / Tq, tg = t0 + (tc - b * Tq);
         const gfloat* p = dp + (int64_t)b * 2 * C + col;
         const f32x4 mean = ld4w(p), mx = ld4w(p + C);
@@ -135,7 +136,7 @@ struct Upstream {
         f32x4 v;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-            const float dmean = mean[r] / (float)T;
+            const float dmean = T > 0 ? mean[r] / (float)T : mean[r];   // T < 0: divided by the head
             v[r] = ((int)a[r] == tg) ? dmean + mx[r] : dmean;
         }
         return v;

@@ -433,6 +433,10 @@ __global__ __launch_bounds__(256) void k_head(mep_head_desc d) {
                     }
                 }
                 if (k < F) {
+                    if (d.mean_div > 0 && 2 * k < F) {   // the mean pool's per-step gradient
+                        a0 = a0 / (float)d.mean_div;
+                        a1 = a1 / (float)d.mean_div;
+                    }
                     dp0[k] = a0;
                     dp1[k] = a1;
                 }

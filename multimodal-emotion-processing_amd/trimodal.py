@@ -398,7 +398,8 @@ class TriModalPlan:
             wo=fl.ptr('out.weight'), bo=fl.ptr('out.bias'), labels=self.labels.data_ptr(),
             logits=self.logits.data_ptr(), row_loss=self.row_loss.data_ptr(),
             partial=self.head_partial.data_ptr(), B=B, F=self.F, NC=NC,
-            labels_are_float=int(self.labels_float), rdrop=0, compute_grad=1, loss_scale=1.0 / B, ext_dlogits=0)
+            labels_are_float=int(self.labels_float), rdrop=0, compute_grad=1, loss_scale=1.0 / B, ext_dlogits=0,
+            mean_div=self.Ttot if self.pool_fold else 0)   # the fold reads dmean / T straight from dpooled
         # backward per layer
         self.d_epib, self.d_attnb, self.t_attnb, self.f_attnb = [], [], [], []
         for i in range(nl):
@@ -477,7 +478,7 @@ class TriModalPlan:
         # upstream gradient: the mean+max pool's backward of this block's slice of Xcat (formed in
         # the kernel from dpooled / argmax) + the next layer's dq
         if self.pool_fold:
-            up = dict(dout=Rows(), pool_T=self.Ttot, pool_dpooled=self.dpooled[e].data_ptr(),
+            up = dict(dout=Rows(), pool_T=-self.Ttot, pool_dpooled=self.dpooled[e].data_ptr(),
                       pool_argmax=self.argmax[e].data_ptr(), pool_C=self.C, pool_Tq=Tq,
                       pool_t0=self.toff[blk['qm']], pool_col=blk['col'])
         else:

@@ -128,9 +128,9 @@ def _epi_bwd(c, d):
     for name in ('dout', 'dout2', 'dz', 'dxp', 'dx', 'dq'):
         c.rows('epi_bwd.' + name, getattr(d, name), f.ntok, f.D)
     c.inside('epi_bwd.ln_partial', d.ln_partial, cdiv(f.ntok, 16) * 2 * f.D * F)
-    if d.pool_T > 0:   # upstream gradient formed from the pool's dpooled / argmax slices
+    if d.pool_T != 0:   # upstream gradient formed from the pool's dpooled / argmax slices
         assert d.dout.ptr == 0 and f.ntok % d.pool_Tq == 0
-        assert d.pool_t0 + d.pool_Tq <= d.pool_T and d.pool_col + f.D <= d.pool_C and d.pool_col % 4 == 0
+        assert d.pool_t0 + d.pool_Tq <= abs(d.pool_T) and d.pool_col + f.D <= d.pool_C and d.pool_col % 4 == 0
         nb = f.ntok // d.pool_Tq
         c.inside('epi_bwd.pool_dpooled', d.pool_dpooled, nb * 2 * d.pool_C * F)
         c.inside('epi_bwd.pool_argmax', d.pool_argmax, nb * d.pool_C * 4)
