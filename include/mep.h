@@ -190,7 +190,10 @@ typedef struct {
     mep_rows q, x, xp, z, out;
     uint64_t wp, wm, ln_w, ln_b;
     uint64_t stats;      /* [ntok][2] */
-    uint64_t seed;       /* device uint64* dropout seed (0: no dropout) */
+    uint64_t seed;       /* device uint64[2] {dropout seed, row0} (0: no dropout).  The mask of
+                            element (token tok, feature f) hashes ((row0 * q.T + tok) * D + f):
+                            row0 = the first GLOBAL batch row of a data-parallel shard, so every
+                            rank draws the masks of the full batch's rows (csrc/common.h drop_scale) */
     int32_t  ntok, D;
     float    drop_p;
     int32_t  drop_stream;/* distinct per block */
@@ -283,6 +286,7 @@ typedef struct {
     int32_t  B, P, D, compute_grad;
     float    loss_scale;
     int32_t  _pad;
+    uint64_t scale;      /* device float[1] loss scale read in place of loss_scale, or 0 */
 } mep_rf_head_desc;
 int mep_rf_head(const mep_rf_head_desc* d, mep_stream_t stream);
 
@@ -364,6 +368,9 @@ typedef struct {
                                     already divided by mean_div (the pool's time length T), i.e.
                                     as the per-step gradient dmean / T of the mean pool */
     int32_t  _pad;
+    uint64_t scale;              /* device float[2] {loss_scale, rdrop_pairs} read at run time in place
+                                    of the two fields above, or 0: a captured graph then replays any
+                                    data-parallel share (1 / B_global changes per batch) unchanged */
 } mep_head_desc;
 int mep_head_fwd_bwd(const mep_head_desc* d, mep_stream_t stream);
 /* Reduce the per-row partials into the gradient buffers and the batch-mean loss:

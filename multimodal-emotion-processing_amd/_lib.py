@@ -91,7 +91,7 @@ class HeadDesc(ctypes.Structure):
                 ('labels', u64), ('logits', u64), ('row_loss', u64), ('partial', u64),
                 ('B', i32), ('F', i32), ('NC', i32), ('labels_are_float', i32), ('rdrop', i32),
                 ('compute_grad', i32), ('loss_scale', f32), ('rdrop_pairs', i32), ('ext_dlogits', u64),
-                ('mean_div', i32), ('_pad', i32)]
+                ('mean_div', i32), ('_pad', i32), ('scale', u64)]
 
 
 class RfEpiDesc(ctypes.Structure):
@@ -115,7 +115,8 @@ class RfHeadDesc(ctypes.Structure):
     _fields_ = [('fc', u64), ('ln_w', u64), ('ln_b', u64), ('wc', u64), ('bc', u64), ('trans', u64),
                 ('labels', u64), ('umask', u64), ('out', u64), ('h', u64), ('d12', u64), ('dfc', u64),
                 ('row_loss', u64), ('partial', u64), ('ext_dout', u64),
-                ('B', i32), ('P', i32), ('D', i32), ('compute_grad', i32), ('loss_scale', f32), ('_pad', i32)]
+                ('B', i32), ('P', i32), ('D', i32), ('compute_grad', i32), ('loss_scale', f32), ('_pad', i32),
+                ('scale', u64)]
 
 
 EVAL_MAX_MODELS, EVAL_MAX_CLASSES = 8, 16   # MEP_EVAL_MAX_* (include/mep.h)

@@ -112,8 +112,7 @@ def cmu_batch(store, pairs, label_dict, lens, device=None):
     prevs = [p for p, _ in pairs]
     curs = [c for _, c in pairs]
     ids = {m: (store.ids(m, prevs), store.ids(m, curs)) for m in MODALITIES}
-    L_l = store.mods['linguistic']['lens'][ids['linguistic'][1]]
-    two = L_l >= lens[0] - 3
+    two = _two_windows(store, ids['linguistic'][1], lens)
     reps = 1 + two.astype(np.int64)
     pair_of_row = np.repeat(np.arange(len(pairs)), reps)
     first_row = np.repeat(np.cumsum(reps) - reps, reps)
@@ -174,23 +173,23 @@ def _device_loader(chunks, build, store, prefetch):
     side = torch.cuda.Stream(store.device) if prefetch else main
 
     def launch(chunk):
-        units, global_rows = chunk
+        units, global_rows, row0 = chunk
         if not units:
-            return None, None, global_rows
+            return None, None, global_rows, row0
         side.wait_stream(main)          # buffers recycled from the caller's stream are free
         with torch.cuda.stream(side):
             out = build(units)
             ev = torch.cuda.Event()
             ev.record(side)
-        return out, ev, global_rows
+        return out, ev, global_rows, row0
 
     nxt = launch(chunks[0]) if chunks else None
     for i in range(len(chunks)):
-        out, ev, global_rows = nxt
+        out, ev, global_rows, row0 = nxt
         if i + 1 < len(chunks):
             nxt = launch(chunks[i + 1])
         if out is None:
-            yield dp.HostShard([], global_rows)
+            yield dp.HostShard([], global_rows, row0)
             continue
         main.wait_event(ev)
         if side is not main:
@@ -198,14 +197,24 @@ def _device_loader(chunks, build, store, prefetch):
                 t.record_stream(main)
         b = DeviceBatch(out)
         b.global_rows = global_rows
+        b.row0 = row0
         yield b
+
+
+def _two_windows(store, cur_ids, lens):
+    """Per pair: does the current text have two windows (cmu-mosei/run.py:172-183)?  A current
+    name missing from the linguistic store (id -1) has no frames: one window."""
+    ids = np.asarray(cur_ids)
+    L = np.where(ids >= 0, store.mods['linguistic']['lens'][np.maximum(ids, 0)], 0)
+    return L >= lens[0] - 3
 
 
 def _cmu_rows(store, pairs, lens):
     """Batch rows of (previous, current) pairs: two when the current text has two windows."""
-    ids = store.ids('linguistic', [c for _, c in pairs])
-    L = np.where(ids >= 0, store.mods['linguistic']['lens'][np.maximum(ids, 0)], 0)
-    return int(len(pairs) + (L >= lens[0] - 3).sum())
+    if not pairs:
+        return 0
+    two = _two_windows(store, store.ids('linguistic', [c for _, c in pairs]), lens)
+    return int(len(pairs) + two.sum())
 
 
 def cmu_data_loader(store, lens, prefetch=True):
@@ -226,7 +235,8 @@ def cmu_data_loader(store, lens, prefetch=True):
         for i in range(0, len(name_list), step):
             g = name_list[i:i + step]
             lo, hi = dp.rank_range(len(g), batch_size)
-            chunks.append((g[lo:hi], _cmu_rows(store, g, lens) if w > 1 else None))
+            chunks.append((g[lo:hi], _cmu_rows(store, g, lens) if w > 1 else None,
+                           _cmu_rows(store, g[:lo], lens) if w > 1 else 0))
         return _device_loader(chunks, lambda pairs: cmu_batch(store, pairs, label_dict, lens), store, prefetch)
 
     return data_loader
@@ -249,7 +259,7 @@ def rf_data_loader(store, labels, lens, prefetch=True):
         for i in range(0, len(name_list), step):
             g = name_list[i:i + step]
             lo, hi = dp.rank_range(len(g), batch_size)
-            chunks.append((g[lo:hi], len(g) if w > 1 else None))
+            chunks.append((g[lo:hi], len(g) if w > 1 else None, lo))
         return _device_loader(chunks, lambda lists: rf_batch(store, lists, labels, lens), store, prefetch)
 
     return data_loader

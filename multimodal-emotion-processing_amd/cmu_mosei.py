@@ -176,7 +176,7 @@ def train(model, iterator, optimizer, device='cuda'):
             continue
         l, v, a, lm, vm, am, label = _to_device(batch, device)
         if engine is not None:
-            loss = engine.step(l, v, a, lm, vm, am, label, global_rows=gr)
+            loss = engine.step(l, v, a, lm, vm, am, label, global_rows=gr, row0=dp.row0_of(batch))
         else:
             optimizer.zero_grad()
             logits = model(l, v, a, lm, vm, am)

@@ -155,6 +155,8 @@ MEP_DEV void epi_fwd_tiles(const mep_epi_desc& d, const AP& wp, const AM& wm, in
     const int ntok = d.ntok;
     const float p = d.drop_p;
     const uint64_t seed = (d.seed && p > 0.f) ? *G<const uint64_t>(d.seed) : 0;
+    // global token offset of this shard's rows (seed[1] = the rank's first global batch row)
+    const uint64_t tok0 = (d.seed && p > 0.f) ? G<const uint64_t>(d.seed)[1] * (uint64_t)d.q.T : 0;
     gfloat* stats = G<float>(d.stats);
     AM wm_x = wm;
     wm_x.pos0 += D;                     // Wm[:, D:], the xp half of the concat
@@ -180,7 +182,7 @@ MEP_DEV void epi_fwd_tiles(const mep_epi_desc& d, const AP& wp, const AM& wm, in
             for (int i = 0; i < NI; ++i)
 #pragma unroll
                 for (int r = 0; r < 4; ++r)
-                    xp[i][r] *= drop_scale(seed, 2u * d.drop_stream, (uint64_t)tok * D + 16 * i + 4 * g + r, p);
+                    xp[i][r] *= drop_scale(seed, 2u * d.drop_stream, (tok0 + (uint64_t)tok) * D + 16 * i + 4 * g + r, p);
         }
         tgemm<NI, KB>(z, wm, [&](int kb) { return qb[kb]; });              // q half of [q | xp]
         tgemm<NI, KB>(z, wm_x, [&](int kb) { return xp[kb]; });            // xp half
@@ -211,7 +213,7 @@ MEP_DEV void epi_fwd_tiles(const mep_epi_desc& d, const AP& wp, const AM& wm, in
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     y[r] = (z[i][r] - mean) * rstd * w[r] + b[r];
-                    if (p > 0.f) y[r] *= drop_scale(seed, 2u * d.drop_stream + 1u, (uint64_t)tok * D + col + r, p);
+                    if (p > 0.f) y[r] *= drop_scale(seed, 2u * d.drop_stream + 1u, (tok0 + (uint64_t)tok) * D + col + r, p);
                 }
                 stg4(zr + col, f4(z[i]));
                 stg4(orow + col, f4(y));
@@ -307,6 +309,8 @@ MEP_DEV void epi_fwd_split(const mep_epi_desc& d, unsigned char* sm, int t_begin
     const int ntok = d.ntok;
     const float p = d.drop_p;
     const uint64_t seed = (d.seed && p > 0.f) ? *G<const uint64_t>(d.seed) : 0;
+    // global token offset of this shard's rows (seed[1] = the rank's first global batch row)
+    const uint64_t tok0 = (d.seed && p > 0.f) ? G<const uint64_t>(d.seed)[1] * (uint64_t)d.q.T : 0;
     gfloat* stats = G<float>(d.stats);
     typedef __attribute__((address_space(3))) unsigned char lbyte;
     const WP wp{(lbyte*)sm, 0};
@@ -340,7 +344,7 @@ MEP_DEV void epi_fwd_split(const mep_epi_desc& d, unsigned char* sm, int t_begin
                 if (p > 0.f) {
 #pragma unroll
                     for (int r = 0; r < 4; ++r)
-                        xp[i][r] *= drop_scale(seed, 2u * d.drop_stream, (uint64_t)tok * D + 16 * i + 4 * g + r, p);
+                        xp[i][r] *= drop_scale(seed, 2u * d.drop_stream, (tok0 + (uint64_t)tok) * D + 16 * i + 4 * g + r, p);
                 }
                 stg4(pr + 16 * i + 4 * g, f4(xp[i]));
             }
@@ -390,7 +394,7 @@ MEP_DEV void epi_fwd_split(const mep_epi_desc& d, unsigned char* sm, int t_begin
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     y[r] = (z[i][r] - mean) * rstd * w[r] + b[r];
-                    if (p > 0.f) y[r] *= drop_scale(seed, 2u * d.drop_stream + 1u, (uint64_t)tok * D + col + r, p);
+                    if (p > 0.f) y[r] *= drop_scale(seed, 2u * d.drop_stream + 1u, (tok0 + (uint64_t)tok) * D + col + r, p);
                 }
                 stg4(zr + col, f4(z[i]));
                 stg4(orow + col, f4(y));
@@ -417,6 +421,8 @@ MEP_DEV void epi_bwd_split(const mep_epi_bwd_desc& bd, unsigned char* sm, int t_
     const int ntok = d.ntok;
     const float p = d.drop_p;
     const uint64_t seed = (d.seed && p > 0.f) ? *G<const uint64_t>(d.seed) : 0;
+    // global token offset of this shard's rows (seed[1] = the rank's first global batch row)
+    const uint64_t tok0 = (d.seed && p > 0.f) ? G<const uint64_t>(d.seed)[1] * (uint64_t)d.q.T : 0;
     const gfloat* stats = G<const float>(d.stats);
     gfloat* lpart = G<float>(bd.ln_partial);
     typedef __attribute__((address_space(3))) unsigned char lbyte;
@@ -464,7 +470,7 @@ MEP_DEV void epi_bwd_split(const mep_epi_bwd_desc& bd, unsigned char* sm, int t_
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 float gg = dz[i][r];
-                if (p > 0.f) gg *= drop_scale(seed, 2u * d.drop_stream + 1u, (uint64_t)tok * D + col + r, p);
+                if (p > 0.f) gg *= drop_scale(seed, 2u * d.drop_stream + 1u, (tok0 + (uint64_t)tok) * D + col + r, p);
                 gg = ok ? gg : 0.f;
                 const float x = (zz[i][r] - mu) * rs;
                 const float gw = gg * w[r];
@@ -507,7 +513,7 @@ MEP_DEV void epi_bwd_split(const mep_epi_bwd_desc& bd, unsigned char* sm, int t_
                 if (p > 0.f) {
 #pragma unroll
                     for (int r = 0; r < 4; ++r)
-                        acc[i][r] *= drop_scale(seed, 2u * d.drop_stream, (uint64_t)tok * D + 16 * i + 4 * g + r, p);
+                        acc[i][r] *= drop_scale(seed, 2u * d.drop_stream, (tok0 + (uint64_t)tok) * D + 16 * i + 4 * g + r, p);
                 }
                 stg4(dzr + 16 * i + 4 * g, f4(dz[i]));
                 stg4(dpr + 16 * i + 4 * g, f4(acc[i]));
@@ -616,6 +622,8 @@ MEP_DEV void epi_bwd_tiles(const mep_epi_bwd_desc& bd, const AM& wmt, const AP& 
     const int ntok = d.ntok;
     const float p = d.drop_p;
     const uint64_t seed = (d.seed && p > 0.f) ? *G<const uint64_t>(d.seed) : 0;
+    // global token offset of this shard's rows (seed[1] = the rank's first global batch row)
+    const uint64_t tok0 = (d.seed && p > 0.f) ? G<const uint64_t>(d.seed)[1] * (uint64_t)d.q.T : 0;
     AM wmt_x = wmt;
     wmt_x.row0 += D;                    // rows D.. of Wm^T = Wm[:, D:]
     const gfloat* stats = G<const float>(d.stats);
@@ -641,7 +649,7 @@ MEP_DEV void epi_bwd_tiles(const mep_epi_bwd_desc& bd, const AM& wmt, const AP& 
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 float gg = a[r];
-                if (p > 0.f) gg *= drop_scale(seed, 2u * d.drop_stream + 1u, (uint64_t)tok * D + col + r, p);
+                if (p > 0.f) gg *= drop_scale(seed, 2u * d.drop_stream + 1u, (tok0 + (uint64_t)tok) * D + col + r, p);
                 gg = ok ? gg : 0.f;
                 const float x = (zz[r] - mean) * rstd;
                 const float gw = gg * w[r];
@@ -682,7 +690,7 @@ MEP_DEV void epi_bwd_tiles(const mep_epi_bwd_desc& bd, const AM& wmt, const AP& 
             for (int i = 0; i < NI; ++i)
 #pragma unroll
                 for (int r = 0; r < 4; ++r)
-                    dxp[i][r] *= drop_scale(seed, 2u * d.drop_stream, (uint64_t)tok * D + 16 * i + 4 * g + r, p);
+                    dxp[i][r] *= drop_scale(seed, 2u * d.drop_stream, (tok0 + (uint64_t)tok) * D + 16 * i + 4 * g + r, p);
         }
         if (ok) {
             gfloat* dzr = row_ptr(bd.dz, tok);

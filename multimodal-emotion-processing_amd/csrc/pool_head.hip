@@ -306,6 +306,11 @@ __global__ __launch_bounds__(256) void k_head(mep_head_desc d) {
                 if (lane < NC) s_dlog[rr][lane] = ext[(r0 + rr) * NC + lane];
             wave_sync();
         }
+        // loss scale and R-Drop divisor: device-resident when d.scale is set (data-parallel
+        // shares replayed from one captured graph)
+        const gfloat* dscale = G<const float>(d.scale);
+        const float loss_scale = dscale ? dscale[0] : d.loss_scale;
+        const int rdrop_pairs = dscale ? (int)dscale[1] : d.rdrop_pairs;
         for (int rr = 0; rr < rows && !ext; ++rr) {
             const int b = r0 + rr;
             const bool ok = lane < NC;
@@ -321,11 +326,11 @@ __global__ __launch_bounds__(256) void k_head(mep_head_desc d) {
             float g = 0.f;
             if (is_neg) g = __expf(x - ln);
             if (is_pos) g = -__expf(-x - lp);
-            if (ok) s_dlog[rr][lane] = g * d.loss_scale;
-            if (lane == 0) row_loss[b] = (ln + lp) * d.loss_scale;
+            if (ok) s_dlog[rr][lane] = g * loss_scale;
+            if (lane == 0) row_loss[b] = (ln + lp) * loss_scale;
         }
         if (d.rdrop && !ext) {
-            const float R = (float)(d.rdrop_pairs > 0 ? d.rdrop_pairs : d.B / 2);   // global pairs under DP
+            const float R = (float)(rdrop_pairs > 0 ? rdrop_pairs : d.B / 2);   // global pairs under DP
             const bool ok = lane < NC;
             const float pv = ok ? s_logit[0][lane] : 0.f, qv = ok ? s_logit[1][lane] : 0.f;
             const float sp = 1.f / (1.f + __expf(-pv)), sq = 1.f / (1.f + __expf(-qv));

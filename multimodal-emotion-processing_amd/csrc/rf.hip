@@ -412,6 +412,7 @@ __global__ __launch_bounds__(64) void k_rf_head(mep_rf_head_desc d) {
         // circle loss (realformer.py:289-298) * utterance mask, mean over B*P
         if (!ext) {
             const bool ok = lane < RF_NC;
+            const float loss_scale = d.scale ? G<const float>(d.scale)[0] : d.loss_scale;
             const float um = (float)G<const int64_t>(d.umask)[r];
             const float t = ok ? (float)G<const int64_t>(d.labels)[(int64_t)r * RF_NC + lane] : 0.f;
             const bool is_pos = ok && t > 0.5f, is_neg = ok && !(t > 0.5f);
@@ -420,11 +421,11 @@ __global__ __launch_bounds__(64) void k_rf_head(mep_rf_head_desc d) {
             const float sn = wave_sum(is_neg ? __expf(vn - mn) : 0.f) + __expf(-mn);
             const float sp = wave_sum(is_pos ? __expf(vp - mp) : 0.f) + __expf(-mp);
             const float ln = mn + logf(sn), lp = mp + logf(sp);
-            loss += (ln + lp) * um * d.loss_scale;
+            loss += (ln + lp) * um * loss_scale;
             float gr = 0.f;
             if (is_neg) gr = __expf(out - ln);
             if (is_pos) gr = -__expf(-out - lp);
-            if (ok) s_dout[i][lane] = gr * um * d.loss_scale;
+            if (ok) s_dout[i][lane] = gr * um * loss_scale;
         } else if (lane < RF_NC) {
             s_dout[i][lane] = ext[(int64_t)r * RF_NC + lane];
         }

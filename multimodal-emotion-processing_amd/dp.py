@@ -50,11 +50,14 @@ def rank_range(n_units, per_rank, r=None):
 
 class HostShard(list):
     """This rank's rows of a host-layout batch (a list of row tuples, as the reference's
-    data_loader yields them); ``global_rows`` = rows of the whole global batch."""
+    data_loader yields them); ``global_rows`` = rows of the whole global batch, ``row0`` = the
+    global index of this share's first row (the dropout masks of row b are those of global row
+    row0 + b, so the ranks together draw exactly the full batch's masks)."""
 
-    def __init__(self, rows, global_rows):
+    def __init__(self, rows, global_rows, row0=0):
         super().__init__(rows)
         self.global_rows = int(global_rows)
+        self.row0 = int(row0)
 
 
 def shard_batches(iterator, unit=1, per_rank=None):
@@ -69,7 +72,7 @@ def shard_batches(iterator, unit=1, per_rank=None):
         units = n // unit
         per = per_rank if per_rank is not None else -(-units // w)
         lo, hi = rank_range(units, per, r)
-        yield HostShard(batch[lo * unit:hi * unit], n)
+        yield HostShard(batch[lo * unit:hi * unit], n, lo * unit)
 
 
 def allreduce_sum(values, device=None):
@@ -85,6 +88,11 @@ def allreduce_sum(values, device=None):
 def global_rows_of(batch):
     """``global_rows`` of a sharded batch, or None (an unsharded, rank-local batch)."""
     return getattr(batch, 'global_rows', None)
+
+
+def row0_of(batch):
+    """Global index of a sharded batch's first row (0 for an unsharded batch)."""
+    return int(getattr(batch, 'row0', 0) or 0)
 
 
 def epoch_mean(local_sum, count, sharded, device=None):

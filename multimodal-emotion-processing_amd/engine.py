@@ -3,7 +3,7 @@ as a fixed launch sequence, captured once per input shape into a hipGraph and re
 
 Data parallelism (one process per GPU, torch.distributed backend "nccl" = RCCL over xGMI): each
 rank runs the step on its own rows; the flat fp32 gradient buffer (2.35 MB for Concat_Trans)
-is all-reduced (SUM) between the backward graph and the optimizer graph, and the optimizer clips
+is all-reduced (SUM) between the backward and the optimizer, and the optimizer clips
 after the reduce, so every rank applies the identical update of the global-batch mean (1-GPU
 large-batch semantics).  Two scalings give that mean:
   * global_rows given (a sharded batch, mep_amd.dp): the rank's loss is scaled by 1/B_global in
@@ -11,23 +11,39 @@ large-batch semantics).  Two scalings give that mean:
   * global_rows None (every rank holds an equal share, e.g. bench.py): the local mean 1/B and
     grad_scale 1/world in the optimizer.
 Ren-MME R-Drop pairs are whole units of a shard (mep_amd.dp), so they never straddle ranks.
-All weight gradients materialise in the backward's last two launches (one grouped weight-
-gradient GEMM and one reduction), so there is no earlier gradient bucket an all-reduce could
-overlap with; the 2.35 MB SUM runs between the two graph replays.
+With the nccl (= RCCL) backend the SUM is captured inside the step's hipGraph between the
+backward and the optimizer (one graph launch per step); with gloo (CPU tests) it is a host call
+between two graph replays.
 """
+import ctypes
+import os
+import warnings
+
 import torch
 import torch.distributed as dist
 
 
 class TrainEngine:
-    def __init__(self, model, optimizer, clip=1.0, rdrop=False, graph=True, process_group=None):
+    def __init__(self, model, optimizer, clip=1.0, rdrop=False, graph=True, process_group=None,
+                 collective=None, capture_allreduce=None):
+        """collective: run the flat-gradient all-reduce (default: when world > 1; True forces it
+        at world 1, e.g. to exercise the RCCL path on one GPU).  capture_allreduce: capture the
+        all-reduce inside the step's hipGraph between the backward and the optimizer (default:
+        with the nccl = RCCL backend; gloo collectives are host calls and are never captured)."""
         self.model = model
         self.opt = optimizer
         self.clip = clip
         self.rdrop = rdrop
         self.graph = graph
         self.pg = process_group
-        self.world = dist.get_world_size(process_group) if dist.is_available() and dist.is_initialized() else 1
+        dist_on = dist.is_available() and dist.is_initialized()
+        self.world = dist.get_world_size(process_group) if dist_on else 1
+        self.collective = (self.world > 1) if collective is None else (bool(collective) and dist_on)
+        backend = dist.get_backend(process_group) if dist_on else None
+        if capture_allreduce is None:
+            env = os.environ.get('MEP_CAPTURE_ALLREDUCE')
+            capture_allreduce = (env != '0') if env is not None else backend == 'nccl'
+        self.capture_allreduce = bool(capture_allreduce) and self.collective and backend == 'nccl'
         self._graphs = {}
         self._initial_broadcast = self.world > 1
 
@@ -53,18 +69,22 @@ class TrainEngine:
             dist.broadcast(runner.flat.buf, 0, group=self.pg)
             self._initial_broadcast = False
 
-    def step_plan(self, plan, global_rows=None):
+    def step_plan(self, plan, global_rows=None, row0=0):
         """Run one training step on the data already in ``plan``'s input buffers; returns the loss
         as a device tensor (the local-batch mean, or with ``global_rows`` this rank's share of
-        the global-batch mean)."""
+        the global-batch mean).  row0: global index of the share's first row (dropout masks)."""
         runner = self._runner(plan.device)
         sharded = self.world > 1 and global_rows is not None
         self.opt._bind()
         self.opt._sync_hyper(self.clip, 1.0 if sharded else 1.0 / self.world)
         plan.set_dropout(runner.drop_p())
-        scale_key = plan.set_global_rows(global_rows if sharded else None)
+        # loss scale and dropout row offset are device-resident: one graph per plan serves every
+        # share size (the head kernel reads them at replay)
+        plan.set_global_rows(global_rows if sharded else None)
+        if plan._drop > 0.0:
+            plan.set_row0(row0 if sharded else 0)
         self._sync_params(runner)
-        key = (id(plan), scale_key)
+        key = id(plan)
         g = self._graphs.get(key)
         if not self.graph:
             self._fwd_bwd(plan)
@@ -77,44 +97,68 @@ class TrainEngine:
             self._allreduce(runner)
             self._opt()
             torch.cuda.synchronize()
-            ga, gb = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
-            with torch.cuda.graph(ga):
-                self._fwd_bwd(plan)
-                if self.world == 1:
-                    self._opt()
-            if self.world > 1:
+            split = self.collective and not self.capture_allreduce
+            ga = None
+            if not split:
+                try:
+                    ga = torch.cuda.CUDAGraph()
+                    with torch.cuda.graph(ga):
+                        self._fwd_bwd(plan)
+                        # RCCL all-reduce captured between the backward and the optimizer: one
+                        # graph launch per step
+                        self._allreduce(runner)
+                        self._opt()
+                except RuntimeError as e:
+                    if not self.collective:
+                        raise
+                    # a collective library that refuses capture: keep it outside the graph
+                    warnings.warn('mep_amd: all-reduce capture failed (%s); running it between two '
+                                  'graph replays' % (str(e).splitlines()[0] if str(e) else type(e).__name__))
+                    torch.cuda.synchronize()
+                    self.capture_allreduce, split, ga = False, True, None
+            if split:
+                ga = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(ga):
+                    self._fwd_bwd(plan)
+            gb = None
+            if split:                 # gloo: host-side collective between two graph replays
+                gb = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(gb):
                     self._opt()
             self._graphs[key] = (ga, gb)
             return plan.loss
         ga, gb = g
         ga.replay()
-        if self.world > 1:
+        if gb is not None:
             self._allreduce(runner)
             gb.replay()
         return plan.loss
 
     def _allreduce(self, runner):
-        if self.world > 1:
+        if self.collective:
             dist.all_reduce(runner.flat.grad, op=dist.ReduceOp.SUM, group=self.pg)
 
-    def step(self, *batch, global_rows=None):
+    def step(self, *batch, global_rows=None, row0=0):
         """Reference-shaped batch in, loss out: the runner copies the batch into the resident
         buffers of the plan for its shape (cmu-mosei / Ren-MME: l, v, a, l_mask, v_mask, a_mask,
         labels; realformer: ... , labels, utterance mask)."""
         first = batch[0][0] if isinstance(batch[0], (tuple, list)) else batch[0]
         plan = self._runner(first.device).stage(*batch)
-        return self.step_plan(plan, global_rows)
+        return self.step_plan(plan, global_rows, row0)
 
     def step_empty(self, device):
         """A rank whose share of the (ragged, last) global batch is empty: zero gradient into the
-        all-reduce, then the same optimizer step as every other rank."""
+        all-reduce, then the same optimizer step as every other rank.  The model's dropout seed
+        advances as in a real step, so the ranks' seed streams stay equal."""
         runner = self._runner(torch.device(device))
         self.opt._bind()
         self.opt._sync_hyper(self.clip, 1.0)
+        if runner.drop_p() > 0.0 and getattr(runner, 'seed_state', None) is not None:
+            from . import _lib
+            _lib.call('mep_seed_advance', ctypes.c_void_p(runner.seed_state.data_ptr()))
         self._sync_params(runner)
         runner.flat.grad.zero_()
-        self._allreduce(runner)
+        self._allreduce(runner)          # eager: an empty share is rare (the ragged last batch)
         self._opt()
         return torch.zeros(1, device=runner.flat.buf.device)
 

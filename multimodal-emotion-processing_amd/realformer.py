@@ -227,7 +227,7 @@ def train(model, iterator, optimizer, device='cuda'):
             continue
         l, v, a, label, lm, vm, am, mask = _to_device(batch, device)
         if engine is not None:
-            loss = engine.step(l, v, a, label, lm, vm, am, mask, global_rows=gr)
+            loss = engine.step(l, v, a, label, lm, vm, am, mask, global_rows=gr, row0=dp.row0_of(batch))
         else:
             optimizer.zero_grad()
             logits = model(l, v, a, lm, vm, am)

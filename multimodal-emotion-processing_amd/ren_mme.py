@@ -192,7 +192,7 @@ def train(model, iterator, optimizer, device='cuda'):
         args, label = cols[:12], cols[12]
         if engine is not None:
             l, v, a, lm, vm, am = _pack(args)
-            loss = engine.step(l, v, a, lm, vm, am, label, global_rows=gr)
+            loss = engine.step(l, v, a, lm, vm, am, label, global_rows=gr, row0=dp.row0_of(batch))
         else:
             optimizer.zero_grad()
             logits = model(*args)

@@ -341,13 +341,17 @@ class RealformerPlan:
             x=crows(self.dfc, 1, D), y=crows(self.dpooled, 1, F), w=fl.ptr(pre + 'fully_connected.weight'),
             bias=0, table=0, ntok=R, N=F, K=D, ldw=F, w_nt=0, accumulate=0, relu=0, alpha=1.0)], dev)
         self.t_fc = cdiv(R, 64)
+        # loss scale read by the head kernel at run time (mep_rf_head_desc.scale): one captured
+        # graph serves every data-parallel share size
+        self.head_scale = torch.full((1,), 1.0 / R, dtype=torch.float32, device=dev)
+        self._head_scale = 1.0 / R
         self.head = RfHeadDesc(fc=self.fc.data_ptr(), ln_w=fl.ptr(pre + 'normalization.weight'),
                                ln_b=fl.ptr(pre + 'normalization.bias'), wc=fl.ptr('classifier.weight'),
                                bc=fl.ptr('classifier.bias'), trans=fl.ptr('trans'), labels=self.labels.data_ptr(),
                                umask=self.umask.data_ptr(), out=self.out.data_ptr(), h=self.h.data_ptr(),
                                d12=self.d12.data_ptr(), dfc=self.dfc.data_ptr(), row_loss=self.row_loss.data_ptr(),
                                partial=self.head_partial.data_ptr(), ext_dout=0, B=self.B, P=self.P, D=D,
-                               compute_grad=1, loss_scale=1.0 / R)
+                               compute_grad=1, loss_scale=1.0 / R, scale=self.head_scale.data_ptr())
 
     def _build_grads(self):
         sp, fl, R, D, FD = self.spec, self.flat, self.R, self.spec.D, self.spec.FD
@@ -409,8 +413,15 @@ class RealformerPlan:
         """Data-parallel share (mep_amd.dp): the masked circle-loss mean over B * P utterance slots
         (others/realformer.py:312) taken over the n global rows (None: the local B)."""
         rows = self.B if n is None else int(n)
-        self.head.loss_scale = 1.0 / (rows * self.P)
+        val = 1.0 / (rows * self.P)
+        if val != self._head_scale:          # a device fill, no host sync
+            self.head_scale.fill_(val)
+            self._head_scale = val
+        self.head.loss_scale = val
         return rows
+
+    def set_row0(self, row0):
+        pass                                 # no dropout on the realformer path
 
     def set_inputs(self, l, v, a, lm, vm, am, labels=None, umask=None):
         """Reference-shaped [B, P, T, d] features / [B, P, T] masks (or [B, T, d] / [B, T] for the

@@ -23,6 +23,10 @@ class ModelRunner:
         self.labels_float = labels_float
         self.flat = FlatParams(model, self.device, no_grad=spec.no_grad_params())
         self.plans = {}
+        # dropout state shared by every plan of this model: {seed, row0}.  One seed stream per
+        # model (not per plan shape), advanced once per training step -- also by an empty
+        # data-parallel share -- so every rank holds the same seed at every step
+        self.seed_state = torch.zeros(2, dtype=torch.int64, device=self.device)
         self._gen = 0
         self._live = None
 
@@ -39,7 +43,8 @@ class ModelRunner:
         key = (int(B),) + tuple(int(t) for t in T) + (bf16,)
         p = self.plans.get(key)
         if p is None:
-            p = TriModalPlan(self.spec, self.flat, key[0], key[1:4], self.device, self.labels_float, bf16=bf16)
+            p = TriModalPlan(self.spec, self.flat, key[0], key[1:4], self.device, self.labels_float, bf16=bf16,
+                             seed_state=self.seed_state)
             self.plans[key] = p
         return p
 
@@ -72,6 +77,7 @@ class ModelRunner:
         p = self.drop_p()
         plan.set_dropout(p)
         if p > 0.0:
+            plan.set_row0(0)
             plan.advance_seed()
         plan.set_inputs(l, v, a, lm, vm, am)
         plan.forward(grad=False)

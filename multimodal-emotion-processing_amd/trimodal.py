@@ -240,7 +240,7 @@ class TriModalSpec:
 
 
 class TriModalPlan:
-    def __init__(self, spec, flat, B, T, device, labels_float=False, bf16=False):
+    def __init__(self, spec, flat, B, T, device, labels_float=False, bf16=False, seed_state=None):
         """bf16: the bf16 path (include/mep.h MEP_PREC_BF16) -- unify, attention, block epilogue and
         weight-gradient products on plain bf16 operands with fp32 accumulation; storage, softmax,
         LayerNorm, pool, head, loss and AdamW in fp32.  Default: the fp32 path (1e-4 parity)."""
@@ -265,7 +265,15 @@ class TriModalPlan:
         self.x_in = {m: torch.zeros(E, B, self.T[m], d, **f32) for m, d in zip(MODS, sp.dims)}
         self.m_in = {m: torch.zeros(B, E, self.T[m], **f32) for m in MODS}
         self.labels = torch.zeros(B, NC, dtype=torch.float32 if labels_float else torch.int64, device=dev)
-        self.seed = torch.zeros(1, dtype=torch.int64, device=dev)
+        # dropout {seed, row0} (include/mep.h mep_epi_desc.seed), usually the runner's shared state
+        self.seed_state = seed_state if seed_state is not None else torch.zeros(2, dtype=torch.int64, device=dev)
+        assert self.seed_state.numel() == 2 and self.seed_state.dtype == torch.int64
+        self.seed = self.seed_state[0:1]
+        self.row0 = self.seed_state[1:2]
+        # {loss_scale, rdrop_pairs} read by the head kernel at run time (mep_head_desc.scale): one
+        # captured graph serves every data-parallel share size
+        self.head_scale = torch.tensor([1.0 / B, 0.0], dtype=torch.float32, device=dev)
+        self._head_scale = (1.0 / B, 0)
         # ---------------- activations
         ntok = {m: B * self.T[m] for m in MODS}
         self.ntok = ntok
@@ -399,7 +407,8 @@ class TriModalPlan:
             logits=self.logits.data_ptr(), row_loss=self.row_loss.data_ptr(),
             partial=self.head_partial.data_ptr(), B=B, F=self.F, NC=NC,
             labels_are_float=int(self.labels_float), rdrop=0, compute_grad=1, loss_scale=1.0 / B, ext_dlogits=0,
-            mean_div=self.Ttot if self.pool_fold else 0)   # the fold reads dmean / T straight from dpooled
+            mean_div=self.Ttot if self.pool_fold else 0,   # the fold reads dmean / T straight from dpooled
+            scale=self.head_scale.data_ptr())
         # backward per layer
         self.d_epib, self.d_attnb, self.t_attnb, self.f_attnb = [], [], [], []
         for i in range(nl):
@@ -468,7 +477,7 @@ class TriModalPlan:
                        wp=fl.ptr(blk['pre'] + 'proj.weight'), wm=fl.ptr(blk['pre'] + 'minus.weight'),
                        ln_w=fl.ptr(blk['pre'] + sp.block_norm + '.weight'),
                        ln_b=fl.ptr(blk['pre'] + sp.block_norm + '.bias'),
-                       stats=blk['estat'].data_ptr(), seed=self.seed.data_ptr(),
+                       stats=blk['estat'].data_ptr(), seed=self.seed_state.data_ptr(),
                        ntok=self.B * Tq, D=D, drop_p=self._drop, drop_stream=stream_id)
 
     def _epi_bwd_desc(self, blk):
@@ -566,12 +575,21 @@ class TriModalPlan:
     def set_global_rows(self, n):
         """Scale the fused loss for a data-parallel share (mep_amd.dp): the circle loss by
         1/n (the rank's part of the global-batch mean) and the R-Drop KL batchmean by n/2 global
-        pairs; None restores the local mean (1/B, B/2).  Returns the key of the scaling (a
-        captured graph holds the head descriptor by value, so the engine keys graphs by it)."""
+        pairs; None restores the local mean (1/B, B/2).  The values live in a device buffer the
+        head kernel reads at run time, so a captured graph replays any share unchanged."""
         rows = self.B if n is None else int(n)
-        self.head.loss_scale = 1.0 / rows
-        self.head.rdrop_pairs = 0 if n is None else rows // 2
+        val = (1.0 / rows, 0 if n is None else rows // 2)
+        if val != self._head_scale:          # two device fills, no host sync
+            self.head_scale[0].fill_(val[0])
+            self.head_scale[1].fill_(float(val[1]))
+            self._head_scale = val
+        self.head.loss_scale, self.head.rdrop_pairs = val
         return rows
+
+    def set_row0(self, row0):
+        """Global index of this batch's first row (data-parallel share): the dropout masks of
+        local row b are the full batch's masks of row row0 + b."""
+        self.row0.fill_(int(row0))          # shared by the model's plans: always written
 
     def set_dropout(self, p):
         """Dropout probability of the block epilogues (Ren-MME DROP at train time, 0 in eval).

@@ -14,7 +14,8 @@ Site numbering (trimodal.py _epi_desc, drop_stream = block index): block j of en
 intensity, 1 = stimulation) with n_layers per chain has index (e * 9 + chain) * n_layers + layer =
 e * 9 * n_layers + (module index in multimodal_blocks); its site 0 is drop(proj(x))
 (Ren-MME/run.py:209), site 1 drop(norm2(minus(.))) (run.py:213); stream = 2 * block + site.
-Element index = token * D + feature, token = b * Tq + t.
+Element index = token * D + feature, token = (row0 + b) * Tq + t, where row0 is the global index
+of a data-parallel share's first row (0 on one GPU): the ranks together draw the full batch's masks.
 """
 import numpy as np
 
@@ -52,7 +53,8 @@ def keep_scale(seed, stream, idx, p):
     return np.where(u >= p32, scale, np.float32(0.0)).astype(np.float32)
 
 
-def block_mask(seed, block, site, B, Tq, D, p):
-    """[B, Tq, D] keep-scale mask of one dropout site of one block."""
-    idx = np.arange(B * Tq * D, dtype=np.uint64)
+def block_mask(seed, block, site, B, Tq, D, p, row0=0):
+    """[B, Tq, D] keep-scale mask of one dropout site of one block (rows row0 .. row0 + B - 1 of
+    the global batch)."""
+    idx = np.arange(row0 * Tq * D, (row0 + B) * Tq * D, dtype=np.uint64)
     return keep_scale(seed, 2 * block + site, idx, p).reshape(B, Tq, D)

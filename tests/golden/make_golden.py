@@ -291,7 +291,7 @@ CASES = {
                                    dict(seed=20, pairs=3, T=[5, 6, 8]), True, 115, 'adamw', drop=(0.1, 20261016)),
     # BASELINE cfg3 shape (B=64, T=50, D=96, H=6) with ragged masks and 'no_name' rows
     'cmu_cfg3': lambda: case_model('cmu_cfg3', 'cmu', CMU_C, cmu_ctor(96, 6, 1),
-                                   dict(seed=17, B=64, T=50, no_name_rows=(0, 13, 40)), False, 112, 'adamw'),
+                                   dict(seed=17, B=64, T=50, no_name_rows=(0, 13, 40)), True, 112, 'adamw'),
     # the reference's own Ren-MME lengths (Ren-MME/run.py:28-30: L_LEN 40, V_LEN 76, A_LEN 275)
     'ren_ref': lambda: case_model('ren_ref', 'ren', REN_C, dict(dim=128, l_len=40, v_len=76, a_len=275,
                                   n_heads=8, n_layers=1, ffn=1),
@@ -299,7 +299,13 @@ CASES = {
     # BASELINE cfg5 shape: T=300 for every modality, d = (768, 640, 205)
     'ren_cfg5': lambda: case_model('ren_cfg5', 'ren', REN_C, dict(dim=128, l_len=300, v_len=300, a_len=300,
                                    n_heads=8, n_layers=1, ffn=1),
-                                   dict(seed=19, pairs=2, T=[300, 300, 300]), False, 114, 'adamw'),
+                                   dict(seed=19, pairs=2, T=[300, 300, 300]), True, 114, 'adamw'),
+    # DROP = 0.1 at Ren-MME's width (D = 128, H = 8) with one modality past 64 steps: the long
+    # (key-chunked) attention path between the dropout sites, every gradient in full
+    'ren_drop_long': lambda: case_model('ren_drop_long', 'ren', dict(REN_C, DROP=0.1),
+                                        dict(dim=128, l_len=8, v_len=12, a_len=80, n_heads=8, n_layers=1, ffn=1),
+                                        dict(seed=22, pairs=2, T=[8, 12, 80]), True, 116, 'adamw',
+                                        drop=(0.1, 20261017)),
     'rf_state_small': lambda: case_model('rf_state_small', 'realformer', rf_consts(6),
                                          dict(l_dim=300, v_dim=35, a_dim=74, dim=32, l_len=6, v_len=6,
                                               a_len=6, n_heads=2, n_layers=2, ffn=2),

@@ -66,7 +66,8 @@ def _shard_worker(rank, world):
     rows = [(n, k) for n in names for k in (0, 1)]
     glob = [rows[i:i + 10] for i in range(0, len(rows), 10)]
     shards = [(list(s), s.global_rows) for s in dp.shard_batches(iter(glob), unit=2)]
-    return dict(order=names, shards=shards)
+    row0s = [s.row0 for s in dp.shard_batches(iter(glob), unit=2)]
+    return dict(order=names, shards=shards, row0s=row0s)
 
 
 def test_shards_world2():
@@ -85,6 +86,9 @@ def test_shards_world2():
     flat = [r for (a, _), (b, _) in zip(s0, s1) for r in list(a) + list(b)]
     assert [tuple(r) for r in flat] == rows
     assert s1[-1][0] == [] or len(s1[-1][0]) < len(s0[-1][0])   # ragged tail: rank 1 has less
+    # row0: global index of each share's first row (rank 1 starts after rank 0's whole share)
+    assert all(r == 0 for r in res[0]['row0s'])
+    assert [r for r in res[1]['row0s']] == [len(a) for (a, _) in s0]
 
 
 # ------------------------------------------------------------------------------ train / run
@@ -93,11 +97,13 @@ class _FakeEngine:
 
     def __init__(self):
         self.calls = []
+        self.row0s = []
 
-    def step(self, *cols, global_rows=None):
+    def step(self, *cols, global_rows=None, row0=0):
         label = cols[6]
         n = global_rows if global_rows is not None else label.shape[0]
         self.calls.append(('step', int(label.shape[0]), global_rows))
+        self.row0s.append(row0)
         return torch.tensor([sum(_row_loss(r) for r in label.tolist()) / n], dtype=torch.float32)
 
     def step_empty(self, device):
@@ -124,7 +130,7 @@ def _train_worker(rank, world):
     model = cmu_mosei.Concat_Trans(32, 5, 5, 5, 2, 1, 1)
     opt = optim.FusedAdamW(model, lr=1e-3)
     loss = cmu_mosei.train(model, dp.shard_batches(iter(glob), per_rank=3), opt, device='cpu')
-    return dict(loss=loss, calls=eng.calls)
+    return dict(loss=loss, calls=eng.calls, row0s=eng.row0s)
 
 
 def test_train_epoch_loss_is_global_world2():
@@ -139,6 +145,7 @@ def test_train_epoch_loss_is_global_world2():
     assert res[1]['calls'][-1][0] == 'empty'
     assert res[0]['calls'][-1] == ('step', 1, 1)
     assert all(c[2] == 6 for c in res[0]['calls'][:-1])
+    assert all(r == 0 for r in res[0]['row0s']) and all(r == 3 for r in res[1]['row0s'])
 
 
 def _run_worker(rank, world, tmp):

@@ -14,9 +14,14 @@ from tests.gpu_util import assert_close, cmu_model, cuda_batch, ren_model
 pytestmark = pytest.mark.gpu
 
 
-def _grads(runner, batch, global_rows):
+def _grads(runner, batch, global_rows, drop=None, row0=0):
+    """drop = (p, seed): the blocks' dropout at probability p with the seed state set to seed and
+    the share's first global row row0 (engine.step_plan's set_row0)."""
     plan = runner.stage(*batch)
-    plan.set_dropout(0.0)
+    plan.set_dropout(0.0 if drop is None else drop[0])
+    if drop is not None:
+        plan.seed.fill_(drop[1])
+        plan.set_row0(row0)
     plan.set_global_rows(global_rows)
     plan.forward(grad=True, rdrop=runner.spec.variant == 'ren')
     plan.backward()
@@ -24,12 +29,14 @@ def _grads(runner, batch, global_rows):
     return runner.flat.grad.clone(), float(plan.loss.item())
 
 
-def _check(runner, full, shares):
-    g_full, l_full = _grads(runner, full, None)
+def _check(runner, full, shares, drop=None):
+    g_full, l_full = _grads(runner, full, None, drop)
     n = full[-1].shape[0]                          # labels: one row per batch row
     g_sum, l_sum = torch.zeros_like(g_full), 0.0
+    row0 = 0
     for s in shares:
-        g, l = _grads(runner, s, n)
+        g, l = _grads(runner, s, n, drop, row0)
+        row0 += s[-1].shape[0]
         g_sum += g
         l_sum += l
     n_grad = runner.flat.n_grad
@@ -71,3 +78,38 @@ def test_dp_shares_sum_to_full_batch_ren(cuda):
         return out
     full = rows(0, 6)                              # the R-Drop KL is far from 0 now
     _check(runner, full, [rows(0, 4), rows(4, 6)])
+    # DROP = 0.1 (Ren-MME/run.py:36): with the shares' global row offsets every rank draws the
+    # full batch's masks, so the SUM of the share gradients is still the full-batch gradient
+    _check(runner, full, [rows(0, 4), rows(4, 6)], drop=(0.1, 987654321))
+    _check(runner, full, [rows(0, 2), rows(2, 4), rows(4, 6)], drop=(0.1, 123456789))
+
+
+def test_dp_dropout_masks_follow_global_rows(cuda):
+    """A share's block outputs equal the full batch's rows row0 .. row0 + n (same seed, DROP = 0.1),
+    and differ from the masks of local row indexing."""
+    from mep_amd import ren_mme
+    meta, _ = fixtures.load('ren_small')
+    model = ren_model(meta, cuda)
+    model.train()
+    runner = model.mep_runner(cuda)
+    inputs, labels = fixtures.batch(meta)
+    packed = list(ren_mme._pack([t.to(cuda) for t in inputs])) + [labels.to(cuda)]
+
+    def rows(lo, hi):
+        return [type(t)(x[lo:hi] for x in t) if isinstance(t, (tuple, list)) else t[lo:hi] for t in packed]
+
+    def xcat(batch, row0):
+        plan = runner.stage(*batch)
+        plan.set_dropout(0.1)
+        plan.seed.fill_(424242)
+        plan.set_row0(row0)
+        plan.forward(grad=False)
+        torch.cuda.synchronize()
+        return [x.clone() for x in plan.Xcat]
+
+    full = xcat(rows(0, 6), 0)
+    share = xcat(rows(2, 6), 2)
+    local = xcat(rows(2, 6), 0)
+    for e in range(2):
+        assert torch.equal(share[e], full[e][2:6]), 'share masks must be the full batch rows 2..5'
+        assert not torch.equal(local[e], full[e][2:6]), 'row0 must change the masks'

@@ -1,0 +1,83 @@
+"""The data-parallel exchange on hardware: a world-1 ``nccl`` (= RCCL) process group
+drives TrainEngine with the flat-gradient all-reduce CAPTURED in the step's hipGraph, between the
+backward and the optimizer.  A SUM over one rank is the identity, so every step must equal the
+no-data-parallel engine's bit for bit -- what this pins is that the RCCL call runs inside the
+replayed graph, on the right buffer, in the right place of the step (before clip + AdamW).
+Reference step: cmu-mosei/run.py:364-369 (backward, clip_grad_norm_, AdamW.step)."""
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+
+from tests.golden import fixtures
+from tests.gpu_util import cmu_model, cuda_batch, ren_model
+
+pytestmark = pytest.mark.gpu
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(('127.0.0.1', 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+@pytest.fixture
+def nccl_world1(cuda):
+    if dist.is_initialized():
+        pytest.skip('a process group already exists')
+    dist.init_process_group('nccl', init_method='tcp://127.0.0.1:%d' % _free_port(), rank=0, world_size=1,
+                            device_id=cuda)
+    try:
+        yield
+    finally:
+        dist.destroy_process_group()
+
+
+def _run(model_fn, batch, steps, collective, rdrop=False, seed=None):
+    from mep_amd.engine import TrainEngine
+    from mep_amd.optim import FusedAdamW
+    model = model_fn()
+    model.train()
+    opt = FusedAdamW(model, lr=1e-3)
+    eng = TrainEngine(model, opt, clip=1.0, rdrop=rdrop, graph=True, collective=collective)
+    if seed is not None:
+        model.mep_runner(batch[0][0].device if isinstance(batch[0], (tuple, list)) else batch[0].device) \
+            .seed_state[0].fill_(seed)
+    losses = [eng.step(*batch).clone() for _ in range(steps)]
+    torch.cuda.synchronize()
+    return eng, model, torch.cat(losses), opt.gnorm.clone()
+
+
+def test_rccl_allreduce_captured_cmu_cfg3(nccl_world1, cuda):
+    """BASELINE cfg3 shape (B = 64, T = 50): one eager step, then graph replays with the captured
+    RCCL all-reduce; equal to the engine without the collective."""
+    meta, _ = fixtures.load('cmu_cfg3')
+    batch = cuda_batch(meta, cuda)
+    e1, m1, l1, g1 = _run(lambda: cmu_model(meta, cuda), batch, 4, collective=True)
+    assert e1.collective and e1.capture_allreduce, 'the RCCL all-reduce was not captured in the graph'
+    assert all(b is None for (_, b) in e1._graphs.values()), 'expected one graph per step'
+    e0, m0, l0, g0 = _run(lambda: cmu_model(meta, cuda), batch, 4, collective=False)
+    assert not e0.collective
+    assert torch.equal(l1, l0), (l1, l0)
+    assert torch.equal(g1, g0)
+    for (k, p1), (_, p0) in zip(m1.named_parameters(), m0.named_parameters()):
+        assert torch.equal(p1, p0), k
+
+
+def test_rccl_allreduce_captured_ren_dropout(nccl_world1, cuda):
+    """Ren-MME at DROP = 0.1 (the seed advances inside the captured graph) through the captured
+    all-reduce, with the R-Drop head."""
+    from mep_amd import ren_mme
+    meta, _ = fixtures.load('ren_drop_long')
+    inputs, labels = fixtures.batch(meta)
+    batch = list(ren_mme._pack([t.to(cuda) for t in inputs])) + [labels.to(cuda)]
+    p = meta['drop']['p']
+    e1, m1, l1, g1 = _run(lambda: ren_model(meta, cuda, drop=p), batch, 3, True, rdrop=True, seed=77)
+    assert e1.capture_allreduce
+    e0, m0, l0, g0 = _run(lambda: ren_model(meta, cuda, drop=p), batch, 3, False, rdrop=True, seed=77)
+    assert torch.equal(l1, l0) and torch.equal(g1, g0)
+    for (k, p1), (_, p0) in zip(m1.named_parameters(), m0.named_parameters()):
+        assert torch.equal(p1, p0), k

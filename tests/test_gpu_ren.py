@@ -101,14 +101,15 @@ def _seed_tensor(v):
     return int(np.array([v], dtype=np.uint64).view(np.int64)[0])
 
 
-def test_base_model_dropout_pinned(cuda):
+@pytest.mark.parametrize('name', ['ren_drop', 'ren_drop_long'])
+def test_base_model_dropout_pinned(name, cuda):
     """DROP = 0.1 pinned against the reference (tests/golden/ren_drop.npz): the reference's
     Base_model ran with each block's nn.Dropout applying the repo's counter-hash masks
     (oracle/dropout.py) of the fixture's seed, so logits, loss and every gradient must match the
     HIP path with the same seed -- mask placement (proj output and block output,
     Ren-MME/run.py:209,213), the 1/(1-p) scale and the gradient routing are all pinned."""
     from mep_amd import ren_mme
-    meta, gold = fixtures.load('ren_drop')
+    meta, gold = fixtures.load(name)
     model = ren_model(meta, cuda, drop=meta['drop']['p'])
     model.train()
     args, labels = _batch(meta, cuda)
@@ -130,14 +131,15 @@ def test_base_model_dropout_pinned(cuda):
 
 
 @pytest.mark.parametrize('graph', [False, True])
-def test_base_model_dropout_engine_step(graph, cuda):
+@pytest.mark.parametrize('name', ['ren_drop', 'ren_drop_long'])
+def test_base_model_dropout_engine_step(name, graph, cuda):
     """The fused engine's training step at DROP = 0.1 (seed advanced once before the forward, as
     every training step does) against the reference step on the same masks: loss, clip norm and
     post-AdamW parameters; then the eval-mode forward (no dropout) of the updated model."""
     from mep_amd import ren_mme
     from mep_amd.engine import TrainEngine
     from mep_amd.optim import FusedAdamW
-    meta, gold = fixtures.load('ren_drop')
+    meta, gold = fixtures.load(name)
     model = ren_model(meta, cuda, drop=meta['drop']['p'])
     model.train()
     opt = FusedAdamW(model, lr=1e-3)

@@ -119,7 +119,7 @@ def _epi(c, d, tag='epi'):
     c.inside(tag + '.ln_w', d.ln_w, d.D * F)
     c.inside(tag + '.ln_b', d.ln_b, d.D * F)
     c.inside(tag + '.stats', d.stats, d.ntok * 2 * F)
-    c.inside(tag + '.seed', d.seed, 8)
+    c.inside(tag + '.seed', d.seed, 16)   # {seed, row0}
 
 
 def _epi_bwd(c, d):
@@ -180,6 +180,8 @@ def _head(c, d, stride, grads):
     c.inside('head.logits', d.logits, B * NC * F)
     c.inside('head.row_loss', d.row_loss, B * F)
     c.inside('head.partial', d.partial, B * stride * F)
+    if d.scale:
+        c.inside('head.scale', d.scale, 2 * F)
     sizes = [NC ** 3, NC, NC, 2 * NC * NC, NC, NC * Fd, NC * Fd, 1]   # mep_head_reduce order
     for i, (gp, n) in enumerate(zip(grads, sizes)):
         c.inside('head_grad%d' % i, int(gp.value if hasattr(gp, 'value') else gp), n * F)
@@ -217,6 +219,8 @@ def _rf_head(c, d):
         c.inside('rf_head.' + name, getattr(d, name), n * F)
     c.inside('rf_head.labels', d.labels, R * 6 * 8)
     c.inside('rf_head.umask', d.umask, R * 8)
+    if d.scale:
+        c.inside('rf_head.scale', d.scale, F)
 
 
 def check_rf_plan(p):
