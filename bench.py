@@ -69,19 +69,22 @@ class LaunchTimer:
 # launch name -> kernel symbol prefix in the rocprofv3 summaries (scripts/parse_prof.py)
 KERNEL_OF = {'mep_attn_bwd': 'k_attn_bwd', 'mep_attn_fwd': 'k_attn_fwd', 'mep_block_epi_fwd': 'k_epi_fwd',
              'mep_block_epi_bwd': 'k_epi_bwd', 'mep_wgrad': 'k_wgrad', 'mep_unify': 'k_unify',
-             'mep_pool_fwd': 'k_pool_fwd', 'mep_pool_bwd': 'k_pool_bwd'}
+             'mep_pool_fwd': 'k_pool_fwd', 'mep_pool_bwd': 'k_pool_bwd', 'mep_gemm': 'k_gemm',
+             'mep_rf_epi_fwd': 'k_rf_epi_fwd', 'mep_rf_epi_bwd': 'k_rf_epi_bwd', 'mep_sum_rows': 'k_sum_rows'}
 
 
-def pmc_traffic(launch):
+def pmc_traffic(launch, tag='cfg3'):
     """(HBM bytes per dispatch, source file) of the kernel behind `launch` from the newest
-    committed PMC pass that measured it (profiles/r<round>_v<n>_pmc.json: (2 FETCH_SIZE +
+    committed PMC pass of this workload that measured it (profiles/r<round>_v<n>_pmc.json for cfg3
+    fp32, profiles/r<round>_v<n>_pmc_<config>[_bf16].json for the others: (2 FETCH_SIZE +
     WRITE_SIZE) x 1024, the gfx950 correction of MI355X_MICROARCH.md section HBM), or (None, None)."""
     def key(f):
         return [int(x) for x in re.findall(r'\d+', os.path.basename(f))]
     prefix = KERNEL_OF.get(launch)
     if prefix is None:
         return None, None
-    for f in sorted(glob.glob(os.path.join(ROOT, 'profiles', 'r*_v*_pmc.json')), key=key, reverse=True):
+    pat = 'r*_v*_pmc.json' if tag == 'cfg3' else 'r*_v*_pmc_%s.json' % tag
+    for f in sorted(glob.glob(os.path.join(ROOT, 'profiles', pat)), key=key, reverse=True):
         for k, v in json.load(open(f)).items():
             if k.startswith(prefix) and 'hbm_bytes_per_dispatch' in v:
                 return int(v['hbm_bytes_per_dispatch']), os.path.relpath(f, ROOT)
@@ -235,10 +238,11 @@ class Cfg5:
         inputs, labels = specs.ren_batch(seed=5, pairs=cls.R // 2, T=cls.TT)
         inputs = [torch.from_numpy(x) for x in inputs]
         labels = torch.from_numpy(labels)
-        n, el = timed_cpu(lambda: oren.train_step(P, opt, inputs, labels, 8, 1), budget_s, max_steps=50)
+        drop = torch.nn.Dropout(0.1).train()      # DROP = 0.1 at both sites of every block, as the GPU step
+        n, el = timed_cpu(lambda: oren.train_step(P, opt, inputs, labels, 8, 1, dropout=drop), budget_s, max_steps=50)
         return dict(value=round(cls.R * n / el, 3), unit='rows/s', n=n, rows=cls.R,
                     sample='%d steps of 32 rows (16 pairs), T=300, Ren-MME Base_model fwd+bwd+KL+clip+AdamW '
-                           '(oracle, fp32 CPU, no dropout)' % n)
+                           '(oracle, fp32 CPU, DROP 0.1)' % n)
 
 
 class Cfg2:
@@ -264,7 +268,8 @@ class Cfg2:
         self.plan = runner.plan(B, 1)
         z = torch.zeros(0, device=dev)
         self.plan.set_inputs(x, z, z, m, z, z)
-        self.plan.dout_chain.copy_((G / G.numel()).reshape(self.plan.dout_chain.shape))   # d mean(out * G) / d out
+        self.G = G.reshape(self.plan.dout_chain.shape)
+        self.plan.dout_chain.copy_(self.G / G.numel())   # d mean(out * G) / d out
         self.opt = _FlatAdam(runner.flat, lr=1e-3)
         self.graph = graph
         self.g = None
@@ -291,7 +296,8 @@ class Cfg2:
         self._body()
 
     def loss(self):
-        return float('nan')
+        """The objective mean(out * G) of the last step's forward."""
+        return float((self.plan.out_chain * self.G).double().mean().item())
 
     def config(self, world, graph):
         return {'workload': 'realformer text encoder fwd+bwd+Adam (Conv1d unify + pos + 2 residual blocks), '
@@ -367,7 +373,7 @@ def roofline_of(work, name, tot, reps, costs):
     flops, nbytes = costs[name]
     rl = roofline.roofline_entry(name, flops / launches_per_step, nbytes / launches_per_step, per_launch_s,
                                  bf16=work.bf16)
-    rl['traffic'], rl['traffic_source'] = pmc_traffic(name) if work.name == 'cfg3' and not work.bf16 else (None, None)
+    rl['traffic'], rl['traffic_source'] = pmc_traffic(name, work.name + ('_bf16' if work.bf16 else ''))
     rl['avg_launch_us'] = round(per_launch_s * 1e6, 2)
     return rl
 

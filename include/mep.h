@@ -164,6 +164,12 @@ typedef struct {
                                     of 64 (max_tiles = ceil(B H ceil(Tq / 16) / 4)); backward: descriptors
                                     with Tk <= 64 also run the workgroup-per-(b, h) kernel, its 4 waves on
                                     separate query tiles (4x the waves of the wave-per-(b, h) kernel) */
+#define MEP_ATTN_KCHUNKS(n) ((n) << 20)  /* backward: n = the largest ceil(Tk / 64) among the launch's
+                                    descriptors with Tk > 64, 2 <= n <= MEP_ATTN_MAX_KCHUNKS: those run the
+                                    chunk-parallel kernel (one workgroup of n waves per (b, h), one wave
+                                    per 64-key chunk, no Tq limit); without it the key-chunk-serial
+                                    kernel with the LDS-carried dQ (MEP_ATTN_DQ_TILES) */
+#define MEP_ATTN_MAX_KCHUNKS 8
 int mep_attn_fwd(const mep_attn_desc* descs, int n_desc, int max_tiles, int flags, mep_stream_t stream);
 
 /* Backward of the attention core.  Inputs dx (grad of X), the forward's q/k/v/x/stats/s_prev.

@@ -267,6 +267,8 @@ PREC_BF16 = 0x10000   # MEP_PREC_BF16: bf16-operand products (attention flags, e
 ATTN_HD32 = 0x20000   # MEP_ATTN_HD32: head dim 32 attention forward (robot_demo)
 ATTN_KV = 0x40000     # MEP_ATTN_KV: backward with k == v and dk == dv on every descriptor
 ATTN_SPLITQ = 0x80000 # MEP_ATTN_SPLITQ: backward, Tk <= 64 descriptors on the workgroup-per-(b, h) kernel
+ATTN_MAX_KCHUNKS = 8  # MEP_ATTN_MAX_KCHUNKS: the chunk-parallel backward (MEP_ATTN_KCHUNKS) up to 512 keys
+ATTN_WIDE = os.environ.get('MEP_ATTN_WIDE', '1') != '0'   # 0: the key-chunk-serial kernel (A/B runs)
 
 
 def attn_fwd_splitq(descs, min_units=1024):
@@ -325,10 +327,15 @@ def attn_bwd_flags(bdescs):
     and dk == dv (the same row view)"""
     same = lambda x, y: (x.ptr, x.sB, x.sT) == (y.ptr, y.sB, y.sT)  # noqa: E731
     kv = bool(bdescs) and all(same(b.f.k, b.f.v) and same(b.dk, b.dv) for b in bdescs)
-    dq_tiles = max([-(-b.f.Tq // 16) for b in bdescs if b.f.Tk > 64] or [0])
+    # Tk > 64: the chunk-parallel kernel (one wave per 64-key chunk, MEP_ATTN_KCHUNKS) up to
+    # 64 * ATTN_MAX_KCHUNKS keys, else the key-chunk-serial kernel with the LDS-carried dQ
+    kchunks = max([-(-b.f.Tk // 64) for b in bdescs if b.f.Tk > 64] or [0])
+    wide = ATTN_WIDE and 2 <= kchunks <= ATTN_MAX_KCHUNKS
+    dq_tiles = 0 if wide else max([-(-b.f.Tq // 16) for b in bdescs if b.f.Tk > 64] or [0])
     assert dq_tiles <= ATTN_MAX_DQ_TILES, 'mep_attn_bwd: Tq > %d with Tk > 64 exceeds the LDS' % (16 * ATTN_MAX_DQ_TILES)
     return (ATTN_PREV if _uniform([b.f.s_prev != 0 for b in bdescs], 's_prev') else 0) | \
            (ATTN_SOUT if _uniform([b.ds_next != 0 for b in bdescs], 'ds_next') else 0) | (dq_tiles << 8) | \
+           ((kchunks << 20) if wide else 0) | \
            (ATTN_SHORT if any(b.f.Tk <= 64 for b in bdescs) else 0) | (ATTN_LONG if any(b.f.Tk > 64 for b in bdescs) else 0) | \
            (ATTN_KV if kv else 0)
 

@@ -61,6 +61,9 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 #ifndef MEP_BWD_WAVES_KV
 #define MEP_BWD_WAVES_KV 4 // waves per SIMD of the short backward with MEP_ATTN_KV (<= 128 registers)
 #endif
+#ifndef MEP_FWD_PVSPLIT
+#define MEP_FWD_PVSPLIT 0  // forward P.V on 2-part bf16 splits (16x16x32) instead of f32 MFMA
+#endif
 #ifndef MEP_FWD_WAVES
 #define MEP_FWD_WAVES 3    // waves per SIMD of the short, non-residual forward
 #endif
@@ -143,6 +146,9 @@ MEP_DEV floatx4 dot_score(const S3& p, const S3& u, floatx4 acc) {
 
 #ifndef MEP_BWD_MF16
 #define MEP_BWD_MF16 1   // backward 2-way products as separate 16x16x16 MFMAs (no operand assembly)
+#endif
+#ifndef MEP_BWD_STACK
+#define MEP_BWD_STACK 0  // KV backward: P^T dO + dS^T Q/4 as one 32-deep contraction on 16x16x32 MFMAs
 #endif
 #ifndef MEP_BWD_DVF32
 #define MEP_BWD_DVF32 0  // dV += P^T dO on f32 MFMA from the raw P / dO (no split): 48.6 vs 45.5 us, off
@@ -427,14 +433,31 @@ MEP_DEV void attn_fwd_task(const mep_attn_desc& d, int qc, int h, int b, int lan
                     for (int hb = 0; hb < NHB; ++hb) oq[hb] = mfma(pb, vbf[kt / 2][hb], oq[hb]);
                     continue;
                 }
-                // fp32 MFMA on the raw P and V (exact fp32 fma chain): a bf16 split of P would need
-                // three parts for fp32-level logits, and its VALU cost more than these 8 MFMAs
+#if MEP_FWD_PVSPLIT
+                // P and V as 2-part bf16 splits, products p0 v0 + p1 v0 + p0 v1 on three 16x16x32
+                // MFMAs per key-tile pair (slots 0-3: tile kt, 4-7: tile kt + 1): relative error
+                // <= ~2^-16 per product, 48 MFMA cycles instead of 8 f32 MFMAs
+                {
+                    const S2 pa = split2(sv[kt]), pb = split2(sv[kt + 1]);
+                    const bf16x8 p0 = op(pa.h0, pa.h1, pb.h0, pb.h1), p1 = op(pa.l0, pa.l1, pb.l0, pb.l1);
+#pragma unroll
+                    for (int hb = 0; hb < NHB; ++hb) {
+                        const S2 va = split2(vf[kt][hb]), vb = split2(vf[kt + 1][hb]);
+                        const bf16x8 v0 = op(va.h0, va.h1, vb.h0, vb.h1);
+                        oq[hb] = mfma(p0, v0, oq[hb]);
+                        oq[hb] = mfma(p1, v0, oq[hb]);
+                        oq[hb] = mfma(p0, op(va.l0, va.l1, vb.l0, vb.l1), oq[hb]);
+                    }
+                }
+#else
+                // fp32 MFMA on the raw P and V (exact fp32 fma chain)
 #pragma unroll
                 for (int k2 = 0; k2 < 2; ++k2)
 #pragma unroll
                     for (int s = 0; s < 4; ++s)
 #pragma unroll
                         for (int hb = 0; hb < NHB; ++hb) oq[hb] = mfma16x4(sv[kt + k2][s], vf[kt + k2][hb][s], oq[hb]);
+#endif
             }
             if (SINGLE) {
                 finish(qt, oq, mnew, lsum);
@@ -689,7 +712,17 @@ struct Bwd {
                 dsv[r] = gsv;
             }
             const S2 ds2 = split2(dsv);
-            if (KV) {                                    // dKV[key][dim] += P^T dO + dS^T Q / 4
+            if (KV && !BF && MEP_BWD_STACK) {
+                // dKV[key][dim] += P^T dO + dS^T Q / 4 as ONE 32-deep contraction [P | dS] . [dO ; Q/4]
+                // (slots 0-3: P / dO of queries 4g..4g+3, slots 4-7: dS / Q/4 of the same queries),
+                // products x0 y0 + x1 y0 + x0 y1 of both terms on three 16x16x32 MFMAs
+                const S2 ps = split2(p);
+                const bf16x8 a0 = op(ps.h0, ps.h1, ds2.h0, ds2.h1), a1 = op(ps.l0, ps.l1, ds2.l0, ds2.l1);
+                const bf16x8 b0 = op(db2.h0, db2.h1, qb2.h0, qb2.h1), b1 = op(db2.l0, db2.l1, qb2.l0, qb2.l1);
+                dk[kt] = mfma(a0, b0, dk[kt]);
+                dk[kt] = mfma(a1, b0, dk[kt]);
+                dk[kt] = mfma(a0, b1, dk[kt]);
+            } else if (KV) {                             // dKV[key][dim] += P^T dO + dS^T Q / 4
                 dk[kt] = dot16<BF>(split2(p), db2, dk[kt]);
             } else if (MEP_BWD_DVF32 && !BF) {           // dV[key][dim] += P^T dO, exact fp32
 #pragma unroll
@@ -697,7 +730,7 @@ struct Bwd {
             } else {
                 dv[kt] = dot16<BF>(split2(p), db2, dv[kt]);
             }
-            dk[kt] = dot16<BF>(ds2, qb2, dk[kt]);        // dK[key][dim] += dS^T Q
+            if (!(KV && !BF && MEP_BWD_STACK)) dk[kt] = dot16<BF>(ds2, qb2, dk[kt]);   // dK[key][dim] += dS^T Q
 #if MEP_BWD_TR
             // the split dS as packed words into [key][16 queries] images (one 8-byte store per
             // part: this lane's queries 4g .. 4g+3 of key kt*16 + c)
@@ -871,7 +904,8 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(2))) vo
     const mep_attn_bwd_desc& bd = descs[blockIdx.y];
     const mep_attn_desc& d = bd.f;
     const int bh = blockIdx.x;
-    if ((d.Tk <= CH && !splitq) || bh >= d.B * d.H) return;   // a SHORT descriptor / past the end: the whole workgroup
+    // splitq bit 0: SHORT descriptors run here too; bit 1: LONG ones ran on the wide kernel
+    if ((d.Tk <= CH && !(splitq & 1)) || (d.Tk > CH && (splitq & 2)) || bh >= d.B * d.H) return;   // the whole workgroup
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     Bwd<PREV, DSN, BF> u(bd, bh / d.H, bh % d.H, lane);
     const int D = d.H * HD;
@@ -931,6 +965,96 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(2))) vo
                 G<float>(bd.dc_partial)[bh * nkc + kc] = ((DC[0] + DC[1]) + DC[2]) + DC[3];
         }
         __syncthreads();                      // R read before the next chunk's transposes
+    }
+}
+
+// WIDE (64 < Tk <= 64 * MEP_ATTN_MAX_KCHUNKS): one WORKGROUP per (b, h) and one WAVE per 64-key
+// chunk (blockDim = 64 x the launch's largest chunk count).  A wave keeps its chunk's K / V rows
+// and its dK / dV accumulators in registers for the whole kernel and walks every query tile, so
+// dK / dV need no cross-wave sum and are stored once from registers.  The query tiles are walked
+// in lockstep: tile qt + 1's Q, dO, O, dQ rows and row statistics are staged once per workgroup
+// by LDS-DMA (one wave issues it, double-buffered) while tile qt computes; after tile qt each wave
+// leaves its 16 x 16 dQ partial in an LDS slot and one wave sums the slots in chunk order
+// (fixed order: deterministic) onto the incoming dQ rows.  One barrier per query tile.
+// LDS: [2][STG] staging | [2][waves][256] dQ slots | [waves][TFL] dS transposes.
+template <bool PREV, bool DSN, bool BF, bool KV>
+__global__ __launch_bounds__(64 * MEP_ATTN_MAX_KCHUNKS) __attribute__((amdgpu_waves_per_eu(bwd_short_waves<PREV, DSN, KV>())))
+void k_attn_bwd_wide(const mep_attn_bwd_desc* __restrict__ descs) {
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    typedef Bwd<PREV, DSN, BF, KV> U;
+    const mep_attn_bwd_desc& bd = descs[blockIdx.y];
+    const mep_attn_desc& d = bd.f;
+    const int bh = blockIdx.x;
+    if (d.Tk <= CH || bh >= d.B * d.H) return;   // a SHORT descriptor / past the end: the whole workgroup
+    const int nwv = blockDim.x >> 6;             // waves = the launch's largest chunk count
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int nkc = (d.Tk + CH - 1) / CH;        // <= nwv (host)
+    const int D = d.H * HD;
+    float* Stg = lds;
+    float* Slot = lds + 2 * U::STG;
+    float* Tr = Slot + 2 * nwv * 256 + wave * TFL;
+    U u(bd, bh / d.H, bh % d.H, lane);
+    const int nqt = (u.Tq + 15) / 16;
+    const bool same_out = bd.dk.ptr == bd.dv.ptr && bd.dk.sB == bd.dv.sB && bd.dk.sT == bd.dv.sT;
+    if (KV && !(u.same_kv && same_out)) {        // broken MEP_ATTN_KV promise: NaN dq rows, loudly
+        if (wave == 0)
+            for (int qt = 0; qt < nqt; ++qt) {
+                const int od = u.dQb.at(qt * 16 + 4 * u.g, u.hc + u.c);
+#pragma unroll
+                for (int r = 0; r < 4; ++r) u.dQb.st1(od, r * u.dQb.sT4, __builtin_nanf(""));
+            }
+        return;                                   // descriptor-uniform: every wave leaves here
+    }
+    const bool active = wave < nkc;
+    const bool dma = u.dma_ok();
+    // rows past Tq receive no DMA data: start from zeros (later finite rows of earlier tiles)
+    for (int e = threadIdx.x; e < 2 * U::STG / 4; e += blockDim.x)
+        reinterpret_cast<f32x4*>(Stg)[e] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (active) u.load_chunk(wave);
+    __syncthreads();
+    if (dma && wave == 0) {
+        u.stage(0, Stg);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+    for (int qt = 0; qt < nqt; ++qt) {
+        typename U::QIn in;
+        if (dma) u.read_staged(in, Stg + (qt & 1) * U::STG);
+        else u.fetch(in, qt);
+        // the other staging buffer held tile qt - 1, read by every wave before the last barrier
+        const int iw = (qt + 1) % nwv;
+        if (dma && wave == iw && qt + 1 < nqt) u.stage(qt + 1, Stg + ((qt + 1) & 1) * U::STG);
+        floatx4 dq = zero4();
+        if (active) dq = u.tile(in, qt, Tr);
+        reinterpret_cast<floatx4*>(Slot + ((qt & 1) * nwv + wave) * 256)[lane] = dq;
+        if (dma && wave == iw) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // tile qt + 1 landed
+        __syncthreads();
+        if (wave == qt % nwv) {                   // chunk-ordered sum onto the incoming dq rows
+            const floatx4* sl = reinterpret_cast<const floatx4*>(Slot + (qt & 1) * nwv * 256) + lane;
+            floatx4 tot = sl[0];
+            for (int w = 1; w < nkc; ++w) tot += sl[w * 64];
+            u.store_dq_rows(in.dqo, qt, tot);
+        }
+    }
+    if (!active) return;
+    const BRow dKb = brow(bd.dk, u.b, u.Tk, D), dVb = brow(bd.dv, u.b, u.Tk, D);   // keys past Tk: dropped
+    const int ok_ = dKb.at(u.k_lo + 4 * u.g, u.hc + u.c), ov_ = dVb.at(u.k_lo + 4 * u.g, u.hc + u.c);
+#pragma unroll
+    for (int kt = 0; kt < NT; ++kt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            if (KV) {
+                dKb.st1(ok_, (16 * kt + r) * dKb.sT4, u.dk[kt][r]);
+            } else if (same_out) {
+                dKb.st1(ok_, (16 * kt + r) * dKb.sT4, u.dk[kt][r] * INV_SCALE + u.dv[kt][r]);
+            } else {
+                dKb.st1(ok_, (16 * kt + r) * dKb.sT4, u.dk[kt][r] * INV_SCALE);
+                dVb.st1(ov_, (16 * kt + r) * dVb.sT4, u.dv[kt][r]);
+            }
+        }
+    if (PREV && bd.dc_partial) {
+        const float w = wave_sum(u.dc_acc);
+        if (lane == 0) G<float>(bd.dc_partial)[bh * nkc + wave] = w;
     }
 }
 
@@ -1008,7 +1132,22 @@ extern "C" int mep_attn_bwd(const mep_attn_bwd_desc* descs, int n_desc, int max_
 #undef MEP_BS
 #undef MEP_BS2
     }
-    if ((flags & MEP_ATTN_LONG) || splitq) {
+    const int kchunks = (flags >> 20) & 0xf;   // MEP_ATTN_KCHUNKS: the wide kernel for the LONG descriptors
+    if ((flags & MEP_ATTN_LONG) && kchunks >= 2) {
+        if (kchunks > MEP_ATTN_MAX_KCHUNKS) { mep_set_error("mep_attn_bwd: MEP_ATTN_KCHUNKS above MEP_ATTN_MAX_KCHUNKS"); return MEP_EINVAL; }
+        const size_t wl = sizeof(float) * (2 * (size_t)Bwd<false, false, false>::STG + (size_t)kchunks * (2 * 256 + TFL));
+        const dim3 grid(max_tiles, n_desc), block(64 * kchunks);
+#define MEP_BW2(P, S, K) \
+    do { if (bf) hipLaunchKernelGGL((k_attn_bwd_wide<P, S, true, K>), grid, block, wl, st, descs); \
+         else hipLaunchKernelGGL((k_attn_bwd_wide<P, S, false, K>), grid, block, wl, st, descs); } while (0)
+#define MEP_BW(P, S) do { if (kv) MEP_BW2(P, S, true); else MEP_BW2(P, S, false); } while (0)
+        if (prev) { if (dsn) MEP_BW(true, true); else MEP_BW(true, false); }
+        else      { if (dsn) MEP_BW(false, true); else MEP_BW(false, false); }
+#undef MEP_BW
+#undef MEP_BW2
+    }
+    if (((flags & MEP_ATTN_LONG) && kchunks < 2) || splitq) {
+        const int mode = (splitq ? 1 : 0) | ((flags & MEP_ATTN_LONG) && kchunks >= 2 ? 2 : 0);
         static bool lds_attr = false;   // allow more than 64 KB of dynamic LDS (long Tq)
         if (!lds_attr) {
             const int mx = 160 * 1024;
@@ -1021,8 +1160,8 @@ extern "C" int mep_attn_bwd(const mep_attn_bwd_desc* descs, int n_desc, int max_
         }
         const dim3 grid(max_tiles, n_desc), block(THREADS);
 #define MEP_BL(P, S) \
-    do { if (bf) hipLaunchKernelGGL((k_attn_bwd_long<P, S, true>), grid, block, lds, st, descs, (int)splitq); \
-         else hipLaunchKernelGGL((k_attn_bwd_long<P, S, false>), grid, block, lds, st, descs, (int)splitq); } while (0)
+    do { if (bf) hipLaunchKernelGGL((k_attn_bwd_long<P, S, true>), grid, block, lds, st, descs, mode); \
+         else hipLaunchKernelGGL((k_attn_bwd_long<P, S, false>), grid, block, lds, st, descs, mode); } while (0)
         if (prev) { if (dsn) MEP_BL(true, true); else MEP_BL(true, false); }
         else      { if (dsn) MEP_BL(false, true); else MEP_BL(false, false); }
 #undef MEP_BL

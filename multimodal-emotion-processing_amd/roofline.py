@@ -9,17 +9,24 @@ Per attention-block instance (batch row b, block j), with n_kv = 1 (k is v):
 Peaks (MI355X_MICROARCH.md): HBM 8.0 TB/s; fp32 MFMA (= vector rate) 157.3 TFLOP/s; bf16 MFMA
 2.5 PFLOP/s dense.  Kernels whose fp32 products run as bf16 parts (split.h) are priced against the
 bf16 peak divided by the bf16 products per fp32 product: the block epilogues and the weight
-gradients (six products) at 2.5 P / 6 = 417 TFLOP/s of fp32 work.  The attention kernels mix fp32
-MFMA (forward P.V) and split products and are priced at the fp32 MFMA peak (they are HBM-bound at
-every benched shape).  bf16 path (MEP_PREC_BF16): one bf16 product per product, every matrix
-kernel priced at the bf16 peak; the bytes are the same (fp32 storage).
+gradients (six products) at 2.5 P / 6 = 417 TFLOP/s of fp32 work; the attention forward (six-product
+scores, f32-MFMA P.V) at 228 TFLOP/s, the attention backward (four products for S, dP, dV, dK,
+three for dQ) at 658 TFLOP/s.  The realformer token GEMMs and epilogues run on f32 MFMA (157 TF).
+bf16 path (MEP_PREC_BF16): one bf16 product per product, every matrix kernel priced at the bf16
+peak; the bytes are the same (fp32 storage).
 """
 from .trimodal import MODS
 
 HBM_PEAK = 8.0e12
 F32_PEAK = 157.3e12
 BF16_PEAK = 2.5e15
-COMPUTE_PEAK = {'mep_block_epi_fwd': BF16_PEAK / 6, 'mep_block_epi_bwd': BF16_PEAK / 6, 'mep_wgrad': BF16_PEAK / 6}
+# fp32 path: the attention forward's scores take six bf16 products (3-part split) and its P.V runs
+# on f32 MFMA; the backward's S, dP, dV, dK take four products (2-part split) and dQ three
+# (csrc/attn.hip): ideal time per 2*Tq*Tk*D-flop contraction at the bf16 peak / products
+ATTN_FWD_PEAK = 4.0 / (12.0 / BF16_PEAK + 2.0 / F32_PEAK)
+ATTN_BWD_PEAK = 10.0 / (2.0 * (4 + 4 + 4 + 4 + 3) / BF16_PEAK)
+COMPUTE_PEAK = {'mep_block_epi_fwd': BF16_PEAK / 6, 'mep_block_epi_bwd': BF16_PEAK / 6, 'mep_wgrad': BF16_PEAK / 6,
+                'mep_attn_fwd': ATTN_FWD_PEAK, 'mep_attn_bwd': ATTN_BWD_PEAK}
 
 
 def launch_costs(plan):
@@ -66,17 +73,30 @@ def launch_costs(plan):
 
 
 def rf_launch_costs(plan):
-    """Attention launches of a realformer plan (RealformerPlan): K and V separately projected
-    (n_kv = 2), the residual scores carried between the chain's layers."""
+    """Every priced launch of a realformer plan (RealformerPlan, others/realformer.py:133-318): the
+    token GEMMs (Conv1d unify + position table, w_qkv, the backward's input-gradient products),
+    attention (K and V separately projected: n_kv = 2, residual scores carried between the chain's
+    layers), the fused RealFormer epilogue (proj, ReZero residual, LN1, FFN, LN2) forward and
+    backward, the weight gradients and the per-modality gradient sums."""
     sp, R = plan.spec, plan.R
-    D, H = sp.D, sp.H
+    D, H, FD = sp.D, sp.H, sp.FD
     out = {}
 
     def add(name, f, b):
         f0, b0 = out.get(name, (0, 0))
         out[name] = (f0 + f, b0 + b)
+
+    def gemm(name, ntok, N, K, accumulate=False, table=0):
+        add(name, 2 * ntok * N * K, 4 * (ntok * K + ntok * N * (2 if accumulate else 1) + N * K + table))
+
+    for m in sp.mods:                                          # unify + position table
+        gemm('mep_gemm', plan.ntok[m], D, sp.dims[m], table=plan.T[m] * D)
     for blk in plan.blocks:
-        Tq, Tk = blk['Tq'], blk['Tk']
+        Tq, Tk, nq, nk = blk['Tq'], blk['Tk'], blk['nq'], blk['nk']
+        gemm('mep_gemm', nk, 2 * D, D)                         # [K | V] = U [W_k; W_v]^T
+        gemm('mep_gemm', nq, D, D)                             # Q = q W_q^T
+        gemm('mep_gemm', nq, D, D, accumulate=True)            # dq_in += dQ W_q
+        gemm('mep_gemm', nk, D, 2 * D)                         # dkv_in = [dK | dV] [W_k; W_v]
         r_in = 1 if blk['i'] > 0 else 0
         r_out = 1 if 'S' in blk else 0
         s_bytes = 4 * H * Tq * Tk
@@ -85,6 +105,19 @@ def rf_launch_costs(plan):
         chained = s_bytes * ((1 if r_out else 0) + (1 if r_in else 0) * 2)
         add('mep_attn_bwd', R * 10 * Tq * Tk * D,
             R * (4 * (5 * Tq * D + 4 * Tk * D) + 4 * Tk + 8 * H * Tq + chained))
+        w = 4 * (D * D + 2 * D * FD + 2 * D + FD + 4 * D)      # Wp, W1, W2, biases, LN weights
+        # forward: reads q, x; writes xp, h, f1, f, out and 4 stats per token
+        add('mep_rf_epi_fwd', 2 * nq * (D * D + 2 * D * FD), 4 * nq * (7 * D + FD + 4) + w)
+        # backward: reads dout, h, f, f1, q, xp, stats; writes df, df1, dxp, dx, dq
+        add('mep_rf_epi_bwd', 2 * nq * (D * D + 2 * D * FD), 4 * nq * (10 * D + 2 * FD + 4) + w)
+        # weight gradients: W_q, [W_k; W_v], Wp, W1, W2
+        for (n, N, K) in ((nq, D, D), (nk, D, 2 * D), (nq, D, D), (nq, D, FD), (nq, D, FD)):
+            add('mep_wgrad', 2 * n * N * K, 4 * n * (N + K))
+    for m in sp.mods:
+        n = plan.ntok[m]
+        add('mep_wgrad', 2 * n * D * sp.dims[m], 4 * n * (D + sp.dims[m]))
+        srcs = sum(1 for (qm, km) in sp.chains if qm == m) + sum(sp.nl for (qm, km) in sp.chains if km == m)
+        add('mep_sum_rows', srcs * n * D, 4 * n * D * (srcs + 1))
     return out
 
 

@@ -23,22 +23,25 @@ def main():
     ap.add_argument('--reps', type=int, default=50)
     ap.add_argument('--layers', type=int, default=1)
     ap.add_argument('--T', type=int, default=50)
+    ap.add_argument('--config', default='cfg3', choices=('cfg3', 'cfg5'))
+    ap.add_argument('--dtype', default='fp32', choices=('fp32', 'bf16'))
     args = ap.parse_args()
     import bench
     from mep_amd._lib import launch
     dev = torch.device('cuda:0')
     bench.T, bench.NL = args.T, args.layers
-    work = bench.Cfg3(dev, 0, graph=False)
+    work = bench.CONFIGS[args.config](dev, 0, graph=False, bf16=args.dtype == 'bf16')
     work.eager_step()
     torch.cuda.synchronize()
     p = work.plan
     D = p.spec.D
+    pr = p.prec
     table = {
         'mep_unify': lambda: launch('mep_unify', p.d_unify, p.t_unify),
-        'mep_attn_fwd': lambda: launch('mep_attn_fwd', p.d_attn[0], p.t_attn[0], threads=p.g_attn[0][2]),
-        'mep_block_epi_fwd': lambda: launch('mep_block_epi_fwd', p.d_epi[0], p.t_epi[0], threads=D),
-        'mep_block_epi_bwd': lambda: launch('mep_block_epi_bwd', p.d_epib[0], p.t_epi[0], threads=D),
-        'mep_attn_bwd': lambda: launch('mep_attn_bwd', p.d_attnb[0], p.t_attnb[0], threads=p.f_attnb[0]),
+        'mep_attn_fwd': lambda: launch('mep_attn_fwd', p.d_attn[0], p.t_attn[0], threads=p.g_attn[0][2] | pr),
+        'mep_block_epi_fwd': lambda: launch('mep_block_epi_fwd', p.d_epi[0], p.t_epi[0], threads=D | pr),
+        'mep_block_epi_bwd': lambda: launch('mep_block_epi_bwd', p.d_epib[0], p.t_epi[0], threads=D | pr),
+        'mep_attn_bwd': lambda: launch('mep_attn_bwd', p.d_attnb[0], p.t_attnb[0], threads=p.f_attnb[0] | pr),
         'mep_wgrad': lambda: launch('mep_wgrad', p.d_wgrad, p.t_wgrad),
         'mep_pool_fwd': lambda: launch('mep_pool_fwd', p.d_pool, p.t_pool),
     }

@@ -2,9 +2,9 @@
 # GPU-box inner loop: gpu tests (stop on failure), then per-kernel timings of the bench workload.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
-timeout -k 10 400 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 120 --timeout-method thread ${PYTEST_ARGS} > gpurun_out/pt.log 2>&1
+timeout -k 10 700 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 120 --timeout-method thread ${PYTEST_ARGS} > gpurun_out/pt.log 2>&1
 rc=$?; tail -n 30 gpurun_out/pt.log | grep -v "amdgpu.ids"; echo "pytest rc=$rc"
 case $rc in 124|134|137|139) exit $rc;; esac
-timeout -k 10 150 python scripts/kbench.py --reps 50 2>&1 | grep -v amdgpu.ids
+true
 [ -n "$BENCH" ] && timeout -k 10 300 python bench.py --steps 100 --warmup 10 --no-cpu-baseline 2>&1 | grep -v amdgpu.ids
 exit $rc
