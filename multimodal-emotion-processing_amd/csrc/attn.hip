@@ -113,6 +113,14 @@ MEP_DEV S3 split3(const float* x) {
     return s;
 }
 
+// hi parts of two 4-vectors as one operand quad {x0 x1 | x2 x3 | y0 y1 | y2 y3}, and the lo parts
+MEP_DEV u32x4 split_hi(const float* x, const float* y) {
+    return u32x4{pk(x[0], x[1]), pk(x[2], x[3]), pk(y[0], y[1]), pk(y[2], y[3])};
+}
+MEP_DEV u32x4 split_lo(const float* x, const float* y, const u32x4& h) {
+    return u32x4{pk(x[0] - bf_lo(h[0]), x[1] - bf_hi(h[0])), pk(x[2] - bf_lo(h[1]), x[3] - bf_hi(h[1])),
+                 pk(y[0] - bf_lo(h[2]), y[1] - bf_hi(h[2])), pk(y[2] - bf_lo(h[3]), y[3] - bf_hi(h[3]))};
+}
 MEP_DEV bf16x8 op(unsigned w0, unsigned w1, unsigned w2, unsigned w3) {
     return __builtin_bit_cast(bf16x8, u32x4{w0, w1, w2, w3});
 }
@@ -182,9 +190,12 @@ MEP_DEV floatx4 dot16(const S2& x, const S2& y, floatx4 acc) {
 
 // 32-deep contraction over two 16-row tiles (slots 0-3: tile 0, 4-7: tile 1), 2-way split,
 // products x0 y0 + x1 y0 + x0 y1 (BF: x0 y0); MEP_BWD_MF16: per tile on 16x16x16
+#ifndef MEP_BWD_MF16_DQ
+#define MEP_BWD_MF16_DQ MEP_BWD_MF16   // dQ's 32-deep contraction on 16x16x16 (1) or 16x16x32 (0)
+#endif
 template <bool BF>
 MEP_DEV floatx4 dot32(const S2& xa, const S2& xb, const S2& ya, const S2& yb, floatx4 acc) {
-#if MEP_BWD_MF16
+#if MEP_BWD_MF16_DQ
     if (!BF) {
         acc = mfma16(op4(xa.h0, xa.h1), op4(ya.h0, ya.h1), acc);
         acc = mfma16(op4(xa.l0, xa.l1), op4(ya.h0, ya.h1), acc);
@@ -655,7 +666,9 @@ struct Bwd {
         }
         const S2 qs = split2(in.qa), do2 = split2(in.da);
         S2 qb2;
-        if (KV) {   // dK folded into the dV accumulator: Q columns times the exact 1/sqrt(hd)
+        if (KV && MEP_BWD_STACK && !BF) {
+            qb2 = S2{};   // in the stacked operand B0 / B1
+        } else if (KV) {   // dK folded into the dV accumulator: Q columns times the exact 1/sqrt(hd)
             float q4[4];
 #pragma unroll
             for (int s = 0; s < 4; ++s) q4[s] = in.qb[s] * INV_SCALE;
@@ -663,7 +676,18 @@ struct Bwd {
         } else {
             qb2 = split2(in.qb);
         }
-        const S2 db2 = (MEP_BWD_DVF32 && !BF) ? S2{} : split2(in.db);
+#if MEP_BWD_STACK
+        // stacked dKV operand [dO ; Q/4] (slots 0-3 / 4-7), split straight into the operand words
+        u32x4 B0 = u32x4{0u, 0u, 0u, 0u}, B1 = B0;
+        if (KV && !BF) {
+            float q4[4];
+#pragma unroll
+            for (int s = 0; s < 4; ++s) q4[s] = in.qb[s] * INV_SCALE;
+            B0 = split_hi(in.db, q4);
+            B1 = split_lo(in.db, q4, B0);
+        }
+#endif
+        const S2 db2 = ((MEP_BWD_DVF32 || (KV && MEP_BWD_STACK)) && !BF) ? S2{} : split2(in.db);
         typedef __attribute__((address_space(3))) unsigned short lushort;
         lushort* Th = (lushort*)Tr;                 // [16 queries][TLD2] bf16 parts of dS
         lushort* Tl = Th + 16 * TLD2;
@@ -711,17 +735,25 @@ struct Bwd {
                 p[r] = pv;
                 dsv[r] = gsv;
             }
-            const S2 ds2 = split2(dsv);
-            if (KV && !BF && MEP_BWD_STACK) {
+#if MEP_BWD_STACK
+            S2 ds2;
+            if (KV && !BF) {
                 // dKV[key][dim] += P^T dO + dS^T Q / 4 as ONE 32-deep contraction [P | dS] . [dO ; Q/4]
                 // (slots 0-3: P / dO of queries 4g..4g+3, slots 4-7: dS / Q/4 of the same queries),
-                // products x0 y0 + x1 y0 + x0 y1 of both terms on three 16x16x32 MFMAs
-                const S2 ps = split2(p);
-                const bf16x8 a0 = op(ps.h0, ps.h1, ds2.h0, ds2.h1), a1 = op(ps.l0, ps.l1, ds2.l0, ds2.l1);
-                const bf16x8 b0 = op(db2.h0, db2.h1, qb2.h0, qb2.h1), b1 = op(db2.l0, db2.l1, qb2.l0, qb2.l1);
-                dk[kt] = mfma(a0, b0, dk[kt]);
-                dk[kt] = mfma(a1, b0, dk[kt]);
-                dk[kt] = mfma(a0, b1, dk[kt]);
+                // products x0 y0 + x1 y0 + x0 y1 of both terms on three 16x16x32 MFMAs; the parts are
+                // split straight into the operand words (no register copies)
+                const u32x4 A0 = split_hi(p, dsv), A1 = split_lo(p, dsv, A0);
+                ds2 = S2{A0[2], A0[3], A1[2], A1[3]};
+                dk[kt] = mfma(__builtin_bit_cast(bf16x8, A0), __builtin_bit_cast(bf16x8, B0), dk[kt]);
+                dk[kt] = mfma(__builtin_bit_cast(bf16x8, A1), __builtin_bit_cast(bf16x8, B0), dk[kt]);
+                dk[kt] = mfma(__builtin_bit_cast(bf16x8, A0), __builtin_bit_cast(bf16x8, B1), dk[kt]);
+            } else {
+                ds2 = split2(dsv);
+            }
+#else
+            const S2 ds2 = split2(dsv);
+#endif
+            if (KV && !BF && MEP_BWD_STACK) {
             } else if (KV) {                             // dKV[key][dim] += P^T dO + dS^T Q / 4
                 dk[kt] = dot16<BF>(split2(p), db2, dk[kt]);
             } else if (MEP_BWD_DVF32 && !BF) {           // dV[key][dim] += P^T dO, exact fp32

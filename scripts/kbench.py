@@ -45,7 +45,7 @@ def main():
         'mep_wgrad': lambda: launch('mep_wgrad', p.d_wgrad, p.t_wgrad),
         'mep_pool_fwd': lambda: launch('mep_pool_fwd', p.d_pool, p.t_pool),
     }
-    names = list(table) if args.kernel == 'all' else [args.kernel]
+    names = list(table) if args.kernel == 'all' else args.kernel.split(',')
     for name in names:
         fn = table[name]
         fn()

@@ -9,9 +9,9 @@ for name in ${NAMES:-$(ls variants)}; do
   lib=variants/$name/libmep_hip.so
   [ -f $lib ] || continue
   for cfg in ${CFGS:-cfg3 cfg5}; do
-    for k in ${KS:-mep_attn_fwd mep_attn_bwd}; do
-      MEP_LIB=$lib timeout -k 10 120 python3 scripts/kbench.py --config $cfg --kernel $k --reps ${REPS:-30} > gpurun_out/ab_$name.log 2>&1
-      rc=$?; echo "== $name $cfg $k: $(tail -1 gpurun_out/ab_$name.log)"; fatal $rc
+    for dt in ${DTYPES:-fp32}; do
+      MEP_LIB=$lib timeout -k 10 120 python3 scripts/kbench.py --config $cfg --dtype $dt --kernel ${KS:-mep_attn_fwd,mep_attn_bwd} --reps ${REPS:-30} > gpurun_out/ab_$name.log 2>&1
+      rc=$?; echo "== $name $cfg $dt: $(grep us/launch gpurun_out/ab_$name.log | tr -s ' ' | tr '\n' ';')"; fatal $rc
     done
   done
   if [ -n "$PARITY" ]; then
