@@ -62,7 +62,8 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 #define MEP_BWD_WAVES_KV 4 // waves per SIMD of the short backward with MEP_ATTN_KV (<= 128 registers)
 #endif
 #ifndef MEP_FWD_PVSPLIT
-#define MEP_FWD_PVSPLIT 0  // forward P.V on 2-part bf16 splits (16x16x32) instead of f32 MFMA
+#define MEP_FWD_PVSPLIT 1  // forward P.V on 2-part bf16 splits (16x16x32) instead of f32 MFMA
+                           // (cfg3 30.1 -> 26.5 us, cfg5 421 -> 368 us)
 #endif
 #ifndef MEP_FWD_WAVES
 #define MEP_FWD_WAVES 3    // waves per SIMD of the short, non-residual forward
@@ -156,7 +157,8 @@ MEP_DEV floatx4 dot_score(const S3& p, const S3& u, floatx4 acc) {
 #define MEP_BWD_MF16 1   // backward 2-way products as separate 16x16x16 MFMAs (no operand assembly)
 #endif
 #ifndef MEP_BWD_STACK
-#define MEP_BWD_STACK 0  // KV backward: P^T dO + dS^T Q/4 as one 32-deep contraction on 16x16x32 MFMAs
+#define MEP_BWD_STACK 1  // KV backward: P^T dO + dS^T Q/4 as one 32-deep contraction on 16x16x32 MFMAs
+                         // (cfg3 39.5 -> 37.2 us, cfg5 663 -> 607 us with MEP_BWD_MF16_DQ = 0)
 #endif
 #ifndef MEP_BWD_DVF32
 #define MEP_BWD_DVF32 0  // dV += P^T dO on f32 MFMA from the raw P / dO (no split): 48.6 vs 45.5 us, off
@@ -191,7 +193,7 @@ MEP_DEV floatx4 dot16(const S2& x, const S2& y, floatx4 acc) {
 // 32-deep contraction over two 16-row tiles (slots 0-3: tile 0, 4-7: tile 1), 2-way split,
 // products x0 y0 + x1 y0 + x0 y1 (BF: x0 y0); MEP_BWD_MF16: per tile on 16x16x16
 #ifndef MEP_BWD_MF16_DQ
-#define MEP_BWD_MF16_DQ MEP_BWD_MF16   // dQ's 32-deep contraction on 16x16x16 (1) or 16x16x32 (0)
+#define MEP_BWD_MF16_DQ 0   // dQ's 32-deep contraction on 16x16x16 (1) or 16x16x32 (0)
 #endif
 template <bool BF>
 MEP_DEV floatx4 dot32(const S2& xa, const S2& xb, const S2& ya, const S2& yb, floatx4 acc) {

@@ -23,6 +23,10 @@
 #ifndef MEP_EPI_SPLIT
 #define MEP_EPI_SPLIT 1   // D <= 96 on split-bf16 MFMA (0: exact fp32 MFMA everywhere)
 #endif
+#ifndef MEP_EPI_SPLIT128
+#define MEP_EPI_SPLIT128 0   // D = 128 on split-bf16 MFMA: weights as 2 parts (the 3-part Wm needs 210 KB
+                             // of LDS), activations 3 parts, five products per k pair
+#endif
 
 using namespace mep;
 
@@ -298,11 +302,11 @@ extern "C" int mep_epi_set_trace(void* p) { return (int)hipMemcpyToSymbol(HIP_SY
 #define MEP_EPI_STAMP(k) ((void)0)
 #endif
 
-template <int D, int NPART>
+template <int D, int NPART, int NW = NPART>
 MEP_DEV void epi_fwd_split(const mep_epi_desc& d, unsigned char* sm, int t_begin, int t_end) {
     constexpr int NI = D / 16, KB = D / 16, NP = D / 32;
-    using WP = SplitW<D, NP, NPART>;
-    using WM = SplitW<D, 2 * NP, NPART>;
+    using WP = SplitW<D, NP, NW>;
+    using WM = SplitW<D, 2 * NP, NW>;
     using Op = OpN<NPART>;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int c = lane & 15, g = lane >> 4;
@@ -324,7 +328,7 @@ MEP_DEV void epi_fwd_split(const mep_epi_desc& d, unsigned char* sm, int t_begin
     // ---- phase 1: xp = drop(x Wp^T)
     MEP_EPI_STAMP(0);
     if (t_begin + wave < t_end) rows_of(d.x, t_begin + wave, ab);
-    stage_split_rows<D, D, NPART>(wp, G<const float>(d.wp));
+    stage_split_rows<D, D, NW>(wp, G<const float>(d.wp));
     __syncthreads();
     MEP_EPI_STAMP(1);
     for (int tile = t_begin + wave; tile < t_end; tile += EWAVES) {
@@ -336,7 +340,7 @@ MEP_DEV void epi_fwd_split(const mep_epi_desc& d, unsigned char* sm, int t_begin
         f32x4 xp[NI];
 #pragma unroll
         for (int i = 0; i < NI; ++i) xp[i] = zero_f4();
-        tgemm_n<NI, NP, NPART>(xp, [&](int i, int pp) { return wp.frag(i, pp); }, [&](int pp) { return xs[pp]; });
+        tgemm_n<NI, NP, NPART, NW>(xp, [&](int i, int pp) { return wp.frag(i, pp); }, [&](int pp) { return xs[pp]; });
         if (tok < ntok) {
             gfloat* pr = row_ptr(d.xp, tok);
 #pragma unroll
@@ -355,7 +359,7 @@ MEP_DEV void epi_fwd_split(const mep_epi_desc& d, unsigned char* sm, int t_begin
     wg_store_barrier();              // xp rows stored; Wp no longer read
     MEP_EPI_STAMP(2);
     if (t_begin + wave < t_end) rows_of(d.xp, t_begin + wave, bb);
-    stage_split_rows<D, 2 * D, NPART>(wm, G<const float>(d.wm));
+    stage_split_rows<D, 2 * D, NW>(wm, G<const float>(d.wm));
     __syncthreads();
     MEP_EPI_STAMP(3);
     for (int tile = t_begin + wave; tile < t_end; tile += EWAVES) {
@@ -367,8 +371,8 @@ MEP_DEV void epi_fwd_split(const mep_epi_desc& d, unsigned char* sm, int t_begin
         f32x4 z[NI];
 #pragma unroll
         for (int i = 0; i < NI; ++i) z[i] = zero_f4();
-        tgemm_n<NI, NP, NPART>(z, [&](int i, int pp) { return wm.frag(i, pp); }, [&](int pp) { return qs[pp]; });
-        tgemm_n<NI, NP, NPART>(z, [&](int i, int pp) { return wm.frag(i, NP + pp); }, [&](int pp) { return ps[pp]; });
+        tgemm_n<NI, NP, NPART, NW>(z, [&](int i, int pp) { return wm.frag(i, pp); }, [&](int pp) { return qs[pp]; });
+        tgemm_n<NI, NP, NPART, NW>(z, [&](int i, int pp) { return wm.frag(i, NP + pp); }, [&](int pp) { return ps[pp]; });
         float sum = 0.f;
 #pragma unroll
         for (int i = 0; i < NI; ++i) sum += (z[i][0] + z[i][1]) + (z[i][2] + z[i][3]);
@@ -409,11 +413,11 @@ MEP_DEV void epi_fwd_split(const mep_epi_desc& d, unsigned char* sm, int t_begin
 #endif
 }
 
-template <int D, int NPART>
+template <int D, int NPART, int NW = NPART>
 MEP_DEV void epi_bwd_split(const mep_epi_bwd_desc& bd, unsigned char* sm, int t_begin, int t_end) {
     constexpr int NI = D / 16, KB = D / 16, NP = D / 32;
-    using WMT = SplitW<2 * D, NP, NPART>;
-    using WPT = SplitW<D, NP, NPART>;
+    using WMT = SplitW<2 * D, NP, NW>;
+    using WPT = SplitW<D, NP, NW>;
     using Op = OpN<NPART>;
     const mep_epi_desc& d = bd.f;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -444,7 +448,7 @@ MEP_DEV void epi_bwd_split(const mep_epi_bwd_desc& bd, unsigned char* sm, int t_
     };
     // ---- phase 1: LayerNorm backward, dxp = drop'(dz Wm[:, D:]), dq (+)= dz Wm[:, :D]
     if (t_begin + wave < t_end) fetch1(t_begin + wave);
-    stage_split_cols<D, 2 * D, NPART>(wmt, G<const float>(d.wm));
+    stage_split_cols<D, 2 * D, NW>(wmt, G<const float>(d.wm));
     __syncthreads();
     for (int tile = t_begin + wave; tile < t_end; tile += EWAVES) {
         const int tok = tile * 16 + c;
@@ -504,7 +508,7 @@ MEP_DEV void epi_bwd_split(const mep_epi_bwd_desc& bd, unsigned char* sm, int t_
         f32x4 acc[NI];
 #pragma unroll
         for (int i = 0; i < NI; ++i) acc[i] = zero_f4();
-        tgemm_n<NI, NP, NPART>(acc, [&](int i, int pp) { return wmt_x.frag(i, pp); }, [&](int pp) { return dzb[pp]; });
+        tgemm_n<NI, NP, NPART, NW>(acc, [&](int i, int pp) { return wmt_x.frag(i, pp); }, [&](int pp) { return dzb[pp]; });
         if (ok) {
             gfloat* dzr = row_ptr(bd.dz, tok);
             gfloat* dpr = row_ptr(bd.dxp, tok);
@@ -521,7 +525,7 @@ MEP_DEV void epi_bwd_split(const mep_epi_bwd_desc& bd, unsigned char* sm, int t_
         }
 #pragma unroll
         for (int i = 0; i < NI; ++i) acc[i] = zero_f4();
-        tgemm_n<NI, NP, NPART>(acc, [&](int i, int pp) { return wmt.frag(i, pp); }, [&](int pp) { return dzb[pp]; });
+        tgemm_n<NI, NP, NPART, NW>(acc, [&](int i, int pp) { return wmt.frag(i, pp); }, [&](int pp) { return dzb[pp]; });
         if (ok) {
             gfloat* qrw = row_ptr(bd.dq, tok);
 #pragma unroll
@@ -540,7 +544,7 @@ MEP_DEV void epi_bwd_split(const mep_epi_bwd_desc& bd, unsigned char* sm, int t_
         for (int kb = 0; kb < KB; ++kb) ga[kb] = ld4w(r + 16 * kb);
     };
     if (t_begin + wave < t_end) fetch2(t_begin + wave);
-    stage_split_cols<D, D, NPART>(wpt, G<const float>(d.wp));
+    stage_split_cols<D, D, NW>(wpt, G<const float>(d.wp));
     __syncthreads();
     for (int tile = t_begin + wave; tile < t_end; tile += EWAVES) {
         const int tok = tile * 16 + c;
@@ -551,7 +555,7 @@ MEP_DEV void epi_bwd_split(const mep_epi_bwd_desc& bd, unsigned char* sm, int t_
         f32x4 acc[NI];
 #pragma unroll
         for (int i = 0; i < NI; ++i) acc[i] = zero_f4();
-        tgemm_n<NI, NP, NPART>(acc, [&](int i, int pp) { return wpt.frag(i, pp); }, [&](int pp) { return xs[pp]; });
+        tgemm_n<NI, NP, NPART, NW>(acc, [&](int i, int pp) { return wpt.frag(i, pp); }, [&](int pp) { return xs[pp]; });
         if (tok < ntok) {
             gfloat* xrw = row_ptr(bd.dx, tok);
 #pragma unroll
@@ -568,11 +572,11 @@ __global__ __launch_bounds__(ETHREADS) void k_epi_fwd(const mep_epi_desc* __rest
     const mep_epi_desc& d = descs[blockIdx.y];
     int t_begin, t_end;
     if (!tile_range(d.ntok, t_begin, t_end)) return;   // whole workgroup
-    if constexpr (BF16 || (MEP_EPI_SPLIT && D <= 96)) {
-        constexpr int NPART = BF16 ? 1 : 3;
-        constexpr int BYTES = SplitW<D, D / 16, NPART>::BYTES;   // the larger phase (Wm)
+    if constexpr (BF16 || (MEP_EPI_SPLIT && D <= 96) || (MEP_EPI_SPLIT128 && D == 128)) {
+        constexpr int NPART = BF16 ? 1 : 3, NW = BF16 ? 1 : (D == 128 ? 2 : 3);
+        constexpr int BYTES = SplitW<D, D / 16, NW>::BYTES;   // the larger phase (Wm)
         __shared__ __attribute__((aligned(16))) unsigned char sm6[BYTES];
-        epi_fwd_split<D, NPART>(d, sm6, t_begin, t_end);
+        epi_fwd_split<D, NPART, NW>(d, sm6, t_begin, t_end);
         return;
     }
     __shared__ __attribute__((aligned(16))) float smem[Geo::FWD];
@@ -723,11 +727,11 @@ __global__ __launch_bounds__(ETHREADS) void k_epi_bwd(const mep_epi_bwd_desc* __
     const mep_epi_desc& d = bd.f;
     int t_begin, t_end;
     if (!tile_range(d.ntok, t_begin, t_end)) return;
-    if constexpr (BF16 || (MEP_EPI_SPLIT && D <= 96)) {
-        constexpr int NPART = BF16 ? 1 : 3;
-        constexpr int BYTES = SplitW<2 * D, D / 32, NPART>::BYTES;   // the larger phase (Wm^T)
+    if constexpr (BF16 || (MEP_EPI_SPLIT && D <= 96) || (MEP_EPI_SPLIT128 && D == 128)) {
+        constexpr int NPART = BF16 ? 1 : 3, NW = BF16 ? 1 : (D == 128 ? 2 : 3);
+        constexpr int BYTES = SplitW<2 * D, D / 32, NW>::BYTES;   // the larger phase (Wm^T)
         __shared__ __attribute__((aligned(16))) unsigned char sm6[BYTES];
-        epi_bwd_split<D, NPART>(bd, sm6, t_begin, t_end);
+        epi_bwd_split<D, NPART, NW>(bd, sm6, t_begin, t_end);
         return;
     }
     __shared__ __attribute__((aligned(16))) float smem[Geo::BWD];

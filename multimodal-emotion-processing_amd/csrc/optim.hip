@@ -15,7 +15,8 @@ using namespace mep;
 
 namespace {
 
-constexpr int NPART = 1024;
+constexpr int NPART = 1016;        // per-workgroup norm partials; partial[NPART ..] holds the step's scalars
+constexpr int SCAL = NPART;        // partial[SCAL + 0..2]: lr / (1 - b1^t), sqrt(1 - b2^t), t
 constexpr int OPT_THREADS = 256;
 constexpr int MAX_SEG = 16;
 
@@ -28,7 +29,8 @@ struct Segs {
 // Segments whose offset is a multiple of 4 floats run as float4 streams (the flat buffers are
 // 256-byte aligned), the rest of a segment (tail, or a misaligned segment) element by element.
 __global__ __launch_bounds__(OPT_THREADS) void k_sqnorm(const float* __restrict__ g, Segs segs,
-                                                        float* __restrict__ partial, int* __restrict__ step) {
+                                                        float* __restrict__ partial, int* __restrict__ step,
+                                                        const float* __restrict__ hyper) {
     float s = 0.f;
     const int64_t gid = (int64_t)blockIdx.x * OPT_THREADS + threadIdx.x;
     const int64_t stride = (int64_t)gridDim.x * OPT_THREADS;
@@ -53,7 +55,14 @@ __global__ __launch_bounds__(OPT_THREADS) void k_sqnorm(const float* __restrict_
         float t = 0.f;
         for (int w = 0; w < OPT_THREADS / 64; ++w) t += red[w];
         partial[blockIdx.x] = t;
-        if (blockIdx.x == 0 && step) step[0] += 1;
+        if (blockIdx.x == 0 && step) {
+            // the step counter and the bias corrections (double pow) once per step, not per thread
+            const int ts = step[0] + 1;
+            step[0] = ts;
+            const double lr = hyper[0], b1 = hyper[1], b2 = hyper[2];
+            partial[SCAL] = (float)(lr / (1.0 - pow(b1, (double)ts)));
+            partial[SCAL + 1] = (float)sqrt(1.0 - pow(b2, (double)ts));
+        }
     }
 }
 
@@ -80,32 +89,30 @@ __global__ __launch_bounds__(OPT_THREADS) void k_clip_adam(float* __restrict__ p
                                                            const float* __restrict__ hyper,
                                                            const int* __restrict__ step, float* gnorm_out,
                                                            int decoupled) {
-    __shared__ float red[OPT_THREADS];
+    // every workgroup sums the partials in the same fixed order (lane-strided, then the wave's
+    // DPP tree, then the 4 waves in order): identical totals, no grid barrier
+    __shared__ float red[OPT_THREADS / 64];
     float s = 0.f;
     for (int i = threadIdx.x; i < npart; i += OPT_THREADS) s += partial[i];
-    red[threadIdx.x] = s;
+    s = wave_sum(s);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
     __syncthreads();
-    for (int w = OPT_THREADS / 2; w > 0; w >>= 1) {
-        if (threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
-        __syncthreads();
-    }
+    const float sum = ((red[0] + red[1]) + red[2]) + red[3];
     const float gscale = hyper[6] > 0.f ? hyper[6] : 1.0f;   // 1/world after a SUM all-reduce
-    const float total = sqrtf(red[0]) * gscale;
+    const float total = sqrtf(sum) * gscale;
     const float max_norm = hyper[5];
     const float coef = fminf(max_norm / (total + 1e-6f), 1.0f);
     if (blockIdx.x == 0 && threadIdx.x == 0 && gnorm_out) *gnorm_out = total;
-    const int t = step[0];
-    const double lr = hyper[0], b1 = hyper[1], b2 = hyper[2], wd = hyper[4];
-    const double bc1 = 1.0 - pow(b1, (double)t), bc2 = 1.0 - pow(b2, (double)t);
+    const float lr = hyper[0], b1 = hyper[1], b2 = hyper[2], wd = hyper[4];
     AdamCoef k;
     k.gs = gscale * coef;
-    k.step_size = (float)(lr / bc1);
-    k.bc2_sqrt = (float)sqrt(bc2);
-    k.decay = (float)(1.0 - lr * wd);
-    k.one_m_b1 = (float)(1.0 - b1);
-    k.b2 = (float)b2;
-    k.one_m_b2 = (float)(1.0 - b2);
-    k.wd = (float)wd;
+    k.step_size = partial[SCAL];
+    k.bc2_sqrt = partial[SCAL + 1];
+    k.decay = (float)(1.0 - (double)lr * (double)wd);
+    k.one_m_b1 = (float)(1.0 - (double)b1);
+    k.b2 = b2;
+    k.one_m_b2 = (float)(1.0 - (double)b2);
+    k.wd = wd;
     k.eps = hyper[3];
     k.decoupled = decoupled;
     const int64_t gid = (int64_t)blockIdx.x * OPT_THREADS + threadIdx.x;
@@ -192,7 +199,7 @@ extern "C" int mep_clip_adam(float* params, float* grads, float* exp_avg, float*
     // thread serialised 4 dependent load -> store trips), one partial per workgroup for the norm
     int grid = (int)((longest + OPT_THREADS * 4 - 1) / (OPT_THREADS * 4));
     grid = grid < 1 ? 1 : (grid > NPART ? NPART : grid);
-    hipLaunchKernelGGL(k_sqnorm, dim3(grid), dim3(OPT_THREADS), 0, (hipStream_t)stream, grads, s, partial, step);
+    hipLaunchKernelGGL(k_sqnorm, dim3(grid), dim3(OPT_THREADS), 0, (hipStream_t)stream, grads, s, partial, step, hyper);
     int rc = mep_check_launch("mep_clip_adam/sqnorm");
     if (rc) return rc;
     hipLaunchKernelGGL(k_clip_adam, dim3(grid), dim3(OPT_THREADS), 0, (hipStream_t)stream, params, grads, exp_avg,

@@ -70,21 +70,27 @@ MEP_DEV OpN<NPART> opn(f32x4 blk0, f32x4 blk1) {
 MEP_DEV f32x4 mfma_bf16(bf16x8 a, bf16x8 b, f32x4 c) { return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0); }
 MEP_DEV floatx16 mfma_bf16(bf16x8 a, bf16x8 b, floatx16 c) { return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0); }
 
-// acc += A B over one k pair: the products x_i y_j with i + j < NPART, in a fixed order
-template <int NPART, typename Acc>
-MEP_DEV Acc mma_n(const OpN<NPART>& a, const OpN<NPART>& b, Acc acc) {
+// acc += A B over one k pair: the products x_i y_j (i < NA parts of A, j < NB parts of B) with
+// i + j < max(NA, NB), in a fixed order.  NA = NB = NPART: the products listed above; NA = 2,
+// NB = 3 (D = 128 epilogue weights kept as two parts, activations three): five products, the
+// weights' representation error <= 2^-18 relative.
+template <int NA, int NB, typename Acc>
+MEP_DEV Acc mma_nm(const OpN<NA>& a, const OpN<NB>& b, Acc acc) {
+    constexpr int N = NA > NB ? NA : NB;
     acc = mfma_bf16(a.p[0], b.p[0], acc);
-    if constexpr (NPART >= 2) {
-        acc = mfma_bf16(a.p[1], b.p[0], acc);
-        acc = mfma_bf16(a.p[0], b.p[1], acc);
+    if constexpr (N >= 2) {
+        if constexpr (NA >= 2) acc = mfma_bf16(a.p[1], b.p[0], acc);
+        if constexpr (NB >= 2) acc = mfma_bf16(a.p[0], b.p[1], acc);
     }
-    if constexpr (NPART >= 3) {
-        acc = mfma_bf16(a.p[1], b.p[1], acc);
-        acc = mfma_bf16(a.p[2], b.p[0], acc);
-        acc = mfma_bf16(a.p[0], b.p[2], acc);
+    if constexpr (N >= 3) {
+        if constexpr (NA >= 2 && NB >= 2) acc = mfma_bf16(a.p[1], b.p[1], acc);
+        if constexpr (NA >= 3) acc = mfma_bf16(a.p[2], b.p[0], acc);
+        if constexpr (NB >= 3) acc = mfma_bf16(a.p[0], b.p[2], acc);
     }
     return acc;
 }
+template <int NPART, typename Acc>
+MEP_DEV Acc mma_n(const OpN<NPART>& a, const OpN<NPART>& b, Acc acc) { return mma_nm<NPART, NPART>(a, b, acc); }
 
 // ---------------------------------------------------------------- split weights in LDS
 // A weight operand of R rows (output features) and K = 32 * NP contraction indices kept in LDS
@@ -125,14 +131,14 @@ struct SplitW {
 #ifndef MEP_TG_GROUP
 #define MEP_TG_GROUP 2   // output tiles per scheduling group of tgemm_n
 #endif
-template <int NI, int NP, int NPART, typename AF, typename BF>
+template <int NI, int NP, int NPART, int NW = NPART, typename AF, typename BF>
 MEP_DEV void tgemm_n(f32x4 (&acc)[NI], AF&& afr, BF&& bfr) {
 #pragma unroll
     for (int p = 0; p < NP; ++p) {
         const OpN<NPART> b = bfr(p);
 #pragma unroll
         for (int i = 0; i < NI; ++i) {
-            acc[i] = mma_n<NPART>(afr(i, p), b, acc[i]);
+            acc[i] = mma_nm<NW, NPART>(afr(i, p), b, acc[i]);   // A: NW weight parts
             // keep the next fragment's reads behind these MFMAs (a fully hoisted, fully unrolled
             // product would hold 4 NPART NI NP fragment VGPRs)
             if (i % MEP_TG_GROUP == MEP_TG_GROUP - 1) __builtin_amdgcn_sched_barrier(0);

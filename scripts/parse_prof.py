@@ -1,6 +1,6 @@
 """Summarise a scripts/profile.sh run into profiles/<tag>_*.
 
-  python scripts/parse_prof.py <tag> [gpurun_out/prof]
+  python scripts/parse_prof.py <tag> [gpurun_out/prof_<workload>] [<workload>: cfg3 | cfg5 | cfg5_bf16 | ...]
 
 Writes profiles/<tag>_kernel_stats.csv (rocprofv3 --stats output, verbatim) and
 profiles/<tag>_pmc.json: per kernel, the average dispatch duration (kernel trace) and the
@@ -10,6 +10,7 @@ bytes of a wide coalesced read -- MI355X_MICROARCH.md section HBM; the x2 is exa
 16-byte-per-lane streams, other widths are uncalibrated).
 """
 import csv
+import glob
 import json
 import os
 import shutil
@@ -24,13 +25,19 @@ def short(name):
 def main():
     tag = sys.argv[1]
     src = sys.argv[2] if len(sys.argv) > 2 else 'gpurun_out/prof'
+    # workload suffix (bench.py pmc_traffic): none for cfg3 fp32, else _<config>[_bf16]
+    sfx = '_' + sys.argv[3] if len(sys.argv) > 3 and sys.argv[3] != 'cfg3' else ''
+    # rocprofv3 -d <dir> -o run writes <dir>/<host>/<pid>_run_*.csv in some versions: find the files
+    def find(sub, name):
+        hits = glob.glob(os.path.join(src, sub, '**', '*' + name), recursive=True)
+        return sorted(hits, key=os.path.getsize)[-1] if hits else os.path.join(src, sub, 'run_' + name)
     os.makedirs('profiles', exist_ok=True)
-    shutil.copy(os.path.join(src, 'trace', 'run_kernel_stats.csv'), 'profiles/%s_kernel_stats.csv' % tag)
+    shutil.copy(find('trace', 'kernel_stats.csv'), 'profiles/%s_kernel_stats%s.csv' % (tag, sfx))
     stats = {short(r['Name']): dict(calls=int(r['Calls']), avg_us=float(r['AverageNs']) / 1e3,
                                     pct=float(r['Percentage']))
-             for r in csv.DictReader(open(os.path.join(src, 'trace', 'run_kernel_stats.csv')))}
+             for r in csv.DictReader(open(find('trace', 'kernel_stats.csv')))}
     for ctr, sub in (('FETCH_SIZE', 'fetch'), ('WRITE_SIZE', 'write')):
-        path = os.path.join(src, sub, 'run_counter_collection.csv')
+        path = find(sub, 'counter_collection.csv')
         if not os.path.exists(path):
             continue
         acc = defaultdict(list)
@@ -42,7 +49,7 @@ def main():
     for k, s in stats.items():
         if 'fetch_size_kb' in s and 'write_size_kb' in s:
             s['hbm_bytes_per_dispatch'] = (2 * s['fetch_size_kb'] + s['write_size_kb']) * 1024
-    json.dump(stats, open('profiles/%s_pmc.json' % tag, 'w'), indent=1, sort_keys=True)
+    json.dump(stats, open('profiles/%s_pmc%s.json' % (tag, sfx), 'w'), indent=1, sort_keys=True)
     for k, s in sorted(stats.items(), key=lambda kv: -kv[1].get('pct', 0))[:16]:
         print('%-22s %8.2f us  %6.2f%%  traffic %s' % (k, s.get('avg_us', 0), s.get('pct', 0),
                                                      '%.2f MB' % (s['hbm_bytes_per_dispatch'] / 1e6)
