@@ -69,7 +69,7 @@ class LaunchTimer:
 # launch name -> kernel symbol prefix in the rocprofv3 summaries (scripts/parse_prof.py)
 KERNEL_OF = {'mep_attn_bwd': 'k_attn_bwd', 'mep_attn_fwd': 'k_attn_fwd', 'mep_block_epi_fwd': 'k_epi_fwd',
              'mep_block_epi_bwd': 'k_epi_bwd', 'mep_wgrad': 'k_wgrad', 'mep_unify': 'k_unify',
-             'mep_pool_fwd': 'k_pool_fwd', 'mep_pool_bwd': 'k_pool_bwd', 'mep_gemm': 'k_gemm',
+             'mep_pool_fwd': 'k_pool_fwd', 'mep_pool_bwd': 'k_pool_bwd', 'mep_gemm': 'k_gemm', 'mep_tgemm': 'k_tgemm',
              'mep_rf_epi_fwd': 'k_rf_epi_fwd', 'mep_rf_epi_bwd': 'k_rf_epi_bwd', 'mep_sum_rows': 'k_sum_rows'}
 
 

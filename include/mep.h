@@ -87,6 +87,16 @@ int mep_gemm(const mep_gemm_desc* descs, int n_desc, int max_tiles, mep_stream_t
  * workgroups split its 16-token tiles into contiguous ranges. */
 int mep_unify(const mep_gemm_desc* descs, int n_desc, int n_wg, mep_stream_t stream);
 
+/* Tiled token GEMM on the bf16 matrix cores, the mep_gemm contract for N % 16 == 0: a workgroup
+ * owns 128 tokens x (up to) 128 output features, the weight is staged in LDS in 32-wide k chunks
+ * already split into bf16 parts (double-buffered), X rows go straight into registers.  fp32 path:
+ * 3-part splits of both operands (six products, fp32-level error); flags | MEP_PREC_BF16: plain
+ * bf16 operands (one product).  Every descriptor of a launch has the same w_nt (MEP_TGEMM_WT:
+ * w_nt = 0, W stored [K][N]); y rows (and bias) 16-byte aligned; N in {32, 64, 96} or >= 128.
+ * Grid: (ceil(max_ntok / 128), n_desc, N tiles). */
+#define MEP_TGEMM_WT 0x1
+int mep_tgemm(const mep_gemm_desc* descs, int n_desc, int max_ntok, int max_n, int flags, mep_stream_t stream);
+
 /* ---------------------------------------------------------------- weight-gradient GEMM
  * dW_i[n, k] (+)= sum_tok A[tok, n] * B_i[tok, k]   for up to 4 operands B_i sharing one A
  * (dW = dY^T X of every nn.Linear on the path; e.g. minus.weight = dZ^T [q | xp] is one

@@ -172,6 +172,7 @@ SIGNATURES.update({
     'mep_rf_head': [ctypes.POINTER(RfHeadDesc), P],
     'mep_threshold_sweep': [ctypes.POINTER(SweepDesc), P],
     'mep_assemble_windows': [ctypes.POINTER(WindowDesc), i32, P],
+    'mep_tgemm': [P, i32, i32, i32, i32, P],
     'mep_abi_version': [],
     'mep_last_error': [ctypes.c_char_p, ctypes.c_size_t],
     'mep_device_sync': [],
@@ -354,3 +355,48 @@ def epi_grid(ntok_max, n_desc):
 def attn_dc_slots(B, H, Tk):
     """floats of the backward's dc_partial (one per (b, h, 64-key chunk))"""
     return B * H * -(-Tk // 64)
+
+
+# ------------------------------------------------------------------ token GEMMs
+TGEMM = os.environ.get('MEP_TGEMM', '1') != '0'   # 0: the mep_unify / mep_gemm kernels (A/B runs)
+TGEMM_WT = 0x1                                     # MEP_TGEMM_WT: every descriptor has w_nt = 0
+
+
+def tgemm_ok(items):
+    """Can mep_tgemm run these GemmDescs (include/mep.h): N % 16 == 0 with N in {32, 64, 96} or
+    >= 128, one w_nt for the launch, 16-byte aligned y rows, bias and table rows."""
+    if not items:
+        return False
+    if len({d.w_nt for d in items}) != 1:
+        return False
+    for d in items:
+        if d.N % 16 or not (d.N in (32, 64, 96) or d.N >= 128):
+            return False
+        if d.y.ptr % 16 or d.y.sB % 4 or d.y.sT % 4 or d.bias % 16:
+            return False
+        if d.table and (d.table % 16 or (d.ldt or d.N) % 4):
+            return False
+        if d.ntok <= 0 or d.K <= 0:
+            return False
+    return True
+
+
+def gemm(name, descs, max_tiles, stream=None, prec=0):
+    """A token-GEMM launch (mep_gemm_desc array): the tiled split-bf16 kernel (mep_tgemm) when
+    the descriptors allow it, else the named launcher (mep_unify / mep_gemm).  prec: MEP_PREC_BF16
+    for the bf16 path (mep_unify reads the per-descriptor bf16 field instead)."""
+    if descs.n == 0:
+        return
+    if TGEMM and tgemm_ok(descs.items):
+        flags = (prec & PREC_BF16) | (0 if descs.items[0].w_nt else TGEMM_WT)
+        if any(d.bf16 for d in descs.items):
+            flags |= PREC_BF16
+        call('mep_tgemm', descs.ptr, descs.n, max(d.ntok for d in descs.items), max(d.N for d in descs.items),
+             flags, stream=stream)
+        return
+    launch(name, descs, max_tiles, stream)
+
+
+def gemm_launcher(name, descs):
+    """Launch name a gemm() call is timed under (bench.py / roofline.py)."""
+    return 'mep_tgemm' if TGEMM and tgemm_ok(descs.items) else name

@@ -1,0 +1,208 @@
+// Tiled token GEMM on the bf16 matrix cores:
+//   Y[tok, n] = act(alpha * sum_k X[tok, k] W(n, k) + bias[n] + table[tok % T, n]) (+ Y)
+// the mep_gemm_desc contract (include/mep.h), for the Linears of Unify_Dimension
+// (cmu-mosei/run.py:210-214, Ren-MME/run.py:161-166), the realformer Conv1d unify + position
+// table and the w_qkv / input-gradient products (others/realformer.py:136-157,182-188).
+//
+// Mapping (CDNA4).  Transposed tiles (common.h): Y^T = W X^T on v_mfma_f32_16x16x32_bf16 with
+// the k-pair slot convention of split.h, so lane (token c, group g) holds output features
+// 16 i + 4g .. +3 of its token in accumulator i and both operands are 16-byte row fragments:
+// W(n, k .. k+3) (the A operand, rows = output features) and X(tok, k .. k+3) (the B operand).
+// A workgroup (4 waves) owns 128 tokens (two 16-token tiles per wave) and an N tile of up to 128
+// output features; the K axis runs in 32-wide chunks.  The W chunk is staged in LDS once per
+// workgroup, already split into its bf16 parts (split.h SplitW, conflict-free 16-byte units),
+// double-buffered: chunk kc+1's W loads are in flight while chunk kc multiplies, and one barrier
+// per chunk.  X fragments go straight from HBM into registers one chunk ahead and are split in
+// registers.  fp32 path: three parts per operand, six products (fp32-level, split.h); bf16 path
+// (desc.bf16): one part, one product.  W columns past K are staged as zeros, so the X columns past
+// K (the next row's data, or zeros past the view through the range-checked buffer loads) never
+// contribute.
+#include "common.h"
+#include "split.h"
+
+using namespace mep;
+
+namespace {
+
+constexpr int TG_WAVES = 4;
+constexpr int TG_THREADS = 64 * TG_WAVES;
+constexpr int TG_TT = 2;                          // 16-token tiles per wave
+constexpr int TG_BM = 16 * TG_TT * TG_WAVES;      // tokens per workgroup
+
+// W(n, k .. k+3) of the staged chunk, zero past K / N
+template <bool WNT>
+MEP_DEV f32x4 tg_wfrag(const gfloat* W, int ldw, bool vec, int n, int N, int k, int K) {
+    if (n >= N) return f32x4{0.f, 0.f, 0.f, 0.f};
+    if (WNT) {
+        const gfloat* p = W + (int64_t)n * ldw;
+        if (vec && k + 3 < K) return ld4w(p + k);
+        f32x4 v;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = k + e < K ? p[k + e] : 0.f;
+        return v;
+    }
+    f32x4 v;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] = k + e < K ? W[(int64_t)(k + e) * ldw + n] : 0.f;
+    return v;
+}
+
+template <int NI, int NPART, bool WNT>
+__global__ __launch_bounds__(TG_THREADS) void k_tgemm(const mep_gemm_desc* __restrict__ descs) {
+    constexpr int BN = 16 * NI;
+    using WS = SplitW<BN, 1, NPART>;                     // one k pair (32 wide) of BN rows
+    __shared__ __attribute__((aligned(16))) unsigned char sm[2 * WS::BYTES];
+    const mep_gemm_desc& d = descs[blockIdx.y];
+    const int n0 = (int)blockIdx.z * BN;
+    const int tok0 = (int)blockIdx.x * TG_BM;
+    if (n0 >= d.N || tok0 >= d.ntok) return;            // the whole workgroup
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int c = lane & 15, g = lane >> 4;
+    const int K = d.K, N = d.N, ntok = d.ntok;
+    const int nkc = (K + 31) >> 5;
+    typedef __attribute__((address_space(3))) unsigned char lbyte;
+    auto wbuf = [&](int b) { return WS{(lbyte*)sm + b * WS::BYTES, 0}; };
+
+    // ---- W chunk staging: unit (n, g) = W(n0 + n, k0 + 4g ..) and W(n0 + n, k0 + 16 + 4g ..);
+    // consecutive threads take consecutive n (coalesced for W stored [k][n])
+    const gfloat* W = G<const float>(d.w);
+    const bool wvec = WNT && (d.ldw % 4 == 0) && ((d.w & 15) == 0);
+    constexpr int NU = BN * 4, UPT = (NU + TG_THREADS - 1) / TG_THREADS;
+    f32x4 wr[UPT][2];
+    auto load_w = [&](int kc) {
+        const int k0 = 32 * kc;
+#pragma unroll
+        for (int u = 0; u < UPT; ++u) {
+            const int idx = threadIdx.x + TG_THREADS * u;
+            const int n = idx % BN, gg = idx / BN;
+            if (idx < NU) {
+                wr[u][0] = tg_wfrag<WNT>(W, d.ldw, wvec, n0 + n, N, k0 + 4 * gg, K);
+                wr[u][1] = tg_wfrag<WNT>(W, d.ldw, wvec, n0 + n, N, k0 + 16 + 4 * gg, K);
+            }
+        }
+    };
+    auto put_w = [&](const WS& ws) {
+#pragma unroll
+        for (int u = 0; u < UPT; ++u) {
+            const int idx = threadIdx.x + TG_THREADS * u;
+            if (idx < NU) ws.put(idx % BN, 0, idx / BN, wr[u][0], wr[u][1]);
+        }
+    };
+
+    // ---- X rows of this wave's tiles (tokens past ntok: clamped rows, never stored)
+    const int64_t last = row_off(d.x, ntok - 1) + K;
+    const auto rsX = __builtin_amdgcn_make_buffer_rsrc((void*)d.x.ptr, 0, (int)min((int64_t)4 * last, (int64_t)0x7fffffff), 0x00020000);
+    const bool xvec = ((d.x.ptr & 15) == 0) && (d.x.sB % 4 == 0) && (d.x.sT % 4 == 0);
+    int xoff[TG_TT];
+#pragma unroll
+    for (int t = 0; t < TG_TT; ++t) {
+        const int tok = min(tok0 + 16 * (TG_TT * wave + t) + c, ntok - 1);
+        xoff[t] = 4 * (int)row_off(d.x, tok) + 16 * g;
+    }
+    f32x4 xr[TG_TT][2];
+    auto load_x = [&](int kc) {
+#pragma unroll
+        for (int t = 0; t < TG_TT; ++t)
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int o = xoff[t] + 128 * kc + 64 * h;   // bytes: k0 + 16 h + 4g
+                if (xvec) {
+                    xr[t][h] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rsX, o, 0, 0));
+                } else {
+#pragma unroll
+                    for (int e = 0; e < 4; ++e)
+                        xr[t][h][e] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsX, o + 4 * e, 0, 0));
+                }
+            }
+    };
+
+    f32x4 acc[TG_TT][NI];
+#pragma unroll
+    for (int t = 0; t < TG_TT; ++t)
+#pragma unroll
+        for (int i = 0; i < NI; ++i) acc[t][i] = zero_f4();
+
+    load_w(0);
+    load_x(0);
+    put_w(wbuf(0));
+    __syncthreads();
+    for (int kc = 0; kc < nkc; ++kc) {
+        OpN<NPART> xo[TG_TT];
+#pragma unroll
+        for (int t = 0; t < TG_TT; ++t) xo[t] = opn<NPART>(xr[t][0], xr[t][1]);
+        if (kc + 1 < nkc) {                 // next chunk's loads in flight across this chunk's MFMAs
+            load_w(kc + 1);
+            load_x(kc + 1);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        const WS ws = wbuf(kc & 1);
+#pragma unroll
+        for (int i = 0; i < NI; ++i) {
+            const OpN<NPART> w = ws.frag(i, 0);
+#pragma unroll
+            for (int t = 0; t < TG_TT; ++t) acc[t][i] = mma_n<NPART>(w, xo[t], acc[t][i]);
+            if (i & 1) __builtin_amdgcn_sched_barrier(0);
+        }
+        if (kc + 1 < nkc) put_w(wbuf((kc + 1) & 1));   // its last readers finished before the last barrier
+        __syncthreads();
+    }
+
+    // ---- epilogue: token c of tile t, features n0 + 16 i + 4g .. +3
+    const gfloat* bias = G<const float>(d.bias);
+    const gfloat* table = G<const float>(d.table);
+    const int ldt = d.ldt ? d.ldt : N;
+#pragma unroll
+    for (int t = 0; t < TG_TT; ++t) {
+        const int tok = tok0 + 16 * (TG_TT * wave + t) + c;
+        if (tok >= ntok) continue;
+        gfloat* yrow = row_ptr(d.y, tok);
+        const gfloat* trow = table ? table + (int64_t)(tok % d.y.T) * ldt : nullptr;
+#pragma unroll
+        for (int i = 0; i < NI; ++i) {
+            const int col = n0 + 16 * i + 4 * g;
+            if (col >= N) continue;
+            f32x4 v = acc[t][i];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[r] = d.alpha * v[r];
+            if (bias) v += ld4w(bias + col);
+            if (trow) {
+#pragma unroll
+                for (int r = 0; r < 4; ++r) v[r] += trow[col + r];
+            }
+            if (d.relu) {
+#pragma unroll
+                for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r], 0.f);
+            }
+            if (d.accumulate) v += ld4w(yrow + col);
+            *reinterpret_cast<MEP_G f32x4*>(yrow + col) = v;
+        }
+    }
+}
+
+}  // namespace
+
+// Grid (ceil(max ntok / 128), n_desc, ceil(max N / (16 * NI))): flags = MEP_PREC_BF16 for the bf16
+// path; the host guarantees N % 16 == 0, 16-byte aligned y rows / bias (and table rows when
+// present) and w_nt shared by every descriptor of the launch (mep_tgemm_ok in the Python binding).
+extern "C" int mep_tgemm(const mep_gemm_desc* descs, int n_desc, int max_ntok, int max_n, int flags,
+                         mep_stream_t stream) {
+    if (n_desc <= 0 || max_ntok <= 0 || max_n <= 0) return 0;
+    const bool bf = flags & MEP_PREC_BF16, wnt = !(flags & MEP_TGEMM_WT);
+    hipStream_t st = (hipStream_t)stream;
+    const int ni = max_n >= 128 ? 8 : (max_n + 15) / 16;   // 16-col tiles per workgroup N tile
+    const dim3 grid((max_ntok + TG_BM - 1) / TG_BM, n_desc, (max_n + 16 * ni - 1) / (16 * ni)), block(TG_THREADS);
+#define MEP_TG3(NI, P, WT) hipLaunchKernelGGL((k_tgemm<NI, P, WT>), grid, block, 0, st, descs)
+#define MEP_TG2(NI, P) do { if (wnt) MEP_TG3(NI, P, true); else MEP_TG3(NI, P, false); } while (0)
+#define MEP_TG(NI) do { if (bf) MEP_TG2(NI, 1); else MEP_TG2(NI, 3); } while (0)
+    switch (ni) {
+        case 2: MEP_TG(2); break;
+        case 4: MEP_TG(4); break;
+        case 6: MEP_TG(6); break;
+        case 8: MEP_TG(8); break;
+        default: mep_set_error("mep_tgemm: N must be 32, 64, 96 or >= 128 (a multiple of 16)"); return MEP_EINVAL;
+    }
+#undef MEP_TG
+#undef MEP_TG2
+#undef MEP_TG3
+    return mep_check_launch("mep_tgemm");
+}

@@ -451,16 +451,16 @@ class RealformerPlan:
         sp, nl = self.spec, self.spec.nl
         assert not rdrop
         ex = (sp.D, sp.FD)
-        launch('mep_gemm', self.d_unify, self.t_unify, stream)
-        launch('mep_gemm', self.d_proj, self.t_proj, stream)
+        _lib.gemm('mep_gemm', self.d_unify, self.t_unify, stream)
+        _lib.gemm('mep_gemm', self.d_proj, self.t_proj, stream)
         for i in range(nl):
             if i > 0:
-                launch('mep_gemm', self.d_q[i], self.t_epi[i], stream)
+                _lib.gemm('mep_gemm', self.d_q[i], self.t_epi[i], stream)
             launch('mep_attn_fwd', self.d_attn[i], self.t_attn[i], stream, threads=self.f_attn[i])
             launch('mep_rf_epi_fwd', self.d_epi[i], self.t_epif[i], stream, extra=ex)
         if sp.head:
             launch('mep_pool_fwd', self.d_pool, self.t_pool, stream)
-            launch('mep_gemm', self.d_fc, self.t_fc, stream)
+            _lib.gemm('mep_gemm', self.d_fc, self.t_fc, stream)
             self.head.compute_grad = int(grad)
             self.head.ext_dout = 0
             _lib.call('mep_rf_head', ctypes.byref(self.head), stream=stream)
@@ -476,7 +476,7 @@ class RealformerPlan:
                 self.head.ext_dout = ext_dout.data_ptr()
                 _lib.call('mep_rf_head', ctypes.byref(self.head), stream=stream)
                 self.head.ext_dout = 0
-            launch('mep_gemm', self.d_fcb, self.t_fc, stream)
+            _lib.gemm('mep_gemm', self.d_fcb, self.t_fc, stream)
             launch('mep_pool_bwd', self.d_pool, self.t_poolb, stream)
         elif ext_dout is not None:
             self.dout_chain.copy_(ext_dout.reshape(self.dout_chain.shape))
@@ -484,7 +484,7 @@ class RealformerPlan:
         for i in reversed(range(nl)):
             launch('mep_rf_epi_bwd', self.d_epib[i], self.t_epib[i], stream, extra=ex)
             launch('mep_attn_bwd', self.d_attnb[i], self.t_attnb[i], stream, threads=self.f_attnb[i])
-            launch('mep_gemm', self.d_ingrad[i], self.t_ingrad, stream)
+            _lib.gemm('mep_gemm', self.d_ingrad[i], self.t_ingrad, stream)
         launch('mep_sum_rows', self.d_sum, self.t_sum, stream)
         launch('mep_wgrad', self.d_wgrad, self.t_wgrad, stream)
         # weight-gradient split sums and LayerNorm / ReZero / residual-coefficient column sums: one

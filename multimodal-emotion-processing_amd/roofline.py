@@ -15,6 +15,7 @@ three for dQ) at 658 TFLOP/s.  The realformer token GEMMs and epilogues run on f
 bf16 path (MEP_PREC_BF16): one bf16 product per product, every matrix kernel priced at the bf16
 peak; the bytes are the same (fp32 storage).
 """
+from . import _lib
 from .trimodal import MODS
 
 HBM_PEAK = 8.0e12
@@ -26,6 +27,7 @@ BF16_PEAK = 2.5e15
 ATTN_FWD_PEAK = 4.0 / (12.0 / BF16_PEAK + 2.0 / F32_PEAK)
 ATTN_BWD_PEAK = 10.0 / (2.0 * (4 + 4 + 4 + 4 + 3) / BF16_PEAK)
 COMPUTE_PEAK = {'mep_block_epi_fwd': BF16_PEAK / 6, 'mep_block_epi_bwd': BF16_PEAK / 6, 'mep_wgrad': BF16_PEAK / 6,
+                'mep_tgemm': BF16_PEAK / 6,
                 'mep_attn_fwd': ATTN_FWD_PEAK, 'mep_attn_bwd': ATTN_BWD_PEAK}
 
 
@@ -37,6 +39,7 @@ def launch_costs(plan):
     sp, B = plan.spec, plan.B
     D, H = sp.D, sp.H
     out = {}
+    UNIFY = _lib.gemm_launcher('mep_unify', plan.d_unify)
 
     def add(name, f, b):
         f0, b0 = out.get(name, (0, 0))
@@ -45,7 +48,7 @@ def launch_costs(plan):
     for e in range(2):
         for m, d in zip(MODS, sp.dims):
             n = plan.ntok[m]
-            add('mep_unify', 2 * n * D * d, 4 * (n * d + n * D + D * d))
+            add(UNIFY, 2 * n * D * d, 4 * (n * d + n * D + D * d))
     for blk in plan.blocks:
         Tq, Tk = blk['Tq'], blk['Tk']
         r_in = 1 if blk['i'] > 0 else 0
@@ -86,8 +89,10 @@ def rf_launch_costs(plan):
         f0, b0 = out.get(name, (0, 0))
         out[name] = (f0 + f, b0 + b)
 
+    GEMM = _lib.gemm_launcher('mep_gemm', plan.d_unify)
+
     def gemm(name, ntok, N, K, accumulate=False, table=0):
-        add(name, 2 * ntok * N * K, 4 * (ntok * K + ntok * N * (2 if accumulate else 1) + N * K + table))
+        add(GEMM, 2 * ntok * N * K, 4 * (ntok * K + ntok * N * (2 if accumulate else 1) + N * K + table))
 
     for m in sp.mods:                                          # unify + position table
         gemm('mep_gemm', plan.ntok[m], D, sp.dims[m], table=plan.T[m] * D)

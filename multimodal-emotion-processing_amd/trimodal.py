@@ -610,7 +610,7 @@ class TriModalPlan:
         loss (row_loss, already scaled by 1/B); grad=True also runs the head backward
         (dpooled + head parameter partials) inside the same launch."""
         sp, nl = self.spec, self.spec.nl
-        launch('mep_unify', self.d_unify, self.t_unify, stream)
+        _lib.gemm('mep_unify', self.d_unify, self.t_unify, stream, prec=self.prec)
         if sp.unify_norm:
             launch('mep_layernorm_fwd', self.d_uln, cdiv(max(self.ntok.values()), 4), stream)
         for i in range(nl):

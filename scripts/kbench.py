@@ -27,6 +27,7 @@ def main():
     ap.add_argument('--dtype', default='fp32', choices=('fp32', 'bf16'))
     args = ap.parse_args()
     import bench
+    from mep_amd import _lib
     from mep_amd._lib import launch
     dev = torch.device('cuda:0')
     bench.T, bench.NL = args.T, args.layers
@@ -37,7 +38,7 @@ def main():
     D = p.spec.D
     pr = p.prec
     table = {
-        'mep_unify': lambda: launch('mep_unify', p.d_unify, p.t_unify),
+        'mep_unify': lambda: _lib.gemm('mep_unify', p.d_unify, p.t_unify, prec=pr),
         'mep_attn_fwd': lambda: launch('mep_attn_fwd', p.d_attn[0], p.t_attn[0], threads=p.g_attn[0][2] | pr),
         'mep_block_epi_fwd': lambda: launch('mep_block_epi_fwd', p.d_epi[0], p.t_epi[0], threads=D | pr),
         'mep_block_epi_bwd': lambda: launch('mep_block_epi_bwd', p.d_epib[0], p.t_epi[0], threads=D | pr),

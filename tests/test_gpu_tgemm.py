@@ -1,0 +1,114 @@
+"""mep_tgemm (csrc/tgemm.hip k_tgemm, the tiled split-bf16 token GEMM) against a float64 torch
+statement of the mep_gemm contract: the Unify_Dimension Linears (cmu-mosei/run.py:210-214,
+Ren-MME/run.py:161-166) on slot views of [B, 2, T, d] inputs with unaligned K (35, 74, 205: scalar
+X loads) and ragged token counts, the realformer Conv1d unify + position table
+(others/realformer.py:136-152), w_qkv with N = 2D = 192 (two N tiles), the input-gradient form
+with W stored [K][N] (w_nt = 0) accumulating onto y, bias + relu, and the bf16 path against
+torch's bf16-operand product."""
+import pytest
+import torch
+
+from tests.gpu_util import assert_close
+
+pytestmark = pytest.mark.gpu
+
+
+def _rows(t, T, sB, sT, off=0):
+    from mep_amd._lib import Rows
+    return Rows(ptr=t.data_ptr() + 4 * off, sB=sB, sT=sT, T=T)
+
+
+def _launch(descs, dev, prec=0):
+    from mep_amd import _lib
+    arr = _lib.DescArray(_lib.GemmDesc, descs, dev)
+    assert _lib.tgemm_ok(arr.items)
+    flags = prec | (0 if descs[0].w_nt else _lib.TGEMM_WT)
+    _lib.call('mep_tgemm', arr.ptr, arr.n, max(d.ntok for d in descs), max(d.N for d in descs), flags)
+    torch.cuda.synchronize()
+    return arr
+
+
+def _gd(x, y, w, ntok, N, K, ldw, w_nt=1, bias=None, table=None, accumulate=0, relu=0, alpha=1.0, bf16=0, ldt=0):
+    from mep_amd._lib import GemmDesc
+    return GemmDesc(x=x, y=y, w=w.data_ptr(), bias=bias.data_ptr() if bias is not None else 0,
+                    table=table.data_ptr() if table is not None else 0, ntok=ntok, N=N, K=K, ldw=ldw, w_nt=w_nt,
+                    accumulate=accumulate, relu=relu, alpha=alpha, bf16=bf16, ldt=ldt)
+
+
+@pytest.mark.parametrize('N,Ks,B,T', [
+    (96, (300, 35, 74), 64, 50),     # cmu-mosei cfg3: both slots, all three modalities in one launch
+    (128, (768, 640, 205), 4, 300),  # Ren-MME cfg5 widths
+    (32, (300, 35, 74), 3, 7),       # ragged: 21 tokens
+    (64, (17,), 5, 1),               # T = 1 rows, K < 32
+])
+def test_tgemm_unify_vs_float64(N, Ks, B, T, cuda):
+    torch.manual_seed(N + B + T)
+    xs = [torch.randn(B, 2, T, K, device=cuda) for K in Ks]
+    ws = [torch.randn(N, K, device=cuda) / K ** 0.5 for K in Ks]
+    ys = [[torch.full((B, T, N), float('nan'), device=cuda) for _ in range(2)] for _ in Ks]
+    descs = []
+    for i, (x, w) in enumerate(zip(xs, ws)):
+        K = x.shape[-1]
+        for e in range(2):
+            descs.append(_gd(_rows(x, T, 2 * T * K, K, e * T * K), _rows(ys[i][e], T, T * N, N), w, B * T, N, K, K))
+    keep = _launch(descs, cuda)
+    for i, (x, w) in enumerate(zip(xs, ws)):
+        for e in range(2):
+            want = x[:, e].double() @ w.double().t()
+            assert_close(ys[i][e], want, rtol=1e-5, atol_frac=1e-6, name='K%d slot%d' % (x.shape[-1], e))
+    del keep
+
+
+def test_tgemm_table_bias_relu_and_wide_n(cuda):
+    """Conv1d unify + position table; N = 192 ([W_k; W_v], two N tiles) with bias and relu."""
+    torch.manual_seed(11)
+    B, T, K = 8, 50, 300
+    x = torch.randn(B * T, K, device=cuda)
+    w = torch.randn(96, K, device=cuda) / K ** 0.5
+    tab = torch.randn(T, 96, device=cuda)
+    y = torch.empty(B * T, 96, device=cuda)
+    keep = _launch([_gd(_rows(x, T, T * K, K), _rows(y, T, T * 96, 96), w, B * T, 96, K, K, table=tab)], cuda)
+    want = (x.double() @ w.double().t()).view(B, T, 96) + tab.double()
+    assert_close(y.view(B, T, 96), want, rtol=1e-5, atol_frac=1e-6, name='table')
+    w2 = torch.randn(192, 96, device=cuda) / 96 ** 0.5
+    b2 = torch.randn(192, device=cuda)
+    y2 = torch.empty(B * T, 192, device=cuda)
+    keep2 = _launch([_gd(_rows(y, T, T * 96, 96), _rows(y2, T, T * 192, 192), w2, B * T, 192, 96, 96, bias=b2,
+                         relu=1)], cuda)
+    want2 = torch.relu(y.double() @ w2.double().t() + b2.double())
+    assert_close(y2, want2, rtol=1e-5, atol_frac=1e-6, name='N192 bias relu')
+    del keep, keep2
+
+
+def test_tgemm_transposed_weight_accumulate(cuda):
+    """dq_in += dQ W_q (W stored [K][N], w_nt = 0) and dkv_in = [dK | dV] [W_k; W_v] (K = 2D)."""
+    torch.manual_seed(12)
+    n, D = 3200, 96
+    dq = torch.randn(n, D, device=cuda)
+    wq = torch.randn(D, D, device=cuda) / D ** 0.5
+    base = torch.randn(n, D, device=cuda)
+    y = base.clone()
+    dkv = torch.randn(n, 2 * D, device=cuda)
+    wkv = torch.randn(2 * D, D, device=cuda) / D ** 0.5
+    y2 = torch.empty(n, D, device=cuda)
+    keep = _launch([_gd(_rows(dq, 50, 50 * D, D), _rows(y, 50, 50 * D, D), wq, n, D, D, D, w_nt=0, accumulate=1),
+                    _gd(_rows(dkv, 50, 100 * D, 2 * D), _rows(y2, 50, 50 * D, D), wkv, n, D, 2 * D, D, w_nt=0)], cuda)
+    assert_close(y, base.double() + dq.double() @ wq.double(), rtol=1e-5, atol_frac=1e-6, name='accumulate')
+    assert_close(y2, dkv.double() @ wkv.double(), rtol=1e-5, atol_frac=1e-6, name='K=2D')
+    del keep
+
+
+def test_tgemm_bf16_path(cuda):
+    """MEP_PREC_BF16: plain bf16 operands, fp32 accumulation -- torch's bf16-operand product."""
+    from mep_amd import _lib
+    torch.manual_seed(13)
+    B, T, K, N = 4, 300, 768, 128
+    x = torch.randn(B * T, K, device=cuda)
+    w = torch.randn(N, K, device=cuda) / K ** 0.5
+    y = torch.empty(B * T, N, device=cuda)
+    keep = _launch([_gd(_rows(x, T, T * K, K), _rows(y, T, T * N, N), w, B * T, N, K, K, bf16=1)], cuda,
+                   prec=_lib.PREC_BF16)
+    want = x.bfloat16().double() @ w.bfloat16().double().t()
+    assert_close(y, want, rtol=1e-4, atol_frac=1e-5, name='bf16')
+    assert (y.double() - x.double() @ w.double().t()).abs().max() > 1e-4, 'bf16 rounding did not happen'
+    del keep
