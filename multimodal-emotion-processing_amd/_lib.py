@@ -359,13 +359,17 @@ def attn_dc_slots(B, H, Tk):
 
 # ------------------------------------------------------------------ token GEMMs
 TGEMM = os.environ.get('MEP_TGEMM', '1') != '0'   # 0: the mep_unify / mep_gemm kernels (A/B runs)
+# mep_tgemm wins where the weight is too large for LDS-resident staging (Ren-MME unify, K = 768 /
+# 640: 153 -> 95 us at cfg5); at K <= 300 its per-32-column chunk latency loses to the
+# weight-stationary kernels (cmu-mosei unify 17 vs 24 us, realformer GEMMs 89 vs 110 us at cfg2)
+TGEMM_MIN_K = int(os.environ.get('MEP_TGEMM_MIN_K', '512'))
 TGEMM_WT = 0x1                                     # MEP_TGEMM_WT: every descriptor has w_nt = 0
 
 
 def tgemm_ok(items):
     """Can mep_tgemm run these GemmDescs (include/mep.h): N % 16 == 0 with N in {32, 64, 96} or
     >= 128, one w_nt for the launch, 16-byte aligned y rows, bias and table rows."""
-    if not items:
+    if not items or max(d.K for d in items) < TGEMM_MIN_K:
         return False
     if len({d.w_nt for d in items}) != 1:
         return False

@@ -9,8 +9,13 @@
 // written once, for the backward's weight gradients).  LayerNorms are wave-per-row shuffle
 // reductions.  D and FD are template parameters so every K loop is fully unrolled.
 #include "common.h"
+#include "split.h"
 
 using namespace mep;
+
+#ifndef MEP_RF_SPLIT
+#define MEP_RF_SPLIT 1   // the Linears on split-bf16 MFMA (split.h mma_tile_split); 0: f32 MFMA 32x32x2
+#endif
 
 namespace {
 
@@ -29,7 +34,14 @@ MEP_DEV void tile_gemm(const float* As, int lda, const gfloat* W, int ldw, bool 
     for (int t = wave; t < NTASK; t += NWAVE) {
         const int mh = t % MH, nblk = t / MH;
         floatx16 acc = zero16();
-        if constexpr (K <= 128) {
+        if constexpr (MEP_RF_SPLIT && K % 16 == 0 && (K <= 128 || (K / 2) % 16 == 0)) {
+            if constexpr (K <= 128) {
+                mma_tile_split<NT, K>(acc, As, lda, mh * 32, W, ldw, nblk * 32, N, 0, K, w_vec);
+            } else {
+                mma_tile_split<NT, K / 2>(acc, As, lda, mh * 32, W, ldw, nblk * 32, N, 0, K, w_vec);
+                mma_tile_split<NT, K / 2>(acc, As + K / 2, lda, mh * 32, W, ldw, nblk * 32, N, K / 2, K, w_vec);
+            }
+        } else if constexpr (K <= 128) {
             mma_tile_pf<NT, K>(acc, As, lda, mh * 32, W, ldw, nblk * 32, N, 0, K, w_vec);
         } else {   // two halves: at most 64 prefetch registers per pass
             mma_tile_pf<NT, K / 2>(acc, As, lda, mh * 32, W, ldw, nblk * 32, N, 0, K, w_vec);

@@ -21,7 +21,11 @@ def _rows(t, T, sB, sT, off=0):
 def _launch(descs, dev, prec=0):
     from mep_amd import _lib
     arr = _lib.DescArray(_lib.GemmDesc, descs, dev)
-    assert _lib.tgemm_ok(arr.items)
+    min_k, _lib.TGEMM_MIN_K = _lib.TGEMM_MIN_K, 0
+    try:
+        assert _lib.tgemm_ok(arr.items)
+    finally:
+        _lib.TGEMM_MIN_K = min_k
     flags = prec | (0 if descs[0].w_nt else _lib.TGEMM_WT)
     _lib.call('mep_tgemm', arr.ptr, arr.n, max(d.ntok for d in descs), max(d.N for d in descs), flags)
     torch.cuda.synchronize()
