@@ -23,6 +23,9 @@
 #ifndef MEP_EPI_SPLIT
 #define MEP_EPI_SPLIT 1   // D <= 96 on split-bf16 MFMA (0: exact fp32 MFMA everywhere)
 #endif
+#ifndef MEP_EPI_ONE
+#define MEP_EPI_ONE 0   // single-phase epilogues (both weights resident, intermediate in registers)
+#endif
 #ifndef MEP_EPI_SPLIT128
 #define MEP_EPI_SPLIT128 0   // D = 128 on split-bf16 MFMA: weights as 2 parts (the 3-part Wm needs 210 KB
                              // of LDS), activations 3 parts, five products per k pair
@@ -564,6 +567,253 @@ MEP_DEV void epi_bwd_split(const mep_epi_bwd_desc& bd, unsigned char* sm, int t_
     }
 }
 
+// ---------------------------------------------------------------- single-phase split epilogues
+// Both weights resident in LDS for the whole workgroup, one pass per tile: the first product's
+// accumulators (C[feature 16 i + 4g + r][token c]) are exactly the B fragments of the second
+// product's k blocks (lane (token c, g): features 16 i + 4g .. +3), so xp (forward) and dxp
+// (backward) go from accumulators to operands in registers -- no store-and-reload of the
+// intermediate, one staging, no second phase.  Parts per weight (NWP, NWM) are chosen so both fit
+// the 160 KB of LDS: D = 96 keeps Wp as two parts (forward; 43 + 120 KB) and Wm^T as two parts
+// (backward; 86 + 65 KB) -- a 2^-18 relative representation error of that weight.
+template <int D, int NPART, int NWP, int NWM>
+MEP_DEV void epi_fwd_one(const mep_epi_desc& d, unsigned char* sm, int t_begin, int t_end) {
+    constexpr int NI = D / 16, KB = D / 16, NP = D / 32;
+    using WP = SplitW<D, NP, NWP>;
+    using WM = SplitW<D, 2 * NP, NWM>;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int c = lane & 15, g = lane >> 4;
+    const int ntok = d.ntok;
+    const float p = d.drop_p;
+    const uint64_t seed = (d.seed && p > 0.f) ? *G<const uint64_t>(d.seed) : 0;
+    const uint64_t tok0 = (d.seed && p > 0.f) ? G<const uint64_t>(d.seed)[1] * (uint64_t)d.q.T : 0;
+    gfloat* stats = G<float>(d.stats);
+    typedef __attribute__((address_space(3))) unsigned char lbyte;
+    const WP wp{(lbyte*)sm, 0};
+    const WM wm{(lbyte*)sm + WP::BYTES, 0};
+    f32x4 ab[KB], bb[KB];            // one tile ahead: x and q rows
+    auto rows_of = [&](const mep_rows& v, int tile, f32x4 (&dst)[KB]) {
+        const gfloat* r = row_ptr(v, min(tile * 16 + c, ntok - 1)) + 4 * g;
+#pragma unroll
+        for (int kb = 0; kb < KB; ++kb) dst[kb] = ld4w(r + 16 * kb);
+    };
+    if (t_begin + wave < t_end) { rows_of(d.x, t_begin + wave, ab); rows_of(d.q, t_begin + wave, bb); }
+    stage_split_rows<D, D, NWP>(wp, G<const float>(d.wp));
+    stage_split_rows<D, 2 * D, NWM>(wm, G<const float>(d.wm));
+    __syncthreads();
+    for (int tile = t_begin + wave; tile < t_end; tile += EWAVES) {
+        const int tok = tile * 16 + c;
+        f32x4 xp[NI], z[NI];
+#pragma unroll
+        for (int i = 0; i < NI; ++i) { xp[i] = zero_f4(); z[i] = zero_f4(); }
+        {
+            OpN<NPART> xs[NP];
+#pragma unroll
+            for (int pp = 0; pp < NP; ++pp) xs[pp] = opn<NPART>(ab[2 * pp], ab[2 * pp + 1]);
+            if (tile + EWAVES < t_end) rows_of(d.x, tile + EWAVES, ab);
+            tgemm_n<NI, NP, NPART, NWP>(xp, [&](int i, int pp) { return wp.frag(i, pp); }, [&](int pp) { return xs[pp]; });
+        }
+        OpN<NPART> qs[NP];
+#pragma unroll
+        for (int pp = 0; pp < NP; ++pp) qs[pp] = opn<NPART>(bb[2 * pp], bb[2 * pp + 1]);
+        if (tile + EWAVES < t_end) rows_of(d.q, tile + EWAVES, bb);
+        if (p > 0.f) {
+#pragma unroll
+            for (int i = 0; i < NI; ++i)
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                    xp[i][r] *= drop_scale(seed, 2u * d.drop_stream, (tok0 + (uint64_t)tok) * D + 16 * i + 4 * g + r, p);
+        }
+        OpN<NPART> ps[NP];
+#pragma unroll
+        for (int pp = 0; pp < NP; ++pp) ps[pp] = opn<NPART>(xp[2 * pp], xp[2 * pp + 1]);
+        tgemm_n<NI, NP, NPART, NWM>(z, [&](int i, int pp) { return wm.frag(i, pp); }, [&](int pp) { return qs[pp]; });
+        tgemm_n<NI, NP, NPART, NWM>(z, [&](int i, int pp) { return wm.frag(i, NP + pp); }, [&](int pp) { return ps[pp]; });
+        float sum = 0.f;
+#pragma unroll
+        for (int i = 0; i < NI; ++i) sum += (z[i][0] + z[i][1]) + (z[i][2] + z[i][3]);
+        sum += __shfl_xor(sum, 16, 64);
+        sum += __shfl_xor(sum, 32, 64);
+        const float mean = sum / (float)D;
+        float var = 0.f;
+#pragma unroll
+        for (int i = 0; i < NI; ++i)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) { const float t = z[i][r] - mean; var += t * t; }
+        var += __shfl_xor(var, 16, 64);
+        var += __shfl_xor(var, 32, 64);
+        const float rstd = 1.0f / sqrtf(var / (float)D + LN_EPS);
+        if (tok < ntok) {
+            gfloat* zr = row_ptr(d.z, tok);
+            gfloat* orow = row_ptr(d.out, tok);
+            gfloat* pr = row_ptr(d.xp, tok);
+#pragma unroll
+            for (int i = 0; i < NI; ++i) {
+                const int col = 16 * i + 4 * g;
+                const f32x4 w = ld4w(G<const float>(d.ln_w) + col), b = ld4w(G<const float>(d.ln_b) + col);
+                f32x4 y;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    y[r] = (z[i][r] - mean) * rstd * w[r] + b[r];
+                    if (p > 0.f) y[r] *= drop_scale(seed, 2u * d.drop_stream + 1u, (tok0 + (uint64_t)tok) * D + col + r, p);
+                }
+                stg4(pr + col, f4(xp[i]));
+                stg4(zr + col, f4(z[i]));
+                stg4(orow + col, f4(y));
+            }
+            if (g == 0) { stats[2 * tok] = mean; stats[2 * tok + 1] = rstd; }
+        }
+    }
+}
+
+template <int D, int NPART, int NWP, int NWM>
+MEP_DEV void epi_bwd_one(const mep_epi_bwd_desc& bd, unsigned char* sm, int t_begin, int t_end) {
+    constexpr int NI = D / 16, KB = D / 16, NP = D / 32;
+    using WMT = SplitW<2 * D, NP, NWM>;
+    using WPT = SplitW<D, NP, NWP>;
+    using Op = OpN<NPART>;
+    const mep_epi_desc& d = bd.f;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int c = lane & 15, g = lane >> 4;
+    const int ntok = d.ntok;
+    const float p = d.drop_p;
+    const uint64_t seed = (d.seed && p > 0.f) ? *G<const uint64_t>(d.seed) : 0;
+    const uint64_t tok0 = (d.seed && p > 0.f) ? G<const uint64_t>(d.seed)[1] * (uint64_t)d.q.T : 0;
+    const gfloat* stats = G<const float>(d.stats);
+    gfloat* lpart = G<float>(bd.ln_partial);
+    typedef __attribute__((address_space(3))) unsigned char lbyte;
+    const WMT wmt{(lbyte*)sm, 0};
+    const WMT wmt_x{(lbyte*)sm, D};
+    const WPT wpt{(lbyte*)sm + WMT::BYTES, 0};
+    f32x4 ga[KB], zb[KB];            // one tile ahead: dout (+ dout2) and z rows
+    float mean = 0.f, rstd = 0.f;
+    const Upstream up(bd);
+    auto fetch1 = [&](int tile) {
+        const int tc = min(tile * 16 + c, ntok - 1);
+        const gfloat* zr = row_ptr(d.z, tc) + 4 * g;
+#pragma unroll
+        for (int kb = 0; kb < KB; ++kb) ga[kb] = up.at(bd, tc, 16 * kb + 4 * g);
+#pragma unroll
+        for (int kb = 0; kb < KB; ++kb) zb[kb] = ld4w(zr + 16 * kb);
+        mean = stats[2 * tc];
+        rstd = stats[2 * tc + 1];
+    };
+    if (t_begin + wave < t_end) fetch1(t_begin + wave);
+    stage_split_cols<D, 2 * D, NWM>(wmt, G<const float>(d.wm));
+    stage_split_cols<D, D, NWP>(wpt, G<const float>(d.wp));
+    __syncthreads();
+    for (int tile = t_begin + wave; tile < t_end; tile += EWAVES) {
+        const int tok = tile * 16 + c;
+        const bool ok = tok < ntok;
+        const int tc = min(tok, ntok - 1);
+        f32x4 dz[NI], zz[NI];
+        const float mu = mean, rs = rstd;
+#pragma unroll
+        for (int i = 0; i < NI; ++i) { dz[i] = ga[i]; zz[i] = zb[i]; }
+        if (bd.dout2.ptr) {
+            const gfloat* g2 = row_ptr(bd.dout2, tc) + 4 * g;
+#pragma unroll
+            for (int i = 0; i < NI; ++i) dz[i] += ld4w(g2 + 16 * i);
+        }
+        if (tile + EWAVES < t_end) fetch1(tile + EWAVES);
+        float s1 = 0.f, s2 = 0.f;
+        gfloat* lp = lpart ? lpart + (int64_t)tile * 2 * D : nullptr;
+#pragma unroll
+        for (int i = 0; i < NI; ++i) {
+            const int col = 16 * i + 4 * g;
+            const f32x4 w = ld4w(G<const float>(d.ln_w) + col);
+            f32x4 pw, pb;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                float gg = dz[i][r];
+                if (p > 0.f) gg *= drop_scale(seed, 2u * d.drop_stream + 1u, (tok0 + (uint64_t)tok) * D + col + r, p);
+                gg = ok ? gg : 0.f;
+                const float x = (zz[i][r] - mu) * rs;
+                const float gw = gg * w[r];
+                s1 += gw;
+                s2 += gw * x;
+                pw[r] = row16_sum(gg * x);
+                pb[r] = row16_sum(gg);
+                dz[i][r] = gw;
+            }
+            if (lp && c == 0) {
+                stg4(lp + col, f4(pw));
+                stg4(lp + D + col, f4(pb));
+            }
+        }
+        s1 += __shfl_xor(s1, 16, 64);
+        s1 += __shfl_xor(s1, 32, 64);
+        s2 += __shfl_xor(s2, 16, 64);
+        s2 += __shfl_xor(s2, 32, 64);
+        s1 /= (float)D;
+        s2 /= (float)D;
+#pragma unroll
+        for (int i = 0; i < NI; ++i)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const float x = (zz[i][r] - mu) * rs;
+                dz[i][r] = ok ? rs * (dz[i][r] - s1 - x * s2) : 0.f;
+            }
+        Op dzb[NP];
+#pragma unroll
+        for (int pp = 0; pp < NP; ++pp) dzb[pp] = opn<NPART>(dz[2 * pp], dz[2 * pp + 1]);
+        f32x4 acc[NI];
+#pragma unroll
+        for (int i = 0; i < NI; ++i) acc[i] = zero_f4();
+        tgemm_n<NI, NP, NPART, NWM>(acc, [&](int i, int pp) { return wmt_x.frag(i, pp); }, [&](int pp) { return dzb[pp]; });
+        if (p > 0.f) {
+#pragma unroll
+            for (int i = 0; i < NI; ++i)
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                    acc[i][r] *= drop_scale(seed, 2u * d.drop_stream, (tok0 + (uint64_t)tok) * D + 16 * i + 4 * g + r, p);
+        }
+        // dx = dxp Wp from the dxp accumulators (tokens past ntok: dz = 0, so dxp = 0)
+        Op xs[NP];
+#pragma unroll
+        for (int pp = 0; pp < NP; ++pp) xs[pp] = opn<NPART>(acc[2 * pp], acc[2 * pp + 1]);
+        if (ok) {
+            gfloat* dzr = row_ptr(bd.dz, tok);
+            gfloat* dpr = row_ptr(bd.dxp, tok);
+#pragma unroll
+            for (int i = 0; i < NI; ++i) {
+                stg4(dzr + 16 * i + 4 * g, f4(dz[i]));
+                stg4(dpr + 16 * i + 4 * g, f4(acc[i]));
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < NI; ++i) acc[i] = zero_f4();
+        tgemm_n<NI, NP, NPART, NWM>(acc, [&](int i, int pp) { return wmt.frag(i, pp); }, [&](int pp) { return dzb[pp]; });
+        if (ok) {
+            gfloat* qrw = row_ptr(bd.dq, tok);
+#pragma unroll
+            for (int i = 0; i < NI; ++i) {
+                f32x4 v = acc[i];
+                if (bd.dq_accumulate) v += ld4w(qrw + 16 * i + 4 * g);
+                stg4(qrw + 16 * i + 4 * g, f4(v));
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < NI; ++i) acc[i] = zero_f4();
+        tgemm_n<NI, NP, NPART, NWP>(acc, [&](int i, int pp) { return wpt.frag(i, pp); }, [&](int pp) { return xs[pp]; });
+        if (ok) {
+            gfloat* xrw = row_ptr(bd.dx, tok);
+#pragma unroll
+            for (int i = 0; i < NI; ++i) stg4(xrw + 16 * i + 4 * g, f4(acc[i]));
+        }
+    }
+}
+
+// parts per weight of the single-phase epilogues (0: the two-phase kernels)
+template <int D, bool BF16> struct EpiOne {
+    static constexpr bool ON = MEP_EPI_ONE && D <= 96;
+    static constexpr int NPART = BF16 ? 1 : 3;
+    static constexpr int FWD_WP = BF16 ? 1 : (D == 96 ? 2 : 3), FWD_WM = NPART;
+    static constexpr int BWD_WP = NPART, BWD_WM = BF16 ? 1 : (D == 96 ? 2 : 3);
+    static constexpr int FWD_BYTES = SplitW<D, D / 32, FWD_WP>::BYTES + SplitW<D, D / 16, FWD_WM>::BYTES;
+    static constexpr int BWD_BYTES = SplitW<2 * D, D / 32, BWD_WM>::BYTES + SplitW<D, D / 32, BWD_WP>::BYTES;
+    static_assert(!ON || (FWD_BYTES <= 163840 && BWD_BYTES <= 163840), "single-phase weights exceed the LDS");
+};
+
 // BF16: the bf16 path (one part per operand, every D); otherwise D <= 96 runs the 3-part split
 // and D = 128 the fp32 MFMA path
 template <int D, bool BF16>
@@ -572,6 +822,12 @@ __global__ __launch_bounds__(ETHREADS) void k_epi_fwd(const mep_epi_desc* __rest
     const mep_epi_desc& d = descs[blockIdx.y];
     int t_begin, t_end;
     if (!tile_range(d.ntok, t_begin, t_end)) return;   // whole workgroup
+    if constexpr (EpiOne<D, BF16>::ON) {
+        using E = EpiOne<D, BF16>;
+        __shared__ __attribute__((aligned(16))) unsigned char sm1[E::FWD_BYTES];
+        epi_fwd_one<D, E::NPART, E::FWD_WP, E::FWD_WM>(d, sm1, t_begin, t_end);
+        return;
+    }
     if constexpr (BF16 || (MEP_EPI_SPLIT && D <= 96) || (MEP_EPI_SPLIT128 && D == 128)) {
         constexpr int NPART = BF16 ? 1 : 3, NW = BF16 ? 1 : (D == 128 ? 2 : 3);
         constexpr int BYTES = SplitW<D, D / 16, NW>::BYTES;   // the larger phase (Wm)
@@ -727,6 +983,12 @@ __global__ __launch_bounds__(ETHREADS) void k_epi_bwd(const mep_epi_bwd_desc* __
     const mep_epi_desc& d = bd.f;
     int t_begin, t_end;
     if (!tile_range(d.ntok, t_begin, t_end)) return;
+    if constexpr (EpiOne<D, BF16>::ON) {
+        using E = EpiOne<D, BF16>;
+        __shared__ __attribute__((aligned(16))) unsigned char sm1[E::BWD_BYTES];
+        epi_bwd_one<D, E::NPART, E::BWD_WP, E::BWD_WM>(bd, sm1, t_begin, t_end);
+        return;
+    }
     if constexpr (BF16 || (MEP_EPI_SPLIT && D <= 96) || (MEP_EPI_SPLIT128 && D == 128)) {
         constexpr int NPART = BF16 ? 1 : 3, NW = BF16 ? 1 : (D == 128 ? 2 : 3);
         constexpr int BYTES = SplitW<2 * D, D / 32, NW>::BYTES;   // the larger phase (Wm^T)
