@@ -95,6 +95,9 @@ int mep_unify(const mep_gemm_desc* descs, int n_desc, int n_wg, mep_stream_t str
  * w_nt = 0, W stored [K][N]); y rows (and bias) 16-byte aligned; N in {32, 64, 96} or >= 128.
  * Grid: (ceil(max_ntok / 128), n_desc, N tiles). */
 #define MEP_TGEMM_WT 0x1
+#define MEP_TGEMM_RESIDENT 0x2   /* every K <= 320: the whole weight tile (N tiles of 96) staged in LDS
+                                    once per workgroup, as 2 bf16 parts on the fp32 path (five
+                                    products per k pair, weight error <= 2^-18 relative) */
 int mep_tgemm(const mep_gemm_desc* descs, int n_desc, int max_ntok, int max_n, int flags, mep_stream_t stream);
 
 /* ---------------------------------------------------------------- weight-gradient GEMM

@@ -359,30 +359,40 @@ def attn_dc_slots(B, H, Tk):
 
 # ------------------------------------------------------------------ token GEMMs
 TGEMM = os.environ.get('MEP_TGEMM', '1') != '0'   # 0: the mep_unify / mep_gemm kernels (A/B runs)
-# mep_tgemm wins where the weight is too large for LDS-resident staging (Ren-MME unify, K = 768 /
-# 640: 153 -> 95 us at cfg5); at K <= 300 its per-32-column chunk latency loses to the
-# weight-stationary kernels (cmu-mosei unify 17 vs 24 us, realformer GEMMs 89 vs 110 us at cfg2)
+TGEMM_RES = os.environ.get('MEP_TGEMM_RES', '1') != '0'   # 0: no resident-weight launches (A/B runs)
+# mep_tgemm chunked (K in 32-wide LDS stages) wins where the weight is too large to keep resident
+# (Ren-MME unify, K = 768 / 640: 153 -> 95 us at cfg5); at K <= 300 its per-chunk staging latency
+# loses to weight-stationary kernels, so there the resident-weight form runs (K <= 320)
 TGEMM_MIN_K = int(os.environ.get('MEP_TGEMM_MIN_K', '512'))
+TGEMM_RES_MAX_K = 320                              # csrc/tgemm.hip TGR_KP * 32
 TGEMM_WT = 0x1                                     # MEP_TGEMM_WT: every descriptor has w_nt = 0
+TGEMM_RESIDENT = 0x2                               # MEP_TGEMM_RESIDENT
+
+
+def tgemm_mode(items):
+    """Which mep_tgemm form can run these GemmDescs (include/mep.h): 'resident' (every K <= 320),
+    'chunked' (some K >= TGEMM_MIN_K) or None (the mep_unify / mep_gemm kernels).  Needs N % 16 == 0
+    with N in {32, 64, 96} or >= 128, one w_nt for the launch, 16-byte aligned y rows, bias and
+    table rows."""
+    if not TGEMM or not items or len({d.w_nt for d in items}) != 1:
+        return None
+    for d in items:
+        if d.N % 16 or not (d.N in (32, 64, 96) or d.N >= 128):
+            return None
+        if d.y.ptr % 16 or d.y.sB % 4 or d.y.sT % 4 or d.bias % 16:
+            return None
+        if d.table and (d.table % 16 or (d.ldt or d.N) % 4):
+            return None
+        if d.ntok <= 0 or d.K <= 0:
+            return None
+    kmax = max(d.K for d in items)
+    if TGEMM_RES and kmax <= TGEMM_RES_MAX_K:
+        return 'resident'
+    return 'chunked' if kmax >= TGEMM_MIN_K else None
 
 
 def tgemm_ok(items):
-    """Can mep_tgemm run these GemmDescs (include/mep.h): N % 16 == 0 with N in {32, 64, 96} or
-    >= 128, one w_nt for the launch, 16-byte aligned y rows, bias and table rows."""
-    if not items or max(d.K for d in items) < TGEMM_MIN_K:
-        return False
-    if len({d.w_nt for d in items}) != 1:
-        return False
-    for d in items:
-        if d.N % 16 or not (d.N in (32, 64, 96) or d.N >= 128):
-            return False
-        if d.y.ptr % 16 or d.y.sB % 4 or d.y.sT % 4 or d.bias % 16:
-            return False
-        if d.table and (d.table % 16 or (d.ldt or d.N) % 4):
-            return False
-        if d.ntok <= 0 or d.K <= 0:
-            return False
-    return True
+    return tgemm_mode(items) is not None
 
 
 def gemm(name, descs, max_tiles, stream=None, prec=0):
@@ -391,8 +401,10 @@ def gemm(name, descs, max_tiles, stream=None, prec=0):
     for the bf16 path (mep_unify reads the per-descriptor bf16 field instead)."""
     if descs.n == 0:
         return
-    if TGEMM and tgemm_ok(descs.items):
+    mode = tgemm_mode(descs.items)
+    if mode is not None:
         flags = (prec & PREC_BF16) | (0 if descs.items[0].w_nt else TGEMM_WT)
+        flags |= TGEMM_RESIDENT if mode == 'resident' else 0
         if any(d.bf16 for d in descs.items):
             flags |= PREC_BF16
         call('mep_tgemm', descs.ptr, descs.n, max(d.ntok for d in descs.items), max(d.N for d in descs.items),
@@ -403,4 +415,4 @@ def gemm(name, descs, max_tiles, stream=None, prec=0):
 
 def gemm_launcher(name, descs):
     """Launch name a gemm() call is timed under (bench.py / roofline.py)."""
-    return 'mep_tgemm' if TGEMM and tgemm_ok(descs.items) else name
+    return 'mep_tgemm' if tgemm_ok(descs.items) else name
