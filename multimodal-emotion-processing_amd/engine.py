@@ -12,8 +12,11 @@ large-batch semantics).  Two scalings give that mean:
     grad_scale 1/world in the optimizer.
 Ren-MME R-Drop pairs are whole units of a shard (mep_amd.dp), so they never straddle ranks.
 With the nccl (= RCCL) backend the SUM is captured inside the step's hipGraph between the
-backward and the optimizer (one graph launch per step); with gloo (CPU tests) it is a host call
-between two graph replays.
+backward and the optimizer (one graph launch per step), in two buckets of the flat buffer
+(FlatParams.split): bucket A -- block weights, block LayerNorms and the fusion head, 86 % of the
+gradient, complete after the last epilogue backward -- is all-reduced on a side stream while the
+last attention backward, the per-modality sums and the unify weight gradients run; bucket B after
+them.  With gloo (CPU tests) the SUM is a host call between two graph replays.
 """
 import ctypes
 import os
@@ -44,6 +47,11 @@ class TrainEngine:
             env = os.environ.get('MEP_CAPTURE_ALLREDUCE')
             capture_allreduce = (env != '0') if env is not None else backend == 'nccl'
         self.capture_allreduce = bool(capture_allreduce) and self.collective and backend == 'nccl'
+        # RCCL: bucket A of the flat gradient (FlatParams.split) is all-reduced on a side stream
+        # while the rest of the backward runs (plans with backward_bucketed)
+        env = os.environ.get('MEP_DP_OVERLAP')
+        self.overlap = self.collective and backend == 'nccl' and (env != '0' if env is not None else True)
+        self._side = None
         self._graphs = {}
         self._initial_broadcast = self.world > 1
 
@@ -59,6 +67,33 @@ class TrainEngine:
             plan.advance_seed()
         plan.forward(grad=True, rdrop=self.rdrop)
         plan.backward()
+
+    def _fwd_bwd_allreduce(self, plan, runner):
+        """forward + backward + the gradient all-reduce; with overlap the first bucket's SUM runs
+        on a side stream behind the last attention backward and the unify weight gradients"""
+        if not (self.overlap and hasattr(plan, 'backward_bucketed')):
+            self._fwd_bwd(plan)
+            self._allreduce(runner)
+            return
+        flat = runner.flat
+        a_end, n = flat.split, flat.n_grad
+        if self._side is None:
+            self._side = torch.cuda.Stream(device=flat.buf.device)
+        side = self._side
+        main = torch.cuda.current_stream()
+
+        def bucket_a_done():
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                if a_end > 0:
+                    dist.all_reduce(flat.grad[:a_end], op=dist.ReduceOp.SUM, group=self.pg)
+        if plan._drop > 0.0:
+            plan.advance_seed()
+        plan.forward(grad=True, rdrop=self.rdrop)
+        plan.backward_bucketed(bucket_a_done)
+        if n > a_end:
+            dist.all_reduce(flat.grad[a_end:n], op=dist.ReduceOp.SUM, group=self.pg)
+        main.wait_stream(side)
 
     def _opt(self):
         self.opt.fused_step()
@@ -87,14 +122,12 @@ class TrainEngine:
         key = id(plan)
         g = self._graphs.get(key)
         if not self.graph:
-            self._fwd_bwd(plan)
-            self._allreduce(runner)
+            self._fwd_bwd_allreduce(plan, runner)
             self._opt()
             return plan.loss
         if g is None:
             # first step eagerly (loads every kernel), then capture for the next ones
-            self._fwd_bwd(plan)
-            self._allreduce(runner)
+            self._fwd_bwd_allreduce(plan, runner)
             self._opt()
             torch.cuda.synchronize()
             split = self.collective and not self.capture_allreduce
@@ -103,10 +136,9 @@ class TrainEngine:
                 try:
                     ga = torch.cuda.CUDAGraph()
                     with torch.cuda.graph(ga):
-                        self._fwd_bwd(plan)
-                        # RCCL all-reduce captured between the backward and the optimizer: one
-                        # graph launch per step
-                        self._allreduce(runner)
+                        # RCCL all-reduce captured between the backward and the optimizer (its
+                        # first bucket overlapping the end of the backward): one graph launch
+                        self._fwd_bwd_allreduce(plan, runner)
                         self._opt()
                 except RuntimeError as e:
                     if not self.collective:

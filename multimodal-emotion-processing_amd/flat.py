@@ -14,22 +14,32 @@ ALIGN = 4  # floats: keep every parameter 16-byte aligned for vector loads
 
 
 class FlatParams:
-    def __init__(self, module, device, no_grad=()):
+    def __init__(self, module, device, no_grad=(), first=None):
+        """first: predicate on parameter names placed at the front of the buffer (a gradient
+        bucket whose all-reduce can start before the rest of the backward; ``split`` = its end)"""
         self.device = torch.device(device)
         named = list(module.named_parameters())
         self.names = [n for n, _ in named]
         self.params = dict(named)
         no_grad = set(no_grad)
-        order = [n for n in self.names if n not in no_grad] + [n for n in self.names if n in no_grad]
+        grad = [n for n in self.names if n not in no_grad]
+        if first is not None:
+            grad = [n for n in grad if first(n)] + [n for n in grad if not first(n)]
+        order = grad + [n for n in self.names if n in no_grad]
         self.offsets, off = {}, 0
         self.n_grad = None
+        self.split = None
         for n in order:
+            if first is not None and self.split is None and (n in no_grad or not first(n)):
+                self.split = off
             if n in no_grad and self.n_grad is None:
                 self.n_grad = off
             self.offsets[n] = off
             off += (self.params[n].numel() + ALIGN - 1) // ALIGN * ALIGN
         if self.n_grad is None:
             self.n_grad = off
+        if self.split is None:
+            self.split = self.n_grad
         self.total = off
         self.has_grad = {n: n not in no_grad for n in self.names}
         self.buf = torch.zeros(self.total, dtype=torch.float32, device=self.device)

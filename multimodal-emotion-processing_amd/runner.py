@@ -21,7 +21,10 @@ class ModelRunner:
         self.spec = spec
         self.device = torch.device(device)
         self.labels_float = labels_float
-        self.flat = FlatParams(model, self.device, no_grad=spec.no_grad_params())
+        # gradient bucket A first (the block weights, LayerNorms and the fusion head: ready after the
+        # last epilogue backward), so a data-parallel all-reduce of it overlaps the attention
+        # backward and the unify weight gradients (engine.py)
+        self.flat = FlatParams(model, self.device, no_grad=spec.no_grad_params(), first=spec.bucket_a)
         self.plans = {}
         # dropout state shared by every plan of this model: {seed, row0}.  One seed stream per
         # model (not per plan shape), advanced once per training step -- also by an empty

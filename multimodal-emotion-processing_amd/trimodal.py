@@ -56,6 +56,31 @@ def wgrad_geometry(N, ktot):
     return mt, kt, cdiv(cdiv(ktot, 32), kt)
 
 
+def _wgrad_units(items):
+    units = []
+    for i, (_, N, n, bs, _) in enumerate(items):
+        mt, kt, ncg = wgrad_geometry(N, sum(b[1] for b in bs))
+        for cg in range(ncg):
+            if n > 0:
+                units.append((i, cg, n))
+    return units
+
+
+def wgrad_chunk(items, n_wg=WG_TARGET):
+    """The smallest multiple of 8 tokens per segment that keeps the items' launch within n_wg
+    workgroups."""
+    items = [tuple(it) + (0,) * (5 - len(it)) for it in items]
+    units = _wgrad_units(items)
+    lo, hi = 1, cdiv(max([n for (_, _, n) in units] or [8]), 8)   # in units of 8 tokens
+    while lo < hi:                        # the segment count only falls as the chunk grows
+        mid = (lo + hi) // 2
+        if sum(cdiv(n, 8 * mid) for (_, _, n) in units) <= n_wg:
+            hi = mid
+        else:
+            lo = mid + 1
+    return 8 * lo
+
+
 def wgrad_segments(items, n_wg=WG_TARGET, tok_per_split=None):
     """Split every (item, column group) token span into segments of at most tok_per_split tokens,
     one segment per workgroup; tok_per_split None: the smallest multiple of 8 that keeps the launch
@@ -65,21 +90,9 @@ def wgrad_segments(items, n_wg=WG_TARGET, tok_per_split=None):
     is bound by HBM traffic and the operand-load rate, so more, smaller segments only add setup
     and partial-reduction work (~10 us per workgroup, scripts/wgrad_trace.py).
     -> (per-workgroup segment lists [(item, cg, t0, t1, slot)], slots per item)."""
-    units = []
-    for i, (_, N, n, bs, _) in enumerate(items):
-        mt, kt, ncg = wgrad_geometry(N, sum(b[1] for b in bs))
-        for cg in range(ncg):
-            if n > 0:
-                units.append((i, cg, n))
+    units = _wgrad_units(items)
     if tok_per_split is None:
-        lo, hi = 1, cdiv(max([n for (_, _, n) in units] or [8]), 8)   # in units of 8 tokens
-        while lo < hi:                        # the segment count only falls as the chunk grows
-            mid = (lo + hi) // 2
-            if sum(cdiv(n, 8 * mid) for (_, _, n) in units) <= n_wg:
-                hi = mid
-            else:
-                lo = mid + 1
-        tok_per_split = 8 * lo
+        tok_per_split = wgrad_chunk(items, n_wg)
     bins = []
     for (i, cg, n) in units:
         tps = tok_per_split[i] if isinstance(tok_per_split, (list, tuple)) else tok_per_split
@@ -229,6 +242,16 @@ class TriModalSpec:
         self.head_norm = 'norm3' if variant == 'ren' else 'norm1'
         self.drop_p = float(drop_p)
         self.prefixes = ('intensity.', 'stimulation.')
+
+    @staticmethod
+    def bucket_a(name):
+        """Parameters whose gradients are complete after the last epilogue backward: the blocks'
+        proj / minus / LayerNorm weights and the fusion head (its gradient partials come from the
+        forward's fused head kernel).  The rest -- unify weights (+ Ren-MME's unify LayerNorm) and
+        the residual coefficients c (attention backward) -- is bucket B."""
+        if 'multimodal_blocks.' in name:
+            return not name.endswith('.c')
+        return 'unify_dimension.' not in name
 
     def no_grad_params(self):
         """c of the first layer of every chain never receives a gradient (scores is None)."""
@@ -528,27 +551,34 @@ class TriModalPlan:
                 items.append((crows(src, self.T[m], D), D, self.ntok[m],
                               [(self._in_rows(e, m), d, g(pre + UNIFY_NAMES[m] + '.weight'), d)]))
         self._wgrad_items = items
+        self._n_block_items = 2 * len(self.blocks)   # items[:n]: block weights (bucket A)
         self.wg_partial, self.d_wgrad, self.t_wgrad, self.t_wgred = make_wgrad(items, dev, bf16=self.bf16)
         # column sums: block LayerNorms, residual coefficients, Ren unify LayerNorm
-        cs = []
+        cs, self._colsum_a, self._colsum_b = [], [], []
         for blk in self.blocks:
             nt = blk['ln_partial'].shape[0]
             base = blk['ln_partial'].data_ptr()
             nm = blk['pre'] + sp.block_norm
-            cs.append(ColsumDesc(partial=base, out=g(nm + '.weight'), n_rows=nt, n_cols=D, ld=2 * D, accumulate=0))
-            cs.append(ColsumDesc(partial=base + 4 * D, out=g(nm + '.bias'), n_rows=nt, n_cols=D, ld=2 * D,
-                                 accumulate=0))
+            for c_ in (ColsumDesc(partial=base, out=g(nm + '.weight'), n_rows=nt, n_cols=D, ld=2 * D, accumulate=0),
+                       ColsumDesc(partial=base + 4 * D, out=g(nm + '.bias'), n_rows=nt, n_cols=D, ld=2 * D,
+                                  accumulate=0)):
+                cs.append(c_)
+                self._colsum_a.append(c_)
             if 'dc_partial' in blk:
-                cs.append(ColsumDesc(partial=blk['dc_partial'].data_ptr(), out=g(blk['pre'] + 'c'),
-                                     n_rows=blk['dc_partial'].numel(), n_cols=1, ld=1, accumulate=0))
+                c_ = ColsumDesc(partial=blk['dc_partial'].data_ptr(), out=g(blk['pre'] + 'c'),
+                                n_rows=blk['dc_partial'].numel(), n_cols=1, ld=1, accumulate=0)
+                cs.append(c_)
+                self._colsum_b.append(c_)
         if sp.unify_norm:
             for e in range(2):
                 pre = sp.prefixes[e] + 'unify_dimension.norm1.'
                 p = self.uln_partial[e]
-                cs.append(ColsumDesc(partial=p.data_ptr(), out=g(pre + 'weight'), n_rows=p.shape[0], n_cols=D,
-                                     ld=2 * D, accumulate=0))
-                cs.append(ColsumDesc(partial=p.data_ptr() + 4 * D, out=g(pre + 'bias'), n_rows=p.shape[0],
-                                     n_cols=D, ld=2 * D, accumulate=0))
+                for c_ in (ColsumDesc(partial=p.data_ptr(), out=g(pre + 'weight'), n_rows=p.shape[0], n_cols=D,
+                                      ld=2 * D, accumulate=0),
+                           ColsumDesc(partial=p.data_ptr() + 4 * D, out=g(pre + 'bias'), n_rows=p.shape[0],
+                                      n_cols=D, ld=2 * D, accumulate=0)):
+                    cs.append(c_)
+                    self._colsum_b.append(c_)
         self.d_colsum = DescArray(ColsumDesc, cs, dev)
         self.t_colsum = cdiv(D, 32)
         hn = sp.head_norm
@@ -648,6 +678,51 @@ class TriModalPlan:
 
     def advance_seed(self, stream=None):
         _lib.call('mep_seed_advance', ctypes.c_void_p(self.seed.data_ptr()), stream=stream)
+
+    def _build_buckets(self):
+        """Weight-gradient and reduction launches split by gradient bucket (FlatParams.split):
+        A = block weights + block LayerNorms + fusion head, B = unify weights (+ unify LayerNorm)
+        + residual coefficients.  Both launches keep the fused launch's token chunk, so every
+        gradient is the same sum in the same order, bit for bit."""
+        if getattr(self, '_buckets', None) is not None:
+            return
+        dev, items, nb = self.device, self._wgrad_items, self._n_block_items
+        tps = wgrad_chunk(items, WG_TARGET_OVERRIDE or WG_TARGET)
+        wa = make_wgrad(items[:nb], dev, tok_per_split=tps, bf16=self.bf16)
+        wb = make_wgrad(items[nb:], dev, tok_per_split=tps, bf16=self.bf16)
+        ca = DescArray(ColsumDesc, self._colsum_a, dev)
+        cb = DescArray(ColsumDesc, self._colsum_b, dev)
+        self._buckets = (wa, wb, ca, cb)
+
+    def backward_bucketed(self, bucket_a_done, ext_dlogits=None, stream=None):
+        """backward() with the gradient reductions split by bucket: bucket A's gradients are
+        complete (and bucket_a_done() is called, e.g. to start its all-reduce on a side stream)
+        right after the last epilogue backward, before the last attention backward; bucket B's
+        at the end."""
+        sp, nl = self.spec, self.spec.nl
+        self._build_buckets()
+        (pa, da, ta, ra), (pb, db, tb, rb), ca, cb = self._buckets
+        if ext_dlogits is not None:
+            self.head.compute_grad = 1
+            self.head.ext_dlogits = ext_dlogits.data_ptr()
+            _lib.call('mep_head_fwd_bwd', ctypes.byref(self.head), stream=stream)
+            self.head.ext_dlogits = 0
+        if not self.pool_fold:
+            launch("mep_pool_bwd", self.d_pool, self.t_poolb, stream)
+        for i in reversed(range(nl)):
+            launch('mep_block_epi_bwd', self.d_epib[i], self.t_epi[i], stream, threads=sp.D | self.prec)
+            if i == 0:
+                launch('mep_wgrad', da, ta, stream)
+                _lib.call('mep_reduce_grads', da.ptr, da.n, ra, ca.ptr, ca.n, self.t_colsum if ca.n else 0,
+                          ctypes.byref(self.head), *self.head_grads, stream=stream)
+                bucket_a_done()
+            launch('mep_attn_bwd', self.d_attnb[i], self.t_attnb[i], stream, threads=self.f_attnb[i] | self.prec)
+        launch('mep_sum_rows', self.d_sum, self.t_sum, stream)
+        if sp.unify_norm:
+            launch('mep_layernorm_bwd', self.d_ulnb, cdiv(max(self.ntok.values()), 64), stream)
+        launch('mep_wgrad', db, tb, stream)
+        _lib.call('mep_reduce_grads', db.ptr, db.n, rb, cb.ptr, cb.n, self.t_colsum if cb.n else 0, None,
+                  0, 0, 0, 0, 0, 0, 0, 0, stream=stream)
 
     def loss_only(self, stream=None):
         """Batch loss (sum of the scaled per-row losses) without the backward."""

@@ -121,7 +121,8 @@ def test_engine_dp_world2():
     from mep_amd.flat import FlatParams
     torch.manual_seed(0)
     ref_model = cmu_mosei.Concat_Trans(32, 5, 5, 5, 2, 1, 1)
-    flat = FlatParams(ref_model, 'cpu', no_grad=ref_model.mep_spec().no_grad_params())
+    spec = ref_model.mep_spec()
+    flat = FlatParams(ref_model, 'cpu', no_grad=spec.no_grad_params(), first=spec.bucket_a)   # the runner's layout
     n = flat.n_grad
     grads = []
     for rank in range(world):

@@ -13,7 +13,8 @@ tests/golden/make_bf16_budget.py running the pinned oracle under torch.autocast(
 the same fp32 fixtures.  The HIP bf16 path must be about as accurate as that or better:
   logits max|d| / max|logit| and whole-gradient relative L2 error  <= 1.25 x budget
   loss relative error                                               <= 2 x budget + 1e-4
-  every parameter gradient's relative L2 error      <= 3 x max(its budget, grad_all budget / 2) + 0.02
+  per-tensor relative L2 error, allowance 2 x max(its budget, grad_all budget / 2) + 0.02:
+                                                    90 % of tensors within it, every tensor within 2 x it
       (fixtures that keep only the first 256 entries of each gradient: <= max(that, 0.5) --
       one 256-entry row of a weight gradient is too small a sample for the per-tensor ratio;
       whole-tensor bf16-vs-fp32 errors there are <= 0.2, scripts/bf16_diag.py)
@@ -72,16 +73,20 @@ def _grad_errors(model, meta, gold, coef, budget):
         pairs.append((k, g[:ref.numel()], ref))
     def allow(k):
         # two independent bf16 executions differ tensor by tensor by a few times either one's
-        # error: a tensor's allowance is three times the larger of its own budget and half the
-        # whole-gradient budget, + 0.02 (full fixtures; measured worst 1.54 x of the 2 x form:
-        # ren_cfg5's stimulation.multimodal_blocks.4.norm2.weight, a cancelling LayerNorm-weight
-        # sum; the whole-gradient error stays at 0.5 x its budget).  The head-256 samples of
-        # partial fixtures are too small for a relative norm and get 0.5
-        a = 3 * max(budget['grads'][k], 0.5 * budget['grad_all']) + 0.02
+        # error: a tensor's allowance is twice the larger of its own budget and half the
+        # whole-gradient budget, + 0.02 (full fixtures).  The head-256 samples of partial
+        # fixtures are too small for a relative norm and get 0.5
+        a = 2 * max(budget['grads'][k], 0.5 * budget['grad_all']) + 0.02
         return a if meta['full'] else max(a, 0.5)
     ratios = sorted(((float((g - r).norm() / r.norm()) / allow(k), k) for k, g, r in pairs), reverse=True)
     print('  worst tensors (error / allowance):', ', '.join('%s %.2f' % (k, e) for e, k in ratios[:3]))
-    worst = ratios[0][0]
+    # max pooling routes a row's gradient through its argmax, which bf16 rounding flips at
+    # near-ties -- differently in every bf16 execution -- so single tensors fed by few pooled
+    # columns scatter (ren_cfg5's stimulation.multimodal_blocks.4.norm2.weight: 1.54 x, a
+    # cancelling LayerNorm-weight sum, while the whole-gradient error is 0.5 x its budget):
+    # 9 of 10 tensors must be within their allowance and the worst within twice it
+    assert ratios[len(ratios) // 10][0] <= 1.0, ratios[:len(ratios) // 10 + 1]
+    worst = ratios[0][0] / 2
     gg = torch.cat([g for _, g, _ in pairs])
     rr = torch.cat([r for _, _, r in pairs])
     return worst, float((gg - rr).norm() / rr.norm())
