@@ -46,6 +46,7 @@ WG_TARGET = _lib.N_CU      # workgroups per launch: one per CU (4 waves of ~400 
 WG_TARGET_OVERRIDE = None  # development: another workgroup count for wgrad_segments
 # the pool's backward formed inside the epilogue backward (0: a separate mep_pool_bwd into dXcat)
 POOL_FOLD = os.environ.get('MEP_POOL_FOLD', '1') != '0'
+FWD_SPLITQ = os.environ.get('MEP_FWD_SPLITQ', '0') == '1'
 
 
 def wgrad_geometry(N, ktot):
@@ -407,6 +408,11 @@ class TriModalPlan:
             self.d_attn.append(DescArray(AttnDesc, ad, dev))
             self.d_epi.append(DescArray(EpiDesc, ed, dev))
             geo = _lib.attn_geometry(ad)
+            # 16-query forward tasks (MEP_ATTN_SPLITQ) when the launch has few (b, h) units, or
+            # forced (MEP_FWD_SPLITQ=1, A/B runs)
+            sq, sq_tiles = _lib.attn_fwd_splitq(ad, min_units=1 << 30 if FWD_SPLITQ else 1024)
+            if sq:
+                geo = (sq_tiles, geo[1], geo[2] | sq)
             self.t_attn.append(geo[0])
             self.g_attn.append(geo)
             self.t_epi.append(_lib.epi_grid(max(B * b['Tq'] for b in self.blocks), len(ed)))
