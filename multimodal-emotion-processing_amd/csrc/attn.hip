@@ -62,7 +62,9 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 #define MEP_BWD_WAVES_KV 4 // waves per SIMD of the short backward with MEP_ATTN_KV (<= 128 registers)
 #endif
 #ifndef MEP_FWD_PVSPLIT
-#define MEP_FWD_PVSPLIT 1  // forward P.V on 2-part bf16 splits (16x16x32) instead of f32 MFMA
+#define MEP_FWD_PVSPLIT 2  // forward P.V on bf16 splits (16x16x32) instead of f32 MFMA: 2 = 3-part P and V,
+                           // six products (fp32-level); 1 = 2-part, three products (~2^-16 per product:
+                           // moved one rf_chain_cfg2 output 3.5e-4 relative); 0 = f32 MFMA
                            // (cfg3 30.1 -> 26.5 us, cfg5 421 -> 368 us)
 #endif
 #ifndef MEP_FWD_WAVES
@@ -446,7 +448,29 @@ MEP_DEV void attn_fwd_task(const mep_attn_desc& d, int qc, int h, int b, int lan
                     for (int hb = 0; hb < NHB; ++hb) oq[hb] = mfma(pb, vbf[kt / 2][hb], oq[hb]);
                     continue;
                 }
-#if MEP_FWD_PVSPLIT
+#if MEP_FWD_PVSPLIT == 2
+                // P and V as 3-part bf16 splits, the six products p_i v_j with i + j <= 2 (the terms
+                // dropped are <= 2^-24 relative: fp32-level) on 16x16x32 MFMAs per key-tile pair
+                // (slots 0-3: tile kt, 4-7: tile kt + 1); the three smallest on a chain of their own
+                {
+                    const S3 pa = split3(sv[kt]), pb = split3(sv[kt + 1]);
+                    const bf16x8 p0 = op(pa.a0, pa.a1, pb.a0, pb.a1), p1 = op(pa.b0, pa.b1, pb.b0, pb.b1),
+                                 p2 = op(pa.c0, pa.c1, pb.c0, pb.c1);
+#pragma unroll
+                    for (int hb = 0; hb < NHB; ++hb) {
+                        const S3 va = split3(vf[kt][hb]), vb = split3(vf[kt + 1][hb]);
+                        const bf16x8 v0 = op(va.a0, va.a1, vb.a0, vb.a1), v1 = op(va.b0, va.b1, vb.b0, vb.b1);
+                        floatx4 t = mfma(p2, v0, zero4());          // two independent chains
+                        oq[hb] = mfma(p1, v0, oq[hb]);
+                        t = mfma(p1, v1, t);
+                        oq[hb] = mfma(p0, v1, oq[hb]);
+                        t = mfma(p0, op(va.c0, va.c1, vb.c0, vb.c1), t);
+                        oq[hb] = mfma(p0, v0, oq[hb]);
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) oq[hb][r] += t[r];
+                    }
+                }
+#elif MEP_FWD_PVSPLIT
                 // P and V as 2-part bf16 splits, products p0 v0 + p1 v0 + p0 v1 on three 16x16x32
                 // MFMAs per key-tile pair (slots 0-3: tile kt, 4-7: tile kt + 1): relative error
                 // <= ~2^-16 per product, 48 MFMA cycles instead of 8 f32 MFMAs

@@ -26,9 +26,27 @@
 #ifndef MEP_EPI_ONE
 #define MEP_EPI_ONE 0   // single-phase epilogues (both weights resident, intermediate in registers)
 #endif
+#ifndef MEP_EPI_ONE_FWD
+#define MEP_EPI_ONE_FWD MEP_EPI_ONE
+#endif
+#ifndef MEP_EPI_ONE_BWD
+#define MEP_EPI_ONE_BWD MEP_EPI_ONE
+#endif
+#ifndef MEP_EPI_ONE_BF16
+#define MEP_EPI_ONE_BF16 1   // single-phase epilogues on the bf16 path (cfg3 bf16: 30.6 / 38.3 -> 26.0 / 33.7 us)
+#endif
+#ifndef MEP_EPI_ONE_BF16_MAXD
+#define MEP_EPI_ONE_BF16_MAXD 96
+#endif
 #ifndef MEP_EPI_SPLIT128
 #define MEP_EPI_SPLIT128 0   // D = 128 on split-bf16 MFMA: weights as 2 parts (the 3-part Wm needs 210 KB
                              // of LDS), activations 3 parts, five products per k pair
+#endif
+#ifndef MEP_EPI_SPLIT128_FWD
+#define MEP_EPI_SPLIT128_FWD MEP_EPI_SPLIT128
+#endif
+#ifndef MEP_EPI_SPLIT128_BWD
+#define MEP_EPI_SPLIT128_BWD MEP_EPI_SPLIT128
 #endif
 
 using namespace mep;
@@ -805,13 +823,16 @@ MEP_DEV void epi_bwd_one(const mep_epi_bwd_desc& bd, unsigned char* sm, int t_be
 
 // parts per weight of the single-phase epilogues (0: the two-phase kernels)
 template <int D, bool BF16> struct EpiOne {
-    static constexpr bool ON = MEP_EPI_ONE && D <= 96;
+    // fp32 path: off by default (the 2-part weight at D = 96 moved one cmu_cfg3 logit 5e-4 relative
+    // and flipped a near-zero Adam update on ren_small); bf16 path: one part per weight, on
+    static constexpr bool ON_BF = BF16 && MEP_EPI_ONE_BF16 && D <= MEP_EPI_ONE_BF16_MAXD;
+    static constexpr bool FWD = (MEP_EPI_ONE_FWD && D <= 96) || ON_BF, BWD = (MEP_EPI_ONE_BWD && D <= 96) || ON_BF;
     static constexpr int NPART = BF16 ? 1 : 3;
     static constexpr int FWD_WP = BF16 ? 1 : (D == 96 ? 2 : 3), FWD_WM = NPART;
     static constexpr int BWD_WP = NPART, BWD_WM = BF16 ? 1 : (D == 96 ? 2 : 3);
     static constexpr int FWD_BYTES = SplitW<D, D / 32, FWD_WP>::BYTES + SplitW<D, D / 16, FWD_WM>::BYTES;
     static constexpr int BWD_BYTES = SplitW<2 * D, D / 32, BWD_WM>::BYTES + SplitW<D, D / 32, BWD_WP>::BYTES;
-    static_assert(!ON || (FWD_BYTES <= 163840 && BWD_BYTES <= 163840), "single-phase weights exceed the LDS");
+    static_assert((!FWD || FWD_BYTES <= 163840) && (!BWD || BWD_BYTES <= 163840), "single-phase weights exceed the LDS");
 };
 
 // BF16: the bf16 path (one part per operand, every D); otherwise D <= 96 runs the 3-part split
@@ -822,13 +843,13 @@ __global__ __launch_bounds__(ETHREADS) void k_epi_fwd(const mep_epi_desc* __rest
     const mep_epi_desc& d = descs[blockIdx.y];
     int t_begin, t_end;
     if (!tile_range(d.ntok, t_begin, t_end)) return;   // whole workgroup
-    if constexpr (EpiOne<D, BF16>::ON) {
+    if constexpr (EpiOne<D, BF16>::FWD) {
         using E = EpiOne<D, BF16>;
         __shared__ __attribute__((aligned(16))) unsigned char sm1[E::FWD_BYTES];
         epi_fwd_one<D, E::NPART, E::FWD_WP, E::FWD_WM>(d, sm1, t_begin, t_end);
         return;
     }
-    if constexpr (BF16 || (MEP_EPI_SPLIT && D <= 96) || (MEP_EPI_SPLIT128 && D == 128)) {
+    if constexpr (BF16 || (MEP_EPI_SPLIT && D <= 96) || (MEP_EPI_SPLIT128_FWD && D == 128)) {
         constexpr int NPART = BF16 ? 1 : 3, NW = BF16 ? 1 : (D == 128 ? 2 : 3);
         constexpr int BYTES = SplitW<D, D / 16, NW>::BYTES;   // the larger phase (Wm)
         __shared__ __attribute__((aligned(16))) unsigned char sm6[BYTES];
@@ -983,13 +1004,13 @@ __global__ __launch_bounds__(ETHREADS) void k_epi_bwd(const mep_epi_bwd_desc* __
     const mep_epi_desc& d = bd.f;
     int t_begin, t_end;
     if (!tile_range(d.ntok, t_begin, t_end)) return;
-    if constexpr (EpiOne<D, BF16>::ON) {
+    if constexpr (EpiOne<D, BF16>::BWD) {
         using E = EpiOne<D, BF16>;
         __shared__ __attribute__((aligned(16))) unsigned char sm1[E::BWD_BYTES];
         epi_bwd_one<D, E::NPART, E::BWD_WP, E::BWD_WM>(bd, sm1, t_begin, t_end);
         return;
     }
-    if constexpr (BF16 || (MEP_EPI_SPLIT && D <= 96) || (MEP_EPI_SPLIT128 && D == 128)) {
+    if constexpr (BF16 || (MEP_EPI_SPLIT && D <= 96) || (MEP_EPI_SPLIT128_BWD && D == 128)) {
         constexpr int NPART = BF16 ? 1 : 3, NW = BF16 ? 1 : (D == 128 ? 2 : 3);
         constexpr int BYTES = SplitW<2 * D, D / 32, NW>::BYTES;   // the larger phase (Wm^T)
         __shared__ __attribute__((aligned(16))) unsigned char sm6[BYTES];

@@ -14,7 +14,9 @@
 using namespace mep;
 
 #ifndef MEP_RF_SPLIT
-#define MEP_RF_SPLIT 1   // the Linears on split-bf16 MFMA (split.h mma_tile_split); 0: f32 MFMA 32x32x2
+#define MEP_RF_SPLIT 0   // 1: the Linears on split-bf16 MFMA (split.h mma_tile_split) -- measured no faster
+                         // (cfg2 epilogues 69 / 66 vs 69 / 69 us: not MFMA-bound) and one rf_chain_cfg2
+                         // output element moved 3.5e-4 relative; 0: f32 MFMA 32x32x2 (exact fp32 products)
 #endif
 
 namespace {

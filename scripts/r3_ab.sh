@@ -15,7 +15,7 @@ for name in ${NAMES:-$(ls variants)}; do
     done
   done
   if [ -n "$PARITY" ]; then
-    MEP_LIB=$lib timeout -k 10 600 python3 -u -m pytest tests/test_gpu_cmu.py tests/test_gpu_ren.py -m gpu -x -q -p no:cacheprovider --timeout 120 --timeout-method thread > gpurun_out/ab_pt_$name.log 2>&1
+    MEP_LIB=$lib timeout -k 10 600 python3 -u -m pytest tests/test_gpu_cmu.py tests/test_gpu_ren.py -m gpu ${PX--x} -q -p no:cacheprovider --timeout 120 --timeout-method thread > gpurun_out/ab_pt_$name.log 2>&1
     rc=$?; echo "== $name parity rc=$rc: $(tail -1 gpurun_out/ab_pt_$name.log)"; fatal $rc
   fi
 done
