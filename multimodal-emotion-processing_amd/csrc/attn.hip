@@ -375,6 +375,27 @@ MEP_DEV void attn_fwd_task(const mep_attn_desc& d, int qc, int h, int b, int lan
                     vbf[kt / 2][hb] = op(pk(vf[kt][hb][0], vf[kt][hb][1]), pk(vf[kt][hb][2], vf[kt][hb][3]),
                                          pk(vf[kt + 1][hb][0], vf[kt + 1][hb][1]), pk(vf[kt + 1][hb][2], vf[kt + 1][hb][3]));
         }
+#if MEP_FWD_PVSPLIT
+        // V of key-tile pairs split once per chunk (not per query tile): parts [pair][hb][part]
+        bf16x8 vsp[NT / 2][NHB][MEP_FWD_PVSPLIT == 2 ? 3 : 2];
+        if (!BF) {
+#pragma unroll
+            for (int kt = 0; kt < NT; kt += 2)
+#pragma unroll
+                for (int hb = 0; hb < NHB; ++hb) {
+#if MEP_FWD_PVSPLIT == 2
+                    const S3 va = split3(vf[kt][hb]), vb = split3(vf[kt + 1][hb]);
+                    vsp[kt / 2][hb][2] = op(va.c0, va.c1, vb.c0, vb.c1);
+                    vsp[kt / 2][hb][0] = op(va.a0, va.a1, vb.a0, vb.a1);
+                    vsp[kt / 2][hb][1] = op(va.b0, va.b1, vb.b0, vb.b1);
+#else
+                    const S2 va = split2(vf[kt][hb]), vb = split2(vf[kt + 1][hb]);
+                    vsp[kt / 2][hb][0] = op(va.h0, va.h1, vb.h0, vb.h1);
+                    vsp[kt / 2][hb][1] = op(va.l0, va.l1, vb.l0, vb.l1);
+#endif
+                }
+        }
+#endif
         float qfa[NT][NHB][4];                                             // B of S^T: Q[q][4g+s]
 #pragma unroll
         for (int qt = 0; qt < NT; ++qt)
@@ -458,13 +479,12 @@ MEP_DEV void attn_fwd_task(const mep_attn_desc& d, int qc, int h, int b, int lan
                                  p2 = op(pa.c0, pa.c1, pb.c0, pb.c1);
 #pragma unroll
                     for (int hb = 0; hb < NHB; ++hb) {
-                        const S3 va = split3(vf[kt][hb]), vb = split3(vf[kt + 1][hb]);
-                        const bf16x8 v0 = op(va.a0, va.a1, vb.a0, vb.a1), v1 = op(va.b0, va.b1, vb.b0, vb.b1);
+                        const bf16x8 v0 = vsp[kt / 2][hb][0], v1 = vsp[kt / 2][hb][1];
                         floatx4 t = mfma(p2, v0, zero4());          // two independent chains
                         oq[hb] = mfma(p1, v0, oq[hb]);
                         t = mfma(p1, v1, t);
                         oq[hb] = mfma(p0, v1, oq[hb]);
-                        t = mfma(p0, op(va.c0, va.c1, vb.c0, vb.c1), t);
+                        t = mfma(p0, vsp[kt / 2][hb][2], t);
                         oq[hb] = mfma(p0, v0, oq[hb]);
 #pragma unroll
                         for (int r = 0; r < 4; ++r) oq[hb][r] += t[r];
@@ -479,11 +499,10 @@ MEP_DEV void attn_fwd_task(const mep_attn_desc& d, int qc, int h, int b, int lan
                     const bf16x8 p0 = op(pa.h0, pa.h1, pb.h0, pb.h1), p1 = op(pa.l0, pa.l1, pb.l0, pb.l1);
 #pragma unroll
                     for (int hb = 0; hb < NHB; ++hb) {
-                        const S2 va = split2(vf[kt][hb]), vb = split2(vf[kt + 1][hb]);
-                        const bf16x8 v0 = op(va.h0, va.h1, vb.h0, vb.h1);
+                        const bf16x8 v0 = vsp[kt / 2][hb][0];
                         oq[hb] = mfma(p0, v0, oq[hb]);
                         oq[hb] = mfma(p1, v0, oq[hb]);
-                        oq[hb] = mfma(p0, op(va.l0, va.l1, vb.l0, vb.l1), oq[hb]);
+                        oq[hb] = mfma(p0, vsp[kt / 2][hb][1], oq[hb]);
                     }
                 }
 #else

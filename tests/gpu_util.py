@@ -57,8 +57,15 @@ def check_post_params(model, meta, gold, lr=1e-3, atol=2e-5, noise=1e-6):
     """Post-optimizer-step parameters vs the reference.  Adam(W)'s first step moves a parameter by
     ~lr * g / (|g| + eps): where the reference gradient is at rounding-noise level (|g| < noise,
     e.g. 2.6e-9 for one ren_small classifier entry) the step direction/size is set by the last
-    ulps of two different fp32 summation orders, so there only |delta| <= 1.1 lr (+ weight decay) is
-    required; everywhere else atol applies."""
+    ulps of two different fp32 summation orders: each side moves by at most lr (the weight decay
+    term is the same on both), in opposite directions when the signs differ (ren_small
+    stimulation.unify_dimension.visual.weight[4439]: reference g = +1.42e-8, here -1.4e-8 .. -2.6e-8
+    with max|g| = 2.1e-2, a 5e-6-of-max error like every other entry), so there only
+    |delta| <= 2 lr is required; everywhere else atol applies.
+
+    Those noise-level entries are then set to the reference's post-step values, so the forward
+    after the step (``logits2``) checks the step everywhere else instead of one coin flip: a flipped
+    entry moved ren_small's logits2 by 1.5e-3 relative."""
     for k, p in model.named_parameters():
         full = meta.get('full', True)
         ref = gold['post/' + k] if full else gold['posthead/' + k]
@@ -68,6 +75,13 @@ def check_post_params(model, meta, gold, lr=1e-3, atol=2e-5, noise=1e-6):
         tol = torch.full_like(err, atol)
         if gkey in gold:
             g = torch.as_tensor(gold[gkey]).double().reshape(err.shape).abs()
-            tol = torch.where(g < noise, torch.full_like(err, 1.1 * lr + atol), tol)
+            tol = torch.where(g < noise, torch.full_like(err, 2.0 * lr + atol), tol)
         bad = err > tol
         assert not bool(bad.any()), (k, float(err.max()), int(bad.sum()))
+        if gkey in gold:
+            noisy = (g < noise).to(p.device)
+            if bool(noisy.any()):
+                with torch.no_grad():
+                    ref_t = torch.as_tensor(ref).to(p.device, p.dtype).reshape(got.shape)
+                    tgt = p.view(-1)[:256].view(got.shape) if not full else p
+                    tgt.copy_(torch.where(noisy, ref_t, tgt))
