@@ -371,8 +371,9 @@ def roofline_of(work, name, tot, reps, costs):
     per_launch_s = t / n
     launches_per_step = max(1, n // reps)
     flops, nbytes = costs[name]
+    spec = getattr(work.plan, 'spec', None)
     rl = roofline.roofline_entry(name, flops / launches_per_step, nbytes / launches_per_step, per_launch_s,
-                                 bf16=work.bf16)
+                                 bf16=work.bf16, D=getattr(spec, 'D', None))
     rl['traffic'], rl['traffic_source'] = pmc_traffic(name, work.name + ('_bf16' if work.bf16 else ''))
     rl['avg_launch_us'] = round(per_launch_s * 1e6, 2)
     return rl

@@ -8,10 +8,12 @@ Per attention-block instance (batch row b, block j), with n_kv = 1 (k is v):
           (+ S_prev, ds_next reads, ds_prev write when chained)
 Peaks (MI355X_MICROARCH.md): HBM 8.0 TB/s; fp32 MFMA (= vector rate) 157.3 TFLOP/s; bf16 MFMA
 2.5 PFLOP/s dense.  Kernels whose fp32 products run as bf16 parts (split.h) are priced against the
-bf16 peak divided by the bf16 products per fp32 product: the block epilogues and the weight
-gradients (six products) at 2.5 P / 6 = 417 TFLOP/s of fp32 work; the attention forward (six-product
-scores, f32-MFMA P.V) at 228 TFLOP/s, the attention backward (four products for S, dP, dV, dK,
-three for dQ) at 658 TFLOP/s.  The realformer token GEMMs and epilogues run on f32 MFMA (157 TF).
+bf16 peak divided by the bf16 products per fp32 product (compute_peak): six for the 3-part x 3-part
+kernels (weight gradients, tiled token GEMM, attention forward scores and P.V, the D <= 96
+epilogue forward): 2.5 P / 6 = 417 TFLOP/s; five for the 2-part-weight x 3-part-activation
+products (D = 128 epilogues; Wm^T of the single-phase D <= 96 epilogue backward, 2/3 of its
+flops, the 3-part Wp^T the rest); four for the attention backward's S, dP, dV, dK and three for
+its dQ: 658 TFLOP/s.  The realformer token GEMMs and epilogues run on f32 MFMA (157 TF).
 bf16 path (MEP_PREC_BF16): one bf16 product per product, every matrix kernel priced at the bf16
 peak; the bytes are the same (fp32 storage).
 """
@@ -21,14 +23,27 @@ from .trimodal import MODS
 HBM_PEAK = 8.0e12
 F32_PEAK = 157.3e12
 BF16_PEAK = 2.5e15
-# fp32 path: the attention forward's scores take six bf16 products (3-part split) and its P.V runs
-# on f32 MFMA; the backward's S, dP, dV, dK take four products (2-part split) and dQ three
-# (csrc/attn.hip): ideal time per 2*Tq*Tk*D-flop contraction at the bf16 peak / products
-ATTN_FWD_PEAK = 4.0 / (12.0 / BF16_PEAK + 2.0 / F32_PEAK)
+# fp32 path (csrc/attn.hip): the forward's scores and P.V take six bf16 products each (3-part
+# splits, MEP_FWD_PVSPLIT = 2); the backward's S, dP, dV, dK four (2-part) and dQ three: ideal
+# time per 2*Tq*Tk*D-flop contraction at the bf16 peak / products
+ATTN_FWD_PEAK = 4.0 / (2.0 * (6 + 6) / BF16_PEAK)
 ATTN_BWD_PEAK = 10.0 / (2.0 * (4 + 4 + 4 + 4 + 3) / BF16_PEAK)
 COMPUTE_PEAK = {'mep_block_epi_fwd': BF16_PEAK / 6, 'mep_block_epi_bwd': BF16_PEAK / 6, 'mep_wgrad': BF16_PEAK / 6,
                 'mep_tgemm': BF16_PEAK / 6,
                 'mep_attn_fwd': ATTN_FWD_PEAK, 'mep_attn_bwd': ATTN_BWD_PEAK}
+
+
+def compute_peak(name, D=None, bf16=False):
+    """The compute peak a launch is priced against (csrc/block.hip: MEP_EPI_SPLIT128 and
+    MEP_EPI_ONE_BWD, both on by default, decide the epilogues' product counts)."""
+    if bf16:
+        return BF16_PEAK
+    if name == 'mep_block_epi_fwd' and D == 128:
+        return BF16_PEAK / 5
+    if name == 'mep_block_epi_bwd' and D is not None and D <= 128:
+        # D = 128: five products; D <= 96 single phase: Wm^T (2/3 of the flops) five, Wp^T six
+        return BF16_PEAK / 5 if D == 128 else 1.0 / ((2.0 / 3.0) * 5 / BF16_PEAK + (1.0 / 3.0) * 6 / BF16_PEAK)
+    return COMPUTE_PEAK.get(name, F32_PEAK)
 
 
 def launch_costs(plan):
@@ -72,6 +87,11 @@ def launch_costs(plan):
             add('mep_wgrad', 2 * n * D * d, 4 * n * (D + d))
     for e in range(2):
         add('mep_pool_fwd', B * plan.Ttot * plan.C, 4 * B * (plan.Ttot * plan.C + 2 * plan.C) + 4 * B * plan.C)
+        for m in MODS:                       # dU = the dQ / dKV rows of every block reading m
+            n = plan.ntok[m]
+            srcs = sum(1 for b in plan.blocks if b['i'] == 0 and b['qm'] == m) // 2 + \
+                sum(1 for b in plan.blocks if b['km'] == m) // 2
+            add('mep_sum_rows', srcs * n * D, 4 * n * D * (srcs + 1))
     return out
 
 
@@ -126,9 +146,9 @@ def rf_launch_costs(plan):
     return out
 
 
-def roofline_entry(name, flops, nbytes, seconds, bf16=False):
+def roofline_entry(name, flops, nbytes, seconds, bf16=False, D=None):
     """The bench's roofline object for one kernel: bound = the larger of the two ideal times."""
-    cpeak = BF16_PEAK if bf16 else COMPUTE_PEAK.get(name, F32_PEAK)
+    cpeak = compute_peak(name, D, bf16)
     t_mem, t_cmp = nbytes / HBM_PEAK, flops / cpeak
     if t_mem >= t_cmp:
         achieved = nbytes / seconds / 1e9
