@@ -67,6 +67,13 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
                            // moved one rf_chain_cfg2 output 3.5e-4 relative); 0 = f32 MFMA
                            // (cfg3 30.1 -> 26.5 us, cfg5 421 -> 368 us)
 #endif
+#ifndef MEP_FWD_EXP2
+#define MEP_FWD_EXP2 1     // forward softmax numerator as exp2(fma(s, log2 e, -max log2 e)): one VALU
+                           // fewer per score (the max's rounding is a common factor of the row)
+#endif
+#ifndef MEP_FWD_QHOIST
+#define MEP_FWD_QHOIST 1   // Tk > 64 forward: the task's Q tiles split once, not once per key chunk
+#endif
 #ifndef MEP_FWD_WAVES
 #define MEP_FWD_WAVES 3    // waves per SIMD of the short, non-residual forward
 #endif
@@ -346,6 +353,18 @@ MEP_DEV void attn_fwd_task(const mep_attn_desc& d, int qc, int h, int b, int lan
         }
     };
 
+    constexpr bool QH = !SINGLE && MEP_FWD_QHOIST;
+    S3 qsh[QH ? NT : 1][NHB];                  // QH: B of S^T for every query tile of the task
+    if (QH) {
+#pragma unroll
+        for (int qt = 0; qt < NT; ++qt)
+#pragma unroll
+            for (int hb = 0; hb < NHB; ++hb) {
+                float qf[4] = {0.f, 0.f, 0.f, 0.f};
+                if (qch == CH || qt < nqt) Qb.ld4(qf, Qb.at(q_lo + qt * 16 + c, hc + 16 * hb + 4 * g));   // past Tq: 0
+                qsh[QH ? qt : 0][hb] = split3(qf);
+            }
+    }
     for (int k_lo = 0; k_lo < Tk; k_lo += CH) {
         // operands of the 4 key tiles of this chunk: K rows (A of S^T: K[k0+c][4g+s], split) and V
         // columns (B of P.V: V[k0+4g+s][c]); past Tk they read 0 (P is 0 there)
@@ -396,21 +415,24 @@ MEP_DEV void attn_fwd_task(const mep_attn_desc& d, int qc, int h, int b, int lan
                 }
         }
 #endif
-        float qfa[NT][NHB][4];                                             // B of S^T: Q[q][4g+s]
+        float qfa[QH ? 1 : NT][NHB][4];                                    // B of S^T: Q[q][4g+s]
+        if (!QH) {
 #pragma unroll
-        for (int qt = 0; qt < NT; ++qt)
+            for (int qt = 0; qt < NT; ++qt)
 #pragma unroll
-            for (int hb = 0; hb < NHB; ++hb) {
-                if (qch == CH || qt < nqt) Qb.ld4(qfa[qt][hb], Qb.at(q_lo + qt * 16 + c, hc + 16 * hb + 4 * g));   // past Tq: 0
-                else qfa[qt][hb][0] = qfa[qt][hb][1] = qfa[qt][hb][2] = qfa[qt][hb][3] = 0.f;
-            }
+                for (int hb = 0; hb < NHB; ++hb) {
+                    float* qf = qfa[QH ? 0 : qt][hb];
+                    if (qch == CH || qt < nqt) Qb.ld4(qf, Qb.at(q_lo + qt * 16 + c, hc + 16 * hb + 4 * g));   // past Tq: 0
+                    else qf[0] = qf[1] = qf[2] = qf[3] = 0.f;
+                }
+        }
 #pragma unroll
         for (int qt = 0; qt < NT; ++qt) {
             if (qt >= nqt) break;
             const int q = q_lo + qt * 16 + c;
             S3 qs[NHB];
 #pragma unroll
-            for (int hb = 0; hb < NHB; ++hb) qs[hb] = split3(qfa[qt][hb]);
+            for (int hb = 0; hb < NHB; ++hb) qs[hb] = QH ? qsh[QH ? qt : 0][hb] : split3(qfa[QH ? 0 : qt][hb]);
             const int srow = (sbase + min(q, Tq - 1)) * Tk;
             float sv[NT][4];
             float mx = -INFINITY;
@@ -439,11 +461,13 @@ MEP_DEV void attn_fwd_task(const mep_attn_desc& d, int qc, int h, int b, int lan
             mx = fmaxf(mx, shfl(mx, lane ^ 32));
             const float mnew = SINGLE ? mx : fmaxf(m[qt], mx);
             float lsum = 0.f;
+            constexpr float L2E = 1.4426950408889634f;
+            const float mb = mnew * L2E;
 #pragma unroll
             for (int kt = 0; kt < NT; ++kt)
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
-                    sv[kt][r] = __expf(sv[kt][r] - mnew);
+                    sv[kt][r] = MEP_FWD_EXP2 ? __builtin_amdgcn_exp2f(fmaf(sv[kt][r], L2E, -mb)) : __expf(sv[kt][r] - mnew);
                     lsum += sv[kt][r];
                 }
             floatx4 oq[NHB];

@@ -1,0 +1,6 @@
+#!/bin/bash
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+for v in old exp2; do for cfg in cfg3 cfg5; do for dt in fp32 bf16; do MEP_LIB=variants/$v/libmep_hip.so timeout -k 10 120 python3 scripts/kbench.py --config $cfg --dtype $dt --kernel mep_attn_fwd --reps 20 2>&1 | grep us/launch | sed "s/^/$v $cfg $dt /"; done; done; done
+for cfg in cfg3 cfg5; do for dt in fp32 bf16; do timeout -k 10 120 python3 scripts/kbench.py --config $cfg --dtype $dt --kernel mep_attn_fwd --reps 20 2>&1 | grep us/launch | sed "s/^/new $cfg $dt /"; done; done
+PYTEST_X=" " bash scripts/quick.sh
