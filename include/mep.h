@@ -262,6 +262,8 @@ typedef struct {
     uint64_t a, b;       /* device float* scalars                   */
     uint64_t stats;      /* [ntok][4]                               */
     int32_t  ntok, D, FD, _pad;
+    uint64_t wparts;     /* mep_rfw_epi_*: mep_wsplit parts of [Wp | W1 | W2 | Wp^T | W1^T | W2^T]
+                            (MEP_RFW_PART_OFFSET); 0 for mep_rf_epi_*                     */
 } mep_rf_epi_desc;
 int mep_rf_epi_fwd(const mep_rf_epi_desc* descs, int n_desc, int max_tiles, int D, int FD, mep_stream_t stream);
 
@@ -278,6 +280,46 @@ typedef struct {
 } mep_rf_epi_bwd_desc;
 int mep_rf_epi_bwd(const mep_rf_epi_bwd_desc* descs, int n_desc, int max_tiles, int D, int FD, mep_stream_t stream);
 #define MEP_RF_PARTIAL_STRIDE(D, FD) (5 * (D) + (FD) + 2)
+/* token rows per workgroup (= rows per partial row of the backward): which 0 = mep_rf_epi_fwd,
+ * 1 = mep_rf_epi_bwd, 2 = mep_rfw_epi_fwd / _bwd and mep_wgemm (the compiled values; hosts size
+ * their grids and partial buffers from this, never from their own constants) */
+int mep_rf_rows(int which, int D);
+
+/* ---------------------------------------------------------------- wave-tiled realformer path
+ * (round 3, others/realformer.py:154-209; csrc/rfw.hip).  Every Linear of the realformer block runs
+ * on pre-split weights: one wave per 16-token tile keeps the whole chain of products in registers
+ * (the transposed-tile layout: a product's accumulators are the next product's operand), six bf16
+ * products per k pair on v_mfma_f32_16x16x32_bf16 (fp32-level, split.h).
+ *
+ * mep_wsplit: W (R x K; element (n, k) = src[n * ld + k], or src[k * ld + n] when trans) -> its
+ * three bf16 parts x = x0 + x1 + x2 (each the round-to-nearest of the remainder), bf16
+ * [3][R][Kp / 32][4][8] with Kp = K rounded up to 32 (zero past K): unit (n, p, g) holds
+ * W(n, 32p + 4g + 0..3) then W(n, 32p + 16 + 4g + 0..3).  One launch per step before the forward:
+ * the weights do not change until the optimizer step. */
+typedef struct {
+    uint64_t src, dst;
+    int32_t  R, K, ld, trans;
+    int32_t  nrows, _pad;   /* rows of W (<= R); rows nrows .. R-1 of the parts are zero */
+} mep_wsplit_desc;
+int mep_wsplit(const mep_wsplit_desc* descs, int n_desc, int max_units, mep_stream_t stream);
+#define MEP_WSPLIT_BYTES(R, K) (3 * 2 * (R) * (((K) + 31) / 32 * 32))
+/* byte offsets of the six parts at mep_rf_epi_desc.wparts: Wp [D][D], W1 [FD][D], W2 [D][FD], then
+ * the transposes Wp^T [D][D], W1^T [D][FD], W2^T [FD][D] (the backward's dY W products) */
+#define MEP_RFW_PART_OFFSET(D, FD, i)                                                               \
+    ((i) <= 0 ? 0 : (i) == 1 ? MEP_WSPLIT_BYTES(D, D) : (i) == 2 ? MEP_WSPLIT_BYTES(D, D) + MEP_WSPLIT_BYTES(FD, D) \
+     : (i) == 3 ? MEP_WSPLIT_BYTES(D, D) + MEP_WSPLIT_BYTES(FD, D) + MEP_WSPLIT_BYTES(D, FD)         \
+     : (i) == 4 ? 2 * MEP_WSPLIT_BYTES(D, D) + MEP_WSPLIT_BYTES(FD, D) + MEP_WSPLIT_BYTES(D, FD)     \
+     : 2 * MEP_WSPLIT_BYTES(D, D) + MEP_WSPLIT_BYTES(FD, D) + 2 * MEP_WSPLIT_BYTES(D, FD))
+#define MEP_RFW_PARTS_BYTES(D, FD) (2 * MEP_WSPLIT_BYTES(D, D) + 2 * MEP_WSPLIT_BYTES(FD, D) + 2 * MEP_WSPLIT_BYTES(D, FD))
+
+/* mep_wgemm: mep_gemm's Y = act(alpha X W'^T + bias + table) (+ Y) with desc.w = the mep_wsplit
+ * parts of W' [N][K] (a Linear weight as it is; a dY W product takes the parts of W^T); one wave
+ * per 16 tokens x all N <= 256 columns.  ldw, w_nt and bf16 are unused. */
+int mep_wgemm(const mep_gemm_desc* descs, int n_desc, int max_tiles, mep_stream_t stream);
+/* mep_rfw_epi_fwd / _bwd: mep_rf_epi_fwd / _bwd on the parts at desc.wparts; one wave per 16-token
+ * tile, one partial row per tile; D in {32, 64, 96, 128}, FD in {D, 2D}. */
+int mep_rfw_epi_fwd(const mep_rf_epi_desc* descs, int n_desc, int max_tiles, int D, int FD, mep_stream_t stream);
+int mep_rfw_epi_bwd(const mep_rf_epi_bwd_desc* descs, int n_desc, int max_tiles, int D, int FD, mep_stream_t stream);
 
 /* ---------------------------------------------------------------- State_Transfer head
  * others/realformer.py:257-286 after the fully_connected Linear (run by mep_gemm):

@@ -98,12 +98,76 @@ class RfEpiDesc(ctypes.Structure):
     _fields_ = [('q', Rows), ('x', Rows), ('xp', Rows), ('h', Rows), ('f1', Rows), ('f', Rows), ('out', Rows),
                 ('wp', u64), ('w1', u64), ('b1', u64), ('w2', u64), ('b2', u64),
                 ('ln1_w', u64), ('ln1_b', u64), ('ln2_w', u64), ('ln2_b', u64), ('a', u64), ('b', u64),
-                ('stats', u64), ('ntok', i32), ('D', i32), ('FD', i32), ('_pad', i32)]
+                ('stats', u64), ('ntok', i32), ('D', i32), ('FD', i32), ('_pad', i32), ('wparts', u64)]
 
 
 class RfEpiBwdDesc(ctypes.Structure):
     _fields_ = [('f', RfEpiDesc), ('dout', Rows), ('dout2', Rows), ('df', Rows), ('df1', Rows), ('dxp', Rows),
                 ('dx', Rows), ('dq', Rows), ('partial', u64), ('dq_accumulate', i32), ('_pad', i32)]
+
+
+class WsplitDesc(ctypes.Structure):
+    _fields_ = [('src', u64), ('dst', u64), ('R', i32), ('K', i32), ('ld', i32), ('trans', i32),
+                ('nrows', i32), ('_pad', i32)]
+
+
+def wsplit_bytes(R, K):
+    """MEP_WSPLIT_BYTES: bytes of the three bf16 parts of an R x K weight (K padded to 32)"""
+    return 3 * 2 * R * (-(-K // 32) * 32)
+
+
+def rfw_part_offsets(D, FD):
+    """MEP_RFW_PART_OFFSET: byte offsets of [Wp, W1, W2, Wp^T, W1^T, W2^T] parts and the total"""
+    sizes = [wsplit_bytes(D, D), wsplit_bytes(FD, D), wsplit_bytes(D, FD), wsplit_bytes(D, D),
+             wsplit_bytes(D, FD), wsplit_bytes(FD, D)]
+    offs, o = [], 0
+    for sz in sizes:
+        offs.append(o)
+        o += sz
+    return offs, o
+
+
+def wsplit_desc(src, dst, N, K, ld, trans):
+    """mep_wsplit descriptor of W' [N][K] (W'(n, k) = src[n * ld + k], or src[k * ld + n] when
+    trans) with its rows padded to a multiple of 32 (the wave kernels' output-tile pairs)"""
+    return WsplitDesc(src=src, dst=dst, R=-(-N // 32) * 32, K=K, ld=ld, trans=int(trans), nrows=N)
+
+
+class PartsArena:
+    """One device buffer holding the mep_wsplit parts of a plan's weights, and the mep_wsplit
+    descriptors that refresh it (once per step, before the forward)."""
+
+    def __init__(self):
+        self.items, self.size = [], 0
+
+    def _take(self, nbytes):
+        off = self.size
+        self.size += -(-nbytes // 256) * 256
+        return off
+
+    def add(self, src, N, K, ld, trans):
+        """parts of W' [N][K]; returns the byte offset in the arena"""
+        assert 0 < N <= 256, 'mep_wgemm: N <= 256'
+        off = self._take(wsplit_bytes(-(-N // 32) * 32, K))
+        self.items.append((off, src, N, K, ld, trans))
+        return off
+
+    def add_epi(self, D, FD, wp, w1, w2):
+        """the six parts of a realformer epilogue (MEP_RFW_PART_OFFSET order, contiguous)"""
+        offs, total = rfw_part_offsets(D, FD)
+        base = self._take(total)
+        for o, (src, N, K, ld, trans) in zip(offs, ((wp, D, D, D, 0), (w1, FD, D, D, 0), (w2, D, FD, FD, 0),
+                                                    (wp, D, D, D, 1), (w1, D, FD, D, 1), (w2, FD, D, FD, 1))):
+            self.items.append((base + o, src, N, K, ld, trans))
+        return base
+
+    def build(self, device):
+        """allocate the arena; returns (buffer, DescArray of mep_wsplit descriptors, max units)"""
+        buf = torch.zeros(max(self.size, 256), dtype=torch.uint8, device=device)
+        base = buf.data_ptr()
+        descs = [wsplit_desc(src, base + off, N, K, ld, trans) for (off, src, N, K, ld, trans) in self.items]
+        units = max((d.R * (-(-d.K // 32)) * 4 for d in descs), default=0)
+        return buf, DescArray(WsplitDesc, descs, device), units
 
 
 def rf_partial_stride(D, FD):
@@ -147,17 +211,17 @@ STRUCTS = {'mep_rows': Rows, 'mep_gemm_desc': GemmDesc, 'mep_wgrad_desc': WgradD
            'mep_epi_bwd_desc': EpiBwdDesc, 'mep_ln_desc': LnDesc, 'mep_colsum_desc': ColsumDesc,
            'mep_sum_desc': SumDesc, 'mep_pool_desc': PoolDesc, 'mep_head_desc': HeadDesc, 'mep_seg': Seg,
            'mep_rf_epi_desc': RfEpiDesc, 'mep_rf_epi_bwd_desc': RfEpiBwdDesc, 'mep_rf_head_desc': RfHeadDesc,
-           'mep_sweep_desc': SweepDesc, 'mep_window_desc': WindowDesc}
+           'mep_sweep_desc': SweepDesc, 'mep_window_desc': WindowDesc, 'mep_wsplit_desc': WsplitDesc}
 
 P = ctypes.c_void_p
 # name -> argtypes (all return int)
-GROUPED = ['mep_gemm', 'mep_unify', 'mep_wgrad', 'mep_wgrad_reduce', 'mep_layernorm_fwd', 'mep_layernorm_bwd', 'mep_colsum', 'mep_sum_rows',
+GROUPED = ['mep_gemm', 'mep_wgemm', 'mep_wsplit', 'mep_unify', 'mep_wgrad', 'mep_wgrad_reduce', 'mep_layernorm_fwd', 'mep_layernorm_bwd', 'mep_colsum', 'mep_sum_rows',
            'mep_pool_fwd', 'mep_pool_bwd']
 GROUPED_T = ['mep_attn_fwd', 'mep_attn_bwd',      # + MEP_ATTN_* variant flags
              'mep_block_epi_fwd', 'mep_block_epi_bwd']  # + D (compiled variant)
 SIGNATURES = {name: [P, i32, i32, P] for name in GROUPED}
 SIGNATURES.update({name: [P, i32, i32, i32, P] for name in GROUPED_T})
-GROUPED_T2 = ['mep_rf_epi_fwd', 'mep_rf_epi_bwd']   # + D, FD (compiled variant)
+GROUPED_T2 = ['mep_rf_epi_fwd', 'mep_rf_epi_bwd', 'mep_rfw_epi_fwd', 'mep_rfw_epi_bwd']   # + D, FD (compiled variant)
 SIGNATURES.update({name: [P, i32, i32, i32, i32, P] for name in GROUPED_T2})
 HP = ctypes.POINTER(HeadDesc)
 SIGNATURES.update({
@@ -174,6 +238,7 @@ SIGNATURES.update({
     'mep_assemble_windows': [ctypes.POINTER(WindowDesc), i32, P],
     'mep_tgemm': [P, i32, i32, i32, i32, P],
     'mep_abi_version': [],
+    'mep_rf_rows': [i32, i32],
     'mep_last_error': [ctypes.c_char_p, ctypes.c_size_t],
     'mep_device_sync': [],
 })
@@ -289,15 +354,19 @@ def attn_bwd_splitq(bdescs, min_units=1024):
     return ATTN_SPLITQ if 0 < units < min_units else 0
 
 
-def rf_bwd_rows():
-    """token rows per workgroup of mep_rf_epi_bwd (csrc/rf.hip MEP_RF_BWD_ROWS): one row of its
-    partial buffer per workgroup"""
-    return int(os.environ.get('MEP_RF_BWD_ROWS', '32'))   # env: A/B builds only
+RFW = os.environ.get('MEP_RFW', '1') != '0'   # 0: the LDS-tiled f32-MFMA realformer kernels (A/B runs)
 
 
-def rf_epi_rows(D):
-    """token rows per workgroup of mep_rf_epi_fwd (csrc/rf.hip rf_fwd_rows)"""
-    return 32 if D > 128 else int(os.environ.get('MEP_RF_FWD_ROWS', '32'))   # env: A/B builds only
+def rf_bwd_rows(wave=None):
+    """token rows per workgroup of the realformer epilogue backward, one row of its partial buffer
+    each: mep_rfw_epi_bwd (wave-tiled, RFW) or mep_rf_epi_bwd -- the value the library was built
+    with (mep_rf_rows), never a host constant"""
+    return lib().mep_rf_rows(2 if (RFW if wave is None else wave) else 1, 0)
+
+
+def rf_epi_rows(D, wave=False):
+    """token rows per workgroup of mep_rf_epi_fwd (mep_rf_rows; 16 for mep_rfw_epi_fwd)"""
+    return lib().mep_rf_rows(2 if wave else 0, D)
 ATTN_MAX_DQ_TILES = (160 * 1024 // 4 - 2 * 4 * 64 * 16 - 4) // 256   # csrc/attn.hip backward LDS
 
 

@@ -1,0 +1,790 @@
+// Wave-tiled realformer path (others/realformer.py:154-209): every Linear of the RealFormer block
+// epilogue and the block's token GEMMs on weights pre-split into bf16 parts (mep_wsplit, once per
+// step), one wave per 16-token tile.
+//
+// Transposed-tile layout (split.h): a product Y^T = W X^T leaves lane (token c = lane & 15,
+// g = lane >> 4) holding features 16 i + 4 g .. +3 of token c in acc[i] -- exactly the B operand
+// of the next product's k pair (features 32 p + 4 g .. +3 in slots 0-3, 32 p + 16 + 4 g .. +3 in
+// slots 4-7).  So the whole epilogue chain xp -> LN1 -> FFN -> LN2 (and its backward) stays in one
+// wave's registers: no LDS, no barriers, no re-reads of its own intermediates.  LayerNorm row sums
+// are the lane's 4 * NI values plus two cross-group shuffles; the LayerNorm / bias parameter
+// partials of the backward are DPP row sums over the tile's 16 tokens.
+//
+// Arithmetic: activations are split into three bf16 parts in registers, weights come pre-split
+// (three 16-byte parts per fragment, L2-resident), six products per k pair on
+// v_mfma_f32_16x16x32_bf16 -- fp32-level (split.h), no per-fragment split VALU for the weights,
+// which feed only 16 tokens each here.  Weight fragments are streamed through a ring of
+// MEP_RFW_DEPTH fragments ahead of their MFMAs.
+#include "common.h"
+#include "split.h"
+
+using namespace mep;
+
+// the token rows per workgroup rf.hip was built with (MEP_RF_FWD_ROWS / MEP_RF_BWD_ROWS)
+#ifndef MEP_RF_FWD_ROWS
+#define MEP_RF_FWD_ROWS 32
+#endif
+#ifndef MEP_RF_BWD_ROWS
+#define MEP_RF_BWD_ROWS 32
+#endif
+#define MEP_RF_FWD_ROWS_BUILT MEP_RF_FWD_ROWS
+#define MEP_RF_BWD_ROWS_BUILT MEP_RF_BWD_ROWS
+
+#ifndef MEP_RFW_DEPTH
+#define MEP_RFW_DEPTH 6   // weight fragments (3 x 16 B per lane each) in flight ahead of their MFMAs
+#endif
+
+namespace {
+
+#ifdef MEP_RFW_TRACE
+// development build only (scripts/rfw_trace.py): per-workgroup shader-clock stamps of wave 0
+__device__ unsigned long long* g_rfw_trace;
+#define MEP_RFW_STAMP(k) do { if (threadIdx.x == 0 && g_rfw_trace) g_rfw_trace[16 * blockIdx.x + (k)] = __builtin_amdgcn_s_memtime(); } while (0)
+#else
+#define MEP_RFW_STAMP(k) ((void)0)
+#endif
+
+constexpr float LN_EPS = 1e-5f;
+typedef const MEP_G u32x4* PartPtr;
+
+// ---------------------------------------------------------------- mep_wsplit
+__global__ __launch_bounds__(256) void k_wsplit(const mep_wsplit_desc* __restrict__ descs) {
+    const mep_wsplit_desc& d = descs[blockIdx.y];
+    const int npk = (d.K + 31) >> 5;
+    const int u = blockIdx.x * 256 + threadIdx.x;        // unit (n, p, g)
+    if (u >= d.R * npk * 4) return;
+    const int g = u & 3, np = u >> 2, n = np / npk, p = np - n * npk;
+    const gfloat* src = G<const float>(d.src);
+    f32x4 lo, hi;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        const int k0 = 32 * p + 4 * g + e, k1 = k0 + 16;
+        const bool nv = n < d.nrows;
+        lo[e] = nv && k0 < d.K ? (d.trans ? src[(int64_t)k0 * d.ld + n] : src[(int64_t)n * d.ld + k0]) : 0.f;
+        hi[e] = nv && k1 < d.K ? (d.trans ? src[(int64_t)k1 * d.ld + n] : src[(int64_t)n * d.ld + k1]) : 0.f;
+    }
+    const Parts<3> a = splitv<3>(lo), b = splitv<3>(hi);
+    MEP_G u32x4* dst = G<u32x4>(d.dst);
+    const int64_t part = (int64_t)d.R * npk * 4;
+#pragma unroll
+    for (int t = 0; t < 3; ++t) dst[t * part + u] = u32x4{a.p[t][0], a.p[t][1], b.p[t][0], b.p[t][1]};
+}
+
+// ---------------------------------------------------------------- products on pre-split weights
+// the activation operands of NPK k pairs from NPK * 2 per-lane f32x4 blocks
+template <int NPK>
+MEP_DEV void split_ops(OpN<3> (&o)[NPK], const f32x4* v) {
+#pragma unroll
+    for (int p = 0; p < NPK; ++p) o[p] = opn<3>(v[2 * p], v[2 * p + 1]);
+}
+
+MEP_DEV PartPtr parts_at(uint64_t base, int off) { return reinterpret_cast<PartPtr>(G<const unsigned char>(base) + off); }
+
+// lane's 4 * NB features (16 kb + 4 g .. +3, kb < NB) of token tc of a row view
+template <int NB>
+MEP_DEV void load_rows(f32x4 (&v)[NB], const mep_rows& r, int tc) {
+    const int g = (threadIdx.x >> 4) & 3;
+    const gfloat* p = row_ptr(r, tc) + 4 * g;
+#pragma unroll
+    for (int kb = 0; kb < NB; ++kb) v[kb] = ld4w(p + 16 * kb);
+}
+template <int NB>
+MEP_DEV void store_rows(const mep_rows& r, int tok, const f32x4 (&v)[NB]) {
+    const int g = (threadIdx.x >> 4) & 3;
+    gfloat* p = row_ptr(r, tok) + 4 * g;
+#pragma unroll
+    for (int kb = 0; kb < NB; ++kb) *reinterpret_cast<MEP_G f32x4*>(p + 16 * kb) = v[kb];
+}
+
+// sum over the row's D features: the lane's values, then the four lane groups of the token
+MEP_DEV float feat_sum(float s) {
+    s += __shfl_xor(s, 16, 64);
+    s += __shfl_xor(s, 32, 64);
+    return s;
+}
+
+// y = LN(z) * w + b over the D = 16 NI features of the lane's token (realformer.py LayerNorm:
+// biased variance, eps 1e-5); mean / rstd returned
+template <int NI>
+MEP_DEV void layer_norm(const f32x4 (&z)[NI], f32x4 (&y)[NI], const gfloat* w, const gfloat* b, float& mean, float& rstd) {
+    constexpr int D = 16 * NI;
+    const int g = (threadIdx.x >> 4) & 3;
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < NI; ++i) s += (z[i][0] + z[i][1]) + (z[i][2] + z[i][3]);
+    mean = feat_sum(s) / (float)D;
+    float v = 0.f;
+#pragma unroll
+    for (int i = 0; i < NI; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) { const float t = z[i][r] - mean; v += t * t; }
+    rstd = 1.0f / sqrtf(feat_sum(v) / (float)D + LN_EPS);
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+        const f32x4 ww = ld4w(w + 16 * i + 4 * g), bb = ld4w(b + 16 * i + 4 * g);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) y[i][r] = (z[i][r] - mean) * rstd * ww[r] + bb[r];
+    }
+}
+
+// ---------------------------------------------------------------- several waves per tile
+// W waves share one 16-token tile: the output tiles of every product are dealt round-robin
+// (wave w owns tiles w, w + W, ...), each wave streams only its tiles' weight fragments, and the
+// full product is exchanged through LDS (one barrier) for the next LayerNorm / product, which
+// every wave then evaluates on whole rows.  W = 6 for D = 96 (6 and 12 output tiles split evenly).
+template <int D> constexpr int rfw_waves() { return D == 96 ? 6 : D >= 64 ? 4 : 2; }
+
+// acc[j] += W'(16 i + c, :) . X for the wave's output tiles i = wave + W j < NI, in two halves:
+// prime() issues the first DEPTH weight fragments (callers prime the NEXT product before the
+// current one's stores / exchange / LayerNorm, so the weight latency hides behind them), run()
+// streams the rest through the ring, one fragment's six MFMAs per step.
+template <int NI, int NPK, int R, int W>
+struct PG {
+    static constexpr int NJ = (NI + W - 1) / W, NS = NJ * NPK;
+    static constexpr int DEPTH = MEP_RFW_DEPTH < NS ? MEP_RFW_DEPTH : NS;
+    OpN<3> ring[DEPTH];
+    PartPtr wl;
+    int wave;
+    MEP_DEV OpN<3> ld(int s) const {
+        const int p = s / NJ, i = wave + W * (s - (s / NJ) * NJ);
+        const int ic = i < NI ? i : NI - 1;   // a wave without this tile loads a valid fragment it never uses
+        OpN<3> o;
+#ifdef MEP_RFW_NOW   // timing-only development build: no weight loads (constant fragments)
+        (void)ic; (void)p;
+#pragma unroll
+        for (int t = 0; t < 3; ++t) o.p[t] = __builtin_bit_cast(bf16x8, u32x4{threadIdx.x, 0u, (unsigned)t, 0u});
+#else
+#pragma unroll
+        for (int t = 0; t < 3; ++t) o.p[t] = __builtin_bit_cast(bf16x8, wl[((t * R + 16 * ic) * NPK + p) * 4]);
+#endif
+        return o;
+    }
+    MEP_DEV void prime(PartPtr w, int wave_) {
+        const int lane = threadIdx.x & 63, c = lane & 15, g = lane >> 4;
+        wl = w + (c * NPK) * 4 + g;
+        wave = wave_;
+#pragma unroll
+        for (int s = 0; s < DEPTH; ++s) ring[s] = ld(s);
+    }
+    MEP_DEV void run(f32x4 (&acc)[NJ], const OpN<3> (&b)[NPK]) {
+#pragma unroll
+        for (int s = 0; s < NS; ++s) {
+            const OpN<3> a = ring[s % DEPTH];
+            if (s + DEPTH < NS) ring[s % DEPTH] = ld(s + DEPTH);
+            const int j = s % NJ;
+            if (wave + W * j < NI) acc[j] = mma_n<3>(a, b[s / NJ], acc[j]);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    }
+};
+
+typedef __attribute__((address_space(3))) f32x4 xf32x4;
+
+// workgroup barrier for LDS hand-offs only: waits for this wave's LDS (and scalar) operations,
+// not for its global loads / stores in flight (__syncthreads waits for vmcnt(0), which would drain
+// the next product's primed weight loads at every exchange)
+MEP_DEV void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// the wave's tiles into the exchange buffer, barrier, every tile back into full[]
+template <int NB, int W>
+MEP_DEV void xchg(f32x4 (&full)[NB], const f32x4 (&mine)[(NB + W - 1) / W], xf32x4* buf, int wave, int lane) {
+#pragma unroll
+    for (int j = 0; j < (NB + W - 1) / W; ++j)
+        if (wave + W * j < NB) buf[(wave + W * j) * 64 + lane] = mine[j];
+    lds_barrier();
+#pragma unroll
+    for (int i = 0; i < NB; ++i) full[i] = buf[i * 64 + lane];
+}
+
+// the wave's tiles of a full row block: store / per-tile transform helpers
+template <int NB, int W>
+MEP_DEV void store_owned(const mep_rows& r, int tok, const f32x4 (&v)[NB], int wave) {
+#ifdef MEP_RFW_NOST   // timing-only development build: no stores of intermediates
+    return;
+#endif
+    const int g = (threadIdx.x >> 4) & 3;
+    gfloat* p = row_ptr(r, tok) + 4 * g;
+#pragma unroll
+    for (int i = 0; i < NB; ++i)
+        if (i % W == wave) *reinterpret_cast<MEP_G f32x4*>(p + 16 * i) = v[i];
+}
+template <int NB, int W>
+MEP_DEV void store_mine(const mep_rows& r, int tok, const f32x4 (&v)[(NB + W - 1) / W], int wave) {
+#ifdef MEP_RFW_NOST
+    return;
+#endif
+    const int g = (threadIdx.x >> 4) & 3;
+    gfloat* p = row_ptr(r, tok) + 4 * g;
+#pragma unroll
+    for (int j = 0; j < (NB + W - 1) / W; ++j)
+        if (wave + W * j < NB) *reinterpret_cast<MEP_G f32x4*>(p + 16 * (wave + W * j)) = v[j];
+}
+
+// ---------------------------------------------------------------- RealFormer epilogue forward
+// Every global load is issued at the top of the kernel (one exposed latency, not one per phase):
+// the x rows in every wave (the first product's operand), the q rows of the wave's own blocks into
+// a shared LDS stash, and the LayerNorm / bias parameters cooperatively into LDS -- both read after
+// the first exchange's barrier.
+typedef __attribute__((address_space(3))) float lds_f;
+
+// parameters [n0 | n1 | ...] -> LDS, cooperatively (the caller's next barrier publishes them)
+template <int TOTAL, int NT, int NSEG>
+MEP_DEV void stage_params(lds_f* dst, const uint64_t (&src)[NSEG], const int (&len)[NSEG]) {
+    constexpr int PER = (TOTAL + NT - 1) / NT;
+    float v[PER];
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {   // every load first (one latency), then the LDS writes
+        const int idx = threadIdx.x + NT * k;
+        int off = idx, sg = 0;
+#pragma unroll
+        for (int q = 0; q < NSEG - 1; ++q)
+            if (sg == q && off >= len[q]) { off -= len[q]; sg = q + 1; }
+        v[k] = idx < TOTAL ? G<const float>(src[sg])[off] : 0.f;
+    }
+#pragma unroll
+    for (int k = 0; k < PER; ++k)
+        if (threadIdx.x + NT * k < TOTAL) dst[threadIdx.x + NT * k] = v[k];
+}
+
+template <int NI, typename P>
+MEP_DEV void layer_norm_l(const f32x4 (&z)[NI], f32x4 (&y)[NI], const P* w, const P* b, float& mean, float& rstd) {
+    constexpr int D = 16 * NI;
+    const int g = (threadIdx.x >> 4) & 3;
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < NI; ++i) s += (z[i][0] + z[i][1]) + (z[i][2] + z[i][3]);
+    mean = feat_sum(s) / (float)D;
+    float v = 0.f;
+#pragma unroll
+    for (int i = 0; i < NI; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) { const float t = z[i][r] - mean; v += t * t; }
+    rstd = 1.0f / sqrtf(feat_sum(v) / (float)D + LN_EPS);
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+        const f32x4 ww = ld4w(w + 16 * i + 4 * g), bb = ld4w(b + 16 * i + 4 * g);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) y[i][r] = (z[i][r] - mean) * rstd * ww[r] + bb[r];
+    }
+}
+
+// the wave's own blocks (i % W == wave) of a token's row -> a shared [NB][64 lanes] LDS stash
+template <int NB, int W>
+MEP_DEV void stash_owned(xf32x4* st, const mep_rows& r, int tc, int wave, int lane) {
+    const int g = (threadIdx.x >> 4) & 3;
+    const gfloat* p = row_ptr(r, tc) + 4 * g;
+    f32x4 v[(NB + W - 1) / W];
+#pragma unroll
+    for (int j = 0; j < (NB + W - 1) / W; ++j)
+        if (wave + W * j < NB) v[j] = ld4w(p + 16 * (wave + W * j));
+#pragma unroll
+    for (int j = 0; j < (NB + W - 1) / W; ++j)
+        if (wave + W * j < NB) st[(wave + W * j) * 64 + lane] = v[j];
+}
+
+template <int D, int FD>
+__global__ __launch_bounds__(64 * rfw_waves<D>()) void k_rfw_fwd(const mep_rf_epi_desc* __restrict__ descs) {
+    constexpr int W = rfw_waves<D>();
+    constexpr int NI = D / 16, NF = FD / 16, NP = D / 32, NPF = FD / 32;
+    constexpr int JI = (NI + W - 1) / W, JF = (NF + W - 1) / W;
+    __shared__ f32x4 xsm[2][NF * 64];
+    __shared__ f32x4 qsm[NI * 64];
+    __shared__ float prm[5 * D + FD];   // ln1_w | ln1_b | ln2_w | ln2_b | b2 | b1
+    xf32x4* xbuf[2] = {(xf32x4*)&xsm[0][0], (xf32x4*)&xsm[1][0]};
+    xf32x4* qst = (xf32x4*)&qsm[0];
+    lds_f* P = (lds_f*)&prm[0];
+    const mep_rf_epi_desc& d = descs[blockIdx.y];
+    const int ntok = d.ntok;
+    const int tile = blockIdx.x;
+    if (tile * 16 >= ntok) return;   // whole workgroup
+    MEP_RFW_STAMP(0);
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, c = lane & 15, g = lane >> 4;
+    const int tok = tile * 16 + c, tc = min(tok, ntok - 1);
+    const bool ok = tok < ntok;
+    const float sa = *G<const float>(d.a), sb = *G<const float>(d.b);
+
+    // every load of the kernel's first phase at once: x (every wave), the first product's weight
+    // fragments, q (the wave's blocks, shared stash) and the parameters (LDS)
+    f32x4 xv[NI];
+    load_rows<NI>(xv, d.x, tc);
+    PG<NI, NP, D, W> g1;
+    g1.prime(parts_at(d.wparts, MEP_RFW_PART_OFFSET(D, FD, 0)), wave);
+    stash_owned<NI, W>(qst, d.q, tc, wave, lane);
+    {
+        const uint64_t src[6] = {d.ln1_w, d.ln1_b, d.ln2_w, d.ln2_b, d.b2, d.b1};
+        const int len[6] = {D, D, D, D, D, FD};
+        stage_params<5 * D + FD, 64 * W, 6>(P, src, len);
+    }
+    MEP_RFW_STAMP(1);
+    // xp = Wp x (the wave's tiles), exchanged (the exchange's barrier also publishes q and the parameters)
+    f32x4 xp[NI];
+    PG<NF, NP, FD, W> g2;
+    {
+        f32x4 acc[JI];
+#pragma unroll
+        for (int j = 0; j < JI; ++j) acc[j] = zero_f4();
+        OpN<3> xs[NP];
+        split_ops<NP>(xs, xv);
+        g1.run(acc, xs);
+        MEP_RFW_STAMP(2);
+        g2.prime(parts_at(d.wparts, MEP_RFW_PART_OFFSET(D, FD, 1)), wave);
+        if (ok) store_mine<NI, W>(d.xp, tok, acc, wave);
+        xchg<NI, W>(xp, acc, xbuf[0], wave, lane);
+        MEP_RFW_STAMP(3);
+    }
+    // h = LN1(q + a xp)  (the reference's q + a * xp: two roundings), on whole rows in every wave
+    f32x4 h[NI];
+    float mean1, rstd1;
+    {
+        f32x4 z[NI];
+#pragma unroll
+        for (int i = 0; i < NI; ++i) {
+            const f32x4 qv = qst[i * 64 + lane];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) z[i][r] = add_rn(qv[r], mul_rn(sa, xp[i][r]));
+        }
+        layer_norm_l<NI>(z, h, P, P + D, mean1, rstd1);
+    }
+    if (ok) store_owned<NI, W>(d.h, tok, h, wave);
+    MEP_RFW_STAMP(4);
+    // f1 = relu(W1 h + b1)
+    f32x4 f1[NF];
+    PG<NI, NPF, D, W> g3;
+    {
+        f32x4 acc[JF];
+#pragma unroll
+        for (int j = 0; j < JF; ++j) acc[j] = zero_f4();
+        OpN<3> hs[NP];
+        split_ops<NP>(hs, h);
+        g2.run(acc, hs);
+        MEP_RFW_STAMP(5);
+        g3.prime(parts_at(d.wparts, MEP_RFW_PART_OFFSET(D, FD, 2)), wave);
+#pragma unroll
+        for (int j = 0; j < JF; ++j) {
+            const f32x4 bb = ld4w(P + 5 * D + 16 * min(wave + W * j, NF - 1) + 4 * g);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) acc[j][r] = fmaxf(acc[j][r] + bb[r], 0.f);
+        }
+        if (ok) store_mine<NF, W>(d.f1, tok, acc, wave);
+        xchg<NF, W>(f1, acc, xbuf[1], wave, lane);
+    }
+    MEP_RFW_STAMP(6);
+    // f = W2 f1 + b2
+    f32x4 f[NI];
+    {
+        f32x4 acc[JI];
+#pragma unroll
+        for (int j = 0; j < JI; ++j) acc[j] = zero_f4();
+        OpN<3> fs[NPF];
+        split_ops<NPF>(fs, f1);
+        g3.run(acc, fs);
+        MEP_RFW_STAMP(7);
+#pragma unroll
+        for (int j = 0; j < JI; ++j) {
+            const f32x4 bb = ld4w(P + 4 * D + 16 * min(wave + W * j, NI - 1) + 4 * g);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) acc[j][r] = acc[j][r] + bb[r];
+        }
+        if (ok) store_mine<NI, W>(d.f, tok, acc, wave);
+        xchg<NI, W>(f, acc, xbuf[0], wave, lane);
+    }
+    MEP_RFW_STAMP(8);
+    // out = LN2(h + b f)
+    f32x4 out[NI];
+    float mean2, rstd2;
+    {
+        f32x4 z[NI];
+#pragma unroll
+        for (int i = 0; i < NI; ++i)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) z[i][r] = add_rn(h[i][r], mul_rn(sb, f[i][r]));
+        layer_norm_l<NI>(z, out, P + 2 * D, P + 3 * D, mean2, rstd2);
+    }
+    if (ok) {
+        store_owned<NI, W>(d.out, tok, out, wave);
+        if (wave == 0 && g == 0)
+            *reinterpret_cast<MEP_G f32x4*>(G<float>(d.stats) + 4 * (int64_t)tok) = f32x4{mean1, rstd1, mean2, rstd2};
+    }
+    MEP_RFW_STAMP(9);
+#ifdef MEP_RFW_TRACE
+    if (threadIdx.x == 0 && g_rfw_trace) {
+        __builtin_amdgcn_s_waitcnt(0);
+        g_rfw_trace[16 * blockIdx.x + 10] = __builtin_amdgcn_s_memtime();
+        g_rfw_trace[16 * blockIdx.x + 11] = __builtin_amdgcn_s_getreg((31 << 11) | 4);    // HW_ID
+        g_rfw_trace[16 * blockIdx.x + 12] = __builtin_amdgcn_s_getreg((31 << 11) | 20);   // XCC_ID
+        g_rfw_trace[16 * blockIdx.x + 13] = __builtin_amdgcn_s_memrealtime();
+    }
+#endif
+}
+
+// ---------------------------------------------------------------- RealFormer epilogue backward
+// column sums over the tile's 16 tokens of the wave's blocks of NB, written by the c == 0 lanes
+template <int NB, int W>
+MEP_DEV void tile_colsum(gfloat* dst, const f32x4 (&v)[NB], int wave, int c, int g) {
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+        if (i % W != wave) continue;
+        f32x4 s;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) s[r] = row16_sum(v[i][r]);
+#ifdef MEP_RFW_NOST
+        if (c == 0 && s[0] == 12345.f) {
+#else
+        if (c == 0) {   // partial rows are 4-byte aligned only (stride 5D + FD + 2)
+#endif
+#pragma unroll
+            for (int r = 0; r < 4; ++r) dst[16 * i + 4 * g + r] = s[r];
+        }
+    }
+}
+
+// LayerNorm backward of one token: g (upstream), xh (normalized input), w (LN weight, lane's
+// blocks) -> dz = rstd (g w - mean(g w) - xh mean(g w xh))
+template <int NI>
+MEP_DEV void ln_bwd(f32x4 (&dz)[NI], const f32x4 (&gu)[NI], const f32x4 (&xh)[NI], const f32x4 (&ww)[NI], float rstd) {
+    constexpr int D = 16 * NI;
+    f32x4 gw[NI];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            gw[i][r] = gu[i][r] * ww[i][r];
+            s1 += gw[i][r];
+            s2 += gw[i][r] * xh[i][r];
+        }
+    }
+    s1 = feat_sum(s1) / (float)D;
+    s2 = feat_sum(s2) / (float)D;
+#pragma unroll
+    for (int i = 0; i < NI; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) dz[i][r] = rstd * (gw[i][r] - s1 - xh[i][r] * s2);
+}
+
+template <int D, int FD>
+__global__ __launch_bounds__(64 * rfw_waves<D>()) void k_rfw_bwd(const mep_rf_epi_bwd_desc* __restrict__ descs) {
+    constexpr int W = rfw_waves<D>();
+    constexpr int NI = D / 16, NF = FD / 16, NP = D / 32, NPF = FD / 32;
+    constexpr int JI = (NI + W - 1) / W, JF = (NF + W - 1) / W;
+    __shared__ f32x4 xsm[2][NF * 64];
+    __shared__ f32x4 ssm[2][NI * 64];   // q | xp rows (shared stash)
+    __shared__ float prm[D];            // ln1_w
+    xf32x4* xbuf[2] = {(xf32x4*)&xsm[0][0], (xf32x4*)&xsm[1][0]};
+    xf32x4* qst = (xf32x4*)&ssm[0][0];
+    xf32x4* xpst = (xf32x4*)&ssm[1][0];
+    lds_f* P = (lds_f*)&prm[0];
+    const mep_rf_epi_bwd_desc& bd = descs[blockIdx.y];
+    const mep_rf_epi_desc& d = bd.f;
+    const int ntok = d.ntok;
+    const int tile = blockIdx.x;
+    if (tile * 16 >= ntok) return;   // whole workgroup
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, c = lane & 15, g = lane >> 4;
+    const int tok = tile * 16 + c, tc = min(tok, ntok - 1);
+    const bool ok = tok < ntok;
+    const float sa = *G<const float>(d.a), sb = *G<const float>(d.b);
+    gfloat* part = G<float>(bd.partial) + (int64_t)tile * MEP_RF_PARTIAL_STRIDE(D, FD);
+
+    // every load up front: the rows the LN2 backward needs now (registers), the first product's
+    // weight fragments, the f1 blocks of the wave's df1 tiles and the old dq blocks (registers),
+    // q / xp (shared stash) and ln1_w (LDS)
+    const f32x4 st = ld4w(G<const float>(d.stats) + 4 * (int64_t)tc);   // mean1, rstd1, mean2, rstd2
+    f32x4 gu[NI], hv[NI], fv[NI], w2v[NI];
+    load_rows<NI>(gu, bd.dout, tc);
+    load_rows<NI>(hv, d.h, tc);
+    load_rows<NI>(fv, d.f, tc);
+#pragma unroll
+    for (int i = 0; i < NI; ++i) w2v[i] = ld4w(G<const float>(d.ln2_w) + 16 * i + 4 * g);
+    PG<NF, NP, FD, W> g1;
+    g1.prime(parts_at(d.wparts, MEP_RFW_PART_OFFSET(D, FD, 5)), wave);
+    f32x4 f1v[JF], dqo[JI];
+    {
+        const gfloat* f1r = row_ptr(d.f1, tc) + 4 * g;
+#pragma unroll
+        for (int j = 0; j < JF; ++j) f1v[j] = ld4w(f1r + 16 * min(wave + W * j, NF - 1));
+        if (bd.dq_accumulate) {
+            const gfloat* o = row_ptr(bd.dq, tc) + 4 * g;
+#pragma unroll
+            for (int j = 0; j < JI; ++j) dqo[j] = ld4w(o + 16 * min(wave + W * j, NI - 1));
+        }
+    }
+    stash_owned<NI, W>(qst, d.q, tc, wave, lane);
+    stash_owned<NI, W>(xpst, d.xp, tc, wave, lane);
+    {
+        const uint64_t src[1] = {d.ln1_w};
+        const int len[1] = {D};
+        stage_params<D, 64 * W, 1>(P, src, len);
+    }
+    if (bd.dout2.ptr) {
+        f32x4 g2[NI];
+        load_rows<NI>(g2, bd.dout2, tc);
+#pragma unroll
+        for (int i = 0; i < NI; ++i) gu[i] += g2[i];
+    }
+#pragma unroll
+    for (int i = 0; i < NI; ++i)
+        if (!ok) gu[i] = zero_f4();
+    // LN2 backward -> dz2; df = b dz2 (whole rows in every wave)
+    f32x4 dz2[NI], df[NI];
+    float db_s = 0.f;
+    f32x4 pw2[NI];
+    {
+        f32x4 xh[NI];
+#pragma unroll
+        for (int i = 0; i < NI; ++i)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) xh[i][r] = (add_rn(hv[i][r], mul_rn(sb, fv[i][r])) - st[2]) * st[3];
+        ln_bwd<NI>(dz2, gu, xh, w2v, st[3]);
+#pragma unroll
+        for (int i = 0; i < NI; ++i)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                pw2[i][r] = gu[i][r] * xh[i][r];
+                df[i][r] = sb * dz2[i][r];
+                db_s += dz2[i][r] * fv[i][r];
+            }
+    }
+    // df1 = relu'(f1) (W2^T df)
+    f32x4 df1[NF];
+    PG<NI, NPF, D, W> g2;
+    {
+        f32x4 acc[JF];
+#pragma unroll
+        for (int j = 0; j < JF; ++j) acc[j] = zero_f4();
+        OpN<3> ds[NP];
+        split_ops<NP>(ds, df);
+        g1.run(acc, ds);
+        g2.prime(parts_at(d.wparts, MEP_RFW_PART_OFFSET(D, FD, 4)), wave);
+        // the LN2 partials and df after the primed loads (stores count in vmcnt with the loads)
+        tile_colsum<NI, W>(part, pw2, wave, c, g);           // dLN2.w
+        tile_colsum<NI, W>(part + D, gu, wave, c, g);        // dLN2.b
+        tile_colsum<NI, W>(part + 4 * D, df, wave, c, g);    // db2
+        if (ok) store_owned<NI, W>(bd.df, tok, df, wave);
+#pragma unroll
+        for (int j = 0; j < JF; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) acc[j][r] = (ok && f1v[j][r] > 0.f) ? acc[j][r] : 0.f;
+        if (ok) store_mine<NF, W>(bd.df1, tok, acc, wave);
+        xchg<NF, W>(df1, acc, xbuf[0], wave, lane);
+    }
+    tile_colsum<NF, W>(part + 5 * D, df1, wave, c, g);       // db1
+    // dh = dz2 + W1^T df1
+    f32x4 dh[NI];
+    PG<NI, NP, D, W> g3;
+    {
+        f32x4 acc[JI];
+#pragma unroll
+        for (int j = 0; j < JI; ++j) acc[j] = zero_f4();
+        OpN<3> ds[NPF];
+        split_ops<NPF>(ds, df1);
+        g2.run(acc, ds);
+        g3.prime(parts_at(d.wparts, MEP_RFW_PART_OFFSET(D, FD, 3)), wave);
+        xchg<NI, W>(dh, acc, xbuf[1], wave, lane);
+    }
+#pragma unroll
+    for (int i = 0; i < NI; ++i) dh[i] += dz2[i];
+    // LN1 backward -> dz1;  dq (+)= dz1;  dxp = a dz1
+    f32x4 dxp[NI];
+    float da_s = 0.f;
+    {
+        f32x4 xh[NI], dz1[NI], w1v[NI], xpv[NI];
+#pragma unroll
+        for (int i = 0; i < NI; ++i) {
+            const f32x4 qv = qst[i * 64 + lane];
+            xpv[i] = xpst[i * 64 + lane];
+            w1v[i] = ld4w(P + 16 * i + 4 * g);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) xh[i][r] = (add_rn(qv[r], mul_rn(sa, xpv[i][r])) - st[0]) * st[1];
+        }
+        ln_bwd<NI>(dz1, dh, xh, w1v, st[1]);
+        f32x4 pw[NI];
+#pragma unroll
+        for (int i = 0; i < NI; ++i)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                pw[i][r] = dh[i][r] * xh[i][r];
+                dxp[i][r] = sa * dz1[i][r];
+                da_s += dz1[i][r] * xpv[i][r];
+            }
+        tile_colsum<NI, W>(part + 2 * D, pw, wave, c, g);    // dLN1.w
+        tile_colsum<NI, W>(part + 3 * D, dh, wave, c, g);    // dLN1.b
+        if (ok) {
+            f32x4 mine[JI];
+#pragma unroll
+            for (int j = 0; j < JI; ++j) {
+                const int i = min(wave + W * j, NI - 1);
+                mine[j] = bd.dq_accumulate ? dqo[j] + dz1[i] : dz1[i];
+            }
+            store_mine<NI, W>(bd.dq, tok, mine, wave);
+            store_owned<NI, W>(bd.dxp, tok, dxp, wave);
+        }
+    }
+    if (wave == 0) {   // every wave holds the whole rows; wave 0 writes the scalars
+        const float da = wave_sum(da_s), db = wave_sum(db_s);
+        if (lane == 0) { part[5 * D + FD] = da; part[5 * D + FD + 1] = db; }
+    }
+    // dx = Wp^T dxp
+    {
+        f32x4 acc[JI];
+#pragma unroll
+        for (int j = 0; j < JI; ++j) acc[j] = zero_f4();
+        OpN<3> ds[NP];
+        split_ops<NP>(ds, dxp);
+        g3.run(acc, ds);
+        if (ok) store_mine<NI, W>(bd.dx, tok, acc, wave);
+    }
+}
+
+// ---------------------------------------------------------------- token GEMM on pre-split weights
+// Y[tok][n] = act(alpha sum_k X[tok][k] W'[n][k] + bias[n] + table[tok % T][n]) (+ Y): one wave per
+// 16 tokens x 32 columns (grid.z = column groups), the X blocks and weight fragments of RP k pairs
+// in flight ahead of their MFMAs (a ring over k pairs, the pair loop unrolled by RP).
+constexpr int WG_RP = 4;
+__global__ __launch_bounds__(64) void k_wgemm(const mep_gemm_desc* __restrict__ descs) {
+    constexpr int NI = 2;
+    const mep_gemm_desc& d = descs[blockIdx.y];
+    const int tile = blockIdx.x, cg = blockIdx.z;
+    const int ntok = d.ntok, N = d.N, K = d.K;
+    if (tile * 16 >= ntok || cg * 32 >= N) return;
+    const int lane = threadIdx.x & 63, c = lane & 15, g = lane >> 4;
+    const int tok = tile * 16 + c, tc = min(tok, ntok - 1);
+    const int npk = (K + 31) >> 5;
+    const bool xvec = (K % 4 == 0) && ((d.x.ptr & 15) == 0) && (d.x.sB % 4 == 0) && (d.x.sT % 4 == 0);
+    const gfloat* xr = row_ptr(d.x, tc);
+    const int rows = (N + 31) & ~31;   // rows of the parts (mep_wsplit R)
+    const PartPtr wl = reinterpret_cast<PartPtr>(G<const unsigned char>(d.w)) + ((32 * cg + c) * npk) * 4 + g;
+    const int tstride = rows * npk * 4;   // units per part
+    f32x4 acc[NI];
+#pragma unroll
+    for (int i = 0; i < NI; ++i) acc[i] = zero_f4();
+    // the epilogue's loads (bias, position-table row, accumulated y) issued before the main loop
+    f32x4 add[NI];
+    {
+        const gfloat* bias = G<const float>(d.bias);
+        const gfloat* trow = d.table ? G<const float>(d.table) + (int64_t)(tc % d.y.T) * (d.ldt ? d.ldt : N) : nullptr;
+        const gfloat* yr = row_ptr(d.y, tc);
+#pragma unroll
+        for (int i = 0; i < NI; ++i)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int n = min(32 * cg + 16 * i + 4 * g + r, N - 1);
+                add[i][r] = (bias ? bias[n] : 0.f) + (trow ? trow[n] : 0.f);
+                acc[i][r] = 0.f;
+                if (d.accumulate) acc[i][r] = yr[n];   // kept apart: y is added after the activation
+            }
+    }
+    f32x4 yold[NI];
+#pragma unroll
+    for (int i = 0; i < NI; ++i) { yold[i] = acc[i]; acc[i] = zero_f4(); }
+    auto xblk = [&](int k) {
+        f32x4 v = zero_f4();
+        if (xvec) {
+            if (k < K) v = ld4w(xr + k);
+        } else {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] = k + e < K ? xr[k + e] : 0.f;
+        }
+        return v;
+    };
+    struct Slot { f32x4 x0, x1; OpN<3> a[NI]; };
+    auto ld = [&](Slot& s, int p) {
+        if (p >= npk) return;
+        s.x0 = xblk(32 * p + 4 * g);
+        s.x1 = xblk(32 * p + 16 + 4 * g);
+#pragma unroll
+        for (int i = 0; i < NI; ++i)
+#pragma unroll
+            for (int t = 0; t < 3; ++t)
+                s.a[i].p[t] = __builtin_bit_cast(bf16x8, wl[t * tstride + (16 * i * npk + p) * 4]);
+    };
+    Slot ring[WG_RP];
+#pragma unroll
+    for (int q = 0; q < WG_RP; ++q) ld(ring[q], q);
+    for (int p0 = 0; p0 < npk; p0 += WG_RP) {
+#pragma unroll
+        for (int q = 0; q < WG_RP; ++q) {
+            const int p = p0 + q;
+            if (p < npk) {
+                const OpN<3> b = opn<3>(ring[q].x0, ring[q].x1);
+                OpN<3> a[NI];
+#pragma unroll
+                for (int i = 0; i < NI; ++i) a[i] = ring[q].a[i];
+                ld(ring[q], p + WG_RP);
+#pragma unroll
+                for (int i = 0; i < NI; ++i) acc[i] = mma_n<3>(a[i], b, acc[i]);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    }
+    if (tok >= ntok) return;
+    gfloat* yr = row_ptr(d.y, tok);
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int n = 32 * cg + 16 * i + 4 * g + r;
+            if (n >= N) continue;
+            float v = d.alpha * acc[i][r] + add[i][r];
+            if (d.relu) v = fmaxf(v, 0.f);
+            if (d.accumulate) v += yold[i][r];
+            yr[n] = v;
+        }
+    }
+}
+
+template <typename F>
+int dispatch_rfw(int D, int FD, F&& f) {
+#define MEP_RFW_CASE(DD, FF) \
+    if (D == DD && FD == FF) { f(std::integral_constant<int, DD>{}, std::integral_constant<int, FF>{}); return 0; }
+    MEP_RFW_CASE(32, 32) MEP_RFW_CASE(32, 64) MEP_RFW_CASE(64, 64) MEP_RFW_CASE(64, 128)
+    MEP_RFW_CASE(96, 96) MEP_RFW_CASE(96, 192) MEP_RFW_CASE(128, 128) MEP_RFW_CASE(128, 256)
+#undef MEP_RFW_CASE
+    return MEP_EINVAL;
+}
+
+}  // namespace
+
+#ifdef MEP_RFW_TRACE
+extern "C" int mep_rfw_set_trace(void* p) {
+    return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_rfw_trace), &p, sizeof(p));
+}
+#endif
+
+extern "C" int mep_rf_rows(int which, int D) {
+    return which == 2 ? 16 : which == 1 ? MEP_RF_BWD_ROWS_BUILT : (D > 128 ? 32 : MEP_RF_FWD_ROWS_BUILT);
+}
+
+extern "C" int mep_wsplit(const mep_wsplit_desc* descs, int n_desc, int max_units, mep_stream_t stream) {
+    if (n_desc <= 0 || max_units <= 0) return 0;
+    hipLaunchKernelGGL(k_wsplit, dim3((max_units + 255) / 256, n_desc), dim3(256), 0, (hipStream_t)stream, descs);
+    return mep_check_launch("mep_wsplit");
+}
+
+extern "C" int mep_wgemm(const mep_gemm_desc* descs, int n_desc, int max_tiles, mep_stream_t stream) {
+    if (n_desc <= 0 || max_tiles <= 0) return 0;
+    // grid.z: 32-column groups of the widest descriptor (N <= 256)
+    hipLaunchKernelGGL(k_wgemm, dim3(max_tiles, n_desc, 8), dim3(64), 0, (hipStream_t)stream, descs);
+    return mep_check_launch("mep_wgemm");
+}
+
+extern "C" int mep_rfw_epi_fwd(const mep_rf_epi_desc* descs, int n_desc, int max_tiles, int D, int FD,
+                               mep_stream_t stream) {
+    if (n_desc <= 0 || max_tiles <= 0) return 0;
+    const int rc = dispatch_rfw(D, FD, [&](auto dc, auto fc) {
+        hipLaunchKernelGGL((k_rfw_fwd<decltype(dc)::value, decltype(fc)::value>), dim3(max_tiles, n_desc),
+                           dim3(64 * rfw_waves<decltype(dc)::value>()), 0, (hipStream_t)stream, descs);
+    });
+    if (rc) { mep_set_error("mep_rfw_epi_fwd: D in {32,64,96,128} and FD in {D, 2D}"); return rc; }
+    return mep_check_launch("mep_rfw_epi_fwd");
+}
+
+extern "C" int mep_rfw_epi_bwd(const mep_rf_epi_bwd_desc* descs, int n_desc, int max_tiles, int D, int FD,
+                               mep_stream_t stream) {
+    if (n_desc <= 0 || max_tiles <= 0) return 0;
+    const int rc = dispatch_rfw(D, FD, [&](auto dc, auto fc) {
+        hipLaunchKernelGGL((k_rfw_bwd<decltype(dc)::value, decltype(fc)::value>), dim3(max_tiles, n_desc),
+                           dim3(64 * rfw_waves<decltype(dc)::value>()), 0, (hipStream_t)stream, descs);
+    });
+    if (rc) { mep_set_error("mep_rfw_epi_bwd: D in {32,64,96,128} and FD in {D, 2D}"); return rc; }
+    return mep_check_launch("mep_rfw_epi_bwd");
+}

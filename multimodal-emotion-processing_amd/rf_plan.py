@@ -92,6 +92,9 @@ class RealformerPlan:
         self.device = dev = torch.device(device)
         sp = spec
         D, H, nl, FD = sp.D, sp.H, sp.nl, sp.FD
+        # wave-tiled kernels on pre-split weights (csrc/rfw.hip: mep_wsplit, mep_wgemm,
+        # mep_rfw_epi_*); MEP_RFW=0 keeps the LDS-tiled f32-MFMA kernels (A/B runs)
+        self.rfw = _lib.RFW
         f32 = dict(dtype=torch.float32, device=dev)
         self.T = {m: sp.Tlen[m] for m in sp.mods}
         self.ntok = {m: R * self.T[m] for m in sp.mods}
@@ -157,7 +160,7 @@ class RealformerPlan:
         blk['dKVin'] = torch.zeros(nk, D, **f32)
         blk['estat'] = torch.zeros(nq, 4, **f32)
         blk['astat'] = torch.zeros(R, H, Tq, 2, **f32)
-        blk['partial'] = torch.zeros(cdiv(nq, _lib.rf_bwd_rows()), _lib.rf_partial_stride(D, FD), **f32)
+        blk['partial'] = torch.zeros(cdiv(nq, _lib.rf_bwd_rows(self.rfw)), _lib.rf_partial_stride(D, FD), **f32)
         if i < nl - 1 or not sp.head:
             blk['OUT'] = torch.zeros(nq, D, **f32)
         if i < nl - 1:
@@ -220,7 +223,7 @@ class RealformerPlan:
                          ln1_w=fl.ptr(p + 'norm1.weight'), ln1_b=fl.ptr(p + 'norm1.bias'),
                          ln2_w=fl.ptr(p + 'norm2.weight'), ln2_b=fl.ptr(p + 'norm2.bias'),
                          a=fl.ptr(p + 'a'), b=fl.ptr(p + 'b'), stats=blk['estat'].data_ptr(),
-                         ntok=blk['nq'], D=D, FD=sp.FD)
+                         ntok=blk['nq'], D=D, FD=sp.FD, wparts=blk.get('wparts', 0))
 
     def _epi_bwd_desc(self, blk):
         D, Tq, FD = self.spec.D, blk['Tq'], self.spec.FD
@@ -259,7 +262,6 @@ class RealformerPlan:
                                w=fl.ptr(sp.prefix + 'unify_dimension.%s.weight' % UNIFY_NAMES[m]),
                                bias=0, table=fl.ptr(sp.prefix + '%s.position_embeddings.weight' % POS_NAMES[m]),
                                ntok=self.ntok[m], N=D, K=d, ldw=d, w_nt=1, accumulate=0, relu=0, alpha=1.0))
-        self.d_unify = DescArray(GemmDesc, ud, dev)
         self.t_unify = max(cdiv(self.ntok[m], 64) for m in sp.mods)
         # projections: KV of every block + Q of layer 0 (all read U only)
         pd = []
@@ -270,29 +272,24 @@ class RealformerPlan:
                 pd.append(GemmDesc(x=self._q_rows(blk), y=crows(blk['QP'], blk['Tq'], D),
                                    w=fl.ptr(blk['pre'] + 'w_qkv.0.weight'), ntok=blk['nq'], N=D, K=D, ldw=D,
                                    w_nt=1, **gemm))
-        self.d_proj = DescArray(GemmDesc, pd, dev)
         self.t_proj = max(cdiv(b['nk'], 64) for b in self.blocks)
         self.d_q, self.d_attn, self.d_epi, self.t_attn, self.t_epi = [], [], [], [], []
         self.t_epif, self.t_epib = [], []   # mep_rf_epi_fwd / _bwd workgroups (t_epi: 64-token tiles)
         self.d_epib, self.d_attnb, self.t_attnb, self.d_ingrad = [], [], [], []
         self.f_attn, self.f_attnb = [], []
+        qd, igd = [], []
         for i in range(nl):
             layer = [b for b in self.blocks if b['i'] == i]
-            self.d_q.append(DescArray(GemmDesc, [
-                GemmDesc(x=self._q_rows(b), y=crows(b['QP'], b['Tq'], D), w=fl.ptr(b['pre'] + 'w_qkv.0.weight'),
-                         ntok=b['nq'], N=D, K=D, ldw=D, w_nt=1, **gemm) for b in layer] if i > 0 else [], dev))
+            qd.append([GemmDesc(x=self._q_rows(b), y=crows(b['QP'], b['Tq'], D), w=fl.ptr(b['pre'] + 'w_qkv.0.weight'),
+                                ntok=b['nq'], N=D, K=D, ldw=D, w_nt=1, **gemm) for b in layer] if i > 0 else [])
             ad = [self._attn_desc(b) for b in layer]
             self.d_attn.append(DescArray(AttnDesc, ad, dev))
-            self.d_epi.append(DescArray(RfEpiDesc, [self._epi_desc(b) for b in layer], dev))
             geo = _lib.attn_geometry(ad)
             sq, sq_tiles = _lib.attn_fwd_splitq(ad) if RF_SPLITQ else (0, None)
             self.t_attn.append(sq_tiles or geo[0])
             self.t_attnb.append(geo[1])
             self.f_attn.append(geo[2] | sq)
-            self.t_epi.append(max(cdiv(b['nq'], 64) for b in layer))
-            self.t_epif.append(max(cdiv(b['nq'], _lib.rf_epi_rows(self.spec.D)) for b in layer))
-            self.t_epib.append(max(cdiv(b['nq'], _lib.rf_bwd_rows()) for b in layer))
-            self.d_epib.append(DescArray(RfEpiBwdDesc, [self._epi_bwd_desc(b) for b in layer], dev))
+            self.t_epi.append(max(cdiv(b['nq'], 16 if self.rfw else 64) for b in layer))
             ab = [self._attn_bwd_desc(b) for b in layer]
             self.d_attnb.append(DescArray(AttnBwdDesc, ab, dev))
             self.f_attnb.append(_lib.attn_bwd_flags(ab) | (_lib.attn_bwd_splitq(ab) if RF_SPLITQ else 0))
@@ -305,8 +302,35 @@ class RealformerPlan:
                 # dkv_in = [dK | dV] [W_k; W_v]
                 ig.append(GemmDesc(x=crows(b['dKV2'], b['Tk'], 2 * D), y=crows(b['dKVin'], b['Tk'], D),
                                    w=fl.ptr(self._wkv(b)), ntok=b['nk'], N=D, K=2 * D, ldw=D, w_nt=0, **gemm))
-            self.d_ingrad.append(DescArray(GemmDesc, ig, dev))
+            igd.append(ig)
         self.t_ingrad = max(max(cdiv(b['nq'], 64), cdiv(b['nk'], 64)) for b in self.blocks)
+        if self.rfw:
+            # every token GEMM and epilogue Linear on mep_wsplit parts (refreshed at the start of
+            # each forward): W' = the weight as it is (w_nt) or its transpose (dY W products)
+            arena = _lib.PartsArena()
+            patch = []
+            for dsc in ud + pd + [x for l_ in qd for x in l_] + [x for l_ in igd for x in l_]:
+                patch.append((dsc, arena.add(dsc.w, dsc.N, dsc.K, dsc.ldw, 0 if dsc.w_nt else 1)))
+            epi_off = [arena.add_epi(D, FD, fl.ptr(b['pre'] + 'proj.weight'), fl.ptr(b['pre'] + 'ffn.0.weight'),
+                                     fl.ptr(b['pre'] + 'ffn.2.weight')) for b in self.blocks]
+            self.wparts, self.d_wsplit, self.t_wsplit = arena.build(dev)
+            for dsc, off in patch:
+                dsc.w = self.wparts.data_ptr() + off
+            for b, off in zip(self.blocks, epi_off):
+                b['wparts'] = self.wparts.data_ptr() + off
+            self.t_unify = max(cdiv(self.ntok[m], 16) for m in sp.mods)
+            self.t_proj = max(cdiv(b['nk'], 16) for b in self.blocks)
+            self.t_ingrad = max(max(cdiv(b['nq'], 16), cdiv(b['nk'], 16)) for b in self.blocks)
+        self.d_unify = DescArray(GemmDesc, ud, dev)
+        self.d_proj = DescArray(GemmDesc, pd, dev)
+        self.d_q = [DescArray(GemmDesc, x, dev) for x in qd]
+        self.d_ingrad = [DescArray(GemmDesc, x, dev) for x in igd]
+        for i in range(nl):
+            layer = [b for b in self.blocks if b['i'] == i]
+            self.d_epi.append(DescArray(RfEpiDesc, [self._epi_desc(b) for b in layer], dev))
+            self.t_epif.append(max(cdiv(b['nq'], _lib.rf_epi_rows(self.spec.D, self.rfw)) for b in layer))
+            self.t_epib.append(max(cdiv(b['nq'], _lib.rf_bwd_rows(self.rfw)) for b in layer))
+            self.d_epib.append(DescArray(RfEpiBwdDesc, [self._epi_bwd_desc(b) for b in layer], dev))
         # per-modality input-gradient sums
         sd = []
         for m in sp.mods:
@@ -451,19 +475,28 @@ class RealformerPlan:
         sp, nl = self.spec, self.spec.nl
         assert not rdrop
         ex = (sp.D, sp.FD)
-        _lib.gemm('mep_gemm', self.d_unify, self.t_unify, stream)
-        _lib.gemm('mep_gemm', self.d_proj, self.t_proj, stream)
+        if self.rfw:
+            launch('mep_wsplit', self.d_wsplit, self.t_wsplit, stream)
+        self._gemm(self.d_unify, self.t_unify, stream)
+        self._gemm(self.d_proj, self.t_proj, stream)
         for i in range(nl):
             if i > 0:
-                _lib.gemm('mep_gemm', self.d_q[i], self.t_epi[i], stream)
+                self._gemm(self.d_q[i], self.t_epi[i], stream)
             launch('mep_attn_fwd', self.d_attn[i], self.t_attn[i], stream, threads=self.f_attn[i])
-            launch('mep_rf_epi_fwd', self.d_epi[i], self.t_epif[i], stream, extra=ex)
+            launch('mep_rfw_epi_fwd' if self.rfw else 'mep_rf_epi_fwd', self.d_epi[i], self.t_epif[i], stream, extra=ex)
         if sp.head:
             launch('mep_pool_fwd', self.d_pool, self.t_pool, stream)
             _lib.gemm('mep_gemm', self.d_fc, self.t_fc, stream)
             self.head.compute_grad = int(grad)
             self.head.ext_dout = 0
             _lib.call('mep_rf_head', ctypes.byref(self.head), stream=stream)
+
+    def _gemm(self, descs, tiles, stream):
+        """a token-GEMM launch: mep_wgemm on the arena's parts, or the mep_gemm path"""
+        if self.rfw:
+            launch('mep_wgemm', descs, tiles, stream)
+        else:
+            _lib.gemm('mep_gemm', descs, tiles, stream)
 
     def backward(self, ext_dout=None, stream=None):
         """Backward from the fused loss (or from ext_dout: [B, P, 6] for the head, the last block's
@@ -482,9 +515,9 @@ class RealformerPlan:
             self.dout_chain.copy_(ext_dout.reshape(self.dout_chain.shape))
         self.dQP_all.zero_()
         for i in reversed(range(nl)):
-            launch('mep_rf_epi_bwd', self.d_epib[i], self.t_epib[i], stream, extra=ex)
+            launch('mep_rfw_epi_bwd' if self.rfw else 'mep_rf_epi_bwd', self.d_epib[i], self.t_epib[i], stream, extra=ex)
             launch('mep_attn_bwd', self.d_attnb[i], self.t_attnb[i], stream, threads=self.f_attnb[i])
-            _lib.gemm('mep_gemm', self.d_ingrad[i], self.t_ingrad, stream)
+            self._gemm(self.d_ingrad[i], self.t_ingrad, stream)
         launch('mep_sum_rows', self.d_sum, self.t_sum, stream)
         launch('mep_wgrad', self.d_wgrad, self.t_wgrad, stream)
         # weight-gradient split sums and LayerNorm / ReZero / residual-coefficient column sums: one

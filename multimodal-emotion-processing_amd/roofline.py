@@ -13,7 +13,9 @@ kernels (weight gradients, tiled token GEMM, attention forward scores and P.V, t
 epilogue forward): 2.5 P / 6 = 417 TFLOP/s; five for the 2-part-weight x 3-part-activation
 products (D = 128 epilogues; Wm^T of the single-phase D <= 96 epilogue backward, 2/3 of its
 flops, the 3-part Wp^T the rest); four for the attention backward's S, dP, dV, dK and three for
-its dQ: 658 TFLOP/s.  The realformer token GEMMs and epilogues run on f32 MFMA (157 TF).
+its dQ: 658 TFLOP/s.  The realformer token GEMMs and epilogues: on the wave-tiled kernels
+(mep_wgemm, mep_rfw_epi_*: six products) 417 TFLOP/s; on the LDS-tiled ones (MEP_RFW=0: mep_gemm,
+mep_rf_epi_*) f32 MFMA, 157 TF.
 bf16 path (MEP_PREC_BF16): one bf16 product per product, every matrix kernel priced at the bf16
 peak; the bytes are the same (fp32 storage).
 """
@@ -29,7 +31,8 @@ BF16_PEAK = 2.5e15
 ATTN_FWD_PEAK = 4.0 / (2.0 * (6 + 6) / BF16_PEAK)
 ATTN_BWD_PEAK = 10.0 / (2.0 * (4 + 4 + 4 + 4 + 3) / BF16_PEAK)
 COMPUTE_PEAK = {'mep_block_epi_fwd': BF16_PEAK / 6, 'mep_block_epi_bwd': BF16_PEAK / 6, 'mep_wgrad': BF16_PEAK / 6,
-                'mep_tgemm': BF16_PEAK / 6,
+                'mep_tgemm': BF16_PEAK / 6, 'mep_wgemm': BF16_PEAK / 6,
+                'mep_rfw_epi_fwd': BF16_PEAK / 6, 'mep_rfw_epi_bwd': BF16_PEAK / 6,
                 'mep_attn_fwd': ATTN_FWD_PEAK, 'mep_attn_bwd': ATTN_BWD_PEAK}
 
 
@@ -109,7 +112,9 @@ def rf_launch_costs(plan):
         f0, b0 = out.get(name, (0, 0))
         out[name] = (f0 + f, b0 + b)
 
-    GEMM = _lib.gemm_launcher('mep_gemm', plan.d_unify)
+    rfw = getattr(plan, 'rfw', False)
+    GEMM = 'mep_wgemm' if rfw else _lib.gemm_launcher('mep_gemm', plan.d_unify)
+    EPI_F, EPI_B = ('mep_rfw_epi_fwd', 'mep_rfw_epi_bwd') if rfw else ('mep_rf_epi_fwd', 'mep_rf_epi_bwd')
 
     def gemm(name, ntok, N, K, accumulate=False, table=0):
         add(GEMM, 2 * ntok * N * K, 4 * (ntok * K + ntok * N * (2 if accumulate else 1) + N * K + table))
@@ -132,12 +137,16 @@ def rf_launch_costs(plan):
             R * (4 * (5 * Tq * D + 4 * Tk * D) + 4 * Tk + 8 * H * Tq + chained))
         w = 4 * (D * D + 2 * D * FD + 2 * D + FD + 4 * D)      # Wp, W1, W2, biases, LN weights
         # forward: reads q, x; writes xp, h, f1, f, out and 4 stats per token
-        add('mep_rf_epi_fwd', 2 * nq * (D * D + 2 * D * FD), 4 * nq * (7 * D + FD + 4) + w)
+        add(EPI_F, 2 * nq * (D * D + 2 * D * FD), 4 * nq * (7 * D + FD + 4) + w)
         # backward: reads dout, h, f, f1, q, xp, stats; writes df, df1, dxp, dx, dq
-        add('mep_rf_epi_bwd', 2 * nq * (D * D + 2 * D * FD), 4 * nq * (10 * D + 2 * FD + 4) + w)
+        add(EPI_B, 2 * nq * (D * D + 2 * D * FD), 4 * nq * (10 * D + 2 * FD + 4) + w)
         # weight gradients: W_q, [W_k; W_v], Wp, W1, W2
         for (n, N, K) in ((nq, D, D), (nk, D, 2 * D), (nq, D, D), (nq, D, FD), (nq, D, FD)):
             add('mep_wgrad', 2 * n * N * K, 4 * n * (N + K))
+    if rfw:
+        # mep_wsplit: every pre-split weight read once (fp32) and its three bf16 parts written
+        nw = sum(d.nrows * d.K for d in plan.d_wsplit.items)
+        add('mep_wsplit', 0, nw * (4 + 6))
     for m in sp.mods:
         n = plan.ntok[m]
         add('mep_wgrad', 2 * n * D * sp.dims[m], 4 * n * (D + sp.dims[m]))

@@ -254,7 +254,17 @@ class _RFBlockFn(torch.autograd.Function):
                             a=a.data_ptr(), b=b.data_ptr(), stats=estat.data_ptr(), ntok=B * Tq, D=D, FD=FD)
         geo = _lib.attn_geometry([ad])
         launch('mep_attn_fwd', DescArray(AttnDesc, [ad], dev), geo[0], threads=geo[2])
-        launch('mep_rf_epi_fwd', DescArray(_lib.RfEpiDesc, [ed], dev), cdiv(B * Tq, _lib.rf_epi_rows(D)), extra=(D, FD))
+        rfw = _lib.RFW
+        ctx.wbuf = None
+        if rfw:   # the epilogue's Linears on mep_wsplit parts (wave-tiled kernels, csrc/rfw.hip)
+            arena = _lib.PartsArena()
+            off = arena.add_epi(D, FD, wp.data_ptr(), w1.data_ptr(), w2.data_ptr())
+            ctx.wbuf, wsd, units = arena.build(dev)
+            launch('mep_wsplit', wsd, units)
+            ed.wparts = ctx.wbuf.data_ptr() + off
+        launch('mep_rfw_epi_fwd' if rfw else 'mep_rf_epi_fwd', DescArray(_lib.RfEpiDesc, [ed], dev),
+               cdiv(B * Tq, _lib.rf_epi_rows(D, rfw)), extra=(D, FD))
+        ctx.rfw = rfw
         ctx.save_for_backward(q, k, v, mask, QP, KV, X, XP, Hh, F1, F, S, astat, estat,
                               wq, wk, wv, wp, n1w, n1b, n2w, n2b, w1, b1, w2, b2, a, b, c)
         ctx.sp = sp
@@ -278,7 +288,7 @@ class _RFBlockFn(torch.autograd.Function):
         dF1 = torch.empty(B, Tq, FD, **f)
         dKV2 = torch.empty(B, Tk, 2 * D, **f)
         dk_in, dv_in = torch.empty(B, Tk, D, **f), torch.empty(B, Tk, D, **f)
-        nt = cdiv(B * Tq, _lib.rf_bwd_rows())
+        nt = cdiv(B * Tq, _lib.rf_bwd_rows(ctx.rfw))
         stride = _lib.rf_partial_stride(D, FD)
         part = torch.empty(nt, stride, **f)
         has_prev = ctx.sp is not None
@@ -291,7 +301,8 @@ class _RFBlockFn(torch.autograd.Function):
         ab = AttnBwdDesc(f=ad, dx=crows(dX, Tq, D), dq=crows(dQP, Tq, D), dk=kv(dKV2, 0), dv=kv(dKV2, 1),
                          ds_next=dS.data_ptr() if dS is not None else 0, ds_prev=dSp.data_ptr() if has_prev else 0,
                          dc_partial=dc_part.data_ptr() if has_prev else 0)
-        launch('mep_rf_epi_bwd', DescArray(_lib.RfEpiBwdDesc, [eb], dev), nt, extra=(D, FD))
+        launch('mep_rfw_epi_bwd' if ctx.rfw else 'mep_rf_epi_bwd', DescArray(_lib.RfEpiBwdDesc, [eb], dev), nt,
+               extra=(D, FD))
         geo = _lib.attn_geometry([ad])
         launch('mep_attn_bwd', DescArray(AttnBwdDesc, [ab], dev), geo[1], threads=_lib.attn_bwd_flags([ab]))
         g = dict(bias=0, table=0, relu=0, alpha=1.0, w_nt=0, K=D, ldw=D, N=D)

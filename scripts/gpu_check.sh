@@ -15,7 +15,7 @@ step() {  # step <name> <timeout> <cmd...>
 STEPS="${STEPS:-pytest smoke bench}"
 for s in $STEPS; do
   case $s in
-    pytest) step pytest_gpu 900 python -m pytest tests -m gpu -x -q -p no:cacheprovider ${PYTEST_ARGS} ;;
+    pytest) step pytest_gpu 900 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 120 --timeout-method thread ${PYTEST_ARGS} ;;
     smoke)  step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench)  step bench 600 python bench.py --steps ${BSTEPS:-100} --warmup 10 --cpu-budget ${CPUB:-8} ;;
     prof)   step prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 50 --warmup 5 --no-cpu-baseline ;;
