@@ -264,6 +264,10 @@ typedef struct {
     int32_t  ntok, D, FD, _pad;
     uint64_t wparts;     /* mep_rfw_epi_*: mep_wsplit parts of [Wp | W1 | W2 | Wp^T | W1^T | W2^T]
                             (MEP_RFW_PART_OFFSET); 0 for mep_rf_epi_*                     */
+    /* mep_rfw_epi_fwd, optional (wq_next 0: off): the next layer's query projection fused after
+     * LN2, qp_next = out Wq_next^T (wq_next = mep_wsplit parts of Wq_next [D][D]) */
+    uint64_t wq_next;
+    mep_rows qp_next;
 } mep_rf_epi_desc;
 int mep_rf_epi_fwd(const mep_rf_epi_desc* descs, int n_desc, int max_tiles, int D, int FD, mep_stream_t stream);
 
@@ -277,6 +281,10 @@ typedef struct {
     mep_rows df, df1, dxp, dx, dq;
     uint64_t partial;
     int32_t  dq_accumulate, _pad;
+    /* mep_rfw_epi_bwd, optional (wq_in 0: off): the next layer's query-projection input gradient
+     * fused before the LN2 backward, dout += dqp_in Wq (wq_in = mep_wsplit parts of Wq^T) */
+    uint64_t wq_in;
+    mep_rows dqp_in;
 } mep_rf_epi_bwd_desc;
 int mep_rf_epi_bwd(const mep_rf_epi_bwd_desc* descs, int n_desc, int max_tiles, int D, int FD, mep_stream_t stream);
 #define MEP_RF_PARTIAL_STRIDE(D, FD) (5 * (D) + (FD) + 2)

@@ -98,12 +98,14 @@ class RfEpiDesc(ctypes.Structure):
     _fields_ = [('q', Rows), ('x', Rows), ('xp', Rows), ('h', Rows), ('f1', Rows), ('f', Rows), ('out', Rows),
                 ('wp', u64), ('w1', u64), ('b1', u64), ('w2', u64), ('b2', u64),
                 ('ln1_w', u64), ('ln1_b', u64), ('ln2_w', u64), ('ln2_b', u64), ('a', u64), ('b', u64),
-                ('stats', u64), ('ntok', i32), ('D', i32), ('FD', i32), ('_pad', i32), ('wparts', u64)]
+                ('stats', u64), ('ntok', i32), ('D', i32), ('FD', i32), ('_pad', i32), ('wparts', u64),
+                ('wq_next', u64), ('qp_next', Rows)]
 
 
 class RfEpiBwdDesc(ctypes.Structure):
     _fields_ = [('f', RfEpiDesc), ('dout', Rows), ('dout2', Rows), ('df', Rows), ('df1', Rows), ('dxp', Rows),
-                ('dx', Rows), ('dq', Rows), ('partial', u64), ('dq_accumulate', i32), ('_pad', i32)]
+                ('dx', Rows), ('dq', Rows), ('partial', u64), ('dq_accumulate', i32), ('_pad', i32),
+                ('wq_in', u64), ('dqp_in', Rows)]
 
 
 class WsplitDesc(ctypes.Structure):

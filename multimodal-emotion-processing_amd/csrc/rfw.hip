@@ -400,6 +400,17 @@ __global__ __launch_bounds__(64 * rfw_waves<D>()) void k_rfw_fwd(const mep_rf_ep
             for (int r = 0; r < 4; ++r) z[i][r] = add_rn(h[i][r], mul_rn(sb, f[i][r]));
         layer_norm_l<NI>(z, out, P + 2 * D, P + 3 * D, mean2, rstd2);
     }
+    if (d.wq_next) {   // the next layer's query projection, qp_next = out Wq_next^T (wave's tiles)
+        PG<NI, NP, D, W> g4;
+        g4.prime(reinterpret_cast<PartPtr>(G<const unsigned char>(d.wq_next)), wave);
+        f32x4 acc[JI];
+#pragma unroll
+        for (int j = 0; j < JI; ++j) acc[j] = zero_f4();
+        OpN<3> os[NP];
+        split_ops<NP>(os, out);
+        g4.run(acc, os);
+        if (ok) store_mine<NI, W>(d.qp_next, tok, acc, wave);
+    }
     if (ok) {
         store_owned<NI, W>(d.out, tok, out, wave);
         if (wave == 0 && g == 0)
@@ -520,6 +531,21 @@ __global__ __launch_bounds__(64 * rfw_waves<D>()) void k_rfw_bwd(const mep_rf_ep
         load_rows<NI>(g2, bd.dout2, tc);
 #pragma unroll
         for (int i = 0; i < NI; ++i) gu[i] += g2[i];
+    }
+    if (bd.wq_in) {   // dout += dqp_in Wq: the next layer's query-projection input gradient (exchanged)
+        PG<NI, NP, D, W> g0;
+        g0.prime(reinterpret_cast<PartPtr>(G<const unsigned char>(bd.wq_in)), wave);
+        f32x4 dv[NI];
+        load_rows<NI>(dv, bd.dqp_in, tc);
+        f32x4 acc[JI], full[NI];
+#pragma unroll
+        for (int j = 0; j < JI; ++j) acc[j] = zero_f4();
+        OpN<3> ds[NP];
+        split_ops<NP>(ds, dv);
+        g0.run(acc, ds);
+        xchg<NI, W>(full, acc, xbuf[1], wave, lane);
+#pragma unroll
+        for (int i = 0; i < NI; ++i) gu[i] += full[i];
     }
 #pragma unroll
     for (int i = 0; i < NI; ++i)

@@ -223,14 +223,16 @@ class RealformerPlan:
                          ln1_w=fl.ptr(p + 'norm1.weight'), ln1_b=fl.ptr(p + 'norm1.bias'),
                          ln2_w=fl.ptr(p + 'norm2.weight'), ln2_b=fl.ptr(p + 'norm2.bias'),
                          a=fl.ptr(p + 'a'), b=fl.ptr(p + 'b'), stats=blk['estat'].data_ptr(),
-                         ntok=blk['nq'], D=D, FD=sp.FD, wparts=blk.get('wparts', 0))
+                         ntok=blk['nq'], D=D, FD=sp.FD, wparts=blk.get('wparts', 0),
+                         wq_next=blk.get('wq_next', 0), qp_next=blk.get('qp_next', Rows()))
 
     def _epi_bwd_desc(self, blk):
         D, Tq, FD = self.spec.D, blk['Tq'], self.spec.FD
         return RfEpiBwdDesc(f=self._epi_desc(blk), dout=self._dout_rows(blk), dout2=Rows(),
                             df=crows(blk['dF'], Tq, D), df1=crows(blk['dF1'], Tq, FD),
                             dxp=crows(blk['dXP'], Tq, D), dx=crows(blk['dX'], Tq, D),
-                            dq=crows(blk['dQin'], Tq, D), partial=blk['partial'].data_ptr(), dq_accumulate=0)
+                            dq=crows(blk['dQin'], Tq, D), partial=blk['partial'].data_ptr(), dq_accumulate=0,
+                            wq_in=blk.get('wq_in', 0), dqp_in=blk.get('dqp_in', Rows()))
 
     def _attn_bwd_desc(self, blk):
         D = self.spec.D
@@ -304,13 +306,27 @@ class RealformerPlan:
                                    w=fl.ptr(self._wkv(b)), ntok=b['nk'], N=D, K=2 * D, ldw=D, w_nt=0, **gemm))
             igd.append(ig)
         self.t_ingrad = max(max(cdiv(b['nq'], 64), cdiv(b['nk'], 64)) for b in self.blocks)
+        ig_all = []
         if self.rfw:
+            # layer i's epilogue forward also runs layer i+1's query projection and layer i's
+            # epilogue backward adds layer i+1's dQP W_q to its upstream gradient, so the q GEMMs
+            # of layers > 0 go away and the remaining input-gradient GEMMs (layer-0 dq_in, every
+            # dkv_in: they only feed the per-modality sums) run as one launch after the backward
+            qd = [[] for _ in range(nl)]
+            ig_all = [x for l_, ig in enumerate(igd) for x in ig if l_ == 0 or x.K == 2 * D]
+            igd = [[] for _ in range(nl)]
             # every token GEMM and epilogue Linear on mep_wsplit parts (refreshed at the start of
             # each forward): W' = the weight as it is (w_nt) or its transpose (dY W products)
             arena = _lib.PartsArena()
             patch = []
-            for dsc in ud + pd + [x for l_ in qd for x in l_] + [x for l_ in igd for x in l_]:
+            for dsc in ud + pd + ig_all:
                 patch.append((dsc, arena.add(dsc.w, dsc.N, dsc.K, dsc.ldw, 0 if dsc.w_nt else 1)))
+            fused = []
+            for b in self.blocks:
+                if b['i'] < nl - 1:
+                    nxt = self._blk(b['j'], b['i'] + 1)
+                    wq = fl.ptr(nxt['pre'] + 'w_qkv.0.weight')
+                    fused.append((b, nxt, arena.add(wq, D, D, D, 0), arena.add(wq, D, D, D, 1)))
             epi_off = [arena.add_epi(D, FD, fl.ptr(b['pre'] + 'proj.weight'), fl.ptr(b['pre'] + 'ffn.0.weight'),
                                      fl.ptr(b['pre'] + 'ffn.2.weight')) for b in self.blocks]
             self.wparts, self.d_wsplit, self.t_wsplit = arena.build(dev)
@@ -318,6 +334,11 @@ class RealformerPlan:
                 dsc.w = self.wparts.data_ptr() + off
             for b, off in zip(self.blocks, epi_off):
                 b['wparts'] = self.wparts.data_ptr() + off
+            for b, nxt, o_fwd, o_bwd in fused:
+                b['wq_next'] = self.wparts.data_ptr() + o_fwd
+                b['qp_next'] = crows(nxt['QP'], nxt['Tq'], D)
+                b['wq_in'] = self.wparts.data_ptr() + o_bwd
+                b['dqp_in'] = crows(nxt['dQP'], nxt['Tq'], D)
             self.t_unify = max(cdiv(self.ntok[m], 16) for m in sp.mods)
             self.t_proj = max(cdiv(b['nk'], 16) for b in self.blocks)
             self.t_ingrad = max(max(cdiv(b['nq'], 16), cdiv(b['nk'], 16)) for b in self.blocks)
@@ -325,6 +346,7 @@ class RealformerPlan:
         self.d_proj = DescArray(GemmDesc, pd, dev)
         self.d_q = [DescArray(GemmDesc, x, dev) for x in qd]
         self.d_ingrad = [DescArray(GemmDesc, x, dev) for x in igd]
+        self.d_ingrad_all = DescArray(GemmDesc, ig_all, dev)
         for i in range(nl):
             layer = [b for b in self.blocks if b['i'] == i]
             self.d_epi.append(DescArray(RfEpiDesc, [self._epi_desc(b) for b in layer], dev))
@@ -518,6 +540,7 @@ class RealformerPlan:
             launch('mep_rfw_epi_bwd' if self.rfw else 'mep_rf_epi_bwd', self.d_epib[i], self.t_epib[i], stream, extra=ex)
             launch('mep_attn_bwd', self.d_attnb[i], self.t_attnb[i], stream, threads=self.f_attnb[i])
             self._gemm(self.d_ingrad[i], self.t_ingrad, stream)
+        self._gemm(self.d_ingrad_all, self.t_ingrad, stream)
         launch('mep_sum_rows', self.d_sum, self.t_sum, stream)
         launch('mep_wgrad', self.d_wgrad, self.t_wgrad, stream)
         # weight-gradient split sums and LayerNorm / ReZero / residual-coefficient column sums: one

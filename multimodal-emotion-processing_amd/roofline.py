@@ -124,8 +124,14 @@ def rf_launch_costs(plan):
     for blk in plan.blocks:
         Tq, Tk, nq, nk = blk['Tq'], blk['Tk'], blk['nq'], blk['nk']
         gemm('mep_gemm', nk, 2 * D, D)                         # [K | V] = U [W_k; W_v]^T
-        gemm('mep_gemm', nq, D, D)                             # Q = q W_q^T
-        gemm('mep_gemm', nq, D, D, accumulate=True)            # dq_in += dQ W_q
+        if rfw and blk['i'] > 0:
+            # fused into the previous layer's epilogue launches (q = that layer's output):
+            # Q = q W_q^T after its LN2, dq_in += dQ W_q before its LN2 backward
+            add(EPI_F, 2 * nq * D * D, 4 * nq * D + 4 * D * D)
+            add(EPI_B, 2 * nq * D * D, 4 * nq * D + 4 * D * D)
+        else:
+            gemm('mep_gemm', nq, D, D)                         # Q = q W_q^T
+            gemm('mep_gemm', nq, D, D, accumulate=True)        # dq_in += dQ W_q
         gemm('mep_gemm', nk, D, 2 * D)                         # dkv_in = [dK | dV] [W_k; W_v]
         r_in = 1 if blk['i'] > 0 else 0
         r_out = 1 if 'S' in blk else 0
