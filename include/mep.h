@@ -322,8 +322,9 @@ int mep_wsplit(const mep_wsplit_desc* descs, int n_desc, int max_units, mep_stre
 
 /* mep_wgemm: mep_gemm's Y = act(alpha X W'^T + bias + table) (+ Y) with desc.w = the mep_wsplit
  * parts of W' [N][K] (a Linear weight as it is; a dY W product takes the parts of W^T); one wave
- * per 16 tokens x all N <= 256 columns.  ldw, w_nt and bf16 are unused. */
-int mep_wgemm(const mep_gemm_desc* descs, int n_desc, int max_tiles, mep_stream_t stream);
+ * per 16 tokens x 32 columns, grid (max_tiles, n_desc, ceil(max_n / 32)), max_n = the largest N
+ * (<= 256).  ldw, w_nt and bf16 are unused. */
+int mep_wgemm(const mep_gemm_desc* descs, int n_desc, int max_tiles, int max_n, mep_stream_t stream);
 /* mep_rfw_epi_fwd / _bwd: mep_rf_epi_fwd / _bwd on the parts at desc.wparts; one wave per 16-token
  * tile, one partial row per tile; D in {32, 64, 96, 128}, FD in {D, 2D}. */
 int mep_rfw_epi_fwd(const mep_rf_epi_desc* descs, int n_desc, int max_tiles, int D, int FD, mep_stream_t stream);

@@ -217,7 +217,7 @@ STRUCTS = {'mep_rows': Rows, 'mep_gemm_desc': GemmDesc, 'mep_wgrad_desc': WgradD
 
 P = ctypes.c_void_p
 # name -> argtypes (all return int)
-GROUPED = ['mep_gemm', 'mep_wgemm', 'mep_wsplit', 'mep_unify', 'mep_wgrad', 'mep_wgrad_reduce', 'mep_layernorm_fwd', 'mep_layernorm_bwd', 'mep_colsum', 'mep_sum_rows',
+GROUPED = ['mep_gemm', 'mep_wsplit', 'mep_unify', 'mep_wgrad', 'mep_wgrad_reduce', 'mep_layernorm_fwd', 'mep_layernorm_bwd', 'mep_colsum', 'mep_sum_rows',
            'mep_pool_fwd', 'mep_pool_bwd']
 GROUPED_T = ['mep_attn_fwd', 'mep_attn_bwd',      # + MEP_ATTN_* variant flags
              'mep_block_epi_fwd', 'mep_block_epi_bwd']  # + D (compiled variant)
@@ -239,6 +239,7 @@ SIGNATURES.update({
     'mep_threshold_sweep': [ctypes.POINTER(SweepDesc), P],
     'mep_assemble_windows': [ctypes.POINTER(WindowDesc), i32, P],
     'mep_tgemm': [P, i32, i32, i32, i32, P],
+    'mep_wgemm': [P, i32, i32, i32, P],
     'mep_abi_version': [],
     'mep_rf_rows': [i32, i32],
     'mep_last_error': [ctypes.c_char_p, ctypes.c_size_t],

@@ -830,7 +830,11 @@ template <int D, bool BF16> struct EpiOne {
     static constexpr bool ON_BF = BF16 && MEP_EPI_ONE_BF16 && D <= MEP_EPI_ONE_BF16_MAXD;
     static constexpr bool FWD = (MEP_EPI_ONE_FWD && D <= 96) || ON_BF, BWD = (MEP_EPI_ONE_BWD && D <= 96) || ON_BF;
     static constexpr int NPART = BF16 ? 1 : 3;
-    static constexpr int FWD_WP = BF16 ? 1 : (D == 96 ? 2 : 3), FWD_WM = NPART;
+#ifndef MEP_EPI_FWD_WM2
+#define MEP_EPI_FWD_WM2 0   // single-phase fp32 forward at D = 96: 1 = 3-part Wp + 2-part Wm (144 KB)
+#endif
+    static constexpr int FWD_WP = BF16 ? 1 : (D == 96 && !MEP_EPI_FWD_WM2 ? 2 : 3);
+    static constexpr int FWD_WM = BF16 ? 1 : (D == 96 && MEP_EPI_FWD_WM2 ? 2 : NPART);
     static constexpr int BWD_WP = NPART, BWD_WM = BF16 ? 1 : (D == 96 ? 2 : 3);
     static constexpr int FWD_BYTES = SplitW<D, D / 32, FWD_WP>::BYTES + SplitW<D, D / 16, FWD_WM>::BYTES;
     static constexpr int BWD_BYTES = SplitW<2 * D, D / 32, BWD_WM>::BYTES + SplitW<D, D / 32, BWD_WP>::BYTES;

@@ -662,17 +662,23 @@ __global__ __launch_bounds__(64 * rfw_waves<D>()) void k_rfw_bwd(const mep_rf_ep
 }
 
 // ---------------------------------------------------------------- token GEMM on pre-split weights
-// Y[tok][n] = act(alpha sum_k X[tok][k] W'[n][k] + bias[n] + table[tok % T][n]) (+ Y): one wave per
-// 16 tokens x 32 columns (grid.z = column groups), the X blocks and weight fragments of RP k pairs
-// in flight ahead of their MFMAs (a ring over k pairs, the pair loop unrolled by RP).
-constexpr int WG_RP = 4;
-__global__ __launch_bounds__(64) void k_wgemm(const mep_gemm_desc* __restrict__ descs) {
-    constexpr int NI = 2;
+// Y[tok][n] = act(alpha sum_k X[tok][k] W'[n][k] + bias[n] + table[tok % T][n]) (+ Y): one workgroup
+// per 16 tokens x 32 columns (grid.z = column groups), its 4 waves splitting the k pairs (wave w
+// takes pairs w, w + 4, ...; every X block and weight fragment of a group of 4 pairs is loaded
+// before its MFMAs, so a small K costs one memory latency, not one per pair); the 4 partial
+// tiles are summed through LDS in wave order (deterministic) and wave 0 runs the epilogue.
+#ifndef MEP_WGM_WAVES
+#define MEP_WGM_WAVES 1   // waves splitting the k pairs of a workgroup (4: all loads of K <= 512 at once)
+#endif
+constexpr int WGM_WAVES = MEP_WGM_WAVES;
+__global__ __launch_bounds__(64 * WGM_WAVES) void k_wgemm(const mep_gemm_desc* __restrict__ descs) {
+    constexpr int NI = 2, GP = 4;   // output tiles per workgroup, pairs per wave per group
+    __shared__ f32x4 red[WGM_WAVES][NI][64];
     const mep_gemm_desc& d = descs[blockIdx.y];
     const int tile = blockIdx.x, cg = blockIdx.z;
     const int ntok = d.ntok, N = d.N, K = d.K;
-    if (tile * 16 >= ntok || cg * 32 >= N) return;
-    const int lane = threadIdx.x & 63, c = lane & 15, g = lane >> 4;
+    if (tile * 16 >= ntok || cg * 32 >= N) return;   // whole workgroup
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, c = lane & 15, g = lane >> 4;
     const int tok = tile * 16 + c, tc = min(tok, ntok - 1);
     const int npk = (K + 31) >> 5;
     const bool xvec = (K % 4 == 0) && ((d.x.ptr & 15) == 0) && (d.x.sB % 4 == 0) && (d.x.sT % 4 == 0);
@@ -680,12 +686,9 @@ __global__ __launch_bounds__(64) void k_wgemm(const mep_gemm_desc* __restrict__ 
     const int rows = (N + 31) & ~31;   // rows of the parts (mep_wsplit R)
     const PartPtr wl = reinterpret_cast<PartPtr>(G<const unsigned char>(d.w)) + ((32 * cg + c) * npk) * 4 + g;
     const int tstride = rows * npk * 4;   // units per part
-    f32x4 acc[NI];
-#pragma unroll
-    for (int i = 0; i < NI; ++i) acc[i] = zero_f4();
-    // the epilogue's loads (bias, position-table row, accumulated y) issued before the main loop
-    f32x4 add[NI];
-    {
+    // wave 0: the epilogue's loads (bias, position-table row, accumulated y), issued first
+    f32x4 add[NI], yold[NI];
+    if (wave == 0) {
         const gfloat* bias = G<const float>(d.bias);
         const gfloat* trow = d.table ? G<const float>(d.table) + (int64_t)(tc % d.y.T) * (d.ldt ? d.ldt : N) : nullptr;
         const gfloat* yr = row_ptr(d.y, tc);
@@ -695,13 +698,9 @@ __global__ __launch_bounds__(64) void k_wgemm(const mep_gemm_desc* __restrict__ 
             for (int r = 0; r < 4; ++r) {
                 const int n = min(32 * cg + 16 * i + 4 * g + r, N - 1);
                 add[i][r] = (bias ? bias[n] : 0.f) + (trow ? trow[n] : 0.f);
-                acc[i][r] = 0.f;
-                if (d.accumulate) acc[i][r] = yr[n];   // kept apart: y is added after the activation
+                yold[i][r] = d.accumulate ? yr[n] : 0.f;
             }
     }
-    f32x4 yold[NI];
-#pragma unroll
-    for (int i = 0; i < NI; ++i) { yold[i] = acc[i]; acc[i] = zero_f4(); }
     auto xblk = [&](int k) {
         f32x4 v = zero_f4();
         if (xvec) {
@@ -712,37 +711,45 @@ __global__ __launch_bounds__(64) void k_wgemm(const mep_gemm_desc* __restrict__ 
         }
         return v;
     };
-    struct Slot { f32x4 x0, x1; OpN<3> a[NI]; };
-    auto ld = [&](Slot& s, int p) {
-        if (p >= npk) return;
-        s.x0 = xblk(32 * p + 4 * g);
-        s.x1 = xblk(32 * p + 16 + 4 * g);
+    f32x4 acc[NI];
 #pragma unroll
-        for (int i = 0; i < NI; ++i)
+    for (int i = 0; i < NI; ++i) acc[i] = zero_f4();
+    for (int p0 = wave; p0 < npk; p0 += WGM_WAVES * GP) {
+        f32x4 x0[GP], x1[GP];
+        OpN<3> a[GP][NI];
 #pragma unroll
-            for (int t = 0; t < 3; ++t)
-                s.a[i].p[t] = __builtin_bit_cast(bf16x8, wl[t * tstride + (16 * i * npk + p) * 4]);
-    };
-    Slot ring[WG_RP];
-#pragma unroll
-    for (int q = 0; q < WG_RP; ++q) ld(ring[q], q);
-    for (int p0 = 0; p0 < npk; p0 += WG_RP) {
-#pragma unroll
-        for (int q = 0; q < WG_RP; ++q) {
-            const int p = p0 + q;
+        for (int u = 0; u < GP; ++u) {
+            const int p = p0 + WGM_WAVES * u;
             if (p < npk) {
-                const OpN<3> b = opn<3>(ring[q].x0, ring[q].x1);
-                OpN<3> a[NI];
+                x0[u] = xblk(32 * p + 4 * g);
+                x1[u] = xblk(32 * p + 16 + 4 * g);
 #pragma unroll
-                for (int i = 0; i < NI; ++i) a[i] = ring[q].a[i];
-                ld(ring[q], p + WG_RP);
+                for (int i = 0; i < NI; ++i)
 #pragma unroll
-                for (int i = 0; i < NI; ++i) acc[i] = mma_n<3>(a[i], b, acc[i]);
+                    for (int t = 0; t < 3; ++t)
+                        a[u][i].p[t] = __builtin_bit_cast(bf16x8, wl[t * tstride + (16 * i * npk + p) * 4]);
             }
-            __builtin_amdgcn_sched_barrier(0);
+        }
+#pragma unroll
+        for (int u = 0; u < GP; ++u) {
+            if (p0 + WGM_WAVES * u < npk) {
+                const OpN<3> b = opn<3>(x0[u], x1[u]);
+#pragma unroll
+                for (int i = 0; i < NI; ++i) acc[i] = mma_n<3>(a[u][i], b, acc[i]);
+            }
         }
     }
-    if (tok >= ntok) return;
+#pragma unroll
+    for (int i = 0; i < NI; ++i) red[wave][i][lane] = acc[i];
+    __syncthreads();
+    if (wave != 0 || tok >= ntok) return;
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+        f32x4 t = red[0][i][lane];
+#pragma unroll
+        for (int w = 1; w < WGM_WAVES; ++w) t += red[w][i][lane];
+        acc[i] = t;
+    }
     gfloat* yr = row_ptr(d.y, tok);
 #pragma unroll
     for (int i = 0; i < NI; ++i) {
@@ -786,10 +793,12 @@ extern "C" int mep_wsplit(const mep_wsplit_desc* descs, int n_desc, int max_unit
     return mep_check_launch("mep_wsplit");
 }
 
-extern "C" int mep_wgemm(const mep_gemm_desc* descs, int n_desc, int max_tiles, mep_stream_t stream) {
+extern "C" int mep_wgemm(const mep_gemm_desc* descs, int n_desc, int max_tiles, int max_n, mep_stream_t stream) {
     if (n_desc <= 0 || max_tiles <= 0) return 0;
-    // grid.z: 32-column groups of the widest descriptor (N <= 256)
-    hipLaunchKernelGGL(k_wgemm, dim3(max_tiles, n_desc, 8), dim3(64), 0, (hipStream_t)stream, descs);
+    if (max_n <= 0 || max_n > 256) { mep_set_error("mep_wgemm: 0 < max_n <= 256"); return MEP_EINVAL; }
+    // grid.z: the 32-column groups of the widest descriptor
+    hipLaunchKernelGGL(k_wgemm, dim3(max_tiles, n_desc, (max_n + 31) / 32), dim3(64 * WGM_WAVES), 0,
+                       (hipStream_t)stream, descs);
     return mep_check_launch("mep_wgemm");
 }
 

@@ -516,7 +516,8 @@ class RealformerPlan:
     def _gemm(self, descs, tiles, stream):
         """a token-GEMM launch: mep_wgemm on the arena's parts, or the mep_gemm path"""
         if self.rfw:
-            launch('mep_wgemm', descs, tiles, stream)
+            if descs.n:
+                _lib.call('mep_wgemm', descs.ptr, descs.n, int(tiles), max(d.N for d in descs.items), stream=stream)
         else:
             _lib.gemm('mep_gemm', descs, tiles, stream)
 
