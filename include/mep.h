@@ -375,7 +375,10 @@ int mep_layernorm_bwd(const mep_ln_desc* descs, int n_desc, int max_tiles, mep_s
 
 /* ---------------------------------------------------------------- reductions
  * Column sums over tiles: out[c] (+)= sum_t partial[t*ld + c].  Used for LayerNorm / bias /
- * position-embedding / per-row head gradient partials. */
+ * position-embedding / per-row head gradient partials.  accumulate: bit 0 = add onto out;
+ * MEP_COLSUM_NOT_GRAD = out is not a gradient (e.g. the batch loss), left out of the norm that
+ * mep_reduce_grads can fold in. */
+#define MEP_COLSUM_NOT_GRAD 2
 typedef struct {
     uint64_t partial, out;
     int32_t  n_rows, n_cols, ld, accumulate;
@@ -456,7 +459,12 @@ int mep_head_reduce(const mep_head_desc* d, uint64_t g_trans, uint64_t g_ln_w, u
 int mep_reduce_grads(const mep_wgrad_desc* wgrad, int n_wgrad, int wgrad_tiles, const mep_colsum_desc* colsum,
                      int n_colsum, int colsum_tiles, const mep_head_desc* head, uint64_t g_trans, uint64_t g_ln_w,
                      uint64_t g_ln_b, uint64_t g_wo, uint64_t g_bo, uint64_t g_wc0, uint64_t g_wc1, uint64_t loss,
-                     mep_stream_t stream);
+                     float* norm, int* step, const float* hyper, mep_stream_t stream);
+/* norm != 0 (a single-process step): the clip's gradient-norm pass folded in -- block k of the
+ * launch writes the sum of squares of the gradients it wrote to norm[1024 + k], block 0 advances
+ * *step and writes the step's Adam scalars (norm = the optimizer workspace of mep_clip_adam_ext,
+ * >= 1024 + mep_reduce_grads_grid(..) floats; step / hyper as there).  norm = 0: no norm pass. */
+int mep_reduce_grads_grid(int n_wgrad, int wgrad_tiles, int n_colsum, int colsum_tiles, const mep_head_desc* head);
 int mep_head_partial_stride(int NC);
 
 /* multi_circle_loss per row (cmu-mosei/run.py:342-351) as a standalone op for callers that
@@ -484,6 +492,13 @@ int mep_clip_adam(float* params, float* grads, float* exp_avg, float* exp_avg_sq
                   const mep_seg* segs, int n_seg, int64_t total_len, float* partial,
                   float* gnorm_out, const float* hyper, int* step, int decoupled,
                   mep_stream_t stream);
+/* n_ext > 0: the norm partials (n_ext of them, at partial[1024 ..]) and the step's scalars were
+ * written by a mep_reduce_grads launch with norm = partial, which also advanced *step: the norm
+ * launch is skipped.  n_ext = 0: mep_clip_adam. */
+int mep_clip_adam_ext(float* params, float* grads, float* exp_avg, float* exp_avg_sq,
+                      const mep_seg* segs, int n_seg, int64_t total_len, float* partial,
+                      float* gnorm_out, const float* hyper, int* step, int decoupled, int n_ext,
+                      mep_stream_t stream);
 
 /* advance the device-side dropout seed (graph-replay safe) */
 int mep_seed_advance(uint64_t* seed, mep_stream_t stream);

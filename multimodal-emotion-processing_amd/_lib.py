@@ -129,6 +129,9 @@ def rfw_part_offsets(D, FD):
     return offs, o
 
 
+COLSUM_NOT_GRAD = 2   # MEP_COLSUM_NOT_GRAD: a column sum that is not a gradient (left out of the folded norm)
+
+
 def wsplit_desc(src, dst, N, K, ld, trans):
     """mep_wsplit descriptor of W' [N][K] (W'(n, k) = src[n * ld + k], or src[k * ld + n] when
     trans) with its rows padded to a multiple of 32 (the wave kernels' output-tile pairs)"""
@@ -230,10 +233,12 @@ SIGNATURES.update({
     'mep_head_fwd_bwd': [HP, P],
     'mep_head_reduce': [HP, u64, u64, u64, u64, u64, u64, u64, u64, P],
     'mep_head_partial_stride': [i32],
-    'mep_reduce_grads': [P, i32, i32, P, i32, i32, HP, u64, u64, u64, u64, u64, u64, u64, u64, P],
+    'mep_reduce_grads': [P, i32, i32, P, i32, i32, HP, u64, u64, u64, u64, u64, u64, u64, u64, P, P, P, P],
+    'mep_reduce_grads_grid': [i32, i32, i32, i32, HP],
     'mep_circle_loss_fwd': [P, P, i32, i32, i32, P, P, P],
     'mep_circle_loss_bwd': [P, P, i32, i32, P, P],
     'mep_clip_adam': [P, P, P, P, P, i32, i64, P, P, P, P, i32, P],
+    'mep_clip_adam_ext': [P, P, P, P, P, i32, i64, P, P, P, P, i32, i32, P],
     'mep_seed_advance': [P, P],
     'mep_rf_head': [ctypes.POINTER(RfHeadDesc), P],
     'mep_threshold_sweep': [ctypes.POINTER(SweepDesc), P],

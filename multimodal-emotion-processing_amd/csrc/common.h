@@ -437,10 +437,12 @@ MEP_DEV void wave_store16(const float* src, int lda, const mep_rows& dst, int r0
 // Block bodies shared by their own launches and the fused mep_reduce_grads launch (256 threads).
 // Weight-gradient split sum (gemm.hip k_wgrad_reduce): block bx of descriptor d sums the
 // n_split partials of 256 consecutive (n, k) entries in a fixed order.
-MEP_DEV void wgrad_reduce_block(const mep_wgrad_desc& d, int bx) {
+// Each returns the sum of squares of the gradient values its thread wrote (the fused gradient-norm
+// partials of mep_reduce_grads; ignored by the standalone launches).
+MEP_DEV float wgrad_reduce_block(const mep_wgrad_desc& d, int bx) {
     const int64_t nk = (int64_t)d.N * d.Ktot;
     const int64_t i = (int64_t)bx * 256 + threadIdx.x;
-    if (i >= nk) return;
+    if (i >= nk) return 0.f;
     const gfloat* part = G<const float>(d.partial);
     float s = 0.f;
 #pragma unroll 8
@@ -450,15 +452,17 @@ MEP_DEV void wgrad_reduce_block(const mep_wgrad_desc& d, int bx) {
     int j = 0;
     while (j < d.n_b - 1 && k >= d.kb[j]) { k -= d.kb[j]; ++j; }
     gfloat* o = G<float>(d.out[j]) + (d.out_trans ? (int64_t)k * d.ldo[j] + n : (int64_t)n * d.ldo[j] + k);
-    *o = d.accumulate ? *o + s : s;
+    const float v = d.accumulate ? *o + s : s;
+    *o = v;
+    return v * v;
 }
 
 // Column sums of a partial matrix (optim.hip k_colsum): block bx = 32 columns x 8 row groups,
 // fixed-order combine.
-MEP_DEV void colsum_block(const mep_colsum_desc& d, int bx) {
+MEP_DEV float colsum_block(const mep_colsum_desc& d, int bx) {
     const int cl = threadIdx.x & 31, g = threadIdx.x >> 5;
     const int c = bx * 32 + cl;
-    if (bx * 32 >= d.n_cols) return;   // whole block
+    if (bx * 32 >= d.n_cols) return 0.f;   // whole block
     __shared__ float red[8][32];
     float s = 0.f;
     if (c < d.n_cols) {
@@ -473,8 +477,25 @@ MEP_DEV void colsum_block(const mep_colsum_desc& d, int bx) {
 #pragma unroll
         for (int k = 0; k < 8; ++k) t += red[k][cl];
         gfloat* o = G<float>(d.out) + c;
-        *o = d.accumulate ? *o + t : t;
+        const float v = (d.accumulate & 1) ? *o + t : t;
+        *o = v;
+        return (d.accumulate & MEP_COLSUM_NOT_GRAD) ? 0.f : v * v;
     }
+    return 0.f;
+}
+
+// clip + optimizer workspace (optim.hip): per-workgroup g^2 partials of the norm pass in
+// [0, OPT_NPART), the step's scalars at OPT_SCAL (lr / (1 - b1^t), sqrt(1 - b2^t)), and from
+// OPT_EXT0 the partials of a mep_reduce_grads launch that folded the norm pass in
+constexpr int OPT_NPART = 1016, OPT_SCAL = OPT_NPART, OPT_EXT0 = 1024;
+
+// the step counter and the bias corrections (double pow) once per step: one thread of one workgroup
+MEP_DEV void opt_step_scalars(float* partial, int* step, const float* hyper) {
+    const int ts = step[0] + 1;
+    step[0] = ts;
+    const double lr = hyper[0], b1 = hyper[1], b2 = hyper[2];
+    partial[OPT_SCAL] = (float)(lr / (1.0 - pow(b1, (double)ts)));
+    partial[OPT_SCAL + 1] = (float)sqrt(1.0 - pow(b2, (double)ts));
 }
 
 }  // namespace mep

@@ -15,8 +15,8 @@ using namespace mep;
 
 namespace {
 
-constexpr int NPART = 1016;        // per-workgroup norm partials; partial[NPART ..] holds the step's scalars
-constexpr int SCAL = NPART;        // partial[SCAL + 0..2]: lr / (1 - b1^t), sqrt(1 - b2^t), t
+constexpr int NPART = OPT_NPART;    // per-workgroup norm partials; partial[NPART ..] holds the step's scalars
+constexpr int SCAL = OPT_SCAL;      // partial[SCAL + 0..1]: lr / (1 - b1^t), sqrt(1 - b2^t)
 constexpr int OPT_THREADS = 256;
 constexpr int MAX_SEG = 16;
 
@@ -55,14 +55,7 @@ __global__ __launch_bounds__(OPT_THREADS) void k_sqnorm(const float* __restrict_
         float t = 0.f;
         for (int w = 0; w < OPT_THREADS / 64; ++w) t += red[w];
         partial[blockIdx.x] = t;
-        if (blockIdx.x == 0 && step) {
-            // the step counter and the bias corrections (double pow) once per step, not per thread
-            const int ts = step[0] + 1;
-            step[0] = ts;
-            const double lr = hyper[0], b1 = hyper[1], b2 = hyper[2];
-            partial[SCAL] = (float)(lr / (1.0 - pow(b1, (double)ts)));
-            partial[SCAL + 1] = (float)sqrt(1.0 - pow(b2, (double)ts));
-        }
+        if (blockIdx.x == 0 && step) opt_step_scalars(partial, step, hyper);
     }
 }
 
@@ -85,7 +78,7 @@ MEP_DEV void adam_elem(float& pv, float& gv, float& mv, float& vv, const AdamCoe
 // hyper: [lr, beta1, beta2, eps, weight_decay, max_norm, grad_scale]
 __global__ __launch_bounds__(OPT_THREADS) void k_clip_adam(float* __restrict__ p, float* __restrict__ g,
                                                            float* __restrict__ m, float* __restrict__ v, Segs segs,
-                                                           const float* __restrict__ partial, int npart,
+                                                           const float* __restrict__ partial, int npart, int pbase,
                                                            const float* __restrict__ hyper,
                                                            const int* __restrict__ step, float* gnorm_out,
                                                            int decoupled) {
@@ -93,7 +86,7 @@ __global__ __launch_bounds__(OPT_THREADS) void k_clip_adam(float* __restrict__ p
     // DPP tree, then the 4 waves in order): identical totals, no grid barrier
     __shared__ float red[OPT_THREADS / 64];
     float s = 0.f;
-    for (int i = threadIdx.x; i < npart; i += OPT_THREADS) s += partial[i];
+    for (int i = threadIdx.x; i < npart; i += OPT_THREADS) s += partial[pbase + i];
     s = wave_sum(s);
     if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
     __syncthreads();
@@ -176,9 +169,9 @@ __global__ __launch_bounds__(256) void k_sum_rows(const mep_sum_desc* __restrict
 
 }  // namespace
 
-extern "C" int mep_clip_adam(float* params, float* grads, float* exp_avg, float* exp_avg_sq, const mep_seg* segs,
-                             int n_seg, int64_t total_len, float* partial, float* gnorm_out, const float* hyper,
-                             int* step, int decoupled, mep_stream_t stream) {
+extern "C" int mep_clip_adam_ext(float* params, float* grads, float* exp_avg, float* exp_avg_sq, const mep_seg* segs,
+                                 int n_seg, int64_t total_len, float* partial, float* gnorm_out, const float* hyper,
+                                 int* step, int decoupled, int n_ext, mep_stream_t stream) {
     if (n_seg <= 0 || n_seg > MAX_SEG || !partial || !hyper || !step) {
         mep_set_error("mep_clip_adam: need 1..16 segments, partial, hyper and step buffers");
         return MEP_EINVAL;
@@ -199,12 +192,22 @@ extern "C" int mep_clip_adam(float* params, float* grads, float* exp_avg, float*
     // thread serialised 4 dependent load -> store trips), one partial per workgroup for the norm
     int grid = (int)((longest + OPT_THREADS * 4 - 1) / (OPT_THREADS * 4));
     grid = grid < 1 ? 1 : (grid > NPART ? NPART : grid);
-    hipLaunchKernelGGL(k_sqnorm, dim3(grid), dim3(OPT_THREADS), 0, (hipStream_t)stream, grads, s, partial, step, hyper);
-    int rc = mep_check_launch("mep_clip_adam/sqnorm");
-    if (rc) return rc;
+    if (n_ext <= 0) {
+        hipLaunchKernelGGL(k_sqnorm, dim3(grid), dim3(OPT_THREADS), 0, (hipStream_t)stream, grads, s, partial, step, hyper);
+        int rc = mep_check_launch("mep_clip_adam/sqnorm");
+        if (rc) return rc;
+    }
     hipLaunchKernelGGL(k_clip_adam, dim3(grid), dim3(OPT_THREADS), 0, (hipStream_t)stream, params, grads, exp_avg,
-                       exp_avg_sq, s, partial, grid, hyper, step, gnorm_out, decoupled);
+                       exp_avg_sq, s, partial, n_ext > 0 ? n_ext : grid, n_ext > 0 ? OPT_EXT0 : 0, hyper, step,
+                       gnorm_out, decoupled);
     return mep_check_launch("mep_clip_adam/update");
+}
+
+extern "C" int mep_clip_adam(float* params, float* grads, float* exp_avg, float* exp_avg_sq, const mep_seg* segs,
+                             int n_seg, int64_t total_len, float* partial, float* gnorm_out, const float* hyper,
+                             int* step, int decoupled, mep_stream_t stream) {
+    return mep_clip_adam_ext(params, grads, exp_avg, exp_avg_sq, segs, n_seg, total_len, partial, gnorm_out, hyper,
+                             step, decoupled, 0, stream);
 }
 
 extern "C" int mep_seed_advance(uint64_t* seed, mep_stream_t stream) {

@@ -459,7 +459,7 @@ struct HeadGrads {
 // records each, 8 row groups per column (+ the batch loss in workgroup 0); workgroups after
 // that: 32 columns k of one classifier e, dWc_e[n][k] = sum_b dlogit_e[b][n] pooled_e[b][k] for
 // every n, rows split over 8 groups.  Fixed summation order (deterministic).
-MEP_DEV void head_reduce_block(const mep_head_desc& d, const HeadGrads& g, int bx) {
+MEP_DEV float head_reduce_block(const mep_head_desc& d, const HeadGrads& g, int bx) {
     const int NC = d.NC, F = d.F, B = d.B;
     const HeadOff o = head_off(NC);
     const int nA = o.dl0;                 // everything before the dlogit records
@@ -475,7 +475,7 @@ MEP_DEV void head_reduce_block(const mep_head_desc& d, const HeadGrads& g, int b
             for (int b = rg; b < B; b += 8) s += part[(int64_t)b * o.stride + i];
         }
         red[rg][0][cl] = s;
-        float ls = 0.f;
+        float ls = 0.f, sq = 0.f;
         if (bx == 0)
             for (int b = threadIdx.x; b < B; b += 256) ls += G<const float>(d.row_loss)[b];
         __syncthreads();
@@ -490,6 +490,7 @@ MEP_DEV void head_reduce_block(const mep_head_desc& d, const HeadGrads& g, int b
             else if (i < o.trans) dst = g.g_lnb + (i - o.lnb);
             else dst = g.g_trans + (i - o.trans);
             *G<float>(reinterpret_cast<uint64_t>(dst)) = t;
+            sq = t * t;
         }
         if (bx == 0) {
             ls = wave_sum(ls);
@@ -499,7 +500,7 @@ MEP_DEV void head_reduce_block(const mep_head_desc& d, const HeadGrads& g, int b
             if (threadIdx.x == 0)
                 *G<float>(reinterpret_cast<uint64_t>(g.loss)) = red[0][1][0] + red[1][1][0] + red[2][1][0] + red[3][1][0];
         }
-        return;
+        return sq;   // the loss is not a gradient
     }
     const int wb = bx - nA32;
     const int nkb = (F + 31) / 32;
@@ -522,6 +523,7 @@ MEP_DEV void head_reduce_block(const mep_head_desc& d, const HeadGrads& g, int b
 #pragma unroll
     for (int n = 0; n < NCMAX; ++n) if (n < NC) red[rg][n][cl] = acc[n];
     __syncthreads();
+    float sq = 0.f;
     if (k < F) {
         float* out = e ? g.g_wc1 : g.g_wc0;
         for (int n = rg; n < NC; n += 8) {
@@ -529,8 +531,10 @@ MEP_DEV void head_reduce_block(const mep_head_desc& d, const HeadGrads& g, int b
 #pragma unroll
             for (int q = 0; q < 8; ++q) t += red[q][n][cl];
             *G<float>(reinterpret_cast<uint64_t>(out + (int64_t)n * F + k)) = t;
+            sq += t * t;
         }
     }
+    return sq;
 }
 
 __global__ __launch_bounds__(256) void k_head_reduce(mep_head_desc d, HeadGrads g) {
@@ -544,15 +548,36 @@ __host__ __device__ inline int head_reduce_blocks(const mep_head_desc& d) {
 // Every gradient reduction of a training step in ONE launch: the head-parameter sums (largest
 // blocks first), the weight-gradient split sums and the column sums, each block taking one job
 // (block bodies in common.h); there are no dependencies between them.
+// norm (optional, single-process steps): the clip's gradient-norm pass folded in -- every block
+// writes the sum of squares of the gradients it wrote to norm[OPT_EXT0 + block] (fixed-order
+// block reduction) and block 0 advances the optimizer step and its scalars (optim.hip
+// mep_clip_adam_ext then skips its own norm launch).
 __global__ __launch_bounds__(256) void k_reduce_grads(const mep_wgrad_desc* __restrict__ wd, int n_wd, int wd_tiles,
                                                       const mep_colsum_desc* __restrict__ cd, int n_cd, int cd_tiles,
-                                                      mep_head_desc hd, HeadGrads hg, int head_blocks) {
+                                                      mep_head_desc hd, HeadGrads hg, int head_blocks,
+                                                      float* norm, int* step, const float* hyper) {
     int bx = blockIdx.x;
-    if (bx < head_blocks) { head_reduce_block(hd, hg, bx); return; }
-    bx -= head_blocks;
-    if (bx < n_wd * wd_tiles) { wgrad_reduce_block(wd[bx / wd_tiles], bx % wd_tiles); return; }
-    bx -= n_wd * wd_tiles;
-    if (bx < n_cd * cd_tiles) colsum_block(cd[bx / cd_tiles], bx % cd_tiles);
+    float sq = 0.f;
+    if (bx < head_blocks) {
+        sq = head_reduce_block(hd, hg, bx);
+    } else {
+        bx -= head_blocks;
+        if (bx < n_wd * wd_tiles) {
+            sq = wgrad_reduce_block(wd[bx / wd_tiles], bx % wd_tiles);
+        } else {
+            bx -= n_wd * wd_tiles;
+            if (bx < n_cd * cd_tiles) sq = colsum_block(cd[bx / cd_tiles], bx % cd_tiles);
+        }
+    }
+    if (!norm) return;
+    __shared__ float nred[4];
+    sq = wave_sum(sq);
+    if ((threadIdx.x & 63) == 0) nred[threadIdx.x >> 6] = sq;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        norm[OPT_EXT0 + blockIdx.x] = (nred[0] + nred[1]) + (nred[2] + nred[3]);
+        if (blockIdx.x == 0 && step) opt_step_scalars(norm, step, hyper);
+    }
 }
 
 __global__ __launch_bounds__(64) void k_circle_fwd(const float* __restrict__ logits, const void* labels, int lf,
@@ -628,7 +653,8 @@ extern "C" int mep_head_fwd_bwd(const mep_head_desc* d, mep_stream_t stream) {
 extern "C" int mep_reduce_grads(const mep_wgrad_desc* wgrad, int n_wgrad, int wgrad_tiles, const mep_colsum_desc* colsum,
                                 int n_colsum, int colsum_tiles, const mep_head_desc* head, uint64_t g_trans,
                                 uint64_t g_ln_w, uint64_t g_ln_b, uint64_t g_wo, uint64_t g_bo, uint64_t g_wc0,
-                                uint64_t g_wc1, uint64_t loss, mep_stream_t stream) {
+                                uint64_t g_wc1, uint64_t loss, float* norm, int* step, const float* hyper,
+                                mep_stream_t stream) {
     if (head && head->NC > NCMAX) { mep_set_error("mep_reduce_grads: invalid head descriptor"); return MEP_EINVAL; }
     if (n_wgrad < 0 || n_colsum < 0 || (n_wgrad && wgrad_tiles <= 0) || (n_colsum && colsum_tiles <= 0)) {
         mep_set_error("mep_reduce_grads: invalid grid");
@@ -646,8 +672,13 @@ extern "C" int mep_reduce_grads(const mep_wgrad_desc* wgrad, int n_wgrad, int wg
     const int blocks = hb + n_wgrad * wgrad_tiles + n_colsum * colsum_tiles;
     if (blocks <= 0) return 0;
     hipLaunchKernelGGL(k_reduce_grads, dim3(blocks), dim3(256), 0, (hipStream_t)stream, wgrad, n_wgrad,
-                       wgrad_tiles, colsum, n_colsum, colsum_tiles, hd, g, hb);
+                       wgrad_tiles, colsum, n_colsum, colsum_tiles, hd, g, hb, norm, step, hyper);
     return mep_check_launch("mep_reduce_grads");
+}
+
+extern "C" int mep_reduce_grads_grid(int n_wgrad, int wgrad_tiles, int n_colsum, int colsum_tiles,
+                                     const mep_head_desc* head) {
+    return (head ? head_reduce_blocks(*head) : 0) + n_wgrad * wgrad_tiles + n_colsum * colsum_tiles;
 }
 
 extern "C" int mep_head_reduce(const mep_head_desc* d, uint64_t g_trans, uint64_t g_ln_w, uint64_t g_ln_b,

@@ -28,11 +28,14 @@ import torch.distributed as dist
 
 class TrainEngine:
     def __init__(self, model, optimizer, clip=1.0, rdrop=False, graph=True, process_group=None,
-                 collective=None, capture_allreduce=None):
+                 collective=None, capture_allreduce=None, fold_norm=None):
         """collective: run the flat-gradient all-reduce (default: when world > 1; True forces it
         at world 1, e.g. to exercise the RCCL path on one GPU).  capture_allreduce: capture the
         all-reduce inside the step's hipGraph between the backward and the optimizer (default:
-        with the nccl = RCCL backend; gloo collectives are host calls and are never captured)."""
+        with the nccl = RCCL backend; gloo collectives are host calls and are never captured).
+        fold_norm: single process, run the clip's norm pass inside the backward's reduction launch
+        (default: on unless MEP_NORM_FOLD=0; its norm sums in another order than the optimizer's
+        own pass, so runs compared bit for bit with a collective engine turn it off)."""
         self.model = model
         self.opt = optimizer
         self.clip = clip
@@ -53,6 +56,7 @@ class TrainEngine:
         self.overlap = self.collective and backend == 'nccl' and (env != '0' if env is not None else True)
         self._side = None
         self._graphs = {}
+        self.fold_norm = (os.environ.get('MEP_NORM_FOLD', '1') != '0') if fold_norm is None else bool(fold_norm)
         self._initial_broadcast = self.world > 1
 
     def _runner(self, device):
@@ -95,8 +99,25 @@ class TrainEngine:
             dist.all_reduce(flat.grad[a_end:n], op=dist.ReduceOp.SUM, group=self.pg)
         main.wait_stream(side)
 
+    _n_ext = 0
+
     def _opt(self):
-        self.opt.fused_step()
+        if self._n_ext:
+            self.opt.fused_step(n_ext=self._n_ext)
+        else:
+            self.opt.fused_step()
+
+    def _norm_fold(self, plan):
+        """Single process: the clip's gradient-norm pass runs inside the backward's reduction
+        launch (mep_reduce_grads writes the norm partials and the step scalars into the optimizer
+        workspace; one launch fewer per step).  With a gradient all-reduce the norm must follow
+        the SUM, so the optimizer keeps its own norm pass."""
+        fold = (self.fold_norm and not self.collective and hasattr(plan, 'reduce_grid')
+                and hasattr(self.opt, 'norm_fold_ptrs'))
+        n = plan.reduce_grid() if fold else 0
+        fold = fold and 0 < n <= self.opt.MAX_EXT
+        plan.norm_fold = self.opt.norm_fold_ptrs() if fold else None
+        self._n_ext = n if fold else 0
 
     def _sync_params(self, runner):
         """Rank 0's parameters (and optimizer moments, all zero at start) to every rank."""
@@ -119,6 +140,7 @@ class TrainEngine:
         if plan._drop > 0.0:
             plan.set_row0(row0 if sharded else 0)
         self._sync_params(runner)
+        self._norm_fold(plan)
         key = id(plan)
         g = self._graphs.get(key)
         if not self.graph:
@@ -191,6 +213,7 @@ class TrainEngine:
         self._sync_params(runner)
         runner.flat.grad.zero_()
         self._allreduce(runner)          # eager: an empty share is rare (the ragged last batch)
+        self._n_ext = 0                  # no reduction ran: the optimizer's own norm pass
         self._opt()
         return torch.zeros(1, device=runner.flat.buf.device)
 

@@ -34,7 +34,9 @@ class FusedAdamW(torch.optim.Optimizer):
             self._flat = flat
             self.exp_avg = torch.zeros_like(flat.buf)
             self.exp_avg_sq = torch.zeros_like(flat.buf)
-            self.partial = torch.zeros(1024, dtype=torch.float32, device=dev)
+            # [0, 1016) norm partials, [1016, 1018) step scalars, [1024, ..) the partials of a
+            # mep_reduce_grads launch that folded the norm pass in (TrainEngine, single process)
+            self.partial = torch.zeros(1024 + self.MAX_EXT, dtype=torch.float32, device=dev)
             self.hyper = torch.zeros(8, dtype=torch.float32, device=dev)
             self.step_t = torch.zeros(1, dtype=torch.int32, device=dev)
             self.gnorm = torch.zeros(1, dtype=torch.float32, device=dev)
@@ -51,15 +53,24 @@ class FusedAdamW(torch.optim.Optimizer):
             self.hyper[:7].copy_(torch.tensor(h, dtype=torch.float32))
             self._host_hyper = h
 
-    def fused_step(self, stream=None):
-        """Clip + update from the flat gradient buffer (engine path; graph-capturable)."""
+    MAX_EXT = 1 << 16   # largest folded-norm launch (mep_reduce_grads blocks)
+
+    def norm_fold_ptrs(self):
+        """(workspace, step, hyper) device pointers a plan's mep_reduce_grads writes the folded
+        norm partials and step scalars to"""
+        return (self.partial.data_ptr(), self.step_t.data_ptr(), self.hyper.data_ptr())
+
+    def fused_step(self, stream=None, n_ext=0):
+        """Clip + update from the flat gradient buffer (engine path; graph-capturable).  n_ext > 0:
+        the backward's reduction already wrote n_ext norm partials and advanced the step."""
+        assert 0 <= n_ext <= self.MAX_EXT
         flat = self._flat
         segs = (_lib.Seg * 1)(_lib.Seg(0, flat.n_grad))
         P = ctypes.c_void_p
-        _lib.call('mep_clip_adam', P(flat.buf.data_ptr()), P(flat.grad.data_ptr()), P(self.exp_avg.data_ptr()),
+        _lib.call('mep_clip_adam_ext', P(flat.buf.data_ptr()), P(flat.grad.data_ptr()), P(self.exp_avg.data_ptr()),
                   P(self.exp_avg_sq.data_ptr()), ctypes.cast(segs, P), 1, flat.total, P(self.partial.data_ptr()),
                   P(self.gnorm.data_ptr()), P(self.hyper.data_ptr()), P(self.step_t.data_ptr()),
-                  int(self.decoupled), stream=stream)
+                  int(self.decoupled), int(n_ext), stream=stream)
 
     @torch.no_grad()
     def step(self, closure=None):

@@ -28,7 +28,7 @@ import torch
 from . import _lib
 from ._lib import (AttnBwdDesc, AttnDesc, ColsumDesc, DescArray, GemmDesc, PoolDesc, RfEpiBwdDesc, RfEpiDesc,
                    RfHeadDesc, Rows, SumDesc, launch)
-from .trimodal import CHAINS, MODS, TIME_ORDER, UNIFY_NAMES, cdiv, crows, make_wgrad, rows
+from .trimodal import CHAINS, MODS, TIME_ORDER, UNIFY_NAMES, _norm_args, cdiv, crows, make_wgrad, rows
 
 RF_SPLITQ = os.environ.get('MEP_RF_SPLITQ', '1') != '0'   # attention backward: query tiles over 4 waves
 
@@ -424,8 +424,9 @@ class RealformerPlan:
         self.wg_partial, self.d_wgrad, self.t_wgrad, self.t_wgred = make_wgrad(items, dev)
         cs = []
 
-        def col(partial, out, n_rows, n_cols, ld):
-            cs.append(ColsumDesc(partial=partial, out=out, n_rows=n_rows, n_cols=n_cols, ld=ld, accumulate=0))
+        def col(partial, out, n_rows, n_cols, ld, not_grad=False):
+            cs.append(ColsumDesc(partial=partial, out=out, n_rows=n_rows, n_cols=n_cols, ld=ld,
+                                 accumulate=_lib.COLSUM_NOT_GRAD if not_grad else 0))
 
         S = _lib.rf_partial_stride(D, FD)
         for b in self.blocks:
@@ -450,7 +451,7 @@ class RealformerPlan:
             col(hp, g(pre + 'normalization.weight'), self.B, D, W)
             col(hp + 4 * D, g(pre + 'normalization.bias'), self.B, D, W)
             col(hp + 8 * D, g('trans'), self.B, NC * NC, W)
-            col(self.row_loss.data_ptr(), self.loss.data_ptr(), self.B, 1, 1)
+            col(self.row_loss.data_ptr(), self.loss.data_ptr(), self.B, 1, 1, not_grad=True)   # the batch loss
         self.d_colsum = DescArray(ColsumDesc, cs, dev)
         self.t_colsum = max(cdiv(c.n_cols, 32) for c in cs)
 
@@ -548,7 +549,14 @@ class RealformerPlan:
         # launch (no head partials here: the State_Transfer head reduces in mep_rf_head)
         _lib.call('mep_reduce_grads', self.d_wgrad.ptr, self.d_wgrad.n, self.t_wgred, self.d_colsum.ptr,
                   self.d_colsum.n, self.t_colsum if self.d_colsum.n else 0, None, 0, 0, 0, 0, 0, 0, 0, 0,
-                  stream=stream)
+                  *_norm_args(self), stream=stream)
+
+    norm_fold = None   # (optimizer workspace, step, hyper) pointers: the clip's norm pass folded into the reduction
+
+    def reduce_grid(self):
+        """blocks of the backward's mep_reduce_grads launch (the optimizer's folded norm partials)"""
+        return _lib.lib().mep_reduce_grads_grid(self.d_wgrad.n, self.t_wgred, self.d_colsum.n,
+                                                self.t_colsum if self.d_colsum.n else 0, None)
 
 
 class RealformerRunner:

@@ -37,6 +37,13 @@ TIME_ORDER = ('l', 'a', 'v')                          # cmu-mosei/run.py:317
 UNIFY_NAMES = {'l': 'linguistic', 'v': 'visual', 'a': 'acoustic'}
 
 
+def _norm_args(plan):
+    """the (norm, step, hyper) arguments of mep_reduce_grads: the optimizer workspace pointers when
+    the plan's engine folds the clip's norm pass into the reduction (TrainEngine, single process)"""
+    nf = plan.norm_fold
+    return (None, None, None) if nf is None else tuple(ctypes.c_void_p(x) for x in nf)
+
+
 def cdiv(a, b):
     return (a + b - 1) // b
 
@@ -680,7 +687,15 @@ class TriModalPlan:
         # weight-gradient split sums, LayerNorm / residual-coefficient column sums and the head
         # parameter sums: one launch
         _lib.call('mep_reduce_grads', self.d_wgrad.ptr, self.d_wgrad.n, self.t_wgred, self.d_colsum.ptr,
-                  self.d_colsum.n, self.t_colsum, ctypes.byref(self.head), *self.head_grads, stream=stream)
+                  self.d_colsum.n, self.t_colsum, ctypes.byref(self.head), *self.head_grads, *_norm_args(self),
+                  stream=stream)
+
+    norm_fold = None   # (optimizer workspace, step, hyper) pointers: the clip's norm pass folded into the reduction
+
+    def reduce_grid(self):
+        """blocks of the backward's mep_reduce_grads launch (the optimizer's folded norm partials)"""
+        return _lib.lib().mep_reduce_grads_grid(self.d_wgrad.n, self.t_wgred, self.d_colsum.n, self.t_colsum,
+                                                ctypes.byref(self.head))
 
     def advance_seed(self, stream=None):
         _lib.call('mep_seed_advance', ctypes.c_void_p(self.seed.data_ptr()), stream=stream)
@@ -720,7 +735,7 @@ class TriModalPlan:
             if i == 0:
                 launch('mep_wgrad', da, ta, stream)
                 _lib.call('mep_reduce_grads', da.ptr, da.n, ra, ca.ptr, ca.n, self.t_colsum if ca.n else 0,
-                          ctypes.byref(self.head), *self.head_grads, stream=stream)
+                          ctypes.byref(self.head), *self.head_grads, None, None, None, stream=stream)
                 bucket_a_done()
             launch('mep_attn_bwd', self.d_attnb[i], self.t_attnb[i], stream, threads=self.f_attnb[i] | self.prec)
         launch('mep_sum_rows', self.d_sum, self.t_sum, stream)
@@ -728,7 +743,7 @@ class TriModalPlan:
             launch('mep_layernorm_bwd', self.d_ulnb, cdiv(max(self.ntok.values()), 64), stream)
         launch('mep_wgrad', db, tb, stream)
         _lib.call('mep_reduce_grads', db.ptr, db.n, rb, cb.ptr, cb.n, self.t_colsum if cb.n else 0, None,
-                  0, 0, 0, 0, 0, 0, 0, 0, stream=stream)
+                  0, 0, 0, 0, 0, 0, 0, 0, None, None, None, stream=stream)
 
     def loss_only(self, stream=None):
         """Batch loss (sum of the scaled per-row losses) without the backward."""

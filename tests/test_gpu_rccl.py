@@ -36,13 +36,15 @@ def nccl_world1(cuda):
         dist.destroy_process_group()
 
 
-def _run(model_fn, batch, steps, collective, rdrop=False, seed=None):
+def _run(model_fn, batch, steps, collective, rdrop=False, seed=None, fold_norm=False):
     from mep_amd.engine import TrainEngine
     from mep_amd.optim import FusedAdamW
     model = model_fn()
     model.train()
     opt = FusedAdamW(model, lr=1e-3)
-    eng = TrainEngine(model, opt, clip=1.0, rdrop=rdrop, graph=True, collective=collective)
+    # the collective engine keeps the optimizer's own norm pass (the norm follows the SUM): the
+    # engine it is compared with bit for bit does too
+    eng = TrainEngine(model, opt, clip=1.0, rdrop=rdrop, graph=True, collective=collective, fold_norm=fold_norm)
     if seed is not None:
         model.mep_runner(batch[0][0].device if isinstance(batch[0], (tuple, list)) else batch[0].device) \
             .seed_state[0].fill_(seed)
@@ -81,3 +83,19 @@ def test_rccl_allreduce_captured_ren_dropout(nccl_world1, cuda):
     assert torch.equal(l1, l0) and torch.equal(g1, g0)
     for (k, p1), (_, p0) in zip(m1.named_parameters(), m0.named_parameters()):
         assert torch.equal(p1, p0), k
+
+
+def test_norm_fold_matches_optimizer_norm_pass(cuda):
+    """Single process: the clip's norm pass folded into the backward's reduction launch (the
+    default) against the optimizer's own norm pass -- the same pre-clip norm up to summation
+    order, and the same parameters after 4 graph-replayed AdamW steps."""
+    meta, _ = fixtures.load('cmu_cfg3')
+    batch = cuda_batch(meta, cuda)
+    e1, m1, l1, g1 = _run(lambda: cmu_model(meta, cuda), batch, 4, collective=False, fold_norm=True)
+    assert e1._n_ext > 0, 'the norm pass was not folded'
+    e0, m0, l0, g0 = _run(lambda: cmu_model(meta, cuda), batch, 4, collective=False, fold_norm=False)
+    assert e0._n_ext == 0
+    assert float((g1 - g0).abs().max() / g0.abs().max()) < 1e-6, (g1, g0)
+    assert float((l1 - l0).abs().max()) <= 1e-6 * float(l0.abs().max()), (l1, l0)
+    for (k, p1), (_, p0) in zip(m1.named_parameters(), m0.named_parameters()):
+        assert float((p1 - p0).abs().max()) <= 1e-6, k
