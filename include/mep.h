@@ -198,6 +198,14 @@ typedef struct {
     uint64_t ds_next;   /* [B,H,Tq,Tk] or 0                        */
     uint64_t ds_prev;   /* [B,H,Tq,Tk] or 0                        */
     uint64_t dc_partial;/* [B * H * ceil(Tk/64)] floats or 0       */
+    /* Per-modality sums folded in (SHORT descriptors only; sum = 0: none).  sum points at the
+     * plan's mep_sum_desc array; sum_q / sum_kv index the sum this descriptor's dq / dk rows are a
+     * source of (-1: none); sum_count holds sum_stride int32 counters per sum, zero before the
+     * first launch (B * H slices).  The (b, h) unit whose arrival completes a slice of a sum (its
+     * n_src-th) adds that slice's sources in source order -- the mep_sum_rows sum, bit for bit --
+     * writes the output slice and re-arms the counter, so no mep_sum_rows launch is needed. */
+    uint64_t sum, sum_count;
+    int32_t  sum_q, sum_kv, sum_stride, _pad;
 } mep_attn_bwd_desc;
 int mep_attn_bwd(const mep_attn_bwd_desc* descs, int n_desc, int max_tiles, int flags, mep_stream_t stream);
 

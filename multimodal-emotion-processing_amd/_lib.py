@@ -45,7 +45,9 @@ class AttnDesc(ctypes.Structure):
 
 class AttnBwdDesc(ctypes.Structure):
     _fields_ = [('f', AttnDesc), ('dx', Rows), ('dq', Rows), ('dk', Rows), ('dv', Rows),
-                ('ds_next', u64), ('ds_prev', u64), ('dc_partial', u64)]
+                ('ds_next', u64), ('ds_prev', u64), ('dc_partial', u64),
+                ('sum', u64), ('sum_count', u64), ('sum_q', i32), ('sum_kv', i32), ('sum_stride', i32),
+                ('_pad', i32)]
 
 
 class EpiDesc(ctypes.Structure):
@@ -73,6 +75,7 @@ class ColsumDesc(ctypes.Structure):
 
 
 SUM_MAX_SRC = 16
+ATTN_FOLD_SRC = 8    # csrc/attn.hip FOLD_SRC: sources per sum the attention backward folds
 
 
 class SumDesc(ctypes.Structure):

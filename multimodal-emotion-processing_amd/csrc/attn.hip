@@ -906,6 +906,57 @@ constexpr int bwd_short_waves() { return PREV ? (KV ? 3 : 2) : (KV && !DSN) ? ME
 #define MEP_BWD_DMA 1   // short backward: query tiles staged one ahead by LDS-DMA (Bwd::stage)
 #endif
 
+// The per-modality gradient sums folded into the short backward (mep_attn_bwd_desc.sum).  A
+// (b, h) unit has written its dq and dk slices (rows of b, columns of head h); it counts them on the
+// slice counters of the sums they feed (one arrival per source, agent-scope release).  The arrival
+// that completes a slice adds the slice's sources in source order -- the k_sum_rows sequence, bit
+// for bit -- writes it, and re-arms the counter for the next step.
+constexpr int FOLD_SRC = 8;    // sources held in flight per row (the plans fold at most 8)
+MEP_DEV void fold_slice(const mep_sum_desc& s, int b, int h, int lane) {
+    const int T = s.out.T, col = h * HD + 4 * (lane & 3);
+    for (int t = lane >> 2; t < T; t += 16) {
+        const int tok = b * T + t;
+        float4 v[FOLD_SRC];
+#pragma unroll
+        for (int k = 0; k < FOLD_SRC; ++k)
+            if (k < s.n_src) v[k] = ldg4(row_ptr(s.src[k], tok) + col);
+        float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+        for (int k = 0; k < FOLD_SRC; ++k)
+            if (k < s.n_src) { a.x += v[k].x; a.y += v[k].y; a.z += v[k].z; a.w += v[k].w; }
+        gfloat* o = row_ptr(s.out, tok) + col;
+        if (s.accumulate) { const float4 w = ldg4(o); a.x += w.x; a.y += w.y; a.z += w.z; a.w += w.w; }
+        stg4(o, a);
+    }
+}
+
+MEP_DEV void fold_sums(const mep_attn_bwd_desc& bd, int b, int h, int lane) {
+    const mep_sum_desc* sums = reinterpret_cast<const mep_sum_desc*>(bd.sum);
+    MEP_G int* cnt = G<int>(bd.sum_count);
+    const int slice = b * bd.f.H + h;
+    __threadfence();                             // this unit's dq / dk stores, before it counts
+    int done = 0;                                // bit 0: sum_q's slice complete, bit 1: sum_kv's
+    if (lane == 0) {
+        const int both = bd.sum_q >= 0 && bd.sum_q == bd.sum_kv;
+        for (int i = 0; i < 2 - both; ++i) {
+            const int idx = i ? bd.sum_kv : bd.sum_q;
+            if (idx < 0) continue;
+            MEP_G int* c = cnt + (int64_t)idx * bd.sum_stride + slice;
+            const int inc = both ? 2 : 1;
+            const int old = __hip_atomic_fetch_add(c, inc, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+            if (old + inc == sums[idx].n_src) {
+                __hip_atomic_store(c, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                done |= 1 << i;
+            }
+        }
+    }
+    done = __shfl(done, 0);
+    if (!done) return;
+    __threadfence();                             // the other units' slices, before they are read
+    if (done & 1) fold_slice(sums[bd.sum_q], b, h, lane);
+    if (done & 2) fold_slice(sums[bd.sum_kv], b, h, lane);
+}
+
 template <bool PREV, bool DSN, bool BF, bool KV>
 __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(bwd_short_waves<PREV, DSN, KV>()))) void k_attn_bwd_short(const mep_attn_bwd_desc* __restrict__ descs) {
     __shared__ __attribute__((aligned(16))) float Tr[WAVES][TFL];
@@ -992,6 +1043,7 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(bwd_sho
         const float w = wave_sum(u.dc_acc);
         if (lane == 0) G<float>(bd.dc_partial)[bh] = w;
     }
+    if (bd.sum) fold_sums(bd, u.b, u.h, lane);
 }
 
 // LONG (Tk > 64): one WORKGROUP per (b, h).  Key chunks are the outer loop; wave w takes query

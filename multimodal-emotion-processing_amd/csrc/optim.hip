@@ -86,7 +86,18 @@ __global__ __launch_bounds__(OPT_THREADS) void k_clip_adam(float* __restrict__ p
     // DPP tree, then the 4 waves in order): identical totals, no grid barrier
     __shared__ float red[OPT_THREADS / 64];
     float s = 0.f;
-    for (int i = threadIdx.x; i < npart; i += OPT_THREADS) s += partial[pbase + i];
+    // 16 partials per thread in flight at once (a folded reduction can leave thousands): one
+    // memory latency per 4096 partials, fixed order
+    for (int i0 = 0; i0 < npart; i0 += 16 * OPT_THREADS) {
+        float v[16];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) {
+            const int i = i0 + (int)threadIdx.x + OPT_THREADS * u;
+            v[u] = i < npart ? partial[pbase + i] : 0.f;
+        }
+#pragma unroll
+        for (int u = 0; u < 16; ++u) s += v[u];
+    }
     s = wave_sum(s);
     if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
     __syncthreads();

@@ -53,6 +53,10 @@ WG_TARGET = _lib.N_CU      # workgroups per launch: one per CU (4 waves of ~400 
 WG_TARGET_OVERRIDE = None  # development: another workgroup count for wgrad_segments
 # the pool's backward formed inside the epilogue backward (0: a separate mep_pool_bwd into dXcat)
 POOL_FOLD = os.environ.get('MEP_POOL_FOLD', '1') != '0'
+# per-modality gradient sums inside the attention backward (no mep_sum_rows launch): correct (bit
+# equal) but off -- the agent-scope release every (b, h) unit needs before it counts its slices
+# took the cfg3 attention backward from 36 to 641 us
+SUM_FOLD = os.environ.get('MEP_SUM_FOLD', '0') == '1'
 FWD_SPLITQ = os.environ.get('MEP_FWD_SPLITQ', '0') == '1'
 
 
@@ -445,17 +449,6 @@ class TriModalPlan:
             labels_are_float=int(self.labels_float), rdrop=0, compute_grad=1, loss_scale=1.0 / B, ext_dlogits=0,
             mean_div=self.Ttot if self.pool_fold else 0,   # the fold reads dmean / T straight from dpooled
             scale=self.head_scale.data_ptr())
-        # backward per layer
-        self.d_epib, self.d_attnb, self.t_attnb, self.f_attnb = [], [], [], []
-        for i in range(nl):
-            eb, ab = [], []
-            for blk in (b for b in self.blocks if b['i'] == i):
-                eb.append(self._epi_bwd_desc(blk))
-                ab.append(self._attn_bwd_desc(blk))
-            self.d_epib.append(DescArray(EpiBwdDesc, eb, dev))
-            self.d_attnb.append(DescArray(AttnBwdDesc, ab, dev))
-            self.t_attnb.append(self.g_attn[i][1])
-            self.f_attnb.append(_lib.attn_bwd_flags(ab))
         # per-modality gradient sums
         sd = []
         self.dU = {}
@@ -472,6 +465,28 @@ class TriModalPlan:
                                   ntok=self.ntok[m], D=D, accumulate=0))
         self.d_sum = DescArray(SumDesc, sd, dev)
         self.t_sum = min(1024, max(cdiv(self.ntok[m] * D // 4, 256) for m in MODS))
+        # the sums folded into the attention backward (SHORT descriptors: every key length <= 64)
+        self.sum_fold = (SUM_FOLD and max(self.T.values()) <= 64
+                         and all(d.n_src <= _lib.ATTN_FOLD_SRC for d in sd))
+        if self.sum_fold:
+            self.sum_count = torch.zeros(len(sd), B * sp.H, dtype=torch.int32, device=dev)
+        # backward per layer
+        self.d_epib, self.d_attnb, self.t_attnb, self.f_attnb = [], [], [], []
+        for i in range(nl):
+            eb, ab = [], []
+            for blk in (b for b in self.blocks if b['i'] == i):
+                eb.append(self._epi_bwd_desc(blk))
+                ab.append(self._attn_bwd_desc(blk))
+                if self.sum_fold:
+                    e = blk['e']
+                    ab[-1].sum, ab[-1].sum_count = self.d_sum.ptr.value, self.sum_count.data_ptr()
+                    ab[-1].sum_q = e * 3 + MODS.index(blk['qm']) if i == 0 else -1
+                    ab[-1].sum_kv = e * 3 + MODS.index(blk['km'])
+                    ab[-1].sum_stride = B * sp.H
+            self.d_epib.append(DescArray(EpiBwdDesc, eb, dev))
+            self.d_attnb.append(DescArray(AttnBwdDesc, ab, dev))
+            self.t_attnb.append(self.g_attn[i][1])
+            self.f_attnb.append(_lib.attn_bwd_flags(ab))
         if sp.unify_norm:
             self.dY = {k: torch.zeros_like(v) for k, v in self.dU.items()}
             tiles = {m: cdiv(self.ntok[m], 64) for m in MODS}
@@ -680,7 +695,8 @@ class TriModalPlan:
         for i in reversed(range(nl)):
             launch('mep_block_epi_bwd', self.d_epib[i], self.t_epi[i], stream, threads=sp.D | self.prec)
             launch('mep_attn_bwd', self.d_attnb[i], self.t_attnb[i], stream, threads=self.f_attnb[i] | self.prec)
-        launch('mep_sum_rows', self.d_sum, self.t_sum, stream)
+        if not self.sum_fold:
+            launch('mep_sum_rows', self.d_sum, self.t_sum, stream)
         if sp.unify_norm:
             launch('mep_layernorm_bwd', self.d_ulnb, cdiv(max(self.ntok.values()), 64), stream)
         launch('mep_wgrad', self.d_wgrad, self.t_wgrad, stream)
@@ -738,7 +754,8 @@ class TriModalPlan:
                           ctypes.byref(self.head), *self.head_grads, None, None, None, stream=stream)
                 bucket_a_done()
             launch('mep_attn_bwd', self.d_attnb[i], self.t_attnb[i], stream, threads=self.f_attnb[i] | self.prec)
-        launch('mep_sum_rows', self.d_sum, self.t_sum, stream)
+        if not self.sum_fold:
+            launch('mep_sum_rows', self.d_sum, self.t_sum, stream)
         if sp.unify_norm:
             launch('mep_layernorm_bwd', self.d_ulnb, cdiv(max(self.ntok.values()), 64), stream)
         launch('mep_wgrad', db, tb, stream)

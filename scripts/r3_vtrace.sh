@@ -4,7 +4,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 mkdir -p gpurun_out
 for v in ${V:-base}; do
-  OUT=gpurun_out/vt_$v; mkdir -p $OUT
+  OUT=gpurun_out/vt_$v; rm -rf $OUT; mkdir -p $OUT
   lib=""; [ "$v" != base ] && lib=variants/$v/libmep_hip.so
   MEP_LIB=$lib timeout -k 10 240 rocprofv3 --kernel-trace --stats -d $OUT -o run --output-format csv -- python3 bench.py --steps 30 --warmup 5 --no-cpu-baseline $BARGS > $OUT/log 2>&1
   rc=$?
