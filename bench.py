@@ -271,6 +271,8 @@ class Cfg2:
         self.G = G.reshape(self.plan.dout_chain.shape)
         self.plan.dout_chain.copy_(self.G / G.numel())   # d mean(out * G) / d out
         self.opt = _FlatAdam(runner.flat, lr=1e-3)
+        if os.environ.get('MEP_NORM_FOLD', '1') != '0':
+            self.opt.fold_into(self.plan)
         self.graph = graph
         self.g = None
         self.rows = B
@@ -347,19 +349,28 @@ class _FlatAdam:
         dev = flat.buf.device
         self.exp_avg = torch.zeros_like(flat.buf)
         self.exp_avg_sq = torch.zeros_like(flat.buf)
-        self.partial = torch.zeros(1024, dtype=torch.float32, device=dev)
+        # workspace: [0, 1024) the norm pass's partials and the step scalars, then the partials of a
+        # backward reduction that folded the norm pass in (optim.py MAX_EXT)
+        self.partial = torch.zeros(1024 + (1 << 16), dtype=torch.float32, device=dev)
+        self.n_ext = 0
         self.gnorm = torch.zeros(1, dtype=torch.float32, device=dev)
         self.step_t = torch.zeros(1, dtype=torch.int32, device=dev)
         self.hyper = torch.tensor([lr, 0.9, 0.999, 1e-8, 0.0, float('inf'), 1.0, 0.0], dtype=torch.float32,
                                   device=dev)
 
+    def fold_into(self, plan):
+        """the norm pass (and the step counter) folded into the plan's backward reduction"""
+        plan.norm_fold = (self.partial.data_ptr(), self.step_t.data_ptr(), self.hyper.data_ptr())
+        self.n_ext = plan.reduce_grid()
+        assert 0 < self.n_ext <= 1 << 16
+
     def step(self):
         P = self.ct.c_void_p
         segs = (self._lib.Seg * 1)(self._lib.Seg(0, self.flat.n_grad))
-        self._lib.call('mep_clip_adam', P(self.flat.buf.data_ptr()), P(self.flat.grad.data_ptr()),
+        self._lib.call('mep_clip_adam_ext', P(self.flat.buf.data_ptr()), P(self.flat.grad.data_ptr()),
                        P(self.exp_avg.data_ptr()), P(self.exp_avg_sq.data_ptr()), self.ct.cast(segs, P), 1,
                        self.flat.total, P(self.partial.data_ptr()), P(self.gnorm.data_ptr()),
-                       P(self.hyper.data_ptr()), P(self.step_t.data_ptr()), 0)
+                       P(self.hyper.data_ptr()), P(self.step_t.data_ptr()), 0, self.n_ext)
 
 
 CONFIGS = {'cfg3': Cfg3, 'cfg5': Cfg5, 'cfg2': Cfg2}
