@@ -131,6 +131,10 @@ typedef struct {
     int32_t  bf16;               /* 1: bf16 operands (MEP_PREC_BF16); 0: 3-part split (fp32)   */
     int32_t  _pad;
 } mep_wgrad_desc;
+/* k_wgrad geometry of this build: column tiles per group for ceil(N / 32) row tiles, and
+ * workgroups per CU the host sizes the launch for (trimodal.wgrad_geometry / wg_target). */
+int mep_wgrad_kt(int mt);
+int mep_wgrad_occupancy(void);
 int mep_wgrad(const mep_wgrad_desc* descs, int n_desc, int max_tiles, mep_stream_t stream);
 int mep_wgrad_reduce(const mep_wgrad_desc* descs, int n_desc, int max_tiles, mep_stream_t stream);
 

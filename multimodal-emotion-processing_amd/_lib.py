@@ -238,6 +238,8 @@ SIGNATURES.update({
     'mep_head_partial_stride': [i32],
     'mep_reduce_grads': [P, i32, i32, P, i32, i32, HP, u64, u64, u64, u64, u64, u64, u64, u64, P, P, P, P],
     'mep_reduce_grads_grid': [i32, i32, i32, i32, HP],
+    'mep_wgrad_kt': [i32],
+    'mep_wgrad_occupancy': [],
     'mep_circle_loss_fwd': [P, P, i32, i32, i32, P, P, P],
     'mep_circle_loss_bwd': [P, P, i32, i32, P, P],
     'mep_clip_adam': [P, P, P, P, P, i32, i64, P, P, P, P, i32, P],

@@ -160,15 +160,30 @@ __global__ __launch_bounds__(GEMM_THREADS) void k_gemm(const mep_gemm_desc* __re
 #ifndef MEP_WG_PARTS
 #define MEP_WG_PARTS 3   // bf16 parts per fp32 operand on the fp32 path (3: fp32-level)
 #endif
+// MEP_WG_OCC: k_wgrad workgroups per CU.  2: two waves per SIMD, each on a 32MT x 64 block (KT = 2
+// at MT = 3; <= 256 registers: no operand prefetch slot), so one wave's operand loads and split VALU overlap the other's
+// products; the LDS reduction buffers shrink to fit two workgroups.
+#ifndef MEP_WG_OCC
+#define MEP_WG_OCC 2
+#endif
+#ifndef MEP_WG_KT4
+#define MEP_WG_KT4 1   // occupancy 2: column tiles per block at MT = 4 (D = 128)
+#endif
 #ifndef MEP_WG_PF
-#define MEP_WG_PF 1   // 2 would need ~300 arch VGPRs (spills): double-buffered operands
+// 2 would need ~300 arch VGPRs (spills): double-buffered operands.  Occupancy 2: none (the other
+// wave hides the loads; a slot spills at KT = 2)
+#define MEP_WG_PF (MEP_WG_OCC > 1 ? 0 : 1)
 #endif
 constexpr int WG_WAVES = 4;
 constexpr int WG_THREADS = 64 * WG_WAVES;
 constexpr int WG_SLOTS = MEP_WG_PF + 1;       // k blocks of operand registers
-constexpr int WG_RED = 96 * (96 + 8);          // largest 32MT x (32KT + 8) reduction buffer (MT = KT = 3)
+// largest 32MT x (32KT + 8) reduction buffer: MT = KT = 3 (occupancy 1), MT = 3, KT = 2 (2)
+constexpr int WG_RED = MEP_WG_OCC > 1 ? (MEP_WG_KT4 > 1 ? 128 : 96) * (64 + 8) : 96 * (96 + 8);
 
-MEP_DEV int wg_kt(int mt) { return mt == 4 ? 2 : mt == 3 ? 3 : 4; }
+__host__ __device__ constexpr int wg_kt(int mt) {
+    if (MEP_WG_OCC > 1) return mt == 4 ? MEP_WG_KT4 : 2;   // <= 96 accumulators (128 at MEP_WG_KT4 = 2)
+    return mt == 4 ? 2 : mt == 3 ? 3 : 4;
+}
 
 // byte extent of a row view's first ntok rows, `width` columns wide (the range the raw buffer
 // loads check; hosts keep it under 2^31)
@@ -448,7 +463,7 @@ MEP_DEV void wgrad_task(const mep_wgrad_desc& d, int t_begin, int t_end, int slo
 // written to partial slot `slot` (slots never written stay zero: hosts zero the workspace once).
 // The host cuts the launch's total MFMA work into n_wg equal contiguous ranges, so a workgroup
 // may finish one descriptor's token range and start another's.
-__global__ __launch_bounds__(WG_THREADS, 1) void k_wgrad(const mep_wgrad_desc* __restrict__ descs, int n_desc, int n_wg) {
+__global__ __launch_bounds__(WG_THREADS) __attribute__((amdgpu_waves_per_eu(MEP_WG_OCC))) void k_wgrad(const mep_wgrad_desc* __restrict__ descs, int n_desc, int n_wg) {
 #ifdef MEP_WG_TRACE
     const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
 #endif
@@ -470,6 +485,7 @@ __global__ __launch_bounds__(WG_THREADS, 1) void k_wgrad(const mep_wgrad_desc* _
         for (int o = 0; o < d.n_b; ++o) lin = lin && wg_linear(d.b[o]);
 #define MEP_WGT(M, K)                                                                          \
         case 8 * M + K:                                                                        \
+            if constexpr (K > wg_kt(M)) break;  /* not a tile block of this build */           \
             if (d.bf16) {                                                                      \
                 if (lin) wgrad_task<M, K, 1, true>(d, t_begin, t_end, slot, kbase, red);       \
                 else wgrad_task<M, K, 1, false>(d, t_begin, t_end, slot, kbase, red);          \
@@ -1000,6 +1016,9 @@ extern "C" int mep_gemm(const mep_gemm_desc* descs, int n_desc, int max_tiles, m
     hipLaunchKernelGGL(k_gemm, dim3(max_tiles, n_desc, GEMM_ZP), dim3(GEMM_THREADS), 0, (hipStream_t)stream, descs);
     return mep_check_launch("mep_gemm");
 }
+
+extern "C" int mep_wgrad_kt(int mt) { return wg_kt(mt); }
+extern "C" int mep_wgrad_occupancy(void) { return MEP_WG_OCC; }
 
 extern "C" int mep_wgrad(const mep_wgrad_desc* descs, int n_desc, int max_tiles, mep_stream_t stream) {
     if (n_desc <= 0 || max_tiles <= 0) return 0;

@@ -21,6 +21,7 @@ never materialised); inputs stay in the reference's [B, 2, T, d] (prev, cur) lay
 through strided row views.
 """
 import ctypes
+import functools
 import os
 
 import torch
@@ -64,8 +65,18 @@ def wgrad_geometry(N, ktot):
     """(row tiles MT, column tiles per group KT, column groups) of k_wgrad's 32x32 tiling of an
     N x ktot weight gradient (csrc/gemm.hip wg_kt)."""
     mt = cdiv(N, 32)
-    kt = {4: 2, 3: 3}.get(mt, 4)
+    kt = _wg_kt(mt)
     return mt, kt, cdiv(cdiv(ktot, 32), kt)
+
+
+@functools.lru_cache(maxsize=None)
+def _wg_kt(mt):
+    return int(_lib.lib().mep_wgrad_kt(mt))
+
+
+def wg_target():
+    """workgroups of a k_wgrad launch: one per CU times the build's occupancy (MEP_WG_OCC)"""
+    return WG_TARGET_OVERRIDE or WG_TARGET * int(_lib.lib().mep_wgrad_occupancy())
 
 
 def _wgrad_units(items):
@@ -199,7 +210,7 @@ def make_wgrad(items, dev, tok_per_split=None, bf16=False):
     the launch's work balanced over one workgroup per CU (wgrad_segments), else fixed token
     chunks.  bf16: plain bf16 operands (the bf16 path) instead of the 3-part split."""
     items = [tuple(it) + (0,) * (5 - len(it)) for it in items]
-    segs, slots = wgrad_segments(items, n_wg=WG_TARGET_OVERRIDE or WG_TARGET, tok_per_split=tok_per_split)
+    segs, slots = wgrad_segments(items, n_wg=wg_target(), tok_per_split=tok_per_split)
     total = sum(max(1, s) * N * sum(b[1] for b in bs) for s, (_, N, n, bs, _) in zip(slots, items))
     ws = torch.zeros(max(total, 1), dtype=torch.float32, device=dev)   # unwritten slots stay 0
     descs, off, rmax = [], 0, 0
@@ -724,7 +735,7 @@ class TriModalPlan:
         if getattr(self, '_buckets', None) is not None:
             return
         dev, items, nb = self.device, self._wgrad_items, self._n_block_items
-        tps = wgrad_chunk(items, WG_TARGET_OVERRIDE or WG_TARGET)
+        tps = wgrad_chunk(items, wg_target())
         wa = make_wgrad(items[:nb], dev, tok_per_split=tps, bf16=self.bf16)
         wb = make_wgrad(items[nb:], dev, tok_per_split=tps, bf16=self.bf16)
         ca = DescArray(ColsumDesc, self._colsum_a, dev)
