@@ -131,11 +131,14 @@ typedef struct {
     int32_t  bf16;               /* 1: bf16 operands (MEP_PREC_BF16); 0: 3-part split (fp32)   */
     int32_t  _pad;
 } mep_wgrad_desc;
-/* k_wgrad geometry of this build: column tiles per group for ceil(N / 32) row tiles, and
- * workgroups per CU the host sizes the launch for (trimodal.wgrad_geometry / wg_target). */
-int mep_wgrad_kt(int mt);
-int mep_wgrad_occupancy(void);
-int mep_wgrad(const mep_wgrad_desc* descs, int n_desc, int max_tiles, mep_stream_t stream);
+/* k_wgrad geometry of this build: column tiles per group for ceil(N / 32) row tiles, and the
+ * workgroups per CU the host sizes the launch for (trimodal.wgrad_geometry / wg_target), for the
+ * fp32-split instance (bf16 = 0) or the bf16-path instance (bf16 = 1).
+ * mep_wgrad flags: MEP_PREC_BF16 selects the bf16-path instance; every descriptor's bf16 field must
+ * match it (a mismatched descriptor gets NaN partials). */
+int mep_wgrad_kt(int mt, int bf16);
+int mep_wgrad_occupancy(int bf16);
+int mep_wgrad(const mep_wgrad_desc* descs, int n_desc, int max_tiles, int flags, mep_stream_t stream);
 int mep_wgrad_reduce(const mep_wgrad_desc* descs, int n_desc, int max_tiles, mep_stream_t stream);
 
 /* ---------------------------------------------------------------- residual attention core

@@ -223,10 +223,11 @@ STRUCTS = {'mep_rows': Rows, 'mep_gemm_desc': GemmDesc, 'mep_wgrad_desc': WgradD
 
 P = ctypes.c_void_p
 # name -> argtypes (all return int)
-GROUPED = ['mep_gemm', 'mep_wsplit', 'mep_unify', 'mep_wgrad', 'mep_wgrad_reduce', 'mep_layernorm_fwd', 'mep_layernorm_bwd', 'mep_colsum', 'mep_sum_rows',
+GROUPED = ['mep_gemm', 'mep_wsplit', 'mep_unify', 'mep_wgrad_reduce', 'mep_layernorm_fwd', 'mep_layernorm_bwd', 'mep_colsum', 'mep_sum_rows',
            'mep_pool_fwd', 'mep_pool_bwd']
 GROUPED_T = ['mep_attn_fwd', 'mep_attn_bwd',      # + MEP_ATTN_* variant flags
-             'mep_block_epi_fwd', 'mep_block_epi_bwd']  # + D (compiled variant)
+             'mep_block_epi_fwd', 'mep_block_epi_bwd',  # + D (compiled variant)
+             'mep_wgrad']                                # + MEP_PREC_BF16 (the bf16-path instance)
 SIGNATURES = {name: [P, i32, i32, P] for name in GROUPED}
 SIGNATURES.update({name: [P, i32, i32, i32, P] for name in GROUPED_T})
 GROUPED_T2 = ['mep_rf_epi_fwd', 'mep_rf_epi_bwd', 'mep_rfw_epi_fwd', 'mep_rfw_epi_bwd']   # + D, FD (compiled variant)
@@ -238,8 +239,8 @@ SIGNATURES.update({
     'mep_head_partial_stride': [i32],
     'mep_reduce_grads': [P, i32, i32, P, i32, i32, HP, u64, u64, u64, u64, u64, u64, u64, u64, P, P, P, P],
     'mep_reduce_grads_grid': [i32, i32, i32, i32, HP],
-    'mep_wgrad_kt': [i32],
-    'mep_wgrad_occupancy': [],
+    'mep_wgrad_kt': [i32, i32],
+    'mep_wgrad_occupancy': [i32],
     'mep_circle_loss_fwd': [P, P, i32, i32, i32, P, P, P],
     'mep_circle_loss_bwd': [P, P, i32, i32, P, P],
     'mep_clip_adam': [P, P, P, P, P, i32, i64, P, P, P, P, i32, P],
@@ -334,6 +335,8 @@ def launch(name, descs, max_tiles, stream=None, threads=None, extra=()):
     fn = getattr(lib(), name)
     if TIMER is not None:
         TIMER.begin(name, stream)
+    if threads is None and name == 'mep_wgrad':
+        threads = getattr(descs, 'prec', 0)   # make_wgrad's precision
     ints = ([] if threads is None else [int(threads)]) + [int(x) for x in extra]
     rc = fn(descs.ptr, descs.n, int(max_tiles), *ints, stream_ptr(stream))
     check(rc, name)

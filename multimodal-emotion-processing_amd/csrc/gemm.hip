@@ -176,12 +176,18 @@ __global__ __launch_bounds__(GEMM_THREADS) void k_gemm(const mep_gemm_desc* __re
 #endif
 constexpr int WG_WAVES = 4;
 constexpr int WG_THREADS = 64 * WG_WAVES;
-constexpr int WG_SLOTS = MEP_WG_PF + 1;       // k blocks of operand registers
-// largest 32MT x (32KT + 8) reduction buffer: MT = KT = 3 (occupancy 1), MT = 3, KT = 2 (2)
-constexpr int WG_RED = MEP_WG_OCC > 1 ? (MEP_WG_KT4 > 1 ? 128 : 96) * (64 + 8) : 96 * (96 + 8);
+constexpr int WG_SLOTS_F = MEP_WG_PF + 1;     // k blocks of operand registers, fp32 instance
+constexpr int WG_SLOTS_B = 2;                 // bf16 instance (one workgroup per CU): one prefetch slot
+// largest 32MT x (32KT + 8) reduction buffer: MT = KT = 3 (occupancy 1, and the bf16 path); two
+// workgroups of 2 x 39 KB fit the CU's 160 KB
+constexpr int WG_RED = 96 * (96 + 8);
 
-__host__ __device__ constexpr int wg_kt(int mt) {
-    if (MEP_WG_OCC > 1) return mt == 4 ? MEP_WG_KT4 : 2;   // <= 96 accumulators (128 at MEP_WG_KT4 = 2)
+// bf16 path (one part per operand, no split registers): its own kernel instance at one workgroup
+// per CU with the wide blocks (the narrow ones double its operand loads: cfg5 bf16 308 vs 170 us at
+// KT = 1; the wide ones spill at 256 registers)
+__host__ __device__ constexpr int wg_occ(bool bf) { return bf ? 1 : MEP_WG_OCC; }
+__host__ __device__ constexpr int wg_kt(int mt, bool bf) {
+    if (MEP_WG_OCC > 1 && !bf) return mt == 4 ? MEP_WG_KT4 : 2;   // <= 96 accumulators (128 at MEP_WG_KT4 = 2)
     return mt == 4 ? 2 : mt == 3 ? 3 : 4;
 }
 
@@ -217,7 +223,7 @@ MEP_DEV void wg_stamp(int k, unsigned long long v) {
 // LIN: every view of the item is linear in the token -- a lane's eight tokens of a k block sit at
 // fixed byte distances, so they are ONE per-lane base (VGPR) plus a wave-uniform per-token offset
 // (the load's SGPR soffset) and the column tile an immediate: no address arithmetic per token.
-template <int MT, int KT, int NPART, bool LIN>
+template <int MT, int KT, int NPART, bool LIN, int WG_SLOTS>
 MEP_DEV void wgrad_task(const mep_wgrad_desc& d, int t_begin, int t_end, int slot, int kbase, lfloat* red) {
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int c = lane & 31, h = lane >> 5;
@@ -463,7 +469,10 @@ MEP_DEV void wgrad_task(const mep_wgrad_desc& d, int t_begin, int t_end, int slo
 // written to partial slot `slot` (slots never written stay zero: hosts zero the workspace once).
 // The host cuts the launch's total MFMA work into n_wg equal contiguous ranges, so a workgroup
 // may finish one descriptor's token range and start another's.
-__global__ __launch_bounds__(WG_THREADS) __attribute__((amdgpu_waves_per_eu(MEP_WG_OCC))) void k_wgrad(const mep_wgrad_desc* __restrict__ descs, int n_desc, int n_wg) {
+// BF: the instance for bf16-path descriptors (MEP_PREC_BF16); a descriptor of the other precision
+// gets NaN partials (loudly wrong, never silently)
+template <bool BF>
+__global__ __launch_bounds__(WG_THREADS) __attribute__((amdgpu_waves_per_eu(wg_occ(BF)))) void k_wgrad(const mep_wgrad_desc* __restrict__ descs, int n_desc, int n_wg) {
 #ifdef MEP_WG_TRACE
     const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
 #endif
@@ -476,7 +485,7 @@ __global__ __launch_bounds__(WG_THREADS) __attribute__((amdgpu_waves_per_eu(MEP_
         const int hdr = seg[4 * si], t_begin = seg[4 * si + 1], t_end = seg[4 * si + 2], slot = seg[4 * si + 3];
         const mep_wgrad_desc& d = descs[hdr >> 8];
         const int cg = hdr & 0xff;
-        const int mt = (d.N + 31) >> 5, ktm = wg_kt(mt);
+        const int mt = (d.N + 31) >> 5, ktm = wg_kt(mt, d.bf16);
         const int ktiles = (d.Ktot + 31) >> 5;
         const int kt = min(ktm, ktiles - cg * ktm);
         const int kbase = 32 * ktm * cg;
@@ -485,15 +494,15 @@ __global__ __launch_bounds__(WG_THREADS) __attribute__((amdgpu_waves_per_eu(MEP_
         for (int o = 0; o < d.n_b; ++o) lin = lin && wg_linear(d.b[o]);
 #define MEP_WGT(M, K)                                                                          \
         case 8 * M + K:                                                                        \
-            if constexpr (K > wg_kt(M)) break;  /* not a tile block of this build */           \
-            if (d.bf16) {                                                                      \
-                if (lin) wgrad_task<M, K, 1, true>(d, t_begin, t_end, slot, kbase, red);       \
-                else wgrad_task<M, K, 1, false>(d, t_begin, t_end, slot, kbase, red);          \
-            } else {                                                                           \
-                if (lin) wgrad_task<M, K, MEP_WG_PARTS, true>(d, t_begin, t_end, slot, kbase, red);  \
-                else wgrad_task<M, K, MEP_WG_PARTS, false>(d, t_begin, t_end, slot, kbase, red);     \
-            }                                                                                  \
+            if constexpr (K > wg_kt(M, BF)) break;   /* not a tile block of this instance */   \
+            if (lin) wgrad_task<M, K, BF ? 1 : MEP_WG_PARTS, true, BF ? WG_SLOTS_B : WG_SLOTS_F>(d, t_begin, t_end, slot, kbase, red);  \
+            else wgrad_task<M, K, BF ? 1 : MEP_WG_PARTS, false, BF ? WG_SLOTS_B : WG_SLOTS_F>(d, t_begin, t_end, slot, kbase, red);     \
             break;
+        if ((d.bf16 != 0) != BF) {
+            gfloat* part = G<float>(d.partial) + (int64_t)slot * d.N * d.Ktot;
+            for (int e = threadIdx.x; e < d.N * d.Ktot; e += WG_THREADS) part[e] = __builtin_nanf("");
+            continue;
+        }
         switch (8 * mt + kt) {
             MEP_WGT(1, 1) MEP_WGT(1, 2) MEP_WGT(1, 3) MEP_WGT(1, 4)
             MEP_WGT(2, 1) MEP_WGT(2, 2) MEP_WGT(2, 3) MEP_WGT(2, 4)
@@ -728,7 +737,7 @@ __global__ __launch_bounds__(WG_THREADS, 1) void k_wgrad_lds(const mep_wgrad_des
         const int hdr = seg[4 * si], t_begin = seg[4 * si + 1], t_end = seg[4 * si + 2], slot = seg[4 * si + 3];
         const mep_wgrad_desc& d = descs[hdr >> 8];
         const int cg = hdr & 0xff;
-        const int mt = (d.N + 31) >> 5, ktm = wg_kt(mt);
+        const int mt = (d.N + 31) >> 5, ktm = wg_kt(mt, d.bf16);
         const int ktiles = (d.Ktot + 31) >> 5;
         const int kt = min(ktm, ktiles - cg * ktm);
         const int kbase = 32 * ktm * cg;
@@ -1017,15 +1026,18 @@ extern "C" int mep_gemm(const mep_gemm_desc* descs, int n_desc, int max_tiles, m
     return mep_check_launch("mep_gemm");
 }
 
-extern "C" int mep_wgrad_kt(int mt) { return wg_kt(mt); }
-extern "C" int mep_wgrad_occupancy(void) { return MEP_WG_OCC; }
+extern "C" int mep_wgrad_kt(int mt, int bf16) { return wg_kt(mt, bf16 != 0); }
+extern "C" int mep_wgrad_occupancy(int bf16) { return wg_occ(bf16 != 0); }
 
-extern "C" int mep_wgrad(const mep_wgrad_desc* descs, int n_desc, int max_tiles, mep_stream_t stream) {
+extern "C" int mep_wgrad(const mep_wgrad_desc* descs, int n_desc, int max_tiles, int flags, mep_stream_t stream) {
     if (n_desc <= 0 || max_tiles <= 0) return 0;
 #if MEP_WGRAD_LDS
     hipLaunchKernelGGL(k_wgrad_lds, dim3(max_tiles), dim3(WG_THREADS), 0, (hipStream_t)stream, descs, n_desc, max_tiles);
 #else
-    hipLaunchKernelGGL(k_wgrad, dim3(max_tiles), dim3(WG_THREADS), 0, (hipStream_t)stream, descs, n_desc, max_tiles);
+    if (flags & MEP_PREC_BF16)
+        hipLaunchKernelGGL(k_wgrad<true>, dim3(max_tiles), dim3(WG_THREADS), 0, (hipStream_t)stream, descs, n_desc, max_tiles);
+    else
+        hipLaunchKernelGGL(k_wgrad<false>, dim3(max_tiles), dim3(WG_THREADS), 0, (hipStream_t)stream, descs, n_desc, max_tiles);
 #endif
     return mep_check_launch("mep_wgrad");
 }

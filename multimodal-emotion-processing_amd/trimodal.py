@@ -61,39 +61,40 @@ SUM_FOLD = os.environ.get('MEP_SUM_FOLD', '0') == '1'
 FWD_SPLITQ = os.environ.get('MEP_FWD_SPLITQ', '0') == '1'
 
 
-def wgrad_geometry(N, ktot):
+def wgrad_geometry(N, ktot, bf16=False):
     """(row tiles MT, column tiles per group KT, column groups) of k_wgrad's 32x32 tiling of an
     N x ktot weight gradient (csrc/gemm.hip wg_kt)."""
     mt = cdiv(N, 32)
-    kt = _wg_kt(mt)
+    kt = _wg_kt(mt, bool(bf16))
     return mt, kt, cdiv(cdiv(ktot, 32), kt)
 
 
 @functools.lru_cache(maxsize=None)
-def _wg_kt(mt):
-    return int(_lib.lib().mep_wgrad_kt(mt))
+def _wg_kt(mt, bf16):
+    return int(_lib.lib().mep_wgrad_kt(mt, int(bf16)))
 
 
-def wg_target():
-    """workgroups of a k_wgrad launch: one per CU times the build's occupancy (MEP_WG_OCC)"""
-    return WG_TARGET_OVERRIDE or WG_TARGET * int(_lib.lib().mep_wgrad_occupancy())
+def wg_target(bf16=False):
+    """workgroups of a k_wgrad launch: one per CU times the instance's occupancy (MEP_WG_OCC; the
+    bf16-path instance runs one per CU)"""
+    return WG_TARGET_OVERRIDE or WG_TARGET * int(_lib.lib().mep_wgrad_occupancy(int(bool(bf16))))
 
 
-def _wgrad_units(items):
+def _wgrad_units(items, bf16=False):
     units = []
     for i, (_, N, n, bs, _) in enumerate(items):
-        mt, kt, ncg = wgrad_geometry(N, sum(b[1] for b in bs))
+        mt, kt, ncg = wgrad_geometry(N, sum(b[1] for b in bs), bf16)
         for cg in range(ncg):
             if n > 0:
                 units.append((i, cg, n))
     return units
 
 
-def wgrad_chunk(items, n_wg=WG_TARGET):
+def wgrad_chunk(items, n_wg=WG_TARGET, bf16=False):
     """The smallest multiple of 8 tokens per segment that keeps the items' launch within n_wg
     workgroups."""
     items = [tuple(it) + (0,) * (5 - len(it)) for it in items]
-    units = _wgrad_units(items)
+    units = _wgrad_units(items, bf16)
     lo, hi = 1, cdiv(max([n for (_, _, n) in units] or [8]), 8)   # in units of 8 tokens
     while lo < hi:                        # the segment count only falls as the chunk grows
         mid = (lo + hi) // 2
@@ -104,7 +105,7 @@ def wgrad_chunk(items, n_wg=WG_TARGET):
     return 8 * lo
 
 
-def wgrad_segments(items, n_wg=WG_TARGET, tok_per_split=None):
+def wgrad_segments(items, n_wg=WG_TARGET, tok_per_split=None, bf16=False):
     """Split every (item, column group) token span into segments of at most tok_per_split tokens,
     one segment per workgroup; tok_per_split None: the smallest multiple of 8 that keeps the launch
     within n_wg workgroups (all resident at once, one per CU).  Uniform chunks beat a cost-balanced
@@ -113,9 +114,9 @@ def wgrad_segments(items, n_wg=WG_TARGET, tok_per_split=None):
     is bound by HBM traffic and the operand-load rate, so more, smaller segments only add setup
     and partial-reduction work (~10 us per workgroup, scripts/wgrad_trace.py).
     -> (per-workgroup segment lists [(item, cg, t0, t1, slot)], slots per item)."""
-    units = _wgrad_units(items)
+    units = _wgrad_units(items, bf16)
     if tok_per_split is None:
-        tok_per_split = wgrad_chunk(items, n_wg)
+        tok_per_split = wgrad_chunk(items, n_wg, bf16)
     bins = []
     for (i, cg, n) in units:
         tps = tok_per_split[i] if isinstance(tok_per_split, (list, tuple)) else tok_per_split
@@ -210,7 +211,7 @@ def make_wgrad(items, dev, tok_per_split=None, bf16=False):
     the launch's work balanced over one workgroup per CU (wgrad_segments), else fixed token
     chunks.  bf16: plain bf16 operands (the bf16 path) instead of the 3-part split."""
     items = [tuple(it) + (0,) * (5 - len(it)) for it in items]
-    segs, slots = wgrad_segments(items, n_wg=wg_target(), tok_per_split=tok_per_split)
+    segs, slots = wgrad_segments(items, n_wg=wg_target(bf16), tok_per_split=tok_per_split, bf16=bf16)
     total = sum(max(1, s) * N * sum(b[1] for b in bs) for s, (_, N, n, bs, _) in zip(slots, items))
     ws = torch.zeros(max(total, 1), dtype=torch.float32, device=dev)   # unwritten slots stay 0
     descs, off, rmax = [], 0, 0
@@ -241,7 +242,9 @@ def make_wgrad(items, dev, tok_per_split=None, bf16=False):
         for (i, cg, t0, t1, s) in b:
             flat += [(i << 8) | cg, t0, t1, s]
         offs.append(offs[-1] + len(b))
-    return ws, DescArray(WgradDesc, descs, dev, tail=offs + flat), len(segs), rmax
+    arr = DescArray(WgradDesc, descs, dev, tail=offs + flat)
+    arr.prec = _lib.PREC_BF16 if bf16 else 0   # the mep_wgrad instance (launch reads it)
+    return ws, arr, len(segs), rmax
 
 
 def rows(t, T, sB, sT, off=0):
@@ -735,7 +738,7 @@ class TriModalPlan:
         if getattr(self, '_buckets', None) is not None:
             return
         dev, items, nb = self.device, self._wgrad_items, self._n_block_items
-        tps = wgrad_chunk(items, wg_target())
+        tps = wgrad_chunk(items, wg_target(self.bf16), bf16=self.bf16)
         wa = make_wgrad(items[:nb], dev, tok_per_split=tps, bf16=self.bf16)
         wb = make_wgrad(items[nb:], dev, tok_per_split=tps, bf16=self.bf16)
         ca = DescArray(ColsumDesc, self._colsum_a, dev)
