@@ -77,6 +77,12 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 #ifndef MEP_FWD_WAVES
 #define MEP_FWD_WAVES 3    // waves per SIMD of the short, non-residual forward
 #endif
+#ifndef MEP_FWD_LONG_WAVES
+#define MEP_FWD_LONG_WAVES 2   // waves per SIMD of the Tk > 64 forward (hd 16), fp32 split path
+#endif
+#ifndef MEP_FWD_LONG_WAVES_BF
+#define MEP_FWD_LONG_WAVES_BF 2   // the same, bf16 path
+#endif
 
 constexpr int HD = 16;
 constexpr int WAVES = 4;
@@ -559,7 +565,7 @@ MEP_DEV void attn_fwd_task(const mep_attn_desc& d, int qc, int h, int b, int lan
 }
 
 template <bool PREV, bool SOUT, bool SINGLE, bool BF, int HDIM = HD, int QCH = CH>
-__global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu((SINGLE && !PREV && HDIM == 16) ? MEP_FWD_WAVES : (HDIM == 32 && !SINGLE) ? 1 : 2))) void k_attn_fwd(const mep_attn_desc* __restrict__ descs) {
+__global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu((SINGLE && !PREV && HDIM == 16) ? MEP_FWD_WAVES : (HDIM == 32 && !SINGLE) ? 1 : !SINGLE ? (BF ? MEP_FWD_LONG_WAVES_BF : MEP_FWD_LONG_WAVES) : 2))) void k_attn_fwd(const mep_attn_desc* __restrict__ descs) {
     const mep_attn_desc& d = descs[blockIdx.y];
     if ((d.Tk <= CH) != SINGLE) return;    // the other variant's descriptor
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;

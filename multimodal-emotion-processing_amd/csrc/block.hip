@@ -58,6 +58,9 @@ namespace {
 constexpr float LN_EPS = 1e-5f;
 constexpr int EWAVES = 8;                 // waves per workgroup of the epilogues
 constexpr int ETHREADS = 64 * EWAVES;
+#ifndef MEP_EPI_WAVES
+#define MEP_EPI_WAVES 1    // minimum waves per SIMD the epilogue kernels are register-limited to
+#endif
 
 // LDS geometry: the fp32 weights of one block stay resident in LDS for the whole workgroup:
 // forward Wm (and Wp for D <= 96), backward Wm^T (and Wp^T for D <= 96) -- at most 135 KB; for
@@ -844,7 +847,7 @@ template <int D, bool BF16> struct EpiOne {
 // BF16: the bf16 path (one part per operand, every D); otherwise D <= 96 runs the 3-part split
 // and D = 128 the fp32 MFMA path
 template <int D, bool BF16>
-__global__ __launch_bounds__(ETHREADS) void k_epi_fwd(const mep_epi_desc* __restrict__ descs) {
+__global__ __launch_bounds__(ETHREADS) __attribute__((amdgpu_waves_per_eu(MEP_EPI_WAVES))) void k_epi_fwd(const mep_epi_desc* __restrict__ descs) {
     using Geo = EpiGeo<D>;
     const mep_epi_desc& d = descs[blockIdx.y];
     int t_begin, t_end;
@@ -1004,7 +1007,7 @@ MEP_DEV void epi_bwd_tiles(const mep_epi_bwd_desc& bd, const AM& wmt, const AP& 
 }
 
 template <int D, bool BF16>
-__global__ __launch_bounds__(ETHREADS) void k_epi_bwd(const mep_epi_bwd_desc* __restrict__ descs) {
+__global__ __launch_bounds__(ETHREADS) __attribute__((amdgpu_waves_per_eu(MEP_EPI_WAVES))) void k_epi_bwd(const mep_epi_bwd_desc* __restrict__ descs) {
     using Geo = EpiGeo<D>;
     const mep_epi_bwd_desc& bd = descs[blockIdx.y];
     const mep_epi_desc& d = bd.f;

@@ -771,6 +771,9 @@ constexpr int UN_WAVES = 8;
 constexpr int UN_THREADS = 64 * UN_WAVES;
 constexpr int UN_LDS = 30720;   // floats (120 KB): W [N][Kp + 4] when N * (Kp + 4) fits
 constexpr int UN_PF = 8;        // X fragments (k blocks) in flight per lane
+#ifndef MEP_UN_STAGE1
+#define MEP_UN_STAGE1 1         // the whole weight's loads in flight per 320-column pass (0: 4 rows at a time, 18.0 vs 16.5 us at cfg3)
+#endif
 
 template <int NIP, bool WL, bool XV>
 MEP_DEV void unify_tasks(const mep_gemm_desc& d, const lfloat* wl, int ldl, int tile_lo, int tile_hi, int np) {
@@ -983,6 +986,31 @@ __global__ __launch_bounds__(UN_THREADS) void k_unify(const mep_gemm_desc* __res
     const int N = d.N, K = d.K, KB = (K + 15) >> 4, ldl = 16 * KB + 4;
     const bool wlds = N * ldl <= UN_LDS;
     if (wlds) {   // W [N][K] -> LDS rows of ldl floats, zero past K
+#if MEP_UN_STAGE1
+        // wave w stages rows w, w + 8, ... (N <= 128: 16 rows per wave), 320 columns per pass:
+        // every load of a pass in flight at once through a range-checked buffer resource (rows
+        // past N / columns past K read 0, no branches), then the LDS writes
+        const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, KP = 16 * KB;
+        const auto rsW = __builtin_amdgcn_make_buffer_rsrc((void*)d.w, 0, 4 * ((N - 1) * d.ldw + K), 0x00020000);
+        for (int k0 = 0; k0 < KP; k0 += 320) {
+            float v[16][5];
+#pragma unroll
+            for (int r = 0; r < 16; ++r)
+#pragma unroll
+                for (int j = 0; j < 5; ++j) {
+                    const int n = wave + UN_WAVES * r, k = k0 + lane + 64 * j;
+                    v[r][j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                        rsW, (n < N && k < K) ? 4 * (n * d.ldw + k) : WG_INV, 0, 0));
+                }
+#pragma unroll
+            for (int r = 0; r < 16; ++r)
+#pragma unroll
+                for (int j = 0; j < 5; ++j) {
+                    const int n = wave + UN_WAVES * r, k = k0 + lane + 64 * j;
+                    if (n < N && k < KP) wl[n * ldl + k] = v[r][j];
+                }
+        }
+#else
         // wave w stages rows w, w + 8, ...; 4 rows x 320 columns of loads in flight per batch
         const gfloat* W = G<const float>(d.w);
         const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, KP = 16 * KB;
@@ -1005,6 +1033,7 @@ __global__ __launch_bounds__(UN_THREADS) void k_unify(const mep_gemm_desc* __res
                     }
             }
         }
+#endif
         __syncthreads();
     }
 #define MEP_UN(NIP)                                                                          \
