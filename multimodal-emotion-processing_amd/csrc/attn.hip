@@ -77,6 +77,9 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 #ifndef MEP_FWD_WAVES
 #define MEP_FWD_WAVES 3    // waves per SIMD of the short, non-residual forward
 #endif
+#ifndef MEP_BWD_WIDE_WAVES
+#define MEP_BWD_WIDE_WAVES 0   // waves per SIMD of the wide Tk > 64 backward (0: as the short one)
+#endif
 #ifndef MEP_FWD_LONG_WAVES
 #define MEP_FWD_LONG_WAVES 2   // waves per SIMD of the Tk > 64 forward (hd 16), fp32 split path
 #endif
@@ -1137,7 +1140,7 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(2))) vo
 // (fixed order: deterministic) onto the incoming dQ rows.  One barrier per query tile.
 // LDS: [2][STG] staging | [2][waves][256] dQ slots | [waves][TFL] dS transposes.
 template <bool PREV, bool DSN, bool BF, bool KV>
-__global__ __launch_bounds__(64 * MEP_ATTN_MAX_KCHUNKS) __attribute__((amdgpu_waves_per_eu(bwd_short_waves<PREV, DSN, KV>())))
+__global__ __launch_bounds__(64 * MEP_ATTN_MAX_KCHUNKS) __attribute__((amdgpu_waves_per_eu(MEP_BWD_WIDE_WAVES ? MEP_BWD_WIDE_WAVES : bwd_short_waves<PREV, DSN, KV>())))
 void k_attn_bwd_wide(const mep_attn_bwd_desc* __restrict__ descs) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     typedef Bwd<PREV, DSN, BF, KV> U;

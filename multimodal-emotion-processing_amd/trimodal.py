@@ -51,7 +51,7 @@ def cdiv(a, b):
 
 WG_WAVES = 4              # csrc/gemm.hip k_wgrad: waves per workgroup (token quarters of a split)
 WG_TARGET = _lib.N_CU      # workgroups per launch: one per CU (4 waves of ~400 registers)
-WG_TARGET_OVERRIDE = None  # development: another workgroup count for wgrad_segments
+WG_TARGET_OVERRIDE = int(os.environ.get('MEP_WG_TARGET', '0')) or None   # development: another k_wgrad workgroup count
 # the pool's backward formed inside the epilogue backward (0: a separate mep_pool_bwd into dXcat)
 POOL_FOLD = os.environ.get('MEP_POOL_FOLD', '1') != '0'
 # per-modality gradient sums inside the attention backward (no mep_sum_rows launch): correct (bit
