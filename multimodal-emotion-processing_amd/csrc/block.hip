@@ -1048,19 +1048,27 @@ __global__ __launch_bounds__(256) void k_ln_fwd(const mep_ln_desc* __restrict__ 
     const int tok = blockIdx.x * 4 + wave;
     if (tok >= d.ntok) return;
     const gfloat* x = row_ptr(d.x, tok);
-    float v[4], s = 0.f;
+    const gfloat* w = G<const float>(d.w);
+    const gfloat* b = G<const float>(d.b);
+    // every load up front (clamped columns, no branches): one memory latency per row
+    float v[4], wv[4], bv[4], s = 0.f;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) { const int c = lane + 64 * j; v[j] = c < d.D ? x[c] : 0.f; s += v[j]; }
+    for (int j = 0; j < 4; ++j) {
+        const int c = min(lane + 64 * j, d.D - 1);
+        v[j] = x[c];
+        wv[j] = w[c];
+        bv[j] = b[c];
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) { v[j] = lane + 64 * j < d.D ? v[j] : 0.f; s += v[j]; }
     const float mean = wave_sum(s) / (float)d.D;
     float q = 0.f;
 #pragma unroll
     for (int j = 0; j < 4; ++j) { const int c = lane + 64 * j; v[j] = c < d.D ? v[j] - mean : 0.f; q += v[j] * v[j]; }
     const float rstd = 1.0f / sqrtf(wave_sum(q) / (float)d.D + LN_EPS);
-    const gfloat* w = G<const float>(d.w);
-    const gfloat* b = G<const float>(d.b);
     gfloat* y = row_ptr(d.y, tok);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) { const int c = lane + 64 * j; if (c < d.D) y[c] = v[j] * rstd * w[c] + b[c]; }
+    for (int j = 0; j < 4; ++j) { const int c = lane + 64 * j; if (c < d.D) y[c] = v[j] * rstd * wv[j] + bv[j]; }
     if (lane == 0) {
         gfloat* st = G<float>(d.stats);
         st[2 * tok] = mean;
@@ -1068,7 +1076,11 @@ __global__ __launch_bounds__(256) void k_ln_fwd(const mep_ln_desc* __restrict__ 
     }
 }
 
-// backward; partial[blockIdx.x][2][D] = per-workgroup (dgamma, dbeta) over its 64 rows
+// backward; partial[blockIdx.x][2][D] = per-workgroup (dgamma, dbeta) over its 64 rows.  A wave
+// takes rows wave, wave + 4, ... in batches of LNB_ROWS: every load of a batch (clamped columns and
+// tokens, no branches) is issued before the batch's arithmetic, which runs row by row in the same
+// order as one row at a time (bit-identical sums).
+constexpr int LNB_ROWS = 4;
 __global__ __launch_bounds__(256) void k_ln_bwd(const mep_ln_desc* __restrict__ descs) {
     const mep_ln_desc& d = descs[blockIdx.y];
     const int tok0 = blockIdx.x * 64;
@@ -1078,34 +1090,51 @@ __global__ __launch_bounds__(256) void k_ln_bwd(const mep_ln_desc* __restrict__ 
     float pw[4] = {0.f, 0.f, 0.f, 0.f}, pb[4] = {0.f, 0.f, 0.f, 0.f};
     const gfloat* w = G<const float>(d.w);
     const gfloat* st = G<const float>(d.stats);
-    for (int row = wave; row < 64; row += 4) {
-        const int tok = tok0 + row;
-        if (tok >= d.ntok) break;
-        const float mean = st[2 * tok], rstd = st[2 * tok + 1];
-        const gfloat* x = row_ptr(d.x, tok);
-        const gfloat* dy = row_ptr(d.dy, tok);
-        float xh[4], gw[4], s1 = 0.f, s2 = 0.f;
+    float wv[4];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const int c = lane + 64 * j;
-            const bool ok = c < d.D;
-            const float g = ok ? dy[c] : 0.f;
-            xh[j] = ok ? (x[c] - mean) * rstd : 0.f;
-            gw[j] = ok ? g * w[c] : 0.f;
-            pw[j] += g * xh[j];
-            pb[j] += g;
-            s1 += gw[j];
-            s2 += gw[j] * xh[j];
+    for (int j = 0; j < 4; ++j) wv[j] = w[min(lane + 64 * j, d.D - 1)];
+    for (int r0 = wave; r0 < 64; r0 += 4 * LNB_ROWS) {
+        float gv[LNB_ROWS][4], xv[LNB_ROWS][4], mean[LNB_ROWS], rstd[LNB_ROWS];
+#pragma unroll
+        for (int i = 0; i < LNB_ROWS; ++i) {
+            const int tk = min(tok0 + r0 + 4 * i, d.ntok - 1);
+            mean[i] = st[2 * tk];
+            rstd[i] = st[2 * tk + 1];
+            const gfloat* x = row_ptr(d.x, tk);
+            const gfloat* dy = row_ptr(d.dy, tk);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int c = min(lane + 64 * j, d.D - 1);
+                gv[i][j] = dy[c];
+                xv[i][j] = x[c];
+            }
         }
-        s1 = wave_sum(s1) / (float)d.D;
-        s2 = wave_sum(s2) / (float)d.D;
-        gfloat* dx = row_ptr(d.dx, tok);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const int c = lane + 64 * j;
-            if (c < d.D) {
-                const float v = rstd * (gw[j] - s1 - xh[j] * s2);
-                dx[c] = d.dx_accumulate ? dx[c] + v : v;
+        for (int i = 0; i < LNB_ROWS; ++i) {
+            const int tok = tok0 + r0 + 4 * i;
+            if (r0 + 4 * i >= 64 || tok >= d.ntok) break;
+            float xh[4], gw[4], s1 = 0.f, s2 = 0.f;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const bool ok = lane + 64 * j < d.D;
+                const float g = ok ? gv[i][j] : 0.f;
+                xh[j] = ok ? (xv[i][j] - mean[i]) * rstd[i] : 0.f;
+                gw[j] = ok ? g * wv[j] : 0.f;
+                pw[j] += g * xh[j];
+                pb[j] += g;
+                s1 += gw[j];
+                s2 += gw[j] * xh[j];
+            }
+            s1 = wave_sum(s1) / (float)d.D;
+            s2 = wave_sum(s2) / (float)d.D;
+            gfloat* dx = row_ptr(d.dx, tok);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int c = lane + 64 * j;
+                if (c < d.D) {
+                    const float v = rstd[i] * (gw[j] - s1 - xh[j] * s2);
+                    dx[c] = d.dx_accumulate ? dx[c] + v : v;
+                }
             }
         }
     }
