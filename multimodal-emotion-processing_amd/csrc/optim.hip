@@ -93,7 +93,8 @@ __global__ __launch_bounds__(OPT_THREADS) void k_clip_adam(float* __restrict__ p
 #pragma unroll
         for (int u = 0; u < 16; ++u) {
             const int i = i0 + (int)threadIdx.x + OPT_THREADS * u;
-            v[u] = i < npart ? partial[pbase + i] : 0.f;
+            const float p = partial[pbase + min(i, npart - 1)];   // clamped: no branch per load
+            v[u] = i < npart ? p : 0.f;
         }
 #pragma unroll
         for (int u = 0; u < 16; ++u) s += v[u];
