@@ -1042,37 +1042,51 @@ __global__ __launch_bounds__(ETHREADS) __attribute__((amdgpu_waves_per_eu(MEP_EP
 }
 
 // ---------------------------------------------------------------- row LayerNorm (D <= 256)
+// forward: a workgroup takes LNF_ROWS x 4 rows (row 4i + wave of its range for wave `wave`), every
+// load of a wave's rows issued before the first row's arithmetic (clamped tokens and columns, no
+// branches); each row's arithmetic is unchanged.  Host grids stay ceil(ntok / 4) "tiles"; the
+// launcher runs ceil(tiles / LNF_ROWS) workgroups.
+constexpr int LNF_ROWS = 4;
 __global__ __launch_bounds__(256) void k_ln_fwd(const mep_ln_desc* __restrict__ descs) {
     const mep_ln_desc& d = descs[blockIdx.y];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int tok = blockIdx.x * 4 + wave;
-    if (tok >= d.ntok) return;
-    const gfloat* x = row_ptr(d.x, tok);
+    const int tok0 = blockIdx.x * 4 * LNF_ROWS + wave;
+    if (tok0 >= d.ntok) return;
     const gfloat* w = G<const float>(d.w);
     const gfloat* b = G<const float>(d.b);
-    // every load up front (clamped columns, no branches): one memory latency per row
-    float v[4], wv[4], bv[4], s = 0.f;
+    float v[LNF_ROWS][4], wv[4], bv[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
         const int c = min(lane + 64 * j, d.D - 1);
-        v[j] = x[c];
         wv[j] = w[c];
         bv[j] = b[c];
     }
 #pragma unroll
-    for (int j = 0; j < 4; ++j) { v[j] = lane + 64 * j < d.D ? v[j] : 0.f; s += v[j]; }
-    const float mean = wave_sum(s) / (float)d.D;
-    float q = 0.f;
+    for (int i = 0; i < LNF_ROWS; ++i) {
+        const gfloat* x = row_ptr(d.x, min(tok0 + 4 * i, d.ntok - 1));
 #pragma unroll
-    for (int j = 0; j < 4; ++j) { const int c = lane + 64 * j; v[j] = c < d.D ? v[j] - mean : 0.f; q += v[j] * v[j]; }
-    const float rstd = 1.0f / sqrtf(wave_sum(q) / (float)d.D + LN_EPS);
-    gfloat* y = row_ptr(d.y, tok);
+        for (int j = 0; j < 4; ++j) v[i][j] = x[min(lane + 64 * j, d.D - 1)];
+    }
 #pragma unroll
-    for (int j = 0; j < 4; ++j) { const int c = lane + 64 * j; if (c < d.D) y[c] = v[j] * rstd * wv[j] + bv[j]; }
-    if (lane == 0) {
-        gfloat* st = G<float>(d.stats);
-        st[2 * tok] = mean;
-        st[2 * tok + 1] = rstd;
+    for (int i = 0; i < LNF_ROWS; ++i) {
+        const int tok = tok0 + 4 * i;
+        if (tok >= d.ntok) break;
+        float s = 0.f;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) { v[i][j] = lane + 64 * j < d.D ? v[i][j] : 0.f; s += v[i][j]; }
+        const float mean = wave_sum(s) / (float)d.D;
+        float q = 0.f;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) { const int c = lane + 64 * j; v[i][j] = c < d.D ? v[i][j] - mean : 0.f; q += v[i][j] * v[i][j]; }
+        const float rstd = 1.0f / sqrtf(wave_sum(q) / (float)d.D + LN_EPS);
+        gfloat* y = row_ptr(d.y, tok);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) { const int c = lane + 64 * j; if (c < d.D) y[c] = v[i][j] * rstd * wv[j] + bv[j]; }
+        if (lane == 0) {
+            gfloat* st = G<float>(d.stats);
+            st[2 * tok] = mean;
+            st[2 * tok + 1] = rstd;
+        }
     }
 }
 
@@ -1192,7 +1206,7 @@ extern "C" int mep_block_epi_bwd(const mep_epi_bwd_desc* descs, int n_desc, int 
 // max_tiles: forward = ceil(ntok / 4) (wave per row), backward = ceil(ntok / 64)
 extern "C" int mep_layernorm_fwd(const mep_ln_desc* descs, int n_desc, int max_tiles, mep_stream_t stream) {
     if (n_desc <= 0 || max_tiles <= 0) return 0;
-    hipLaunchKernelGGL(k_ln_fwd, dim3(max_tiles, n_desc), dim3(256), 0, (hipStream_t)stream, descs);
+    hipLaunchKernelGGL(k_ln_fwd, dim3((max_tiles + LNF_ROWS - 1) / LNF_ROWS, n_desc), dim3(256), 0, (hipStream_t)stream, descs);
     return mep_check_launch("mep_layernorm_fwd");
 }
 
