@@ -26,7 +26,13 @@ namespace {
 
 constexpr int TG_WAVES = 4;
 constexpr int TG_THREADS = 64 * TG_WAVES;
-constexpr int TG_TT = 2;                          // 16-token tiles per wave
+#ifndef MEP_TG_TT
+#define MEP_TG_TT 2
+#endif
+#ifndef MEP_TG_NI
+#define MEP_TG_NI 8        // 16-column tiles of a workgroup's N tile at N >= 128
+#endif
+constexpr int TG_TT = MEP_TG_TT;                  // 16-token tiles per wave
 constexpr int TG_BM = 16 * TG_TT * TG_WAVES;      // tokens per workgroup
 
 // W(n, k .. k+3) of the staged chunk, zero past K / N
@@ -338,7 +344,7 @@ extern "C" int mep_tgemm(const mep_gemm_desc* descs, int n_desc, int max_ntok, i
 #undef MEP_TR3
         return mep_check_launch("mep_tgemm");
     }
-    const int ni = max_n >= 128 ? 8 : (max_n + 15) / 16;   // 16-col tiles per workgroup N tile
+    const int ni = max_n >= 16 * MEP_TG_NI ? MEP_TG_NI : (max_n + 15) / 16;   // 16-col tiles per workgroup N tile
     const dim3 grid((max_ntok + TG_BM - 1) / TG_BM, n_desc, (max_n + 16 * ni - 1) / (16 * ni)), block(TG_THREADS);
 #define MEP_TG3(NI, P, WT) hipLaunchKernelGGL((k_tgemm<NI, P, WT>), grid, block, 0, st, descs)
 #define MEP_TG2(NI, P) do { if (wnt) MEP_TG3(NI, P, true); else MEP_TG3(NI, P, false); } while (0)
