@@ -103,6 +103,20 @@ def cpu_model():
     return platform.processor() or 'unknown'
 
 
+def host_cpus():
+    """(CPUs this process may run on, the cgroup CPU quota or None): a GPU box's affinity mask can
+    list the whole machine while its cgroup grants a share of it"""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        q, period = open('/sys/fs/cgroup/cpu.max').read().split()[:2]
+        if q != 'max':
+            quota = max(1, int(int(q) // int(period)))
+    except (OSError, ValueError):
+        pass
+    return aff, quota
+
+
 def timed_cpu(step, budget_s, max_steps=200):
     step()                                   # warmup
     n, t0 = 0, time.perf_counter()
@@ -468,9 +482,17 @@ def main():
         'roofline_attention': roofline_of(work, 'mep_attn_bwd', tot, reps, costs),
         'kernels': per_kernel,
     }
+    out['switches'] = {'read': {k: v['value'] for k, v in sorted(_lib.SWITCHES.items())},
+                       'set_in_env': _lib.switches_from_env()}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        # the oracle on the box's host cores -- every CPU this process may use
+        # (capped by the cgroup quota when there is one)
+        aff, quota = host_cpus()
+        threads = min(aff, quota) if quota else aff
+        torch.set_num_threads(threads)
         cb = CONFIGS[args.config].cpu_baseline(args.cpu_budget)
-        cb.update(cores=torch.get_num_threads(), kind='port', cpu_model=cpu_model())
+        cb.update(cores=torch.get_num_threads(), kind='port', cpu_model=cpu_model(), affinity_cpus=aff,
+                  cgroup_cpus=quota)
         out['cpu_baseline'] = cb
         out['gpu_vs_cpu'] = round(out['value'] / cb['value'], 1)
     if rank == 0:

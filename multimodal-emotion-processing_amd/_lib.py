@@ -11,8 +11,26 @@ import os
 import torch
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+
+# Every MEP_* development switch the package reads, with the value in effect (bench.py prints it,
+# so a stray variable on a box shows up in the line it changed).  Defaults are the product path.
+SWITCHES = {}
+
+
+def switch(name, default):
+    """os.environ[name] or default, recorded in SWITCHES (with whether the environment set it)"""
+    v = os.environ.get(name)
+    SWITCHES[name] = {'value': default if v is None else v, 'from_env': v is not None}
+    return default if v is None else v
+
+
+def switches_from_env():
+    """the MEP_* variables set in this process's environment (any, read or not)"""
+    return {k: v for k, v in sorted(os.environ.items()) if k.startswith('MEP_')}
+
+
 # MEP_LIB: development override (A/B experiments with variant builds); never set in normal use
-LIB_PATH = os.environ.get('MEP_LIB') or os.path.join(PKG_DIR, 'libmep_hip.so')
+LIB_PATH = switch('MEP_LIB', '') or os.path.join(PKG_DIR, 'libmep_hip.so')
 
 u64, i64, i32, f32 = ctypes.c_uint64, ctypes.c_int64, ctypes.c_int32, ctypes.c_float
 
@@ -350,7 +368,7 @@ ATTN_HD32 = 0x20000   # MEP_ATTN_HD32: head dim 32 attention forward (robot_demo
 ATTN_KV = 0x40000     # MEP_ATTN_KV: backward with k == v and dk == dv on every descriptor
 ATTN_SPLITQ = 0x80000 # MEP_ATTN_SPLITQ: backward, Tk <= 64 descriptors on the workgroup-per-(b, h) kernel
 ATTN_MAX_KCHUNKS = 8  # MEP_ATTN_MAX_KCHUNKS: the chunk-parallel backward (MEP_ATTN_KCHUNKS) up to 512 keys
-ATTN_WIDE = os.environ.get('MEP_ATTN_WIDE', '1') != '0'   # 0: the key-chunk-serial kernel (A/B runs)
+ATTN_WIDE = switch('MEP_ATTN_WIDE', '1') != '0'   # 0: the key-chunk-serial kernel (A/B runs)
 
 
 def attn_fwd_splitq(descs, min_units=1024):
@@ -370,7 +388,7 @@ def attn_bwd_splitq(bdescs, min_units=1024):
     return ATTN_SPLITQ if 0 < units < min_units else 0
 
 
-RFW = os.environ.get('MEP_RFW', '1') != '0'   # 0: the LDS-tiled f32-MFMA realformer kernels (A/B runs)
+RFW = switch('MEP_RFW', '1') != '0'   # 0: the LDS-tiled f32-MFMA realformer kernels (A/B runs)
 
 
 def rf_bwd_rows(wave=None):
@@ -443,15 +461,15 @@ def attn_dc_slots(B, H, Tk):
 
 
 # ------------------------------------------------------------------ token GEMMs
-TGEMM = os.environ.get('MEP_TGEMM', '1') != '0'   # 0: the mep_unify / mep_gemm kernels (A/B runs)
+TGEMM = switch('MEP_TGEMM', '1') != '0'   # 0: the mep_unify / mep_gemm kernels (A/B runs)
 # mep_tgemm chunked (K in 32-wide LDS stages) wins where the weight is too large to keep resident
 # (Ren-MME unify, K = 768 / 640: 153 -> 94 us at cfg5); at K <= 300 its per-chunk staging latency
 # loses to the weight-stationary mep_unify / mep_gemm (cmu-mosei unify 22 vs 17 us).  The
 # resident-weight form (MEP_TGEMM_RESIDENT, opt-in with MEP_TGEMM_RES=1) lost too: 22.3 vs 17.4 us
 # (cmu-mosei unify), 99.7 vs 89.8 us (cfg2's five GEMMs), and its 2-part weight moved a cmu_cfg1
 # logit by 1.1e-3 relative -- outside the 1e-4 parity
-TGEMM_RES = os.environ.get('MEP_TGEMM_RES', '0') == '1'
-TGEMM_MIN_K = int(os.environ.get('MEP_TGEMM_MIN_K', '512'))
+TGEMM_RES = switch('MEP_TGEMM_RES', '0') == '1'
+TGEMM_MIN_K = int(switch('MEP_TGEMM_MIN_K', '512'))
 TGEMM_RES_MAX_K = 320                              # csrc/tgemm.hip TGR_KP * 32
 TGEMM_WT = 0x1                                     # MEP_TGEMM_WT: every descriptor has w_nt = 0
 TGEMM_RESIDENT = 0x2                               # MEP_TGEMM_RESIDENT

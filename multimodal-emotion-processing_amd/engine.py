@@ -19,11 +19,12 @@ last attention backward, the per-modality sums and the unify weight gradients ru
 them.  With gloo (CPU tests) the SUM is a host call between two graph replays.
 """
 import ctypes
-import os
 import warnings
 
 import torch
 import torch.distributed as dist
+
+from . import _lib
 
 
 class TrainEngine:
@@ -47,16 +48,16 @@ class TrainEngine:
         self.collective = (self.world > 1) if collective is None else (bool(collective) and dist_on)
         backend = dist.get_backend(process_group) if dist_on else None
         if capture_allreduce is None:
-            env = os.environ.get('MEP_CAPTURE_ALLREDUCE')
+            env = _lib.switch('MEP_CAPTURE_ALLREDUCE', None)
             capture_allreduce = (env != '0') if env is not None else backend == 'nccl'
         self.capture_allreduce = bool(capture_allreduce) and self.collective and backend == 'nccl'
         # RCCL: bucket A of the flat gradient (FlatParams.split) is all-reduced on a side stream
         # while the rest of the backward runs (plans with backward_bucketed)
-        env = os.environ.get('MEP_DP_OVERLAP')
+        env = _lib.switch('MEP_DP_OVERLAP', None)
         self.overlap = self.collective and backend == 'nccl' and (env != '0' if env is not None else True)
         self._side = None
         self._graphs = {}
-        self.fold_norm = (os.environ.get('MEP_NORM_FOLD', '1') != '0') if fold_norm is None else bool(fold_norm)
+        self.fold_norm = (_lib.switch('MEP_NORM_FOLD', '1') != '0') if fold_norm is None else bool(fold_norm)
         self._initial_broadcast = self.world > 1
 
     def _runner(self, device):
@@ -208,7 +209,6 @@ class TrainEngine:
         self.opt._bind()
         self.opt._sync_hyper(self.clip, 1.0)
         if runner.drop_p() > 0.0 and getattr(runner, 'seed_state', None) is not None:
-            from . import _lib
             _lib.call('mep_seed_advance', ctypes.c_void_p(runner.seed_state.data_ptr()))
         self._sync_params(runner)
         runner.flat.grad.zero_()

@@ -21,7 +21,6 @@ adjacent [w_qkv.1; w_qkv.2] weights, one [ntok, 2D] gradient); last-layer output
 straight into the pooled tensor [R, T_l+T_a+T_v, 3D] (torch.cat at realformer.py:258-261).
 """
 import ctypes
-import os
 
 import torch
 
@@ -30,7 +29,7 @@ from ._lib import (AttnBwdDesc, AttnDesc, ColsumDesc, DescArray, GemmDesc, PoolD
                    RfHeadDesc, Rows, SumDesc, launch)
 from .trimodal import CHAINS, MODS, TIME_ORDER, UNIFY_NAMES, _norm_args, cdiv, crows, make_wgrad, rows
 
-RF_SPLITQ = os.environ.get('MEP_RF_SPLITQ', '1') != '0'   # attention backward: query tiles over 4 waves
+RF_SPLITQ = _lib.switch('MEP_RF_SPLITQ', '1') != '0'   # attention backward: query tiles over 4 waves
 
 NC = 6  # State_Transfer classes (realformer.py:268-269)
 POS_NAMES = {'l': 'linguistic_position', 'v': 'visual_position', 'a': 'acoustic_position'}

@@ -22,7 +22,6 @@ through strided row views.
 """
 import ctypes
 import functools
-import os
 
 import torch
 
@@ -51,14 +50,14 @@ def cdiv(a, b):
 
 WG_WAVES = 4              # csrc/gemm.hip k_wgrad: waves per workgroup (token quarters of a split)
 WG_TARGET = _lib.N_CU      # workgroups per launch: one per CU (4 waves of ~400 registers)
-WG_TARGET_OVERRIDE = int(os.environ.get('MEP_WG_TARGET', '0')) or None   # development: another k_wgrad workgroup count
+WG_TARGET_OVERRIDE = int(_lib.switch('MEP_WG_TARGET', '0')) or None   # development: another k_wgrad workgroup count
 # the pool's backward formed inside the epilogue backward (0: a separate mep_pool_bwd into dXcat)
-POOL_FOLD = os.environ.get('MEP_POOL_FOLD', '1') != '0'
+POOL_FOLD = _lib.switch('MEP_POOL_FOLD', '1') != '0'
 # per-modality gradient sums inside the attention backward (no mep_sum_rows launch): correct (bit
 # equal) but off -- the agent-scope release every (b, h) unit needs before it counts its slices
 # took the cfg3 attention backward from 36 to 641 us
-SUM_FOLD = os.environ.get('MEP_SUM_FOLD', '0') == '1'
-FWD_SPLITQ = os.environ.get('MEP_FWD_SPLITQ', '0') == '1'
+SUM_FOLD = _lib.switch('MEP_SUM_FOLD', '0') == '1'
+FWD_SPLITQ = _lib.switch('MEP_FWD_SPLITQ', '0') == '1'
 
 
 def wgrad_geometry(N, ktot, bf16=False):
@@ -139,7 +138,7 @@ def wgrad_segments(items, n_wg=WG_TARGET, tok_per_split=None, bf16=False):
     return segs, slots
 
 
-WG_XCD_PAIR = os.environ.get('MEP_WG_XCD', '1') != '0'
+WG_XCD_PAIR = _lib.switch('MEP_WG_XCD', '1') != '0'
 
 
 def _xcd_pairs(segs, n_wg):
@@ -743,7 +742,32 @@ class TriModalPlan:
         wb = make_wgrad(items[nb:], dev, tok_per_split=tps, bf16=self.bf16)
         ca = DescArray(ColsumDesc, self._colsum_a, dev)
         cb = DescArray(ColsumDesc, self._colsum_b, dev)
+        self._check_bucket_ranges(wa[1], wb[1], ca, cb)
         self._buckets = (wa, wb, ca, cb)
+
+    def _check_bucket_ranges(self, wa, wb, ca, cb):
+        """Bucket membership is defined twice -- by parameter name (TriModalSpec.bucket_a, which
+        orders the flat buffer) and by descriptor order (_n_block_items, _colsum_a / _colsum_b) --
+        so check on the host that every gradient byte bucket A's launches write lies in
+        flat.grad[:split] and every byte bucket B's write lies in flat.grad[split:n_grad]: a write
+        outside its bucket would race the side-stream all-reduce (engine.py)."""
+        fl = self.flat
+        g0 = fl.grad.data_ptr()
+        lo_hi = {'A': (g0, g0 + 4 * fl.split), 'B': (g0 + 4 * fl.split, g0 + 4 * fl.n_grad)}
+
+        def extents(warr, carr):
+            for d in warr.items:
+                for b in range(d.n_b):
+                    rows_, cols_ = (d.kb[b], d.N) if d.out_trans else (d.N, d.kb[b])
+                    yield d.out[b], d.out[b] + 4 * ((rows_ - 1) * d.ldo[b] + cols_)
+            for c in carr.items:
+                yield c.out, c.out + 4 * c.n_cols
+        head = [p for p in self.head_grads[:-1]]          # the last entry is the loss, not a gradient
+        for name, warr, carr, extra in (('A', wa, ca, head), ('B', wb, cb, [])):
+            lo, hi = lo_hi[name]
+            for a, b in list(extents(warr, carr)) + [(p, p + 4) for p in extra]:
+                assert lo <= a and b <= hi, ('gradient write [%#x, %#x) outside bucket %s [%#x, %#x)'
+                                             % (a, b, name, lo, hi))
 
     def backward_bucketed(self, bucket_a_done, ext_dlogits=None, stream=None):
         """backward() with the gradient reductions split by bucket: bucket A's gradients are

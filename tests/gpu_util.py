@@ -80,6 +80,10 @@ def check_post_params(model, meta, gold, lr=1e-3, atol=2e-5, noise=1e-6):
         assert not bool(bad.any()), (k, float(err.max()), int(bad.sum()))
         if gkey in gold:
             noisy = (g < noise).to(p.device)
+            # the 2 lr exemption may only ever be USED by a few rounding-noise entries of a tensor
+            # (coin-flip step directions), never by a real share of it
+            used = int(((g < noise) & (err > tol.new_full((), atol))).sum())
+            assert used <= max(2, err.numel() // 1000), (k, used, err.numel(), 'noise-level entries beyond atol')
             if bool(noisy.any()):
                 with torch.no_grad():
                     ref_t = torch.as_tensor(ref).to(p.device, p.dtype).reshape(got.shape)

@@ -99,3 +99,59 @@ def test_norm_fold_matches_optimizer_norm_pass(cuda):
     assert float((l1 - l0).abs().max()) <= 1e-6 * float(l0.abs().max()), (l1, l0)
     for (k, p1), (_, p0) in zip(m1.named_parameters(), m0.named_parameters()):
         assert float((p1 - p0).abs().max()) <= 1e-6, k
+
+
+def _fold_pair(build, steps=4):
+    """(engine, model, losses, gnorms) with the norm pass folded and with the optimizer's own pass;
+    build(fold_norm) -> (engine, model, step function)"""
+    out = []
+    for fold in (True, False):
+        eng, model, step = build(fold)
+        losses, gn = [], []
+        for _ in range(steps):
+            losses.append(step(eng).clone())
+            gn.append(eng.opt.gnorm.clone())
+        torch.cuda.synchronize()
+        assert (eng._n_ext > 0) == fold, 'fold_norm=%s not honoured' % fold
+        out.append((model, torch.cat(losses), torch.cat([g.reshape(1) for g in gn])))
+    (m1, l1, g1), (m0, l0, g0) = out
+    assert float((g1 - g0).abs().max() / g0.abs().max()) < 1e-6, (g1, g0)
+    assert float((l1 - l0).abs().max()) <= 1e-6 * float(l0.abs().max()), (l1, l0)
+    for (k, p1), (_, p0) in zip(m1.named_parameters(), m0.named_parameters()):
+        assert float((p1 - p0).abs().max()) <= 1e-6, k
+
+
+def test_norm_fold_matches_optimizer_norm_pass_ren_dropout(cuda):
+    """Ren-MME at DROP = 0.1 with R-Drop: the shared unify LayerNorm's column sums and the dropout
+    epilogues write gradients the folded norm must see; the pre-clip norm at every step and the
+    parameters after 4 graph-replayed AdamW steps match the optimizer's own norm pass."""
+    from mep_amd import ren_mme
+    from mep_amd.engine import TrainEngine
+    from mep_amd.optim import FusedAdamW
+    meta, _ = fixtures.load('ren_drop_long')
+    inputs, labels = fixtures.batch(meta)
+    batch = list(ren_mme._pack([t.to(cuda) for t in inputs])) + [labels.to(cuda)]
+
+    def build(fold):
+        model = ren_model(meta, cuda, drop=meta['drop']['p'])
+        model.train()
+        eng = TrainEngine(model, FusedAdamW(model, lr=1e-3), clip=1.0, rdrop=True, graph=True, fold_norm=fold)
+        model.mep_runner(cuda).seed_state[0].fill_(31337)
+        return eng, model, lambda e: e.step(*batch)
+    _fold_pair(build)
+
+
+def test_norm_fold_matches_optimizer_norm_pass_realformer(cuda):
+    """realformer State_Transfer (Adam, position-embedding column sums, the batch-loss column sum
+    that is not a gradient): folded norm vs the optimizer's own norm pass over 4 steps."""
+    from mep_amd.engine import TrainEngine
+    from mep_amd.optim import FusedAdam
+    from tests.test_gpu_realformer import _batch, _state
+    meta, _ = fixtures.load('rf_state_small')
+    batch = _batch(meta, cuda)
+
+    def build(fold):
+        model = _state(meta, cuda)
+        eng = TrainEngine(model, FusedAdam(model, lr=1e-3), clip=1.0, graph=True, fold_norm=fold)
+        return eng, model, lambda e: e.step(*batch)
+    _fold_pair(build)

@@ -64,10 +64,15 @@ def _decode(arr):
     return [arr.struct.from_buffer_copy(raw[i * sz:(i + 1) * sz]) for i in range(arr.n)]
 
 
-def _gemm(c, d):
+def _gemm(c, d, parts=False):
+    """parts: the weight is a mep_wsplit parts image (wave-tiled realformer path: mep_wgemm reads
+    W' [N][K] as three bf16 parts with rows padded to 32), not the fp32 parameter"""
     c.rows('gemm.x', d.x, d.ntok, d.K)
     c.rows('gemm.y', d.y, d.ntok, d.N)
-    c.inside('gemm.w', d.w, ((d.N - 1) * d.ldw + d.K if d.w_nt else (d.K - 1) * d.ldw + d.N) * F)
+    if parts:
+        c.inside('gemm.wparts', d.w, _lib.wsplit_bytes(cdiv(d.N, 32) * 32, d.K))
+    else:
+        c.inside('gemm.w', d.w, ((d.N - 1) * d.ldw + d.K if d.w_nt else (d.K - 1) * d.ldw + d.N) * F)
     c.inside('gemm.bias', d.bias, d.N * F)
     c.inside('gemm.table', d.table, d.y.T * d.N * F)
 
@@ -200,11 +205,27 @@ def _rf_epi(c, d, tag='rf_epi'):
     c.inside(tag + '.a', d.a, F)
     c.inside(tag + '.b', d.b, F)
     c.inside(tag + '.stats', d.stats, d.ntok * 4 * F)
+    if d.wparts:       # wave-tiled epilogue: the six parts of Wp, W1, W2 and their transposes
+        c.inside(tag + '.wparts', d.wparts, _lib.rfw_part_offsets(d.D, d.FD)[1])
+    if d.wq_next:      # fused query projection of the next layer: W_q parts, QP rows
+        c.inside(tag + '.wq_next', d.wq_next, _lib.wsplit_bytes(cdiv(d.D, 32) * 32, d.D))
+        c.rows(tag + '.qp_next', d.qp_next, d.ntok, d.D)
+
+
+def _wsplit(c, d):
+    """mep_wsplit: W' [nrows][K] read from the fp32 parameter, parts written into the arena"""
+    assert d.R == cdiv(d.nrows, 32) * 32 and d.nrows > 0 and d.K > 0
+    ext = (d.K - 1) * d.ld + d.nrows if d.trans else (d.nrows - 1) * d.ld + d.K
+    c.inside('wsplit.src', d.src, ext * F)
+    c.inside('wsplit.dst', d.dst, _lib.wsplit_bytes(d.R, d.K))
 
 
 def _rf_epi_bwd(c, d):
     f = d.f
     _rf_epi(c, f, 'rf_epi_bwd')
+    if d.wq_in:        # fused dQP W_q input gradient of the next layer
+        c.inside('rf_epi_bwd.wq_in', d.wq_in, _lib.wsplit_bytes(cdiv(f.D, 32) * 32, f.D))
+        c.rows('rf_epi_bwd.dqp_in', d.dqp_in, f.ntok, f.D)
     for name in ('dout', 'dout2', 'df', 'dxp', 'dx', 'dq'):
         c.rows('rf_epi_bwd.' + name, getattr(d, name), f.ntok, f.D)
     c.rows('rf_epi_bwd.df1', d.df1, f.ntok, f.FD)
@@ -225,10 +246,16 @@ def _rf_head(c, d):
 
 def check_rf_plan(p):
     c = Checker(p)
-    for arr in [p.d_unify, p.d_proj] + list(p.d_q) + list(p.d_ingrad) + \
-            ([p.d_fc, p.d_fcb] if p.spec.head else []):
+    # on the wave path (MEP_RFW, the default) the token GEMMs read mep_wsplit parts
+    for arr in [p.d_unify, p.d_proj] + list(p.d_q) + list(p.d_ingrad) + [p.d_ingrad_all]:
+        for d in _decode(arr):
+            _gemm(c, d, parts=p.rfw)
+    for arr in ([p.d_fc, p.d_fcb] if p.spec.head else []):
         for d in _decode(arr):
             _gemm(c, d)
+    if p.rfw:
+        for d in _decode(p.d_wsplit):
+            _wsplit(c, d)
     for d in _decode(p.d_wgrad):
         _wgrad(c, d)
     for arrs, fn in ((p.d_attn, _attn), (p.d_attnb, _attn_bwd), (p.d_epi, _rf_epi), (p.d_epib, _rf_epi_bwd)):
@@ -321,3 +348,63 @@ def test_realformer_plan_descriptors_in_bounds(kw, B, P, head):
     finally:
         rf.FFN = old
     assert check_rf_plan(plan) > 20
+
+
+def _writes(arr_w, arr_c, head=None, NC=None, Fd=None):
+    """(first float, count) runs of the flat gradient buffer a bucket's launches write: the weight
+    gradients' output rows, the column sums and the fused head's parameter sums"""
+    out = []
+    for d in (arr_w.items if arr_w is not None else []):
+        for b in range(d.n_b):
+            rows_, cols_ = (d.kb[b], d.N) if d.out_trans else (d.N, d.kb[b])
+            out += [(d.out[b] + 4 * r * d.ldo[b], cols_) for r in range(rows_)]
+    for c in (arr_c.items if arr_c is not None else []):
+        out.append((c.out, c.n_cols))
+    if head is not None:
+        sizes = [NC ** 3, NC, NC, 2 * NC * NC, NC, NC * Fd, NC * Fd]   # mep_head_reduce order
+        out += [(int(p), n) for p, n in zip(head, sizes)]
+    return out
+
+
+@pytest.mark.parametrize('family,kw,B,T', CASES)
+def test_gradient_buckets_partition_the_flat_gradient(family, kw, B, T):
+    """The data-parallel exchange all-reduces flat.grad[:split] (bucket A) on a side stream while
+    bucket B's launches still run (engine.py).  Every gradient element must be written by exactly
+    one launch of exactly the bucket whose all-reduce covers it, and nothing outside [0, n_grad)
+    may be written -- else a gradient would be summed before it is final, or never."""
+    from mep_amd import cmu_mosei, ren_mme
+    Tl, Tv, Ta = T
+    if family == 'cmu':
+        m = cmu_mosei.Concat_Trans(kw['dim'], Tl, Tv, Ta, kw['n_heads'], kw['n_layers'], 1)
+    else:
+        m = ren_mme.Base_model(dim=kw['dim'], l_len=Tl, v_len=Tv, a_len=Ta, n_heads=kw['n_heads'],
+                               n_layers=kw['n_layers'])
+    plan = m.mep_runner('cpu').plan(B, T)
+    plan._build_buckets()          # asserts every write range against its bucket (_check_bucket_ranges)
+    (_, wa, _, _), (_, wb, _, _), ca, cb = plan._buckets
+    fl = plan.flat
+    g0 = fl.grad.data_ptr()
+    count = torch.zeros(fl.total, dtype=torch.int32)
+    owner = torch.full((fl.total,), -1, dtype=torch.int32)
+    NC, Fd = plan.spec.NC, plan.F
+    for k, (w, c, head) in enumerate(((wa, ca, plan.head_grads[:-1]), (wb, cb, None))):
+        for ptr, n in _writes(w, c, head, NC, Fd):
+            assert (ptr - g0) % 4 == 0
+            o = (ptr - g0) // 4
+            assert 0 <= o and o + n <= fl.n_grad, (k, o, n, fl.n_grad)
+            count[o:o + n] += 1
+            owner[o:o + n] = k
+    for name in fl.names:
+        o, n = fl.offsets[name], fl.params[name].numel()
+        if not fl.has_grad[name]:
+            assert int(count[o:o + n].sum()) == 0, name
+            continue
+        assert bool((count[o:o + n] == 1).all()), (name, count[o:o + n].min(), count[o:o + n].max())
+        want = 0 if o < fl.split else 1
+        assert bool((owner[o:o + n] == want).all()), (name, 'written by the other bucket')
+    # the same launches, unsplit, write the same elements (backward() without the exchange)
+    full = torch.zeros(fl.total, dtype=torch.int32)
+    for ptr, n in _writes(plan.d_wgrad, plan.d_colsum, plan.head_grads[:-1], NC, Fd):
+        o = (ptr - g0) // 4
+        full[o:o + n] += 1
+    assert torch.equal(full, count)
