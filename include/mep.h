@@ -32,17 +32,25 @@ extern "C" {
 #endif
 
 #define MEP_EINVAL (-1000)
-#define MEP_ABI_VERSION 1
+#define MEP_ABI_VERSION 2
 
 typedef void* mep_stream_t; /* a hipStream_t */
 
 /* Arithmetic precision.  Default (fp32 path): fp32 storage and every product at fp32 level --
  * f32 MFMA, or fp32 operands split into bf16 parts on the bf16 matrix cores (3 parts: fp32-level
  * error).  MEP_PREC_BF16 (bf16 path, BASELINE cfg3/cfg5): the matrix products take plain bf16
- * operands (round-to-nearest of the fp32 values) with fp32 accumulation -- one MFMA per k block
- * -- while storage, softmax, LayerNorm, scores and optimizer state stay fp32.  OR-ed into the
- * `flags` of mep_attn_fwd / mep_attn_bwd and the `D` argument of mep_block_epi_fwd /
- * mep_block_epi_bwd; the `bf16` field of mep_gemm_desc (mep_unify) and mep_wgrad_desc. */
+ * operands with fp32 accumulation -- one MFMA per k block -- and the ACTIVATIONS are stored as
+ * bf16 (what torch.autocast(bfloat16) keeps between ops): the features, the unified rows, the
+ * attention outputs, the epilogue intermediates xp / z and every gradient of those rows (dx, dq,
+ * dk / dv, dz, dxp, the per-modality sums).  Scores, softmax / LayerNorm statistics, the block
+ * outputs the pool reads, loss, parameters, their gradients and the optimizer state stay fp32.
+ * Row views keep counting ELEMENTS (2 bytes for bf16 rows).  OR-ed into the `flags` of
+ * mep_attn_fwd / mep_attn_bwd (q k v x dx dq dk dv bf16) and the `D` argument of
+ * mep_block_epi_fwd / mep_block_epi_bwd (q x xp z dout2 dz dxp dx dq out_h bf16; out, dout
+ * fp32); the `bf16` field of mep_gemm_desc (mep_unify / mep_tgemm) and mep_wgrad_desc take
+ * MEP_BF16_OPS (bf16 operands) | MEP_BF16_STORE (bf16 x / y, or a / b, rows). */
+#define MEP_BF16_OPS 1
+#define MEP_BF16_STORE 2
 #define MEP_PREC_BF16 0x10000
 
 typedef struct {
@@ -231,6 +239,8 @@ typedef struct {
     int32_t  ntok, D;
     float    drop_p;
     int32_t  drop_stream;/* distinct per block */
+    mep_rows out_h;      /* MEP_PREC_BF16: optional bf16 copy of out (ptr 0: none) -- the next
+                            layer's q of a residual chain, whose out stays fp32 for the pool */
 } mep_epi_desc;
 /* D (32/64/96/128, shared by every descriptor of the launch) selects the compiled variant.
  * Geometry: max_tiles = workgroups PER DESCRIPTOR; each workgroup (512 threads) stages its block's
@@ -383,7 +393,7 @@ typedef struct {
     uint64_t w, b, stats, partial;
     int32_t  ntok, D;
     int32_t  dx_accumulate;
-    int32_t  _pad;
+    int32_t  bf16;       /* MEP_BF16_STORE: x, y, dy, dx rows are bf16 (statistics fp32) */
 } mep_ln_desc;
 int mep_layernorm_fwd(const mep_ln_desc* descs, int n_desc, int max_tiles, mep_stream_t stream);
 int mep_layernorm_bwd(const mep_ln_desc* descs, int n_desc, int max_tiles, mep_stream_t stream);
@@ -400,8 +410,10 @@ typedef struct {
 } mep_colsum_desc;
 int mep_colsum(const mep_colsum_desc* descs, int n_desc, int max_tiles, mep_stream_t stream);
 
-/* out = sum_i src_i (up to 16 sources), elementwise over ntok x D rows. */
+/* out = sum_i src_i (up to 16 sources), elementwise over ntok x D rows.  accumulate: bit 0 = add
+ * onto out; MEP_SUM_BF16 = bf16 source and output rows (the bf16 path), summed in fp32. */
 #define MEP_SUM_MAX_SRC 16
+#define MEP_SUM_BF16 2
 typedef struct {
     mep_rows src[MEP_SUM_MAX_SRC];
     mep_rows out;

@@ -71,7 +71,7 @@ class AttnBwdDesc(ctypes.Structure):
 class EpiDesc(ctypes.Structure):
     _fields_ = [('q', Rows), ('x', Rows), ('xp', Rows), ('z', Rows), ('out', Rows),
                 ('wp', u64), ('wm', u64), ('ln_w', u64), ('ln_b', u64), ('stats', u64), ('seed', u64),
-                ('ntok', i32), ('D', i32), ('drop_p', f32), ('drop_stream', i32)]
+                ('ntok', i32), ('D', i32), ('drop_p', f32), ('drop_stream', i32), ('out_h', Rows)]
 
 
 class EpiBwdDesc(ctypes.Structure):
@@ -84,7 +84,7 @@ class EpiBwdDesc(ctypes.Structure):
 class LnDesc(ctypes.Structure):
     _fields_ = [('x', Rows), ('y', Rows), ('dy', Rows), ('dx', Rows), ('w', u64), ('b', u64),
                 ('stats', u64), ('partial', u64), ('ntok', i32), ('D', i32), ('dx_accumulate', i32),
-                ('_pad', i32)]
+                ('bf16', i32)]
 
 
 class ColsumDesc(ctypes.Structure):
@@ -93,6 +93,7 @@ class ColsumDesc(ctypes.Structure):
 
 
 SUM_MAX_SRC = 16
+SUM_BF16 = 2         # MEP_SUM_BF16: mep_sum_desc.accumulate bit, bf16 source / output rows
 ATTN_FOLD_SRC = 8    # csrc/attn.hip FOLD_SRC: sources per sum the attention backward folds
 
 
@@ -150,6 +151,7 @@ def rfw_part_offsets(D, FD):
     return offs, o
 
 
+BF16_OPS, BF16_STORE = 1, 2   # MEP_BF16_OPS / MEP_BF16_STORE: the bf16 fields of the descriptors
 COLSUM_NOT_GRAD = 2   # MEP_COLSUM_NOT_GRAD: a column sum that is not a gradient (left out of the folded norm)
 
 
@@ -418,6 +420,10 @@ def attn_geometry(descs):
     for d in descs:
         ft = max(ft, -(-(d.B * d.H * -(-d.Tq // 64)) // 4))
         bt = max(bt, d.B * d.H)
+    # backward x extent a multiple of 16: the Tk > 64 kernels then put heads 2j, 2j + 1 of a row
+    # on one XCD (csrc/attn.hip head_pair_order); the extra workgroups leave at once
+    if any(d.Tk > 64 for d in descs):
+        bt = -(-bt // 16) * 16
     flags = (ATTN_PREV if _uniform([d.s_prev != 0 for d in descs], 's_prev') else 0) | \
             (ATTN_SOUT if _uniform([d.s_out != 0 for d in descs], 's_out') else 0) | \
             (ATTN_SHORT if any(d.Tk <= 64 for d in descs) else 0) | (ATTN_LONG if any(d.Tk > 64 for d in descs) else 0)

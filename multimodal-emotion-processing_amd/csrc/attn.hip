@@ -83,6 +83,9 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 #ifndef MEP_FWD_LONG_WAVES
 #define MEP_FWD_LONG_WAVES 2   // waves per SIMD of the Tk > 64 forward (hd 16), fp32 split path
 #endif
+#ifndef MEP_ATTN_HEADPAIR
+#define MEP_ATTN_HEADPAIR 1    // Tk > 64 kernels: heads 2j, 2j + 1 of a row on one CU / XCD (64-byte head slices of 128-byte lines)
+#endif
 #ifndef MEP_FWD_LONG_WAVES_BF
 #define MEP_FWD_LONG_WAVES_BF 2   // the same, bf16 path
 #endif
@@ -258,41 +261,53 @@ MEP_DEV bool aligned16(const mep_rows& r) {
 }
 
 // One batch row of a row view as a range-checked buffer (csrc/common.h raw buffer ops): row t,
-// column col at byte t * sT + 4 col.  Rows t >= n lie past the range (every view has sT >= its
-// D used columns), so their loads return 0 and their stores are dropped -- no clamps, no
-// branches, 32-bit offsets.  The base is wave-uniform by construction (one (b, h) per wave or
-// workgroup); readfirstlane makes that provable so the descriptor lives in SGPRs.
-struct BRow {
+// column col at byte t * sT + ES col (ES = 4, or 2 for the bf16 path's bf16 rows, HS).  Rows
+// t >= n lie past the range (every view has sT >= its D used columns), so their loads return 0
+// and their stores are dropped -- no clamps, no branches, 32-bit offsets.  The base is
+// wave-uniform by construction (one (b, h) per wave or workgroup); readfirstlane makes that
+// provable so the descriptor lives in SGPRs.  Values are fp32 in registers either way (bf16 ->
+// fp32 exact; fp32 -> bf16 round to nearest even on stores).
+template <bool HS>
+struct BRowT {
+    static constexpr int ES = HS ? 2 : 4;
     __amdgpu_buffer_rsrc_t rs;
     int sT4;   // row stride in bytes (wave-uniform)
-    bool vec;  // 16-byte loads allowed
+    bool vec;  // 4-element loads as one access (16 bytes fp32, 8 bytes bf16)
     // byte offset of (row t, column col); loads / stores take a per-lane part plus a wave-uniform
     // part (SGPR soffset: whole rows ahead), so row steps cost no vector instructions
-    MEP_DEV int at(int t, int col) const { return t * sT4 + 4 * col; }
+    MEP_DEV int at(int t, int col) const { return t * sT4 + ES * col; }
     MEP_DEV float ld1(int voff, int soff = 0) const {
+        if (HS) return __builtin_bit_cast(float, (unsigned)__builtin_amdgcn_raw_buffer_load_b16(rs, voff, soff, 0) << 16);
         return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, voff, soff, 0));
     }
     MEP_DEV void ld4(float* dst, int voff) const {
-        if (vec) {
+        if (HS && vec) {
+            const u32x2 w = __builtin_bit_cast(u32x2, __builtin_amdgcn_raw_buffer_load_b64(rs, voff, 0, 0));
+            dst[0] = bf_lo(w[0]); dst[1] = bf_hi(w[0]); dst[2] = bf_lo(w[1]); dst[3] = bf_hi(w[1]);
+        } else if (vec) {
             const f32x4 v = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, voff, 0, 0));
             dst[0] = v[0]; dst[1] = v[1]; dst[2] = v[2]; dst[3] = v[3];
         } else {
 #pragma unroll
-            for (int e = 0; e < 4; ++e) dst[e] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, voff + 4 * e, 0, 0));
+            for (int e = 0; e < 4; ++e) dst[e] = ld1(voff + ES * e);
         }
     }
     MEP_DEV void st1(int voff, int soff, float v) const {
-        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), rs, voff, soff, 0);
+        if (HS) __builtin_amdgcn_raw_buffer_store_b16((unsigned short)pk(v, 0.f), rs, voff, soff, 0);
+        else __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), rs, voff, soff, 0);
     }
     MEP_DEV void st4(int voff, f32x4 v) const {
-        if (vec) {
+        if (HS && vec) {
+            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(__attribute__((ext_vector_type(2))) unsigned, u32x2{pk(v[0], v[1]), pk(v[2], v[3])}), rs, voff, 0, 0);
+        } else if (vec) {
             __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rs, voff, 0, 0);
         } else {
 #pragma unroll
-            for (int e = 0; e < 4; ++e) st1(voff + 4 * e, 0, v[e]);
+            for (int e = 0; e < 4; ++e) st1(voff + ES * e, 0, v[e]);
         }
     }
 };
+typedef BRowT<false> BRow;
 
 MEP_DEV __amdgpu_buffer_rsrc_t uniform_rsrc(uint64_t base, int64_t bytes) {
 #ifdef MEP_ATTN_NOLOAD   // timing-only development build: row / stats loads return 0, stores dropped
@@ -304,10 +319,13 @@ MEP_DEV __amdgpu_buffer_rsrc_t uniform_rsrc(uint64_t base, int64_t bytes) {
     return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), 0, n, 0x00020000);
 }
 
-// rows [0, n) of batch row b of a view whose used columns are [0, D)
-MEP_DEV BRow brow(const mep_rows& v, int b, int n, int D) {
-    return BRow{uniform_rsrc(v.ptr + 4ull * (uint64_t)((int64_t)b * v.sB), 4 * ((int64_t)(n - 1) * v.sT + D)),
-                4 * (int)v.sT, aligned16(v)};
+// rows [0, n) of batch row b of a view whose used columns are [0, D) (HS: bf16 elements)
+template <bool HS = false>
+MEP_DEV BRowT<HS> brow(const mep_rows& v, int b, int n, int D) {
+    constexpr int ES = HS ? 2 : 4;
+    const bool vec = HS ? (((v.ptr & 7) == 0) && (v.sB % 4 == 0) && (v.sT % 4 == 0)) : aligned16(v);
+    return BRowT<HS>{uniform_rsrc(v.ptr + (uint64_t)ES * (uint64_t)((int64_t)b * v.sB), (int64_t)ES * ((int64_t)(n - 1) * v.sT + D)),
+                     ES * (int)v.sT, vec};
 }
 
 // ================================================================== forward
@@ -328,7 +346,8 @@ MEP_DEV void attn_fwd_task(const mep_attn_desc& d, int qc, int h, int b, int lan
     gfloat* sout = G<float>(d.s_out);
     const gfloat* mask = G<const float>(d.mask) + (int64_t)b * d.mask_sB;
     const int D = d.H * HDIM;
-    const BRow Qb = brow(d.q, b, Tq, D), Kb = brow(d.k, b, Tk, D), Vb = brow(d.v, b, Tk, D), Xb = brow(d.x, b, Tq, D);
+    const BRowT<BF> Qb = brow<BF>(d.q, b, Tq, D), Kb = brow<BF>(d.k, b, Tk, D), Vb = brow<BF>(d.v, b, Tk, D),
+                    Xb = brow<BF>(d.x, b, Tq, D);
     const int sbase = (b * d.H + h) * Tq;        // row of (b, h, query 0) in [B,H,Tq,Tk]
     const int q_lo = qc * qch;                   // qch: queries per task (64, or 16 with MEP_ATTN_SPLITQ)
     const int nqt = min(qch / 16, (Tq - q_lo + 15) / 16);
@@ -575,6 +594,15 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu((SINGLE
     const int nqc = (d.Tq + QCH - 1) / QCH;   // QCH: queries per wave task (64, or 16 with MEP_ATTN_SPLITQ)
     const int task = blockIdx.x * WAVES + wave;
     if (task >= d.B * d.H * nqc) return;   // whole wave leaves; no barriers below
+    if (!SINGLE && MEP_ATTN_HEADPAIR && !(d.H & 1)) {
+        // Tk > 64: waves 2i and 2i + 1 of a workgroup take the same queries of heads 2j and 2j + 1
+        // of one row, so the 128-byte line of K / V / Q rows each needs half of is fetched once
+        // for both, into the CU they share (head_pair_order below has the backward's reason)
+        const int m = task & 1, r = task >> 1;
+        const int qc = r % nqc, bhp = r / nqc, hp = d.H >> 1;
+        attn_fwd_task<PREV, SOUT, SINGLE, BF, HDIM, QCH>(d, qc, 2 * (bhp % hp) + m, bhp / hp, lane);
+        return;
+    }
     const int qc = task % nqc, bh = task / nqc;
     attn_fwd_task<PREV, SOUT, SINGLE, BF, HDIM, QCH>(d, qc, bh % d.H, bh / d.H, lane);
 }
@@ -606,7 +634,7 @@ struct Bwd {
     float cres;
     const gfloat *sprev, *dsn, *mask;
     gfloat* dsp;
-    BRow Qb, Kb, Vb, Ob, Gb, dQb;
+    BRowT<BF> Qb, Kb, Vb, Ob, Gb, dQb;   // BF: bf16 rows
     __amdgpu_buffer_rsrc_t rsStat;
     bool same_kv;
     int k_lo;
@@ -628,12 +656,12 @@ struct Bwd {
         dsn = G<const float>(bd.ds_next);
         dsp = G<float>(bd.ds_prev);
         mask = G<const float>(d.mask) + (int64_t)b * d.mask_sB;
-        Qb = brow(d.q, b, Tq, D);
-        Kb = brow(d.k, b, Tk, D);
-        Vb = brow(d.v, b, Tk, D);
-        Ob = brow(d.x, b, Tq, D);
-        Gb = brow(bd.dx, b, Tq, D);
-        dQb = brow(bd.dq, b, Tq, D);
+        Qb = brow<BF>(d.q, b, Tq, D);
+        Kb = brow<BF>(d.k, b, Tk, D);
+        Vb = brow<BF>(d.v, b, Tk, D);
+        Ob = brow<BF>(d.x, b, Tq, D);
+        Gb = brow<BF>(bd.dx, b, Tq, D);
+        dQb = brow<BF>(bd.dq, b, Tq, D);
         same_kv = d.k.ptr == d.v.ptr && d.k.sB == d.v.sB && d.k.sT == d.v.sT;
         sbase = (b * d.H + h) * Tq;
         rsStat = uniform_rsrc(d.stats + 8ull * (uint64_t)sbase, 8 * (int64_t)Tq);
@@ -684,7 +712,7 @@ struct Bwd {
     // instead of 22.  Rows past Tq fall outside the row views (no data: the area is zeroed at the
     // wave's start and later holds finite rows of earlier tiles, whose products are masked).
     static constexpr int STG = 4 * 256 + 32;   // floats: Q, dO, O, dQ [16][16], stats [16][2]
-    MEP_DEV bool dma_ok() const { return Qb.vec && Gb.vec && Ob.vec && dQb.vec; }
+    MEP_DEV bool dma_ok() const { return !BF && Qb.vec && Gb.vec && Ob.vec && dQb.vec; }   // fp32 rows only
     MEP_DEV void stage(int qt, float* S) const {
         typedef __attribute__((address_space(3))) void lvoid;
         const int row = qt * 16 + (lane >> 2), col = hc + 4 * (lane & 3);
@@ -1033,7 +1061,7 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(bwd_sho
     }
 #endif
     }
-    const BRow dKb = brow(bd.dk, u.b, u.Tk, bd.f.H * HD), dVb = brow(bd.dv, u.b, u.Tk, bd.f.H * HD);
+    const BRowT<BF> dKb = brow<BF>(bd.dk, u.b, u.Tk, bd.f.H * HD), dVb = brow<BF>(bd.dv, u.b, u.Tk, bd.f.H * HD);
     const int ok_ = dKb.at(4 * u.g, u.hc + u.c), ov_ = dVb.at(4 * u.g, u.hc + u.c);   // keys past Tk: dropped
 #pragma unroll
     for (int kt = 0; kt < NT; ++kt)
@@ -1073,7 +1101,7 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(2))) vo
     const int D = d.H * HD;
     const int nqt = (u.Tq + 15) / 16, nkc = (u.Tk + CH - 1) / CH;
     const int nw = min(WAVES, nqt);          // waves that own query tiles
-    const BRow dKb = brow(bd.dk, u.b, u.Tk, D), dVb = brow(bd.dv, u.b, u.Tk, D);   // keys past Tk: dropped
+    const BRowT<BF> dKb = brow<BF>(bd.dk, u.b, u.Tk, D), dVb = brow<BF>(bd.dv, u.b, u.Tk, D);   // keys past Tk: dropped
     const bool same_out = bd.dk.ptr == bd.dv.ptr && bd.dk.sB == bd.dv.sB && bd.dk.sT == bd.dv.sT;
     float* Tr = lds + wave * TFL;            // inside the R region
     float* R = lds;
@@ -1130,6 +1158,19 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(2))) vo
     }
 }
 
+// (b, h) of workgroup P of a one-workgroup-per-(b, h) launch.  A head's 16 dims are 64 bytes of a
+// row; the HBM / L2 line is 128.  Heads 2i and 2i + 1 of one row go to workgroups P and P + 8,
+// which the round-robin dispatch puts on ONE XCD at about the same time, so the line each of them
+// needs half of is fetched once into that XCD's L2 (both in the plain order they run on different
+// XCDs and each fetches the whole line: 1.87x the algorithmic reads at cfg5).  Needs
+// the x extent (gridDim.x) a multiple of 16 -- the linear workgroup id is x + gridDim.x * y, so
+// its XCD is x mod 8 -- and H even; otherwise the plain order.  A bijection of [0, gridDim.x).
+MEP_DEV int head_pair_order(int P, int H) {
+    if (!MEP_ATTN_HEADPAIR || (gridDim.x & 15) || (H & 1)) return P;
+    const int x = P & 7, j = P >> 3;
+    return ((((j >> 1) << 3) + x) << 1) + (j & 1);
+}
+
 // WIDE (64 < Tk <= 64 * MEP_ATTN_MAX_KCHUNKS): one WORKGROUP per (b, h) and one WAVE per 64-key
 // chunk (blockDim = 64 x the launch's largest chunk count).  A wave keeps its chunk's K / V rows
 // and its dK / dV accumulators in registers for the whole kernel and walks every query tile, so
@@ -1146,7 +1187,7 @@ void k_attn_bwd_wide(const mep_attn_bwd_desc* __restrict__ descs) {
     typedef Bwd<PREV, DSN, BF, KV> U;
     const mep_attn_bwd_desc& bd = descs[blockIdx.y];
     const mep_attn_desc& d = bd.f;
-    const int bh = blockIdx.x;
+    const int bh = head_pair_order(blockIdx.x, d.H);
     if (d.Tk <= CH || bh >= d.B * d.H) return;   // a SHORT descriptor / past the end: the whole workgroup
     const int nwv = blockDim.x >> 6;             // waves = the launch's largest chunk count
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -1199,7 +1240,7 @@ void k_attn_bwd_wide(const mep_attn_bwd_desc* __restrict__ descs) {
         }
     }
     if (!active) return;
-    const BRow dKb = brow(bd.dk, u.b, u.Tk, D), dVb = brow(bd.dv, u.b, u.Tk, D);   // keys past Tk: dropped
+    const BRowT<BF> dKb = brow<BF>(bd.dk, u.b, u.Tk, D), dVb = brow<BF>(bd.dv, u.b, u.Tk, D);   // keys past Tk: dropped
     const int ok_ = dKb.at(u.k_lo + 4 * u.g, u.hc + u.c), ov_ = dVb.at(u.k_lo + 4 * u.g, u.hc + u.c);
 #pragma unroll
     for (int kt = 0; kt < NT; ++kt)
@@ -1330,3 +1371,14 @@ extern "C" int mep_attn_bwd(const mep_attn_bwd_desc* descs, int n_desc, int max_
     }
     return mep_check_launch("mep_attn_bwd");
 }
+
+// hipcc (ROCm 7.2) leaves the host stubs of k_attn_bwd_wide undefined when they are only named
+// inside mep_attn_bwd's launch macros (the device code is emitted); instantiating them explicitly
+// here emits them
+namespace {
+#define MEP_BWI(P, S, B, K) template __global__ void k_attn_bwd_wide<P, S, B, K>(const mep_attn_bwd_desc* __restrict__);
+#define MEP_BWI2(P, S) MEP_BWI(P, S, false, false) MEP_BWI(P, S, false, true) MEP_BWI(P, S, true, false) MEP_BWI(P, S, true, true)
+MEP_BWI2(false, false) MEP_BWI2(false, true) MEP_BWI2(true, false) MEP_BWI2(true, true)
+#undef MEP_BWI2
+#undef MEP_BWI
+}  // namespace

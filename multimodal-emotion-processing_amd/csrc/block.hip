@@ -334,6 +334,7 @@ MEP_DEV void epi_fwd_split(const mep_epi_desc& d, unsigned char* sm, int t_begin
     using WP = SplitW<D, NP, NW>;
     using WM = SplitW<D, 2 * NP, NW>;
     using Op = OpN<NPART>;
+    constexpr bool HS = NPART == 1;      // bf16 path: bf16 activations (common.h ld4a / st4a)
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int c = lane & 15, g = lane >> 4;
     const int ntok = d.ntok;
@@ -347,9 +348,9 @@ MEP_DEV void epi_fwd_split(const mep_epi_desc& d, unsigned char* sm, int t_begin
     const WM wm{(lbyte*)sm, 0};
     f32x4 ab[KB], bb[KB];            // one tile ahead: phase 1 x rows; phase 2 q and xp rows
     auto rows_of = [&](const mep_rows& v, int tile, f32x4 (&dst)[KB]) {
-        const gfloat* r = row_ptr(v, min(tile * 16 + c, ntok - 1)) + 4 * g;
+        const auto r = rowa<HS>(v, min(tile * 16 + c, ntok - 1)) + 4 * g;
 #pragma unroll
-        for (int kb = 0; kb < KB; ++kb) dst[kb] = ld4w(r + 16 * kb);
+        for (int kb = 0; kb < KB; ++kb) dst[kb] = ld4a(r + 16 * kb);
     };
     // ---- phase 1: xp = drop(x Wp^T)
     MEP_EPI_STAMP(0);
@@ -368,7 +369,7 @@ MEP_DEV void epi_fwd_split(const mep_epi_desc& d, unsigned char* sm, int t_begin
         for (int i = 0; i < NI; ++i) xp[i] = zero_f4();
         tgemm_n<NI, NP, NPART, NW>(xp, [&](int i, int pp) { return wp.frag(i, pp); }, [&](int pp) { return xs[pp]; });
         if (tok < ntok) {
-            gfloat* pr = row_ptr(d.xp, tok);
+            const auto pr = rowa<HS>(d.xp, tok);
 #pragma unroll
             for (int i = 0; i < NI; ++i) {
                 if (p > 0.f) {
@@ -376,7 +377,7 @@ MEP_DEV void epi_fwd_split(const mep_epi_desc& d, unsigned char* sm, int t_begin
                     for (int r = 0; r < 4; ++r)
                         xp[i][r] *= drop_scale(seed, 2u * d.drop_stream, (tok0 + (uint64_t)tok) * D + 16 * i + 4 * g + r, p);
                 }
-                stg4(pr + 16 * i + 4 * g, f4(xp[i]));
+                st4a(pr + 16 * i + 4 * g, xp[i]);
             }
         }
     }
@@ -414,8 +415,9 @@ MEP_DEV void epi_fwd_split(const mep_epi_desc& d, unsigned char* sm, int t_begin
         var += __shfl_xor(var, 32, 64);
         const float rstd = 1.0f / sqrtf(var / (float)D + LN_EPS);
         if (tok < ntok) {
-            gfloat* zr = row_ptr(d.z, tok);
+            const auto zr = rowa<HS>(d.z, tok);
             gfloat* orow = row_ptr(d.out, tok);
+            const auto hrow = (HS && d.out_h.ptr) ? rowa<true>(d.out_h, tok) : nullptr;   // next layer's q
 #pragma unroll
             for (int i = 0; i < NI; ++i) {
                 const int col = 16 * i + 4 * g;
@@ -426,8 +428,9 @@ MEP_DEV void epi_fwd_split(const mep_epi_desc& d, unsigned char* sm, int t_begin
                     y[r] = (z[i][r] - mean) * rstd * w[r] + b[r];
                     if (p > 0.f) y[r] *= drop_scale(seed, 2u * d.drop_stream + 1u, (tok0 + (uint64_t)tok) * D + col + r, p);
                 }
-                stg4(zr + col, f4(z[i]));
+                st4a(zr + col, z[i]);
                 stg4(orow + col, f4(y));
+                if (HS && d.out_h.ptr) st4a(hrow + col, y);
             }
             if (g == 0) { stats[2 * tok] = mean; stats[2 * tok + 1] = rstd; }
         }
@@ -445,6 +448,7 @@ MEP_DEV void epi_bwd_split(const mep_epi_bwd_desc& bd, unsigned char* sm, int t_
     using WMT = SplitW<2 * D, NP, NW>;
     using WPT = SplitW<D, NP, NW>;
     using Op = OpN<NPART>;
+    constexpr bool HS = NPART == 1;      // bf16 path: bf16 activations and their gradients
     const mep_epi_desc& d = bd.f;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int c = lane & 15, g = lane >> 4;
@@ -464,11 +468,11 @@ MEP_DEV void epi_bwd_split(const mep_epi_bwd_desc& bd, unsigned char* sm, int t_
     const Upstream up(bd);
     auto fetch1 = [&](int tile) {
         const int tc = min(tile * 16 + c, ntok - 1);
-        const gfloat* zr = row_ptr(d.z, tc) + 4 * g;
+        const auto zr = rowa<HS>(d.z, tc) + 4 * g;
 #pragma unroll
         for (int kb = 0; kb < KB; ++kb) ga[kb] = up.at(bd, tc, 16 * kb + 4 * g);
 #pragma unroll
-        for (int kb = 0; kb < KB; ++kb) zb[kb] = ld4w(zr + 16 * kb);
+        for (int kb = 0; kb < KB; ++kb) zb[kb] = ld4a(zr + 16 * kb);
         mean = stats[2 * tc];
         rstd = stats[2 * tc + 1];
     };
@@ -485,9 +489,9 @@ MEP_DEV void epi_bwd_split(const mep_epi_bwd_desc& bd, unsigned char* sm, int t_
 #pragma unroll
         for (int i = 0; i < NI; ++i) { dz[i] = ga[i]; zz[i] = zb[i]; }
         if (bd.dout2.ptr) {
-            const gfloat* g2 = row_ptr(bd.dout2, tc) + 4 * g;
+            const auto g2 = rowa<HS>(bd.dout2, tc) + 4 * g;
 #pragma unroll
-            for (int i = 0; i < NI; ++i) dz[i] += ld4w(g2 + 16 * i);
+            for (int i = 0; i < NI; ++i) dz[i] += ld4a(g2 + 16 * i);
         }
         if (tile + EWAVES < t_end) fetch1(tile + EWAVES);
         float s1 = 0.f, s2 = 0.f;
@@ -536,8 +540,8 @@ MEP_DEV void epi_bwd_split(const mep_epi_bwd_desc& bd, unsigned char* sm, int t_
         for (int i = 0; i < NI; ++i) acc[i] = zero_f4();
         tgemm_n<NI, NP, NPART, NW>(acc, [&](int i, int pp) { return wmt_x.frag(i, pp); }, [&](int pp) { return dzb[pp]; });
         if (ok) {
-            gfloat* dzr = row_ptr(bd.dz, tok);
-            gfloat* dpr = row_ptr(bd.dxp, tok);
+            const auto dzr = rowa<HS>(bd.dz, tok);
+            const auto dpr = rowa<HS>(bd.dxp, tok);
 #pragma unroll
             for (int i = 0; i < NI; ++i) {
                 if (p > 0.f) {
@@ -545,29 +549,29 @@ MEP_DEV void epi_bwd_split(const mep_epi_bwd_desc& bd, unsigned char* sm, int t_
                     for (int r = 0; r < 4; ++r)
                         acc[i][r] *= drop_scale(seed, 2u * d.drop_stream, (tok0 + (uint64_t)tok) * D + 16 * i + 4 * g + r, p);
                 }
-                stg4(dzr + 16 * i + 4 * g, f4(dz[i]));
-                stg4(dpr + 16 * i + 4 * g, f4(acc[i]));
+                st4a(dzr + 16 * i + 4 * g, dz[i]);
+                st4a(dpr + 16 * i + 4 * g, acc[i]);
             }
         }
 #pragma unroll
         for (int i = 0; i < NI; ++i) acc[i] = zero_f4();
         tgemm_n<NI, NP, NPART, NW>(acc, [&](int i, int pp) { return wmt.frag(i, pp); }, [&](int pp) { return dzb[pp]; });
         if (ok) {
-            gfloat* qrw = row_ptr(bd.dq, tok);
+            const auto qrw = rowa<HS>(bd.dq, tok);
 #pragma unroll
             for (int i = 0; i < NI; ++i) {
                 f32x4 v = acc[i];
-                if (bd.dq_accumulate) v += ld4w(qrw + 16 * i + 4 * g);
-                stg4(qrw + 16 * i + 4 * g, f4(v));
+                if (bd.dq_accumulate) v += ld4a(qrw + 16 * i + 4 * g);
+                st4a(qrw + 16 * i + 4 * g, v);
             }
         }
     }
     // ---- phase 2: dx = dxp Wp (this workgroup's own dxp rows, L2-hot)
     wg_store_barrier();
     auto fetch2 = [&](int tile) {
-        const gfloat* r = row_ptr(bd.dxp, min(tile * 16 + c, ntok - 1)) + 4 * g;
+        const auto r = rowa<HS>(bd.dxp, min(tile * 16 + c, ntok - 1)) + 4 * g;
 #pragma unroll
-        for (int kb = 0; kb < KB; ++kb) ga[kb] = ld4w(r + 16 * kb);
+        for (int kb = 0; kb < KB; ++kb) ga[kb] = ld4a(r + 16 * kb);
     };
     if (t_begin + wave < t_end) fetch2(t_begin + wave);
     stage_split_cols<D, D, NW>(wpt, G<const float>(d.wp));
@@ -583,9 +587,9 @@ MEP_DEV void epi_bwd_split(const mep_epi_bwd_desc& bd, unsigned char* sm, int t_
         for (int i = 0; i < NI; ++i) acc[i] = zero_f4();
         tgemm_n<NI, NP, NPART, NW>(acc, [&](int i, int pp) { return wpt.frag(i, pp); }, [&](int pp) { return xs[pp]; });
         if (tok < ntok) {
-            gfloat* xrw = row_ptr(bd.dx, tok);
+            const auto xrw = rowa<HS>(bd.dx, tok);
 #pragma unroll
-            for (int i = 0; i < NI; ++i) stg4(xrw + 16 * i + 4 * g, f4(acc[i]));
+            for (int i = 0; i < NI; ++i) st4a(xrw + 16 * i + 4 * g, acc[i]);
         }
     }
 }
@@ -603,6 +607,7 @@ MEP_DEV void epi_fwd_one(const mep_epi_desc& d, unsigned char* sm, int t_begin, 
     constexpr int NI = D / 16, KB = D / 16, NP = D / 32;
     using WP = SplitW<D, NP, NWP>;
     using WM = SplitW<D, 2 * NP, NWM>;
+    constexpr bool HS = NPART == 1;      // bf16 path: bf16 activations (common.h ld4a / st4a)
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int c = lane & 15, g = lane >> 4;
     const int ntok = d.ntok;
@@ -615,9 +620,9 @@ MEP_DEV void epi_fwd_one(const mep_epi_desc& d, unsigned char* sm, int t_begin, 
     const WM wm{(lbyte*)sm + WP::BYTES, 0};
     f32x4 ab[KB], bb[KB];            // one tile ahead: x and q rows
     auto rows_of = [&](const mep_rows& v, int tile, f32x4 (&dst)[KB]) {
-        const gfloat* r = row_ptr(v, min(tile * 16 + c, ntok - 1)) + 4 * g;
+        const auto r = rowa<HS>(v, min(tile * 16 + c, ntok - 1)) + 4 * g;
 #pragma unroll
-        for (int kb = 0; kb < KB; ++kb) dst[kb] = ld4w(r + 16 * kb);
+        for (int kb = 0; kb < KB; ++kb) dst[kb] = ld4a(r + 16 * kb);
     };
     if (t_begin + wave < t_end) { rows_of(d.x, t_begin + wave, ab); rows_of(d.q, t_begin + wave, bb); }
     stage_split_rows<D, D, NWP>(wp, G<const float>(d.wp));
@@ -666,9 +671,10 @@ MEP_DEV void epi_fwd_one(const mep_epi_desc& d, unsigned char* sm, int t_begin, 
         var += __shfl_xor(var, 32, 64);
         const float rstd = 1.0f / sqrtf(var / (float)D + LN_EPS);
         if (tok < ntok) {
-            gfloat* zr = row_ptr(d.z, tok);
+            const auto zr = rowa<HS>(d.z, tok);
             gfloat* orow = row_ptr(d.out, tok);
-            gfloat* pr = row_ptr(d.xp, tok);
+            const auto pr = rowa<HS>(d.xp, tok);
+            const auto hrow = (HS && d.out_h.ptr) ? rowa<true>(d.out_h, tok) : nullptr;   // next layer's q
 #pragma unroll
             for (int i = 0; i < NI; ++i) {
                 const int col = 16 * i + 4 * g;
@@ -679,9 +685,10 @@ MEP_DEV void epi_fwd_one(const mep_epi_desc& d, unsigned char* sm, int t_begin, 
                     y[r] = (z[i][r] - mean) * rstd * w[r] + b[r];
                     if (p > 0.f) y[r] *= drop_scale(seed, 2u * d.drop_stream + 1u, (tok0 + (uint64_t)tok) * D + col + r, p);
                 }
-                stg4(pr + col, f4(xp[i]));
-                stg4(zr + col, f4(z[i]));
+                st4a(pr + col, xp[i]);
+                st4a(zr + col, z[i]);
                 stg4(orow + col, f4(y));
+                if (HS && d.out_h.ptr) st4a(hrow + col, y);
             }
             if (g == 0) { stats[2 * tok] = mean; stats[2 * tok + 1] = rstd; }
         }
@@ -694,6 +701,7 @@ MEP_DEV void epi_bwd_one(const mep_epi_bwd_desc& bd, unsigned char* sm, int t_be
     using WMT = SplitW<2 * D, NP, NWM>;
     using WPT = SplitW<D, NP, NWP>;
     using Op = OpN<NPART>;
+    constexpr bool HS = NPART == 1;      // bf16 path: bf16 activations and their gradients
     const mep_epi_desc& d = bd.f;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int c = lane & 15, g = lane >> 4;
@@ -712,11 +720,11 @@ MEP_DEV void epi_bwd_one(const mep_epi_bwd_desc& bd, unsigned char* sm, int t_be
     const Upstream up(bd);
     auto fetch1 = [&](int tile) {
         const int tc = min(tile * 16 + c, ntok - 1);
-        const gfloat* zr = row_ptr(d.z, tc) + 4 * g;
+        const auto zr = rowa<HS>(d.z, tc) + 4 * g;
 #pragma unroll
         for (int kb = 0; kb < KB; ++kb) ga[kb] = up.at(bd, tc, 16 * kb + 4 * g);
 #pragma unroll
-        for (int kb = 0; kb < KB; ++kb) zb[kb] = ld4w(zr + 16 * kb);
+        for (int kb = 0; kb < KB; ++kb) zb[kb] = ld4a(zr + 16 * kb);
         mean = stats[2 * tc];
         rstd = stats[2 * tc + 1];
     };
@@ -733,9 +741,9 @@ MEP_DEV void epi_bwd_one(const mep_epi_bwd_desc& bd, unsigned char* sm, int t_be
 #pragma unroll
         for (int i = 0; i < NI; ++i) { dz[i] = ga[i]; zz[i] = zb[i]; }
         if (bd.dout2.ptr) {
-            const gfloat* g2 = row_ptr(bd.dout2, tc) + 4 * g;
+            const auto g2 = rowa<HS>(bd.dout2, tc) + 4 * g;
 #pragma unroll
-            for (int i = 0; i < NI; ++i) dz[i] += ld4w(g2 + 16 * i);
+            for (int i = 0; i < NI; ++i) dz[i] += ld4a(g2 + 16 * i);
         }
         if (tile + EWAVES < t_end) fetch1(tile + EWAVES);
         float s1 = 0.f, s2 = 0.f;
@@ -795,33 +803,33 @@ MEP_DEV void epi_bwd_one(const mep_epi_bwd_desc& bd, unsigned char* sm, int t_be
 #pragma unroll
         for (int pp = 0; pp < NP; ++pp) xs[pp] = opn<NPART>(acc[2 * pp], acc[2 * pp + 1]);
         if (ok) {
-            gfloat* dzr = row_ptr(bd.dz, tok);
-            gfloat* dpr = row_ptr(bd.dxp, tok);
+            const auto dzr = rowa<HS>(bd.dz, tok);
+            const auto dpr = rowa<HS>(bd.dxp, tok);
 #pragma unroll
             for (int i = 0; i < NI; ++i) {
-                stg4(dzr + 16 * i + 4 * g, f4(dz[i]));
-                stg4(dpr + 16 * i + 4 * g, f4(acc[i]));
+                st4a(dzr + 16 * i + 4 * g, dz[i]);
+                st4a(dpr + 16 * i + 4 * g, acc[i]);
             }
         }
 #pragma unroll
         for (int i = 0; i < NI; ++i) acc[i] = zero_f4();
         tgemm_n<NI, NP, NPART, NWM>(acc, [&](int i, int pp) { return wmt.frag(i, pp); }, [&](int pp) { return dzb[pp]; });
         if (ok) {
-            gfloat* qrw = row_ptr(bd.dq, tok);
+            const auto qrw = rowa<HS>(bd.dq, tok);
 #pragma unroll
             for (int i = 0; i < NI; ++i) {
                 f32x4 v = acc[i];
-                if (bd.dq_accumulate) v += ld4w(qrw + 16 * i + 4 * g);
-                stg4(qrw + 16 * i + 4 * g, f4(v));
+                if (bd.dq_accumulate) v += ld4a(qrw + 16 * i + 4 * g);
+                st4a(qrw + 16 * i + 4 * g, v);
             }
         }
 #pragma unroll
         for (int i = 0; i < NI; ++i) acc[i] = zero_f4();
         tgemm_n<NI, NP, NPART, NWP>(acc, [&](int i, int pp) { return wpt.frag(i, pp); }, [&](int pp) { return xs[pp]; });
         if (ok) {
-            gfloat* xrw = row_ptr(bd.dx, tok);
+            const auto xrw = rowa<HS>(bd.dx, tok);
 #pragma unroll
-            for (int i = 0; i < NI; ++i) stg4(xrw + 16 * i + 4 * g, f4(acc[i]));
+            for (int i = 0; i < NI; ++i) st4a(xrw + 16 * i + 4 * g, acc[i]);
         }
     }
 }
@@ -1047,8 +1055,9 @@ __global__ __launch_bounds__(ETHREADS) __attribute__((amdgpu_waves_per_eu(MEP_EP
 // branches); each row's arithmetic is unchanged.  Host grids stay ceil(ntok / 4) "tiles"; the
 // launcher runs ceil(tiles / LNF_ROWS) workgroups.
 constexpr int LNF_ROWS = 4;
-__global__ __launch_bounds__(256) void k_ln_fwd(const mep_ln_desc* __restrict__ descs) {
-    const mep_ln_desc& d = descs[blockIdx.y];
+// HS: bf16 x / y rows (mep_ln_desc.bf16 = MEP_BF16_STORE, the bf16 path); statistics stay fp32
+template <bool HS>
+MEP_DEV void ln_fwd_rows(const mep_ln_desc& d) {
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int tok0 = blockIdx.x * 4 * LNF_ROWS + wave;
     if (tok0 >= d.ntok) return;
@@ -1063,9 +1072,9 @@ __global__ __launch_bounds__(256) void k_ln_fwd(const mep_ln_desc* __restrict__ 
     }
 #pragma unroll
     for (int i = 0; i < LNF_ROWS; ++i) {
-        const gfloat* x = row_ptr(d.x, min(tok0 + 4 * i, d.ntok - 1));
+        const auto x = rowa<HS>(d.x, min(tok0 + 4 * i, d.ntok - 1));
 #pragma unroll
-        for (int j = 0; j < 4; ++j) v[i][j] = x[min(lane + 64 * j, d.D - 1)];
+        for (int j = 0; j < 4; ++j) v[i][j] = ld1a(x + min(lane + 64 * j, d.D - 1));
     }
 #pragma unroll
     for (int i = 0; i < LNF_ROWS; ++i) {
@@ -1079,9 +1088,9 @@ __global__ __launch_bounds__(256) void k_ln_fwd(const mep_ln_desc* __restrict__ 
 #pragma unroll
         for (int j = 0; j < 4; ++j) { const int c = lane + 64 * j; v[i][j] = c < d.D ? v[i][j] - mean : 0.f; q += v[i][j] * v[i][j]; }
         const float rstd = 1.0f / sqrtf(wave_sum(q) / (float)d.D + LN_EPS);
-        gfloat* y = row_ptr(d.y, tok);
+        const auto y = rowa<HS>(d.y, tok);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) { const int c = lane + 64 * j; if (c < d.D) y[c] = v[i][j] * rstd * wv[j] + bv[j]; }
+        for (int j = 0; j < 4; ++j) { const int c = lane + 64 * j; if (c < d.D) st1a(y + c, v[i][j] * rstd * wv[j] + bv[j]); }
         if (lane == 0) {
             gfloat* st = G<float>(d.stats);
             st[2 * tok] = mean;
@@ -1090,13 +1099,19 @@ __global__ __launch_bounds__(256) void k_ln_fwd(const mep_ln_desc* __restrict__ 
     }
 }
 
+__global__ __launch_bounds__(256) void k_ln_fwd(const mep_ln_desc* __restrict__ descs) {
+    const mep_ln_desc& d = descs[blockIdx.y];
+    if (d.bf16 & MEP_BF16_STORE) ln_fwd_rows<true>(d);
+    else ln_fwd_rows<false>(d);
+}
+
 // backward; partial[blockIdx.x][2][D] = per-workgroup (dgamma, dbeta) over its 64 rows.  A wave
 // takes rows wave, wave + 4, ... in batches of LNB_ROWS: every load of a batch (clamped columns and
 // tokens, no branches) is issued before the batch's arithmetic, which runs row by row in the same
 // order as one row at a time (bit-identical sums).
 constexpr int LNB_ROWS = 4;
-__global__ __launch_bounds__(256) void k_ln_bwd(const mep_ln_desc* __restrict__ descs) {
-    const mep_ln_desc& d = descs[blockIdx.y];
+template <bool HS>
+MEP_DEV void ln_bwd_rows(const mep_ln_desc& d) {
     const int tok0 = blockIdx.x * 64;
     if (tok0 >= d.ntok) return;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -1114,13 +1129,13 @@ __global__ __launch_bounds__(256) void k_ln_bwd(const mep_ln_desc* __restrict__ 
             const int tk = min(tok0 + r0 + 4 * i, d.ntok - 1);
             mean[i] = st[2 * tk];
             rstd[i] = st[2 * tk + 1];
-            const gfloat* x = row_ptr(d.x, tk);
-            const gfloat* dy = row_ptr(d.dy, tk);
+            const auto x = rowa<HS>(d.x, tk);
+            const auto dy = rowa<HS>(d.dy, tk);
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
                 const int c = min(lane + 64 * j, d.D - 1);
-                gv[i][j] = dy[c];
-                xv[i][j] = x[c];
+                gv[i][j] = ld1a(dy + c);
+                xv[i][j] = ld1a(x + c);
             }
         }
 #pragma unroll
@@ -1141,13 +1156,13 @@ __global__ __launch_bounds__(256) void k_ln_bwd(const mep_ln_desc* __restrict__ 
             }
             s1 = wave_sum(s1) / (float)d.D;
             s2 = wave_sum(s2) / (float)d.D;
-            gfloat* dx = row_ptr(d.dx, tok);
+            const auto dx = rowa<HS>(d.dx, tok);
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
                 const int c = lane + 64 * j;
                 if (c < d.D) {
                     const float v = rstd[i] * (gw[j] - s1 - xh[j] * s2);
-                    dx[c] = d.dx_accumulate ? dx[c] + v : v;
+                    st1a(dx + c, d.dx_accumulate ? ld1a(dx + c) + v : v);
                 }
             }
         }
@@ -1162,6 +1177,12 @@ __global__ __launch_bounds__(256) void k_ln_bwd(const mep_ln_desc* __restrict__ 
             lp[idx] = red[0][which][c] + red[1][which][c] + red[2][which][c] + red[3][which][c];
         }
     }
+}
+
+__global__ __launch_bounds__(256) void k_ln_bwd(const mep_ln_desc* __restrict__ descs) {
+    const mep_ln_desc& d = descs[blockIdx.y];
+    if (d.bf16 & MEP_BF16_STORE) ln_bwd_rows<true>(d);
+    else ln_bwd_rows<false>(d);
 }
 
 template <typename F>

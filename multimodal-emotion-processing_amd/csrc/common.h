@@ -29,6 +29,39 @@ MEP_DEV void stg4(gfloat* p, float4 v) { *reinterpret_cast<MEP_G f32x4*>(p) = f3
 
 constexpr int kWave = 64;
 
+// ------------------------------------------------------------------ activation storage
+// Activations of the bf16 path (MEP_PREC_BF16 plans: features, unified rows, attention outputs,
+// epilogue intermediates and their gradients) are stored as bf16, everything else (block outputs,
+// scores, statistics, parameters and their gradients) as fp32.  Row views count elements, so
+// the same mep_rows addresses either; HS (half storage) selects the element type at compile time.
+// 4 consecutive elements are one 16-byte (fp32) or 8-byte (bf16) access; bf16 -> fp32 is exact,
+// fp32 -> bf16 rounds to nearest even (v_cvt_pk_bf16_f32).
+typedef MEP_G unsigned short ghalf;
+typedef unsigned u32x2a __attribute__((ext_vector_type(2)));
+template <bool HS> struct AElem { typedef float T; };
+template <> struct AElem<true> { typedef unsigned short T; };
+template <bool HS> using aelem = MEP_G typename AElem<HS>::T;
+MEP_DEV unsigned pk_bf16x2(float a, float b) {
+    typedef float f2 __attribute__((ext_vector_type(2)));
+    typedef __bf16 b2 __attribute__((ext_vector_type(2)));
+    return __builtin_bit_cast(unsigned, __builtin_convertvector(f2{a, b}, b2));
+}
+MEP_DEV float bf16_word_lo(unsigned w) { return __builtin_bit_cast(float, w << 16); }
+MEP_DEV float bf16_word_hi(unsigned w) { return __builtin_bit_cast(float, w & 0xffff0000u); }
+MEP_DEV f32x4 ld4a(const gfloat* p) { return *reinterpret_cast<const MEP_G f32x4*>(p); }
+MEP_DEV f32x4 ld4a(const ghalf* p) {
+    const u32x2a w = *reinterpret_cast<const MEP_G u32x2a*>(p);
+    return f32x4{bf16_word_lo(w[0]), bf16_word_hi(w[0]), bf16_word_lo(w[1]), bf16_word_hi(w[1])};
+}
+MEP_DEV void st4a(gfloat* p, f32x4 v) { *reinterpret_cast<MEP_G f32x4*>(p) = v; }
+MEP_DEV void st4a(ghalf* p, f32x4 v) {
+    *reinterpret_cast<MEP_G u32x2a*>(p) = u32x2a{pk_bf16x2(v[0], v[1]), pk_bf16x2(v[2], v[3])};
+}
+MEP_DEV float ld1a(const gfloat* p) { return *p; }
+MEP_DEV float ld1a(const ghalf* p) { return __builtin_bit_cast(float, (unsigned)*p << 16); }
+MEP_DEV void st1a(gfloat* p, float v) { *p = v; }
+MEP_DEV void st1a(ghalf* p, float v) { *p = (unsigned short)pk_bf16x2(v, 0.f); }
+
 // ------------------------------------------------------------------ row views
 // tok -> (b, t) = (tok / T, tok % T) without an integer division: the quotient from the f32
 // reciprocal (v_rcp_f32, 1 ulp) is off by at most one for tok < 2^22 (relative error of the
@@ -43,6 +76,11 @@ MEP_DEV int64_t row_off(const mep_rows& r, int tok) {
     return (int64_t)b * r.sB + (int64_t)t * r.sT;
 }
 MEP_DEV gfloat* row_ptr(const mep_rows& r, int tok) { return G<float>(r.ptr) + row_off(r, tok); }
+// row of an activation view in HS storage (element pointer: ld4a / st4a / ld1a / st1a)
+template <bool HS>
+MEP_DEV aelem<HS>* rowa(const mep_rows& r, int tok) {
+    return reinterpret_cast<aelem<HS>*>(r.ptr) + row_off(r, tok);
+}
 
 // ------------------------------------------------------------------ exact-rounding scalar ops
 // The residual-score sequence of the reference ((q.k)/sqrt(d) + c*S_prev - 1e8*(1-m)) is

@@ -191,14 +191,14 @@ __host__ __device__ constexpr int wg_kt(int mt, bool bf) {
     return mt == 4 ? 2 : mt == 3 ? 3 : 4;
 }
 
-// byte extent of a row view's first ntok rows, `width` columns wide (the range the raw buffer
-// loads check; hosts keep it under 2^31)
-MEP_DEV int wg_extent(const mep_rows& r, int T, int ntok, int width) {
+// byte extent of a row view's first ntok rows, `width` columns wide, es bytes per element (the
+// range the raw buffer loads check; hosts keep it under 2^31)
+MEP_DEV int wg_extent(const mep_rows& r, int T, int ntok, int width, int es = 4) {
 #ifdef MEP_WG_NOLOAD   // timing-only development build: every operand load returns 0 (compute time alone)
     return 0;
 #endif
     const int64_t last = (int64_t)((ntok - 1) / T) * r.sB + (int64_t)((ntok - 1) % T) * r.sT + width;
-    return (int)min((int64_t)4 * last, (int64_t)0x7fffffff);
+    return (int)min((int64_t)es * last, (int64_t)0x7fffffff);
 }
 
 constexpr int WG_INV = (int)0x80000000u;   // byte offset past every view: the buffer load returns 0
@@ -225,6 +225,13 @@ MEP_DEV void wg_stamp(int k, unsigned long long v) {
 // (the load's SGPR soffset) and the column tile an immediate: no address arithmetic per token.
 template <int MT, int KT, int NPART, bool LIN, int WG_SLOTS>
 MEP_DEV void wgrad_task(const mep_wgrad_desc& d, int t_begin, int t_end, int slot, int kbase, lfloat* red) {
+    // the bf16 path (one part) reads bf16 operand rows (MEP_BF16_STORE): 2-byte elements
+    constexpr bool HS = NPART == 1;
+    constexpr int ES = HS ? 2 : 4;
+    auto ld = [&](__amdgpu_buffer_rsrc_t rs, int voff, int soff) -> float {
+        if (HS) return __builtin_bit_cast(float, (unsigned)__builtin_amdgcn_raw_buffer_load_b16(rs, voff, soff, 0) << 16);
+        return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, voff, soff, 0));
+    };
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int c = lane & 31, h = lane >> 5;
     const int N = d.N;
@@ -240,10 +247,10 @@ MEP_DEV void wgrad_task(const mep_wgrad_desc& d, int t_begin, int t_end, int slo
     // Operand columns of this lane, clamped in range: a column past N (past Ktot) only feeds
     // output rows (columns) that are never stored.  Tokens past the lane half's range read 0
     // through the buffer range check (offset WG_INV).
-    const auto rsA = __builtin_amdgcn_make_buffer_rsrc((void*)d.a.ptr, 0, wg_extent(d.a, T, d.ntok, N), 0x00020000);
+    const auto rsA = __builtin_amdgcn_make_buffer_rsrc((void*)d.a.ptr, 0, wg_extent(d.a, T, d.ntok, N, ES), 0x00020000);
     int colA[MT];
 #pragma unroll
-    for (int i = 0; i < MT; ++i) colA[i] = 4 * min(32 * i + c, N - 1);
+    for (int i = 0; i < MT; ++i) colA[i] = ES * min(32 * i + c, N - 1);
     const int asB = (int)d.a.sB, asT = (int)d.a.sT;
     __amdgpu_buffer_rsrc_t rsB[KT];
     int colB[KT], bsB[KT], bsT[KT];
@@ -253,8 +260,8 @@ MEP_DEV void wgrad_task(const mep_wgrad_desc& d, int t_begin, int t_end, int slo
         int k0 = min(kbase + 32 * j, d.Ktot - 1), o = 0;
         while (o < d.n_b - 1 && k0 >= d.kb[o]) { k0 -= d.kb[o]; ++o; }
         const mep_rows& b = d.b[o];
-        rsB[j] = __builtin_amdgcn_make_buffer_rsrc((void*)b.ptr, 0, wg_extent(b, T, d.ntok, d.kb[o]), 0x00020000);
-        colB[j] = 4 * min(k0 + c, d.kb[o] - 1);
+        rsB[j] = __builtin_amdgcn_make_buffer_rsrc((void*)b.ptr, 0, wg_extent(b, T, d.ntok, d.kb[o], ES), 0x00020000);
+        colB[j] = ES * min(k0 + c, d.kb[o] - 1);
         bsB[j] = (int)b.sB;
         bsT[j] = (int)b.sT;
     }
@@ -287,15 +294,15 @@ MEP_DEV void wgrad_task(const mep_wgrad_desc& d, int t_begin, int t_end, int slo
     // base + (8 s + e) * step (bytes, soffset); columns unclamped (a column past N / Ktot reads
     // neighbouring data or 0 and only feeds output entries that are never stored)
     const int t0 = min(w0 + h * half, d.ntok);
-    const int stA = 4 * (LIN ? wg_step(d.a) : 0);
+    const int stA = ES * (LIN ? wg_step(d.a) : 0);
     int stB[KT], baseB[KT];
-    const int baseA = LIN ? t0 * stA + 4 * c : 0;
+    const int baseA = LIN ? t0 * stA + ES * c : 0;
 #pragma unroll
     for (int j = 0; j < KT; ++j) {
         int k0 = min(kbase + 32 * j, d.Ktot - 1), o = 0;
         while (o < d.n_b - 1 && k0 >= d.kb[o]) { k0 -= d.kb[o]; ++o; }
-        stB[j] = LIN ? 4 * wg_step(d.b[o]) : 0;
-        baseB[j] = LIN ? t0 * stB[j] + 4 * (k0 + c) : 0;
+        stB[j] = LIN ? ES * wg_step(d.b[o]) : 0;
+        baseB[j] = LIN ? t0 * stB[j] + ES * (k0 + c) : 0;
     }
     int blk = 0;   // LIN: next k block to load
     auto load_lin = [&](int p, bool checked) {
@@ -308,13 +315,10 @@ MEP_DEV void wgrad_task(const mep_wgrad_desc& d, int t_begin, int t_end, int slo
             // soffset would turn every load into a waterfall loop)
 #pragma unroll
             for (int i = 0; i < MT; ++i)
-                ra[p][i][e] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsA, va + 128 * i,
-                                                 __builtin_amdgcn_readfirstlane(tk * stA), 0));
+                ra[p][i][e] = ld(rsA, va + 32 * ES * i, __builtin_amdgcn_readfirstlane(tk * stA));
 #pragma unroll
             for (int j = 0; j < KT; ++j)
-                rb[p][j][e] = __builtin_bit_cast(
-                    float, __builtin_amdgcn_raw_buffer_load_b32(rsB[j], ok ? baseB[j] : WG_INV,
-                                                                __builtin_amdgcn_readfirstlane(tk * stB[j]), 0));
+                rb[p][j][e] = ld(rsB[j], ok ? baseB[j] : WG_INV, __builtin_amdgcn_readfirstlane(tk * stB[j]));
         }
         ++blk;
     };
@@ -343,14 +347,11 @@ MEP_DEV void wgrad_task(const mep_wgrad_desc& d, int t_begin, int t_end, int slo
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
             const bool ok = idx < nh;
-            const int va = ok ? 4 * offA : WG_INV;
+            const int va = ok ? ES * offA : WG_INV;
 #pragma unroll
-            for (int i = 0; i < MT; ++i)
-                ra[p][i][e] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsA, va + colA[i], 0, 0));
+            for (int i = 0; i < MT; ++i) ra[p][i][e] = ld(rsA, va + colA[i], 0);
 #pragma unroll
-            for (int j = 0; j < KT; ++j)
-                rb[p][j][e] = __builtin_bit_cast(
-                    float, __builtin_amdgcn_raw_buffer_load_b32(rsB[j], (ok ? 4 * offB[j] : WG_INV) + colB[j], 0, 0));
+            for (int j = 0; j < KT; ++j) rb[p][j][e] = ld(rsB[j], (ok ? ES * offB[j] : WG_INV) + colB[j], 0);
             ++idx;
             ++t;
             const bool wrap = t >= T;
@@ -498,7 +499,8 @@ __global__ __launch_bounds__(WG_THREADS) __attribute__((amdgpu_waves_per_eu(wg_o
             if (lin) wgrad_task<M, K, BF ? 1 : MEP_WG_PARTS, true, BF ? WG_SLOTS_B : WG_SLOTS_F>(d, t_begin, t_end, slot, kbase, red);  \
             else wgrad_task<M, K, BF ? 1 : MEP_WG_PARTS, false, BF ? WG_SLOTS_B : WG_SLOTS_F>(d, t_begin, t_end, slot, kbase, red);     \
             break;
-        if ((d.bf16 != 0) != BF) {
+        // the bf16-path instance needs bf16 operands AND bf16 operand rows (MEP_BF16_OPS | MEP_BF16_STORE)
+        if ((d.bf16 != 0) != BF || (BF && d.bf16 != (MEP_BF16_OPS | MEP_BF16_STORE))) {
             gfloat* part = G<float>(d.partial) + (int64_t)slot * d.N * d.Ktot;
             for (int e = threadIdx.x; e < d.N * d.Ktot; e += WG_THREADS) part[e] = __builtin_nanf("");
             continue;
@@ -856,13 +858,15 @@ MEP_DEV void unify_tasks(const mep_gemm_desc& d, const lfloat* wl, int ldl, int 
 // LDS already rounded, in 16-byte units (n, pair p, lane group g) at n * RS + (4p + g) * 16,
 // RS = 64 NP + 32 bytes (conflict-free fragment reads, split.h SplitW), zero past K; when it does
 // not fit, fragments are read from L2 and rounded on the fly (K % 16 == 0).
-template <int NIP, bool WL, bool XV>
+// HS: bf16 X and Y rows (MEP_BF16_STORE, the bf16 path's features and unified rows)
+template <int NIP, bool WL, bool XV, bool HS>
 MEP_DEV void unify_tasks_bf(const mep_gemm_desc& d, const __attribute__((address_space(3))) unsigned char* wl, int tile_lo, int tile_hi, int np) {
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int c = lane & 15, g = lane >> 4;
     const int K = d.K, NPK = (K + 31) >> 5, ntok = d.ntok, RS = 64 * NPK + 32;
     const int T = d.x.T;
-    const auto rsX = __builtin_amdgcn_make_buffer_rsrc((void*)d.x.ptr, 0, wg_extent(d.x, T, ntok, K), 0x00020000);
+    constexpr int ES = HS ? 2 : 4;
+    const auto rsX = __builtin_amdgcn_make_buffer_rsrc((void*)d.x.ptr, 0, wg_extent(d.x, T, ntok, K, ES), 0x00020000);
     const gfloat* wg = G<const float>(d.w);
     const gfloat* table = G<const float>(d.table);
     const int ntask = (tile_hi - tile_lo) * np;
@@ -874,7 +878,7 @@ MEP_DEV void unify_tasks_bf(const mep_gemm_desc& d, const __attribute__((address
         int xo = WG_INV;
         if (ok) {
             const int b = tok / T, t = tok - b * T;
-            xo = 4 * ((int)(b * d.x.sB + t * d.x.sT) + 4 * g);
+            xo = ES * ((int)(b * d.x.sB + t * d.x.sT) + 4 * g);
         }
         const int n0 = 16 * NIP * part;
         f32x4 acc[NIP];
@@ -883,7 +887,14 @@ MEP_DEV void unify_tasks_bf(const mep_gemm_desc& d, const __attribute__((address
         f32x4 xf[PP][2];
         auto ld = [&](int o) {
             f32x4 v;
-            if (XV) {
+            if (HS && XV) {
+                const u32x2a w = __builtin_bit_cast(u32x2a, __builtin_amdgcn_raw_buffer_load_b64(rsX, o, 0, 0));
+                v = f32x4{bf16_word_lo(w[0]), bf16_word_hi(w[0]), bf16_word_lo(w[1]), bf16_word_hi(w[1])};
+            } else if (HS) {
+#pragma unroll
+                for (int e = 0; e < 4; ++e)
+                    v[e] = __builtin_bit_cast(float, (unsigned)__builtin_amdgcn_raw_buffer_load_b16(rsX, o + 2 * e, 0, 0) << 16);
+            } else if (XV) {
                 v = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rsX, o, 0, 0));
             } else {
 #pragma unroll
@@ -892,9 +903,9 @@ MEP_DEV void unify_tasks_bf(const mep_gemm_desc& d, const __attribute__((address
             return v;
         };
         auto load = [&](int s, int pp) {
-            const int o = pp < NPK ? xo + 128 * pp : WG_INV;
+            const int o = pp < NPK ? xo + 32 * ES * pp : WG_INV;
             xf[s][0] = ld(o);
-            xf[s][1] = ld(o == WG_INV || 32 * pp + 16 >= K ? WG_INV : o + 64);
+            xf[s][1] = ld(o == WG_INV || 32 * pp + 16 >= K ? WG_INV : o + 16 * ES);
         };
         auto mma = [&](int s, int pp) {
             const OpN<1> xb = opn<1>(xf[s][0], xf[s][1]);
@@ -926,14 +937,14 @@ MEP_DEV void unify_tasks_bf(const mep_gemm_desc& d, const __attribute__((address
         for (int s = 0; s < PP - 1; ++s)
             if (p0 + s < NPK) mma(s, p0 + s);
         if (ok) {
-            gfloat* yr = row_ptr(d.y, tok);
+            const auto yr = rowa<HS>(d.y, tok);
             const gfloat* tr = table ? table + (int64_t)(tok % d.y.T) * (d.ldt ? d.ldt : d.N) : nullptr;
 #pragma unroll
             for (int i = 0; i < NIP; ++i) {
                 const int col = n0 + 16 * i + 4 * g;
                 f32x4 v = acc[i];
                 if (tr) v += ld4w(tr + col);
-                stg4(yr + col, make_float4(v[0], v[1], v[2], v[3]));
+                st4a(yr + col, v);
             }
         }
     }
@@ -948,7 +959,8 @@ __global__ __launch_bounds__(UN_THREADS) void k_unify(const mep_gemm_desc* __res
     const int tile_lo = w * per, tile_hi = min(ntiles, tile_lo + per);
     if (tile_lo >= tile_hi) return;   // whole workgroup
     __shared__ __attribute__((aligned(16))) float smem[UN_LDS];
-    const bool xv = (d.K % 4 == 0) && ((d.x.ptr & 15) == 0) && (d.x.sB % 4 == 0) && (d.x.sT % 4 == 0);
+    const bool hs = d.bf16 & MEP_BF16_STORE;   // bf16 X / Y rows
+    const bool xv = (d.K % 4 == 0) && ((d.x.ptr & (hs ? 7 : 15)) == 0) && (d.x.sB % 4 == 0) && (d.x.sT % 4 == 0);
     const int np = d.N >= 64 ? 2 : 1, nip = d.N / (16 * np);
     if (d.bf16) {
         // W [N][K] -> rounded bf16 units in LDS (zero past K) when N * RS fits
@@ -972,14 +984,15 @@ __global__ __launch_bounds__(UN_THREADS) void k_unify(const mep_gemm_desc* __res
             }
             __syncthreads();
         }
+#define MEP_UNB2(NIP, HS)                                                                                \
+            if (wlds) { if (xv) unify_tasks_bf<NIP, true, true, HS>(d, wl, tile_lo, tile_hi, np);        \
+                        else unify_tasks_bf<NIP, true, false, HS>(d, wl, tile_lo, tile_hi, np); }        \
+            else unify_tasks_bf<NIP, false, true, HS>(d, wl, tile_lo, tile_hi, np);
 #define MEP_UNB(NIP)                                                                                     \
-        if (nip == NIP) {                                                                                \
-            if (wlds) { if (xv) unify_tasks_bf<NIP, true, true>(d, wl, tile_lo, tile_hi, np);            \
-                        else unify_tasks_bf<NIP, true, false>(d, wl, tile_lo, tile_hi, np); }            \
-            else unify_tasks_bf<NIP, false, true>(d, wl, tile_lo, tile_hi, np);                          \
-        }
+        if (nip == NIP) { if (hs) { MEP_UNB2(NIP, true) } else { MEP_UNB2(NIP, false) } }
         MEP_UNB(1) MEP_UNB(2) MEP_UNB(3) MEP_UNB(4)
 #undef MEP_UNB
+#undef MEP_UNB2
         return;
     }
     lfloat* wl = (lfloat*)&smem[0];

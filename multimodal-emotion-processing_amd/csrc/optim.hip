@@ -161,22 +161,25 @@ __global__ __launch_bounds__(256) void k_colsum(const mep_colsum_desc* __restric
     colsum_block(descs[blockIdx.y], blockIdx.x);
 }
 
-// out = sum of sources, 4 columns per thread (D % 4 == 0 for every model width)
-__global__ __launch_bounds__(256) void k_sum_rows(const mep_sum_desc* __restrict__ descs) {
-    const mep_sum_desc& d = descs[blockIdx.y];
+// out = sum of sources, 4 columns per thread (D % 4 == 0 for every model width); HS: bf16 source
+// and output rows (MEP_SUM_BF16, the bf16 path), summed in fp32
+template <bool HS>
+MEP_DEV void sum_rows(const mep_sum_desc& d) {
     const int D4 = d.D / 4;
     const int64_t total = (int64_t)d.ntok * D4;
     for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
         const int tok = (int)(i / D4), c = 4 * (int)(i - (int64_t)tok * D4);
-        float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
-        for (int k = 0; k < d.n_src; ++k) {
-            const float4 v = ldg4(row_ptr(d.src[k], tok) + c);
-            s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
-        }
-        gfloat* o = row_ptr(d.out, tok) + c;
-        if (d.accumulate) { const float4 v = ldg4(o); s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w; }
-        stg4(o, s);
+        f32x4 s = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int k = 0; k < d.n_src; ++k) s += ld4a(rowa<HS>(d.src[k], tok) + c);
+        const auto o = rowa<HS>(d.out, tok) + c;
+        if (d.accumulate & 1) s += ld4a(o);
+        st4a(o, s);
     }
+}
+__global__ __launch_bounds__(256) void k_sum_rows(const mep_sum_desc* __restrict__ descs) {
+    const mep_sum_desc& d = descs[blockIdx.y];
+    if (d.accumulate & MEP_SUM_BF16) sum_rows<true>(d);
+    else sum_rows<false>(d);
 }
 
 }  // namespace

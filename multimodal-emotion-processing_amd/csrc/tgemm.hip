@@ -96,14 +96,17 @@ __global__ __launch_bounds__(TG_THREADS) void k_tgemm(const mep_gemm_desc* __res
     };
 
     // ---- X rows of this wave's tiles (tokens past ntok: clamped rows, never stored)
+    // the bf16 path (one part) reads bf16 X rows and writes bf16 Y rows (MEP_BF16_STORE)
+    constexpr bool HS = NPART == 1;
+    constexpr int ES = HS ? 2 : 4;
     const int64_t last = row_off(d.x, ntok - 1) + K;
-    const auto rsX = __builtin_amdgcn_make_buffer_rsrc((void*)d.x.ptr, 0, (int)min((int64_t)4 * last, (int64_t)0x7fffffff), 0x00020000);
-    const bool xvec = ((d.x.ptr & 15) == 0) && (d.x.sB % 4 == 0) && (d.x.sT % 4 == 0);
+    const auto rsX = __builtin_amdgcn_make_buffer_rsrc((void*)d.x.ptr, 0, (int)min((int64_t)ES * last, (int64_t)0x7fffffff), 0x00020000);
+    const bool xvec = ((d.x.ptr & (HS ? 7 : 15)) == 0) && (d.x.sB % 4 == 0) && (d.x.sT % 4 == 0);
     int xoff[TG_TT];
 #pragma unroll
     for (int t = 0; t < TG_TT; ++t) {
         const int tok = min(tok0 + 16 * (TG_TT * wave + t) + c, ntok - 1);
-        xoff[t] = 4 * (int)row_off(d.x, tok) + 16 * g;
+        xoff[t] = ES * ((int)row_off(d.x, tok) + 4 * g);
     }
     f32x4 xr[TG_TT][2];
     auto load_x = [&](int kc) {
@@ -111,8 +114,15 @@ __global__ __launch_bounds__(TG_THREADS) void k_tgemm(const mep_gemm_desc* __res
         for (int t = 0; t < TG_TT; ++t)
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
-                const int o = xoff[t] + 128 * kc + 64 * h;   // bytes: k0 + 16 h + 4g
-                if (xvec) {
+                const int o = xoff[t] + 32 * ES * kc + 16 * ES * h;   // bytes: k0 + 16 h + 4g
+                if (HS && xvec) {
+                    const u32x2a w = __builtin_bit_cast(u32x2a, __builtin_amdgcn_raw_buffer_load_b64(rsX, o, 0, 0));
+                    xr[t][h] = f32x4{bf16_word_lo(w[0]), bf16_word_hi(w[0]), bf16_word_lo(w[1]), bf16_word_hi(w[1])};
+                } else if (HS) {
+#pragma unroll
+                    for (int e = 0; e < 4; ++e)
+                        xr[t][h][e] = __builtin_bit_cast(float, (unsigned)__builtin_amdgcn_raw_buffer_load_b16(rsX, o + 2 * e, 0, 0) << 16);
+                } else if (xvec) {
                     xr[t][h] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rsX, o, 0, 0));
                 } else {
 #pragma unroll
@@ -161,7 +171,7 @@ __global__ __launch_bounds__(TG_THREADS) void k_tgemm(const mep_gemm_desc* __res
     for (int t = 0; t < TG_TT; ++t) {
         const int tok = tok0 + 16 * (TG_TT * wave + t) + c;
         if (tok >= ntok) continue;
-        gfloat* yrow = row_ptr(d.y, tok);
+        const auto yrow = rowa<HS>(d.y, tok);
         const gfloat* trow = table ? table + (int64_t)(tok % d.y.T) * ldt : nullptr;
 #pragma unroll
         for (int i = 0; i < NI; ++i) {
@@ -179,8 +189,8 @@ __global__ __launch_bounds__(TG_THREADS) void k_tgemm(const mep_gemm_desc* __res
 #pragma unroll
                 for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r], 0.f);
             }
-            if (d.accumulate) v += ld4w(yrow + col);
-            *reinterpret_cast<MEP_G f32x4*>(yrow + col) = v;
+            if (d.accumulate) v += ld4a(yrow + col);
+            st4a(yrow + col, v);
         }
     }
 }
@@ -210,14 +220,17 @@ __global__ __launch_bounds__(TG_THREADS) void k_tgemm_res(const mep_gemm_desc* _
     const WS ws{(lbyte*)sm, 0};
 
     // ---- X: this wave's token tiles, k pair 0 in flight while W is staged
+    // the bf16 path (one part) reads bf16 X rows and writes bf16 Y rows (MEP_BF16_STORE)
+    constexpr bool HS = NPART == 1;
+    constexpr int ES = HS ? 2 : 4;
     const int64_t last = row_off(d.x, ntok - 1) + K;
-    const auto rsX = __builtin_amdgcn_make_buffer_rsrc((void*)d.x.ptr, 0, (int)min((int64_t)4 * last, (int64_t)0x7fffffff), 0x00020000);
-    const bool xvec = ((d.x.ptr & 15) == 0) && (d.x.sB % 4 == 0) && (d.x.sT % 4 == 0);
+    const auto rsX = __builtin_amdgcn_make_buffer_rsrc((void*)d.x.ptr, 0, (int)min((int64_t)ES * last, (int64_t)0x7fffffff), 0x00020000);
+    const bool xvec = ((d.x.ptr & (HS ? 7 : 15)) == 0) && (d.x.sB % 4 == 0) && (d.x.sT % 4 == 0);
     int xoff[TG_TT];
 #pragma unroll
     for (int t = 0; t < TG_TT; ++t) {
         const int tok = min(tok0 + 16 * (TG_TT * wave + t) + c, ntok - 1);
-        xoff[t] = 4 * (int)row_off(d.x, tok) + 16 * g;
+        xoff[t] = ES * ((int)row_off(d.x, tok) + 4 * g);
     }
     f32x4 xr[TG_TT][2];
     auto load_x = [&](int kp) {
@@ -225,8 +238,15 @@ __global__ __launch_bounds__(TG_THREADS) void k_tgemm_res(const mep_gemm_desc* _
         for (int t = 0; t < TG_TT; ++t)
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
-                const int o = xoff[t] + 128 * kp + 64 * h;
-                if (xvec) {
+                const int o = xoff[t] + 32 * ES * kp + 16 * ES * h;
+                if (HS && xvec) {
+                    const u32x2a w = __builtin_bit_cast(u32x2a, __builtin_amdgcn_raw_buffer_load_b64(rsX, o, 0, 0));
+                    xr[t][h] = f32x4{bf16_word_lo(w[0]), bf16_word_hi(w[0]), bf16_word_lo(w[1]), bf16_word_hi(w[1])};
+                } else if (HS) {
+#pragma unroll
+                    for (int e = 0; e < 4; ++e)
+                        xr[t][h][e] = __builtin_bit_cast(float, (unsigned)__builtin_amdgcn_raw_buffer_load_b16(rsX, o + 2 * e, 0, 0) << 16);
+                } else if (xvec) {
                     xr[t][h] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rsX, o, 0, 0));
                 } else {
 #pragma unroll
@@ -293,7 +313,7 @@ __global__ __launch_bounds__(TG_THREADS) void k_tgemm_res(const mep_gemm_desc* _
     for (int t = 0; t < TG_TT; ++t) {
         const int tok = tok0 + 16 * (TG_TT * wave + t) + c;
         if (tok >= ntok) continue;
-        gfloat* yrow = row_ptr(d.y, tok);
+        const auto yrow = rowa<HS>(d.y, tok);
         const gfloat* trow = table ? table + (int64_t)(tok % d.y.T) * ldt : nullptr;
 #pragma unroll
         for (int i = 0; i < NI; ++i) {
@@ -311,8 +331,8 @@ __global__ __launch_bounds__(TG_THREADS) void k_tgemm_res(const mep_gemm_desc* _
 #pragma unroll
                 for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r], 0.f);
             }
-            if (d.accumulate) v += ld4w(yrow + col);
-            *reinterpret_cast<MEP_G f32x4*>(yrow + col) = v;
+            if (d.accumulate) v += ld4a(yrow + col);
+            st4a(yrow + col, v);
         }
     }
 }

@@ -17,7 +17,9 @@ its dQ: 658 TFLOP/s.  The realformer token GEMMs and epilogues: on the wave-tile
 (mep_wgemm, mep_rfw_epi_*: six products) 417 TFLOP/s; on the LDS-tiled ones (MEP_RFW=0: mep_gemm,
 mep_rf_epi_*) f32 MFMA, 157 TF.
 bf16 path (MEP_PREC_BF16): one bf16 product per product, every matrix kernel priced at the bf16
-peak; the bytes are the same (fp32 storage).
+peak; the activations (features, unified rows, attention outputs, xp / z and their gradients) are
+stored as bf16, so their bytes count 2 per element (include/mep.h); block outputs (the pooled
+tensor), scores, statistics and parameters stay 4.
 """
 from . import _lib
 from .trimodal import MODS
@@ -56,6 +58,7 @@ def launch_costs(plan):
         return rf_launch_costs(plan)
     sp, B = plan.spec, plan.B
     D, H = sp.D, sp.H
+    a = 2 if getattr(plan, 'bf16', False) else 4     # bytes per activation element
     out = {}
     UNIFY = _lib.gemm_launcher('mep_unify', plan.d_unify)
 
@@ -66,35 +69,38 @@ def launch_costs(plan):
     for e in range(2):
         for m, d in zip(MODS, sp.dims):
             n = plan.ntok[m]
-            add(UNIFY, 2 * n * D * d, 4 * (n * d + n * D + D * d))
+            add(UNIFY, 2 * n * D * d, a * (n * d + n * D) + 4 * D * d)
     for blk in plan.blocks:
         Tq, Tk = blk['Tq'], blk['Tk']
         r_in = 1 if blk['i'] > 0 else 0
         r_out = 1 if 'S' in blk else 0
         s_bytes = 4 * H * Tq * Tk
         add('mep_attn_fwd', B * 4 * Tq * Tk * D,
-            B * (4 * (2 * Tq * D + Tk * D) + 4 * Tk + 8 * H * Tq + s_bytes * (r_in + r_out)))
+            B * (a * (2 * Tq * D + Tk * D) + 4 * Tk + 8 * H * Tq + s_bytes * (r_in + r_out)))
         n = B * Tq
-        add('mep_block_epi_fwd', 2 * n * D * 3 * D + 8 * n * D, 4 * n * D * 5 + 8 * n + 4 * 3 * D * D + 8 * D)
+        # reads q, x; writes xp, z (activations) and out (the pooled tensor, fp32) [+ its bf16
+        # copy for the next layer's q]
+        out_h = a if (a == 2 and blk['i'] < sp.nl - 1) else 0
+        add('mep_block_epi_fwd', 2 * n * D * 3 * D + 8 * n * D, a * n * D * 4 + (4 + out_h) * n * D + 8 * n + 4 * 3 * D * D + 8 * D)
         # upstream gradient formed from this block's dpooled / argmax slices (B x 3D), not read
         # as [n, D] rows (the pool backward is folded into this launch)
         add('mep_block_epi_bwd', 2 * n * D * 3 * D + 10 * n * D,
-            4 * n * D * 6 + 8 * n + 4 * 3 * D * D + 4 * (n // 64 + 1) * 2 * D + 4 * B * 3 * D)
+            a * n * D * 6 + 8 * n + 4 * 3 * D * D + 4 * (n // 64 + 1) * 2 * D + 4 * B * 3 * D)
         chained = s_bytes * ((1 if r_out else 0) + (1 if r_in else 0) * 2)
         add('mep_attn_bwd', B * 10 * Tq * Tk * D,
-            B * (4 * (5 * Tq * D + 2 * Tk * D) + 4 * Tk + 8 * H * Tq + chained))
-        add('mep_wgrad', 2 * n * D * 3 * D, 4 * n * D * 5)
+            B * (a * (5 * Tq * D + 2 * Tk * D) + 4 * Tk + 8 * H * Tq + chained))
+        add('mep_wgrad', 2 * n * D * 3 * D, a * n * D * 5)
     for e in range(2):
         for m, d in zip(MODS, sp.dims):
             n = plan.ntok[m]
-            add('mep_wgrad', 2 * n * D * d, 4 * n * (D + d))
+            add('mep_wgrad', 2 * n * D * d, a * n * (D + d))
     for e in range(2):
         add('mep_pool_fwd', B * plan.Ttot * plan.C, 4 * B * (plan.Ttot * plan.C + 2 * plan.C) + 4 * B * plan.C)
         for m in MODS:                       # dU = the dQ / dKV rows of every block reading m
             n = plan.ntok[m]
             srcs = sum(1 for b in plan.blocks if b['i'] == 0 and b['qm'] == m) // 2 + \
                 sum(1 for b in plan.blocks if b['km'] == m) // 2
-            add('mep_sum_rows', srcs * n * D, 4 * n * D * (srcs + 1))
+            add('mep_sum_rows', srcs * n * D, a * n * D * (srcs + 1))
     return out
 
 

@@ -170,8 +170,27 @@ def _xcd_pairs(segs, n_wg):
             for r in range(m):
                 out += [blk[q][r] if q < len(blk) else [] for q in range(8)]
     if len(out) > max(n_wg, len(segs)):
-        return segs
+        # few, large chunk groups (cfg5: one chunk per item, 4-24 column groups each): the 8-group
+        # blocks would pad past the launch, so pack whole groups onto the 8 XCDs instead
+        return _xcd_pack([groups[k] for k in order], n_wg, segs)
     return out
+
+
+def _xcd_pack(groups, n_wg, segs):
+    """Every chunk group whole on one XCD (workgroup ids x, x + 8, x + 16, ...), groups dealt
+    largest first to the XCD with the fewest workgroups so far; the XCD lists interleave into the
+    launch order, short lists padded with empty workgroups.  Without it the column groups of one
+    chunk land on every XCD and each streams the shared A rows from HBM (cfg5 k_wgrad: 2.9x the
+    algorithmic bytes).  Falls back to the plain order if the padding would push the
+    launch past n_wg."""
+    lists = [[] for _ in range(8)]
+    for g in sorted(groups, key=len, reverse=True):
+        x = min(range(8), key=lambda i: (len(lists[i]), i))
+        lists[x] += g
+    depth = max(len(l) for l in lists)
+    if 8 * depth > max(n_wg, len(segs)):
+        return segs
+    return [lists[x][j] if j < len(lists[x]) else [] for j in range(depth) for x in range(8)]
 
 
 UN_LDS = 30720   # csrc/gemm.hip k_unify: floats of LDS for the staged weight
@@ -232,7 +251,8 @@ def make_wgrad(items, dev, tok_per_split=None, bf16=False):
                                ldo=(ctypes.c_int32 * _lib.WG_MAX_B)(*[b[3] for b in allb]),
                                partial=ws.data_ptr() + 4 * off, n_b=len(bs), ntok=n, N=N, Ktot=ktot,
                                tok_per_split=0, n_split=ns, accumulate=0, out_trans=int(trans),
-                               bf16=int(bool(bf16))))
+                               # the bf16-path instance: bf16 operands from bf16 rows
+                               bf16=(_lib.BF16_OPS | _lib.BF16_STORE) if bf16 else 0))
         off += ns * N * ktot
         rmax = max(rmax, cdiv(N * ktot, 256))
     assert len(descs) < 2 ** 23 and all(cg < 256 for b in segs for (_, cg, _, _, _) in b)
@@ -247,7 +267,8 @@ def make_wgrad(items, dev, tok_per_split=None, bf16=False):
 
 
 def rows(t, T, sB, sT, off=0):
-    return Rows(ptr=t.data_ptr() + 4 * off, sB=sB, sT=sT, T=T)
+    """row view of tensor t (strides and offset in elements: 4-byte fp32 or 2-byte bf16 rows)"""
+    return Rows(ptr=t.data_ptr() + t.element_size() * off, sB=sB, sT=sT, T=T)
 
 
 def crows(t, T, D, off=0):
@@ -303,6 +324,10 @@ class TriModalPlan:
         D, H, nl, NC = sp.D, sp.H, sp.nl, sp.NC
         dev = self.device
         f32 = dict(dtype=torch.float32, device=dev)
+        # activations (include/mep.h MEP_PREC_BF16): bf16 on the bf16 path -- the features, unified
+        # rows, attention outputs, epilogue intermediates and their gradients -- else fp32
+        act = dict(dtype=torch.bfloat16 if self.bf16 else torch.float32, device=dev)
+        self.act = act
         self.Ttot = sum(self.T.values())
         self.C = 3 * nl * D
         self.F = 2 * self.C
@@ -310,7 +335,7 @@ class TriModalPlan:
         # ---------------- static input buffers ([B, 2, T, d] prev/cur layout)
         # encoder-major [E, B, T, d]: each encoder's input rows are contiguous (linear in the token,
         # the fast addressing of k_wgrad); the masks keep the [B, E, T] prev/cur layout
-        self.x_in = {m: torch.zeros(E, B, self.T[m], d, **f32) for m, d in zip(MODS, sp.dims)}
+        self.x_in = {m: torch.zeros(E, B, self.T[m], d, **act) for m, d in zip(MODS, sp.dims)}
         self.m_in = {m: torch.zeros(B, E, self.T[m], **f32) for m in MODS}
         self.labels = torch.zeros(B, NC, dtype=torch.float32 if labels_float else torch.int64, device=dev)
         # dropout {seed, row0} (include/mep.h mep_epi_desc.seed), usually the runner's shared state
@@ -326,9 +351,9 @@ class TriModalPlan:
         ntok = {m: B * self.T[m] for m in MODS}
         self.ntok = ntok
         assert max(ntok.values()) < 1 << 22, 'row views are limited to 2^22 rows (csrc/common.h row_off)'
-        self.U = {(e, m): torch.zeros(ntok[m], D, **f32) for e in range(E) for m in MODS}
+        self.U = {(e, m): torch.zeros(ntok[m], D, **act) for e in range(E) for m in MODS}
         if sp.unify_norm:
-            self.Y = {(e, m): torch.zeros(ntok[m], D, **f32) for e in range(E) for m in MODS}
+            self.Y = {(e, m): torch.zeros(ntok[m], D, **act) for e in range(E) for m in MODS}
             self.Ystat = {(e, m): torch.zeros(ntok[m], 2, **f32) for e in range(E) for m in MODS}
         self.Xcat = [torch.zeros(B, self.Ttot, self.C, **f32) for _ in range(E)]
         self.pool_fold = POOL_FOLD
@@ -363,10 +388,13 @@ class TriModalPlan:
         blk = dict(idx=len(self.blocks), e=e, j=j, i=i, qm=qm, km=km, Tq=Tq, Tk=Tk,
                    pre=sp.prefixes[e] + 'multimodal_blocks.%d.' % (sp.nl * j + i))
         for name in ('X', 'XP', 'Z', 'dZ', 'dXP', 'dX', 'dQ'):
-            blk[name] = torch.zeros(nq, D, **f32)
+            blk[name] = torch.zeros(nq, D, **self.act)
+        if self.bf16 and i < sp.nl - 1:
+            # bf16 copy of the block output (fp32 in the pooled tensor) for the next layer's q
+            blk['Qh'] = torch.zeros(nq, D, **self.act)
         blk['estat'] = torch.zeros(nq, 2, **f32)
         blk['astat'] = torch.zeros(B, H, Tq, 2, **f32)
-        blk['dKV'] = torch.zeros(nk, D, **f32)
+        blk['dKV'] = torch.zeros(nk, D, **self.act)
         blk['ln_partial'] = torch.zeros(cdiv(nq, 16), 2, D, **f32)   # one row per 16-token wave
         if i < sp.nl - 1:
             blk['S'] = torch.zeros(B, H, Tq, Tk, **f32)
@@ -384,7 +412,10 @@ class TriModalPlan:
     def _q_rows(self, blk):
         if blk['i'] == 0:
             return crows(self.U[(blk['e'], blk['qm'])], blk['Tq'], self.spec.D)
-        return self._out_rows(self._blk(blk['e'], blk['j'], blk['i'] - 1))
+        prev = self._blk(blk['e'], blk['j'], blk['i'] - 1)
+        if 'Qh' in prev:                      # bf16 path: the previous block's bf16 output copy
+            return crows(prev['Qh'], blk['Tq'], self.spec.D)
+        return self._out_rows(prev)
 
     def _blk(self, e, j, i):
         return self.blocks[(e * 9 + j) * self.spec.nl + i]
@@ -409,7 +440,7 @@ class TriModalPlan:
                 ud.append(GemmDesc(x=self._in_rows(e, m), y=crows(out, self.T[m], D),
                                    w=fl.ptr(pre + UNIFY_NAMES[m] + '.weight'), bias=0, table=0,
                                    ntok=self.ntok[m], N=D, K=d, ldw=d, w_nt=1, accumulate=0, relu=0, alpha=1.0,
-                                   bf16=int(self.bf16)))
+                                   bf16=(_lib.BF16_OPS | _lib.BF16_STORE) if self.bf16 else 0))
         self.d_unify, self.t_unify = make_unify(ud, dev)
         if sp.unify_norm:
             ln = []
@@ -420,7 +451,7 @@ class TriModalPlan:
                     ln.append(LnDesc(x=crows(self.Y[(e, m)], T, D), y=crows(self.U[(e, m)], T, D),
                                      dy=Rows(), dx=Rows(), w=fl.ptr(pre + 'weight'), b=fl.ptr(pre + 'bias'),
                                      stats=self.Ystat[(e, m)].data_ptr(), partial=0, ntok=self.ntok[m], D=D,
-                                     dx_accumulate=0))
+                                     dx_accumulate=0, bf16=_lib.BF16_STORE if self.bf16 else 0))
             self.d_uln = DescArray(LnDesc, ln, dev)
         # per layer: attention + epilogue forward
         self.d_attn, self.d_epi, self.t_attn, self.t_epi, self.g_attn = [], [], [], [], []
@@ -468,18 +499,18 @@ class TriModalPlan:
         for e in range(E):
             for m in MODS:
                 T = self.T[m]
-                self.dU[(e, m)] = torch.zeros(self.ntok[m], D, dtype=torch.float32, device=dev)
+                self.dU[(e, m)] = torch.zeros(self.ntok[m], D, **self.act)
                 srcs = [crows(self._blk(e, j, 0)['dQ'], T, D) for j, (qm, km) in enumerate(CHAINS) if qm == m]
                 srcs += [crows(self._blk(e, j, i)['dKV'], T, D) for j, (qm, km) in enumerate(CHAINS) if km == m
                          for i in range(nl)]
                 assert len(srcs) <= _lib.SUM_MAX_SRC
                 arr = (Rows * _lib.SUM_MAX_SRC)(*srcs)
                 sd.append(SumDesc(src=arr, out=crows(self.dU[(e, m)], T, D), n_src=len(srcs),
-                                  ntok=self.ntok[m], D=D, accumulate=0))
+                                  ntok=self.ntok[m], D=D, accumulate=_lib.SUM_BF16 if self.bf16 else 0))
         self.d_sum = DescArray(SumDesc, sd, dev)
         self.t_sum = min(1024, max(cdiv(self.ntok[m] * D // 4, 256) for m in MODS))
         # the sums folded into the attention backward (SHORT descriptors: every key length <= 64)
-        self.sum_fold = (SUM_FOLD and max(self.T.values()) <= 64
+        self.sum_fold = (SUM_FOLD and not self.bf16 and max(self.T.values()) <= 64
                          and all(d.n_src <= _lib.ATTN_FOLD_SRC for d in sd))
         if self.sum_fold:
             self.sum_count = torch.zeros(len(sd), B * sp.H, dtype=torch.int32, device=dev)
@@ -515,7 +546,8 @@ class TriModalPlan:
                                      dx=crows(self.dY[(e, m)], T, D), w=fl.ptr(pre + 'weight'), b=0,
                                      stats=self.Ystat[(e, m)].data_ptr(),
                                      partial=self.uln_partial[e].data_ptr() + 4 * r0 * 2 * D,
-                                     ntok=self.ntok[m], D=D, dx_accumulate=0))
+                                     ntok=self.ntok[m], D=D, dx_accumulate=0,
+                                     bf16=_lib.BF16_STORE if self.bf16 else 0))
                     r0 += tiles[m]
             self.d_ulnb = DescArray(LnDesc, lb, dev)
         self._build_grad_descriptors()
@@ -542,7 +574,8 @@ class TriModalPlan:
                        ln_w=fl.ptr(blk['pre'] + sp.block_norm + '.weight'),
                        ln_b=fl.ptr(blk['pre'] + sp.block_norm + '.bias'),
                        stats=blk['estat'].data_ptr(), seed=self.seed_state.data_ptr(),
-                       ntok=self.B * Tq, D=D, drop_p=self._drop, drop_stream=stream_id)
+                       ntok=self.B * Tq, D=D, drop_p=self._drop, drop_stream=stream_id,
+                       out_h=crows(blk['Qh'], Tq, D) if 'Qh' in blk else Rows())
 
     def _epi_bwd_desc(self, blk):
         D, Tq = self.spec.D, blk['Tq']

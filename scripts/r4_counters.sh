@@ -1,0 +1,41 @@
+#!/bin/bash
+# Round-4 evidence passes, one rocprofv3 counter group per invocation, kernel
+# trace only, never combined with other tracing:
+#   1. FETCH_SIZE / WRITE_SIZE / TCC_EA0 request counters over scripts/micro/fetch_cal (known byte
+#      counts per access width) -> the per-width correction (scripts/fetch_cal.py)
+#   2. SQ instruction / cycle / MFMA / LDS-conflict groups over every kernel of the bench workloads
+#      (cfg3, cfg3 bf16, cfg2, cfg5) -> per-kernel MFMA utilisation (scripts/r4_ctr_summary.py)
+#   STAGE=cal|sq|all CFGS="cfg3 cfg2 cfg5" bash scripts/r4_counters.sh
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+OUT=gpurun_out/r4ctr
+mkdir -p $OUT
+STAGE=${STAGE:-all}
+pass() { local dir=$1; shift
+  timeout -k 10 ${PT:-240} "$@" > $OUT/$dir.log 2>&1; local rc=$?
+  echo "$dir rc=$rc"
+  case $rc in 0) ;; *) tail -5 $OUT/$dir.log; exit $rc;; esac; }
+if [ $STAGE = cal ] || [ $STAGE = all ]; then
+  test -x scripts/micro/fetch_cal || { echo "build scripts/micro/fetch_cal first"; exit 1; }
+  pass cal_plain ./scripts/micro/fetch_cal
+  pass cal_fetch rocprofv3 --pmc FETCH_SIZE --kernel-trace -d $OUT/cal_fetch -o run --output-format csv -- ./scripts/micro/fetch_cal
+  pass cal_write rocprofv3 --pmc WRITE_SIZE --kernel-trace -d $OUT/cal_write -o run --output-format csv -- ./scripts/micro/fetch_cal
+  pass cal_req rocprofv3 --pmc TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum --kernel-trace -d $OUT/cal_req -o run --output-format csv -- ./scripts/micro/fetch_cal
+fi
+if [ $STAGE = sq ] || [ $STAGE = all ]; then
+  G1="SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS GRBM_GUI_ACTIVE"
+  G2="SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_MFMA SQ_INSTS_VALU_MFMA_MOPS_BF16 SQ_INSTS_VALU_MFMA_MOPS_F32"
+  G3="SQ_VALU_MFMA_BUSY_CYCLES SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_ACTIVE_INST_VMEM SQ_WAIT_INST_LDS SQ_INST_CYCLES_VMEM_RD GRBM_GUI_ACTIVE"
+  for cfg in ${CFGS:-cfg3 cfg3_bf16 cfg2 cfg5}; do
+    case $cfg in
+      cfg3) A="--config cfg3";; cfg3_bf16) A="--config cfg3 --dtype bf16";;
+      cfg2) A="--config cfg2";; cfg5) A="--config cfg5";; cfg5_bf16) A="--config cfg5 --dtype bf16";;
+    esac
+    i=0
+    for grp in "$G1" "$G2" "$G3"; do
+      i=$((i+1))
+      pass ${cfg}_g$i rocprofv3 --pmc $grp --kernel-trace -d $OUT/${cfg}_g$i -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline $A
+    done
+  done
+fi
+echo done

@@ -36,24 +36,34 @@ class Checker:
         ts = _tensors(plan, [])
         fl = plan.flat
         ts += [fl.buf, fl.grad]
-        self.allocs = sorted({(t.data_ptr(), t.untyped_storage().nbytes()) for t in ts if t.numel()})
+        # whole storages (a view's data_ptr plus its storage's size would run past the storage)
+        self.allocs = sorted({(t.untyped_storage().data_ptr(), t.untyped_storage().nbytes(), t.element_size())
+                              for t in ts if t.numel()})
         self.n = 0
 
     def inside(self, label, ptr, nbytes):
         if ptr == 0 or nbytes <= 0:
             return
         self.n += 1
-        for base, size in self.allocs:
+        for base, size, _ in self.allocs:
             if base <= ptr and ptr + nbytes <= base + size:
                 return
         raise AssertionError('%s: [%#x, +%d) is outside every plan buffer' % (label, ptr, nbytes))
 
-    def rows(self, label, r, ntok, cols):
+    def elsize(self, ptr):
+        """bytes per element of the buffer a row view points into (bf16 activations on the bf16
+        path, include/mep.h MEP_PREC_BF16)"""
+        for base, size, es in self.allocs:
+            if base <= ptr < base + size:
+                return es
+        return F
+
+    def rows(self, label, r, ntok, cols, es=None):
         if r.ptr == 0 or ntok == 0:
             return
         assert r.T > 0, label
         last = (ntok - 1) // r.T * r.sB + (ntok - 1) % r.T * r.sT
-        self.inside(label, r.ptr, (last + cols) * F)
+        self.inside(label, r.ptr, (last + cols) * (es or self.elsize(r.ptr)))
 
 
 def _decode(arr):
@@ -308,8 +318,9 @@ CASES = [
 ]
 
 
+@pytest.mark.parametrize('bf16', [False, True], ids=['fp32', 'bf16'])
 @pytest.mark.parametrize('family,kw,B,T', CASES)
-def test_plan_descriptors_in_bounds(family, kw, B, T):
+def test_plan_descriptors_in_bounds(family, kw, B, T, bf16):
     from mep_amd import cmu_mosei, ren_mme
     Tl, Tv, Ta = T
     if family == 'cmu':
@@ -318,10 +329,42 @@ def test_plan_descriptors_in_bounds(family, kw, B, T):
         m = ren_mme.Base_model(dim=kw['dim'], l_len=Tl, v_len=Tv, a_len=Ta, n_heads=kw['n_heads'],
                                n_layers=kw['n_layers'])
     runner = m.mep_runner('cpu')
-    plan = runner.plan(B, T)
+    plan = runner.plan(B, T, bf16=bf16)
     n = check_plan(plan)
     assert n > 50
     assert len(plan.blocks) == 18 * kw['n_layers']
+    if bf16:
+        _check_bf16_views(plan)
+
+
+def _check_bf16_views(plan):
+    """The bf16 path's storage contract (include/mep.h MEP_PREC_BF16): every activation view the
+    bf16 kernels read or write as bf16 points into a bf16 buffer, the pooled tensor, scores and
+    statistics into fp32 ones -- a view into a buffer of the other width would be read as garbage."""
+    c = Checker(plan)
+    half = lambda r: r.ptr == 0 or c.elsize(r.ptr) == 2     # noqa: E731
+    full = lambda r: r.ptr == 0 or c.elsize(r.ptr) == 4     # noqa: E731
+    for d in _decode(plan.d_unify):
+        assert d.bf16 == 3 and half(d.x) and half(d.y)
+    for arr in plan.d_attn:
+        for d in _decode(arr):
+            assert all(half(getattr(d, k)) for k in ('q', 'k', 'v', 'x'))
+    for arr in plan.d_attnb:
+        for d in _decode(arr):
+            assert all(half(getattr(d, k)) for k in ('dx', 'dq', 'dk', 'dv'))
+    for arr in plan.d_epi:
+        for d in _decode(arr):
+            assert all(half(getattr(d, k)) for k in ('q', 'x', 'xp', 'z', 'out_h')) and full(d.out)
+    for arr in plan.d_epib:
+        for d in _decode(arr):
+            assert all(half(getattr(d, k)) for k in ('dout2', 'dz', 'dxp', 'dx', 'dq'))
+    for d in _decode(plan.d_wgrad):
+        assert d.bf16 == 3 and half(d.a) and all(half(d.b[i]) for i in range(d.n_b))
+    for d in _decode(plan.d_sum):
+        assert d.accumulate == 2 and half(d.out) and all(half(d.src[i]) for i in range(d.n_src))
+    for name in ('d_uln', 'd_ulnb'):
+        for d in _decode(getattr(plan, name, None)):
+            assert d.bf16 == 2 and all(half(getattr(d, k)) for k in ('x', 'y', 'dy', 'dx'))
 
 
 RF_CASES = [
