@@ -78,8 +78,12 @@ KERNEL_OF = {'mep_attn_bwd': 'k_attn_bwd', 'mep_attn_fwd': 'k_attn_fwd', 'mep_bl
 def pmc_traffic(launch, tag='cfg3'):
     """(HBM bytes per dispatch, source file) of the kernel behind `launch` from the newest
     committed PMC pass of this workload that measured it (profiles/r<round>_v<n>_pmc.json for cfg3
-    fp32, profiles/r<round>_v<n>_pmc_<config>[_bf16].json for the others: (2 FETCH_SIZE +
-    WRITE_SIZE) x 1024, the gfx950 correction of MI355X_MICROARCH.md section HBM), or (None, None)."""
+    fp32, profiles/r<round>_v<n>_pmc_<config>[_bf16].json for the others), or (None, None).
+    Round 4 on (scripts/r4_traffic.py): reads = 32 x TCC_EA0_RDREQ_{DRAM,GMI,IO}_32B_sum, exact for
+    every request size, writes = 1024 x WRITE_SIZE.  Rounds 2-3 used (2 FETCH_SIZE + WRITE_SIZE) x
+    1024, which the r04 calibration (profiles/r04_fetch_cal.json) shows exact only for whole-line
+    (128-B) reads -- FETCH_SIZE counts 64-B requests (half-line reads such as the attention's 64-byte
+    head slices) at their full size, so the x2 doubled those."""
     def key(f):
         return [int(x) for x in re.findall(r'\d+', os.path.basename(f))]
     prefix = KERNEL_OF.get(launch)
@@ -88,7 +92,7 @@ def pmc_traffic(launch, tag='cfg3'):
     pat = 'r*_v*_pmc.json' if tag == 'cfg3' else 'r*_v*_pmc_%s.json' % tag
     for f in sorted(glob.glob(os.path.join(ROOT, 'profiles', pat)), key=key, reverse=True):
         for k, v in json.load(open(f)).items():
-            if k.startswith(prefix) and 'hbm_bytes_per_dispatch' in v:
+            if k.startswith(prefix) and isinstance(v, dict) and 'hbm_bytes_per_dispatch' in v:
                 return int(v['hbm_bytes_per_dispatch']), os.path.relpath(f, ROOT)
     return None, None
 

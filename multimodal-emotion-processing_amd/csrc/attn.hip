@@ -711,10 +711,28 @@ struct Bwd {
     // staging area while this tile computes: no VGPRs in flight, 5 load instructions per tile
     // instead of 22.  Rows past Tq fall outside the row views (no data: the area is zeroed at the
     // wave's start and later holds finite rows of earlier tiles, whose products are masked).
+    // BF (bf16 rows): 16 rows x 32 B per operand, lanes 0-31 (lane L = row L / 2, 16-byte piece
+    // L % 2) into [16][16] bf16 images at the same float offsets (half of each slot used)
     static constexpr int STG = 4 * 256 + 32;   // floats: Q, dO, O, dQ [16][16], stats [16][2]
-    MEP_DEV bool dma_ok() const { return !BF && Qb.vec && Gb.vec && Ob.vec && dQb.vec; }   // fp32 rows only
+    MEP_DEV static bool dma_view(const mep_rows& v) {   // 16-byte aligned pieces of every row
+        return BF ? ((v.ptr & 15) == 0 && v.sB % 8 == 0 && v.sT % 8 == 0) : aligned16(v);
+    }
+    MEP_DEV bool dma_ok() const {
+        return dma_view(bd.f.q) && dma_view(bd.dx) && dma_view(bd.f.x) && dma_view(bd.dq);
+    }
     MEP_DEV void stage(int qt, float* S) const {
         typedef __attribute__((address_space(3))) void lvoid;
+        if (BF) {
+            if (lane < 32) {
+                const int row = qt * 16 + (lane >> 1), col = hc + 8 * (lane & 1);
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(Qb.rs, (lvoid*)(S), 16, Qb.at(row, col), 0, 0, 0);
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(Gb.rs, (lvoid*)(S + 256), 16, Gb.at(row, col), 0, 0, 0);
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(Ob.rs, (lvoid*)(S + 512), 16, Ob.at(row, col), 0, 0, 0);
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(dQb.rs, (lvoid*)(S + 768), 16, dQb.at(row, col), 0, 0, 0);
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(rsStat, (lvoid*)(S + 1024), 4, 8 * 16 * qt + 4 * lane, 0, 0, 0);
+            }
+            return;
+        }
         const int row = qt * 16 + (lane >> 2), col = hc + 4 * (lane & 3);
         __builtin_amdgcn_raw_ptr_buffer_load_lds(Qb.rs, (lvoid*)(S), 16, Qb.at(row, col), 0, 0, 0);
         __builtin_amdgcn_raw_ptr_buffer_load_lds(Gb.rs, (lvoid*)(S + 256), 16, Gb.at(row, col), 0, 0, 0);
@@ -729,6 +747,24 @@ struct Bwd {
         typedef __attribute__((address_space(3))) const f32x4 lcf4;
         typedef __attribute__((address_space(3))) const f32x2 lcf2;
         lcf* L = (lcf*)S;
+        if (BF) {
+            typedef __attribute__((address_space(3))) const unsigned short lcu16;
+            typedef __attribute__((address_space(3))) const u32x2 lcu2;
+            lcu16* H = (lcu16*)S;                 // operand o at H + 512 o: [16 rows][16] bf16
+            const u32x2 qa = *(lcu2*)(H + 16 * c + 4 * g), da = *(lcu2*)(H + 512 + 16 * c + 4 * g);
+            in.qa[0] = bf_lo(qa[0]); in.qa[1] = bf_hi(qa[0]); in.qa[2] = bf_lo(qa[1]); in.qa[3] = bf_hi(qa[1]);
+            in.da[0] = bf_lo(da[0]); in.da[1] = bf_hi(da[0]); in.da[2] = bf_lo(da[1]); in.da[3] = bf_hi(da[1]);
+#pragma unroll
+            for (int s4 = 0; s4 < 4; ++s4) {
+                const int r = (4 * g + s4) * 16 + c;
+                in.qb[s4] = __builtin_bit_cast(float, (unsigned)H[r] << 16);
+                in.db[s4] = __builtin_bit_cast(float, (unsigned)H[512 + r] << 16);
+                in.ob[s4] = __builtin_bit_cast(float, (unsigned)H[1024 + r] << 16);
+                in.dqo[s4] = __builtin_bit_cast(float, (unsigned)H[1536 + r] << 16);
+                in.st[s4] = *(lcf2*)(L + 1024 + 2 * (4 * g + s4));
+            }
+            return;
+        }
         const f32x4 qa = *(lcf4*)(L + 16 * c + 4 * g), da = *(lcf4*)(L + 256 + 16 * c + 4 * g);
 #pragma unroll
         for (int e = 0; e < 4; ++e) { in.qa[e] = qa[e]; in.da[e] = da[e]; }

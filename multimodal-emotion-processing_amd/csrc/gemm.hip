@@ -11,6 +11,8 @@
 #include "common.h"
 #include "split.h"
 
+#include <type_traits>
+
 using namespace mep;
 
 namespace {
@@ -225,13 +227,25 @@ MEP_DEV void wg_stamp(int k, unsigned long long v) {
 // (the load's SGPR soffset) and the column tile an immediate: no address arithmetic per token.
 template <int MT, int KT, int NPART, bool LIN, int WG_SLOTS>
 MEP_DEV void wgrad_task(const mep_wgrad_desc& d, int t_begin, int t_end, int slot, int kbase, lfloat* red) {
-    // the bf16 path (one part) reads bf16 operand rows (MEP_BF16_STORE): 2-byte elements
+    // The bf16 path (one part) reads bf16 operand rows (MEP_BF16_STORE, 2-byte elements) as
+    // column PAIRS: per 8-token block and 32-column tile a lane loads 4 dwords -- columns
+    // 2(c & 15), +1 of tokens 4(c >> 4) .. +3 of its lane half's 8 -- and one v_permlane16_swap
+    // per operand dword trades the odd column of tokens 0-3 (lane c < 16) for the even column of
+    // tokens 4-7 (lane c + 16).  Lane c < 16 then holds column 2c, lane c + 16 column 2c + 1, each
+    // for all 8 tokens: MFMA row / column m is tensor column sg(m) = 2(m & 15) + (m >> 4) of the
+    // tile (undone when the accumulators are written).  Half the load instructions of the fp32
+    // path (dword per column), no conversion; LIN views only (the bf16 plans' views all are).
     constexpr bool HS = NPART == 1;
+    static_assert(!HS || LIN, "bf16 operand rows need linear views");
     constexpr int ES = HS ? 2 : 4;
-    auto ld = [&](__amdgpu_buffer_rsrc_t rs, int voff, int soff) -> float {
-        if (HS) return __builtin_bit_cast(float, (unsigned)__builtin_amdgcn_raw_buffer_load_b16(rs, voff, soff, 0) << 16);
-        return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, voff, soff, 0));
+    constexpr int NE = HS ? 4 : 8;                         // operand registers per tile and block
+    typedef typename AElem<HS>::T RT0;
+    typedef std::conditional_t<HS, unsigned, float> RT;
+    auto ld = [&](__amdgpu_buffer_rsrc_t rs, int voff, int soff) -> RT {
+        if constexpr (HS) return __builtin_amdgcn_raw_buffer_load_b32(rs, voff, soff, 0);
+        else return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, voff, soff, 0));
     };
+    (void)sizeof(RT0);
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int c = lane & 31, h = lane >> 5;
     const int N = d.N;
@@ -289,27 +303,29 @@ MEP_DEV void wgrad_task(const mep_wgrad_desc& d, int t_begin, int t_end, int slo
 #pragma unroll
     for (int j = 0; j < KT; ++j) wB[j] = bsB[j] - T * bsT[j];
 
-    float ra[WG_SLOTS][MT][8], rb[WG_SLOTS][KT][8];
+    RT ra[WG_SLOTS][MT][NE], rb[WG_SLOTS][KT][NE];
     // LIN addressing: half h's tokens start at w0 + h * half; token 8 s + e of the half is at
     // base + (8 s + e) * step (bytes, soffset); columns unclamped (a column past N / Ktot reads
     // neighbouring data or 0 and only feeds output entries that are never stored)
     const int t0 = min(w0 + h * half, d.ntok);
     const int stA = ES * (LIN ? wg_step(d.a) : 0);
     int stB[KT], baseB[KT];
-    const int baseA = LIN ? t0 * stA + ES * c : 0;
+    // HS: column pair 2 (c & 15) of tokens 4 (c >> 4) + e (the lane's token offset in its base)
+    const int lcol = HS ? 2 * (c & 15) : c, ltok = HS ? 4 * (c >> 4) : 0;
+    const int baseA = LIN ? (t0 + ltok) * stA + ES * lcol : 0;
 #pragma unroll
     for (int j = 0; j < KT; ++j) {
         int k0 = min(kbase + 32 * j, d.Ktot - 1), o = 0;
         while (o < d.n_b - 1 && k0 >= d.kb[o]) { k0 -= d.kb[o]; ++o; }
         stB[j] = LIN ? ES * wg_step(d.b[o]) : 0;
-        baseB[j] = LIN ? t0 * stB[j] + ES * (k0 + c) : 0;
+        baseB[j] = LIN ? (t0 + ltok) * stB[j] + ES * (k0 + lcol) : 0;
     }
     int blk = 0;   // LIN: next k block to load
     auto load_lin = [&](int p, bool checked) {
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-            const int tk = 8 * blk + e;
-            const bool ok = !checked || tk < nh;
+        for (int e = 0; e < NE; ++e) {
+            const int tk = 8 * blk + e;                   // wave-uniform part of the token
+            const bool ok = !checked || tk + ltok < nh;
             const int va = ok ? baseA : WG_INV;
             // per-token offsets are wave-uniform: readfirstlane keeps them in SGPRs (a VGPR
             // soffset would turn every load into a waterfall loop)
@@ -328,11 +344,11 @@ MEP_DEV void wgrad_task(const mep_wgrad_desc& d, int t_begin, int t_end, int slo
 #pragma unroll
             for (int q = 0; q < WG_SLOTS; ++q) {
 #pragma unroll
-                for (int e = 0; e < 8; ++e) {
+                for (int e = 0; e < NE; ++e) {
 #pragma unroll
-                    for (int i = 0; i < MT; ++i) ra[q][i][e] = 0.f;
+                    for (int i = 0; i < MT; ++i) ra[q][i][e] = 0;
 #pragma unroll
-                    for (int j = 0; j < KT; ++j) rb[q][j][e] = 0.f;
+                    for (int j = 0; j < KT; ++j) rb[q][j][e] = 0;
                 }
             }
         }
@@ -343,7 +359,7 @@ MEP_DEV void wgrad_task(const mep_wgrad_desc& d, int t_begin, int t_end, int slo
             if (8 * blk + 8 <= n - half) load_lin(p, false);   // every token of both halves valid
             else load_lin(p, true);
             return;
-        }
+        } else {
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
             const bool ok = idx < nh;
@@ -360,6 +376,7 @@ MEP_DEV void wgrad_task(const mep_wgrad_desc& d, int t_begin, int t_end, int slo
 #pragma unroll
             for (int j = 0; j < KT; ++j) offB[j] += bsT[j] + (wrap ? wB[j] : 0);
         }
+        }
     };
     auto mma = [&](int p) {
 #ifdef MEP_WG_NOMMA   // timing-only development build: loads kept live by one add each, no products
@@ -373,14 +390,25 @@ MEP_DEV void wgrad_task(const mep_wgrad_desc& d, int t_begin, int t_end, int slo
         return;
 #endif
         OpN<NPART> bo[KT];
+        auto op = [&](const RT (&v)[NE]) -> OpN<NPART> {
+            if constexpr (HS) {
+                // even / odd columns of tokens 0-3 (own) ... then the swap (see above)
+                unsigned e0 = (v[0] & 0xffffu) | (v[1] << 16), e1 = (v[2] & 0xffffu) | (v[3] << 16);
+                unsigned o0 = (v[0] >> 16) | (v[1] & 0xffff0000u), o1 = (v[2] >> 16) | (v[3] & 0xffff0000u);
+                const auto s0 = __builtin_amdgcn_permlane16_swap(e0, o0, false, false);
+                const auto s1 = __builtin_amdgcn_permlane16_swap(e1, o1, false, false);
+                OpN<NPART> o;
+                o.p[0] = __builtin_bit_cast(bf16x8, u32x4{s0[0], s1[0], s0[1], s1[1]});
+                return o;
+            } else {
+                return opn<NPART>(f32x4{v[0], v[1], v[2], v[3]}, f32x4{v[4], v[5], v[6], v[7]});
+            }
+        };
 #pragma unroll
-        for (int j = 0; j < KT; ++j)
-            bo[j] = opn<NPART>(f32x4{rb[p][j][0], rb[p][j][1], rb[p][j][2], rb[p][j][3]},
-                               f32x4{rb[p][j][4], rb[p][j][5], rb[p][j][6], rb[p][j][7]});
+        for (int j = 0; j < KT; ++j) bo[j] = op(rb[p][j]);
 #pragma unroll
         for (int i = 0; i < MT; ++i) {
-            const OpN<NPART> ao = opn<NPART>(f32x4{ra[p][i][0], ra[p][i][1], ra[p][i][2], ra[p][i][3]},
-                                             f32x4{ra[p][i][4], ra[p][i][5], ra[p][i][6], ra[p][i][7]});
+            const OpN<NPART> ao = op(ra[p][i]);
 #pragma unroll
             for (int j = 0; j < KT; ++j) acc[i][j] = mma_n<NPART>(ao, bo[j], acc[i][j]);
         }
@@ -434,13 +462,16 @@ MEP_DEV void wgrad_task(const mep_wgrad_desc& d, int t_begin, int t_end, int slo
     constexpr int LDR = 32 * KT + 8;            // == 8 mod 16: lane halves 32 banks apart
     constexpr int BUF = 32 * MT * LDR;
     lfloat* mine = red + (wave & 1) * BUF;
+    // MFMA row / column -> tile column (HS: sg(m) = 2 (m & 15) + (m >> 4), the pair layout)
+    auto sg = [](int m) { return HS ? 2 * (m & 15) + (m >> 4) : m; };
+    const int cc = sg(c);
     if (wave >= 2) {
 #pragma unroll
         for (int i = 0; i < MT; ++i)
 #pragma unroll
             for (int j = 0; j < KT; ++j)
 #pragma unroll
-                for (int r = 0; r < 16; ++r) mine[(32 * i + acc_row(r, lane)) * LDR + 32 * j + c] = acc[i][j][r];
+                for (int r = 0; r < 16; ++r) mine[(32 * i + sg(acc_row(r, lane))) * LDR + 32 * j + cc] = acc[i][j][r];
     }
     __syncthreads();
     if (wave < 2) {
@@ -450,7 +481,7 @@ MEP_DEV void wgrad_task(const mep_wgrad_desc& d, int t_begin, int t_end, int slo
             for (int j = 0; j < KT; ++j)
 #pragma unroll
                 for (int r = 0; r < 16; ++r) {
-                    lfloat* q = mine + (32 * i + acc_row(r, lane)) * LDR + 32 * j + c;
+                    lfloat* q = mine + (32 * i + sg(acc_row(r, lane))) * LDR + 32 * j + cc;
                     *q = acc[i][j][r] + *q;
                 }
     }
@@ -462,6 +493,12 @@ MEP_DEV void wgrad_task(const mep_wgrad_desc& d, int t_begin, int t_end, int slo
         if (k < kcnt) part[(int64_t)nn * d.Ktot + k] = red[nn * LDR + k] + red[BUF + nn * LDR + k];
     }
     MEP_WG_STAMP(3);
+}
+
+// a descriptor this instance cannot run: NaN partials (loudly wrong, never silently)
+MEP_DEV void wg_nan_partial(const mep_wgrad_desc& d, int slot) {
+    gfloat* part = G<float>(d.partial) + (int64_t)slot * d.N * d.Ktot;
+    for (int e = threadIdx.x; e < d.N * d.Ktot; e += WG_THREADS) part[e] = __builtin_nanf("");
 }
 
 // Flat grid of n_wg workgroups.  The map after the n_desc descriptors: off[n_wg + 1] (CSR), then
@@ -497,12 +534,12 @@ __global__ __launch_bounds__(WG_THREADS) __attribute__((amdgpu_waves_per_eu(wg_o
         case 8 * M + K:                                                                        \
             if constexpr (K > wg_kt(M, BF)) break;   /* not a tile block of this instance */   \
             if (lin) wgrad_task<M, K, BF ? 1 : MEP_WG_PARTS, true, BF ? WG_SLOTS_B : WG_SLOTS_F>(d, t_begin, t_end, slot, kbase, red);  \
-            else wgrad_task<M, K, BF ? 1 : MEP_WG_PARTS, false, BF ? WG_SLOTS_B : WG_SLOTS_F>(d, t_begin, t_end, slot, kbase, red);     \
+            else if constexpr (!BF) wgrad_task<M, K, MEP_WG_PARTS, false, WG_SLOTS_F>(d, t_begin, t_end, slot, kbase, red);         \
+            else wg_nan_partial(d, slot);   /* bf16 rows: linear views only */                                                       \
             break;
         // the bf16-path instance needs bf16 operands AND bf16 operand rows (MEP_BF16_OPS | MEP_BF16_STORE)
         if ((d.bf16 != 0) != BF || (BF && d.bf16 != (MEP_BF16_OPS | MEP_BF16_STORE))) {
-            gfloat* part = G<float>(d.partial) + (int64_t)slot * d.N * d.Ktot;
-            for (int e = threadIdx.x; e < d.N * d.Ktot; e += WG_THREADS) part[e] = __builtin_nanf("");
+            wg_nan_partial(d, slot);
             continue;
         }
         switch (8 * mt + kt) {
@@ -960,7 +997,9 @@ __global__ __launch_bounds__(UN_THREADS) void k_unify(const mep_gemm_desc* __res
     if (tile_lo >= tile_hi) return;   // whole workgroup
     __shared__ __attribute__((aligned(16))) float smem[UN_LDS];
     const bool hs = d.bf16 & MEP_BF16_STORE;   // bf16 X / Y rows
-    const bool xv = (d.K % 4 == 0) && ((d.x.ptr & (hs ? 7 : 15)) == 0) && (d.x.sB % 4 == 0) && (d.x.sT % 4 == 0);
+    // bf16 rows: 8-byte loads whenever the rows are 8-byte aligned -- columns past K meet zero
+    // weight columns (staged as zeros), and the plans pad their bf16 feature rows with zeros
+    const bool xv = (hs || d.K % 4 == 0) && ((d.x.ptr & (hs ? 7 : 15)) == 0) && (d.x.sB % 4 == 0) && (d.x.sT % 4 == 0);
     const int np = d.N >= 64 ? 2 : 1, nip = d.N / (16 * np);
     if (d.bf16) {
         // W [N][K] -> rounded bf16 units in LDS (zero past K) when N * RS fits

@@ -242,6 +242,9 @@ def make_wgrad(items, dev, tok_per_split=None, bf16=False):
             # k_wgrad: one token -> (b, t) map for every view of the item; 32-bit byte offsets
             assert v.T == a.T, 'wgrad views of one item must share T'
             assert 4 * ((cdiv(n, v.T) - 1) * v.sB + (v.T - 1) * v.sT + w) < 2 ** 31
+            if bf16:   # bf16 rows read as column-pair dwords: 4-byte aligned rows, linear views
+                assert v.ptr % 4 == 0 and v.sB % 2 == 0 and v.sT % 2 == 0, 'bf16 wgrad rows must be 4-byte aligned'
+                assert v.T == 1 or v.sB == v.T * v.sT, 'bf16 wgrad views must be linear in the token' 
         ns = max(1, ns)
         pad = [(Rows(), 0, 0, 0)] * (_lib.WG_MAX_B - len(bs))
         allb = list(bs) + pad
@@ -335,7 +338,10 @@ class TriModalPlan:
         # ---------------- static input buffers ([B, 2, T, d] prev/cur layout)
         # encoder-major [E, B, T, d]: each encoder's input rows are contiguous (linear in the token,
         # the fast addressing of k_wgrad); the masks keep the [B, E, T] prev/cur layout
-        self.x_in = {m: torch.zeros(E, B, self.T[m], d, **act) for m, d in zip(MODS, sp.dims)}
+        # bf16 feature rows padded to 8 elements (16 bytes): the bf16 kernels read column pairs
+        # as dwords (k_wgrad) and 4 columns as 8 bytes (unify); the pad columns stay zero
+        self.dpad = {m: (-(-d // 8) * 8 if self.bf16 else d) for m, d in zip(MODS, sp.dims)}
+        self.x_in = {m: torch.zeros(E, B, self.T[m], self.dpad[m], **act) for m in MODS}
         self.m_in = {m: torch.zeros(B, E, self.T[m], **f32) for m in MODS}
         self.labels = torch.zeros(B, NC, dtype=torch.float32 if labels_float else torch.int64, device=dev)
         # dropout {seed, row0} (include/mep.h mep_epi_desc.seed), usually the runner's shared state
@@ -423,7 +429,8 @@ class TriModalPlan:
     def _in_rows(self, e, m):
         d = self.spec.dims[MODS.index(m)]
         T = self.T[m]
-        return rows(self.x_in[m], T, T * d, d, e * self.B * T * d)
+        dp = self.dpad[m]
+        return rows(self.x_in[m], T, T * dp, dp, e * self.B * T * dp)
 
     # ------------------------------------------------------------------ descriptors
     def _build_descriptors(self):
@@ -668,10 +675,10 @@ class TriModalPlan:
             for m, x, mk in (('l', l, lm), ('v', v, vm), ('a', a, am)):
                 if isinstance(x, (tuple, list)):      # (prev, cur) pair of [B, T, d]
                     for e in range(2):
-                        self.x_in[m][e].copy_(x[e])
+                        self.x_in[m][e, ..., :x[e].shape[-1]].copy_(x[e])
                         self.m_in[m][:, e].copy_(mk[e])
                 else:                                 # [B, 2, T, d]
-                    self.x_in[m].copy_(x.transpose(0, 1))
+                    self.x_in[m][..., :x.shape[-1]].copy_(x.transpose(0, 1))
                     self.m_in[m].copy_(mk)
             if labels is not None:
                 self.labels.copy_(labels)

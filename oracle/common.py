@@ -52,9 +52,26 @@ def linear(x, w, b=None):
     return y if b is None else y + b
 
 
+# Max-pool routing hook (test infrastructure: tests/test_gpu_bf16.py, make_bf16_budget.py).  A bf16
+# execution picks different max-pool argmaxes than the fp32 one wherever two time steps are within
+# bf16 noise, and one such flip moves a block's whole gradient: the bf16 checks compare against
+# the fp32 arithmetic on the SAME routing.  POOL_ROUTE: None, or a list of [B, C] time indices
+# consumed one per pool call (in call order: intensity, then stimulation); the max half of the pool
+# then gathers x at those steps (and its gradient goes to them).  POOL_SEEN collects the indices
+# every call used (torch.max's first-index tie rule when not routed).
+POOL_ROUTE = None
+POOL_SEEN = []
+
+
 def mean_max_pool(x):
     """cat(mean over time, max over time) -- cmu-mosei/run.py:318 (padded rows included)."""
-    return torch.cat([x.mean(dim=1), x.max(dim=1)[0]], dim=1)
+    if POOL_ROUTE:
+        idx = POOL_ROUTE.pop(0).to(x.device).long()
+        mx = x.gather(1, idx.unsqueeze(1)).squeeze(1)
+    else:
+        mx, idx = x.max(dim=1)
+    POOL_SEEN.append(idx.detach().clone())
+    return torch.cat([x.mean(dim=1), mx], dim=1)
 
 
 def bilinear_transfer(this, last, trans):

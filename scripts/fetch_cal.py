@@ -46,6 +46,8 @@ def main():
     write = counters(os.path.join(src, 'cal_write'), {'WRITE_SIZE'})
     req = counters(os.path.join(src, 'cal_req'), {'TCC_EA0_RDREQ_sum', 'TCC_EA0_RDREQ_32B_sum',
                                                   'TCC_EA0_WRREQ_sum', 'TCC_EA0_WRREQ_64B_sum'})
+    rd32 = ('TCC_EA0_RDREQ_DRAM_32B_sum', 'TCC_EA0_RDREQ_GMI_32B_sum', 'TCC_EA0_RDREQ_IO_32B_sum')
+    req2 = counters(os.path.join(src, 'cal_req2'), set(rd32)) if os.path.isdir(os.path.join(src, 'cal_req2')) else {}
 
     def find(tab, name):
         # rocprof kernel names carry the template arguments: k_rd<4> -> "k_rd<4>" or "void k_rd<4>"
@@ -69,11 +71,18 @@ def main():
                 e[c] = q[c]
         if q.get('TCC_EA0_RDREQ_sum'):
             e['bytes_per_rdreq'] = round(kd['bytes'] / q['TCC_EA0_RDREQ_sum'], 2)
+        q2 = find(req2, name)
+        if q2:
+            units = sum(q2.get(c, 0.0) for c in rd32)
+            e.update({c: q2[c] for c in rd32 if c in q2})
+            if units and not name.startswith('k_wr'):
+                e['rd32_factor'] = round(kd['bytes'] / (32 * units), 4)   # 1.0: 32 x units is exact
         out['kernels'][name] = e
     json.dump(out, open(dst, 'w'), indent=1)
     for k, e in out['kernels'].items():
-        print('%-22s %6.3f TB/s  fetch x%-7s write x%-7s B/rdreq %s' % (k, e['TBps'], e.get('fetch_factor', '-'),
-                                                                      e.get('write_factor', '-'), e.get('bytes_per_rdreq', '-')))
+        print('%-22s %6.3f TB/s  fetch x%-7s write x%-7s B/rdreq %-7s 32B-units x%s' % (
+            k, e['TBps'], e.get('fetch_factor', '-'), e.get('write_factor', '-'), e.get('bytes_per_rdreq', '-'),
+            e.get('rd32_factor', '-')))
 
 
 if __name__ == '__main__':

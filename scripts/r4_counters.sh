@@ -5,12 +5,14 @@
 #      counts per access width) -> the per-width correction (scripts/fetch_cal.py)
 #   2. SQ instruction / cycle / MFMA / LDS-conflict groups over every kernel of the bench workloads
 #      (cfg3, cfg3 bf16, cfg2, cfg5) -> per-kernel MFMA utilisation (scripts/r4_ctr_summary.py)
-#   STAGE=cal|sq|all CFGS="cfg3 cfg2 cfg5" bash scripts/r4_counters.sh
+#   3. traffic: kernel trace + stats and the read / write byte counters per workload
+#   STAGE=cal|sq|traffic|all CFGS="cfg3 cfg2 cfg5" bash scripts/r4_counters.sh
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 OUT=gpurun_out/r4ctr
 mkdir -p $OUT
 STAGE=${STAGE:-all}
+RD32="TCC_EA0_RDREQ_DRAM_32B_sum TCC_EA0_RDREQ_GMI_32B_sum TCC_EA0_RDREQ_IO_32B_sum TCC_EA0_RDREQ_sum"
 pass() { local dir=$1; shift
   timeout -k 10 ${PT:-240} "$@" > $OUT/$dir.log 2>&1; local rc=$?
   echo "$dir rc=$rc"
@@ -21,6 +23,22 @@ if [ $STAGE = cal ] || [ $STAGE = all ]; then
   pass cal_fetch rocprofv3 --pmc FETCH_SIZE --kernel-trace -d $OUT/cal_fetch -o run --output-format csv -- ./scripts/micro/fetch_cal
   pass cal_write rocprofv3 --pmc WRITE_SIZE --kernel-trace -d $OUT/cal_write -o run --output-format csv -- ./scripts/micro/fetch_cal
   pass cal_req rocprofv3 --pmc TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum --kernel-trace -d $OUT/cal_req -o run --output-format csv -- ./scripts/micro/fetch_cal
+  # bytes by request size: 32 B units of DRAM / GMI / IO read requests (a 64-B request counts 2,
+  # a 128-B one 4)
+  pass cal_req2 rocprofv3 --pmc $RD32 --kernel-trace -d $OUT/cal_req2 -o run --output-format csv -- ./scripts/micro/fetch_cal
+fi
+if [ $STAGE = traffic ] || [ $STAGE = all ]; then
+  # per workload: kernel trace + stats, the 32-B read units and WRITE_SIZE (separate passes)
+  for cfg in ${CFGS:-cfg3 cfg3_bf16 cfg2 cfg5 cfg5_bf16}; do
+    case $cfg in
+      cfg3) A="--config cfg3";; cfg3_bf16) A="--config cfg3 --dtype bf16";;
+      cfg2) A="--config cfg2";; cfg5) A="--config cfg5";; cfg5_bf16) A="--config cfg5 --dtype bf16";;
+    esac
+    B="--steps ${PSTEPS:-30} --warmup 5 --no-cpu-baseline $A"
+    pass ${cfg}_trace rocprofv3 --kernel-trace --stats -d $OUT/${cfg}_trace -o run --output-format csv -- python3 bench.py $B
+    pass ${cfg}_rd rocprofv3 --pmc $RD32 --kernel-trace -d $OUT/${cfg}_rd -o run --output-format csv -- python3 bench.py $B
+    pass ${cfg}_wr rocprofv3 --pmc WRITE_SIZE --kernel-trace -d $OUT/${cfg}_wr -o run --output-format csv -- python3 bench.py $B
+  done
 fi
 if [ $STAGE = sq ] || [ $STAGE = all ]; then
   G1="SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS GRBM_GUI_ACTIVE"

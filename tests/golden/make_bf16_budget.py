@@ -9,6 +9,18 @@ parameters against the fixture's fp32 values are written to bf16_budget.json.
 tests/test_gpu_bf16.py holds the HIP bf16 path to this budget: on the same inputs it must be at
 least about as accurate as torch's own bf16 execution of the reference model.
 
+Routing and spread.  A bf16 execution picks other max-pool argmaxes than the fp32 one
+wherever two time steps are within bf16 noise, and one such flip moves a block's whole gradient --
+a heavy-tailed, per-execution effect, not an arithmetic error.  So every error here is measured
+against the fp32 step on the SAME routing (the bf16 run's own argmaxes replayed in fp32 through
+oracle/common.py POOL_ROUTE), which leaves the continuous bf16 rounding error; and the budget is
+the WORST of RUNS executions: the fixture as it is, and RUNS - 1 runs with every parameter scaled by
+(1 + 2^-18 N(0, 1)) -- far below bf16's 2^-9 rounding, enough to move the bf16 roundings a
+different execution would move.  Every per-tensor, logits, loss and whole-gradient figure is the
+maximum over the runs (post_frac the minimum), and 'runs' records how many.  tests/test_gpu_bf16.py
+measures the HIP bf16 path the same way (its own argmaxes, plan.argmax, replayed in the fp32
+oracle).
+
     python tests/golden/make_bf16_budget.py
 """
 import json
@@ -27,33 +39,76 @@ CASES = ['cmu_small_l2', 'cmu_cfg3', 'ren_small', 'ren_ref', 'ren_cfg5']
 LR = 1e-3
 
 
+RUNS = 4
+EPS = 2.0 ** -18
+
+
 def budget(name):
+    recs = [one_run(name, r) for r in range(RUNS)]
+    out = {'runs': RUNS, 'perturb_eps': EPS}
+    for k in ('logits', 'loss', 'grad_all'):
+        out[k] = max(r[k] for r in recs)
+    out['grads'] = {k: max(r['grads'][k] for r in recs) for k in recs[0]['grads']}
+    if 'post_frac' in recs[0]:
+        out['post_frac'] = min(r['post_frac'] for r in recs)
+    out['base'] = {k: recs[0][k] for k in ('logits', 'loss', 'grad_all')}
+    return out
+
+
+def one_run(name, run):
+    """errors of one autocast(bf16) training step against the fp32 step on the SAME max-pool
+    routing (oracle/common.py POOL_ROUTE): the bf16 execution's own argmaxes, replayed in fp32"""
+    from oracle import common
     meta, gold = fixtures.load(name)
-    with torch.autocast('cpu', dtype=torch.bfloat16):
-        out = oracle_runner.run_model_case(meta, steps=1)
-    want = torch.as_tensor(gold['logits']).double()
+    params = fixtures.params
+    if run > 0:
+        def perturbed(m):
+            P = params(m)
+            g = torch.Generator().manual_seed(1000 + run)
+            with torch.no_grad():
+                for p in P.values():
+                    p.mul_(1.0 + EPS * torch.randn(p.shape, generator=g, dtype=torch.float64).to(p.dtype))
+            return P
+        fixtures.params = perturbed
+    try:
+        common.POOL_SEEN, common.POOL_ROUTE = [], None
+        with torch.autocast('cpu', dtype=torch.bfloat16):
+            out = oracle_runner.run_model_case(meta, steps=1)
+        route = common.POOL_SEEN[:2]                  # the step's forward: intensity, stimulation
+        common.POOL_SEEN, common.POOL_ROUTE = [], list(route)
+        ref = oracle_runner.run_model_case(meta, steps=1)
+    finally:
+        fixtures.params = params
+        common.POOL_SEEN, common.POOL_ROUTE = [], None
+    return errors(meta, gold, out, ref)
+
+
+def errors(meta, gold, out, ref):
+    """relative errors of a bf16 step (out) against an fp32 step (ref) on the same routing;
+    gradients compared on the fixture's extent (whole tensors, or the first 256 entries)"""
+    want = ref['logits'].double()
     rec = {'logits': float((out['logits'].double() - want).abs().max() / want.abs().max()),
-           'loss': abs(float(out['loss']) - float(gold['loss'])) / abs(float(gold['loss']))}
+           'loss': abs(float(out['loss']) - float(ref['loss'])) / abs(float(ref['loss']))}
     grads, gg, rr = {}, [], []
     for k, g in out['grads'].items():
         if g is None or 'nograd/' + k in gold:
             continue
-        ref = torch.as_tensor(gold[('grad/' if meta['full'] else 'gradhead/') + k]).double().reshape(-1)
-        got = g.double().reshape(-1)[:ref.numel()]
-        grads[k] = float((got - ref).norm() / max(float(ref.norm()), 1e-30))
+        n = gold[('grad/' if meta['full'] else 'gradhead/') + k].size
+        r = ref['grads'][k].double().reshape(-1)[:n]
+        got = g.double().reshape(-1)[:n]
+        grads[k] = float((got - r).norm() / max(float(r.norm()), 1e-30))
         gg.append(got)
-        rr.append(ref)
+        rr.append(r)
     rec['grads'] = grads
     rec['grad_all'] = float((torch.cat(gg) - torch.cat(rr)).norm() / torch.cat(rr).norm())
     n_ok = n_all = 0
-    if meta['steps'] == 1:
-        for k, p in out['post'].items():
-            ref = gold['post/' + k] if meta['full'] else gold['posthead/' + k]
-            ref = torch.as_tensor(ref).double().reshape(-1)
-            err = (p.double().reshape(-1)[:ref.numel()] - ref).abs()
-            n_ok += int((err <= 0.25 * LR).sum())
-            n_all += err.numel()
-        rec['post_frac'] = n_ok / n_all
+    for k, p in out['post'].items():
+        n = gold[('post/' if meta['full'] else 'posthead/') + k].size
+        r = ref['post'][k].double().reshape(-1)[:n]
+        err = (p.double().reshape(-1)[:n] - r).abs()
+        n_ok += int((err <= 0.25 * LR).sum())
+        n_all += err.numel()
+    rec['post_frac'] = n_ok / n_all
     return rec
 
 

@@ -327,6 +327,10 @@ CASES = {
     'rf_chain_cfg2': lambda: case_chain('rf_chain_cfg2', rf_consts(50),
                                         dict(l_dim=300, v_dim=35, a_dim=74, dim=96, l_len=50, v_len=50,
                                              a_len=50, n_heads=6, n_layers=2, ffn=2), 8, 50, 2, 111),
+    # the cfg2 bench shape itself (B = 64): the wave kernels' B = 64 launches parity-pinned
+    'rf_chain_cfg2_b64': lambda: case_chain('rf_chain_cfg2_b64', rf_consts(50),
+                                            dict(l_dim=300, v_dim=35, a_dim=74, dim=96, l_len=50, v_len=50,
+                                                 a_len=50, n_heads=6, n_layers=2, ffn=2), 64, 50, 2, 112),
 }
 
 

@@ -14,10 +14,11 @@ would compute exactly this.
 Checked, eager and under graph capture:
   * the recorded ranges partition [0, n_grad) exactly once per step;
   * bucket A as the collective sees it (the snapshot) is final: times 2 it equals, bit for bit,
-    the gradient of the engine without any collective at the same step (1/(2B) loss scale times
-    the SUM's 2 is exact in fp32), so no launch of the backward was still writing it -- no
-    readiness race -- and bucket B likewise;
-  * the post-SUM gradient, loss and post-step parameters equal the no-collective engine's bit for
+    the gradient of the engine without any collective at the same step, taken right before its
+    optimizer (1/(2B) loss scale times the SUM's 2 is exact in fp32), so no launch of the backward
+    was still writing it -- no readiness race -- and bucket B likewise;
+  * the post-SUM gradient (before clip + AdamW, which scale the gradient in place as
+    clip_grad_norm_ does), loss and post-step parameters equal the no-collective engine's bit for
     bit at every step;
   * the post-step parameters equal a one-rank step on the batch concatenated with itself (2 B rows;
     summation order differs, so within fp32 noise).
@@ -88,7 +89,21 @@ def _engine(model, collective, graph):
     opt = FusedAdamW(model, lr=LR)
     # the collective engine keeps the optimizer's own norm pass (the norm follows the SUM); the
     # engines it is compared with bit for bit do too
-    return TrainEngine(model, opt, clip=1.0, rdrop=False, graph=graph, collective=collective, fold_norm=False)
+    eng = TrainEngine(model, opt, clip=1.0, rdrop=False, graph=graph, collective=collective, fold_norm=False)
+    # the flat gradient as the optimizer receives it (clip + AdamW then scale it in place), copied
+    # on the step's stream -- inside the captured graph too, so a replay refreshes the copy
+    eng.pre_opt = None
+    run_opt = eng._opt
+
+    def opt_with_copy():
+        flat = model.mep_runner(next(model.parameters()).device).flat
+        if eng.pre_opt is None:
+            assert not torch.cuda.is_current_stream_capturing()
+            eng.pre_opt = torch.empty_like(flat.grad[:flat.n_grad])
+        eng.pre_opt.copy_(flat.grad[:flat.n_grad])
+        run_opt()
+    eng._opt = opt_with_copy
+    return eng
 
 
 def _double(batch):
@@ -129,7 +144,7 @@ def _exchange_case(model_fn, batch, B, graph, monkeypatch, rdrop=False):
             want = sorted(want * 2) if k == 0 else []
         assert sorted(fake.calls) == want, ('step %d' % k, fake.calls, fl.split, fl.n_grad)
         snaps = {key: s.clone() for key, s in fake.snaps.items()}
-        c_steps.append((loss, fl.grad[:fl.n_grad].clone(), snaps, _params(mc)))
+        c_steps.append((loss, ec.pre_opt.clone(), snaps, _params(mc)))
     if graph:
         assert ec.capture_allreduce and all(b is None for (_, b) in ec._graphs.values()), \
             'the all-reduce was not captured in the step graph'
@@ -145,7 +160,7 @@ def _exchange_case(model_fn, batch, B, graph, monkeypatch, rdrop=False):
         loss = er.step(*batch).clone()
         torch.cuda.synchronize()
         lc, gc, snaps, pc = c_steps[k]
-        gr = flr.grad[:flr.n_grad]
+        gr = er.pre_opt
         a = snaps[(0, fl.split)]
         b = snaps[(fl.split, fl.n_grad - fl.split)]
         assert torch.equal(2.0 * a, gr[:fl.split]), 'step %d: bucket A was not final at its all-reduce' % k
@@ -163,10 +178,12 @@ def _exchange_case(model_fn, batch, B, graph, monkeypatch, rdrop=False):
     ed.step(*_double(batch))
     torch.cuda.synchronize()
     fld = md.mep_runner(batch[-1].device).flat
-    gd = fld.grad[:fld.n_grad]
+    gd = ed.pre_opt
     _, gc1, _, pc1 = c_steps[0]
     assert_close(gc1, gd, 1e-4, 1e-5, 'DP gradient vs the doubled batch')
-    gd_view = {n: fld.view(fld.grad, n) for n in fld.names if fld.has_grad[n]}
+    gfull = torch.zeros_like(fld.grad)
+    gfull[:fld.n_grad] = gd
+    gd_view = {n: fld.view(gfull, n) for n in fld.names if fld.has_grad[n]}
     for name, p in md.named_parameters():
         err = (pc1[name] - p.detach()).abs()
         tol = torch.full_like(err, 2e-6)

@@ -59,21 +59,24 @@ def test_wgrad_vs_torch(N, Ks, B, T, cuda):
     del keep
 
 
-@pytest.mark.parametrize('N,Ks,B,T', [CASES[1], CASES[3], CASES[5], CASES[7], CASES[8]])
+@pytest.mark.parametrize('N,Ks,B,T', [CASES[1], CASES[3], CASES[5], CASES[7], CASES[8], CASES[6]])
 def test_wgrad_bf16_vs_torch(N, Ks, B, T, cuda):
-    """bf16 path: bf16 operand rows (include/mep.h MEP_BF16_STORE), exactly the products of the
-    bf16 values (each exact in fp32), summed in fp32 -- checked against float64 sums."""
+    """bf16 path: bf16 operand rows (include/mep.h MEP_BF16_STORE), read as column-pair dwords --
+    4-byte aligned, token-linear rows (odd widths padded to even, as the plans pad the features) --
+    and exactly the products of the bf16 values (each exact in fp32), summed in fp32: checked
+    against float64 sums."""
     torch.manual_seed(N * 1000 + sum(Ks) + B * 7 + T + 1)
     n = B * T
     A = torch.randn(B, T, N, device=cuda).bfloat16()
-    Bs = [torch.randn(B, 2, T, K, device=cuda).bfloat16() for K in Ks]
+    Kp = [K + K % 2 for K in Ks]
+    Bs = [torch.randn(B, T, k, device=cuda).bfloat16() for k in Kp]
     outs = [torch.full((N, K), float('nan'), device=cuda) for K in Ks]
     item = (_rows(A, T, T * N, N), N, n,
-            [(_rows(b, T, 2 * T * K, K, T * K), K, o.data_ptr(), K) for b, K, o in zip(Bs, Ks, outs)])
+            [(_rows(b, T, T * k, k), K, o.data_ptr(), K) for b, k, K, o in zip(Bs, Kp, Ks, outs)])
     keep = _run([item], cuda, bf16=True)
     a2 = A.reshape(n, N).double()
     for b, K, o in zip(Bs, Ks, outs):
-        want = a2.t() @ b[:, 1].reshape(n, K).double()
+        want = a2.t() @ b.reshape(n, -1)[:, :K].double()
         assert_close(o, want, rtol=1e-5, atol_frac=1e-6, name='bf16 N%d K%d' % (N, K))
     del keep
 
