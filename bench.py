@@ -5,15 +5,17 @@ B=64 utterance pairs per GPU, T=50 for text (d=300), visual (d=35) and audio (d=
 forward of both encoders + head + circle loss + backward + clip_grad_norm_(1.0) + AdamW (lr 1e-3)
 [+ RCCL all-reduce of the flat gradient when N > 1].  Synthetic N(0,1) features, all-ones masks,
 Bernoulli(0.3) labels, random-init weights; inputs resident in HBM before the timed region.
-Arithmetic (--dtype fp32, default): fp32 storage, softmax, LayerNorm and accumulation; the
+Arithmetic: the dtype BASELINE.json names for the config -- bf16 for cfg3 / cfg4 / cfg5, fp32 for
+cfg2.  bf16 (the default of cfg3 / cfg5): plain bf16 operands on every encoder product with fp32
+accumulation, encoder activations stored in bf16, scores, softmax and LayerNorm statistics, pooled
+tensor, loss, gradients and AdamW in fp32; held to torch.autocast(bf16)'s own error on the oracle
+(tests/test_gpu_bf16.py).  --dtype fp32: fp32 storage, softmax, LayerNorm and accumulation; the
 products run on the matrix cores either in fp32 (v_mfma_f32_*) or as fp32 operands split into
-bf16 parts, within the 1e-4 logits parity of the fp32 reference.  --dtype bf16
-(BASELINE cfg3 / cfg5 name bf16): the same step with plain bf16 operands on every encoder product
-(fp32 accumulation, storage, softmax, LayerNorm, loss, AdamW; tests/test_gpu_bf16.py).
+bf16 parts, within the 1e-4 logits parity of the fp32 reference.
 
-    python bench.py [--gpus N --steps K --warmup W]                  BASELINE cfg3 (cfg4 with N > 1)
+    python bench.py [--gpus N --steps K --warmup W]                  BASELINE cfg3 (cfg4 with N > 1), bf16
     python bench.py --config cfg2 | cfg5                            the other BASELINE configs
-    python bench.py [--config cfg5] --dtype bf16                    the bf16 path
+    python bench.py [--config cfg5] --dtype fp32                    the fp32 (1e-4 parity) path
     torchrun --nproc-per-node N bench.py --gpus N ...                (one process per GPU, RCCL)
 Rank 0 prints one JSON line.
 """
@@ -138,6 +140,7 @@ class Cfg3:
     name = 'cfg3'
     metric = METRIC
     unit = 'utt/s'
+    baseline_dtype = 'bf16'       # BASELINE.json configs[2]: "Full tri-modal fusion ... bf16"
 
     def __init__(self, dev, rank, graph, bf16=False):
         from mep_amd import cmu_mosei
@@ -199,6 +202,7 @@ class Cfg5:
     name = 'cfg5'
     metric = 'rows/sec fwd+bwd, Ren-MME Base_model T=300 (d=768/640/205), 32 rows per MI355X'
     unit = 'rows/s'
+    baseline_dtype = 'bf16'       # BASELINE.json configs[4]: "Ren-MME long-sequence config ... bf16"
     R, TT, DIMS5 = 32, 300, (768, 640, 205)
 
     def __init__(self, dev, rank, graph, bf16=False):
@@ -272,6 +276,7 @@ class Cfg2:
     name = 'cfg2'
     metric = 'rows/sec fwd+bwd, realformer text encoder (2 residual blocks) B=64 T=50 d=300'
     unit = 'rows/s'
+    baseline_dtype = 'fp32'       # BASELINE.json configs[1]: "... realformer attention only) fp32"
 
     def __init__(self, dev, rank, graph, bf16=False):
         from mep_amd import realformer as rf
@@ -419,9 +424,12 @@ def main():
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-graph', action='store_true')
     ap.add_argument('--cpu-budget', type=float, default=12.0)
-    ap.add_argument('--dtype', default='fp32', choices=('fp32', 'bf16'),
-                    help='fp32: the 1e-4 parity path (default); bf16: bf16-operand products (cfg3 / cfg5)')
+    ap.add_argument('--dtype', default=None, choices=('fp32', 'bf16'),
+                    help="default: the config's BASELINE dtype (bf16 for cfg3 / cfg5, fp32 for cfg2); "
+                         'fp32: the 1e-4 parity path')
     args = ap.parse_args()
+    if args.dtype is None:
+        args.dtype = CONFIGS[args.config].baseline_dtype
 
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))

@@ -261,7 +261,9 @@ MEP_DEV void wgrad_task(const mep_wgrad_desc& d, int t_begin, int t_end, int slo
     // Operand columns of this lane, clamped in range: a column past N (past Ktot) only feeds
     // output rows (columns) that are never stored.  Tokens past the lane half's range read 0
     // through the buffer range check (offset WG_INV).
-    const auto rsA = __builtin_amdgcn_make_buffer_rsrc((void*)d.a.ptr, 0, wg_extent(d.a, T, d.ntok, N, ES), 0x00020000);
+    // HS: the range covers whole column pairs (a dword past the range would read as 0 -- the
+    // last row's odd last column; rows are padded to even widths, so the pad element is ours)
+    const auto rsA = __builtin_amdgcn_make_buffer_rsrc((void*)d.a.ptr, 0, wg_extent(d.a, T, d.ntok, N + (HS ? N & 1 : 0), ES), 0x00020000);
     int colA[MT];
 #pragma unroll
     for (int i = 0; i < MT; ++i) colA[i] = ES * min(32 * i + c, N - 1);
@@ -274,7 +276,7 @@ MEP_DEV void wgrad_task(const mep_wgrad_desc& d, int t_begin, int t_end, int slo
         int k0 = min(kbase + 32 * j, d.Ktot - 1), o = 0;
         while (o < d.n_b - 1 && k0 >= d.kb[o]) { k0 -= d.kb[o]; ++o; }
         const mep_rows& b = d.b[o];
-        rsB[j] = __builtin_amdgcn_make_buffer_rsrc((void*)b.ptr, 0, wg_extent(b, T, d.ntok, d.kb[o], ES), 0x00020000);
+        rsB[j] = __builtin_amdgcn_make_buffer_rsrc((void*)b.ptr, 0, wg_extent(b, T, d.ntok, d.kb[o] + (HS ? d.kb[o] & 1 : 0), ES), 0x00020000);
         colB[j] = ES * min(k0 + c, d.kb[o] - 1);
         bsB[j] = (int)b.sB;
         bsT[j] = (int)b.sT;

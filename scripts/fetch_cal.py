@@ -60,7 +60,7 @@ def main():
     for name, kd in known.items():
         e = dict(bytes=kd['bytes'], us=kd['us'], TBps=kd['TBps'])
         f, w, q = find(fetch, name), find(write, name), find(req, name)
-        if f.get('FETCH_SIZE'):
+        if f.get('FETCH_SIZE') and not name.startswith('k_wr'):     # store kernels read ~nothing
             e['fetch_kb'] = f['FETCH_SIZE']
             e['fetch_factor'] = round(kd['bytes'] / (1024 * f['FETCH_SIZE']), 4)
         if w.get('WRITE_SIZE'):
@@ -69,7 +69,7 @@ def main():
         for c in ('TCC_EA0_RDREQ_sum', 'TCC_EA0_RDREQ_32B_sum', 'TCC_EA0_WRREQ_sum', 'TCC_EA0_WRREQ_64B_sum'):
             if c in q:
                 e[c] = q[c]
-        if q.get('TCC_EA0_RDREQ_sum'):
+        if q.get('TCC_EA0_RDREQ_sum') and not name.startswith('k_wr'):
             e['bytes_per_rdreq'] = round(kd['bytes'] / q['TCC_EA0_RDREQ_sum'], 2)
         q2 = find(req2, name)
         if q2:

@@ -31,8 +31,8 @@ if [ $STAGE = traffic ] || [ $STAGE = all ]; then
   # per workload: kernel trace + stats, the 32-B read units and WRITE_SIZE (separate passes)
   for cfg in ${CFGS:-cfg3 cfg3_bf16 cfg2 cfg5 cfg5_bf16}; do
     case $cfg in
-      cfg3) A="--config cfg3";; cfg3_bf16) A="--config cfg3 --dtype bf16";;
-      cfg2) A="--config cfg2";; cfg5) A="--config cfg5";; cfg5_bf16) A="--config cfg5 --dtype bf16";;
+      cfg3) A="--config cfg3 --dtype fp32";; cfg3_bf16) A="--config cfg3 --dtype bf16";;
+      cfg2) A="--config cfg2";; cfg5) A="--config cfg5 --dtype fp32";; cfg5_bf16) A="--config cfg5 --dtype bf16";;
     esac
     B="--steps ${PSTEPS:-30} --warmup 5 --no-cpu-baseline $A"
     pass ${cfg}_trace rocprofv3 --kernel-trace --stats -d $OUT/${cfg}_trace -o run --output-format csv -- python3 bench.py $B
@@ -44,10 +44,15 @@ if [ $STAGE = sq ] || [ $STAGE = all ]; then
   G1="SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS GRBM_GUI_ACTIVE"
   G2="SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_MFMA SQ_INSTS_VALU_MFMA_MOPS_BF16 SQ_INSTS_VALU_MFMA_MOPS_F32"
   G3="SQ_VALU_MFMA_BUSY_CYCLES SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_ACTIVE_INST_VMEM SQ_WAIT_INST_LDS SQ_INST_CYCLES_VMEM_RD GRBM_GUI_ACTIVE"
-  for cfg in ${CFGS:-cfg3 cfg3_bf16 cfg2 cfg5}; do
+  # keep only the counters this rocprofv3 lists (an unknown name fails the pass)
+  timeout -k 10 120 rocprofv3 -L > $OUT/list.txt 2>&1 || true
+  known() { local out=""; for c in $1; do grep -qw "$c" $OUT/list.txt && out="$out $c"; done; echo $out; }
+  G1=$(known "$G1"); G2=$(known "$G2"); G3=$(known "$G3")
+  echo "G1: $G1"; echo "G2: $G2"; echo "G3: $G3"
+  for cfg in ${CFGS:-cfg3 cfg3_bf16 cfg2 cfg5 cfg5_bf16}; do
     case $cfg in
-      cfg3) A="--config cfg3";; cfg3_bf16) A="--config cfg3 --dtype bf16";;
-      cfg2) A="--config cfg2";; cfg5) A="--config cfg5";; cfg5_bf16) A="--config cfg5 --dtype bf16";;
+      cfg3) A="--config cfg3 --dtype fp32";; cfg3_bf16) A="--config cfg3 --dtype bf16";;
+      cfg2) A="--config cfg2";; cfg5) A="--config cfg5 --dtype fp32";; cfg5_bf16) A="--config cfg5 --dtype bf16";;
     esac
     i=0
     for grp in "$G1" "$G2" "$G3"; do

@@ -5,12 +5,14 @@
            profiles/<tag>_pmc[_<cfg>].json          (per kernel: avg_us, reads, writes)
 (no suffix for cfg3: bench.py pmc_traffic's naming).
 
-Read bytes = 32 x (TCC_EA0_RDREQ_DRAM_32B_sum + _GMI_32B_sum + _IO_32B_sum): those counters count a
-read request in 32-byte units (a 64-B request as 2, a 128-B one as 4), so they are exact for every
-request size.  FETCH_SIZE is not: it is TCC_EA0_RDREQ x 64 B, which is half the bytes of 128-B
-requests (whole-line reads) and exact for 64-B ones (the attention's 64-byte head slices of a row)
--- profiles/r04_fetch_cal.json, scripts/micro/fetch_cal.hip.  Write bytes = WRITE_SIZE x 1024
-(exact for every store width measured there)."""
+Read bytes = 32 x (TCC_EA0_RDREQ_DRAM_32B_sum + _GMI_32B_sum + _IO_32B_sum): the DRAM-side bytes
+of the read requests, in 32-byte units.  Calibrated with scripts/micro/fetch_cal.hip
+(profiles/r04_fetch_cal.json): exact for whole-line (128-B) reads of every access width, dword to
+dwordx4 and LDS-DMA; a 64-B request (a 64-byte head slice of a longer row) counts as 128 B -- and
+the 64-B slice kernels stream at half the rate of the 128-B slice kernel, so that is what such a
+read costs.  FETCH_SIZE (TCC_EA0_RDREQ x 64 B) is half the bytes of whole-line reads and exactly
+the requested bytes of 64-B ones, so no single factor corrects it.  Write bytes = WRITE_SIZE x 1024
+(exact for every store width measured)."""
 import collections
 import csv
 import glob

@@ -185,10 +185,13 @@ def _exchange_case(model_fn, batch, B, graph, monkeypatch, rdrop=False):
     gfull[:fld.n_grad] = gd
     gd_view = {n: fld.view(gfull, n) for n in fld.names if fld.has_grad[n]}
     for name, p in md.named_parameters():
+        # the suite's post-step standard (gpu_util.check_post_params): atol 2e-5, and |delta| <= 2 lr
+        # where the gradient is at rounding-noise level (|g| < 1e-6: Adam's first step follows
+        # its last ulps)
         err = (pc1[name] - p.detach()).abs()
-        tol = torch.full_like(err, 2e-6)
-        if name in gd_view:       # Adam(W) steps of noise-level gradients follow their last ulps
-            tol = torch.where(gd_view[name].abs() < 1e-7, torch.full_like(err, 2 * LR), tol)
+        tol = torch.full_like(err, 2e-5)
+        if name in gd_view:
+            tol = torch.where(gd_view[name].abs() < 1e-6, torch.full_like(err, 2 * LR + 2e-5), tol)
         assert bool((err <= tol).all()), (name, float(err.max()))
 
 
