@@ -10,9 +10,14 @@ of each kernel.  Derived per kernel:
                   products included -- a 3-part fp32 product issues 6 bf16 products)
   mfma_tflops     mfma_flops / the kernel's rocprofv3 average duration (the kernel-stats CSV)
   mfma_util       mfma_tflops / the dense bf16 peak (2.5 PFLOP/s; f32 MOPS priced at 157 TF)
-  mfma_busy       SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE x 256 CUs x 4 SIMDs)
-                  (rocprofiler's MfmaUtil formula)
-  valu_busy       SQ_ACTIVE_INST_VALU x 4 / (1024 SIMDs x GRBM_GUI_ACTIVE) (rocprofiler's VALUBusy)
+  mfma_busy       SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x duration x 2.4 GHz): the share of every
+                  SIMD's cycles its matrix core was busy
+  valu_busy       SQ_ACTIVE_INST_VALU x 4 / (1024 SIMDs x duration x 2.4 GHz) (quad-cycles)
+                  Both use the kernel's rocprofv3 duration at the 2.4 GHz peak clock, not
+                  GRBM_GUI_ACTIVE: that counter is summed over the 8 XCDs and reads high on
+                  dispatches this short (MI355X_MICROARCH.md, DVFS), which made rocprofiler's
+                  MfmaUtil / VALUBusy formulas 8-11x too small here.  Under load the clock runs
+                  at ~1.9-2.3 GHz, so these are lower bounds (by up to ~20%).
   per wave        VALU / MFMA / VMEM-read / LDS instructions, and the shares of a wave's cycles
                   waiting (SQ_WAIT_ANY), issue-stalled (SQ_WAIT_INST_ANY) and issuing
                   (SQ_ACTIVE_INST_ANY) -- quad-cycle counters, ratios only
@@ -27,6 +32,7 @@ import sys
 
 BF16_PEAK, F32_PEAK = 2.5e15, 157.3e12
 N_CU, N_SIMD = 256, 1024
+CLK = 2.4e9
 
 
 def short(name):
@@ -72,11 +78,14 @@ def main():
             e['mfma_tflops'] = round(512 * (mops_b + mops_f) / dur[k] / 1e12, 2)
             # time the issued products need at their peaks, over the kernel's time
             e['mfma_util'] = round((512 * mops_b / BF16_PEAK + 512 * mops_f / F32_PEAK) / dur[k], 4)
-        if gui:
+        if k in dur and dur[k] > 0:
+            cyc = N_SIMD * dur[k] * CLK
             if 'SQ_VALU_MFMA_BUSY_CYCLES' in c:
-                e['mfma_busy'] = round(c['SQ_VALU_MFMA_BUSY_CYCLES'] / (gui * N_CU * 4), 4)
+                e['mfma_busy'] = round(c['SQ_VALU_MFMA_BUSY_CYCLES'] / cyc, 4)
             if 'SQ_ACTIVE_INST_VALU' in c:
-                e['valu_busy'] = round(c['SQ_ACTIVE_INST_VALU'] * 4 / (N_SIMD * gui), 4)
+                e['valu_busy'] = round(c['SQ_ACTIVE_INST_VALU'] * 4 / cyc, 4)
+        if gui and k in dur and dur[k] > 0:
+            e['grbm_clock_ghz'] = round(gui / 8 / dur[k] / 1e9, 2)   # reads high on short dispatches
         if w:
             for name, ctr in (('valu', 'SQ_INSTS_VALU'), ('mfma', 'SQ_INSTS_MFMA'), ('vmem_rd', 'SQ_INSTS_VMEM_RD'),
                               ('vmem_wr', 'SQ_INSTS_VMEM_WR'), ('lds', 'SQ_INSTS_LDS'), ('salu', 'SQ_INSTS_SALU')):
