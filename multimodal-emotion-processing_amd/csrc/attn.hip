@@ -86,6 +86,15 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 #ifndef MEP_ATTN_HEADPAIR
 #define MEP_ATTN_HEADPAIR 1    // Tk > 64 kernels: heads 2j, 2j + 1 of a row on one CU / XCD (64-byte head slices of 128-byte lines)
 #endif
+#ifndef MEP_FWD_MFSUM
+#define MEP_FWD_MFSUM 1       // bf16 forward: softmax row sums on the matrix core (ones-row A operand)
+#endif
+#ifndef MEP_XG_PERMLANE
+#define MEP_XG_PERMLANE 0     // cross-lane-group max / sum with v_permlane16/32_swap (0: ds_bpermute).
+                              // Off: this hipcc miscompiles float arithmetic on the swap's second
+                              // result (x + y of the two results came out as x + x; stores of the
+                              // raw words are correct -- the weight gradient's use)
+#endif
 #ifndef MEP_FWD_LONG_WAVES_BF
 #define MEP_FWD_LONG_WAVES_BF 2   // the same, bf16 path
 #endif
@@ -246,6 +255,41 @@ MEP_DEV float mask_term(const gfloat* mask, int k, int Tk) {
 
 MEP_DEV float shfl(float v, int src) { return __shfl(v, src, 64); }
 
+// max / sum over the four lanes l, l ^ 16, l ^ 32, l ^ 48 (a query's lane groups g) with
+// v_permlane16_swap / v_permlane32_swap (VALU, no LDS round trip): the same operands in the same
+// order as x op shfl(x, l ^ 16), then op shfl(., l ^ 32)
+MEP_DEV unsigned opaque_copy(unsigned x) {
+    unsigned y;
+    asm volatile("v_mov_b32 %0, %1" : "=v"(y) : "v"(x));
+    return y;
+}
+MEP_DEV float xg_max(float x) {
+    if (!MEP_XG_PERMLANE) {
+        x = fmaxf(x, shfl(x, (int)(threadIdx.x & 63) ^ 16));
+        return fmaxf(x, shfl(x, (int)(threadIdx.x & 63) ^ 32));
+    }
+    const unsigned u = __builtin_bit_cast(unsigned, x);
+    const auto a = __builtin_amdgcn_permlane16_swap(u, opaque_copy(u), false, false);
+    const float m = fmaxf(__builtin_bit_cast(float, a[0]), __builtin_bit_cast(float, a[1]));
+    const unsigned v = __builtin_bit_cast(unsigned, m);
+    const auto b = __builtin_amdgcn_permlane32_swap(v, opaque_copy(v), false, false);
+    return fmaxf(__builtin_bit_cast(float, b[0]), __builtin_bit_cast(float, b[1]));
+}
+MEP_DEV float xg_sum(float x) {
+    if (!MEP_XG_PERMLANE) {
+        x = x + shfl(x, (int)(threadIdx.x & 63) ^ 16);
+        return x + shfl(x, (int)(threadIdx.x & 63) ^ 32);
+    }
+    const unsigned u = __builtin_bit_cast(unsigned, x);
+    const auto a = __builtin_amdgcn_permlane16_swap(u, opaque_copy(u), false, false);
+    // rows 0 / 2 of the first result hold x_l, of the second x_(l+16); rows 1 / 3: x_(l-16), x_l --
+    // x_l + x_(l^16) either way (addition of two operands commutes exactly)
+    const float t = __builtin_bit_cast(float, a[0]) + __builtin_bit_cast(float, a[1]);
+    const unsigned v = __builtin_bit_cast(unsigned, t);
+    const auto b = __builtin_amdgcn_permlane32_swap(v, opaque_copy(v), false, false);
+    return __builtin_bit_cast(float, b[0]) + __builtin_bit_cast(float, b[1]);
+}
+
 // s = dot / sqrt(hd) [+ c*sp] - 1e8 * (1 - m)      (op order of cmu-mosei/run.py:244-253); hd = 16:
 // the exact * 0.25; hd = 32 (robot_demo.py:356): a correctly rounded division by float(sqrt(32)),
 // as torch divides by the Python scalar
@@ -291,6 +335,18 @@ struct BRowT {
 #pragma unroll
             for (int e = 0; e < 4; ++e) dst[e] = ld1(voff + ES * e);
         }
+    }
+    // HS only: 4 bf16 elements as the two operand words {e0 | e1 << 16, e2 | e3 << 16} (no fp32
+    // round trip), and one element as a zero-extended word
+    MEP_DEV u32x2 ld4raw(int voff) const {
+        if (vec) return __builtin_bit_cast(u32x2, __builtin_amdgcn_raw_buffer_load_b64(rs, voff, 0, 0));
+        unsigned e[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) e[i] = ld1raw(voff + 2 * i);
+        return u32x2{e[0] | (e[1] << 16), e[2] | (e[3] << 16)};
+    }
+    MEP_DEV unsigned ld1raw(int voff, int soff = 0) const {
+        return (unsigned)__builtin_amdgcn_raw_buffer_load_b16(rs, voff, soff, 0);
     }
     MEP_DEV void st1(int voff, int soff, float v) const {
         if (HS) __builtin_amdgcn_raw_buffer_store_b16((unsigned short)pk(v, 0.f), rs, voff, soff, 0);
@@ -364,20 +420,35 @@ MEP_DEV void attn_fwd_task(const mep_attn_desc& d, int qc, int h, int b, int lan
             l[qt] = 0.f;
         }
     }
+    // O^T = V^T P^T: the accumulator lane (c, g) holds query c, dims 4g .. 4g+3 of each head
+    // block, so the row's 1/sum is the lane's own and a row's 4 dims are one 16-byte (8-byte bf16)
+    // store.  BF: 1/sum as v_rcp_f32 (fp32: the IEEE division)
+    // lq: BF -- the row's full sum already (from the ones-row MFMA); fp32 -- this lane's keys
     auto finish = [&](int qt, const floatx4 (&oq)[NHB], float mq, float lq) {
-        float lt = lq + shfl(lq, lane ^ 16);
-        lt += shfl(lt, lane ^ 32);
-        const float inv = 1.0f / lt;
+        const float lt = BF && MEP_FWD_MFSUM ? lq : xg_sum(lq);
+        const float inv = BF ? __builtin_amdgcn_rcpf(lt) : 1.0f / lt;
         const int q = q_lo + qt * 16 + c;
         if (g == 0 && q < Tq) {
             stats[2 * (sbase + q)] = mq;
             stats[2 * (sbase + q) + 1] = inv;
         }
 #pragma unroll
-        for (int hb = 0; hb < NHB; ++hb) {
-            const int ox = Xb.at(q_lo + qt * 16 + 4 * g, hc + 16 * hb + c);   // rows past Tq: dropped
-#pragma unroll
-            for (int r = 0; r < 4; ++r) Xb.st1(ox, r * Xb.sT4, oq[hb][r] * shfl(inv, 4 * g + r));
+        for (int hb = 0; hb < NHB; ++hb)   // rows past Tq: dropped by the range check
+            Xb.st4(Xb.at(q, hc + 16 * hb + 4 * g), f32x4{oq[hb][0] * inv, oq[hb][1] * inv, oq[hb][2] * inv, oq[hb][3] * inv});
+    };
+    // 4 consecutive row elements (columns 4g ..) as a score operand: the fp32 path's 3-part
+    // split, the bf16 path's raw words (no fp32 round trip)
+    auto ld_op = [&](const BRowT<BF>& R, int off) -> S3 {
+        if constexpr (BF) {
+            const u32x2 w = R.ld4raw(off);
+            S3 r{};
+            r.a0 = w[0];
+            r.a1 = w[1];
+            return r;
+        } else {
+            float f[4];
+            R.ld4(f, off);
+            return split3(f);
         }
     };
 
@@ -388,44 +459,47 @@ MEP_DEV void attn_fwd_task(const mep_attn_desc& d, int qc, int h, int b, int lan
         for (int qt = 0; qt < NT; ++qt)
 #pragma unroll
             for (int hb = 0; hb < NHB; ++hb) {
-                float qf[4] = {0.f, 0.f, 0.f, 0.f};
-                if (qch == CH || qt < nqt) Qb.ld4(qf, Qb.at(q_lo + qt * 16 + c, hc + 16 * hb + 4 * g));   // past Tq: 0
-                qsh[QH ? qt : 0][hb] = split3(qf);
+                S3 z{};
+                if (qch == CH || qt < nqt) z = ld_op(Qb, Qb.at(q_lo + qt * 16 + c, hc + 16 * hb + 4 * g));   // past Tq: 0
+                qsh[QH ? qt : 0][hb] = z;
             }
     }
     for (int k_lo = 0; k_lo < Tk; k_lo += CH) {
         // operands of the 4 key tiles of this chunk: K rows (A of S^T: K[k0+c][4g+s], split) and V
         // columns (B of P.V: V[k0+4g+s][c]); past Tk they read 0 (P is 0 there)
         S3 ks[NT][NHB];
-        float vf[NT][NHB][4], mt[NT][4];
+        float vf[BF ? 1 : NT][NHB][4], mt[NT][4];
+        unsigned vr[BF ? NT : 1][NHB][4];   // BF: raw bf16 V elements
         bf16x8 vbf[NT / 2][NHB];     // BF: V of key-tile pairs (kt, kt+1) in slots 0-3 / 4-7
 #pragma unroll
         for (int kt = 0; kt < NT; ++kt) {
             const int k0 = k_lo + kt * 16;
 #pragma unroll
             for (int hb = 0; hb < NHB; ++hb) {
-                float kf[4];
-                Kb.ld4(kf, Kb.at(k0 + c, hc + 16 * hb + 4 * g));
                 const int ov = Vb.at(k0 + 4 * g, hc + 16 * hb + c);
 #pragma unroll
-                for (int s = 0; s < 4; ++s) vf[kt][hb][s] = Vb.ld1(ov, s * Vb.sT4);
-                ks[kt][hb] = split3(kf);
+                for (int s = 0; s < 4; ++s) {
+                    if constexpr (BF) vr[kt][hb][s] = Vb.ld1raw(ov, s * Vb.sT4);
+                    else vf[kt][hb][s] = Vb.ld1(ov, s * Vb.sT4);
+                }
+                ks[kt][hb] = ld_op(Kb, Kb.at(k0 + c, hc + 16 * hb + 4 * g));
             }
 #pragma unroll
             for (int s = 0; s < 4; ++s) mt[kt][s] = mask_term(mask, k0 + 4 * g + s, Tk);
         }
-        if (BF) {
+        if constexpr (BF) {
 #pragma unroll
             for (int kt = 0; kt < NT; kt += 2)
 #pragma unroll
                 for (int hb = 0; hb < NHB; ++hb)
-                    vbf[kt / 2][hb] = op(pk(vf[kt][hb][0], vf[kt][hb][1]), pk(vf[kt][hb][2], vf[kt][hb][3]),
-                                         pk(vf[kt + 1][hb][0], vf[kt + 1][hb][1]), pk(vf[kt + 1][hb][2], vf[kt + 1][hb][3]));
+                    vbf[kt / 2][hb] = op(vr[kt][hb][0] | (vr[kt][hb][1] << 16), vr[kt][hb][2] | (vr[kt][hb][3] << 16),
+                                         vr[kt + 1][hb][0] | (vr[kt + 1][hb][1] << 16),
+                                         vr[kt + 1][hb][2] | (vr[kt + 1][hb][3] << 16));
         }
 #if MEP_FWD_PVSPLIT
         // V of key-tile pairs split once per chunk (not per query tile): parts [pair][hb][part]
         bf16x8 vsp[NT / 2][NHB][MEP_FWD_PVSPLIT == 2 ? 3 : 2];
-        if (!BF) {
+        if constexpr (!BF) {
 #pragma unroll
             for (int kt = 0; kt < NT; kt += 2)
 #pragma unroll
@@ -443,15 +517,23 @@ MEP_DEV void attn_fwd_task(const mep_attn_desc& d, int qc, int h, int b, int lan
                 }
         }
 #endif
-        float qfa[QH ? 1 : NT][NHB][4];                                    // B of S^T: Q[q][4g+s]
+        float qfa[QH || BF ? 1 : NT][NHB][4];                              // B of S^T: Q[q][4g+s]
+        S3 qbf[!QH && BF ? NT : 1][NHB];                                   // BF: raw Q words
         if (!QH) {
 #pragma unroll
             for (int qt = 0; qt < NT; ++qt)
 #pragma unroll
                 for (int hb = 0; hb < NHB; ++hb) {
-                    float* qf = qfa[QH ? 0 : qt][hb];
-                    if (qch == CH || qt < nqt) Qb.ld4(qf, Qb.at(q_lo + qt * 16 + c, hc + 16 * hb + 4 * g));   // past Tq: 0
-                    else qf[0] = qf[1] = qf[2] = qf[3] = 0.f;
+                    const bool in = qch == CH || qt < nqt;                 // past Tq: 0
+                    if constexpr (BF) {
+                        S3 z{};
+                        if (in) z = ld_op(Qb, Qb.at(q_lo + qt * 16 + c, hc + 16 * hb + 4 * g));
+                        qbf[!QH && BF ? qt : 0][hb] = z;
+                    } else {
+                        float* qf = qfa[QH ? 0 : qt][hb];
+                        if (in) Qb.ld4(qf, Qb.at(q_lo + qt * 16 + c, hc + 16 * hb + 4 * g));
+                        else qf[0] = qf[1] = qf[2] = qf[3] = 0.f;
+                    }
                 }
         }
 #pragma unroll
@@ -460,7 +542,8 @@ MEP_DEV void attn_fwd_task(const mep_attn_desc& d, int qc, int h, int b, int lan
             const int q = q_lo + qt * 16 + c;
             S3 qs[NHB];
 #pragma unroll
-            for (int hb = 0; hb < NHB; ++hb) qs[hb] = QH ? qsh[QH ? qt : 0][hb] : split3(qfa[QH ? 0 : qt][hb]);
+            for (int hb = 0; hb < NHB; ++hb)
+                qs[hb] = QH ? qsh[QH ? qt : 0][hb] : BF ? qbf[!QH && BF ? qt : 0][hb] : split3(qfa[QH || BF ? 0 : qt][hb]);
             const int srow = (sbase + min(q, Tq - 1)) * Tk;
             float sv[NT][4];
             float mx = -INFINITY;
@@ -485,8 +568,7 @@ MEP_DEV void attn_fwd_task(const mep_attn_desc& d, int qc, int h, int b, int lan
                     mx = fmaxf(mx, sv[kt][r]);
                 }
             }
-            mx = fmaxf(mx, shfl(mx, lane ^ 16));
-            mx = fmaxf(mx, shfl(mx, lane ^ 32));
+            mx = xg_max(mx);
             const float mnew = SINGLE ? mx : fmaxf(m[qt], mx);
             float lsum = 0.f;
             constexpr float L2E = 1.4426950408889634f;
@@ -496,29 +578,32 @@ MEP_DEV void attn_fwd_task(const mep_attn_desc& d, int qc, int h, int b, int lan
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     sv[kt][r] = MEP_FWD_EXP2 ? __builtin_amdgcn_exp2f(fmaf(sv[kt][r], L2E, -mb)) : __expf(sv[kt][r] - mnew);
-                    lsum += sv[kt][r];
+                    if (!(BF && MEP_FWD_MFSUM)) lsum += sv[kt][r];
                 }
             floatx4 oq[NHB];
 #pragma unroll
             for (int hb = 0; hb < NHB; ++hb) oq[hb] = SINGLE ? zero4() : o[qt][hb];
-            if (!SINGLE && k_lo > 0) {   // rescale the running state
+            if (!SINGLE && k_lo > 0) {   // rescale the running state (O^T: the lane's own query c)
                 const float corr = __expf(m[qt] - mnew);
                 l[qt] *= corr;
 #pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const float cr = shfl(corr, 4 * g + r);                  // O row 4g+r <- query 4g+r
+                for (int r = 0; r < 4; ++r)
 #pragma unroll
-                    for (int hb = 0; hb < NHB; ++hb) oq[hb][r] *= cr;
-                }
+                    for (int hb = 0; hb < NHB; ++hb) oq[hb][r] *= corr;
             }
-            // O += P V over the chunk's 64 keys: key-tile pairs (slots 0-3 / 4-7)
+            // O^T += V^T P^T over the chunk's 64 keys: key-tile pairs (slots 0-3 / 4-7); V^T is the
+            // A operand (row: dim c), P^T the B operand (column: query c).  BF: the row sums of the
+            // bf16 P too, as a ones-row A operand against the same P^T (every accumulator row is
+            // the query's sum over the chunk's keys: no VALU add per score, no lane reduction)
+            floatx4 lacc = zero4();
 #pragma unroll
             for (int kt = 0; kt < NT; kt += 2) {
                 if (BF) {   // bf16 P (slots: keys 4g+s of tiles kt / kt+1) against bf16 V
                     const bf16x8 pb = op(pk(sv[kt][0], sv[kt][1]), pk(sv[kt][2], sv[kt][3]), pk(sv[kt + 1][0], sv[kt + 1][1]),
                                          pk(sv[kt + 1][2], sv[kt + 1][3]));
 #pragma unroll
-                    for (int hb = 0; hb < NHB; ++hb) oq[hb] = mfma(pb, vbf[kt / 2][hb], oq[hb]);
+                    for (int hb = 0; hb < NHB; ++hb) oq[hb] = mfma(vbf[kt / 2][hb], pb, oq[hb]);
+                    if (MEP_FWD_MFSUM) lacc = mfma(op(0x3f803f80u, 0x3f803f80u, 0x3f803f80u, 0x3f803f80u), pb, lacc);
                     continue;
                 }
 #if MEP_FWD_PVSPLIT == 2
@@ -532,12 +617,12 @@ MEP_DEV void attn_fwd_task(const mep_attn_desc& d, int qc, int h, int b, int lan
 #pragma unroll
                     for (int hb = 0; hb < NHB; ++hb) {
                         const bf16x8 v0 = vsp[kt / 2][hb][0], v1 = vsp[kt / 2][hb][1];
-                        floatx4 t = mfma(p2, v0, zero4());          // two independent chains
-                        oq[hb] = mfma(p1, v0, oq[hb]);
-                        t = mfma(p1, v1, t);
-                        oq[hb] = mfma(p0, v1, oq[hb]);
-                        t = mfma(p0, vsp[kt / 2][hb][2], t);
-                        oq[hb] = mfma(p0, v0, oq[hb]);
+                        floatx4 t = mfma(v0, p2, zero4());          // two independent chains
+                        oq[hb] = mfma(v0, p1, oq[hb]);
+                        t = mfma(v1, p1, t);
+                        oq[hb] = mfma(v1, p0, oq[hb]);
+                        t = mfma(vsp[kt / 2][hb][2], p0, t);
+                        oq[hb] = mfma(v0, p0, oq[hb]);
 #pragma unroll
                         for (int r = 0; r < 4; ++r) oq[hb][r] += t[r];
                     }
@@ -552,9 +637,9 @@ MEP_DEV void attn_fwd_task(const mep_attn_desc& d, int qc, int h, int b, int lan
 #pragma unroll
                     for (int hb = 0; hb < NHB; ++hb) {
                         const bf16x8 v0 = vsp[kt / 2][hb][0];
-                        oq[hb] = mfma(p0, v0, oq[hb]);
-                        oq[hb] = mfma(p1, v0, oq[hb]);
-                        oq[hb] = mfma(p0, vsp[kt / 2][hb][1], oq[hb]);
+                        oq[hb] = mfma(v0, p0, oq[hb]);
+                        oq[hb] = mfma(v0, p1, oq[hb]);
+                        oq[hb] = mfma(vsp[kt / 2][hb][1], p0, oq[hb]);
                     }
                 }
 #else
@@ -564,9 +649,10 @@ MEP_DEV void attn_fwd_task(const mep_attn_desc& d, int qc, int h, int b, int lan
 #pragma unroll
                     for (int s = 0; s < 4; ++s)
 #pragma unroll
-                        for (int hb = 0; hb < NHB; ++hb) oq[hb] = mfma16x4(sv[kt + k2][s], vf[kt + k2][hb][s], oq[hb]);
+                        for (int hb = 0; hb < NHB; ++hb) oq[hb] = mfma16x4(vf[kt + k2][hb][s], sv[kt + k2][s], oq[hb]);
 #endif
             }
+            if (BF && MEP_FWD_MFSUM) lsum = lacc[0];
             if (SINGLE) {
                 finish(qt, oq, mnew, lsum);
             } else {

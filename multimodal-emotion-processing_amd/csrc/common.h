@@ -474,46 +474,87 @@ MEP_DEV void wave_store16(const float* src, int lda, const mep_rows& dst, int r0
 // ------------------------------------------------------------------ gradient reductions
 // Block bodies shared by their own launches and the fused mep_reduce_grads launch (256 threads).
 // Weight-gradient split sum (gemm.hip k_wgrad_reduce): block bx of descriptor d sums the
-// n_split partials of 256 consecutive (n, k) entries in a fixed order.
+// n_split partials of WG_RED_PER = 1024 consecutive (n, k) entries in a fixed order, 4 per thread
+// (one 16-byte load per partial when N * Ktot and the workspace allow it; hosts count tiles of
+// 256 entries, the launches run cdiv(tiles, 4) blocks: wg_red_blocks).
 // Each returns the sum of squares of the gradient values its thread wrote (the fused gradient-norm
 // partials of mep_reduce_grads; ignored by the standalone launches).
+constexpr int WG_RED_PER = 1024;
+__host__ __device__ inline int wg_red_blocks(int tiles256) { return (tiles256 + 3) / 4; }
+
 MEP_DEV float wgrad_reduce_block(const mep_wgrad_desc& d, int bx) {
     const int64_t nk = (int64_t)d.N * d.Ktot;
-    const int64_t i = (int64_t)bx * 256 + threadIdx.x;
-    if (i >= nk) return 0.f;
+    const int64_t i0 = (int64_t)bx * WG_RED_PER + 4 * threadIdx.x;
+    if (i0 >= nk) return 0.f;
     const gfloat* part = G<const float>(d.partial);
-    float s = 0.f;
+    float s[4] = {0.f, 0.f, 0.f, 0.f};
+    const int cnt = (int)min((int64_t)4, nk - i0);
+    if (cnt == 4 && (nk & 3) == 0 && (d.partial & 15) == 0) {
 #pragma unroll 8
-    for (int sp = 0; sp < d.n_split; ++sp) s += part[sp * nk + i];
-    const int n = (int)(i / d.Ktot);
-    int k = (int)(i - (int64_t)n * d.Ktot);
-    int j = 0;
-    while (j < d.n_b - 1 && k >= d.kb[j]) { k -= d.kb[j]; ++j; }
-    gfloat* o = G<float>(d.out[j]) + (d.out_trans ? (int64_t)k * d.ldo[j] + n : (int64_t)n * d.ldo[j] + k);
-    const float v = d.accumulate ? *o + s : s;
-    *o = v;
-    return v * v;
+        for (int sp = 0; sp < d.n_split; ++sp) {
+            const f32x4 v = *reinterpret_cast<const __attribute__((address_space(1))) f32x4*>(part + sp * nk + i0);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) s[e] += v[e];
+        }
+    } else {
+        for (int e = 0; e < cnt; ++e) {
+            float t = 0.f;
+            for (int sp = 0; sp < d.n_split; ++sp) t += part[sp * nk + i0 + e];
+            s[e] = t;
+        }
+    }
+    float sq = 0.f;
+    for (int e = 0; e < cnt; ++e) {
+        const int64_t i = i0 + e;
+        const int n = (int)(i / d.Ktot);
+        int k = (int)(i - (int64_t)n * d.Ktot);
+        int j = 0;
+        while (j < d.n_b - 1 && k >= d.kb[j]) { k -= d.kb[j]; ++j; }
+        gfloat* o = G<float>(d.out[j]) + (d.out_trans ? (int64_t)k * d.ldo[j] + n : (int64_t)n * d.ldo[j] + k);
+        const float v = d.accumulate ? *o + s[e] : s[e];
+        *o = v;
+        sq += v * v;
+    }
+    return sq;
 }
 
-// Column sums of a partial matrix (optim.hip k_colsum): block bx = 32 columns x 8 row groups,
-// fixed-order combine.
+// Column sums of a partial matrix (optim.hip k_colsum): block bx = 32 columns.  16-byte rows
+// (ld, n_cols multiples of 4, aligned): 8 lanes x 4 columns x 32 row groups, each thread's rows
+// loaded at once, the 32 groups combined in a fixed order; else 32 columns x 8 row groups.
 MEP_DEV float colsum_block(const mep_colsum_desc& d, int bx) {
-    const int cl = threadIdx.x & 31, g = threadIdx.x >> 5;
-    const int c = bx * 32 + cl;
     if (bx * 32 >= d.n_cols) return 0.f;   // whole block
-    __shared__ float red[8][32];
-    float s = 0.f;
-    if (c < d.n_cols) {
-        const gfloat* p = G<const float>(d.partial) + c;
-#pragma unroll 8
-        for (int r = g; r < d.n_rows; r += 8) s += p[(int64_t)r * d.ld];
-    }
-    red[g][cl] = s;
-    __syncthreads();
-    if (g == 0 && c < d.n_cols) {
-        float t = 0.f;
+    __shared__ float red[32][33];
+    const bool v4 = (d.ld % 4 == 0) && (d.n_cols % 4 == 0) && (d.partial & 15) == 0;
+    if (v4) {
+        const int q = threadIdx.x & 7, g = threadIdx.x >> 3;
+        const int c0 = bx * 32 + 4 * q;
+        f32x4 s = f32x4{0.f, 0.f, 0.f, 0.f};
+        if (c0 < d.n_cols) {
+            const gfloat* p = G<const float>(d.partial) + c0;
+#pragma unroll 16
+            for (int r = g; r < d.n_rows; r += 32)
+                s += *reinterpret_cast<const __attribute__((address_space(1))) f32x4*>(p + (int64_t)r * d.ld);
+        }
 #pragma unroll
-        for (int k = 0; k < 8; ++k) t += red[k][cl];
+        for (int e = 0; e < 4; ++e) red[g][4 * q + e] = s[e];
+    } else {
+        const int cl = threadIdx.x & 31, g = threadIdx.x >> 5;
+        const int c = bx * 32 + cl;
+        float s = 0.f;
+        if (c < d.n_cols) {
+            const gfloat* p = G<const float>(d.partial) + c;
+#pragma unroll 8
+            for (int r = g; r < d.n_rows; r += 8) s += p[(int64_t)r * d.ld];
+        }
+        red[g][cl] = s;
+    }
+    __syncthreads();
+    const int cl = threadIdx.x;
+    const int c = bx * 32 + cl;
+    if (cl < 32 && c < d.n_cols) {
+        float t = 0.f;
+        const int ng = v4 ? 32 : 8;
+        for (int k = 0; k < ng; ++k) t += red[k][cl];
         gfloat* o = G<float>(d.out) + c;
         const float v = (d.accumulate & 1) ? *o + t : t;
         *o = v;

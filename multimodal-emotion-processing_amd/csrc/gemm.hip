@@ -897,9 +897,66 @@ MEP_DEV void unify_tasks(const mep_gemm_desc& d, const lfloat* wl, int ldl, int 
 // LDS already rounded, in 16-byte units (n, pair p, lane group g) at n * RS + (4p + g) * 16,
 // RS = 64 NP + 32 bytes (conflict-free fragment reads, split.h SplitW), zero past K; when it does
 // not fit, fragments are read from L2 and rounded on the fly (K % 16 == 0).
-// HS: bf16 X and Y rows (MEP_BF16_STORE, the bf16 path's features and unified rows)
+// HS: bf16 X and Y rows (MEP_BF16_STORE, the bf16 path's features and unified rows): X fragments
+// stay raw bf16 words (no fp32 round trip).  A wave's first task issues its first UN_PPB k pairs
+// of X loads BEFORE the weight staging, so the staging's L2 round trip and the first X fetch from
+// HBM overlap (most waves run one task: the launch is latency-bound).
+#ifndef MEP_UN_PPB
+#define MEP_UN_PPB 8    // k pairs of X fragments in flight per lane (bf16 path)
+#endif
+typedef __attribute__((address_space(3))) unsigned char un_lbyte;
+
+MEP_DEV void unify_stage_bf(const mep_gemm_desc& d, un_lbyte* wl) {
+    // W [N][K] -> rounded bf16 units in LDS (zero past K): UN_SU units per thread per pass, every
+    // load of a pass in flight before the first LDS write (a text weight, N = 96 x K = 300, is one
+    // pass)
+    constexpr int UN_SU = 8;
+    const int N = d.N, K = d.K, NPK = (K + 31) >> 5, RS = 64 * NPK + 32;
+    const int units = N * NPK * 4;
+    const auto rsW = __builtin_amdgcn_make_buffer_rsrc((void*)d.w, 0, 4 * ((N - 1) * d.ldw + K), 0x00020000);
+    // a unit is two runs of 4 consecutive k: one 16-byte load each when the runs are aligned and
+    // K splits into whole runs (4 lanes of a unit row cover 64 contiguous bytes; 4x fewer
+    // address-unit passes than dword loads), else 8 dword loads
+    const bool v4 = K % 4 == 0 && d.ldw % 4 == 0 && (d.w & 15) == 0;
+    for (int u0 = 0; u0 < units; u0 += UN_SU * UN_THREADS) {
+        float v[UN_SU][8];
+#pragma unroll
+        for (int q = 0; q < UN_SU; ++q) {
+            const int u = u0 + q * UN_THREADS + (int)threadIdx.x;
+            const int gg = u & 3, pp = (u >> 2) % NPK, n = (u >> 2) / NPK;
+            if (v4) {
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    const int k = 32 * pp + 16 * h + 4 * gg;
+                    const f32x4 x = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                        rsW, (u < units && k < K) ? 4 * (n * d.ldw + k) : WG_INV, 0, 0));
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) v[q][4 * h + e] = x[e];
+                }
+            } else {
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const int k = 32 * pp + (j < 4 ? 0 : 16) + 4 * gg + (j & 3);
+                    v[q][j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                        rsW, (u < units && k < K) ? 4 * (n * d.ldw + k) : WG_INV, 0, 0));
+                }
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < UN_SU; ++q) {
+            const int u = u0 + q * UN_THREADS + (int)threadIdx.x;
+            const int gg = u & 3, pp = (u >> 2) % NPK, n = (u >> 2) / NPK;
+            typedef __attribute__((address_space(3))) u32x4 lu32x4;
+            if (u < units)
+                *reinterpret_cast<lu32x4*>(wl + n * RS + (4 * pp + gg) * 16) =
+                    u32x4{pk_bf16(v[q][0], v[q][1]), pk_bf16(v[q][2], v[q][3]),
+                          pk_bf16(v[q][4], v[q][5]), pk_bf16(v[q][6], v[q][7])};
+        }
+    }
+}
+
 template <int NIP, bool WL, bool XV, bool HS>
-MEP_DEV void unify_tasks_bf(const mep_gemm_desc& d, const __attribute__((address_space(3))) unsigned char* wl, int tile_lo, int tile_hi, int np) {
+MEP_DEV void unify_tasks_bf(const mep_gemm_desc& d, un_lbyte* wl, int tile_lo, int tile_hi, int np) {
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int c = lane & 15, g = lane >> 4;
     const int K = d.K, NPK = (K + 31) >> 5, ntok = d.ntok, RS = 64 * NPK + 32;
@@ -909,45 +966,71 @@ MEP_DEV void unify_tasks_bf(const mep_gemm_desc& d, const __attribute__((address
     const gfloat* wg = G<const float>(d.w);
     const gfloat* table = G<const float>(d.table);
     const int ntask = (tile_hi - tile_lo) * np;
-    constexpr int PP = UN_PF / 2;   // k pairs of X fragments in flight
-    for (int task = wave; task < ntask; task += UN_WAVES) {
-        const int tile = tile_lo + task / np, part = task - (task / np) * np;
-        const int tok = tile * 16 + c;
-        const bool ok = tok < ntok;
-        int xo = WG_INV;
-        if (ok) {
-            const int b = tok / T, t = tok - b * T;
-            xo = ES * ((int)(b * d.x.sB + t * d.x.sT) + 4 * g);
-        }
-        const int n0 = 16 * NIP * part;
-        f32x4 acc[NIP];
+    constexpr int PP = HS ? MEP_UN_PPB : UN_PF / 2;   // k pairs of X fragments in flight
+    // one X fragment (4 consecutive k of the lane's token): raw bf16 words (HS) or fp32
+    typedef std::conditional_t<HS, u32x2, f32x4> XF;
+    auto ld = [&](int o) -> XF {
+        if constexpr (HS) {
+            if (XV) return __builtin_bit_cast(u32x2, __builtin_amdgcn_raw_buffer_load_b64(rsX, o, 0, 0));
+            unsigned e[4];
 #pragma unroll
-        for (int i = 0; i < NIP; ++i) acc[i] = zero_f4();
-        f32x4 xf[PP][2];
-        auto ld = [&](int o) {
+            for (int i = 0; i < 4; ++i) e[i] = (unsigned)__builtin_amdgcn_raw_buffer_load_b16(rsX, o + 2 * i, 0, 0);
+            return u32x2{e[0] | (e[1] << 16), e[2] | (e[3] << 16)};
+        } else {
             f32x4 v;
-            if (HS && XV) {
-                const u32x2a w = __builtin_bit_cast(u32x2a, __builtin_amdgcn_raw_buffer_load_b64(rsX, o, 0, 0));
-                v = f32x4{bf16_word_lo(w[0]), bf16_word_hi(w[0]), bf16_word_lo(w[1]), bf16_word_hi(w[1])};
-            } else if (HS) {
-#pragma unroll
-                for (int e = 0; e < 4; ++e)
-                    v[e] = __builtin_bit_cast(float, (unsigned)__builtin_amdgcn_raw_buffer_load_b16(rsX, o + 2 * e, 0, 0) << 16);
-            } else if (XV) {
+            if (XV) {
                 v = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rsX, o, 0, 0));
             } else {
 #pragma unroll
                 for (int e = 0; e < 4; ++e) v[e] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsX, o + 4 * e, 0, 0));
             }
             return v;
-        };
-        auto load = [&](int s, int pp) {
-            const int o = pp < NPK ? xo + 32 * ES * pp : WG_INV;
-            xf[s][0] = ld(o);
-            xf[s][1] = ld(o == WG_INV || 32 * pp + 16 >= K ? WG_INV : o + 16 * ES);
-        };
+        }
+    };
+    XF xf[PP][2];
+    int xo = WG_INV;
+    auto setup = [&](int task) {   // the lane's X row for this task
+        const int tile = tile_lo + task / np;
+        const int tok = tile * 16 + c;
+        xo = WG_INV;
+        if (tok < ntok) {
+            const int b = tok / T, t = tok - b * T;
+            xo = ES * ((int)(b * d.x.sB + t * d.x.sT) + 4 * g);
+        }
+    };
+    auto load = [&](int s, int pp) {
+        const int o = pp < NPK ? xo + 32 * ES * pp : WG_INV;
+        xf[s][0] = ld(o);
+        xf[s][1] = ld(o == WG_INV || 32 * pp + 16 >= K ? WG_INV : o + 16 * ES);
+    };
+    auto prologue = [&]() {
+#pragma unroll
+        for (int s = 0; s < PP - 1; ++s) load(s, s);
+    };
+    int task = wave;
+    if (task < ntask) {
+        setup(task);
+        prologue();
+    }
+    if (WL) {   // every wave reaches the barrier, with or without a task
+        unify_stage_bf(d, wl);
+        __syncthreads();
+    }
+    for (; task < ntask; task += UN_WAVES) {
+        if (task != wave) {
+            setup(task);
+            prologue();
+        }
+        const int tile = tile_lo + task / np, part = task - (task / np) * np;
+        const int tok = tile * 16 + c;
+        const int n0 = 16 * NIP * part;
+        f32x4 acc[NIP];
+#pragma unroll
+        for (int i = 0; i < NIP; ++i) acc[i] = zero_f4();
         auto mma = [&](int s, int pp) {
-            const OpN<1> xb = opn<1>(xf[s][0], xf[s][1]);
+            OpN<1> xb;
+            if constexpr (HS) xb.p[0] = kpair(xf[s][0], xf[s][1]);
+            else xb = opn<1>(xf[s][0], xf[s][1]);
 #pragma unroll
             for (int i = 0; i < NIP; ++i) {
                 const int row = n0 + 16 * i + c;
@@ -962,8 +1045,6 @@ MEP_DEV void unify_tasks_bf(const mep_gemm_desc& d, const __attribute__((address
                 acc[i] = mma_n<1>(a, xb, acc[i]);
             }
         };
-#pragma unroll
-        for (int s = 0; s < PP - 1; ++s) load(s, s);
         int p0 = 0;
         for (; p0 + PP <= NPK; p0 += PP) {
 #pragma unroll
@@ -975,7 +1056,7 @@ MEP_DEV void unify_tasks_bf(const mep_gemm_desc& d, const __attribute__((address
 #pragma unroll
         for (int s = 0; s < PP - 1; ++s)
             if (p0 + s < NPK) mma(s, p0 + s);
-        if (ok) {
+        if (tok < ntok) {
             const auto yr = rowa<HS>(d.y, tok);
             const gfloat* tr = table ? table + (int64_t)(tok % d.y.T) * (d.ldt ? d.ldt : d.N) : nullptr;
 #pragma unroll
@@ -1004,27 +1085,11 @@ __global__ __launch_bounds__(UN_THREADS) void k_unify(const mep_gemm_desc* __res
     const bool xv = (hs || d.K % 4 == 0) && ((d.x.ptr & (hs ? 7 : 15)) == 0) && (d.x.sB % 4 == 0) && (d.x.sT % 4 == 0);
     const int np = d.N >= 64 ? 2 : 1, nip = d.N / (16 * np);
     if (d.bf16) {
-        // W [N][K] -> rounded bf16 units in LDS (zero past K) when N * RS fits
+        // W [N][K] -> rounded bf16 units in LDS (zero past K) when N * RS fits, staged inside the
+        // task function (after each wave's first X loads)
         const int N = d.N, K = d.K, NPK = (K + 31) >> 5, RS = 64 * NPK + 32;
         const bool wlds = N * RS <= 4 * UN_LDS;
-        typedef __attribute__((address_space(3))) unsigned char lbyte;
-        lbyte* wl = (lbyte*)&smem[0];
-        if (wlds) {
-            const gfloat* W = G<const float>(d.w);
-            for (int u = threadIdx.x; u < N * NPK * 4; u += UN_THREADS) {
-                const int gg = u & 3, pp = (u >> 2) % NPK, n = (u >> 2) / NPK;
-                float v[8];
-#pragma unroll
-                for (int j = 0; j < 8; ++j) {
-                    const int k = 32 * pp + (j < 4 ? 0 : 16) + 4 * gg + (j & 3);
-                    v[j] = k < K ? W[(int64_t)n * d.ldw + k] : 0.f;
-                }
-                typedef __attribute__((address_space(3))) u32x4 lu32x4;
-                *reinterpret_cast<lu32x4*>(wl + n * RS + (4 * pp + gg) * 16) =
-                    u32x4{pk_bf16(v[0], v[1]), pk_bf16(v[2], v[3]), pk_bf16(v[4], v[5]), pk_bf16(v[6], v[7])};
-            }
-            __syncthreads();
-        }
+        un_lbyte* wl = (un_lbyte*)&smem[0];
 #define MEP_UNB2(NIP, HS)                                                                                \
             if (wlds) { if (xv) unify_tasks_bf<NIP, true, true, HS>(d, wl, tile_lo, tile_hi, np);        \
                         else unify_tasks_bf<NIP, true, false, HS>(d, wl, tile_lo, tile_hi, np); }        \
@@ -1127,7 +1192,7 @@ extern "C" int mep_wgrad(const mep_wgrad_desc* descs, int n_desc, int max_tiles,
 
 extern "C" int mep_wgrad_reduce(const mep_wgrad_desc* descs, int n_desc, int max_tiles, mep_stream_t stream) {
     if (n_desc <= 0 || max_tiles <= 0) return 0;
-    hipLaunchKernelGGL(k_wgrad_reduce, dim3(max_tiles, n_desc), dim3(256), 0, (hipStream_t)stream, descs);
+    hipLaunchKernelGGL(k_wgrad_reduce, dim3(wg_red_blocks(max_tiles), n_desc), dim3(256), 0, (hipStream_t)stream, descs);
     return mep_check_launch("mep_wgrad_reduce");
 }
 

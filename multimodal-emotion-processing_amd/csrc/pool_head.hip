@@ -562,10 +562,11 @@ __global__ __launch_bounds__(256) void k_reduce_grads(const mep_wgrad_desc* __re
         sq = head_reduce_block(hd, hg, bx);
     } else {
         bx -= head_blocks;
-        if (bx < n_wd * wd_tiles) {
-            sq = wgrad_reduce_block(wd[bx / wd_tiles], bx % wd_tiles);
+        const int wt = wg_red_blocks(wd_tiles);   // blocks of WG_RED_PER entries per descriptor
+        if (bx < n_wd * wt) {
+            sq = wgrad_reduce_block(wd[bx / wt], bx % wt);
         } else {
-            bx -= n_wd * wd_tiles;
+            bx -= n_wd * wt;
             if (bx < n_cd * cd_tiles) sq = colsum_block(cd[bx / cd_tiles], bx % cd_tiles);
         }
     }
@@ -669,7 +670,7 @@ extern "C" int mep_reduce_grads(const mep_wgrad_desc* wgrad, int n_wgrad, int wg
                       (float*)g_wc0, (float*)g_wc1, (float*)loss};
         hb = head_reduce_blocks(hd);
     }
-    const int blocks = hb + n_wgrad * wgrad_tiles + n_colsum * colsum_tiles;
+    const int blocks = hb + n_wgrad * wg_red_blocks(wgrad_tiles) + n_colsum * colsum_tiles;
     if (blocks <= 0) return 0;
     hipLaunchKernelGGL(k_reduce_grads, dim3(blocks), dim3(256), 0, (hipStream_t)stream, wgrad, n_wgrad,
                        wgrad_tiles, colsum, n_colsum, colsum_tiles, hd, g, hb, norm, step, hyper);
@@ -678,7 +679,7 @@ extern "C" int mep_reduce_grads(const mep_wgrad_desc* wgrad, int n_wgrad, int wg
 
 extern "C" int mep_reduce_grads_grid(int n_wgrad, int wgrad_tiles, int n_colsum, int colsum_tiles,
                                      const mep_head_desc* head) {
-    return (head ? head_reduce_blocks(*head) : 0) + n_wgrad * wgrad_tiles + n_colsum * colsum_tiles;
+    return (head ? head_reduce_blocks(*head) : 0) + n_wgrad * wg_red_blocks(wgrad_tiles) + n_colsum * colsum_tiles;
 }
 
 extern "C" int mep_head_reduce(const mep_head_desc* d, uint64_t g_trans, uint64_t g_ln_w, uint64_t g_ln_b,
