@@ -714,6 +714,7 @@ struct Bwd {
     struct QIn {
         float qa[4], da[4], db[4], qb[4], ob[4], dqo[4];
         f32x2 st[4];
+        u32x2 qaw, daw;   // BF: Q / dO rows as raw bf16 operand words (no fp32 round trip)
     };
     const mep_attn_bwd_desc& bd;
     int b, h, lane, c, g, hc, Tq, Tk, sbase;
@@ -726,6 +727,7 @@ struct Bwd {
     int k_lo;
     S2 kb[NT], vb[NT], kq[NT];
     float mtk[NT], mtl[NT];   // mask term, and the same times log2(e)
+    float mts[BF ? NT : 1];   // BF: -4 x the mask term, the score accumulator's initial value (EXP2)
     floatx4 dk[NT], dv[NT];
     float dc_acc;
 
@@ -763,6 +765,7 @@ struct Bwd {
             if (!KV && !same_kv) Vb.ld4(vf, Vb.at(k0 + c, hc + 4 * g));
             mtk[kt] = mask_term(mask, k0 + c, Tk);
             mtl[kt] = mtk[kt] * 1.4426950408889634f;
+            if (BF) mts[BF ? kt : 0] = -4.0f * mtk[kt];
             const int okq = Kb.at(k0 + 4 * g, hc + c);
 #pragma unroll
             for (int s = 0; s < 4; ++s) kc4[s] = Kb.ld1(okq, s * Kb.sT4);
@@ -777,8 +780,13 @@ struct Bwd {
 
     MEP_DEV void fetch(QIn& in, int qt) const {
         const int q0 = qt * 16;   // rows past Tq read zeros
-        Qb.ld4(in.qa, Qb.at(q0 + c, hc + 4 * g));
-        Gb.ld4(in.da, Gb.at(q0 + c, hc + 4 * g));
+        if constexpr (BF) {
+            in.qaw = Qb.ld4raw(Qb.at(q0 + c, hc + 4 * g));
+            in.daw = Gb.ld4raw(Gb.at(q0 + c, hc + 4 * g));
+        } else {
+            Qb.ld4(in.qa, Qb.at(q0 + c, hc + 4 * g));
+            Gb.ld4(in.da, Gb.at(q0 + c, hc + 4 * g));
+        }
         const int qg = q0 + 4 * g;
         const int og = Gb.at(qg, hc + c), oq = Qb.at(qg, hc + c), oo = Ob.at(qg, hc + c), od = dQb.at(qg, hc + c);
 #pragma unroll
@@ -837,9 +845,8 @@ struct Bwd {
             typedef __attribute__((address_space(3))) const unsigned short lcu16;
             typedef __attribute__((address_space(3))) const u32x2 lcu2;
             lcu16* H = (lcu16*)S;                 // operand o at H + 512 o: [16 rows][16] bf16
-            const u32x2 qa = *(lcu2*)(H + 16 * c + 4 * g), da = *(lcu2*)(H + 512 + 16 * c + 4 * g);
-            in.qa[0] = bf_lo(qa[0]); in.qa[1] = bf_hi(qa[0]); in.qa[2] = bf_lo(qa[1]); in.qa[3] = bf_hi(qa[1]);
-            in.da[0] = bf_lo(da[0]); in.da[1] = bf_hi(da[0]); in.da[2] = bf_lo(da[1]); in.da[3] = bf_hi(da[1]);
+            in.qaw = *(lcu2*)(H + 16 * c + 4 * g);
+            in.daw = *(lcu2*)(H + 512 + 16 * c + 4 * g);
 #pragma unroll
             for (int s4 = 0; s4 < 4; ++s4) {
                 const int r = (4 * g + s4) * 16 + c;
@@ -892,7 +899,8 @@ struct Bwd {
             mm[s] = qok ? mm[s] - __builtin_amdgcn_logf(li[s]) : INFINITY;
 #endif
         }
-        const S2 qs = split2(in.qa), do2 = split2(in.da);
+        const S2 qs = BF ? S2{in.qaw[0], in.qaw[1], 0u, 0u} : split2(in.qa);
+        const S2 do2 = BF ? S2{in.daw[0], in.daw[1], 0u, 0u} : split2(in.da);
         S2 qb2;
         if (KV && MEP_BWD_STACK && !BF) {
             qb2 = S2{};   // in the stacked operand B0 / B1
@@ -924,7 +932,13 @@ struct Bwd {
             const int kk = k_lo + kt * 16 + c;
             // recomputed scores on the 2-way split (the forward's are 3-way): P differs from the
             // forward's by <= ~2^-16 relative, far inside the gradient tolerance
-            const floatx4 st = dot16<BF>(qs, kb[kt], zero4());           // C[query 4g+r][key c]
+            // C[query 4g+r][key c].  BF + EXP2: the accumulator starts at -4 x the key's mask term,
+            // so the exponent below needs no per-score mask add (0 for kept keys: the same bits; a
+            // masked or padding key's score stays ~-4e8 / -inf and its P exactly 0).  The fp32
+            // instances keep the add (four more live registers spill the 128-register short kernel)
+            constexpr bool MI = BF && MEP_BWD_EXP2;
+            const float m0 = MI ? mts[BF ? kt : 0] : 0.f;
+            const floatx4 st = dot16<BF>(qs, kb[kt], floatx4{m0, m0, m0, m0});
 #if MEP_BWD_EXP2
             // dP - delta: the accumulator starts at -delta (query 4g+r)
             const floatx4 dp = dot16<BF>(do2, KV ? kb[kt] : vb[kt], floatx4{-del[0], -del[1], -del[2], -del[3]});
@@ -943,7 +957,7 @@ struct Bwd {
                 }
 #if MEP_BWD_EXP2
                 // (dot / 4 [+ c sp] - mask) log2 e - max log2 e with the mask and max terms combined
-                float arg = fmaf(st[r], INV_SCALE * LOG2E, -(mtl[kt] + mm[r]));
+                float arg = fmaf(st[r], INV_SCALE * LOG2E, MI ? -mm[r] : -(mtl[kt] + mm[r]));
                 if (PREV) arg = fmaf(cres * LOG2E, spv, arg);
                 const float pv = __builtin_amdgcn_exp2f(arg);
                 float gsv = pv * dp[r];
