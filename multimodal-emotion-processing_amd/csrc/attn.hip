@@ -429,7 +429,10 @@ MEP_DEV void attn_fwd_task(const mep_attn_desc& d, int qc, int h, int b, int lan
         const float inv = BF ? __builtin_amdgcn_rcpf(lt) : 1.0f / lt;
         const int q = q_lo + qt * 16 + c;
         if (g == 0 && q < Tq) {
-            stats[2 * (sbase + q)] = mq;
+            // row statistics for the backward: (max log2 e - log2(1/sum), 1/sum) -- the exp2
+            // backward's per-row exponent offset, formed once here instead of per backward tile and
+            // key-chunk wave (MEP_BWD_EXP2 = 0: (max, 1/sum))
+            stats[2 * (sbase + q)] = MEP_BWD_EXP2 ? mq * 1.4426950408889634f - __builtin_amdgcn_logf(inv) : mq;
             stats[2 * (sbase + q) + 1] = inv;
         }
 #pragma unroll
@@ -892,11 +895,15 @@ struct Bwd {
             // padded queries: max = +inf, 1/sum = 0 make P = exp(-inf) * 0 = 0 (and with it dS);
             // the max is kept pre-scaled by log2(e) for exp2
             const bool qok = qq < Tq;
+#if MEP_BWD_EXP2
+            mm[s] = qok ? in.st[s][0] : INFINITY;   // the forward's max log2 e - log2(1/sum)
+#else
             mm[s] = qok ? in.st[s][0] * LOG2E : INFINITY;
+#endif
             li[s] = qok ? in.st[s][1] : 0.f;
 #if MEP_BWD_EXP2
             // 1/sum folded into the exponent: P = exp2(.. - (max log2 e - log2(1/sum)))
-            mm[s] = qok ? mm[s] - __builtin_amdgcn_logf(li[s]) : INFINITY;
+            // (1/sum folded into the exponent by the forward's statistics)
 #endif
         }
         const S2 qs = BF ? S2{in.qaw[0], in.qaw[1], 0u, 0u} : split2(in.qa);

@@ -179,7 +179,13 @@ __global__ __launch_bounds__(GEMM_THREADS) void k_gemm(const mep_gemm_desc* __re
 constexpr int WG_WAVES = 4;
 constexpr int WG_THREADS = 64 * WG_WAVES;
 constexpr int WG_SLOTS_F = MEP_WG_PF + 1;     // k blocks of operand registers, fp32 instance
-constexpr int WG_SLOTS_B = 2;                 // bf16 instance (one workgroup per CU): one prefetch slot
+#ifndef MEP_WG_SLOTS_B
+#define MEP_WG_SLOTS_B 3   // bf16 instance: k blocks of operand registers (3: two prefetch slots; cfg3 28.2 -> 25.6 us, 4 slower)
+#endif
+#ifndef MEP_WG_OCC_BF
+#define MEP_WG_OCC_BF 1    // bf16 instance: workgroups per CU (2: the fp32 instance's narrow blocks)
+#endif
+constexpr int WG_SLOTS_B = MEP_WG_SLOTS_B;
 // largest 32MT x (32KT + 8) reduction buffer: MT = KT = 3 (occupancy 1, and the bf16 path); two
 // workgroups of 2 x 39 KB fit the CU's 160 KB
 constexpr int WG_RED = 96 * (96 + 8);
@@ -187,9 +193,9 @@ constexpr int WG_RED = 96 * (96 + 8);
 // bf16 path (one part per operand, no split registers): its own kernel instance at one workgroup
 // per CU with the wide blocks (the narrow ones double its operand loads: cfg5 bf16 308 vs 170 us at
 // KT = 1; the wide ones spill at 256 registers)
-__host__ __device__ constexpr int wg_occ(bool bf) { return bf ? 1 : MEP_WG_OCC; }
+__host__ __device__ constexpr int wg_occ(bool bf) { return bf ? MEP_WG_OCC_BF : MEP_WG_OCC; }
 __host__ __device__ constexpr int wg_kt(int mt, bool bf) {
-    if (MEP_WG_OCC > 1 && !bf) return mt == 4 ? MEP_WG_KT4 : 2;   // <= 96 accumulators (128 at MEP_WG_KT4 = 2)
+    if (wg_occ(bf) > 1) return mt == 4 ? (bf ? 2 : MEP_WG_KT4) : 2;   // <= 96 accumulators (128 at KT = 2, MT = 4)
     return mt == 4 ? 2 : mt == 3 ? 3 : 4;
 }
 

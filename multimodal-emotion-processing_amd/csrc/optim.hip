@@ -163,6 +163,9 @@ __global__ __launch_bounds__(256) void k_colsum(const mep_colsum_desc* __restric
 
 // out = sum of sources, 4 columns per thread (D % 4 == 0 for every model width); HS: bf16 source
 // and output rows (MEP_SUM_BF16, the bf16 path), summed in fp32
+// Sources in groups of SR_GROUP: every load of a group is issued before its first add (one
+// memory round trip per group, not per source); the adds keep source order.
+constexpr int SR_GROUP = 8;
 template <bool HS>
 MEP_DEV void sum_rows(const mep_sum_desc& d) {
     const int D4 = d.D / 4;
@@ -170,7 +173,15 @@ MEP_DEV void sum_rows(const mep_sum_desc& d) {
     for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
         const int tok = (int)(i / D4), c = 4 * (int)(i - (int64_t)tok * D4);
         f32x4 s = f32x4{0.f, 0.f, 0.f, 0.f};
-        for (int k = 0; k < d.n_src; ++k) s += ld4a(rowa<HS>(d.src[k], tok) + c);
+        for (int k0 = 0; k0 < d.n_src; k0 += SR_GROUP) {
+            f32x4 v[SR_GROUP];
+#pragma unroll
+            for (int k = 0; k < SR_GROUP; ++k)
+                if (k0 + k < d.n_src) v[k] = ld4a(rowa<HS>(d.src[k0 + k], tok) + c);
+#pragma unroll
+            for (int k = 0; k < SR_GROUP; ++k)
+                if (k0 + k < d.n_src) s += v[k];
+        }
         const auto o = rowa<HS>(d.out, tok) + c;
         if (d.accumulate & 1) s += ld4a(o);
         st4a(o, s);
@@ -205,15 +216,19 @@ extern "C" int mep_clip_adam_ext(float* params, float* grads, float* exp_avg, fl
     }
     // one float4 per thread (a single HBM round trip per lane in the update pass; 4 float4 per
     // thread serialised 4 dependent load -> store trips), one partial per workgroup for the norm
-    int grid = (int)((longest + OPT_THREADS * 4 - 1) / (OPT_THREADS * 4));
-    grid = grid < 1 ? 1 : (grid > NPART ? NPART : grid);
+    // The norm pass has one partial slot per workgroup (at most NPART); the update pass is not
+    // bound by the slots and runs one float4 per thread of the longest segment (at most 65535
+    // workgroups), so no thread loops over dependent load -> store trips
+    int grid_u = (int)((longest + OPT_THREADS * 4 - 1) / (OPT_THREADS * 4));
+    grid_u = grid_u < 1 ? 1 : (grid_u > 65535 ? 65535 : grid_u);
+    const int grid_n = grid_u > NPART ? NPART : grid_u;
     if (n_ext <= 0) {
-        hipLaunchKernelGGL(k_sqnorm, dim3(grid), dim3(OPT_THREADS), 0, (hipStream_t)stream, grads, s, partial, step, hyper);
+        hipLaunchKernelGGL(k_sqnorm, dim3(grid_n), dim3(OPT_THREADS), 0, (hipStream_t)stream, grads, s, partial, step, hyper);
         int rc = mep_check_launch("mep_clip_adam/sqnorm");
         if (rc) return rc;
     }
-    hipLaunchKernelGGL(k_clip_adam, dim3(grid), dim3(OPT_THREADS), 0, (hipStream_t)stream, params, grads, exp_avg,
-                       exp_avg_sq, s, partial, n_ext > 0 ? n_ext : grid, n_ext > 0 ? OPT_EXT0 : 0, hyper, step,
+    hipLaunchKernelGGL(k_clip_adam, dim3(grid_u), dim3(OPT_THREADS), 0, (hipStream_t)stream, params, grads, exp_avg,
+                       exp_avg_sq, s, partial, n_ext > 0 ? n_ext : grid_n, n_ext > 0 ? OPT_EXT0 : 0, hyper, step,
                        gnorm_out, decoupled);
     return mep_check_launch("mep_clip_adam/update");
 }
