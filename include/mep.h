@@ -165,7 +165,7 @@ typedef struct {
     uint64_t s_prev;    /* [B,H,Tq,Tk] or 0                                     */
     uint64_t c;         /* residual coefficient (device float*), used iff s_prev */
     uint64_t s_out;     /* [B,H,Tq,Tk] or 0                                     */
-    uint64_t stats;     /* [B,H,Tq,2]: row (max log2 e - log2(1/sum), 1/sum), the backward's input 
+    uint64_t stats;     /* [B,H,Tq,2]: (max log2 e - log2(1/sum), 1/sum) per row */
     int32_t  B, H, Tq, Tk;
 } mep_attn_desc;
 /* Launch geometry: forward one wave per (b, h, 64-query chunk), 4 waves (256 threads) per
