@@ -718,6 +718,7 @@ struct Bwd {
         float qa[4], da[4], db[4], qb[4], ob[4], dqo[4];
         f32x2 st[4];
         u32x2 qaw, daw;   // BF: Q / dO rows as raw bf16 operand words (no fp32 round trip)
+        u32x2 oaw;        // BF: O row (delta on the matrix core)
     };
     const mep_attn_bwd_desc& bd;
     int b, h, lane, c, g, hc, Tq, Tk, sbase;
@@ -786,6 +787,7 @@ struct Bwd {
         if constexpr (BF) {
             in.qaw = Qb.ld4raw(Qb.at(q0 + c, hc + 4 * g));
             in.daw = Gb.ld4raw(Gb.at(q0 + c, hc + 4 * g));
+            in.oaw = Ob.ld4raw(Ob.at(q0 + c, hc + 4 * g));
         } else {
             Qb.ld4(in.qa, Qb.at(q0 + c, hc + 4 * g));
             Gb.ld4(in.da, Gb.at(q0 + c, hc + 4 * g));
@@ -796,7 +798,7 @@ struct Bwd {
         for (int s = 0; s < 4; ++s) {
             in.db[s] = Gb.ld1(og, s * Gb.sT4);
             in.qb[s] = Qb.ld1(oq, s * Qb.sT4);
-            in.ob[s] = Ob.ld1(oo, s * Ob.sT4);
+            if (!BF) in.ob[s] = Ob.ld1(oo, s * Ob.sT4);
             in.st[s] = __builtin_bit_cast(f32x2, __builtin_amdgcn_raw_buffer_load_b64(rsStat, 8 * qg, 8 * s, 0));
             in.dqo[s] = dQb.ld1(od, s * dQb.sT4);
         }
@@ -850,12 +852,12 @@ struct Bwd {
             lcu16* H = (lcu16*)S;                 // operand o at H + 512 o: [16 rows][16] bf16
             in.qaw = *(lcu2*)(H + 16 * c + 4 * g);
             in.daw = *(lcu2*)(H + 512 + 16 * c + 4 * g);
+            in.oaw = *(lcu2*)(H + 1024 + 16 * c + 4 * g);
 #pragma unroll
             for (int s4 = 0; s4 < 4; ++s4) {
                 const int r = (4 * g + s4) * 16 + c;
                 in.qb[s4] = __builtin_bit_cast(float, (unsigned)H[r] << 16);
                 in.db[s4] = __builtin_bit_cast(float, (unsigned)H[512 + r] << 16);
-                in.ob[s4] = __builtin_bit_cast(float, (unsigned)H[1024 + r] << 16);
                 in.dqo[s4] = __builtin_bit_cast(float, (unsigned)H[1536 + r] << 16);
                 in.st[s4] = *(lcf2*)(L + 1024 + 2 * (4 * g + s4));
             }
@@ -887,11 +889,19 @@ struct Bwd {
         const int q0 = qt * 16;
         constexpr float LOG2E = 1.4426950408889634f;
         float mm[4], li[4], del[4];
+        floatx4 dd = zero4();
+        if constexpr (BF) {
+            // delta = rowsum(dO * O) as the diagonal of dO O^T: one 16x16x16 MFMA on the row words
+            // (lane (c, g) holds C[query 4g + r][query c]; C[q][q] sits in lane q of group q >> 2,
+            // register q & 3), gathered below -- instead of 4 products and 4 DPP row sums
+            dd = mfma16(op4(in.daw[0], in.daw[1]), op4(in.oaw[0], in.oaw[1]), zero4());
+        }
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
             const int qq = q0 + 4 * g + s;
             // delta = rowsum(dO * O): the 16 dims of query qq sit in one DPP row (lanes c)
-            del[s] = row16_sum(in.db[s] * in.ob[s]);
+            if constexpr (BF) del[s] = shfl(dd[s], 20 * g + s);
+            else del[s] = row16_sum(in.db[s] * in.ob[s]);
             // padded queries: max = +inf, 1/sum = 0 make P = exp(-inf) * 0 = 0 (and with it dS);
             // the max is kept pre-scaled by log2(e) for exp2
             const bool qok = qq < Tq;

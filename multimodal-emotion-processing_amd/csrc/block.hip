@@ -328,7 +328,7 @@ extern "C" int mep_epi_set_trace(void* p) { return (int)hipMemcpyToSymbol(HIP_SY
 #define MEP_EPI_STAMP(k) ((void)0)
 #endif
 
-template <int D, int NPART, int NW = NPART>
+template <int D, int NPART, int NW, bool DROP>
 MEP_DEV void epi_fwd_split(const mep_epi_desc& d, unsigned char* sm, int t_begin, int t_end) {
     constexpr int NI = D / 16, KB = D / 16, NP = D / 32;
     using WP = SplitW<D, NP, NW>;
@@ -338,7 +338,7 @@ MEP_DEV void epi_fwd_split(const mep_epi_desc& d, unsigned char* sm, int t_begin
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int c = lane & 15, g = lane >> 4;
     const int ntok = d.ntok;
-    const float p = d.drop_p;
+    const float p = DROP ? d.drop_p : 0.f;
     const uint64_t seed = (d.seed && p > 0.f) ? *G<const uint64_t>(d.seed) : 0;
     // global token offset of this shard's rows (seed[1] = the rank's first global batch row)
     const uint64_t tok0 = (d.seed && p > 0.f) ? G<const uint64_t>(d.seed)[1] * (uint64_t)d.q.T : 0;
@@ -442,7 +442,7 @@ MEP_DEV void epi_fwd_split(const mep_epi_desc& d, unsigned char* sm, int t_begin
 #endif
 }
 
-template <int D, int NPART, int NW = NPART>
+template <int D, int NPART, int NW, bool DROP>
 MEP_DEV void epi_bwd_split(const mep_epi_bwd_desc& bd, unsigned char* sm, int t_begin, int t_end) {
     constexpr int NI = D / 16, KB = D / 16, NP = D / 32;
     using WMT = SplitW<2 * D, NP, NW>;
@@ -453,7 +453,7 @@ MEP_DEV void epi_bwd_split(const mep_epi_bwd_desc& bd, unsigned char* sm, int t_
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int c = lane & 15, g = lane >> 4;
     const int ntok = d.ntok;
-    const float p = d.drop_p;
+    const float p = DROP ? d.drop_p : 0.f;
     const uint64_t seed = (d.seed && p > 0.f) ? *G<const uint64_t>(d.seed) : 0;
     // global token offset of this shard's rows (seed[1] = the rank's first global batch row)
     const uint64_t tok0 = (d.seed && p > 0.f) ? G<const uint64_t>(d.seed)[1] * (uint64_t)d.q.T : 0;
@@ -602,7 +602,9 @@ MEP_DEV void epi_bwd_split(const mep_epi_bwd_desc& bd, unsigned char* sm, int t_
 // intermediate, one staging, no second phase.  Parts per weight (NWP, NWM) are chosen so both fit
 // the 160 KB of LDS: D = 96 keeps Wp as two parts (forward; 43 + 120 KB) and Wm^T as two parts
 // (backward; 86 + 65 KB) -- a 2^-18 relative representation error of that weight.
-template <int D, int NPART, int NWP, int NWM>
+// DROP: a launch with dropout (drop_p > 0); the no-dropout instance has no hash code at all (the
+// dropout hash is most of the loop's instructions: a smaller, branch-free body)
+template <int D, int NPART, int NWP, int NWM, bool DROP>
 MEP_DEV void epi_fwd_one(const mep_epi_desc& d, unsigned char* sm, int t_begin, int t_end) {
     constexpr int NI = D / 16, KB = D / 16, NP = D / 32;
     using WP = SplitW<D, NP, NWP>;
@@ -611,7 +613,7 @@ MEP_DEV void epi_fwd_one(const mep_epi_desc& d, unsigned char* sm, int t_begin, 
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int c = lane & 15, g = lane >> 4;
     const int ntok = d.ntok;
-    const float p = d.drop_p;
+    const float p = DROP ? d.drop_p : 0.f;
     const uint64_t seed = (d.seed && p > 0.f) ? *G<const uint64_t>(d.seed) : 0;
     const uint64_t tok0 = (d.seed && p > 0.f) ? G<const uint64_t>(d.seed)[1] * (uint64_t)d.q.T : 0;
     gfloat* stats = G<float>(d.stats);
@@ -695,7 +697,7 @@ MEP_DEV void epi_fwd_one(const mep_epi_desc& d, unsigned char* sm, int t_begin, 
     }
 }
 
-template <int D, int NPART, int NWP, int NWM>
+template <int D, int NPART, int NWP, int NWM, bool DROP>
 MEP_DEV void epi_bwd_one(const mep_epi_bwd_desc& bd, unsigned char* sm, int t_begin, int t_end) {
     constexpr int NI = D / 16, KB = D / 16, NP = D / 32;
     using WMT = SplitW<2 * D, NP, NWM>;
@@ -706,7 +708,7 @@ MEP_DEV void epi_bwd_one(const mep_epi_bwd_desc& bd, unsigned char* sm, int t_be
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int c = lane & 15, g = lane >> 4;
     const int ntok = d.ntok;
-    const float p = d.drop_p;
+    const float p = DROP ? d.drop_p : 0.f;
     const uint64_t seed = (d.seed && p > 0.f) ? *G<const uint64_t>(d.seed) : 0;
     const uint64_t tok0 = (d.seed && p > 0.f) ? G<const uint64_t>(d.seed)[1] * (uint64_t)d.q.T : 0;
     const gfloat* stats = G<const float>(d.stats);
@@ -863,14 +865,16 @@ __global__ __launch_bounds__(ETHREADS) __attribute__((amdgpu_waves_per_eu(MEP_EP
     if constexpr (EpiOne<D, BF16>::FWD) {
         using E = EpiOne<D, BF16>;
         __shared__ __attribute__((aligned(16))) unsigned char sm1[E::FWD_BYTES];
-        epi_fwd_one<D, E::NPART, E::FWD_WP, E::FWD_WM>(d, sm1, t_begin, t_end);
+        if (d.drop_p > 0.f) epi_fwd_one<D, E::NPART, E::FWD_WP, E::FWD_WM, true>(d, sm1, t_begin, t_end);
+        else epi_fwd_one<D, E::NPART, E::FWD_WP, E::FWD_WM, false>(d, sm1, t_begin, t_end);
         return;
     }
     if constexpr (BF16 || (MEP_EPI_SPLIT && D <= 96) || (MEP_EPI_SPLIT128_FWD && D == 128)) {
         constexpr int NPART = BF16 ? 1 : 3, NW = BF16 ? 1 : (D == 128 ? 2 : 3);
         constexpr int BYTES = SplitW<D, D / 16, NW>::BYTES;   // the larger phase (Wm)
         __shared__ __attribute__((aligned(16))) unsigned char sm6[BYTES];
-        epi_fwd_split<D, NPART, NW>(d, sm6, t_begin, t_end);
+        if (d.drop_p > 0.f) epi_fwd_split<D, NPART, NW, true>(d, sm6, t_begin, t_end);
+        else epi_fwd_split<D, NPART, NW, false>(d, sm6, t_begin, t_end);
         return;
     }
     __shared__ __attribute__((aligned(16))) float smem[Geo::FWD];
@@ -1024,14 +1028,16 @@ __global__ __launch_bounds__(ETHREADS) __attribute__((amdgpu_waves_per_eu(MEP_EP
     if constexpr (EpiOne<D, BF16>::BWD) {
         using E = EpiOne<D, BF16>;
         __shared__ __attribute__((aligned(16))) unsigned char sm1[E::BWD_BYTES];
-        epi_bwd_one<D, E::NPART, E::BWD_WP, E::BWD_WM>(bd, sm1, t_begin, t_end);
+        if (d.drop_p > 0.f) epi_bwd_one<D, E::NPART, E::BWD_WP, E::BWD_WM, true>(bd, sm1, t_begin, t_end);
+        else epi_bwd_one<D, E::NPART, E::BWD_WP, E::BWD_WM, false>(bd, sm1, t_begin, t_end);
         return;
     }
     if constexpr (BF16 || (MEP_EPI_SPLIT && D <= 96) || (MEP_EPI_SPLIT128_BWD && D == 128)) {
         constexpr int NPART = BF16 ? 1 : 3, NW = BF16 ? 1 : (D == 128 ? 2 : 3);
         constexpr int BYTES = SplitW<2 * D, D / 32, NW>::BYTES;   // the larger phase (Wm^T)
         __shared__ __attribute__((aligned(16))) unsigned char sm6[BYTES];
-        epi_bwd_split<D, NPART, NW>(bd, sm6, t_begin, t_end);
+        if (d.drop_p > 0.f) epi_bwd_split<D, NPART, NW, true>(bd, sm6, t_begin, t_end);
+        else epi_bwd_split<D, NPART, NW, false>(bd, sm6, t_begin, t_end);
         return;
     }
     __shared__ __attribute__((aligned(16))) float smem[Geo::BWD];

@@ -120,7 +120,7 @@ def _params(model):
     return {k: p.detach().clone() for k, p in model.named_parameters()}
 
 
-def _exchange_case(model_fn, batch, B, graph, monkeypatch, rdrop=False):
+def _exchange_case(model_fn, batch, B, graph, monkeypatch, rdrop=False, doubled=True):
     # -- the DP engine: rank 0 of two identical ranks
     mc = model_fn()
     ec = _engine(mc, True, graph)
@@ -171,6 +171,8 @@ def _exchange_case(model_fn, batch, B, graph, monkeypatch, rdrop=False):
         for name in pr:
             assert torch.equal(pc[name], pr[name]), 'step %d: %s' % (k, name)
 
+    if not doubled:
+        return
     # -- one rank, the batch concatenated with itself (2 B rows), one step
     md = model_fn()
     ed = _engine(md, False, False)
@@ -201,6 +203,23 @@ def test_dp_exchange_two_rank_sum_cmu_cfg3(nccl_world1, cuda, graph, monkeypatch
     meta, _ = fixtures.load('cmu_cfg3')
     batch = cuda_batch(meta, cuda)
     _exchange_case(lambda: cmu_model(meta, cuda), batch, batch[-1].shape[0], graph, monkeypatch)
+
+
+@pytest.mark.parametrize('graph', [False, True], ids=['eager', 'graph'])
+def test_dp_exchange_two_rank_sum_cmu_cfg3_bf16(nccl_world1, cuda, graph, monkeypatch):
+    """The same exchange on the bf16 path (the bench's default precision for cfg3 / cfg4): bf16
+    activations, fp32 flat gradient and optimizer.  Every bit-for-bit check holds as on the fp32
+    path (the power-of-two loss scale and the SUM's 2 are exact); the doubled-batch comparison is
+    left to the fp32 cases (2 B rows change the weight-gradient chunking, whose bf16 rounding then
+    differs by more than the fp32 post-step tolerance)."""
+    meta, _ = fixtures.load('cmu_cfg3')
+    batch = cuda_batch(meta, cuda)
+
+    def model():
+        m = cmu_model(meta, cuda)
+        m.mep_precision = 'bf16'
+        return m
+    _exchange_case(model, batch, batch[-1].shape[0], graph, monkeypatch, doubled=False)
 
 
 @pytest.mark.parametrize('graph', [False, True], ids=['eager', 'graph'])
