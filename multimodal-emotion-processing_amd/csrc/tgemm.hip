@@ -33,6 +33,12 @@ constexpr int TG_THREADS = 64 * TG_WAVES;
 #define MEP_TG_NI 8        // 16-column tiles of a workgroup's N tile at N >= 128
 #endif
 constexpr int TG_TT = MEP_TG_TT;                  // 16-token tiles per wave
+#ifndef MEP_TG_PF
+#define MEP_TG_PF 4        // fp32 path: k chunks of W / X in registers (loads 3 chunks ahead; cfg5 125 -> 104 us)
+#endif
+#ifndef MEP_TG_PF_BF
+#define MEP_TG_PF_BF 2     // bf16 path: one chunk ahead keeps two workgroups per CU (3-6 chunks: one, 92 vs 76 us)
+#endif
 constexpr int TG_BM = 16 * TG_TT * TG_WAVES;      // tokens per workgroup
 
 // W(n, k .. k+3) of the staged chunk, zero past K / N
@@ -56,6 +62,7 @@ MEP_DEV f32x4 tg_wfrag(const gfloat* W, int ldw, bool vec, int n, int N, int k, 
 template <int NI, int NPART, bool WNT>
 __global__ __launch_bounds__(TG_THREADS) void k_tgemm(const mep_gemm_desc* __restrict__ descs) {
     constexpr int BN = 16 * NI;
+    constexpr int TG_PF = NPART == 1 ? MEP_TG_PF_BF : MEP_TG_PF;
     using WS = SplitW<BN, 1, NPART>;                     // one k pair (32 wide) of BN rows
     __shared__ __attribute__((aligned(16))) unsigned char sm[2 * WS::BYTES];
     const mep_gemm_desc& d = descs[blockIdx.y];
@@ -74,24 +81,27 @@ __global__ __launch_bounds__(TG_THREADS) void k_tgemm(const mep_gemm_desc* __res
     const gfloat* W = G<const float>(d.w);
     const bool wvec = WNT && (d.ldw % 4 == 0) && ((d.w & 15) == 0);
     constexpr int NU = BN * 4, UPT = (NU + TG_THREADS - 1) / TG_THREADS;
-    f32x4 wr[UPT][2];
-    auto load_w = [&](int kc) {
+    // TG_PF chunks of W and X in registers: chunk kc + TG_PF - 1's loads go out while chunk kc
+    // multiplies, so a chunk's loads have TG_PF - 1 chunks of work to arrive in (one chunk ahead
+    // left every chunk waiting a full memory latency: the launch was latency-bound)
+    f32x4 wr[TG_PF][UPT][2];
+    auto load_w = [&](int s, int kc) {
         const int k0 = 32 * kc;
 #pragma unroll
         for (int u = 0; u < UPT; ++u) {
             const int idx = threadIdx.x + TG_THREADS * u;
             const int n = idx % BN, gg = idx / BN;
             if (idx < NU) {
-                wr[u][0] = tg_wfrag<WNT>(W, d.ldw, wvec, n0 + n, N, k0 + 4 * gg, K);
-                wr[u][1] = tg_wfrag<WNT>(W, d.ldw, wvec, n0 + n, N, k0 + 16 + 4 * gg, K);
+                wr[s][u][0] = tg_wfrag<WNT>(W, d.ldw, wvec, n0 + n, N, k0 + 4 * gg, K);
+                wr[s][u][1] = tg_wfrag<WNT>(W, d.ldw, wvec, n0 + n, N, k0 + 16 + 4 * gg, K);
             }
         }
     };
-    auto put_w = [&](const WS& ws) {
+    auto put_w = [&](int s, const WS& ws) {
 #pragma unroll
         for (int u = 0; u < UPT; ++u) {
             const int idx = threadIdx.x + TG_THREADS * u;
-            if (idx < NU) ws.put(idx % BN, 0, idx / BN, wr[u][0], wr[u][1]);
+            if (idx < NU) ws.put(idx % BN, 0, idx / BN, wr[s][u][0], wr[s][u][1]);
         }
     };
 
@@ -108,8 +118,8 @@ __global__ __launch_bounds__(TG_THREADS) void k_tgemm(const mep_gemm_desc* __res
         const int tok = min(tok0 + 16 * (TG_TT * wave + t) + c, ntok - 1);
         xoff[t] = ES * ((int)row_off(d.x, tok) + 4 * g);
     }
-    f32x4 xr[TG_TT][2];
-    auto load_x = [&](int kc) {
+    f32x4 xr[TG_PF][TG_TT][2];
+    auto load_x = [&](int s, int kc) {
 #pragma unroll
         for (int t = 0; t < TG_TT; ++t)
 #pragma unroll
@@ -117,17 +127,17 @@ __global__ __launch_bounds__(TG_THREADS) void k_tgemm(const mep_gemm_desc* __res
                 const int o = xoff[t] + 32 * ES * kc + 16 * ES * h;   // bytes: k0 + 16 h + 4g
                 if (HS && xvec) {
                     const u32x2a w = __builtin_bit_cast(u32x2a, __builtin_amdgcn_raw_buffer_load_b64(rsX, o, 0, 0));
-                    xr[t][h] = f32x4{bf16_word_lo(w[0]), bf16_word_hi(w[0]), bf16_word_lo(w[1]), bf16_word_hi(w[1])};
+                    xr[s][t][h] = f32x4{bf16_word_lo(w[0]), bf16_word_hi(w[0]), bf16_word_lo(w[1]), bf16_word_hi(w[1])};
                 } else if (HS) {
 #pragma unroll
                     for (int e = 0; e < 4; ++e)
-                        xr[t][h][e] = __builtin_bit_cast(float, (unsigned)__builtin_amdgcn_raw_buffer_load_b16(rsX, o + 2 * e, 0, 0) << 16);
+                        xr[s][t][h][e] = __builtin_bit_cast(float, (unsigned)__builtin_amdgcn_raw_buffer_load_b16(rsX, o + 2 * e, 0, 0) << 16);
                 } else if (xvec) {
-                    xr[t][h] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rsX, o, 0, 0));
+                    xr[s][t][h] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rsX, o, 0, 0));
                 } else {
 #pragma unroll
                     for (int e = 0; e < 4; ++e)
-                        xr[t][h][e] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsX, o + 4 * e, 0, 0));
+                        xr[s][t][h][e] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsX, o + 4 * e, 0, 0));
                 }
             }
     };
@@ -138,17 +148,20 @@ __global__ __launch_bounds__(TG_THREADS) void k_tgemm(const mep_gemm_desc* __res
 #pragma unroll
         for (int i = 0; i < NI; ++i) acc[t][i] = zero_f4();
 
-    load_w(0);
-    load_x(0);
-    put_w(wbuf(0));
+    // chunk kc lives in register slot kc % TG_PF and LDS buffer kc & 1
+#pragma unroll
+    for (int s = 0; s < TG_PF - 1; ++s)
+        if (s < nkc) { load_w(s, s); load_x(s, s); }
+    put_w(0, wbuf(0));
     __syncthreads();
-    for (int kc = 0; kc < nkc; ++kc) {
+    auto step = [&](int kc, int s) {   // s = kc % TG_PF (compile-time in the unrolled loop)
         OpN<NPART> xo[TG_TT];
 #pragma unroll
-        for (int t = 0; t < TG_TT; ++t) xo[t] = opn<NPART>(xr[t][0], xr[t][1]);
-        if (kc + 1 < nkc) {                 // next chunk's loads in flight across this chunk's MFMAs
-            load_w(kc + 1);
-            load_x(kc + 1);
+        for (int t = 0; t < TG_TT; ++t) xo[t] = opn<NPART>(xr[s][t][0], xr[s][t][1]);
+        const int kn = kc + TG_PF - 1, sn = (s + TG_PF - 1) % TG_PF;
+        if (kn < nkc) {                     // TG_PF - 1 chunks ahead, in flight across this chunk's MFMAs
+            load_w(sn, kn);
+            load_x(sn, kn);
         }
         __builtin_amdgcn_sched_barrier(0);
         const WS ws = wbuf(kc & 1);
@@ -159,9 +172,17 @@ __global__ __launch_bounds__(TG_THREADS) void k_tgemm(const mep_gemm_desc* __res
             for (int t = 0; t < TG_TT; ++t) acc[t][i] = mma_n<NPART>(w, xo[t], acc[t][i]);
             if (i & 1) __builtin_amdgcn_sched_barrier(0);
         }
-        if (kc + 1 < nkc) put_w(wbuf((kc + 1) & 1));   // its last readers finished before the last barrier
+        if (kc + 1 < nkc) put_w((s + 1) % TG_PF, wbuf((kc + 1) & 1));   // its last readers finished before the last barrier
         __syncthreads();
+    };
+    int kc = 0;
+    for (; kc + TG_PF <= nkc; kc += TG_PF) {
+#pragma unroll
+        for (int s = 0; s < TG_PF; ++s) step(kc + s, s);
     }
+#pragma unroll
+    for (int s = 0; s < TG_PF - 1; ++s)
+        if (kc + s < nkc) step(kc + s, s);
 
     // ---- epilogue: token c of tile t, features n0 + 16 i + 4g .. +3
     const gfloat* bias = G<const float>(d.bias);
