@@ -32,7 +32,7 @@ extern "C" {
 #endif
 
 #define MEP_EINVAL (-1000)
-#define MEP_ABI_VERSION 2
+#define MEP_ABI_VERSION 3
 
 typedef void* mep_stream_t; /* a hipStream_t */
 
@@ -241,6 +241,11 @@ typedef struct {
     int32_t  drop_stream;/* distinct per block */
     mep_rows out_h;      /* MEP_PREC_BF16: optional bf16 copy of out (ptr 0: none) -- the next
                             layer's q of a residual chain, whose out stays fp32 for the pool */
+    uint64_t drop_bits;  /* optional (0: none) uint32 [ceil(ntok/16)][2][64], zeroed once: with
+                            dropout the forward writes the keep bits of every 16-token tile and
+                            site (0: xp, 1: out) -- lane (c, g) of the tile's wave, bit 4 i + r =
+                            feature 16 i + 4 g + r of token 16 tile + c -- and the backward reads
+                            them instead of re-hashing (the same masks; ABI 3) */
 } mep_epi_desc;
 /* D (32/64/96/128, shared by every descriptor of the launch) selects the compiled variant.
  * Geometry: max_tiles = workgroups PER DESCRIPTOR; each workgroup (512 threads) stages its block's

@@ -71,7 +71,8 @@ class AttnBwdDesc(ctypes.Structure):
 class EpiDesc(ctypes.Structure):
     _fields_ = [('q', Rows), ('x', Rows), ('xp', Rows), ('z', Rows), ('out', Rows),
                 ('wp', u64), ('wm', u64), ('ln_w', u64), ('ln_b', u64), ('stats', u64), ('seed', u64),
-                ('ntok', i32), ('D', i32), ('drop_p', f32), ('drop_stream', i32), ('out_h', Rows)]
+                ('ntok', i32), ('D', i32), ('drop_p', f32), ('drop_stream', i32), ('out_h', Rows),
+                ('drop_bits', u64)]
 
 
 class EpiBwdDesc(ctypes.Structure):
@@ -278,6 +279,7 @@ SIGNATURES.update({
 })
 
 _LIB = None
+ABI_VERSION = 3   # include/mep.h MEP_ABI_VERSION
 
 
 def lib():
@@ -292,6 +294,8 @@ def lib():
             fn = getattr(L, name)
             fn.argtypes = args
             fn.restype = ctypes.c_int
+        if L.mep_abi_version() != ABI_VERSION:   # descriptor layouts would not match: fail loudly
+            raise OSError('%s has ABI %d, this host expects %d: rebuild it' % (LIB_PATH, L.mep_abi_version(), ABI_VERSION))
         _LIB = L
     return _LIB
 

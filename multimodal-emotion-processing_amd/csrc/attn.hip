@@ -196,6 +196,11 @@ MEP_DEV floatx4 dot_score(const S3& p, const S3& u, floatx4 acc) {
 #ifndef MEP_BWD_TR
 #define MEP_BWD_TR 0     // dS transposed as packed [key][query] words + ds_read_b64_tr_b16 (47.6-48.5 vs 45.6 us: off)
 #endif
+#ifndef MEP_BWD_DELTA_MF
+#define MEP_BWD_DELTA_MF 0   // fp32 backward: delta = rowsum(dO O) on the matrix core (2-part splits).
+                             // Off: delta is subtracted from dP, and its 2^-16 product error moved one
+                             // ren_drop_long unify-weight gradient 3.9e-3 relative (rtol 1e-3)
+#endif
 #ifndef MEP_BWD_EXP2
 #define MEP_BWD_EXP2 1   // P = exp2(dot * log2e/sqrt(hd) - (mask * log2e + max * log2e)): one fma per score
 #endif
@@ -719,6 +724,7 @@ struct Bwd {
         f32x2 st[4];
         u32x2 qaw, daw;   // BF: Q / dO rows as raw bf16 operand words (no fp32 round trip)
         u32x2 oaw;        // BF: O row (delta on the matrix core)
+        float oa[4];      // fp32 path, MEP_BWD_DELTA_MF: O row (query c, dims 4g ..)
     };
     const mep_attn_bwd_desc& bd;
     int b, h, lane, c, g, hc, Tq, Tk, sbase;
@@ -791,6 +797,7 @@ struct Bwd {
         } else {
             Qb.ld4(in.qa, Qb.at(q0 + c, hc + 4 * g));
             Gb.ld4(in.da, Gb.at(q0 + c, hc + 4 * g));
+            if (MEP_BWD_DELTA_MF) Ob.ld4(in.oa, Ob.at(q0 + c, hc + 4 * g));
         }
         const int qg = q0 + 4 * g;
         const int og = Gb.at(qg, hc + c), oq = Qb.at(qg, hc + c), oo = Ob.at(qg, hc + c), od = dQb.at(qg, hc + c);
@@ -798,7 +805,7 @@ struct Bwd {
         for (int s = 0; s < 4; ++s) {
             in.db[s] = Gb.ld1(og, s * Gb.sT4);
             in.qb[s] = Qb.ld1(oq, s * Qb.sT4);
-            if (!BF) in.ob[s] = Ob.ld1(oo, s * Ob.sT4);
+            if (!BF && !MEP_BWD_DELTA_MF) in.ob[s] = Ob.ld1(oo, s * Ob.sT4);
             in.st[s] = __builtin_bit_cast(f32x2, __builtin_amdgcn_raw_buffer_load_b64(rsStat, 8 * qg, 8 * s, 0));
             in.dqo[s] = dQb.ld1(od, s * dQb.sT4);
         }
@@ -866,12 +873,17 @@ struct Bwd {
         const f32x4 qa = *(lcf4*)(L + 16 * c + 4 * g), da = *(lcf4*)(L + 256 + 16 * c + 4 * g);
 #pragma unroll
         for (int e = 0; e < 4; ++e) { in.qa[e] = qa[e]; in.da[e] = da[e]; }
+        if (MEP_BWD_DELTA_MF) {
+            const f32x4 oa = *(lcf4*)(L + 512 + 16 * c + 4 * g);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) in.oa[e] = oa[e];
+        }
 #pragma unroll
         for (int s4 = 0; s4 < 4; ++s4) {
             const int r = (4 * g + s4) * 16 + c;
             in.qb[s4] = L[r];
             in.db[s4] = L[256 + r];
-            in.ob[s4] = L[512 + r];
+            if (!MEP_BWD_DELTA_MF) in.ob[s4] = L[512 + r];
             in.dqo[s4] = L[768 + r];
             in.st[s4] = *(lcf2*)(L + 1024 + 2 * (4 * g + s4));
         }
@@ -890,6 +902,15 @@ struct Bwd {
         constexpr float LOG2E = 1.4426950408889634f;
         float mm[4], li[4], del[4];
         floatx4 dd = zero4();
+        constexpr bool DMF = BF || MEP_BWD_DELTA_MF;   // delta on the matrix core
+        if constexpr (!BF && MEP_BWD_DELTA_MF) {
+            // fp32 path: dO and O rows as 2-part splits, products d0 o0 + d1 o0 + d0 o1 (<= 2^-16
+            // relative per product, the accuracy of the dP it is subtracted from)
+            const S2 d2 = split2(in.da), o2 = split2(in.oa);
+            dd = mfma16(op4(d2.h0, d2.h1), op4(o2.h0, o2.h1), dd);
+            dd = mfma16(op4(d2.l0, d2.l1), op4(o2.h0, o2.h1), dd);
+            dd = mfma16(op4(d2.h0, d2.h1), op4(o2.l0, o2.l1), dd);
+        }
         if constexpr (BF) {
             // delta = rowsum(dO * O) as the diagonal of dO O^T: one 16x16x16 MFMA on the row words
             // (lane (c, g) holds C[query 4g + r][query c]; C[q][q] sits in lane q of group q >> 2,
@@ -900,7 +921,7 @@ struct Bwd {
         for (int s = 0; s < 4; ++s) {
             const int qq = q0 + 4 * g + s;
             // delta = rowsum(dO * O): the 16 dims of query qq sit in one DPP row (lanes c)
-            if constexpr (BF) del[s] = shfl(dd[s], 20 * g + s);
+            if constexpr (DMF) del[s] = shfl(dd[s], 20 * g + s);
             else del[s] = row16_sum(in.db[s] * in.ob[s]);
             // padded queries: max = +inf, 1/sum = 0 make P = exp(-inf) * 0 = 0 (and with it dS);
             // the max is kept pre-scaled by log2(e) for exp2

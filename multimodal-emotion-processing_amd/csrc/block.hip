@@ -26,6 +26,9 @@
 #ifndef MEP_EPI_ONE
 #define MEP_EPI_ONE 0   // single-phase epilogues (both weights resident, intermediate in registers)
 #endif
+#ifndef MEP_NO_DROPBITS
+#define MEP_NO_DROPBITS 0  // 1: ignore mep_epi_desc.drop_bits (the backward re-hashes; A/B only)
+#endif
 #ifndef MEP_EPI_ONE_FWD
 #define MEP_EPI_ONE_FWD MEP_EPI_ONE
 #endif
@@ -187,6 +190,10 @@ MEP_DEV void epi_fwd_tiles(const mep_epi_desc& d, const AP& wp, const AM& wm, in
     const uint64_t seed = (d.seed && p > 0.f) ? *G<const uint64_t>(d.seed) : 0;
     // global token offset of this shard's rows (seed[1] = the rank's first global batch row)
     const uint64_t tok0 = (d.seed && p > 0.f) ? G<const uint64_t>(d.seed)[1] * (uint64_t)d.q.T : 0;
+    const uint64_t dbits = p > 0.f && !MEP_NO_DROPBITS ? d.drop_bits : 0;   // the forward's keep bits (0: hash)
+    const bool have_bits = dbits != 0;
+    const float keep_s = p > 0.f ? 1.0f / (1.0f - p) : 1.0f;   // == drop_scale's kept value
+    (void)have_bits; (void)keep_s;
     gfloat* stats = G<float>(d.stats);
     AM wm_x = wm;
     wm_x.pos0 += D;                     // Wm[:, D:], the xp half of the concat
@@ -208,11 +215,13 @@ MEP_DEV void epi_fwd_tiles(const mep_epi_desc& d, const AP& wp, const AM& wm, in
         for (int i = 0; i < NI; ++i) { xp[i] = zero_f4(); z[i] = zero_f4(); }
         tgemm<NI, KB>(xp, wp, [&](int kb) { return xb[kb]; });
         if (p > 0.f) {
+            uint32_t kb0 = 0;
 #pragma unroll
             for (int i = 0; i < NI; ++i)
 #pragma unroll
                 for (int r = 0; r < 4; ++r)
-                    xp[i][r] *= drop_scale(seed, 2u * d.drop_stream, (tok0 + (uint64_t)tok) * D + 16 * i + 4 * g + r, p);
+                    xp[i][r] *= drop_rec(seed, 2u * d.drop_stream, (tok0 + (uint64_t)tok) * D + 16 * i + 4 * g + r, p, kb0, 4 * i + r);
+            drop_bits_put(drop_bits_ptr(dbits, tok, 0), kb0);
         }
         tgemm<NI, KB>(z, wm, [&](int kb) { return qb[kb]; });              // q half of [q | xp]
         tgemm<NI, KB>(z, wm_x, [&](int kb) { return xp[kb]; });            // xp half
@@ -235,6 +244,7 @@ MEP_DEV void epi_fwd_tiles(const mep_epi_desc& d, const AP& wp, const AM& wm, in
             gfloat* zr = row_ptr(d.z, tok);
             gfloat* orow = row_ptr(d.out, tok);
             gfloat* pr = row_ptr(d.xp, tok);
+            uint32_t kb1 = 0;   // keep bits of the out site
 #pragma unroll
             for (int i = 0; i < NI; ++i) {
                 const int col = 16 * i + 4 * g;
@@ -243,12 +253,13 @@ MEP_DEV void epi_fwd_tiles(const mep_epi_desc& d, const AP& wp, const AM& wm, in
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     y[r] = (z[i][r] - mean) * rstd * w[r] + b[r];
-                    if (p > 0.f) y[r] *= drop_scale(seed, 2u * d.drop_stream + 1u, (tok0 + (uint64_t)tok) * D + col + r, p);
+                    if (p > 0.f) y[r] *= drop_rec(seed, 2u * d.drop_stream + 1u, (tok0 + (uint64_t)tok) * D + col + r, p, kb1, 4 * i + r);
                 }
                 stg4(zr + col, f4(z[i]));
                 stg4(orow + col, f4(y));
                 stg4(pr + col, f4(xp[i]));
             }
+            if (p > 0.f) drop_bits_put(drop_bits_ptr(dbits, tok, 1), kb1);
             if (g == 0) { stats[2 * tok] = mean; stats[2 * tok + 1] = rstd; }
         }
     }
@@ -342,6 +353,10 @@ MEP_DEV void epi_fwd_split(const mep_epi_desc& d, unsigned char* sm, int t_begin
     const uint64_t seed = (d.seed && p > 0.f) ? *G<const uint64_t>(d.seed) : 0;
     // global token offset of this shard's rows (seed[1] = the rank's first global batch row)
     const uint64_t tok0 = (d.seed && p > 0.f) ? G<const uint64_t>(d.seed)[1] * (uint64_t)d.q.T : 0;
+    const uint64_t dbits = p > 0.f && !MEP_NO_DROPBITS ? d.drop_bits : 0;   // the forward's keep bits (0: hash)
+    const bool have_bits = dbits != 0;
+    const float keep_s = p > 0.f ? 1.0f / (1.0f - p) : 1.0f;   // == drop_scale's kept value
+    (void)have_bits; (void)keep_s;
     gfloat* stats = G<float>(d.stats);
     typedef __attribute__((address_space(3))) unsigned char lbyte;
     const WP wp{(lbyte*)sm, 0};
@@ -370,15 +385,17 @@ MEP_DEV void epi_fwd_split(const mep_epi_desc& d, unsigned char* sm, int t_begin
         tgemm_n<NI, NP, NPART, NW>(xp, [&](int i, int pp) { return wp.frag(i, pp); }, [&](int pp) { return xs[pp]; });
         if (tok < ntok) {
             const auto pr = rowa<HS>(d.xp, tok);
+            uint32_t kb0 = 0;
 #pragma unroll
             for (int i = 0; i < NI; ++i) {
                 if (p > 0.f) {
 #pragma unroll
                     for (int r = 0; r < 4; ++r)
-                        xp[i][r] *= drop_scale(seed, 2u * d.drop_stream, (tok0 + (uint64_t)tok) * D + 16 * i + 4 * g + r, p);
+                        xp[i][r] *= drop_rec(seed, 2u * d.drop_stream, (tok0 + (uint64_t)tok) * D + 16 * i + 4 * g + r, p, kb0, 4 * i + r);
                 }
                 st4a(pr + 16 * i + 4 * g, xp[i]);
             }
+            if (p > 0.f) drop_bits_put(drop_bits_ptr(dbits, tok, 0), kb0);
         }
     }
     // ---- phase 2: z = [q | xp] Wm^T, out = drop(LayerNorm(z))
@@ -418,6 +435,7 @@ MEP_DEV void epi_fwd_split(const mep_epi_desc& d, unsigned char* sm, int t_begin
             const auto zr = rowa<HS>(d.z, tok);
             gfloat* orow = row_ptr(d.out, tok);
             const auto hrow = (HS && d.out_h.ptr) ? rowa<true>(d.out_h, tok) : nullptr;   // next layer's q
+            uint32_t kb1 = 0;   // keep bits of the out site
 #pragma unroll
             for (int i = 0; i < NI; ++i) {
                 const int col = 16 * i + 4 * g;
@@ -426,12 +444,13 @@ MEP_DEV void epi_fwd_split(const mep_epi_desc& d, unsigned char* sm, int t_begin
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     y[r] = (z[i][r] - mean) * rstd * w[r] + b[r];
-                    if (p > 0.f) y[r] *= drop_scale(seed, 2u * d.drop_stream + 1u, (tok0 + (uint64_t)tok) * D + col + r, p);
+                    if (p > 0.f) y[r] *= drop_rec(seed, 2u * d.drop_stream + 1u, (tok0 + (uint64_t)tok) * D + col + r, p, kb1, 4 * i + r);
                 }
                 st4a(zr + col, z[i]);
                 stg4(orow + col, f4(y));
                 if (HS && d.out_h.ptr) st4a(hrow + col, y);
             }
+            if (p > 0.f) drop_bits_put(drop_bits_ptr(dbits, tok, 1), kb1);
             if (g == 0) { stats[2 * tok] = mean; stats[2 * tok + 1] = rstd; }
         }
     }
@@ -457,6 +476,10 @@ MEP_DEV void epi_bwd_split(const mep_epi_bwd_desc& bd, unsigned char* sm, int t_
     const uint64_t seed = (d.seed && p > 0.f) ? *G<const uint64_t>(d.seed) : 0;
     // global token offset of this shard's rows (seed[1] = the rank's first global batch row)
     const uint64_t tok0 = (d.seed && p > 0.f) ? G<const uint64_t>(d.seed)[1] * (uint64_t)d.q.T : 0;
+    const uint64_t dbits = p > 0.f && !MEP_NO_DROPBITS ? d.drop_bits : 0;   // the forward's keep bits (0: hash)
+    const bool have_bits = dbits != 0;
+    const float keep_s = p > 0.f ? 1.0f / (1.0f - p) : 1.0f;   // == drop_scale's kept value
+    (void)have_bits; (void)keep_s;
     const gfloat* stats = G<const float>(d.stats);
     gfloat* lpart = G<float>(bd.ln_partial);
     typedef __attribute__((address_space(3))) unsigned char lbyte;
@@ -482,6 +505,8 @@ MEP_DEV void epi_bwd_split(const mep_epi_bwd_desc& bd, unsigned char* sm, int t_
     __syncthreads();
     for (int tile = t_begin + wave; tile < t_end; tile += EWAVES) {
         const int tok = tile * 16 + c;
+        const uint32_t kbb0 = have_bits ? drop_bits_get(drop_bits_ptr(dbits, tok, 0)) : 0u;   // the forward's keep bits
+        const uint32_t kbb1 = have_bits ? drop_bits_get(drop_bits_ptr(dbits, tok, 1)) : 0u;
         const bool ok = tok < ntok;
         const int tc = min(tok, ntok - 1);
         f32x4 dz[NI], zz[NI];
@@ -504,7 +529,7 @@ MEP_DEV void epi_bwd_split(const mep_epi_bwd_desc& bd, unsigned char* sm, int t_
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 float gg = dz[i][r];
-                if (p > 0.f) gg *= drop_scale(seed, 2u * d.drop_stream + 1u, (tok0 + (uint64_t)tok) * D + col + r, p);
+                if (p > 0.f) gg *= drop_use(have_bits, kbb1, 4 * i + r, keep_s, seed, 2u * d.drop_stream + 1u, (tok0 + (uint64_t)tok) * D + col + r, p);
                 gg = ok ? gg : 0.f;
                 const float x = (zz[i][r] - mu) * rs;
                 const float gw = gg * w[r];
@@ -547,7 +572,7 @@ MEP_DEV void epi_bwd_split(const mep_epi_bwd_desc& bd, unsigned char* sm, int t_
                 if (p > 0.f) {
 #pragma unroll
                     for (int r = 0; r < 4; ++r)
-                        acc[i][r] *= drop_scale(seed, 2u * d.drop_stream, (tok0 + (uint64_t)tok) * D + 16 * i + 4 * g + r, p);
+                        acc[i][r] *= drop_use(have_bits, kbb0, 4 * i + r, keep_s, seed, 2u * d.drop_stream, (tok0 + (uint64_t)tok) * D + 16 * i + 4 * g + r, p);
                 }
                 st4a(dzr + 16 * i + 4 * g, dz[i]);
                 st4a(dpr + 16 * i + 4 * g, acc[i]);
@@ -616,6 +641,10 @@ MEP_DEV void epi_fwd_one(const mep_epi_desc& d, unsigned char* sm, int t_begin, 
     const float p = DROP ? d.drop_p : 0.f;
     const uint64_t seed = (d.seed && p > 0.f) ? *G<const uint64_t>(d.seed) : 0;
     const uint64_t tok0 = (d.seed && p > 0.f) ? G<const uint64_t>(d.seed)[1] * (uint64_t)d.q.T : 0;
+    const uint64_t dbits = p > 0.f && !MEP_NO_DROPBITS ? d.drop_bits : 0;   // the forward's keep bits (0: hash)
+    const bool have_bits = dbits != 0;
+    const float keep_s = p > 0.f ? 1.0f / (1.0f - p) : 1.0f;   // == drop_scale's kept value
+    (void)have_bits; (void)keep_s;
     gfloat* stats = G<float>(d.stats);
     typedef __attribute__((address_space(3))) unsigned char lbyte;
     const WP wp{(lbyte*)sm, 0};
@@ -647,11 +676,13 @@ MEP_DEV void epi_fwd_one(const mep_epi_desc& d, unsigned char* sm, int t_begin, 
         for (int pp = 0; pp < NP; ++pp) qs[pp] = opn<NPART>(bb[2 * pp], bb[2 * pp + 1]);
         if (tile + EWAVES < t_end) rows_of(d.q, tile + EWAVES, bb);
         if (p > 0.f) {
+            uint32_t kb0 = 0;
 #pragma unroll
             for (int i = 0; i < NI; ++i)
 #pragma unroll
                 for (int r = 0; r < 4; ++r)
-                    xp[i][r] *= drop_scale(seed, 2u * d.drop_stream, (tok0 + (uint64_t)tok) * D + 16 * i + 4 * g + r, p);
+                    xp[i][r] *= drop_rec(seed, 2u * d.drop_stream, (tok0 + (uint64_t)tok) * D + 16 * i + 4 * g + r, p, kb0, 4 * i + r);
+            drop_bits_put(drop_bits_ptr(dbits, tok, 0), kb0);
         }
         OpN<NPART> ps[NP];
 #pragma unroll
@@ -677,6 +708,7 @@ MEP_DEV void epi_fwd_one(const mep_epi_desc& d, unsigned char* sm, int t_begin, 
             gfloat* orow = row_ptr(d.out, tok);
             const auto pr = rowa<HS>(d.xp, tok);
             const auto hrow = (HS && d.out_h.ptr) ? rowa<true>(d.out_h, tok) : nullptr;   // next layer's q
+            uint32_t kb1 = 0;   // keep bits of the out site
 #pragma unroll
             for (int i = 0; i < NI; ++i) {
                 const int col = 16 * i + 4 * g;
@@ -685,13 +717,14 @@ MEP_DEV void epi_fwd_one(const mep_epi_desc& d, unsigned char* sm, int t_begin, 
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     y[r] = (z[i][r] - mean) * rstd * w[r] + b[r];
-                    if (p > 0.f) y[r] *= drop_scale(seed, 2u * d.drop_stream + 1u, (tok0 + (uint64_t)tok) * D + col + r, p);
+                    if (p > 0.f) y[r] *= drop_rec(seed, 2u * d.drop_stream + 1u, (tok0 + (uint64_t)tok) * D + col + r, p, kb1, 4 * i + r);
                 }
                 st4a(pr + col, xp[i]);
                 st4a(zr + col, z[i]);
                 stg4(orow + col, f4(y));
                 if (HS && d.out_h.ptr) st4a(hrow + col, y);
             }
+            if (p > 0.f) drop_bits_put(drop_bits_ptr(dbits, tok, 1), kb1);
             if (g == 0) { stats[2 * tok] = mean; stats[2 * tok + 1] = rstd; }
         }
     }
@@ -711,6 +744,10 @@ MEP_DEV void epi_bwd_one(const mep_epi_bwd_desc& bd, unsigned char* sm, int t_be
     const float p = DROP ? d.drop_p : 0.f;
     const uint64_t seed = (d.seed && p > 0.f) ? *G<const uint64_t>(d.seed) : 0;
     const uint64_t tok0 = (d.seed && p > 0.f) ? G<const uint64_t>(d.seed)[1] * (uint64_t)d.q.T : 0;
+    const uint64_t dbits = p > 0.f && !MEP_NO_DROPBITS ? d.drop_bits : 0;   // the forward's keep bits (0: hash)
+    const bool have_bits = dbits != 0;
+    const float keep_s = p > 0.f ? 1.0f / (1.0f - p) : 1.0f;   // == drop_scale's kept value
+    (void)have_bits; (void)keep_s;
     const gfloat* stats = G<const float>(d.stats);
     gfloat* lpart = G<float>(bd.ln_partial);
     typedef __attribute__((address_space(3))) unsigned char lbyte;
@@ -736,6 +773,8 @@ MEP_DEV void epi_bwd_one(const mep_epi_bwd_desc& bd, unsigned char* sm, int t_be
     __syncthreads();
     for (int tile = t_begin + wave; tile < t_end; tile += EWAVES) {
         const int tok = tile * 16 + c;
+        const uint32_t kbb0 = have_bits ? drop_bits_get(drop_bits_ptr(dbits, tok, 0)) : 0u;   // the forward's keep bits
+        const uint32_t kbb1 = have_bits ? drop_bits_get(drop_bits_ptr(dbits, tok, 1)) : 0u;
         const bool ok = tok < ntok;
         const int tc = min(tok, ntok - 1);
         f32x4 dz[NI], zz[NI];
@@ -758,7 +797,7 @@ MEP_DEV void epi_bwd_one(const mep_epi_bwd_desc& bd, unsigned char* sm, int t_be
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 float gg = dz[i][r];
-                if (p > 0.f) gg *= drop_scale(seed, 2u * d.drop_stream + 1u, (tok0 + (uint64_t)tok) * D + col + r, p);
+                if (p > 0.f) gg *= drop_use(have_bits, kbb1, 4 * i + r, keep_s, seed, 2u * d.drop_stream + 1u, (tok0 + (uint64_t)tok) * D + col + r, p);
                 gg = ok ? gg : 0.f;
                 const float x = (zz[i][r] - mu) * rs;
                 const float gw = gg * w[r];
@@ -798,7 +837,7 @@ MEP_DEV void epi_bwd_one(const mep_epi_bwd_desc& bd, unsigned char* sm, int t_be
             for (int i = 0; i < NI; ++i)
 #pragma unroll
                 for (int r = 0; r < 4; ++r)
-                    acc[i][r] *= drop_scale(seed, 2u * d.drop_stream, (tok0 + (uint64_t)tok) * D + 16 * i + 4 * g + r, p);
+                    acc[i][r] *= drop_use(have_bits, kbb0, 4 * i + r, keep_s, seed, 2u * d.drop_stream, (tok0 + (uint64_t)tok) * D + 16 * i + 4 * g + r, p);
         }
         // dx = dxp Wp from the dxp accumulators (tokens past ntok: dz = 0, so dxp = 0)
         Op xs[NP];
@@ -926,6 +965,10 @@ MEP_DEV void epi_bwd_tiles(const mep_epi_bwd_desc& bd, const AM& wmt, const AP& 
     const uint64_t seed = (d.seed && p > 0.f) ? *G<const uint64_t>(d.seed) : 0;
     // global token offset of this shard's rows (seed[1] = the rank's first global batch row)
     const uint64_t tok0 = (d.seed && p > 0.f) ? G<const uint64_t>(d.seed)[1] * (uint64_t)d.q.T : 0;
+    const uint64_t dbits = p > 0.f && !MEP_NO_DROPBITS ? d.drop_bits : 0;   // the forward's keep bits (0: hash)
+    const bool have_bits = dbits != 0;
+    const float keep_s = p > 0.f ? 1.0f / (1.0f - p) : 1.0f;   // == drop_scale's kept value
+    (void)have_bits; (void)keep_s;
     AM wmt_x = wmt;
     wmt_x.row0 += D;                    // rows D.. of Wm^T = Wm[:, D:]
     const gfloat* stats = G<const float>(d.stats);
@@ -933,6 +976,8 @@ MEP_DEV void epi_bwd_tiles(const mep_epi_bwd_desc& bd, const AM& wmt, const AP& 
     const Upstream up(bd);
     for (int tile = t_begin + wave; tile < t_end; tile += EWAVES) {
         const int tok = tile * 16 + c;
+        const uint32_t kbb0 = have_bits ? drop_bits_get(drop_bits_ptr(dbits, tok, 0)) : 0u;   // the forward's keep bits
+        const uint32_t kbb1 = have_bits ? drop_bits_get(drop_bits_ptr(dbits, tok, 1)) : 0u;
         const bool ok = tok < ntok;
         const int tc = min(tok, ntok - 1);
         const gfloat* g2 = bd.dout2.ptr ? row_ptr(bd.dout2, tc) : nullptr;
@@ -951,7 +996,7 @@ MEP_DEV void epi_bwd_tiles(const mep_epi_bwd_desc& bd, const AM& wmt, const AP& 
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 float gg = a[r];
-                if (p > 0.f) gg *= drop_scale(seed, 2u * d.drop_stream + 1u, (tok0 + (uint64_t)tok) * D + col + r, p);
+                if (p > 0.f) gg *= drop_use(have_bits, kbb1, 4 * i + r, keep_s, seed, 2u * d.drop_stream + 1u, (tok0 + (uint64_t)tok) * D + col + r, p);
                 gg = ok ? gg : 0.f;
                 const float x = (zz[r] - mean) * rstd;
                 const float gw = gg * w[r];
@@ -992,7 +1037,7 @@ MEP_DEV void epi_bwd_tiles(const mep_epi_bwd_desc& bd, const AM& wmt, const AP& 
             for (int i = 0; i < NI; ++i)
 #pragma unroll
                 for (int r = 0; r < 4; ++r)
-                    dxp[i][r] *= drop_scale(seed, 2u * d.drop_stream, (tok0 + (uint64_t)tok) * D + 16 * i + 4 * g + r, p);
+                    dxp[i][r] *= drop_use(have_bits, kbb0, 4 * i + r, keep_s, seed, 2u * d.drop_stream, (tok0 + (uint64_t)tok) * D + 16 * i + 4 * g + r, p);
         }
         if (ok) {
             gfloat* dzr = row_ptr(bd.dz, tok);

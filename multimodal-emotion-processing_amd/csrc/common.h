@@ -128,6 +128,27 @@ MEP_DEV float drop_scale(uint64_t seed, uint32_t stream, uint64_t idx, float p) 
     return u >= p ? 1.0f / (1.0f - p) : 0.0f;
 }
 
+// The forward's keep bits of a 16-token tile and dropout site (mep_epi_desc.drop_bits): one
+// dword per lane, bit 4 i + r = element (feature 16 i + 4 g + r, token 16 tile + c) kept.
+MEP_DEV gfloat* drop_bits_ptr(uint64_t base, int tok, int site) {
+    return base ? G<float>(base) + ((tok >> 4) * 2 + site) * 64 + (threadIdx.x & 63) : nullptr;
+}
+// forward: the hash's scale, recording the keep bit
+MEP_DEV float drop_rec(uint64_t seed, uint32_t stream, uint64_t idx, float p, uint32_t& bits, int pos) {
+    const float s = drop_scale(seed, stream, idx, p);
+    bits |= (s != 0.f ? 1u : 0u) << pos;
+    return s;
+}
+MEP_DEV void drop_bits_put(gfloat* bp, uint32_t bits) {
+    if (bp) *bp = __builtin_bit_cast(float, bits);
+}
+MEP_DEV uint32_t drop_bits_get(const gfloat* bp) { return bp ? __builtin_bit_cast(uint32_t, *bp) : 0u; }
+// backward: the scale from the forward's bits (the same value as drop_scale: 1/(1-p) or 0), or the
+// hash when there are none
+MEP_DEV float drop_use(bool have, uint32_t bits, int pos, float keep, uint64_t seed, uint32_t stream, uint64_t idx, float p) {
+    return have ? (((bits >> pos) & 1u) ? keep : 0.0f) : drop_scale(seed, stream, idx, p);
+}
+
 // ------------------------------------------------------------------ f32 MFMA 32x32x2
 // lane l supplies A[l&31][k], B[k][l&31] with k = l>>5 of the 2-wide step; C/D register r of
 // lane l is C[(r&3) + 8*(r>>2) + 4*(l>>5)][l&31].

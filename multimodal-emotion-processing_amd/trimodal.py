@@ -402,6 +402,9 @@ class TriModalPlan:
         blk['astat'] = torch.zeros(B, H, Tq, 2, **f32)
         blk['dKV'] = torch.zeros(nk, D, **self.act)
         blk['ln_partial'] = torch.zeros(cdiv(nq, 16), 2, D, **f32)   # one row per 16-token wave
+        if sp.drop_p > 0:
+            # the forward epilogue's dropout keep bits, read by the backward (mep_epi_desc.drop_bits)
+            blk['dbits'] = torch.zeros(cdiv(nq, 16) * 2 * 64, dtype=torch.int32, device=self.device)
         if i < sp.nl - 1:
             blk['S'] = torch.zeros(B, H, Tq, Tk, **f32)
         if i >= 1:
@@ -582,7 +585,8 @@ class TriModalPlan:
                        ln_b=fl.ptr(blk['pre'] + sp.block_norm + '.bias'),
                        stats=blk['estat'].data_ptr(), seed=self.seed_state.data_ptr(),
                        ntok=self.B * Tq, D=D, drop_p=self._drop, drop_stream=stream_id,
-                       out_h=crows(blk['Qh'], Tq, D) if 'Qh' in blk else Rows())
+                       out_h=crows(blk['Qh'], Tq, D) if 'Qh' in blk else Rows(),
+                       drop_bits=blk['dbits'].data_ptr() if 'dbits' in blk else 0)
 
     def _epi_bwd_desc(self, blk):
         D, Tq = self.spec.D, blk['Tq']

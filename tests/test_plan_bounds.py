@@ -135,6 +135,8 @@ def _epi(c, d, tag='epi'):
     c.inside(tag + '.ln_b', d.ln_b, d.D * F)
     c.inside(tag + '.stats', d.stats, d.ntok * 2 * F)
     c.inside(tag + '.seed', d.seed, 16)   # {seed, row0}
+    if d.drop_bits:   # uint32 [ceil(ntok / 16)][2 sites][64 lanes]
+        c.inside(tag + '.drop_bits', d.drop_bits, -(-d.ntok // 16) * 2 * 64 * 4)
 
 
 def _epi_bwd(c, d):
