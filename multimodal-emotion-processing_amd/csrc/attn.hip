@@ -86,6 +86,9 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 #ifndef MEP_ATTN_HEADPAIR
 #define MEP_ATTN_HEADPAIR 1    // Tk > 64 kernels: heads 2j, 2j + 1 of a row on one CU / XCD (64-byte head slices of 128-byte lines)
 #endif
+#ifndef MEP_FWD_CHUNK_PF
+#define MEP_FWD_CHUNK_PF 0    // bf16 long forward: the next key chunk's loads issued before this chunk's tiles
+#endif
 #ifndef MEP_FWD_MFSUM
 #define MEP_FWD_MFSUM 1       // bf16 forward: softmax row sums on the matrix core (ones-row A operand)
 #endif
@@ -406,6 +409,10 @@ MEP_DEV void attn_fwd_task(const mep_attn_desc& d, int qc, int h, int b, int lan
     const gfloat* sprev = G<const float>(d.s_prev);
     gfloat* sout = G<float>(d.s_out);
     const gfloat* mask = G<const float>(d.mask) + (int64_t)b * d.mask_sB;
+    const uint64_t mrow = d.mask + 4ull * (uint64_t)((int64_t)b * d.mask_sB);
+    const auto rsMask = uniform_rsrc(mrow, 4 * (int64_t)Tk);
+    const bool mask16 = (mrow & 15) == 0;   // wave-uniform
+    (void)mask;
     const int D = d.H * HDIM;
     const BRowT<BF> Qb = brow<BF>(d.q, b, Tq, D), Kb = brow<BF>(d.k, b, Tk, D), Vb = brow<BF>(d.v, b, Tk, D),
                     Xb = brow<BF>(d.x, b, Tq, D);
@@ -472,9 +479,54 @@ MEP_DEV void attn_fwd_task(const mep_attn_desc& d, int qc, int h, int b, int lan
                 qsh[QH ? qt : 0][hb] = z;
             }
     }
+    // the raw loads of one key chunk (K rows, V columns, the keys' mask values); PF (bf16 long
+    // forward, MEP_FWD_CHUNK_PF): the next chunk's loads are issued before this chunk's query tiles
+    constexpr bool PF = BF && !SINGLE && MEP_FWD_CHUNK_PF;
+    struct Raw {
+        u32x2 kw[NT][NHB];        // BF: K rows as words
+        float kf[BF ? 1 : NT][NHB][4];
+        unsigned vr[BF ? NT : 1][NHB][4];
+        float vf[BF ? 1 : NT][NHB][4];
+        f32x4 m4[NT];
+    };
+    auto fetch = [&](Raw& R, int k_lo) {
+#pragma unroll
+        for (int kt = 0; kt < NT; ++kt) {
+            const int k0 = k_lo + kt * 16;
+#pragma unroll
+            for (int hb = 0; hb < NHB; ++hb) {
+                const int ov = Vb.at(k0 + 4 * g, hc + 16 * hb + c);
+#pragma unroll
+                for (int s = 0; s < 4; ++s) {
+                    if constexpr (BF) R.vr[kt][hb][s] = Vb.ld1raw(ov, s * Vb.sT4);
+                    else R.vf[BF ? 0 : kt][hb][s] = Vb.ld1(ov, s * Vb.sT4);
+                }
+                if constexpr (BF) R.kw[kt][hb] = Kb.ld4raw(Kb.at(k0 + c, hc + 16 * hb + 4 * g));
+                else Kb.ld4(R.kf[BF ? 0 : kt][hb], Kb.at(k0 + c, hc + 16 * hb + 4 * g));
+            }
+            // the lane's 4 keys' mask values in one 16-byte load (range-checked: past Tk -> 0, and
+            // those keys get +inf below)
+            if (mask16) {
+                R.m4[kt] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rsMask, 4 * (k0 + 4 * g), 0, 0));
+            } else {   // a row that is not 16-byte aligned: 4 dword loads
+#pragma unroll
+                for (int s = 0; s < 4; ++s)
+                    R.m4[kt][s] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsMask, 4 * (k0 + 4 * g + s), 0, 0));
+            }
+        }
+    };
+    Raw nxt;
+    if (PF) fetch(nxt, 0);
     for (int k_lo = 0; k_lo < Tk; k_lo += CH) {
         // operands of the 4 key tiles of this chunk: K rows (A of S^T: K[k0+c][4g+s], split) and V
         // columns (B of P.V: V[k0+4g+s][c]); past Tk they read 0 (P is 0 there)
+        Raw cur;
+        if (PF) {
+            cur = nxt;
+            if (k_lo + CH < Tk) fetch(nxt, k_lo + CH);
+        } else {
+            fetch(cur, k_lo);
+        }
         S3 ks[NT][NHB];
         float vf[BF ? 1 : NT][NHB][4], mt[NT][4];
         unsigned vr[BF ? NT : 1][NHB][4];   // BF: raw bf16 V elements
@@ -484,16 +536,22 @@ MEP_DEV void attn_fwd_task(const mep_attn_desc& d, int qc, int h, int b, int lan
             const int k0 = k_lo + kt * 16;
 #pragma unroll
             for (int hb = 0; hb < NHB; ++hb) {
-                const int ov = Vb.at(k0 + 4 * g, hc + 16 * hb + c);
+                if constexpr (BF) {
+                    S3 r{};
+                    r.a0 = cur.kw[kt][hb][0];
+                    r.a1 = cur.kw[kt][hb][1];
+                    ks[kt][hb] = r;
 #pragma unroll
-                for (int s = 0; s < 4; ++s) {
-                    if constexpr (BF) vr[kt][hb][s] = Vb.ld1raw(ov, s * Vb.sT4);
-                    else vf[kt][hb][s] = Vb.ld1(ov, s * Vb.sT4);
+                    for (int s = 0; s < 4; ++s) vr[kt][hb][s] = cur.vr[kt][hb][s];
+                } else {
+                    ks[kt][hb] = split3(cur.kf[BF ? 0 : kt][hb]);
+#pragma unroll
+                    for (int s = 0; s < 4; ++s) vf[BF ? 0 : kt][hb][s] = cur.vf[BF ? 0 : kt][hb][s];
                 }
-                ks[kt][hb] = ld_op(Kb, Kb.at(k0 + c, hc + 16 * hb + 4 * g));
             }
 #pragma unroll
-            for (int s = 0; s < 4; ++s) mt[kt][s] = mask_term(mask, k0 + 4 * g + s, Tk);
+            for (int s = 0; s < 4; ++s)
+                mt[kt][s] = k0 + 4 * g + s < Tk ? mul_rn(1.0e8f, sub_rn(1.0f, cur.m4[kt][s])) : INFINITY;
         }
         if constexpr (BF) {
 #pragma unroll
