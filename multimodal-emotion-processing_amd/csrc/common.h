@@ -94,9 +94,12 @@ MEP_DEV float mul_rn(float a, float b) { return __fmul_rn(a, b); }
 // DPP within each row of 16 lanes (quad butterflies xor 1 / xor 2, then the half-row and row
 // mirrors), then the four row results through readlane, combined as (r0 + r1) + (r2 + r3): no
 // LDS round trips (ds_bpermute), result wave-uniform, fixed order.
+// update_dpp with old = 0 and bound_ctrl set: the same lanes move (every source lane of these
+// row-local patterns is valid), and the form lets the compiler fold the move into the consuming
+// add as one v_add_f32_dpp (half the instructions of v_mov_b32_dpp + v_add_f32)
 template <int CTRL>
 MEP_DEV float dpp_mov(float v) {
-    return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false));
+    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xF, 0xF, true));
 }
 MEP_DEV float lane_f(float v, int l) { return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), l)); }
 MEP_DEV float wave_sum(float v) {
@@ -439,10 +442,10 @@ struct WCols {
 // sum over the 16 lanes of a DPP row (lanes sharing g = lane >> 4), result in every lane: quad
 // butterflies (xor 1, xor 2), then the half-row and row mirrors pair the quads
 MEP_DEV float row16_sum(float v) {
-    v += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0xB1, 0xF, 0xF, false));
-    v += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x4E, 0xF, 0xF, false));
-    v += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x141, 0xF, 0xF, false));
-    v += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x140, 0xF, 0xF, false));
+    v += dpp_mov<0xB1>(v);
+    v += dpp_mov<0x4E>(v);
+    v += dpp_mov<0x141>(v);
+    v += dpp_mov<0x140>(v);
     return v;
 }
 
