@@ -124,10 +124,22 @@ MEP_DEV uint64_t mix64(uint64_t x) {
     x ^= x >> 31;
     return x;
 }
-// keep-scale for element `idx` of dropout stream `stream`: 0 (dropped) or 1/(1-p).
+// 32-bit avalanche hash (two multiplies): the per-element part of the dropout hash
+MEP_DEV uint32_t lowbias32(uint32_t x) {
+    x ^= x >> 16; x *= 0x7feb352du;
+    x ^= x >> 15; x *= 0x846ca68bu;
+    x ^= x >> 16;
+    return x;
+}
+// keep-scale for element `idx` of dropout stream `stream`: 0 (dropped) or 1/(1-p).  The stream's
+// 32-bit key is one 64-bit mix of (seed, stream) -- loop-invariant, hoisted out of the element
+// loops -- and each element costs two 32-bit hashes of its index halves (four 32-bit multiplies;
+// round 3's two 64-bit mixes per element were most of the dropout epilogues' instructions).
+// Restated bit for bit by oracle/dropout.py keep_scale.
 MEP_DEV float drop_scale(uint64_t seed, uint32_t stream, uint64_t idx, float p) {
-    uint64_t h = mix64(seed ^ (0x9E3779B97F4A7C15ull * (uint64_t)(stream + 1)) ^ mix64(idx + 0x632BE59BD9B4E019ull));
-    float u = (float)(h >> 40) * (1.0f / 16777216.0f);
+    const uint32_t key = (uint32_t)mix64(seed ^ (0x9E3779B97F4A7C15ull * (uint64_t)(stream + 1)));
+    const uint32_t h = lowbias32((uint32_t)idx ^ lowbias32((uint32_t)(idx >> 32) ^ key));
+    const float u = (float)(h >> 8) * (1.0f / 16777216.0f);
     return u >= p ? 1.0f / (1.0f - p) : 0.0f;
 }
 

@@ -40,14 +40,28 @@ def seed_advance(seed):
         return int(_mix64(np.uint64(seed) + GOLDEN))
 
 
+def _lowbias32(x):
+    x = np.asarray(x, dtype=np.uint32)
+    with np.errstate(over='ignore'):
+        x = x ^ (x >> np.uint32(16))
+        x = x * np.uint32(0x7FEB352D)
+        x = x ^ (x >> np.uint32(15))
+        x = x * np.uint32(0x846CA68B)
+        x = x ^ (x >> np.uint32(16))
+    return x
+
+
 def keep_scale(seed, stream, idx, p):
     """float32 keep-scale (0 or 1/(1-p)) of elements ``idx`` (uint64 array) of dropout stream
-    ``stream`` -- csrc/common.h drop_scale."""
+    ``stream`` -- csrc/common.h drop_scale: the stream key is the low 32 bits of one 64-bit mix of
+    (seed, stream); an element hashes its index halves with the 32-bit lowbias32 mix."""
     idx = np.asarray(idx, dtype=np.uint64)
     with np.errstate(over='ignore'):
-        key = np.uint64(seed) ^ (GOLDEN * np.uint64(stream + 1))
-        h = _mix64(key ^ _mix64(idx + np.uint64(0x632BE59BD9B4E019)))
-    u = (h >> np.uint64(40)).astype(np.float32) * np.float32(1.0 / 16777216.0)
+        key = np.uint32(int(_mix64(np.uint64(seed) ^ (GOLDEN * np.uint64(stream + 1)))) & 0xFFFFFFFF)
+        lo = (idx & np.uint64(0xFFFFFFFF)).astype(np.uint32)
+        hi = (idx >> np.uint64(32)).astype(np.uint32)
+        h = _lowbias32(lo ^ _lowbias32(hi ^ key))
+    u = (h >> np.uint32(8)).astype(np.float32) * np.float32(1.0 / 16777216.0)
     p32 = np.float32(p)
     scale = np.float32(1.0) / (np.float32(1.0) - p32)
     return np.where(u >= p32, scale, np.float32(0.0)).astype(np.float32)
