@@ -118,7 +118,8 @@ def _fold_pair(build, steps=4):
     assert float((g1 - g0).abs().max() / g0.abs().max()) < 1e-6, (g1, g0)
     assert float((l1 - l0).abs().max()) <= 1e-6 * float(l0.abs().max()), (l1, l0)
     for (k, p1), (_, p0) in zip(m1.named_parameters(), m0.named_parameters()):
-        assert float((p1 - p0).abs().max()) <= 1e-6, k
+        e = (p1 - p0).abs()
+        assert float(e.max()) <= 1e-6, (k, float(e.max()), int((e > 1e-6).sum()), e.numel(), g1, g0)
 
 
 def test_norm_fold_matches_optimizer_norm_pass_ren_dropout(cuda):
