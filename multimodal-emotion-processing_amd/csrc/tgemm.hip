@@ -216,6 +216,183 @@ __global__ __launch_bounds__(TG_THREADS) void k_tgemm(const mep_gemm_desc* __res
     }
 }
 
+// bf16 path with the weight staged by LDS-DMA (MEP_TGEMM_DMA: w_nt).  The fp32 W chunk [BN rows][32 k]
+// goes straight from HBM / L2 into a ring of TGB_NS LDS slots (no VGPRs in flight: TGB_NS - 1 chunks
+// ahead instead of one), one 1-KiB wave instruction per 8 rows; the fragment read converts to bf16
+// (v_cvt_pk_bf16_f32, round to nearest: the same operand as the register-staged kernel).  X rows
+// stay raw bf16 words in registers, TGB_PFX chunks deep.  Slot layout: row r, 16-byte unit s holds
+// k piece q = s ^ ((r >> 1) & 7) (a ds_read_b128 of 16 rows x one piece covers the 64 banks once).
+#ifndef MEP_TGB_NS
+#define MEP_TGB_NS 4       // LDS weight-ring slots (4 x 16 KiB at BN = 128)
+#endif
+#ifndef MEP_TGB_PFX
+#define MEP_TGB_PFX 3      // X chunks in registers
+#endif
+template <int NI>
+MEP_DEV void tgemm_bf(const mep_gemm_desc* __restrict__ descs) {
+    constexpr int BN = 16 * NI, NS = MEP_TGB_NS, PFX = MEP_TGB_PFX;
+    constexpr int CHB = BN * 128;                    // bytes of one fp32 chunk slot
+    constexpr int UPW = BN / (8 * TG_WAVES);         // DMA instructions per wave per chunk
+    static_assert(BN % (8 * TG_WAVES) == 0 && NS >= 2 && PFX >= 2, "tgemm_bf geometry");
+    __shared__ __attribute__((aligned(16))) unsigned char sm[NS * CHB];
+    const mep_gemm_desc& d = descs[blockIdx.y];
+    const int n0 = (int)blockIdx.z * BN;
+    const int tok0 = (int)blockIdx.x * TG_BM;
+    if (n0 >= d.N || tok0 >= d.ntok) return;         // the whole workgroup
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int c = lane & 15, g = lane >> 4;
+    const int K = d.K, N = d.N, ntok = d.ntok;
+    const int nkc = (K + 31) >> 5;
+    typedef __attribute__((address_space(3))) unsigned char lbyte;
+    typedef __attribute__((address_space(3))) void lvoid;
+    typedef __attribute__((address_space(3))) const f32x4 lcf4;
+
+    // a lane's 16-byte unit goes by LDS-DMA when it is whole (row < N, k + 3 < K) and the weight rows
+    // are 16-byte aligned; otherwise (the K tail, rows past N, unaligned rows) the lane loads what
+    // exists, zero-fills the rest and writes the unit with a plain LDS store
+    const gfloat* W = G<const float>(d.w);
+    const bool wdma = (d.ldw % 4 == 0) && ((d.w & 15) == 0);
+    const auto rsW = __builtin_amdgcn_make_buffer_rsrc((void*)d.w, 0, (int)min((int64_t)4 * N * d.ldw, (int64_t)0x7fffffff), 0x00020000);
+    int wrow[UPW], wq[UPW];
+#pragma unroll
+    for (int u = 0; u < UPW; ++u) {
+        wrow[u] = n0 + 8 * (wave * UPW + u) + (lane >> 3);
+        wq[u] = 4 * ((lane & 7) ^ (((wrow[u] - n0) >> 1) & 7));
+    }
+    auto issue_w = [&](int kc) {
+        lbyte* dst = (lbyte*)sm + (kc % NS) * CHB + wave * UPW * 1024;
+#pragma unroll
+        for (int u = 0; u < UPW; ++u) {
+            const int k = 32 * kc + wq[u];
+            if (wdma && wrow[u] < N && k + 3 < K) {
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(rsW, (lvoid*)(dst + u * 1024), 16, 4 * (wrow[u] * d.ldw + wq[u]),
+                                                         128 * kc, 0, 0);
+            } else {
+                f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
+                if (wrow[u] < N) {
+#pragma unroll
+                    for (int e = 0; e < 4; ++e)
+                        if (k + e < K) v[e] = W[(int64_t)wrow[u] * d.ldw + k + e];
+                }
+                *(__attribute__((address_space(3))) f32x4*)(dst + u * 1024 + 16 * lane) = v;
+            }
+        }
+    };
+
+    // X: raw bf16 words; rows not 8-byte aligned take four 2-byte loads per unit.  X columns past K
+    // (the next row's bf16 values, or zeros past the view) meet zero weight units
+    const int64_t last = row_off(d.x, ntok - 1) + K;
+    const auto rsX = __builtin_amdgcn_make_buffer_rsrc((void*)d.x.ptr, 0, (int)min((int64_t)2 * last, (int64_t)0x7fffffff), 0x00020000);
+    const bool xvec = ((d.x.ptr & 7) == 0) && (d.x.sB % 4 == 0) && (d.x.sT % 4 == 0);
+    int xoff[TG_TT];
+#pragma unroll
+    for (int t = 0; t < TG_TT; ++t) {
+        const int tok = min(tok0 + 16 * (TG_TT * wave + t) + c, ntok - 1);
+        xoff[t] = 2 * ((int)row_off(d.x, tok) + 4 * g);
+    }
+    u32x2 xr[PFX][TG_TT][2];
+    auto load_x = [&](int s, int kc) {
+#pragma unroll
+        for (int t = 0; t < TG_TT; ++t)
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int o = xoff[t] + 64 * kc + 32 * h;
+                if (xvec) {
+                    xr[s][t][h] = __builtin_bit_cast(u32x2, __builtin_amdgcn_raw_buffer_load_b64(rsX, o, 0, 0));
+                } else {
+                    unsigned e[4];
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) e[j] = (unsigned)__builtin_amdgcn_raw_buffer_load_b16(rsX, o + 2 * j, 0, 0);
+                    xr[s][t][h] = u32x2{e[0] | (e[1] << 16), e[2] | (e[3] << 16)};
+                }
+            }
+    };
+
+    f32x4 acc[TG_TT][NI];
+#pragma unroll
+    for (int t = 0; t < TG_TT; ++t)
+#pragma unroll
+        for (int i = 0; i < NI; ++i) acc[t][i] = zero_f4();
+
+#pragma unroll
+    for (int k = 0; k < NS - 1; ++k)
+        if (k < nkc) issue_w(k);
+#pragma unroll
+    for (int k = 0; k < PFX - 1; ++k)
+        if (k < nkc) load_x(k, k);
+    // vector-memory operations a wave issues after chunk kc's weight in the steady state
+    constexpr int XI = 2 * TG_TT;
+    constexpr int NEWER = (NS - 2) * UPW + (NS - 1) * XI;
+    auto step = [&](int kc, int s) {                  // s = kc % PFX (compile-time in the unrolled loop)
+        const bool steady = kc >= NS - 1 && kc + NS - 2 < nkc && kc + PFX - 2 < nkc;
+        if (steady) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(NEWER) : "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();                              // chunk kc landed; slot (kc - 1) % NS free
+        if (kc + NS - 1 < nkc) issue_w(kc + NS - 1);
+        if (kc + PFX - 1 < nkc) load_x((s + PFX - 1) % PFX, kc + PFX - 1);
+        const lbyte* ws = (const lbyte*)sm + (kc % NS) * CHB;
+        bf16x8 xo[TG_TT];
+#pragma unroll
+        for (int t = 0; t < TG_TT; ++t) xo[t] = kpair(xr[s][t][0], xr[s][t][1]);
+#pragma unroll
+        for (int i = 0; i < NI; ++i) {
+            const int r = 16 * i + c, sw = (r >> 1) & 7;
+            const f32x4 a0 = *(lcf4*)(ws + r * 128 + 16 * (g ^ sw));
+            const f32x4 a1 = *(lcf4*)(ws + r * 128 + 16 * ((4 + g) ^ sw));
+            const bf16x8 wo = kpair(u32x2{pk_bf16(a0[0], a0[1]), pk_bf16(a0[2], a0[3])},
+                                    u32x2{pk_bf16(a1[0], a1[1]), pk_bf16(a1[2], a1[3])});
+#pragma unroll
+            for (int t = 0; t < TG_TT; ++t) acc[t][i] = mfma_bf16(wo, xo[t], acc[t][i]);
+        }
+    };
+    int kc = 0;
+    for (; kc + PFX <= nkc; kc += PFX) {
+#pragma unroll
+        for (int s = 0; s < PFX; ++s) step(kc + s, s);
+    }
+#pragma unroll
+    for (int s = 0; s < PFX - 1; ++s)
+        if (kc + s < nkc) step(kc + s, s);
+
+    // ---- epilogue: token c of tile t, features n0 + 16 i + 4g .. +3 (bf16 rows)
+    const gfloat* bias = G<const float>(d.bias);
+    const gfloat* table = G<const float>(d.table);
+    const int ldt = d.ldt ? d.ldt : N;
+#pragma unroll
+    for (int t = 0; t < TG_TT; ++t) {
+        const int tok = tok0 + 16 * (TG_TT * wave + t) + c;
+        if (tok >= ntok) continue;
+        const auto yrow = rowa<true>(d.y, tok);
+        const gfloat* trow = table ? table + (int64_t)(tok % d.y.T) * ldt : nullptr;
+#pragma unroll
+        for (int i = 0; i < NI; ++i) {
+            const int col = n0 + 16 * i + 4 * g;
+            if (col >= N) continue;
+            f32x4 v = acc[t][i];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[r] = d.alpha * v[r];
+            if (bias) v += ld4w(bias + col);
+            if (trow) {
+#pragma unroll
+                for (int r = 0; r < 4; ++r) v[r] += trow[col + r];
+            }
+            if (d.relu) {
+#pragma unroll
+                for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r], 0.f);
+            }
+            if (d.accumulate) v += ld4a(yrow + col);
+            st4a(yrow + col, v);
+        }
+    }
+}
+
+// one kernel per N tile (plain kernels: hipcc leaves the host stubs of kernel templates named only
+// inside a switch undefined)
+#define MEP_TGB_K(NI) \
+    __global__ __launch_bounds__(TG_THREADS) void k_tgemm_bf##NI(const mep_gemm_desc* __restrict__ descs) { tgemm_bf<NI>(descs); }
+MEP_TGB_K(2) MEP_TGB_K(4) MEP_TGB_K(6) MEP_TGB_K(8)
+#undef MEP_TGB_K
+
 // Resident-weight variant for K <= 32 * TGR_KP (the cmu-mosei unify, K <= 300, and the realformer
 // Linears, K <= 192): the workgroup's whole N tile of W (BN <= 96 rows) is staged in LDS ONCE, as
 // NW bf16 parts (NW = 2 on the fp32 path: 3 parts of a 96 x 320 tile would need 184 KB; the
@@ -386,6 +563,18 @@ extern "C" int mep_tgemm(const mep_gemm_desc* descs, int n_desc, int max_ntok, i
         return mep_check_launch("mep_tgemm");
     }
     const int ni = max_n >= 16 * MEP_TG_NI ? MEP_TG_NI : (max_n + 15) / 16;   // 16-col tiles per workgroup N tile
+    if (flags & MEP_TGEMM_DMA) {   // bf16 path, w_nt
+        if (!bf || !wnt) { mep_set_error("mep_tgemm: MEP_TGEMM_DMA needs MEP_PREC_BF16 and w_nt"); return MEP_EINVAL; }
+        const dim3 grid((max_ntok + TG_BM - 1) / TG_BM, n_desc, (max_n + 16 * ni - 1) / (16 * ni)), block(TG_THREADS);
+        switch (ni) {
+            case 2: hipLaunchKernelGGL(k_tgemm_bf2, grid, block, 0, st, descs); break;
+            case 4: hipLaunchKernelGGL(k_tgemm_bf4, grid, block, 0, st, descs); break;
+            case 6: hipLaunchKernelGGL(k_tgemm_bf6, grid, block, 0, st, descs); break;
+            case 8: hipLaunchKernelGGL(k_tgemm_bf8, grid, block, 0, st, descs); break;
+            default: mep_set_error("mep_tgemm: N must be 32, 64, 96 or >= 128 (a multiple of 16)"); return MEP_EINVAL;
+        }
+        return mep_check_launch("mep_tgemm");
+    }
     const dim3 grid((max_ntok + TG_BM - 1) / TG_BM, n_desc, (max_n + 16 * ni - 1) / (16 * ni)), block(TG_THREADS);
 #define MEP_TG3(NI, P, WT) hipLaunchKernelGGL((k_tgemm<NI, P, WT>), grid, block, 0, st, descs)
 #define MEP_TG2(NI, P) do { if (wnt) MEP_TG3(NI, P, true); else MEP_TG3(NI, P, false); } while (0)
@@ -402,3 +591,4 @@ extern "C" int mep_tgemm(const mep_gemm_desc* descs, int n_desc, int max_ntok, i
 #undef MEP_TG3
     return mep_check_launch("mep_tgemm");
 }
+

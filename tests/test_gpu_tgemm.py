@@ -132,3 +132,53 @@ def test_tgemm_bf16_path(K, res, cuda):
     assert_close(y, want, rtol=4e-3, atol_frac=1e-4, name="bf16")
     assert torch.equal(y, y.float().bfloat16())
     del keep
+
+
+def _launch_flags(descs, dev, flags):
+    from mep_amd import _lib
+    arr = _lib.DescArray(_lib.GemmDesc, descs, dev)
+    _lib.call('mep_tgemm', arr.ptr, arr.n, max(d.ntok for d in descs), max(d.N for d in descs), flags)
+    torch.cuda.synchronize()
+    return arr
+
+
+@pytest.mark.parametrize('N,Ks,B,T,extra', [
+    (128, (768, 640, 205), 4, 300, False),   # Ren-MME cfg5 unify widths (K = 205: a K tail, unaligned rows)
+    (128, (768, 640, 35), 3, 7, True),       # ragged: 21 tokens; bias + position table + accumulate
+    (96, (320, 64, 74), 5, 50, False),       # N tile 96 (6 column tiles)
+    (256, (512,), 2, 130, True),             # two N tiles; 260 tokens (a partial last workgroup)
+])
+def test_tgemm_bf16_dma_matches_register_staging(N, Ks, B, T, extra, cuda):
+    """MEP_TGEMM_DMA (weight ring by LDS-DMA, X as raw bf16 words) against the register-staged bf16
+    kernel on the same descriptors -- the same operands, MFMAs and order: bit-identical -- and
+    against torch's bf16-operand product; K tails and unaligned weight / X rows (K = 205, 35, 74)
+    take the plain-load units of the same kernel."""
+    from mep_amd import _lib
+    torch.manual_seed(N + B + T)
+    xs = [torch.randn(B, 2, T, K, device=cuda).bfloat16() for K in Ks]
+    ws = [torch.randn(N, K, device=cuda) / K ** 0.5 for K in Ks]
+    bias = torch.randn(N, device=cuda) if extra else None
+    tab = torch.randn(T, N, device=cuda) if extra else None
+    base = [[torch.randn(B, T, N, device=cuda).bfloat16() if extra else
+             torch.full((B, T, N), float('nan'), device=cuda).bfloat16() for _ in range(2)] for _ in Ks]
+    outs = {}
+    for dma in (False, True):
+        ys = [[b.clone() for b in bb] for bb in base]
+        descs = []
+        for i, (x, w) in enumerate(zip(xs, ws)):
+            K = x.shape[-1]
+            for e in range(2):
+                descs.append(_gd(_rows(x, T, 2 * T * K, K, e * T * K), _rows(ys[i][e], T, T * N, N), w, B * T, N, K, K,
+                                 bias=bias, table=tab, accumulate=int(extra), bf16=_lib.BF16_OPS | _lib.BF16_STORE))
+        assert _lib.tgemm_dma_ok(descs)
+        keep = _launch_flags(descs, cuda, _lib.PREC_BF16 | (_lib.TGEMM_DMA if dma else 0))
+        outs[dma] = ys
+        del keep
+    for i, (x, w) in enumerate(zip(xs, ws)):
+        for e in range(2):
+            assert torch.equal(outs[True][i][e], outs[False][i][e]), (i, e)
+            want = x[:, e].double() @ w.bfloat16().double().t()
+            if extra:
+                want = want + bias.double() + tab.double() + base[i][e].double()
+            assert_close(outs[True][i][e], want, rtol=4e-3, atol_frac=1e-4, name='K%d slot%d' % (x.shape[-1], e))
+
