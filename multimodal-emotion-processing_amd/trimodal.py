@@ -89,11 +89,13 @@ def _wgrad_units(items, bf16=False):
     return units
 
 
-def wgrad_chunk(items, n_wg=WG_TARGET, bf16=False):
-    """The smallest multiple of 8 tokens per segment that keeps the items' launch within n_wg
-    workgroups."""
-    items = [tuple(it) + (0,) * (5 - len(it)) for it in items]
-    units = _wgrad_units(items, bf16)
+# k_wgrad cost per workgroup ~ a * tokens + c (cfg3 / cfg5 bf16 fits, scripts/r4_gpu23.sh: a = 8.5 ns per
+# token, c = 16 us of setup + partial write); in tokens, c / a:
+WG_SETUP_TOKENS = int(_lib.switch('MEP_WG_SETUP_TOKENS', '1900'))
+
+
+def _wgrad_fit(units, n_wg):
+    """the smallest multiple of 8 tokens per segment that keeps the units within n_wg segments"""
     lo, hi = 1, cdiv(max([n for (_, _, n) in units] or [8]), 8)   # in units of 8 tokens
     while lo < hi:                        # the segment count only falls as the chunk grows
         mid = (lo + hi) // 2
@@ -102,6 +104,26 @@ def wgrad_chunk(items, n_wg=WG_TARGET, bf16=False):
         else:
             lo = mid + 1
     return 8 * lo
+
+
+def wgrad_chunk(items, n_wg=WG_TARGET, bf16=False):
+    """Tokens per segment: n_wg workgroups are resident at once.  bf16 instance (one workgroup per
+    CU): of the chunks that fill 1, 2, 3 or 4 such rounds, the one with the least modelled time
+    rounds x (chunk + WG_SETUP_TOKENS) -- one round is the usual answer (cfg3: 1,072 tokens), but
+    cfg5's 9,600-token spans would fill only 160 of 256 CUs in one round, and two rounds of 3,200
+    run 98 -> 87 us.  The fp32 instance (two per CU) keeps one round: two measured slower at cfg5
+    (259 vs 254 us)."""
+    items = [tuple(it) + (0,) * (5 - len(it)) for it in items]
+    units = _wgrad_units(items, bf16)
+    if WG_TARGET_OVERRIDE or not bf16:
+        return _wgrad_fit(units, n_wg)
+    best = None
+    for r in (1, 2, 3, 4):
+        ch = _wgrad_fit(units, r * n_wg)
+        cost = r * (ch + WG_SETUP_TOKENS)
+        if best is None or cost < best[0]:
+            best = (cost, ch)
+    return best[1]
 
 
 def wgrad_segments(items, n_wg=WG_TARGET, tok_per_split=None, bf16=False):
