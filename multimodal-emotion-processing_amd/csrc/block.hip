@@ -1150,10 +1150,174 @@ MEP_DEV void ln_fwd_rows(const mep_ln_desc& d) {
     }
 }
 
+// 16 lanes per row (MEP_LN_Q; D <= 128, D % 8 == 0, 16-byte aligned rows): lane j of a 16-lane
+// group holds features 8j .. 8j+7 of its row -- one 16-byte access per row and lane (two on the fp32
+// path) instead of one 2- / 4-byte access per feature -- and the row sums are 16-lane DPP sums
+// (row16_sum), not wave sums: a wave takes 4 rows at once.  Same workgroup geometry as the rows
+// kernels above (forward 16 rows, backward 64 rows and one partial row per workgroup).
+#ifndef MEP_LN_Q
+#define MEP_LN_Q 1
+#endif
+typedef unsigned u32x4g __attribute__((ext_vector_type(4)));
+template <bool HS>
+MEP_DEV void ln_ld8(const mep_rows& r, int tok, int c0, float (&v)[8]) {
+    const auto p = rowa<HS>(r, tok) + c0;
+    if constexpr (HS) {
+        const u32x4g w = *reinterpret_cast<const MEP_G u32x4g*>(p);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) { v[2 * e] = bf16_word_lo(w[e]); v[2 * e + 1] = bf16_word_hi(w[e]); }
+    } else {
+        const f32x4 a = ld4a(p), b = ld4a(p + 4);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) { v[e] = a[e]; v[4 + e] = b[e]; }
+    }
+}
+template <bool HS>
+MEP_DEV void ln_st8(const mep_rows& r, int tok, int c0, const float (&v)[8]) {
+    const auto p = rowa<HS>(r, tok) + c0;
+    if constexpr (HS) {
+        *reinterpret_cast<MEP_G u32x4g*>(p) = u32x4g{pk_bf16x2(v[0], v[1]), pk_bf16x2(v[2], v[3]),
+                                                     pk_bf16x2(v[4], v[5]), pk_bf16x2(v[6], v[7])};
+    } else {
+        st4a(p, f32x4{v[0], v[1], v[2], v[3]});
+        st4a(p + 4, f32x4{v[4], v[5], v[6], v[7]});
+    }
+}
+MEP_DEV void ld8w(const gfloat* p, float (&v)[8]) {
+    const f32x4 a = ld4w(p), b = ld4w(p + 4);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) { v[e] = a[e]; v[4 + e] = b[e]; }
+}
+MEP_DEV bool ln_rows16(const mep_rows& r, bool hs) {
+    const int al = hs ? 8 : 4;
+    return r.ptr % 16 == 0 && r.sB % al == 0 && r.sT % al == 0;
+}
+MEP_DEV bool ln_q_ok(const mep_ln_desc& d, bool fwd) {
+    const bool hs = d.bf16 & MEP_BF16_STORE;
+    if (!MEP_LN_Q || d.D > 128 || d.D % 8 || d.w % 16 || d.b % 16 || !ln_rows16(d.x, hs)) return false;
+    return fwd ? ln_rows16(d.y, hs) : (ln_rows16(d.dy, hs) && ln_rows16(d.dx, hs));
+}
+
+template <bool HS>
+MEP_DEV void ln_fwd_q(const mep_ln_desc& d) {
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, j = lane & 15;
+    if (blockIdx.x * 16 >= d.ntok) return;                 // the whole workgroup
+    const int tok = blockIdx.x * 16 + 4 * wave + (lane >> 4);
+    const int c0 = 8 * j;
+    const bool on = c0 < d.D;
+    float v[8];
+    ln_ld8<HS>(d.x, min(tok, d.ntok - 1), on ? c0 : 0, v);
+    float s = 0.f;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { v[e] = on ? v[e] : 0.f; s += v[e]; }
+    const float mean = row16_sum(s) / (float)d.D;
+    float q = 0.f;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { v[e] = on ? v[e] - mean : 0.f; q += v[e] * v[e]; }
+    const float rstd = 1.0f / sqrtf(row16_sum(q) / (float)d.D + LN_EPS);
+    if (tok >= d.ntok) return;
+    if (on) {
+        float w[8], b[8];
+        ld8w(G<const float>(d.w) + c0, w);
+        ld8w(G<const float>(d.b) + c0, b);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = v[e] * rstd * w[e] + b[e];
+        ln_st8<HS>(d.y, tok, c0, v);
+    }
+    if (j == 0) {
+        gfloat* st = G<float>(d.stats);
+        st[2 * tok] = mean;
+        st[2 * tok + 1] = rstd;
+    }
+}
+
+template <bool HS>
+MEP_DEV void ln_bwd_q(const mep_ln_desc& d) {
+    const int tok0 = blockIdx.x * 64;
+    if (tok0 >= d.ntok) return;                            // the whole workgroup
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, j = lane & 15;
+    const int c0 = 8 * j;
+    const bool on = c0 < d.D;
+    const int cc = on ? c0 : 0;
+    __shared__ float red[4][2][128];
+    float wv[8], pw[8], pb[8];
+    ld8w(G<const float>(d.w) + cc, wv);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) pw[e] = pb[e] = 0.f;
+    const gfloat* st = G<const float>(d.stats);
+    constexpr int P = 4;                                   // rows 16 p + 4 wave + group of the 64
+    float xv[P][8], gv[P][8], mean[P], rstd[P];
+#pragma unroll
+    for (int pp = 0; pp < P; ++pp) {
+        const int tk = min(tok0 + 16 * pp + 4 * wave + (lane >> 4), d.ntok - 1);
+        mean[pp] = st[2 * tk];
+        rstd[pp] = st[2 * tk + 1];
+        ln_ld8<HS>(d.x, tk, cc, xv[pp]);
+        ln_ld8<HS>(d.dy, tk, cc, gv[pp]);
+    }
+#pragma unroll
+    for (int pp = 0; pp < P; ++pp) {
+        const int tok = tok0 + 16 * pp + 4 * wave + (lane >> 4);
+        const bool ok = on && tok < d.ntok;                // rows past ntok: no contribution
+        float xh[8], gw[8], s1 = 0.f, s2 = 0.f;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            const float g = ok ? gv[pp][e] : 0.f;
+            xh[e] = on ? (xv[pp][e] - mean[pp]) * rstd[pp] : 0.f;
+            gw[e] = g * wv[e];
+            pw[e] += g * xh[e];
+            pb[e] += g;
+            s1 += gw[e];
+            s2 += gw[e] * xh[e];
+        }
+        s1 = row16_sum(s1) / (float)d.D;
+        s2 = row16_sum(s2) / (float)d.D;
+        if (ok) {
+            float v[8];
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] = rstd[pp] * (gw[e] - s1 - xh[e] * s2);
+            if (d.dx_accumulate) {
+                float o[8];
+                ln_ld8<HS>(d.dx, tok, c0, o);
+#pragma unroll
+                for (int e = 0; e < 8; ++e) v[e] += o[e];
+            }
+            ln_st8<HS>(d.dx, tok, c0, v);
+        }
+    }
+    // the wave's four row groups, then the workgroup's four waves, in a fixed order
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+        pw[e] += __shfl_xor(pw[e], 16, 64);
+        pw[e] += __shfl_xor(pw[e], 32, 64);
+        pb[e] += __shfl_xor(pb[e], 16, 64);
+        pb[e] += __shfl_xor(pb[e], 32, 64);
+    }
+    if (lane < 16 && on) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) { red[wave][0][c0 + e] = pw[e]; red[wave][1][c0 + e] = pb[e]; }
+    }
+    __syncthreads();
+    if (d.partial) {
+        gfloat* lp = G<float>(d.partial) + (int64_t)blockIdx.x * 2 * d.D;
+        for (int idx = threadIdx.x; idx < 2 * d.D; idx += 256) {
+            const int which = idx / d.D, c = idx - which * d.D;
+            lp[idx] = red[0][which][c] + red[1][which][c] + red[2][which][c] + red[3][which][c];
+        }
+    }
+}
+
 __global__ __launch_bounds__(256) void k_ln_fwd(const mep_ln_desc* __restrict__ descs) {
     const mep_ln_desc& d = descs[blockIdx.y];
-    if (d.bf16 & MEP_BF16_STORE) ln_fwd_rows<true>(d);
-    else ln_fwd_rows<false>(d);
+    const bool hs = d.bf16 & MEP_BF16_STORE;
+    if (ln_q_ok(d, true)) {
+        if (hs) ln_fwd_q<true>(d);
+        else ln_fwd_q<false>(d);
+    } else if (hs) {
+        ln_fwd_rows<true>(d);
+    } else {
+        ln_fwd_rows<false>(d);
+    }
 }
 
 // backward; partial[blockIdx.x][2][D] = per-workgroup (dgamma, dbeta) over its 64 rows.  A wave
@@ -1232,8 +1396,15 @@ MEP_DEV void ln_bwd_rows(const mep_ln_desc& d) {
 
 __global__ __launch_bounds__(256) void k_ln_bwd(const mep_ln_desc* __restrict__ descs) {
     const mep_ln_desc& d = descs[blockIdx.y];
-    if (d.bf16 & MEP_BF16_STORE) ln_bwd_rows<true>(d);
-    else ln_bwd_rows<false>(d);
+    const bool hs = d.bf16 & MEP_BF16_STORE;
+    if (ln_q_ok(d, false)) {
+        if (hs) ln_bwd_q<true>(d);
+        else ln_bwd_q<false>(d);
+    } else if (hs) {
+        ln_bwd_rows<true>(d);
+    } else {
+        ln_bwd_rows<false>(d);
+    }
 }
 
 template <typename F>
