@@ -725,8 +725,13 @@ class TriModalPlan:
 
     def set_row0(self, row0):
         """Global index of this batch's first row (data-parallel share): the dropout masks of
-        local row b are the full batch's masks of row row0 + b."""
-        self.row0.fill_(int(row0))          # shared by the model's plans: always written
+        local row b are the full batch's masks of row row0 + b.  The slot lives in the model's
+        seed_state (shared by its plans; only this method writes it), so the value last written
+        is kept on that tensor and an unchanged row0 costs no device fill per step."""
+        row0 = int(row0)
+        if getattr(self.seed_state, '_mep_row0', None) != row0:
+            self.row0.fill_(row0)
+            self.seed_state._mep_row0 = row0
 
     def set_dropout(self, p):
         """Dropout probability of the block epilogues (Ren-MME DROP at train time, 0 in eval).
