@@ -106,9 +106,10 @@ int mep_unify(const mep_gemm_desc* descs, int n_desc, int n_wg, mep_stream_t str
 #define MEP_TGEMM_RESIDENT 0x2   /* every K <= 320: the whole weight tile (N tiles of 96) staged in LDS
                                     once per workgroup, as 2 bf16 parts on the fp32 path (five
                                     products per k pair, weight error <= 2^-18 relative) */
-#define MEP_TGEMM_DMA 0x4        /* bf16 path with w_nt = 1 only: the fp32 weight chunks staged by LDS-DMA
-                                    into a ring of 4 slots (3 chunks in flight; K tails, rows past N
-                                    and unaligned rows by plain loads), X rows kept as bf16 words */
+#define MEP_TGEMM_DMA 0x4        /* w_nt = 1 only: the fp32 weight chunks staged by LDS-DMA into a ring of
+                                    4 slots (3 chunks in flight; K tails, rows past N and unaligned rows
+                                    by plain loads) and split into the path's bf16 parts on the
+                                    fragment read (bit-identical to the register-staged kernel) */
 int mep_tgemm(const mep_gemm_desc* descs, int n_desc, int max_ntok, int max_n, int flags, mep_stream_t stream);
 
 /* ---------------------------------------------------------------- weight-gradient GEMM

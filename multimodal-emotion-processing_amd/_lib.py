@@ -483,12 +483,12 @@ TGEMM_MIN_K = int(switch('MEP_TGEMM_MIN_K', '512'))
 TGEMM_RES_MAX_K = 320                              # csrc/tgemm.hip TGR_KP * 32
 TGEMM_WT = 0x1                                     # MEP_TGEMM_WT: every descriptor has w_nt = 0
 TGEMM_RESIDENT = 0x2                               # MEP_TGEMM_RESIDENT
-TGEMM_DMA = 0x4                                    # MEP_TGEMM_DMA (bf16 path: weight ring by LDS-DMA)
+TGEMM_DMA = 0x4                                    # MEP_TGEMM_DMA (weight ring by LDS-DMA)
 TGEMM_DMA_ON = switch('MEP_TGEMM_DMA', '1') != '0'
 
 
 def tgemm_dma_ok(items):
-    """MEP_TGEMM_DMA (include/mep.h) takes the bf16-path launches whose weights are stored [N][K]."""
+    """MEP_TGEMM_DMA (include/mep.h) takes the chunked launches whose weights are stored [N][K]."""
     return all(d.w_nt for d in items)
 
 
@@ -530,7 +530,7 @@ def gemm(name, descs, max_tiles, stream=None, prec=0):
         flags |= TGEMM_RESIDENT if mode == 'resident' else 0
         if any(d.bf16 for d in descs.items):
             flags |= PREC_BF16
-        if mode == 'chunked' and flags & PREC_BF16 and TGEMM_DMA_ON and tgemm_dma_ok(descs.items):
+        if mode == 'chunked' and TGEMM_DMA_ON and tgemm_dma_ok(descs.items):
             flags |= TGEMM_DMA
         call('mep_tgemm', descs.ptr, descs.n, max(d.ntok for d in descs.items), max(d.N for d in descs.items),
              flags, stream=stream)

@@ -17,6 +17,8 @@
 // (desc.bf16): one part, one product.  W columns past K are staged as zeros, so the X columns past
 // K (the next row's data, or zeros past the view through the range-checked buffer loads) never
 // contribute.
+#include <type_traits>
+
 #include "common.h"
 #include "split.h"
 
@@ -216,21 +218,27 @@ __global__ __launch_bounds__(TG_THREADS) void k_tgemm(const mep_gemm_desc* __res
     }
 }
 
-// bf16 path with the weight staged by LDS-DMA (MEP_TGEMM_DMA: w_nt).  The fp32 W chunk [BN rows][32 k]
+// Weight staged by LDS-DMA (MEP_TGEMM_DMA: w_nt; both paths).  The fp32 W chunk [BN rows][32 k]
 // goes straight from HBM / L2 into a ring of TGB_NS LDS slots (no VGPRs in flight: TGB_NS - 1 chunks
-// ahead instead of one), one 1-KiB wave instruction per 8 rows; the fragment read converts to bf16
-// (v_cvt_pk_bf16_f32, round to nearest: the same operand as the register-staged kernel).  X rows
-// stay raw bf16 words in registers, TGB_PFX chunks deep.  Slot layout: row r, 16-byte unit s holds
+// ahead instead of one), one 1-KiB wave instruction per 8 rows; the fragment read splits it into
+// its bf16 parts (one on the bf16 path, three on the fp32 path: the operand the register-staged
+// kernel's SplitW::put stores).  X rows stay in registers, TGB_PFX chunks deep (raw bf16 words on
+// the bf16 path).  Slot layout: row r, 16-byte unit s holds
 // k piece q = s ^ ((r >> 1) & 7) (a ds_read_b128 of 16 rows x one piece covers the 64 banks once).
 #ifndef MEP_TGB_NS
 #define MEP_TGB_NS 4       // LDS weight-ring slots (4 x 16 KiB at BN = 128)
 #endif
 #ifndef MEP_TGB_PFX
-#define MEP_TGB_PFX 3      // X chunks in registers
+#define MEP_TGB_PFX 3      // X chunks in registers (bf16 path)
 #endif
-template <int NI>
-MEP_DEV void tgemm_bf(const mep_gemm_desc* __restrict__ descs) {
-    constexpr int BN = 16 * NI, NS = MEP_TGB_NS, PFX = MEP_TGB_PFX;
+#ifndef MEP_TGD_PFX
+#define MEP_TGD_PFX 2      // X chunks in registers (fp32 path: two workgroups per CU)
+#endif
+template <int NI, int NPART>
+MEP_DEV void tgemm_dma(const mep_gemm_desc* __restrict__ descs) {
+    constexpr bool HS = NPART == 1;                  // bf16 path: bf16 X / Y rows
+    constexpr int ES = HS ? 2 : 4;
+    constexpr int BN = 16 * NI, NS = MEP_TGB_NS, PFX = HS ? MEP_TGB_PFX : MEP_TGD_PFX;
     constexpr int CHB = BN * 128;                    // bytes of one fp32 chunk slot
     constexpr int UPW = BN / (8 * TG_WAVES);         // DMA instructions per wave per chunk
     static_assert(BN % (8 * TG_WAVES) == 0 && NS >= 2 && PFX >= 2, "tgemm_bf geometry");
@@ -279,31 +287,43 @@ MEP_DEV void tgemm_bf(const mep_gemm_desc* __restrict__ descs) {
         }
     };
 
-    // X: raw bf16 words; rows not 8-byte aligned take four 2-byte loads per unit.  X columns past K
-    // (the next row's bf16 values, or zeros past the view) meet zero weight units
+    // X: bf16 path raw bf16 words (rows not 8-byte aligned: four 2-byte loads per unit); fp32 path
+    // fp32 units (rows not 16-byte aligned: four 4-byte loads), split into 3 parts per chunk.  X
+    // columns past K (the next row's values, or zeros past the view) meet zero weight units
     const int64_t last = row_off(d.x, ntok - 1) + K;
-    const auto rsX = __builtin_amdgcn_make_buffer_rsrc((void*)d.x.ptr, 0, (int)min((int64_t)2 * last, (int64_t)0x7fffffff), 0x00020000);
-    const bool xvec = ((d.x.ptr & 7) == 0) && (d.x.sB % 4 == 0) && (d.x.sT % 4 == 0);
+    const auto rsX = __builtin_amdgcn_make_buffer_rsrc((void*)d.x.ptr, 0, (int)min((int64_t)ES * last, (int64_t)0x7fffffff), 0x00020000);
+    const bool xvec = ((d.x.ptr & (HS ? 7 : 15)) == 0) && (d.x.sB % 4 == 0) && (d.x.sT % 4 == 0);
     int xoff[TG_TT];
 #pragma unroll
     for (int t = 0; t < TG_TT; ++t) {
         const int tok = min(tok0 + 16 * (TG_TT * wave + t) + c, ntok - 1);
-        xoff[t] = 2 * ((int)row_off(d.x, tok) + 4 * g);
+        xoff[t] = ES * ((int)row_off(d.x, tok) + 4 * g);
     }
-    u32x2 xr[PFX][TG_TT][2];
+    typedef typename std::conditional<HS, u32x2, f32x4>::type XU;
+    XU xr[PFX][TG_TT][2];
     auto load_x = [&](int s, int kc) {
 #pragma unroll
         for (int t = 0; t < TG_TT; ++t)
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
-                const int o = xoff[t] + 64 * kc + 32 * h;
-                if (xvec) {
-                    xr[s][t][h] = __builtin_bit_cast(u32x2, __builtin_amdgcn_raw_buffer_load_b64(rsX, o, 0, 0));
-                } else {
-                    unsigned e[4];
+                const int o = xoff[t] + 32 * ES * kc + 16 * ES * h;
+                if constexpr (HS) {
+                    if (xvec) {
+                        xr[s][t][h] = __builtin_bit_cast(u32x2, __builtin_amdgcn_raw_buffer_load_b64(rsX, o, 0, 0));
+                    } else {
+                        unsigned e[4];
 #pragma unroll
-                    for (int j = 0; j < 4; ++j) e[j] = (unsigned)__builtin_amdgcn_raw_buffer_load_b16(rsX, o + 2 * j, 0, 0);
-                    xr[s][t][h] = u32x2{e[0] | (e[1] << 16), e[2] | (e[3] << 16)};
+                        for (int j = 0; j < 4; ++j) e[j] = (unsigned)__builtin_amdgcn_raw_buffer_load_b16(rsX, o + 2 * j, 0, 0);
+                        xr[s][t][h] = u32x2{e[0] | (e[1] << 16), e[2] | (e[3] << 16)};
+                    }
+                } else {
+                    if (xvec) {
+                        xr[s][t][h] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rsX, o, 0, 0));
+                    } else {
+#pragma unroll
+                        for (int j = 0; j < 4; ++j)
+                            xr[s][t][h][j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsX, o + 4 * j, 0, 0));
+                    }
                 }
             }
     };
@@ -331,18 +351,20 @@ MEP_DEV void tgemm_bf(const mep_gemm_desc* __restrict__ descs) {
         if (kc + NS - 1 < nkc) issue_w(kc + NS - 1);
         if (kc + PFX - 1 < nkc) load_x((s + PFX - 1) % PFX, kc + PFX - 1);
         const lbyte* ws = (const lbyte*)sm + (kc % NS) * CHB;
-        bf16x8 xo[TG_TT];
+        OpN<NPART> xo[TG_TT];
 #pragma unroll
-        for (int t = 0; t < TG_TT; ++t) xo[t] = kpair(xr[s][t][0], xr[s][t][1]);
+        for (int t = 0; t < TG_TT; ++t) {
+            if constexpr (HS) xo[t].p[0] = kpair(xr[s][t][0], xr[s][t][1]);
+            else xo[t] = opn<NPART>(xr[s][t][0], xr[s][t][1]);
+        }
 #pragma unroll
         for (int i = 0; i < NI; ++i) {
             const int r = 16 * i + c, sw = (r >> 1) & 7;
             const f32x4 a0 = *(lcf4*)(ws + r * 128 + 16 * (g ^ sw));
             const f32x4 a1 = *(lcf4*)(ws + r * 128 + 16 * ((4 + g) ^ sw));
-            const bf16x8 wo = kpair(u32x2{pk_bf16(a0[0], a0[1]), pk_bf16(a0[2], a0[3])},
-                                    u32x2{pk_bf16(a1[0], a1[1]), pk_bf16(a1[2], a1[3])});
+            const OpN<NPART> wo = opn<NPART>(a0, a1);     // the parts SplitW::put would store
 #pragma unroll
-            for (int t = 0; t < TG_TT; ++t) acc[t][i] = mfma_bf16(wo, xo[t], acc[t][i]);
+            for (int t = 0; t < TG_TT; ++t) acc[t][i] = mma_n<NPART>(wo, xo[t], acc[t][i]);
         }
     };
     int kc = 0;
@@ -354,7 +376,7 @@ MEP_DEV void tgemm_bf(const mep_gemm_desc* __restrict__ descs) {
     for (int s = 0; s < PFX - 1; ++s)
         if (kc + s < nkc) step(kc + s, s);
 
-    // ---- epilogue: token c of tile t, features n0 + 16 i + 4g .. +3 (bf16 rows)
+    // ---- epilogue: token c of tile t, features n0 + 16 i + 4g .. +3
     const gfloat* bias = G<const float>(d.bias);
     const gfloat* table = G<const float>(d.table);
     const int ldt = d.ldt ? d.ldt : N;
@@ -362,7 +384,7 @@ MEP_DEV void tgemm_bf(const mep_gemm_desc* __restrict__ descs) {
     for (int t = 0; t < TG_TT; ++t) {
         const int tok = tok0 + 16 * (TG_TT * wave + t) + c;
         if (tok >= ntok) continue;
-        const auto yrow = rowa<true>(d.y, tok);
+        const auto yrow = rowa<HS>(d.y, tok);
         const gfloat* trow = table ? table + (int64_t)(tok % d.y.T) * ldt : nullptr;
 #pragma unroll
         for (int i = 0; i < NI; ++i) {
@@ -389,7 +411,8 @@ MEP_DEV void tgemm_bf(const mep_gemm_desc* __restrict__ descs) {
 // one kernel per N tile (plain kernels: hipcc leaves the host stubs of kernel templates named only
 // inside a switch undefined)
 #define MEP_TGB_K(NI) \
-    __global__ __launch_bounds__(TG_THREADS) void k_tgemm_bf##NI(const mep_gemm_desc* __restrict__ descs) { tgemm_bf<NI>(descs); }
+    __global__ __launch_bounds__(TG_THREADS) void k_tgemm_bf##NI(const mep_gemm_desc* __restrict__ descs) { tgemm_dma<NI, 1>(descs); } \
+    __global__ __launch_bounds__(TG_THREADS) void k_tgemm_dma##NI(const mep_gemm_desc* __restrict__ descs) { tgemm_dma<NI, 3>(descs); }
 MEP_TGB_K(2) MEP_TGB_K(4) MEP_TGB_K(6) MEP_TGB_K(8)
 #undef MEP_TGB_K
 
@@ -563,16 +586,19 @@ extern "C" int mep_tgemm(const mep_gemm_desc* descs, int n_desc, int max_ntok, i
         return mep_check_launch("mep_tgemm");
     }
     const int ni = max_n >= 16 * MEP_TG_NI ? MEP_TG_NI : (max_n + 15) / 16;   // 16-col tiles per workgroup N tile
-    if (flags & MEP_TGEMM_DMA) {   // bf16 path, w_nt
-        if (!bf || !wnt) { mep_set_error("mep_tgemm: MEP_TGEMM_DMA needs MEP_PREC_BF16 and w_nt"); return MEP_EINVAL; }
+    if (flags & MEP_TGEMM_DMA) {   // w_nt (host)
+        if (!wnt) { mep_set_error("mep_tgemm: MEP_TGEMM_DMA needs w_nt"); return MEP_EINVAL; }
         const dim3 grid((max_ntok + TG_BM - 1) / TG_BM, n_desc, (max_n + 16 * ni - 1) / (16 * ni)), block(TG_THREADS);
+#define MEP_TGD(NI) do { if (bf) hipLaunchKernelGGL(k_tgemm_bf##NI, grid, block, 0, st, descs); \
+                         else hipLaunchKernelGGL(k_tgemm_dma##NI, grid, block, 0, st, descs); } while (0)
         switch (ni) {
-            case 2: hipLaunchKernelGGL(k_tgemm_bf2, grid, block, 0, st, descs); break;
-            case 4: hipLaunchKernelGGL(k_tgemm_bf4, grid, block, 0, st, descs); break;
-            case 6: hipLaunchKernelGGL(k_tgemm_bf6, grid, block, 0, st, descs); break;
-            case 8: hipLaunchKernelGGL(k_tgemm_bf8, grid, block, 0, st, descs); break;
+            case 2: MEP_TGD(2); break;
+            case 4: MEP_TGD(4); break;
+            case 6: MEP_TGD(6); break;
+            case 8: MEP_TGD(8); break;
             default: mep_set_error("mep_tgemm: N must be 32, 64, 96 or >= 128 (a multiple of 16)"); return MEP_EINVAL;
         }
+#undef MEP_TGD
         return mep_check_launch("mep_tgemm");
     }
     const dim3 grid((max_ntok + TG_BM - 1) / TG_BM, n_desc, (max_n + 16 * ni - 1) / (16 * ni)), block(TG_THREADS);

@@ -142,25 +142,27 @@ def _launch_flags(descs, dev, flags):
     return arr
 
 
+@pytest.mark.parametrize('bf', [True, False], ids=['bf16', 'fp32'])
 @pytest.mark.parametrize('N,Ks,B,T,extra', [
     (128, (768, 640, 205), 4, 300, False),   # Ren-MME cfg5 unify widths (K = 205: a K tail, unaligned rows)
     (128, (768, 640, 35), 3, 7, True),       # ragged: 21 tokens; bias + position table + accumulate
     (96, (320, 64, 74), 5, 50, False),       # N tile 96 (6 column tiles)
     (256, (512,), 2, 130, True),             # two N tiles; 260 tokens (a partial last workgroup)
 ])
-def test_tgemm_bf16_dma_matches_register_staging(N, Ks, B, T, extra, cuda):
-    """MEP_TGEMM_DMA (weight ring by LDS-DMA, X as raw bf16 words) against the register-staged bf16
-    kernel on the same descriptors -- the same operands, MFMAs and order: bit-identical -- and
-    against torch's bf16-operand product; K tails and unaligned weight / X rows (K = 205, 35, 74)
-    take the plain-load units of the same kernel."""
+def test_tgemm_dma_matches_register_staging(N, Ks, B, T, extra, bf, cuda):
+    """MEP_TGEMM_DMA (weight ring by LDS-DMA) against the register-staged kernel on the same
+    descriptors -- the same operands (one bf16 part, or three on the fp32 path), MFMAs and order:
+    bit-identical -- and against torch's product (bf16 operands; float64 on the fp32 path); K tails
+    and unaligned weight / X rows (K = 205, 35, 74) take the plain-load units of the same kernel."""
     from mep_amd import _lib
     torch.manual_seed(N + B + T)
-    xs = [torch.randn(B, 2, T, K, device=cuda).bfloat16() for K in Ks]
+    dt = torch.bfloat16 if bf else torch.float32
+    xs = [torch.randn(B, 2, T, K, device=cuda).to(dt) for K in Ks]
     ws = [torch.randn(N, K, device=cuda) / K ** 0.5 for K in Ks]
     bias = torch.randn(N, device=cuda) if extra else None
     tab = torch.randn(T, N, device=cuda) if extra else None
-    base = [[torch.randn(B, T, N, device=cuda).bfloat16() if extra else
-             torch.full((B, T, N), float('nan'), device=cuda).bfloat16() for _ in range(2)] for _ in Ks]
+    base = [[torch.randn(B, T, N, device=cuda).to(dt) if extra else
+             torch.full((B, T, N), float('nan'), device=cuda).to(dt) for _ in range(2)] for _ in Ks]
     outs = {}
     for dma in (False, True):
         ys = [[b.clone() for b in bb] for bb in base]
@@ -169,16 +171,18 @@ def test_tgemm_bf16_dma_matches_register_staging(N, Ks, B, T, extra, cuda):
             K = x.shape[-1]
             for e in range(2):
                 descs.append(_gd(_rows(x, T, 2 * T * K, K, e * T * K), _rows(ys[i][e], T, T * N, N), w, B * T, N, K, K,
-                                 bias=bias, table=tab, accumulate=int(extra), bf16=_lib.BF16_OPS | _lib.BF16_STORE))
+                                 bias=bias, table=tab, accumulate=int(extra),
+                                 bf16=(_lib.BF16_OPS | _lib.BF16_STORE) if bf else 0))
         assert _lib.tgemm_dma_ok(descs)
-        keep = _launch_flags(descs, cuda, _lib.PREC_BF16 | (_lib.TGEMM_DMA if dma else 0))
+        keep = _launch_flags(descs, cuda, (_lib.PREC_BF16 if bf else 0) | (_lib.TGEMM_DMA if dma else 0))
         outs[dma] = ys
         del keep
     for i, (x, w) in enumerate(zip(xs, ws)):
         for e in range(2):
             assert torch.equal(outs[True][i][e], outs[False][i][e]), (i, e)
-            want = x[:, e].double() @ w.bfloat16().double().t()
+            want = x[:, e].double() @ (w.bfloat16() if bf else w).double().t()
             if extra:
                 want = want + bias.double() + tab.double() + base[i][e].double()
-            assert_close(outs[True][i][e], want, rtol=4e-3, atol_frac=1e-4, name='K%d slot%d' % (x.shape[-1], e))
+            tol = dict(rtol=4e-3, atol_frac=1e-4) if bf else dict(rtol=1e-5, atol_frac=1e-6)
+            assert_close(outs[True][i][e], want, name='K%d slot%d' % (x.shape[-1], e), **tol)
 
