@@ -1,5 +1,5 @@
 #!/bin/bash
-# round-4 GPU session 19: profile set v3 (32-bit dropout hash, LDS-DMA bf16 token GEMM): GPU suite,
+# round-4 GPU session 19 (re-run as the v4 set: 16-lane LayerNorm, weight-gradient rounds, fp32 DMA GEMM): GPU suite,
 # smoke(); per workload the kernel trace + stats, the 32-B read units and WRITE_SIZE; the SQ groups
 # of cfg5 bf16; then the bench lines of every config
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
