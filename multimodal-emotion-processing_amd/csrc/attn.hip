@@ -77,6 +77,9 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 #ifndef MEP_FWD_WAVES
 #define MEP_FWD_WAVES 3    // waves per SIMD of the short, non-residual forward
 #endif
+#ifndef MEP_FWD_MASKACC
+#define MEP_FWD_MASKACC 1      // bf16 forward: mask term as the score accumulator's initial value (MI)
+#endif
 #ifndef MEP_BWD_WIDE_WAVES
 #define MEP_BWD_WIDE_WAVES 0   // waves per SIMD of the wide Tk > 64 backward (0: as the short one)
 #endif
@@ -467,6 +470,12 @@ MEP_DEV void attn_fwd_task(const mep_attn_desc& d, int qc, int h, int b, int lan
         }
     };
 
+    // MI (bf16, no residual scores, hd 16): the key's mask term enters as the score accumulator's
+    // initial value (-4 mask: the dot is scaled by 1/4 later), the max runs on the raw dot and the
+    // 1/4 folds into the exponent's fma -- per score one max, one fma and the exp2 instead of a
+    // scale, a mask subtraction, the max, the fma and the exp2.  Kept keys (mask 0) give the same
+    // bits: 1/4 is a power of two, so scaling commutes with every rounding on the way
+    constexpr bool MI = BF && !PREV && !SOUT && HDIM == 16 && MEP_FWD_MASKACC;
     constexpr bool QH = !SINGLE && MEP_FWD_QHOIST;
     S3 qsh[QH ? NT : 1][NHB];                  // QH: B of S^T for every query tile of the task
     if (QH) {
@@ -615,7 +624,8 @@ MEP_DEV void attn_fwd_task(const mep_attn_desc& d, int qc, int h, int b, int lan
             float mx = -INFINITY;
 #pragma unroll
             for (int kt = 0; kt < NT; ++kt) {
-                floatx4 st = zero4();                                      // C[key 4g+r][query c]
+                floatx4 st = MI ? floatx4{-4.f * mt[kt][0], -4.f * mt[kt][1], -4.f * mt[kt][2], -4.f * mt[kt][3]}
+                                : zero4();                                 // C[key 4g+r][query c]
 #pragma unroll
                 for (int hb = 0; hb < NHB; ++hb) st = dot_score<true, BF>(ks[kt][hb], qs[hb], st);
 #pragma unroll
@@ -628,6 +638,8 @@ MEP_DEV void attn_fwd_task(const mep_attn_desc& d, int qc, int h, int b, int lan
                         const float v = score<PREV, HDIM>(st[r], cres, spv, mt[kt][r]);
                         if (SOUT && kk < Tk && q < Tq) sout[si] = v;
                         sv[kt][r] = v;
+                    } else if (MI) {
+                        sv[kt][r] = st[r];                                 // 4 x the score (dot - 4 mask)
                     } else {
                         sv[kt][r] = score<false, HDIM>(st[r], 0.f, 0.f, mt[kt][r]);
                     }
@@ -638,19 +650,20 @@ MEP_DEV void attn_fwd_task(const mep_attn_desc& d, int qc, int h, int b, int lan
             const float mnew = SINGLE ? mx : fmaxf(m[qt], mx);
             float lsum = 0.f;
             constexpr float L2E = 1.4426950408889634f;
-            const float mb = mnew * L2E;
+            constexpr float SL2E = MI ? INV_SCALE * L2E : L2E;            // MI: raw dots
+            const float mb = mnew * SL2E;
 #pragma unroll
             for (int kt = 0; kt < NT; ++kt)
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
-                    sv[kt][r] = MEP_FWD_EXP2 ? __builtin_amdgcn_exp2f(fmaf(sv[kt][r], L2E, -mb)) : __expf(sv[kt][r] - mnew);
+                    sv[kt][r] = MEP_FWD_EXP2 || MI ? __builtin_amdgcn_exp2f(fmaf(sv[kt][r], SL2E, -mb)) : __expf(sv[kt][r] - mnew);
                     if (!(BF && MEP_FWD_MFSUM)) lsum += sv[kt][r];
                 }
             floatx4 oq[NHB];
 #pragma unroll
             for (int hb = 0; hb < NHB; ++hb) oq[hb] = SINGLE ? zero4() : o[qt][hb];
             if (!SINGLE && k_lo > 0) {   // rescale the running state (O^T: the lane's own query c)
-                const float corr = __expf(m[qt] - mnew);
+                const float corr = __expf(MI ? (m[qt] - mnew) * INV_SCALE : m[qt] - mnew);
                 l[qt] *= corr;
 #pragma unroll
                 for (int r = 0; r < 4; ++r)
@@ -720,7 +733,7 @@ MEP_DEV void attn_fwd_task(const mep_attn_desc& d, int qc, int h, int b, int lan
             }
             if (BF && MEP_FWD_MFSUM) lsum = lacc[0];
             if (SINGLE) {
-                finish(qt, oq, mnew, lsum);
+                finish(qt, oq, MI ? mnew * INV_SCALE : mnew, lsum);
             } else {
 #pragma unroll
                 for (int hb = 0; hb < NHB; ++hb) o[qt][hb] = oq[hb];
@@ -733,7 +746,7 @@ MEP_DEV void attn_fwd_task(const mep_attn_desc& d, int qc, int h, int b, int lan
 #pragma unroll
         for (int qt = 0; qt < NT; ++qt) {
             if (qt >= nqt) break;
-            finish(qt, o[qt], m[qt], l[qt]);
+            finish(qt, o[qt], MI ? m[qt] * INV_SCALE : m[qt], l[qt]);
         }
     }
 }
