@@ -80,6 +80,9 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 #ifndef MEP_FWD_MASKACC
 #define MEP_FWD_MASKACC 1      // bf16 forward: mask term as the score accumulator's initial value (MI)
 #endif
+#ifndef MEP_FWD_MASKACC_F32
+#define MEP_FWD_MASKACC_F32 0  // the same on the fp32 forward (not yet measured on the GPU: off)
+#endif
 #ifndef MEP_BWD_WIDE_WAVES
 #define MEP_BWD_WIDE_WAVES 0   // waves per SIMD of the wide Tk > 64 backward (0: as the short one)
 #endif
@@ -470,12 +473,12 @@ MEP_DEV void attn_fwd_task(const mep_attn_desc& d, int qc, int h, int b, int lan
         }
     };
 
-    // MI (bf16, no residual scores, hd 16): the key's mask term enters as the score accumulator's
+    // MI (no residual scores, hd 16): the key's mask term enters as the score accumulator's
     // initial value (-4 mask: the dot is scaled by 1/4 later), the max runs on the raw dot and the
     // 1/4 folds into the exponent's fma -- per score one max, one fma and the exp2 instead of a
     // scale, a mask subtraction, the max, the fma and the exp2.  Kept keys (mask 0) give the same
     // bits: 1/4 is a power of two, so scaling commutes with every rounding on the way
-    constexpr bool MI = BF && !PREV && !SOUT && HDIM == 16 && MEP_FWD_MASKACC;
+    constexpr bool MI = !PREV && !SOUT && HDIM == 16 && (BF ? MEP_FWD_MASKACC : MEP_FWD_MASKACC_F32);
     constexpr bool QH = !SINGLE && MEP_FWD_QHOIST;
     S3 qsh[QH ? NT : 1][NHB];                  // QH: B of S^T for every query tile of the task
     if (QH) {
