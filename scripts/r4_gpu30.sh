@@ -3,7 +3,7 @@
 # accumulator's initial value (variants/mif) against the scale / subtract form (base)
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/t30.log 2>&1
+MEP_LIB=$PWD/variants/mif/libmep_hip.so timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/t30.log 2>&1
 rc=$?; echo "pytest rc=$rc"; grep -E "passed|failed" gpurun_out/t30.log | tail -2; grep -E "^FAILED|^ERROR|Error" gpurun_out/t30.log | head -20
 [ $rc -eq 0 ] || exit $rc
 V="base=X=1;mif=MEP_LIB=$PWD/variants/mif/libmep_hip.so"
