@@ -5,18 +5,23 @@ B=64 utterance pairs per GPU, T=50 for text (d=300), visual (d=35) and audio (d=
 forward of both encoders + head + circle loss + backward + clip_grad_norm_(1.0) + AdamW (lr 1e-3)
 [+ RCCL all-reduce of the flat gradient when N > 1].  Synthetic N(0,1) features, all-ones masks,
 Bernoulli(0.3) labels, random-init weights; inputs resident in HBM before the timed region.
-Arithmetic: the dtype BASELINE.json names for the config -- bf16 for cfg3 / cfg4 / cfg5, fp32 for
-cfg2.  bf16 (the default of cfg3 / cfg5): plain bf16 operands on every encoder product with fp32
-accumulation, encoder activations stored in bf16, scores, softmax and LayerNorm statistics, pooled
-tensor, loss, gradients and AdamW in fp32; held to torch.autocast(bf16)'s own error on the oracle
-(tests/test_gpu_bf16.py).  --dtype fp32: fp32 storage, softmax, LayerNorm and accumulation; the
-products run on the matrix cores either in fp32 (v_mfma_f32_*) or as fp32 operands split into
-bf16 parts, within the 1e-4 logits parity of the fp32 reference.
 
-    python bench.py [--gpus N --steps K --warmup W]                  BASELINE cfg3 (cfg4 with N > 1), bf16
-    python bench.py --config cfg2 | cfg5                            the other BASELINE configs
-    python bench.py [--config cfg5] --dtype fp32                    the fp32 (1e-4 parity) path
-    torchrun --nproc-per-node N bench.py --gpus N ...                (one process per GPU, RCCL)
+Arithmetic of the headline line: fp32, the reference's own precision (cmu-mosei/run.py:360-369 has
+no AMP) -- fp32 storage, softmax, LayerNorm and accumulation; the products run on the matrix cores
+as fp32 operands split into bf16 parts, within the 1e-4 logits parity of the
+reference.  BASELINE.json names bf16 for cfg3 / cfg5: that path (bf16 operands and activation
+storage, fp32 accumulation, statistics, loss, gradients and AdamW; held to torch.autocast(bf16)'s
+own error, tests/test_gpu_bf16.py) is timed in the same run and nested as "bf16".
+
+Per-kernel times ("kernels", "roofline*") are in-step device times
+(time_launches: real-time-counter stamps around each launch of a captured step), so they
+exclude host submission gaps and sum to at most the step time.
+"hbm_measured" is the box's measured HBM peak (mep_hbm_probe) beside the 8 TB/s spec.
+
+    python bench.py [--gpus N --steps K --warmup W]        BASELINE cfg3 (cfg4 with N > 1), fp32 + bf16
+    python bench.py --config cfg2 | cfg5 | rfstate        the other workloads
+    python bench.py --dtype bf16                          the bf16 path as the headline line
+    torchrun --nproc-per-node N bench.py --gpus N ...      (one process per GPU, RCCL)
 Rank 0 prints one JSON line.
 """
 import argparse
@@ -43,29 +48,127 @@ B, T, D, H, NL = 64, 50, 96, 6, 1
 DIMS = (300, 35, 74)
 
 
-class LaunchTimer:
-    """HIP events around every libmep launch of an eager step, on the launching stream."""
+class StampTimer:
+    """_lib.TIMER hook: a mep_stamp kernel (the device's real-time counter, stored when it starts)
+    before and after every entry-point call, on the call's stream."""
 
-    def __init__(self):
-        self.ev = []
+    def __init__(self, slots):
+        self.slots, self.names, self.n = slots, [], 0
+
+    def _stamp(self, stream):
+        import ctypes
+        from mep_amd import _lib
+        assert self.n < self.slots.numel()
+        _lib.check(_lib.lib().mep_stamp(ctypes.c_void_p(self.slots.data_ptr()), self.n, _lib.stream_ptr(stream)),
+                   'mep_stamp')
+        self.n += 1
 
     def begin(self, name, stream=None):
-        e = torch.cuda.Event(enable_timing=True)
-        e.record(stream if stream is not None else torch.cuda.current_stream())
-        self.ev.append([name, e, None])
+        self.names.append(name)
+        self._stamp(stream)
 
     def end(self, name, stream=None):
-        e = torch.cuda.Event(enable_timing=True)
-        e.record(stream if stream is not None else torch.cuda.current_stream())
-        self.ev[-1][2] = e
+        self._stamp(stream)
 
-    def totals(self):
+
+def time_launches(work, reps=20):
+    """Device time of every libmep launch of a training step, where it runs in the step.
+
+    The step body (forward, backward, clip + optimizer) is captured into a graph with a mep_stamp
+    kernel before and after every launch (a one-wave kernel storing the 100-MHz real-time counter
+    as it starts; graph kernels run back to back) and replayed `reps` times.  A launch's time is
+    the interval between its two stamps minus the interval of two stamps with nothing between
+    them (measured in a graph of 64 such pairs): the launch's execution plus its dispatch, in
+    the step -- after the same producers, with the same cache contents -- which is what a
+    rocprofv3 trace of a graph step reports per kernel (a kernel's start there is its
+    predecessor's end).  HIP events cannot give this on ROCm: timing markers add ~3-5 us to every
+    bracketed launch (hipExtLaunchKernel's events included), external event nodes are refused
+    under capture, and a launch replayed alone re-reads what its previous replay left in the
+    256-MB Infinity Cache (up to ~15% fast).  The replays update the model: this runs after the
+    timed region and the loss readout.
+
+    Returns ({launch name: (seconds per step over its launches, launches per step)}, method)."""
+    import ctypes
+    from mep_amd import _lib
+    L = _lib.lib()
+    khz = L.mep_stamp_khz()
+    assert khz > 0, _lib.last_error()
+    tick = 1.0 / (khz * 1e3)
+    dev = work.plan.device if hasattr(work.plan, 'device') else torch.device('cuda', torch.cuda.current_device())
+    slots = torch.zeros(4096, dtype=torch.int64, device=dev)
+
+    def capture(body):
+        timer = StampTimer(slots)
         torch.cuda.synchronize()
-        out = {}
-        for name, a, b in self.ev:
-            t, n = out.get(name, (0.0, 0))
-            out[name] = (t + a.elapsed_time(b) / 1e3, n + 1)
-        return out
+        g = torch.cuda.CUDAGraph()
+        _lib.TIMER = timer
+        try:
+            with torch.cuda.graph(g):
+                body()
+        finally:
+            _lib.TIMER = None
+        return g, timer
+
+    def intervals(g, n):
+        acc = torch.zeros(n // 2, dtype=torch.float64)
+        for _ in range(reps):
+            g.replay()
+            torch.cuda.synchronize()
+            s = slots[:n].cpu().double().reshape(-1, 2)
+            acc += (s[:, 1] - s[:, 0]) * tick
+        return acc / reps
+
+    def empty_pairs():
+        for _ in range(64):
+            _lib.TIMER.begin('empty')
+            _lib.TIMER.end('empty')
+    g0, t0 = capture(empty_pairs)
+    overhead = float(intervals(g0, t0.n).mean())
+    del g0
+    g, timer = capture(work.step_body)
+    per = intervals(g, timer.n) - overhead
+    del g
+    tot = {}
+    for name, t in zip(timer.names, per.tolist()):
+        s0, c = tot.get(name, (0.0, 0))
+        tot[name] = (s0 + t, c + 1)
+    method = ('in-step: real-time-counter stamps around each launch of a captured step, %d replays, minus '
+              'the %.2f-us interval of two adjacent stamps' % (reps, overhead * 1e6))
+    return tot, method
+
+
+def hbm_probe(dev, gib=2):
+    """Measured HBM peaks (GB/s) of mep_hbm_probe's copy / read / write streams over 2-GiB
+    buffers (8x the 256-MB Infinity Cache), best over a few grid sizes (the
+    vendor spec and a measured copy-kernel peak, both reported)."""
+    import ctypes
+    from mep_amd import _lib
+    n16 = (gib << 30) // 16
+    src = torch.ones(n16 * 4, dtype=torch.float32, device=dev)
+    dst = torch.empty_like(src)
+    out = {}
+    for mode, key, factor in ((0, 'copy', 2), (1, 'read', 1), (2, 'write', 1)):
+        best = 0.0
+        for n_wg in (1024, 2048, 4096):
+            def go():
+                _lib.call('mep_hbm_probe', ctypes.c_void_p(src.data_ptr()), ctypes.c_void_p(dst.data_ptr()), n16,
+                          mode, n_wg)
+            go()
+            torch.cuda.synchronize()
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            reps = 10
+            a.record()
+            for _ in range(reps):
+                go()
+            b.record()
+            torch.cuda.synchronize()
+            best = max(best, factor * 16 * n16 * reps / (a.elapsed_time(b) / 1e3) / 1e9)
+        out[key + '_GBps'] = round(best, 1)
+    out.update(buffer_GiB=gib, kernel='mep_hbm_probe (csrc/probe.hip): dwordx4 grid-stride, 8 loads in flight per '
+               'thread, best of 1024 / 2048 / 4096 workgroups')
+    del src, dst
+    torch.cuda.empty_cache()
+    return out
 
 
 # launch name -> kernel symbol prefix in the rocprofv3 summaries (scripts/parse_prof.py)
@@ -74,7 +177,8 @@ KERNEL_OF = {'mep_attn_bwd': 'k_attn_bwd', 'mep_attn_fwd': 'k_attn_fwd', 'mep_bl
              'mep_pool_fwd': 'k_pool_fwd', 'mep_pool_bwd': 'k_pool_bwd', 'mep_gemm': 'k_gemm', 'mep_tgemm': 'k_tgemm',
              'mep_rf_epi_fwd': 'k_rf_epi_fwd', 'mep_rf_epi_bwd': 'k_rf_epi_bwd', 'mep_sum_rows': 'k_sum_rows',
              'mep_wgemm': 'k_wgemm', 'mep_rfw_epi_fwd': 'k_rfw_fwd', 'mep_rfw_epi_bwd': 'k_rfw_bwd',
-             'mep_wsplit': 'k_wsplit'}
+             'mep_wsplit': 'k_wsplit', 'mep_reduce_grads': 'k_reduce_grads', 'mep_head_fwd_bwd': 'k_head',
+             'mep_clip_adam_ext': 'k_clip_adam', 'mep_rf_head': 'k_rf_head'}
 
 
 def pmc_traffic(launch, tag='cfg3'):
@@ -169,6 +273,11 @@ class Cfg3:
     def eager_step(self):
         self.eng_eager.step_plan(self.plan)
 
+    def step_body(self):
+        """the body the engine captures for one step: forward, backward, clip + AdamW"""
+        self.eng._fwd_bwd_allreduce(self.plan, self.eng._runner(self.plan.device))
+        self.eng._opt()
+
     def loss(self):
         return float(self.plan.loss.item())
 
@@ -238,6 +347,11 @@ class Cfg5:
 
     def eager_step(self):
         self.eng_eager.step_plan(self.plan)
+
+    def step_body(self):
+        """the body the engine captures for one step: forward, backward, clip + AdamW"""
+        self.eng._fwd_bwd_allreduce(self.plan, self.eng._runner(self.plan.device))
+        self.eng._opt()
 
     def loss(self):
         return float(self.plan.loss.item())
@@ -322,6 +436,9 @@ class Cfg2:
     def eager_step(self):
         self._body()
 
+    def step_body(self):
+        self._body()
+
     def loss(self):
         """The objective mean(out * G) of the last step's forward."""
         return float((self.plan.out_chain * self.G).double().mean().item())
@@ -401,56 +518,37 @@ class _FlatAdam:
 CONFIGS = {'cfg3': Cfg3, 'cfg5': Cfg5, 'cfg2': Cfg2}
 
 
-def roofline_of(work, name, tot, reps, costs):
+def roofline_of(work, name, tot, costs, probe=None):
+    """roofline object of launch `name`: the plan's algorithmic flops / bytes per launch over the
+    launch's in-step time (time_launches), plus the committed PMC traffic and, when
+    measured, the fraction of the box's measured HBM peak"""
     from mep_amd import roofline
     t, n = tot[name]
     per_launch_s = t / n
-    launches_per_step = max(1, n // reps)
     flops, nbytes = costs[name]
     spec = getattr(work.plan, 'spec', None)
-    rl = roofline.roofline_entry(name, flops / launches_per_step, nbytes / launches_per_step, per_launch_s,
-                                 bf16=work.bf16, D=getattr(spec, 'D', None))
+    rl = roofline.roofline_entry(name, flops / n, nbytes / n, per_launch_s, bf16=work.bf16, D=getattr(spec, 'D', None))
     rl['traffic'], rl['traffic_source'] = pmc_traffic(name, work.name + ('_bf16' if work.bf16 else ''))
     rl['avg_launch_us'] = round(per_launch_s * 1e6, 2)
+    rl['launches_per_step'] = n
+    if probe and rl['bound'] == 'hbm':
+        rl['peak_measured'] = probe['read_GBps']
+        rl['frac_measured'] = round(rl['achieved'] / probe['read_GBps'], 4)
     return rl
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument('--gpus', type=int, default=1)
-    ap.add_argument('--steps', type=int, default=200)
-    ap.add_argument('--warmup', type=int, default=20)
-    ap.add_argument('--config', default='cfg3', choices=sorted(CONFIGS))
-    ap.add_argument('--no-cpu-baseline', action='store_true')
-    ap.add_argument('--no-graph', action='store_true')
-    ap.add_argument('--cpu-budget', type=float, default=12.0)
-    ap.add_argument('--dtype', default=None, choices=('fp32', 'bf16'),
-                    help="default: the config's BASELINE dtype (bf16 for cfg3 / cfg5, fp32 for cfg2); "
-                         'fp32: the 1e-4 parity path')
-    args = ap.parse_args()
-    if args.dtype is None:
-        args.dtype = CONFIGS[args.config].baseline_dtype
-
-    world = int(os.environ.get('WORLD_SIZE', '1'))
-    rank = int(os.environ.get('RANK', '0'))
-    local = int(os.environ.get('LOCAL_RANK', '0'))
-    if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group('nccl', device_id=torch.device('cuda', local))
-    dev = torch.device('cuda', local)
-
+def run_config(cls, dev, rank, world, graph, bf16, steps, warmup):
+    """time `steps` steps of one workload at one precision, then its launches one by one"""
     from mep_amd import _lib, roofline
-    graph = not args.no_graph
-    work = CONFIGS[args.config](dev, rank, graph, bf16=args.dtype == 'bf16')
-
-    for _ in range(args.warmup):
+    work = cls(dev, rank, graph, bf16=bf16)
+    for _ in range(warmup):
         work.step()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for _ in range(steps):
         work.step()
     torch.cuda.synchronize()
     if world > 1:
@@ -462,38 +560,87 @@ def main():
         el = float(t.item())
     loss = work.loss()
 
-    # per-launch HIP-event timing of eager steps -> dominant kernel and attention rooflines
-    timer = LaunchTimer()
-    reps = 20
-    _lib.TIMER = timer
-    for _ in range(reps):
-        work.eager_step()
-    _lib.TIMER = None
-    tot = timer.totals()
+    # every launch of the step, timed where it runs (time_launches)
+    tot, method = time_launches(work)
     costs = roofline.launch_costs(work.plan)
-    per_kernel = {k: dict(ms_per_step=round(t / reps * 1e3, 4), launches_per_step=n // reps)
-                  for k, (t, n) in sorted(tot.items(), key=lambda kv: -kv[1][0])}
+    kernels = {k: dict(ms_per_step=round(t * 1e3, 4), launches_per_step=n, avg_launch_us=round(t / n * 1e6, 2))
+               for k, (t, n) in sorted(tot.items(), key=lambda kv: -kv[1][0])}
     dom = max((k for k in tot if k in costs), key=lambda k: tot[k][0])
+    res = {
+        'value': round(work.rows * world * steps / el, 2),
+        'ms_per_step': round(el / steps * 1e3, 4),
+        'loss': round(loss, 6),
+        'kernels': kernels,
+        'kernels_sum_ms': round(sum(t for t, _ in tot.values()) * 1e3, 4),
+        'kernel_timing': method,
+    }
+    return work, res, tot, costs, dom
 
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--steps', type=int, default=200)
+    ap.add_argument('--warmup', type=int, default=20)
+    ap.add_argument('--config', default='cfg3', choices=sorted(CONFIGS))
+    ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--no-graph', action='store_true')
+    ap.add_argument('--no-bf16', action='store_true', help='skip the nested bf16 line of cfg3 / cfg5')
+    ap.add_argument('--no-probe', action='store_true', help='skip the measured HBM peak')
+    ap.add_argument('--cpu-budget', type=float, default=12.0)
+    ap.add_argument('--dtype', default='fp32', choices=('fp32', 'bf16'),
+                    help="fp32 (default): the reference's own precision, the 1e-4 parity path; the "
+                         "config's BASELINE bf16 line is nested in the same JSON")
+    args = ap.parse_args()
+    cls = CONFIGS[args.config]
+
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local = int(os.environ.get('LOCAL_RANK', '0'))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+    dev = torch.device('cuda', local)
+
+    from mep_amd import _lib
+    graph = not args.no_graph
+    probe = None if args.no_probe else hbm_probe(dev)
+    work, res, tot, costs, dom = run_config(cls, dev, rank, world, graph, args.dtype == 'bf16', args.steps,
+                                            args.warmup)
     out = {
         'metric': work.metric,
-        'value': round(work.rows * world * args.steps / el, 2),
+        'value': res['value'],
         'unit': work.unit,
         'n_gpus': world,
         'steps': args.steps,
         'warmup': args.warmup,
-        'ms_per_step': round(el / args.steps * 1e3, 4),
+        'ms_per_step': res['ms_per_step'],
         'higher_is_better': True,
         'scaling': 'weak',
         'vs_baseline': None,
         'dtype': args.dtype,
         'data': 'synthetic N(0,1) features, all-ones masks, Bernoulli(0.3) labels, random-init weights',
         'config': work.config(world, graph),
-        'loss': round(loss, 6),
-        'roofline': roofline_of(work, dom, tot, reps, costs),
-        'roofline_attention': roofline_of(work, 'mep_attn_bwd', tot, reps, costs),
-        'kernels': per_kernel,
+        'loss': res['loss'],
+        'roofline': roofline_of(work, dom, tot, costs, probe),
+        'roofline_attention': roofline_of(work, 'mep_attn_bwd', tot, costs, probe),
+        'kernels': res['kernels'],
+        'kernels_sum_ms': res['kernels_sum_ms'],
+        'kernel_timing': res['kernel_timing'],
     }
+    if probe:
+        out['hbm_measured'] = probe
+    del work
+    torch.cuda.empty_cache()
+    if args.dtype == 'fp32' and cls.baseline_dtype == 'bf16' and not args.no_bf16:
+        # BASELINE.json names bf16 for this config: the bf16 path's line, same steps, same box
+        w2, r2, tot2, costs2, dom2 = run_config(cls, dev, rank, world, graph, True, args.steps, args.warmup)
+        r2['roofline'] = roofline_of(w2, dom2, tot2, costs2, probe)
+        r2['roofline_attention'] = roofline_of(w2, 'mep_attn_bwd', tot2, costs2, probe)
+        r2['dtype'] = 'bf16'
+        out['bf16'] = r2
+        del w2
+        torch.cuda.empty_cache()
     out['switches'] = {'read': {k: v['value'] for k, v in sorted(_lib.SWITCHES.items())},
                        'set_in_env': _lib.switches_from_env()}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -502,7 +649,7 @@ def main():
         aff, quota = host_cpus()
         threads = min(aff, quota) if quota else aff
         torch.set_num_threads(threads)
-        cb = CONFIGS[args.config].cpu_baseline(args.cpu_budget)
+        cb = cls.cpu_baseline(args.cpu_budget)
         cb.update(cores=torch.get_num_threads(), kind='port', cpu_model=cpu_model(), affinity_cpus=aff,
                   cgroup_cpus=quota)
         out['cpu_baseline'] = cb

@@ -92,7 +92,11 @@ int mep_gemm(const mep_gemm_desc* descs, int n_desc, int max_tiles, mep_stream_t
  * read from L2 and needs K % 16 == 0 and 16-byte aligned W and X rows.  `descs` holds the n_desc
  * descriptors FOLLOWED BY n_wg int32 task entries (descriptor << 20 | workgroups of that
  * descriptor << 10 | workgroup index), one per workgroup of the flat grid; a descriptor's
- * workgroups split its 16-token tiles into contiguous ranges. */
+ * workgroups split its 16-token tiles into contiguous ranges.
+ * bf16 rows (MEP_BF16_STORE) with 8-byte aligned rows are read 4 elements at a time: when
+ * K % 4 != 0 the row's elements K .. 4 ceil(K / 4) - 1 are read too and MUST be finite (they meet
+ * zero weight columns; 0 x inf is nan).  The plans zero-pad their bf16 feature rows to a
+ * multiple of 8 elements. */
 int mep_unify(const mep_gemm_desc* descs, int n_desc, int n_wg, mep_stream_t stream);
 
 /* Tiled token GEMM on the bf16 matrix cores, the mep_gemm contract for N % 16 == 0: a workgroup
@@ -599,6 +603,21 @@ typedef struct {
     int32_t  n_out, m_len, d, src_f64, summary, clean, n_seq, _pad;
 } mep_window_desc;
 int mep_assemble_windows(const mep_window_desc* descs, int n_desc, mep_stream_t stream);
+
+/* ---------------------------------------------------------------- measurement
+ * Not a reference interface: the measured HBM peak bench.py reports beside the 8 TB/s spec
+ * ("vendor spec and a measured copy-kernel peak on the box").  Streams n16 16-byte units with
+ * n_wg workgroups of 256 threads: mode 0 copies src -> dst (2 x 16 n16 bytes), mode 1 reads src
+ * (16 n16 bytes; one xor dword per thread written to dst, so dst holds n_wg * 256 dwords), mode 2
+ * zero-fills dst (16 n16 bytes).  Buffers 16-byte aligned. */
+int mep_hbm_probe(const void* src, void* dst, int64_t n16, int mode, int n_wg, mep_stream_t stream);
+
+/* Writes the device's 100-MHz real-time counter to slots[i] (uint64) when this one-wave kernel
+ * starts (measurement, not a reference interface): stamps placed between the launches of a
+ * captured step bracket each launch's device time (bench.py). */
+int mep_stamp(void* slots, int i, mep_stream_t stream);
+/* The counter's rate in kHz (hipDeviceAttributeWallClockRate of the current device), or < 0. */
+int mep_stamp_khz(void);
 
 /* ---------------------------------------------------------------- misc */
 int mep_abi_version(void);

@@ -276,6 +276,9 @@ SIGNATURES.update({
     'mep_rf_rows': [i32, i32],
     'mep_last_error': [ctypes.c_char_p, ctypes.c_size_t],
     'mep_device_sync': [],
+    'mep_hbm_probe': [P, P, i64, i32, i32, P],
+    'mep_stamp': [P, i32, P],
+    'mep_stamp_khz': [],
 })
 
 _LIB = None
@@ -316,18 +319,23 @@ def stream_ptr(stream=None):
     return ctypes.c_void_p(s.cuda_stream)
 
 
-# Optional per-launch timer (bench.py): an object with begin(name, stream) / end(name, stream) that
-# records HIP events on the launching stream.  None in normal operation.
+# Optional per-launch hook (bench.py, scripts/bench_aux.py), None in normal operation: an object
+# with begin(name, stream) / end(name, stream), called around every entry-point call (bench.py
+# places its mep_stamp kernels there).
 TIMER = None
+
+
+def _run(name, run, stream):
+    if TIMER is not None:
+        TIMER.begin(name, stream)
+    run()
+    if TIMER is not None:
+        TIMER.end(name, stream)
 
 
 def call(name, *args, stream=None):
     fn = getattr(lib(), name)
-    if TIMER is not None:
-        TIMER.begin(name, stream)
-    check(fn(*args, stream_ptr(stream)), name)
-    if TIMER is not None:
-        TIMER.end(name, stream)
+    _run(name, lambda: check(fn(*args, stream_ptr(stream)), name), stream)
 
 
 class DescArray:
@@ -357,15 +365,11 @@ def launch(name, descs, max_tiles, stream=None, threads=None, extra=()):
     if descs.n == 0 or max_tiles <= 0:
         return
     fn = getattr(lib(), name)
-    if TIMER is not None:
-        TIMER.begin(name, stream)
     if threads is None and name == 'mep_wgrad':
         threads = getattr(descs, 'prec', 0)   # make_wgrad's precision
     ints = ([] if threads is None else [int(threads)]) + [int(x) for x in extra]
-    rc = fn(descs.ptr, descs.n, int(max_tiles), *ints, stream_ptr(stream))
-    check(rc, name)
-    if TIMER is not None:
-        TIMER.end(name, stream)
+    ptr, n = descs.ptr, descs.n
+    _run(name, lambda: check(fn(ptr, n, int(max_tiles), *ints, stream_ptr(stream)), name), stream)
 
 
 ATTN_PREV, ATTN_SOUT, ATTN_SHORT, ATTN_LONG = 1, 2, 4, 8   # MEP_ATTN_* (include/mep.h)

@@ -9,6 +9,7 @@
 
 namespace {
 thread_local std::string g_last_error;
+
 }
 
 extern "C" void mep_set_error(const char* msg) { g_last_error = msg ? msg : ""; }
@@ -38,3 +39,4 @@ extern "C" int mep_device_sync(void) {
     g_last_error = std::string("hipDeviceSynchronize: ") + hipGetErrorString(e);
     return -(int)e;
 }
+

@@ -618,3 +618,4 @@ MEP_DEV void opt_step_scalars(float* partial, int* step, const float* hyper) {
 // error plumbing shared by the launchers (api.cpp)
 extern "C" void mep_set_error(const char* msg);
 int mep_check_launch(const char* what);
+

@@ -255,25 +255,31 @@ MEP_DEV void tgemm_dma(const mep_gemm_desc* __restrict__ descs) {
     typedef __attribute__((address_space(3))) void lvoid;
     typedef __attribute__((address_space(3))) const f32x4 lcf4;
 
-    // a lane's 16-byte unit goes by LDS-DMA when it is whole (row < N, k + 3 < K) and the weight rows
-    // are 16-byte aligned; otherwise (the K tail, rows past N, unaligned rows) the lane loads what
-    // exists, zero-fills the rest and writes the unit with a plain LDS store
+    // a lane's 16-byte unit goes by LDS-DMA when it is whole (k + 3 < K) and the weight rows are
+    // 16-byte aligned; otherwise (the K tail, unaligned rows) the lane loads what exists, zero-fills
+    // the rest and writes the unit with a plain LDS store (a plain load is waited for before its
+    // store, so that path is synchronous).  Rows past N take their DMA from row N - 1: every wave
+    // then issues exactly UPW DMA instructions per whole chunk, which the steady-state
+    // vmcnt(NEWER) below counts on (a wave skipping the DMA of its rows past N would let the wait
+    // pass with its chunk-kc DMA still in flight).  Rows past N only feed output columns >= N,
+    // which are never stored.
     const gfloat* W = G<const float>(d.w);
     const bool wdma = (d.ldw % 4 == 0) && ((d.w & 15) == 0);
     const auto rsW = __builtin_amdgcn_make_buffer_rsrc((void*)d.w, 0, (int)min((int64_t)4 * N * d.ldw, (int64_t)0x7fffffff), 0x00020000);
-    int wrow[UPW], wq[UPW];
+    int wrow[UPW], wq[UPW], wsrc[UPW];
 #pragma unroll
     for (int u = 0; u < UPW; ++u) {
         wrow[u] = n0 + 8 * (wave * UPW + u) + (lane >> 3);
         wq[u] = 4 * ((lane & 7) ^ (((wrow[u] - n0) >> 1) & 7));
+        wsrc[u] = min(wrow[u], N - 1);
     }
     auto issue_w = [&](int kc) {
         lbyte* dst = (lbyte*)sm + (kc % NS) * CHB + wave * UPW * 1024;
 #pragma unroll
         for (int u = 0; u < UPW; ++u) {
             const int k = 32 * kc + wq[u];
-            if (wdma && wrow[u] < N && k + 3 < K) {
-                __builtin_amdgcn_raw_ptr_buffer_load_lds(rsW, (lvoid*)(dst + u * 1024), 16, 4 * (wrow[u] * d.ldw + wq[u]),
+            if (wdma && k + 3 < K) {
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(rsW, (lvoid*)(dst + u * 1024), 16, 4 * (wsrc[u] * d.ldw + wq[u]),
                                                          128 * kc, 0, 0);
             } else {
                 f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};

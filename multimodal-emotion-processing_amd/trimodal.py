@@ -89,7 +89,7 @@ def _wgrad_units(items, bf16=False):
     return units
 
 
-# k_wgrad cost per workgroup ~ a * tokens + c (cfg3 / cfg5 bf16 fits, scripts/r4_gpu23.sh: a = 8.5 ns per
+# k_wgrad cost per workgroup ~ a * tokens + c (cfg3 / cfg5 bf16 fits, scripts/ab/r4_gpu23.sh: a = 8.5 ns per
 # token, c = 16 us of setup + partial write); in tokens, c / a:
 WG_SETUP_TOKENS = int(_lib.switch('MEP_WG_SETUP_TOKENS', '1900'))
 
@@ -726,12 +726,14 @@ class TriModalPlan:
     def set_row0(self, row0):
         """Global index of this batch's first row (data-parallel share): the dropout masks of
         local row b are the full batch's masks of row row0 + b.  The slot lives in the model's
-        seed_state (shared by its plans; only this method writes it), so the value last written
-        is kept on that tensor and an unchanged row0 costs no device fill per step."""
+        seed_state (shared by its plans), so the value last written is kept on that tensor with
+        the tensor's version counter: an unchanged row0 costs no device fill per step, and any
+        other in-place write of seed_state through torch (zero_, copy_ from a saved state, a test
+        poking it) bumps the version and forces the fill.  mep_seed_advance writes seed[0] only."""
         row0 = int(row0)
-        if getattr(self.seed_state, '_mep_row0', None) != row0:
+        if getattr(self.seed_state, '_mep_row0', None) != (row0, self.seed_state._version):
             self.row0.fill_(row0)
-            self.seed_state._mep_row0 = row0
+            self.seed_state._mep_row0 = (row0, self.seed_state._version)
 
     def set_dropout(self, p):
         """Dropout probability of the block epilogues (Ren-MME DROP at train time, 0 in eval).

@@ -61,6 +61,11 @@ def linear(x, w, b=None):
 # every call used (torch.max's first-index tie rule when not routed).
 POOL_ROUTE = None
 POOL_SEEN = []
+# with POOL_ROUTE: the largest accepted shortfall of a replayed step below the true max of its
+# column, relative to the column's max |x| over time (None: unchecked).  A routing taken from a
+# bf16 execution may pick another step only where the two are within bf16 noise (a near tie); a
+# wrong argmax lands far below the max.
+POOL_ROUTE_RTOL = None
 
 
 def mean_max_pool(x):
@@ -68,6 +73,14 @@ def mean_max_pool(x):
     if POOL_ROUTE:
         idx = POOL_ROUTE.pop(0).to(x.device).long()
         mx = x.gather(1, idx.unsqueeze(1)).squeeze(1)
+        if POOL_ROUTE_RTOL is not None:
+            with torch.no_grad():
+                gap = x.max(dim=1).values - mx
+                lim = POOL_ROUTE_RTOL * x.abs().amax(dim=1)
+                bad = gap > lim
+                assert not bool(bad.any()), ('routed max-pool: %d of %d replayed steps fall below the column max by '
+                                             'more than %.3g of its scale (worst gap %.3g)'
+                                             % (int(bad.sum()), bad.numel(), POOL_ROUTE_RTOL, float((gap - lim).max())))
     else:
         mx, idx = x.max(dim=1)
     POOL_SEEN.append(idx.detach().clone())

@@ -8,7 +8,7 @@ function; tests/golden/make_golden.py uses it to run the REFERENCE Base_model wi
 layers replaced by "multiply by this mask" -- exactly what nn.Dropout computes for a given mask
 (input * bernoulli / (1 - p)) -- so the fixture pins where the masks apply, their 1/(1-p) scale
 and the gradient routing through them, while the mask statistics are checked as properties
-(keep rate, scale) in tests/test_dropout.py.
+(keep rate, scale) in tests/test_gpu_ren.py (test_dropout_mask_statistics).
 
 Site numbering (trimodal.py _epi_desc, drop_stream = block index): block j of encoder e (0 =
 intensity, 1 = stimulation) with n_layers per chain has index (e * 9 + chain) * n_layers + layer =

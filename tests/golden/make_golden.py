@@ -108,10 +108,13 @@ class MaskDrop(nn.Module):
         return x * torch.from_numpy(odrop.block_mask(self.seed, self.block, site, B, T, D, self.p))
 
 
-def case_model(name, family, consts, ctor, batch, full, seed, opt, steps=1, drop=None):
+def case_model(name, family, consts, ctor, batch, full, seed, opt, steps=1, drop=None, noise64=False):
     """Whole-model train step(s) as the reference ``train`` performs them.  drop = (p, seed0):
     the blocks' dropout uses the masks of seed advance(seed0) (the engine advances the seed once
-    before a training forward)."""
+    before a training forward).  noise64: also run the reference's first step in float64 and store,
+    per gradient, how far its own fp32 result lies from that (noise/<param>: max |g32 - g64| over
+    the stored extent; noisenorm/<param>: the difference of the norms; noise/logits): the fp32
+    rounding noise of the reference on this input, the floor of any fp32 parity check of it."""
     ns = load_reference(family, consts)
     torch.manual_seed(0)
     if family == 'cmu':
@@ -146,6 +149,8 @@ def case_model(name, family, consts, ctor, batch, full, seed, opt, steps=1, drop
     else:
         optimizer = optim.Adam(model.parameters(), lr=1e-3)
     out = {}
+    if noise64:
+        out.update(fp64_noise(ns, family, model, args, labels, um if family == 'realformer' else None, full))
     for step in range(steps):
         optimizer.zero_grad()
         logits = model(*args)
@@ -178,6 +183,83 @@ def case_model(name, family, consts, ctor, batch, full, seed, opt, steps=1, drop
     if drop is not None:   # its own kind: the CPU oracle has no per-site masks
         meta.update(kind='model_drop', drop=dict(p=drop[0], seed0=drop[1], seed=odrop.seed_advance(drop[1])))
     return meta, out
+
+
+def _loss_of(ns, family, logits, labels, um):
+    if family == 'cmu':
+        return ns['multi_circle_loss'](logits, labels).mean()
+    if family == 'ren':
+        kl_0 = F.kl_div(F.logsigmoid(logits[::2]), torch.sigmoid(logits[1::2]), reduction='batchmean')
+        kl_1 = F.kl_div(F.logsigmoid(logits[1::2]), torch.sigmoid(logits[::2]), reduction='batchmean')
+        return ns['multi_loss'](logits, labels) + (kl_0 + kl_1) / 2
+    return (ns['multi_circle_loss'](logits, labels) * um).mean()
+
+
+def fp64_noise(ns, family, model, args, labels, um, full, runs=6):
+    """The fp32 rounding noise of this step's gradients on this input, as a budget for fp32 parity
+    checks of it (realformer only).  On deep, gated inputs such as State_Transfer's (2-layer
+    residual chains, ReLU FFNs, max-pools routing a column's gradient to one time step, a 6-step
+    gate recurrence) single fp32 gradient entries land up to percent-level of a tensor's max away
+    from the exact value, differently in every fp32 execution (a near tie resolved the other way).
+    Stored:
+      grad64/<param> (or grad64head/<param>): the reference's post-clip gradient in float64 from
+        the fixture's parameters -- what fp32 executions are compared against;
+      budget/<param>: the largest relative L2 error (over the stored extent) of a fp32 execution
+        against its own float64 run, over `runs` executions of the reference and `runs` of the
+        repo's CPU oracle (another fp32 summation order), each with the parameters scaled by
+        1 + 2^-18 N(0, 1) except the first reference run.
+    The caller's model is untouched."""
+    import copy
+    from oracle import realformer as orf
+    assert family == 'realformer'
+    gen = torch.Generator().manual_seed(20261018)
+
+    def ref_grads(base, dt):
+        m = copy.deepcopy(base).to(dt)
+        a = [x.to(dt) if x.is_floating_point() else x for x in args]
+        lab = labels.to(dt) if labels.is_floating_point() else labels
+        _loss_of(ns, family, m(*a), lab, um.to(dt)).backward()
+        nn.utils.clip_grad_norm_(m.parameters(), 1.0)
+        return {k: None if p.grad is None else p.grad.detach().double() for k, p in m.named_parameters()}
+
+    def oracle_grads(base, dt):
+        P = {k: v.detach().to(dt).clone().requires_grad_(True) for k, v in base.state_dict().items()}
+        l, v, a, lm, vm, am = [x.to(dt) for x in args]
+        out = orf.state_transfer(P, l, v, a, lm, vm, am, ctor_heads(base), ctor_layers(base))
+        orf.loss_fn(out, labels.to(dt) if labels.is_floating_point() else labels, um.to(dt)).backward()
+        torch.nn.utils.clip_grad_norm_([p for p in P.values() if p.grad is not None], 1.0)
+        return {k: None if p.grad is None else p.grad.detach().double() for k, p in P.items()}
+
+    def extent(g):
+        return g if full else g.reshape(-1)[:256]
+
+    out = {}
+    for r in range(runs):
+        base = copy.deepcopy(model)
+        if r:
+            with torch.no_grad():
+                for p in base.parameters():
+                    p.mul_(1 + 2.0 ** -18 * torch.randn(p.shape, generator=gen))
+        g64 = ref_grads(base, torch.float64)
+        if r == 0:
+            for k, g in g64.items():
+                if g is not None:
+                    out[('grad64/' if full else 'grad64head/') + k] = extent(g).numpy()
+        for g32 in (ref_grads(base, torch.float32), oracle_grads(base, torch.float32)):
+            for k, g in g32.items():
+                if g is None:
+                    continue
+                e = float((extent(g) - extent(g64[k])).norm() / max(float(extent(g64[k]).norm()), 1e-30))
+                out['budget/' + k] = np.float64(max(e, float(out.get('budget/' + k, 0.0))))
+    return out
+
+
+def ctor_heads(m):
+    return m.feature.multimodal_blocks[0].n_heads
+
+
+def ctor_layers(m):
+    return len(m.feature.multimodal_blocks) // 9
 
 
 def case_block(name, family, consts, ctor, B, Tq, Tk, seed, with_prev=True, g_scores=True):
@@ -310,6 +392,12 @@ CASES = {
                                          dict(l_dim=300, v_dim=35, a_dim=74, dim=32, l_len=6, v_len=6,
                                               a_len=6, n_heads=2, n_layers=2, ffn=2),
                                          dict(seed=16, B=3, P=3, T=6), True, 106, 'adam'),
+    # State_Transfer at the reference's own configuration (others/realformer.py:23-38: P_LEN 6
+    # utterances, DIM 96, N_HEADS 6, N_LAYERS 2, FFN 2, L/V/A_LEN 50), gate recurrence :266-286
+    'rf_state_ref': lambda: case_model('rf_state_ref', 'realformer', rf_consts(50),
+                                       dict(l_dim=300, v_dim=35, a_dim=74, dim=96, l_len=50, v_len=50,
+                                            a_len=50, n_heads=6, n_layers=2, ffn=2),
+                                       dict(seed=23, B=8, P=6, T=50), False, 117, 'adam', noise64=True),
     'block_cmu': lambda: case_block('block_cmu', 'cmu', CMU_C, dict(dim=32, n_heads=2, ffn=1),
                                     3, 7, 11, 107),
     'block_cmu_noprev': lambda: case_block('block_cmu_noprev', 'cmu', CMU_C, dict(dim=32, n_heads=2, ffn=1),

@@ -21,7 +21,8 @@ import pytest
 import torch
 
 from tests.golden import fixtures
-from tests.gpu_util import assert_close, check_post_params, load_params
+from tests.gpu_util import (assert_close, check_grad_budget, check_post_budget, check_post_params, has_fp32_budget,
+                            load_params)
 
 pytestmark = pytest.mark.gpu
 
@@ -100,9 +101,40 @@ def _batch(meta, cuda):
     return l, v, a, labels, lm, vm, am, um
 
 
-def test_state_transfer_autograd(cuda):
+STATE = ['rf_state_small', 'rf_state_ref']
+
+
+def _check_state_grads(model, meta, gold, coef):
+    """rf_state_small: every gradient at rtol 1e-3 (floor 1e-5 x max) against the reference.
+    rf_state_ref (the reference's own configuration, others/realformer.py:23-38): its fp32
+    gradients scatter around the exact values (near ties of the ReLU FFNs and max-pools over a
+    6-step gate recurrence: the reference's own fp32 run lies up to 0.6% relative L2 from float64
+    on some tensors), so each gradient is held against the reference in float64 to twice the
+    fp32 budget the fixture measured over 12 reference and oracle executions
+    (gpu_util.check_grad_budget), plus its norm within 1e-3 of the reference's."""
+    budget = has_fp32_budget(gold)
+    worst = 0.0
+    for k, p in model.named_parameters():
+        if 'nograd/' + k in gold:
+            assert p.grad is None, k
+            continue
+        g = p.grad * coef
+        if budget:
+            worst = max(worst, check_grad_budget(g, gold, k, meta['full']))
+            assert_close(torch.linalg.vector_norm(g.double()), gold['gradnorm/' + k], 1e-3, 0, k)
+        elif meta['full']:
+            assert_close(g, gold['grad/' + k], 1e-3, 1e-5, k)
+        else:
+            assert_close(g.reshape(-1)[:256], gold['gradhead/' + k], 1e-3, 1e-5, k)
+            assert_close(torch.linalg.vector_norm(g.double()), gold['gradnorm/' + k], 1e-3, 0, k)
+    if budget:
+        print('worst gradient error / allowance: %.3f' % worst)
+
+
+@pytest.mark.parametrize('name', STATE)
+def test_state_transfer_autograd(name, cuda):
     from mep_amd import realformer as rf
-    meta, gold = fixtures.load('rf_state_small')
+    meta, gold = fixtures.load(name)
     model = _state(meta, cuda)
     l, v, a, labels, lm, vm, am, um = _batch(meta, cuda)
     out = model(l, v, a, lm, vm, am)
@@ -110,19 +142,15 @@ def test_state_transfer_autograd(cuda):
     loss = (rf.multi_circle_loss(out, labels) * um).mean()
     assert_close(loss.reshape(()), gold['loss'], 1e-4, 0, 'loss')
     loss.backward()
-    coef = float(gold['clipcoef'])
-    for k, p in model.named_parameters():
-        if 'nograd/' + k in gold:
-            assert p.grad is None, k
-            continue
-        assert_close(p.grad * coef, gold['grad/' + k], 1e-3, 1e-5, k)
+    _check_state_grads(model, meta, gold, float(gold['clipcoef']))
 
 
 @pytest.mark.parametrize('graph', [False, True])
-def test_state_transfer_engine_step(graph, cuda):
+@pytest.mark.parametrize('name', STATE)
+def test_state_transfer_engine_step(name, graph, cuda):
     from mep_amd.engine import TrainEngine
     from mep_amd.optim import FusedAdam
-    meta, gold = fixtures.load('rf_state_small')
+    meta, gold = fixtures.load(name)
     model = _state(meta, cuda)
     opt = FusedAdam(model, lr=1e-3)
     eng = TrainEngine(model, opt, clip=1.0, graph=graph)
@@ -130,7 +158,10 @@ def test_state_transfer_engine_step(graph, cuda):
     loss = float(eng.step(*batch).item())
     assert_close(loss, gold['loss'], 1e-4, 0, 'loss')
     assert_close(opt.gnorm.reshape(()), gold['gnorm'], 1e-4, 0, 'gnorm')
-    check_post_params(model, meta, gold)
+    if has_fp32_budget(gold):
+        check_post_budget(model, meta, gold)
+    else:
+        check_post_params(model, meta, gold)
     l, v, a, labels, lm, vm, am, um = batch
     model.eval()
     with torch.no_grad():

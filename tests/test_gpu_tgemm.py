@@ -148,6 +148,8 @@ def _launch_flags(descs, dev, flags):
     (128, (768, 640, 35), 3, 7, True),       # ragged: 21 tokens; bias + position table + accumulate
     (96, (320, 64, 74), 5, 50, False),       # N tile 96 (6 column tiles)
     (256, (512,), 2, 130, True),             # two N tiles; 260 tokens (a partial last workgroup)
+    (144, (768, 205), 3, 40, False),         # N % 32 = 16: waves whose weight rows end inside / past N
+    (176, (640,), 2, 33, True),              # (every wave still issues its full DMA count per chunk)
 ])
 def test_tgemm_dma_matches_register_staging(N, Ks, B, T, extra, bf, cuda):
     """MEP_TGEMM_DMA (weight ring by LDS-DMA) against the register-staged kernel on the same
