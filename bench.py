@@ -71,14 +71,14 @@ class StampTimer:
         self._stamp(stream)
 
 
-def time_launches(work, reps=20):
+def time_launches(work, reps=41):
     """Device time of every libmep launch of a training step, where it runs in the step.
 
     The step body (forward, backward, clip + optimizer) is captured into a graph with a mep_stamp
     kernel before and after every launch (a one-wave kernel storing the 100-MHz real-time counter
     as it starts; graph kernels run back to back) and replayed `reps` times.  A launch's time is
     the interval between its two stamps minus the interval of two stamps with nothing between
-    them (measured in a graph of 64 such pairs): the launch's execution plus its dispatch, in
+    them (16 such pairs at the head of the same graph): the launch's execution plus its dispatch, in
     the step -- after the same producers, with the same cache contents -- which is what a
     rocprofv3 trace of a graph step reports per kernel (a kernel's start there is its
     predecessor's end).  HIP events cannot give this on ROCm: timing markers add ~3-5 us to every
@@ -110,30 +110,38 @@ def time_launches(work, reps=20):
         return g, timer
 
     def intervals(g, n):
-        acc = torch.zeros(n // 2, dtype=torch.float64)
+        """per stamp pair, the median over `reps` replays (robust to a replay caught by a clock or
+        queue hiccup)"""
+        for _ in range(3):
+            g.replay()
+        runs = []
         for _ in range(reps):
             g.replay()
             torch.cuda.synchronize()
             s = slots[:n].cpu().double().reshape(-1, 2)
-            acc += (s[:, 1] - s[:, 0]) * tick
-        return acc / reps
+            runs.append((s[:, 1] - s[:, 0]) * tick)
+        return torch.stack(runs).median(dim=0).values
 
-    def empty_pairs():
-        for _ in range(64):
-            _lib.TIMER.begin('empty')
-            _lib.TIMER.end('empty')
-    g0, t0 = capture(empty_pairs)
-    overhead = float(intervals(g0, t0.n).mean())
-    del g0
-    g, timer = capture(work.step_body)
-    per = intervals(g, timer.n) - overhead
+    def body():
+        # calibration pairs first, in the same graph: two adjacent stamps under the step's own
+        # clocks and queue state
+        for _ in range(CAL):
+            _lib.TIMER.begin('stamp pair')
+            _lib.TIMER.end('stamp pair')
+        work.step_body()
+    CAL = 16
+    g, timer = capture(body)
+    iv = intervals(g, timer.n)
+    overhead = float(iv[:CAL].mean())
+    per = iv[CAL:] - overhead
+    timer.names = timer.names[CAL:]
     del g
     tot = {}
     for name, t in zip(timer.names, per.tolist()):
         s0, c = tot.get(name, (0.0, 0))
         tot[name] = (s0 + t, c + 1)
-    method = ('in-step: real-time-counter stamps around each launch of a captured step, %d replays, minus '
-              'the %.2f-us interval of two adjacent stamps' % (reps, overhead * 1e6))
+    method = ('in-step: real-time-counter stamps around each launch of a captured step, median of %d replays, '
+              'minus the %.2f-us interval of two adjacent stamps' % (reps, overhead * 1e6))
     return tot, method
 
 
@@ -480,6 +488,79 @@ class Cfg2:
                     sample='%d steps of B=64,T=50 realformer text chain fwd+bwd+Adam (oracle, fp32 CPU)' % n)
 
 
+class RfState:
+    """realformer State_Transfer training step at the reference's own configuration
+    (others/realformer.py:23-38: BATCH 64, P_LEN 6 utterances, L/V/A_LEN 50, DIM 96, N_HEADS 6,
+    N_LAYERS 2, FFN 2): the shared Multi_class encoder over all B x P utterances, the
+    State_Transfer head with its gate recurrence over the 6 utterances (:266-286), the masked
+    circle loss (:311-312), clip_grad_norm_(1.0) and Adam (lr 1e-3, no weight decay; :342).  One
+    row = one sequence of 6 utterances.  Synthetic N(0,1) features, all-ones frame and utterance
+    masks, Bernoulli(0.3) labels.  fp32 (the reference has no AMP)."""
+    name = 'rfstate'
+    metric = 'sequences/sec fwd+bwd, realformer State_Transfer B=64 P=6 T=50 (d=300/35/74)'
+    unit = 'seq/s'
+    baseline_dtype = 'fp32'
+    P = 6
+
+    def __init__(self, dev, rank, graph, bf16=False):
+        from mep_amd import realformer as rf
+        from mep_amd.engine import TrainEngine
+        from mep_amd.optim import FusedAdam
+        assert not bf16, 'rfstate is an fp32 workload (the reference has no AMP)'
+        self.bf16 = False
+        torch.manual_seed(0)
+        self.model = rf.State_Transfer(l_dim=300, v_dim=35, a_dim=74, dim=96, l_len=T, v_len=T, a_len=T, n_heads=6,
+                                       n_layers=2, ffn=2).to(dev).train()
+        self.opt = FusedAdam(self.model, lr=1e-3)
+        self.eng = TrainEngine(self.model, self.opt, clip=1.0, graph=graph)
+        self.eng_eager = TrainEngine(self.model, self.opt, clip=1.0, graph=False)
+        rng = np.random.default_rng(20261015 + rank)
+        f = lambda d: torch.from_numpy(rng.standard_normal((B, self.P, T, d), dtype=np.float32)).to(dev)  # noqa: E731
+        l, v, a = (f(d) for d in DIMS)
+        m = torch.ones(B, self.P, T, device=dev)
+        labels = torch.from_numpy((rng.random((B, self.P, 6)) < 0.3).astype(np.int64)).to(dev)
+        um = torch.ones(B, self.P, dtype=torch.int64, device=dev)
+        self.plan = self.model.mep_runner(dev).stage(l, v, a, labels, m, m.clone(), m.clone(), um)
+        self.rows = B
+
+    def step(self):
+        self.eng.step_plan(self.plan)
+
+    def eager_step(self):
+        self.eng_eager.step_plan(self.plan)
+
+    def step_body(self):
+        self.eng._fwd_bwd_allreduce(self.plan, self.eng._runner(self.plan.device))
+        self.eng._opt()
+
+    def loss(self):
+        return float(self.plan.loss.item())
+
+    def config(self, world, graph):
+        return {'workload': 'realformer State_Transfer train step (fwd+bwd+clip+Adam), reference configuration',
+                'global_batch': B * world, 'per_gpu_batch': B, 'utterances_per_row': self.P, 'seq_len': T,
+                'dims': list(DIMS), 'D': 96, 'heads': 6, 'n_layers': 2, 'ffn': 2, 'parallelism': 'dp%d' % world,
+                'graph': graph}
+
+    @classmethod
+    def cpu_baseline(cls, budget_s):
+        """The CPU oracle's State_Transfer step (fp32 CPU, Adam) on the same shape."""
+        from oracle import common
+        from oracle import realformer as orf
+        from tests.golden import specs
+        from mep_amd import realformer as rf
+        m = rf.State_Transfer(l_dim=300, v_dim=35, a_dim=74, dim=96, l_len=T, v_len=T, a_len=T, n_heads=6,
+                              n_layers=2, ffn=2)
+        shapes = {k: list(v.shape) for k, v in m.state_dict().items()}
+        P = {k: torch.tensor(v, requires_grad=True) for k, v in specs.param_values(shapes, 1).items()}
+        opt = common.AdamState(P.values(), lr=1e-3, weight_decay=0.0, decoupled=False)
+        batch = [torch.from_numpy(x) for x in specs.realformer_batch(seed=5, B=B, P=cls.P, T=T)]
+        n, el = timed_cpu(lambda: orf.train_step(P, opt, batch, 6, 2), budget_s, max_steps=50)
+        return dict(value=round(B * n / el, 3), unit='seq/s', n=n, rows=B,
+                    sample='%d steps of B=64 sequences x 6 utterances, T=50, State_Transfer fwd+bwd+clip+Adam '
+                           '(oracle, fp32 CPU)' % n)
+
+
 class _FlatAdam:
     """Adam (weight decay 0, no clip: others/realformer.py:342) over a runner's flat buffer with the
     fused clip+Adam kernel (mep_clip_adam), graph-capturable."""
@@ -515,7 +596,7 @@ class _FlatAdam:
                        P(self.hyper.data_ptr()), P(self.step_t.data_ptr()), 0, self.n_ext)
 
 
-CONFIGS = {'cfg3': Cfg3, 'cfg5': Cfg5, 'cfg2': Cfg2}
+CONFIGS = {'cfg3': Cfg3, 'cfg5': Cfg5, 'cfg2': Cfg2, 'rfstate': RfState}
 
 
 def roofline_of(work, name, tot, costs, probe=None):

@@ -730,6 +730,171 @@ MEP_DEV void epi_fwd_one(const mep_epi_desc& d, unsigned char* sm, int t_begin, 
     }
 }
 
+// Single-phase fp32 forward at D = 96 with all six products of the 3-part split on both products
+// (fp32-level, like the two-phase kernel).  LDS (unpadded, swizzled SplitWS layouts) holds the
+// 3-part Wm (108 KB), Wp's first two parts (36 KB) and Wp's third part for rows 0 .. 16 (NI - 1)
+// - 1 (15 KB: 159 KB in all); the third part of the last 16 rows -- used only in the product
+// w2 x0 -- is held in registers (each wave splits its NP fragments of the fp32 Wp once, 4 NP
+// VGPRs).  Per tile: x (loaded a tile ahead) -> xp = Wp x, stored; the tile's q rows are loaded
+// at its start, behind the xp product; z = Wm [q | xp] with xp from the accumulators; LayerNorm.
+// Against the two-phase kernel the xp rows are not re-read, the weights are staged once, and no
+// phase barrier splits the workgroup's tiles.
+template <int D>
+struct EpiWp2r {
+    static constexpr int NI = D / 16, NP = D / 32, R2 = D - 16;
+    using WP01 = SplitWS<D, NP, 2>;
+    using WP2 = SplitWS<R2, NP, 1>;
+    using WM = SplitWS<D, 2 * NP, 3>;
+    static constexpr int BYTES = WP01::BYTES + WP2::BYTES + WM::BYTES;
+};
+
+template <int D>
+MEP_DEV void epi_fwd_wp2r(const mep_epi_desc& d, unsigned char* sm, int t_begin, int t_end) {
+    using E = EpiWp2r<D>;
+    constexpr int NI = E::NI, KB = D / 16, NP = E::NP, R2 = E::R2;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int c = lane & 15, g = lane >> 4;
+    const int ntok = d.ntok;
+    gfloat* stats = G<float>(d.stats);
+    typedef __attribute__((address_space(3))) unsigned char lbyte;
+    const typename E::WP01 wp{(lbyte*)sm, 0};
+    const typename E::WP2 wp2{(lbyte*)sm + E::WP01::BYTES, 0};
+    const typename E::WM wm{(lbyte*)sm + E::WP01::BYTES + E::WP2::BYTES, 0};
+    auto rows_of = [&](const mep_rows& v, int tile, f32x4 (&dst)[KB]) {
+        const gfloat* r = row_ptr(v, min(tile * 16 + c, ntok - 1)) + 4 * g;
+#pragma unroll
+        for (int kb = 0; kb < KB; ++kb) dst[kb] = ld4w(r + 16 * kb);
+    };
+    f32x4 ab[KB];                    // x rows, one tile ahead
+    if (t_begin + wave < t_end) rows_of(d.x, t_begin + wave, ab);
+    const gfloat* W = G<const float>(d.wp);
+    // the third part of the last 16 rows' fragments: unit (row R2 + c, k pair pp, group g)
+    bf16x8 w2r[NP];
+#pragma unroll
+    for (int pp = 0; pp < NP; ++pp) {
+        const gfloat* r = W + (R2 + c) * D + 32 * pp + 4 * g;
+        w2r[pp] = opn<3>(ld4w(r), ld4w(r + 16)).p[2];
+    }
+    {   // Wp: unit (n, pp, g) = Wp[n][32 pp + 4 g ..], [.. + 16 ..] -> parts 0, 1 (and 2 for n < R2)
+        constexpr int NU = D * NP * 4, PER = (NU + ETHREADS - 1) / ETHREADS;
+        f32x4 v[PER][2];
+#pragma unroll
+        for (int k = 0; k < PER; ++k) {
+            const int u = threadIdx.x + ETHREADS * k;
+            if (u < NU) {
+                const int gg = u & 3, pp = (u >> 2) % NP, n = (u >> 2) / NP;
+                v[k][0] = ld4w(W + n * D + 32 * pp + 4 * gg);
+                v[k][1] = ld4w(W + n * D + 32 * pp + 16 + 4 * gg);
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < PER; ++k) {
+            const int u = threadIdx.x + ETHREADS * k;
+            if (u < NU) {
+                const int gg = u & 3, pp = (u >> 2) % NP, n = (u >> 2) / NP;
+                const Parts<3> lo = splitv<3>(v[k][0]), hi = splitv<3>(v[k][1]);
+                wp.put_part(0, n, pp, gg, lo.p[0], hi.p[0]);
+                wp.put_part(1, n, pp, gg, lo.p[1], hi.p[1]);
+                if (n < R2) wp2.put_part(0, n, pp, gg, lo.p[2], hi.p[2]);
+            }
+        }
+    }
+    {   // Wm [D][2D]: unit (n, pp, g), all three parts
+        constexpr int NU = D * 2 * NP * 4, PER = (NU + ETHREADS - 1) / ETHREADS;
+        const gfloat* M = G<const float>(d.wm);
+        f32x4 v[PER][2];
+#pragma unroll
+        for (int k = 0; k < PER; ++k) {
+            const int u = threadIdx.x + ETHREADS * k;
+            if (u < NU) {
+                const int gg = u & 3, pp = (u >> 2) % (2 * NP), n = (u >> 2) / (2 * NP);
+                v[k][0] = ld4w(M + n * 2 * D + 32 * pp + 4 * gg);
+                v[k][1] = ld4w(M + n * 2 * D + 32 * pp + 16 + 4 * gg);
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < PER; ++k) {
+            const int u = threadIdx.x + ETHREADS * k;
+            if (u < NU) {
+                const int gg = u & 3, pp = (u >> 2) % (2 * NP), n = (u >> 2) / (2 * NP);
+                const Parts<3> lo = splitv<3>(v[k][0]), hi = splitv<3>(v[k][1]);
+#pragma unroll
+                for (int t = 0; t < 3; ++t) wm.put_part(t, n, pp, gg, lo.p[t], hi.p[t]);
+            }
+        }
+    }
+    __syncthreads();
+    for (int tile = t_begin + wave; tile < t_end; tile += EWAVES) {
+        const int tok = tile * 16 + c;
+        f32x4 bb[KB];                // q rows of this tile, loaded behind the xp product
+        rows_of(d.q, tile, bb);
+        f32x4 xp[NI];
+#pragma unroll
+        for (int i = 0; i < NI; ++i) xp[i] = zero_f4();
+        // the six products in mma_nm<3, 3>'s order: w0x0, w1x0, w0x1, w1x1, w2x0, w0x2; operands
+        // are split one k pair at a time
+#pragma unroll
+        for (int pp = 0; pp < NP; ++pp) {
+            const OpN<3> xs = opn<3>(ab[2 * pp], ab[2 * pp + 1]);
+#pragma unroll
+            for (int i = 0; i < NI; ++i) {
+                const OpN<2> a = wp.frag(i, pp);
+                const bf16x8 a2 = i < NI - 1 ? wp2.frag(i, pp).p[0] : w2r[pp];
+                f32x4 acc = xp[i];
+                acc = mfma_bf16(a.p[0], xs.p[0], acc);
+                acc = mfma_bf16(a.p[1], xs.p[0], acc);
+                acc = mfma_bf16(a.p[0], xs.p[1], acc);
+                acc = mfma_bf16(a.p[1], xs.p[1], acc);
+                acc = mfma_bf16(a2, xs.p[0], acc);
+                xp[i] = mfma_bf16(a.p[0], xs.p[2], acc);
+                if (i % MEP_TG_GROUP == MEP_TG_GROUP - 1) __builtin_amdgcn_sched_barrier(0);
+            }
+        }
+        if (tile + EWAVES < t_end) rows_of(d.x, tile + EWAVES, ab);   // behind the z product
+        if (tok < ntok) {
+            gfloat* pr = row_ptr(d.xp, tok);
+#pragma unroll
+            for (int i = 0; i < NI; ++i) stg4(pr + 16 * i + 4 * g, f4(xp[i]));
+        }
+        f32x4 z[NI];
+#pragma unroll
+        for (int i = 0; i < NI; ++i) z[i] = zero_f4();
+        tgemm_n<NI, NP, 3, 3>(z, [&](int i, int pp) { return wm.frag(i, pp); },
+                              [&](int pp) { return opn<3>(bb[2 * pp], bb[2 * pp + 1]); });
+        tgemm_n<NI, NP, 3, 3>(z, [&](int i, int pp) { return wm.frag(i, NP + pp); },
+                              [&](int pp) { return opn<3>(xp[2 * pp], xp[2 * pp + 1]); });
+        float sum = 0.f;
+#pragma unroll
+        for (int i = 0; i < NI; ++i) sum += (z[i][0] + z[i][1]) + (z[i][2] + z[i][3]);
+        sum += __shfl_xor(sum, 16, 64);
+        sum += __shfl_xor(sum, 32, 64);
+        const float mean = sum / (float)D;
+        float var = 0.f;
+#pragma unroll
+        for (int i = 0; i < NI; ++i)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) { const float t = z[i][r] - mean; var += t * t; }
+        var += __shfl_xor(var, 16, 64);
+        var += __shfl_xor(var, 32, 64);
+        const float rstd = 1.0f / sqrtf(var / (float)D + LN_EPS);
+        if (tok < ntok) {
+            gfloat* zr = row_ptr(d.z, tok);
+            gfloat* orow = row_ptr(d.out, tok);
+#pragma unroll
+            for (int i = 0; i < NI; ++i) {
+                const int col = 16 * i + 4 * g;
+                const f32x4 w = ld4w(G<const float>(d.ln_w) + col), b = ld4w(G<const float>(d.ln_b) + col);
+                f32x4 y;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) y[r] = (z[i][r] - mean) * rstd * w[r] + b[r];
+                stg4(zr + col, f4(z[i]));
+                stg4(orow + col, f4(y));
+            }
+            if (g == 0) { stats[2 * tok] = mean; stats[2 * tok + 1] = rstd; }
+        }
+    }
+}
+
 template <int D, int NPART, int NWP, int NWM, bool DROP>
 MEP_DEV void epi_bwd_one(const mep_epi_bwd_desc& bd, unsigned char* sm, int t_begin, int t_end) {
     constexpr int NI = D / 16, KB = D / 16, NP = D / 32;
@@ -875,20 +1040,25 @@ MEP_DEV void epi_bwd_one(const mep_epi_bwd_desc& bd, unsigned char* sm, int t_be
     }
 }
 
+#ifndef MEP_EPI_FWD_WP2R
+#define MEP_EPI_FWD_WP2R 1  // single-phase fp32 forward at D = 96, all six products (epi_fwd_wp2r)
+#endif
 // parts per weight of the single-phase epilogues (0: the two-phase kernels)
 template <int D, bool BF16> struct EpiOne {
     // fp32 path: off by default (the 2-part weight at D = 96 moved one cmu_cfg3 logit 5e-4 relative
     // and flipped a near-zero Adam update on ren_small); bf16 path: one part per weight, on
     static constexpr bool ON_BF = BF16 && MEP_EPI_ONE_BF16 && D <= MEP_EPI_ONE_BF16_MAXD;
-    static constexpr bool FWD = (MEP_EPI_ONE_FWD && D <= 96) || ON_BF, BWD = (MEP_EPI_ONE_BWD && D <= 96) || ON_BF;
+    static constexpr bool FWD = (MEP_EPI_ONE_FWD && D <= 96) || ON_BF || (!BF16 && D == 96 && MEP_EPI_FWD_WP2R),
+                          BWD = (MEP_EPI_ONE_BWD && D <= 96) || ON_BF;
     static constexpr int NPART = BF16 ? 1 : 3;
 #ifndef MEP_EPI_FWD_WM2
 #define MEP_EPI_FWD_WM2 0   // single-phase fp32 forward at D = 96: 1 = 3-part Wp + 2-part Wm (144 KB)
 #endif
+    static constexpr bool FWD_WP2R = !BF16 && D == 96 && MEP_EPI_FWD_WP2R && !MEP_EPI_FWD_WM2;
     static constexpr int FWD_WP = BF16 ? 1 : (D == 96 && !MEP_EPI_FWD_WM2 ? 2 : 3);
     static constexpr int FWD_WM = BF16 ? 1 : (D == 96 && MEP_EPI_FWD_WM2 ? 2 : NPART);
     static constexpr int BWD_WP = NPART, BWD_WM = BF16 ? 1 : (D == 96 ? 2 : 3);
-    static constexpr int FWD_BYTES = SplitW<D, D / 32, FWD_WP>::BYTES + SplitW<D, D / 16, FWD_WM>::BYTES;
+    static constexpr int FWD_BYTES = FWD_WP2R ? EpiWp2r<D>::BYTES : SplitW<D, D / 32, FWD_WP>::BYTES + SplitW<D, D / 16, FWD_WM>::BYTES;
     static constexpr int BWD_BYTES = SplitW<2 * D, D / 32, BWD_WM>::BYTES + SplitW<D, D / 32, BWD_WP>::BYTES;
     static_assert((!FWD || FWD_BYTES <= 163840) && (!BWD || BWD_BYTES <= 163840), "single-phase weights exceed the LDS");
 };
@@ -904,8 +1074,14 @@ __global__ __launch_bounds__(ETHREADS) __attribute__((amdgpu_waves_per_eu(MEP_EP
     if constexpr (EpiOne<D, BF16>::FWD) {
         using E = EpiOne<D, BF16>;
         __shared__ __attribute__((aligned(16))) unsigned char sm1[E::FWD_BYTES];
-        if (d.drop_p > 0.f) epi_fwd_one<D, E::NPART, E::FWD_WP, E::FWD_WM, true>(d, sm1, t_begin, t_end);
-        else epi_fwd_one<D, E::NPART, E::FWD_WP, E::FWD_WM, false>(d, sm1, t_begin, t_end);
+        if constexpr (E::FWD_WP2R) {
+            // dropout (Ren-MME; no D = 96 configuration runs it): the two-phase kernel
+            if (d.drop_p > 0.f) epi_fwd_split<D, 3, 3, true>(d, sm1, t_begin, t_end);
+            else epi_fwd_wp2r<D>(d, sm1, t_begin, t_end);
+        } else {
+            if (d.drop_p > 0.f) epi_fwd_one<D, E::NPART, E::FWD_WP, E::FWD_WM, true>(d, sm1, t_begin, t_end);
+            else epi_fwd_one<D, E::NPART, E::FWD_WP, E::FWD_WM, false>(d, sm1, t_begin, t_end);
+        }
         return;
     }
     if constexpr (BF16 || (MEP_EPI_SPLIT && D <= 96) || (MEP_EPI_SPLIT128_FWD && D == 128)) {

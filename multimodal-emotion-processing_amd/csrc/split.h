@@ -126,6 +126,41 @@ struct SplitW {
     }
 };
 
+// The same operand without row padding (RS = 64 NP bytes): unit u of row n is stored at unit
+// position u ^ ((n / M) & (16 / M - 1)) of its row, where M is the period (in rows) of the row
+// stride's bank offset (16-byte bank groups: 4 NP n mod 16).  The 16 lanes of a fragment read --
+// rows c = 0..15 of a tile, one logical unit -- then hit 16 distinct bank groups, the 64 banks
+// once, as with the padded layout (D = 96: 15 KB of padding less for the 3-part Wp + Wm pair).
+// The XOR stays inside aligned groups of 16 / M units, and a row holds 4 NP units, a multiple of
+// 16 / M for every NP.
+template <int R, int NP, int NPART = 3>
+struct SplitWS {
+    static constexpr int RS = 64 * NP;
+    static constexpr int BYTES = NPART * R * RS;
+    static constexpr int GB = (4 * NP) % 16 == 0 ? 16 : ((4 * NP) % 8 == 0 ? 8 : 4);   // gcd(16, 4 NP)
+    static constexpr int M = 16 / GB, XM = 16 / M - 1;
+    static_assert((4 * NP) % (XM + 1) == 0, "SplitWS: the swizzle group must divide a row");
+    __attribute__((address_space(3))) unsigned char* base;
+    int row0;
+    MEP_DEV static int unit(int n, int u) { return u ^ ((n / M) & XM); }
+    MEP_DEV OpN<NPART> frag(int i, int p) const {
+        const int lane = threadIdx.x & 63;
+        const int n = row0 + 16 * i + (lane & 15);
+        const int off = n * RS + unit(n, 4 * p + (lane >> 4)) * 16;
+        typedef __attribute__((address_space(3))) u32x4 lu32x4;
+        OpN<NPART> o;
+#pragma unroll
+        for (int t = 0; t < NPART; ++t)
+            o.p[t] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const lu32x4*>(base + t * R * RS + off));
+        return o;
+    }
+    // part t of unit (n, p, g) from its two words per k block
+    MEP_DEV void put_part(int t, int n, int p, int g, u32x2 lo, u32x2 hi) const {
+        typedef __attribute__((address_space(3))) u32x4 lu32x4;
+        *reinterpret_cast<lu32x4*>(base + t * R * RS + n * RS + unit(n, 4 * p + g) * 16) = u32x4{lo[0], lo[1], hi[0], hi[1]};
+    }
+};
+
 // acc[i] (i < NI) += A_i B over NP k pairs: afr(i, p) -> OpN (A fragment of output tile i),
 // bfr(p) -> OpN (B fragment, shared by the NI tiles).
 #ifndef MEP_TG_GROUP

@@ -54,7 +54,7 @@ def compute_peak(name, D=None, bf16=False):
 def launch_costs(plan):
     """{launch name: (flops, bytes)} for one eager training step of the plan (summed over the
     layers when a launch repeats)."""
-    if not hasattr(plan, 'ntok') or not hasattr(plan, 'Xcat'):
+    if hasattr(plan, 'rfw') or not hasattr(plan, 'Xcat'):      # RealformerPlan (chain or State_Transfer)
         return rf_launch_costs(plan)
     sp, B = plan.spec, plan.B
     D, H = sp.D, sp.H

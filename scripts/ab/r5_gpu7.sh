@@ -11,3 +11,7 @@ timeout -k 10 300 python3 bench.py > gpurun_out/r5_bench7.log 2>&1; rc=$?; echo 
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/r5_prof7 -o run --output-format csv -- python3 bench.py --no-cpu-baseline > gpurun_out/r5_bench7_prof.log 2>&1; rc=$?; echo "prof rc=$rc"
 python3 scripts/cmp_prof.py gpurun_out/r5_bench7_prof.log gpurun_out/r5_prof7
 echo ALLDONE
+timeout -k 10 300 python3 bench.py --config rfstate > gpurun_out/r5_bench7_rfstate.log 2>&1; rc=$?; echo "rfstate bench rc=$rc"; tail -c 800 gpurun_out/r5_bench7_rfstate.log
+[ $rc -eq 0 ] || exit $rc
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/r5_prof7_rfstate -o run --output-format csv -- python3 bench.py --config rfstate --no-cpu-baseline > gpurun_out/r5_bench7_rfstate_prof.log 2>&1; rc=$?; echo "rfstate prof rc=$rc"
+echo ALLDONE2
