@@ -428,10 +428,10 @@ def attn_geometry(descs):
     for d in descs:
         ft = max(ft, -(-(d.B * d.H * -(-d.Tq // 64)) // 4))
         bt = max(bt, d.B * d.H)
-    # backward x extent a multiple of 16: the Tk > 64 kernels then put heads 2j, 2j + 1 of a row
-    # on one XCD (csrc/attn.hip head_pair_order); the extra workgroups leave at once
+    # backward x extent a multiple of 32: the Tk > 64 kernels then put heads 4j .. 4j + 3 (or 2j,
+    # 2j + 1) of a row on one XCD (csrc/attn.hip head_pair_order); the extra workgroups leave at once
     if any(d.Tk > 64 for d in descs):
-        bt = -(-bt // 16) * 16
+        bt = -(-bt // 32) * 32          # a multiple of 32 for head quads (H % 4 == 0)
     flags = (ATTN_PREV if _uniform([d.s_prev != 0 for d in descs], 's_prev') else 0) | \
             (ATTN_SOUT if _uniform([d.s_out != 0 for d in descs], 's_out') else 0) | \
             (ATTN_SHORT if any(d.Tk <= 64 for d in descs) else 0) | (ATTN_LONG if any(d.Tk > 64 for d in descs) else 0)

@@ -92,6 +92,9 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 #ifndef MEP_ATTN_HEADPAIR
 #define MEP_ATTN_HEADPAIR 1    // Tk > 64 kernels: heads 2j, 2j + 1 of a row on one CU / XCD (64-byte head slices of 128-byte lines)
 #endif
+#ifndef MEP_ATTN_HEADQUAD
+#define MEP_ATTN_HEADQUAD 1    // ... heads 4j .. 4j + 3 when H % 4 == 0 (bf16 rows: 32-byte head slices, four to a 128-byte line)
+#endif
 #ifndef MEP_FWD_CHUNK_PF
 #define MEP_FWD_CHUNK_PF 0    // bf16 long forward: the next key chunk's loads issued before this chunk's tiles
 #endif
@@ -204,6 +207,11 @@ MEP_DEV floatx4 dot_score(const S3& p, const S3& u, floatx4 acc) {
 #endif
 #ifndef MEP_BWD_TR
 #define MEP_BWD_TR 0     // dS transposed as packed [key][query] words + ds_read_b64_tr_b16 (47.6-48.5 vs 45.6 us: off)
+#endif
+#ifndef MEP_BWD_TPAIR
+#define MEP_BWD_TPAIR 0  // dS transpose as key-pair words after a lane-pair swap (conflict-free ds_write_b32): its
+                         // DPP / select / perm VALU costs more than the conflicts (cfg3 fp32 38.3 -> 40.8 us,
+                         // cfg5 fp32 548 -> 574 us, bf16 within noise): off
 #endif
 #ifndef MEP_BWD_DELTA_MF
 #define MEP_BWD_DELTA_MF 0   // fp32 backward: delta = rowsum(dO O) on the matrix core (2-part splits).
@@ -762,6 +770,15 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu((SINGLE
     const int nqc = (d.Tq + QCH - 1) / QCH;   // QCH: queries per wave task (64, or 16 with MEP_ATTN_SPLITQ)
     const int task = blockIdx.x * WAVES + wave;
     if (task >= d.B * d.H * nqc) return;   // whole wave leaves; no barriers below
+    if (!SINGLE && MEP_ATTN_HEADQUAD && !(d.H & 3)) {
+        // Tk > 64, H % 4 == 0: the workgroup's 4 waves take the same queries of heads 4j .. 4j + 3
+        // of one row -- the 128-byte line of a bf16 K / V / Q row that each reads a quarter of is
+        // fetched once for all four, into the CU they share
+        const int m = task & 3, r = task >> 2;
+        const int qc = r % nqc, bhq = r / nqc, hq = d.H >> 2;
+        attn_fwd_task<PREV, SOUT, SINGLE, BF, HDIM, QCH>(d, qc, 4 * (bhq % hq) + m, bhq / hq, lane);
+        return;
+    }
     if (!SINGLE && MEP_ATTN_HEADPAIR && !(d.H & 1)) {
         // Tk > 64: waves 2i and 2i + 1 of a workgroup take the same queries of heads 2j and 2j + 1
         // of one row, so the 128-byte line of K / V / Q rows each needs half of is fetched once
@@ -1127,6 +1144,25 @@ struct Bwd {
                 Ih[e] = u32x2{ds2.h0, ds2.h1};
                 if (!BF) Ih[CH * 4 + e] = u32x2{ds2.l0, ds2.l1};
             }
+#elif MEP_BWD_TPAIR
+            // the split dS into Th / Tl[query][key] as 32-bit words of key pairs: lanes c and c ^ 1
+            // trade half their queries (one DPP swap per part), then lane c (even) writes queries
+            // 4g, 4g+1 and lane c+1 queries 4g+2, 4g+3 of keys (c, c+1) -- two ds_write_b32 per part
+            // instead of four ds_write_b16, every lane on its own bank (TLD2 / 2 = 36 dwords)
+            {
+                const bool odd = c & 1;
+                typedef __attribute__((address_space(3))) unsigned lu32;
+                const int rw = (4 * g + (odd ? 2 : 0)) * TLD2 + kt * 16 + (c & ~1);
+                auto put = [&](lushort* T, unsigned w01, unsigned w23) {
+                    const unsigned mine = odd ? w23 : w01;
+                    const unsigned other = (unsigned)__builtin_amdgcn_update_dpp(0, (int)(odd ? w01 : w23), 0xB1, 0xF, 0xF, true);
+                    const unsigned lo = odd ? other : mine, hi = odd ? mine : other;   // key c & ~1 / (c & ~1) + 1
+                    *(lu32*)(T + rw) = __builtin_amdgcn_perm(hi, lo, 0x05040100u);          // query row rw: low halves
+                    *(lu32*)(T + rw + TLD2) = __builtin_amdgcn_perm(hi, lo, 0x07060302u);   // next query: high halves
+                };
+                put(Th, ds2.h0, ds2.h1);
+                if (!BF) put(Tl, ds2.l0, ds2.l1);
+            }
 #else
             // the split dS, element by element, into Th / Tl[query][key] (bf16)
             const unsigned hw[4] = {ds2.h0, ds2.h0 >> 16, ds2.h1, ds2.h1 >> 16};
@@ -1414,6 +1450,12 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(2))) vo
 // the x extent (gridDim.x) a multiple of 16 -- the linear workgroup id is x + gridDim.x * y, so
 // its XCD is x mod 8 -- and H even; otherwise the plain order.  A bijection of [0, gridDim.x).
 MEP_DEV int head_pair_order(int P, int H) {
+    if (MEP_ATTN_HEADQUAD && !(gridDim.x & 31) && !(H & 3)) {
+        // heads 4j .. 4j + 3 of a row on one XCD, dispatched one after another (its L2 fetches a
+        // 128-byte line of bf16 rows once for the four 32-byte head slices)
+        const int x = P & 7, j = P >> 3;
+        return ((((j >> 2) << 3) + x) << 2) + (j & 3);
+    }
     if (!MEP_ATTN_HEADPAIR || (gridDim.x & 15) || (H & 1)) return P;
     const int x = P & 7, j = P >> 3;
     return ((((j >> 1) << 3) + x) << 1) + (j & 1);

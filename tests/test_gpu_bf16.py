@@ -104,6 +104,8 @@ def _grad_errors(model, meta, gold, ref, budget):
         return 2 * a if k.endswith('.c') else a
     ratios = sorted(((float((g - r).norm() / r.norm()) / allow(k), k) for k, g, r in pairs), reverse=True)
     print('  worst tensors (error / allowance):', ', '.join('%s %.2f' % (k, e) for e, k in ratios[:3]))
+    raw = sorted(((float((g - r).norm() / r.norm()) / budget['grads'][k], k) for k, g, r in pairs), reverse=True)
+    print('  RAWBUDGET worst tensors (error / budget):', ', '.join('%s %.3f' % (k, e) for e, k in raw[:4]))
     assert ratios[0][0] <= 1.0, ratios[:5]          # every tensor (strict)
     gg = torch.cat([g for _, g, _ in pairs])
     rr = torch.cat([r for _, _, r in pairs])
