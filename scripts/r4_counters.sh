@@ -9,7 +9,7 @@
 #   STAGE=cal|sq|traffic|all CFGS="cfg3 cfg2 cfg5" bash scripts/r4_counters.sh
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
-OUT=gpurun_out/r4ctr
+OUT=${OUT:-gpurun_out/r4ctr}
 mkdir -p $OUT
 STAGE=${STAGE:-all}
 RD32="TCC_EA0_RDREQ_DRAM_32B_sum TCC_EA0_RDREQ_GMI_32B_sum TCC_EA0_RDREQ_IO_32B_sum TCC_EA0_RDREQ_sum"
@@ -33,8 +33,10 @@ if [ $STAGE = traffic ] || [ $STAGE = all ]; then
     case $cfg in
       cfg3) A="--config cfg3 --dtype fp32";; cfg3_bf16) A="--config cfg3 --dtype bf16";;
       cfg2) A="--config cfg2";; cfg5) A="--config cfg5 --dtype fp32";; cfg5_bf16) A="--config cfg5 --dtype bf16";;
+      rfstate) A="--config rfstate";;
     esac
-    B="--steps ${PSTEPS:-30} --warmup 5 --no-cpu-baseline $A"
+    # one precision per pass (kernel instances of the two paths share name prefixes), no HBM probe
+    B="--steps ${PSTEPS:-30} --warmup 5 --no-cpu-baseline --no-bf16 --no-probe $A"
     pass ${cfg}_trace rocprofv3 --kernel-trace --stats -d $OUT/${cfg}_trace -o run --output-format csv -- python3 bench.py $B
     pass ${cfg}_rd rocprofv3 --pmc $RD32 --kernel-trace -d $OUT/${cfg}_rd -o run --output-format csv -- python3 bench.py $B
     pass ${cfg}_wr rocprofv3 --pmc WRITE_SIZE --kernel-trace -d $OUT/${cfg}_wr -o run --output-format csv -- python3 bench.py $B
@@ -53,7 +55,9 @@ if [ $STAGE = sq ] || [ $STAGE = all ]; then
     case $cfg in
       cfg3) A="--config cfg3 --dtype fp32";; cfg3_bf16) A="--config cfg3 --dtype bf16";;
       cfg2) A="--config cfg2";; cfg5) A="--config cfg5 --dtype fp32";; cfg5_bf16) A="--config cfg5 --dtype bf16";;
+      rfstate) A="--config rfstate";;
     esac
+    A="$A --no-bf16 --no-probe"
     i=0
     for grp in "$G1" "$G2" "$G3"; do
       i=$((i+1))

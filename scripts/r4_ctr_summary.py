@@ -1,7 +1,7 @@
 """Per-kernel SQ counter summary of a scripts/r4_counters.sh STAGE=sq run.
 
-    python scripts/r4_ctr_summary.py <cfg> [gpurun_out/r4ctr] [profiles/r04_kernel_stats_<cfg>.csv]
-        -> profiles/r04_counters_<cfg>.txt and .json
+    python scripts/r4_ctr_summary.py <cfg> [gpurun_out/r4ctr] [profiles/r04_kernel_stats_<cfg>.csv] [tag r04]
+        -> profiles/<tag>_counters_<cfg>.txt and .json
 
 Counters are per dispatch (rocprofv3 --pmc ... --kernel-trace; each group its own run of
 `bench.py --steps 2 --warmup 1`, every launch of the step counted), averaged over the dispatches
@@ -61,6 +61,7 @@ def main():
     cfg = sys.argv[1]
     src = sys.argv[2] if len(sys.argv) > 2 else 'gpurun_out/r4ctr'
     stats = sys.argv[3] if len(sys.argv) > 3 else 'profiles/r04_kernel_stats_%s.csv' % cfg
+    tag = sys.argv[4] if len(sys.argv) > 4 else 'r04'
     tab = collections.defaultdict(dict)
     for g in (1, 2, 3):
         for k, cs in load(os.path.join(src, '%s_g%d' % (cfg, g))).items():
@@ -102,9 +103,9 @@ def main():
         e['raw'] = {kk: round(v, 1) for kk, v in sorted(c.items())}
         res[k] = e
     os.makedirs('profiles', exist_ok=True)
-    json.dump(res, open('profiles/r04_counters_%s.json' % cfg, 'w'), indent=1, sort_keys=True)
+    json.dump(res, open('profiles/%s_counters_%s.json' % (tag, cfg), 'w'), indent=1, sort_keys=True)
     order = sorted(res, key=lambda k: -(res[k]['avg_us'] or 0))
-    lines = ['# r04 SQ counters, %s bench workload (scripts/r4_counters.sh, scripts/r4_ctr_summary.py); '
+    lines = ['# %s SQ counters' % tag + ', %s bench workload (scripts/r4_counters.sh, scripts/r4_ctr_summary.py); '
              'durations: %s' % (cfg, os.path.basename(stats)),
              '%-18s %8s %7s %8s %7s %7s %7s %7s %7s %7s %6s %6s %6s %6s' % (
                  'kernel', 'avg_us', 'waves', 'TFLOP/s', 'mfmaU', 'mfmaBz', 'valuBz', 'VALU/w', 'MFMA/w', 'VMEM/w',
@@ -117,7 +118,7 @@ def main():
             f(e.get('mfma_busy')), f(e.get('valu_busy')), f(e.get('valu_per_wave'), '%7.0f'),
             f(e.get('mfma_per_wave'), '%7.0f'), f(e.get('vmem_rd_per_wave'), '%7.0f'), f(e.get('wait_frac'), '%6.2f'),
             f(e.get('issue_stall_frac'), '%6.2f'), f(e.get('active_frac'), '%6.2f'), f(e.get('lds_conflict'), '%6.3f')))
-    open('profiles/r04_counters_%s.txt' % cfg, 'w').write('\n'.join(lines) + '\n')
+    open('profiles/%s_counters_%s.txt' % (tag, cfg), 'w').write('\n'.join(lines) + '\n')
     print('\n'.join(lines))
 
 
