@@ -18,8 +18,9 @@ worst of 4 executions (the fixture and 3 with parameters scaled by 1 + 2^-18 N(0
 path must be about as accurate:
   logits max|d| / max|logit| and whole-gradient relative L2 error  <= 1.25 x budget
   loss relative error                                               <= 2 x budget + 1e-4
-  EVERY gradient tensor's relative L2 error                         <= 1.5 x its budget + 0.005
-      (the scalar residual coefficients c: twice that -- one ill-conditioned sum each)
+  EVERY gradient tensor's relative L2 error                         <= 1.5 x its budget
+      (the scalar residual coefficients c: 4.3 x -- one ill-conditioned sum each; both factors
+      are 2x the worst ratio measured on the five fixtures)
   post-AdamW parameters within lr/4 of the reference step           >= budget fraction - 0.01
 and it must differ from the fp32 path (the bf16 kernels really ran).  The bf16 path stores its
 activations as bf16 (include/mep.h MEP_PREC_BF16), as torch.autocast does between ops.
@@ -96,12 +97,13 @@ def _grad_errors(model, meta, gold, ref, budget):
         pairs.append((k, g, r))
 
     def allow(k):
-        # named exemption: the residual coefficient c is ONE scalar whose gradient sums
+        # 1.5 x the tensor's budget: 2x the worst error / budget measured over every tensor of the
+        # five fixtures (0.77, ren_small; round-5 session 14, RAWBUDGET lines), no absolute floor.
+        # Named exemption: the residual coefficient c is ONE scalar whose gradient sums
         # B x H x Tq x Tk score terms dS * S_prev with heavy cancellation -- its relative error is
         # ill-conditioned (torch's own bf16 runs scatter it 3x between executions, bf16_budget
-        # 'runs'); it gets twice the tensor allowance
-        a = 1.5 * budget['grads'][k] + 0.005
-        return 2 * a if k.endswith('.c') else a
+        # 'runs'); it gets 4.3 x its budget (2x the worst measured, 2.16 on cmu_small_l2)
+        return (4.3 if k.endswith('.c') else 1.5) * budget['grads'][k]
     ratios = sorted(((float((g - r).norm() / r.norm()) / allow(k), k) for k, g, r in pairs), reverse=True)
     print('  worst tensors (error / allowance):', ', '.join('%s %.2f' % (k, e) for e, k in ratios[:3]))
     raw = sorted(((float((g - r).norm() / r.norm()) / budget['grads'][k], k) for k, g, r in pairs), reverse=True)
