@@ -133,15 +133,30 @@ MEP_DEV void layer_norm(const f32x4 (&z)[NI], f32x4 (&y)[NI], const gfloat* w, c
 // full product is exchanged through LDS (one barrier) for the next LayerNorm / product, which
 // every wave then evaluates on whole rows.  W = 6 for D = 96 (6 and 12 output tiles split evenly).
 template <int D> constexpr int rfw_waves() { return D == 96 ? 6 : D >= 64 ? 4 : 2; }
+// Large launches (State_Transfer: B x P x T tokens per block, MEP_RFW_BIG_TILES or more 16-token
+// tiles) at D = 96 run the forward with a shallower weight ring (MEP_RFW_BIG_DEPTH fragments) at
+// MEP_RFW_BIG_WPE waves per SIMD, so two 6-wave workgroups (two tiles) share a CU and one's
+// exchange barriers and weight latency hide behind the other's products; the default kernels fit
+// one 6-wave workgroup per CU (their register count leaves 8 wave slots) and run one tile per CU at
+// a time, which suits the cfg2 chain's few tiles.
+#ifndef MEP_RFW_BIG_TILES
+#define MEP_RFW_BIG_TILES 2048
+#endif
+#ifndef MEP_RFW_BIG_WPE
+#define MEP_RFW_BIG_WPE 3
+#endif
+#ifndef MEP_RFW_BIG_DEPTH
+#define MEP_RFW_BIG_DEPTH 4
+#endif
 
 // acc[j] += W'(16 i + c, :) . X for the wave's output tiles i = wave + W j < NI, in two halves:
 // prime() issues the first DEPTH weight fragments (callers prime the NEXT product before the
 // current one's stores / exchange / LayerNorm, so the weight latency hides behind them), run()
 // streams the rest through the ring, one fragment's six MFMAs per step.
-template <int NI, int NPK, int R, int W>
+template <int NI, int NPK, int R, int W, int DEP = MEP_RFW_DEPTH>
 struct PG {
     static constexpr int NJ = (NI + W - 1) / W, NS = NJ * NPK;
-    static constexpr int DEPTH = MEP_RFW_DEPTH < NS ? MEP_RFW_DEPTH : NS;
+    static constexpr int DEPTH = DEP < NS ? DEP : NS;
     OpN<3> ring[DEPTH];
     PartPtr wl;
     int wave;
@@ -282,9 +297,8 @@ MEP_DEV void stash_owned(xf32x4* st, const mep_rows& r, int tc, int wave, int la
         if (wave + W * j < NB) st[(wave + W * j) * 64 + lane] = v[j];
 }
 
-template <int D, int FD>
-__global__ __launch_bounds__(64 * rfw_waves<D>()) void k_rfw_fwd(const mep_rf_epi_desc* __restrict__ descs) {
-    constexpr int W = rfw_waves<D>();
+template <int D, int FD, int W = rfw_waves<D>(), int WPE = 1, int DEP = MEP_RFW_DEPTH>
+__global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(WPE))) void k_rfw_fwd(const mep_rf_epi_desc* __restrict__ descs) {
     constexpr int NI = D / 16, NF = FD / 16, NP = D / 32, NPF = FD / 32;
     constexpr int JI = (NI + W - 1) / W, JF = (NF + W - 1) / W;
     __shared__ f32x4 xsm[2][NF * 64];
@@ -307,7 +321,7 @@ __global__ __launch_bounds__(64 * rfw_waves<D>()) void k_rfw_fwd(const mep_rf_ep
     // fragments, q (the wave's blocks, shared stash) and the parameters (LDS)
     f32x4 xv[NI];
     load_rows<NI>(xv, d.x, tc);
-    PG<NI, NP, D, W> g1;
+    PG<NI, NP, D, W, DEP> g1;
     g1.prime(parts_at(d.wparts, MEP_RFW_PART_OFFSET(D, FD, 0)), wave);
     stash_owned<NI, W>(qst, d.q, tc, wave, lane);
     {
@@ -318,7 +332,7 @@ __global__ __launch_bounds__(64 * rfw_waves<D>()) void k_rfw_fwd(const mep_rf_ep
     MEP_RFW_STAMP(1);
     // xp = Wp x (the wave's tiles), exchanged (the exchange's barrier also publishes q and the parameters)
     f32x4 xp[NI];
-    PG<NF, NP, FD, W> g2;
+    PG<NF, NP, FD, W, DEP> g2;
     {
         f32x4 acc[JI];
 #pragma unroll
@@ -349,7 +363,7 @@ __global__ __launch_bounds__(64 * rfw_waves<D>()) void k_rfw_fwd(const mep_rf_ep
     MEP_RFW_STAMP(4);
     // f1 = relu(W1 h + b1)
     f32x4 f1[NF];
-    PG<NI, NPF, D, W> g3;
+    PG<NI, NPF, D, W, DEP> g3;
     {
         f32x4 acc[JF];
 #pragma unroll
@@ -401,7 +415,7 @@ __global__ __launch_bounds__(64 * rfw_waves<D>()) void k_rfw_fwd(const mep_rf_ep
         layer_norm_l<NI>(z, out, P + 2 * D, P + 3 * D, mean2, rstd2);
     }
     if (d.wq_next) {   // the next layer's query projection, qp_next = out Wq_next^T (wave's tiles)
-        PG<NI, NP, D, W> g4;
+        PG<NI, NP, D, W, DEP> g4;
         g4.prime(reinterpret_cast<PartPtr>(G<const unsigned char>(d.wq_next)), wave);
         f32x4 acc[JI];
 #pragma unroll
@@ -473,9 +487,8 @@ MEP_DEV void ln_bwd(f32x4 (&dz)[NI], const f32x4 (&gu)[NI], const f32x4 (&xh)[NI
         for (int r = 0; r < 4; ++r) dz[i][r] = rstd * (gw[i][r] - s1 - xh[i][r] * s2);
 }
 
-template <int D, int FD>
-__global__ __launch_bounds__(64 * rfw_waves<D>()) void k_rfw_bwd(const mep_rf_epi_bwd_desc* __restrict__ descs) {
-    constexpr int W = rfw_waves<D>();
+template <int D, int FD, int W = rfw_waves<D>(), int WPE = 1, int DEP = MEP_RFW_DEPTH>
+__global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(WPE))) void k_rfw_bwd(const mep_rf_epi_bwd_desc* __restrict__ descs) {
     constexpr int NI = D / 16, NF = FD / 16, NP = D / 32, NPF = FD / 32;
     constexpr int JI = (NI + W - 1) / W, JF = (NF + W - 1) / W;
     __shared__ f32x4 xsm[2][NF * 64];
@@ -506,7 +519,7 @@ __global__ __launch_bounds__(64 * rfw_waves<D>()) void k_rfw_bwd(const mep_rf_ep
     load_rows<NI>(fv, d.f, tc);
 #pragma unroll
     for (int i = 0; i < NI; ++i) w2v[i] = ld4w(G<const float>(d.ln2_w) + 16 * i + 4 * g);
-    PG<NF, NP, FD, W> g1;
+    PG<NF, NP, FD, W, DEP> g1;
     g1.prime(parts_at(d.wparts, MEP_RFW_PART_OFFSET(D, FD, 5)), wave);
     f32x4 f1v[JF], dqo[JI];
     {
@@ -533,7 +546,7 @@ __global__ __launch_bounds__(64 * rfw_waves<D>()) void k_rfw_bwd(const mep_rf_ep
         for (int i = 0; i < NI; ++i) gu[i] += g2[i];
     }
     if (bd.wq_in) {   // dout += dqp_in Wq: the next layer's query-projection input gradient (exchanged)
-        PG<NI, NP, D, W> g0;
+        PG<NI, NP, D, W, DEP> g0;
         g0.prime(reinterpret_cast<PartPtr>(G<const unsigned char>(bd.wq_in)), wave);
         f32x4 dv[NI];
         load_rows<NI>(dv, bd.dqp_in, tc);
@@ -572,7 +585,7 @@ __global__ __launch_bounds__(64 * rfw_waves<D>()) void k_rfw_bwd(const mep_rf_ep
     }
     // df1 = relu'(f1) (W2^T df)
     f32x4 df1[NF];
-    PG<NI, NPF, D, W> g2;
+    PG<NI, NPF, D, W, DEP> g2;
     {
         f32x4 acc[JF];
 #pragma unroll
@@ -596,7 +609,7 @@ __global__ __launch_bounds__(64 * rfw_waves<D>()) void k_rfw_bwd(const mep_rf_ep
     tile_colsum<NF, W>(part + 5 * D, df1, wave, c, g);       // db1
     // dh = dz2 + W1^T df1
     f32x4 dh[NI];
-    PG<NI, NP, D, W> g3;
+    PG<NI, NP, D, W, DEP> g3;
     {
         f32x4 acc[JI];
 #pragma unroll
@@ -805,9 +818,15 @@ extern "C" int mep_wgemm(const mep_gemm_desc* descs, int n_desc, int max_tiles, 
 extern "C" int mep_rfw_epi_fwd(const mep_rf_epi_desc* descs, int n_desc, int max_tiles, int D, int FD,
                                mep_stream_t stream) {
     if (n_desc <= 0 || max_tiles <= 0) return 0;
+    const bool big = (int64_t)max_tiles * n_desc >= MEP_RFW_BIG_TILES;
     const int rc = dispatch_rfw(D, FD, [&](auto dc, auto fc) {
-        hipLaunchKernelGGL((k_rfw_fwd<decltype(dc)::value, decltype(fc)::value>), dim3(max_tiles, n_desc),
-                           dim3(64 * rfw_waves<decltype(dc)::value>()), 0, (hipStream_t)stream, descs);
+        constexpr int DD = decltype(dc)::value, FF = decltype(fc)::value;
+        if (DD == 96 && big)
+            hipLaunchKernelGGL((k_rfw_fwd<DD, FF, rfw_waves<DD>(), MEP_RFW_BIG_WPE, MEP_RFW_BIG_DEPTH>), dim3(max_tiles, n_desc),
+                               dim3(64 * rfw_waves<DD>()), 0, (hipStream_t)stream, descs);
+        else
+            hipLaunchKernelGGL((k_rfw_fwd<DD, FF>), dim3(max_tiles, n_desc), dim3(64 * rfw_waves<DD>()), 0,
+                               (hipStream_t)stream, descs);
     });
     if (rc) { mep_set_error("mep_rfw_epi_fwd: D in {32,64,96,128} and FD in {D, 2D}"); return rc; }
     return mep_check_launch("mep_rfw_epi_fwd");
