@@ -363,6 +363,17 @@ int mep_wsplit(const mep_wsplit_desc* descs, int n_desc, int max_units, mep_stre
  * per 16 tokens x 32 columns, grid (max_tiles, n_desc, ceil(max_n / 32)), max_n = the largest N
  * (<= 256).  ldw, w_nt and bf16 are unused. */
 int mep_wgemm(const mep_gemm_desc* descs, int n_desc, int max_tiles, int max_n, mep_stream_t stream);
+/* mep_wgemm_ws: mep_wgemm's contract (bit-identical results) with each workgroup's column block of
+ * the parts resident in LDS and its waves walking 16-token tiles (persistent grid sized from the
+ * device's CU count); max_ntok / max_n / max_k = the largest ntok / N / K of the descriptors,
+ * max_k <= 320.  The same token GEMMs as mep_wgemm (others/realformer.py:136-157,182-188).
+ * flags: MEP_WGEMM_XVEC when every descriptor's X rows are 16-byte aligned (x.ptr, sB, sT
+ * multiples of 4 floats) and readable up to K rounded up to 4 (K % 4 == 0, or rows padded): the
+ * X rows are then read in 16-byte blocks (values past K are read and ignored), else one float at
+ * a time. */
+#define MEP_WGEMM_XVEC 0x1
+int mep_wgemm_ws(const mep_gemm_desc* descs, int n_desc, int max_ntok, int max_n, int max_k, int flags,
+                 mep_stream_t stream);
 /* mep_rfw_epi_fwd / _bwd: mep_rf_epi_fwd / _bwd on the parts at desc.wparts; one wave per 16-token
  * tile, one partial row per tile; D in {32, 64, 96, 128}, FD in {D, 2D}. */
 int mep_rfw_epi_fwd(const mep_rf_epi_desc* descs, int n_desc, int max_tiles, int D, int FD, mep_stream_t stream);

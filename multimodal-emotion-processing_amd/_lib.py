@@ -272,6 +272,7 @@ SIGNATURES.update({
     'mep_assemble_windows': [ctypes.POINTER(WindowDesc), i32, P],
     'mep_tgemm': [P, i32, i32, i32, i32, P],
     'mep_wgemm': [P, i32, i32, i32, P],
+    'mep_wgemm_ws': [P, i32, i32, i32, i32, i32, P],
     'mep_abi_version': [],
     'mep_rf_rows': [i32, i32],
     'mep_last_error': [ctypes.c_char_p, ctypes.c_size_t],
@@ -399,6 +400,29 @@ def attn_bwd_splitq(bdescs, min_units=1024):
 
 
 RFW = switch('MEP_RFW', '1') != '0'   # 0: the LDS-tiled f32-MFMA realformer kernels (A/B runs)
+# realformer token GEMMs on the LDS-resident weight kernel (mep_wgemm_ws) from WGEMM_WS_MIN
+# 16 x 32 output tiles per launch (State_Transfer, B x P x T tokens: 1133 -> 400 us per step),
+# below it one wave per 16 tokens x 32 columns (mep_wgemm: cfg2's 3200-token launches, where the
+# per-workgroup weight copy does not pay, 41.9 vs 42.6 us); MEP_WGEMM_WS=0: always mep_wgemm
+WGEMM_WS = switch('MEP_WGEMM_WS', '1') != '0'
+WGEMM_WS_MIN = 8192
+WGEMM_XVEC = 0x1                                   # MEP_WGEMM_XVEC
+
+
+def wgemm_tiles(items):
+    """16-token x 32-column output tiles of a token-GEMM launch (mep_wgemm's waves)"""
+    return sum(-(-d.ntok // 16) * -(-d.N // 32) for d in items)
+
+
+def wgemm_ws(descs, stream=None, x_padded=()):
+    """mep_wgemm_ws over a DescArray of GemmDescs: MEP_WGEMM_XVEC when every X row view is
+    16-byte aligned and K % 4 == 0 or the view's rows are padded (x_padded: x.ptr values whose
+    buffers hold K rounded up to 4 readable floats per row)"""
+    it = descs.items
+    xvec = all(d.x.ptr % 16 == 0 and d.x.sB % 4 == 0 and d.x.sT % 4 == 0 and
+               (d.K % 4 == 0 or d.x.ptr in x_padded) for d in it)
+    call('mep_wgemm_ws', descs.ptr, descs.n, max(d.ntok for d in it), max(d.N for d in it), max(d.K for d in it),
+         WGEMM_XVEC if xvec else 0, stream=stream)
 
 
 def rf_bwd_rows(wave=None):

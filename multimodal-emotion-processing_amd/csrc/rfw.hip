@@ -15,6 +15,8 @@
 // v_mfma_f32_16x16x32_bf16 -- fp32-level (split.h), no per-fragment split VALU for the weights,
 // which feed only 16 tokens each here.  Weight fragments are streamed through a ring of
 // MEP_RFW_DEPTH fragments ahead of their MFMAs.
+#include <algorithm>
+
 #include "common.h"
 #include "split.h"
 
@@ -778,6 +780,189 @@ __global__ __launch_bounds__(64 * WGM_WAVES) void k_wgemm(const mep_gemm_desc* _
     }
 }
 
+// ---------------------------------------------------------------- weight-stationary token GEMM
+// mep_wgemm's contract with the weight block resident in LDS.  A workgroup owns the 16 NT output
+// columns [16 NT z, 16 NT (z + 1)) of one descriptor (grid (gx, n_desc, z)): it copies their parts
+// (every k pair) from the mep_wsplit image into LDS once (SplitWS: conflict-free 16-byte fragment
+// reads), then its W waves walk the 16-token tiles (blockIdx.x + gridDim.x j) W + wave, each
+// wave holding the next tile's X rows in registers while it multiplies the current one.  A
+// fragment read (three ds_read_b128, 12 LDS cycles) feeds six 16-cycle MFMAs, so four SIMDs keep
+// the LDS array half busy.  Products and summation order are k_wgemm's (k pairs in order, six
+// products each, then alpha, bias + table, relu, + y), so the two agree bit for bit.
+// NT * NPK <= 36 (110.6 KB of LDS).
+constexpr int WGS_MAX_WAVES = 8;
+#ifndef MEP_WGS_RING
+#define MEP_WGS_RING 3   // weight fragments (3 x 16 B per lane each) read ahead of their MFMAs
+#endif
+template <int NT, int NPK, bool XV>
+__global__ __launch_bounds__(64 * WGS_MAX_WAVES) void k_wgemm_ws(const mep_gemm_desc* __restrict__ descs) {
+    using WS = SplitWS<16 * NT, NPK, 3>;
+    __shared__ __attribute__((aligned(16))) unsigned char sm[WS::BYTES];
+    const mep_gemm_desc& d = descs[blockIdx.y];
+    const int ntok = d.ntok, N = d.N, K = d.K;
+    const int W = blockDim.x >> 6;
+    const int ntile = (ntok + 15) >> 4;
+    const int n0 = (int)blockIdx.z * 16 * NT;
+    if (n0 >= N || (int)blockIdx.x * W >= ntile) return;   // the whole workgroup
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, c = lane & 15, g = lane >> 4;
+    const int npk = (K + 31) >> 5;
+    const int nt = min(NT, (N - n0 + 15) >> 4);
+    typedef __attribute__((address_space(3))) unsigned char lbyte;
+    const WS ws{(lbyte*)sm, 0};
+    const bool yvec = ((d.y.ptr & 15) == 0) && (d.y.sB % 4 == 0) && (d.y.sT % 4 == 0);
+    // X blocks of a tile with no branches or selects (either makes the compiler wait for the
+    // loads where they are issued): clamped addresses only -- the values loaded for k >= K are
+    // finite row data that meet zero weights (mep_wsplit pads K with zeros, pairs past the
+    // descriptor's K are zero in LDS).  XV: 16-byte loads of K rounded up to 4 (the host's
+    // MEP_WGEMM_XVEC contract), else one float at a time.
+    const int KV = XV ? (K + 3) & ~3 : K;
+    auto load_x = [&](int tile, f32x4 (&v)[2 * NPK]) {
+        const gfloat* xr = row_ptr(d.x, min(min(tile, ntile - 1) * 16 + c, ntok - 1));
+#pragma unroll
+        for (int h = 0; h < 2 * NPK; ++h) {
+            const int k = 16 * h + 4 * g;   // block h = (pair h / 2, half h % 2)
+            if constexpr (XV) {
+                v[h] = ld4w(xr + min(k, KV - 4));
+            } else {
+#pragma unroll
+                for (int e = 0; e < 4; ++e) v[h][e] = xr[min(k + e, K - 1)];
+            }
+        }
+    };
+    {
+        int tile = (int)blockIdx.x * W + wave;
+        const int step = (int)gridDim.x * W;
+        f32x4 xc[2 * NPK];
+        load_x(tile, xc);   // in flight across the weight copy
+        {
+            // k pairs past the descriptor's K are stored as zeros and its X blocks there are zeros, so
+            // every tile runs all NPK pairs and all NT output tiles with no guards (tiles past N read
+            // rows never stored and are never written back); a launch's short-K / narrow descriptors
+            // then do the work of its widest, on workgroups of their own
+            const PartPtr src = parts_at(d.w, 0);
+            const int64_t part = (int64_t)((N + 31) & ~31) * npk * 4;   // units per part (mep_wsplit R)
+            constexpr int UNITS = 16 * NT * NPK * 4;                     // per part
+            const int units = 16 * nt * NPK * 4;
+            // FB units per thread loaded before any is stored: one memory latency per FB rounds
+            constexpr int FB = 8;
+            for (int u0 = threadIdx.x; u0 < 3 * units; u0 += FB * blockDim.x) {
+                u32x4 v[FB];
+#pragma unroll
+                for (int j = 0; j < FB; ++j) {
+                    const int u = min(u0 + j * (int)blockDim.x, 3 * units - 1);
+                    const int t = u / units, r = u - t * units;
+                    const int np = r >> 2, nl = np / NPK, p = np - nl * NPK;
+                    const u32x4 w = src[t * part + ((int64_t)(n0 + nl) * npk + min(p, npk - 1)) * 4 + (r & 3)];
+                    v[j] = p < npk ? w : u32x4{0u, 0u, 0u, 0u};
+                }
+#pragma unroll
+                for (int j = 0; j < FB; ++j) {
+                    const int u = u0 + j * blockDim.x;
+                    const int t = u / units, r = u - t * units;
+                    const int np = r >> 2, nl = np / NPK, p = np - nl * NPK;
+                    if (u < 3 * units) ws.put_unit(t, nl, p, r & 3, v[j]);
+                }
+            }
+            static_assert(3 * UNITS * 16 == WS::BYTES, "k_wgemm_ws: LDS image size");
+        }
+        __syncthreads();
+        const gfloat* bias = d.bias ? G<const float>(d.bias) : nullptr;
+        const gfloat* table = d.table ? G<const float>(d.table) : nullptr;
+        const int ldt = d.ldt ? d.ldt : N;
+        // the next tile's X blocks prefetched into registers while this one multiplies (PF), or
+        // (NPK = 10: 80 more registers) loaded at the top of each tile, behind the other waves
+        constexpr bool PF = NPK <= 6;
+        // one tile on X blocks xcur (loaded), the next tile's blocks into xnext: the loop runs
+        // tiles in pairs with the two buffers swapping roles, so no register copy makes the
+        // compiler wait for the prefetch (and, behind it, for the epilogue's stores)
+        auto one_tile = [&](f32x4 (&xcur)[2 * NPK], f32x4 (&xnext)[2 * NPK]) {
+            if constexpr (PF) {
+                load_x(tile + step, xnext);
+            } else {
+                if (tile != (int)blockIdx.x * W + wave) load_x(tile, xcur);
+            }
+            f32x4 acc[NT];
+#pragma unroll
+            for (int i = 0; i < NT; ++i) acc[i] = zero_f4();
+            // steps s = (pair p, tile i), p-major; fragments MEP_WGS_RING steps ahead of their MFMAs
+            constexpr int S = NPK * NT, RING = MEP_WGS_RING < S ? MEP_WGS_RING : S;
+            OpN<3> ring[RING];
+#pragma unroll
+            for (int s = 0; s < RING; ++s) ring[s] = ws.frag(s % NT, s / NT);
+            OpN<3> b;
+#pragma unroll
+            for (int s = 0; s < S; ++s) {
+                const int p = s / NT, i = s % NT;
+                if (i == 0) b = opn<3>(xcur[2 * p], xcur[2 * p + 1]);
+                const OpN<3> a = ring[s % RING];
+                if (s + RING < S) ring[s % RING] = ws.frag((s + RING) % NT, (s + RING) / NT);
+                acc[i] = mma_n<3>(a, b, acc[i]);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+            const int tok = tile * 16 + c;
+            // the lane's column offset as a loop-variant value: otherwise the compiler hoists the
+            // epilogue's NT x 4 column clamps, compare masks and addresses out of the tile loop
+            // (~100 registers live across the products, spilled)
+            int gcol = 4 * g;
+            asm volatile("" : "+v"(gcol));
+            if (tok < ntok) {
+                gfloat* yr = row_ptr(d.y, tok);
+                const gfloat* trow = table ? table + (int64_t)(tok % d.y.T) * ldt : nullptr;
+                // three output tiles at a time: the bias / table / y loads of a group in flight
+                // together, never all NT groups' (their registers on top of the accumulators)
+#pragma unroll
+                for (int i0 = 0; i0 < NT; i0 += 3) {
+                    f32x4 add[3], yo[3];
+#pragma unroll
+                    for (int j = 0; j < 3; ++j) {
+                        const int nb = n0 + 16 * (i0 + j) + gcol;
+                        add[j] = yo[j] = zero_f4();
+                        if (i0 + j >= nt) continue;
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) {
+                            const int n = min(nb + r, N - 1);
+                            add[j][r] = (bias ? bias[n] : 0.f) + (trow ? trow[n] : 0.f);
+                            if (d.accumulate) yo[j][r] = yr[n];
+                        }
+                    }
+#pragma unroll
+                    for (int j = 0; j < 3; ++j) {
+                        const int i = i0 + j, nb = n0 + 16 * i + gcol;
+                        if (i >= nt) continue;
+                        f32x4 v;
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) {
+                            float s = d.alpha * acc[i][r] + add[j][r];
+                            if (d.relu) s = fmaxf(s, 0.f);
+                            v[r] = d.accumulate ? s + yo[j][r] : s;
+                        }
+                        if (yvec && nb + 3 < N) {
+                            *reinterpret_cast<MEP_G f32x4*>(yr + nb) = v;
+                        } else {
+#pragma unroll
+                            for (int r = 0; r < 4; ++r)
+                                if (nb + r < N) yr[nb + r] = v[r];
+                        }
+                    }
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+            }
+        };
+        if constexpr (PF) {
+            f32x4 xn[2 * NPK];
+            while (tile < ntile) {
+                one_tile(xc, xn);
+                tile += step;
+                if (tile >= ntile) break;
+                one_tile(xn, xc);
+                tile += step;
+            }
+        } else {
+            for (; tile < ntile; tile += step) one_tile(xc, xc);
+        }
+    }
+}
+
 template <typename F>
 int dispatch_rfw(int D, int FD, F&& f) {
 #define MEP_RFW_CASE(DD, FF) \
@@ -813,6 +998,47 @@ extern "C" int mep_wgemm(const mep_gemm_desc* descs, int n_desc, int max_tiles, 
     hipLaunchKernelGGL(k_wgemm, dim3(max_tiles, n_desc, (max_n + 31) / 32), dim3(64 * WGM_WAVES), 0,
                        (hipStream_t)stream, descs);
     return mep_check_launch("mep_wgemm");
+}
+
+#ifndef MEP_WGS_MIN_WG
+#define MEP_WGS_MIN_WG 256   // column blocks narrow (12 -> 6 -> 3 tiles) until a launch has this many workgroups
+#endif
+extern "C" int mep_wgemm_ws(const mep_gemm_desc* descs, int n_desc, int max_ntok, int max_n, int max_k,
+                            int flags, mep_stream_t stream) {
+    if (n_desc <= 0 || max_ntok <= 0) return 0;
+    const int npk = (max_k + 31) / 32, ntf = (max_n + 15) / 16;
+    if (max_n <= 0 || max_k <= 0 || npk > 10) { mep_set_error("mep_wgemm_ws: 0 < max_n, 0 < max_k <= 320"); return MEP_EINVAL; }
+    const int NPK = npk <= 3 ? 3 : npk <= 6 ? 6 : 10;
+    int NT = NPK == 3 ? 12 : NPK == 6 ? 6 : 3;          // NT * NPK <= 36
+    while (NT > 3 && ntf <= NT / 2) NT /= 2;            // no wider than the widest descriptor needs
+    const int tiles = (max_ntok + 15) / 16;
+    auto blocks = [&](int nt, int w) { return (int64_t)n_desc * ((ntf + nt - 1) / nt) * ((tiles + w - 1) / w); };
+    while (NT > 3 && blocks(NT, WGS_MAX_WAVES) < MEP_WGS_MIN_WG) NT /= 2;
+    const int W = blocks(NT, WGS_MAX_WAVES) < MEP_WGS_MIN_WG ? WGS_MAX_WAVES / 2 : WGS_MAX_WAVES;
+    const int nz = (ntf + NT - 1) / NT;
+    const dim3 block(64 * W);
+    hipStream_t st = (hipStream_t)stream;
+    // persistent: one resident round of workgroups (occupancy by registers and LDS, cached per
+    // instance and block size), each walking its tiles
+    auto run = [&](auto kern, int slot) {
+        static int per_cu[2][16];
+        int& pc = per_cu[W == WGS_MAX_WAVES][slot];
+        if (pc == 0 && hipOccupancyMaxActiveBlocksPerMultiprocessor(&pc, kern, 64 * W, 0) != hipSuccess) pc = 1;
+        pc = std::max(pc, 1);
+        static int n_cu = 0;
+        if (n_cu == 0) {
+            int dev = 0;
+            if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n_cu <= 0) n_cu = 256;
+        }
+        const int64_t fit = std::max<int64_t>(1, (int64_t)n_cu * pc / ((int64_t)n_desc * nz));
+        const int gx = (int)std::min<int64_t>((tiles + W - 1) / W, fit);
+        hipLaunchKernelGGL(kern, dim3(gx, n_desc, nz), block, 0, st, descs);
+    };
+    const bool xv = flags & MEP_WGEMM_XVEC;
+#define MEP_WGS(A, B, S) if (NT == A && NPK == B) { if (xv) run(k_wgemm_ws<A, B, true>, 2 * S); else run(k_wgemm_ws<A, B, false>, 2 * S + 1); }
+    MEP_WGS(12, 3, 0); MEP_WGS(6, 3, 1); MEP_WGS(3, 3, 2); MEP_WGS(6, 6, 3); MEP_WGS(3, 6, 4); MEP_WGS(3, 10, 5);
+#undef MEP_WGS
+    return mep_check_launch("mep_wgemm_ws");
 }
 
 extern "C" int mep_rfw_epi_fwd(const mep_rf_epi_desc* descs, int n_desc, int max_tiles, int D, int FD,

@@ -159,6 +159,11 @@ struct SplitWS {
         typedef __attribute__((address_space(3))) u32x4 lu32x4;
         *reinterpret_cast<lu32x4*>(base + t * R * RS + n * RS + unit(n, 4 * p + g) * 16) = u32x4{lo[0], lo[1], hi[0], hi[1]};
     }
+    // part t of unit (n, p, g) as stored by mep_wsplit (one 16-byte unit)
+    MEP_DEV void put_unit(int t, int n, int p, int g, u32x4 v) const {
+        typedef __attribute__((address_space(3))) u32x4 lu32x4;
+        *reinterpret_cast<lu32x4*>(base + t * R * RS + n * RS + unit(n, 4 * p + g) * 16) = v;
+    }
 };
 
 // acc[i] (i < NI) += A_i B over NP k pairs: afr(i, p) -> OpN (A fragment of output tile i),

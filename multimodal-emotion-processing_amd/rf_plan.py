@@ -99,7 +99,11 @@ class RealformerPlan:
         self.ntok = {m: R * self.T[m] for m in sp.mods}
         assert max(self.ntok.values()) < 1 << 22, 'row views are limited to 2^22 rows (csrc/common.h row_off)'
         # ---------------- static inputs ([R, T, d] = the reference's [B, P, T, d])
-        self.x_in = {m: torch.zeros(R, self.T[m], sp.dims[m], **f32) for m in sp.mods}
+        # feature rows padded to a multiple of 4 floats (zeros, never written): the token GEMMs
+        # read them in 16-byte blocks (MEP_WGEMM_XVEC); x_in[m] is the [R, T, d] view
+        self.x_pad = {m: torch.zeros(R, self.T[m], -(-sp.dims[m] // 4) * 4, **f32) for m in sp.mods}
+        self.x_in = {m: self.x_pad[m][..., :sp.dims[m]] for m in sp.mods}
+        self.x_padded = frozenset(t.data_ptr() for t in self.x_pad.values())
         self.m_in = {m: torch.zeros(R, self.T[m], **f32) for m in sp.mods}
         self.U = {m: torch.zeros(self.ntok[m], D, **f32) for m in sp.mods}
         self.dU = {m: torch.zeros(self.ntok[m], D, **f32) for m in sp.mods}
@@ -193,8 +197,8 @@ class RealformerPlan:
         return rows(self.dXcat, blk['Tq'], self.Ttot * self.C, self.C, self.toff[blk['qm']] * self.C + blk['col'])
 
     def _in_rows(self, m):
-        d, T = self.spec.dims[m], self.T[m]
-        return rows(self.x_in[m], T, T * d, d)
+        T, dp = self.T[m], self.x_pad[m].shape[-1]
+        return rows(self.x_pad[m], T, T * dp, dp)
 
     def _kv_rows(self, blk, which, t):
         """K (which=0) or V (which=1) half of a [ntok, 2D] buffer t"""
@@ -476,7 +480,7 @@ class RealformerPlan:
             for m, x, mk in (('l', l, lm), ('v', v, vm), ('a', a, am)):
                 if m not in self.spec.mods:
                     continue
-                self.x_in[m].copy_(x.reshape(self.x_in[m].shape))
+                self.x_in[m].copy_(x.reshape(self.x_in[m].shape))   # into the padded rows
                 self.m_in[m].copy_(mk.reshape(self.m_in[m].shape))
             if labels is not None:
                 self.labels.copy_(labels)
@@ -513,10 +517,19 @@ class RealformerPlan:
             self.head.ext_dout = 0
             _lib.call('mep_rf_head', ctypes.byref(self.head), stream=stream)
 
+    def gemm_launcher(self, descs):
+        """launch name a token-GEMM descriptor array runs under (bench.py / roofline.py)"""
+        if not self.rfw:
+            return _lib.gemm_launcher('mep_gemm', descs)
+        ws = _lib.WGEMM_WS and _lib.wgemm_tiles(descs.items) >= _lib.WGEMM_WS_MIN
+        return 'mep_wgemm_ws' if ws else 'mep_wgemm'
+
     def _gemm(self, descs, tiles, stream):
         """a token-GEMM launch: mep_wgemm on the arena's parts, or the mep_gemm path"""
         if self.rfw:
-            if descs.n:
+            if descs.n and self.gemm_launcher(descs) == 'mep_wgemm_ws':
+                _lib.wgemm_ws(descs, stream, self.x_padded)
+            elif descs.n:
                 _lib.call('mep_wgemm', descs.ptr, descs.n, int(tiles), max(d.N for d in descs.items), stream=stream)
         else:
             _lib.gemm('mep_gemm', descs, tiles, stream)

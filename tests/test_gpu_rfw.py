@@ -117,6 +117,62 @@ def test_wgemm_vs_float64(B, T, cuda):
     assert_close(y35, ref35.cpu().numpy(), 1e-5, 1e-6, 'K = 35, bias + relu')
 
 
+def _wgemm_ws(descs, dev):
+    from mep_amd import _lib
+    _lib.wgemm_ws(_lib.DescArray(_lib.GemmDesc, descs, dev))
+    torch.cuda.synchronize()
+
+
+# descriptor mixes of one launch -> the LDS-resident instance (column tiles NT, k pairs NPK) the
+# host picks: rfstate-sized w_qkv (12, 3), the input gradients (6, 6), unify K = 300 (3, 10),
+# small launches narrowing the column block (3, 3), (3, 6), ragged N / K and a single tile
+WS_CASES = {
+    'qkv_big': (64 * 6 * 50, [(96, 192, 0), (96, 96, 0)]),
+    'ingrad': (64 * 6 * 50, [(96, 96, 1), (192, 96, 1)]),
+    'unify': (32 * 6 * 50, [(300, 96, 0), (35, 96, 0), (74, 96, 0)]),
+    'small': (50 * 3, [(96, 192, 0), (96, 96, 0)]),
+    'small_k192': (50 * 3, [(192, 96, 1)]),
+    'ragged': (37, [(70, 42, 1), (33, 18, 0)]),
+}
+
+
+@pytest.mark.parametrize('case', sorted(WS_CASES))
+def test_wgemm_ws_matches_wgemm(case, cuda):
+    """mep_wgemm_ws == mep_wgemm bit for bit (same products, same order) and both within fp32
+    level of float64: every (K, N, accumulate) descriptor of the case in one launch; the
+    bias / table / relu epilogue on the first descriptor."""
+    n, shapes = WS_CASES[case]
+    torch.manual_seed(len(case) * 1000 + n)
+    T = 50 if n % 50 == 0 else n
+    ws, xs, ys, y0s = [], [], [], []
+    for (K, N, acc) in shapes:
+        ws.append((torch.randn(N, K, device=cuda) / K ** 0.5, N, K, K, 0))
+        xs.append(torch.randn(n, K, device=cuda))
+        y0s.append(torch.randn(n, N, device=cuda) if acc else torch.zeros(n, N, device=cuda))
+    bias = torch.randn(shapes[0][1], device=cuda)
+    table = torch.randn(T, shapes[0][1], device=cuda)
+    buf, offs = _parts(ws, cuda)
+    outs = []
+    for run in (_wgemm, _wgemm_ws):
+        ys = [y.clone() for y in y0s]
+        descs = []
+        for i, ((K, N, acc), x, y, o) in enumerate(zip(shapes, xs, ys, offs)):
+            extra = dict(bias=bias, table=table, relu=1) if i == 0 else {}
+            descs.append(_gd(_rows(x, T, T * K, K), _rows(y, T, T * N, N), buf.data_ptr() + o, n, N, K,
+                             accumulate=acc, **extra))
+        run(descs, cuda)
+        outs.append(ys)
+    for i, ((K, N, acc), x, y0, (w, *_)) in enumerate(zip(shapes, xs, y0s, ws)):
+        a, b = outs[0][i], outs[1][i]
+        assert torch.equal(a, b), '%s desc %d: max |diff| %.3g' % (case, i, (a - b).abs().max().item())
+        ref = x.double() @ w.double().t()
+        if i == 0:
+            ref = torch.relu(ref + bias.double() + table.double().repeat(n // T, 1))
+        if acc:
+            ref = ref + y0.double()
+        assert_close(b, ref.cpu().numpy(), 1e-5, 1e-6, '%s desc %d' % (case, i))
+
+
 def test_rfw_fused_query_projection(cuda):
     """qp_next from the fused epilogue tail equals out Wq^T (float64) of the same launch's out."""
     from mep_amd import _lib
