@@ -374,6 +374,31 @@ int mep_wgemm(const mep_gemm_desc* descs, int n_desc, int max_tiles, int max_n, 
 #define MEP_WGEMM_XVEC 0x1
 int mep_wgemm_ws(const mep_gemm_desc* descs, int n_desc, int max_ntok, int max_n, int max_k, int flags,
                  mep_stream_t stream);
+
+/* mep_rfw_front: the realformer front of one modality in one launch -- the Conv1d unify + position
+ * table (others/realformer.py:136-152,224-227) and every projection that reads its output U: the
+ * [K | V] = U [W_k; W_v]^T of the blocks keyed on this modality and the Q = U W_q^T of its
+ * layer-0 blocks (realformer.py:157).  One workgroup (6 waves) per 16-token tile: U's six 16-feature
+ * tiles (one per wave) are stored and exchanged through LDS, then the products' output tiles are
+ * dealt round-robin to the waves.  unify: the mep_wgemm contract on mep_wsplit parts with D = N =
+ * 96, alpha / bias / table as mep_gemm, no relu / accumulate, x rows 16-byte aligned and readable
+ * up to K rounded up to 4 (MEP_WGEMM_XVEC), ceil(K / 32) = npk_u in {2, 3, 10}; out[o]: parts of a
+ * [N_o][96] weight (N_o % 16 == 0), y_o = U W_o^T written; tile_map[t] = o << 8 | (16-column tile
+ * of out[o]) for the t < n_tiles output tiles.  Bit-identical to mep_wgemm on the same parts. */
+#define MEP_RF_FRONT_MAX_OUT 12
+#define MEP_RF_FRONT_MAX_TILES 96
+typedef struct {
+    uint64_t w;      /* mep_wsplit parts of W_o [N][96] */
+    mep_rows y;      /* output rows, N columns          */
+    int32_t  N, _pad;
+} mep_rf_front_out;
+typedef struct {
+    mep_gemm_desc unify;
+    int32_t n_out, n_tiles;
+    mep_rf_front_out out[MEP_RF_FRONT_MAX_OUT];
+    int16_t tile_map[MEP_RF_FRONT_MAX_TILES];
+} mep_rf_front_desc;
+int mep_rfw_front(const mep_rf_front_desc* descs, int n_desc, int max_tiles, int npk_u, mep_stream_t stream);
 /* mep_rfw_epi_fwd / _bwd: mep_rf_epi_fwd / _bwd on the parts at desc.wparts; one wave per 16-token
  * tile, one partial row per tile; D in {32, 64, 96, 128}, FD in {D, 2D}. */
 int mep_rfw_epi_fwd(const mep_rf_epi_desc* descs, int n_desc, int max_tiles, int D, int FD, mep_stream_t stream);

@@ -45,6 +45,19 @@ class GemmDesc(ctypes.Structure):
                 ('accumulate', i32), ('relu', i32), ('alpha', f32), ('bf16', i32), ('ldt', i32)]
 
 
+RF_FRONT_MAX_OUT = 12         # MEP_RF_FRONT_MAX_OUT
+RF_FRONT_MAX_TILES = 96       # MEP_RF_FRONT_MAX_TILES
+
+
+class RfFrontOut(ctypes.Structure):
+    _fields_ = [('w', u64), ('y', Rows), ('N', i32), ('_pad', i32)]
+
+
+class RfFrontDesc(ctypes.Structure):
+    _fields_ = [('unify', GemmDesc), ('n_out', i32), ('n_tiles', i32), ('out', RfFrontOut * RF_FRONT_MAX_OUT),
+                ('tile_map', ctypes.c_int16 * RF_FRONT_MAX_TILES)]
+
+
 WG_MAX_B = 4
 
 
@@ -273,6 +286,7 @@ SIGNATURES.update({
     'mep_tgemm': [P, i32, i32, i32, i32, P],
     'mep_wgemm': [P, i32, i32, i32, P],
     'mep_wgemm_ws': [P, i32, i32, i32, i32, i32, P],
+    'mep_rfw_front': [P, i32, i32, i32, P],
     'mep_abi_version': [],
     'mep_rf_rows': [i32, i32],
     'mep_last_error': [ctypes.c_char_p, ctypes.c_size_t],

@@ -963,6 +963,102 @@ __global__ __launch_bounds__(64 * WGS_MAX_WAVES) void k_wgemm_ws(const mep_gemm_
     }
 }
 
+// ---------------------------------------------------------------- realformer front
+// mep_rfw_front (include/mep.h): the unify of a 16-token tile (wave w: U features 16 w .. +15, its
+// K pairs streamed through a fragment ring), U stored and exchanged through LDS, then every
+// projection of U with the output tiles dealt round-robin to the six waves, the fragments of a
+// wave's next tile in flight while it multiplies the current one (two register sets in turn).
+// The products, their order and the unify epilogue are mep_wgemm's, so U, K / V and Q agree with
+// the mep_wgemm launches bit for bit.
+#ifndef MEP_FRONT_DEPTH
+#define MEP_FRONT_DEPTH 4   // unify weight fragments in flight ahead of their MFMAs
+#endif
+template <int NPKU>
+__global__ __launch_bounds__(384) void k_rfw_front(const mep_rf_front_desc* __restrict__ descs) {
+    constexpr int NI = 6, W = 6, RU = 96;   // U tiles (D = 96), waves, rows of the unify parts
+    __shared__ f32x4 ubuf[NI * 64];
+    const mep_rf_front_desc& fd = descs[blockIdx.y];
+    const mep_gemm_desc& u = fd.unify;
+    const int ntok = u.ntok;
+    if ((int)blockIdx.x * 16 >= ntok) return;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, c = lane & 15, g = lane >> 4;
+    const int tok = (int)blockIdx.x * 16 + c, tc = min(tok, ntok - 1);
+    // X row blocks: 16-byte loads of K rounded up to 4, clamped (values past K meet zero weights)
+    const int KV = (u.K + 3) & ~3;
+    f32x4 xr[2 * NPKU];
+    {
+        const gfloat* xp = row_ptr(u.x, tc);
+#pragma unroll
+        for (int h = 0; h < 2 * NPKU; ++h) xr[h] = ld4w(xp + min(16 * h + 4 * g, KV - 4));
+    }
+    const int n = 16 * wave + 4 * g;   // the lane's U features n .. n + 3
+    f32x4 add;
+    {
+        const gfloat* bias = u.bias ? G<const float>(u.bias) : nullptr;
+        const gfloat* trow = u.table ? G<const float>(u.table) + (int64_t)(tc % u.y.T) * (u.ldt ? u.ldt : RU) : nullptr;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) add[r] = (bias ? bias[n + r] : 0.f) + (trow ? trow[n + r] : 0.f);
+    }
+    const PartPtr wu = parts_at(u.w, 0) + ((16 * wave + c) * NPKU) * 4 + g;
+    auto fragu = [&](int p) {
+        OpN<3> o;
+#pragma unroll
+        for (int t = 0; t < 3; ++t) o.p[t] = __builtin_bit_cast(bf16x8, wu[(t * RU * NPKU + p) * 4]);
+        return o;
+    };
+    constexpr int DEP = MEP_FRONT_DEPTH < NPKU ? MEP_FRONT_DEPTH : NPKU;
+    OpN<3> ring[DEP];
+#pragma unroll
+    for (int s = 0; s < DEP; ++s) ring[s] = fragu(s);
+    // the projections' tiles: wave's j-th tile t = wave + W j; fragment (t, p) of out[o] rows
+    // 16 lt + c, three k pairs (K = 96)
+    const int nt = fd.n_tiles, nj = (nt - wave + W - 1) / W;
+    auto frag2 = [&](int j, OpN<3> (&f)[3]) {
+        const int m = fd.tile_map[wave + W * min(j, nj - 1)];
+        const mep_rf_front_out& q = fd.out[m >> 8];
+        const int R = (q.N + 31) & ~31;
+        const PartPtr w = parts_at(q.w, 0) + ((16 * (m & 255) + c) * 3) * 4 + g;
+#pragma unroll
+        for (int p = 0; p < 3; ++p)
+#pragma unroll
+            for (int t = 0; t < 3; ++t) f[p].p[t] = __builtin_bit_cast(bf16x8, w[(t * R * 3 + p) * 4]);
+    };
+    f32x4 acc = zero_f4();
+#pragma unroll
+    for (int p = 0; p < NPKU; ++p) {
+        const OpN<3> a = ring[p % DEP];
+        if (p + DEP < NPKU) ring[p % DEP] = fragu(p + DEP);
+        acc = mma_n<3>(a, opn<3>(xr[2 * p], xr[2 * p + 1]), acc);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    OpN<3> fa[3], fb[3];
+    frag2(0, fa);   // the first projection tile's weights in flight across the exchange (n_tiles >= 6)
+    f32x4 uv;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) uv[r] = u.alpha * acc[r] + add[r];
+    if (tok < ntok) *reinterpret_cast<MEP_G f32x4*>(row_ptr(u.y, tok) + n) = uv;
+    ubuf[wave * 64 + lane] = uv;
+    lds_barrier();
+    OpN<3> bu[3];
+#pragma unroll
+    for (int p = 0; p < 3; ++p) bu[p] = opn<3>(ubuf[2 * p * 64 + lane], ubuf[(2 * p + 1) * 64 + lane]);
+    auto tile_out = [&](int j, const OpN<3> (&f)[3]) {
+        f32x4 o = zero_f4();
+#pragma unroll
+        for (int p = 0; p < 3; ++p) o = mma_n<3>(f[p], bu[p], o);
+        const int m = fd.tile_map[wave + W * j];
+        const mep_rf_front_out& q = fd.out[m >> 8];
+        if (tok < ntok) *reinterpret_cast<MEP_G f32x4*>(row_ptr(q.y, tok) + 16 * (m & 255) + 4 * g) = o;
+    };
+    for (int j = 0; j < nj; j += 2) {
+        frag2(j + 1, fb);
+        tile_out(j, fa);
+        if (j + 1 >= nj) break;
+        frag2(j + 2, fa);
+        tile_out(j + 1, fb);
+    }
+}
+
 template <typename F>
 int dispatch_rfw(int D, int FD, F&& f) {
 #define MEP_RFW_CASE(DD, FF) \
@@ -1039,6 +1135,19 @@ extern "C" int mep_wgemm_ws(const mep_gemm_desc* descs, int n_desc, int max_ntok
     MEP_WGS(12, 3, 0); MEP_WGS(6, 3, 1); MEP_WGS(3, 3, 2); MEP_WGS(6, 6, 3); MEP_WGS(3, 6, 4); MEP_WGS(3, 10, 5);
 #undef MEP_WGS
     return mep_check_launch("mep_wgemm_ws");
+}
+
+extern "C" int mep_rfw_front(const mep_rf_front_desc* descs, int n_desc, int max_tiles, int npk_u, mep_stream_t stream) {
+    if (n_desc <= 0 || max_tiles <= 0) return 0;
+    const dim3 grid(max_tiles, n_desc), block(384);
+    hipStream_t st = (hipStream_t)stream;
+    switch (npk_u) {
+        case 2: hipLaunchKernelGGL(k_rfw_front<2>, grid, block, 0, st, descs); break;
+        case 3: hipLaunchKernelGGL(k_rfw_front<3>, grid, block, 0, st, descs); break;
+        case 10: hipLaunchKernelGGL(k_rfw_front<10>, grid, block, 0, st, descs); break;
+        default: mep_set_error("mep_rfw_front: npk_u in {2, 3, 10}"); return MEP_EINVAL;
+    }
+    return mep_check_launch("mep_rfw_front");
 }
 
 extern "C" int mep_rfw_epi_fwd(const mep_rf_epi_desc* descs, int n_desc, int max_tiles, int D, int FD,

@@ -30,6 +30,12 @@ from ._lib import (AttnBwdDesc, AttnDesc, ColsumDesc, DescArray, GemmDesc, PoolD
 from .trimodal import CHAINS, MODS, TIME_ORDER, UNIFY_NAMES, _norm_args, cdiv, crows, make_wgrad, rows
 
 RF_SPLITQ = _lib.switch('MEP_RF_SPLITQ', '1') != '0'   # attention backward: query tiles over 4 waves
+# unify + projections of each modality in one launch (mep_rfw_front) up to RF_FRONT_MAX_TILES
+# 16-token tiles per step (cfg2's chain, 200: 27.5 -> 19.7 us); larger plans keep the GEMM
+# launches (State_Transfer, 3600 tiles: 196 us on mep_wgemm_ws against 373 us on the front kernel,
+# whose per-tile weight streaming from L2 grows with the tile count); 0: never
+RF_FRONT = _lib.switch('MEP_RF_FRONT', '1') != '0'
+RF_FRONT_MAX_TILES = 1024
 
 NC = 6  # State_Transfer classes (realformer.py:268-269)
 POS_NAMES = {'l': 'linguistic_position', 'v': 'visual_position', 'a': 'acoustic_position'}
@@ -206,6 +212,37 @@ class RealformerPlan:
         return rows(t, blk['Tk'], blk['Tk'] * 2 * D, 2 * D, which * D)
 
     # ------------------------------------------------------------------ descriptors
+    def _build_front(self, ud, pd, dev):
+        """mep_rfw_front launches (unify + the projections of its output in one kernel per
+        modality) when every modality's launch fits the kernel's contract; else self.front = None
+        and the forward runs the unify and projection GEMM launches"""
+        self.front = None
+        if not RF_FRONT or self.spec.D != 96 or sum(cdiv(d.ntok, 16) for d in ud) > RF_FRONT_MAX_TILES:
+            return
+        groups = {}
+        for dsc in ud:
+            m = next(k for k in self.spec.mods if dsc.y.ptr == self.U[k].data_ptr())
+            outs = [q for q in pd if q.x.ptr == self.U[m].data_ptr()]
+            npk = -(-dsc.K // 32)
+            tiles = sum(q.N // 16 for q in outs)
+            ok = (npk in (2, 3, 10) and dsc.N == 96 and not dsc.relu and not dsc.accumulate and
+                  dsc.x.ptr in self.x_padded and 0 < len(outs) <= _lib.RF_FRONT_MAX_OUT and
+                  6 <= tiles <= _lib.RF_FRONT_MAX_TILES and
+                  all(q.K == 96 and q.N % 16 == 0 and q.alpha == 1.0 and not (q.bias or q.table or q.accumulate or q.relu)
+                      for q in outs))
+            if not ok:
+                return
+            fd = _lib.RfFrontDesc(unify=dsc, n_out=len(outs), n_tiles=tiles)
+            t = 0
+            for o, q in enumerate(outs):
+                fd.out[o] = _lib.RfFrontOut(w=q.w, y=q.y, N=q.N)
+                for lt in range(q.N // 16):
+                    fd.tile_map[t] = (o << 8) | lt
+                    t += 1
+            groups.setdefault(npk, []).append((fd, dsc.ntok))
+        self.front = [(DescArray(_lib.RfFrontDesc, [fd for fd, _ in g], dev), cdiv(max(n for _, n in g), 16), npk)
+                      for npk, g in sorted(groups.items())]
+
     def _attn_desc(self, blk):
         sp, fl, D = self.spec, self.flat, self.spec.D
         prev = self._blk(blk['j'], blk['i'] - 1) if blk['i'] > 0 else None
@@ -337,6 +374,7 @@ class RealformerPlan:
                 dsc.w = self.wparts.data_ptr() + off
             for b, off in zip(self.blocks, epi_off):
                 b['wparts'] = self.wparts.data_ptr() + off
+            self._build_front(ud, pd, dev)
             for b, nxt, o_fwd, o_bwd in fused:
                 b['wq_next'] = self.wparts.data_ptr() + o_fwd
                 b['qp_next'] = crows(nxt['QP'], nxt['Tq'], D)
@@ -503,8 +541,12 @@ class RealformerPlan:
         ex = (sp.D, sp.FD)
         if self.rfw:
             launch('mep_wsplit', self.d_wsplit, self.t_wsplit, stream)
-        self._gemm(self.d_unify, self.t_unify, stream)
-        self._gemm(self.d_proj, self.t_proj, stream)
+        if getattr(self, 'front', None):
+            for descs, tiles, npk in self.front:
+                _lib.call('mep_rfw_front', descs.ptr, descs.n, tiles, npk, stream=stream)
+        else:
+            self._gemm(self.d_unify, self.t_unify, stream)
+            self._gemm(self.d_proj, self.t_proj, stream)
         for i in range(nl):
             if i > 0:
                 self._gemm(self.d_q[i], self.t_epi[i], stream)

@@ -33,7 +33,7 @@ BF16_PEAK = 2.5e15
 ATTN_FWD_PEAK = 4.0 / (2.0 * (6 + 6) / BF16_PEAK)
 ATTN_BWD_PEAK = 10.0 / (2.0 * (4 + 4 + 4 + 4 + 3) / BF16_PEAK)
 COMPUTE_PEAK = {'mep_block_epi_fwd': BF16_PEAK / 6, 'mep_block_epi_bwd': BF16_PEAK / 6, 'mep_wgrad': BF16_PEAK / 6,
-                'mep_tgemm': BF16_PEAK / 6, 'mep_wgemm': BF16_PEAK / 6, 'mep_wgemm_ws': BF16_PEAK / 6,
+                'mep_tgemm': BF16_PEAK / 6, 'mep_wgemm': BF16_PEAK / 6, 'mep_wgemm_ws': BF16_PEAK / 6, 'mep_rfw_front': BF16_PEAK / 6,
                 'mep_rfw_epi_fwd': BF16_PEAK / 6, 'mep_rfw_epi_bwd': BF16_PEAK / 6,
                 'mep_attn_fwd': ATTN_FWD_PEAK, 'mep_attn_bwd': ATTN_BWD_PEAK}
 
@@ -122,23 +122,26 @@ def rf_launch_costs(plan):
     # the launcher of each token-GEMM group (rfw: mep_wgemm_ws for large launches, else mep_wgemm)
     G_UNIFY, G_PROJ = plan.gemm_launcher(plan.d_unify), plan.gemm_launcher(plan.d_proj)
     G_IN = plan.gemm_launcher(plan.d_ingrad_all) if rfw else G_PROJ
+    front = bool(getattr(plan, 'front', None))
+    if front:   # mep_rfw_front: the projections read U from registers, not HBM
+        G_UNIFY = G_PROJ = 'mep_rfw_front'
     EPI_F, EPI_B = ('mep_rfw_epi_fwd', 'mep_rfw_epi_bwd') if rfw else ('mep_rf_epi_fwd', 'mep_rf_epi_bwd')
 
-    def gemm(name, ntok, N, K, accumulate=False, table=0):
-        add(name, 2 * ntok * N * K, 4 * (ntok * K + ntok * N * (2 if accumulate else 1) + N * K + table))
+    def gemm(name, ntok, N, K, accumulate=False, table=0, x_read=True):
+        add(name, 2 * ntok * N * K, 4 * (ntok * K * x_read + ntok * N * (2 if accumulate else 1) + N * K + table))
 
     for m in sp.mods:                                          # unify + position table
         gemm(G_UNIFY, plan.ntok[m], D, sp.dims[m], table=plan.T[m] * D)
     for blk in plan.blocks:
         Tq, Tk, nq, nk = blk['Tq'], blk['Tk'], blk['nq'], blk['nk']
-        gemm(G_PROJ, nk, 2 * D, D)                             # [K | V] = U [W_k; W_v]^T
+        gemm(G_PROJ, nk, 2 * D, D, x_read=not front)           # [K | V] = U [W_k; W_v]^T
         if rfw and blk['i'] > 0:
             # fused into the previous layer's epilogue launches (q = that layer's output):
             # Q = q W_q^T after its LN2, dq_in += dQ W_q before its LN2 backward
             add(EPI_F, 2 * nq * D * D, 4 * nq * D + 4 * D * D)
             add(EPI_B, 2 * nq * D * D, 4 * nq * D + 4 * D * D)
         else:
-            gemm(G_PROJ, nq, D, D)                             # Q = q W_q^T
+            gemm(G_PROJ, nq, D, D, x_read=not front)           # Q = q W_q^T
             gemm(G_IN, nq, D, D, accumulate=True)              # dq_in += dQ W_q
         gemm(G_IN, nk, D, 2 * D)                               # dkv_in = [dK | dV] [W_k; W_v]
         r_in = 1 if blk['i'] > 0 else 0

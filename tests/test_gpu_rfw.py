@@ -218,3 +218,41 @@ def test_rfw_fused_query_projection(cuda):
     out_r = torch.nn.functional.layer_norm(h_r + dd(bb) * f_r, (D,), dd(l2w), dd(l2b), 1e-5)
     assert_close(out, out_r.cpu().numpy(), 1e-4, 1e-6, 'out')
     assert_close(f1, f1_r.cpu().numpy(), 1e-4, 1e-6, 'f1')
+
+
+@pytest.mark.parametrize('family', ['chain', 'state'])
+def test_rfw_front_matches_gemm_launches(family, cuda):
+    """mep_rfw_front (unify + every projection of U in one launch per modality) writes U, [K | V]
+    and the layer-0 Q bit-identical to the mep_wgemm / mep_wgemm_ws launches it replaces: the
+    cfg2 text chain (d = 300) and a State_Transfer plan (d = 300 / 35 / 74, three launches)."""
+    from mep_amd import realformer as rf
+    from mep_amd import rf_plan
+    torch.manual_seed(11)
+    B, P, T = 8, 3, 50
+    if family == 'chain':
+        mc = rf.Multi_class(l_dim=300, v_dim=35, a_dim=74, dim=96, l_len=T, v_len=T, a_len=T, n_heads=6,
+                            n_layers=2, ffn=2).to(cuda)
+        runner, PP = mc.mep_chain_runner(2, cuda), 1
+        feats = (torch.randn(B, T, 300, device=cuda), torch.zeros(0, device=cuda), torch.zeros(0, device=cuda))
+        masks = (torch.ones(B, T, device=cuda), torch.zeros(0, device=cuda), torch.zeros(0, device=cuda))
+    else:
+        st = rf.State_Transfer(300, 35, 74, 96, T, T, T, 6, 2, 2).to(cuda)
+        runner, PP = st.mep_runner(cuda), P
+        feats = tuple(torch.randn(B, P, T, d, device=cuda) for d in (300, 35, 74))
+        masks = tuple((torch.rand(B, P, T, device=cuda) > 0.2).float() for _ in range(3))
+    outs = []
+    for on in (True, False):
+        old = rf_plan.RF_FRONT, rf_plan.RF_FRONT_MAX_TILES
+        rf_plan.RF_FRONT, rf_plan.RF_FRONT_MAX_TILES = on, 1 << 30
+        try:
+            plan = rf_plan.RealformerPlan(runner.spec, runner.flat, B, PP, cuda)
+        finally:
+            rf_plan.RF_FRONT, rf_plan.RF_FRONT_MAX_TILES = old
+        assert bool(plan.front) == on
+        plan.set_inputs(*feats, *masks)
+        plan.forward(grad=False)
+        torch.cuda.synchronize()
+        outs.append([plan.U[m].clone() for m in plan.spec.mods] +
+                    [b['KV'].clone() for b in plan.blocks] + [b['QP'].clone() for b in plan.blocks if b['i'] == 0])
+    for i, (a, b) in enumerate(zip(*outs)):
+        assert torch.equal(a, b), 'tensor %d: max |diff| %.3g' % (i, (a - b).abs().max().item())
