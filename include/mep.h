@@ -306,6 +306,10 @@ typedef struct {
      * LN2, qp_next = out Wq_next^T (wq_next = mep_wsplit parts of Wq_next [D][D]) */
     uint64_t wq_next;
     mep_rows qp_next;
+    /* mep_rfw_epi_fwd, optional (zero.ptr 0: off): [ntok, D] rows set to zero for the tile's
+     * tokens (the realformer plan's accumulated attention dq, cleared in the forward instead of
+     * by a separate fill) */
+    mep_rows zero;
 } mep_rf_epi_desc;
 int mep_rf_epi_fwd(const mep_rf_epi_desc* descs, int n_desc, int max_tiles, int D, int FD, mep_stream_t stream);
 

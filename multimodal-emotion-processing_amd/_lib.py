@@ -135,7 +135,7 @@ class RfEpiDesc(ctypes.Structure):
                 ('wp', u64), ('w1', u64), ('b1', u64), ('w2', u64), ('b2', u64),
                 ('ln1_w', u64), ('ln1_b', u64), ('ln2_w', u64), ('ln2_b', u64), ('a', u64), ('b', u64),
                 ('stats', u64), ('ntok', i32), ('D', i32), ('FD', i32), ('_pad', i32), ('wparts', u64),
-                ('wq_next', u64), ('qp_next', Rows)]
+                ('wq_next', u64), ('qp_next', Rows), ('zero', Rows)]
 
 
 class RfEpiBwdDesc(ctypes.Structure):

@@ -431,6 +431,12 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(WPE))) v
         store_owned<NI, W>(d.out, tok, out, wave);
         if (wave == 0 && g == 0)
             *reinterpret_cast<MEP_G f32x4*>(G<float>(d.stats) + 4 * (int64_t)tok) = f32x4{mean1, rstd1, mean2, rstd2};
+        if (d.zero.ptr) {   // the backward's accumulated rows of these tokens, cleared for this step
+            f32x4 z[JI];
+#pragma unroll
+            for (int j = 0; j < JI; ++j) z[j] = zero_f4();
+            store_mine<NI, W>(d.zero, tok, z, wave);
+        }
     }
     MEP_RFW_STAMP(9);
 #ifdef MEP_RFW_TRACE

@@ -264,7 +264,8 @@ class RealformerPlan:
                          ln2_w=fl.ptr(p + 'norm2.weight'), ln2_b=fl.ptr(p + 'norm2.bias'),
                          a=fl.ptr(p + 'a'), b=fl.ptr(p + 'b'), stats=blk['estat'].data_ptr(),
                          ntok=blk['nq'], D=D, FD=sp.FD, wparts=blk.get('wparts', 0),
-                         wq_next=blk.get('wq_next', 0), qp_next=blk.get('qp_next', Rows()))
+                         wq_next=blk.get('wq_next', 0), qp_next=blk.get('qp_next', Rows()),
+                         zero=crows(blk['dQP'], Tq, D) if self.rfw else Rows())
 
     def _epi_bwd_desc(self, blk):
         D, Tq, FD = self.spec.D, blk['Tq'], self.spec.FD
@@ -591,7 +592,8 @@ class RealformerPlan:
             launch('mep_pool_bwd', self.d_pool, self.t_poolb, stream)
         elif ext_dout is not None:
             self.dout_chain.copy_(ext_dout.reshape(self.dout_chain.shape))
-        self.dQP_all.zero_()
+        if not self.rfw:
+            self.dQP_all.zero_()   # (rfw: cleared by the forward epilogues, mep_rf_epi_desc.zero)
         for i in reversed(range(nl)):
             launch('mep_rfw_epi_bwd' if self.rfw else 'mep_rf_epi_bwd', self.d_epib[i], self.t_epib[i], stream, extra=ex)
             launch('mep_attn_bwd', self.d_attnb[i], self.t_attnb[i], stream, threads=self.f_attnb[i])
