@@ -88,7 +88,7 @@ int mep_gemm(const mep_gemm_desc* descs, int n_desc, int max_tiles, mep_stream_t
 /* Unify projection: the forward bias-free Linear of Unify_Dimension (cmu-mosei/run.py:210-214,
  * Ren-MME/run.py:161-166) on the same descriptor, restricted to w_nt = 1, N in {16, 32, 48, 64,
  * 96, 128}, no bias / relu / accumulate, alpha = 1 (table allowed), 16-byte aligned output rows.
- * The weight is staged in LDS when N * (16 * ceil(K / 16) + 4) <= 30720 floats; otherwise it is
+ * The weight is staged in LDS when N * (16 * ceil(K / 16) + 8) <= 30720 floats; otherwise it is
  * read from L2 and needs K % 16 == 0 and 16-byte aligned W and X rows.  `descs` holds the n_desc
  * descriptors FOLLOWED BY n_wg int32 task entries (descriptor << 20 | workgroups of that
  * descriptor << 10 | workgroup index), one per workgroup of the flat grid; a descriptor's

@@ -816,7 +816,7 @@ __global__ __launch_bounds__(256) void k_wgrad_reduce(const mep_wgrad_desc* __re
 // ahead of their MFMAs.  Flat grid: workgroup w runs map[w] = desc << 20 | n_wg << 10 | index.
 constexpr int UN_WAVES = 8;
 constexpr int UN_THREADS = 64 * UN_WAVES;
-constexpr int UN_LDS = 30720;   // floats (120 KB): W [N][Kp + 4] when N * (Kp + 4) fits
+constexpr int UN_LDS = 30720;   // floats (120 KB): W [N][Kp + 8] when N * (Kp + 8) fits
 constexpr int UN_PF = 8;        // X fragments (k blocks) in flight per lane
 #ifndef MEP_UN_STAGE1
 #define MEP_UN_STAGE1 1         // the whole weight's loads in flight per 320-column pass (0: 4 rows at a time, 18.0 vs 16.5 us at cfg3)
@@ -1108,7 +1108,10 @@ __global__ __launch_bounds__(UN_THREADS) void k_unify(const mep_gemm_desc* __res
         return;
     }
     lfloat* wl = (lfloat*)&smem[0];
-    const int N = d.N, K = d.K, KB = (K + 15) >> 4, ldl = 16 * KB + 4;
+    // rows of 16 KB + 8 floats: a row stride of 2 mod 4 sixteen-byte units puts every lane group of
+    // the fragment reads' ds_read_b128 ({0-3, 12-15, 20-27}, ...: rows c, units g) on 16 distinct
+    // bank quads (+ 4 floats: two rows per quad, 2-way conflicts -- 0.41 of the kernel's LDS cycles)
+    const int N = d.N, K = d.K, KB = (K + 15) >> 4, ldl = 16 * KB + 8;
     const bool wlds = N * ldl <= UN_LDS;
     if (wlds) {   // W [N][K] -> LDS rows of ldl floats, zero past K
 #if MEP_UN_STAGE1

@@ -58,6 +58,13 @@ POOL_FOLD = _lib.switch('MEP_POOL_FOLD', '1') != '0'
 # took the cfg3 attention backward from 36 to 641 us
 SUM_FOLD = _lib.switch('MEP_SUM_FOLD', '0') == '1'
 FWD_SPLITQ = _lib.switch('MEP_FWD_SPLITQ', '0') == '1'
+# single-process backward: the block-weight gradients (mep_wgrad of bucket A, which read only the
+# epilogue backward's outputs) on a side stream, concurrent with the attention backward and the
+# per-modality sums; the unify-weight launch after them, one reduction for both (captured graphs
+# run the two branches concurrently).  Off by default: measured slower -- each launch's persistent
+# grid fills every CU, so the branches contend instead of filling each other's gaps (cfg3 fp32
+# 0.234 -> 0.259 ms per step, attention backward 37 -> 59 us; cfg5 1.61 -> 1.74 ms)
+OVERLAP_WGRAD = _lib.switch('MEP_OVERLAP_WGRAD', '0') == '1'
 
 
 def wgrad_geometry(N, ktot, bf16=False):
@@ -229,7 +236,7 @@ def make_unify(descs, dev, n_wg=_lib.N_CU):
         assert d.bias == 0 and d.alpha == 1.0 and d.y.ptr % 16 == 0 and d.y.sB % 4 == 0 and d.y.sT % 4 == 0
         kb = cdiv(d.K, 16)
         xv = d.K % 4 == 0 and d.x.ptr % 16 == 0 and d.x.sB % 4 == 0 and d.x.sT % 4 == 0
-        if d.N * (16 * kb + 4) > UN_LDS:   # weight read from L2: 16-byte fragments, no k tail
+        if d.N * (16 * kb + 8) > UN_LDS:   # weight read from L2: 16-byte fragments, no k tail
             assert d.K % 16 == 0 and d.ldw % 4 == 0 and d.w % 16 == 0 and xv, 'mep_unify: unsupported shape'
         assert 4 * ((cdiv(d.ntok, d.x.T) - 1) * d.x.sB + (d.x.T - 1) * d.x.sT + d.K) < 2 ** 31
         ntiles.append(cdiv(d.ntok, 16))
@@ -583,6 +590,10 @@ class TriModalPlan:
                     r0 += tiles[m]
             self.d_ulnb = DescArray(LnDesc, lb, dev)
         self._build_grad_descriptors()
+        # the overlapped backward needs a device with concurrent streams and a split with work on
+        # both sides (bucket A = the block weights, B = the unify weights)
+        self.overlap = (OVERLAP_WGRAD and self.device.type == 'cuda' and not self.sum_fold
+                        and 0 < self._n_block_items < len(self._wgrad_items))
 
     def _attn_desc(self, blk):
         sp, fl, D = self.spec, self.flat, self.spec.D
@@ -766,6 +777,27 @@ class TriModalPlan:
         self.head.ext_dlogits = 0
         _lib.call('mep_head_fwd_bwd', ctypes.byref(self.head), stream=stream)
 
+    def _build_overlap(self):
+        """The overlapped backward's launches: bucket A / B weight gradients with the fused launch's
+        token chunk (every gradient the same sum in the same order as one launch, bit for bit) and
+        one reduction descriptor array over both."""
+        if getattr(self, '_ovl', None) is not None:
+            return self._ovl
+        dev, items, nb = self.device, self._wgrad_items, self._n_block_items
+        tps = wgrad_chunk(items, wg_target(self.bf16), bf16=self.bf16)
+        wa = make_wgrad(items[:nb], dev, tok_per_split=tps, bf16=self.bf16)
+        wb = make_wgrad(items[nb:], dev, tok_per_split=tps, bf16=self.bf16)
+        red = DescArray(WgradDesc, wa[1].items + wb[1].items, dev)
+        self._ovl = (wa, wb, red, max(wa[3], wb[3]), torch.cuda.Stream(device=dev))
+        return self._ovl
+
+    def _reduce_args(self):
+        """(wgrad descriptor array, reduce tiles) of the step's mep_reduce_grads launch"""
+        if self.overlap:
+            _, _, red, t_red, _ = self._build_overlap()
+            return red, t_red
+        return self.d_wgrad, self.t_wgred
+
     def backward(self, ext_dlogits=None, stream=None):
         """Backward from the fused-loss head partials, or from external dlogits [B, NC].
         Writes every parameter gradient into the flat gradient buffer (flat.grad) and the batch
@@ -778,17 +810,33 @@ class TriModalPlan:
             self.head.ext_dlogits = 0
         if not self.pool_fold:
             launch("mep_pool_bwd", self.d_pool, self.t_poolb, stream)
+        ovl = self._build_overlap() if self.overlap else None
+        main = side = None
         for i in reversed(range(nl)):
             launch('mep_block_epi_bwd', self.d_epib[i], self.t_epi[i], stream, threads=sp.D | self.prec)
+            if ovl is not None and i == 0:
+                # every block-weight operand is final here: bucket A's weight gradients on the side
+                # stream while the attention backward and the sums run on this one
+                (_, da, ta, _), side = ovl[0], ovl[4]
+                main = stream if stream is not None else torch.cuda.current_stream()
+                side.wait_stream(main)
+                with torch.cuda.stream(side):
+                    launch('mep_wgrad', da, ta, side)
             launch('mep_attn_bwd', self.d_attnb[i], self.t_attnb[i], stream, threads=self.f_attnb[i] | self.prec)
         if not self.sum_fold:
             launch('mep_sum_rows', self.d_sum, self.t_sum, stream)
         if sp.unify_norm:
             launch('mep_layernorm_bwd', self.d_ulnb, cdiv(max(self.ntok.values()), 64), stream)
-        launch('mep_wgrad', self.d_wgrad, self.t_wgrad, stream)
+        if ovl is not None:
+            _, db, tb, _ = ovl[1]
+            launch('mep_wgrad', db, tb, stream)
+            main.wait_stream(side)
+        else:
+            launch('mep_wgrad', self.d_wgrad, self.t_wgrad, stream)
         # weight-gradient split sums, LayerNorm / residual-coefficient column sums and the head
         # parameter sums: one launch
-        _lib.call('mep_reduce_grads', self.d_wgrad.ptr, self.d_wgrad.n, self.t_wgred, self.d_colsum.ptr,
+        red, t_red = self._reduce_args()
+        _lib.call('mep_reduce_grads', red.ptr, red.n, t_red, self.d_colsum.ptr,
                   self.d_colsum.n, self.t_colsum, ctypes.byref(self.head), *self.head_grads, *_norm_args(self),
                   stream=stream)
 
@@ -796,8 +844,8 @@ class TriModalPlan:
 
     def reduce_grid(self):
         """blocks of the backward's mep_reduce_grads launch (the optimizer's folded norm partials)"""
-        return _lib.lib().mep_reduce_grads_grid(self.d_wgrad.n, self.t_wgred, self.d_colsum.n, self.t_colsum,
-                                                ctypes.byref(self.head))
+        red, t_red = self._reduce_args()
+        return _lib.lib().mep_reduce_grads_grid(red.n, t_red, self.d_colsum.n, self.t_colsum, ctypes.byref(self.head))
 
     def advance_seed(self, stream=None):
         _lib.call('mep_seed_advance', ctypes.c_void_p(self.seed.data_ptr()), stream=stream)
