@@ -32,7 +32,7 @@ extern "C" {
 #endif
 
 #define MEP_EINVAL (-1000)
-#define MEP_ABI_VERSION 3
+#define MEP_ABI_VERSION 4
 
 typedef void* mep_stream_t; /* a hipStream_t */
 
@@ -254,6 +254,10 @@ typedef struct {
                             site (0: xp, 1: out) -- lane (c, g) of the tile's wave, bit 4 i + r =
                             feature 16 i + 4 g + r of token 16 tile + c -- and the backward reads
                             them instead of re-hashing (the same masks; ABI 3) */
+    uint64_t image;      /* optional (0: none): the forward's LDS weight image for this block, built
+                            by mep_epi_images (mep_epi_image_bytes(D, 0) bytes): the workgroups
+                            copy it into LDS by LDS-DMA instead of splitting Wp / Wm themselves
+                            (ABI 4) */
 } mep_epi_desc;
 /* D (32/64/96/128, shared by every descriptor of the launch) selects the compiled variant.
  * Geometry: max_tiles = workgroups PER DESCRIPTOR; each workgroup (512 threads) stages its block's
@@ -282,8 +286,19 @@ typedef struct {
     uint64_t pool_dpooled;   /* [B][2 * pool_C] floats (mean part, then max part) */
     uint64_t pool_argmax;    /* [B][pool_C] int32 */
     int32_t  pool_C, pool_Tq, pool_t0, pool_col;
+    uint64_t image;          /* optional (0: none): the backward's LDS weight image (Wm^T, Wp^T
+                                split), mep_epi_image_bytes(D, 1) bytes, built by mep_epi_images */
 } mep_epi_bwd_desc;
 int mep_block_epi_bwd(const mep_epi_bwd_desc* descs, int n_desc, int max_tiles, int D, mep_stream_t stream);
+/* The epilogues' weight images, built once per step instead of once per workgroup: for every
+ * descriptor, f.image (when nonzero) receives the forward's LDS image of Wp / Wm and image (when
+ * nonzero) the backward's of Wm^T / Wp^T -- the exact bytes the kernels would stage (bf16 parts of
+ * the fp32 weights in the split.h layouts), so results are bit-identical with and without images.
+ * D as mep_block_epi_fwd (| MEP_PREC_BF16).  mep_epi_image_bytes(D, which): bytes of the forward
+ * (which = 0) / backward (1) image, 0 when that configuration stages in the kernel only (two-phase
+ * kernels, dropout forward at D = 96 fp32: f.image is ignored there). */
+int mep_epi_images(const mep_epi_bwd_desc* descs, int n_desc, int D, mep_stream_t stream);
+int mep_epi_image_bytes(int D, int which);
 
 /* ---------------------------------------------------------------- realformer block epilogue
  * others/realformer.py:182-209 after the attention core (x = attention output, q = block input):

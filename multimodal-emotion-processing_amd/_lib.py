@@ -85,14 +85,14 @@ class EpiDesc(ctypes.Structure):
     _fields_ = [('q', Rows), ('x', Rows), ('xp', Rows), ('z', Rows), ('out', Rows),
                 ('wp', u64), ('wm', u64), ('ln_w', u64), ('ln_b', u64), ('stats', u64), ('seed', u64),
                 ('ntok', i32), ('D', i32), ('drop_p', f32), ('drop_stream', i32), ('out_h', Rows),
-                ('drop_bits', u64)]
+                ('drop_bits', u64), ('image', u64)]
 
 
 class EpiBwdDesc(ctypes.Structure):
     _fields_ = [('f', EpiDesc), ('dout', Rows), ('dout2', Rows), ('dz', Rows), ('dxp', Rows), ('dx', Rows),
                 ('dq', Rows), ('ln_partial', u64), ('dq_accumulate', i32), ('pool_T', i32),
                 ('pool_dpooled', u64), ('pool_argmax', u64), ('pool_C', i32), ('pool_Tq', i32),
-                ('pool_t0', i32), ('pool_col', i32)]
+                ('pool_t0', i32), ('pool_col', i32), ('image', u64)]
 
 
 class LnDesc(ctypes.Structure):
@@ -287,6 +287,8 @@ SIGNATURES.update({
     'mep_wgemm': [P, i32, i32, i32, P],
     'mep_wgemm_ws': [P, i32, i32, i32, i32, i32, P],
     'mep_rfw_front': [P, i32, i32, i32, P],
+    'mep_epi_images': [P, i32, i32, P],
+    'mep_epi_image_bytes': [i32, i32],
     'mep_abi_version': [],
     'mep_rf_rows': [i32, i32],
     'mep_last_error': [ctypes.c_char_p, ctypes.c_size_t],
@@ -297,7 +299,7 @@ SIGNATURES.update({
 })
 
 _LIB = None
-ABI_VERSION = 3   # include/mep.h MEP_ABI_VERSION
+ABI_VERSION = 4   # include/mep.h MEP_ABI_VERSION
 
 
 def lib():

@@ -137,10 +137,31 @@ MEP_DEV void stage_cols_t(lfloat* dst, int L, const gfloat* src) {
 MEP_DEV float4 f4(const f32x4 v) { return make_float4(v[0], v[1], v[2], v[3]); }
 
 // tiles [t_begin, t_end) of 16 tokens owned by this workgroup (contiguous range per workgroup)
-MEP_DEV bool tile_range(int ntok, int& t_begin, int& t_end) {
+// The epilogue grid is (slices, descriptors).  XCD-aware order (MEP_EPI_XCD): workgroups are
+// dispatched to the 8 XCDs round-robin by linear id, so id -> (descriptor, slice) is remapped to
+// give XCD x a contiguous run of the descriptor-major work list -- every XCD then stages the
+// weights of one or two blocks instead of all of them, and its L2 serves the other workgroups'
+// staging reads of those weights (the first reads of each block's weights come from MALL / HBM
+// once per XCD, not once per workgroup).
+#ifndef MEP_EPI_XCD
+#define MEP_EPI_XCD 1
+#endif
+MEP_DEV bool epi_slot(int& desc, int& slice) {
+    const int G = gridDim.x * gridDim.y, id = blockIdx.x + gridDim.x * blockIdx.y;
+    int unit = id;
+    if (MEP_EPI_XCD) {
+        // XCD x = id % 8 holds q + (x < r) of the G workgroups (G = 8 q + r): the x-th run
+        const int q = G / 8, r = G % 8, x = id % 8;
+        unit = x * q + min(x, r) + id / 8;
+    }
+    desc = unit / (int)gridDim.x;
+    slice = unit - desc * (int)gridDim.x;
+    return true;
+}
+MEP_DEV bool tile_range(int ntok, int slice, int& t_begin, int& t_end) {
     const int ntiles = (ntok + 15) >> 4;
     const int per = (ntiles + (int)gridDim.x - 1) / (int)gridDim.x;
-    t_begin = blockIdx.x * per;
+    t_begin = slice * per;
     t_end = min(ntiles, t_begin + per);
     return t_begin < t_end;
 }
@@ -269,6 +290,9 @@ MEP_DEV void epi_fwd_tiles(const mep_epi_desc& d, const AP& wp, const AM& wm, in
 // W[n][32p + 16 + 4g ..]; every load of the thread is issued before its first LDS write
 template <int R, int C, int NPART>
 MEP_DEV void stage_split_rows(const SplitW<R, C / 32, NPART>& dst, const gfloat* src) {
+#ifdef MEP_EPI_NOSTAGE   // timing-only development build: no weight staging (LDS left as it is)
+    return;
+#endif
     constexpr int NU = R * (C / 32) * 4;
     constexpr int PER = (NU + ETHREADS - 1) / ETHREADS;
     f32x4 v[PER][2];
@@ -296,6 +320,9 @@ MEP_DEV void stage_split_rows(const SplitW<R, C / 32, NPART>& dst, const gfloat*
 // threads take consecutive n (coalesced), loads issued before the LDS writes
 template <int R, int C, int NPART>
 MEP_DEV void stage_split_cols(const SplitW<C, R / 32, NPART>& dst, const gfloat* src) {
+#ifdef MEP_EPI_NOSTAGE
+    return;
+#endif
     constexpr int NP = R / 32, NU = C * NP * 4;
     constexpr int PER = (NU + ETHREADS - 1) / ETHREADS;
     float v[PER][8];
@@ -328,6 +355,22 @@ MEP_DEV void wg_store_barrier() {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
 }
+
+// A weight image built by mep_epi_images (global, BYTES a multiple of 1 KB: the exact LDS bytes
+// the staging below would write) into LDS by LDS-DMA: wave w copies the 1-KB chunks w, w + EWAVES,
+// ... (lane l: bytes 16 l .. 16 l + 15 of the chunk) without passing through registers.  The
+// caller waits (image_ready) before its barrier.
+template <int BYTES>
+MEP_DEV void dma_image(unsigned char* sm, uint64_t img) {
+    static_assert(BYTES % 1024 == 0, "epilogue weight images are whole 1-KB chunks");
+    typedef __attribute__((address_space(3))) void lvoid;
+    typedef __attribute__((address_space(3))) unsigned char lbyte;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const auto rs = __builtin_amdgcn_make_buffer_rsrc((void*)img, 0, BYTES, 0x00020000);
+    for (int ch = wave; ch < BYTES / 1024; ch += EWAVES)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lvoid*)((lbyte*)sm + ch * 1024), 16, 16 * lane, ch * 1024, 0, 0);
+}
+MEP_DEV void image_ready() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
 #ifdef MEP_EPI_TRACE
 // development build only (scripts/epi_trace.py): per-workgroup phase stamps, 8 words per workgroup
@@ -656,8 +699,13 @@ MEP_DEV void epi_fwd_one(const mep_epi_desc& d, unsigned char* sm, int t_begin, 
         for (int kb = 0; kb < KB; ++kb) dst[kb] = ld4a(r + 16 * kb);
     };
     if (t_begin + wave < t_end) { rows_of(d.x, t_begin + wave, ab); rows_of(d.q, t_begin + wave, bb); }
-    stage_split_rows<D, D, NWP>(wp, G<const float>(d.wp));
-    stage_split_rows<D, 2 * D, NWM>(wm, G<const float>(d.wm));
+    if (d.image) {
+        dma_image<WP::BYTES + WM::BYTES>(sm, d.image);
+        image_ready();
+    } else {
+        stage_split_rows<D, D, NWP>(wp, G<const float>(d.wp));
+        stage_split_rows<D, 2 * D, NWM>(wm, G<const float>(d.wm));
+    }
     __syncthreads();
     for (int tile = t_begin + wave; tile < t_end; tile += EWAVES) {
         const int tok = tile * 16 + c;
@@ -775,6 +823,11 @@ MEP_DEV void epi_fwd_wp2r(const mep_epi_desc& d, unsigned char* sm, int t_begin,
         const gfloat* r = W + (R2 + c) * D + 32 * pp + 4 * g;
         w2r[pp] = opn<3>(ld4w(r), ld4w(r + 16)).p[2];
     }
+    if (d.image) {
+        dma_image<E::BYTES>(sm, d.image);
+        image_ready();
+    } else {
+#ifndef MEP_EPI_NOSTAGE
     {   // Wp: unit (n, pp, g) = Wp[n][32 pp + 4 g ..], [.. + 16 ..] -> parts 0, 1 (and 2 for n < R2)
         constexpr int NU = D * NP * 4, PER = (NU + ETHREADS - 1) / ETHREADS;
         f32x4 v[PER][2];
@@ -822,6 +875,8 @@ MEP_DEV void epi_fwd_wp2r(const mep_epi_desc& d, unsigned char* sm, int t_begin,
                 for (int t = 0; t < 3; ++t) wm.put_part(t, n, pp, gg, lo.p[t], hi.p[t]);
             }
         }
+    }
+#endif
     }
     __syncthreads();
     for (int tile = t_begin + wave; tile < t_end; tile += EWAVES) {
@@ -933,8 +988,13 @@ MEP_DEV void epi_bwd_one(const mep_epi_bwd_desc& bd, unsigned char* sm, int t_be
         rstd = stats[2 * tc + 1];
     };
     if (t_begin + wave < t_end) fetch1(t_begin + wave);
-    stage_split_cols<D, 2 * D, NWM>(wmt, G<const float>(d.wm));
-    stage_split_cols<D, D, NWP>(wpt, G<const float>(d.wp));
+    if (bd.image) {
+        dma_image<WMT::BYTES + WPT::BYTES>(sm, bd.image);
+        image_ready();
+    } else {
+        stage_split_cols<D, 2 * D, NWM>(wmt, G<const float>(d.wm));
+        stage_split_cols<D, D, NWP>(wpt, G<const float>(d.wp));
+    }
     __syncthreads();
     for (int tile = t_begin + wave; tile < t_end; tile += EWAVES) {
         const int tok = tile * 16 + c;
@@ -1068,9 +1128,11 @@ template <int D, bool BF16> struct EpiOne {
 template <int D, bool BF16>
 __global__ __launch_bounds__(ETHREADS) __attribute__((amdgpu_waves_per_eu(MEP_EPI_WAVES))) void k_epi_fwd(const mep_epi_desc* __restrict__ descs) {
     using Geo = EpiGeo<D>;
-    const mep_epi_desc& d = descs[blockIdx.y];
+    int di, slice;
+    if (!epi_slot(di, slice)) return;
+    const mep_epi_desc& d = descs[di];
     int t_begin, t_end;
-    if (!tile_range(d.ntok, t_begin, t_end)) return;   // whole workgroup
+    if (!tile_range(d.ntok, slice, t_begin, t_end)) return;   // whole workgroup
     if constexpr (EpiOne<D, BF16>::FWD) {
         using E = EpiOne<D, BF16>;
         __shared__ __attribute__((aligned(16))) unsigned char sm1[E::FWD_BYTES];
@@ -1242,10 +1304,12 @@ MEP_DEV void epi_bwd_tiles(const mep_epi_bwd_desc& bd, const AM& wmt, const AP& 
 template <int D, bool BF16>
 __global__ __launch_bounds__(ETHREADS) __attribute__((amdgpu_waves_per_eu(MEP_EPI_WAVES))) void k_epi_bwd(const mep_epi_bwd_desc* __restrict__ descs) {
     using Geo = EpiGeo<D>;
-    const mep_epi_bwd_desc& bd = descs[blockIdx.y];
+    int di, slice;
+    if (!epi_slot(di, slice)) return;
+    const mep_epi_bwd_desc& bd = descs[di];
     const mep_epi_desc& d = bd.f;
     int t_begin, t_end;
-    if (!tile_range(d.ntok, t_begin, t_end)) return;
+    if (!tile_range(d.ntok, slice, t_begin, t_end)) return;
     if constexpr (EpiOne<D, BF16>::BWD) {
         using E = EpiOne<D, BF16>;
         __shared__ __attribute__((aligned(16))) unsigned char sm1[E::BWD_BYTES];
@@ -1273,6 +1337,93 @@ __global__ __launch_bounds__(ETHREADS) __attribute__((amdgpu_waves_per_eu(MEP_EP
     } else {
         __syncthreads();
         epi_bwd_tiles<D>(bd, am, WCols{G<const float>(d.wp), D, 0, 0}, t_begin, t_end);
+    }
+}
+
+// ---------------------------------------------------------------- weight images
+// mep_epi_images: the single-phase epilogues' LDS weight images, once per step.  Thread u of
+// descriptor blockIdx.y writes one 16-byte unit (all its parts) of the forward image (units 0 ..
+// FU-1: Wp then Wm, the staging order of epi_fwd_wp2r / epi_fwd_one) or of the backward image
+// (FU ..: Wm^T then Wp^T, epi_bwd_one's stage_split_cols), with the staging code's loads, split
+// and layout offsets -- the same bytes the workgroups would write into LDS.
+template <int D, bool BF16>
+struct EpiImg {
+    using E = EpiOne<D, BF16>;
+    static constexpr int NP = D / 32;
+    static constexpr int FU = E::FWD ? 3 * D * NP * 4 : 0, BU = E::BWD ? 3 * D * NP * 4 : 0;
+    static constexpr bool FWD_OK = E::FWD && E::FWD_BYTES % 1024 == 0;
+    static constexpr bool BWD_OK = E::BWD && E::BWD_BYTES % 1024 == 0;
+};
+
+template <typename L, int NPART>
+MEP_DEV void put_global(MEP_G unsigned char* img, int base, int n, int p, int g, f32x4 blk0, f32x4 blk1) {
+    const Parts<NPART> a = splitv<NPART>(blk0), b = splitv<NPART>(blk1);
+#pragma unroll
+    for (int t = 0; t < NPART; ++t)
+        *reinterpret_cast<MEP_G u32x4*>(img + base + L::off(t, n, p, g)) = u32x4{a.p[t][0], a.p[t][1], b.p[t][0], b.p[t][1]};
+}
+
+template <int D, bool BF16>
+__global__ __launch_bounds__(256) void k_epi_image(const mep_epi_bwd_desc* __restrict__ descs) {
+    using I = EpiImg<D, BF16>;
+    using E = typename I::E;
+    constexpr int NP = I::NP;
+    const mep_epi_bwd_desc& bd = descs[blockIdx.y];
+    const mep_epi_desc& d = bd.f;
+    int u = blockIdx.x * 256 + (int)threadIdx.x;
+    if (u < I::FU) {
+        if constexpr (I::FWD_OK) {
+            if (!d.image) return;
+            MEP_G unsigned char* img = G<unsigned char>(d.image);
+            const int wu = D * NP * 4;                 // Wp units; Wm units after them
+            const bool is_wp = u < wu;
+            const int v = is_wp ? u : u - wu, np2 = is_wp ? NP : 2 * NP, C = is_wp ? D : 2 * D;
+            const int gg = v & 3, pp = (v >> 2) % np2, n = (v >> 2) / np2;
+            const gfloat* src = G<const float>(is_wp ? d.wp : d.wm) + n * C + 32 * pp + 4 * gg;
+            const f32x4 b0 = ld4w(src), b1 = ld4w(src + 16);
+            if constexpr (E::FWD_WP2R) {
+                using W = EpiWp2r<D>;
+                if (is_wp) {
+                    const Parts<3> lo = splitv<3>(b0), hi = splitv<3>(b1);
+#pragma unroll
+                    for (int t = 0; t < 2; ++t)
+                        *reinterpret_cast<MEP_G u32x4*>(img + W::WP01::off(t, n, pp, gg)) =
+                            u32x4{lo.p[t][0], lo.p[t][1], hi.p[t][0], hi.p[t][1]};
+                    if (n < W::R2)
+                        *reinterpret_cast<MEP_G u32x4*>(img + W::WP01::BYTES + W::WP2::off(0, n, pp, gg)) =
+                            u32x4{lo.p[2][0], lo.p[2][1], hi.p[2][0], hi.p[2][1]};
+                } else {
+                    put_global<typename W::WM, 3>(img, W::WP01::BYTES + W::WP2::BYTES, n, pp, gg, b0, b1);
+                }
+            } else {
+                using WP = SplitW<D, NP, E::FWD_WP>;
+                using WM = SplitW<D, 2 * NP, E::FWD_WM>;
+                if (is_wp) put_global<WP, E::FWD_WP>(img, 0, n, pp, gg, b0, b1);
+                else put_global<WM, E::FWD_WM>(img, WP::BYTES, n, pp, gg, b0, b1);
+            }
+        }
+        return;
+    }
+    u -= I::FU;
+    if constexpr (I::BWD_OK) {
+        if (u >= I::BU || !bd.image) return;
+        MEP_G unsigned char* img = G<unsigned char>(bd.image);
+        using WMT = SplitW<2 * D, NP, E::BWD_WM>;
+        using WPT = SplitW<D, NP, E::BWD_WP>;
+        const int mu = 2 * D * NP * 4;                  // Wm^T units; Wp^T units after them
+        const bool is_wm = u < mu;
+        const int v = is_wm ? u : u - mu, C = is_wm ? 2 * D : D;
+        // stage_split_cols<D, C>: unit (n, pp, g) = W[32 pp + 4 g + j][n], W[32 pp + 16 + 4 g + j][n]
+        const int n = v % C, pg = v / C, gg = pg & 3, pp = pg >> 2;
+        const gfloat* src = G<const float>(is_wm ? d.wm : d.wp);
+        f32x4 b0, b1;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            b0[j] = src[(32 * pp + 4 * gg + j) * C + n];
+            b1[j] = src[(32 * pp + 16 + 4 * gg + j) * C + n];
+        }
+        if (is_wm) put_global<WMT, E::BWD_WM>(img, 0, n, pp, gg, b0, b1);
+        else put_global<WPT, E::BWD_WP>(img, WMT::BYTES, n, pp, gg, b0, b1);
     }
 }
 
@@ -1620,6 +1771,42 @@ extern "C" int mep_block_epi_bwd(const mep_epi_bwd_desc* descs, int n_desc, int 
     });
     if (rc) { mep_set_error("mep_block_epi_bwd: D must be 32, 64, 96 or 128"); return rc; }
     return mep_check_launch("mep_block_epi_bwd");
+}
+
+extern "C" int mep_epi_image_bytes(int D, int which) {
+    const bool bf16 = D & MEP_PREC_BF16;
+    int bytes = 0;
+    const int rc = dispatch_D(D & ~MEP_PREC_BF16, [&](auto dc) {
+        constexpr int DD = decltype(dc)::value;
+        auto get = [&](auto bc) {
+            using I = EpiImg<DD, decltype(bc)::value>;
+            using E = typename I::E;
+            bytes = which == 0 ? (I::FWD_OK ? E::FWD_BYTES : 0) : (I::BWD_OK ? E::BWD_BYTES : 0);
+        };
+        if (bf16) get(std::true_type{});
+        else get(std::false_type{});
+    });
+    return rc ? 0 : bytes;
+}
+
+extern "C" int mep_epi_images(const mep_epi_bwd_desc* descs, int n_desc, int D, mep_stream_t stream) {
+    if (n_desc <= 0) return 0;
+    const bool bf16 = D & MEP_PREC_BF16;
+    const int rc = dispatch_D(D & ~MEP_PREC_BF16, [&](auto dc) {
+        constexpr int DD = decltype(dc)::value;
+        auto go = [&](auto bc) {
+            constexpr bool BF = decltype(bc)::value;
+            using I = EpiImg<DD, BF>;
+            const int units = I::FU + I::BU;
+            if (units > 0)
+                hipLaunchKernelGGL((k_epi_image<DD, BF>), dim3((units + 255) / 256, n_desc), dim3(256), 0,
+                                   (hipStream_t)stream, descs);
+        };
+        if (bf16) go(std::true_type{});
+        else go(std::false_type{});
+    });
+    if (rc) { mep_set_error("mep_epi_images: D must be 32, 64, 96 or 128"); return rc; }
+    return mep_check_launch("mep_epi_images");
 }
 
 // max_tiles: forward = ceil(ntok / 4) (wave per row), backward = ceil(ntok / 64)

@@ -105,6 +105,8 @@ struct SplitW {
     static constexpr int BYTES = NPART * R * RS;
     __attribute__((address_space(3))) unsigned char* base;
     int row0;   // first row of the operand (output tile 0)
+    // byte offset of part t of unit (n, p, g) (the LDS image; global copies of it use the same)
+    MEP_DEV static int off(int t, int n, int p, int g) { return t * R * RS + n * RS + (4 * p + g) * 16; }
     MEP_DEV OpN<NPART> frag(int i, int p) const {
         const int lane = threadIdx.x & 63;
         const int off = (row0 + 16 * i + (lane & 15)) * RS + (4 * p + (lane >> 4)) * 16;
@@ -151,6 +153,7 @@ struct SplitWS {
         if constexpr (M == 4) return u ^ ((0x78 >> (2 * ((n >> 2) & 3))) & 3);   // [0, 2, 3, 1]
         else return u ^ ((n / M) & XM);
     }
+    MEP_DEV static int off(int t, int n, int p, int g) { return t * R * RS + n * RS + unit(n, 4 * p + g) * 16; }
     MEP_DEV OpN<NPART> frag(int i, int p) const {
         const int lane = threadIdx.x & 63;
         const int n = row0 + 16 * i + (lane & 15);

@@ -65,6 +65,15 @@ FWD_SPLITQ = _lib.switch('MEP_FWD_SPLITQ', '0') == '1'
 # grid fills every CU, so the branches contend instead of filling each other's gaps (cfg3 fp32
 # 0.234 -> 0.259 ms per step, attention backward 37 -> 59 us; cfg5 1.61 -> 1.74 ms)
 OVERLAP_WGRAD = _lib.switch('MEP_OVERLAP_WGRAD', '0') == '1'
+# the epilogues' weights split into their LDS images once per step (mep_epi_images, at the start of
+# the forward) and copied into LDS by LDS-DMA, instead of every workgroup splitting them.  Off by
+# default: the copy of the (1.5x larger) 3-part image takes as long as the staging it replaces
+# (cfg3 fp32 forward 30.5 vs 30.4 us, backward 34.3 vs 33.8, plus 5.4 us for the image launch;
+# bf16 -0.6 us per epilogue against 3.8 us) -- the staging is bound by moving the weights into every
+# CU, not by its split VALU
+EPI_IMAGE = _lib.switch('MEP_EPI_IMAGE', '0') == '1'
+# mep_unify workgroups in XCD-contiguous descriptor order (xcd_order); 0: descriptor-major by id
+UNIFY_XCD = _lib.switch('MEP_UNIFY_XCD', '1') != '0'
 
 
 def wgrad_geometry(N, ktot, bf16=False):
@@ -248,7 +257,18 @@ def make_unify(descs, dev, n_wg=_lib.N_CU):
         nw[i] -= 1
     assert all(0 < w < 1024 for w in nw) and len(descs) < 2048
     tasks = [(i << 20) | (w << 10) | k for i, w in enumerate(nw) for k in range(w)]
+    if UNIFY_XCD:
+        tasks = xcd_order(tasks)
     return DescArray(GemmDesc, descs, dev, tail=tasks), len(tasks)
+
+
+def xcd_order(work):
+    """work list -> launch order: workgroups go to the 8 XCDs round-robin by id, so XCD x (ids x,
+    x + 8, ...) receives the x-th contiguous run of the list (csrc/block.hip epi_slot): the
+    workgroups of one descriptor share an XCD and its L2 for the weight they stage"""
+    G = len(work)
+    q, r = divmod(G, 8)
+    return [work[(i % 8) * q + min(i % 8, r) + i // 8] for i in range(G)]
 
 
 def make_wgrad(items, dev, tok_per_split=None, bf16=False):
@@ -431,6 +451,13 @@ class TriModalPlan:
         blk['astat'] = torch.zeros(B, H, Tq, 2, **f32)
         blk['dKV'] = torch.zeros(nk, D, **self.act)
         blk['ln_partial'] = torch.zeros(cdiv(nq, 16), 2, D, **f32)   # one row per 16-token wave
+        if EPI_IMAGE:
+            # the epilogues' LDS weight images (mep_epi_images, once per step; 0 bytes: staged in
+            # the kernel)
+            for key, which in (('img_f', 0), ('img_b', 1)):
+                nb = _lib.lib().mep_epi_image_bytes(D | self.prec, which)
+                if nb:
+                    blk[key] = torch.zeros(nb, dtype=torch.uint8, device=self.device)
         if sp.drop_p > 0:
             # the forward epilogue's dropout keep bits, read by the backward (mep_epi_desc.drop_bits)
             blk['dbits'] = torch.zeros(cdiv(nq, 16) * 2 * 64, dtype=torch.int32, device=self.device)
@@ -590,6 +617,8 @@ class TriModalPlan:
                     r0 += tiles[m]
             self.d_ulnb = DescArray(LnDesc, lb, dev)
         self._build_grad_descriptors()
+        imgs = [self._epi_bwd_desc(b) for b in self.blocks if 'img_f' in b or 'img_b' in b]
+        self.d_img = DescArray(EpiBwdDesc, imgs, dev) if imgs else None
         # the overlapped backward needs a device with concurrent streams and a split with work on
         # both sides (bucket A = the block weights, B = the unify weights)
         self.overlap = (OVERLAP_WGRAD and self.device.type == 'cuda' and not self.sum_fold
@@ -619,7 +648,8 @@ class TriModalPlan:
                        stats=blk['estat'].data_ptr(), seed=self.seed_state.data_ptr(),
                        ntok=self.B * Tq, D=D, drop_p=self._drop, drop_stream=stream_id,
                        out_h=crows(blk['Qh'], Tq, D) if 'Qh' in blk else Rows(),
-                       drop_bits=blk['dbits'].data_ptr() if 'dbits' in blk else 0)
+                       drop_bits=blk['dbits'].data_ptr() if 'dbits' in blk else 0,
+                       image=blk['img_f'].data_ptr() if 'img_f' in blk else 0)
 
     def _epi_bwd_desc(self, blk):
         D, Tq = self.spec.D, blk['Tq']
@@ -638,7 +668,7 @@ class TriModalPlan:
                           dout2=crows(nxt['dQ'], Tq, D) if nxt is not None else Rows(),
                           dz=crows(blk['dZ'], Tq, D), dxp=crows(blk['dXP'], Tq, D), dx=crows(blk['dX'], Tq, D),
                           dq=crows(blk['dQ'], Tq, D), ln_partial=blk['ln_partial'].data_ptr(), dq_accumulate=0,
-                          **up)
+                          image=blk['img_b'].data_ptr() if 'img_b' in blk else 0, **up)
 
     def _attn_bwd_desc(self, blk):
         D = self.spec.D
@@ -765,6 +795,8 @@ class TriModalPlan:
         loss (row_loss, already scaled by 1/B); grad=True also runs the head backward
         (dpooled + head parameter partials) inside the same launch."""
         sp, nl = self.spec, self.spec.nl
+        if self.d_img is not None:
+            _lib.call('mep_epi_images', self.d_img.ptr, self.d_img.n, sp.D | self.prec, stream=stream)
         _lib.gemm('mep_unify', self.d_unify, self.t_unify, stream, prec=self.prec)
         if sp.unify_norm:
             launch('mep_layernorm_fwd', self.d_uln, cdiv(max(self.ntok.values()), 4), stream)
