@@ -372,6 +372,15 @@ MEP_DEV void dma_image(unsigned char* sm, uint64_t img) {
 }
 MEP_DEV void image_ready() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
+// the LayerNorm weight (and bias) into LDS with the weight staging (published by its barrier): the
+// per-tile LayerNorm then reads them from LDS instead of waiting on a global load at every tile's end
+template <int D, bool BIAS>
+MEP_DEV void stage_ln(lfloat* dst, const mep_epi_desc& d) {
+    const int t = threadIdx.x;
+    if (t < D) dst[t] = G<const float>(d.ln_w)[t];
+    else if (BIAS && t < 2 * D) dst[t] = G<const float>(d.ln_b)[t - D];
+}
+
 #ifdef MEP_EPI_TRACE
 // development build only (scripts/epi_trace.py): per-workgroup phase stamps, 8 words per workgroup
 // of the launch grid (x + gridDim.x * y): start, weight 1 staged, phase 1 done, weight 2 staged, end
@@ -698,6 +707,8 @@ MEP_DEV void epi_fwd_one(const mep_epi_desc& d, unsigned char* sm, int t_begin, 
 #pragma unroll
         for (int kb = 0; kb < KB; ++kb) dst[kb] = ld4a(r + 16 * kb);
     };
+    __shared__ __attribute__((aligned(16))) float lnp[2 * D];   // LayerNorm weight | bias
+    stage_ln<D, true>((lfloat*)lnp, d);
     if (t_begin + wave < t_end) { rows_of(d.x, t_begin + wave, ab); rows_of(d.q, t_begin + wave, bb); }
     if (d.image) {
         dma_image<WP::BYTES + WM::BYTES>(sm, d.image);
@@ -760,7 +771,7 @@ MEP_DEV void epi_fwd_one(const mep_epi_desc& d, unsigned char* sm, int t_begin, 
 #pragma unroll
             for (int i = 0; i < NI; ++i) {
                 const int col = 16 * i + 4 * g;
-                const f32x4 w = ld4w(G<const float>(d.ln_w) + col), b = ld4w(G<const float>(d.ln_b) + col);
+                const f32x4 w = ld4w((const lfloat*)lnp + col), b = ld4w((const lfloat*)lnp + D + col);
                 f32x4 y;
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
@@ -813,8 +824,11 @@ MEP_DEV void epi_fwd_wp2r(const mep_epi_desc& d, unsigned char* sm, int t_begin,
 #pragma unroll
         for (int kb = 0; kb < KB; ++kb) dst[kb] = ld4w(r + 16 * kb);
     };
-    f32x4 ab[KB];                    // x rows, one tile ahead
-    if (t_begin + wave < t_end) rows_of(d.x, t_begin + wave, ab);
+    MEP_EPI_STAMP(0);
+    __shared__ __attribute__((aligned(16))) float lnp[2 * D];   // LayerNorm weight | bias
+    stage_ln<D, true>((lfloat*)lnp, d);
+    f32x4 ab[KB], bb[KB];            // x rows and q rows, one tile ahead
+    if (t_begin + wave < t_end) { rows_of(d.x, t_begin + wave, ab); rows_of(d.q, t_begin + wave, bb); }
     const gfloat* W = G<const float>(d.wp);
     // the third part of the last 16 rows' fragments: unit (row R2 + c, k pair pp, group g)
     bf16x8 w2r[NP];
@@ -879,32 +893,43 @@ MEP_DEV void epi_fwd_wp2r(const mep_epi_desc& d, unsigned char* sm, int t_begin,
 #endif
     }
     __syncthreads();
+    MEP_EPI_STAMP(1);
     for (int tile = t_begin + wave; tile < t_end; tile += EWAVES) {
         const int tok = tile * 16 + c;
-        f32x4 bb[KB];                // q rows of this tile, loaded behind the xp product
-        rows_of(d.q, tile, bb);
         f32x4 xp[NI];
 #pragma unroll
         for (int i = 0; i < NI; ++i) xp[i] = zero_f4();
         // the six products in mma_nm<3, 3>'s order: w0x0, w1x0, w0x1, w1x1, w2x0, w0x2; operands
-        // are split one k pair at a time
+        // are split one k pair at a time; the weight fragments of step s + RING (steps (pp, i),
+        // pp-major) are read while step s's MFMAs run (MEP_TG_RING, as tgemm_n)
+        {
+            struct Frag { OpN<2> a; bf16x8 a2; };
+            auto frag = [&](int s) {
+                const int pp = s / NI, i = s % NI;
+                return Frag{wp.frag(i, pp), i < NI - 1 ? wp2.frag(i, pp).p[0] : w2r[pp]};
+            };
+            constexpr int S = NI * NP, RING = MEP_TG_RING > 0 ? (MEP_TG_RING < S ? MEP_TG_RING : S) : 1;
+            Frag ring[RING];
 #pragma unroll
-        for (int pp = 0; pp < NP; ++pp) {
-            const OpN<3> xs = opn<3>(ab[2 * pp], ab[2 * pp + 1]);
+            for (int s = 0; s < RING; ++s) ring[s] = frag(s);
+            OpN<3> xs;
 #pragma unroll
-            for (int i = 0; i < NI; ++i) {
-                const OpN<2> a = wp.frag(i, pp);
-                const bf16x8 a2 = i < NI - 1 ? wp2.frag(i, pp).p[0] : w2r[pp];
+            for (int s = 0; s < S; ++s) {
+                const int pp = s / NI, i = s % NI;
+                if (i == 0) xs = opn<3>(ab[2 * pp], ab[2 * pp + 1]);
+                const Frag f = ring[s % RING];
+                if (s + RING < S) ring[s % RING] = frag(s + RING);
                 f32x4 acc = xp[i];
-                acc = mfma_bf16(a.p[0], xs.p[0], acc);
-                acc = mfma_bf16(a.p[1], xs.p[0], acc);
-                acc = mfma_bf16(a.p[0], xs.p[1], acc);
-                acc = mfma_bf16(a.p[1], xs.p[1], acc);
-                acc = mfma_bf16(a2, xs.p[0], acc);
-                xp[i] = mfma_bf16(a.p[0], xs.p[2], acc);
-                if (i % MEP_TG_GROUP == MEP_TG_GROUP - 1) __builtin_amdgcn_sched_barrier(0);
+                acc = mfma_bf16(f.a.p[0], xs.p[0], acc);
+                acc = mfma_bf16(f.a.p[1], xs.p[0], acc);
+                acc = mfma_bf16(f.a.p[0], xs.p[1], acc);
+                acc = mfma_bf16(f.a.p[1], xs.p[1], acc);
+                acc = mfma_bf16(f.a2, xs.p[0], acc);
+                xp[i] = mfma_bf16(f.a.p[0], xs.p[2], acc);
+                __builtin_amdgcn_sched_barrier(0);
             }
         }
+        if (tile == t_begin + wave) MEP_EPI_STAMP(3);
         if (tile + EWAVES < t_end) rows_of(d.x, tile + EWAVES, ab);   // behind the z product
         if (tok < ntok) {
             gfloat* pr = row_ptr(d.xp, tok);
@@ -918,6 +943,7 @@ MEP_DEV void epi_fwd_wp2r(const mep_epi_desc& d, unsigned char* sm, int t_begin,
                               [&](int pp) { return opn<3>(bb[2 * pp], bb[2 * pp + 1]); });
         tgemm_n<NI, NP, 3, 3>(z, [&](int i, int pp) { return wm.frag(i, NP + pp); },
                               [&](int pp) { return opn<3>(xp[2 * pp], xp[2 * pp + 1]); });
+        if (tile == t_begin + wave) MEP_EPI_STAMP(4);
         float sum = 0.f;
 #pragma unroll
         for (int i = 0; i < NI; ++i) sum += (z[i][0] + z[i][1]) + (z[i][2] + z[i][3]);
@@ -932,13 +958,16 @@ MEP_DEV void epi_fwd_wp2r(const mep_epi_desc& d, unsigned char* sm, int t_begin,
         var += __shfl_xor(var, 16, 64);
         var += __shfl_xor(var, 32, 64);
         const float rstd = 1.0f / sqrtf(var / (float)D + LN_EPS);
+        // the next tile's q rows before this tile's stores: the wait for them (in-order vmcnt)
+        // then does not wait for the stores
+        if (tile + EWAVES < t_end) rows_of(d.q, tile + EWAVES, bb);
         if (tok < ntok) {
             gfloat* zr = row_ptr(d.z, tok);
             gfloat* orow = row_ptr(d.out, tok);
 #pragma unroll
             for (int i = 0; i < NI; ++i) {
                 const int col = 16 * i + 4 * g;
-                const f32x4 w = ld4w(G<const float>(d.ln_w) + col), b = ld4w(G<const float>(d.ln_b) + col);
+                const f32x4 w = ld4w((const lfloat*)lnp + col), b = ld4w((const lfloat*)lnp + D + col);
                 f32x4 y;
 #pragma unroll
                 for (int r = 0; r < 4; ++r) y[r] = (z[i][r] - mean) * rstd * w[r] + b[r];
@@ -947,7 +976,15 @@ MEP_DEV void epi_fwd_wp2r(const mep_epi_desc& d, unsigned char* sm, int t_begin,
             }
             if (g == 0) { stats[2 * tok] = mean; stats[2 * tok + 1] = rstd; }
         }
+#ifdef MEP_EPI_TRACE
+        if (tile == t_begin + wave) { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); MEP_EPI_STAMP(5); }
+#endif
     }
+#ifdef MEP_EPI_TRACE
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    MEP_EPI_STAMP(2);
+#endif
 }
 
 template <int D, int NPART, int NWP, int NWM, bool DROP>
@@ -987,6 +1024,8 @@ MEP_DEV void epi_bwd_one(const mep_epi_bwd_desc& bd, unsigned char* sm, int t_be
         mean = stats[2 * tc];
         rstd = stats[2 * tc + 1];
     };
+    __shared__ __attribute__((aligned(16))) float lnp[D];   // LayerNorm weight
+    stage_ln<D, false>((lfloat*)lnp, d);
     if (t_begin + wave < t_end) fetch1(t_begin + wave);
     if (bd.image) {
         dma_image<WMT::BYTES + WPT::BYTES>(sm, bd.image);
@@ -1017,7 +1056,7 @@ MEP_DEV void epi_bwd_one(const mep_epi_bwd_desc& bd, unsigned char* sm, int t_be
 #pragma unroll
         for (int i = 0; i < NI; ++i) {
             const int col = 16 * i + 4 * g;
-            const f32x4 w = ld4w(G<const float>(d.ln_w) + col);
+            const f32x4 w = ld4w((const lfloat*)lnp + col);
             f32x4 pw, pb;
 #pragma unroll
             for (int r = 0; r < 4; ++r) {

@@ -180,19 +180,42 @@ struct SplitWS {
 // acc[i] (i < NI) += A_i B over NP k pairs: afr(i, p) -> OpN (A fragment of output tile i),
 // bfr(p) -> OpN (B fragment, shared by the NI tiles).
 #ifndef MEP_TG_GROUP
-#define MEP_TG_GROUP 2   // output tiles per scheduling group of tgemm_n
+#define MEP_TG_GROUP 2   // output tiles per scheduling group of tgemm_n (MEP_TG_RING = 0)
+#endif
+#ifndef MEP_TG_RING
+#define MEP_TG_RING 2    // A fragments read this many steps ahead of their MFMAs (0: grouped reads)
 #endif
 template <int NI, int NP, int NPART, int NW = NPART, typename AF, typename BF>
 MEP_DEV void tgemm_n(f32x4 (&acc)[NI], AF&& afr, BF&& bfr) {
+    if constexpr (MEP_TG_RING > 0) {
+        // steps s = (k pair p, tile i), p-major (the grouped order below, so the sums are the
+        // same): fragment s + RING is read while step s's MFMAs run, so the LDS latency hides
+        // behind them instead of opening every group
+        constexpr int S = NI * NP, RING = MEP_TG_RING < S ? MEP_TG_RING : S;
+        OpN<NW> ring[RING];
 #pragma unroll
-    for (int p = 0; p < NP; ++p) {
-        const OpN<NPART> b = bfr(p);
+        for (int s = 0; s < RING; ++s) ring[s] = afr(s % NI, s / NI);
+        OpN<NPART> b;
 #pragma unroll
-        for (int i = 0; i < NI; ++i) {
-            acc[i] = mma_nm<NW, NPART>(afr(i, p), b, acc[i]);   // A: NW weight parts
-            // keep the next fragment's reads behind these MFMAs (a fully hoisted, fully unrolled
-            // product would hold 4 NPART NI NP fragment VGPRs)
-            if (i % MEP_TG_GROUP == MEP_TG_GROUP - 1) __builtin_amdgcn_sched_barrier(0);
+        for (int s = 0; s < S; ++s) {
+            const int p = s / NI, i = s % NI;
+            if (i == 0) b = bfr(p);
+            const OpN<NW> a = ring[s % RING];
+            if (s + RING < S) ring[s % RING] = afr((s + RING) % NI, (s + RING) / NI);
+            acc[i] = mma_nm<NW, NPART>(a, b, acc[i]);   // A: NW weight parts
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    } else {
+#pragma unroll
+        for (int p = 0; p < NP; ++p) {
+            const OpN<NPART> b = bfr(p);
+#pragma unroll
+            for (int i = 0; i < NI; ++i) {
+                acc[i] = mma_nm<NW, NPART>(afr(i, p), b, acc[i]);   // A: NW weight parts
+                // keep the next fragment's reads behind these MFMAs (a fully hoisted, fully unrolled
+                // product would hold 4 NPART NI NP fragment VGPRs)
+                if (i % MEP_TG_GROUP == MEP_TG_GROUP - 1) __builtin_amdgcn_sched_barrier(0);
+            }
         }
     }
 }

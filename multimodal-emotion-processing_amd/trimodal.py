@@ -74,6 +74,8 @@ OVERLAP_WGRAD = _lib.switch('MEP_OVERLAP_WGRAD', '0') == '1'
 EPI_IMAGE = _lib.switch('MEP_EPI_IMAGE', '0') == '1'
 # mep_unify workgroups in XCD-contiguous descriptor order (xcd_order); 0: descriptor-major by id
 UNIFY_XCD = _lib.switch('MEP_UNIFY_XCD', '1') != '0'
+_DEV_EPI_TWICE = _lib.switch('MEP_DEV_EPI_TWICE', '0') == '1'   # development timing runs only
+_DEV_SUMFOLD_PROBE = _lib.switch('MEP_DEV_SUMFOLD_PROBE', '0') == '1'   # development timing runs only
 
 
 def wgrad_geometry(N, ktot, bf16=False):
@@ -562,6 +564,7 @@ class TriModalPlan:
         # per-modality gradient sums
         sd = []
         self.dU = {}
+        self._sum_srcs = {}
         for e in range(E):
             for m in MODS:
                 T = self.T[m]
@@ -570,6 +573,7 @@ class TriModalPlan:
                 srcs += [crows(self._blk(e, j, i)['dKV'], T, D) for j, (qm, km) in enumerate(CHAINS) if km == m
                          for i in range(nl)]
                 assert len(srcs) <= _lib.SUM_MAX_SRC
+                self._sum_srcs[(e, m)] = srcs
                 arr = (Rows * _lib.SUM_MAX_SRC)(*srcs)
                 sd.append(SumDesc(src=arr, out=crows(self.dU[(e, m)], T, D), n_src=len(srcs),
                                   ntok=self.ntok[m], D=D, accumulate=_lib.SUM_BF16 if self.bf16 else 0))
@@ -696,6 +700,14 @@ class TriModalPlan:
             pre = sp.prefixes[e] + 'unify_dimension.'
             for m, d in zip(MODS, sp.dims):
                 src = self.dY[(e, m)] if sp.unify_norm else self.dU[(e, m)]
+                if _DEV_SUMFOLD_PROBE and not sp.unify_norm:
+                    # development timing probe (wrong gradients): the unify weight gradient as one
+                    # item per per-modality source, no mep_sum_rows -- what folding the sums into
+                    # the weight-gradient launch as extra token slots would cost
+                    for a in self._sum_srcs[(e, m)]:
+                        items.append((a, D, self.ntok[m],
+                                      [(self._in_rows(e, m), d, g(pre + UNIFY_NAMES[m] + '.weight'), d)]))
+                    continue
                 items.append((crows(src, self.T[m], D), D, self.ntok[m],
                               [(self._in_rows(e, m), d, g(pre + UNIFY_NAMES[m] + '.weight'), d)]))
         self._wgrad_items = items
@@ -803,6 +815,8 @@ class TriModalPlan:
         for i in range(nl):
             launch('mep_attn_fwd', self.d_attn[i], self.t_attn[i], stream, threads=self.g_attn[i][2] | self.prec)
             launch('mep_block_epi_fwd', self.d_epi[i], self.t_epi[i], stream, threads=sp.D | self.prec)
+            if _DEV_EPI_TWICE:   # development: the same (idempotent) launch again, on a warm L2
+                launch('mep_block_epi_fwd', self.d_epi[i], self.t_epi[i], stream, threads=sp.D | self.prec)
         launch('mep_pool_fwd', self.d_pool, self.t_pool, stream)
         self.head.compute_grad = int(grad)
         self.head.rdrop = int(rdrop)
@@ -846,6 +860,8 @@ class TriModalPlan:
         main = side = None
         for i in reversed(range(nl)):
             launch('mep_block_epi_bwd', self.d_epib[i], self.t_epi[i], stream, threads=sp.D | self.prec)
+            if _DEV_EPI_TWICE:
+                launch('mep_block_epi_bwd', self.d_epib[i], self.t_epi[i], stream, threads=sp.D | self.prec)
             if ovl is not None and i == 0:
                 # every block-weight operand is final here: bucket A's weight gradients on the side
                 # stream while the attention backward and the sums run on this one
@@ -855,7 +871,7 @@ class TriModalPlan:
                 with torch.cuda.stream(side):
                     launch('mep_wgrad', da, ta, side)
             launch('mep_attn_bwd', self.d_attnb[i], self.t_attnb[i], stream, threads=self.f_attnb[i] | self.prec)
-        if not self.sum_fold:
+        if not self.sum_fold and not (_DEV_SUMFOLD_PROBE and not sp.unify_norm):
             launch('mep_sum_rows', self.d_sum, self.t_sum, stream)
         if sp.unify_norm:
             launch('mep_layernorm_bwd', self.d_ulnb, cdiv(max(self.ntok.values()), 64), stream)
