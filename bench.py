@@ -184,7 +184,8 @@ KERNEL_OF = {'mep_attn_bwd': 'k_attn_bwd', 'mep_attn_fwd': 'k_attn_fwd', 'mep_bl
              'mep_block_epi_bwd': 'k_epi_bwd', 'mep_wgrad': 'k_wgrad', 'mep_unify': 'k_unify',
              'mep_pool_fwd': 'k_pool_fwd', 'mep_pool_bwd': 'k_pool_bwd', 'mep_gemm': 'k_gemm', 'mep_tgemm': 'k_tgemm',
              'mep_rf_epi_fwd': 'k_rf_epi_fwd', 'mep_rf_epi_bwd': 'k_rf_epi_bwd', 'mep_sum_rows': 'k_sum_rows',
-             'mep_wgemm': 'k_wgemm', 'mep_wgemm_ws': 'k_wgemm_ws', 'mep_rfw_front': 'k_rfw_front', 'mep_rfw_epi_fwd': 'k_rfw_fwd', 'mep_rfw_epi_bwd': 'k_rfw_bwd',
+             'mep_wgemm': 'k_wgemm', 'mep_wgemm_ws': 'k_wgemm_ws', 'mep_wgemm_sum': 'k_wgemm_sum',
+             'mep_rfw_front': 'k_rfw_front', 'mep_rfw_epi_fwd': 'k_rfw_fwd', 'mep_rfw_epi_bwd': 'k_rfw_bwd',
              'mep_wsplit': 'k_wsplit', 'mep_reduce_grads': 'k_reduce_grads', 'mep_head_fwd_bwd': 'k_head',
              'mep_clip_adam_ext': 'k_clip_adam', 'mep_rf_head': 'k_rf_head'}
 
@@ -206,7 +207,7 @@ def pmc_traffic(launch, tag='cfg3'):
     pat = 'r*_v*_pmc.json' if tag == 'cfg3' else 'r*_v*_pmc_%s.json' % tag
     for f in sorted(glob.glob(os.path.join(ROOT, 'profiles', pat)), key=key, reverse=True):
         for k, v in json.load(open(f)).items():
-            if launch == 'mep_wgemm' and k.startswith('k_wgemm_ws'):
+            if launch == 'mep_wgemm' and k.startswith(('k_wgemm_ws', 'k_wgemm_sum')):
                 continue                                 # the prefix of the other GEMM
             if k.startswith(prefix) and isinstance(v, dict) and 'hbm_bytes_per_dispatch' in v:
                 return int(v['hbm_bytes_per_dispatch']), os.path.relpath(f, ROOT)

@@ -388,8 +388,8 @@ int mep_wgemm(const mep_gemm_desc* descs, int n_desc, int max_tiles, int max_n, 
  * max_k <= 320.  The same token GEMMs as mep_wgemm (others/realformer.py:136-157,182-188).
  * flags: MEP_WGEMM_XVEC when every descriptor's X rows are 16-byte aligned (x.ptr, sB, sT
  * multiples of 4 floats) and readable up to K rounded up to 4 (K % 4 == 0, or rows padded): the
- * X rows are then read in 16-byte blocks (values past K are read and ignored), else one float at
- * a time. */
+ * X rows are then read in 16-byte blocks (values past K are read and multiplied by zero weights:
+ * they must be finite), else one float at a time. */
 #define MEP_WGEMM_XVEC 0x1
 int mep_wgemm_ws(const mep_gemm_desc* descs, int n_desc, int max_ntok, int max_n, int max_k, int flags,
                  mep_stream_t stream);
@@ -404,6 +404,20 @@ int mep_wgemm_ws(const mep_gemm_desc* descs, int n_desc, int max_ntok, int max_n
  * up to K rounded up to 4 (MEP_WGEMM_XVEC), ceil(K / 32) = npk_u in {2, 3, 10}; out[o]: parts of a
  * [N_o][96] weight (N_o % 16 == 0), y_o = U W_o^T written; tile_map[t] = o << 8 | (16-column tile
  * of out[o]) for the t < n_tiles output tiles.  Bit-identical to mep_wgemm on the same parts. */
+/* mep_wgemm_sum: out = sum over s < n_src, in order, of mep_wgemm(src[s]) -- the input-gradient
+ * products of one modality and their per-modality sum (mep_sum_rows) in one launch, bit-identical
+ * to those launches (each source's mep_wgemm epilogue: alpha * acc (+ its y rows when accumulate),
+ * then ((0 + v_0) + v_1) + ...).  The sources' y views are read (accumulate) but not written; all
+ * sources share ntok and N (<= 256).  Grid (max_tiles, n_desc, ceil(max_n / 16)).
+ * (others/realformer.py:157,188: the dQ W_q and [dK | dV] [W_k; W_v] input gradients of U.) */
+#define MEP_WGEMM_SUM_MAX 4
+typedef struct {
+    mep_gemm_desc src[MEP_WGEMM_SUM_MAX];
+    int32_t n_src, _pad;
+    mep_rows out;
+} mep_gemm_sum_desc;
+int mep_wgemm_sum(const mep_gemm_sum_desc* descs, int n_desc, int max_tiles, int max_n, mep_stream_t stream);
+
 #define MEP_RF_FRONT_MAX_OUT 12
 #define MEP_RF_FRONT_MAX_TILES 96
 typedef struct {

@@ -45,6 +45,13 @@ class GemmDesc(ctypes.Structure):
                 ('accumulate', i32), ('relu', i32), ('alpha', f32), ('bf16', i32), ('ldt', i32)]
 
 
+WGEMM_SUM_MAX = 4             # MEP_WGEMM_SUM_MAX
+
+
+class GemmSumDesc(ctypes.Structure):
+    _fields_ = [('src', GemmDesc * WGEMM_SUM_MAX), ('n_src', i32), ('_pad', i32), ('out', Rows)]
+
+
 RF_FRONT_MAX_OUT = 12         # MEP_RF_FRONT_MAX_OUT
 RF_FRONT_MAX_TILES = 96       # MEP_RF_FRONT_MAX_TILES
 
@@ -248,7 +255,7 @@ class Seg(ctypes.Structure):
     _fields_ = [('offset', i64), ('length', i64)]
 
 
-STRUCTS = {'mep_rows': Rows, 'mep_gemm_desc': GemmDesc, 'mep_wgrad_desc': WgradDesc,
+STRUCTS = {'mep_rows': Rows, 'mep_gemm_desc': GemmDesc, 'mep_gemm_sum_desc': GemmSumDesc, 'mep_wgrad_desc': WgradDesc,
            'mep_attn_desc': AttnDesc, 'mep_attn_bwd_desc': AttnBwdDesc, 'mep_epi_desc': EpiDesc,
            'mep_epi_bwd_desc': EpiBwdDesc, 'mep_ln_desc': LnDesc, 'mep_colsum_desc': ColsumDesc,
            'mep_sum_desc': SumDesc, 'mep_pool_desc': PoolDesc, 'mep_head_desc': HeadDesc, 'mep_seg': Seg,
@@ -286,6 +293,7 @@ SIGNATURES.update({
     'mep_tgemm': [P, i32, i32, i32, i32, P],
     'mep_wgemm': [P, i32, i32, i32, P],
     'mep_wgemm_ws': [P, i32, i32, i32, i32, i32, P],
+    'mep_wgemm_sum': [P, i32, i32, i32, P],
     'mep_rfw_front': [P, i32, i32, i32, P],
     'mep_epi_images': [P, i32, i32, P],
     'mep_epi_image_bytes': [i32, i32],

@@ -896,6 +896,7 @@ MEP_DEV void epi_fwd_wp2r(const mep_epi_desc& d, unsigned char* sm, int t_begin,
     MEP_EPI_STAMP(1);
     for (int tile = t_begin + wave; tile < t_end; tile += EWAVES) {
         const int tok = tile * 16 + c;
+        if (tile == t_begin + wave + EWAVES) MEP_EPI_STAMP(6);   // wave 0's second tile starts
         f32x4 xp[NI];
 #pragma unroll
         for (int i = 0; i < NI; ++i) xp[i] = zero_f4();
@@ -978,6 +979,7 @@ MEP_DEV void epi_fwd_wp2r(const mep_epi_desc& d, unsigned char* sm, int t_begin,
         }
 #ifdef MEP_EPI_TRACE
         if (tile == t_begin + wave) { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); MEP_EPI_STAMP(5); }
+        if (tile == t_begin + wave + EWAVES) { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); MEP_EPI_STAMP(7); }
 #endif
     }
 #ifdef MEP_EPI_TRACE

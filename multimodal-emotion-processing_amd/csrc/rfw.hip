@@ -786,6 +786,116 @@ __global__ __launch_bounds__(64 * WGM_WAVES) void k_wgemm(const mep_gemm_desc* _
     }
 }
 
+// ---------------------------------------------------------------- input-gradient GEMMs + their sum
+// mep_wgemm_sum: wave s of a workgroup runs source s's 16 x 32 tile exactly as k_wgemm with one
+// wave does (its k pairs in order, groups of 4 loaded before their MFMAs, then alpha, bias +
+// table, relu, + y), parks the result in LDS, and wave 0 adds the sources in order onto 0 (the
+// k_sum_rows sequence) and writes the sum.  The sources' y rows are read, never written.
+// A workgroup covers 16 tokens x 16 NI columns; every fragment of GP k pairs is loaded before
+// their MFMAs (GP = 6: K <= 192 in one memory latency).
+#ifndef MEP_WGSUM_NI
+#define MEP_WGSUM_NI 1
+#endif
+#ifndef MEP_WGSUM_GP
+#define MEP_WGSUM_GP 6
+#endif
+__global__ __launch_bounds__(64 * MEP_WGEMM_SUM_MAX) void k_wgemm_sum(const mep_gemm_sum_desc* __restrict__ descs) {
+    constexpr int NI = MEP_WGSUM_NI, GP = MEP_WGSUM_GP, CW = 16 * NI;
+    __shared__ f32x4 red[MEP_WGEMM_SUM_MAX][NI][64];
+    const mep_gemm_sum_desc& sd = descs[blockIdx.y];
+    const int tile = blockIdx.x, cg = blockIdx.z;
+    const int ntok = sd.src[0].ntok, N = sd.src[0].N, n_src = min(sd.n_src, MEP_WGEMM_SUM_MAX);
+    if (tile * 16 >= ntok || cg * CW >= N) return;   // whole workgroup
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    const int c = lane & 15, g = lane >> 4;
+    const int tok = tile * 16 + c, tc = min(tok, ntok - 1);
+    if (wave < n_src) {
+        const mep_gemm_desc& d = sd.src[wave];
+        const int K = d.K, npk = (K + 31) >> 5;
+        const bool xvec = (K % 4 == 0) && ((d.x.ptr & 15) == 0) && (d.x.sB % 4 == 0) && (d.x.sT % 4 == 0);
+        const gfloat* xr = row_ptr(d.x, tc);
+        const int tstride = ((N + 31) & ~31) * npk * 4;
+        const PartPtr wl = reinterpret_cast<PartPtr>(G<const unsigned char>(d.w)) + ((CW * cg + c) * npk) * 4 + g;
+        f32x4 add[NI], yold[NI];
+        {
+            const gfloat* bias = G<const float>(d.bias);
+            const gfloat* trow = d.table ? G<const float>(d.table) + (int64_t)(tc % d.y.T) * (d.ldt ? d.ldt : N) : nullptr;
+            const gfloat* yr = row_ptr(d.y, tc);
+#pragma unroll
+            for (int i = 0; i < NI; ++i)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int n = min(CW * cg + 16 * i + 4 * g + r, N - 1);
+                    add[i][r] = (bias ? bias[n] : 0.f) + (trow ? trow[n] : 0.f);
+                    yold[i][r] = d.accumulate ? yr[n] : 0.f;
+                }
+        }
+        auto xblk = [&](int k) {
+            f32x4 v = zero_f4();
+            if (xvec) {
+                if (k < K) v = ld4w(xr + k);
+            } else {
+#pragma unroll
+                for (int e = 0; e < 4; ++e) v[e] = k + e < K ? xr[k + e] : 0.f;
+            }
+            return v;
+        };
+        f32x4 acc[NI];
+#pragma unroll
+        for (int i = 0; i < NI; ++i) acc[i] = zero_f4();
+        for (int p0 = 0; p0 < npk; p0 += GP) {
+            f32x4 x0[GP], x1[GP];
+            OpN<3> a[GP][NI];
+#pragma unroll
+            for (int u = 0; u < GP; ++u) {
+                const int p = p0 + u;
+                if (p < npk) {
+                    x0[u] = xblk(32 * p + 4 * g);
+                    x1[u] = xblk(32 * p + 16 + 4 * g);
+#pragma unroll
+                    for (int i = 0; i < NI; ++i)
+#pragma unroll
+                        for (int t = 0; t < 3; ++t)
+                            a[u][i].p[t] = __builtin_bit_cast(bf16x8, wl[t * tstride + (16 * i * npk + p) * 4]);
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < GP; ++u) {
+                if (p0 + u < npk) {
+                    const OpN<3> b = opn<3>(x0[u], x1[u]);
+#pragma unroll
+                    for (int i = 0; i < NI; ++i) acc[i] = mma_n<3>(a[u][i], b, acc[i]);
+                }
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < NI; ++i) {
+            f32x4 v;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                float e = d.alpha * acc[i][r] + add[i][r];
+                if (d.relu) e = fmaxf(e, 0.f);
+                if (d.accumulate) e += yold[i][r];
+                v[r] = e;
+            }
+            red[wave][i][lane] = v;
+        }
+    }
+    __syncthreads();
+    if (wave != 0 || tok >= ntok) return;
+    gfloat* o = row_ptr(sd.out, tok);
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+        f32x4 s = zero_f4();
+        for (int w = 0; w < n_src; ++w) s += red[w][i][lane];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int n = CW * cg + 16 * i + 4 * g + r;
+            if (n < N) o[n] = s[r];
+        }
+    }
+}
+
 // ---------------------------------------------------------------- weight-stationary token GEMM
 // mep_wgemm's contract with the weight block resident in LDS.  A workgroup owns the 16 NT output
 // columns [16 NT z, 16 NT (z + 1)) of one descriptor (grid (gx, n_desc, z)): it copies their parts
@@ -1100,6 +1210,15 @@ extern "C" int mep_wgemm(const mep_gemm_desc* descs, int n_desc, int max_tiles, 
     hipLaunchKernelGGL(k_wgemm, dim3(max_tiles, n_desc, (max_n + 31) / 32), dim3(64 * WGM_WAVES), 0,
                        (hipStream_t)stream, descs);
     return mep_check_launch("mep_wgemm");
+}
+
+extern "C" int mep_wgemm_sum(const mep_gemm_sum_desc* descs, int n_desc, int max_tiles, int max_n, mep_stream_t stream) {
+    if (n_desc <= 0 || max_tiles <= 0) return 0;
+    if (max_n <= 0 || max_n > 256) { mep_set_error("mep_wgemm_sum: 0 < max_n <= 256"); return MEP_EINVAL; }
+    hipLaunchKernelGGL(k_wgemm_sum, dim3(max_tiles, n_desc, (max_n + 16 * MEP_WGSUM_NI - 1) / (16 * MEP_WGSUM_NI)),
+                       dim3(64 * MEP_WGEMM_SUM_MAX), 0,
+                       (hipStream_t)stream, descs);
+    return mep_check_launch("mep_wgemm_sum");
 }
 
 #ifndef MEP_WGS_MIN_WG

@@ -36,6 +36,9 @@ RF_SPLITQ = _lib.switch('MEP_RF_SPLITQ', '1') != '0'   # attention backward: que
 # whose per-tile weight streaming from L2 grows with the tile count); 0: never
 RF_FRONT = _lib.switch('MEP_RF_FRONT', '1') != '0'
 RF_FRONT_MAX_TILES = 1024
+# the input-gradient GEMMs and their per-modality sums in one launch (mep_wgemm_sum) when every
+# sum has at most 4 sources, each the output of one of those GEMMs (cfg2's chain); 0: never
+RF_WGEMM_SUM = _lib.switch('MEP_RF_WGEMM_SUM', '1') != '0'
 
 NC = 6  # State_Transfer classes (realformer.py:268-269)
 POS_NAMES = {'l': 'linguistic_position', 'v': 'visual_position', 'a': 'acoustic_position'}
@@ -407,9 +410,36 @@ class RealformerPlan:
                               ntok=self.ntok[m], D=D, accumulate=0))
         self.d_sum = DescArray(SumDesc, sd, dev)
         self.t_sum = min(1024, max(cdiv(self.ntok[m] * D // 4, 256) for m in sp.mods))
+        self.d_isum = self._fuse_sums(ig_all, sd, dev) if self.rfw and RF_WGEMM_SUM and ig_all else None
         if sp.head:
             self._build_head()
         self._build_grads()
+
+    def _fuse_sums(self, ig_all, sd, dev):
+        """mep_wgemm_sum descriptors replacing the ingrad launch + mep_sum_rows, or None when some
+        sum has more than WGEMM_SUM_MAX sources, a source no single GEMM writes, or a GEMM feeds
+        no sum (or the ingrad launch would take the weight-stationary kernel)"""
+        if self.gemm_launcher(self.d_ingrad_all) != 'mep_wgemm':
+            return None
+        by_y = {}
+        for g in ig_all:
+            by_y.setdefault((g.y.ptr, g.y.sB, g.y.sT), []).append(g)
+        out, used = [], 0
+        for s in sd:
+            if s.n_src > _lib.WGEMM_SUM_MAX or s.accumulate:
+                return None
+            src = []
+            for k in range(s.n_src):
+                r = s.src[k]
+                g = by_y.get((r.ptr, r.sB, r.sT), [])
+                if len(g) != 1 or g[0].ntok != s.ntok or g[0].N != s.D:
+                    return None
+                src.append(g[0])
+            used += len(src)
+            out.append(_lib.GemmSumDesc(src=(GemmDesc * _lib.WGEMM_SUM_MAX)(*src), n_src=len(src), out=s.out))
+        if used != len(ig_all):
+            return None
+        return DescArray(_lib.GemmSumDesc, out, dev)
 
     def _build_head(self):
         sp, fl, R, D = self.spec, self.flat, self.R, self.spec.D
@@ -598,8 +628,11 @@ class RealformerPlan:
             launch('mep_rfw_epi_bwd' if self.rfw else 'mep_rf_epi_bwd', self.d_epib[i], self.t_epib[i], stream, extra=ex)
             launch('mep_attn_bwd', self.d_attnb[i], self.t_attnb[i], stream, threads=self.f_attnb[i])
             self._gemm(self.d_ingrad[i], self.t_ingrad, stream)
-        self._gemm(self.d_ingrad_all, self.t_ingrad, stream)
-        launch('mep_sum_rows', self.d_sum, self.t_sum, stream)
+        if self.d_isum is not None:
+            _lib.call('mep_wgemm_sum', self.d_isum.ptr, self.d_isum.n, int(self.t_ingrad), self.spec.D, stream=stream)
+        else:
+            self._gemm(self.d_ingrad_all, self.t_ingrad, stream)
+            launch('mep_sum_rows', self.d_sum, self.t_sum, stream)
         launch('mep_wgrad', self.d_wgrad, self.t_wgrad, stream)
         # weight-gradient split sums and LayerNorm / ReZero / residual-coefficient column sums: one
         # launch (no head partials here: the State_Transfer head reduces in mep_rf_head)

@@ -33,7 +33,7 @@ BF16_PEAK = 2.5e15
 ATTN_FWD_PEAK = 4.0 / (2.0 * (6 + 6) / BF16_PEAK)
 ATTN_BWD_PEAK = 10.0 / (2.0 * (4 + 4 + 4 + 4 + 3) / BF16_PEAK)
 COMPUTE_PEAK = {'mep_block_epi_fwd': BF16_PEAK / 6, 'mep_block_epi_bwd': BF16_PEAK / 6, 'mep_wgrad': BF16_PEAK / 6,
-                'mep_tgemm': BF16_PEAK / 6, 'mep_wgemm': BF16_PEAK / 6, 'mep_wgemm_ws': BF16_PEAK / 6, 'mep_rfw_front': BF16_PEAK / 6,
+                'mep_tgemm': BF16_PEAK / 6, 'mep_wgemm': BF16_PEAK / 6, 'mep_wgemm_ws': BF16_PEAK / 6, 'mep_wgemm_sum': BF16_PEAK / 6, 'mep_rfw_front': BF16_PEAK / 6,
                 'mep_rfw_epi_fwd': BF16_PEAK / 6, 'mep_rfw_epi_bwd': BF16_PEAK / 6,
                 'mep_attn_fwd': ATTN_FWD_PEAK, 'mep_attn_bwd': ATTN_BWD_PEAK}
 
@@ -122,6 +122,9 @@ def rf_launch_costs(plan):
     # the launcher of each token-GEMM group (rfw: mep_wgemm_ws for large launches, else mep_wgemm)
     G_UNIFY, G_PROJ = plan.gemm_launcher(plan.d_unify), plan.gemm_launcher(plan.d_proj)
     G_IN = plan.gemm_launcher(plan.d_ingrad_all) if rfw else G_PROJ
+    isum = getattr(plan, 'd_isum', None) is not None
+    if isum:    # mep_wgemm_sum: the input-gradient GEMMs write their per-modality sums only
+        G_IN = 'mep_wgemm_sum'
     front = bool(getattr(plan, 'front', None))
     if front:   # mep_rfw_front: the projections read U from registers, not HBM
         G_UNIFY = G_PROJ = 'mep_rfw_front'
@@ -144,6 +147,8 @@ def rf_launch_costs(plan):
             gemm(G_PROJ, nq, D, D, x_read=not front)           # Q = q W_q^T
             gemm(G_IN, nq, D, D, accumulate=True)              # dq_in += dQ W_q
         gemm(G_IN, nk, D, 2 * D)                               # dkv_in = [dK | dV] [W_k; W_v]
+        if isum:   # (no per-source row writes: one sum row per token, below)
+            add(G_IN, 0, -4 * (nk * D + (nq * D if blk['i'] == 0 else 0)))
         r_in = 1 if blk['i'] > 0 else 0
         r_out = 1 if 'S' in blk else 0
         s_bytes = 4 * H * Tq * Tk
@@ -168,7 +173,10 @@ def rf_launch_costs(plan):
         n = plan.ntok[m]
         add('mep_wgrad', 2 * n * D * sp.dims[m], 4 * n * (D + sp.dims[m]))
         srcs = sum(1 for (qm, km) in sp.chains if qm == m) + sum(sp.nl for (qm, km) in sp.chains if km == m)
-        add('mep_sum_rows', srcs * n * D, 4 * n * D * (srcs + 1))
+        if isum:
+            add(G_IN, srcs * n * D, 4 * n * D)
+        else:
+            add('mep_sum_rows', srcs * n * D, 4 * n * D * (srcs + 1))
     return out
 
 

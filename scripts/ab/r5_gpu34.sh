@@ -5,6 +5,11 @@
 # dropped), then the bench lines of every workload, whose traffic fields cite those passes
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export TMPDIR=/tmp
+mkdir -p gpurun_out
+timeout -k 10 900 python -u -m pytest tests -m gpu -q --timeout 120 --timeout-method thread > gpurun_out/r5_t34.log 2>&1
+rc=$?; echo "pytest rc=$rc"; grep -E "passed|failed" gpurun_out/r5_t34.log | tail -2; grep -E "^FAILED|^ERROR" gpurun_out/r5_t34.log | head -20
+[ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > gpurun_out/r5_smoke34.log 2>&1; rc=$?; tail -2 gpurun_out/r5_smoke34.log; [ $rc -eq 0 ] || exit $rc
 R=gpurun_out/r5ctr
 OUT=$R STAGE=traffic CFGS="cfg3 cfg3_bf16 cfg5 cfg5_bf16 cfg2 rfstate" PSTEPS=20 bash scripts/r4_counters.sh || exit $?
 OUT=$R STAGE=sq CFGS="cfg3 cfg3_bf16" bash scripts/r4_counters.sh || exit $?

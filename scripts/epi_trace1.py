@@ -41,6 +41,11 @@ def main():
         # wave 0's first tile: staged -> xp product done (3) -> z product done (4) -> LN + stores (5)
         ph = [(t[:, 3] - t[:, 1]) / 100.0, (t[:, 4] - t[:, 3]) / 100.0, (t[:, 5] - t[:, 4]) / 100.0]
         print('    wave 0 first tile: xp %s | z %s | LN + stores %s' % tuple(q(x) for x in ph))
+        two = t[:, 7] > 0   # workgroups whose wave 0 ran a second tile
+        if two.any():
+            u = t[two]
+            print('    wave 0 second tile (%d wgs): %s us; first tile of those: %s'
+                  % (int(two.sum()), q((u[:, 7] - u[:, 6]) / 100.0), q((u[:, 5] - u[:, 1]) / 100.0)))
     L.mep_epi_set_trace(ctypes.c_void_p(0))
 
 

@@ -256,3 +256,90 @@ def test_rfw_front_matches_gemm_launches(family, cuda):
                     [b['KV'].clone() for b in plan.blocks] + [b['QP'].clone() for b in plan.blocks if b['i'] == 0])
     for i, (a, b) in enumerate(zip(*outs)):
         assert torch.equal(a, b), 'tensor %d: max |diff| %.3g' % (i, (a - b).abs().max().item())
+
+
+def _sum_rows(srcs, out, ntok, D, dev):
+    from mep_amd import _lib
+    src = (_lib.Rows * _lib.SUM_MAX_SRC)(*srcs)
+    arr = _lib.DescArray(_lib.SumDesc, [_lib.SumDesc(src=src, out=out, n_src=len(srcs), ntok=ntok, D=D,
+                                                    accumulate=0)], dev)
+    _lib.call('mep_sum_rows', arr.ptr, arr.n, min(1024, -(-ntok * D // 1024)))
+    torch.cuda.synchronize()
+
+
+# (tokens, T, [(K, accumulate) per source]) of one fused sum: cfg2's chain modality (layer-0
+# dq_in onto the epilogue residual + two dkv_in), four sources, one source, ragged tokens
+SUM_CASES = {
+    'chain': (64 * 50, 50, [(96, 1), (192, 0), (192, 0)]),
+    'four': (8 * 50, 50, [(192, 0), (96, 1), (192, 1), (35, 0)]),
+    'one': (3 * 7, 7, [(96, 1)]),
+    'ragged': (37, 37, [(70, 0), (192, 1)]),
+}
+
+
+@pytest.mark.parametrize('case', sorted(SUM_CASES))
+def test_wgemm_sum_matches_wgemm_and_sum_rows(case, cuda):
+    """mep_wgemm_sum == mep_wgemm per source + mep_sum_rows bit for bit, the sources' y rows
+    untouched, and within fp32 level of the float64 sum of products."""
+    from mep_amd import _lib
+    n, T, shapes = SUM_CASES[case]
+    D = 96
+    torch.manual_seed(n + len(shapes))
+    ws = [(torch.randn(D, K, device=cuda) / K ** 0.5, D, K, K, 0) for K, _ in shapes]
+    xs = [torch.randn(n, K, device=cuda) for K, _ in shapes]
+    y0s = [torch.randn(n, D, device=cuda) if acc else torch.zeros(n, D, device=cuda) for _, acc in shapes]
+    buf, offs = _parts(ws, cuda)
+
+    def descs(ys):
+        return [_gd(_rows(x, T, T * K, K), _rows(y, T, T * D, D), buf.data_ptr() + o, n, D, K, accumulate=acc)
+                for (K, acc), x, y, o in zip(shapes, xs, ys, offs)]
+
+    ys = [y.clone() for y in y0s]
+    _wgemm(descs(ys), cuda)
+    want = torch.full((n, D), float('nan'), device=cuda)
+    _sum_rows([_rows(y, T, T * D, D) for y in ys], _rows(want, T, T * D, D), n, D, cuda)
+    ys2 = [y.clone() for y in y0s]
+    got = torch.full((n, D), float('nan'), device=cuda)
+    src = (_lib.GemmDesc * _lib.WGEMM_SUM_MAX)(*descs(ys2))
+    arr = _lib.DescArray(_lib.GemmSumDesc, [_lib.GemmSumDesc(src=src, n_src=len(shapes),
+                                                             out=_rows(got, T, T * D, D))], cuda)
+    _lib.call('mep_wgemm_sum', arr.ptr, arr.n, -(-n // 16), D)
+    torch.cuda.synchronize()
+    assert torch.equal(got, want), '%s: max |diff| %.3g' % (case, (got - want).abs().max().item())
+    for y, y0 in zip(ys2, y0s):
+        assert torch.equal(y, y0)
+    ref = sum(x.double() @ w.double().t() + y0.double() for x, y0, (w, *_) in zip(xs, y0s, ws))
+    assert_close(got, ref.cpu().numpy(), 1e-5, 1e-6, case)
+
+
+def test_rfw_wgemm_sum_plan_gradients(cuda):
+    """cfg2's text chain: the backward with the fused input-gradient sums (mep_wgemm_sum) writes
+    every gradient bit-identical to the ingrad GEMM + mep_sum_rows launches."""
+    from mep_amd import realformer as rf
+    from mep_amd import rf_plan
+    torch.manual_seed(12)
+    B, T = 8, 50
+    mc = rf.Multi_class(l_dim=300, v_dim=35, a_dim=74, dim=96, l_len=T, v_len=T, a_len=T, n_heads=6,
+                        n_layers=2, ffn=2).to(cuda)
+    runner = mc.mep_chain_runner(2, cuda)
+    feats = (torch.randn(B, T, 300, device=cuda), torch.zeros(0, device=cuda), torch.zeros(0, device=cuda))
+    masks = (torch.ones(B, T, device=cuda), torch.zeros(0, device=cuda), torch.zeros(0, device=cuda))
+    dout = None
+    grads = []
+    for on in (True, False):
+        old = rf_plan.RF_WGEMM_SUM
+        rf_plan.RF_WGEMM_SUM = on
+        try:
+            plan = rf_plan.RealformerPlan(runner.spec, runner.flat, B, 1, cuda)
+        finally:
+            rf_plan.RF_WGEMM_SUM = old
+        assert (plan.d_isum is not None) == on
+        plan.set_inputs(*feats, *masks)
+        plan.forward(grad=True)
+        if dout is None:
+            dout = torch.randn_like(plan.dout_chain)
+        runner.flat.grad.zero_()
+        plan.backward(ext_dout=dout)
+        torch.cuda.synchronize()
+        grads.append(runner.flat.grad.clone())
+    assert torch.equal(grads[0], grads[1]), 'max |diff| %.3g' % (grads[0] - grads[1]).abs().max().item()
