@@ -288,17 +288,17 @@ MEP_DEV void epi_fwd_tiles(const mep_epi_desc& d, const AP& wp, const AM& wm, in
 
 // stage W [R][C] (fp32, row stride C) split into LDS: unit (n, p, g) = W[n][32p + 4g ..] and
 // W[n][32p + 16 + 4g ..]; every load of the thread is issued before its first LDS write
-template <int R, int C, int NPART>
+template <int R, int C, int NPART, int NT = ETHREADS>
 MEP_DEV void stage_split_rows(const SplitW<R, C / 32, NPART>& dst, const gfloat* src) {
 #ifdef MEP_EPI_NOSTAGE   // timing-only development build: no weight staging (LDS left as it is)
     return;
 #endif
     constexpr int NU = R * (C / 32) * 4;
-    constexpr int PER = (NU + ETHREADS - 1) / ETHREADS;
+    constexpr int PER = (NU + NT - 1) / NT;
     f32x4 v[PER][2];
 #pragma unroll
     for (int k = 0; k < PER; ++k) {
-        const int u = threadIdx.x + ETHREADS * k;
+        const int u = threadIdx.x + NT * k;
         if (u < NU) {
             const int g = u & 3, pp = (u >> 2) % (C / 32), n = (u >> 2) / (C / 32);
             v[k][0] = ld4w(src + n * C + 32 * pp + 4 * g);
@@ -307,7 +307,7 @@ MEP_DEV void stage_split_rows(const SplitW<R, C / 32, NPART>& dst, const gfloat*
     }
 #pragma unroll
     for (int k = 0; k < PER; ++k) {
-        const int u = threadIdx.x + ETHREADS * k;
+        const int u = threadIdx.x + NT * k;
         if (u < NU) {
             const int g = u & 3, pp = (u >> 2) % (C / 32), n = (u >> 2) / (C / 32);
             dst.put(n, pp, g, v[k][0], v[k][1]);
@@ -318,17 +318,17 @@ MEP_DEV void stage_split_rows(const SplitW<R, C / 32, NPART>& dst, const gfloat*
 // stage W^T of W [R][C] (fp32, row stride C) split into LDS (rows = the C columns of W, k = the R
 // rows): unit (n, p, g) = W[32p + 4g + j][n] and W[32p + 16 + 4g + j][n], j < 4; consecutive
 // threads take consecutive n (coalesced), loads issued before the LDS writes
-template <int R, int C, int NPART>
+template <int R, int C, int NPART, int NT = ETHREADS>
 MEP_DEV void stage_split_cols(const SplitW<C, R / 32, NPART>& dst, const gfloat* src) {
 #ifdef MEP_EPI_NOSTAGE
     return;
 #endif
     constexpr int NP = R / 32, NU = C * NP * 4;
-    constexpr int PER = (NU + ETHREADS - 1) / ETHREADS;
+    constexpr int PER = (NU + NT - 1) / NT;
     float v[PER][8];
 #pragma unroll
     for (int k = 0; k < PER; ++k) {
-        const int u = threadIdx.x + ETHREADS * k;
+        const int u = threadIdx.x + NT * k;
         if (u < NU) {
             const int n = u % C, pg = u / C, g = pg & 3, pp = pg >> 2;
 #pragma unroll
@@ -340,7 +340,7 @@ MEP_DEV void stage_split_cols(const SplitW<C, R / 32, NPART>& dst, const gfloat*
     }
 #pragma unroll
     for (int k = 0; k < PER; ++k) {
-        const int u = threadIdx.x + ETHREADS * k;
+        const int u = threadIdx.x + NT * k;
         if (u < NU) {
             const int n = u % C, pg = u / C, g = pg & 3, pp = pg >> 2;
             dst.put(n, pp, g, f32x4{v[k][0], v[k][1], v[k][2], v[k][3]}, f32x4{v[k][4], v[k][5], v[k][6], v[k][7]});
@@ -360,14 +360,14 @@ MEP_DEV void wg_store_barrier() {
 // the staging below would write) into LDS by LDS-DMA: wave w copies the 1-KB chunks w, w + EWAVES,
 // ... (lane l: bytes 16 l .. 16 l + 15 of the chunk) without passing through registers.  The
 // caller waits (image_ready) before its barrier.
-template <int BYTES>
+template <int BYTES, int NW = EWAVES>
 MEP_DEV void dma_image(unsigned char* sm, uint64_t img) {
     static_assert(BYTES % 1024 == 0, "epilogue weight images are whole 1-KB chunks");
     typedef __attribute__((address_space(3))) void lvoid;
     typedef __attribute__((address_space(3))) unsigned char lbyte;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const auto rs = __builtin_amdgcn_make_buffer_rsrc((void*)img, 0, BYTES, 0x00020000);
-    for (int ch = wave; ch < BYTES / 1024; ch += EWAVES)
+    for (int ch = wave; ch < BYTES / 1024; ch += NW)
         __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lvoid*)((lbyte*)sm + ch * 1024), 16, 16 * lane, ch * 1024, 0, 0);
 }
 MEP_DEV void image_ready() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
@@ -681,7 +681,7 @@ MEP_DEV void epi_bwd_split(const mep_epi_bwd_desc& bd, unsigned char* sm, int t_
 // (backward; 86 + 65 KB) -- a 2^-18 relative representation error of that weight.
 // DROP: a launch with dropout (drop_p > 0); the no-dropout instance has no hash code at all (the
 // dropout hash is most of the loop's instructions: a smaller, branch-free body)
-template <int D, int NPART, int NWP, int NWM, bool DROP>
+template <int D, int NPART, int NWP, int NWM, bool DROP, int NW = EWAVES>
 MEP_DEV void epi_fwd_one(const mep_epi_desc& d, unsigned char* sm, int t_begin, int t_end) {
     constexpr int NI = D / 16, KB = D / 16, NP = D / 32;
     using WP = SplitW<D, NP, NWP>;
@@ -711,14 +711,14 @@ MEP_DEV void epi_fwd_one(const mep_epi_desc& d, unsigned char* sm, int t_begin, 
     stage_ln<D, true>((lfloat*)lnp, d);
     if (t_begin + wave < t_end) { rows_of(d.x, t_begin + wave, ab); rows_of(d.q, t_begin + wave, bb); }
     if (d.image) {
-        dma_image<WP::BYTES + WM::BYTES>(sm, d.image);
+        dma_image<WP::BYTES + WM::BYTES, NW>(sm, d.image);
         image_ready();
     } else {
-        stage_split_rows<D, D, NWP>(wp, G<const float>(d.wp));
-        stage_split_rows<D, 2 * D, NWM>(wm, G<const float>(d.wm));
+        stage_split_rows<D, D, NWP, 64 * NW>(wp, G<const float>(d.wp));
+        stage_split_rows<D, 2 * D, NWM, 64 * NW>(wm, G<const float>(d.wm));
     }
     __syncthreads();
-    for (int tile = t_begin + wave; tile < t_end; tile += EWAVES) {
+    for (int tile = t_begin + wave; tile < t_end; tile += NW) {
         const int tok = tile * 16 + c;
         f32x4 xp[NI], z[NI];
 #pragma unroll
@@ -727,13 +727,13 @@ MEP_DEV void epi_fwd_one(const mep_epi_desc& d, unsigned char* sm, int t_begin, 
             OpN<NPART> xs[NP];
 #pragma unroll
             for (int pp = 0; pp < NP; ++pp) xs[pp] = opn<NPART>(ab[2 * pp], ab[2 * pp + 1]);
-            if (tile + EWAVES < t_end) rows_of(d.x, tile + EWAVES, ab);
+            if (tile + NW < t_end) rows_of(d.x, tile + NW, ab);
             tgemm_n<NI, NP, NPART, NWP>(xp, [&](int i, int pp) { return wp.frag(i, pp); }, [&](int pp) { return xs[pp]; });
         }
         OpN<NPART> qs[NP];
 #pragma unroll
         for (int pp = 0; pp < NP; ++pp) qs[pp] = opn<NPART>(bb[2 * pp], bb[2 * pp + 1]);
-        if (tile + EWAVES < t_end) rows_of(d.q, tile + EWAVES, bb);
+        if (tile + NW < t_end) rows_of(d.q, tile + NW, bb);
         if (p > 0.f) {
             uint32_t kb0 = 0;
 #pragma unroll
@@ -989,7 +989,7 @@ MEP_DEV void epi_fwd_wp2r(const mep_epi_desc& d, unsigned char* sm, int t_begin,
 #endif
 }
 
-template <int D, int NPART, int NWP, int NWM, bool DROP>
+template <int D, int NPART, int NWP, int NWM, bool DROP, int NW = EWAVES>
 MEP_DEV void epi_bwd_one(const mep_epi_bwd_desc& bd, unsigned char* sm, int t_begin, int t_end) {
     constexpr int NI = D / 16, KB = D / 16, NP = D / 32;
     using WMT = SplitW<2 * D, NP, NWM>;
@@ -1030,14 +1030,14 @@ MEP_DEV void epi_bwd_one(const mep_epi_bwd_desc& bd, unsigned char* sm, int t_be
     stage_ln<D, false>((lfloat*)lnp, d);
     if (t_begin + wave < t_end) fetch1(t_begin + wave);
     if (bd.image) {
-        dma_image<WMT::BYTES + WPT::BYTES>(sm, bd.image);
+        dma_image<WMT::BYTES + WPT::BYTES, NW>(sm, bd.image);
         image_ready();
     } else {
-        stage_split_cols<D, 2 * D, NWM>(wmt, G<const float>(d.wm));
-        stage_split_cols<D, D, NWP>(wpt, G<const float>(d.wp));
+        stage_split_cols<D, 2 * D, NWM, 64 * NW>(wmt, G<const float>(d.wm));
+        stage_split_cols<D, D, NWP, 64 * NW>(wpt, G<const float>(d.wp));
     }
     __syncthreads();
-    for (int tile = t_begin + wave; tile < t_end; tile += EWAVES) {
+    for (int tile = t_begin + wave; tile < t_end; tile += NW) {
         const int tok = tile * 16 + c;
         const uint32_t kbb0 = have_bits ? drop_bits_get(drop_bits_ptr(dbits, tok, 0)) : 0u;   // the forward's keep bits
         const uint32_t kbb1 = have_bits ? drop_bits_get(drop_bits_ptr(dbits, tok, 1)) : 0u;
@@ -1052,7 +1052,7 @@ MEP_DEV void epi_bwd_one(const mep_epi_bwd_desc& bd, unsigned char* sm, int t_be
 #pragma unroll
             for (int i = 0; i < NI; ++i) dz[i] += ld4a(g2 + 16 * i);
         }
-        if (tile + EWAVES < t_end) fetch1(tile + EWAVES);
+        if (tile + NW < t_end) fetch1(tile + NW);
         float s1 = 0.f, s2 = 0.f;
         gfloat* lp = lpart ? lpart + (int64_t)tile * 2 * D : nullptr;
 #pragma unroll
@@ -1379,6 +1379,43 @@ __global__ __launch_bounds__(ETHREADS) __attribute__((amdgpu_waves_per_eu(MEP_EP
         __syncthreads();
         epi_bwd_tiles<D>(bd, am, WCols{G<const float>(d.wp), D, 0, 0}, t_begin, t_end);
     }
+}
+
+// The bf16 epilogue forward at D = 96 with MEP_EPI_FWD_BF16_NW waves per workgroup (as below;
+// 168 VGPRs with 25 spilled; cfg3 bf16 18.2 -> 17.6 us)
+#ifndef MEP_EPI_FWD_BF16_NW
+#define MEP_EPI_FWD_BF16_NW 12
+#endif
+constexpr int EPI_FWD_BF16_NW = MEP_EPI_FWD_BF16_NW;
+__global__ __launch_bounds__(64 * EPI_FWD_BF16_NW) void k_epi_fwd_bf16w(const mep_epi_desc* __restrict__ descs) {
+    using E = EpiOne<96, true>;
+    int di, slice;
+    if (!epi_slot(di, slice)) return;
+    const mep_epi_desc& d = descs[di];
+    int t_begin, t_end;
+    if (!tile_range(d.ntok, slice, t_begin, t_end)) return;
+    __shared__ __attribute__((aligned(16))) unsigned char sm1[E::FWD_BYTES];
+    if (d.drop_p > 0.f) epi_fwd_one<96, 1, E::FWD_WP, E::FWD_WM, true, EPI_FWD_BF16_NW>(d, sm1, t_begin, t_end);
+    else epi_fwd_one<96, 1, E::FWD_WP, E::FWD_WM, false, EPI_FWD_BF16_NW>(d, sm1, t_begin, t_end);
+}
+
+// The bf16 epilogue backward at D = 96 with MEP_EPI_BWD_BF16_NW waves per workgroup (12: one
+// 16-token tile per wave at one workgroup per CU over cfg3's 2,400 tiles, instead of two tiles on
+// some of 8 waves; 3 waves per SIMD at <= 168 VGPRs, no spills): cfg3 bf16 25.6 -> 23.2 us
+#ifndef MEP_EPI_BWD_BF16_NW
+#define MEP_EPI_BWD_BF16_NW 12
+#endif
+constexpr int EPI_BWD_BF16_NW = MEP_EPI_BWD_BF16_NW;
+__global__ __launch_bounds__(64 * EPI_BWD_BF16_NW) void k_epi_bwd_bf16w(const mep_epi_bwd_desc* __restrict__ descs) {
+    using E = EpiOne<96, true>;
+    int di, slice;
+    if (!epi_slot(di, slice)) return;
+    const mep_epi_bwd_desc& bd = descs[di];
+    int t_begin, t_end;
+    if (!tile_range(bd.f.ntok, slice, t_begin, t_end)) return;
+    __shared__ __attribute__((aligned(16))) unsigned char sm1[E::BWD_BYTES];
+    if (bd.f.drop_p > 0.f) epi_bwd_one<96, 1, E::BWD_WP, E::BWD_WM, true, EPI_BWD_BF16_NW>(bd, sm1, t_begin, t_end);
+    else epi_bwd_one<96, 1, E::BWD_WP, E::BWD_WM, false, EPI_BWD_BF16_NW>(bd, sm1, t_begin, t_end);
 }
 
 // ---------------------------------------------------------------- weight images
@@ -1791,6 +1828,10 @@ int dispatch_D(int D, F&& f) {
 extern "C" int mep_block_epi_fwd(const mep_epi_desc* descs, int n_desc, int max_tiles, int D, mep_stream_t stream) {
     if (n_desc <= 0 || max_tiles <= 0) return 0;
     const bool bf16 = D & MEP_PREC_BF16;
+    if (bf16 && (D & ~MEP_PREC_BF16) == 96 && EPI_FWD_BF16_NW != EWAVES) {
+        hipLaunchKernelGGL(k_epi_fwd_bf16w, dim3(max_tiles, n_desc), dim3(64 * EPI_FWD_BF16_NW), 0, (hipStream_t)stream, descs);
+        return mep_check_launch("mep_block_epi_fwd");
+    }
     const int rc = dispatch_D(D & ~MEP_PREC_BF16, [&](auto dc) {
         if (bf16) hipLaunchKernelGGL((k_epi_fwd<decltype(dc)::value, true>), dim3(max_tiles, n_desc), dim3(ETHREADS), 0,
                                      (hipStream_t)stream, descs);
@@ -1804,6 +1845,10 @@ extern "C" int mep_block_epi_fwd(const mep_epi_desc* descs, int n_desc, int max_
 extern "C" int mep_block_epi_bwd(const mep_epi_bwd_desc* descs, int n_desc, int max_tiles, int D, mep_stream_t stream) {
     if (n_desc <= 0 || max_tiles <= 0) return 0;
     const bool bf16 = D & MEP_PREC_BF16;
+    if (bf16 && (D & ~MEP_PREC_BF16) == 96 && EPI_BWD_BF16_NW != EWAVES) {
+        hipLaunchKernelGGL(k_epi_bwd_bf16w, dim3(max_tiles, n_desc), dim3(64 * EPI_BWD_BF16_NW), 0, (hipStream_t)stream, descs);
+        return mep_check_launch("mep_block_epi_bwd");
+    }
     const int rc = dispatch_D(D & ~MEP_PREC_BF16, [&](auto dc) {
         if (bf16) hipLaunchKernelGGL((k_epi_bwd<decltype(dc)::value, true>), dim3(max_tiles, n_desc), dim3(ETHREADS), 0,
                                      (hipStream_t)stream, descs);
