@@ -171,6 +171,15 @@ MEP_DEV bool tile_range(int ntok, int slice, int& t_begin, int& t_end) {
 // (pool_head.hip: dmean = dpooled / T, + dmax at the argmax step), so the pooled tensor's gradient
 // [B, T, C] is never written or read (cmu-mosei/run.py:314-318).  pool_T < 0: the head already
 // wrote the mean half of dpooled divided by |pool_T| (the same division, done once per column).
+// dmean = the mean half / T, IEEE division (pool_T > 0, no plan of this repository): out of line, so
+// the compiler cannot evaluate it speculatively on the pool_T < 0 path and select the result (it
+// did: ~10 VALU per element of every tile)
+__attribute__((noinline)) MEP_DEV f32x4 pool_div(f32x4 m, int T) {
+    f32x4 v;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[r] = m[r] / (float)T;
+    return v;
+}
 struct Upstream {
     const gfloat* dp;      // pool: this block's columns of dpooled (mean part; max part at + C)
     const MEP_G int* am;   // pool: this block's columns of argmax
@@ -187,12 +196,10 @@ struct Upstream {
         // moves/selects may flush to zero
         typedef MEP_G const u32x4 gu32x4;
         const u32x4 a = *reinterpret_cast<gu32x4*>(am + (int64_t)b * C + col);
+        const f32x4 dm = T > 0 ? pool_div(mean, T) : mean;   // T < 0: divided by the head
         f32x4 v;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const float dmean = T > 0 ? mean[r] / (float)T : mean[r];   // T < 0: divided by the head
-            v[r] = ((int)a[r] == tg) ? dmean + mx[r] : dmean;
-        }
+        for (int r = 0; r < 4; ++r) v[r] = ((int)a[r] == tg) ? dm[r] + mx[r] : dm[r];
         return v;
     }
 };
