@@ -53,6 +53,9 @@ typedef void* mep_stream_t; /* a hipStream_t */
 #define MEP_BF16_STORE 2
 #define MEP_PREC_BF16 0x10000
 
+/* A row view: token tok = b * T + t sits at ptr + b * sB + t * sT (elements).  Strides are
+ * below 2^24 elements and every element offset of a view below 2^32 (the kernels address rows on
+ * the 24-bit multiplier, csrc/common.h row_off). */
 typedef struct {
     uint64_t ptr;   /* float* base                                  */
     int64_t  sB;    /* stride (floats) between consecutive batch rows */

@@ -189,13 +189,15 @@ struct Upstream {
           C(bd.pool_C), T(bd.pool_T), Tq(bd.pool_Tq), t0(bd.pool_t0) {}
     MEP_DEV f32x4 at(const mep_epi_bwd_desc& bd, int tc, int col) const {
         if (T == 0) return ld4w(row_ptr(bd.dout, tc) + col);
-        const int b = tc / Tq, tg = t0 + (tc - b * Tq);
-        const gfloat* p = dp + (int64_t)b * 2 * C + col;
+        int b, tq;
+        tok_split(tc, Tq, b, tq);
+        const int tg = t0 + tq;
+        const gfloat* p = dp + (int64_t)__umul24((unsigned)b, (unsigned)(2 * C)) + col;
         const f32x4 mean = ld4w(p), mx = ld4w(p + C);
         // the indices as an integer vector: as float bits they would be denormals, which float
         // moves/selects may flush to zero
         typedef MEP_G const u32x4 gu32x4;
-        const u32x4 a = *reinterpret_cast<gu32x4*>(am + (int64_t)b * C + col);
+        const u32x4 a = *reinterpret_cast<gu32x4*>(am + (int64_t)__umul24((unsigned)b, (unsigned)C) + col);
         const f32x4 dm = T > 0 ? pool_div(mean, T) : mean;   // T < 0: divided by the head
         f32x4 v;
 #pragma unroll

@@ -67,13 +67,34 @@ MEP_DEV void st1a(ghalf* p, float v) { *p = (unsigned short)pk_bf16x2(v, 0.f); }
 // reciprocal (v_rcp_f32, 1 ulp) is off by at most one for tok < 2^22 (relative error of the
 // product <= 2^-22), and one correction step each way makes it exact.  Hosts keep every row view
 // under 2^22 rows (4M tokens).
+//
+// MEP_ROW24 (default): the products on the 24-bit multiplier (full rate; v_mul_lo_u32 and the
+// 64-bit multiplies are quarter rate, and an epilogue tile addresses ~8 views).  Needs strides
+// sB, sT < 2^24 elements and every view's element offsets < 2^32 (mep.h, mep_rows; the Python
+// hosts check both when they build a view).
+#ifndef MEP_ROW24
+#define MEP_ROW24 1
+#endif
+// (b, t) = (tok / T, tok % T), tok < 2^22, T < 2^24
+MEP_DEV void tok_split(int tok, int T, int& b, int& t) {
+    b = (int)((float)tok * __builtin_amdgcn_rcpf((float)T));
+    t = tok - (int)__umul24((unsigned)b, (unsigned)T);
+    if (t < 0) { --b; t += T; }
+    if (t >= T) { ++b; t -= T; }
+}
 MEP_DEV int64_t row_off(const mep_rows& r, int tok) {
     const int T = r.T;
+#if MEP_ROW24
+    int b, t;
+    tok_split(tok, T, b, t);
+    return (int64_t)(uint32_t)(__umul24((unsigned)b, (unsigned)r.sB) + __umul24((unsigned)t, (unsigned)r.sT));
+#else
     int b = (int)((float)tok * __builtin_amdgcn_rcpf((float)T));
     int t = tok - b * T;
     if (t < 0) { --b; t += T; }
     if (t >= T) { ++b; t -= T; }
     return (int64_t)b * r.sB + (int64_t)t * r.sT;
+#endif
 }
 MEP_DEV gfloat* row_ptr(const mep_rows& r, int tok) { return G<float>(r.ptr) + row_off(r, tok); }
 // row of an activation view in HS storage (element pointer: ld4a / st4a / ld1a / st1a)

@@ -321,7 +321,11 @@ def make_wgrad(items, dev, tok_per_split=None, bf16=False):
 
 
 def rows(t, T, sB, sT, off=0):
-    """row view of tensor t (strides and offset in elements: 4-byte fp32 or 2-byte bf16 rows)"""
+    """row view of tensor t (strides and offset in elements: 4-byte fp32 or 2-byte bf16 rows);
+    the kernels' 24-bit row addressing (include/mep.h mep_rows) bounds the strides and offsets"""
+    if not (0 <= sB < 1 << 24 and 0 <= sT < 1 << 24 and t.numel() - off <= 1 << 32):
+        raise ValueError('row view out of the kernels\' addressing range: sB %d, sT %d, %d elements'
+                         % (sB, sT, t.numel() - off))
     return Rows(ptr=t.data_ptr() + t.element_size() * off, sB=sB, sT=sT, T=T)
 
 
