@@ -278,6 +278,13 @@ def check_rf_plan(p):
         _colsum(c, d)
     for d in _decode(p.d_sum):
         _sum(c, d)
+    for d in _decode(getattr(p, 'd_isum', None)):
+        # mep_wgemm_sum: every source GEMM's rows and parts, then the sum's output rows
+        assert 1 <= d.n_src <= _lib.WGEMM_SUM_MAX
+        for i in range(d.n_src):
+            _gemm(c, d.src[i], parts=True)
+            assert d.src[i].ntok == d.src[0].ntok and d.src[i].N == d.src[0].N
+        c.rows('wgemm_sum.out', d.out, d.src[0].ntok, d.src[0].N)
     if p.spec.head:
         for d in _decode(p.d_pool):
             _pool(c, d)
@@ -393,6 +400,21 @@ def test_realformer_plan_descriptors_in_bounds(kw, B, P, head):
     finally:
         rf.FFN = old
     assert check_rf_plan(plan) > 20
+    # the cfg2 chain's input gradients run fused with their per-modality sum (<= 4 sources per
+    # sum); State_Transfer's sums have 9 sources and keep the two launches
+    assert (plan.d_isum is not None) == (not head)
+
+
+def test_row_views_within_24_bit_addressing():
+    """include/mep.h mep_rows: strides below 2^24 elements (the kernels' 24-bit row addressing);
+    a host view past that is refused when it is built, not mis-addressed on the GPU"""
+    from mep_amd.trimodal import rows
+    t = torch.zeros(8, 4)
+    assert rows(t, 2, 8, 4).sB == 8
+    with pytest.raises(ValueError):
+        rows(t, 2, 1 << 24, 4)
+    with pytest.raises(ValueError):
+        rows(t, 2, 8, 1 << 24)
 
 
 def _writes(arr_w, arr_c, head=None, NC=None, Fd=None):
