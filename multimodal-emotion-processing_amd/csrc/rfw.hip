@@ -787,12 +787,13 @@ __global__ __launch_bounds__(64 * WGM_WAVES) void k_wgemm(const mep_gemm_desc* _
 }
 
 // ---------------------------------------------------------------- input-gradient GEMMs + their sum
-// mep_wgemm_sum: wave s of a workgroup runs source s's 16 x 32 tile exactly as k_wgemm with one
-// wave does (its k pairs in order, groups of 4 loaded before their MFMAs, then alpha, bias +
-// table, relu, + y), parks the result in LDS, and wave 0 adds the sources in order onto 0 (the
-// k_sum_rows sequence) and writes the sum.  The sources' y rows are read, never written.
-// A workgroup covers 16 tokens x 16 NI columns; every fragment of GP k pairs is loaded before
-// their MFMAs (GP = 6: K <= 192 in one memory latency).
+// mep_wgemm_sum: wave s of a workgroup computes source s's output tile with k_wgemm's arithmetic
+// (one accumulator chain over the k pairs in order, then alpha, bias + table, relu, + y), parks
+// it in LDS, and wave 0 adds the sources in order onto 0 (the k_sum_rows sequence) and writes
+// the sum.  The sources' y rows are read, never written.  A workgroup covers 16 tokens x 16 NI
+// columns; the fragments of GP k pairs are loaded before their MFMAs (GP = 6: K <= 192 in one
+// memory latency).  The group size only schedules loads, so the results match k_wgemm bit for
+// bit (test_wgemm_sum_matches_wgemm_and_sum_rows).
 #ifndef MEP_WGSUM_NI
 #define MEP_WGSUM_NI 1
 #endif
