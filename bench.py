@@ -22,7 +22,9 @@ exclude host submission gaps and sum to at most the step time.
     python bench.py --config cfg2 | cfg5 | rfstate        the other workloads
     python bench.py --dtype bf16                          the bf16 path as the headline line
     torchrun --nproc-per-node N bench.py --gpus N ...      (one process per GPU, RCCL)
-Rank 0 prints one JSON line.
+Rank 0 prints one JSON line.  `--gpus N` without WORLD_SIZE starts the N ranks itself
+(launch_ranks: torch.distributed.run as a child process); with WORLD_SIZE set it must equal N, and
+a node with fewer than N GPUs is refused (exit 2) rather than reported as a smaller run.
 """
 import argparse
 import glob
@@ -661,9 +663,69 @@ def run_config(cls, dev, rank, world, graph, bf16, steps, warmup):
     return work, res, tot, costs, dom
 
 
+def free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(('127.0.0.1', 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n, argv, selftest=False):
+    """`bench.py --gpus N` started without WORLD_SIZE: run N fresh child ranks, one per GPU, under
+    torch.distributed.run (127.0.0.1 rendezvous) and exit with its code.  The children inherit
+    stdout, so rank 0's JSON line is the only line printed.  This parent makes no HIP call and does
+    not exec: torch.cuda.device_count() does not initialise the GPU on this image."""
+    import subprocess
+    if not selftest:
+        have = torch.cuda.device_count()
+        if have < n:
+            print('bench.py: --gpus %d needs %d GPUs, this node has %d; refusing to report a %d-GPU line'
+                  % (n, n, have, n), file=sys.stderr, flush=True)
+            return 2
+    cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', '--nproc-per-node=%d' % n,
+           '--master-addr=127.0.0.1', '--master-port=%d' % free_port(), os.path.abspath(__file__)] + list(argv)
+    env = dict(os.environ)
+    env.setdefault('HSA_ENABLE_IPC_MODE_LEGACY', '0')     # dmabuf IPC (RCCL / shared CUDA tensors)
+    return subprocess.call(cmd, env=env)
+
+
+def rank_devices(dev, world):
+    """[(rank, local rank, device index, PCI bus id)] of every rank (rank 0 reports them all)"""
+    p = torch.cuda.get_device_properties(dev)
+    mine = [int(os.environ.get('RANK', '0')), int(os.environ.get('LOCAL_RANK', '0')), dev.index,
+            '%04x:%02x:%02x' % (getattr(p, 'pci_domain_id', 0), getattr(p, 'pci_bus_id', 0),
+                                getattr(p, 'pci_device_id', 0))]
+    if world == 1:
+        return [mine]
+    got = [None] * world
+    dist.all_gather_object(got, mine)
+    return got
+
+
+def launch_selftest(world, rank):
+    """--launch-selftest (CPU tests): the ranks started by launch_ranks join a gloo group, SUM
+    their rank ids and rank 0 prints one line -- the launcher path without a GPU."""
+    if world > 1:
+        dist.init_process_group('gloo')
+    t = torch.tensor([float(rank + 1)])
+    if world > 1:
+        dist.all_reduce(t)
+    ranks = [rank]
+    if world > 1:
+        ranks = [None] * world
+        dist.all_gather_object(ranks, rank)
+    if rank == 0:
+        print(json.dumps({'metric': 'launcher self-test', 'n_gpus': world, 'rccl_world': world,
+                          'ranks': ranks, 'rank_sum': float(t.item()), 'pid': os.getpid()}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+    return 0
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--launch-selftest', action='store_true', help=argparse.SUPPRESS)
     ap.add_argument('--steps', type=int, default=200)
     ap.add_argument('--warmup', type=int, default=20)
     ap.add_argument('--config', default='cfg3', choices=sorted(CONFIGS))
@@ -677,14 +739,30 @@ def main():
                          "config's BASELINE bf16 line is nested in the same JSON")
     args = ap.parse_args()
     cls = CONFIGS[args.config]
+    if args.gpus < 1:
+        ap.error('--gpus must be >= 1')
 
-    world = int(os.environ.get('WORLD_SIZE', '1'))
+    env_world = os.environ.get('WORLD_SIZE')
+    if env_world is None and args.gpus > 1:
+        return launch_ranks(args.gpus, sys.argv[1:], selftest=args.launch_selftest)
+    world = int(env_world or '1')
+    if world != args.gpus:
+        print('bench.py: --gpus %d but WORLD_SIZE=%d; launch one rank per GPU with matching counts'
+              % (args.gpus, world), file=sys.stderr, flush=True)
+        return 2
     rank = int(os.environ.get('RANK', '0'))
     local = int(os.environ.get('LOCAL_RANK', '0'))
+    if args.launch_selftest:
+        return launch_selftest(world, rank)
     if world > 1:
         torch.cuda.set_device(local)
         dist.init_process_group('nccl', device_id=torch.device('cuda', local))
     dev = torch.device('cuda', local)
+    devices = rank_devices(dev, world)
+    rccl_world = dist.get_world_size() if world > 1 else 1
+    if world > 1 and len({d[3] for d in devices}) != world:
+        print('bench.py: ranks share a GPU: %s' % devices, file=sys.stderr, flush=True)
+        return 2
 
     from mep_amd import _lib
     graph = not args.no_graph
@@ -696,6 +774,8 @@ def main():
         'value': res['value'],
         'unit': work.unit,
         'n_gpus': world,
+        'rccl_world': rccl_world,
+        'rank_devices': devices,
         'steps': args.steps,
         'warmup': args.warmup,
         'ms_per_step': res['ms_per_step'],
@@ -742,7 +822,8 @@ def main():
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+    return 0
 
 
 if __name__ == '__main__':
-    main()
+    sys.exit(main())
