@@ -406,7 +406,10 @@ int mep_wgemm_ws(const mep_gemm_desc* descs, int n_desc, int max_ntok, int max_n
  * 96, alpha / bias / table as mep_gemm, no relu / accumulate, x rows 16-byte aligned and readable
  * up to K rounded up to 4 (MEP_WGEMM_XVEC), ceil(K / 32) = npk_u in {2, 3, 10}; out[o]: parts of a
  * [N_o][96] weight (N_o % 16 == 0), y_o = U W_o^T written; tile_map[t] = o << 8 | (16-column tile
- * of out[o]) for the t < n_tiles output tiles.  Bit-identical to mep_wgemm on the same parts. */
+ * of out[o]) for the t < n_tiles output tiles, 0 <= n_tiles <= MEP_RF_FRONT_MAX_TILES,
+ * 0 < n_out <= MEP_RF_FRONT_MAX_OUT (a descriptor outside these bounds writes nothing), every
+ * tile_map entry naming an o < n_out and a tile < N_o / 16.  Bit-identical to mep_wgemm on the
+ * same parts. */
 /* mep_wgemm_sum: out = sum over s < n_src, in order, of mep_wgemm(src[s]) -- the input-gradient
  * products of one modality and their per-modality sum (mep_sum_rows) in one launch, bit-identical
  * to those launches (each source's mep_wgemm epilogue: alpha * acc (+ its y rows when accumulate),

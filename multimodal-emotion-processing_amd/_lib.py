@@ -430,7 +430,15 @@ RFW = switch('MEP_RFW', '1') != '0'   # 0: the LDS-tiled f32-MFMA realformer ker
 # per-workgroup weight copy does not pay, 41.9 vs 42.6 us); MEP_WGEMM_WS=0: always mep_wgemm
 WGEMM_WS = switch('MEP_WGEMM_WS', '1') != '0'
 WGEMM_WS_MIN = 8192
+WGEMM_WS_MAX_K = 320                               # mep_wgemm_ws: a column block's parts of every k pair in LDS
 WGEMM_XVEC = 0x1                                   # MEP_WGEMM_XVEC
+
+
+def wgemm_ws_fits(items):
+    """mep_wgemm_ws takes the launch: enough tiles to pay for the per-workgroup weight copy, and
+    every K within the LDS-resident column block (mep_wgemm has no K limit)"""
+    return (WGEMM_WS and wgemm_tiles(items) >= WGEMM_WS_MIN and
+            max(d.K for d in items) <= WGEMM_WS_MAX_K)
 
 
 def wgemm_tiles(items):

@@ -15,6 +15,7 @@
 // v_mfma_f32_16x16x32_bf16 -- fp32-level (split.h), no per-fragment split VALU for the weights,
 // which feed only 16 tokens each here.  Weight fragments are streamed through a ring of
 // MEP_RFW_DEPTH fragments ahead of their MFMAs.
+#include <atomic>
 #include <algorithm>
 
 #include "common.h"
@@ -1098,6 +1099,8 @@ __global__ __launch_bounds__(384) void k_rfw_front(const mep_rf_front_desc* __re
     const mep_gemm_desc& u = fd.unify;
     const int ntok = u.ntok;
     if ((int)blockIdx.x * 16 >= ntok) return;
+    // descriptor bounds (uniform per workgroup): tile_map / out[] are fixed-size arrays
+    if (fd.n_tiles < 0 || fd.n_tiles > MEP_RF_FRONT_MAX_TILES || fd.n_out <= 0 || fd.n_out > MEP_RF_FRONT_MAX_OUT) return;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, c = lane & 15, g = lane >> 4;
     const int tok = (int)blockIdx.x * 16 + c, tc = min(tok, ntok - 1);
     // X row blocks: 16-byte loads of K rounded up to 4, clamped (values past K meet zero weights)
@@ -1149,7 +1152,7 @@ __global__ __launch_bounds__(384) void k_rfw_front(const mep_rf_front_desc* __re
         __builtin_amdgcn_sched_barrier(0);
     }
     OpN<3> fa[3], fb[3];
-    frag2(0, fa);   // the first projection tile's weights in flight across the exchange (n_tiles >= 6)
+    if (nj > 0) frag2(0, fa);   // the first projection tile's weights in flight across the exchange
     f32x4 uv;
 #pragma unroll
     for (int r = 0; r < 4; ++r) uv[r] = u.alpha * acc[r] + add[r];
@@ -1240,18 +1243,24 @@ extern "C" int mep_wgemm_ws(const mep_gemm_desc* descs, int n_desc, int max_ntok
     const int nz = (ntf + NT - 1) / NT;
     const dim3 block(64 * W);
     hipStream_t st = (hipStream_t)stream;
-    // persistent: one resident round of workgroups (occupancy by registers and LDS, cached per
-    // instance and block size), each walking its tiles
+    // persistent: one resident round of workgroups, each walking its tiles.  The occupancy (by
+    // registers and LDS) is cached per instance, block size and device -- any host thread may
+    // launch on any device; the cached values are idempotent, so relaxed atomics suffice -- and
+    // the CU count is read per call
     auto run = [&](auto kern, int slot) {
-        static int per_cu[2][16];
-        int& pc = per_cu[W == WGS_MAX_WAVES][slot];
-        if (pc == 0 && hipOccupancyMaxActiveBlocksPerMultiprocessor(&pc, kern, 64 * W, 0) != hipSuccess) pc = 1;
-        pc = std::max(pc, 1);
-        static int n_cu = 0;
-        if (n_cu == 0) {
-            int dev = 0;
-            if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n_cu <= 0) n_cu = 256;
+        constexpr int MAX_DEV = 64;
+        static std::atomic<int> per_cu[MAX_DEV][2][16];
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess || dev < 0) dev = 0;
+        std::atomic<int>& cached = per_cu[dev % MAX_DEV][W == WGS_MAX_WAVES][slot];
+        int pc = cached.load(std::memory_order_relaxed);
+        if (pc == 0) {
+            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&pc, kern, 64 * W, 0) != hipSuccess) pc = 1;
+            pc = std::max(pc, 1);
+            cached.store(pc, std::memory_order_relaxed);
         }
+        int n_cu = 0;
+        if (hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n_cu <= 0) n_cu = 256;
         const int64_t fit = std::max<int64_t>(1, (int64_t)n_cu * pc / ((int64_t)n_desc * nz));
         const int gx = (int)std::min<int64_t>((tiles + W - 1) / W, fit);
         hipLaunchKernelGGL(kern, dim3(gx, n_desc, nz), block, 0, st, descs);

@@ -232,6 +232,12 @@ class RealformerPlan:
                   dsc.x.ptr in self.x_padded and 0 < len(outs) <= _lib.RF_FRONT_MAX_OUT and
                   6 <= tiles <= _lib.RF_FRONT_MAX_TILES and
                   all(q.K == 96 and q.N % 16 == 0 and q.alpha == 1.0 and not (q.bias or q.table or q.accumulate or q.relu)
+                      for q in outs) and
+                  # the kernel reads U from its LDS exchange at the unify's token index and stores
+                  # each output row with 16-byte stores: the projections read U's dense rows of the
+                  # same tokens and write aligned rows
+                  all(q.ntok == dsc.ntok and (q.x.sB, q.x.sT, q.x.T) == (dsc.y.sB, dsc.y.sT, dsc.y.T) and
+                      dsc.y.sT == 96 and q.y.ptr % 16 == 0 and q.y.sB % 4 == 0 and q.y.sT % 4 == 0
                       for q in outs))
             if not ok:
                 return
@@ -583,6 +589,9 @@ class RealformerPlan:
                 self._gemm(self.d_q[i], self.t_epi[i], stream)
             launch('mep_attn_fwd', self.d_attn[i], self.t_attn[i], stream, threads=self.f_attn[i])
             launch('mep_rfw_epi_fwd' if self.rfw else 'mep_rf_epi_fwd', self.d_epi[i], self.t_epif[i], stream, extra=ex)
+        # rfw: the forward epilogues cleared the attention dq rows (mep_rf_epi_desc.zero); the
+        # first backward after this forward may accumulate onto them
+        self._dq_clean = self.rfw
         if sp.head:
             launch('mep_pool_fwd', self.d_pool, self.t_pool, stream)
             _lib.gemm('mep_gemm', self.d_fc, self.t_fc, stream)
@@ -594,8 +603,7 @@ class RealformerPlan:
         """launch name a token-GEMM descriptor array runs under (bench.py / roofline.py)"""
         if not self.rfw:
             return _lib.gemm_launcher('mep_gemm', descs)
-        ws = _lib.WGEMM_WS and _lib.wgemm_tiles(descs.items) >= _lib.WGEMM_WS_MIN
-        return 'mep_wgemm_ws' if ws else 'mep_wgemm'
+        return 'mep_wgemm_ws' if _lib.wgemm_ws_fits(descs.items) else 'mep_wgemm'
 
     def _gemm(self, descs, tiles, stream):
         """a token-GEMM launch: mep_wgemm on the arena's parts, or the mep_gemm path"""
@@ -622,8 +630,11 @@ class RealformerPlan:
             launch('mep_pool_bwd', self.d_pool, self.t_poolb, stream)
         elif ext_dout is not None:
             self.dout_chain.copy_(ext_dout.reshape(self.dout_chain.shape))
-        if not self.rfw:
-            self.dQP_all.zero_()   # (rfw: cleared by the forward epilogues, mep_rf_epi_desc.zero)
+        if not getattr(self, '_dq_clean', False):
+            # the attention backward accumulates dq: a second backward of one forward (retain_graph)
+            # or the round-2 kernels clear the rows here (rfw forwards clear them in their epilogues)
+            self.dQP_all.zero_()
+        self._dq_clean = False
         for i in reversed(range(nl)):
             launch('mep_rfw_epi_bwd' if self.rfw else 'mep_rf_epi_bwd', self.d_epib[i], self.t_epib[i], stream, extra=ex)
             launch('mep_attn_bwd', self.d_attnb[i], self.t_attnb[i], stream, threads=self.f_attnb[i])

@@ -167,3 +167,51 @@ def test_state_transfer_engine_step(name, graph, cuda):
     with torch.no_grad():
         out2 = model(l, v, a, lm, vm, am)
     _check_out(out2, gold['logits2'], um, 1e-3, 1e-5)
+
+
+def test_state_transfer_backward_twice_is_idempotent(cuda):
+    """retain_graph: a second backward of one forward gives the same gradients (the rfw forward
+    clears the attention dq rows once; a second backward clears them itself -- ADVICE r5)"""
+    from mep_amd import realformer as rf
+    meta, gold = fixtures.load('rf_state_small')
+    model = _state(meta, cuda)
+    l, v, a, labels, lm, vm, am, um = _batch(meta, cuda)
+    out = model(l, v, a, lm, vm, am)
+    loss = (rf.multi_circle_loss(out, labels) * um).mean()
+    loss.backward(retain_graph=True)
+    g1 = {k: p.grad.clone() for k, p in model.named_parameters() if p.grad is not None}
+    model.zero_grad(set_to_none=True)
+    loss.backward()
+    g2 = {k: p.grad.clone() for k, p in model.named_parameters() if p.grad is not None}
+    assert g1.keys() == g2.keys() and len(g1) > 10
+    for k in g1:
+        assert torch.equal(g1[k], g2[k]), k
+
+
+def test_state_transfer_wide_features_on_large_plans(cuda):
+    """A State_Transfer plan big enough for mep_wgemm_ws (>= 8192 output tiles per launch) with a
+    feature dim above its K <= 320 limit runs its unify on mep_wgemm: the logits of a
+    B = 64 batch equal, row for row, those of a 2-row batch of the same sequences (rows are
+    independent; the 2-row plan runs the small-launch kernels)."""
+    from mep_amd import _lib
+    from mep_amd import realformer as rf
+    torch.manual_seed(3)
+    T, P, B = 50, 6, 64
+    old = rf.FFN
+    rf.FFN = 2
+    try:
+        m = rf.State_Transfer(l_dim=400, v_dim=35, a_dim=74, dim=96, l_len=T, v_len=T, a_len=T, n_heads=6,
+                              n_layers=2, ffn=2).to(cuda).eval()
+    finally:
+        rf.FFN = old
+    g = torch.Generator(device='cpu').manual_seed(7)
+    feats = [torch.randn(B, P, T, d, generator=g).to(cuda) for d in (400, 35, 74)]
+    masks = [torch.ones(B, P, T, device=cuda) for _ in range(3)]
+    with torch.no_grad():
+        big = m(*feats, *masks)
+        small = m(*[f[:2] for f in feats], *[k[:2] for k in masks])
+    plan = m.mep_runner(cuda).plan(B, P)
+    assert _lib.wgemm_tiles(plan.d_unify.items) >= _lib.WGEMM_WS_MIN
+    assert plan.gemm_launcher(plan.d_unify) == 'mep_wgemm'
+    assert torch.isfinite(big).all()
+    assert_close(big[:2], small.cpu(), 1e-5, 1e-7, 'logits')

@@ -475,3 +475,16 @@ def test_gradient_buckets_partition_the_flat_gradient(family, kw, B, T):
         o = (ptr - g0) // 4
         full[o:o + n] += 1
     assert torch.equal(full, count)
+
+
+def test_wgemm_ws_only_within_its_k_limit():
+    """mep_wgemm_ws keeps a column block's parts of every k pair in LDS and refuses K > 320
+    (rfw.hip mep_wgemm_ws); a large launch with a wider feature dim goes to mep_wgemm"""
+    from types import SimpleNamespace as NS
+    big = [NS(ntok=19200, N=96, K=300), NS(ntok=19200, N=96, K=74), NS(ntok=19200, N=96, K=35)]
+    assert _lib.wgemm_tiles(big) >= _lib.WGEMM_WS_MIN
+    assert _lib.wgemm_ws_fits(big) == _lib.WGEMM_WS
+    wide = [NS(ntok=19200, N=96, K=400)] + big[1:]
+    assert not _lib.wgemm_ws_fits(wide)
+    small = [NS(ntok=3200, N=96, K=300)]
+    assert not _lib.wgemm_ws_fits(small)
