@@ -458,7 +458,8 @@ MEP_DEV void attn_fwd_task(const mep_attn_desc& d, int qc, int h, int b, int lan
             // row statistics for the backward: (max log2 e - log2(1/sum), 1/sum) -- the exp2
             // backward's per-row exponent offset, formed once here instead of per backward tile and
             // key-chunk wave (MEP_BWD_EXP2 = 0: (max, 1/sum))
-            stats[2 * (sbase + q)] = MEP_BWD_EXP2 ? mq * 1.4426950408889634f - __builtin_amdgcn_logf(inv) : mq;
+            // PREV: the raw max -- the backward forms exp(s - max) with s - max exact (F7 below)
+            stats[2 * (sbase + q)] = MEP_BWD_EXP2 && !PREV ? mq * 1.4426950408889634f - __builtin_amdgcn_logf(inv) : mq;
             stats[2 * (sbase + q) + 1] = inv;
         }
 #pragma unroll
@@ -667,7 +668,8 @@ MEP_DEV void attn_fwd_task(const mep_attn_desc& d, int qc, int h, int b, int lan
             for (int kt = 0; kt < NT; ++kt)
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
-                    sv[kt][r] = MEP_FWD_EXP2 || MI ? __builtin_amdgcn_exp2f(fmaf(sv[kt][r], SL2E, -mb)) : __expf(sv[kt][r] - mnew);
+                    sv[kt][r] = (MEP_FWD_EXP2 && !PREV) || MI ? __builtin_amdgcn_exp2f(fmaf(sv[kt][r], SL2E, -mb))
+                                                              : __expf(sv[kt][r] - mnew);
                     if (!(BF && MEP_FWD_MFSUM)) lsum += sv[kt][r];
                 }
             floatx4 oq[NHB];
@@ -1018,7 +1020,7 @@ struct Bwd {
             // the max is kept pre-scaled by log2(e) for exp2
             const bool qok = qq < Tq;
 #if MEP_BWD_EXP2
-            mm[s] = qok ? in.st[s][0] : INFINITY;   // the forward's max log2 e - log2(1/sum)
+            mm[s] = qok ? in.st[s][0] : INFINITY;   // the forward's max log2 e - log2(1/sum) (PREV: max)
 #else
             mm[s] = qok ? in.st[s][0] * LOG2E : INFINITY;
 #endif
@@ -1065,7 +1067,7 @@ struct Bwd {
             // so the exponent below needs no per-score mask add (0 for kept keys: the same bits; a
             // masked or padding key's score stays ~-4e8 / -inf and its P exactly 0).  The fp32
             // instances keep the add (four more live registers spill the 128-register short kernel)
-            constexpr bool MI = BF && MEP_BWD_EXP2;
+            constexpr bool MI = BF && MEP_BWD_EXP2 && !PREV;
             const float m0 = MI ? mts[BF ? kt : 0] : 0.f;
             const floatx4 st = dot16<BF>(qs, kb[kt], floatx4{m0, m0, m0, m0});
 #if MEP_BWD_EXP2
@@ -1085,10 +1087,19 @@ struct Bwd {
                     if (PREV) spv = sprev[si];
                 }
 #if MEP_BWD_EXP2
-                // (dot / 4 [+ c sp] - mask) log2 e - max log2 e with the mask and max terms combined
-                float arg = fmaf(st[r], INV_SCALE * LOG2E, MI ? -mm[r] : -(mtl[kt] + mm[r]));
-                if (PREV) arg = fmaf(cres * LOG2E, spv, arg);
-                const float pv = __builtin_amdgcn_exp2f(arg);
+                float pv;
+                if constexpr (PREV) {
+                    // residual scores (F7): the score in the forward's op order, then exp(s - max) /
+                    // sum with s - max exact.  c * S_prev is ~1e8 at masked keys: for c <= -1 those
+                    // slots carry the row's maximum (~5e7, c < -1) or a score of ~0 (c = -1), and a
+                    // fused (s log2 e - max log2 e) rounds ~1e8-sized terms to whole units of the
+                    // exponent
+                    const float sv = score<PREV>(st[r], cres, spv, mtk[kt]);
+                    pv = __builtin_amdgcn_exp2f((sv - mm[r]) * LOG2E) * li[r];
+                } else {
+                    // (dot / 4 - mask) log2 e - max log2 e with the mask and max terms combined
+                    pv = __builtin_amdgcn_exp2f(fmaf(st[r], INV_SCALE * LOG2E, MI ? -mm[r] : -(mtl[kt] + mm[r])));
+                }
                 float gsv = pv * dp[r];
 #else
                 const float sv = score<PREV>(st[r], cres, spv, mtk[kt]);

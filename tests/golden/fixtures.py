@@ -30,7 +30,7 @@ def load(name):
 
 
 def params(meta, requires_grad=True, device='cpu'):
-    vals = specs.param_values(meta['shapes'], meta['seed'])
+    vals = specs.param_values(meta['shapes'], meta['seed'], meta.get('overrides'))
     return {k: torch.tensor(v, device=device, requires_grad=requires_grad) for k, v in vals.items()}
 
 

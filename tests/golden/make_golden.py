@@ -18,6 +18,7 @@ or ``gradnorm/<key>`` + ``gradhead/<key>`` (first 256 entries, large cases), ``p
 and block cases' ``out``, ``scores`` and input grads.
 """
 import ast
+import copy
 import json
 import math
 import os
@@ -54,11 +55,20 @@ def load_reference(family, overrides):
     return ns
 
 
-def set_params(model, seed):
+def set_params(model, seed, overrides=None):
     shapes = {k: list(v.shape) for k, v in model.state_dict().items()}
-    vals = specs.param_values(shapes, seed)
+    vals = specs.param_values(shapes, seed, overrides)
     model.load_state_dict({k: torch.from_numpy(v) for k, v in vals.items()})
     return shapes
+
+
+def leaf_overrides(model, leaf_values):
+    """{state_dict key: value} for every key whose last component is in leaf_values (e.g. every
+    residual coefficient ``c``)"""
+    if not leaf_values:
+        return None
+    return {k: float(leaf_values[k.rsplit('.', 1)[-1]]) for k in model.state_dict()
+            if k.rsplit('.', 1)[-1] in leaf_values}
 
 
 def t(x):
@@ -108,7 +118,7 @@ class MaskDrop(nn.Module):
         return x * torch.from_numpy(odrop.block_mask(self.seed, self.block, site, B, T, D, self.p))
 
 
-def case_model(name, family, consts, ctor, batch, full, seed, opt, steps=1, drop=None, noise64=False):
+def case_model(name, family, consts, ctor, batch, full, seed, opt, steps=1, drop=None, noise64=False, leaf=None):
     """Whole-model train step(s) as the reference ``train`` performs them.  drop = (p, seed0):
     the blocks' dropout uses the masks of seed advance(seed0) (the engine advances the seed once
     before a training forward).  noise64: also run the reference's first step in float64 and store,
@@ -123,7 +133,8 @@ def case_model(name, family, consts, ctor, batch, full, seed, opt, steps=1, drop
         model = ns['Base_model'](**ctor)
     else:
         model = ns['State_Transfer'](**ctor)
-    shapes = set_params(model, seed)
+    overrides = leaf_overrides(model, leaf)
+    shapes = set_params(model, seed, overrides)
     if drop is not None:
         p, seed0 = drop
         s1 = odrop.seed_advance(seed0)
@@ -132,6 +143,7 @@ def case_model(name, family, consts, ctor, batch, full, seed, opt, steps=1, drop
             for m, blk in enumerate(enc.multimodal_blocks):
                 blk.drop = MaskDrop(e * 9 * nl + m, s1, p)
     model.train()
+    model_for_noise = copy.deepcopy(model) if overrides else None
     if family == 'cmu':
         l, v, a, lm, vm, am, labels = specs.cmu_batch(**batch)
         args = [t(x) for x in (l, v, a, lm, vm, am)]
@@ -180,6 +192,21 @@ def case_model(name, family, consts, ctor, batch, full, seed, opt, steps=1, drop
     dump_params(out, model, 'post', full)
     meta = dict(kind='model', family=family, consts=consts, ctor=ctor, batch=batch, seed=seed,
                 opt=opt, steps=steps, full=full, shapes=shapes)
+    if overrides:
+        meta['overrides'] = overrides
+        out.update(f7_reference_noise(ns, family, model_for_noise, args, labels, full))
+
+        def run(m):
+            logits = m(*args)
+            _loss_of(ns, family, logits, labels, None).backward()
+            nn.utils.clip_grad_norm_(m.parameters(), 1.0)
+            r = {'logits': logits.detach().numpy()}
+            for k, p in m.named_parameters():
+                if p.grad is not None:
+                    g = p.grad.detach().numpy()
+                    r[('grad/' if full else 'gradhead/') + k] = g if full else g.reshape(-1)[:256]
+            return r
+        out.update(perturbed_spread(model_for_noise, run, out, skip=overrides))
     if drop is not None:   # its own kind: the CPU oracle has no per-site masks
         meta.update(kind='model_drop', drop=dict(p=drop[0], seed0=drop[1], seed=odrop.seed_advance(drop[1])))
     return meta, out
@@ -254,6 +281,26 @@ def fp64_noise(ns, family, model, args, labels, um, full, runs=6):
     return out
 
 
+def f7_reference_noise(ns, family, model, args, labels, full):
+    """The reference's first step in float64 on the fixture's own parameters and inputs (F7
+    fixtures, c <= -1): logits64 and grad64/<param> (post-clip, like grad/<param>).  Where the
+    masked slots carry the row's maximum (c < -1) or lose their -1e8 (c = -1) the reference's fp32
+    scores there are set by the fp32 rounding of ~1e8-sized terms, so its float64 run is a
+    different function; the pair shows which entries depend on that rounding."""
+    m = copy.deepcopy(model).double()
+    a = [x.double() if x.is_floating_point() else x for x in args]
+    lab = labels.double() if labels.is_floating_point() else labels
+    logits = m(*a)
+    _loss_of(ns, family, logits, lab, None).backward()
+    nn.utils.clip_grad_norm_(m.parameters(), 1.0)
+    out = {'logits64': logits.detach().numpy()}
+    for k, p in m.named_parameters():
+        if p.grad is not None:
+            g = p.grad.detach().numpy()
+            out[('grad64/' if full else 'grad64head/') + k] = g if full else g.reshape(-1)[:256]
+    return out
+
+
 def ctor_heads(m):
     return m.feature.multimodal_blocks[0].n_heads
 
@@ -262,59 +309,122 @@ def ctor_layers(m):
     return len(m.feature.multimodal_blocks) // 9
 
 
-def case_block(name, family, consts, ctor, B, Tq, Tk, seed, with_prev=True, g_scores=True):
+def perturbed_spread(module, run, base, skip=(), runs=6, seed=20261019):
+    """F7 fixtures: the reference's own fp32 sensitivity.  `run(copy)` evaluates the case on a copy
+    of `module` and returns {name: array}; it is repeated on `runs` copies with every parameter
+    scaled by 1 + 2^-18 N(0, 1) -- except the overridden ones in `skip` (c = -1 is a singular
+    point: any other c leaves the masked slots ~1e8 * (1 + c) away from cancelling), and
+    spread/<name> is the largest relative L2 distance of such a
+    run from the unperturbed fp32 result `base` (spreadabs/<name>: the largest elementwise
+    absolute distance).  Quantities that are sums of ~1e8-sized
+    cancelling terms (the gradient of c through S_prev = -1e8 at masked keys) scatter by far more
+    than fp32's epsilon between two such runs; a parity check of them can be no tighter."""
+    gen = torch.Generator().manual_seed(seed)
+    out = {}
+    for _ in range(runs):
+        m = copy.deepcopy(module)
+        with torch.no_grad():
+            for k, prm in m.named_parameters():
+                noise = torch.randn(prm.shape, generator=gen)
+                if k not in skip:
+                    prm.mul_(1 + 2.0 ** -18 * noise)
+        for k, v in run(m).items():
+            b = np.asarray(base[k], np.float64)
+            e = float(np.linalg.norm(np.asarray(v, np.float64) - b) / max(np.linalg.norm(b), 1e-30))
+            out['spread/' + k] = np.float64(max(e, float(out.get('spread/' + k, 0.0))))
+            a = float(np.abs(np.asarray(v, np.float64) - b).max()) if b.size else 0.0
+            out['spreadabs/' + k] = np.float64(max(a, float(out.get('spreadabs/' + k, 0.0))))
+    return out
+
+
+def case_block(name, family, consts, ctor, B, Tq, Tk, seed, with_prev=True, g_scores=True, leaf=None):
     """Standalone Attention_Block forward/backward with residual scores and an upstream
-    gradient on both outputs (out, post-mask scores)."""
+    gradient on both outputs (out, post-mask scores).  leaf: constant parameter overrides (the
+    F7 fixtures' c <= -1); those also store the same computation in float64 (<key>64) and the
+    reference's fp32 spread under parameter perturbation (perturbed_spread)."""
     ns = load_reference(family, consts)
     blk = ns['Attention_Block'](**ctor)
-    shapes = set_params(blk, seed)
+    overrides = leaf_overrides(blk, leaf)
+    shapes = set_params(blk, seed, overrides)
     D, H = ctor['dim'], ctor['n_heads']
     q, kv, mask, s_prev, g_out = specs.block_inputs(seed + 1, B, Tq, Tk, D, H, with_prev)
-    qt, kvt = t(q).requires_grad_(), t(kv).requires_grad_()
-    sp = t(s_prev).requires_grad_() if with_prev else None
-    y, s = blk(qt, kvt, kvt, t(mask), sp)
-    obj = (y * t(g_out)).sum()
     rng = np.random.default_rng(seed + 2)
-    g_s = (0.05 * rng.standard_normal(s.shape)).astype(np.float32)
-    if g_scores:
-        obj = obj + (s * t(g_s)).sum()
-    obj.backward()
-    out = {'out': y.detach().numpy(), 'scores': s.detach().numpy(), 'g_scores': g_s,
-           'grad_q': qt.grad.numpy(), 'grad_kv': kvt.grad.numpy()}
-    if with_prev:
-        out['grad_sprev'] = sp.grad.numpy()
+    g_s = (0.05 * rng.standard_normal((B, H, Tq, Tk))).astype(np.float32)
+
+    def run(b, dt=torch.float32):
+        qt, kvt = t(q).to(dt).requires_grad_(), t(kv).to(dt).requires_grad_()
+        sp = t(s_prev).to(dt).requires_grad_() if with_prev else None
+        y, s = b(qt, kvt, kvt, t(mask).to(dt), sp)
+        obj = (y * t(g_out).to(dt)).sum()
+        if g_scores:
+            obj = obj + (s * t(g_s).to(dt)).sum()
+        obj.backward()
+        r = {'out': y.detach().numpy(), 'scores': s.detach().numpy(), 'grad_q': qt.grad.numpy(),
+             'grad_kv': kvt.grad.numpy()}
+        if with_prev:
+            r['grad_sprev'] = sp.grad.numpy()
+        for k, p in b.named_parameters():
+            if p.grad is not None:
+                r['grad/' + k] = p.grad.numpy().copy()
+        return r
+    out = {'g_scores': g_s}
+    base = run(blk)
+    out.update({k: v for k, v in base.items() if not k.startswith('grad/')})
     dump_grads(out, blk, True)
+    if overrides:
+        fresh = copy.deepcopy(blk)
+        fresh.zero_grad(set_to_none=True)
+        for k, v in run(copy.deepcopy(fresh).double(), torch.float64).items():
+            out[k.replace('grad/', 'grad64/') if k.startswith('grad/') else k + '64'] = v
+        out.update(perturbed_spread(fresh, run, base, skip=overrides))
     meta = dict(kind='block', family=family, consts=consts, ctor=ctor, B=B, Tq=Tq, Tk=Tk,
                 seed=seed, with_prev=with_prev, g_scores=g_scores, shapes=shapes)
+    if overrides:
+        meta['overrides'] = overrides
     return meta, out
 
 
-def case_chain(name, consts, ctor, B, T, n_layers, seed):
+def case_chain(name, consts, ctor, B, T, n_layers, seed, leaf=None):
     """realformer "text chain" (BASELINE cfg2): Conv1d unify of l + position embedding +
-    ``n_layers`` residual blocks (multimodal_blocks[0..n_layers-1]); objective mean(out * G)."""
+    ``n_layers`` residual blocks (multimodal_blocks[0..n_layers-1]); objective mean(out * G).
+    leaf: constant parameter overrides (F7: c <= -1), stored with every layer's post-mask scores
+    (scores<i>), the float64 twin (<key>64) and the reference's fp32 spread (perturbed_spread)."""
     ns = load_reference('realformer', consts)
     mc = ns['Multi_class'](**ctor)
-    shapes = set_params(mc, seed)
+    overrides = leaf_overrides(mc, leaf)
+    shapes = set_params(mc, seed, overrides)
     rng = np.random.default_rng(seed + 1)
     lm = specs.masks_for(rng, (B,), T)
     x = specs.features(rng, (B, T, consts['L_DIM']), lm)
     G = rng.standard_normal((B, T, ctor['dim'])).astype(np.float32)
-    xt = t(x)
-    lt = mc.unify_dimension.linguistic(xt.transpose(1, 2)).transpose(1, 2)
-    lt = lt + mc.linguistic_position(lt)
-    h, s = lt, None
-    for i in range(n_layers):
-        h, s = mc.multimodal_blocks[i](h, lt, lt, t(lm), s)
-    obj = (h * t(G)).mean()
-    obj.backward()
-    out = {'out': h.detach().numpy(), 'obj': np.float64(obj.item())}
-    grads = {}
-    for k, p in mc.named_parameters():
-        if p.grad is not None:
-            grads['grad/' + k] = p.grad.numpy().copy()
-    out.update(grads)
+
+    def run(m, dt=torch.float32):
+        xt = t(x).to(dt)
+        lt = m.unify_dimension.linguistic(xt.transpose(1, 2)).transpose(1, 2)
+        lt = lt + m.linguistic_position(lt)
+        h, s = lt, None
+        r = {}
+        for i in range(n_layers):
+            h, s = m.multimodal_blocks[i](h, lt, lt, t(lm).to(dt), s)
+            if overrides:
+                r['scores%d' % i] = s.detach().numpy()
+        obj = (h * t(G).to(dt)).mean()
+        obj.backward()
+        r.update({'out': h.detach().numpy(), 'obj': np.float64(obj.item())})
+        for k, p in m.named_parameters():
+            if p.grad is not None:
+                r['grad/' + k] = p.grad.numpy().copy()
+        return r
+    fresh = copy.deepcopy(mc)
+    out = run(mc)
+    if overrides:
+        for k, v in run(copy.deepcopy(fresh).double(), torch.float64).items():
+            out[k.replace('grad/', 'grad64/') if k.startswith('grad/') else k + '64'] = v
+        out.update(perturbed_spread(fresh, run, {k: v for k, v in out.items() if '64' not in k}, skip=overrides))
     meta = dict(kind='chain', family='realformer', consts=consts, ctor=ctor, B=B, T=T,
                 n_layers=n_layers, seed=seed, shapes=shapes)
+    if overrides:
+        meta['overrides'] = overrides
     return meta, out
 
 
@@ -420,6 +530,24 @@ CASES = {
                                             dict(l_dim=300, v_dim=35, a_dim=74, dim=96, l_len=50, v_len=50,
                                                  a_len=50, n_heads=6, n_layers=2, ffn=2), 64, 50, 2, 112),
 }
+
+# F7: residual coefficients c <= -1.  The post-mask scores carry
+# -1e8 at masked keys; c * S_prev flips them to about +1.5e8 (c = -1.5: after the mask term the
+# masked slots hold ~+5e7, the row's maximum, and take the whole softmax) or cancels the mask
+# term exactly (c = -1: masked slots score ~0 beside the kept keys): cmu-mosei/run.py:243-254,
+# others/realformer.py:190-201.  Every c of the model is set (first-layer c take no gradient).
+for _c, _tag in ((-1.5, 'm15'), (-1.0, 'm1')):
+    CASES['cmu_f7_' + _tag] = (lambda c=_c, tag=_tag: case_model(
+        'cmu_f7_' + tag, 'cmu', CMU_C, cmu_ctor(32, 2, 2), dict(seed=12, B=4, T=[6, 10, 8]), True, 102, 'adamw',
+        leaf={'c': c}))
+    CASES['rf_chain_f7_' + _tag] = (lambda c=_c, tag=_tag: case_chain(
+        'rf_chain_f7_' + tag, rf_consts(10), dict(l_dim=300, v_dim=35, a_dim=74, dim=32, l_len=10, v_len=10,
+                                               a_len=10, n_heads=2, n_layers=2, ffn=2), 4, 10, 2, 110,
+        leaf={'c': c}))
+    CASES['block_cmu_f7_' + _tag] = (lambda c=_c, tag=_tag: case_block(
+        'block_cmu_f7_' + tag, 'cmu', CMU_C, dict(dim=32, n_heads=2, ffn=1), 3, 7, 11, 107, leaf={'c': c}))
+    CASES['block_rf_f7_' + _tag] = (lambda c=_c, tag=_tag: case_block(
+        'block_rf_f7_' + tag, 'realformer', rf_consts(8), dict(dim=32, n_heads=2), 3, 8, 10, 109, leaf={'c': c}))
 
 
 def main(names):

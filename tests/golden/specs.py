@@ -10,11 +10,14 @@ import zlib
 import numpy as np
 
 
-def param_values(shapes, seed):
+def param_values(shapes, seed, overrides=None):
     """shapes: {state_dict key: shape}.  Returns {key: float32 ndarray} with values spread wide
     enough that every parameter influences the output (LayerNorm affine != identity, residual
-    scalars c/a/b != 0, bilinear ``trans`` U[0,1) like torch.rand)."""
+    scalars c/a/b != 0, bilinear ``trans`` U[0,1) like torch.rand).  overrides: {key: value}
+    sets whole tensors to a constant (the F7 fixtures' residual coefficients c <= -1)."""
     out = {}
+    overrides = overrides or {}
+    assert set(overrides) <= set(shapes), sorted(set(overrides) - set(shapes))
     for key, shape in shapes.items():
         rng = np.random.default_rng((seed * 1000003) ^ zlib.crc32(key.encode()))
         shape = tuple(shape)
@@ -32,6 +35,8 @@ def param_values(shapes, seed):
         else:
             fan_in = int(np.prod(shape[1:])) if len(shape) > 1 else shape[0]
             v = rng.standard_normal(shape) / np.sqrt(fan_in)
+        if key in overrides:
+            v = np.full(shape, overrides[key])
         out[key] = v.astype(np.float32)
     return out
 

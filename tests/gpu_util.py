@@ -25,6 +25,27 @@ def assert_close(got, want, rtol, atol_frac=1e-5, name=''):
                              % (name, int(bad.sum()), bad.size, i, g[i], w[i], rtol, atol))
 
 
+def close_or_spread(got, gold, key, rtol, atol_frac=1e-5, name=None):
+    """assert_close against gold[key]; on an F7 fixture (residual coefficients c <= -1,
+    make_golden.py perturbed_spread) a tensor the reference's own fp32 scatters on may instead lie
+    within twice that scatter: max |got - want| <= 2 spreadabs/<key> (the largest elementwise
+    distance of a reference fp32 run with its other parameters scaled by 1 + 2^-18 N from the
+    fixture).  Sums of ~1e8-sized cancelling terms -- the gradient of c through S_prev = -1e8 at
+    masked keys -- land anywhere in that range from one fp32 execution to the next."""
+    want = gold[key]
+    try:
+        assert_close(got, want, rtol, atol_frac, name or key)
+        return
+    except AssertionError:
+        if 'spreadabs/' + key not in gold:
+            raise
+    g = got.detach().double().cpu().numpy() if torch.is_tensor(got) else np.asarray(got, np.float64)
+    w = np.asarray(want, np.float64).reshape(g.shape)
+    err = float(np.abs(g - w).max())
+    allow = 2.0 * float(gold['spreadabs/' + key])
+    assert err <= allow, '%s: max error %.3g beyond 2x the reference fp32 scatter %.3g' % (name or key, err, allow)
+
+
 def _role(k):
     import re
     return re.sub(r'blocks\.\d+\.', 'blocks.*.', k)
@@ -97,7 +118,7 @@ def check_post_budget(model, meta, gold, lr=1e-3, atol=2e-5):
 
 
 def load_params(model, meta):
-    vals = specs.param_values(meta['shapes'], meta['seed'])
+    vals = specs.param_values(meta['shapes'], meta['seed'], meta.get('overrides'))
     model.load_state_dict({k: torch.from_numpy(v) for k, v in vals.items()})
     return model
 

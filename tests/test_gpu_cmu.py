@@ -9,7 +9,7 @@ import pytest
 import torch
 
 from tests.golden import fixtures
-from tests.gpu_util import OUT_ATOL_FRAC, assert_close, check_post_params, cmu_model, cuda_batch
+from tests.gpu_util import OUT_ATOL_FRAC, assert_close, check_post_params, close_or_spread, cmu_model, cuda_batch
 
 pytestmark = pytest.mark.gpu
 CMU = [n for n in fixtures.names('model') if fixtures.load(n)[0]['family'] == 'cmu']
@@ -34,7 +34,7 @@ def test_concat_trans_autograd(name, cuda):
             continue
         g = p.grad * coef  # fixture holds post-clip gradients
         if meta['full']:
-            assert_close(g, gold['grad/' + k], 1e-3, 1e-5, k)
+            close_or_spread(g, gold, 'grad/' + k, 1e-3, 1e-5)
         else:
             assert_close(g.reshape(-1)[:256], gold['gradhead/' + k], 1e-3, 1e-5, k)
             assert_close(torch.linalg.vector_norm(g.double()), gold['gradnorm/' + k], 1e-3, 0, k)
@@ -85,13 +85,13 @@ def test_attention_block_standalone(name, cuda):
     if meta['g_scores']:
         obj = obj + (s * torch.tensor(gold['g_scores'], device=cuda)).sum()
     obj.backward()
-    assert_close(qt.grad, gold['grad_q'], 1e-3, 1e-5, 'grad_q')
-    assert_close(kvt.grad, gold['grad_kv'], 1e-3, 1e-5, 'grad_kv')
+    close_or_spread(qt.grad, gold, 'grad_q', 1e-3, 1e-5)
+    close_or_spread(kvt.grad, gold, 'grad_kv', 1e-3, 1e-5)
     if sp is not None:
-        assert_close(sp.grad, gold['grad_sprev'], 1e-3, 1e-5, 'grad_sprev')
+        close_or_spread(sp.grad, gold, 'grad_sprev', 1e-3, 1e-5)
     for k, p in blk.named_parameters():
         if 'nograd/' + k in gold:
             assert p.grad is None, k
         else:
-            assert_close(p.grad, gold['grad/' + k], 1e-3, 1e-5, k)
+            close_or_spread(p.grad, gold, 'grad/' + k, 1e-3, 1e-5)
     assert np.isfinite(y.detach().cpu().numpy()).all()

@@ -21,8 +21,8 @@ import pytest
 import torch
 
 from tests.golden import fixtures
-from tests.gpu_util import (assert_close, check_grad_budget, check_post_budget, check_post_params, has_fp32_budget,
-                            load_params)
+from tests.gpu_util import (assert_close, check_grad_budget, check_post_budget, check_post_params, close_or_spread,
+                            has_fp32_budget, load_params)
 
 pytestmark = pytest.mark.gpu
 
@@ -39,8 +39,14 @@ def ffn_const(meta):
         rf.FFN = old
 
 
-def test_realformer_block_standalone(cuda):
-    meta, gold = fixtures.load('block_rf')
+RF_BLOCKS = [n for n in fixtures.names('block') if fixtures.load(n)[0]['family'] == 'realformer']
+
+
+@pytest.mark.parametrize('name', RF_BLOCKS)
+def test_realformer_block_standalone(name, cuda):
+    """block_rf, and the F7 fixtures block_rf_f7_m15 / _m1 (c = -1.5 / -1: the masked slots carry
+    the row's maximum / lose their -1e8; make_golden.py F7)"""
+    meta, gold = fixtures.load(name)
     with ffn_const(meta) as rf:
         blk = rf.Attention_Block(meta['ctor']['dim'], meta['ctor']['n_heads'])
     load_params(blk, meta)
@@ -50,15 +56,15 @@ def test_realformer_block_standalone(cuda):
     kvt = torch.tensor(kv, device=cuda, requires_grad=True)
     sp = torch.tensor(s_prev, device=cuda, requires_grad=True)
     y, s = blk(qt, kvt, kvt, torch.tensor(mask, device=cuda), sp)
-    assert_close(y, gold['out'], 1e-4, 1e-6, 'out')
-    assert_close(s, gold['scores'], 1e-5, 1e-7, 'scores')
+    close_or_spread(y, gold, 'out', 1e-4, 1e-6)
+    close_or_spread(s, gold, 'scores', 1e-5, 1e-7)
     obj = (y * torch.tensor(g_out, device=cuda)).sum() + (s * torch.tensor(gold['g_scores'], device=cuda)).sum()
     obj.backward()
-    assert_close(qt.grad, gold['grad_q'], 1e-3, 1e-5, 'grad_q')
-    assert_close(kvt.grad, gold['grad_kv'], 1e-3, 1e-5, 'grad_kv')
-    assert_close(sp.grad, gold['grad_sprev'], 1e-3, 1e-5, 'grad_sprev')
+    close_or_spread(qt.grad, gold, 'grad_q', 1e-3, 1e-5)
+    close_or_spread(kvt.grad, gold, 'grad_kv', 1e-3, 1e-5)
+    close_or_spread(sp.grad, gold, 'grad_sprev', 1e-3, 1e-5)
     for k, p in blk.named_parameters():
-        assert_close(p.grad, gold['grad/' + k], 1e-3, 1e-5, k)
+        close_or_spread(p.grad, gold, 'grad/' + k, 1e-3, 1e-5)
 
 
 @pytest.mark.parametrize('name', fixtures.names('chain'))
@@ -77,7 +83,7 @@ def test_text_chain(name, cuda):
     obj.backward()
     for k, p in mc.named_parameters():
         if 'grad/' + k in gold:
-            assert_close(p.grad, gold['grad/' + k], 1e-3, 1e-5, k)
+            close_or_spread(p.grad, gold, 'grad/' + k, 1e-3, 1e-5)
         else:
             assert p.grad is None or float(p.grad.abs().max()) == 0.0, k
 
