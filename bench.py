@@ -157,25 +157,32 @@ def hbm_probe(dev, gib=2):
     src = torch.ones(n16 * 4, dtype=torch.float32, device=dev)
     dst = torch.empty_like(src)
     out = {}
+    variants = {0: 'grid-stride', 4: 'blocked', 12: 'blocked+nontemporal'}   # MEP_PROBE_BLOCKED / _NT
     for mode, key, factor in ((0, 'copy', 2), (1, 'read', 1), (2, 'write', 1)):
-        best = 0.0
-        for n_wg in (1024, 2048, 4096):
-            def go():
-                _lib.call('mep_hbm_probe', ctypes.c_void_p(src.data_ptr()), ctypes.c_void_p(dst.data_ptr()), n16,
-                          mode, n_wg)
-            go()
-            torch.cuda.synchronize()
-            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            reps = 10
-            a.record()
-            for _ in range(reps):
+        best, how = 0.0, None
+        for flags, vname in variants.items():
+            for n_wg in (1024, 2048, 4096):
+                def go():
+                    _lib.call('mep_hbm_probe', ctypes.c_void_p(src.data_ptr()), ctypes.c_void_p(dst.data_ptr()), n16,
+                              mode | flags, n_wg)
                 go()
-            b.record()
-            torch.cuda.synchronize()
-            best = max(best, factor * 16 * n16 * reps / (a.elapsed_time(b) / 1e3) / 1e9)
+                torch.cuda.synchronize()
+                a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                reps = 10
+                a.record()
+                for _ in range(reps):
+                    go()
+                b.record()
+                torch.cuda.synchronize()
+                rate = factor * 16 * n16 * reps / (a.elapsed_time(b) / 1e3) / 1e9
+                if rate > best:
+                    best, how = rate, '%s, %d workgroups' % (vname, n_wg)
         out[key + '_GBps'] = round(best, 1)
-    out.update(buffer_GiB=gib, kernel='mep_hbm_probe (csrc/probe.hip): dwordx4 grid-stride, 8 loads in flight per '
-               'thread, best of 1024 / 2048 / 4096 workgroups')
+        out[key + '_best'] = how
+    out.update(buffer_GiB=gib, kernel='mep_hbm_probe (csrc/probe.hip): dwordx4 streams, 8 loads in flight per '
+               'thread; best of grid-stride / blocked / blocked nontemporal orders x 1024 / 2048 / 4096 workgroups',
+               guide_GBps=6290.0,
+               guide='MI355X_MICROARCH.md: 6.29 TB/s measured float4 copy (79% of the 8 TB/s spec)')
     del src, dst
     torch.cuda.empty_cache()
     return out
@@ -213,6 +220,25 @@ def pmc_traffic(launch, tag='cfg3'):
                 continue                                 # the prefix of the other GEMM
             if k.startswith(prefix) and isinstance(v, dict) and 'hbm_bytes_per_dispatch' in v:
                 return int(v['hbm_bytes_per_dispatch']), os.path.relpath(f, ROOT)
+    return None, None
+
+
+def pmc_valu(launch, tag='cfg3'):
+    """(VALU instructions per dispatch, source file) of the kernels behind `launch` from the newest
+    committed SQ counter pass of this workload (profiles/r<round>_counters_<tag>.json, SQ_INSTS_VALU),
+    or (None, None)."""
+    prefix = KERNEL_OF.get(launch)
+    if prefix is None:
+        return None, None
+    longer = [p for p in set(KERNEL_OF.values()) if p != prefix and p.startswith(prefix)]
+    files = glob.glob(os.path.join(ROOT, 'profiles', 'r*_counters_%s.json' % tag))
+    for f in sorted(files, key=lambda f: [int(x) for x in re.findall(r'\d+', os.path.basename(f))], reverse=True):
+        tot = 0.0
+        for k, v in json.load(open(f)).items():
+            if k.startswith(prefix) and not any(k.startswith(p) for p in longer) and isinstance(v, dict):
+                tot += float(v.get('raw', {}).get('SQ_INSTS_VALU', 0.0))
+        if tot > 0:
+            return tot, os.path.relpath(f, ROOT)
     return None, None
 
 
@@ -613,14 +639,23 @@ def roofline_of(work, name, tot, costs, probe=None):
     per_launch_s = t / n
     flops, nbytes = costs[name]
     spec = getattr(work.plan, 'spec', None)
-    rl = roofline.roofline_entry(name, flops / n, nbytes / n, per_launch_s, bf16=work.bf16, D=getattr(spec, 'D', None))
-    rl['traffic'], rl['traffic_source'] = pmc_traffic(name, work.name + ('_bf16' if work.bf16 else ''))
+    tag = work.name + ('_bf16' if work.bf16 else '')
+    valu, vsrc = pmc_valu(name, tag)
+    rl = roofline.roofline_entry(name, flops / n, nbytes / n, per_launch_s, bf16=work.bf16, D=getattr(spec, 'D', None),
+                                 valu=(valu / n, vsrc) if valu else None)
+    rl['traffic'], rl['traffic_source'] = pmc_traffic(name, tag)
     rl['avg_launch_us'] = round(per_launch_s * 1e6, 2)
     rl['launches_per_step'] = n
     if probe and rl['bound'] == 'hbm':
         rl['peak_measured'] = probe['read_GBps']
         rl['frac_measured'] = round(rl['achieved'] / probe['read_GBps'], 4)
+        rl['frac_guide'] = round(rl['achieved'] / probe['guide_GBps'], 4)
     return rl
+
+
+def roofline_all(work, tot, costs, probe=None):
+    """every priced launch of the step: {launch: roofline object} (bound, frac, VALU floor, limiter)"""
+    return {k: roofline_of(work, k, tot, costs, probe) for k in sorted(tot, key=lambda k: -tot[k][0]) if k in costs}
 
 
 def run_config(cls, dev, rank, world, graph, bf16, steps, warmup):
@@ -788,6 +823,7 @@ def main():
         'loss': res['loss'],
         'roofline': roofline_of(work, dom, tot, costs, probe),
         'roofline_attention': roofline_of(work, 'mep_attn_bwd', tot, costs, probe),
+        'rooflines': roofline_all(work, tot, costs, probe),
         'kernels': res['kernels'],
         'kernels_sum_ms': res['kernels_sum_ms'],
         'kernel_timing': res['kernel_timing'],
@@ -801,6 +837,7 @@ def main():
         w2, r2, tot2, costs2, dom2 = run_config(cls, dev, rank, world, graph, True, args.steps, args.warmup)
         r2['roofline'] = roofline_of(w2, dom2, tot2, costs2, probe)
         r2['roofline_attention'] = roofline_of(w2, 'mep_attn_bwd', tot2, costs2, probe)
+        r2['rooflines'] = roofline_all(w2, tot2, costs2, probe)
         r2['dtype'] = 'bf16'
         out['bf16'] = r2
         del w2

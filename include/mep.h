@@ -32,7 +32,7 @@ extern "C" {
 #endif
 
 #define MEP_EINVAL (-1000)
-#define MEP_ABI_VERSION 4
+#define MEP_ABI_VERSION 5
 
 typedef void* mep_stream_t; /* a hipStream_t */
 
@@ -110,9 +110,6 @@ int mep_unify(const mep_gemm_desc* descs, int n_desc, int n_wg, mep_stream_t str
  * w_nt = 0, W stored [K][N]); y rows (and bias) 16-byte aligned; N in {32, 64, 96} or >= 128.
  * Grid: (ceil(max_ntok / 128), n_desc, N tiles). */
 #define MEP_TGEMM_WT 0x1
-#define MEP_TGEMM_RESIDENT 0x2   /* every K <= 320: the whole weight tile (N tiles of 96) staged in LDS
-                                    once per workgroup, as 2 bf16 parts on the fp32 path (five
-                                    products per k pair, weight error <= 2^-18 relative) */
 #define MEP_TGEMM_DMA 0x4        /* w_nt = 1 only: the fp32 weight chunks staged by LDS-DMA into a ring of
                                     4 slots (3 chunks in flight; K tails, rows past N and unaligned rows
                                     by plain loads) and split into the path's bf16 parts on the
@@ -211,6 +208,30 @@ typedef struct {
 #define MEP_ATTN_MAX_KCHUNKS 8
 int mep_attn_fwd(const mep_attn_desc* descs, int n_desc, int max_tiles, int flags, mep_stream_t stream);
 
+/* mep_attn_general_fwd / _bwd: the reference multi_head_attention for every mask form it accepts
+ * (cmu-mosei/run.py:236-257): f.mask = 0 (no mask: nothing subtracted), a key mask (mask_sQ = 0) or
+ * a [B, Tq, Tk] mask (element mask[b * mask_sB + q * mask_sQ + k], shared by the heads), residual
+ * scores as mep_attn_fwd, k != v, head dim hd <= 64, s = (q . k) / scale with scale = float(sqrt(hd))
+ * (a correctly rounded division), Tk <= 4096.  fp32, the score in the reference's op order, one
+ * workgroup per (b, h) (grid max_bh = max B * H), every sum in a fixed order.  f.stats receives the
+ * raw (max, 1/sum) per row.  Backward: dq accumulated (+=), dk / dv written (dk.ptr == dv.ptr: k is v, their
+ * sum written), ds_prev = c * dS (0: none), dc_partial one float per (b, h) (0: none), ds_next the
+ * gradient on the post-mask scores output (0: none).  The standalone Attention_Block.forward with a
+ * 3-D mask runs here; the model plans never pass one. */
+typedef struct {
+    mep_attn_desc f;
+    int64_t  mask_sQ;
+    int32_t  hd;
+    float    scale;
+} mep_attn_gen_desc;
+typedef struct {
+    mep_attn_gen_desc g;
+    mep_rows dx, dq, dk, dv;
+    uint64_t ds_next, ds_prev, dc_partial;
+} mep_attn_gen_bwd_desc;
+int mep_attn_general_fwd(const mep_attn_gen_desc* descs, int n_desc, int max_bh, mep_stream_t stream);
+int mep_attn_general_bwd(const mep_attn_gen_bwd_desc* descs, int n_desc, int max_bh, int max_hd, mep_stream_t stream);
+
 /* Backward of the attention core.  Inputs dx (grad of X), the forward's q/k/v/x/stats/s_prev.
  * Outputs: dq += (written with accumulate semantics onto dq_base), dk, dv (dk==dv pointer ->
  * summed, for k is v), ds_prev = c * dS (grad of S_prev) and a per-workgroup partial of
@@ -224,14 +245,6 @@ typedef struct {
     uint64_t ds_next;   /* [B,H,Tq,Tk] or 0                        */
     uint64_t ds_prev;   /* [B,H,Tq,Tk] or 0                        */
     uint64_t dc_partial;/* [B * H * ceil(Tk/64)] floats or 0       */
-    /* Per-modality sums folded in (SHORT descriptors only; sum = 0: none).  sum points at the
-     * plan's mep_sum_desc array; sum_q / sum_kv index the sum this descriptor's dq / dk rows are a
-     * source of (-1: none); sum_count holds sum_stride int32 counters per sum, zero before the
-     * first launch (B * H slices).  The (b, h) unit whose arrival completes a slice of a sum (its
-     * n_src-th) adds that slice's sources in source order -- the mep_sum_rows sum, bit for bit --
-     * writes the output slice and re-arms the counter, so no mep_sum_rows launch is needed. */
-    uint64_t sum, sum_count;
-    int32_t  sum_q, sum_kv, sum_stride, _pad;
 } mep_attn_bwd_desc;
 int mep_attn_bwd(const mep_attn_bwd_desc* descs, int n_desc, int max_tiles, int flags, mep_stream_t stream);
 
@@ -257,10 +270,6 @@ typedef struct {
                             site (0: xp, 1: out) -- lane (c, g) of the tile's wave, bit 4 i + r =
                             feature 16 i + 4 g + r of token 16 tile + c -- and the backward reads
                             them instead of re-hashing (the same masks; ABI 3) */
-    uint64_t image;      /* optional (0: none): the forward's LDS weight image for this block, built
-                            by mep_epi_images (mep_epi_image_bytes(D, 0) bytes): the workgroups
-                            copy it into LDS by LDS-DMA instead of splitting Wp / Wm themselves
-                            (ABI 4) */
 } mep_epi_desc;
 /* D (32/64/96/128, shared by every descriptor of the launch) selects the compiled variant.
  * Geometry: max_tiles = workgroups PER DESCRIPTOR; each workgroup (512 threads) stages its block's
@@ -289,19 +298,8 @@ typedef struct {
     uint64_t pool_dpooled;   /* [B][2 * pool_C] floats (mean part, then max part) */
     uint64_t pool_argmax;    /* [B][pool_C] int32 */
     int32_t  pool_C, pool_Tq, pool_t0, pool_col;
-    uint64_t image;          /* optional (0: none): the backward's LDS weight image (Wm^T, Wp^T
-                                split), mep_epi_image_bytes(D, 1) bytes, built by mep_epi_images */
 } mep_epi_bwd_desc;
 int mep_block_epi_bwd(const mep_epi_bwd_desc* descs, int n_desc, int max_tiles, int D, mep_stream_t stream);
-/* The epilogues' weight images, built once per step instead of once per workgroup: for every
- * descriptor, f.image (when nonzero) receives the forward's LDS image of Wp / Wm and image (when
- * nonzero) the backward's of Wm^T / Wp^T -- the exact bytes the kernels would stage (bf16 parts of
- * the fp32 weights in the split.h layouts), so results are bit-identical with and without images.
- * D as mep_block_epi_fwd (| MEP_PREC_BF16).  mep_epi_image_bytes(D, which): bytes of the forward
- * (which = 0) / backward (1) image, 0 when that configuration stages in the kernel only (two-phase
- * kernels, dropout forward at D = 96 fp32: f.image is ignored there). */
-int mep_epi_images(const mep_epi_bwd_desc* descs, int n_desc, int D, mep_stream_t stream);
-int mep_epi_image_bytes(int D, int which);
 
 /* ---------------------------------------------------------------- realformer block epilogue
  * others/realformer.py:182-209 after the attention core (x = attention output, q = block input):
@@ -684,7 +682,11 @@ int mep_assemble_windows(const mep_window_desc* descs, int n_desc, mep_stream_t 
  * ("vendor spec and a measured copy-kernel peak on the box").  Streams n16 16-byte units with
  * n_wg workgroups of 256 threads: mode 0 copies src -> dst (2 x 16 n16 bytes), mode 1 reads src
  * (16 n16 bytes; one xor dword per thread written to dst, so dst holds n_wg * 256 dwords), mode 2
- * zero-fills dst (16 n16 bytes).  Buffers 16-byte aligned. */
+ * zero-fills dst (16 n16 bytes).  Buffers 16-byte aligned.  mode | MEP_PROBE_BLOCKED: each
+ * workgroup streams one contiguous span (32 KiB per step) instead of the grid-stride order (mode 1
+ * then writes n_wg * 256 dwords too); | MEP_PROBE_NT: nontemporal loads / stores (blocked only). */
+#define MEP_PROBE_BLOCKED 4
+#define MEP_PROBE_NT 8
 int mep_hbm_probe(const void* src, void* dst, int64_t n16, int mode, int n_wg, mep_stream_t stream);
 
 /* Writes the device's 100-MHz real-time counter to slots[i] (uint64) when this one-wave kernel

@@ -81,25 +81,32 @@ class AttnDesc(ctypes.Structure):
                 ('B', i32), ('H', i32), ('Tq', i32), ('Tk', i32)]
 
 
+class AttnGenDesc(ctypes.Structure):
+    _fields_ = [('f', AttnDesc), ('mask_sQ', i64), ('hd', i32), ('scale', ctypes.c_float)]
+
+
+class AttnGenBwdDesc(ctypes.Structure):
+    _fields_ = [('g', AttnGenDesc), ('dx', Rows), ('dq', Rows), ('dk', Rows), ('dv', Rows),
+                ('ds_next', u64), ('ds_prev', u64), ('dc_partial', u64)]
+
+
 class AttnBwdDesc(ctypes.Structure):
     _fields_ = [('f', AttnDesc), ('dx', Rows), ('dq', Rows), ('dk', Rows), ('dv', Rows),
-                ('ds_next', u64), ('ds_prev', u64), ('dc_partial', u64),
-                ('sum', u64), ('sum_count', u64), ('sum_q', i32), ('sum_kv', i32), ('sum_stride', i32),
-                ('_pad', i32)]
+                ('ds_next', u64), ('ds_prev', u64), ('dc_partial', u64)]
 
 
 class EpiDesc(ctypes.Structure):
     _fields_ = [('q', Rows), ('x', Rows), ('xp', Rows), ('z', Rows), ('out', Rows),
                 ('wp', u64), ('wm', u64), ('ln_w', u64), ('ln_b', u64), ('stats', u64), ('seed', u64),
                 ('ntok', i32), ('D', i32), ('drop_p', f32), ('drop_stream', i32), ('out_h', Rows),
-                ('drop_bits', u64), ('image', u64)]
+                ('drop_bits', u64)]
 
 
 class EpiBwdDesc(ctypes.Structure):
     _fields_ = [('f', EpiDesc), ('dout', Rows), ('dout2', Rows), ('dz', Rows), ('dxp', Rows), ('dx', Rows),
                 ('dq', Rows), ('ln_partial', u64), ('dq_accumulate', i32), ('pool_T', i32),
                 ('pool_dpooled', u64), ('pool_argmax', u64), ('pool_C', i32), ('pool_Tq', i32),
-                ('pool_t0', i32), ('pool_col', i32), ('image', u64)]
+                ('pool_t0', i32), ('pool_col', i32)]
 
 
 class LnDesc(ctypes.Structure):
@@ -115,7 +122,6 @@ class ColsumDesc(ctypes.Structure):
 
 SUM_MAX_SRC = 16
 SUM_BF16 = 2         # MEP_SUM_BF16: mep_sum_desc.accumulate bit, bf16 source / output rows
-ATTN_FOLD_SRC = 8    # csrc/attn.hip FOLD_SRC: sources per sum the attention backward folds
 
 
 class SumDesc(ctypes.Structure):
@@ -256,7 +262,8 @@ class Seg(ctypes.Structure):
 
 
 STRUCTS = {'mep_rows': Rows, 'mep_gemm_desc': GemmDesc, 'mep_gemm_sum_desc': GemmSumDesc, 'mep_wgrad_desc': WgradDesc,
-           'mep_attn_desc': AttnDesc, 'mep_attn_bwd_desc': AttnBwdDesc, 'mep_epi_desc': EpiDesc,
+           'mep_attn_desc': AttnDesc, 'mep_attn_bwd_desc': AttnBwdDesc, 'mep_attn_gen_desc': AttnGenDesc,
+           'mep_attn_gen_bwd_desc': AttnGenBwdDesc, 'mep_epi_desc': EpiDesc,
            'mep_epi_bwd_desc': EpiBwdDesc, 'mep_ln_desc': LnDesc, 'mep_colsum_desc': ColsumDesc,
            'mep_sum_desc': SumDesc, 'mep_pool_desc': PoolDesc, 'mep_head_desc': HeadDesc, 'mep_seg': Seg,
            'mep_rf_epi_desc': RfEpiDesc, 'mep_rf_epi_bwd_desc': RfEpiBwdDesc, 'mep_rf_head_desc': RfHeadDesc,
@@ -292,11 +299,11 @@ SIGNATURES.update({
     'mep_assemble_windows': [ctypes.POINTER(WindowDesc), i32, P],
     'mep_tgemm': [P, i32, i32, i32, i32, P],
     'mep_wgemm': [P, i32, i32, i32, P],
+    'mep_attn_general_fwd': [P, i32, i32, P],
+    'mep_attn_general_bwd': [P, i32, i32, i32, P],
     'mep_wgemm_ws': [P, i32, i32, i32, i32, i32, P],
     'mep_wgemm_sum': [P, i32, i32, i32, P],
     'mep_rfw_front': [P, i32, i32, i32, P],
-    'mep_epi_images': [P, i32, i32, P],
-    'mep_epi_image_bytes': [i32, i32],
     'mep_abi_version': [],
     'mep_rf_rows': [i32, i32],
     'mep_last_error': [ctypes.c_char_p, ctypes.c_size_t],
@@ -307,7 +314,7 @@ SIGNATURES.update({
 })
 
 _LIB = None
-ABI_VERSION = 4   # include/mep.h MEP_ABI_VERSION
+ABI_VERSION = 5   # include/mep.h MEP_ABI_VERSION
 
 
 def lib():
@@ -534,15 +541,10 @@ def attn_dc_slots(B, H, Tk):
 TGEMM = switch('MEP_TGEMM', '1') != '0'   # 0: the mep_unify / mep_gemm kernels (A/B runs)
 # mep_tgemm chunked (K in 32-wide LDS stages) wins where the weight is too large to keep resident
 # (Ren-MME unify, K = 768 / 640: 153 -> 94 us at cfg5); at K <= 300 its per-chunk staging latency
-# loses to the weight-stationary mep_unify / mep_gemm (cmu-mosei unify 22 vs 17 us).  The
-# resident-weight form (MEP_TGEMM_RESIDENT, opt-in with MEP_TGEMM_RES=1) lost too: 22.3 vs 17.4 us
-# (cmu-mosei unify), 99.7 vs 89.8 us (cfg2's five GEMMs), and its 2-part weight moved a cmu_cfg1
-# logit by 1.1e-3 relative -- outside the 1e-4 parity
-TGEMM_RES = switch('MEP_TGEMM_RES', '0') == '1'
+# loses to the weight-stationary mep_unify / mep_gemm (cmu-mosei unify 22 vs 17 us; a
+# resident-weight tgemm form measured 22.3 vs 17.4 us there, round 3, and was removed)
 TGEMM_MIN_K = int(switch('MEP_TGEMM_MIN_K', '512'))
-TGEMM_RES_MAX_K = 320                              # csrc/tgemm.hip TGR_KP * 32
 TGEMM_WT = 0x1                                     # MEP_TGEMM_WT: every descriptor has w_nt = 0
-TGEMM_RESIDENT = 0x2                               # MEP_TGEMM_RESIDENT
 TGEMM_DMA = 0x4                                    # MEP_TGEMM_DMA (weight ring by LDS-DMA)
 TGEMM_DMA_ON = switch('MEP_TGEMM_DMA', '1') != '0'
 
@@ -553,8 +555,8 @@ def tgemm_dma_ok(items):
 
 
 def tgemm_mode(items):
-    """Which mep_tgemm form can run these GemmDescs (include/mep.h): 'resident' (every K <= 320),
-    'chunked' (some K >= TGEMM_MIN_K) or None (the mep_unify / mep_gemm kernels).  Needs N % 16 == 0
+    """Which mep_tgemm form can run these GemmDescs (include/mep.h): 'chunked' (some K >=
+    TGEMM_MIN_K) or None (the mep_unify / mep_gemm kernels).  Needs N % 16 == 0
     with N in {32, 64, 96} or >= 128, one w_nt for the launch, 16-byte aligned y rows, bias and
     table rows."""
     if not TGEMM or not items or len({d.w_nt for d in items}) != 1:
@@ -568,10 +570,7 @@ def tgemm_mode(items):
             return None
         if d.ntok <= 0 or d.K <= 0:
             return None
-    kmax = max(d.K for d in items)
-    if TGEMM_RES and kmax <= TGEMM_RES_MAX_K:
-        return 'resident'
-    return 'chunked' if kmax >= TGEMM_MIN_K else None
+    return 'chunked' if max(d.K for d in items) >= TGEMM_MIN_K else None
 
 
 def tgemm_ok(items):
@@ -587,10 +586,9 @@ def gemm(name, descs, max_tiles, stream=None, prec=0):
     mode = tgemm_mode(descs.items)
     if mode is not None:
         flags = (prec & PREC_BF16) | (0 if descs.items[0].w_nt else TGEMM_WT)
-        flags |= TGEMM_RESIDENT if mode == 'resident' else 0
         if any(d.bf16 for d in descs.items):
             flags |= PREC_BF16
-        if mode == 'chunked' and TGEMM_DMA_ON and tgemm_dma_ok(descs.items):
+        if TGEMM_DMA_ON and tgemm_dma_ok(descs.items):
             flags |= TGEMM_DMA
         call('mep_tgemm', descs.ptr, descs.n, max(d.ntok for d in descs.items), max(d.N for d in descs.items),
              flags, stream=stream)

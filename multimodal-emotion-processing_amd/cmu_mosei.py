@@ -74,7 +74,7 @@ class Attention_Block(nn.Module):
 
     def forward(self, q, k, v, mask, scores=None):
         from .standalone import block_forward
-        return block_forward(self, q, k, v, mask, scores, norm=self.norm1, drop_p=0.0)
+        return block_forward(self, q, k, v, mask, scores, norm=self.norm1, drop_p=self.drop.p)
 
 
 class Multi_ATTN(nn.Module):

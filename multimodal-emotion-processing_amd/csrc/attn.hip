@@ -51,61 +51,20 @@ typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
 typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
-#ifndef MEP_BWD_DB
-#define MEP_BWD_DB 0       // short backward: next query tile's loads in a second register set (3 waves
-                           // per SIMD without it beat 2 with it: 46 vs 51 us at cfg3)
-#endif
 #ifndef MEP_BWD_WAVES
 #define MEP_BWD_WAVES 3    // waves per SIMD of the short backward
 #endif
 #ifndef MEP_BWD_WAVES_KV
 #define MEP_BWD_WAVES_KV 4 // waves per SIMD of the short backward with MEP_ATTN_KV (<= 128 registers)
 #endif
-#ifndef MEP_FWD_PVSPLIT
-#define MEP_FWD_PVSPLIT 2  // forward P.V on bf16 splits (16x16x32) instead of f32 MFMA: 2 = 3-part P and V,
-                           // six products (fp32-level); 1 = 2-part, three products (~2^-16 per product:
-                           // moved one rf_chain_cfg2 output 3.5e-4 relative); 0 = f32 MFMA
-                           // (cfg3 30.1 -> 26.5 us, cfg5 421 -> 368 us)
-#endif
-#ifndef MEP_FWD_EXP2
-#define MEP_FWD_EXP2 1     // forward softmax numerator as exp2(fma(s, log2 e, -max log2 e)): one VALU
-                           // fewer per score (the max's rounding is a common factor of the row)
-#endif
-#ifndef MEP_FWD_QHOIST
-#define MEP_FWD_QHOIST 1   // Tk > 64 forward: the task's Q tiles split once, not once per key chunk
-#endif
 #ifndef MEP_FWD_WAVES
 #define MEP_FWD_WAVES 3    // waves per SIMD of the short, non-residual forward
-#endif
-#ifndef MEP_FWD_MASKACC
-#define MEP_FWD_MASKACC 1      // bf16 forward: mask term as the score accumulator's initial value (MI)
-#endif
-#ifndef MEP_FWD_MASKACC_F32
-#define MEP_FWD_MASKACC_F32 1  // the same on the fp32 forward (cfg5 fp32 291 -> 289 us, cfg3 26.7 -> 26.2 us)
 #endif
 #ifndef MEP_BWD_WIDE_WAVES
 #define MEP_BWD_WIDE_WAVES 0   // waves per SIMD of the wide Tk > 64 backward (0: as the short one)
 #endif
 #ifndef MEP_FWD_LONG_WAVES
 #define MEP_FWD_LONG_WAVES 2   // waves per SIMD of the Tk > 64 forward (hd 16), fp32 split path
-#endif
-#ifndef MEP_ATTN_HEADPAIR
-#define MEP_ATTN_HEADPAIR 1    // Tk > 64 kernels: heads 2j, 2j + 1 of a row on one CU / XCD (64-byte head slices of 128-byte lines)
-#endif
-#ifndef MEP_ATTN_HEADQUAD
-#define MEP_ATTN_HEADQUAD 1    // ... heads 4j .. 4j + 3 when H % 4 == 0 (bf16 rows: 32-byte head slices, four to a 128-byte line)
-#endif
-#ifndef MEP_FWD_CHUNK_PF
-#define MEP_FWD_CHUNK_PF 0    // bf16 long forward: the next key chunk's loads issued before this chunk's tiles
-#endif
-#ifndef MEP_FWD_MFSUM
-#define MEP_FWD_MFSUM 1       // bf16 forward: softmax row sums on the matrix core (ones-row A operand)
-#endif
-#ifndef MEP_XG_PERMLANE
-#define MEP_XG_PERMLANE 0     // cross-lane-group max / sum with v_permlane16/32_swap (0: ds_bpermute).
-                              // Off: this hipcc miscompiles float arithmetic on the swap's second
-                              // result (x + y of the two results came out as x + x; stores of the
-                              // raw words are correct -- the weight gradient's use)
 #endif
 #ifndef MEP_FWD_LONG_WAVES_BF
 #define MEP_FWD_LONG_WAVES_BF 2   // the same, bf16 path
@@ -195,31 +154,9 @@ MEP_DEV floatx4 dot_score(const S3& p, const S3& u, floatx4 acc) {
     return acc;
 }
 
-#ifndef MEP_BWD_MF16
-#define MEP_BWD_MF16 1   // backward 2-way products as separate 16x16x16 MFMAs (no operand assembly)
-#endif
-#ifndef MEP_BWD_STACK
-#define MEP_BWD_STACK 1  // KV backward: P^T dO + dS^T Q/4 as one 32-deep contraction on 16x16x32 MFMAs
-                         // (cfg3 39.5 -> 37.2 us, cfg5 663 -> 607 us with MEP_BWD_MF16_DQ = 0)
-#endif
-#ifndef MEP_BWD_DVF32
-#define MEP_BWD_DVF32 0  // dV += P^T dO on f32 MFMA from the raw P / dO (no split): 48.6 vs 45.5 us, off
-#endif
-#ifndef MEP_BWD_TR
-#define MEP_BWD_TR 0     // dS transposed as packed [key][query] words + ds_read_b64_tr_b16 (47.6-48.5 vs 45.6 us: off)
-#endif
-#ifndef MEP_BWD_TPAIR
-#define MEP_BWD_TPAIR 0  // dS transpose as key-pair words after a lane-pair swap (conflict-free ds_write_b32): its
-                         // DPP / select / perm VALU costs more than the conflicts (cfg3 fp32 38.3 -> 40.8 us,
-                         // cfg5 fp32 548 -> 574 us, bf16 within noise): off
-#endif
-#ifndef MEP_BWD_DELTA_MF
-#define MEP_BWD_DELTA_MF 0   // fp32 backward: delta = rowsum(dO O) on the matrix core (2-part splits).
-                             // Off: delta is subtracted from dP, and its 2^-16 product error moved one
-                             // ren_drop_long unify-weight gradient 3.9e-3 relative (rtol 1e-3)
-#endif
-#ifndef MEP_BWD_EXP2
-#define MEP_BWD_EXP2 1   // P = exp2(dot * log2e/sqrt(hd) - (mask * log2e + max * log2e)): one fma per score
+#ifndef MEP_BWD_TR_BF
+#define MEP_BWD_TR_BF 0  // the bf16 instances only: dS as one 8-byte [key][query] word per key tile (one
+                         // ds_write_b64 instead of four ds_write_b16) read back by ds_read_b64_tr_b16
 #endif
 
 // 16-deep contraction, 2-way split, all four products.  MEP_BWD_MF16: four v_mfma_f32_16x16x16_bf16
@@ -228,38 +165,17 @@ MEP_DEV floatx4 dot_score(const S3& p, const S3& u, floatx4 acc) {
 template <bool BF>
 MEP_DEV floatx4 dot16(const S2& x, const S2& y, floatx4 acc) {
     if (BF) return mfma16(op4(x.h0, x.h1), op4(y.h0, y.h1), acc);
-#if MEP_BWD_MF16
     acc = mfma16(op4(x.h0, x.h1), op4(y.h0, y.h1), acc);
     acc = mfma16(op4(x.l0, x.l1), op4(y.h0, y.h1), acc);
     acc = mfma16(op4(x.h0, x.h1), op4(y.l0, y.l1), acc);
     acc = mfma16(op4(x.l0, x.l1), op4(y.l0, y.l1), acc);
     return acc;
-#else
-    const bf16x8 a = op(x.h0, x.h1, x.l0, x.l1);
-    acc = mfma(a, op(y.h0, y.h1, y.h0, y.h1), acc);
-    acc = mfma(a, op(y.l0, y.l1, y.l0, y.l1), acc);
-    return acc;
-#endif
 }
 
 // 32-deep contraction over two 16-row tiles (slots 0-3: tile 0, 4-7: tile 1), 2-way split,
 // products x0 y0 + x1 y0 + x0 y1 (BF: x0 y0); MEP_BWD_MF16: per tile on 16x16x16
-#ifndef MEP_BWD_MF16_DQ
-#define MEP_BWD_MF16_DQ 0   // dQ's 32-deep contraction on 16x16x16 (1) or 16x16x32 (0)
-#endif
 template <bool BF>
 MEP_DEV floatx4 dot32(const S2& xa, const S2& xb, const S2& ya, const S2& yb, floatx4 acc) {
-#if MEP_BWD_MF16_DQ
-    if (!BF) {
-        acc = mfma16(op4(xa.h0, xa.h1), op4(ya.h0, ya.h1), acc);
-        acc = mfma16(op4(xa.l0, xa.l1), op4(ya.h0, ya.h1), acc);
-        acc = mfma16(op4(xa.h0, xa.h1), op4(ya.l0, ya.l1), acc);
-        acc = mfma16(op4(xb.h0, xb.h1), op4(yb.h0, yb.h1), acc);
-        acc = mfma16(op4(xb.l0, xb.l1), op4(yb.h0, yb.h1), acc);
-        acc = mfma16(op4(xb.h0, xb.h1), op4(yb.l0, yb.l1), acc);
-        return acc;
-    }
-#endif
     const bf16x8 x0 = op(xa.h0, xa.h1, xb.h0, xb.h1), y0 = op(ya.h0, ya.h1, yb.h0, yb.h1);
     acc = mfma(x0, y0, acc);
     if (BF) return acc;
@@ -277,39 +193,15 @@ MEP_DEV float mask_term(const gfloat* mask, int k, int Tk) {
 
 MEP_DEV float shfl(float v, int src) { return __shfl(v, src, 64); }
 
-// max / sum over the four lanes l, l ^ 16, l ^ 32, l ^ 48 (a query's lane groups g) with
-// v_permlane16_swap / v_permlane32_swap (VALU, no LDS round trip): the same operands in the same
-// order as x op shfl(x, l ^ 16), then op shfl(., l ^ 32)
-MEP_DEV unsigned opaque_copy(unsigned x) {
-    unsigned y;
-    asm volatile("v_mov_b32 %0, %1" : "=v"(y) : "v"(x));
-    return y;
-}
+// max / sum over the four lanes l, l ^ 16, l ^ 32, l ^ 48 (a query's lane groups g), in the order
+// x op shfl(x, l ^ 16), then op shfl(., l ^ 32)
 MEP_DEV float xg_max(float x) {
-    if (!MEP_XG_PERMLANE) {
-        x = fmaxf(x, shfl(x, (int)(threadIdx.x & 63) ^ 16));
-        return fmaxf(x, shfl(x, (int)(threadIdx.x & 63) ^ 32));
-    }
-    const unsigned u = __builtin_bit_cast(unsigned, x);
-    const auto a = __builtin_amdgcn_permlane16_swap(u, opaque_copy(u), false, false);
-    const float m = fmaxf(__builtin_bit_cast(float, a[0]), __builtin_bit_cast(float, a[1]));
-    const unsigned v = __builtin_bit_cast(unsigned, m);
-    const auto b = __builtin_amdgcn_permlane32_swap(v, opaque_copy(v), false, false);
-    return fmaxf(__builtin_bit_cast(float, b[0]), __builtin_bit_cast(float, b[1]));
+    x = fmaxf(x, shfl(x, (int)(threadIdx.x & 63) ^ 16));
+    return fmaxf(x, shfl(x, (int)(threadIdx.x & 63) ^ 32));
 }
 MEP_DEV float xg_sum(float x) {
-    if (!MEP_XG_PERMLANE) {
-        x = x + shfl(x, (int)(threadIdx.x & 63) ^ 16);
-        return x + shfl(x, (int)(threadIdx.x & 63) ^ 32);
-    }
-    const unsigned u = __builtin_bit_cast(unsigned, x);
-    const auto a = __builtin_amdgcn_permlane16_swap(u, opaque_copy(u), false, false);
-    // rows 0 / 2 of the first result hold x_l, of the second x_(l+16); rows 1 / 3: x_(l-16), x_l --
-    // x_l + x_(l^16) either way (addition of two operands commutes exactly)
-    const float t = __builtin_bit_cast(float, a[0]) + __builtin_bit_cast(float, a[1]);
-    const unsigned v = __builtin_bit_cast(unsigned, t);
-    const auto b = __builtin_amdgcn_permlane32_swap(v, opaque_copy(v), false, false);
-    return __builtin_bit_cast(float, b[0]) + __builtin_bit_cast(float, b[1]);
+    x = x + shfl(x, (int)(threadIdx.x & 63) ^ 16);
+    return x + shfl(x, (int)(threadIdx.x & 63) ^ 32);
 }
 
 // s = dot / sqrt(hd) [+ c*sp] - 1e8 * (1 - m)      (op order of cmu-mosei/run.py:244-253); hd = 16:
@@ -388,9 +280,6 @@ struct BRowT {
 typedef BRowT<false> BRow;
 
 MEP_DEV __amdgpu_buffer_rsrc_t uniform_rsrc(uint64_t base, int64_t bytes) {
-#ifdef MEP_ATTN_NOLOAD   // timing-only development build: row / stats loads return 0, stores dropped
-    bytes = 0;
-#endif
     const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)base);
     const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(base >> 32));
     const int n = __builtin_amdgcn_readfirstlane((int)min(bytes, (int64_t)0x7fffffff));
@@ -451,15 +340,15 @@ MEP_DEV void attn_fwd_task(const mep_attn_desc& d, int qc, int h, int b, int lan
     // store.  BF: 1/sum as v_rcp_f32 (fp32: the IEEE division)
     // lq: BF -- the row's full sum already (from the ones-row MFMA); fp32 -- this lane's keys
     auto finish = [&](int qt, const floatx4 (&oq)[NHB], float mq, float lq) {
-        const float lt = BF && MEP_FWD_MFSUM ? lq : xg_sum(lq);
+        const float lt = BF ? lq : xg_sum(lq);
         const float inv = BF ? __builtin_amdgcn_rcpf(lt) : 1.0f / lt;
         const int q = q_lo + qt * 16 + c;
         if (g == 0 && q < Tq) {
             // row statistics for the backward: (max log2 e - log2(1/sum), 1/sum) -- the exp2
             // backward's per-row exponent offset, formed once here instead of per backward tile and
-            // key-chunk wave (MEP_BWD_EXP2 = 0: (max, 1/sum))
-            // PREV: the raw max -- the backward forms exp(s - max) with s - max exact (F7 below)
-            stats[2 * (sbase + q)] = MEP_BWD_EXP2 && !PREV ? mq * 1.4426950408889634f - __builtin_amdgcn_logf(inv) : mq;
+            // key-chunk wave.  PREV: (max, 1/sum) -- the backward forms exp(s - max) with s - max
+            // exact (F7, Bwd::tile)
+            stats[2 * (sbase + q)] = !PREV ? mq * 1.4426950408889634f - __builtin_amdgcn_logf(inv) : mq;
             stats[2 * (sbase + q) + 1] = inv;
         }
 #pragma unroll
@@ -487,8 +376,8 @@ MEP_DEV void attn_fwd_task(const mep_attn_desc& d, int qc, int h, int b, int lan
     // 1/4 folds into the exponent's fma -- per score one max, one fma and the exp2 instead of a
     // scale, a mask subtraction, the max, the fma and the exp2.  Kept keys (mask 0) give the same
     // bits: 1/4 is a power of two, so scaling commutes with every rounding on the way
-    constexpr bool MI = !PREV && !SOUT && HDIM == 16 && (BF ? MEP_FWD_MASKACC : MEP_FWD_MASKACC_F32);
-    constexpr bool QH = !SINGLE && MEP_FWD_QHOIST;
+    constexpr bool MI = !PREV && !SOUT && HDIM == 16;
+    constexpr bool QH = !SINGLE;
     S3 qsh[QH ? NT : 1][NHB];                  // QH: B of S^T for every query tile of the task
     if (QH) {
 #pragma unroll
@@ -500,9 +389,7 @@ MEP_DEV void attn_fwd_task(const mep_attn_desc& d, int qc, int h, int b, int lan
                 qsh[QH ? qt : 0][hb] = z;
             }
     }
-    // the raw loads of one key chunk (K rows, V columns, the keys' mask values); PF (bf16 long
-    // forward, MEP_FWD_CHUNK_PF): the next chunk's loads are issued before this chunk's query tiles
-    constexpr bool PF = BF && !SINGLE && MEP_FWD_CHUNK_PF;
+    // the raw loads of one key chunk (K rows, V columns, the keys' mask values)
     struct Raw {
         u32x2 kw[NT][NHB];        // BF: K rows as words
         float kf[BF ? 1 : NT][NHB][4];
@@ -536,18 +423,11 @@ MEP_DEV void attn_fwd_task(const mep_attn_desc& d, int qc, int h, int b, int lan
             }
         }
     };
-    Raw nxt;
-    if (PF) fetch(nxt, 0);
     for (int k_lo = 0; k_lo < Tk; k_lo += CH) {
         // operands of the 4 key tiles of this chunk: K rows (A of S^T: K[k0+c][4g+s], split) and V
         // columns (B of P.V: V[k0+4g+s][c]); past Tk they read 0 (P is 0 there)
         Raw cur;
-        if (PF) {
-            cur = nxt;
-            if (k_lo + CH < Tk) fetch(nxt, k_lo + CH);
-        } else {
-            fetch(cur, k_lo);
-        }
+        fetch(cur, k_lo);
         S3 ks[NT][NHB];
         float vf[BF ? 1 : NT][NHB][4], mt[NT][4];
         unsigned vr[BF ? NT : 1][NHB][4];   // BF: raw bf16 V elements
@@ -583,27 +463,19 @@ MEP_DEV void attn_fwd_task(const mep_attn_desc& d, int qc, int h, int b, int lan
                                          vr[kt + 1][hb][0] | (vr[kt + 1][hb][1] << 16),
                                          vr[kt + 1][hb][2] | (vr[kt + 1][hb][3] << 16));
         }
-#if MEP_FWD_PVSPLIT
         // V of key-tile pairs split once per chunk (not per query tile): parts [pair][hb][part]
-        bf16x8 vsp[NT / 2][NHB][MEP_FWD_PVSPLIT == 2 ? 3 : 2];
+        bf16x8 vsp[NT / 2][NHB][3];
         if constexpr (!BF) {
 #pragma unroll
             for (int kt = 0; kt < NT; kt += 2)
 #pragma unroll
                 for (int hb = 0; hb < NHB; ++hb) {
-#if MEP_FWD_PVSPLIT == 2
                     const S3 va = split3(vf[kt][hb]), vb = split3(vf[kt + 1][hb]);
                     vsp[kt / 2][hb][2] = op(va.c0, va.c1, vb.c0, vb.c1);
                     vsp[kt / 2][hb][0] = op(va.a0, va.a1, vb.a0, vb.a1);
                     vsp[kt / 2][hb][1] = op(va.b0, va.b1, vb.b0, vb.b1);
-#else
-                    const S2 va = split2(vf[kt][hb]), vb = split2(vf[kt + 1][hb]);
-                    vsp[kt / 2][hb][0] = op(va.h0, va.h1, vb.h0, vb.h1);
-                    vsp[kt / 2][hb][1] = op(va.l0, va.l1, vb.l0, vb.l1);
-#endif
                 }
         }
-#endif
         float qfa[QH || BF ? 1 : NT][NHB][4];                              // B of S^T: Q[q][4g+s]
         S3 qbf[!QH && BF ? NT : 1][NHB];                                   // BF: raw Q words
         if (!QH) {
@@ -668,9 +540,9 @@ MEP_DEV void attn_fwd_task(const mep_attn_desc& d, int qc, int h, int b, int lan
             for (int kt = 0; kt < NT; ++kt)
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
-                    sv[kt][r] = (MEP_FWD_EXP2 && !PREV) || MI ? __builtin_amdgcn_exp2f(fmaf(sv[kt][r], SL2E, -mb))
+                    sv[kt][r] = !PREV ? __builtin_amdgcn_exp2f(fmaf(sv[kt][r], SL2E, -mb))
                                                               : __expf(sv[kt][r] - mnew);
-                    if (!(BF && MEP_FWD_MFSUM)) lsum += sv[kt][r];
+                    if (!BF) lsum += sv[kt][r];
                 }
             floatx4 oq[NHB];
 #pragma unroll
@@ -695,10 +567,9 @@ MEP_DEV void attn_fwd_task(const mep_attn_desc& d, int qc, int h, int b, int lan
                                          pk(sv[kt + 1][2], sv[kt + 1][3]));
 #pragma unroll
                     for (int hb = 0; hb < NHB; ++hb) oq[hb] = mfma(vbf[kt / 2][hb], pb, oq[hb]);
-                    if (MEP_FWD_MFSUM) lacc = mfma(op(0x3f803f80u, 0x3f803f80u, 0x3f803f80u, 0x3f803f80u), pb, lacc);
+                    lacc = mfma(op(0x3f803f80u, 0x3f803f80u, 0x3f803f80u, 0x3f803f80u), pb, lacc);
                     continue;
                 }
-#if MEP_FWD_PVSPLIT == 2
                 // P and V as 3-part bf16 splits, the six products p_i v_j with i + j <= 2 (the terms
                 // dropped are <= 2^-24 relative: fp32-level) on 16x16x32 MFMAs per key-tile pair
                 // (slots 0-3: tile kt, 4-7: tile kt + 1); the three smallest on a chain of their own
@@ -719,32 +590,8 @@ MEP_DEV void attn_fwd_task(const mep_attn_desc& d, int qc, int h, int b, int lan
                         for (int r = 0; r < 4; ++r) oq[hb][r] += t[r];
                     }
                 }
-#elif MEP_FWD_PVSPLIT
-                // P and V as 2-part bf16 splits, products p0 v0 + p1 v0 + p0 v1 on three 16x16x32
-                // MFMAs per key-tile pair (slots 0-3: tile kt, 4-7: tile kt + 1): relative error
-                // <= ~2^-16 per product, 48 MFMA cycles instead of 8 f32 MFMAs
-                {
-                    const S2 pa = split2(sv[kt]), pb = split2(sv[kt + 1]);
-                    const bf16x8 p0 = op(pa.h0, pa.h1, pb.h0, pb.h1), p1 = op(pa.l0, pa.l1, pb.l0, pb.l1);
-#pragma unroll
-                    for (int hb = 0; hb < NHB; ++hb) {
-                        const bf16x8 v0 = vsp[kt / 2][hb][0];
-                        oq[hb] = mfma(v0, p0, oq[hb]);
-                        oq[hb] = mfma(v0, p1, oq[hb]);
-                        oq[hb] = mfma(vsp[kt / 2][hb][1], p0, oq[hb]);
-                    }
-                }
-#else
-                // fp32 MFMA on the raw P and V (exact fp32 fma chain)
-#pragma unroll
-                for (int k2 = 0; k2 < 2; ++k2)
-#pragma unroll
-                    for (int s = 0; s < 4; ++s)
-#pragma unroll
-                        for (int hb = 0; hb < NHB; ++hb) oq[hb] = mfma16x4(vf[kt + k2][hb][s], sv[kt + k2][s], oq[hb]);
-#endif
             }
-            if (BF && MEP_FWD_MFSUM) lsum = lacc[0];
+            if (BF) lsum = lacc[0];
             if (SINGLE) {
                 finish(qt, oq, MI ? mnew * INV_SCALE : mnew, lsum);
             } else {
@@ -772,7 +619,7 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu((SINGLE
     const int nqc = (d.Tq + QCH - 1) / QCH;   // QCH: queries per wave task (64, or 16 with MEP_ATTN_SPLITQ)
     const int task = blockIdx.x * WAVES + wave;
     if (task >= d.B * d.H * nqc) return;   // whole wave leaves; no barriers below
-    if (!SINGLE && MEP_ATTN_HEADQUAD && !(d.H & 3)) {
+    if (!SINGLE && !(d.H & 3)) {
         // Tk > 64, H % 4 == 0: the workgroup's 4 waves take the same queries of heads 4j .. 4j + 3
         // of one row -- the 128-byte line of a bf16 K / V / Q row that each reads a quarter of is
         // fetched once for all four, into the CU they share
@@ -781,7 +628,7 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu((SINGLE
         attn_fwd_task<PREV, SOUT, SINGLE, BF, HDIM, QCH>(d, qc, 4 * (bhq % hq) + m, bhq / hq, lane);
         return;
     }
-    if (!SINGLE && MEP_ATTN_HEADPAIR && !(d.H & 1)) {
+    if (!SINGLE && !(d.H & 1)) {
         // Tk > 64: waves 2i and 2i + 1 of a workgroup take the same queries of heads 2j and 2j + 1
         // of one row, so the 128-byte line of K / V / Q rows each needs half of is fetched once
         // for both, into the CU they share (head_pair_order below has the backward's reason)
@@ -817,7 +664,6 @@ struct Bwd {
         f32x2 st[4];
         u32x2 qaw, daw;   // BF: Q / dO rows as raw bf16 operand words (no fp32 round trip)
         u32x2 oaw;        // BF: O row (delta on the matrix core)
-        float oa[4];      // fp32 path, MEP_BWD_DELTA_MF: O row (query c, dims 4g ..)
     };
     const mep_attn_bwd_desc& bd;
     int b, h, lane, c, g, hc, Tq, Tk, sbase;
@@ -890,7 +736,6 @@ struct Bwd {
         } else {
             Qb.ld4(in.qa, Qb.at(q0 + c, hc + 4 * g));
             Gb.ld4(in.da, Gb.at(q0 + c, hc + 4 * g));
-            if (MEP_BWD_DELTA_MF) Ob.ld4(in.oa, Ob.at(q0 + c, hc + 4 * g));
         }
         const int qg = q0 + 4 * g;
         const int og = Gb.at(qg, hc + c), oq = Qb.at(qg, hc + c), oo = Ob.at(qg, hc + c), od = dQb.at(qg, hc + c);
@@ -898,7 +743,7 @@ struct Bwd {
         for (int s = 0; s < 4; ++s) {
             in.db[s] = Gb.ld1(og, s * Gb.sT4);
             in.qb[s] = Qb.ld1(oq, s * Qb.sT4);
-            if (!BF && !MEP_BWD_DELTA_MF) in.ob[s] = Ob.ld1(oo, s * Ob.sT4);
+            if (!BF) in.ob[s] = Ob.ld1(oo, s * Ob.sT4);
             in.st[s] = __builtin_bit_cast(f32x2, __builtin_amdgcn_raw_buffer_load_b64(rsStat, 8 * qg, 8 * s, 0));
             in.dqo[s] = dQb.ld1(od, s * dQb.sT4);
         }
@@ -966,17 +811,12 @@ struct Bwd {
         const f32x4 qa = *(lcf4*)(L + 16 * c + 4 * g), da = *(lcf4*)(L + 256 + 16 * c + 4 * g);
 #pragma unroll
         for (int e = 0; e < 4; ++e) { in.qa[e] = qa[e]; in.da[e] = da[e]; }
-        if (MEP_BWD_DELTA_MF) {
-            const f32x4 oa = *(lcf4*)(L + 512 + 16 * c + 4 * g);
-#pragma unroll
-            for (int e = 0; e < 4; ++e) in.oa[e] = oa[e];
-        }
 #pragma unroll
         for (int s4 = 0; s4 < 4; ++s4) {
             const int r = (4 * g + s4) * 16 + c;
             in.qb[s4] = L[r];
             in.db[s4] = L[256 + r];
-            if (!MEP_BWD_DELTA_MF) in.ob[s4] = L[512 + r];
+            in.ob[s4] = L[512 + r];
             in.dqo[s4] = L[768 + r];
             in.st[s4] = *(lcf2*)(L + 1024 + 2 * (4 * g + s4));
         }
@@ -990,20 +830,12 @@ struct Bwd {
     // one 16-query tile against the chunk's 64 keys: accumulates dK / dV, returns this chunk's
     // dQ contribution (C[query 4g+r][dim c], before the 1/sqrt(hd) scale).  Tr: the wave's
     // transpose scratch in LDS (TFL floats: the bf16 hi and lo parts of dS, 16 x TLD2 each).
+    static constexpr bool TRX = BF && MEP_BWD_TR_BF;   // the dS transpose layout
     MEP_DEV floatx4 tile(const QIn& in, int qt, float* Tr) {
         const int q0 = qt * 16;
         constexpr float LOG2E = 1.4426950408889634f;
         float mm[4], li[4], del[4];
         floatx4 dd = zero4();
-        constexpr bool DMF = BF || MEP_BWD_DELTA_MF;   // delta on the matrix core
-        if constexpr (!BF && MEP_BWD_DELTA_MF) {
-            // fp32 path: dO and O rows as 2-part splits, products d0 o0 + d1 o0 + d0 o1 (<= 2^-16
-            // relative per product, the accuracy of the dP it is subtracted from)
-            const S2 d2 = split2(in.da), o2 = split2(in.oa);
-            dd = mfma16(op4(d2.h0, d2.h1), op4(o2.h0, o2.h1), dd);
-            dd = mfma16(op4(d2.l0, d2.l1), op4(o2.h0, o2.h1), dd);
-            dd = mfma16(op4(d2.h0, d2.h1), op4(o2.l0, o2.l1), dd);
-        }
         if constexpr (BF) {
             // delta = rowsum(dO * O) as the diagonal of dO O^T: one 16x16x16 MFMA on the row words
             // (lane (c, g) holds C[query 4g + r][query c]; C[q][q] sits in lane q of group q >> 2,
@@ -1013,27 +845,23 @@ struct Bwd {
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
             const int qq = q0 + 4 * g + s;
-            // delta = rowsum(dO * O): the 16 dims of query qq sit in one DPP row (lanes c)
-            if constexpr (DMF) del[s] = shfl(dd[s], 20 * g + s);
+            // delta = rowsum(dO * O): the 16 dims of query qq sit in one DPP row (lanes c) (fp32:
+            // exact products; a 2-part matrix-core delta, subtracted from dP, moved one
+            // ren_drop_long unify-weight gradient 3.9e-3 relative)
+            if constexpr (BF) del[s] = shfl(dd[s], 20 * g + s);
             else del[s] = row16_sum(in.db[s] * in.ob[s]);
             // padded queries: max = +inf, 1/sum = 0 make P = exp(-inf) * 0 = 0 (and with it dS);
             // the max is kept pre-scaled by log2(e) for exp2
             const bool qok = qq < Tq;
-#if MEP_BWD_EXP2
             mm[s] = qok ? in.st[s][0] : INFINITY;   // the forward's max log2 e - log2(1/sum) (PREV: max)
-#else
-            mm[s] = qok ? in.st[s][0] * LOG2E : INFINITY;
-#endif
             li[s] = qok ? in.st[s][1] : 0.f;
-#if MEP_BWD_EXP2
-            // 1/sum folded into the exponent: P = exp2(.. - (max log2 e - log2(1/sum)))
-            // (1/sum folded into the exponent by the forward's statistics)
-#endif
+            // 1/sum folded into the exponent by the forward's statistics:
+            // P = exp2(.. - (max log2 e - log2(1/sum)))
         }
         const S2 qs = BF ? S2{in.qaw[0], in.qaw[1], 0u, 0u} : split2(in.qa);
         const S2 do2 = BF ? S2{in.daw[0], in.daw[1], 0u, 0u} : split2(in.da);
         S2 qb2;
-        if (KV && MEP_BWD_STACK && !BF) {
+        if (KV && !BF) {
             qb2 = S2{};   // in the stacked operand B0 / B1
         } else if (KV) {   // dK folded into the dV accumulator: Q columns times the exact 1/sqrt(hd)
             float q4[4];
@@ -1043,7 +871,6 @@ struct Bwd {
         } else {
             qb2 = split2(in.qb);
         }
-#if MEP_BWD_STACK
         // stacked dKV operand [dO ; Q/4] (slots 0-3 / 4-7), split straight into the operand words
         u32x4 B0 = u32x4{0u, 0u, 0u, 0u}, B1 = B0;
         if (KV && !BF) {
@@ -1053,8 +880,7 @@ struct Bwd {
             B0 = split_hi(in.db, q4);
             B1 = split_lo(in.db, q4, B0);
         }
-#endif
-        const S2 db2 = ((MEP_BWD_DVF32 || (KV && MEP_BWD_STACK)) && !BF) ? S2{} : split2(in.db);
+        const S2 db2 = (KV && !BF) ? S2{} : split2(in.db);
         typedef __attribute__((address_space(3))) unsigned short lushort;
         lushort* Th = (lushort*)Tr;                 // [16 queries][TLD2] bf16 parts of dS
         lushort* Tl = Th + 16 * TLD2;
@@ -1067,15 +893,11 @@ struct Bwd {
             // so the exponent below needs no per-score mask add (0 for kept keys: the same bits; a
             // masked or padding key's score stays ~-4e8 / -inf and its P exactly 0).  The fp32
             // instances keep the add (four more live registers spill the 128-register short kernel)
-            constexpr bool MI = BF && MEP_BWD_EXP2 && !PREV;
+            constexpr bool MI = BF && !PREV;
             const float m0 = MI ? mts[BF ? kt : 0] : 0.f;
             const floatx4 st = dot16<BF>(qs, kb[kt], floatx4{m0, m0, m0, m0});
-#if MEP_BWD_EXP2
             // dP - delta: the accumulator starts at -delta (query 4g+r)
             const floatx4 dp = dot16<BF>(do2, KV ? kb[kt] : vb[kt], floatx4{-del[0], -del[1], -del[2], -del[3]});
-#else
-            const floatx4 dp = dot16<BF>(do2, KV ? kb[kt] : vb[kt], zero4());
-#endif
             float p[4], dsv[4];
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
@@ -1086,7 +908,6 @@ struct Bwd {
                     si = (sbase + min(qq, Tq - 1)) * Tk + min(kk, Tk - 1);
                     if (PREV) spv = sprev[si];
                 }
-#if MEP_BWD_EXP2
                 float pv;
                 if constexpr (PREV) {
                     // residual scores (F7): the score in the forward's op order, then exp(s - max) /
@@ -1101,11 +922,6 @@ struct Bwd {
                     pv = __builtin_amdgcn_exp2f(fmaf(st[r], INV_SCALE * LOG2E, MI ? -mm[r] : -(mtl[kt] + mm[r])));
                 }
                 float gsv = pv * dp[r];
-#else
-                const float sv = score<PREV>(st[r], cres, spv, mtk[kt]);
-                const float pv = __builtin_amdgcn_exp2f(fmaf(sv, LOG2E, -mm[r])) * li[r];
-                float gsv = pv * (dp[r] - del[r]);
-#endif
                 if (DSN || PREV) {
                     const bool ok = (qq < Tq) && (kk < Tk);
                     if (DSN) gsv += ok ? dsn[si] : 0.f;
@@ -1117,7 +933,6 @@ struct Bwd {
                 p[r] = pv;
                 dsv[r] = gsv;
             }
-#if MEP_BWD_STACK
             S2 ds2;
             if (KV && !BF) {
                 // dKV[key][dim] += P^T dO + dS^T Q / 4 as ONE 32-deep contraction [P | dS] . [dO ; Q/4]
@@ -1132,49 +947,22 @@ struct Bwd {
             } else {
                 ds2 = split2(dsv);
             }
-#else
-            const S2 ds2 = split2(dsv);
-#endif
-            if (KV && !BF && MEP_BWD_STACK) {
+            if (KV && !BF) {
             } else if (KV) {                             // dKV[key][dim] += P^T dO + dS^T Q / 4
                 dk[kt] = dot16<BF>(split2(p), db2, dk[kt]);
-            } else if (MEP_BWD_DVF32 && !BF) {           // dV[key][dim] += P^T dO, exact fp32
-#pragma unroll
-                for (int s = 0; s < 4; ++s) dv[kt] = mfma16x4(p[s], in.db[s], dv[kt]);
             } else {
                 dv[kt] = dot16<BF>(split2(p), db2, dv[kt]);
             }
-            if (!(KV && !BF && MEP_BWD_STACK)) dk[kt] = dot16<BF>(ds2, qb2, dk[kt]);   // dK[key][dim] += dS^T Q
-#if MEP_BWD_TR
-            // the split dS as packed words into [key][16 queries] images (one 8-byte store per
-            // part: this lane's queries 4g .. 4g+3 of key kt*16 + c)
-            {
+            if (!(KV && !BF)) dk[kt] = dot16<BF>(ds2, qb2, dk[kt]);   // dK[key][dim] += dS^T Q
+            if constexpr (TRX) {
+                // the split dS as packed words into [key][16 queries] images (one 8-byte store per
+                // part: this lane's queries 4g .. 4g+3 of key kt*16 + c)
                 typedef __attribute__((address_space(3))) u32x2 lu32x2w;
                 lu32x2w* Ih = (lu32x2w*)Tr;
                 const int e = (kt * 16 + c) * 4 + g;       // u32x2 index: row (key) * 4 + column block
                 Ih[e] = u32x2{ds2.h0, ds2.h1};
                 if (!BF) Ih[CH * 4 + e] = u32x2{ds2.l0, ds2.l1};
-            }
-#elif MEP_BWD_TPAIR
-            // the split dS into Th / Tl[query][key] as 32-bit words of key pairs: lanes c and c ^ 1
-            // trade half their queries (one DPP swap per part), then lane c (even) writes queries
-            // 4g, 4g+1 and lane c+1 queries 4g+2, 4g+3 of keys (c, c+1) -- two ds_write_b32 per part
-            // instead of four ds_write_b16, every lane on its own bank (TLD2 / 2 = 36 dwords)
-            {
-                const bool odd = c & 1;
-                typedef __attribute__((address_space(3))) unsigned lu32;
-                const int rw = (4 * g + (odd ? 2 : 0)) * TLD2 + kt * 16 + (c & ~1);
-                auto put = [&](lushort* T, unsigned w01, unsigned w23) {
-                    const unsigned mine = odd ? w23 : w01;
-                    const unsigned other = (unsigned)__builtin_amdgcn_update_dpp(0, (int)(odd ? w01 : w23), 0xB1, 0xF, 0xF, true);
-                    const unsigned lo = odd ? other : mine, hi = odd ? mine : other;   // key c & ~1 / (c & ~1) + 1
-                    *(lu32*)(T + rw) = __builtin_amdgcn_perm(hi, lo, 0x05040100u);          // query row rw: low halves
-                    *(lu32*)(T + rw + TLD2) = __builtin_amdgcn_perm(hi, lo, 0x07060302u);   // next query: high halves
-                };
-                put(Th, ds2.h0, ds2.h1);
-                if (!BF) put(Tl, ds2.l0, ds2.l1);
-            }
-#else
+            } else {
             // the split dS, element by element, into Th / Tl[query][key] (bf16)
             const unsigned hw[4] = {ds2.h0, ds2.h0 >> 16, ds2.h1, ds2.h1 >> 16};
             const unsigned lw[4] = {ds2.l0, ds2.l0 >> 16, ds2.l1, ds2.l1 >> 16};
@@ -1183,34 +971,34 @@ struct Bwd {
                 Th[(4 * g + r) * TLD2 + kt * 16 + c] = (unsigned short)hw[r];
                 if (!BF) Tl[(4 * g + r) * TLD2 + kt * 16 + c] = (unsigned short)lw[r];
             }
-#endif
+            }
         }
         // dQ += dS K with the query on the lane: the transposed 16 x 64 dS parts, already split,
         // come back as packed words (keys 4g .. 4g+3 of each key tile, one 8-byte read per part)
         wave_lds_sync();
         S2 tq[NT];
         typedef __attribute__((address_space(3))) u32x2 lu32x2;
-#if MEP_BWD_TR
-        // ds_read_b64_tr_b16: lane 4q+p of group g addresses key row kt*16 + 4g + q, queries
-        // 4p .. 4p+3; lane c of the group receives query column c of those 4 key rows -- dS[query
-        // c][keys 4g .. 4g+3], the A operand of dQ += dS K (EXEC is full here: no divergence)
-        typedef __attribute__((address_space(3))) s16x4 ls16x4;
+        if constexpr (TRX) {
+            // ds_read_b64_tr_b16: lane 4q+p of group g addresses key row kt*16 + 4g + q, queries
+            // 4p .. 4p+3; lane c of the group receives query column c of those 4 key rows -- dS[query
+            // c][keys 4g .. 4g+3], the A operand of dQ += dS K (EXEC is full here: no divergence)
+            typedef __attribute__((address_space(3))) s16x4 ls16x4;
 #pragma unroll
-        for (int kt = 0; kt < NT; ++kt) {
-            const int e = (kt * 16 + 4 * g + (c >> 2)) * 4 + (c & 3);
-            const u32x2 hh = __builtin_bit_cast(u32x2, __builtin_amdgcn_ds_read_tr16_b64_v4i16((ls16x4*)Tr + e));
-            const u32x2 ll = BF ? u32x2{0u, 0u}
-                                : __builtin_bit_cast(u32x2, __builtin_amdgcn_ds_read_tr16_b64_v4i16((ls16x4*)Tr + CH * 4 + e));
-            tq[kt] = S2{hh[0], hh[1], ll[0], ll[1]};
-        }
-#else
+            for (int kt = 0; kt < NT; ++kt) {
+                const int e = (kt * 16 + 4 * g + (c >> 2)) * 4 + (c & 3);
+                const u32x2 hh = __builtin_bit_cast(u32x2, __builtin_amdgcn_ds_read_tr16_b64_v4i16((ls16x4*)Tr + e));
+                const u32x2 ll = BF ? u32x2{0u, 0u}
+                                    : __builtin_bit_cast(u32x2, __builtin_amdgcn_ds_read_tr16_b64_v4i16((ls16x4*)Tr + CH * 4 + e));
+                tq[kt] = S2{hh[0], hh[1], ll[0], ll[1]};
+            }
+        } else {
 #pragma unroll
-        for (int kt = 0; kt < NT; ++kt) {
-            const u32x2 hh = *reinterpret_cast<const lu32x2*>(Th + c * TLD2 + kt * 16 + 4 * g);
-            const u32x2 ll = BF ? u32x2{0u, 0u} : *reinterpret_cast<const lu32x2*>(Tl + c * TLD2 + kt * 16 + 4 * g);
-            tq[kt] = S2{hh[0], hh[1], ll[0], ll[1]};
+            for (int kt = 0; kt < NT; ++kt) {
+                const u32x2 hh = *reinterpret_cast<const lu32x2*>(Th + c * TLD2 + kt * 16 + 4 * g);
+                const u32x2 ll = BF ? u32x2{0u, 0u} : *reinterpret_cast<const lu32x2*>(Tl + c * TLD2 + kt * 16 + 4 * g);
+                tq[kt] = S2{hh[0], hh[1], ll[0], ll[1]};
+            }
         }
-#endif
         wave_lds_sync();
         floatx4 dq = zero4();
 #pragma unroll
@@ -1234,67 +1022,11 @@ struct Bwd {
 template <bool PREV, bool DSN, bool KV>
 constexpr int bwd_short_waves() { return PREV ? (KV ? 3 : 2) : (KV && !DSN) ? MEP_BWD_WAVES_KV : MEP_BWD_WAVES; }
 
-#ifndef MEP_BWD_DMA
-#define MEP_BWD_DMA 1   // short backward: query tiles staged one ahead by LDS-DMA (Bwd::stage)
-#endif
-
-// The per-modality gradient sums folded into the short backward (mep_attn_bwd_desc.sum).  A
-// (b, h) unit has written its dq and dk slices (rows of b, columns of head h); it counts them on the
-// slice counters of the sums they feed (one arrival per source, agent-scope release).  The arrival
-// that completes a slice adds the slice's sources in source order -- the k_sum_rows sequence, bit
-// for bit -- writes it, and re-arms the counter for the next step.
-constexpr int FOLD_SRC = 8;    // sources held in flight per row (the plans fold at most 8)
-MEP_DEV void fold_slice(const mep_sum_desc& s, int b, int h, int lane) {
-    const int T = s.out.T, col = h * HD + 4 * (lane & 3);
-    for (int t = lane >> 2; t < T; t += 16) {
-        const int tok = b * T + t;
-        float4 v[FOLD_SRC];
-#pragma unroll
-        for (int k = 0; k < FOLD_SRC; ++k)
-            if (k < s.n_src) v[k] = ldg4(row_ptr(s.src[k], tok) + col);
-        float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-        for (int k = 0; k < FOLD_SRC; ++k)
-            if (k < s.n_src) { a.x += v[k].x; a.y += v[k].y; a.z += v[k].z; a.w += v[k].w; }
-        gfloat* o = row_ptr(s.out, tok) + col;
-        if (s.accumulate) { const float4 w = ldg4(o); a.x += w.x; a.y += w.y; a.z += w.z; a.w += w.w; }
-        stg4(o, a);
-    }
-}
-
-MEP_DEV void fold_sums(const mep_attn_bwd_desc& bd, int b, int h, int lane) {
-    const mep_sum_desc* sums = reinterpret_cast<const mep_sum_desc*>(bd.sum);
-    MEP_G int* cnt = G<int>(bd.sum_count);
-    const int slice = b * bd.f.H + h;
-    __threadfence();                             // this unit's dq / dk stores, before it counts
-    int done = 0;                                // bit 0: sum_q's slice complete, bit 1: sum_kv's
-    if (lane == 0) {
-        const int both = bd.sum_q >= 0 && bd.sum_q == bd.sum_kv;
-        for (int i = 0; i < 2 - both; ++i) {
-            const int idx = i ? bd.sum_kv : bd.sum_q;
-            if (idx < 0) continue;
-            MEP_G int* c = cnt + (int64_t)idx * bd.sum_stride + slice;
-            const int inc = both ? 2 : 1;
-            const int old = __hip_atomic_fetch_add(c, inc, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-            if (old + inc == sums[idx].n_src) {
-                __hip_atomic_store(c, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                done |= 1 << i;
-            }
-        }
-    }
-    done = __shfl(done, 0);
-    if (!done) return;
-    __threadfence();                             // the other units' slices, before they are read
-    if (done & 1) fold_slice(sums[bd.sum_q], b, h, lane);
-    if (done & 2) fold_slice(sums[bd.sum_kv], b, h, lane);
-}
 
 template <bool PREV, bool DSN, bool BF, bool KV>
 __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(bwd_short_waves<PREV, DSN, KV>()))) void k_attn_bwd_short(const mep_attn_bwd_desc* __restrict__ descs) {
     __shared__ __attribute__((aligned(16))) float Tr[WAVES][TFL];
-#if MEP_BWD_DMA
     __shared__ __attribute__((aligned(16))) float Stg[WAVES][Bwd<PREV, DSN, BF, KV>::STG];
-#endif
     const mep_attn_bwd_desc& bd = descs[blockIdx.y];
     if (bd.f.Tk > CH) return;                // a LONG descriptor
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -1311,7 +1043,6 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(bwd_sho
         }
         return;
     }
-#if MEP_BWD_DMA
     if (u.dma_ok()) {
         float* S = Stg[wave];
         typedef __attribute__((address_space(3))) f32x4 lf4;
@@ -1334,27 +1065,13 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(bwd_sho
         }
         if (nqt > 0) u.store_dq_rows(dqo_prev, nqt - 1, dq_prev);
     } else
-#endif
     {
     u.load_chunk(0);
-#if MEP_BWD_DB
-    typename Bwd<PREV, DSN, BF, KV>::QIn bufA, bufB;
-    u.fetch(bufA, 0);
-    for (int qt = 0; qt < nqt; qt += 2) {
-        u.fetch(bufB, qt + 1);               // past the end: range-checked zeros, never used
-        u.store_dq(bufA, qt, u.tile(bufA, qt, Tr[wave]));
-        if (qt + 1 < nqt) {
-            u.fetch(bufA, qt + 2);
-            u.store_dq(bufB, qt + 1, u.tile(bufB, qt + 1, Tr[wave]));
-        }
-    }
-#else
     for (int qt = 0; qt < nqt; ++qt) {
         typename Bwd<PREV, DSN, BF, KV>::QIn in;
         u.fetch(in, qt);
         u.store_dq(in, qt, u.tile(in, qt, Tr[wave]));
     }
-#endif
     }
     const BRowT<BF> dKb = brow<BF>(bd.dk, u.b, u.Tk, bd.f.H * HD), dVb = brow<BF>(bd.dv, u.b, u.Tk, bd.f.H * HD);
     const int ok_ = dKb.at(4 * u.g, u.hc + u.c), ov_ = dVb.at(4 * u.g, u.hc + u.c);   // keys past Tk: dropped
@@ -1375,7 +1092,6 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(bwd_sho
         const float w = wave_sum(u.dc_acc);
         if (lane == 0) G<float>(bd.dc_partial)[bh] = w;
     }
-    if (bd.sum) fold_sums(bd, u.b, u.h, lane);
 }
 
 // LONG (Tk > 64): one WORKGROUP per (b, h).  Key chunks are the outer loop; wave w takes query
@@ -1461,13 +1177,13 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(2))) vo
 // the x extent (gridDim.x) a multiple of 16 -- the linear workgroup id is x + gridDim.x * y, so
 // its XCD is x mod 8 -- and H even; otherwise the plain order.  A bijection of [0, gridDim.x).
 MEP_DEV int head_pair_order(int P, int H) {
-    if (MEP_ATTN_HEADQUAD && !(gridDim.x & 31) && !(H & 3)) {
+    if (!(gridDim.x & 31) && !(H & 3)) {
         // heads 4j .. 4j + 3 of a row on one XCD, dispatched one after another (its L2 fetches a
         // 128-byte line of bf16 rows once for the four 32-byte head slices)
         const int x = P & 7, j = P >> 3;
         return ((((j >> 2) << 3) + x) << 2) + (j & 3);
     }
-    if (!MEP_ATTN_HEADPAIR || (gridDim.x & 15) || (H & 1)) return P;
+    if ((gridDim.x & 15) || (H & 1)) return P;
     const int x = P & 7, j = P >> 3;
     return ((((j >> 1) << 3) + x) << 1) + (j & 1);
 }

@@ -20,38 +20,8 @@
 #include "common.h"
 #include "split.h"
 
-#ifndef MEP_EPI_SPLIT
-#define MEP_EPI_SPLIT 1   // D <= 96 on split-bf16 MFMA (0: exact fp32 MFMA everywhere)
-#endif
-#ifndef MEP_EPI_ONE
-#define MEP_EPI_ONE 0   // single-phase epilogues (both weights resident, intermediate in registers)
-#endif
-#ifndef MEP_NO_DROPBITS
-#define MEP_NO_DROPBITS 0  // 1: ignore mep_epi_desc.drop_bits (the backward re-hashes; A/B only)
-#endif
-#ifndef MEP_EPI_ONE_FWD
-#define MEP_EPI_ONE_FWD MEP_EPI_ONE
-#endif
-#ifndef MEP_EPI_ONE_BWD
-#define MEP_EPI_ONE_BWD 1   // fp32 backward D <= 96 single-phase: Wm^T as 2 bf16 parts (<= 2^-17
-                            // relative), Wp^T 3 parts; cfg3 45.2 -> 37.9 us, GPU suite green
-#endif
-#ifndef MEP_EPI_ONE_BF16
-#define MEP_EPI_ONE_BF16 1   // single-phase epilogues on the bf16 path (cfg3 bf16: 30.6 / 38.3 -> 26.0 / 33.7 us)
-#endif
 #ifndef MEP_EPI_ONE_BF16_MAXD
 #define MEP_EPI_ONE_BF16_MAXD 96
-#endif
-#ifndef MEP_EPI_SPLIT128
-#define MEP_EPI_SPLIT128 1   // D = 128 on split-bf16 MFMA: weights as 2 parts (the 3-part Wm needs 210 KB
-                             // of LDS), activations 3 parts, five products per k pair (cfg5 fwd / bwd
-                             // 259 / 338 -> 185 / 195 us against exact f32 MFMA; GPU suite green)
-#endif
-#ifndef MEP_EPI_SPLIT128_FWD
-#define MEP_EPI_SPLIT128_FWD MEP_EPI_SPLIT128
-#endif
-#ifndef MEP_EPI_SPLIT128_BWD
-#define MEP_EPI_SPLIT128_BWD MEP_EPI_SPLIT128
 #endif
 
 using namespace mep;
@@ -65,95 +35,20 @@ constexpr int ETHREADS = 64 * EWAVES;
 #define MEP_EPI_WAVES 1    // minimum waves per SIMD the epilogue kernels are register-limited to
 #endif
 
-// LDS geometry: the fp32 weights of one block stay resident in LDS for the whole workgroup:
-// forward Wm (and Wp for D <= 96), backward Wm^T (and Wp^T for D <= 96) -- at most 135 KB; for
-// D = 128 the Wp operand is read from L2.  Rows are padded by 4 floats so the 16 rows of a
-// fragment read (lanes c = 0..15, one float4 each) fall in 16 distinct bank groups.
-template <int D>
-struct EpiGeo {
-    static constexpr bool WP_LDS = D <= 96;
-    static constexpr int LP = D + 4;       // D-wide rows
-    static constexpr int LM = 2 * D + 4;   // 2D-wide rows
-    static constexpr int FWD = D * LM + (WP_LDS ? D * LP : 0);
-    static constexpr int BWD = 2 * D * LP + (WP_LDS ? D * LP : 0);
-};
-
-// W [R][C] (row stride C, 16-byte rows) -> LDS rows of stride L; every 16-byte load of the
-// thread is issued before its first LDS write (one L2 latency for the whole staging)
-template <int R, int C>
-MEP_DEV void stage_rows(lfloat* dst, int L, const gfloat* src) {
-    constexpr int n4 = C / 4, NQ = R * n4;
-    constexpr int PER = (NQ + ETHREADS - 1) / ETHREADS;
-    f32x4 v[PER];
-#pragma unroll
-    for (int k = 0; k < PER; ++k) {
-        const int idx = threadIdx.x + ETHREADS * k;
-        if (idx < NQ) {
-            const int r = idx / n4, c4 = idx - r * n4;
-            v[k] = ld4w(src + r * C + 4 * c4);
-        }
-    }
-#pragma unroll
-    for (int k = 0; k < PER; ++k) {
-        const int idx = threadIdx.x + ETHREADS * k;
-        if (idx < NQ) {
-            const int r = idx / n4, c4 = idx - r * n4;
-            *reinterpret_cast<lf32x4*>(dst + r * L + 4 * c4) = v[k];
-        }
-    }
-}
-// W [R][C] -> W^T in LDS rows of stride L (row c = column c of W), in 4 x 4 blocks: a thread
-// loads 4 rows x 4 consecutive columns (16-byte loads, consecutive threads along C: coalesced)
-// and writes 4 transposed 16-byte rows; every load of the thread is issued before the first
-// LDS write, so the staging costs about one L2 latency, not one per element.
-template <int R, int C>
-MEP_DEV void stage_cols_t(lfloat* dst, int L, const gfloat* src) {
-    static_assert(R % 4 == 0 && C % 4 == 0, "4 x 4 blocks");
-    constexpr int CB = C / 4, NB = (R / 4) * CB;
-    constexpr int PER = (NB + ETHREADS - 1) / ETHREADS;
-    f32x4 v[PER][4];
-#pragma unroll
-    for (int k = 0; k < PER; ++k) {
-        const int b = threadIdx.x + ETHREADS * k;
-        if (b < NB) {
-            const int rb = b / CB, cj = b - rb * CB;
-#pragma unroll
-            for (int e = 0; e < 4; ++e) v[k][e] = ld4w(src + (4 * rb + e) * C + 4 * cj);
-        }
-    }
-#pragma unroll
-    for (int k = 0; k < PER; ++k) {
-        const int b = threadIdx.x + ETHREADS * k;
-        if (b < NB) {
-            const int rb = b / CB, cj = b - rb * CB;
-#pragma unroll
-            for (int e = 0; e < 4; ++e)
-                *reinterpret_cast<lf32x4*>(dst + (4 * cj + e) * L + 4 * rb) =
-                    f32x4{v[k][0][e], v[k][1][e], v[k][2][e], v[k][3][e]};
-        }
-    }
-}
-
 MEP_DEV float4 f4(const f32x4 v) { return make_float4(v[0], v[1], v[2], v[3]); }
 
 // tiles [t_begin, t_end) of 16 tokens owned by this workgroup (contiguous range per workgroup)
-// The epilogue grid is (slices, descriptors).  XCD-aware order (MEP_EPI_XCD): workgroups are
+// The epilogue grid is (slices, descriptors).  XCD-aware order: workgroups are
 // dispatched to the 8 XCDs round-robin by linear id, so id -> (descriptor, slice) is remapped to
 // give XCD x a contiguous run of the descriptor-major work list -- every XCD then stages the
 // weights of one or two blocks instead of all of them, and its L2 serves the other workgroups'
 // staging reads of those weights (the first reads of each block's weights come from MALL / HBM
 // once per XCD, not once per workgroup).
-#ifndef MEP_EPI_XCD
-#define MEP_EPI_XCD 1
-#endif
 MEP_DEV bool epi_slot(int& desc, int& slice) {
     const int G = gridDim.x * gridDim.y, id = blockIdx.x + gridDim.x * blockIdx.y;
-    int unit = id;
-    if (MEP_EPI_XCD) {
-        // XCD x = id % 8 holds q + (x < r) of the G workgroups (G = 8 q + r): the x-th run
-        const int q = G / 8, r = G % 8, x = id % 8;
-        unit = x * q + min(x, r) + id / 8;
-    }
+    // XCD x = id % 8 holds q + (x < r) of the G workgroups (G = 8 q + r): the x-th run
+    const int q = G / 8, r = G % 8, x = id % 8;
+    const int unit = x * q + min(x, r) + id / 8;
     desc = unit / (int)gridDim.x;
     slice = unit - desc * (int)gridDim.x;
     return true;
@@ -207,101 +102,10 @@ struct Upstream {
 };
 
 // ---------------------------------------------------------------- forward
-// Per tile of 16 tokens (common.h, transposed tiles): xp^T = Wp x^T, then z^T = Wm [q | xp]^T
-// with the xp accumulators as the B operand of the second product; LayerNorm on the
-// accumulators.  x and q rows are read straight from HBM into B fragments (no LDS).
-template <int D, typename AP, typename AM>
-MEP_DEV void epi_fwd_tiles(const mep_epi_desc& d, const AP& wp, const AM& wm, int t_begin, int t_end) {
-    constexpr int NI = D / 16, KB = D / 16;
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int c = lane & 15, g = lane >> 4;
-    const int ntok = d.ntok;
-    const float p = d.drop_p;
-    const uint64_t seed = (d.seed && p > 0.f) ? *G<const uint64_t>(d.seed) : 0;
-    // global token offset of this shard's rows (seed[1] = the rank's first global batch row)
-    const uint64_t tok0 = (d.seed && p > 0.f) ? G<const uint64_t>(d.seed)[1] * (uint64_t)d.q.T : 0;
-    const uint64_t dbits = p > 0.f && !MEP_NO_DROPBITS ? d.drop_bits : 0;   // the forward's keep bits (0: hash)
-    const bool have_bits = dbits != 0;
-    const float keep_s = p > 0.f ? 1.0f / (1.0f - p) : 1.0f;   // == drop_scale's kept value
-    (void)have_bits; (void)keep_s;
-    gfloat* stats = G<float>(d.stats);
-    AM wm_x = wm;
-    wm_x.pos0 += D;                     // Wm[:, D:], the xp half of the concat
-    for (int tile = t_begin + wave; tile < t_end; tile += EWAVES) {
-        const int tok = tile * 16 + c;
-        const bool ok = tok < ntok;
-        const int tc = min(tok, ntok - 1);
-        const gfloat* xr = row_ptr(d.x, tc) + 4 * g;
-        const gfloat* qr = row_ptr(d.q, tc) + 4 * g;
-        // every B fragment of the tile (x and q rows, 4 consecutive features per lane) is issued
-        // before the first MFMA: one memory latency per tile instead of one per k block
-        f32x4 xb[KB], qb[KB];
-#pragma unroll
-        for (int kb = 0; kb < KB; ++kb) xb[kb] = ld4w(xr + 16 * kb);
-#pragma unroll
-        for (int kb = 0; kb < KB; ++kb) qb[kb] = ld4w(qr + 16 * kb);
-        f32x4 xp[NI], z[NI];
-#pragma unroll
-        for (int i = 0; i < NI; ++i) { xp[i] = zero_f4(); z[i] = zero_f4(); }
-        tgemm<NI, KB>(xp, wp, [&](int kb) { return xb[kb]; });
-        if (p > 0.f) {
-            uint32_t kb0 = 0;
-#pragma unroll
-            for (int i = 0; i < NI; ++i)
-#pragma unroll
-                for (int r = 0; r < 4; ++r)
-                    xp[i][r] *= drop_rec(seed, 2u * d.drop_stream, (tok0 + (uint64_t)tok) * D + 16 * i + 4 * g + r, p, kb0, 4 * i + r);
-            drop_bits_put(drop_bits_ptr(dbits, tok, 0), kb0);
-        }
-        tgemm<NI, KB>(z, wm, [&](int kb) { return qb[kb]; });              // q half of [q | xp]
-        tgemm<NI, KB>(z, wm_x, [&](int kb) { return xp[kb]; });            // xp half
-        // LayerNorm over the D features of token c: in-lane sum + the 4 lane groups
-        float sum = 0.f;
-#pragma unroll
-        for (int i = 0; i < NI; ++i) sum += (z[i][0] + z[i][1]) + (z[i][2] + z[i][3]);
-        sum += __shfl_xor(sum, 16, 64);
-        sum += __shfl_xor(sum, 32, 64);
-        const float mean = sum / (float)D;
-        float var = 0.f;
-#pragma unroll
-        for (int i = 0; i < NI; ++i)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) { const float t = z[i][r] - mean; var += t * t; }
-        var += __shfl_xor(var, 16, 64);
-        var += __shfl_xor(var, 32, 64);
-        const float rstd = 1.0f / sqrtf(var / (float)D + LN_EPS);
-        if (ok) {
-            gfloat* zr = row_ptr(d.z, tok);
-            gfloat* orow = row_ptr(d.out, tok);
-            gfloat* pr = row_ptr(d.xp, tok);
-            uint32_t kb1 = 0;   // keep bits of the out site
-#pragma unroll
-            for (int i = 0; i < NI; ++i) {
-                const int col = 16 * i + 4 * g;
-                const f32x4 w = ld4w(G<const float>(d.ln_w) + col), b = ld4w(G<const float>(d.ln_b) + col);
-                f32x4 y;
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    y[r] = (z[i][r] - mean) * rstd * w[r] + b[r];
-                    if (p > 0.f) y[r] *= drop_rec(seed, 2u * d.drop_stream + 1u, (tok0 + (uint64_t)tok) * D + col + r, p, kb1, 4 * i + r);
-                }
-                stg4(zr + col, f4(z[i]));
-                stg4(orow + col, f4(y));
-                stg4(pr + col, f4(xp[i]));
-            }
-            if (p > 0.f) drop_bits_put(drop_bits_ptr(dbits, tok, 1), kb1);
-            if (g == 0) { stats[2 * tok] = mean; stats[2 * tok + 1] = rstd; }
-        }
-    }
-}
-
 // stage W [R][C] (fp32, row stride C) split into LDS: unit (n, p, g) = W[n][32p + 4g ..] and
 // W[n][32p + 16 + 4g ..]; every load of the thread is issued before its first LDS write
 template <int R, int C, int NPART, int NT = ETHREADS>
 MEP_DEV void stage_split_rows(const SplitW<R, C / 32, NPART>& dst, const gfloat* src) {
-#ifdef MEP_EPI_NOSTAGE   // timing-only development build: no weight staging (LDS left as it is)
-    return;
-#endif
     constexpr int NU = R * (C / 32) * 4;
     constexpr int PER = (NU + NT - 1) / NT;
     f32x4 v[PER][2];
@@ -329,9 +133,6 @@ MEP_DEV void stage_split_rows(const SplitW<R, C / 32, NPART>& dst, const gfloat*
 // threads take consecutive n (coalesced), loads issued before the LDS writes
 template <int R, int C, int NPART, int NT = ETHREADS>
 MEP_DEV void stage_split_cols(const SplitW<C, R / 32, NPART>& dst, const gfloat* src) {
-#ifdef MEP_EPI_NOSTAGE
-    return;
-#endif
     constexpr int NP = R / 32, NU = C * NP * 4;
     constexpr int PER = (NU + NT - 1) / NT;
     float v[PER][8];
@@ -365,21 +166,6 @@ MEP_DEV void wg_store_barrier() {
     __syncthreads();
 }
 
-// A weight image built by mep_epi_images (global, BYTES a multiple of 1 KB: the exact LDS bytes
-// the staging below would write) into LDS by LDS-DMA: wave w copies the 1-KB chunks w, w + EWAVES,
-// ... (lane l: bytes 16 l .. 16 l + 15 of the chunk) without passing through registers.  The
-// caller waits (image_ready) before its barrier.
-template <int BYTES, int NW = EWAVES>
-MEP_DEV void dma_image(unsigned char* sm, uint64_t img) {
-    static_assert(BYTES % 1024 == 0, "epilogue weight images are whole 1-KB chunks");
-    typedef __attribute__((address_space(3))) void lvoid;
-    typedef __attribute__((address_space(3))) unsigned char lbyte;
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const auto rs = __builtin_amdgcn_make_buffer_rsrc((void*)img, 0, BYTES, 0x00020000);
-    for (int ch = wave; ch < BYTES / 1024; ch += NW)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lvoid*)((lbyte*)sm + ch * 1024), 16, 16 * lane, ch * 1024, 0, 0);
-}
-MEP_DEV void image_ready() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
 // the LayerNorm weight (and bias) into LDS with the weight staging (published by its barrier): the
 // per-tile LayerNorm then reads them from LDS instead of waiting on a global load at every tile's end
@@ -389,16 +175,6 @@ MEP_DEV void stage_ln(lfloat* dst, const mep_epi_desc& d) {
     if (t < D) dst[t] = G<const float>(d.ln_w)[t];
     else if (BIAS && t < 2 * D) dst[t] = G<const float>(d.ln_b)[t - D];
 }
-
-#ifdef MEP_EPI_TRACE
-// development build only (scripts/epi_trace.py): per-workgroup phase stamps, 8 words per workgroup
-// of the launch grid (x + gridDim.x * y): start, weight 1 staged, phase 1 done, weight 2 staged, end
-__device__ unsigned long long* g_epi_trace;
-extern "C" int mep_epi_set_trace(void* p) { return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_epi_trace), &p, sizeof(p)); }
-#define MEP_EPI_STAMP(k) do { if (threadIdx.x == 0 && g_epi_trace) g_epi_trace[8 * (blockIdx.x + gridDim.x * blockIdx.y) + (k)] = __builtin_amdgcn_s_memrealtime(); } while (0)
-#else
-#define MEP_EPI_STAMP(k) ((void)0)
-#endif
 
 template <int D, int NPART, int NW, bool DROP>
 MEP_DEV void epi_fwd_split(const mep_epi_desc& d, unsigned char* sm, int t_begin, int t_end) {
@@ -414,7 +190,7 @@ MEP_DEV void epi_fwd_split(const mep_epi_desc& d, unsigned char* sm, int t_begin
     const uint64_t seed = (d.seed && p > 0.f) ? *G<const uint64_t>(d.seed) : 0;
     // global token offset of this shard's rows (seed[1] = the rank's first global batch row)
     const uint64_t tok0 = (d.seed && p > 0.f) ? G<const uint64_t>(d.seed)[1] * (uint64_t)d.q.T : 0;
-    const uint64_t dbits = p > 0.f && !MEP_NO_DROPBITS ? d.drop_bits : 0;   // the forward's keep bits (0: hash)
+    const uint64_t dbits = p > 0.f ? d.drop_bits : 0;   // the forward's keep bits (0: hash)
     const bool have_bits = dbits != 0;
     const float keep_s = p > 0.f ? 1.0f / (1.0f - p) : 1.0f;   // == drop_scale's kept value
     (void)have_bits; (void)keep_s;
@@ -429,11 +205,9 @@ MEP_DEV void epi_fwd_split(const mep_epi_desc& d, unsigned char* sm, int t_begin
         for (int kb = 0; kb < KB; ++kb) dst[kb] = ld4a(r + 16 * kb);
     };
     // ---- phase 1: xp = drop(x Wp^T)
-    MEP_EPI_STAMP(0);
     if (t_begin + wave < t_end) rows_of(d.x, t_begin + wave, ab);
     stage_split_rows<D, D, NW>(wp, G<const float>(d.wp));
     __syncthreads();
-    MEP_EPI_STAMP(1);
     for (int tile = t_begin + wave; tile < t_end; tile += EWAVES) {
         const int tok = tile * 16 + c;
         Op xs[NP];
@@ -462,11 +236,9 @@ MEP_DEV void epi_fwd_split(const mep_epi_desc& d, unsigned char* sm, int t_begin
     // ---- phase 2: z = [q | xp] Wm^T, out = drop(LayerNorm(z))
     if (t_begin + wave < t_end) rows_of(d.q, t_begin + wave, ab);
     wg_store_barrier();              // xp rows stored; Wp no longer read
-    MEP_EPI_STAMP(2);
     if (t_begin + wave < t_end) rows_of(d.xp, t_begin + wave, bb);
     stage_split_rows<D, 2 * D, NW>(wm, G<const float>(d.wm));
     __syncthreads();
-    MEP_EPI_STAMP(3);
     for (int tile = t_begin + wave; tile < t_end; tile += EWAVES) {
         const int tok = tile * 16 + c;
         Op qs[NP], ps[NP];
@@ -515,11 +287,6 @@ MEP_DEV void epi_fwd_split(const mep_epi_desc& d, unsigned char* sm, int t_begin
             if (g == 0) { stats[2 * tok] = mean; stats[2 * tok + 1] = rstd; }
         }
     }
-#ifdef MEP_EPI_TRACE
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    MEP_EPI_STAMP(4);
-#endif
 }
 
 template <int D, int NPART, int NW, bool DROP>
@@ -537,7 +304,7 @@ MEP_DEV void epi_bwd_split(const mep_epi_bwd_desc& bd, unsigned char* sm, int t_
     const uint64_t seed = (d.seed && p > 0.f) ? *G<const uint64_t>(d.seed) : 0;
     // global token offset of this shard's rows (seed[1] = the rank's first global batch row)
     const uint64_t tok0 = (d.seed && p > 0.f) ? G<const uint64_t>(d.seed)[1] * (uint64_t)d.q.T : 0;
-    const uint64_t dbits = p > 0.f && !MEP_NO_DROPBITS ? d.drop_bits : 0;   // the forward's keep bits (0: hash)
+    const uint64_t dbits = p > 0.f ? d.drop_bits : 0;   // the forward's keep bits (0: hash)
     const bool have_bits = dbits != 0;
     const float keep_s = p > 0.f ? 1.0f / (1.0f - p) : 1.0f;   // == drop_scale's kept value
     (void)have_bits; (void)keep_s;
@@ -702,7 +469,7 @@ MEP_DEV void epi_fwd_one(const mep_epi_desc& d, unsigned char* sm, int t_begin, 
     const float p = DROP ? d.drop_p : 0.f;
     const uint64_t seed = (d.seed && p > 0.f) ? *G<const uint64_t>(d.seed) : 0;
     const uint64_t tok0 = (d.seed && p > 0.f) ? G<const uint64_t>(d.seed)[1] * (uint64_t)d.q.T : 0;
-    const uint64_t dbits = p > 0.f && !MEP_NO_DROPBITS ? d.drop_bits : 0;   // the forward's keep bits (0: hash)
+    const uint64_t dbits = p > 0.f ? d.drop_bits : 0;   // the forward's keep bits (0: hash)
     const bool have_bits = dbits != 0;
     const float keep_s = p > 0.f ? 1.0f / (1.0f - p) : 1.0f;   // == drop_scale's kept value
     (void)have_bits; (void)keep_s;
@@ -719,13 +486,8 @@ MEP_DEV void epi_fwd_one(const mep_epi_desc& d, unsigned char* sm, int t_begin, 
     __shared__ __attribute__((aligned(16))) float lnp[2 * D];   // LayerNorm weight | bias
     stage_ln<D, true>((lfloat*)lnp, d);
     if (t_begin + wave < t_end) { rows_of(d.x, t_begin + wave, ab); rows_of(d.q, t_begin + wave, bb); }
-    if (d.image) {
-        dma_image<WP::BYTES + WM::BYTES, NW>(sm, d.image);
-        image_ready();
-    } else {
-        stage_split_rows<D, D, NWP, 64 * NW>(wp, G<const float>(d.wp));
-        stage_split_rows<D, 2 * D, NWM, 64 * NW>(wm, G<const float>(d.wm));
-    }
+    stage_split_rows<D, D, NWP, 64 * NW>(wp, G<const float>(d.wp));
+    stage_split_rows<D, 2 * D, NWM, 64 * NW>(wm, G<const float>(d.wm));
     __syncthreads();
     for (int tile = t_begin + wave; tile < t_end; tile += NW) {
         const int tok = tile * 16 + c;
@@ -833,7 +595,6 @@ MEP_DEV void epi_fwd_wp2r(const mep_epi_desc& d, unsigned char* sm, int t_begin,
 #pragma unroll
         for (int kb = 0; kb < KB; ++kb) dst[kb] = ld4w(r + 16 * kb);
     };
-    MEP_EPI_STAMP(0);
     __shared__ __attribute__((aligned(16))) float lnp[2 * D];   // LayerNorm weight | bias
     stage_ln<D, true>((lfloat*)lnp, d);
     f32x4 ab[KB], bb[KB];            // x rows and q rows, one tile ahead
@@ -846,11 +607,6 @@ MEP_DEV void epi_fwd_wp2r(const mep_epi_desc& d, unsigned char* sm, int t_begin,
         const gfloat* r = W + (R2 + c) * D + 32 * pp + 4 * g;
         w2r[pp] = opn<3>(ld4w(r), ld4w(r + 16)).p[2];
     }
-    if (d.image) {
-        dma_image<E::BYTES>(sm, d.image);
-        image_ready();
-    } else {
-#ifndef MEP_EPI_NOSTAGE
     {   // Wp: unit (n, pp, g) = Wp[n][32 pp + 4 g ..], [.. + 16 ..] -> parts 0, 1 (and 2 for n < R2)
         constexpr int NU = D * NP * 4, PER = (NU + ETHREADS - 1) / ETHREADS;
         f32x4 v[PER][2];
@@ -899,13 +655,9 @@ MEP_DEV void epi_fwd_wp2r(const mep_epi_desc& d, unsigned char* sm, int t_begin,
             }
         }
     }
-#endif
-    }
     __syncthreads();
-    MEP_EPI_STAMP(1);
     for (int tile = t_begin + wave; tile < t_end; tile += EWAVES) {
         const int tok = tile * 16 + c;
-        if (tile == t_begin + wave + EWAVES) MEP_EPI_STAMP(6);   // wave 0's second tile starts
         f32x4 xp[NI];
 #pragma unroll
         for (int i = 0; i < NI; ++i) xp[i] = zero_f4();
@@ -939,7 +691,6 @@ MEP_DEV void epi_fwd_wp2r(const mep_epi_desc& d, unsigned char* sm, int t_begin,
                 __builtin_amdgcn_sched_barrier(0);
             }
         }
-        if (tile == t_begin + wave) MEP_EPI_STAMP(3);
         if (tile + EWAVES < t_end) rows_of(d.x, tile + EWAVES, ab);   // behind the z product
         if (tok < ntok) {
             gfloat* pr = row_ptr(d.xp, tok);
@@ -953,7 +704,6 @@ MEP_DEV void epi_fwd_wp2r(const mep_epi_desc& d, unsigned char* sm, int t_begin,
                               [&](int pp) { return opn<3>(bb[2 * pp], bb[2 * pp + 1]); });
         tgemm_n<NI, NP, 3, 3>(z, [&](int i, int pp) { return wm.frag(i, NP + pp); },
                               [&](int pp) { return opn<3>(xp[2 * pp], xp[2 * pp + 1]); });
-        if (tile == t_begin + wave) MEP_EPI_STAMP(4);
         float sum = 0.f;
 #pragma unroll
         for (int i = 0; i < NI; ++i) sum += (z[i][0] + z[i][1]) + (z[i][2] + z[i][3]);
@@ -986,16 +736,7 @@ MEP_DEV void epi_fwd_wp2r(const mep_epi_desc& d, unsigned char* sm, int t_begin,
             }
             if (g == 0) { stats[2 * tok] = mean; stats[2 * tok + 1] = rstd; }
         }
-#ifdef MEP_EPI_TRACE
-        if (tile == t_begin + wave) { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); MEP_EPI_STAMP(5); }
-        if (tile == t_begin + wave + EWAVES) { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); MEP_EPI_STAMP(7); }
-#endif
     }
-#ifdef MEP_EPI_TRACE
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    MEP_EPI_STAMP(2);
-#endif
 }
 
 template <int D, int NPART, int NWP, int NWM, bool DROP, int NW = EWAVES>
@@ -1012,7 +753,7 @@ MEP_DEV void epi_bwd_one(const mep_epi_bwd_desc& bd, unsigned char* sm, int t_be
     const float p = DROP ? d.drop_p : 0.f;
     const uint64_t seed = (d.seed && p > 0.f) ? *G<const uint64_t>(d.seed) : 0;
     const uint64_t tok0 = (d.seed && p > 0.f) ? G<const uint64_t>(d.seed)[1] * (uint64_t)d.q.T : 0;
-    const uint64_t dbits = p > 0.f && !MEP_NO_DROPBITS ? d.drop_bits : 0;   // the forward's keep bits (0: hash)
+    const uint64_t dbits = p > 0.f ? d.drop_bits : 0;   // the forward's keep bits (0: hash)
     const bool have_bits = dbits != 0;
     const float keep_s = p > 0.f ? 1.0f / (1.0f - p) : 1.0f;   // == drop_scale's kept value
     (void)have_bits; (void)keep_s;
@@ -1038,13 +779,8 @@ MEP_DEV void epi_bwd_one(const mep_epi_bwd_desc& bd, unsigned char* sm, int t_be
     __shared__ __attribute__((aligned(16))) float lnp[D];   // LayerNorm weight
     stage_ln<D, false>((lfloat*)lnp, d);
     if (t_begin + wave < t_end) fetch1(t_begin + wave);
-    if (bd.image) {
-        dma_image<WMT::BYTES + WPT::BYTES, NW>(sm, bd.image);
-        image_ready();
-    } else {
-        stage_split_cols<D, 2 * D, NWM, 64 * NW>(wmt, G<const float>(d.wm));
-        stage_split_cols<D, D, NWP, 64 * NW>(wpt, G<const float>(d.wp));
-    }
+    stage_split_cols<D, 2 * D, NWM, 64 * NW>(wmt, G<const float>(d.wm));
+    stage_split_cols<D, D, NWP, 64 * NW>(wpt, G<const float>(d.wp));
     __syncthreads();
     for (int tile = t_begin + wave; tile < t_end; tile += NW) {
         const int tok = tile * 16 + c;
@@ -1150,23 +886,17 @@ MEP_DEV void epi_bwd_one(const mep_epi_bwd_desc& bd, unsigned char* sm, int t_be
     }
 }
 
-#ifndef MEP_EPI_FWD_WP2R
-#define MEP_EPI_FWD_WP2R 1  // single-phase fp32 forward at D = 96, all six products (epi_fwd_wp2r)
-#endif
 // parts per weight of the single-phase epilogues (0: the two-phase kernels)
 template <int D, bool BF16> struct EpiOne {
-    // fp32 path: off by default (the 2-part weight at D = 96 moved one cmu_cfg3 logit 5e-4 relative
-    // and flipped a near-zero Adam update on ren_small); bf16 path: one part per weight, on
-    static constexpr bool ON_BF = BF16 && MEP_EPI_ONE_BF16 && D <= MEP_EPI_ONE_BF16_MAXD;
-    static constexpr bool FWD = (MEP_EPI_ONE_FWD && D <= 96) || ON_BF || (!BF16 && D == 96 && MEP_EPI_FWD_WP2R),
-                          BWD = (MEP_EPI_ONE_BWD && D <= 96) || ON_BF;
+    // fp32 forward: single phase at D = 96 with all six products (epi_fwd_wp2r; a 2-part weight moved
+    // one cmu_cfg3 logit 5e-4 relative), two phases below; fp32 backward: single phase for
+    // D <= 96 (Wm^T as 2 parts); bf16 path: one part per weight, single phase
+    static constexpr bool ON_BF = BF16 && D <= MEP_EPI_ONE_BF16_MAXD;
+    static constexpr bool FWD = ON_BF || (!BF16 && D == 96), BWD = D <= 96 || ON_BF;
     static constexpr int NPART = BF16 ? 1 : 3;
-#ifndef MEP_EPI_FWD_WM2
-#define MEP_EPI_FWD_WM2 0   // single-phase fp32 forward at D = 96: 1 = 3-part Wp + 2-part Wm (144 KB)
-#endif
-    static constexpr bool FWD_WP2R = !BF16 && D == 96 && MEP_EPI_FWD_WP2R && !MEP_EPI_FWD_WM2;
-    static constexpr int FWD_WP = BF16 ? 1 : (D == 96 && !MEP_EPI_FWD_WM2 ? 2 : 3);
-    static constexpr int FWD_WM = BF16 ? 1 : (D == 96 && MEP_EPI_FWD_WM2 ? 2 : NPART);
+    static constexpr bool FWD_WP2R = !BF16 && D == 96;
+    static constexpr int FWD_WP = BF16 ? 1 : (D == 96 ? 2 : 3);
+    static constexpr int FWD_WM = BF16 ? 1 : NPART;
     static constexpr int BWD_WP = NPART, BWD_WM = BF16 ? 1 : (D == 96 ? 2 : 3);
     static constexpr int FWD_BYTES = FWD_WP2R ? EpiWp2r<D>::BYTES : SplitW<D, D / 32, FWD_WP>::BYTES + SplitW<D, D / 16, FWD_WM>::BYTES;
     static constexpr int BWD_BYTES = SplitW<2 * D, D / 32, BWD_WM>::BYTES + SplitW<D, D / 32, BWD_WP>::BYTES;
@@ -1177,7 +907,6 @@ template <int D, bool BF16> struct EpiOne {
 // and D = 128 the fp32 MFMA path
 template <int D, bool BF16>
 __global__ __launch_bounds__(ETHREADS) __attribute__((amdgpu_waves_per_eu(MEP_EPI_WAVES))) void k_epi_fwd(const mep_epi_desc* __restrict__ descs) {
-    using Geo = EpiGeo<D>;
     int di, slice;
     if (!epi_slot(di, slice)) return;
     const mep_epi_desc& d = descs[di];
@@ -1196,164 +925,20 @@ __global__ __launch_bounds__(ETHREADS) __attribute__((amdgpu_waves_per_eu(MEP_EP
         }
         return;
     }
-    if constexpr (BF16 || (MEP_EPI_SPLIT && D <= 96) || (MEP_EPI_SPLIT128_FWD && D == 128)) {
-        constexpr int NPART = BF16 ? 1 : 3, NW = BF16 ? 1 : (D == 128 ? 2 : 3);
-        constexpr int BYTES = SplitW<D, D / 16, NW>::BYTES;   // the larger phase (Wm)
-        __shared__ __attribute__((aligned(16))) unsigned char sm6[BYTES];
-        if (d.drop_p > 0.f) epi_fwd_split<D, NPART, NW, true>(d, sm6, t_begin, t_end);
-        else epi_fwd_split<D, NPART, NW, false>(d, sm6, t_begin, t_end);
-        return;
-    }
-    __shared__ __attribute__((aligned(16))) float smem[Geo::FWD];
-    lfloat* wm = (lfloat*)&smem[0];
-    stage_rows<D, 2 * D>(wm, Geo::LM, G<const float>(d.wm));
-    const WRows<lfloat> am{wm, Geo::LM, 0, 0};
-    if constexpr (Geo::WP_LDS) {
-        lfloat* wp = wm + D * Geo::LM;
-        stage_rows<D, D>(wp, Geo::LP, G<const float>(d.wp));
-        __syncthreads();
-        epi_fwd_tiles<D>(d, WRows<lfloat>{wp, Geo::LP, 0, 0}, am, t_begin, t_end);
-    } else {
-        __syncthreads();
-        epi_fwd_tiles<D>(d, WRows<gfloat>{G<const float>(d.wp), D, 0, 0}, am, t_begin, t_end);
-    }
+    constexpr int NPART = BF16 ? 1 : 3, NW = BF16 ? 1 : (D == 128 ? 2 : 3);
+    constexpr int BYTES = SplitW<D, D / 16, NW>::BYTES;   // the larger phase (Wm)
+    __shared__ __attribute__((aligned(16))) unsigned char sm6[BYTES];
+    if (d.drop_p > 0.f) epi_fwd_split<D, NPART, NW, true>(d, sm6, t_begin, t_end);
+    else epi_fwd_split<D, NPART, NW, false>(d, sm6, t_begin, t_end);
 }
 
 // ---------------------------------------------------------------- backward
-// Same mapping.  dout (+dout2) and z are read straight into the accumulator layout, the
-// LayerNorm backward runs in registers, and dz^T feeds the three products directly:
-// dxp^T = Wm[:, D:]^T dz^T (rows D.. of Wm^T), dq^T = Wm[:, :D]^T dz^T and dx^T = Wp^T dxp^T.
-// LayerNorm parameter partials: per tile, sums over its 16 tokens (DPP row reductions) into the
-// tile's ln_partial row [2][D].  For D = 128 the dq / dx products run in two halves of output
-// tiles so the live accumulators stay within the register budget.
-template <int NI, int KB, int NH, typename AF, typename BF, typename ST>
-MEP_DEV void tgemm_store(AF afr, BF&& bfr, ST&& store) {
-    constexpr int NS = NI / NH;
-#pragma unroll
-    for (int h = 0; h < NH; ++h) {
-        f32x4 acc[NS];
-#pragma unroll
-        for (int i = 0; i < NS; ++i) acc[i] = zero_f4();
-        AF a = afr;
-        a.row0 += 16 * NS * h;
-        tgemm<NS, KB>(acc, a, bfr);
-#pragma unroll
-        for (int i = 0; i < NS; ++i) store(NS * h + i, acc[i]);
-    }
-}
-
-template <int D, typename AM, typename AP>
-MEP_DEV void epi_bwd_tiles(const mep_epi_bwd_desc& bd, const AM& wmt, const AP& wpt, int t_begin, int t_end) {
-    constexpr int NI = D / 16, KB = D / 16, NH = D > 96 ? 2 : 1;
-    const mep_epi_desc& d = bd.f;
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int c = lane & 15, g = lane >> 4;
-    const int ntok = d.ntok;
-    const float p = d.drop_p;
-    const uint64_t seed = (d.seed && p > 0.f) ? *G<const uint64_t>(d.seed) : 0;
-    // global token offset of this shard's rows (seed[1] = the rank's first global batch row)
-    const uint64_t tok0 = (d.seed && p > 0.f) ? G<const uint64_t>(d.seed)[1] * (uint64_t)d.q.T : 0;
-    const uint64_t dbits = p > 0.f && !MEP_NO_DROPBITS ? d.drop_bits : 0;   // the forward's keep bits (0: hash)
-    const bool have_bits = dbits != 0;
-    const float keep_s = p > 0.f ? 1.0f / (1.0f - p) : 1.0f;   // == drop_scale's kept value
-    (void)have_bits; (void)keep_s;
-    AM wmt_x = wmt;
-    wmt_x.row0 += D;                    // rows D.. of Wm^T = Wm[:, D:]
-    const gfloat* stats = G<const float>(d.stats);
-    gfloat* lpart = G<float>(bd.ln_partial);
-    const Upstream up(bd);
-    for (int tile = t_begin + wave; tile < t_end; tile += EWAVES) {
-        const int tok = tile * 16 + c;
-        const uint32_t kbb0 = have_bits ? drop_bits_get(drop_bits_ptr(dbits, tok, 0)) : 0u;   // the forward's keep bits
-        const uint32_t kbb1 = have_bits ? drop_bits_get(drop_bits_ptr(dbits, tok, 1)) : 0u;
-        const bool ok = tok < ntok;
-        const int tc = min(tok, ntok - 1);
-        const gfloat* g2 = bd.dout2.ptr ? row_ptr(bd.dout2, tc) : nullptr;
-        const gfloat* zr = row_ptr(d.z, tc);
-        const float mean = stats[2 * tc], rstd = stats[2 * tc + 1];
-        f32x4 dz[NI];                   // g * w first, dz after the row sums
-        float s1 = 0.f, s2 = 0.f;
-        gfloat* lp = lpart ? lpart + (int64_t)tile * 2 * D : nullptr;
-#pragma unroll
-        for (int i = 0; i < NI; ++i) {
-            const int col = 16 * i + 4 * g;
-            f32x4 a = up.at(bd, tc, col);
-            if (g2) a += ld4w(g2 + col);
-            const f32x4 zz = ld4w(zr + col), w = ld4w(G<const float>(d.ln_w) + col);
-            f32x4 pw, pb;
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                float gg = a[r];
-                if (p > 0.f) gg *= drop_use(have_bits, kbb1, 4 * i + r, keep_s, seed, 2u * d.drop_stream + 1u, (tok0 + (uint64_t)tok) * D + col + r, p);
-                gg = ok ? gg : 0.f;
-                const float x = (zz[r] - mean) * rstd;
-                const float gw = gg * w[r];
-                s1 += gw;
-                s2 += gw * x;
-                pw[r] = row16_sum(gg * x);
-                pb[r] = row16_sum(gg);
-                dz[i][r] = gw;
-            }
-            if (lp && c == 0) {
-                stg4(lp + col, f4(pw));
-                stg4(lp + D + col, f4(pb));
-            }
-        }
-        s1 += __shfl_xor(s1, 16, 64);
-        s1 += __shfl_xor(s1, 32, 64);
-        s2 += __shfl_xor(s2, 16, 64);
-        s2 += __shfl_xor(s2, 32, 64);
-        s1 /= (float)D;
-        s2 /= (float)D;
-        // dz = rstd * (g w - s1 - x-hat s2), x-hat recomputed from z (L1-hot) instead of kept live
-#pragma unroll
-        for (int i = 0; i < NI; ++i) {
-            const f32x4 zz = ld4w(zr + 16 * i + 4 * g);
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const float x = (zz[r] - mean) * rstd;
-                dz[i][r] = ok ? rstd * (dz[i][r] - s1 - x * s2) : 0.f;
-            }
-        }
-        // dxp^T = Wm[:, D:]^T dz^T, then the xp dropout mask
-        f32x4 dxp[NI];
-#pragma unroll
-        for (int i = 0; i < NI; ++i) dxp[i] = zero_f4();
-        tgemm<NI, KB>(dxp, wmt_x, [&](int kb) { return dz[kb]; });
-        if (p > 0.f) {
-#pragma unroll
-            for (int i = 0; i < NI; ++i)
-#pragma unroll
-                for (int r = 0; r < 4; ++r)
-                    dxp[i][r] *= drop_use(have_bits, kbb0, 4 * i + r, keep_s, seed, 2u * d.drop_stream, (tok0 + (uint64_t)tok) * D + 16 * i + 4 * g + r, p);
-        }
-        if (ok) {
-            gfloat* dzr = row_ptr(bd.dz, tok);
-            gfloat* dpr = row_ptr(bd.dxp, tok);
-#pragma unroll
-            for (int i = 0; i < NI; ++i) {
-                stg4(dzr + 16 * i + 4 * g, f4(dz[i]));
-                stg4(dpr + 16 * i + 4 * g, f4(dxp[i]));
-            }
-        }
-        // dq^T (direct part) = Wm[:, :D]^T dz^T
-        gfloat* qrw = row_ptr(bd.dq, tc);
-        tgemm_store<NI, KB, NH>(wmt, [&](int kb) { return dz[kb]; }, [&](int i, f32x4 v) {
-            if (!ok) return;
-            if (bd.dq_accumulate) v += ld4w(qrw + 16 * i + 4 * g);
-            stg4(qrw + 16 * i + 4 * g, f4(v));
-        });
-        // dx^T = Wp^T dxp^T
-        gfloat* xrw = row_ptr(bd.dx, tc);
-        tgemm_store<NI, KB, NH>(wpt, [&](int kb) { return dxp[kb]; }, [&](int i, f32x4 v) {
-            if (ok) stg4(xrw + 16 * i + 4 * g, f4(v));
-        });
-    }
-}
-
+// dout (+dout2) and z are read straight into the accumulator layout, the LayerNorm backward runs
+// in registers, and dz^T feeds the products directly: dxp^T = Wm[:, D:]^T dz^T, dq^T =
+// Wm[:, :D]^T dz^T and dx^T = Wp^T dxp^T; LayerNorm parameter partials per 16-token tile into its
+// ln_partial row [2][D] (epi_bwd_one / epi_bwd_split).
 template <int D, bool BF16>
 __global__ __launch_bounds__(ETHREADS) __attribute__((amdgpu_waves_per_eu(MEP_EPI_WAVES))) void k_epi_bwd(const mep_epi_bwd_desc* __restrict__ descs) {
-    using Geo = EpiGeo<D>;
     int di, slice;
     if (!epi_slot(di, slice)) return;
     const mep_epi_bwd_desc& bd = descs[di];
@@ -1367,27 +952,11 @@ __global__ __launch_bounds__(ETHREADS) __attribute__((amdgpu_waves_per_eu(MEP_EP
         else epi_bwd_one<D, E::NPART, E::BWD_WP, E::BWD_WM, false>(bd, sm1, t_begin, t_end);
         return;
     }
-    if constexpr (BF16 || (MEP_EPI_SPLIT && D <= 96) || (MEP_EPI_SPLIT128_BWD && D == 128)) {
-        constexpr int NPART = BF16 ? 1 : 3, NW = BF16 ? 1 : (D == 128 ? 2 : 3);
-        constexpr int BYTES = SplitW<2 * D, D / 32, NW>::BYTES;   // the larger phase (Wm^T)
-        __shared__ __attribute__((aligned(16))) unsigned char sm6[BYTES];
-        if (d.drop_p > 0.f) epi_bwd_split<D, NPART, NW, true>(bd, sm6, t_begin, t_end);
-        else epi_bwd_split<D, NPART, NW, false>(bd, sm6, t_begin, t_end);
-        return;
-    }
-    __shared__ __attribute__((aligned(16))) float smem[Geo::BWD];
-    lfloat* wmt = (lfloat*)&smem[0];              // Wm^T [2D][LP]
-    stage_cols_t<D, 2 * D>(wmt, Geo::LP, G<const float>(d.wm));
-    const WRows<lfloat> am{wmt, Geo::LP, 0, 0};
-    if constexpr (Geo::WP_LDS) {
-        lfloat* wpt = wmt + 2 * D * Geo::LP;      // Wp^T [D][LP]
-        stage_cols_t<D, D>(wpt, Geo::LP, G<const float>(d.wp));
-        __syncthreads();
-        epi_bwd_tiles<D>(bd, am, WRows<lfloat>{wpt, Geo::LP, 0, 0}, t_begin, t_end);
-    } else {
-        __syncthreads();
-        epi_bwd_tiles<D>(bd, am, WCols{G<const float>(d.wp), D, 0, 0}, t_begin, t_end);
-    }
+    constexpr int NPART = BF16 ? 1 : 3, NW = BF16 ? 1 : (D == 128 ? 2 : 3);
+    constexpr int BYTES = SplitW<2 * D, D / 32, NW>::BYTES;   // the larger phase (Wm^T)
+    __shared__ __attribute__((aligned(16))) unsigned char sm6[BYTES];
+    if (d.drop_p > 0.f) epi_bwd_split<D, NPART, NW, true>(bd, sm6, t_begin, t_end);
+    else epi_bwd_split<D, NPART, NW, false>(bd, sm6, t_begin, t_end);
 }
 
 // The bf16 epilogue forward at D = 96 with MEP_EPI_FWD_BF16_NW waves per workgroup (as below;
@@ -1427,92 +996,6 @@ __global__ __launch_bounds__(64 * EPI_BWD_BF16_NW) void k_epi_bwd_bf16w(const me
     else epi_bwd_one<96, 1, E::BWD_WP, E::BWD_WM, false, EPI_BWD_BF16_NW>(bd, sm1, t_begin, t_end);
 }
 
-// ---------------------------------------------------------------- weight images
-// mep_epi_images: the single-phase epilogues' LDS weight images, once per step.  Thread u of
-// descriptor blockIdx.y writes one 16-byte unit (all its parts) of the forward image (units 0 ..
-// FU-1: Wp then Wm, the staging order of epi_fwd_wp2r / epi_fwd_one) or of the backward image
-// (FU ..: Wm^T then Wp^T, epi_bwd_one's stage_split_cols), with the staging code's loads, split
-// and layout offsets -- the same bytes the workgroups would write into LDS.
-template <int D, bool BF16>
-struct EpiImg {
-    using E = EpiOne<D, BF16>;
-    static constexpr int NP = D / 32;
-    static constexpr int FU = E::FWD ? 3 * D * NP * 4 : 0, BU = E::BWD ? 3 * D * NP * 4 : 0;
-    static constexpr bool FWD_OK = E::FWD && E::FWD_BYTES % 1024 == 0;
-    static constexpr bool BWD_OK = E::BWD && E::BWD_BYTES % 1024 == 0;
-};
-
-template <typename L, int NPART>
-MEP_DEV void put_global(MEP_G unsigned char* img, int base, int n, int p, int g, f32x4 blk0, f32x4 blk1) {
-    const Parts<NPART> a = splitv<NPART>(blk0), b = splitv<NPART>(blk1);
-#pragma unroll
-    for (int t = 0; t < NPART; ++t)
-        *reinterpret_cast<MEP_G u32x4*>(img + base + L::off(t, n, p, g)) = u32x4{a.p[t][0], a.p[t][1], b.p[t][0], b.p[t][1]};
-}
-
-template <int D, bool BF16>
-__global__ __launch_bounds__(256) void k_epi_image(const mep_epi_bwd_desc* __restrict__ descs) {
-    using I = EpiImg<D, BF16>;
-    using E = typename I::E;
-    constexpr int NP = I::NP;
-    const mep_epi_bwd_desc& bd = descs[blockIdx.y];
-    const mep_epi_desc& d = bd.f;
-    int u = blockIdx.x * 256 + (int)threadIdx.x;
-    if (u < I::FU) {
-        if constexpr (I::FWD_OK) {
-            if (!d.image) return;
-            MEP_G unsigned char* img = G<unsigned char>(d.image);
-            const int wu = D * NP * 4;                 // Wp units; Wm units after them
-            const bool is_wp = u < wu;
-            const int v = is_wp ? u : u - wu, np2 = is_wp ? NP : 2 * NP, C = is_wp ? D : 2 * D;
-            const int gg = v & 3, pp = (v >> 2) % np2, n = (v >> 2) / np2;
-            const gfloat* src = G<const float>(is_wp ? d.wp : d.wm) + n * C + 32 * pp + 4 * gg;
-            const f32x4 b0 = ld4w(src), b1 = ld4w(src + 16);
-            if constexpr (E::FWD_WP2R) {
-                using W = EpiWp2r<D>;
-                if (is_wp) {
-                    const Parts<3> lo = splitv<3>(b0), hi = splitv<3>(b1);
-#pragma unroll
-                    for (int t = 0; t < 2; ++t)
-                        *reinterpret_cast<MEP_G u32x4*>(img + W::WP01::off(t, n, pp, gg)) =
-                            u32x4{lo.p[t][0], lo.p[t][1], hi.p[t][0], hi.p[t][1]};
-                    if (n < W::R2)
-                        *reinterpret_cast<MEP_G u32x4*>(img + W::WP01::BYTES + W::WP2::off(0, n, pp, gg)) =
-                            u32x4{lo.p[2][0], lo.p[2][1], hi.p[2][0], hi.p[2][1]};
-                } else {
-                    put_global<typename W::WM, 3>(img, W::WP01::BYTES + W::WP2::BYTES, n, pp, gg, b0, b1);
-                }
-            } else {
-                using WP = SplitW<D, NP, E::FWD_WP>;
-                using WM = SplitW<D, 2 * NP, E::FWD_WM>;
-                if (is_wp) put_global<WP, E::FWD_WP>(img, 0, n, pp, gg, b0, b1);
-                else put_global<WM, E::FWD_WM>(img, WP::BYTES, n, pp, gg, b0, b1);
-            }
-        }
-        return;
-    }
-    u -= I::FU;
-    if constexpr (I::BWD_OK) {
-        if (u >= I::BU || !bd.image) return;
-        MEP_G unsigned char* img = G<unsigned char>(bd.image);
-        using WMT = SplitW<2 * D, NP, E::BWD_WM>;
-        using WPT = SplitW<D, NP, E::BWD_WP>;
-        const int mu = 2 * D * NP * 4;                  // Wm^T units; Wp^T units after them
-        const bool is_wm = u < mu;
-        const int v = is_wm ? u : u - mu, C = is_wm ? 2 * D : D;
-        // stage_split_cols<D, C>: unit (n, pp, g) = W[32 pp + 4 g + j][n], W[32 pp + 16 + 4 g + j][n]
-        const int n = v % C, pg = v / C, gg = pg & 3, pp = pg >> 2;
-        const gfloat* src = G<const float>(is_wm ? d.wm : d.wp);
-        f32x4 b0, b1;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            b0[j] = src[(32 * pp + 4 * gg + j) * C + n];
-            b1[j] = src[(32 * pp + 16 + 4 * gg + j) * C + n];
-        }
-        if (is_wm) put_global<WMT, E::BWD_WM>(img, 0, n, pp, gg, b0, b1);
-        else put_global<WPT, E::BWD_WP>(img, WMT::BYTES, n, pp, gg, b0, b1);
-    }
-}
 
 // ---------------------------------------------------------------- row LayerNorm (D <= 256)
 // forward: a workgroup takes LNF_ROWS x 4 rows (row 4i + wave of its range for wave `wave`), every
@@ -1564,14 +1047,11 @@ MEP_DEV void ln_fwd_rows(const mep_ln_desc& d) {
     }
 }
 
-// 16 lanes per row (MEP_LN_Q; D <= 128, D % 8 == 0, 16-byte aligned rows): lane j of a 16-lane
+// 16 lanes per row (D <= 128, D % 8 == 0, 16-byte aligned rows): lane j of a 16-lane
 // group holds features 8j .. 8j+7 of its row -- one 16-byte access per row and lane (two on the fp32
 // path) instead of one 2- / 4-byte access per feature -- and the row sums are 16-lane DPP sums
 // (row16_sum), not wave sums: a wave takes 4 rows at once.  Same workgroup geometry as the rows
 // kernels above (forward 16 rows, backward 64 rows and one partial row per workgroup).
-#ifndef MEP_LN_Q
-#define MEP_LN_Q 1
-#endif
 typedef unsigned u32x4g __attribute__((ext_vector_type(4)));
 template <bool HS>
 MEP_DEV void ln_ld8(const mep_rows& r, int tok, int c0, float (&v)[8]) {
@@ -1608,7 +1088,7 @@ MEP_DEV bool ln_rows16(const mep_rows& r, bool hs) {
 }
 MEP_DEV bool ln_q_ok(const mep_ln_desc& d, bool fwd) {
     const bool hs = d.bf16 & MEP_BF16_STORE;
-    if (!MEP_LN_Q || d.D > 128 || d.D % 8 || d.w % 16 || d.b % 16 || !ln_rows16(d.x, hs)) return false;
+    if (d.D > 128 || d.D % 8 || d.w % 16 || d.b % 16 || !ln_rows16(d.x, hs)) return false;
     return fwd ? ln_rows16(d.y, hs) : (ln_rows16(d.dy, hs) && ln_rows16(d.dx, hs));
 }
 
@@ -1868,41 +1348,6 @@ extern "C" int mep_block_epi_bwd(const mep_epi_bwd_desc* descs, int n_desc, int 
     return mep_check_launch("mep_block_epi_bwd");
 }
 
-extern "C" int mep_epi_image_bytes(int D, int which) {
-    const bool bf16 = D & MEP_PREC_BF16;
-    int bytes = 0;
-    const int rc = dispatch_D(D & ~MEP_PREC_BF16, [&](auto dc) {
-        constexpr int DD = decltype(dc)::value;
-        auto get = [&](auto bc) {
-            using I = EpiImg<DD, decltype(bc)::value>;
-            using E = typename I::E;
-            bytes = which == 0 ? (I::FWD_OK ? E::FWD_BYTES : 0) : (I::BWD_OK ? E::BWD_BYTES : 0);
-        };
-        if (bf16) get(std::true_type{});
-        else get(std::false_type{});
-    });
-    return rc ? 0 : bytes;
-}
-
-extern "C" int mep_epi_images(const mep_epi_bwd_desc* descs, int n_desc, int D, mep_stream_t stream) {
-    if (n_desc <= 0) return 0;
-    const bool bf16 = D & MEP_PREC_BF16;
-    const int rc = dispatch_D(D & ~MEP_PREC_BF16, [&](auto dc) {
-        constexpr int DD = decltype(dc)::value;
-        auto go = [&](auto bc) {
-            constexpr bool BF = decltype(bc)::value;
-            using I = EpiImg<DD, BF>;
-            const int units = I::FU + I::BU;
-            if (units > 0)
-                hipLaunchKernelGGL((k_epi_image<DD, BF>), dim3((units + 255) / 256, n_desc), dim3(256), 0,
-                                   (hipStream_t)stream, descs);
-        };
-        if (bf16) go(std::true_type{});
-        else go(std::false_type{});
-    });
-    if (rc) { mep_set_error("mep_epi_images: D must be 32, 64, 96 or 128"); return rc; }
-    return mep_check_launch("mep_epi_images");
-}
 
 // max_tiles: forward = ceil(ntok / 4) (wave per row), backward = ceil(ntok / 64)
 extern "C" int mep_layernorm_fwd(const mep_ln_desc* descs, int n_desc, int max_tiles, mep_stream_t stream) {

@@ -72,9 +72,6 @@ MEP_DEV void st1a(ghalf* p, float v) { *p = (unsigned short)pk_bf16x2(v, 0.f); }
 // 64-bit multiplies are quarter rate, and an epilogue tile addresses ~8 views).  Needs strides
 // sB, sT < 2^24 elements and every view's element offsets < 2^32 (mep.h, mep_rows; the Python
 // hosts check both when they build a view).
-#ifndef MEP_ROW24
-#define MEP_ROW24 1
-#endif
 // (b, t) = (tok / T, tok % T), tok < 2^22, T < 2^24
 MEP_DEV void tok_split(int tok, int T, int& b, int& t) {
     b = (int)((float)tok * __builtin_amdgcn_rcpf((float)T));
@@ -84,17 +81,9 @@ MEP_DEV void tok_split(int tok, int T, int& b, int& t) {
 }
 MEP_DEV int64_t row_off(const mep_rows& r, int tok) {
     const int T = r.T;
-#if MEP_ROW24
     int b, t;
     tok_split(tok, T, b, t);
     return (int64_t)(uint32_t)(__umul24((unsigned)b, (unsigned)r.sB) + __umul24((unsigned)t, (unsigned)r.sT));
-#else
-    int b = (int)((float)tok * __builtin_amdgcn_rcpf((float)T));
-    int t = tok - b * T;
-    if (t < 0) { --b; t += T; }
-    if (t >= T) { ++b; t -= T; }
-    return (int64_t)b * r.sB + (int64_t)t * r.sT;
-#endif
 }
 MEP_DEV gfloat* row_ptr(const mep_rows& r, int tok) { return G<float>(r.ptr) + row_off(r, tok); }
 // row of an activation view in HS storage (element pointer: ld4a / st4a / ld1a / st1a)
@@ -106,10 +95,21 @@ MEP_DEV aelem<HS>* rowa(const mep_rows& r, int tok) {
 // ------------------------------------------------------------------ exact-rounding scalar ops
 // The residual-score sequence of the reference ((q.k)/sqrt(d) + c*S_prev - 1e8*(1-m)) is
 // evaluated with one rounding per op, no FMA contraction (masked slots sit at ~1e8 where
-// ulp = 8).
-MEP_DEV float add_rn(float a, float b) { return __fadd_rn(a, b); }
-MEP_DEV float sub_rn(float a, float b) { return __fsub_rn(a, b); }
-MEP_DEV float mul_rn(float a, float b) { return __fmul_rn(a, b); }
+// ulp = 8).  __fadd_rn / __fmul_rn do not stop hipcc from fusing a product into the
+// following sum (v_fmac_f32: one rounding fewer, a different grid value at ~1e8); the operations
+// below are compiled with contraction off, so they keep their own rounding after inlining.
+MEP_DEV float add_rn(float a, float b) {
+#pragma clang fp contract(off)
+    return a + b;
+}
+MEP_DEV float sub_rn(float a, float b) {
+#pragma clang fp contract(off)
+    return a - b;
+}
+MEP_DEV float mul_rn(float a, float b) {
+#pragma clang fp contract(off)
+    return a * b;
+}
 
 // ------------------------------------------------------------------ wave reductions (64 lanes)
 // DPP within each row of 16 lanes (quad butterflies xor 1 / xor 2, then the half-row and row
@@ -363,12 +363,8 @@ MEP_DEV void wave_lds_fence() {
 
 // weight operand of k block kb for output column block j:
 //   NT: W[n][k] = W[n * ldw + k] (nn.Linear weight, forward);  else W[k][n] = W[k * ldw + n]
-#ifndef MEP_EXP
-#define MEP_EXP 0
-#endif
 template <bool NT>
 MEP_DEV float4 wfrag(const gfloat* W, int ldw, int n, int k, bool w_vec) {
-    if (MEP_EXP & 16) return make_float4(1e-3f * n, 1e-3f * k, 0.f, 1.f);   // A/B: no weight loads
     if (NT) {
         const gfloat* p = W + (int64_t)n * ldw + k;
         if (w_vec) return ldg4(p);

@@ -159,9 +159,6 @@ __global__ __launch_bounds__(GEMM_THREADS) void k_gemm(const mep_gemm_desc* __re
 // column group; the four accumulator blocks are summed through LDS in a fixed order
 // ((w0 + w2) + (w1 + w3)) and written once as partial[split][n][k]; mep_wgrad_reduce sums the
 // splits.  Row views are addressed with 32-bit offsets (hosts keep every view under 2^31 floats).
-#ifndef MEP_WG_PARTS
-#define MEP_WG_PARTS 3   // bf16 parts per fp32 operand on the fp32 path (3: fp32-level)
-#endif
 // MEP_WG_OCC: k_wgrad workgroups per CU.  2: two waves per SIMD, each on a 32MT x 64 block (KT = 2
 // at MT = 3; <= 256 registers: no operand prefetch slot), so one wave's operand loads and split VALU overlap the other's
 // products; the LDS reduction buffers shrink to fit two workgroups.
@@ -202,9 +199,6 @@ __host__ __device__ constexpr int wg_kt(int mt, bool bf) {
 // byte extent of a row view's first ntok rows, `width` columns wide, es bytes per element (the
 // range the raw buffer loads check; hosts keep it under 2^31)
 MEP_DEV int wg_extent(const mep_rows& r, int T, int ntok, int width, int es = 4) {
-#ifdef MEP_WG_NOLOAD   // timing-only development build: every operand load returns 0 (compute time alone)
-    return 0;
-#endif
     const int64_t last = (int64_t)((ntok - 1) / T) * r.sB + (int64_t)((ntok - 1) % T) * r.sT + width;
     return (int)min((int64_t)es * last, (int64_t)0x7fffffff);
 }
@@ -215,18 +209,7 @@ constexpr int WG_INV = (int)0x80000000u;   // byte offset past every view: the b
 MEP_DEV bool wg_linear(const mep_rows& r) { return r.T == 1 || r.sB == (int64_t)r.T * r.sT; }
 MEP_DEV int wg_step(const mep_rows& r) { return (int)(r.T == 1 ? r.sB : r.sT); }
 
-#ifdef MEP_WG_TRACE
-// development build only (scripts/wgrad_trace.py): per-workgroup wall-clock stamps and hardware
-// ids, 8 words per workgroup: start, main loop start, main loop end, partial written, end, HW_ID,
-// XCC_ID, k blocks of wave 0
-__device__ unsigned long long* g_wg_trace;
-MEP_DEV void wg_stamp(int k, unsigned long long v) {
-    if (threadIdx.x == 0 && g_wg_trace) g_wg_trace[8 * blockIdx.x + k] = v;
-}
-#define MEP_WG_STAMP(k) wg_stamp(k, __builtin_amdgcn_s_memrealtime())
-#else
 #define MEP_WG_STAMP(k) ((void)0)
-#endif
 
 // LIN: every view of the item is linear in the token -- a lane's eight tokens of a k block sit at
 // fixed byte distances, so they are ONE per-lane base (VGPR) plus a wave-uniform per-token offset
@@ -347,22 +330,6 @@ MEP_DEV void wgrad_task(const mep_wgrad_desc& d, int t_begin, int t_end, int slo
         ++blk;
     };
     auto load = [&](int p) {
-#ifdef MEP_WG_NOLD    // timing-only development build: no operand loads (registers hold zeros)
-        if (blk == 0) {
-#pragma unroll
-            for (int q = 0; q < WG_SLOTS; ++q) {
-#pragma unroll
-                for (int e = 0; e < NE; ++e) {
-#pragma unroll
-                    for (int i = 0; i < MT; ++i) ra[q][i][e] = 0;
-#pragma unroll
-                    for (int j = 0; j < KT; ++j) rb[q][j][e] = 0;
-                }
-            }
-        }
-        ++blk;
-        return;
-#endif
         if constexpr (LIN) {
             if (8 * blk + 8 <= n - half) load_lin(p, false);   // every token of both halves valid
             else load_lin(p, true);
@@ -387,16 +354,6 @@ MEP_DEV void wgrad_task(const mep_wgrad_desc& d, int t_begin, int t_end, int slo
         }
     };
     auto mma = [&](int p) {
-#ifdef MEP_WG_NOMMA   // timing-only development build: loads kept live by one add each, no products
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-#pragma unroll
-            for (int i = 0; i < MT; ++i) acc[i][0][e] += ra[p][i][e];
-#pragma unroll
-            for (int j = 0; j < KT; ++j) acc[0][j][8 + e] += rb[p][j][e];
-        }
-        return;
-#endif
         OpN<NPART> bo[KT];
         auto op = [&](const RT (&v)[NE]) -> OpN<NPART> {
             if constexpr (HS) {
@@ -422,9 +379,6 @@ MEP_DEV void wgrad_task(const mep_wgrad_desc& d, int t_begin, int t_end, int slo
         }
     };
     MEP_WG_STAMP(1);
-#ifdef MEP_WG_TRACE
-    wg_stamp(7, nblk);
-#endif
     if (nblk > 0) {
         // blocks 0 .. S-2 go to slots 0 .. S-2; step s loads block s + S - 1 into the slot that
         // step s - 1 consumed, then runs the MFMAs of block s
@@ -439,11 +393,7 @@ MEP_DEV void wgrad_task(const mep_wgrad_desc& d, int t_begin, int t_end, int slo
             for (; s0 + WG_SLOTS <= nblk && s0 + 2 * WG_SLOTS - 2 < nfast; s0 += WG_SLOTS) {
 #pragma unroll
                 for (int p = 0; p < WG_SLOTS; ++p) {
-#ifdef MEP_WG_NOLD
-                    load((p + WG_SLOTS - 1) % WG_SLOTS);
-#else
                     load_lin((p + WG_SLOTS - 1) % WG_SLOTS, false);
-#endif
                     __builtin_amdgcn_sched_barrier(0);
                     mma(p);
                 }
@@ -519,9 +469,6 @@ MEP_DEV void wg_nan_partial(const mep_wgrad_desc& d, int slot) {
 // gets NaN partials (loudly wrong, never silently)
 template <bool BF>
 __global__ __launch_bounds__(WG_THREADS) __attribute__((amdgpu_waves_per_eu(wg_occ(BF)))) void k_wgrad(const mep_wgrad_desc* __restrict__ descs, int n_desc, int n_wg) {
-#ifdef MEP_WG_TRACE
-    const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
-#endif
     const int* map = reinterpret_cast<const int*>(descs + n_desc);
     const int s0 = map[blockIdx.x], s1 = map[blockIdx.x + 1];
     const int* seg = map + n_wg + 1;
@@ -541,8 +488,8 @@ __global__ __launch_bounds__(WG_THREADS) __attribute__((amdgpu_waves_per_eu(wg_o
 #define MEP_WGT(M, K)                                                                          \
         case 8 * M + K:                                                                        \
             if constexpr (K > wg_kt(M, BF)) break;   /* not a tile block of this instance */   \
-            if (lin) wgrad_task<M, K, BF ? 1 : MEP_WG_PARTS, true, BF ? WG_SLOTS_B : WG_SLOTS_F>(d, t_begin, t_end, slot, kbase, red);  \
-            else if constexpr (!BF) wgrad_task<M, K, MEP_WG_PARTS, false, WG_SLOTS_F>(d, t_begin, t_end, slot, kbase, red);         \
+            if (lin) wgrad_task<M, K, BF ? 1 : 3, true, BF ? WG_SLOTS_B : WG_SLOTS_F>(d, t_begin, t_end, slot, kbase, red);  \
+            else if constexpr (!BF) wgrad_task<M, K, 3, false, WG_SLOTS_F>(d, t_begin, t_end, slot, kbase, red);         \
             else wg_nan_partial(d, slot);   /* bf16 rows: linear views only */                                                       \
             break;
         // the bf16-path instance needs bf16 operands AND bf16 operand rows (MEP_BF16_OPS | MEP_BF16_STORE)
@@ -559,246 +506,8 @@ __global__ __launch_bounds__(WG_THREADS) __attribute__((amdgpu_waves_per_eu(wg_o
         }
 #undef MEP_WGT
     }
-#ifdef MEP_WG_TRACE
-    __syncthreads();
-    if (threadIdx.x == 0 && g_wg_trace) {
-        const unsigned long long t_end = __builtin_amdgcn_s_memrealtime();
-        const unsigned hw = __builtin_amdgcn_s_getreg((31 << 11) | 4), xcc = __builtin_amdgcn_s_getreg((31 << 11) | 20);
-        unsigned long long* o = g_wg_trace + 8 * blockIdx.x;
-        o[0] = t_start;
-        o[4] = t_end;
-        o[5] = hw;
-        o[6] = xcc;
-    }
-#endif
 }
 
-#ifdef MEP_WG_TRACE
-extern "C" int mep_wgrad_set_trace(void* p) {
-    return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_wg_trace), &p, sizeof(p));
-}
-#endif
-
-// ---------------------------------------------------------------- LDS-staged weight gradient
-// Same segments, partial slots and reduction as k_wgrad (round 3, MEP_WGRAD_LDS): a workgroup
-// walks its token range in chunks of LT = 32 tokens.  Every chunk of A [tok][N] and of the column
-// group's B [tok][32 kt] is loaded with 16-byte row loads (coalesced), split once into its bf16
-// parts in registers and written to LDS as row-major [token][column] images (one per part, rows
-// padded to L = 32 / 96 / 160 columns: the transposed reads below are then bank-conflict free);
-// the MFMA operands -- 8 consecutive tokens of one column -- come back with two
-// ds_read_b64_tr_b16 per part.  Each wave owns whole 32x32 output tiles of the block (no
-// cross-wave reduction), so it needs ~50 accumulator registers instead of ~150, and the chunk
-// loads run PD chunks ahead of the products in registers (double-buffered images, one barrier
-// per chunk).
-#ifndef MEP_WGRAD_LDS
-#define MEP_WGRAD_LDS 0   // measured slower at cfg3: 95 vs 47 us (per-chunk image write + barrier + address
-                          // work dominate 36 MFMAs per wave per chunk; prefetch depth 1-3 made no difference)
-#endif
-#ifndef MEP_WGL_PD
-#define MEP_WGL_PD 2   // token chunks loaded ahead of the one being multiplied
-#endif
-constexpr int WGL_LT = 32;              // tokens per chunk
-MEP_DEV constexpr int wgl_pad(int c) { return c <= 32 ? 32 : c <= 96 ? 96 : 160; }   // L mod 128 in {32, 96}
-constexpr int WGL_IMG = WGL_LT * 160;   // bf16 elements of the largest image
-typedef short s16x4w __attribute__((ext_vector_type(4)));
-typedef __attribute__((address_space(3))) s16x4w ls16x4w;
-
-// Per thread: 8 float4 units u = threadIdx.x + 256 k of a chunk ([A units | B units], row-major in
-// the chunk).  A unit's column (and with it its row view) is the same in every chunk, so its
-// column base and strides are computed once per segment; every chunk then issues exactly 8
-// loads per thread with no branches (invalid units read a valid address and are zeroed), so the
-// compiler's wait counts stay exact and the next chunks' loads stay in flight across the products.
-struct WglUnit {
-    uint64_t base;   // byte address of (token 0 of the view, the unit's column); 0: never valid
-    int sB, sT;      // byte strides
-    int row, lim;    // row in the chunk; columns left in its operand row (>= 4: one 16-byte load)
-};
-
-template <int NPART, bool VEC>
-MEP_DEV void wgl_task(const mep_wgrad_desc& d, int t_begin, int t_end, int slot, int kbase, int mt, int kt,
-                      unsigned short* img) {
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int N = d.N;
-    t_end = min(d.ntok, t_end);
-    const int ntk = max(0, t_end - t_begin);
-    const int nch = (ntk + WGL_LT - 1) / WGL_LT;
-    const int LA = wgl_pad(32 * mt), LB = wgl_pad(32 * kt);
-    const int ua = WGL_LT * (32 * mt) / 4, ub = WGL_LT * (32 * kt) / 4;   // float4 units of A and B per chunk
-    const int nunit = ua + ub;
-    const int T = d.a.T;
-    constexpr int IMGS = 2 * WGL_IMG;         // one part: A image + B image
-    WglUnit un[8];
-    int woff[8];                              // element offset of the unit in its part's image
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-        const int u = threadIdx.x + 256 * k;
-        const bool isa = u < ua;
-        const int w4 = isa ? 8 * mt : 8 * kt;
-        const int uu = isa ? u : u - ua;
-        const int row = uu / w4, c = 4 * (uu - row * w4);
-        WglUnit x{0, 0, 0, row, 0};
-        woff[k] = (isa ? 0 : WGL_IMG) + row * (isa ? LA : LB) + c;
-        if (u < nunit) {
-            if (isa) {
-                if (c < N) x = WglUnit{d.a.ptr + 4ull * c, 4 * (int)d.a.sB, 4 * (int)d.a.sT, row, N - c};
-            } else {
-                int kc = kbase + c, o = 0;
-                if (kc < d.Ktot) {
-                    while (o < d.n_b - 1 && kc >= d.kb[o]) { kc -= d.kb[o]; ++o; }
-                    const mep_rows& bv = d.b[o];
-                    x = WglUnit{bv.ptr + 4ull * kc, 4 * (int)bv.sB, 4 * (int)bv.sT, row, d.kb[o] - kc};
-                }
-            }
-        } else {
-            woff[k] = -1;
-        }
-        un[k] = x;
-    }
-    const uint64_t dummy = d.a.ptr;
-    auto load_chunk = [&](f32x4 (&r)[8], int ch) {
-        const int t0 = t_begin + ch * WGL_LT;
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            const int t = t0 + un[k].row;
-            const bool ok = un[k].base != 0 && t < t_end;
-            const int bq = (int)((float)t * __builtin_amdgcn_rcpf((float)T));   // t / T, corrected below
-            int b = bq, tt = t - bq * T;
-            if (tt < 0) { --b; tt += T; }
-            if (tt >= T) { ++b; tt -= T; }
-            const uint64_t addr = ok ? un[k].base + (int64_t)b * un[k].sB + (int64_t)tt * un[k].sT : dummy;
-            const MEP_G float* p = reinterpret_cast<const MEP_G float*>(addr);
-            f32x4 v;
-            if constexpr (VEC) {
-                v = *reinterpret_cast<const MEP_G f32x4*>(p);
-            } else {
-#pragma unroll
-                for (int e = 0; e < 4; ++e) v[e] = p[e < un[k].lim ? e : 0];
-                const int lim = un[k].lim;
-#pragma unroll
-                for (int e = 0; e < 4; ++e) v[e] = e < lim ? v[e] : 0.f;
-            }
-            r[k] = ok ? v : f32x4{0.f, 0.f, 0.f, 0.f};
-        }
-    };
-    // split the raw units into NPART bf16 parts: row-major images [part][token][L]
-    auto write_chunk = [&](const f32x4 (&r)[8], int buf) {
-        unsigned short* base = img + buf * NPART * IMGS;
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            if (woff[k] >= 0) {
-                const Parts<NPART> pr = splitv<NPART>(r[k]);
-#pragma unroll
-                for (int t = 0; t < NPART; ++t)
-                    *reinterpret_cast<__attribute__((address_space(3))) u32x2*>(
-                        (__attribute__((address_space(3))) unsigned short*)(base + t * IMGS + woff[k])) = pr.p[t];
-            }
-        }
-    };
-    // the operand of 32 image columns m0 .. m0+31 x 16 tokens kb*16 ..: two transposed reads per part
-    const int grp = lane >> 4, q = (lane >> 2) & 3, pp = lane & 3;
-    auto frag = [&](const unsigned short* im, int L, int m0, int kb) {
-        OpN<NPART> o;
-        const int row = kb * 16 + 8 * (grp >> 1) + q, col = m0 + 16 * (grp & 1) + 4 * pp;
-#pragma unroll
-        for (int t = 0; t < NPART; ++t) {
-            const unsigned short* e = im + t * IMGS + row * L + col;
-            const u32x2 lo = __builtin_bit_cast(u32x2, __builtin_amdgcn_ds_read_tr16_b64_v4i16((ls16x4w*)(e)));
-            const u32x2 hi = __builtin_bit_cast(u32x2, __builtin_amdgcn_ds_read_tr16_b64_v4i16((ls16x4w*)(e + 4 * L)));
-            o.p[t] = __builtin_bit_cast(bf16x8, u32x4{lo[0], lo[1], hi[0], hi[1]});
-        }
-        return o;
-    };
-    const int ntile = mt * kt;
-    floatx16 acc[3];
-#pragma unroll
-    for (int j = 0; j < 3; ++j)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
-    auto compute = [&](int buf) {
-        const unsigned short* cur = img + buf * NPART * IMGS;
-#pragma unroll
-        for (int j = 0; j < 3; ++j) {
-            const int qt = wave + 4 * j;
-            if (qt < ntile) {   // wave-uniform: EXEC stays full for the transposed reads
-                const int ti = qt / kt, tj = qt - (qt / kt) * kt;
-#pragma unroll
-                for (int kb = 0; kb < WGL_LT / 16; ++kb) {
-                    const OpN<NPART> a = frag(cur, LA, 32 * ti, kb);
-                    const OpN<NPART> b = frag(cur + WGL_IMG, LB, 32 * tj, kb);
-                    acc[j] = mma_n<NPART>(a, b, acc[j]);
-                }
-            }
-        }
-    };
-    constexpr int PD = MEP_WGL_PD;
-    f32x4 raw[PD][8];
-#pragma unroll
-    for (int s2 = 0; s2 < PD; ++s2) load_chunk(raw[s2], min(s2, max(nch - 1, 0)));
-    if (nch > 0) write_chunk(raw[0], 0);
-    __syncthreads();
-    // chunk ch: refill its register set with chunk ch + PD (clamped: the tail reloads the last
-    // chunk), multiply image ch & 1, write chunk ch + 1 into the other image, one barrier
-    for (int ch0 = 0; ch0 < nch; ch0 += PD) {
-#pragma unroll
-        for (int s2 = 0; s2 < PD; ++s2) {
-            const int ch = ch0 + s2;
-            if (ch >= nch) break;
-            load_chunk(raw[s2], min(ch + PD, nch - 1));
-            compute(ch & 1);
-            write_chunk(raw[(s2 + 1) % PD], (ch + 1) & 1);
-            __syncthreads();
-        }
-    }
-    // each wave writes its own tiles: partial[slot][n][kbase + k]
-    gfloat* part = G<float>(d.partial) + (int64_t)slot * N * d.Ktot + kbase;
-    const int kcnt = min(32 * kt, d.Ktot - kbase);
-#pragma unroll
-    for (int j = 0; j < 3; ++j) {
-        const int qt = wave + 4 * j;
-        if (qt < ntile) {
-            const int ti = qt / kt, tj = qt - (qt / kt) * kt;
-            const int k = 32 * tj + (lane & 31);
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int n = 32 * ti + acc_row(r, lane);
-                if (n < N && k < kcnt) part[(int64_t)n * d.Ktot + k] = acc[j][r];
-            }
-        }
-    }
-}
-
-// 16-byte loads for every unit: N, every operand width and every row view on 4-float boundaries
-MEP_DEV bool wgl_vec(const mep_wgrad_desc& d) {
-    auto al = [](const mep_rows& r) { return (r.ptr & 15) == 0 && r.sB % 4 == 0 && r.sT % 4 == 0; };
-    bool v = d.N % 4 == 0 && al(d.a);
-    for (int o = 0; o < d.n_b; ++o) v = v && d.kb[o] % 4 == 0 && al(d.b[o]);
-    return v;
-}
-
-__global__ __launch_bounds__(WG_THREADS, 1) void k_wgrad_lds(const mep_wgrad_desc* __restrict__ descs, int n_desc, int n_wg) {
-    const int* map = reinterpret_cast<const int*>(descs + n_desc);
-    const int s0 = map[blockIdx.x], s1 = map[blockIdx.x + 1];
-    const int* seg = map + n_wg + 1;
-    __shared__ __attribute__((aligned(16))) unsigned short img[2 * 3 * 2 * WGL_IMG];
-    for (int si = s0; si < s1; ++si) {
-        const int hdr = seg[4 * si], t_begin = seg[4 * si + 1], t_end = seg[4 * si + 2], slot = seg[4 * si + 3];
-        const mep_wgrad_desc& d = descs[hdr >> 8];
-        const int cg = hdr & 0xff;
-        const int mt = (d.N + 31) >> 5, ktm = wg_kt(mt, d.bf16);
-        const int ktiles = (d.Ktot + 31) >> 5;
-        const int kt = min(ktm, ktiles - cg * ktm);
-        const int kbase = 32 * ktm * cg;
-        if (si > s0) __syncthreads();   // the previous segment's last chunk has been read
-        const bool vec = wgl_vec(d);
-        if (d.bf16) {
-            if (vec) wgl_task<1, true>(d, t_begin, t_end, slot, kbase, mt, kt, img);
-            else wgl_task<1, false>(d, t_begin, t_end, slot, kbase, mt, kt, img);
-        } else {
-            if (vec) wgl_task<MEP_WG_PARTS, true>(d, t_begin, t_end, slot, kbase, mt, kt, img);
-            else wgl_task<MEP_WG_PARTS, false>(d, t_begin, t_end, slot, kbase, mt, kt, img);
-        }
-    }
-}
 
 __global__ __launch_bounds__(256) void k_wgrad_reduce(const mep_wgrad_desc* __restrict__ descs) {
     wgrad_reduce_block(descs[blockIdx.y], blockIdx.x);
@@ -818,9 +527,6 @@ constexpr int UN_WAVES = 8;
 constexpr int UN_THREADS = 64 * UN_WAVES;
 constexpr int UN_LDS = 30720;   // floats (120 KB): W [N][Kp + 8] when N * (Kp + 8) fits
 constexpr int UN_PF = 8;        // X fragments (k blocks) in flight per lane
-#ifndef MEP_UN_STAGE1
-#define MEP_UN_STAGE1 1         // the whole weight's loads in flight per 320-column pass (0: 4 rows at a time, 18.0 vs 16.5 us at cfg3)
-#endif
 
 template <int NIP, bool WL, bool XV>
 MEP_DEV void unify_tasks(const mep_gemm_desc& d, const lfloat* wl, int ldl, int tile_lo, int tile_hi, int np) {
@@ -1114,7 +820,6 @@ __global__ __launch_bounds__(UN_THREADS) void k_unify(const mep_gemm_desc* __res
     const int N = d.N, K = d.K, KB = (K + 15) >> 4, ldl = 16 * KB + 8;
     const bool wlds = N * ldl <= UN_LDS;
     if (wlds) {   // W [N][K] -> LDS rows of ldl floats, zero past K
-#if MEP_UN_STAGE1
         // wave w stages rows w, w + 8, ... (N <= 128: 16 rows per wave), 320 columns per pass:
         // every load of a pass in flight at once through a range-checked buffer resource (rows
         // past N / columns past K read 0, no branches), then the LDS writes
@@ -1138,30 +843,6 @@ __global__ __launch_bounds__(UN_THREADS) void k_unify(const mep_gemm_desc* __res
                     if (n < N && k < KP) wl[n * ldl + k] = v[r][j];
                 }
         }
-#else
-        // wave w stages rows w, w + 8, ...; 4 rows x 320 columns of loads in flight per batch
-        const gfloat* W = G<const float>(d.w);
-        const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, KP = 16 * KB;
-        for (int n0 = wave; n0 < N; n0 += 4 * UN_WAVES) {
-            for (int k0 = 0; k0 < KP; k0 += 320) {
-                float v[4][5];
-#pragma unroll
-                for (int r = 0; r < 4; ++r)
-#pragma unroll
-                    for (int j = 0; j < 5; ++j) {
-                        const int n = n0 + UN_WAVES * r, k = k0 + lane + 64 * j;
-                        v[r][j] = (n < N && k < K) ? W[(int64_t)n * d.ldw + k] : 0.f;
-                    }
-#pragma unroll
-                for (int r = 0; r < 4; ++r)
-#pragma unroll
-                    for (int j = 0; j < 5; ++j) {
-                        const int n = n0 + UN_WAVES * r, k = k0 + lane + 64 * j;
-                        if (n < N && k < KP) wl[n * ldl + k] = v[r][j];
-                    }
-            }
-        }
-#endif
         __syncthreads();
     }
 #define MEP_UN(NIP)                                                                          \
@@ -1188,14 +869,10 @@ extern "C" int mep_wgrad_occupancy(int bf16) { return wg_occ(bf16 != 0); }
 
 extern "C" int mep_wgrad(const mep_wgrad_desc* descs, int n_desc, int max_tiles, int flags, mep_stream_t stream) {
     if (n_desc <= 0 || max_tiles <= 0) return 0;
-#if MEP_WGRAD_LDS
-    hipLaunchKernelGGL(k_wgrad_lds, dim3(max_tiles), dim3(WG_THREADS), 0, (hipStream_t)stream, descs, n_desc, max_tiles);
-#else
     if (flags & MEP_PREC_BF16)
         hipLaunchKernelGGL(k_wgrad<true>, dim3(max_tiles), dim3(WG_THREADS), 0, (hipStream_t)stream, descs, n_desc, max_tiles);
     else
         hipLaunchKernelGGL(k_wgrad<false>, dim3(max_tiles), dim3(WG_THREADS), 0, (hipStream_t)stream, descs, n_desc, max_tiles);
-#endif
     return mep_check_launch("mep_wgrad");
 }
 

@@ -131,26 +131,14 @@ MEP_DEV void wave_sync() {
 MEP_DEV float log_sigmoid(float x) { return fminf(x, 0.f) - log1pf(__expf(-fabsf(x))); }
 
 
-#ifdef MEP_HEAD_TRACE   // development only: phase timestamps of block 0 / the last block (printf)
-#define HT(i) do { if (threadIdx.x == 0) ht_clk[i] = wall_clock64(); } while (0)
-#define HT_PRINT() do { if (threadIdx.x == 0 && (blockIdx.x == 0 || blockIdx.x == gridDim.x - 1)) \
-    printf("head blk %d: %lld %lld %lld %lld %lld %lld | %lld %lld %lld (x10ns)\n", (int)blockIdx.x, \
-           ht_clk[1] - ht_clk[0], ht_clk[2] - ht_clk[1], ht_clk[3] - ht_clk[2], ht_clk[4] - ht_clk[3], \
-           ht_clk[5] - ht_clk[4], ht_clk[6] - ht_clk[5], ht_clk[7] - ht_clk[3], ht_clk[8] - ht_clk[7], \
-           ht_clk[9] - ht_clk[8]); } while (0)
-#else
 #define HT(i) do { } while (0)
 #define HT_PRINT() do { } while (0)
-#endif
 // NCT: the class count as a compile-time constant (7 cmu-mosei, 9 Ren-MME; 0 = runtime, <= NCMAX):
 // exact unrolls, constant index arithmetic and a small code footprint (each workgroup runs the
 // kernel body once, so instruction fetch is on the critical path)
 template <int NCT>
 __global__ __launch_bounds__(256) void k_head(mep_head_desc d) {
     constexpr int NU = NCT ? NCT : NCMAX;
-#ifdef MEP_HEAD_TRACE
-    long long ht_clk[12];
-#endif
     HT(0);
     const int rows = d.rdrop ? 2 : 1;
     const int r0 = blockIdx.x * rows;

@@ -13,11 +13,6 @@
 
 using namespace mep;
 
-#ifndef MEP_RF_SPLIT
-#define MEP_RF_SPLIT 0   // 1: the Linears on split-bf16 MFMA (split.h mma_tile_split) -- measured no faster
-                         // (cfg2 epilogues 69 / 66 vs 69 / 69 us: not MFMA-bound) and one rf_chain_cfg2
-                         // output element moved 3.5e-4 relative; 0: f32 MFMA 32x32x2 (exact fp32 products)
-#endif
 
 namespace {
 
@@ -36,14 +31,7 @@ MEP_DEV void tile_gemm(const float* As, int lda, const gfloat* W, int ldw, bool 
     for (int t = wave; t < NTASK; t += NWAVE) {
         const int mh = t % MH, nblk = t / MH;
         floatx16 acc = zero16();
-        if constexpr (MEP_RF_SPLIT && K % 16 == 0 && (K <= 128 || (K / 2) % 16 == 0)) {
-            if constexpr (K <= 128) {
-                mma_tile_split<NT, K>(acc, As, lda, mh * 32, W, ldw, nblk * 32, N, 0, K, w_vec);
-            } else {
-                mma_tile_split<NT, K / 2>(acc, As, lda, mh * 32, W, ldw, nblk * 32, N, 0, K, w_vec);
-                mma_tile_split<NT, K / 2>(acc, As + K / 2, lda, mh * 32, W, ldw, nblk * 32, N, K / 2, K, w_vec);
-            }
-        } else if constexpr (K <= 128) {
+        if constexpr (K <= 128) {
             mma_tile_pf<NT, K>(acc, As, lda, mh * 32, W, ldw, nblk * 32, N, 0, K, w_vec);
         } else {   // two halves: at most 64 prefetch registers per pass
             mma_tile_pf<NT, K / 2>(acc, As, lda, mh * 32, W, ldw, nblk * 32, N, 0, K, w_vec);

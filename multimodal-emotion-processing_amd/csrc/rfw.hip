@@ -39,13 +39,7 @@ using namespace mep;
 
 namespace {
 
-#ifdef MEP_RFW_TRACE
-// development build only (scripts/rfw_trace.py): per-workgroup shader-clock stamps of wave 0
-__device__ unsigned long long* g_rfw_trace;
-#define MEP_RFW_STAMP(k) do { if (threadIdx.x == 0 && g_rfw_trace) g_rfw_trace[16 * blockIdx.x + (k)] = __builtin_amdgcn_s_memtime(); } while (0)
-#else
 #define MEP_RFW_STAMP(k) ((void)0)
-#endif
 
 constexpr float LN_EPS = 1e-5f;
 typedef const MEP_G u32x4* PartPtr;
@@ -167,14 +161,8 @@ struct PG {
         const int p = s / NJ, i = wave + W * (s - (s / NJ) * NJ);
         const int ic = i < NI ? i : NI - 1;   // a wave without this tile loads a valid fragment it never uses
         OpN<3> o;
-#ifdef MEP_RFW_NOW   // timing-only development build: no weight loads (constant fragments)
-        (void)ic; (void)p;
-#pragma unroll
-        for (int t = 0; t < 3; ++t) o.p[t] = __builtin_bit_cast(bf16x8, u32x4{threadIdx.x, 0u, (unsigned)t, 0u});
-#else
 #pragma unroll
         for (int t = 0; t < 3; ++t) o.p[t] = __builtin_bit_cast(bf16x8, wl[((t * R + 16 * ic) * NPK + p) * 4]);
-#endif
         return o;
     }
     MEP_DEV void prime(PartPtr w, int wave_) {
@@ -217,9 +205,6 @@ MEP_DEV void xchg(f32x4 (&full)[NB], const f32x4 (&mine)[(NB + W - 1) / W], xf32
 // the wave's tiles of a full row block: store / per-tile transform helpers
 template <int NB, int W>
 MEP_DEV void store_owned(const mep_rows& r, int tok, const f32x4 (&v)[NB], int wave) {
-#ifdef MEP_RFW_NOST   // timing-only development build: no stores of intermediates
-    return;
-#endif
     const int g = (threadIdx.x >> 4) & 3;
     gfloat* p = row_ptr(r, tok) + 4 * g;
 #pragma unroll
@@ -228,9 +213,6 @@ MEP_DEV void store_owned(const mep_rows& r, int tok, const f32x4 (&v)[NB], int w
 }
 template <int NB, int W>
 MEP_DEV void store_mine(const mep_rows& r, int tok, const f32x4 (&v)[(NB + W - 1) / W], int wave) {
-#ifdef MEP_RFW_NOST
-    return;
-#endif
     const int g = (threadIdx.x >> 4) & 3;
     gfloat* p = row_ptr(r, tok) + 4 * g;
 #pragma unroll
@@ -440,15 +422,6 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(WPE))) v
         }
     }
     MEP_RFW_STAMP(9);
-#ifdef MEP_RFW_TRACE
-    if (threadIdx.x == 0 && g_rfw_trace) {
-        __builtin_amdgcn_s_waitcnt(0);
-        g_rfw_trace[16 * blockIdx.x + 10] = __builtin_amdgcn_s_memtime();
-        g_rfw_trace[16 * blockIdx.x + 11] = __builtin_amdgcn_s_getreg((31 << 11) | 4);    // HW_ID
-        g_rfw_trace[16 * blockIdx.x + 12] = __builtin_amdgcn_s_getreg((31 << 11) | 20);   // XCC_ID
-        g_rfw_trace[16 * blockIdx.x + 13] = __builtin_amdgcn_s_memrealtime();
-    }
-#endif
 }
 
 // ---------------------------------------------------------------- RealFormer epilogue backward
@@ -461,11 +434,7 @@ MEP_DEV void tile_colsum(gfloat* dst, const f32x4 (&v)[NB], int wave, int c, int
         f32x4 s;
 #pragma unroll
         for (int r = 0; r < 4; ++r) s[r] = row16_sum(v[i][r]);
-#ifdef MEP_RFW_NOST
-        if (c == 0 && s[0] == 12345.f) {
-#else
         if (c == 0) {   // partial rows are 4-byte aligned only (stride 5D + FD + 2)
-#endif
 #pragma unroll
             for (int r = 0; r < 4; ++r) dst[16 * i + 4 * g + r] = s[r];
         }
@@ -1191,11 +1160,6 @@ int dispatch_rfw(int D, int FD, F&& f) {
 
 }  // namespace
 
-#ifdef MEP_RFW_TRACE
-extern "C" int mep_rfw_set_trace(void* p) {
-    return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_rfw_trace), &p, sizeof(p));
-}
-#endif
 
 extern "C" int mep_rf_rows(int which, int D) {
     return which == 2 ? 16 : which == 1 ? MEP_RF_BWD_ROWS_BUILT : (D > 128 ? 32 : MEP_RF_FWD_ROWS_BUILT);

@@ -220,49 +220,4 @@ MEP_DEV void tgemm_n(f32x4 (&acc)[NI], AF&& afr, BF&& bfr) {
     }
 }
 
-// mma_tile_pf (common.h) on the bf16 matrix cores: C[32 x 32] += A_lds[m0.., k0..k0+KC) W(n0.., ..)
-// with both operands split into three bf16 parts (six products per 16-wide k block, fp32-level).
-// The operands are the fragments mma_tile_pf loads (lane (r, h): k 8i + 4h .. +3 of 8-step i);
-// the 16-wide block p takes steps 2p (slots 0-3) and 2p + 1 (slots 4-7) on
-// v_mfma_f32_32x32x16_bf16 -- A and B agree on the slots, the accumulator layout is the one of
-// the 32x32x2 f32 form: 192 MFMA cycles per k block against 512.
-template <bool NT, int KC>
-MEP_DEV void mma_tile_split(floatx16& acc, const float* __restrict__ As, int lda, int m0,
-                            const gfloat* __restrict__ W, int ldw, int n0, int N, int k0, int K, bool w_vec) {
-    static_assert(KC % 16 == 0, "split tiles need KC % 16 == 0");
-    constexpr int NS = KC / 8;
-    const int lane = threadIdx.x & 63;
-    const int r = lane & 31;
-    const int h = lane >> 5;
-    const float* arow = As + (m0 + r) * lda + 4 * h;
-    const int n = n0 + r;
-    const bool nval = n < N;
-    f32x4 b[NS];
-#pragma unroll
-    for (int i = 0; i < NS; ++i) {
-        const int kg = k0 + 8 * i + 4 * h;
-        f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
-        if (NT) {
-            const gfloat* wp = W + (int64_t)n * ldw + kg;
-            if (nval && w_vec && kg + 3 < K) {
-                v = *reinterpret_cast<const MEP_G f32x4*>(wp);
-            } else if (nval) {
-#pragma unroll
-                for (int e = 0; e < 4; ++e) if (kg + e < K) v[e] = wp[e];
-            }
-        } else if (nval) {
-            const gfloat* wp = W + (int64_t)kg * ldw + n;
-#pragma unroll
-            for (int e = 0; e < 4; ++e) if (kg + e < K) v[e] = wp[(int64_t)e * ldw];
-        }
-        b[i] = v;
-    }
-#pragma unroll
-    for (int p = 0; p < NS / 2; ++p) {
-        const f32x4 a0 = *reinterpret_cast<const f32x4*>(arow + 16 * p);
-        const f32x4 a1 = *reinterpret_cast<const f32x4*>(arow + 16 * p + 8);
-        acc = mma_n<3>(opn<3>(a0, a1), opn<3>(b[2 * p], b[2 * p + 1]), acc);
-    }
-}
-
 }  // namespace mep

@@ -422,148 +422,6 @@ MEP_DEV void tgemm_dma(const mep_gemm_desc* __restrict__ descs) {
 MEP_TGB_K(2) MEP_TGB_K(4) MEP_TGB_K(6) MEP_TGB_K(8)
 #undef MEP_TGB_K
 
-// Resident-weight variant for K <= 32 * TGR_KP (the cmu-mosei unify, K <= 300, and the realformer
-// Linears, K <= 192): the workgroup's whole N tile of W (BN <= 96 rows) is staged in LDS ONCE, as
-// NW bf16 parts (NW = 2 on the fp32 path: 3 parts of a 96 x 320 tile would need 184 KB; the
-// weight's representation error is then <= 2^-18 relative, five products per k pair), and the
-// waves run their token tiles through all k pairs with no barrier -- the per-chunk staging
-// latency of k_tgemm is paid once.  X k pairs are loaded one pair ahead of their MFMAs.
-constexpr int TGR_KP = 10;
-
-template <int NI, int NPART, int NW, bool WNT>
-__global__ __launch_bounds__(TG_THREADS) void k_tgemm_res(const mep_gemm_desc* __restrict__ descs) {
-    constexpr int BN = 16 * NI;
-    using WS = SplitW<BN, TGR_KP, NW>;
-    __shared__ __attribute__((aligned(16))) unsigned char sm[WS::BYTES];
-    const mep_gemm_desc& d = descs[blockIdx.y];
-    const int n0 = (int)blockIdx.z * BN;
-    const int tok0 = (int)blockIdx.x * TG_BM;
-    if (n0 >= d.N || tok0 >= d.ntok) return;            // the whole workgroup
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int c = lane & 15, g = lane >> 4;
-    const int K = d.K, N = d.N, ntok = d.ntok;
-    const int nkp = (K + 31) >> 5;                        // <= TGR_KP (host)
-    typedef __attribute__((address_space(3))) unsigned char lbyte;
-    const WS ws{(lbyte*)sm, 0};
-
-    // ---- X: this wave's token tiles, k pair 0 in flight while W is staged
-    // the bf16 path (one part) reads bf16 X rows and writes bf16 Y rows (MEP_BF16_STORE)
-    constexpr bool HS = NPART == 1;
-    constexpr int ES = HS ? 2 : 4;
-    const int64_t last = row_off(d.x, ntok - 1) + K;
-    const auto rsX = __builtin_amdgcn_make_buffer_rsrc((void*)d.x.ptr, 0, (int)min((int64_t)ES * last, (int64_t)0x7fffffff), 0x00020000);
-    const bool xvec = ((d.x.ptr & (HS ? 7 : 15)) == 0) && (d.x.sB % 4 == 0) && (d.x.sT % 4 == 0);
-    int xoff[TG_TT];
-#pragma unroll
-    for (int t = 0; t < TG_TT; ++t) {
-        const int tok = min(tok0 + 16 * (TG_TT * wave + t) + c, ntok - 1);
-        xoff[t] = ES * ((int)row_off(d.x, tok) + 4 * g);
-    }
-    f32x4 xr[TG_TT][2];
-    auto load_x = [&](int kp) {
-#pragma unroll
-        for (int t = 0; t < TG_TT; ++t)
-#pragma unroll
-            for (int h = 0; h < 2; ++h) {
-                const int o = xoff[t] + 32 * ES * kp + 16 * ES * h;
-                if (HS && xvec) {
-                    const u32x2a w = __builtin_bit_cast(u32x2a, __builtin_amdgcn_raw_buffer_load_b64(rsX, o, 0, 0));
-                    xr[t][h] = f32x4{bf16_word_lo(w[0]), bf16_word_hi(w[0]), bf16_word_lo(w[1]), bf16_word_hi(w[1])};
-                } else if (HS) {
-#pragma unroll
-                    for (int e = 0; e < 4; ++e)
-                        xr[t][h][e] = __builtin_bit_cast(float, (unsigned)__builtin_amdgcn_raw_buffer_load_b16(rsX, o + 2 * e, 0, 0) << 16);
-                } else if (xvec) {
-                    xr[t][h] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rsX, o, 0, 0));
-                } else {
-#pragma unroll
-                    for (int e = 0; e < 4; ++e)
-                        xr[t][h][e] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsX, o + 4 * e, 0, 0));
-                }
-            }
-    };
-    load_x(0);
-
-    // ---- W: every unit (n, p, g) of the tile, loads issued before the LDS writes (per batch)
-    {
-        const gfloat* W = G<const float>(d.w);
-        const bool wvec = WNT && (d.ldw % 4 == 0) && ((d.w & 15) == 0);
-        const int NU = BN * nkp * 4;
-        constexpr int BATCH = 4;
-        for (int u0 = 0; u0 < NU; u0 += BATCH * TG_THREADS) {
-            f32x4 v[BATCH][2];
-#pragma unroll
-            for (int b = 0; b < BATCH; ++b) {
-                const int idx = u0 + b * TG_THREADS + threadIdx.x;
-                if (idx < NU) {
-                    const int n = idx % BN, pg = idx / BN, gg = pg & 3, pp = pg >> 2;
-                    v[b][0] = tg_wfrag<WNT>(W, d.ldw, wvec, n0 + n, N, 32 * pp + 4 * gg, K);
-                    v[b][1] = tg_wfrag<WNT>(W, d.ldw, wvec, n0 + n, N, 32 * pp + 16 + 4 * gg, K);
-                }
-            }
-#pragma unroll
-            for (int b = 0; b < BATCH; ++b) {
-                const int idx = u0 + b * TG_THREADS + threadIdx.x;
-                if (idx < NU) {
-                    const int n = idx % BN, pg = idx / BN;
-                    ws.put(n, pg >> 2, pg & 3, v[b][0], v[b][1]);
-                }
-            }
-        }
-    }
-    __syncthreads();
-
-    f32x4 acc[TG_TT][NI];
-#pragma unroll
-    for (int t = 0; t < TG_TT; ++t)
-#pragma unroll
-        for (int i = 0; i < NI; ++i) acc[t][i] = zero_f4();
-    for (int kp = 0; kp < nkp; ++kp) {
-        OpN<NPART> xo[TG_TT];
-#pragma unroll
-        for (int t = 0; t < TG_TT; ++t) xo[t] = opn<NPART>(xr[t][0], xr[t][1]);
-        if (kp + 1 < nkp) load_x(kp + 1);
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int i = 0; i < NI; ++i) {
-            const OpN<NW> w = ws.frag(i, kp);
-#pragma unroll
-            for (int t = 0; t < TG_TT; ++t) acc[t][i] = mma_nm<NW, NPART>(w, xo[t], acc[t][i]);
-            if (i & 1) __builtin_amdgcn_sched_barrier(0);
-        }
-    }
-
-    const gfloat* bias = G<const float>(d.bias);
-    const gfloat* table = G<const float>(d.table);
-    const int ldt = d.ldt ? d.ldt : N;
-#pragma unroll
-    for (int t = 0; t < TG_TT; ++t) {
-        const int tok = tok0 + 16 * (TG_TT * wave + t) + c;
-        if (tok >= ntok) continue;
-        const auto yrow = rowa<HS>(d.y, tok);
-        const gfloat* trow = table ? table + (int64_t)(tok % d.y.T) * ldt : nullptr;
-#pragma unroll
-        for (int i = 0; i < NI; ++i) {
-            const int col = n0 + 16 * i + 4 * g;
-            if (col >= N) continue;
-            f32x4 v = acc[t][i];
-#pragma unroll
-            for (int r = 0; r < 4; ++r) v[r] = d.alpha * v[r];
-            if (bias) v += ld4w(bias + col);
-            if (trow) {
-#pragma unroll
-                for (int r = 0; r < 4; ++r) v[r] += trow[col + r];
-            }
-            if (d.relu) {
-#pragma unroll
-                for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r], 0.f);
-            }
-            if (d.accumulate) v += ld4a(yrow + col);
-            st4a(yrow + col, v);
-        }
-    }
-}
-
 }  // namespace
 
 // Grid (ceil(max ntok / 128), n_desc, ceil(max N / (16 * NI))): flags = MEP_PREC_BF16 for the bf16
@@ -574,23 +432,6 @@ extern "C" int mep_tgemm(const mep_gemm_desc* descs, int n_desc, int max_ntok, i
     if (n_desc <= 0 || max_ntok <= 0 || max_n <= 0) return 0;
     const bool bf = flags & MEP_PREC_BF16, wnt = !(flags & MEP_TGEMM_WT);
     hipStream_t st = (hipStream_t)stream;
-    if (flags & MEP_TGEMM_RESIDENT) {   // K <= 320 (host): the whole weight tile resident, N tiles of 96
-        const int ni = max_n >= 96 ? 6 : (max_n + 15) / 16;
-        const dim3 grid((max_ntok + TG_BM - 1) / TG_BM, n_desc, (max_n + 16 * ni - 1) / (16 * ni)), block(TG_THREADS);
-#define MEP_TR3(NI, P, NW, WT) hipLaunchKernelGGL((k_tgemm_res<NI, P, NW, WT>), grid, block, 0, st, descs)
-#define MEP_TR2(NI, P, NW) do { if (wnt) MEP_TR3(NI, P, NW, true); else MEP_TR3(NI, P, NW, false); } while (0)
-#define MEP_TR(NI) do { if (bf) MEP_TR2(NI, 1, 1); else MEP_TR2(NI, 3, 2); } while (0)
-        switch (ni) {
-            case 2: MEP_TR(2); break;
-            case 4: MEP_TR(4); break;
-            case 6: MEP_TR(6); break;
-            default: mep_set_error("mep_tgemm: resident N must be 32, 64 or >= 96 (a multiple of 16)"); return MEP_EINVAL;
-        }
-#undef MEP_TR
-#undef MEP_TR2
-#undef MEP_TR3
-        return mep_check_launch("mep_tgemm");
-    }
     const int ni = max_n >= 16 * MEP_TG_NI ? MEP_TG_NI : (max_n + 15) / 16;   // 16-col tiles per workgroup N tile
     if (flags & MEP_TGEMM_DMA) {   // w_nt (host)
         if (!wnt) { mep_set_error("mep_tgemm: MEP_TGEMM_DMA needs w_nt"); return MEP_EINVAL; }

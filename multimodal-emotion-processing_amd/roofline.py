@@ -1,11 +1,18 @@
 """Algorithmic FLOPs and HBM bytes per launch of a TriModalPlan step.
 
-"Algorithmic" = the minimum the math needs: every input read once, every output written once,
-no recomputation (the attention backward's recomputed S / dP are not counted).  fp32 (4 B).
+"Algorithmic" = the minimum the launch must move: every DISTINCT input tensor read once, every
+output written once, no recomputation (the attention backward's recomputed S / dP are not
+counted).  fp32 (4 B).  Inputs shared by several blocks of one launch count once (round 6): a
+modality's unified features are the queries of three chains and the keys / values of three more,
+so the attention launches read each of them once, and L2 / the Infinity Cache serve the rest.
 Per attention-block instance (batch row b, block j), with n_kv = 1 (k is v):
-  fwd flops = 4*Tq*Tk*D;  bytes = 4*(2*Tq*D + Tk*D) + 4*Tk + 8*H*Tq + 4*H*Tq*Tk*(r_in + r_out)
-  bwd flops = 10*Tq*Tk*D; bytes = 4*(Tq*D*(q, x, dx, dq r+w) + Tk*D*(kv, dkv)) + 4*Tk + 8*H*Tq
-          (+ S_prev, ds_next reads, ds_prev write when chained)
+  fwd flops = 4*Tq*Tk*D;  bytes = 4*(Tq*D (x) + [q, kv rows once per distinct tensor]) + 4*Tk
+          + 8*H*Tq + 4*H*Tq*Tk*(r_in + r_out)
+  bwd flops = 10*Tq*Tk*D; bytes = 4*(Tq*D*(x, dx, dq r+w) + Tk*D*dkv + [q, kv once per distinct
+          tensor]) + 4*Tk + 8*H*Tq (+ S_prev, ds_next reads, ds_prev write when chained)
+VALU issue floor (valu_floor): a wave64 VALU instruction occupies its SIMD for 4 cycles, so a
+launch issuing N of them needs at least 4 N / (1,024 SIMDs x 2.4 GHz); N per dispatch comes from
+the committed SQ_INSTS_VALU counter pass of the workload (profiles/r*_counters_*.json).
 Peaks (MI355X_MICROARCH.md): HBM 8.0 TB/s; fp32 MFMA (= vector rate) 157.3 TFLOP/s; bf16 MFMA
 2.5 PFLOP/s dense.  Kernels whose fp32 products run as bf16 parts (split.h) are priced against the
 bf16 peak divided by the bf16 products per fp32 product (compute_peak): six for the 3-part x 3-part
@@ -25,6 +32,7 @@ from . import _lib
 from .trimodal import MODS
 
 HBM_PEAK = 8.0e12
+SIMDS, CLOCK, VALU_CYCLES = 1024, 2.4e9, 4          # 256 CUs x 4 SIMDs; wave64 VALU issue cycles
 F32_PEAK = 157.3e12
 BF16_PEAK = 2.5e15
 # fp32 path (csrc/attn.hip): the forward's scores and P.V take six bf16 products each (3-part
@@ -70,13 +78,11 @@ def launch_costs(plan):
         for m, d in zip(MODS, sp.dims):
             n = plan.ntok[m]
             add(UNIFY, 2 * n * D * d, a * (n * d + n * D) + 4 * D * d)
+    for name, (f, b) in attn_costs(plan, a).items():
+        add(name, f, b)
+    shared_q = set()
     for blk in plan.blocks:
         Tq, Tk = blk['Tq'], blk['Tk']
-        r_in = 1 if blk['i'] > 0 else 0
-        r_out = 1 if 'S' in blk else 0
-        s_bytes = 4 * H * Tq * Tk
-        add('mep_attn_fwd', B * 4 * Tq * Tk * D,
-            B * (a * (2 * Tq * D + Tk * D) + 4 * Tk + 8 * H * Tq + s_bytes * (r_in + r_out)))
         n = B * Tq
         # reads q, x; writes xp, z (activations) and out (the pooled tensor, fp32) [+ its bf16
         # copy for the next layer's q]
@@ -86,10 +92,11 @@ def launch_costs(plan):
         # as [n, D] rows (the pool backward is folded into this launch)
         add('mep_block_epi_bwd', 2 * n * D * 3 * D + 10 * n * D,
             a * n * D * 6 + 8 * n + 4 * 3 * D * D + 4 * (n // 64 + 1) * 2 * D + 4 * B * 3 * D)
-        chained = s_bytes * ((1 if r_out else 0) + (1 if r_in else 0) * 2)
-        add('mep_attn_bwd', B * 10 * Tq * Tk * D,
-            B * (a * (5 * Tq * D + 2 * Tk * D) + 4 * Tk + 8 * H * Tq + chained))
-        add('mep_wgrad', 2 * n * D * 3 * D, a * n * D * 5)
+        # dXP, X, dZ, XP per block; q (layer 0: the query modality's unified rows, shared by its
+        # three chains) once per distinct tensor
+        q_key = (blk['e'], blk['qm']) if blk['i'] == 0 else id(blk)
+        add('mep_wgrad', 2 * n * D * 3 * D, a * n * D * (4 + (q_key not in shared_q)))
+        shared_q.add(q_key)
     for e in range(2):
         for m, d in zip(MODS, sp.dims):
             n = plan.ntok[m]
@@ -101,6 +108,49 @@ def launch_costs(plan):
             srcs = sum(1 for b in plan.blocks if b['i'] == 0 and b['qm'] == m) // 2 + \
                 sum(1 for b in plan.blocks if b['km'] == m) // 2
             add('mep_sum_rows', srcs * n * D, a * n * D * (srcs + 1))
+    return out
+
+
+def _distinct(views):
+    """bytes of the distinct tensors among (ptr, bytes) views (a tensor read by several
+    descriptors of one launch counts once)"""
+    seen = {}
+    for p, nb in views:
+        seen[p] = max(seen.get(p, 0), nb)
+    return sum(seen.values())
+
+
+def attn_costs(plan, a):
+    """(flops, algorithmic bytes) of the attention launches of a plan, from its descriptors:
+    q / k / v rows and masks once per distinct tensor, per-block outputs, statistics and score
+    tensors once per descriptor (a: bytes per activation element)."""
+    out = {}
+    D = plan.spec.D
+    fwd = [d for arr in plan.d_attn for d in arr.items]
+    bwd = [d for arr in plan.d_attnb for d in arr.items]
+
+    def rows(v, B):
+        return v.ptr, a * B * v.T * D
+
+    def fwd_bytes(d):
+        s_bytes = 4 * d.H * d.Tq * d.Tk * d.B
+        return (a * d.B * d.Tq * D + 8 * d.B * d.H * d.Tq +
+                s_bytes * ((1 if d.s_prev else 0) + (1 if d.s_out else 0)))
+    f = sum(4 * d.B * d.Tq * d.Tk * D for d in fwd)
+    shared = _distinct([rows(d.q, d.B) for d in fwd] + [rows(d.k, d.B) for d in fwd] + [rows(d.v, d.B) for d in fwd] +
+                       [(d.mask, 4 * d.B * d.Tk) for d in fwd])
+    out['mep_attn_fwd'] = (f, shared + sum(fwd_bytes(d) for d in fwd))
+
+    def bwd_bytes(bd):
+        d = bd.f
+        s_bytes = 4 * d.H * d.Tq * d.Tk * d.B
+        dkv = 1 if bd.dk.ptr == bd.dv.ptr else 2
+        chained = s_bytes * ((1 if bd.ds_next else 0) + (2 if d.s_prev else 0))
+        return a * d.B * (4 * d.Tq * D + dkv * d.Tk * D) + 8 * d.B * d.H * d.Tq + chained
+    f = sum(10 * bd.f.B * bd.f.Tq * bd.f.Tk * D for bd in bwd)
+    shared = _distinct([rows(bd.f.q, bd.f.B) for bd in bwd] + [rows(bd.f.k, bd.f.B) for bd in bwd] +
+                       [rows(bd.f.v, bd.f.B) for bd in bwd] + [(bd.f.mask, 4 * bd.f.B * bd.f.Tk) for bd in bwd])
+    out['mep_attn_bwd'] = (f, shared + sum(bwd_bytes(bd) for bd in bwd))
     return out
 
 
@@ -149,14 +199,6 @@ def rf_launch_costs(plan):
         gemm(G_IN, nk, D, 2 * D)                               # dkv_in = [dK | dV] [W_k; W_v]
         if isum:   # (no per-source row writes: one sum row per token, below)
             add(G_IN, 0, -4 * (nk * D + (nq * D if blk['i'] == 0 else 0)))
-        r_in = 1 if blk['i'] > 0 else 0
-        r_out = 1 if 'S' in blk else 0
-        s_bytes = 4 * H * Tq * Tk
-        add('mep_attn_fwd', R * 4 * Tq * Tk * D,
-            R * (4 * (2 * Tq * D + 2 * Tk * D) + 4 * Tk + 8 * H * Tq + s_bytes * (r_in + r_out)))
-        chained = s_bytes * ((1 if r_out else 0) + (1 if r_in else 0) * 2)
-        add('mep_attn_bwd', R * 10 * Tq * Tk * D,
-            R * (4 * (5 * Tq * D + 4 * Tk * D) + 4 * Tk + 8 * H * Tq + chained))
         w = 4 * (D * D + 2 * D * FD + 2 * D + FD + 4 * D)      # Wp, W1, W2, biases, LN weights
         # forward: reads q, x; writes xp, h, f1, f, out and 4 stats per token
         add(EPI_F, 2 * nq * (D * D + 2 * D * FD), 4 * nq * (7 * D + FD + 4) + w)
@@ -165,6 +207,8 @@ def rf_launch_costs(plan):
         # weight gradients: W_q, [W_k; W_v], Wp, W1, W2
         for (n, N, K) in ((nq, D, D), (nk, D, 2 * D), (nq, D, D), (nq, D, FD), (nq, D, FD)):
             add('mep_wgrad', 2 * n * N * K, 4 * n * (N + K))
+    for name, (f, b) in attn_costs(plan, 4).items():
+        add(name, f, b)
     if rfw:
         # mep_wsplit: every pre-split weight read once (fp32) and its three bf16 parts written
         nw = sum(d.nrows * d.K for d in plan.d_wsplit.items)
@@ -180,14 +224,34 @@ def rf_launch_costs(plan):
     return out
 
 
-def roofline_entry(name, flops, nbytes, seconds, bf16=False, D=None):
-    """The bench's roofline object for one kernel: bound = the larger of the two ideal times."""
+def valu_floor(valu_insts):
+    """seconds the VALU issue of `valu_insts` wave64 instructions takes with every SIMD busy"""
+    return VALU_CYCLES * valu_insts / (SIMDS * CLOCK)
+
+
+def roofline_entry(name, flops, nbytes, seconds, bf16=False, D=None, valu=None):
+    """The bench's roofline object for one kernel: bound = the larger of the HBM and matrix-core
+    ideal times (the contract's two bounds).  valu = (VALU instructions per launch, source): the
+    VALU issue floor beside them (`valu`), and `limiter` names whichever of the three floors is
+    largest -- 'valu' for kernels whose instruction issue, not bytes or matrix flops, sets the
+    floor."""
     cpeak = compute_peak(name, D, bf16)
     t_mem, t_cmp = nbytes / HBM_PEAK, flops / cpeak
     if t_mem >= t_cmp:
         achieved = nbytes / seconds / 1e9
-        return dict(kernel=name, bound='hbm', achieved=round(achieved, 2), peak=HBM_PEAK / 1e9, unit='GB/s',
-                    frac=round(achieved / (HBM_PEAK / 1e9), 4), algorithmic_bytes=int(nbytes))
-    achieved = flops / seconds / 1e12
-    return dict(kernel=name, bound='mfma', achieved=round(achieved, 3), peak=round(cpeak / 1e12, 1), unit='TFLOP/s',
-                frac=round(achieved / (cpeak / 1e12), 4), algorithmic_flops=int(flops))
+        out = dict(kernel=name, bound='hbm', achieved=round(achieved, 2), peak=HBM_PEAK / 1e9, unit='GB/s',
+                   frac=round(achieved / (HBM_PEAK / 1e9), 4), algorithmic_bytes=int(nbytes))
+    else:
+        achieved = flops / seconds / 1e12
+        out = dict(kernel=name, bound='mfma', achieved=round(achieved, 3), peak=round(cpeak / 1e12, 1), unit='TFLOP/s',
+                   frac=round(achieved / (cpeak / 1e12), 4), algorithmic_flops=int(flops))
+    floors = {'hbm': t_mem, 'mfma': t_cmp}
+    if valu is not None and valu[0]:
+        t_valu = valu_floor(valu[0])
+        floors['valu'] = t_valu
+        out['valu'] = dict(insts_per_launch=int(valu[0]), floor_us=round(t_valu * 1e6, 2),
+                           frac=round(t_valu / seconds, 4), source=valu[1],
+                           model='4 cycles per wave64 VALU instruction on 1,024 SIMDs at 2.4 GHz')
+    out['floors_us'] = {k: round(v * 1e6, 2) for k, v in floors.items()}
+    out['limiter'] = max(floors, key=floors.get)
+    return out

@@ -28,10 +28,39 @@ def _wgrad(items, dev):
     return ws, arr
 
 
+def _mask_of(mask, q, k):
+    """The reference's mask forms (cmu-mosei/run.py:247-252) -> (fp32 mask tensor, 3-D?):
+    None -> an all-ones [B, Tk] key mask (the reference subtracts nothing; s - 1e8 * (1 - 1) is
+    s - 0 = s, bit for bit), [B, Tk] -> the key mask of the fused kernels, [B, Tq, Tk] -> the
+    general kernels (mep_attn_general_*)."""
+    B, Tq, Tk = q.shape[0], q.shape[1], k.shape[1]
+    if mask is None:
+        return torch.ones(B, Tk, dtype=torch.float32, device=q.device), False
+    if mask.dim() == 2 and tuple(mask.shape) == (B, Tk):
+        return _c(mask), False
+    if mask.dim() == 3 and tuple(mask.shape) == (B, Tq, Tk):
+        return _c(mask), True
+    raise ValueError('mask must be None, [batch, kv_len] or [batch, q_len, kv_len]; got %s' % (tuple(mask.shape),))
+
+
+def _gen_desc(ad, H, D, Tq, Tk):
+    """mep_attn_gen_desc of a [B, Tq, Tk] mask: scale = float32(np.sqrt(hd)), the divisor the
+    reference's q @ k^T / np.sqrt(k.size(-1)) uses"""
+    import numpy as np
+    hd = D // H
+    ad.mask_sB = Tq * Tk
+    return _lib.AttnGenDesc(f=ad, mask_sQ=Tk, hd=hd, scale=float(np.float32(np.sqrt(hd))))
+
+
+def _advance_seed(seed):
+    _lib.call('mep_seed_advance', ctypes.c_void_p(seed.data_ptr()))
+
+
 class _BlockFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, H, drop_p, q, k, v, mask, s_prev, c, wp, wm, lnw, lnb):
-        q, k, v, mask = _c(q), _c(k), _c(v), _c(mask)
+    def forward(ctx, H, drop_p, seed, q, k, v, mask, s_prev, c, wp, wm, lnw, lnb):
+        q, k, v = _c(q), _c(k), _c(v)
+        mask, general = _mask_of(mask, q, k)
         B, Tq, D = q.shape
         Tk = k.shape[1]
         dev = q.device
@@ -46,18 +75,30 @@ class _BlockFn(torch.autograd.Function):
                       mask=mask.data_ptr(), mask_sB=Tk, s_prev=sp.data_ptr() if sp is not None else 0,
                       c=c.data_ptr(), s_out=S.data_ptr(), stats=astat.data_ptr(), B=B, H=H, Tq=Tq, Tk=Tk)
         wp, wm = _c(wp), _c(wm)
+        # training-mode dropout (Ren-MME DROP = 0.1, run.py:173, 209, 213): the epilogue's two
+        # sites on the counter-hash masks of the block's seed, advanced per forward like a fresh
+        # nn.Dropout draw; the forward records the keep bits the backward reads
+        bits = torch.zeros(cdiv(B * Tq, 16), 2, 64, dtype=torch.int32, device=dev) if drop_p > 0.0 else None
+        if bits is not None:
+            _advance_seed(seed)
         ed = EpiDesc(q=crows(q, Tq, D), x=crows(X, Tq, D), xp=crows(XP, Tq, D), z=crows(Z, Tq, D),
                      out=crows(out, Tq, D), wp=wp.data_ptr(), wm=wm.data_ptr(), ln_w=lnw.data_ptr(),
-                     ln_b=lnb.data_ptr(), stats=estat.data_ptr(), seed=0, ntok=B * Tq, D=D, drop_p=0.0,
-                     drop_stream=0)
-        a_arr, e_arr = DescArray(AttnDesc, [ad], dev), DescArray(EpiDesc, [ed], dev)
-        geo = _lib.attn_geometry([ad])
-        launch('mep_attn_fwd', a_arr, geo[0], threads=geo[2])
+                     ln_b=lnb.data_ptr(), stats=estat.data_ptr(), seed=seed.data_ptr() if bits is not None else 0,
+                     ntok=B * Tq, D=D, drop_p=drop_p if bits is not None else 0.0, drop_stream=0,
+                     drop_bits=bits.data_ptr() if bits is not None else 0)
+        e_arr = DescArray(EpiDesc, [ed], dev)
+        if general:
+            gd = _gen_desc(ad, H, D, Tq, Tk)
+            _lib.call('mep_attn_general_fwd', DescArray(_lib.AttnGenDesc, [gd], dev).ptr, 1, B * H)
+        else:
+            gd = None
+            geo = _lib.attn_geometry([ad])
+            launch('mep_attn_fwd', DescArray(AttnDesc, [ad], dev), geo[0], threads=geo[2])
         launch('mep_block_epi_fwd', e_arr, _lib.epi_grid(B * Tq, 1), threads=D)
         ctx.save_for_backward(q, k, v, mask, X, XP, Z, S, astat, estat, c, wp, wm, lnw, lnb)
-        ctx.sp = sp
+        ctx.sp, ctx.bits, ctx.seed = sp, bits, seed
         ctx.meta = (B, Tq, Tk, D, H, same_kv)
-        ctx.descs = (ad, ed)
+        ctx.descs = (ad, ed, gd)
         return out, S
 
     @staticmethod
@@ -65,7 +106,7 @@ class _BlockFn(torch.autograd.Function):
     def backward(ctx, dout, dS):
         (q, k, v, mask, X, XP, Z, S, astat, estat, c, wp, wm, lnw, lnb) = ctx.saved_tensors
         B, Tq, Tk, D, H, same_kv = ctx.meta
-        ad, ed = ctx.descs
+        ad, ed, gd = ctx.descs
         dev = q.device
         f = dict(dtype=torch.float32, device=dev)
         dout = _c(dout) if dout is not None else torch.zeros(B, Tq, D, **f)
@@ -76,16 +117,21 @@ class _BlockFn(torch.autograd.Function):
         ln_part = torch.empty(cdiv(B * Tq, 16), 2, D, **f)
         has_prev = ctx.sp is not None
         dSp = torch.empty(B, H, Tq, Tk, **f) if has_prev else None
-        dc_part = torch.empty(_lib.attn_dc_slots(B, H, Tk), **f) if has_prev else None
+        n_dc = B * H if gd is not None else _lib.attn_dc_slots(B, H, Tk)
+        dc_part = torch.empty(n_dc, **f) if has_prev else None
         eb = EpiBwdDesc(f=ed, dout=crows(dout, Tq, D), dout2=Rows(), dz=crows(dZ, Tq, D), dxp=crows(dXP, Tq, D),
                         dx=crows(dX, Tq, D), dq=crows(dQ, Tq, D), ln_partial=ln_part.data_ptr(), dq_accumulate=0)
-        ab = AttnBwdDesc(f=ad, dx=crows(dX, Tq, D), dq=crows(dQ, Tq, D), dk=crows(dK, Tk, D), dv=crows(dV, Tk, D),
-                         ds_next=dS.data_ptr() if dS is not None else 0,
-                         ds_prev=dSp.data_ptr() if has_prev else 0,
-                         dc_partial=dc_part.data_ptr() if has_prev else 0)
         launch('mep_block_epi_bwd', DescArray(EpiBwdDesc, [eb], dev), _lib.epi_grid(B * Tq, 1), threads=D)
-        geo = _lib.attn_geometry([ad])
-        launch('mep_attn_bwd', DescArray(AttnBwdDesc, [ab], dev), geo[1], threads=_lib.attn_bwd_flags([ab]))
+        outs = dict(dx=crows(dX, Tq, D), dq=crows(dQ, Tq, D), dk=crows(dK, Tk, D), dv=crows(dV, Tk, D),
+                    ds_next=dS.data_ptr() if dS is not None else 0, ds_prev=dSp.data_ptr() if has_prev else 0,
+                    dc_partial=dc_part.data_ptr() if has_prev else 0)
+        if gd is not None:
+            gb = _lib.AttnGenBwdDesc(g=gd, **outs)
+            _lib.call('mep_attn_general_bwd', DescArray(_lib.AttnGenBwdDesc, [gb], dev).ptr, 1, B * H, gd.hd)
+        else:
+            ab = AttnBwdDesc(f=ad, **outs)
+            geo = _lib.attn_geometry([ad])
+            launch('mep_attn_bwd', DescArray(AttnBwdDesc, [ab], dev), geo[1], threads=_lib.attn_bwd_flags([ab]))
         gwp, gwm = torch.empty_like(wp), torch.empty_like(wm)
         glw, glb, gc = torch.empty_like(lnw), torch.empty_like(lnb), torch.empty_like(c)
         n = B * Tq
@@ -101,19 +147,30 @@ class _BlockFn(torch.autograd.Function):
                                  ld=1, accumulate=0))
         launch('mep_colsum', DescArray(ColsumDesc, cs, dev), cdiv(D, 32))
         del keep
-        return (None, None, dQ, dK, None if same_kv else dV, None, dSp, gc if has_prev else None,
+        return (None, None, None, dQ, dK, None if same_kv else dV, None, dSp, gc if has_prev else None,
                 gwp, gwm, glw, glb)
 
 
+def block_seed(block, device):
+    """The standalone block's dropout seed state (device uint64 {seed, row0 = 0}, the plans'
+    layout): drawn from torch's generator on first use, advanced on the device by every
+    training-mode forward (a fresh mask per call, as nn.Dropout draws)"""
+    s = getattr(block, '_mep_seed', None)
+    if s is None or s.device != torch.device(device):
+        seed = int(torch.randint(0, 2 ** 62, (1,)).item())
+        s = torch.tensor([seed, 0], dtype=torch.int64, device=device)
+        block._mep_seed = s
+    return s
+
+
 def block_forward(block, q, k, v, mask, scores, norm, drop_p=0.0):
+    """cmu-mosei / Ren-MME Attention_Block.forward(q, k, v, mask, scores=None): every mask form the
+    reference accepts (None, [B, Tk], [B, Tq, Tk]) and, in training mode, the block's dropout."""
     from ._autograd import require_cuda
     require_cuda(q, k, v, mask)
-    if mask is None or mask.dim() != 2:
-        raise NotImplementedError('mep_amd attention takes a [batch, kv_len] key mask (the only form the '
-                                  'reference models pass)')
-    if block.training and drop_p > 0.0:
-        raise NotImplementedError('standalone block dropout: run the block inside its model plan')
-    return _BlockFn.apply(block.n_heads, drop_p, q, k, v, mask, scores, block.c, block.proj.weight,
+    p = float(drop_p) if block.training else 0.0
+    seed = block_seed(block, q.device) if p > 0.0 else torch.zeros(2, dtype=torch.int64, device=q.device)
+    return _BlockFn.apply(block.n_heads, p, seed, q, k, v, mask, scores, block.c, block.proj.weight,
                           block.minus.weight, norm.weight, norm.bias)
 
 
@@ -225,7 +282,8 @@ class _RFBlockFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, H, q, k, v, mask, s_prev, wq, wk, wv, wp, n1w, n1b, n2w, n2b, w1, b1, w2, b2, a, b, c):
-        q, k, v, mask = _c(q), _c(k), _c(v), _c(mask)
+        q, k, v = _c(q), _c(k), _c(v)
+        mask, general = _mask_of(mask, q, k)
         B, Tq, D = q.shape
         Tk = k.shape[1]
         FD = w1.shape[0]
@@ -252,8 +310,13 @@ class _RFBlockFn(torch.autograd.Function):
                             w1=w1.data_ptr(), b1=b1.data_ptr(), w2=w2.data_ptr(), b2=b2.data_ptr(),
                             ln1_w=n1w.data_ptr(), ln1_b=n1b.data_ptr(), ln2_w=n2w.data_ptr(), ln2_b=n2b.data_ptr(),
                             a=a.data_ptr(), b=b.data_ptr(), stats=estat.data_ptr(), ntok=B * Tq, D=D, FD=FD)
-        geo = _lib.attn_geometry([ad])
-        launch('mep_attn_fwd', DescArray(AttnDesc, [ad], dev), geo[0], threads=geo[2])
+        if general:
+            gd = _gen_desc(ad, H, D, Tq, Tk)
+            _lib.call('mep_attn_general_fwd', DescArray(_lib.AttnGenDesc, [gd], dev).ptr, 1, B * H)
+        else:
+            gd = None
+            geo = _lib.attn_geometry([ad])
+            launch('mep_attn_fwd', DescArray(AttnDesc, [ad], dev), geo[0], threads=geo[2])
         rfw = _lib.RFW
         ctx.wbuf = None
         if rfw:   # the epilogue's Linears on mep_wsplit parts (wave-tiled kernels, csrc/rfw.hip)
@@ -269,7 +332,7 @@ class _RFBlockFn(torch.autograd.Function):
                               wq, wk, wv, wp, n1w, n1b, n2w, n2b, w1, b1, w2, b2, a, b, c)
         ctx.sp = sp
         ctx.meta = (B, Tq, Tk, D, H, FD)
-        ctx.descs = (ad, ed)
+        ctx.descs = (ad, ed, gd)
         return out, S
 
     @staticmethod
@@ -278,7 +341,7 @@ class _RFBlockFn(torch.autograd.Function):
         (q, k, v, mask, QP, KV, X, XP, Hh, F1, F, S, astat, estat,
          wq, wk, wv, wp, n1w, n1b, n2w, n2b, w1, b1, w2, b2, a, b, c) = ctx.saved_tensors
         B, Tq, Tk, D, H, FD = ctx.meta
-        ad, ed = ctx.descs
+        ad, ed, gd = ctx.descs
         dev = q.device
         f = dict(dtype=torch.float32, device=dev)
         dout = _c(dout) if dout is not None else torch.zeros(B, Tq, D, **f)
@@ -293,18 +356,23 @@ class _RFBlockFn(torch.autograd.Function):
         part = torch.empty(nt, stride, **f)
         has_prev = ctx.sp is not None
         dSp = torch.empty(B, H, Tq, Tk, **f) if has_prev else None
-        dc_part = torch.empty(_lib.attn_dc_slots(B, H, Tk), **f) if has_prev else None
+        dc_part = torch.empty(B * H if gd is not None else _lib.attn_dc_slots(B, H, Tk), **f) if has_prev else None
         kv = lambda t, which: _lib.Rows(ptr=t.data_ptr() + 4 * which * D, sB=Tk * 2 * D, sT=2 * D, T=Tk)  # noqa: E731
         eb = _lib.RfEpiBwdDesc(f=ed, dout=crows(dout, Tq, D), dout2=Rows(), df=crows(dF, Tq, D),
                                df1=crows(dF1, Tq, FD), dxp=crows(dXP, Tq, D), dx=crows(dX, Tq, D),
                                dq=crows(dQin, Tq, D), partial=part.data_ptr(), dq_accumulate=0)
-        ab = AttnBwdDesc(f=ad, dx=crows(dX, Tq, D), dq=crows(dQP, Tq, D), dk=kv(dKV2, 0), dv=kv(dKV2, 1),
-                         ds_next=dS.data_ptr() if dS is not None else 0, ds_prev=dSp.data_ptr() if has_prev else 0,
-                         dc_partial=dc_part.data_ptr() if has_prev else 0)
+        outs = dict(dx=crows(dX, Tq, D), dq=crows(dQP, Tq, D), dk=kv(dKV2, 0), dv=kv(dKV2, 1),
+                    ds_next=dS.data_ptr() if dS is not None else 0, ds_prev=dSp.data_ptr() if has_prev else 0,
+                    dc_partial=dc_part.data_ptr() if has_prev else 0)
         launch('mep_rfw_epi_bwd' if ctx.rfw else 'mep_rf_epi_bwd', DescArray(_lib.RfEpiBwdDesc, [eb], dev), nt,
                extra=(D, FD))
-        geo = _lib.attn_geometry([ad])
-        launch('mep_attn_bwd', DescArray(AttnBwdDesc, [ab], dev), geo[1], threads=_lib.attn_bwd_flags([ab]))
+        if gd is not None:
+            gb = _lib.AttnGenBwdDesc(g=gd, **outs)
+            _lib.call('mep_attn_general_bwd', DescArray(_lib.AttnGenBwdDesc, [gb], dev).ptr, 1, B * H, gd.hd)
+        else:
+            ab = AttnBwdDesc(f=ad, **outs)
+            geo = _lib.attn_geometry([ad])
+            launch('mep_attn_bwd', DescArray(AttnBwdDesc, [ab], dev), geo[1], threads=_lib.attn_bwd_flags([ab]))
         g = dict(bias=0, table=0, relu=0, alpha=1.0, w_nt=0, K=D, ldw=D, N=D)
         gd = [GemmDesc(x=crows(dQP, Tq, D), y=crows(dQin, Tq, D), w=wq.data_ptr(), ntok=B * Tq, accumulate=1, **g),
               GemmDesc(x=kv(dKV2, 0), y=crows(dk_in, Tk, D), w=wk.data_ptr(), ntok=B * Tk, accumulate=0, **g),
@@ -341,9 +409,6 @@ class _RFBlockFn(torch.autograd.Function):
 def rf_block_forward(block, q, k, v, mask, scores):
     from ._autograd import require_cuda
     require_cuda(q, k, v, mask)
-    if mask is None or mask.dim() != 2:
-        raise NotImplementedError('mep_amd attention takes a [batch, kv_len] key mask (the only form the '
-                                  'reference models pass)')
     if block.training and block.drop.p > 0.0:
         raise NotImplementedError('realformer dropout: the reference runs DROP = 0 (others/realformer.py:37)')
     ffn0, ffn2 = block.ffn[0], block.ffn[2]

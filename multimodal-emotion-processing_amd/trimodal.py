@@ -53,29 +53,8 @@ WG_TARGET = _lib.N_CU      # workgroups per launch: one per CU (4 waves of ~400 
 WG_TARGET_OVERRIDE = int(_lib.switch('MEP_WG_TARGET', '0')) or None   # development: another k_wgrad workgroup count
 # the pool's backward formed inside the epilogue backward (0: a separate mep_pool_bwd into dXcat)
 POOL_FOLD = _lib.switch('MEP_POOL_FOLD', '1') != '0'
-# per-modality gradient sums inside the attention backward (no mep_sum_rows launch): correct (bit
-# equal) but off -- the agent-scope release every (b, h) unit needs before it counts its slices
-# took the cfg3 attention backward from 36 to 641 us
-SUM_FOLD = _lib.switch('MEP_SUM_FOLD', '0') == '1'
-FWD_SPLITQ = _lib.switch('MEP_FWD_SPLITQ', '0') == '1'
-# single-process backward: the block-weight gradients (mep_wgrad of bucket A, which read only the
-# epilogue backward's outputs) on a side stream, concurrent with the attention backward and the
-# per-modality sums; the unify-weight launch after them, one reduction for both (captured graphs
-# run the two branches concurrently).  Off by default: measured slower -- each launch's persistent
-# grid fills every CU, so the branches contend instead of filling each other's gaps (cfg3 fp32
-# 0.234 -> 0.259 ms per step, attention backward 37 -> 59 us; cfg5 1.61 -> 1.74 ms)
-OVERLAP_WGRAD = _lib.switch('MEP_OVERLAP_WGRAD', '0') == '1'
-# the epilogues' weights split into their LDS images once per step (mep_epi_images, at the start of
-# the forward) and copied into LDS by LDS-DMA, instead of every workgroup splitting them.  Off by
-# default: the copy of the (1.5x larger) 3-part image takes as long as the staging it replaces
-# (cfg3 fp32 forward 30.5 vs 30.4 us, backward 34.3 vs 33.8, plus 5.4 us for the image launch;
-# bf16 -0.6 us per epilogue against 3.8 us) -- the staging is bound by moving the weights into every
-# CU, not by its split VALU
-EPI_IMAGE = _lib.switch('MEP_EPI_IMAGE', '0') == '1'
 # mep_unify workgroups in XCD-contiguous descriptor order (xcd_order); 0: descriptor-major by id
 UNIFY_XCD = _lib.switch('MEP_UNIFY_XCD', '1') != '0'
-_DEV_EPI_TWICE = _lib.switch('MEP_DEV_EPI_TWICE', '0') == '1'   # development timing runs only
-_DEV_SUMFOLD_PROBE = _lib.switch('MEP_DEV_SUMFOLD_PROBE', '0') == '1'   # development timing runs only
 
 
 def wgrad_geometry(N, ktot, bf16=False):
@@ -107,7 +86,7 @@ def _wgrad_units(items, bf16=False):
     return units
 
 
-# k_wgrad cost per workgroup ~ a * tokens + c (cfg3 / cfg5 bf16 fits, scripts/ab/r4_gpu23.sh: a = 8.5 ns per
+# k_wgrad cost per workgroup ~ a * tokens + c (cfg3 / cfg5 bf16 fits, round 4: a = 8.5 ns per
 # token, c = 16 us of setup + partial write); in tokens, c / a:
 WG_SETUP_TOKENS = int(_lib.switch('MEP_WG_SETUP_TOKENS', '1900'))
 
@@ -151,7 +130,7 @@ def wgrad_segments(items, n_wg=WG_TARGET, tok_per_split=None, bf16=False):
     water-filling over all n_wg CUs (47.3 vs 49.6 us at cfg3, scripts/wgrad_balance.py); a span
     longer than the chunk is cut into near-equal pieces.  The loop
     is bound by HBM traffic and the operand-load rate, so more, smaller segments only add setup
-    and partial-reduction work (~10 us per workgroup, scripts/wgrad_trace.py).
+    and partial-reduction work (~10 us per workgroup, round-3 per-workgroup traces).
     -> (per-workgroup segment lists [(item, cg, t0, t1, slot)], slots per item)."""
     units = _wgrad_units(items, bf16)
     if tok_per_split is None:
@@ -457,13 +436,6 @@ class TriModalPlan:
         blk['astat'] = torch.zeros(B, H, Tq, 2, **f32)
         blk['dKV'] = torch.zeros(nk, D, **self.act)
         blk['ln_partial'] = torch.zeros(cdiv(nq, 16), 2, D, **f32)   # one row per 16-token wave
-        if EPI_IMAGE:
-            # the epilogues' LDS weight images (mep_epi_images, once per step; 0 bytes: staged in
-            # the kernel)
-            for key, which in (('img_f', 0), ('img_b', 1)):
-                nb = _lib.lib().mep_epi_image_bytes(D | self.prec, which)
-                if nb:
-                    blk[key] = torch.zeros(nb, dtype=torch.uint8, device=self.device)
         if sp.drop_p > 0:
             # the forward epilogue's dropout keep bits, read by the backward (mep_epi_desc.drop_bits)
             blk['dbits'] = torch.zeros(cdiv(nq, 16) * 2 * 64, dtype=torch.int32, device=self.device)
@@ -535,9 +507,8 @@ class TriModalPlan:
             self.d_attn.append(DescArray(AttnDesc, ad, dev))
             self.d_epi.append(DescArray(EpiDesc, ed, dev))
             geo = _lib.attn_geometry(ad)
-            # 16-query forward tasks (MEP_ATTN_SPLITQ) when the launch has few (b, h) units, or
-            # forced (MEP_FWD_SPLITQ=1, A/B runs)
-            sq, sq_tiles = _lib.attn_fwd_splitq(ad, min_units=1 << 30 if FWD_SPLITQ else 1024)
+            # 16-query forward tasks (MEP_ATTN_SPLITQ) when the launch has few (b, h) units
+            sq, sq_tiles = _lib.attn_fwd_splitq(ad, min_units=1024)
             if sq:
                 geo = (sq_tiles, geo[1], geo[2] | sq)
             self.t_attn.append(geo[0])
@@ -568,7 +539,6 @@ class TriModalPlan:
         # per-modality gradient sums
         sd = []
         self.dU = {}
-        self._sum_srcs = {}
         for e in range(E):
             for m in MODS:
                 T = self.T[m]
@@ -577,17 +547,11 @@ class TriModalPlan:
                 srcs += [crows(self._blk(e, j, i)['dKV'], T, D) for j, (qm, km) in enumerate(CHAINS) if km == m
                          for i in range(nl)]
                 assert len(srcs) <= _lib.SUM_MAX_SRC
-                self._sum_srcs[(e, m)] = srcs
                 arr = (Rows * _lib.SUM_MAX_SRC)(*srcs)
                 sd.append(SumDesc(src=arr, out=crows(self.dU[(e, m)], T, D), n_src=len(srcs),
                                   ntok=self.ntok[m], D=D, accumulate=_lib.SUM_BF16 if self.bf16 else 0))
         self.d_sum = DescArray(SumDesc, sd, dev)
         self.t_sum = min(1024, max(cdiv(self.ntok[m] * D // 4, 256) for m in MODS))
-        # the sums folded into the attention backward (SHORT descriptors: every key length <= 64)
-        self.sum_fold = (SUM_FOLD and not self.bf16 and max(self.T.values()) <= 64
-                         and all(d.n_src <= _lib.ATTN_FOLD_SRC for d in sd))
-        if self.sum_fold:
-            self.sum_count = torch.zeros(len(sd), B * sp.H, dtype=torch.int32, device=dev)
         # backward per layer
         self.d_epib, self.d_attnb, self.t_attnb, self.f_attnb = [], [], [], []
         for i in range(nl):
@@ -595,12 +559,6 @@ class TriModalPlan:
             for blk in (b for b in self.blocks if b['i'] == i):
                 eb.append(self._epi_bwd_desc(blk))
                 ab.append(self._attn_bwd_desc(blk))
-                if self.sum_fold:
-                    e = blk['e']
-                    ab[-1].sum, ab[-1].sum_count = self.d_sum.ptr.value, self.sum_count.data_ptr()
-                    ab[-1].sum_q = e * 3 + MODS.index(blk['qm']) if i == 0 else -1
-                    ab[-1].sum_kv = e * 3 + MODS.index(blk['km'])
-                    ab[-1].sum_stride = B * sp.H
             self.d_epib.append(DescArray(EpiBwdDesc, eb, dev))
             self.d_attnb.append(DescArray(AttnBwdDesc, ab, dev))
             self.t_attnb.append(self.g_attn[i][1])
@@ -625,12 +583,6 @@ class TriModalPlan:
                     r0 += tiles[m]
             self.d_ulnb = DescArray(LnDesc, lb, dev)
         self._build_grad_descriptors()
-        imgs = [self._epi_bwd_desc(b) for b in self.blocks if 'img_f' in b or 'img_b' in b]
-        self.d_img = DescArray(EpiBwdDesc, imgs, dev) if imgs else None
-        # the overlapped backward needs a device with concurrent streams and a split with work on
-        # both sides (bucket A = the block weights, B = the unify weights)
-        self.overlap = (OVERLAP_WGRAD and self.device.type == 'cuda' and not self.sum_fold
-                        and 0 < self._n_block_items < len(self._wgrad_items))
 
     def _attn_desc(self, blk):
         sp, fl, D = self.spec, self.flat, self.spec.D
@@ -656,8 +608,7 @@ class TriModalPlan:
                        stats=blk['estat'].data_ptr(), seed=self.seed_state.data_ptr(),
                        ntok=self.B * Tq, D=D, drop_p=self._drop, drop_stream=stream_id,
                        out_h=crows(blk['Qh'], Tq, D) if 'Qh' in blk else Rows(),
-                       drop_bits=blk['dbits'].data_ptr() if 'dbits' in blk else 0,
-                       image=blk['img_f'].data_ptr() if 'img_f' in blk else 0)
+                       drop_bits=blk['dbits'].data_ptr() if 'dbits' in blk else 0)
 
     def _epi_bwd_desc(self, blk):
         D, Tq = self.spec.D, blk['Tq']
@@ -676,7 +627,7 @@ class TriModalPlan:
                           dout2=crows(nxt['dQ'], Tq, D) if nxt is not None else Rows(),
                           dz=crows(blk['dZ'], Tq, D), dxp=crows(blk['dXP'], Tq, D), dx=crows(blk['dX'], Tq, D),
                           dq=crows(blk['dQ'], Tq, D), ln_partial=blk['ln_partial'].data_ptr(), dq_accumulate=0,
-                          image=blk['img_b'].data_ptr() if 'img_b' in blk else 0, **up)
+                          **up)
 
     def _attn_bwd_desc(self, blk):
         D = self.spec.D
@@ -704,14 +655,6 @@ class TriModalPlan:
             pre = sp.prefixes[e] + 'unify_dimension.'
             for m, d in zip(MODS, sp.dims):
                 src = self.dY[(e, m)] if sp.unify_norm else self.dU[(e, m)]
-                if _DEV_SUMFOLD_PROBE and not sp.unify_norm:
-                    # development timing probe (wrong gradients): the unify weight gradient as one
-                    # item per per-modality source, no mep_sum_rows -- what folding the sums into
-                    # the weight-gradient launch as extra token slots would cost
-                    for a in self._sum_srcs[(e, m)]:
-                        items.append((a, D, self.ntok[m],
-                                      [(self._in_rows(e, m), d, g(pre + UNIFY_NAMES[m] + '.weight'), d)]))
-                    continue
                 items.append((crows(src, self.T[m], D), D, self.ntok[m],
                               [(self._in_rows(e, m), d, g(pre + UNIFY_NAMES[m] + '.weight'), d)]))
         self._wgrad_items = items
@@ -811,41 +754,20 @@ class TriModalPlan:
         loss (row_loss, already scaled by 1/B); grad=True also runs the head backward
         (dpooled + head parameter partials) inside the same launch."""
         sp, nl = self.spec, self.spec.nl
-        if self.d_img is not None:
-            _lib.call('mep_epi_images', self.d_img.ptr, self.d_img.n, sp.D | self.prec, stream=stream)
         _lib.gemm('mep_unify', self.d_unify, self.t_unify, stream, prec=self.prec)
         if sp.unify_norm:
             launch('mep_layernorm_fwd', self.d_uln, cdiv(max(self.ntok.values()), 4), stream)
         for i in range(nl):
             launch('mep_attn_fwd', self.d_attn[i], self.t_attn[i], stream, threads=self.g_attn[i][2] | self.prec)
             launch('mep_block_epi_fwd', self.d_epi[i], self.t_epi[i], stream, threads=sp.D | self.prec)
-            if _DEV_EPI_TWICE:   # development: the same (idempotent) launch again, on a warm L2
-                launch('mep_block_epi_fwd', self.d_epi[i], self.t_epi[i], stream, threads=sp.D | self.prec)
         launch('mep_pool_fwd', self.d_pool, self.t_pool, stream)
         self.head.compute_grad = int(grad)
         self.head.rdrop = int(rdrop)
         self.head.ext_dlogits = 0
         _lib.call('mep_head_fwd_bwd', ctypes.byref(self.head), stream=stream)
 
-    def _build_overlap(self):
-        """The overlapped backward's launches: bucket A / B weight gradients with the fused launch's
-        token chunk (every gradient the same sum in the same order as one launch, bit for bit) and
-        one reduction descriptor array over both."""
-        if getattr(self, '_ovl', None) is not None:
-            return self._ovl
-        dev, items, nb = self.device, self._wgrad_items, self._n_block_items
-        tps = wgrad_chunk(items, wg_target(self.bf16), bf16=self.bf16)
-        wa = make_wgrad(items[:nb], dev, tok_per_split=tps, bf16=self.bf16)
-        wb = make_wgrad(items[nb:], dev, tok_per_split=tps, bf16=self.bf16)
-        red = DescArray(WgradDesc, wa[1].items + wb[1].items, dev)
-        self._ovl = (wa, wb, red, max(wa[3], wb[3]), torch.cuda.Stream(device=dev))
-        return self._ovl
-
     def _reduce_args(self):
         """(wgrad descriptor array, reduce tiles) of the step's mep_reduce_grads launch"""
-        if self.overlap:
-            _, _, red, t_red, _ = self._build_overlap()
-            return red, t_red
         return self.d_wgrad, self.t_wgred
 
     def backward(self, ext_dlogits=None, stream=None):
@@ -860,31 +782,13 @@ class TriModalPlan:
             self.head.ext_dlogits = 0
         if not self.pool_fold:
             launch("mep_pool_bwd", self.d_pool, self.t_poolb, stream)
-        ovl = self._build_overlap() if self.overlap else None
-        main = side = None
         for i in reversed(range(nl)):
             launch('mep_block_epi_bwd', self.d_epib[i], self.t_epi[i], stream, threads=sp.D | self.prec)
-            if _DEV_EPI_TWICE:
-                launch('mep_block_epi_bwd', self.d_epib[i], self.t_epi[i], stream, threads=sp.D | self.prec)
-            if ovl is not None and i == 0:
-                # every block-weight operand is final here: bucket A's weight gradients on the side
-                # stream while the attention backward and the sums run on this one
-                (_, da, ta, _), side = ovl[0], ovl[4]
-                main = stream if stream is not None else torch.cuda.current_stream()
-                side.wait_stream(main)
-                with torch.cuda.stream(side):
-                    launch('mep_wgrad', da, ta, side)
             launch('mep_attn_bwd', self.d_attnb[i], self.t_attnb[i], stream, threads=self.f_attnb[i] | self.prec)
-        if not self.sum_fold and not (_DEV_SUMFOLD_PROBE and not sp.unify_norm):
-            launch('mep_sum_rows', self.d_sum, self.t_sum, stream)
+        launch('mep_sum_rows', self.d_sum, self.t_sum, stream)
         if sp.unify_norm:
             launch('mep_layernorm_bwd', self.d_ulnb, cdiv(max(self.ntok.values()), 64), stream)
-        if ovl is not None:
-            _, db, tb, _ = ovl[1]
-            launch('mep_wgrad', db, tb, stream)
-            main.wait_stream(side)
-        else:
-            launch('mep_wgrad', self.d_wgrad, self.t_wgrad, stream)
+        launch('mep_wgrad', self.d_wgrad, self.t_wgrad, stream)
         # weight-gradient split sums, LayerNorm / residual-coefficient column sums and the head
         # parameter sums: one launch
         red, t_red = self._reduce_args()
@@ -965,8 +869,7 @@ class TriModalPlan:
                           ctypes.byref(self.head), *self.head_grads, None, None, None, stream=stream)
                 bucket_a_done()
             launch('mep_attn_bwd', self.d_attnb[i], self.t_attnb[i], stream, threads=self.f_attnb[i] | self.prec)
-        if not self.sum_fold:
-            launch('mep_sum_rows', self.d_sum, self.t_sum, stream)
+        launch('mep_sum_rows', self.d_sum, self.t_sum, stream)
         if sp.unify_norm:
             launch('mep_layernorm_bwd', self.d_ulnb, cdiv(max(self.ntok.values()), 64), stream)
         launch('mep_wgrad', db, tb, stream)

@@ -29,7 +29,8 @@ def residual_attention(q, k, v, mask, n_heads, c=None, s_prev=None):
     """Residual scaled-dot-product attention, cmu-mosei/run.py:236-256 (== realformer.py:189-203).
 
     q [B,Tq,D], k/v [B,Tk,D] already projected (or raw features for cmu/Ren-MME), mask [B,Tk]
-    (1 = keep).  Returns (x [B,Tq,D] before ``proj``, post-mask scores [B,H,Tq,Tk]).
+    or [B,Tq,Tk] (1 = keep; the 3-D form is shared by the heads, run.py:250-252) or None.
+    Returns (x [B,Tq,D] before ``proj``, post-mask scores [B,H,Tq,Tk]).
     Op order: (q.k^T)/sqrt(hd)  [+ c*S_prev]  then  -= 1e8*(1-mask)   (run.py:243-253).
     """
     qh, kh, vh = heads(q, n_heads), heads(k, n_heads), heads(v, n_heads)
@@ -38,7 +39,8 @@ def residual_attention(q, k, v, mask, n_heads, c=None, s_prev=None):
     if s_prev is not None:
         s = s + c * s_prev
     if mask is not None:
-        s = s - MASK_BIG * (1.0 - mask[:, None, None, :])
+        m = mask[:, None, None, :] if mask.dim() == 2 else mask[:, None, :, :]
+        s = s - MASK_BIG * (1.0 - m)
     p = torch.softmax(s, dim=-1)
     return merge(torch.matmul(p, vh)), s
 

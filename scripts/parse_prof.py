@@ -1,4 +1,4 @@
-"""Summarise a scripts/profile.sh run into profiles/<tag>_*.
+"""Summarise a rocprofv3 run (scripts/session.sh prof / traffic stages) into profiles/<tag>_*.
 
   python scripts/parse_prof.py <tag> [gpurun_out/prof_<workload>] [<workload>: cfg3 | cfg5 | cfg5_bf16 | ...]
 

@@ -49,7 +49,8 @@ def batch(meta):
 
 def block_inputs(meta):
     D, H = meta['ctor']['dim'], meta['ctor']['n_heads']
-    return specs.block_inputs(meta['seed'] + 1, meta['B'], meta['Tq'], meta['Tk'], D, H, meta['with_prev'])
+    return specs.block_inputs(meta['seed'] + 1, meta['B'], meta['Tq'], meta['Tk'], D, H, meta['with_prev'],
+                              meta.get('mask_kind', 'key'))
 
 
 def chain_inputs(meta):

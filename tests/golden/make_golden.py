@@ -337,24 +337,31 @@ def perturbed_spread(module, run, base, skip=(), runs=6, seed=20261019):
     return out
 
 
-def case_block(name, family, consts, ctor, B, Tq, Tk, seed, with_prev=True, g_scores=True, leaf=None):
+def case_block(name, family, consts, ctor, B, Tq, Tk, seed, with_prev=True, g_scores=True, leaf=None,
+               mask_kind='key', drop=None):
     """Standalone Attention_Block forward/backward with residual scores and an upstream
     gradient on both outputs (out, post-mask scores).  leaf: constant parameter overrides (the
     F7 fixtures' c <= -1); those also store the same computation in float64 (<key>64) and the
-    reference's fp32 spread under parameter perturbation (perturbed_spread)."""
+    reference's fp32 spread under parameter perturbation (perturbed_spread).  mask_kind: the mask
+    form passed (specs.block_inputs).  drop = (p, seed0): the block in training mode with its
+    nn.Dropout at p, on the masks of the repo's counter hash for seed advance(seed0), stream 0
+    (MaskDrop: the standalone block advances its seed once per training forward)."""
     ns = load_reference(family, consts)
     blk = ns['Attention_Block'](**ctor)
     overrides = leaf_overrides(blk, leaf)
     shapes = set_params(blk, seed, overrides)
+    if drop is not None:
+        blk.drop = MaskDrop(0, odrop.seed_advance(drop[1]), drop[0])
+        blk.train()
     D, H = ctor['dim'], ctor['n_heads']
-    q, kv, mask, s_prev, g_out = specs.block_inputs(seed + 1, B, Tq, Tk, D, H, with_prev)
+    q, kv, mask, s_prev, g_out = specs.block_inputs(seed + 1, B, Tq, Tk, D, H, with_prev, mask_kind)
     rng = np.random.default_rng(seed + 2)
     g_s = (0.05 * rng.standard_normal((B, H, Tq, Tk))).astype(np.float32)
 
     def run(b, dt=torch.float32):
         qt, kvt = t(q).to(dt).requires_grad_(), t(kv).to(dt).requires_grad_()
         sp = t(s_prev).to(dt).requires_grad_() if with_prev else None
-        y, s = b(qt, kvt, kvt, t(mask).to(dt), sp)
+        y, s = b(qt, kvt, kvt, None if mask is None else t(mask).to(dt), sp)
         obj = (y * t(g_out).to(dt)).sum()
         if g_scores:
             obj = obj + (s * t(g_s).to(dt)).sum()
@@ -378,9 +385,11 @@ def case_block(name, family, consts, ctor, B, Tq, Tk, seed, with_prev=True, g_sc
             out[k.replace('grad/', 'grad64/') if k.startswith('grad/') else k + '64'] = v
         out.update(perturbed_spread(fresh, run, base, skip=overrides))
     meta = dict(kind='block', family=family, consts=consts, ctor=ctor, B=B, Tq=Tq, Tk=Tk,
-                seed=seed, with_prev=with_prev, g_scores=g_scores, shapes=shapes)
+                seed=seed, with_prev=with_prev, g_scores=g_scores, shapes=shapes, mask_kind=mask_kind)
     if overrides:
         meta['overrides'] = overrides
+    if drop is not None:
+        meta['drop'] = dict(p=drop[0], seed0=drop[1])
     return meta, out
 
 
@@ -548,6 +557,28 @@ for _c, _tag in ((-1.5, 'm15'), (-1.0, 'm1')):
         'block_cmu_f7_' + tag, 'cmu', CMU_C, dict(dim=32, n_heads=2, ffn=1), 3, 7, 11, 107, leaf={'c': c}))
     CASES['block_rf_f7_' + _tag] = (lambda c=_c, tag=_tag: case_block(
         'block_rf_f7_' + tag, 'realformer', rf_consts(8), dict(dim=32, n_heads=2), 3, 8, 10, 109, leaf={'c': c}))
+
+
+# the standalone Attention_Block.forward surface beyond the models' [B, Tk] key masks
+# (cmu-mosei/run.py:236-262, Ren-MME/run.py:171-214, others/realformer.py:182-209): mask=None,
+# [B, Tq, Tk] masks, and Ren-MME's block in training mode with DROP = 0.1
+CASES.update({
+    'block_cmu_nomask': lambda: case_block('block_cmu_nomask', 'cmu', CMU_C, dict(dim=32, n_heads=2, ffn=1),
+                                           3, 7, 11, 131, mask_kind='none'),
+    'block_cmu_mask3': lambda: case_block('block_cmu_mask3', 'cmu', CMU_C, dict(dim=32, n_heads=2, ffn=1),
+                                          3, 7, 11, 132, mask_kind='q3'),
+    'block_cmu_mask3_long': lambda: case_block('block_cmu_mask3_long', 'cmu', CMU_C, dict(dim=64, n_heads=4, ffn=1),
+                                               2, 9, 300, 133, mask_kind='q3'),
+    'block_rf_nomask': lambda: case_block('block_rf_nomask', 'realformer', rf_consts(8), dict(dim=32, n_heads=2),
+                                          3, 8, 10, 134, mask_kind='none'),
+    'block_rf_mask3': lambda: case_block('block_rf_mask3', 'realformer', rf_consts(8), dict(dim=32, n_heads=2),
+                                         3, 8, 10, 135, mask_kind='q3'),
+    'block_ren_drop': lambda: case_block('block_ren_drop', 'ren', dict(REN_C, DROP=0.1),
+                                         dict(dim=32, n_heads=2, ffn=1), 3, 7, 11, 136, drop=(0.1, 20261020)),
+    'block_ren_drop_mask3': lambda: case_block('block_ren_drop_mask3', 'ren', dict(REN_C, DROP=0.1),
+                                               dict(dim=128, n_heads=8, ffn=1), 2, 12, 40, 137, mask_kind='q3',
+                                               drop=(0.1, 20261021)),
+})
 
 
 def main(names):

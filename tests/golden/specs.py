@@ -107,19 +107,25 @@ def realformer_batch(seed, B, P, T, dims=(300, 35, 74)):
     return l, v, a, labels, lm, vm, am, um
 
 
-def block_inputs(seed, B, Tq, Tk, D, H, with_prev=True):
-    """Standalone Attention_Block inputs: q [B,Tq,D], kv [B,Tk,D], mask [B,Tk], S_prev
-    [B,H,Tq,Tk] built like a previous layer's post-mask scores, and an upstream gradient."""
+def block_inputs(seed, B, Tq, Tk, D, H, with_prev=True, mask_kind='key'):
+    """Standalone Attention_Block inputs: q [B,Tq,D], kv [B,Tk,D], the mask, S_prev [B,H,Tq,Tk]
+    built like a previous layer's post-mask scores, and an upstream gradient.  mask_kind: 'key'
+    ([B, Tk] right-padded), 'none' (mask=None: S_prev unmasked) or 'q3' (a [B, Tq, Tk] mask,
+    Bernoulli(0.7) per (query, key): the 3-D form multi_head_attention accepts, run.py:250-252)."""
     rng = np.random.default_rng(seed)
     q = rng.standard_normal((B, Tq, D)).astype(np.float32)
     kv = rng.standard_normal((B, Tk, D)).astype(np.float32)
     mask = masks_for(rng, (B,), Tk)
+    if mask_kind == 'q3':
+        mask = (rng.random((B, Tq, Tk)) < 0.7).astype(np.float32)
     s_prev = None
     if with_prev:
         s_prev = (0.5 * rng.standard_normal((B, H, Tq, Tk))).astype(np.float32)
-        s_prev = (s_prev - np.float32(1e8) * (np.float32(1.0) - mask[:, None, None, :])).astype(np.float32)
+        m4 = {'key': lambda: mask[:, None, None, :], 'q3': lambda: mask[:, None, :, :],
+              'none': lambda: np.ones((1, 1, 1, 1), np.float32)}[mask_kind]()
+        s_prev = (s_prev - np.float32(1e8) * (np.float32(1.0) - m4)).astype(np.float32)
     g_out = rng.standard_normal((B, Tq, D)).astype(np.float32)
-    return q, kv, mask, s_prev, g_out
+    return q, kv, None if mask_kind == 'none' else mask, s_prev, g_out
 
 
 def robot_batch(seed, B, T, dims=(768, 256, 512, 1024, 40)):

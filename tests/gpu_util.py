@@ -46,6 +46,32 @@ def close_or_spread(got, gold, key, rtol, atol_frac=1e-5, name=None):
     assert err <= allow, '%s: max error %.3g beyond 2x the reference fp32 scatter %.3g' % (name or key, err, allow)
 
 
+def assert_scores(got, gold, meta, c, s_prev, mask, q, k, name='scores'):
+    """Post-mask scores s = fl(fl(fl(q.k / sqrt(hd)) + fl(c S_prev)) - fl(1e8 (1 - m))) against the
+    reference's.  Error model: the dot term q.k / sqrt(hd) is an fp32 sum computed in another order
+    (and on split-bf16 products), so it may differ by a few ulps of the magnitude of its products,
+    bounded here by 2^-20 |q_h| |k_h| / sqrt(hd) (q, k: the block's attention inputs [B, T, D],
+    after any projection) -- much more than 1e-6 |s| where c S_prev or the dot itself cancels
+    (|c| ~ 1, the F7 fixtures) -- plus 1e-6 |s| for ordinary scores.  Scores of magnitude >= 1e6
+    (masked slots flipped by c < -1 to ~+5e7, on a grid of 4-16) get no relative allowance: the
+    ~1e8-sized terms are the same fp32 operations on both sides, so they must land on the
+    reference's grid value."""
+    g = got.detach().double().cpu().numpy()
+    w = np.asarray(gold[name], np.float64)
+    B, H, Tq, Tk = w.shape
+    qh = np.asarray(q, np.float64).reshape(B, Tq, H, -1).transpose(0, 2, 1, 3)
+    kh = np.asarray(k, np.float64).reshape(B, Tk, H, -1).transpose(0, 2, 1, 3)
+    hd = qh.shape[-1]
+    dn = np.linalg.norm(qh, axis=-1)[..., :, None] * np.linalg.norm(kh, axis=-1)[..., None, :] / np.sqrt(hd)
+    tol = (2.0 ** -20 * dn + np.where(np.abs(w) < 1e6, 1e-6 * np.abs(w), 0.0)
+           + 1e-12 * max(float(np.abs(w).max()), 1e-30))
+    bad = np.abs(g - w) > tol
+    if bad.any():
+        i = np.unravel_index(np.argmax(np.abs(g - w) - tol), w.shape)
+        raise AssertionError('%s: %d/%d mismatches; worst at %s got %r want %r (tol %g)'
+                             % (name, int(bad.sum()), bad.size, i, g[i], w[i], tol[i]))
+
+
 def _role(k):
     import re
     return re.sub(r'blocks\.\d+\.', 'blocks.*.', k)

@@ -36,6 +36,22 @@ def run_model_case(meta, steps=None):
     return out
 
 
+def block_dropout(meta, B, Tq, D):
+    """A block fixture's dropout (meta['drop']): the counter-hash masks of seed advance(seed0),
+    stream 0, site 0 then 1 -- what the standalone block draws in training mode"""
+    d = meta.get('drop')
+    if not d:
+        return None
+    from oracle import dropout as odrop
+    seed, calls = odrop.seed_advance(d['seed0']), [0]
+
+    def drop(t):
+        site = calls[0] % 2
+        calls[0] += 1
+        return t * torch.from_numpy(odrop.block_mask(seed, 0, site, B, Tq, D, d['p']))
+    return drop
+
+
 def run_block_case(meta):
     P = fixtures.params(meta)
     q, kv, mask, s_prev, g_out = fixtures.block_inputs(meta)
@@ -43,8 +59,13 @@ def run_block_case(meta):
     qt = torch.tensor(q, requires_grad=True)
     kvt = torch.tensor(kv, requires_grad=True)
     sp = torch.tensor(s_prev, requires_grad=True) if s_prev is not None else None
-    fn = cmu_mosei.block if meta['family'] == 'cmu' else realformer.block
-    y, s = fn(P, '', qt, kvt, torch.tensor(mask), H, s_prev=sp)
+    m = torch.tensor(mask) if mask is not None else None
+    if meta['family'] == 'realformer':
+        y, s = realformer.block(P, '', qt, kvt, m, H, s_prev=sp)
+    else:
+        norm = 'norm2' if meta['family'] == 'ren' else 'norm1'
+        y, s = cmu_mosei.block(P, '', qt, kvt, m, H, s_prev=sp, norm=norm,
+                               dropout=block_dropout(meta, q.shape[0], q.shape[1], q.shape[2]))
     return P, (qt, kvt, sp), y, s
 
 

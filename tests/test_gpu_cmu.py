@@ -9,7 +9,8 @@ import pytest
 import torch
 
 from tests.golden import fixtures
-from tests.gpu_util import OUT_ATOL_FRAC, assert_close, check_post_params, close_or_spread, cmu_model, cuda_batch
+from tests.gpu_util import (OUT_ATOL_FRAC, assert_close, assert_scores, check_post_params, close_or_spread, cmu_model,
+                            cuda_batch)
 
 pytestmark = pytest.mark.gpu
 CMU = [n for n in fixtures.names('model') if fixtures.load(n)[0]['family'] == 'cmu']
@@ -62,25 +63,35 @@ def test_concat_trans_engine_step(name, graph, cuda):
     assert_close(logits2, gold['logits2'], 1e-3, 1e-5, 'logits2')
 
 
-@pytest.mark.parametrize('name', fixtures.names('block'))
+BLOCKS = [n for n in fixtures.names('block') if fixtures.load(n)[0]['family'] in ('cmu', 'ren')]
+
+
+@pytest.mark.parametrize('name', BLOCKS)
 def test_attention_block_standalone(name, cuda):
+    """cmu-mosei / Ren-MME Attention_Block.forward called directly, against the reference block:
+    [B, Tk] key masks, mask=None, [B, Tq, Tk] masks (the general attention kernels), residual
+    scores including the F7 coefficients c = -1.5 / -1, and Ren-MME's block in training mode at
+    DROP = 0.1 (the block's seed state set to the fixture's; masks of oracle/dropout.py)."""
     import numpy as np
-    from mep_amd import cmu_mosei
+    from mep_amd import cmu_mosei, ren_mme
     meta, gold = fixtures.load(name)
-    if meta['family'] != 'cmu':
-        pytest.skip('realformer block covered by test_gpu_realformer')
     c = meta['ctor']
-    blk = cmu_mosei.Attention_Block(c['dim'], c['n_heads'], c['ffn'])
+    mod = cmu_mosei if meta['family'] == 'cmu' else ren_mme
+    blk = mod.Attention_Block(c['dim'], c['n_heads'], c['ffn'])
     from tests.gpu_util import load_params
     load_params(blk, meta)
-    blk = blk.to(cuda)
+    blk = blk.to(cuda).train()
+    drop = meta.get('drop')
+    blk.drop.p = drop['p'] if drop else 0.0
+    if drop:
+        blk._mep_seed = torch.tensor([drop['seed0'], 0], dtype=torch.int64, device=cuda)
     q, kv, mask, s_prev, g_out = fixtures.block_inputs(meta)
     qt = torch.tensor(q, device=cuda, requires_grad=True)
     kvt = torch.tensor(kv, device=cuda, requires_grad=True)
     sp = torch.tensor(s_prev, device=cuda, requires_grad=True) if s_prev is not None else None
-    y, s = blk(qt, kvt, kvt, torch.tensor(mask, device=cuda), sp)
+    y, s = blk(qt, kvt, kvt, None if mask is None else torch.tensor(mask, device=cuda), sp)
     assert_close(y, gold['out'], 1e-4, OUT_ATOL_FRAC, 'out')
-    assert_close(s, gold['scores'], 1e-6, 1e-12, 'scores')
+    assert_scores(s, gold, meta, blk.c.detach().cpu().numpy(), s_prev, mask, q, kv)
     obj = (y * torch.tensor(g_out, device=cuda)).sum()
     if meta['g_scores']:
         obj = obj + (s * torch.tensor(gold['g_scores'], device=cuda)).sum()

@@ -21,8 +21,8 @@ import pytest
 import torch
 
 from tests.golden import fixtures
-from tests.gpu_util import (assert_close, check_grad_budget, check_post_budget, check_post_params, close_or_spread,
-                            has_fp32_budget, load_params)
+from tests.gpu_util import (assert_close, assert_scores, check_grad_budget, check_post_budget, check_post_params,
+                            close_or_spread, has_fp32_budget, load_params)
 
 pytestmark = pytest.mark.gpu
 
@@ -44,8 +44,9 @@ RF_BLOCKS = [n for n in fixtures.names('block') if fixtures.load(n)[0]['family']
 
 @pytest.mark.parametrize('name', RF_BLOCKS)
 def test_realformer_block_standalone(name, cuda):
-    """block_rf, and the F7 fixtures block_rf_f7_m15 / _m1 (c = -1.5 / -1: the masked slots carry
-    the row's maximum / lose their -1e8; make_golden.py F7)"""
+    """block_rf, the F7 fixtures block_rf_f7_m15 / _m1 (c = -1.5 / -1: the masked slots carry the
+    row's maximum / lose their -1e8; make_golden.py F7), and the other mask forms the reference
+    accepts: mask=None (block_rf_nomask) and [B, Tq, Tk] (block_rf_mask3, the general kernels)"""
     meta, gold = fixtures.load(name)
     with ffn_const(meta) as rf:
         blk = rf.Attention_Block(meta['ctor']['dim'], meta['ctor']['n_heads'])
@@ -55,9 +56,10 @@ def test_realformer_block_standalone(name, cuda):
     qt = torch.tensor(q, device=cuda, requires_grad=True)
     kvt = torch.tensor(kv, device=cuda, requires_grad=True)
     sp = torch.tensor(s_prev, device=cuda, requires_grad=True)
-    y, s = blk(qt, kvt, kvt, torch.tensor(mask, device=cuda), sp)
+    y, s = blk(qt, kvt, kvt, None if mask is None else torch.tensor(mask, device=cuda), sp)
     close_or_spread(y, gold, 'out', 1e-4, 1e-6)
-    close_or_spread(s, gold, 'scores', 1e-5, 1e-7)
+    wq, wk = (blk.w_qkv[i].weight.detach().double().cpu().numpy() for i in (0, 1))
+    assert_scores(s, gold, meta, blk.c.detach().cpu().numpy(), s_prev, mask, q @ wq.T, kv @ wk.T)
     obj = (y * torch.tensor(g_out, device=cuda)).sum() + (s * torch.tensor(gold['g_scores'], device=cuda)).sum()
     obj.backward()
     close_or_spread(qt.grad, gold, 'grad_q', 1e-3, 1e-5)

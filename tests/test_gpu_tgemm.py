@@ -18,8 +18,8 @@ def _rows(t, T, sB, sT, off=0):
     return Rows(ptr=t.data_ptr() + t.element_size() * off, sB=sB, sT=sT, T=T)
 
 
-def _launch(descs, dev, prec=0, resident=False):
-    """resident: the resident-weight form (every K <= 320), else the chunked form"""
+def _launch(descs, dev, prec=0):
+    """the chunked form (TGEMM_MIN_K lowered so every K runs on it)"""
     from mep_amd import _lib
     arr = _lib.DescArray(_lib.GemmDesc, descs, dev)
     min_k, _lib.TGEMM_MIN_K = _lib.TGEMM_MIN_K, 0
@@ -27,16 +27,14 @@ def _launch(descs, dev, prec=0, resident=False):
         assert _lib.tgemm_ok(arr.items)
     finally:
         _lib.TGEMM_MIN_K = min_k
-    flags = prec | (0 if descs[0].w_nt else _lib.TGEMM_WT) | (_lib.TGEMM_RESIDENT if resident else 0)
+    flags = prec | (0 if descs[0].w_nt else _lib.TGEMM_WT)
     _lib.call('mep_tgemm', arr.ptr, arr.n, max(d.ntok for d in descs), max(d.N for d in descs), flags)
     torch.cuda.synchronize()
     return arr
 
 
-def _tol(res):
-    """resident form: the weight as two bf16 parts (<= 2^-18 relative) -> rtol 1e-4 / atol 1e-5
-    of max|y|; chunked: three parts on both operands (fp32-level) -> 1e-5 / 1e-6"""
-    return dict(rtol=1e-4, atol_frac=1e-5) if res else dict(rtol=1e-5, atol_frac=1e-6)
+# three bf16 parts on both operands (fp32-level): rtol 1e-5, atol 1e-6 of max|y|
+TOL = dict(rtol=1e-5, atol_frac=1e-6)
 
 
 def _gd(x, y, w, ntok, N, K, ldw, w_nt=1, bias=None, table=None, accumulate=0, relu=0, alpha=1.0, bf16=0, ldt=0):
@@ -46,15 +44,13 @@ def _gd(x, y, w, ntok, N, K, ldw, w_nt=1, bias=None, table=None, accumulate=0, r
                     accumulate=accumulate, relu=relu, alpha=alpha, bf16=bf16, ldt=ldt)
 
 
-@pytest.mark.parametrize('N,Ks,B,T,res', [
-    (96, (300, 35, 74), 64, 50, False),     # cmu-mosei cfg3: both slots, all three modalities in one launch
-    (96, (300, 35, 74), 64, 50, True),      # ... on the resident-weight form
-    (128, (768, 640, 205), 4, 300, False),  # Ren-MME cfg5 widths
-    (32, (300, 35, 74), 3, 7, False),       # ragged: 21 tokens
-    (32, (300, 35, 74), 3, 7, True),
-    (64, (17,), 5, 1, True),                # T = 1 rows, K < 32
+@pytest.mark.parametrize('N,Ks,B,T', [
+    (96, (300, 35, 74), 64, 50),     # cmu-mosei cfg3: both slots, all three modalities in one launch
+    (128, (768, 640, 205), 4, 300),  # Ren-MME cfg5 widths
+    (32, (300, 35, 74), 3, 7),       # ragged: 21 tokens
+    (64, (17,), 5, 1),               # T = 1 rows, K < 32
 ])
-def test_tgemm_unify_vs_float64(N, Ks, B, T, res, cuda):
+def test_tgemm_unify_vs_float64(N, Ks, B, T, cuda):
     torch.manual_seed(N + B + T)
     xs = [torch.randn(B, 2, T, K, device=cuda) for K in Ks]
     ws = [torch.randn(N, K, device=cuda) / K ** 0.5 for K in Ks]
@@ -64,16 +60,15 @@ def test_tgemm_unify_vs_float64(N, Ks, B, T, res, cuda):
         K = x.shape[-1]
         for e in range(2):
             descs.append(_gd(_rows(x, T, 2 * T * K, K, e * T * K), _rows(ys[i][e], T, T * N, N), w, B * T, N, K, K))
-    keep = _launch(descs, cuda, resident=res)
+    keep = _launch(descs, cuda)
     for i, (x, w) in enumerate(zip(xs, ws)):
         for e in range(2):
             want = x[:, e].double() @ w.double().t()
-            assert_close(ys[i][e], want, name='K%d slot%d' % (x.shape[-1], e), **_tol(res))
+            assert_close(ys[i][e], want, name='K%d slot%d' % (x.shape[-1], e), **TOL)
     del keep
 
 
-@pytest.mark.parametrize('res', [False, True])
-def test_tgemm_table_bias_relu_and_wide_n(res, cuda):
+def test_tgemm_table_bias_relu_and_wide_n(cuda):
     """Conv1d unify + position table; N = 192 ([W_k; W_v], two N tiles) with bias and relu."""
     torch.manual_seed(11)
     B, T, K = 8, 50, 300
@@ -81,22 +76,20 @@ def test_tgemm_table_bias_relu_and_wide_n(res, cuda):
     w = torch.randn(96, K, device=cuda) / K ** 0.5
     tab = torch.randn(T, 96, device=cuda)
     y = torch.empty(B * T, 96, device=cuda)
-    keep = _launch([_gd(_rows(x, T, T * K, K), _rows(y, T, T * 96, 96), w, B * T, 96, K, K, table=tab)], cuda,
-                   resident=res)
+    keep = _launch([_gd(_rows(x, T, T * K, K), _rows(y, T, T * 96, 96), w, B * T, 96, K, K, table=tab)], cuda)
     want = (x.double() @ w.double().t()).view(B, T, 96) + tab.double()
-    assert_close(y.view(B, T, 96), want, name='table', **_tol(res))
+    assert_close(y.view(B, T, 96), want, name='table', **TOL)
     w2 = torch.randn(192, 96, device=cuda) / 96 ** 0.5
     b2 = torch.randn(192, device=cuda)
     y2 = torch.empty(B * T, 192, device=cuda)
     keep2 = _launch([_gd(_rows(y, T, T * 96, 96), _rows(y2, T, T * 192, 192), w2, B * T, 192, 96, 96, bias=b2,
-                         relu=1)], cuda, resident=res)
+                         relu=1)], cuda)
     want2 = torch.relu(y.double() @ w2.double().t() + b2.double())
-    assert_close(y2, want2, name='N192 bias relu', **_tol(res))
+    assert_close(y2, want2, name='N192 bias relu', **TOL)
     del keep, keep2
 
 
-@pytest.mark.parametrize('res', [False, True])
-def test_tgemm_transposed_weight_accumulate(res, cuda):
+def test_tgemm_transposed_weight_accumulate(cuda):
     """dq_in += dQ W_q (W stored [K][N], w_nt = 0) and dkv_in = [dK | dV] [W_k; W_v] (K = 2D)."""
     torch.manual_seed(12)
     n, D = 3200, 96
@@ -108,15 +101,14 @@ def test_tgemm_transposed_weight_accumulate(res, cuda):
     wkv = torch.randn(2 * D, D, device=cuda) / D ** 0.5
     y2 = torch.empty(n, D, device=cuda)
     keep = _launch([_gd(_rows(dq, 50, 50 * D, D), _rows(y, 50, 50 * D, D), wq, n, D, D, D, w_nt=0, accumulate=1),
-                    _gd(_rows(dkv, 50, 100 * D, 2 * D), _rows(y2, 50, 50 * D, D), wkv, n, D, 2 * D, D, w_nt=0)], cuda,
-                   resident=res)
-    assert_close(y, base.double() + dq.double() @ wq.double(), name='accumulate', **_tol(res))
-    assert_close(y2, dkv.double() @ wkv.double(), name='K=2D', **_tol(res))
+                    _gd(_rows(dkv, 50, 100 * D, 2 * D), _rows(y2, 50, 50 * D, D), wkv, n, D, 2 * D, D, w_nt=0)], cuda)
+    assert_close(y, base.double() + dq.double() @ wq.double(), name='accumulate', **TOL)
+    assert_close(y2, dkv.double() @ wkv.double(), name='K=2D', **TOL)
     del keep
 
 
-@pytest.mark.parametrize('K,res', [(768, False), (300, True)])
-def test_tgemm_bf16_path(K, res, cuda):
+@pytest.mark.parametrize('K', [768, 300])
+def test_tgemm_bf16_path(K, cuda):
     """MEP_PREC_BF16: bf16 X and Y rows (MEP_BF16_STORE), plain bf16 operands, fp32 accumulation
     rounded to bf16 once on the store -- torch's bf16-operand product rounded to bf16."""
     from mep_amd import _lib
@@ -126,7 +118,7 @@ def test_tgemm_bf16_path(K, res, cuda):
     w = torch.randn(N, K, device=cuda) / K ** 0.5
     y = torch.empty(B * T, N, device=cuda, dtype=torch.bfloat16)
     keep = _launch([_gd(_rows(x, T, T * K, K), _rows(y, T, T * N, N), w, B * T, N, K, K,
-                        bf16=_lib.BF16_OPS | _lib.BF16_STORE)], cuda, prec=_lib.PREC_BF16, resident=res)
+                        bf16=_lib.BF16_OPS | _lib.BF16_STORE)], cuda, prec=_lib.PREC_BF16)
     want = x.double() @ w.bfloat16().double().t()
     # one bf16 rounding of the output (2^-9 relative) on top of fp32 accumulation
     assert_close(y, want, rtol=4e-3, atol_frac=1e-4, name="bf16")
