@@ -32,7 +32,7 @@ extern "C" {
 #endif
 
 #define MEP_EINVAL (-1000)
-#define MEP_ABI_VERSION 5
+#define MEP_ABI_VERSION 6
 
 typedef void* mep_stream_t; /* a hipStream_t */
 
@@ -173,7 +173,12 @@ typedef struct {
     uint64_t s_prev;    /* [B,H,Tq,Tk] or 0                                     */
     uint64_t c;         /* residual coefficient (device float*), used iff s_prev */
     uint64_t s_out;     /* [B,H,Tq,Tk] or 0                                     */
-    uint64_t stats;     /* [B,H,Tq,2]: (max log2 e - log2(1/sum), 1/sum) per row */
+    uint64_t stats;     /* [B,H,Tq,2]: (max log2 e - log2(1/sum), 1/sum) per row;
+                           with s_prev: (max, 1/sum) per row, then [B,H,Tq] more floats (ABI 6):
+                           each row's P-weighted mean of S_prev, sum_k P_ik S_prev_ik, which
+                           the backward subtracts from S_prev in the dc sum (its softmax part
+                           sums to 0 over a row; F7 rows at c <= -1 would otherwise cancel
+                           ~1e8-sized terms) -- 3 B H Tq floats in all */
     int32_t  B, H, Tq, Tk;
 } mep_attn_desc;
 /* Launch geometry: forward one wave per (b, h, 64-query chunk), 4 waves (256 threads) per

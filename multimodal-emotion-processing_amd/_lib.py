@@ -314,7 +314,7 @@ SIGNATURES.update({
 })
 
 _LIB = None
-ABI_VERSION = 5   # include/mep.h MEP_ABI_VERSION
+ABI_VERSION = 6   # include/mep.h MEP_ABI_VERSION
 
 
 def lib():

@@ -154,11 +154,6 @@ MEP_DEV floatx4 dot_score(const S3& p, const S3& u, floatx4 acc) {
     return acc;
 }
 
-#ifndef MEP_BWD_TR_BF
-#define MEP_BWD_TR_BF 0  // the bf16 instances only: dS as one 8-byte [key][query] word per key tile (one
-                         // ds_write_b64 instead of four ds_write_b16) read back by ds_read_b64_tr_b16
-#endif
-
 // 16-deep contraction, 2-way split, all four products.  MEP_BWD_MF16: four v_mfma_f32_16x16x16_bf16
 // on the parts as they come out of the split (each a register pair: no operand assembly moves);
 // else two 16x16x32 with A = [x0 | x1], B = [y0 | y0] then [y1 | y1].  (BF: x0 y0.)
@@ -323,6 +318,7 @@ MEP_DEV void attn_fwd_task(const mep_attn_desc& d, int qc, int h, int b, int lan
     const int q_lo = qc * qch;                   // qch: queries per task (64, or 16 with MEP_ATTN_SPLITQ)
     const int nqt = min(qch / 16, (Tq - q_lo + 15) / 16);
     gfloat* stats = G<float>(d.stats);
+    const int stat_rows = d.B * d.H * Tq;        // PREV: the tail of stats holds one float per row
 
     floatx4 o[SINGLE ? 1 : NT][NHB];
     float m[SINGLE ? 1 : NT], l[SINGLE ? 1 : NT];
@@ -347,7 +343,8 @@ MEP_DEV void attn_fwd_task(const mep_attn_desc& d, int qc, int h, int b, int lan
             // row statistics for the backward: (max log2 e - log2(1/sum), 1/sum) -- the exp2
             // backward's per-row exponent offset, formed once here instead of per backward tile and
             // key-chunk wave.  PREV: (max, 1/sum) -- the backward forms exp(s - max) with s - max
-            // exact (F7, Bwd::tile)
+            // exact (F7, Bwd::tile); the stats' tail (S_prev at the row maximum) is written by the
+            // key-chunk loop
             stats[2 * (sbase + q)] = !PREV ? mq * 1.4426950408889634f - __builtin_amdgcn_logf(inv) : mq;
             stats[2 * (sbase + q) + 1] = inv;
         }
@@ -505,7 +502,7 @@ MEP_DEV void attn_fwd_task(const mep_attn_desc& d, int qc, int h, int b, int lan
                 qs[hb] = QH ? qsh[QH ? qt : 0][hb] : BF ? qbf[!QH && BF ? qt : 0][hb] : split3(qfa[QH || BF ? 0 : qt][hb]);
             const int srow = (sbase + min(q, Tq - 1)) * Tk;
             float sv[NT][4];
-            float mx = -INFINITY;
+            float mx = -INFINITY, spm = 0.f;   // PREV: S_prev at the lane's largest score
 #pragma unroll
             for (int kt = 0; kt < NT; ++kt) {
                 floatx4 st = MI ? floatx4{-4.f * mt[kt][0], -4.f * mt[kt][1], -4.f * mt[kt][2], -4.f * mt[kt][3]}
@@ -520,6 +517,7 @@ MEP_DEV void attn_fwd_task(const mep_attn_desc& d, int qc, int h, int b, int lan
                         const int si = srow + min(kk, Tk - 1);
                         if (PREV) spv = sprev[si];
                         const float v = score<PREV, HDIM>(st[r], cres, spv, mt[kt][r]);
+                        if (PREV) spm = v > mx ? spv : spm;   // mx below: the running max before v
                         if (SOUT && kk < Tk && q < Tq) sout[si] = v;
                         sv[kt][r] = v;
                     } else if (MI) {
@@ -530,7 +528,18 @@ MEP_DEV void attn_fwd_task(const mep_attn_desc& d, int qc, int h, int b, int lan
                     mx = fmaxf(mx, sv[kt][r]);
                 }
             }
-            mx = xg_max(mx);
+            if (PREV) {
+                // the stats' tail: S_prev at the row's maximum score (of tied lanes the largest:
+                // deterministic), the shift of the backward's dc sum (Bwd::tile); a later key chunk
+                // with a larger maximum overwrites it (no register state across chunks)
+                const float ml = mx;
+                mx = xg_max(mx);
+                const float spr = xg_max(ml == mx ? spm : -INFINITY);
+                if (g == 0 && q < Tq && (SINGLE || k_lo == 0 || mx > m[SINGLE ? 0 : qt]))
+                    stats[2 * stat_rows + sbase + q] = spr;
+            } else {
+                mx = xg_max(mx);
+            }
             const float mnew = SINGLE ? mx : fmaxf(m[qt], mx);
             float lsum = 0.f;
             constexpr float L2E = 1.4426950408889634f;
@@ -612,7 +621,7 @@ MEP_DEV void attn_fwd_task(const mep_attn_desc& d, int qc, int h, int b, int lan
 }
 
 template <bool PREV, bool SOUT, bool SINGLE, bool BF, int HDIM = HD, int QCH = CH>
-__global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu((SINGLE && !PREV && HDIM == 16) ? MEP_FWD_WAVES : (HDIM == 32 && !SINGLE) ? 1 : !SINGLE ? (BF ? MEP_FWD_LONG_WAVES_BF : MEP_FWD_LONG_WAVES) : 2))) void k_attn_fwd(const mep_attn_desc* __restrict__ descs) {
+__global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu((SINGLE && !PREV && HDIM == 16) ? MEP_FWD_WAVES : (HDIM == 32 && !SINGLE) ? 1 : !SINGLE ? (BF ? MEP_FWD_LONG_WAVES_BF : PREV ? 1 : MEP_FWD_LONG_WAVES) : 2))) void k_attn_fwd(const mep_attn_desc* __restrict__ descs) {
     const mep_attn_desc& d = descs[blockIdx.y];
     if ((d.Tk <= CH) != SINGLE) return;    // the other variant's descriptor
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -662,6 +671,7 @@ struct Bwd {
     struct QIn {
         float qa[4], da[4], db[4], qb[4], ob[4], dqo[4];
         f32x2 st[4];
+        float rp[4];      // PREV: the rows' P-weighted mean of S_prev (the forward's stats tail)
         u32x2 qaw, daw;   // BF: Q / dO rows as raw bf16 operand words (no fp32 round trip)
         u32x2 oaw;        // BF: O row (delta on the matrix core)
     };
@@ -671,7 +681,7 @@ struct Bwd {
     const gfloat *sprev, *dsn, *mask;
     gfloat* dsp;
     BRowT<BF> Qb, Kb, Vb, Ob, Gb, dQb;   // BF: bf16 rows
-    __amdgpu_buffer_rsrc_t rsStat;
+    __amdgpu_buffer_rsrc_t rsStat, rsRp;
     bool same_kv;
     int k_lo;
     S2 kb[NT], vb[NT], kq[NT];
@@ -702,6 +712,7 @@ struct Bwd {
         same_kv = d.k.ptr == d.v.ptr && d.k.sB == d.v.sB && d.k.sT == d.v.sT;
         sbase = (b * d.H + h) * Tq;
         rsStat = uniform_rsrc(d.stats + 8ull * (uint64_t)sbase, 8 * (int64_t)Tq);
+        if (PREV) rsRp = uniform_rsrc(d.stats + 4ull * (uint64_t)(2 * d.B * d.H * Tq + sbase), 4 * (int64_t)Tq);
     }
 
     MEP_DEV void load_chunk(int kc) {
@@ -745,6 +756,7 @@ struct Bwd {
             in.qb[s] = Qb.ld1(oq, s * Qb.sT4);
             if (!BF) in.ob[s] = Ob.ld1(oo, s * Ob.sT4);
             in.st[s] = __builtin_bit_cast(f32x2, __builtin_amdgcn_raw_buffer_load_b64(rsStat, 8 * qg, 8 * s, 0));
+            if (PREV) in.rp[s] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsRp, 4 * qg, 4 * s, 0));
             in.dqo[s] = dQb.ld1(od, s * dQb.sT4);
         }
     }
@@ -757,7 +769,7 @@ struct Bwd {
     // wave's start and later holds finite rows of earlier tiles, whose products are masked).
     // BF (bf16 rows): 16 rows x 32 B per operand, lanes 0-31 (lane L = row L / 2, 16-byte piece
     // L % 2) into [16][16] bf16 images at the same float offsets (half of each slot used)
-    static constexpr int STG = 4 * 256 + 32;   // floats: Q, dO, O, dQ [16][16], stats [16][2]
+    static constexpr int STG = 4 * 256 + 48;   // floats: Q, dO, O, dQ [16][16], stats [16][2], PREV's rp [16]
     MEP_DEV static bool dma_view(const mep_rows& v) {   // 16-byte aligned pieces of every row
         return BF ? ((v.ptr & 15) == 0 && v.sB % 8 == 0 && v.sT % 8 == 0) : aligned16(v);
     }
@@ -775,6 +787,8 @@ struct Bwd {
                 __builtin_amdgcn_raw_ptr_buffer_load_lds(dQb.rs, (lvoid*)(S + 768), 16, dQb.at(row, col), 0, 0, 0);
                 __builtin_amdgcn_raw_ptr_buffer_load_lds(rsStat, (lvoid*)(S + 1024), 4, 8 * 16 * qt + 4 * lane, 0, 0, 0);
             }
+            if (PREV && lane < 16)
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(rsRp, (lvoid*)(S + 1056), 4, 4 * (16 * qt + lane), 0, 0, 0);
             return;
         }
         const int row = qt * 16 + (lane >> 2), col = hc + 4 * (lane & 3);
@@ -784,6 +798,8 @@ struct Bwd {
         __builtin_amdgcn_raw_ptr_buffer_load_lds(dQb.rs, (lvoid*)(S + 768), 16, dQb.at(row, col), 0, 0, 0);
         if (lane < 32)   // dword pieces: the range check drops exactly the rows past Tq
             __builtin_amdgcn_raw_ptr_buffer_load_lds(rsStat, (lvoid*)(S + 1024), 4, 8 * 16 * qt + 4 * lane, 0, 0, 0);
+        if (PREV && lane < 16)
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rsRp, (lvoid*)(S + 1056), 4, 4 * (16 * qt + lane), 0, 0, 0);
     }
     // the staged tile in the operand layouts of fetch()
     MEP_DEV void read_staged(QIn& in, const float* S) const {
@@ -805,6 +821,7 @@ struct Bwd {
                 in.db[s4] = __builtin_bit_cast(float, (unsigned)H[512 + r] << 16);
                 in.dqo[s4] = __builtin_bit_cast(float, (unsigned)H[1536 + r] << 16);
                 in.st[s4] = *(lcf2*)(L + 1024 + 2 * (4 * g + s4));
+                if (PREV) in.rp[s4] = L[1056 + 4 * g + s4];
             }
             return;
         }
@@ -819,6 +836,7 @@ struct Bwd {
             in.ob[s4] = L[512 + r];
             in.dqo[s4] = L[768 + r];
             in.st[s4] = *(lcf2*)(L + 1024 + 2 * (4 * g + s4));
+            if (PREV) in.rp[s4] = L[1056 + 4 * g + s4];
         }
     }
     MEP_DEV void store_dq_rows(const float (&dqo)[4], int qt, const floatx4& dq) const {
@@ -830,7 +848,6 @@ struct Bwd {
     // one 16-query tile against the chunk's 64 keys: accumulates dK / dV, returns this chunk's
     // dQ contribution (C[query 4g+r][dim c], before the 1/sqrt(hd) scale).  Tr: the wave's
     // transpose scratch in LDS (TFL floats: the bf16 hi and lo parts of dS, 16 x TLD2 each).
-    static constexpr bool TRX = BF && MEP_BWD_TR_BF;   // the dS transpose layout
     MEP_DEV floatx4 tile(const QIn& in, int qt, float* Tr) {
         const int q0 = qt * 16;
         constexpr float LOG2E = 1.4426950408889634f;
@@ -924,10 +941,18 @@ struct Bwd {
                 float gsv = pv * dp[r];
                 if (DSN || PREV) {
                     const bool ok = (qq < Tq) && (kk < Tk);
-                    if (DSN) gsv += ok ? dsn[si] : 0.f;
+                    const float gn = DSN && ok ? dsn[si] : 0.f;
+                    // dc = sum dS S_prev.  The softmax part P (dP - delta) sums to 0 over a row, so
+                    // its S_prev is taken relative to the row's P-weighted mean rp (exact in real
+                    // arithmetic): where c <= -1 puts the row's weight on masked keys, S_prev there is
+                    // -1e8 and the unshifted sum cancels ~1e8-sized terms, leaving 1e8 x the rounding
+                    // of dP; the shifted terms are small.  The gradient arriving on the scores (DSN)
+                    // has no such identity and keeps S_prev itself
+                    if (PREV) dc_acc = fmaf(gsv, spv - in.rp[r], dc_acc);
+                    gsv += gn;
                     if (PREV) {
                         if (ok) dsp[si] = cres * gsv;
-                        dc_acc = fmaf(gsv, spv, dc_acc);
+                        if (DSN) dc_acc = fmaf(gn, spv, dc_acc);
                     }
                 }
                 p[r] = pv;
@@ -954,16 +979,9 @@ struct Bwd {
                 dv[kt] = dot16<BF>(split2(p), db2, dv[kt]);
             }
             if (!(KV && !BF)) dk[kt] = dot16<BF>(ds2, qb2, dk[kt]);   // dK[key][dim] += dS^T Q
-            if constexpr (TRX) {
-                // the split dS as packed words into [key][16 queries] images (one 8-byte store per
-                // part: this lane's queries 4g .. 4g+3 of key kt*16 + c)
-                typedef __attribute__((address_space(3))) u32x2 lu32x2w;
-                lu32x2w* Ih = (lu32x2w*)Tr;
-                const int e = (kt * 16 + c) * 4 + g;       // u32x2 index: row (key) * 4 + column block
-                Ih[e] = u32x2{ds2.h0, ds2.h1};
-                if (!BF) Ih[CH * 4 + e] = u32x2{ds2.l0, ds2.l1};
-            } else {
-            // the split dS, element by element, into Th / Tl[query][key] (bf16)
+            // the split dS, element by element, into Th / Tl[query][key] (bf16).  (A packed
+            // [key][query] word per key tile read back by ds_read_b64_tr_b16 measured no faster on
+            // the bf16 path: 26.5 vs 26.4 us at cfg3, round 6)
             const unsigned hw[4] = {ds2.h0, ds2.h0 >> 16, ds2.h1, ds2.h1 >> 16};
             const unsigned lw[4] = {ds2.l0, ds2.l0 >> 16, ds2.l1, ds2.l1 >> 16};
 #pragma unroll
@@ -971,33 +989,17 @@ struct Bwd {
                 Th[(4 * g + r) * TLD2 + kt * 16 + c] = (unsigned short)hw[r];
                 if (!BF) Tl[(4 * g + r) * TLD2 + kt * 16 + c] = (unsigned short)lw[r];
             }
-            }
         }
         // dQ += dS K with the query on the lane: the transposed 16 x 64 dS parts, already split,
         // come back as packed words (keys 4g .. 4g+3 of each key tile, one 8-byte read per part)
         wave_lds_sync();
         S2 tq[NT];
         typedef __attribute__((address_space(3))) u32x2 lu32x2;
-        if constexpr (TRX) {
-            // ds_read_b64_tr_b16: lane 4q+p of group g addresses key row kt*16 + 4g + q, queries
-            // 4p .. 4p+3; lane c of the group receives query column c of those 4 key rows -- dS[query
-            // c][keys 4g .. 4g+3], the A operand of dQ += dS K (EXEC is full here: no divergence)
-            typedef __attribute__((address_space(3))) s16x4 ls16x4;
 #pragma unroll
-            for (int kt = 0; kt < NT; ++kt) {
-                const int e = (kt * 16 + 4 * g + (c >> 2)) * 4 + (c & 3);
-                const u32x2 hh = __builtin_bit_cast(u32x2, __builtin_amdgcn_ds_read_tr16_b64_v4i16((ls16x4*)Tr + e));
-                const u32x2 ll = BF ? u32x2{0u, 0u}
-                                    : __builtin_bit_cast(u32x2, __builtin_amdgcn_ds_read_tr16_b64_v4i16((ls16x4*)Tr + CH * 4 + e));
-                tq[kt] = S2{hh[0], hh[1], ll[0], ll[1]};
-            }
-        } else {
-#pragma unroll
-            for (int kt = 0; kt < NT; ++kt) {
-                const u32x2 hh = *reinterpret_cast<const lu32x2*>(Th + c * TLD2 + kt * 16 + 4 * g);
-                const u32x2 ll = BF ? u32x2{0u, 0u} : *reinterpret_cast<const lu32x2*>(Tl + c * TLD2 + kt * 16 + 4 * g);
-                tq[kt] = S2{hh[0], hh[1], ll[0], ll[1]};
-            }
+        for (int kt = 0; kt < NT; ++kt) {
+            const u32x2 hh = *reinterpret_cast<const lu32x2*>(Th + c * TLD2 + kt * 16 + 4 * g);
+            const u32x2 ll = BF ? u32x2{0u, 0u} : *reinterpret_cast<const lu32x2*>(Tl + c * TLD2 + kt * 16 + 4 * g);
+            tq[kt] = S2{hh[0], hh[1], ll[0], ll[1]};
         }
         wave_lds_sync();
         floatx4 dq = zero4();
@@ -1020,7 +1022,7 @@ struct Bwd {
 // waves per SIMD of the short backward by register need (scripts/resusage.py, fp32 path; the bf16
 // instances need fewer): KV frees the V rows and the dV accumulators
 template <bool PREV, bool DSN, bool KV>
-constexpr int bwd_short_waves() { return PREV ? (KV ? 3 : 2) : (KV && !DSN) ? MEP_BWD_WAVES_KV : MEP_BWD_WAVES; }
+constexpr int bwd_short_waves() { return PREV ? 2 : (KV && !DSN) ? MEP_BWD_WAVES_KV : MEP_BWD_WAVES; }
 
 
 template <bool PREV, bool DSN, bool BF, bool KV>

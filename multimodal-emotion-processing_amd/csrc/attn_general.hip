@@ -79,13 +79,15 @@ __global__ __launch_bounds__(GEN_THREADS) void k_attn_gen_fwd(const mep_attn_gen
             mx = fmaxf(mx, s);
         }
         mx = block_reduce<true>(mx, red);
-        float sum = 0.f;
+        float sum = 0.f, rs = 0.f;
         for (int k = tid; k < Tk; k += GEN_THREADS) {
             const float p = expf(sbuf[k] - mx);                  // softmax: exp(s - max), s - max exact
             sbuf[k] = p;
             sum += p;
+            if (sp) rs = fmaf(p, sp[srow + k], rs);
         }
         sum = block_reduce<false>(sum, red);
+        if (sp) rs = block_reduce<false>(rs, red);
         const float inv = 1.0f / sum;
         // att @ v: thread e < hd sums its output column over the keys in order
         if (tid < hd) {
@@ -96,6 +98,8 @@ __global__ __launch_bounds__(GEN_THREADS) void k_attn_gen_fwd(const mep_attn_gen
         if (tid == 0) {
             stats[2 * ((b * d.H + h) * Tq + q)] = mx;            // raw (max, 1/sum)
             stats[2 * ((b * d.H + h) * Tq + q) + 1] = inv;
+            // residual scores: the row's P-weighted mean of S_prev in the stats' tail (attn.hip)
+            if (sp) stats[2 * d.B * d.H * Tq + (b * d.H + h) * Tq + q] = rs * inv;
         }
     }
 }
@@ -149,6 +153,7 @@ __global__ __launch_bounds__(GEN_THREADS) void k_attn_gen_bwd(const mep_attn_gen
             const int64_t si = ((int64_t)(b * d.H + h) * Tq + q) * Tk + kc;
             const float mx = stats[2 * ((b * d.H + h) * Tq + q)];
             const float inv = stats[2 * ((b * d.H + h) * Tq + q) + 1];
+            const float rp = sp ? stats[2 * d.B * d.H * Tq + (b * d.H + h) * Tq + q] : 0.f;
             float dot = 0.f, dp = 0.f;
 #pragma unroll
             for (int e = 0; e < HDP; ++e) {
@@ -158,9 +163,15 @@ __global__ __launch_bounds__(GEN_THREADS) void k_attn_gen_bwd(const mep_attn_gen
             const float s = gen_score(g, dot, c, sp, si, b, q, kc);
             const float att = kok ? expf(s - mx) * inv : 0.f;
             float ds = att * (dp - delta);
-            if (dsn && kok) ds += dsn[si];                       // gradient on the post-mask scores output
+            // d / dc = sum dS * S_prev, the softmax part against S_prev - rp (its row sum is 0:
+            // attn.hip Bwd::tile), the gradient on the post-mask scores against S_prev itself
+            if (sp && kok) dc_acc = fmaf(ds, sp[si] - rp, dc_acc);
+            if (dsn && kok) {
+                const float gn = dsn[si];                        // gradient on the post-mask scores output
+                ds += gn;
+                if (sp) dc_acc = fmaf(gn, sp[si], dc_acc);
+            }
             if (dsp && kok) dsp[si] = c * ds;                    // d(c * scores) / d scores
-            if (sp && kok) dc_acc = fmaf(ds, sp[si], dc_acc);    // d / dc: sum dS * scores
             const float gs = kok ? __fdiv_rn(ds, g.scale) : 0.f; // through q k^T / sqrt(hd)
 #pragma unroll
             for (int e = 0; e < HDP; ++e) {

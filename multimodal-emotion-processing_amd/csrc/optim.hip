@@ -82,6 +82,20 @@ __global__ __launch_bounds__(OPT_THREADS) void k_clip_adam(float* __restrict__ p
                                                            const float* __restrict__ hyper,
                                                            const int* __restrict__ step, float* gnorm_out,
                                                            int decoupled) {
+    const int64_t gid = (int64_t)blockIdx.x * OPT_THREADS + threadIdx.x;
+    const int64_t stride = (int64_t)gridDim.x * OPT_THREADS;
+    // the thread's first float4 of segment 0 is loaded before the norm reduction: the update's
+    // operands do not depend on the norm, so their latency runs under the partial-sum loads (the
+    // launch is sized to about one float4 per thread, so this is most of the update's reads)
+    float4 P0 = {}, G0 = {}, M0 = {}, V0 = {};
+    const bool pre = segs.n > 0 && (segs.off[0] & 3) == 0 && gid < (segs.len[0] >> 2);
+    if (pre) {
+        const int64_t j = segs.off[0] + 4 * gid;
+        P0 = ldg4(G<float>(reinterpret_cast<uint64_t>(p)) + j);
+        G0 = ldg4(G<float>(reinterpret_cast<uint64_t>(g)) + j);
+        M0 = ldg4(G<float>(reinterpret_cast<uint64_t>(m)) + j);
+        V0 = ldg4(G<float>(reinterpret_cast<uint64_t>(v)) + j);
+    }
     // every workgroup sums the partials in the same fixed order (lane-strided, then the wave's
     // DPP tree, then the 4 waves in order): identical totals, no grid barrier
     __shared__ float red[OPT_THREADS / 64];
@@ -120,8 +134,6 @@ __global__ __launch_bounds__(OPT_THREADS) void k_clip_adam(float* __restrict__ p
     k.wd = wd;
     k.eps = hyper[3];
     k.decoupled = decoupled;
-    const int64_t gid = (int64_t)blockIdx.x * OPT_THREADS + threadIdx.x;
-    const int64_t stride = (int64_t)gridDim.x * OPT_THREADS;
     for (int si = 0; si < segs.n; ++si) {
         const int64_t off = segs.off[si], n = segs.len[si];
         const int64_t n4 = (off & 3) == 0 ? n >> 2 : 0;
@@ -131,7 +143,12 @@ __global__ __launch_bounds__(OPT_THREADS) void k_clip_adam(float* __restrict__ p
             gfloat* gp = G<float>(reinterpret_cast<uint64_t>(g)) + j;
             gfloat* mp = G<float>(reinterpret_cast<uint64_t>(m)) + j;
             gfloat* vp = G<float>(reinterpret_cast<uint64_t>(v)) + j;
-            float4 P4 = ldg4(pp), G4 = ldg4(gp), M4 = ldg4(mp), V4 = ldg4(vp);
+            float4 P4, G4, M4, V4;
+            if (si == 0 && i == gid) {   // prefetched above (pre holds exactly when this runs)
+                P4 = P0; G4 = G0; M4 = M0; V4 = V0;
+            } else {
+                P4 = ldg4(pp); G4 = ldg4(gp); M4 = ldg4(mp); V4 = ldg4(vp);
+            }
             adam_elem(P4.x, G4.x, M4.x, V4.x, k);
             adam_elem(P4.y, G4.y, M4.y, V4.y, k);
             adam_elem(P4.z, G4.z, M4.z, V4.z, k);

@@ -195,6 +195,10 @@ __global__ __launch_bounds__(256) void k_head(mep_head_desc d) {
     // classifiers (Multi_ATTN.classifier, no bias): every thread takes columns k = tid + 256 j
     // of all 2 NC outputs (all loads of a column issued together), then one block reduction
     __shared__ float s_red[2][4][2 * NCMAX];
+    // F <= 256 HEAD_KU (one pass, every configuration of the three models): the classifier
+    // columns stay in registers from the classifier pass to the dpooled pass (no second L2 read)
+    const bool one_pass = F <= 256 * HEAD_KU;
+    float kw0[HEAD_KU][NU], kw1[HEAD_KU][NU];
     for (int rr = 0; rr < rows; ++rr) {
         const int b = r0 + rr;
         const gfloat* p0 = G<const float>(d.pooled0) + (int64_t)b * F;
@@ -218,6 +222,15 @@ __global__ __launch_bounds__(256) void k_head(mep_head_desc d) {
                     w0[u][n] = wc0[o];
                     w1[u][n] = wc1[o];
                 }
+            }
+            if (rr == 0 && k0 == 0) {
+#pragma unroll
+                for (int u = 0; u < HEAD_KU; ++u)
+#pragma unroll
+                    for (int n = 0; n < NU; ++n) {
+                        kw0[u][n] = w0[u][n];
+                        kw1[u][n] = w1[u][n];
+                    }
             }
 #pragma unroll
             for (int u = 0; u < HEAD_KU; ++u) {
@@ -404,14 +417,24 @@ __global__ __launch_bounds__(256) void k_head(mep_head_desc d) {
         gfloat* dp1 = G<float>(d.dpooled1) + (int64_t)b * F;
         for (int k0 = 0; k0 < F; k0 += 256 * HEAD_KU) {
             float w0[HEAD_KU][NCMAX], w1[HEAD_KU][NCMAX];
+            if (one_pass) {
 #pragma unroll
-            for (int u = 0; u < HEAD_KU; ++u) {   // all loads of the pass in flight at once
-                const int k = min(k0 + 256 * u + (int)threadIdx.x, F - 1);
+                for (int u = 0; u < HEAD_KU; ++u)
 #pragma unroll
-                for (int n = 0; n < NU; ++n) {
-                    const int64_t o = (int64_t)min(n, NC - 1) * F + k;
-                    w0[u][n] = wc0[o];
-                    w1[u][n] = wc1[o];
+                    for (int n = 0; n < NU; ++n) {
+                        w0[u][n] = kw0[u][n];
+                        w1[u][n] = kw1[u][n];
+                    }
+            } else {
+#pragma unroll
+                for (int u = 0; u < HEAD_KU; ++u) {   // all loads of the pass in flight at once
+                    const int k = min(k0 + 256 * u + (int)threadIdx.x, F - 1);
+#pragma unroll
+                    for (int n = 0; n < NU; ++n) {
+                        const int64_t o = (int64_t)min(n, NC - 1) * F + k;
+                        w0[u][n] = wc0[o];
+                        w1[u][n] = wc1[o];
+                    }
                 }
             }
 #pragma unroll

@@ -171,7 +171,7 @@ class RealformerPlan:
         blk['dKV2'] = torch.zeros(nk, 2 * D, **f32)
         blk['dKVin'] = torch.zeros(nk, D, **f32)
         blk['estat'] = torch.zeros(nq, 4, **f32)
-        blk['astat'] = torch.zeros(R, H, Tq, 2, **f32)
+        blk['astat'] = torch.zeros(3 * R * H * Tq, **f32)   # (max, 1/sum) per row, then the residual rows' S_prev means
         blk['partial'] = torch.zeros(cdiv(nq, _lib.rf_bwd_rows(self.rfw)), _lib.rf_partial_stride(D, FD), **f32)
         if i < nl - 1 or not sp.head:
             blk['OUT'] = torch.zeros(nq, D, **f32)

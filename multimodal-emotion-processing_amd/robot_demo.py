@@ -176,7 +176,7 @@ class RobotPlan:
                 b['K'], b['V'] = torch.zeros(nk, D, **f32), torch.zeros(nk, D, **f32)
                 b['F1'] = torch.zeros(nq, FD, **f32)
                 b['estat'] = torch.zeros(nq, 4, **f32)
-                b['astat'] = torch.zeros(B, H, Tq, 2, **f32)
+                b['astat'] = torch.zeros(3 * B * H * Tq, **f32)   # (max, 1/sum) per row, then the residual rows' S_prev means
                 if i < nl - 1:
                     b['S'] = torch.zeros(B, H, Tq, Tk, **f32)
                 self.blocks.append(b)

@@ -134,7 +134,8 @@ def attn_costs(plan, a):
 
     def fwd_bytes(d):
         s_bytes = 4 * d.H * d.Tq * d.Tk * d.B
-        return (a * d.B * d.Tq * D + 8 * d.B * d.H * d.Tq +
+        stat = 12 if d.s_prev else 8   # (max, 1/sum) per row, + the S_prev mean (mep.h, ABI 6)
+        return (a * d.B * d.Tq * D + stat * d.B * d.H * d.Tq +
                 s_bytes * ((1 if d.s_prev else 0) + (1 if d.s_out else 0)))
     f = sum(4 * d.B * d.Tq * d.Tk * D for d in fwd)
     shared = _distinct([rows(d.q, d.B) for d in fwd] + [rows(d.k, d.B) for d in fwd] + [rows(d.v, d.B) for d in fwd] +
@@ -146,7 +147,8 @@ def attn_costs(plan, a):
         s_bytes = 4 * d.H * d.Tq * d.Tk * d.B
         dkv = 1 if bd.dk.ptr == bd.dv.ptr else 2
         chained = s_bytes * ((1 if bd.ds_next else 0) + (2 if d.s_prev else 0))
-        return a * d.B * (4 * d.Tq * D + dkv * d.Tk * D) + 8 * d.B * d.H * d.Tq + chained
+        stat = 12 if d.s_prev else 8
+        return a * d.B * (4 * d.Tq * D + dkv * d.Tk * D) + stat * d.B * d.H * d.Tq + chained
     f = sum(10 * bd.f.B * bd.f.Tq * bd.f.Tk * D for bd in bwd)
     shared = _distinct([rows(bd.f.q, bd.f.B) for bd in bwd] + [rows(bd.f.k, bd.f.B) for bd in bwd] +
                        [rows(bd.f.v, bd.f.B) for bd in bwd] + [(bd.f.mask, 4 * bd.f.B * bd.f.Tk) for bd in bwd])

@@ -68,7 +68,7 @@ class _BlockFn(torch.autograd.Function):
         f = dict(dtype=torch.float32, device=dev)
         X, XP, Z, out = (torch.empty(B, Tq, D, **f) for _ in range(4))
         S = torch.empty(B, H, Tq, Tk, **f)
-        astat = torch.empty(B, H, Tq, 2, **f)
+        astat = torch.empty(3 * B * H * Tq, **f)   # (max, 1/sum) per row, then S_prev means (mep.h)
         estat = torch.empty(B * Tq, 2, **f)
         sp = _c(s_prev) if s_prev is not None else None
         ad = AttnDesc(q=crows(q, Tq, D), k=crows(k, Tk, D), v=crows(v, Tk, D), x=crows(X, Tq, D),
@@ -293,7 +293,7 @@ class _RFBlockFn(torch.autograd.Function):
         KV = torch.empty(B, Tk, 2 * D, **f)
         F1 = torch.empty(B, Tq, FD, **f)
         S = torch.empty(B, H, Tq, Tk, **f)
-        astat = torch.empty(B, H, Tq, 2, **f)
+        astat = torch.empty(3 * B * H * Tq, **f)   # (max, 1/sum) per row, then S_prev means (mep.h)
         estat = torch.empty(B * Tq, 4, **f)
         sp = _c(s_prev) if s_prev is not None else None
         kv = lambda t, which: _lib.Rows(ptr=t.data_ptr() + 4 * which * D, sB=Tk * 2 * D, sT=2 * D, T=Tk)  # noqa: E731

@@ -433,7 +433,7 @@ class TriModalPlan:
             # bf16 copy of the block output (fp32 in the pooled tensor) for the next layer's q
             blk['Qh'] = torch.zeros(nq, D, **self.act)
         blk['estat'] = torch.zeros(nq, 2, **f32)
-        blk['astat'] = torch.zeros(B, H, Tq, 2, **f32)
+        blk['astat'] = torch.zeros(3 * B * H * Tq, **f32)   # (max, 1/sum) per row, then the residual rows' S_prev means
         blk['dKV'] = torch.zeros(nk, D, **self.act)
         blk['ln_partial'] = torch.zeros(cdiv(nq, 16), 2, D, **f32)   # one row per 16-token wave
         if sp.drop_p > 0:

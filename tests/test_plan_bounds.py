@@ -109,7 +109,7 @@ def _attn(c, d, tag='attn'):
     c.inside(tag + '.s_prev', d.s_prev, S)
     c.inside(tag + '.s_out', d.s_out, S)
     c.inside(tag + '.c', d.c, F)
-    c.inside(tag + '.stats', d.stats, d.B * d.H * d.Tq * 2 * F)
+    c.inside(tag + '.stats', d.stats, d.B * d.H * d.Tq * (3 if d.s_prev else 2) * F)   # + S_prev means (mep.h)
 
 
 def _attn_bwd(c, d):
