@@ -46,7 +46,7 @@ for s in ${STAGES:-tests smoke bench}; do
       step smoke 300 python3 -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')";;
     bench)
       for c in $CFGS; do
-        step bench_$c 400 python3 bench.py $(bargs ${c%_bf16}) $BARGS
+        step bench_$c 400 python3 bench.py $(bargs $c) $BARGS
         cp $OUT/bench_$c.log $OUT/bench_$c.json
       done;;
     prof)
