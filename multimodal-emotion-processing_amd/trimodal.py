@@ -288,15 +288,72 @@ def make_wgrad(items, dev, tok_per_split=None, bf16=False):
                                bf16=(_lib.BF16_OPS | _lib.BF16_STORE) if bf16 else 0))
         off += ns * N * ktot
         rmax = max(rmax, cdiv(N * ktot, 256))
+    # mep_wgrad_fused: every (item, column group) needs at least one arrival -- an item without
+    # tokens gets one empty segment per column group (a zero slot)
+    ncgs = [wgrad_geometry(N, sum(b[1] for b in bs), bf16)[2] for (_, N, _, bs, _) in items]
+    seen = {(i, cg) for b in segs for (i, cg, _, _, _) in b}
+    segs = list(segs) + [[(i, cg, 0, 0, 0)] for i, ncg in enumerate(ncgs) for cg in range(ncg) if (i, cg) not in seen]
     assert len(descs) < 2 ** 23 and all(cg < 256 for b in segs for (_, cg, _, _, _) in b)
     offs, flat = [0], []
     for b in segs:
         for (i, cg, t0, t1, s) in b:
             flat += [(i << 8) | cg, t0, t1, s]
         offs.append(offs[-1] + len(b))
-    arr = DescArray(WgradDesc, descs, dev, tail=offs + flat)
+    # the fused launch's map tail: column-group offsets per descriptor, then arrivals per group
+    cg_off = [sum(ncgs[:i]) for i in range(len(ncgs))]
+    arrivals = [0] * sum(ncgs)
+    for b in segs:
+        for (i, cg, _, _, _) in b:
+            arrivals[cg_off[i] + cg] += 1
+    arr = DescArray(WgradDesc, descs, dev, tail=offs + flat + cg_off + arrivals)
     arr.prec = _lib.PREC_BF16 if bf16 else 0   # the mep_wgrad instance (launch reads it)
+    arr.n_cg = len(arrivals)
+    arr.tickets = torch.zeros(max(1, len(arrivals)), dtype=torch.int32, device=dev)   # left zero by every launch
     return ws, arr, len(segs), rmax
+
+
+# mep_wgrad_fused: the split sums, head-parameter sums and column sums inside the weight-gradient
+# launch (0: mep_wgrad + mep_reduce_grads, the two-launch form; A/B runs)
+WGRAD_FOLD = _lib.switch('MEP_WGRAD_FOLD', '1') != '0'
+
+
+def fold_jobs(n_colsum, colsum_tiles, head):
+    """jobs of a fused launch that are not split sums: head-parameter sums, then column sums"""
+    hb = _lib.lib().mep_reduce_grads_grid(0, 0, 0, 0, ctypes.byref(head)) if head is not None else 0
+    return hb + (n_colsum * colsum_tiles if n_colsum else 0)
+
+
+def fold_job_wg(jobs, n_wg, bf16):
+    """job workgroups of a fused launch: the workgroup slots the weight-gradient workgroups leave
+    free (the launch is sized to be resident at once), at least 16, at most one per job"""
+    return 0 if jobs <= 0 else min(jobs, max(wg_target(bf16) - n_wg, 16))
+
+
+def fold_parts(arr, n_wg, n_colsum, colsum_tiles, head):
+    """norm partials a fused launch writes (mep_clip_adam_ext's n_ext): one per column group and
+    job workgroup"""
+    return arr.n_cg + fold_job_wg(fold_jobs(n_colsum, colsum_tiles, head), n_wg, arr.prec != 0)
+
+
+def wgrad_fused(arr, n_wg, colsum, colsum_tiles, head, head_grads, norm, stream):
+    """one mep_wgrad_fused launch: weight gradients + every gradient reduction of the step
+    (colsum: DescArray of ColsumDesc; head: HeadDesc or None; norm: the (workspace, step, hyper)
+    pointers of the folded norm pass or Nones).  Timed as the mep_wgrad launch."""
+    if arr.n == 0 or n_wg <= 0:
+        return
+    ncs = colsum.n if colsum is not None else 0
+    jobs = fold_jobs(ncs, colsum_tiles, head)
+    hg = [int(x) for x in head_grads] if head is not None else [0] * 8
+    nv = [int(x.value or 0) if isinstance(x, ctypes.c_void_p) else int(x or 0) for x in norm]
+    f = _lib.WgradFold(tickets=arr.tickets.data_ptr(), n_cg=arr.n_cg, n_job_wg=fold_job_wg(jobs, n_wg, arr.prec != 0),
+                       colsum=colsum.dev.data_ptr() if ncs else 0, n_colsum=ncs, colsum_tiles=colsum_tiles if ncs else 0,
+                       head=head if head is not None else HeadDesc(), has_head=int(head is not None),
+                       g_trans=hg[0], g_ln_w=hg[1], g_ln_b=hg[2], g_wo=hg[3], g_bo=hg[4], g_wc0=hg[5], g_wc1=hg[6],
+                       loss=hg[7], norm=nv[0], step=nv[1], hyper=nv[2])
+    fn = _lib.lib().mep_wgrad_fused
+    ptr, n, prec = arr.ptr, arr.n, arr.prec
+    _lib._run('mep_wgrad', lambda: _lib.check(fn(ptr, n, int(n_wg), prec, ctypes.byref(f), _lib.stream_ptr(stream)),
+                                              'mep_wgrad_fused'), stream)
 
 
 def rows(t, T, sB, sT, off=0):
@@ -788,6 +845,12 @@ class TriModalPlan:
         launch('mep_sum_rows', self.d_sum, self.t_sum, stream)
         if sp.unify_norm:
             launch('mep_layernorm_bwd', self.d_ulnb, cdiv(max(self.ntok.values()), 64), stream)
+        if WGRAD_FOLD:
+            # weight gradients, their split sums, the LayerNorm / residual-coefficient column sums
+            # and the head parameter sums: one launch
+            wgrad_fused(self.d_wgrad, self.t_wgrad, self.d_colsum, self.t_colsum, self.head, self.head_grads,
+                        _norm_args(self), stream)
+            return
         launch('mep_wgrad', self.d_wgrad, self.t_wgrad, stream)
         # weight-gradient split sums, LayerNorm / residual-coefficient column sums and the head
         # parameter sums: one launch
@@ -800,6 +863,8 @@ class TriModalPlan:
 
     def reduce_grid(self):
         """blocks of the backward's mep_reduce_grads launch (the optimizer's folded norm partials)"""
+        if WGRAD_FOLD:
+            return fold_parts(self.d_wgrad, self.t_wgrad, self.d_colsum.n, self.t_colsum, self.head)
         red, t_red = self._reduce_args()
         return _lib.lib().mep_reduce_grads_grid(red.n, t_red, self.d_colsum.n, self.t_colsum, ctypes.byref(self.head))
 
@@ -864,14 +929,20 @@ class TriModalPlan:
         for i in reversed(range(nl)):
             launch('mep_block_epi_bwd', self.d_epib[i], self.t_epi[i], stream, threads=sp.D | self.prec)
             if i == 0:
-                launch('mep_wgrad', da, ta, stream)
-                _lib.call('mep_reduce_grads', da.ptr, da.n, ra, ca.ptr, ca.n, self.t_colsum if ca.n else 0,
-                          ctypes.byref(self.head), *self.head_grads, None, None, None, stream=stream)
+                if WGRAD_FOLD:
+                    wgrad_fused(da, ta, ca, self.t_colsum, self.head, self.head_grads, (None, None, None), stream)
+                else:
+                    launch('mep_wgrad', da, ta, stream)
+                    _lib.call('mep_reduce_grads', da.ptr, da.n, ra, ca.ptr, ca.n, self.t_colsum if ca.n else 0,
+                              ctypes.byref(self.head), *self.head_grads, None, None, None, stream=stream)
                 bucket_a_done()
             launch('mep_attn_bwd', self.d_attnb[i], self.t_attnb[i], stream, threads=self.f_attnb[i] | self.prec)
         launch('mep_sum_rows', self.d_sum, self.t_sum, stream)
         if sp.unify_norm:
             launch('mep_layernorm_bwd', self.d_ulnb, cdiv(max(self.ntok.values()), 64), stream)
+        if WGRAD_FOLD:
+            wgrad_fused(db, tb, cb, self.t_colsum, None, None, (None, None, None), stream)
+            return
         launch('mep_wgrad', db, tb, stream)
         _lib.call('mep_reduce_grads', db.ptr, db.n, rb, cb.ptr, cb.n, self.t_colsum if cb.n else 0, None,
                   0, 0, 0, 0, 0, 0, 0, 0, None, None, None, stream=stream)
