@@ -32,7 +32,7 @@ extern "C" {
 #endif
 
 #define MEP_EINVAL (-1000)
-#define MEP_ABI_VERSION 7
+#define MEP_ABI_VERSION 6
 
 typedef void* mep_stream_t; /* a hipStream_t */
 
@@ -584,36 +584,6 @@ int mep_reduce_grads(const mep_wgrad_desc* wgrad, int n_wgrad, int wgrad_tiles, 
  * >= 1024 + mep_reduce_grads_grid(..) floats; step / hyper as there).  norm = 0: no norm pass. */
 int mep_reduce_grads_grid(int n_wgrad, int wgrad_tiles, int n_colsum, int colsum_tiles, const mep_head_desc* head);
 int mep_head_partial_stride(int NC);
-
-/* mep_wgrad with the step's gradient reductions in the same launch (ABI 7; replaces mep_wgrad +
- * mep_reduce_grads, the weight-gradient half of cmu-mosei/run.py:367 loss.backward()):
- * - every segment's partial slot is stored write-through (agent-coherent stores) and the
- *   workgroup then draws an arrival ticket for its (descriptor, column group); the last of the
- *   group's arrivals sums the group's slots in slot order -- mep_wgrad_reduce's arithmetic, so dW
- *   is bitwise the two-launch result -- and writes dW_i;
- * - n_job_wg workgroups after the n_wg weight-gradient ones run the jobs of mep_reduce_grads that
- *   are not split sums: the fusion-head parameter sums (has_head) then the column sums, job j on
- *   job workgroup j % n_job_wg, in order;
- * - the int32 map after mep_wgrad's segment list holds n_desc column-group offsets (group g of
- *   descriptor d has index cg_off[d] + g < n_cg) then n_cg arrival counts (the segments of
- *   each group);
- * - tickets: n_cg int32, zero before the first launch; every launch leaves them zero.  No
- *   workgroup waits for another, so residency is not required;
- * - norm != 0 (single-process steps): column group c writes the sum of squares of its dW to
- *   norm[1024 + c], job workgroup j its jobs' to norm[1024 + n_cg + j] (mep_clip_adam_ext's
- *   n_ext = n_cg + n_job_wg) and workgroup 0 advances *step (mep_reduce_grads' norm contract). */
-typedef struct {
-    uint64_t tickets;            /* int32 [n_cg]                                   */
-    int32_t  n_cg, n_job_wg;
-    uint64_t colsum;             /* device mep_colsum_desc [n_colsum]              */
-    int32_t  n_colsum, colsum_tiles;
-    mep_head_desc head;          /* used when has_head                              */
-    int32_t  has_head, _pad;
-    uint64_t g_trans, g_ln_w, g_ln_b, g_wo, g_bo, g_wc0, g_wc1, loss;   /* as mep_head_reduce */
-    uint64_t norm, step, hyper;  /* as mep_reduce_grads; norm = 0: no norm partials */
-} mep_wgrad_fold;
-int mep_wgrad_fused(const mep_wgrad_desc* descs, int n_desc, int n_wg, int flags, const mep_wgrad_fold* fold,
-                    mep_stream_t stream);
 
 /* multi_circle_loss per row (cmu-mosei/run.py:342-351) as a standalone op for callers that
  * compute the loss outside the model: row_loss[b] and dunit[b, :] = d row_loss[b] / d logits[b, :].

@@ -143,14 +143,6 @@ class HeadDesc(ctypes.Structure):
                 ('mean_div', i32), ('_pad', i32), ('scale', u64)]
 
 
-class WgradFold(ctypes.Structure):
-    """mep_wgrad_fold (include/mep.h): the in-launch reductions of mep_wgrad_fused"""
-    _fields_ = [('tickets', u64), ('n_cg', i32), ('n_job_wg', i32), ('colsum', u64), ('n_colsum', i32),
-                ('colsum_tiles', i32), ('head', HeadDesc), ('has_head', i32), ('_pad', i32),
-                ('g_trans', u64), ('g_ln_w', u64), ('g_ln_b', u64), ('g_wo', u64), ('g_bo', u64), ('g_wc0', u64),
-                ('g_wc1', u64), ('loss', u64), ('norm', u64), ('step', u64), ('hyper', u64)]
-
-
 class RfEpiDesc(ctypes.Structure):
     _fields_ = [('q', Rows), ('x', Rows), ('xp', Rows), ('h', Rows), ('f1', Rows), ('f', Rows), ('out', Rows),
                 ('wp', u64), ('w1', u64), ('b1', u64), ('w2', u64), ('b2', u64),
@@ -275,8 +267,7 @@ STRUCTS = {'mep_rows': Rows, 'mep_gemm_desc': GemmDesc, 'mep_gemm_sum_desc': Gem
            'mep_epi_bwd_desc': EpiBwdDesc, 'mep_ln_desc': LnDesc, 'mep_colsum_desc': ColsumDesc,
            'mep_sum_desc': SumDesc, 'mep_pool_desc': PoolDesc, 'mep_head_desc': HeadDesc, 'mep_seg': Seg,
            'mep_rf_epi_desc': RfEpiDesc, 'mep_rf_epi_bwd_desc': RfEpiBwdDesc, 'mep_rf_head_desc': RfHeadDesc,
-           'mep_sweep_desc': SweepDesc, 'mep_window_desc': WindowDesc, 'mep_wsplit_desc': WsplitDesc,
-           'mep_wgrad_fold': WgradFold}
+           'mep_sweep_desc': SweepDesc, 'mep_window_desc': WindowDesc, 'mep_wsplit_desc': WsplitDesc}
 
 P = ctypes.c_void_p
 # name -> argtypes (all return int)
@@ -298,7 +289,6 @@ SIGNATURES.update({
     'mep_reduce_grads_grid': [i32, i32, i32, i32, HP],
     'mep_wgrad_kt': [i32, i32],
     'mep_wgrad_occupancy': [i32],
-    'mep_wgrad_fused': [P, i32, i32, i32, ctypes.POINTER(WgradFold), P],
     'mep_circle_loss_fwd': [P, P, i32, i32, i32, P, P, P],
     'mep_circle_loss_bwd': [P, P, i32, i32, P, P],
     'mep_clip_adam': [P, P, P, P, P, i32, i64, P, P, P, P, i32, P],
@@ -324,7 +314,7 @@ SIGNATURES.update({
 })
 
 _LIB = None
-ABI_VERSION = 7   # include/mep.h MEP_ABI_VERSION
+ABI_VERSION = 6   # include/mep.h MEP_ABI_VERSION
 
 
 def lib():

@@ -611,9 +611,9 @@ MEP_DEV float wgrad_reduce_block(const mep_wgrad_desc& d, int bx) {
 // Column sums of a partial matrix (optim.hip k_colsum): block bx = 32 columns.  16-byte rows
 // (ld, n_cols multiples of 4, aligned): 8 lanes x 4 columns x 32 row groups, each thread's rows
 // loaded at once, the 32 groups combined in a fixed order; else 32 columns x 8 row groups.
-MEP_DEV float colsum_block(const mep_colsum_desc& d, int bx, lfloat* lds) {
+MEP_DEV float colsum_block(const mep_colsum_desc& d, int bx) {
     if (bx * 32 >= d.n_cols) return 0.f;   // whole block
-    auto red = [&](int g, int c) -> lfloat& { return lds[g * 33 + c]; };
+    __shared__ float red[32][33];
     const bool v4 = (d.ld % 4 == 0) && (d.n_cols % 4 == 0) && (d.partial & 15) == 0;
     if (v4) {
         const int q = threadIdx.x & 7, g = threadIdx.x >> 3;
@@ -626,7 +626,7 @@ MEP_DEV float colsum_block(const mep_colsum_desc& d, int bx, lfloat* lds) {
                 s += *reinterpret_cast<const __attribute__((address_space(1))) f32x4*>(p + (int64_t)r * d.ld);
         }
 #pragma unroll
-        for (int e = 0; e < 4; ++e) red(g, 4 * q + e) = s[e];
+        for (int e = 0; e < 4; ++e) red[g][4 * q + e] = s[e];
     } else {
         const int cl = threadIdx.x & 31, g = threadIdx.x >> 5;
         const int c = bx * 32 + cl;
@@ -636,7 +636,7 @@ MEP_DEV float colsum_block(const mep_colsum_desc& d, int bx, lfloat* lds) {
 #pragma unroll 8
             for (int r = g; r < d.n_rows; r += 8) s += p[(int64_t)r * d.ld];
         }
-        red(g, cl) = s;
+        red[g][cl] = s;
     }
     __syncthreads();
     const int cl = threadIdx.x;
@@ -644,7 +644,7 @@ MEP_DEV float colsum_block(const mep_colsum_desc& d, int bx, lfloat* lds) {
     if (cl < 32 && c < d.n_cols) {
         float t = 0.f;
         const int ng = v4 ? 32 : 8;
-        for (int k = 0; k < ng; ++k) t += red(k, cl);
+        for (int k = 0; k < ng; ++k) t += red[k][cl];
         gfloat* o = G<float>(d.out) + c;
         const float v = (d.accumulate & 1) ? *o + t : t;
         *o = v;
@@ -652,124 +652,6 @@ MEP_DEV float colsum_block(const mep_colsum_desc& d, int bx, lfloat* lds) {
     }
     return 0.f;
 }
-
-// LDS scratch (floats) of the reduction bodies: colsum_block, head_reduce_block
-constexpr int COLSUM_LDS = 32 * 33;
-
-// ------------------------------------------------------------------ fusion-head parameter sums
-// (pool_head.hip k_head_reduce, mep_reduce_grads, the jobs of a folded mep_wgrad launch)
-constexpr int NCMAX = 16;
-
-struct HeadOff {
-    int wo, bo, lnw, lnb, trans, dl0, dl1, stride;
-};
-__host__ __device__ inline HeadOff head_off(int NC) {
-    HeadOff o;
-    o.wo = 0;
-    o.bo = o.wo + 2 * NC * NC;
-    o.lnw = o.bo + NC;
-    o.lnb = o.lnw + NC;
-    o.trans = o.lnb + NC;
-    o.dl0 = o.trans + NC * NC * NC;
-    o.dl1 = o.dl0 + NC;
-    o.stride = o.dl1 + NC;
-    return o;
-}
-
-struct HeadGrads {
-    float *g_trans, *g_lnw, *g_lnb, *g_wo, *g_bo, *g_wc0, *g_wc1, *loss;
-};
-
-// Sum of the per-row head partials.  Workgroups [0, nA32): 32 columns of the small-parameter
-// records each, 8 row groups per column (+ the batch loss in workgroup 0); workgroups after
-// that: 32 columns k of one classifier e, dWc_e[n][k] = sum_b dlogit_e[b][n] pooled_e[b][k] for
-// every n, rows split over 8 groups.  Fixed summation order (deterministic).
-MEP_DEV float head_reduce_block(const mep_head_desc& d, const HeadGrads& g, int bx, lfloat* lds) {
-    const int NC = d.NC, F = d.F, B = d.B;
-    const HeadOff o = head_off(NC);
-    const int nA = o.dl0;                 // everything before the dlogit records
-    const int nA32 = (nA + 31) / 32;
-    const int cl = threadIdx.x & 31, rg = threadIdx.x >> 5;
-    const gfloat* part = G<const float>(d.partial);
-    auto red = [&](int q, int n, int c) -> lfloat& { return lds[(q * NCMAX + n) * 33 + c]; };
-    if ((int)bx < nA32) {
-        const int i = bx * 32 + cl;
-        float s = 0.f;
-        if (i < nA) {
-#pragma unroll 8
-            for (int b = rg; b < B; b += 8) s += part[(int64_t)b * o.stride + i];
-        }
-        red(rg, 0, cl) = s;
-        float ls = 0.f, sq = 0.f;
-        if (bx == 0)
-            for (int b = threadIdx.x; b < B; b += 256) ls += G<const float>(d.row_loss)[b];
-        __syncthreads();
-        if (rg == 0 && i < nA) {
-            float t = 0.f;
-#pragma unroll
-            for (int k = 0; k < 8; ++k) t += red(k, 0, cl);
-            float* dst;
-            if (i < o.bo) dst = g.g_wo + (i - o.wo);
-            else if (i < o.lnw) dst = g.g_bo + (i - o.bo);
-            else if (i < o.lnb) dst = g.g_lnw + (i - o.lnw);
-            else if (i < o.trans) dst = g.g_lnb + (i - o.lnb);
-            else dst = g.g_trans + (i - o.trans);
-            *G<float>(reinterpret_cast<uint64_t>(dst)) = t;
-            sq = t * t;
-        }
-        if (bx == 0) {
-            ls = wave_sum(ls);
-            __syncthreads();
-            if ((threadIdx.x & 63) == 0) red(threadIdx.x >> 6, 1, 0) = ls;
-            __syncthreads();
-            if (threadIdx.x == 0)
-                *G<float>(reinterpret_cast<uint64_t>(g.loss)) = red(0, 1, 0) + red(1, 1, 0) + red(2, 1, 0) + red(3, 1, 0);
-        }
-        return sq;   // the loss is not a gradient
-    }
-    const int wb = bx - nA32;
-    const int nkb = (F + 31) / 32;
-    const int e = wb / nkb, k = (wb - e * nkb) * 32 + cl;
-    const float* pooled = reinterpret_cast<const float*>(e ? d.pooled1 : d.pooled0);
-    const int off = e ? o.dl1 : o.dl0;
-    float acc[NCMAX];
-#pragma unroll
-    for (int n = 0; n < NCMAX; ++n) acc[n] = 0.f;
-    // every load unconditional (clamped column and class): a load under a per-class branch is a
-    // basic block of its own with its own wait, so the row's loads ran one round trip each
-    const int kc = min(k, F - 1);
-#pragma unroll 4
-    for (int b = rg; b < B; b += 8) {
-        const float pk = pooled[(int64_t)b * F + kc];
-        const gfloat* pr = part + (int64_t)b * o.stride + off;
-#pragma unroll
-        for (int n = 0; n < NCMAX; ++n) {
-            const float x = pr[min(n, NC - 1)];
-            acc[n] = n < NC ? fmaf(x, pk, acc[n]) : acc[n];
-        }
-    }
-#pragma unroll
-    for (int n = 0; n < NCMAX; ++n) if (n < NC) red(rg, n, cl) = acc[n];
-    __syncthreads();
-    float sq = 0.f;
-    if (k < F) {
-        float* out = e ? g.g_wc1 : g.g_wc0;
-        for (int n = rg; n < NC; n += 8) {
-            float t = 0.f;
-#pragma unroll
-            for (int q = 0; q < 8; ++q) t += red(q, n, cl);
-            *G<float>(reinterpret_cast<uint64_t>(out + (int64_t)n * F + k)) = t;
-            sq += t * t;
-        }
-    }
-    return sq;
-}
-
-__host__ __device__ inline int head_reduce_blocks(const mep_head_desc& d) {
-    return (head_off(d.NC).dl0 + 31) / 32 + 2 * ((d.F + 31) / 32);
-}
-
-constexpr int HEAD_RED_LDS = 8 * NCMAX * 33;
 
 // clip + optimizer workspace (optim.hip): per-workgroup g^2 partials of the norm pass in
 // [0, OPT_NPART), the step's scalars at OPT_SCAL (lr / (1 - b1^t), sqrt(1 - b2^t)), and from

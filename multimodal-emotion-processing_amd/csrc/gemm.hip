@@ -203,11 +203,6 @@ MEP_DEV int wg_extent(const mep_rows& r, int T, int ntok, int width, int es = 4)
     return (int)min((int64_t)es * last, (int64_t)0x7fffffff);
 }
 
-// Cache-policy bit of a buffer access: sc1 -- stores write through to memory, loads miss this
-// CU's L1, so slots handed between workgroups of one launch need no release / acquire fences
-// (cdna_hip_programming.md section 6 Guideline 16, R1).
-constexpr int WT_SC1 = 16;
-
 constexpr int WG_INV = (int)0x80000000u;   // byte offset past every view: the buffer load returns 0
 
 // a view whose element offset is linear in the token, tok * step (contiguous rows, or T = 1)
@@ -216,8 +211,7 @@ MEP_DEV int wg_step(const mep_rows& r) { return (int)(r.T == 1 ? r.sB : r.sT); }
 
 // MEP_WG_TRACE (development builds, scripts/wg_trace.py): thread 0 of every workgroup stores the
 // real-time counter at phase k of its (last) segment into g_wg_trace[block][k]:
-// 0 start, 1 main loop start, 2 main loop end, 3 slot written, 4 ticket drawn, 5 reducer end,
-// 6 reducer loads back, 7 jobs done
+// 0 start, 1 main loop start, 2 main loop end, 3 slot written
 #ifdef MEP_WG_TRACE
 }  // namespace
 __device__ unsigned long long g_wg_trace[8192 * 8];
@@ -233,7 +227,7 @@ namespace {
 // LIN: every view of the item is linear in the token -- a lane's eight tokens of a k block sit at
 // fixed byte distances, so they are ONE per-lane base (VGPR) plus a wave-uniform per-token offset
 // (the load's SGPR soffset) and the column tile an immediate: no address arithmetic per token.
-template <int MT, int KT, int NPART, bool LIN, int WG_SLOTS, bool FOLD>
+template <int MT, int KT, int NPART, bool LIN, int WG_SLOTS>
 MEP_DEV void wgrad_task(const mep_wgrad_desc& d, int t_begin, int t_end, int slot, int kbase, lfloat* red) {
     // The bf16 path (one part) reads bf16 operand rows (MEP_BF16_STORE, 2-byte elements) as
     // column PAIRS: per 8-token block and 32-column tile a lane loads 4 dwords -- columns
@@ -465,165 +459,17 @@ MEP_DEV void wgrad_task(const mep_wgrad_desc& d, int t_begin, int t_end, int slo
     __syncthreads();
     const int kcnt = min(32 * KT, d.Ktot - kbase);
     gfloat* part = G<float>(d.partial) + (int64_t)slot * N * d.Ktot + kbase;
-    // FOLD: write-through stores (sc1), the slot is read by another workgroup of this launch
-    const auto rsP = __builtin_amdgcn_make_buffer_rsrc((void*)part, 0, 0x7fffffff, 0x00020000);
     for (int e = threadIdx.x; e < N * 32 * KT; e += WG_THREADS) {
         const int nn = e / (32 * KT), k = e - nn * (32 * KT);
-        const float v = red[nn * LDR + k] + red[BUF + nn * LDR + k];
-        if (k < kcnt) {
-            if constexpr (FOLD) __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rsP, 4 * (nn * d.Ktot + k), 0, WT_SC1);
-            else part[(int64_t)nn * d.Ktot + k] = v;
-        }
+        if (k < kcnt) part[(int64_t)nn * d.Ktot + k] = red[nn * LDR + k] + red[BUF + nn * LDR + k];
     }
     MEP_WG_STAMP(3);
 }
 
-// ---------------------------------------------------------------- in-launch reductions (mep_wgrad_fused)
-
-// the workgroup's sum of squares -> *dst (fixed order: the 4 waves in order); every thread
-MEP_DEV void wg_norm_partial(float sq, float* dst, lfloat* red) {
-    sq = wave_sum(sq);
-    __syncthreads();
-    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = sq;
-    __syncthreads();
-    if (threadIdx.x == 0) *G<float>(reinterpret_cast<uint64_t>(dst)) = (red[0] + red[1]) + (red[2] + red[3]);
-}
-
-// After a segment's slot is stored: draw the (descriptor, column group) ticket; the group's last
-// arrival sums its n_split slots in slot order (mep_wgrad_reduce's arithmetic) and writes dW.
-template <bool BF>
-MEP_DEV void wg_fold_group(const mep_wgrad_desc& d, int ci, int cg, int arrivals, const mep_wgrad_fold& f, lfloat* red) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every wave's slot stores are complete
-    __syncthreads();                                    // ... before the one ticket of the workgroup
-    MEP_G int* tk = G<int>(f.tickets) + ci;
-    if (threadIdx.x == 0)
-        red[0] = __int_as_float(__hip_atomic_fetch_add(tk, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-    __syncthreads();
-    MEP_WG_STAMP(4);
-    if (__float_as_int(red[0]) != arrivals - 1) { MEP_WG_STAMP(5); return; }
-    if (threadIdx.x == 0) __hip_atomic_store(tk, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // next launch
-    const int N = d.N, Ktot = d.Ktot;
-    const int ktm = wg_kt((N + 31) >> 5, BF);
-    const int kbase = 32 * ktm * cg;
-    const int kcnt = min(32 * ktm, Ktot - kbase);
-    const int nk = N * Ktot;
-    const auto rsP = __builtin_amdgcn_make_buffer_rsrc((void*)(d.partial + 4ull * kbase), 0, 0x7fffffff, 0x00020000);
-    float sq = 0.f;
-    // the slots of WF_U entries per thread are loaded WF_S at a time before their adds (one
-    // memory round trip per WF_S slots, not per slot and entry); the adds keep slot order
-    const WgOuts wo(d);
-    const bool acc = d.accumulate != 0;
-    auto put = [&](int n, int kk, float s) {
-        gfloat* o = wo.at(n, kbase + kk);
-        const float v = acc ? *o + s : s;
-        *o = v;
-        sq += v * v;
-    };
-    constexpr int WF_U = 6, WF_S = 4;   // cfg3 fp32: one batch of loads per reducer thread (6 x 4 slots)
-    if ((Ktot & 3) == 0 && (kcnt & 3) == 0) {   // 16-byte slot rows: 4 columns per entry
-        const int kc4 = kcnt >> 2, E = N * kc4;
-        for (int e0 = threadIdx.x; e0 < E; e0 += WF_U * WG_THREADS) {
-            f32x4 s[WF_U];
-            int off[WF_U];
-#pragma unroll
-            for (int u = 0; u < WF_U; ++u) {
-                const int e = min(e0 + u * WG_THREADS, E - 1), n = e / kc4;
-                off[u] = 4 * (n * Ktot + 4 * (e - n * kc4));
-                s[u] = f32x4{0.f, 0.f, 0.f, 0.f};
-            }
-            for (int s0 = 0; s0 < d.n_split; s0 += WF_S) {
-                f32x4 v[WF_S][WF_U];
-#pragma unroll
-                for (int q = 0; q < WF_S; ++q)
-#pragma unroll
-                    for (int u = 0; u < WF_U; ++u)
-                        v[q][u] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
-                            rsP, off[u] + 4 * min(s0 + q, d.n_split - 1) * nk, 0, WT_SC1));   // unconditional
-#pragma unroll
-                for (int q = 0; q < WF_S; ++q)
-#pragma unroll
-                    for (int u = 0; u < WF_U; ++u)
-                        s[u] = s0 + q < d.n_split ? s[u] + v[q][u] : s[u];
-            }
-            if (e0 == (int)threadIdx.x) MEP_WG_STAMP(6);
-#pragma unroll
-            for (int u = 0; u < WF_U; ++u) {
-                const int e = e0 + u * WG_THREADS;
-                if (e < E) {
-                    const int n = e / kc4, kk = 4 * (e - n * kc4);
-#pragma unroll
-                    for (int c = 0; c < 4; ++c) put(n, kk + c, s[u][c]);
-                }
-            }
-        }
-    } else {
-        const int E = N * kcnt;
-        for (int e0 = threadIdx.x; e0 < E; e0 += 4 * WF_U * WG_THREADS) {
-            float s[4 * WF_U];
-            int off[4 * WF_U];
-#pragma unroll
-            for (int u = 0; u < 4 * WF_U; ++u) {
-                const int e = min(e0 + u * WG_THREADS, E - 1), n = e / kcnt;
-                off[u] = 4 * (n * Ktot + (e - n * kcnt));
-                s[u] = 0.f;
-            }
-            for (int s0 = 0; s0 < d.n_split; s0 += WF_S) {
-                float v[WF_S][4 * WF_U];
-#pragma unroll
-                for (int q = 0; q < WF_S; ++q)
-#pragma unroll
-                    for (int u = 0; u < 4 * WF_U; ++u)
-                        v[q][u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
-                            rsP, off[u] + 4 * min(s0 + q, d.n_split - 1) * nk, 0, WT_SC1));   // unconditional
-#pragma unroll
-                for (int q = 0; q < WF_S; ++q)
-#pragma unroll
-                    for (int u = 0; u < 4 * WF_U; ++u)
-                        s[u] = s0 + q < d.n_split ? s[u] + v[q][u] : s[u];
-            }
-#pragma unroll
-            for (int u = 0; u < 4 * WF_U; ++u) {
-                const int e = e0 + u * WG_THREADS;
-                if (e < E) {
-                    const int n = e / kcnt;
-                    put(n, e - n * kcnt, s[u]);
-                }
-            }
-        }
-    }
-    if (f.norm) wg_norm_partial(sq, reinterpret_cast<float*>(f.norm) + OPT_EXT0 + ci, red);
-    MEP_WG_STAMP(5);
-}
-
-// A job workgroup of mep_wgrad_fused (blockIdx >= n_wg, in the workgroup slots the weight-gradient
-// workgroups leave free, so it runs beside them): the jobs of mep_reduce_grads that are not split
-// sums -- head-parameter sums, then column sums, mep_reduce_grads' bodies -- j, j + n_job_wg, ...
-// in order; its norm partial goes to norm[OPT_EXT0 + n_cg + j].  (Taking the jobs dynamically
-// in the weight-gradient workgroups as they finish measured slower: the workgroups that finish
-// first are few and the jobs' loads wait behind the others' streams.)
-MEP_DEV void wg_fold_jobs(const mep_wgrad_fold& f, int j, lfloat* red) {
-    const HeadGrads hg{reinterpret_cast<float*>(f.g_trans), reinterpret_cast<float*>(f.g_ln_w),
-                       reinterpret_cast<float*>(f.g_ln_b), reinterpret_cast<float*>(f.g_wo),
-                       reinterpret_cast<float*>(f.g_bo), reinterpret_cast<float*>(f.g_wc0),
-                       reinterpret_cast<float*>(f.g_wc1), reinterpret_cast<float*>(f.loss)};
-    const int hb = f.has_head ? head_reduce_blocks(f.head) : 0;
-    const int njobs = hb + f.n_colsum * f.colsum_tiles;
-    const mep_colsum_desc* cd = reinterpret_cast<const mep_colsum_desc*>(f.colsum);
-    float sq = 0.f;
-    for (int q = j; q < njobs; q += f.n_job_wg) {
-        if (q > j) __syncthreads();   // the previous job has read its LDS
-        sq += q < hb ? head_reduce_block(f.head, hg, q, red)
-                     : colsum_block(cd[(q - hb) / f.colsum_tiles], (q - hb) % f.colsum_tiles, red);
-    }
-    if (f.norm) wg_norm_partial(sq, reinterpret_cast<float*>(f.norm) + OPT_EXT0 + f.n_cg + j, red);
-    MEP_WG_STAMP(7);
-}
-
 // a descriptor this instance cannot run: NaN partials (loudly wrong, never silently)
 MEP_DEV void wg_nan_partial(const mep_wgrad_desc& d, int slot) {
-    const auto rsP = __builtin_amdgcn_make_buffer_rsrc((void*)(d.partial + 4ull * slot * d.N * d.Ktot), 0, 0x7fffffff, 0x00020000);
-    for (int e = threadIdx.x; e < d.N * d.Ktot; e += WG_THREADS)   // write-through: a fused launch's reducer reads them
-        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(__builtin_nanf("")), rsP, 4 * e, 0, WT_SC1);
+    gfloat* part = G<float>(d.partial) + (int64_t)slot * d.N * d.Ktot;
+    for (int e = threadIdx.x; e < d.N * d.Ktot; e += WG_THREADS) part[e] = __builtin_nanf("");
 }
 
 // Flat grid of n_wg workgroups.  The map after the n_desc descriptors: off[n_wg + 1] (CSR), then
@@ -634,25 +480,14 @@ MEP_DEV void wg_nan_partial(const mep_wgrad_desc& d, int slot) {
 // may finish one descriptor's token range and start another's.
 // BF: the instance for bf16-path descriptors (MEP_PREC_BF16); a descriptor of the other precision
 // gets NaN partials (loudly wrong, never silently)
-template <bool BF, bool FOLD>
-__global__ __launch_bounds__(WG_THREADS) __attribute__((amdgpu_waves_per_eu(wg_occ(BF)))) void k_wgrad(const mep_wgrad_desc* __restrict__ descs, int n_desc, int n_wg, mep_wgrad_fold fold) {
+template <bool BF>
+__global__ __launch_bounds__(WG_THREADS) __attribute__((amdgpu_waves_per_eu(wg_occ(BF)))) void k_wgrad(const mep_wgrad_desc* __restrict__ descs, int n_desc, int n_wg) {
     const int* map = reinterpret_cast<const int*>(descs + n_desc);
+    const int s0 = map[blockIdx.x], s1 = map[blockIdx.x + 1];
+    const int* seg = map + n_wg + 1;
     __shared__ __attribute__((aligned(16))) float smem[2 * WG_RED];
     lfloat* red = (lfloat*)&smem[0];
     MEP_WG_STAMP(0);
-    if constexpr (FOLD) {
-        if (blockIdx.x == 0 && threadIdx.x == 0 && fold.norm && fold.step)
-            opt_step_scalars(reinterpret_cast<float*>(fold.norm), reinterpret_cast<int*>(fold.step),
-                             reinterpret_cast<const float*>(fold.hyper));
-        if ((int)blockIdx.x >= n_wg) {
-            wg_fold_jobs(fold, blockIdx.x - n_wg, red);
-            return;
-        }
-    }
-    const int s0 = map[blockIdx.x], s1 = map[blockIdx.x + 1];
-    const int* seg = map + n_wg + 1;
-    const int* cg_off = seg + 4 * map[n_wg];          // FOLD: column-group offsets, then arrivals
-    const int* cg_arr = cg_off + n_desc;
     for (int si = s0; si < s1; ++si) {
         const int hdr = seg[4 * si], t_begin = seg[4 * si + 1], t_end = seg[4 * si + 2], slot = seg[4 * si + 3];
         const mep_wgrad_desc& d = descs[hdr >> 8];
@@ -661,33 +496,29 @@ __global__ __launch_bounds__(WG_THREADS) __attribute__((amdgpu_waves_per_eu(wg_o
         const int ktiles = (d.Ktot + 31) >> 5;
         const int kt = min(ktm, ktiles - cg * ktm);
         const int kbase = 32 * ktm * cg;
-        if (si > s0) __syncthreads();   // the previous segment's partial write (and fold) has read `red`
+        if (si > s0) __syncthreads();   // the previous segment's partial write has read `red`
         bool lin = wg_linear(d.a);
         for (int o = 0; o < d.n_b; ++o) lin = lin && wg_linear(d.b[o]);
 #define MEP_WGT(M, K)                                                                          \
         case 8 * M + K:                                                                        \
             if constexpr (K > wg_kt(M, BF)) break;   /* not a tile block of this instance */   \
-            if (lin) wgrad_task<M, K, BF ? 1 : 3, true, BF ? WG_SLOTS_B : WG_SLOTS_F, FOLD>(d, t_begin, t_end, slot, kbase, red);  \
-            else if constexpr (!BF) wgrad_task<M, K, 3, false, WG_SLOTS_F, FOLD>(d, t_begin, t_end, slot, kbase, red);         \
+            if (lin) wgrad_task<M, K, BF ? 1 : 3, true, BF ? WG_SLOTS_B : WG_SLOTS_F>(d, t_begin, t_end, slot, kbase, red);  \
+            else if constexpr (!BF) wgrad_task<M, K, 3, false, WG_SLOTS_F>(d, t_begin, t_end, slot, kbase, red);         \
             else wg_nan_partial(d, slot);   /* bf16 rows: linear views only */                                                       \
             break;
         // the bf16-path instance needs bf16 operands AND bf16 operand rows (MEP_BF16_OPS | MEP_BF16_STORE)
         if ((d.bf16 != 0) != BF || (BF && d.bf16 != (MEP_BF16_OPS | MEP_BF16_STORE))) {
             wg_nan_partial(d, slot);
-        } else {
-            switch (8 * mt + kt) {
-                MEP_WGT(1, 1) MEP_WGT(1, 2) MEP_WGT(1, 3) MEP_WGT(1, 4)
-                MEP_WGT(2, 1) MEP_WGT(2, 2) MEP_WGT(2, 3) MEP_WGT(2, 4)
-                MEP_WGT(3, 1) MEP_WGT(3, 2) MEP_WGT(3, 3)
-                MEP_WGT(4, 1) MEP_WGT(4, 2)
-                default: break;
-            }
+            continue;
+        }
+        switch (8 * mt + kt) {
+            MEP_WGT(1, 1) MEP_WGT(1, 2) MEP_WGT(1, 3) MEP_WGT(1, 4)
+            MEP_WGT(2, 1) MEP_WGT(2, 2) MEP_WGT(2, 3) MEP_WGT(2, 4)
+            MEP_WGT(3, 1) MEP_WGT(3, 2) MEP_WGT(3, 3)
+            MEP_WGT(4, 1) MEP_WGT(4, 2)
+            default: break;
         }
 #undef MEP_WGT
-        if constexpr (FOLD) {
-            const int ci = cg_off[hdr >> 8] + cg;
-            wg_fold_group<BF>(d, ci, cg, cg_arr[ci], fold, red);
-        }
     }
 }
 
@@ -1052,33 +883,11 @@ extern "C" int mep_wgrad_occupancy(int bf16) { return wg_occ(bf16 != 0); }
 
 extern "C" int mep_wgrad(const mep_wgrad_desc* descs, int n_desc, int max_tiles, int flags, mep_stream_t stream) {
     if (n_desc <= 0 || max_tiles <= 0) return 0;
-    const mep_wgrad_fold none{};
     if (flags & MEP_PREC_BF16)
-        hipLaunchKernelGGL((k_wgrad<true, false>), dim3(max_tiles), dim3(WG_THREADS), 0, (hipStream_t)stream, descs, n_desc, max_tiles, none);
+        hipLaunchKernelGGL(k_wgrad<true>, dim3(max_tiles), dim3(WG_THREADS), 0, (hipStream_t)stream, descs, n_desc, max_tiles);
     else
-        hipLaunchKernelGGL((k_wgrad<false, false>), dim3(max_tiles), dim3(WG_THREADS), 0, (hipStream_t)stream, descs, n_desc, max_tiles, none);
+        hipLaunchKernelGGL(k_wgrad<false>, dim3(max_tiles), dim3(WG_THREADS), 0, (hipStream_t)stream, descs, n_desc, max_tiles);
     return mep_check_launch("mep_wgrad");
-}
-
-extern "C" int mep_wgrad_fused(const mep_wgrad_desc* descs, int n_desc, int n_wg, int flags, const mep_wgrad_fold* fold,
-                               mep_stream_t stream) {
-    if (!fold || n_desc <= 0 || n_wg <= 0 || !fold->tickets || fold->n_cg <= 0 || fold->n_job_wg < 0 ||
-        fold->n_colsum < 0 || (fold->n_colsum && (fold->colsum_tiles <= 0 || !fold->colsum)) ||
-        (fold->has_head && (fold->head.NC <= 0 || fold->head.NC > NCMAX))) {
-        mep_set_error("mep_wgrad_fused: invalid fold (tickets, n_cg > 0, colsum / head descriptors)");
-        return MEP_EINVAL;
-    }
-    const int jobs = (fold->has_head ? head_reduce_blocks(fold->head) : 0) + fold->n_colsum * fold->colsum_tiles;
-    if ((jobs > 0) != (fold->n_job_wg > 0) || fold->n_job_wg > jobs) {
-        mep_set_error("mep_wgrad_fused: n_job_wg must be in [1, jobs] when there are jobs, else 0");
-        return MEP_EINVAL;
-    }
-    const dim3 grid(n_wg + fold->n_job_wg);
-    if (flags & MEP_PREC_BF16)
-        hipLaunchKernelGGL((k_wgrad<true, true>), grid, dim3(WG_THREADS), 0, (hipStream_t)stream, descs, n_desc, n_wg, *fold);
-    else
-        hipLaunchKernelGGL((k_wgrad<false, true>), grid, dim3(WG_THREADS), 0, (hipStream_t)stream, descs, n_desc, n_wg, *fold);
-    return mep_check_launch("mep_wgrad_fused");
 }
 
 extern "C" int mep_wgrad_reduce(const mep_wgrad_desc* descs, int n_desc, int max_tiles, mep_stream_t stream) {

@@ -175,8 +175,7 @@ __global__ void k_seed(uint64_t* seed) { seed[0] = mix64(seed[0] + 0x9E3779B97F4
 // ---------------------------------------------------------------- colsum / row sums
 // workgroup = 32 columns x 8 row groups; fixed-order combine (deterministic)
 __global__ __launch_bounds__(256) void k_colsum(const mep_colsum_desc* __restrict__ descs) {
-    __shared__ float scratch[COLSUM_LDS];
-    colsum_block(descs[blockIdx.y], blockIdx.x, (lfloat*)&scratch[0]);
+    colsum_block(descs[blockIdx.y], blockIdx.x);
 }
 
 // out = sum of sources, 4 columns per thread (D % 4 == 0 for every model width); HS: bf16 source

@@ -96,7 +96,25 @@ __global__ __launch_bounds__(256) void k_pool_bwd(const mep_pool_desc* __restric
 }
 
 // ---------------------------------------------------------------- fusion head
+constexpr int NCMAX = 16;
 constexpr int HEAD_KU = 3;   // classifier columns per thread per pass
+
+struct HeadOff {
+    int wo, bo, lnw, lnb, trans, dl0, dl1, stride;
+};
+__host__ __device__ inline HeadOff head_off(int NC) {
+    HeadOff o;
+    o.wo = 0;
+    o.bo = o.wo + 2 * NC * NC;
+    o.lnw = o.bo + NC;
+    o.lnb = o.lnw + NC;
+    o.trans = o.lnb + NC;
+    o.dl0 = o.trans + NC * NC * NC;
+    o.dl1 = o.dl0 + NC;
+    o.stride = o.dl1 + NC;
+    return o;
+}
+
 MEP_DEV float label_at(const mep_head_desc& d, int b, int n) {
     if (d.labels_are_float) return G<const float>(d.labels)[b * d.NC + n];
     return (float)G<const int64_t>(d.labels)[b * d.NC + n];
@@ -444,9 +462,101 @@ __global__ __launch_bounds__(256) void k_head(mep_head_desc d) {
     HT(6); HT_PRINT();
 }
 
+struct HeadGrads {
+    float *g_trans, *g_lnw, *g_lnb, *g_wo, *g_bo, *g_wc0, *g_wc1, *loss;
+};
+
+// Sum of the per-row head partials.  Workgroups [0, nA32): 32 columns of the small-parameter
+// records each, 8 row groups per column (+ the batch loss in workgroup 0); workgroups after
+// that: 32 columns k of one classifier e, dWc_e[n][k] = sum_b dlogit_e[b][n] pooled_e[b][k] for
+// every n, rows split over 8 groups.  Fixed summation order (deterministic).
+MEP_DEV float head_reduce_block(const mep_head_desc& d, const HeadGrads& g, int bx) {
+    const int NC = d.NC, F = d.F, B = d.B;
+    const HeadOff o = head_off(NC);
+    const int nA = o.dl0;                 // everything before the dlogit records
+    const int nA32 = (nA + 31) / 32;
+    const int cl = threadIdx.x & 31, rg = threadIdx.x >> 5;
+    const gfloat* part = G<const float>(d.partial);
+    __shared__ float red[8][NCMAX][33];
+    if ((int)bx < nA32) {
+        const int i = bx * 32 + cl;
+        float s = 0.f;
+        if (i < nA) {
+#pragma unroll 8
+            for (int b = rg; b < B; b += 8) s += part[(int64_t)b * o.stride + i];
+        }
+        red[rg][0][cl] = s;
+        float ls = 0.f, sq = 0.f;
+        if (bx == 0)
+            for (int b = threadIdx.x; b < B; b += 256) ls += G<const float>(d.row_loss)[b];
+        __syncthreads();
+        if (rg == 0 && i < nA) {
+            float t = 0.f;
+#pragma unroll
+            for (int k = 0; k < 8; ++k) t += red[k][0][cl];
+            float* dst;
+            if (i < o.bo) dst = g.g_wo + (i - o.wo);
+            else if (i < o.lnw) dst = g.g_bo + (i - o.bo);
+            else if (i < o.lnb) dst = g.g_lnw + (i - o.lnw);
+            else if (i < o.trans) dst = g.g_lnb + (i - o.lnb);
+            else dst = g.g_trans + (i - o.trans);
+            *G<float>(reinterpret_cast<uint64_t>(dst)) = t;
+            sq = t * t;
+        }
+        if (bx == 0) {
+            ls = wave_sum(ls);
+            __syncthreads();
+            if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6][1][0] = ls;
+            __syncthreads();
+            if (threadIdx.x == 0)
+                *G<float>(reinterpret_cast<uint64_t>(g.loss)) = red[0][1][0] + red[1][1][0] + red[2][1][0] + red[3][1][0];
+        }
+        return sq;   // the loss is not a gradient
+    }
+    const int wb = bx - nA32;
+    const int nkb = (F + 31) / 32;
+    const int e = wb / nkb, k = (wb - e * nkb) * 32 + cl;
+    const float* pooled = reinterpret_cast<const float*>(e ? d.pooled1 : d.pooled0);
+    const int off = e ? o.dl1 : o.dl0;
+    float acc[NCMAX];
+#pragma unroll
+    for (int n = 0; n < NCMAX; ++n) acc[n] = 0.f;
+    // every load unconditional (clamped column and class): a load under a per-class branch is a
+    // basic block of its own with its own wait
+    const int kc = min(k, F - 1);
+#pragma unroll 4
+    for (int b = rg; b < B; b += 8) {
+        const float pk = pooled[(int64_t)b * F + kc];
+        const gfloat* pr = part + (int64_t)b * o.stride + off;
+#pragma unroll
+        for (int n = 0; n < NCMAX; ++n) {
+            const float x = pr[min(n, NC - 1)];
+            acc[n] = n < NC ? fmaf(x, pk, acc[n]) : acc[n];
+        }
+    }
+#pragma unroll
+    for (int n = 0; n < NCMAX; ++n) if (n < NC) red[rg][n][cl] = acc[n];
+    __syncthreads();
+    float sq = 0.f;
+    if (k < F) {
+        float* out = e ? g.g_wc1 : g.g_wc0;
+        for (int n = rg; n < NC; n += 8) {
+            float t = 0.f;
+#pragma unroll
+            for (int q = 0; q < 8; ++q) t += red[q][n][cl];
+            *G<float>(reinterpret_cast<uint64_t>(out + (int64_t)n * F + k)) = t;
+            sq += t * t;
+        }
+    }
+    return sq;
+}
+
 __global__ __launch_bounds__(256) void k_head_reduce(mep_head_desc d, HeadGrads g) {
-    __shared__ float scratch[HEAD_RED_LDS];
-    head_reduce_block(d, g, blockIdx.x, (lfloat*)&scratch[0]);
+    head_reduce_block(d, g, blockIdx.x);
+}
+
+__host__ __device__ inline int head_reduce_blocks(const mep_head_desc& d) {
+    return (head_off(d.NC).dl0 + 31) / 32 + 2 * ((d.F + 31) / 32);
 }
 
 // Every gradient reduction of a training step in ONE launch: the head-parameter sums (largest
@@ -460,12 +570,10 @@ __global__ __launch_bounds__(256) void k_reduce_grads(const mep_wgrad_desc* __re
                                                       const mep_colsum_desc* __restrict__ cd, int n_cd, int cd_tiles,
                                                       mep_head_desc hd, HeadGrads hg, int head_blocks,
                                                       float* norm, int* step, const float* hyper) {
-    __shared__ float scratch[HEAD_RED_LDS];
-    lfloat* lds = (lfloat*)&scratch[0];
     int bx = blockIdx.x;
     float sq = 0.f;
     if (bx < head_blocks) {
-        sq = head_reduce_block(hd, hg, bx, lds);
+        sq = head_reduce_block(hd, hg, bx);
     } else {
         bx -= head_blocks;
         const int wt = wg_red_blocks(wd_tiles);   // blocks of WG_RED_PER entries per descriptor
@@ -473,7 +581,7 @@ __global__ __launch_bounds__(256) void k_reduce_grads(const mep_wgrad_desc* __re
             sq = wgrad_reduce_block(wd[bx / wt], bx % wt);
         } else {
             bx -= n_wd * wt;
-            if (bx < n_cd * cd_tiles) sq = colsum_block(cd[bx / cd_tiles], bx % cd_tiles, lds);
+            if (bx < n_cd * cd_tiles) sq = colsum_block(cd[bx / cd_tiles], bx % cd_tiles);
         }
     }
     if (!norm) return;

@@ -27,9 +27,7 @@ import torch
 from . import _lib
 from ._lib import (AttnBwdDesc, AttnDesc, ColsumDesc, DescArray, GemmDesc, PoolDesc, RfEpiBwdDesc, RfEpiDesc,
                    RfHeadDesc, Rows, SumDesc, launch)
-from . import trimodal as _tm
-from .trimodal import (CHAINS, MODS, TIME_ORDER, UNIFY_NAMES, _norm_args, cdiv, crows, fold_parts,
-                       make_wgrad, rows, wgrad_fused)
+from .trimodal import CHAINS, MODS, TIME_ORDER, UNIFY_NAMES, _norm_args, cdiv, crows, make_wgrad, rows
 
 RF_SPLITQ = _lib.switch('MEP_RF_SPLITQ', '1') != '0'   # attention backward: query tiles over 4 waves
 # unify + projections of each modality in one launch (mep_rfw_front) up to RF_FRONT_MAX_TILES
@@ -646,12 +644,6 @@ class RealformerPlan:
         else:
             self._gemm(self.d_ingrad_all, self.t_ingrad, stream)
             launch('mep_sum_rows', self.d_sum, self.t_sum, stream)
-        if _tm.WGRAD_FOLD:
-            # weight gradients with their split sums and the LayerNorm / ReZero / residual-coefficient
-            # column sums in one launch (no head partials here: the State_Transfer head reduces in
-            # mep_rf_head)
-            wgrad_fused(self.d_wgrad, self.t_wgrad, self.d_colsum, self.t_colsum, None, None, _norm_args(self), stream)
-            return
         launch('mep_wgrad', self.d_wgrad, self.t_wgrad, stream)
         # weight-gradient split sums and LayerNorm / ReZero / residual-coefficient column sums: one
         # launch (no head partials here: the State_Transfer head reduces in mep_rf_head)
@@ -663,8 +655,6 @@ class RealformerPlan:
 
     def reduce_grid(self):
         """blocks of the backward's mep_reduce_grads launch (the optimizer's folded norm partials)"""
-        if _tm.WGRAD_FOLD:
-            return fold_parts(self.d_wgrad, self.t_wgrad, self.d_colsum.n, self.t_colsum if self.d_colsum.n else 0, None)
         return _lib.lib().mep_reduce_grads_grid(self.d_wgrad.n, self.t_wgred, self.d_colsum.n,
                                                 self.t_colsum if self.d_colsum.n else 0, None)
 

@@ -123,22 +123,80 @@ def wgrad_chunk(items, n_wg=WG_TARGET, bf16=False):
     return best[1]
 
 
-def wgrad_segments(items, n_wg=WG_TARGET, tok_per_split=None, bf16=False):
+# per-(item, column group) segment counts, cost-weighted over every workgroup slot (0: one token
+# chunk for the whole launch, wgrad_chunk)
+WG_BALANCE = _lib.switch('MEP_WG_BALANCE', '1') != '0'
+
+
+def wgrad_counts(items, n_wg=WG_TARGET, bf16=False):
+    """Segments per (item, column group) unit, {(i, cg): k}: every unit's span cut into k near-equal
+    chunks so that the launch fills its rounds of n_wg workgroup slots exactly and the costliest
+    segment is as cheap as it can be.  A segment's cost is its tokens x (MT + KT), the 32 x 32
+    operand tiles a token loads (and multiplies): a unit with fewer column tiles (the last column
+    group of a 96- or 74-wide weight, one tile) gets fewer, longer segments.  One uniform chunk
+    left 88 of the 512 fp32 slots empty at cfg3: the workgroups alone on a CU finished their 800
+    tokens in 60% of the time of those that share one (scripts/wg_trace.py), and the shared ones
+    bound the launch.  Rounds as wgrad_chunk: the bf16 instance picks 1-4 by rounds x (segment +
+    WG_SETUP_TOKENS), the fp32 instance one."""
+    import heapq
+    items = [tuple(it) + (0,) * (5 - len(it)) for it in items]
+    units = []
+    for i, (_, N, n, bs, _) in enumerate(items):
+        mt, kt, ncg = wgrad_geometry(N, sum(b[1] for b in bs), bf16)
+        ktiles = cdiv(sum(b[1] for b in bs), 32)
+        for cg in range(ncg):
+            if n > 0:
+                units.append(((i, cg), n, mt + min(kt, ktiles - cg * kt)))
+
+    def fill(budget):
+        k = {u: 1 for (u, _, _) in units}
+        heap = [(-(n * c), u, n, c) for (u, n, c) in units]
+        heapq.heapify(heap)
+        total = len(units)
+        while heap and total < budget:
+            _, u, n, c = heapq.heappop(heap)
+            if n < 8 * (k[u] + 1):            # chunks stay >= 8 tokens
+                continue
+            k[u] += 1
+            total += 1
+            heapq.heappush(heap, (-(n * c / k[u]), u, n, c))
+        worst = max((cdiv(n, k[u]) * c for (u, n, c) in units), default=0)
+        return worst, k
+    if not units:
+        return {}
+    setup = WG_SETUP_TOKENS * 5   # tokens x tiles, the MT + KT = 5 tiles of a cfg3 segment
+    best = None
+    for r in ((1, 2, 3, 4) if bf16 and not WG_TARGET_OVERRIDE else (1,)):
+        worst, k = fill(r * n_wg)
+        cost = r * (worst + setup)
+        if best is None or cost < best[0]:
+            best = (cost, k)
+    return best[1]
+
+
+def wgrad_segments(items, n_wg=WG_TARGET, tok_per_split=None, bf16=False, counts=None):
     """Split every (item, column group) token span into segments of at most tok_per_split tokens,
-    one segment per workgroup; tok_per_split None: the smallest multiple of 8 that keeps the launch
-    within n_wg workgroups (all resident at once, one per CU).  Uniform chunks beat a cost-balanced
-    water-filling over all n_wg CUs (47.3 vs 49.6 us at cfg3, scripts/wgrad_balance.py); a span
-    longer than the chunk is cut into near-equal pieces.  The loop
+    one segment per workgroup; counts (or, tok_per_split and counts None, wgrad_counts under
+    WG_BALANCE): k segments per (item, column group); tok_per_split: chunks of at most that many
+    tokens (MEP_WG_BALANCE=0: the smallest multiple of 8 that keeps the launch within n_wg
+    workgroups).  A span is cut into near-equal pieces at multiples of 8.  The loop
     is bound by HBM traffic and the operand-load rate, so more, smaller segments only add setup
     and partial-reduction work (~10 us per workgroup, round-3 per-workgroup traces).
     -> (per-workgroup segment lists [(item, cg, t0, t1, slot)], slots per item)."""
     units = _wgrad_units(items, bf16)
-    if tok_per_split is None:
-        tok_per_split = wgrad_chunk(items, n_wg, bf16)
+    if tok_per_split is None and counts is None:
+        if WG_BALANCE:
+            counts = wgrad_counts(items, n_wg, bf16)
+        else:
+            tok_per_split = wgrad_chunk(items, n_wg, bf16)
     bins = []
     for (i, cg, n) in units:
-        tps = tok_per_split[i] if isinstance(tok_per_split, (list, tuple)) else tok_per_split
-        k = cdiv(n, tps)                      # k near-equal chunks, cut at multiples of 8
+        if counts is not None:
+            k = counts[(i, cg)]
+        else:
+            tps = tok_per_split[i] if isinstance(tok_per_split, (list, tuple)) else tok_per_split
+            k = cdiv(n, tps)
+        # k near-equal chunks, cut at multiples of 8
         cuts = [min(n, cdiv(n * q, 8 * k) * 8) for q in range(k)] + [n]
         bins += [[(i, cg, a, b)] for a, b in zip(cuts[:-1], cuts[1:]) if b > a]
     slots = [0] * len(items)
@@ -252,14 +310,14 @@ def xcd_order(work):
     return [work[(i % 8) * q + min(i % 8, r) + i // 8] for i in range(G)]
 
 
-def make_wgrad(items, dev, tok_per_split=None, bf16=False):
+def make_wgrad(items, dev, tok_per_split=None, bf16=False, counts=None):
     """items: [(a_rows, N, ntok, [(b_rows, K, out_ptr, ldo), ...][, out_trans]), ...] ->
     (workspace, descs, wgrad workgroups, reduce tiles).  One descriptor per A operand; its B operands
     concatenate on K.  out_trans: dW written transposed (out[k * ldo + n]).  tok_per_split: None =
     the launch's work balanced over one workgroup per CU (wgrad_segments), else fixed token
     chunks.  bf16: plain bf16 operands (the bf16 path) instead of the 3-part split."""
     items = [tuple(it) + (0,) * (5 - len(it)) for it in items]
-    segs, slots = wgrad_segments(items, n_wg=wg_target(bf16), tok_per_split=tok_per_split, bf16=bf16)
+    segs, slots = wgrad_segments(items, n_wg=wg_target(bf16), tok_per_split=tok_per_split, bf16=bf16, counts=counts)
     total = sum(max(1, s) * N * sum(b[1] for b in bs) for s, (_, N, n, bs, _) in zip(slots, items))
     ws = torch.zeros(max(total, 1), dtype=torch.float32, device=dev)   # unwritten slots stay 0
     descs, off, rmax = [], 0, 0
@@ -288,72 +346,15 @@ def make_wgrad(items, dev, tok_per_split=None, bf16=False):
                                bf16=(_lib.BF16_OPS | _lib.BF16_STORE) if bf16 else 0))
         off += ns * N * ktot
         rmax = max(rmax, cdiv(N * ktot, 256))
-    # mep_wgrad_fused: every (item, column group) needs at least one arrival -- an item without
-    # tokens gets one empty segment per column group (a zero slot)
-    ncgs = [wgrad_geometry(N, sum(b[1] for b in bs), bf16)[2] for (_, N, _, bs, _) in items]
-    seen = {(i, cg) for b in segs for (i, cg, _, _, _) in b}
-    segs = list(segs) + [[(i, cg, 0, 0, 0)] for i, ncg in enumerate(ncgs) for cg in range(ncg) if (i, cg) not in seen]
     assert len(descs) < 2 ** 23 and all(cg < 256 for b in segs for (_, cg, _, _, _) in b)
     offs, flat = [0], []
     for b in segs:
         for (i, cg, t0, t1, s) in b:
             flat += [(i << 8) | cg, t0, t1, s]
         offs.append(offs[-1] + len(b))
-    # the fused launch's map tail: column-group offsets per descriptor, then arrivals per group
-    cg_off = [sum(ncgs[:i]) for i in range(len(ncgs))]
-    arrivals = [0] * sum(ncgs)
-    for b in segs:
-        for (i, cg, _, _, _) in b:
-            arrivals[cg_off[i] + cg] += 1
-    arr = DescArray(WgradDesc, descs, dev, tail=offs + flat + cg_off + arrivals)
+    arr = DescArray(WgradDesc, descs, dev, tail=offs + flat)
     arr.prec = _lib.PREC_BF16 if bf16 else 0   # the mep_wgrad instance (launch reads it)
-    arr.n_cg = len(arrivals)
-    arr.tickets = torch.zeros(max(1, len(arrivals)), dtype=torch.int32, device=dev)   # left zero by every launch
     return ws, arr, len(segs), rmax
-
-
-# mep_wgrad_fused: the split sums, head-parameter sums and column sums inside the weight-gradient
-# launch (0: mep_wgrad + mep_reduce_grads, the two-launch form; A/B runs)
-WGRAD_FOLD = _lib.switch('MEP_WGRAD_FOLD', '1') != '0'
-
-
-def fold_jobs(n_colsum, colsum_tiles, head):
-    """jobs of a fused launch that are not split sums: head-parameter sums, then column sums"""
-    hb = _lib.lib().mep_reduce_grads_grid(0, 0, 0, 0, ctypes.byref(head)) if head is not None else 0
-    return hb + (n_colsum * colsum_tiles if n_colsum else 0)
-
-
-def fold_job_wg(jobs, n_wg, bf16):
-    """job workgroups of a fused launch: the workgroup slots the weight-gradient workgroups leave
-    free (the launch is sized to be resident at once), at least 16, at most one per job"""
-    return 0 if jobs <= 0 else min(jobs, max(wg_target(bf16) - n_wg, 16))
-
-
-def fold_parts(arr, n_wg, n_colsum, colsum_tiles, head):
-    """norm partials a fused launch writes (mep_clip_adam_ext's n_ext): one per column group and
-    job workgroup"""
-    return arr.n_cg + fold_job_wg(fold_jobs(n_colsum, colsum_tiles, head), n_wg, arr.prec != 0)
-
-
-def wgrad_fused(arr, n_wg, colsum, colsum_tiles, head, head_grads, norm, stream):
-    """one mep_wgrad_fused launch: weight gradients + every gradient reduction of the step
-    (colsum: DescArray of ColsumDesc; head: HeadDesc or None; norm: the (workspace, step, hyper)
-    pointers of the folded norm pass or Nones).  Timed as the mep_wgrad launch."""
-    if arr.n == 0 or n_wg <= 0:
-        return
-    ncs = colsum.n if colsum is not None else 0
-    jobs = fold_jobs(ncs, colsum_tiles, head)
-    hg = [int(x) for x in head_grads] if head is not None else [0] * 8
-    nv = [int(x.value or 0) if isinstance(x, ctypes.c_void_p) else int(x or 0) for x in norm]
-    f = _lib.WgradFold(tickets=arr.tickets.data_ptr(), n_cg=arr.n_cg, n_job_wg=fold_job_wg(jobs, n_wg, arr.prec != 0),
-                       colsum=colsum.dev.data_ptr() if ncs else 0, n_colsum=ncs, colsum_tiles=colsum_tiles if ncs else 0,
-                       head=head if head is not None else HeadDesc(), has_head=int(head is not None),
-                       g_trans=hg[0], g_ln_w=hg[1], g_ln_b=hg[2], g_wo=hg[3], g_bo=hg[4], g_wc0=hg[5], g_wc1=hg[6],
-                       loss=hg[7], norm=nv[0], step=nv[1], hyper=nv[2])
-    fn = _lib.lib().mep_wgrad_fused
-    ptr, n, prec = arr.ptr, arr.n, arr.prec
-    _lib._run('mep_wgrad', lambda: _lib.check(fn(ptr, n, int(n_wg), prec, ctypes.byref(f), _lib.stream_ptr(stream)),
-                                              'mep_wgrad_fused'), stream)
 
 
 def rows(t, T, sB, sT, off=0):
@@ -845,12 +846,6 @@ class TriModalPlan:
         launch('mep_sum_rows', self.d_sum, self.t_sum, stream)
         if sp.unify_norm:
             launch('mep_layernorm_bwd', self.d_ulnb, cdiv(max(self.ntok.values()), 64), stream)
-        if WGRAD_FOLD:
-            # weight gradients, their split sums, the LayerNorm / residual-coefficient column sums
-            # and the head parameter sums: one launch
-            wgrad_fused(self.d_wgrad, self.t_wgrad, self.d_colsum, self.t_colsum, self.head, self.head_grads,
-                        _norm_args(self), stream)
-            return
         launch('mep_wgrad', self.d_wgrad, self.t_wgrad, stream)
         # weight-gradient split sums, LayerNorm / residual-coefficient column sums and the head
         # parameter sums: one launch
@@ -863,8 +858,6 @@ class TriModalPlan:
 
     def reduce_grid(self):
         """blocks of the backward's mep_reduce_grads launch (the optimizer's folded norm partials)"""
-        if WGRAD_FOLD:
-            return fold_parts(self.d_wgrad, self.t_wgrad, self.d_colsum.n, self.t_colsum, self.head)
         red, t_red = self._reduce_args()
         return _lib.lib().mep_reduce_grads_grid(red.n, t_red, self.d_colsum.n, self.t_colsum, ctypes.byref(self.head))
 
@@ -879,9 +872,15 @@ class TriModalPlan:
         if getattr(self, '_buckets', None) is not None:
             return
         dev, items, nb = self.device, self._wgrad_items, self._n_block_items
-        tps = wgrad_chunk(items, wg_target(self.bf16), bf16=self.bf16)
-        wa = make_wgrad(items[:nb], dev, tok_per_split=tps, bf16=self.bf16)
-        wb = make_wgrad(items[nb:], dev, tok_per_split=tps, bf16=self.bf16)
+        if WG_BALANCE:   # the one-launch form's segment counts, the B items renumbered from 0
+            cnt = wgrad_counts(items, wg_target(self.bf16), bf16=self.bf16)
+            wa = make_wgrad(items[:nb], dev, bf16=self.bf16, counts={u: k for u, k in cnt.items() if u[0] < nb})
+            wb = make_wgrad(items[nb:], dev, bf16=self.bf16,
+                            counts={(i - nb, cg): k for (i, cg), k in cnt.items() if i >= nb})
+        else:
+            tps = wgrad_chunk(items, wg_target(self.bf16), bf16=self.bf16)
+            wa = make_wgrad(items[:nb], dev, tok_per_split=tps, bf16=self.bf16)
+            wb = make_wgrad(items[nb:], dev, tok_per_split=tps, bf16=self.bf16)
         ca = DescArray(ColsumDesc, self._colsum_a, dev)
         cb = DescArray(ColsumDesc, self._colsum_b, dev)
         self._check_bucket_ranges(wa[1], wb[1], ca, cb)
@@ -929,20 +928,14 @@ class TriModalPlan:
         for i in reversed(range(nl)):
             launch('mep_block_epi_bwd', self.d_epib[i], self.t_epi[i], stream, threads=sp.D | self.prec)
             if i == 0:
-                if WGRAD_FOLD:
-                    wgrad_fused(da, ta, ca, self.t_colsum, self.head, self.head_grads, (None, None, None), stream)
-                else:
-                    launch('mep_wgrad', da, ta, stream)
-                    _lib.call('mep_reduce_grads', da.ptr, da.n, ra, ca.ptr, ca.n, self.t_colsum if ca.n else 0,
-                              ctypes.byref(self.head), *self.head_grads, None, None, None, stream=stream)
+                launch('mep_wgrad', da, ta, stream)
+                _lib.call('mep_reduce_grads', da.ptr, da.n, ra, ca.ptr, ca.n, self.t_colsum if ca.n else 0,
+                          ctypes.byref(self.head), *self.head_grads, None, None, None, stream=stream)
                 bucket_a_done()
             launch('mep_attn_bwd', self.d_attnb[i], self.t_attnb[i], stream, threads=self.f_attnb[i] | self.prec)
         launch('mep_sum_rows', self.d_sum, self.t_sum, stream)
         if sp.unify_norm:
             launch('mep_layernorm_bwd', self.d_ulnb, cdiv(max(self.ntok.values()), 64), stream)
-        if WGRAD_FOLD:
-            wgrad_fused(db, tb, cb, self.t_colsum, None, None, (None, None, None), stream)
-            return
         launch('mep_wgrad', db, tb, stream)
         _lib.call('mep_reduce_grads', db.ptr, db.n, rb, cb.ptr, cb.n, self.t_colsum if cb.n else 0, None,
                   0, 0, 0, 0, 0, 0, 0, 0, None, None, None, stream=stream)
