@@ -521,18 +521,33 @@ MEP_DEV float head_reduce_block(const mep_head_desc& d, const HeadGrads& g, int 
     float acc[NCMAX];
 #pragma unroll
     for (int n = 0; n < NCMAX; ++n) acc[n] = 0.f;
-    // every load unconditional (clamped column and class): a load under a per-class branch is a
-    // basic block of its own with its own wait
+    // rows in chunks of 64: the chunk's dlogit records (64 x NC floats, one or two loads per
+    // thread) are staged in LDS while each thread's 8 pooled loads are in flight, then the products
+    // run from registers and LDS.  Loading the records per row and class from global memory left
+    // these blocks at ~10 us, the long pole of the launch (scripts/wg_trace.py --reduce).  Same
+    // products in the same order: rows rg, rg + 8, ... ascending.
+    __shared__ float s_dl[64 * NCMAX];
     const int kc = min(k, F - 1);
-#pragma unroll 4
-    for (int b = rg; b < B; b += 8) {
-        const float pk = pooled[(int64_t)b * F + kc];
-        const gfloat* pr = part + (int64_t)b * o.stride + off;
-#pragma unroll
-        for (int n = 0; n < NCMAX; ++n) {
-            const float x = pr[min(n, NC - 1)];
-            acc[n] = n < NC ? fmaf(x, pk, acc[n]) : acc[n];
+    for (int b0 = 0; b0 < B; b0 += 64) {
+        const int nb = min(64, B - b0);
+        for (int t = threadIdx.x; t < nb * NC; t += 256) {
+            const int bb = t / NC, n = t - bb * NC;
+            s_dl[bb * NCMAX + n] = part[(int64_t)(b0 + bb) * o.stride + off + n];
         }
+        float pk[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) pk[u] = pooled[(int64_t)min(b0 + rg + 8 * u, B - 1) * F + kc];
+        __syncthreads();
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int bb = rg + 8 * u;
+            if (bb < nb) {
+#pragma unroll
+                for (int n = 0; n < NCMAX; ++n)
+                    if (n < NC) acc[n] = fmaf(s_dl[bb * NCMAX + n], pk[u], acc[n]);
+            }
+        }
+        __syncthreads();
     }
 #pragma unroll
     for (int n = 0; n < NCMAX; ++n) if (n < NC) red[rg][n][cl] = acc[n];
@@ -559,6 +574,21 @@ __host__ __device__ inline int head_reduce_blocks(const mep_head_desc& d) {
     return (head_off(d.NC).dl0 + 31) / 32 + 2 * ((d.F + 31) / 32);
 }
 
+// MEP_WG_TRACE (development builds, scripts/wg_trace.py --reduce): thread 0 of every block of
+// k_reduce_grads stores the real-time counter at its start (0), after its job (1) and at its end
+// (2), and its job kind (3: 0 head, 1 split sum, 2 column sum, 3 empty) into g_rg_trace[block]
+#ifdef MEP_WG_TRACE
+}  // namespace
+__device__ unsigned long long g_rg_trace[8192 * 4];
+extern "C" int mep_rg_trace_read(void* dst) {
+    return (int)hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_rg_trace), sizeof(g_rg_trace));
+}
+namespace {
+#define MEP_RG_STAMP(k, v) do { if (threadIdx.x == 0) g_rg_trace[blockIdx.x * 4 + (k)] = (v); } while (0)
+#else
+#define MEP_RG_STAMP(k, v) ((void)0)
+#endif
+
 // Every gradient reduction of a training step in ONE launch: the head-parameter sums (largest
 // blocks first), the weight-gradient split sums and the column sums, each block taking one job
 // (block bodies in common.h); there are no dependencies between them.
@@ -572,19 +602,25 @@ __global__ __launch_bounds__(256) void k_reduce_grads(const mep_wgrad_desc* __re
                                                       float* norm, int* step, const float* hyper) {
     int bx = blockIdx.x;
     float sq = 0.f;
+    MEP_RG_STAMP(0, __builtin_amdgcn_s_memrealtime());
     if (bx < head_blocks) {
+        MEP_RG_STAMP(3, 0);
         sq = head_reduce_block(hd, hg, bx);
     } else {
         bx -= head_blocks;
         const int wt = wg_red_blocks(wd_tiles);   // blocks of WG_RED_PER entries per descriptor
         if (bx < n_wd * wt) {
-            sq = wgrad_reduce_block(wd[bx / wt], bx % wt);
+            const mep_wgrad_desc& d = wd[bx / wt];
+            MEP_RG_STAMP(3, (int64_t)(bx % wt) * WG_RED_PER < (int64_t)d.N * d.Ktot ? 1 : 3);
+            sq = wgrad_reduce_block(d, bx % wt);
         } else {
             bx -= n_wd * wt;
+            MEP_RG_STAMP(3, 2);
             if (bx < n_cd * cd_tiles) sq = colsum_block(cd[bx / cd_tiles], bx % cd_tiles);
         }
     }
-    if (!norm) return;
+    MEP_RG_STAMP(1, __builtin_amdgcn_s_memrealtime());
+    if (!norm) { MEP_RG_STAMP(2, __builtin_amdgcn_s_memrealtime()); return; }
     __shared__ float nred[4];
     sq = wave_sum(sq);
     if ((threadIdx.x & 63) == 0) nred[threadIdx.x >> 6] = sq;
@@ -593,6 +629,7 @@ __global__ __launch_bounds__(256) void k_reduce_grads(const mep_wgrad_desc* __re
         norm[OPT_EXT0 + blockIdx.x] = (nred[0] + nred[1]) + (nred[2] + nred[3]);
         if (blockIdx.x == 0 && step) opt_step_scalars(norm, step, hyper);
     }
+    MEP_RG_STAMP(2, __builtin_amdgcn_s_memrealtime());
 }
 
 __global__ __launch_bounds__(64) void k_circle_fwd(const float* __restrict__ logits, const void* labels, int lf,

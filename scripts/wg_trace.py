@@ -24,6 +24,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--dtype', default='fp32', choices=('fp32', 'bf16'))
     ap.add_argument('--balance', type=int, default=1)
+    ap.add_argument('--reduce', type=int, default=0, help='1: trace the mep_reduce_grads launch instead')
     args = ap.parse_args()
     import bench
     from mep_amd import _lib, trimodal
@@ -35,6 +36,8 @@ def main():
         work.eager_step()
     torch.cuda.synchronize()
     p = work.plan
+    if args.reduce:
+        return trace_reduce(work, args)
     fn = _lib.lib().mep_wg_trace_read
     fn.argtypes, fn.restype = [ctypes.c_void_p], ctypes.c_int
     buf = np.zeros((8192, 8), dtype=np.uint64)
@@ -50,6 +53,34 @@ def main():
     for k, nm in enumerate(['start', 'loop', 'loop end', 'slot written']):
         q = np.nanpercentile(us[:, k], [0, 10, 50, 90, 100])
         print('  %-13s ' % nm + ' '.join('%7.2f' % v for v in q))
+
+
+def trace_reduce(work, args):
+    """k_reduce_grads blocks: start / job done / end per job kind, with the launch's norm pass on
+    (the bench's engine plan folds the clip's norm into this launch)"""
+    from mep_amd import _lib
+    p = work.plan
+    fn = _lib.lib().mep_rg_trace_read
+    fn.argtypes, fn.restype = [ctypes.c_void_p], ctypes.c_int
+    buf = np.zeros((8192, 4), dtype=np.int64)
+    for _ in range(3):
+        work.eager_step()
+        torch.cuda.synchronize()
+        fn(buf.ctypes.data)
+    n = p.reduce_grid()
+    t = buf[:n].astype(np.float64)
+    t0 = t[:, 0].min()
+    us = (t[:, :3] - t0) / 100.0
+    kind = buf[:n, 3]
+    print('%s: %d blocks, span %.2f us' % (args.dtype, n, us[:, 2].max()))
+    for k, nm in enumerate(['head', 'split sum', 'column sum', 'empty']):
+        sel = kind == k
+        if not sel.any():
+            continue
+        print('  %-10s %4d blocks  start %s  job %s  end %s' % (
+            nm, int(sel.sum()), ' '.join('%6.2f' % v for v in np.percentile(us[sel, 0], [0, 50, 100])),
+            ' '.join('%6.2f' % v for v in np.percentile(us[sel, 1] - us[sel, 0], [0, 50, 100])),
+            ' '.join('%6.2f' % v for v in np.percentile(us[sel, 2], [0, 50, 100]))))
 
 
 if __name__ == '__main__':
