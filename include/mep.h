@@ -32,7 +32,7 @@ extern "C" {
 #endif
 
 #define MEP_EINVAL (-1000)
-#define MEP_ABI_VERSION 6
+#define MEP_ABI_VERSION 7
 
 typedef void* mep_stream_t; /* a hipStream_t */
 
@@ -583,6 +583,17 @@ int mep_reduce_grads(const mep_wgrad_desc* wgrad, int n_wgrad, int wgrad_tiles, 
  * *step and writes the step's Adam scalars (norm = the optimizer workspace of mep_clip_adam_ext,
  * >= 1024 + mep_reduce_grads_grid(..) floats; step / hyper as there).  norm = 0: no norm pass. */
 int mep_reduce_grads_grid(int n_wgrad, int wgrad_tiles, int n_colsum, int colsum_tiles, const mep_head_desc* head);
+/* mep_reduce_grads over a compact block map (ABI 7): block b of the n_blocks runs job bmap[b] (device
+ * uint32) = kind << 30 | descriptor << 12 | block within the descriptor -- kind 0: fusion-head block
+ * (as mep_head_reduce's blocks), 1: split-sum block of wgrad[descriptor] (1,024 entries each), 2:
+ * column-sum tile of colsum[descriptor] (32 columns) -- so the empty blocks of the rectangular grid
+ * (every descriptor padded to the largest one's block count) are never launched: State_Transfer's
+ * reduction is 29,430 rectangular blocks for a few thousand jobs.  Results are those of
+ * mep_reduce_grads; with norm, block b writes norm[1024 + b] (n_ext = n_blocks). */
+int mep_reduce_grads_mapped(const mep_wgrad_desc* wgrad, const mep_colsum_desc* colsum, const mep_head_desc* head,
+                            uint64_t g_trans, uint64_t g_ln_w, uint64_t g_ln_b, uint64_t g_wo, uint64_t g_bo,
+                            uint64_t g_wc0, uint64_t g_wc1, uint64_t loss, float* norm, int* step, const float* hyper,
+                            const uint32_t* bmap, int n_blocks, mep_stream_t stream);
 int mep_head_partial_stride(int NC);
 
 /* multi_circle_loss per row (cmu-mosei/run.py:342-351) as a standalone op for callers that

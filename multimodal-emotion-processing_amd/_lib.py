@@ -287,6 +287,7 @@ SIGNATURES.update({
     'mep_head_partial_stride': [i32],
     'mep_reduce_grads': [P, i32, i32, P, i32, i32, HP, u64, u64, u64, u64, u64, u64, u64, u64, P, P, P, P],
     'mep_reduce_grads_grid': [i32, i32, i32, i32, HP],
+    'mep_reduce_grads_mapped': [P, P, HP, u64, u64, u64, u64, u64, u64, u64, u64, P, P, P, P, i32, P],
     'mep_wgrad_kt': [i32, i32],
     'mep_wgrad_occupancy': [i32],
     'mep_circle_loss_fwd': [P, P, i32, i32, i32, P, P, P],
@@ -314,7 +315,7 @@ SIGNATURES.update({
 })
 
 _LIB = None
-ABI_VERSION = 6   # include/mep.h MEP_ABI_VERSION
+ABI_VERSION = 7   # include/mep.h MEP_ABI_VERSION
 
 
 def lib():

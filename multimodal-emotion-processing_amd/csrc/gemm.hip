@@ -219,7 +219,7 @@ extern "C" int mep_wg_trace_read(void* dst) {
     return (int)hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_wg_trace), sizeof(g_wg_trace));
 }
 namespace {
-#define MEP_WG_STAMP(k) do { if (threadIdx.x == 0) g_wg_trace[blockIdx.x * 8 + (k)] = __builtin_amdgcn_s_memrealtime(); } while (0)
+#define MEP_WG_STAMP(k) do { if (threadIdx.x == 0 && blockIdx.x < 8192) g_wg_trace[blockIdx.x * 8 + (k)] = __builtin_amdgcn_s_memrealtime(); } while (0)
 #else
 #define MEP_WG_STAMP(k) ((void)0)
 #endif

@@ -584,7 +584,7 @@ extern "C" int mep_rg_trace_read(void* dst) {
     return (int)hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_rg_trace), sizeof(g_rg_trace));
 }
 namespace {
-#define MEP_RG_STAMP(k, v) do { if (threadIdx.x == 0) g_rg_trace[blockIdx.x * 4 + (k)] = (v); } while (0)
+#define MEP_RG_STAMP(k, v) do { if (threadIdx.x == 0 && blockIdx.x < 8192) g_rg_trace[blockIdx.x * 4 + (k)] = (v); } while (0)
 #else
 #define MEP_RG_STAMP(k, v) ((void)0)
 #endif
@@ -596,14 +596,25 @@ namespace {
 // writes the sum of squares of the gradients it wrote to norm[OPT_EXT0 + block] (fixed-order
 // block reduction) and block 0 advances the optimizer step and its scalars (optim.hip
 // mep_clip_adam_ext then skips its own norm launch).
+// bmap (optional, mep_reduce_grads_mapped): block b runs job bmap[b] = kind << 30 | descriptor << 12
+// | block within the descriptor (kind 0 head, 1 split sum, 2 column sum), so only real jobs are
+// launched; without it the grid is the rectangle head + descriptors x max tiles.
 __global__ __launch_bounds__(256) void k_reduce_grads(const mep_wgrad_desc* __restrict__ wd, int n_wd, int wd_tiles,
                                                       const mep_colsum_desc* __restrict__ cd, int n_cd, int cd_tiles,
                                                       mep_head_desc hd, HeadGrads hg, int head_blocks,
-                                                      float* norm, int* step, const float* hyper) {
+                                                      float* norm, int* step, const float* hyper,
+                                                      const unsigned* __restrict__ bmap) {
     int bx = blockIdx.x;
     float sq = 0.f;
     MEP_RG_STAMP(0, __builtin_amdgcn_s_memrealtime());
-    if (bx < head_blocks) {
+    if (bmap) {
+        const unsigned job = bmap[bx];
+        const int kind = (int)(job >> 30), di = (int)((job >> 12) & 0x3ffffu), blk = (int)(job & 0xfffu);
+        MEP_RG_STAMP(3, kind);
+        if (kind == 0) sq = head_reduce_block(hd, hg, blk);
+        else if (kind == 1) sq = wgrad_reduce_block(wd[di], blk);
+        else sq = colsum_block(cd[di], blk);
+    } else if (bx < head_blocks) {
         MEP_RG_STAMP(3, 0);
         sq = head_reduce_block(hd, hg, bx);
     } else {
@@ -702,6 +713,26 @@ extern "C" int mep_head_fwd_bwd(const mep_head_desc* d, mep_stream_t stream) {
     return mep_check_launch("mep_head_fwd_bwd");
 }
 
+extern "C" int mep_reduce_grads_mapped(const mep_wgrad_desc* wgrad, const mep_colsum_desc* colsum,
+                                       const mep_head_desc* head, uint64_t g_trans, uint64_t g_ln_w, uint64_t g_ln_b,
+                                       uint64_t g_wo, uint64_t g_bo, uint64_t g_wc0, uint64_t g_wc1, uint64_t loss,
+                                       float* norm, int* step, const float* hyper, const unsigned* bmap, int n_blocks,
+                                       mep_stream_t stream) {
+    if (head && head->NC > NCMAX) { mep_set_error("mep_reduce_grads_mapped: invalid head descriptor"); return MEP_EINVAL; }
+    if (!bmap || n_blocks < 0) { mep_set_error("mep_reduce_grads_mapped: need the block map"); return MEP_EINVAL; }
+    if (n_blocks == 0) return 0;
+    mep_head_desc hd{};
+    HeadGrads g{};
+    if (head) {
+        hd = *head;
+        g = HeadGrads{(float*)g_trans, (float*)g_ln_w, (float*)g_ln_b, (float*)g_wo, (float*)g_bo,
+                      (float*)g_wc0, (float*)g_wc1, (float*)loss};
+    }
+    hipLaunchKernelGGL(k_reduce_grads, dim3(n_blocks), dim3(256), 0, (hipStream_t)stream, wgrad, 0, 0, colsum, 0, 0,
+                       hd, g, 0, norm, step, hyper, bmap);
+    return mep_check_launch("mep_reduce_grads_mapped");
+}
+
 extern "C" int mep_reduce_grads(const mep_wgrad_desc* wgrad, int n_wgrad, int wgrad_tiles, const mep_colsum_desc* colsum,
                                 int n_colsum, int colsum_tiles, const mep_head_desc* head, uint64_t g_trans,
                                 uint64_t g_ln_w, uint64_t g_ln_b, uint64_t g_wo, uint64_t g_bo, uint64_t g_wc0,
@@ -724,7 +755,7 @@ extern "C" int mep_reduce_grads(const mep_wgrad_desc* wgrad, int n_wgrad, int wg
     const int blocks = hb + n_wgrad * wg_red_blocks(wgrad_tiles) + n_colsum * colsum_tiles;
     if (blocks <= 0) return 0;
     hipLaunchKernelGGL(k_reduce_grads, dim3(blocks), dim3(256), 0, (hipStream_t)stream, wgrad, n_wgrad,
-                       wgrad_tiles, colsum, n_colsum, colsum_tiles, hd, g, hb, norm, step, hyper);
+                       wgrad_tiles, colsum, n_colsum, colsum_tiles, hd, g, hb, norm, step, hyper, nullptr);
     return mep_check_launch("mep_reduce_grads");
 }
 

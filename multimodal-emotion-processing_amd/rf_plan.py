@@ -27,7 +27,8 @@ import torch
 from . import _lib
 from ._lib import (AttnBwdDesc, AttnDesc, ColsumDesc, DescArray, GemmDesc, PoolDesc, RfEpiBwdDesc, RfEpiDesc,
                    RfHeadDesc, Rows, SumDesc, launch)
-from .trimodal import CHAINS, MODS, TIME_ORDER, UNIFY_NAMES, _norm_args, cdiv, crows, make_wgrad, rows
+from .trimodal import (CHAINS, MODS, TIME_ORDER, UNIFY_NAMES, _norm_args, cdiv, crows, make_wgrad, reduce_map,
+                       reduce_mapped, rows)
 
 RF_SPLITQ = _lib.switch('MEP_RF_SPLITQ', '1') != '0'   # attention backward: query tiles over 4 waves
 # unify + projections of each modality in one launch (mep_rfw_front) up to RF_FRONT_MAX_TILES
@@ -532,6 +533,7 @@ class RealformerPlan:
             col(self.row_loss.data_ptr(), self.loss.data_ptr(), self.B, 1, 1, not_grad=True)   # the batch loss
         self.d_colsum = DescArray(ColsumDesc, cs, dev)
         self.t_colsum = max(cdiv(c.n_cols, 32) for c in cs)
+        self.redmap = reduce_map(self.d_wgrad, self.d_colsum, None, dev)
 
     # ------------------------------------------------------------------ execution
     def set_global_rows(self, n):
@@ -647,16 +649,13 @@ class RealformerPlan:
         launch('mep_wgrad', self.d_wgrad, self.t_wgrad, stream)
         # weight-gradient split sums and LayerNorm / ReZero / residual-coefficient column sums: one
         # launch (no head partials here: the State_Transfer head reduces in mep_rf_head)
-        _lib.call('mep_reduce_grads', self.d_wgrad.ptr, self.d_wgrad.n, self.t_wgred, self.d_colsum.ptr,
-                  self.d_colsum.n, self.t_colsum if self.d_colsum.n else 0, None, 0, 0, 0, 0, 0, 0, 0, 0,
-                  *_norm_args(self), stream=stream)
+        reduce_mapped(self.d_wgrad, self.d_colsum, None, None, _norm_args(self), self.redmap, stream)
 
     norm_fold = None   # (optimizer workspace, step, hyper) pointers: the clip's norm pass folded into the reduction
 
     def reduce_grid(self):
         """blocks of the backward's mep_reduce_grads launch (the optimizer's folded norm partials)"""
-        return _lib.lib().mep_reduce_grads_grid(self.d_wgrad.n, self.t_wgred, self.d_colsum.n,
-                                                self.t_colsum if self.d_colsum.n else 0, None)
+        return self.redmap[1]
 
 
 class RealformerRunner:

@@ -357,6 +357,35 @@ def make_wgrad(items, dev, tok_per_split=None, bf16=False, counts=None):
     return ws, arr, len(segs), rmax
 
 
+def reduce_map(wgrad, colsum, head, dev):
+    """The job list of a mep_reduce_grads_mapped launch: the head-parameter blocks (head: HeadDesc
+    or None), every split-sum block of each weight-gradient descriptor (1,024 entries each), every
+    32-column tile of each column sum -- only real jobs, kind << 30 | descriptor << 12 | block.
+    -> (device uint32 map, block count)"""
+    import numpy as np
+    jobs = []
+    if head is not None:
+        jobs += [j for j in range(_lib.lib().mep_reduce_grads_grid(0, 0, 0, 0, ctypes.byref(head)))]
+    for i, d in enumerate(wgrad.items if wgrad is not None else []):
+        jobs += [(1 << 30) | (i << 12) | b for b in range(cdiv(d.N * d.Ktot, 1024))]
+    for i, c in enumerate(colsum.items if colsum is not None else []):
+        jobs += [(2 << 30) | (i << 12) | b for b in range(cdiv(c.n_cols, 32))]
+    assert all((j & 0xfff) < 4096 and ((j >> 12) & 0x3ffff) < (1 << 18) for j in jobs)
+    arr = np.array(jobs or [0], dtype=np.uint32).view(np.int32)
+    return torch.from_numpy(arr.copy()).to(dev), len(jobs)
+
+
+def reduce_mapped(wgrad, colsum, head, head_grads, norm, bmap, stream=None):
+    """one mep_reduce_grads_mapped launch over reduce_map's jobs (bmap = (map, blocks))"""
+    m, n = bmap
+    if n == 0:
+        return
+    hg = [int(x) for x in head_grads] if head is not None else [0] * 8
+    _lib.call('mep_reduce_grads_mapped', wgrad.ptr if wgrad is not None else None,
+              colsum.ptr if colsum is not None else None, ctypes.byref(head) if head is not None else None,
+              *hg, *norm, ctypes.c_void_p(m.data_ptr()), int(n), stream=stream)
+
+
 def rows(t, T, sB, sT, off=0):
     """row view of tensor t (strides and offset in elements: 4-byte fp32 or 2-byte bf16 rows);
     the kernels' 24-bit row addressing (include/mep.h mep_rows) bounds the strides and offsets"""
@@ -752,6 +781,7 @@ class TriModalPlan:
                            self.loss.data_ptr())
         self.d_losssum = DescArray(ColsumDesc, [ColsumDesc(partial=self.row_loss.data_ptr(), out=self.loss.data_ptr(),
                                                            n_rows=self.B, n_cols=1, ld=1, accumulate=0)], dev)
+        self.redmap = reduce_map(self.d_wgrad, self.d_colsum, self.head, dev)
 
     # ------------------------------------------------------------------ execution
     def set_inputs(self, l, v, a, lm, vm, am, labels=None):
@@ -824,10 +854,6 @@ class TriModalPlan:
         self.head.ext_dlogits = 0
         _lib.call('mep_head_fwd_bwd', ctypes.byref(self.head), stream=stream)
 
-    def _reduce_args(self):
-        """(wgrad descriptor array, reduce tiles) of the step's mep_reduce_grads launch"""
-        return self.d_wgrad, self.t_wgred
-
     def backward(self, ext_dlogits=None, stream=None):
         """Backward from the fused-loss head partials, or from external dlogits [B, NC].
         Writes every parameter gradient into the flat gradient buffer (flat.grad) and the batch
@@ -848,18 +874,14 @@ class TriModalPlan:
             launch('mep_layernorm_bwd', self.d_ulnb, cdiv(max(self.ntok.values()), 64), stream)
         launch('mep_wgrad', self.d_wgrad, self.t_wgrad, stream)
         # weight-gradient split sums, LayerNorm / residual-coefficient column sums and the head
-        # parameter sums: one launch
-        red, t_red = self._reduce_args()
-        _lib.call('mep_reduce_grads', red.ptr, red.n, t_red, self.d_colsum.ptr,
-                  self.d_colsum.n, self.t_colsum, ctypes.byref(self.head), *self.head_grads, *_norm_args(self),
-                  stream=stream)
+        # parameter sums: one launch over the real jobs only
+        reduce_mapped(self.d_wgrad, self.d_colsum, self.head, self.head_grads, _norm_args(self), self.redmap, stream)
 
     norm_fold = None   # (optimizer workspace, step, hyper) pointers: the clip's norm pass folded into the reduction
 
     def reduce_grid(self):
         """blocks of the backward's mep_reduce_grads launch (the optimizer's folded norm partials)"""
-        red, t_red = self._reduce_args()
-        return _lib.lib().mep_reduce_grads_grid(red.n, t_red, self.d_colsum.n, self.t_colsum, ctypes.byref(self.head))
+        return self.redmap[1]
 
     def advance_seed(self, stream=None):
         _lib.call('mep_seed_advance', ctypes.c_void_p(self.seed.data_ptr()), stream=stream)
@@ -885,6 +907,7 @@ class TriModalPlan:
         cb = DescArray(ColsumDesc, self._colsum_b, dev)
         self._check_bucket_ranges(wa[1], wb[1], ca, cb)
         self._buckets = (wa, wb, ca, cb)
+        self._bucket_maps = (reduce_map(wa[1], ca, self.head, dev), reduce_map(wb[1], cb, None, dev))
 
     def _check_bucket_ranges(self, wa, wb, ca, cb):
         """Bucket membership is defined twice -- by parameter name (TriModalSpec.bucket_a, which
@@ -929,16 +952,14 @@ class TriModalPlan:
             launch('mep_block_epi_bwd', self.d_epib[i], self.t_epi[i], stream, threads=sp.D | self.prec)
             if i == 0:
                 launch('mep_wgrad', da, ta, stream)
-                _lib.call('mep_reduce_grads', da.ptr, da.n, ra, ca.ptr, ca.n, self.t_colsum if ca.n else 0,
-                          ctypes.byref(self.head), *self.head_grads, None, None, None, stream=stream)
+                reduce_mapped(da, ca, self.head, self.head_grads, (None, None, None), self._bucket_maps[0], stream)
                 bucket_a_done()
             launch('mep_attn_bwd', self.d_attnb[i], self.t_attnb[i], stream, threads=self.f_attnb[i] | self.prec)
         launch('mep_sum_rows', self.d_sum, self.t_sum, stream)
         if sp.unify_norm:
             launch('mep_layernorm_bwd', self.d_ulnb, cdiv(max(self.ntok.values()), 64), stream)
         launch('mep_wgrad', db, tb, stream)
-        _lib.call('mep_reduce_grads', db.ptr, db.n, rb, cb.ptr, cb.n, self.t_colsum if cb.n else 0, None,
-                  0, 0, 0, 0, 0, 0, 0, 0, None, None, None, stream=stream)
+        reduce_mapped(db, cb, None, None, (None, None, None), self._bucket_maps[1], stream)
 
     def loss_only(self, stream=None):
         """Batch loss (sum of the scaled per-row losses) without the backward."""

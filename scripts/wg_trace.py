@@ -25,13 +25,15 @@ def main():
     ap.add_argument('--dtype', default='fp32', choices=('fp32', 'bf16'))
     ap.add_argument('--balance', type=int, default=1)
     ap.add_argument('--reduce', type=int, default=0, help='1: trace the mep_reduce_grads launch instead')
+    ap.add_argument('--config', default='cfg3')
     args = ap.parse_args()
     import bench
     from mep_amd import _lib, trimodal
     from mep_amd._lib import launch
     trimodal.WG_BALANCE = bool(args.balance)
     dev = torch.device('cuda:0')
-    work = bench.CONFIGS['cfg3'](dev, 0, graph=False, bf16=args.dtype == 'bf16')
+    kw = {} if args.config in ('cfg2', 'rfstate') else dict(bf16=args.dtype == 'bf16')
+    work = bench.CONFIGS[args.config](dev, 0, graph=False, **kw)
     for _ in range(3):
         work.eager_step()
     torch.cuda.synchronize()
@@ -67,7 +69,7 @@ def trace_reduce(work, args):
         work.eager_step()
         torch.cuda.synchronize()
         fn(buf.ctypes.data)
-    n = p.reduce_grid()
+    n = min(p.reduce_grid(), 8192)   # the trace buffer holds the first 8,192 blocks
     t = buf[:n].astype(np.float64)
     t0 = t[:, 0].min()
     us = (t[:, :3] - t0) / 100.0

@@ -24,7 +24,7 @@ def declared_functions():
 
 def test_library_loads_and_version():
     L = _lib.lib()
-    assert L.mep_abi_version() == _lib.ABI_VERSION == 6
+    assert L.mep_abi_version() == _lib.ABI_VERSION == 7
 
 
 def test_every_declared_symbol_is_exported():

@@ -488,3 +488,38 @@ def test_wgemm_ws_only_within_its_k_limit():
     assert not _lib.wgemm_ws_fits(wide)
     small = [NS(ntok=3200, N=96, K=300)]
     assert not _lib.wgemm_ws_fits(small)
+
+
+def _check_reduce_map(bmap, wgrad, colsum, head):
+    """a mep_reduce_grads_mapped job list: every real job once, nothing else"""
+    import numpy as np
+    m, n = bmap
+    jobs = m.cpu().numpy().view(np.uint32)[:n]
+    want = set()
+    if head is not None:
+        want |= {(0, 0, j) for j in range(_lib.lib().mep_reduce_grads_grid(0, 0, 0, 0, ctypes.byref(head)))}
+    for i, d in enumerate(wgrad.items):
+        want |= {(1, i, b) for b in range(cdiv(d.N * d.Ktot, 1024))}
+    for i, c in enumerate(colsum.items if colsum is not None else []):
+        want |= {(2, i, b) for b in range(cdiv(c.n_cols, 32))}
+    got = [(int(j) >> 30, (int(j) >> 12) & 0x3ffff, int(j) & 0xfff) for j in jobs]
+    assert len(got) == len(set(got)) == len(want) and set(got) == want
+
+
+def test_reduce_maps_list_every_real_job():
+    """the compact block maps of the gradient reduction (trimodal.reduce_map): cfg3 (one launch and
+    the two data-parallel buckets) and State_Transfer, whose rectangular grid was 29,430 blocks"""
+    from mep_amd import cmu_mosei
+    from mep_amd import realformer as rf, rf_plan
+    p = cmu_mosei.Concat_Trans(96, 50, 50, 50, 6, 1, 1).mep_runner('cpu').plan(64, (50, 50, 50))
+    _check_reduce_map(p.redmap, p.d_wgrad, p.d_colsum, p.head)
+    assert p.redmap[1] < p.reduce_grid() + 1 and p.redmap[1] < 1377
+    p._build_buckets()
+    (_, da, _, _), (_, db, _, _), ca, cb = p._buckets
+    _check_reduce_map(p._bucket_maps[0], da, ca, p.head)
+    _check_reduce_map(p._bucket_maps[1], db, cb, None)
+    st = rf.State_Transfer(300, 35, 74, 96, 50, 50, 50, 6, 2, 2)
+    r = st.mep_runner('cpu')
+    q = rf_plan.RealformerPlan(r.spec, r.flat, 64, 6, 'cpu')
+    _check_reduce_map(q.redmap, q.d_wgrad, q.d_colsum, None)
+    assert q.reduce_grid() == q.redmap[1] < 3000
