@@ -27,8 +27,8 @@ import torch
 from . import _lib
 from ._lib import (AttnBwdDesc, AttnDesc, ColsumDesc, DescArray, GemmDesc, PoolDesc, RfEpiBwdDesc, RfEpiDesc,
                    RfHeadDesc, Rows, SumDesc, launch)
-from .trimodal import (CHAINS, MODS, TIME_ORDER, UNIFY_NAMES, _norm_args, cdiv, crows, make_wgrad, reduce_map,
-                       reduce_mapped, rows)
+from .trimodal import (CHAINS, MODS, TIME_ORDER, UNIFY_NAMES, _norm_args, cdiv, crows, make_wgrad, reduce_blocks,
+                       reduce_map, reduce_mapped, rows)
 
 RF_SPLITQ = _lib.switch('MEP_RF_SPLITQ', '1') != '0'   # attention backward: query tiles over 4 waves
 # unify + projections of each modality in one launch (mep_rfw_front) up to RF_FRONT_MAX_TILES
@@ -655,7 +655,7 @@ class RealformerPlan:
 
     def reduce_grid(self):
         """blocks of the backward's mep_reduce_grads launch (the optimizer's folded norm partials)"""
-        return self.redmap[1]
+        return reduce_blocks(self.d_wgrad, self.d_colsum, None, self.redmap)
 
 
 class RealformerRunner:

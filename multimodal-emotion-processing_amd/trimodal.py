@@ -375,9 +375,36 @@ def reduce_map(wgrad, colsum, head, dev):
     return torch.from_numpy(arr.copy()).to(dev), len(jobs)
 
 
+# 0: the rectangular mep_reduce_grads grid (A/B runs)
+REDUCE_MAP = _lib.switch('MEP_REDUCE_MAP', '1') != '0'
+
+
+def reduce_rect_blocks(wgrad, colsum, head):
+    """blocks of the rectangular mep_reduce_grads grid over the same descriptors"""
+    wt = max((cdiv(d.N * d.Ktot, 256) for d in (wgrad.items if wgrad is not None else [])), default=0)
+    ct = max((cdiv(c.n_cols, 32) for c in (colsum.items if colsum is not None else [])), default=0)
+    return _lib.lib().mep_reduce_grads_grid(wgrad.n if wgrad is not None else 0, wt,
+                                            colsum.n if colsum is not None else 0, ct,
+                                            ctypes.byref(head) if head is not None else None)
+
+
+def reduce_blocks(wgrad, colsum, head, bmap):
+    """blocks (= norm partials) of the step's reduction launch"""
+    return bmap[1] if REDUCE_MAP else reduce_rect_blocks(wgrad, colsum, head)
+
+
 def reduce_mapped(wgrad, colsum, head, head_grads, norm, bmap, stream=None):
-    """one mep_reduce_grads_mapped launch over reduce_map's jobs (bmap = (map, blocks))"""
+    """one mep_reduce_grads_mapped launch over reduce_map's jobs (bmap = (map, blocks)); with
+    REDUCE_MAP off the rectangular mep_reduce_grads launch"""
     m, n = bmap
+    if not REDUCE_MAP:
+        wt = max((cdiv(d.N * d.Ktot, 256) for d in (wgrad.items if wgrad is not None else [])), default=0)
+        ct = max((cdiv(c.n_cols, 32) for c in (colsum.items if colsum is not None else [])), default=0)
+        hg = [int(x) for x in head_grads] if head is not None else [0] * 8
+        _lib.call('mep_reduce_grads', wgrad.ptr if wgrad is not None else None, wgrad.n if wgrad is not None else 0, wt,
+                  colsum.ptr if colsum is not None else None, colsum.n if colsum is not None else 0, ct,
+                  ctypes.byref(head) if head is not None else None, *hg, *norm, stream=stream)
+        return
     if n == 0:
         return
     hg = [int(x) for x in head_grads] if head is not None else [0] * 8
@@ -881,7 +908,7 @@ class TriModalPlan:
 
     def reduce_grid(self):
         """blocks of the backward's mep_reduce_grads launch (the optimizer's folded norm partials)"""
-        return self.redmap[1]
+        return reduce_blocks(self.d_wgrad, self.d_colsum, self.head, self.redmap)
 
     def advance_seed(self, stream=None):
         _lib.call('mep_seed_advance', ctypes.c_void_p(self.seed.data_ptr()), stream=stream)
