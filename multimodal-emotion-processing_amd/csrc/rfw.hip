@@ -137,7 +137,10 @@ template <int D> constexpr int rfw_waves() { return D == 96 ? 6 : D >= 64 ? 4 : 
 // one 6-wave workgroup per CU (their register count leaves 8 wave slots) and run one tile per CU at
 // a time, which suits the cfg2 chain's few tiles.
 #ifndef MEP_RFW_BIG_TILES
-#define MEP_RFW_BIG_TILES 2048
+#define MEP_RFW_BIG_TILES 1024   // (round 6: 1024, so the rf_state_ref fixture's 1,350 tiles run these kernels)
+#endif
+#ifndef MEP_RFW_BIG_WPARTS
+#define MEP_RFW_BIG_WPARTS 2     // weight parts of the large-launch kernels (PG NW)
 #endif
 #ifndef MEP_RFW_BIG_WPE
 #define MEP_RFW_BIG_WPE 3
@@ -150,19 +153,23 @@ template <int D> constexpr int rfw_waves() { return D == 96 ? 6 : D >= 64 ? 4 : 
 // prime() issues the first DEPTH weight fragments (callers prime the NEXT product before the
 // current one's stores / exchange / LayerNorm, so the weight latency hides behind them), run()
 // streams the rest through the ring, one fragment's six MFMAs per step.
-template <int NI, int NPK, int R, int W, int DEP = MEP_RFW_DEPTH>
+// NW: weight parts read (3: every product of the six, fp32-level; 2: the large-launch kernels, whose
+// weight fragments stream from L2 per 16-token tile and bound them -- the third part feeds only
+// w2 x0, and without it the products are split.h's five, weights represented to <= 2^-18
+// relative, as the D = 128 tri-modal epilogues; 2/3 of the fragment bytes)
+template <int NI, int NPK, int R, int W, int DEP = MEP_RFW_DEPTH, int NW = 3>
 struct PG {
     static constexpr int NJ = (NI + W - 1) / W, NS = NJ * NPK;
     static constexpr int DEPTH = DEP < NS ? DEP : NS;
-    OpN<3> ring[DEPTH];
+    OpN<NW> ring[DEPTH];
     PartPtr wl;
     int wave;
-    MEP_DEV OpN<3> ld(int s) const {
+    MEP_DEV OpN<NW> ld(int s) const {
         const int p = s / NJ, i = wave + W * (s - (s / NJ) * NJ);
         const int ic = i < NI ? i : NI - 1;   // a wave without this tile loads a valid fragment it never uses
-        OpN<3> o;
+        OpN<NW> o;
 #pragma unroll
-        for (int t = 0; t < 3; ++t) o.p[t] = __builtin_bit_cast(bf16x8, wl[((t * R + 16 * ic) * NPK + p) * 4]);
+        for (int t = 0; t < NW; ++t) o.p[t] = __builtin_bit_cast(bf16x8, wl[((t * R + 16 * ic) * NPK + p) * 4]);
         return o;
     }
     MEP_DEV void prime(PartPtr w, int wave_) {
@@ -175,10 +182,10 @@ struct PG {
     MEP_DEV void run(f32x4 (&acc)[NJ], const OpN<3> (&b)[NPK]) {
 #pragma unroll
         for (int s = 0; s < NS; ++s) {
-            const OpN<3> a = ring[s % DEPTH];
+            const OpN<NW> a = ring[s % DEPTH];
             if (s + DEPTH < NS) ring[s % DEPTH] = ld(s + DEPTH);
             const int j = s % NJ;
-            if (wave + W * j < NI) acc[j] = mma_n<3>(a, b[s / NJ], acc[j]);
+            if (wave + W * j < NI) acc[j] = mma_nm<NW, 3>(a, b[s / NJ], acc[j]);
             __builtin_amdgcn_sched_barrier(0);
         }
     }
@@ -282,7 +289,7 @@ MEP_DEV void stash_owned(xf32x4* st, const mep_rows& r, int tc, int wave, int la
         if (wave + W * j < NB) st[(wave + W * j) * 64 + lane] = v[j];
 }
 
-template <int D, int FD, int W = rfw_waves<D>(), int WPE = 1, int DEP = MEP_RFW_DEPTH>
+template <int D, int FD, int W = rfw_waves<D>(), int WPE = 1, int DEP = MEP_RFW_DEPTH, int NW = 3>
 __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(WPE))) void k_rfw_fwd(const mep_rf_epi_desc* __restrict__ descs) {
     constexpr int NI = D / 16, NF = FD / 16, NP = D / 32, NPF = FD / 32;
     constexpr int JI = (NI + W - 1) / W, JF = (NF + W - 1) / W;
@@ -306,7 +313,7 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(WPE))) v
     // fragments, q (the wave's blocks, shared stash) and the parameters (LDS)
     f32x4 xv[NI];
     load_rows<NI>(xv, d.x, tc);
-    PG<NI, NP, D, W, DEP> g1;
+    PG<NI, NP, D, W, DEP, NW> g1;
     g1.prime(parts_at(d.wparts, MEP_RFW_PART_OFFSET(D, FD, 0)), wave);
     stash_owned<NI, W>(qst, d.q, tc, wave, lane);
     {
@@ -317,7 +324,7 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(WPE))) v
     MEP_RFW_STAMP(1);
     // xp = Wp x (the wave's tiles), exchanged (the exchange's barrier also publishes q and the parameters)
     f32x4 xp[NI];
-    PG<NF, NP, FD, W, DEP> g2;
+    PG<NF, NP, FD, W, DEP, NW> g2;
     {
         f32x4 acc[JI];
 #pragma unroll
@@ -348,7 +355,7 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(WPE))) v
     MEP_RFW_STAMP(4);
     // f1 = relu(W1 h + b1)
     f32x4 f1[NF];
-    PG<NI, NPF, D, W, DEP> g3;
+    PG<NI, NPF, D, W, DEP, NW> g3;
     {
         f32x4 acc[JF];
 #pragma unroll
@@ -400,7 +407,7 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(WPE))) v
         layer_norm_l<NI>(z, out, P + 2 * D, P + 3 * D, mean2, rstd2);
     }
     if (d.wq_next) {   // the next layer's query projection, qp_next = out Wq_next^T (wave's tiles)
-        PG<NI, NP, D, W, DEP> g4;
+        PG<NI, NP, D, W, DEP, NW> g4;
         g4.prime(reinterpret_cast<PartPtr>(G<const unsigned char>(d.wq_next)), wave);
         f32x4 acc[JI];
 #pragma unroll
@@ -465,7 +472,7 @@ MEP_DEV void ln_bwd(f32x4 (&dz)[NI], const f32x4 (&gu)[NI], const f32x4 (&xh)[NI
         for (int r = 0; r < 4; ++r) dz[i][r] = rstd * (gw[i][r] - s1 - xh[i][r] * s2);
 }
 
-template <int D, int FD, int W = rfw_waves<D>(), int WPE = 1, int DEP = MEP_RFW_DEPTH>
+template <int D, int FD, int W = rfw_waves<D>(), int WPE = 1, int DEP = MEP_RFW_DEPTH, int NW = 3>
 __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(WPE))) void k_rfw_bwd(const mep_rf_epi_bwd_desc* __restrict__ descs) {
     constexpr int NI = D / 16, NF = FD / 16, NP = D / 32, NPF = FD / 32;
     constexpr int JI = (NI + W - 1) / W, JF = (NF + W - 1) / W;
@@ -497,7 +504,7 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(WPE))) v
     load_rows<NI>(fv, d.f, tc);
 #pragma unroll
     for (int i = 0; i < NI; ++i) w2v[i] = ld4w(G<const float>(d.ln2_w) + 16 * i + 4 * g);
-    PG<NF, NP, FD, W, DEP> g1;
+    PG<NF, NP, FD, W, DEP, NW> g1;
     g1.prime(parts_at(d.wparts, MEP_RFW_PART_OFFSET(D, FD, 5)), wave);
     f32x4 f1v[JF], dqo[JI];
     {
@@ -524,7 +531,7 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(WPE))) v
         for (int i = 0; i < NI; ++i) gu[i] += g2[i];
     }
     if (bd.wq_in) {   // dout += dqp_in Wq: the next layer's query-projection input gradient (exchanged)
-        PG<NI, NP, D, W, DEP> g0;
+        PG<NI, NP, D, W, DEP, NW> g0;
         g0.prime(reinterpret_cast<PartPtr>(G<const unsigned char>(bd.wq_in)), wave);
         f32x4 dv[NI];
         load_rows<NI>(dv, bd.dqp_in, tc);
@@ -563,7 +570,7 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(WPE))) v
     }
     // df1 = relu'(f1) (W2^T df)
     f32x4 df1[NF];
-    PG<NI, NPF, D, W, DEP> g2;
+    PG<NI, NPF, D, W, DEP, NW> g2;
     {
         f32x4 acc[JF];
 #pragma unroll
@@ -587,7 +594,7 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(WPE))) v
     tile_colsum<NF, W>(part + 5 * D, df1, wave, c, g);       // db1
     // dh = dz2 + W1^T df1
     f32x4 dh[NI];
-    PG<NI, NP, D, W, DEP> g3;
+    PG<NI, NP, D, W, DEP, NW> g3;
     {
         f32x4 acc[JI];
 #pragma unroll
@@ -1256,7 +1263,7 @@ extern "C" int mep_rfw_epi_fwd(const mep_rf_epi_desc* descs, int n_desc, int max
     const int rc = dispatch_rfw(D, FD, [&](auto dc, auto fc) {
         constexpr int DD = decltype(dc)::value, FF = decltype(fc)::value;
         if (DD == 96 && big)
-            hipLaunchKernelGGL((k_rfw_fwd<DD, FF, rfw_waves<DD>(), MEP_RFW_BIG_WPE, MEP_RFW_BIG_DEPTH>), dim3(max_tiles, n_desc),
+            hipLaunchKernelGGL((k_rfw_fwd<DD, FF, rfw_waves<DD>(), MEP_RFW_BIG_WPE, MEP_RFW_BIG_DEPTH, MEP_RFW_BIG_WPARTS>), dim3(max_tiles, n_desc),
                                dim3(64 * rfw_waves<DD>()), 0, (hipStream_t)stream, descs);
         else
             hipLaunchKernelGGL((k_rfw_fwd<DD, FF>), dim3(max_tiles, n_desc), dim3(64 * rfw_waves<DD>()), 0,
@@ -1269,9 +1276,15 @@ extern "C" int mep_rfw_epi_fwd(const mep_rf_epi_desc* descs, int n_desc, int max
 extern "C" int mep_rfw_epi_bwd(const mep_rf_epi_bwd_desc* descs, int n_desc, int max_tiles, int D, int FD,
                                mep_stream_t stream) {
     if (n_desc <= 0 || max_tiles <= 0) return 0;
+    const bool big = (int64_t)max_tiles * n_desc >= MEP_RFW_BIG_TILES;
     const int rc = dispatch_rfw(D, FD, [&](auto dc, auto fc) {
-        hipLaunchKernelGGL((k_rfw_bwd<decltype(dc)::value, decltype(fc)::value>), dim3(max_tiles, n_desc),
-                           dim3(64 * rfw_waves<decltype(dc)::value>()), 0, (hipStream_t)stream, descs);
+        constexpr int DD = decltype(dc)::value, FF = decltype(fc)::value;
+        if (DD == 96 && big)
+            hipLaunchKernelGGL((k_rfw_bwd<DD, FF, rfw_waves<DD>(), 1, MEP_RFW_DEPTH, MEP_RFW_BIG_WPARTS>), dim3(max_tiles, n_desc),
+                               dim3(64 * rfw_waves<DD>()), 0, (hipStream_t)stream, descs);
+        else
+            hipLaunchKernelGGL((k_rfw_bwd<DD, FF>), dim3(max_tiles, n_desc), dim3(64 * rfw_waves<DD>()), 0,
+                               (hipStream_t)stream, descs);
     });
     if (rc) { mep_set_error("mep_rfw_epi_bwd: D in {32,64,96,128} and FD in {D, 2D}"); return rc; }
     return mep_check_launch("mep_rfw_epi_bwd");

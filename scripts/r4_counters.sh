@@ -49,8 +49,9 @@ if [ $STAGE = sq ] || [ $STAGE = all ]; then
   # keep only the counters this rocprofv3 lists (an unknown name fails the pass)
   timeout -k 10 120 rocprofv3 -L > $OUT/list.txt 2>&1 || true
   known() { local out=""; for c in $1; do grep -qw "$c" $OUT/list.txt && out="$out $c"; done; echo $out; }
-  G1=$(known "$G1"); G2=$(known "$G2"); G3=$(known "$G3")
-  echo "G1: $G1"; echo "G2: $G2"; echo "G3: $G3"
+  G4="TCC_HIT_sum TCC_MISS_sum TCC_REQ_sum TCC_READ_sum"   # L2 (round 6): hits / requests per kernel
+  G1=$(known "$G1"); G2=$(known "$G2"); G3=$(known "$G3"); G4=$(known "$G4")
+  echo "G1: $G1"; echo "G2: $G2"; echo "G3: $G3"; echo "G4: $G4"
   for cfg in ${CFGS:-cfg3 cfg3_bf16 cfg2 cfg5 cfg5_bf16}; do
     case $cfg in
       cfg3) A="--config cfg3 --dtype fp32";; cfg3_bf16) A="--config cfg3 --dtype bf16";;
@@ -59,7 +60,7 @@ if [ $STAGE = sq ] || [ $STAGE = all ]; then
     esac
     A="$A --no-bf16 --no-probe"
     i=0
-    for grp in "$G1" "$G2" "$G3"; do
+    for grp in "$G1" "$G2" "$G3" ${SQ_L2:+"$G4"}; do
       i=$((i+1))
       pass ${cfg}_g$i rocprofv3 --pmc $grp --kernel-trace -d $OUT/${cfg}_g$i -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline $A
     done

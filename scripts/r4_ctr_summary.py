@@ -63,7 +63,9 @@ def main():
     stats = sys.argv[3] if len(sys.argv) > 3 else 'profiles/r04_kernel_stats_%s.csv' % cfg
     tag = sys.argv[4] if len(sys.argv) > 4 else 'r04'
     tab = collections.defaultdict(dict)
-    for g in (1, 2, 3):
+    for g in (1, 2, 3, 4):   # g4 (optional, SQ_L2=1): the L2 group
+        if g == 4 and not os.path.isdir(os.path.join(src, '%s_g4' % cfg)):
+            continue
         for k, cs in load(os.path.join(src, '%s_g%d' % (cfg, g))).items():
             for c, v in cs.items():
                 tab[k].setdefault(c, v)          # GRBM_GUI_ACTIVE is in two groups: keep the first
@@ -100,6 +102,9 @@ def main():
                     e[name + '_frac'] = round(c[ctr] / wc, 4)
         if c.get('SQ_LDS_IDX_ACTIVE'):
             e['lds_conflict'] = round(c.get('SQ_LDS_BANK_CONFLICT', 0.0) / c['SQ_LDS_IDX_ACTIVE'], 4)
+        if c.get('TCC_HIT_sum', 0.0) + c.get('TCC_MISS_sum', 0.0) > 0:
+            e['l2_hit'] = round(c['TCC_HIT_sum'] / (c['TCC_HIT_sum'] + c['TCC_MISS_sum']), 4)
+            e['l2_req_per_dispatch'] = c.get('TCC_REQ_sum')
         e['raw'] = {kk: round(v, 1) for kk, v in sorted(c.items())}
         res[k] = e
     os.makedirs('profiles', exist_ok=True)
@@ -107,17 +112,18 @@ def main():
     order = sorted(res, key=lambda k: -(res[k]['avg_us'] or 0))
     lines = ['# %s SQ counters' % tag + ', %s bench workload (scripts/r4_counters.sh, scripts/r4_ctr_summary.py); '
              'durations: %s' % (cfg, os.path.basename(stats)),
-             '%-18s %8s %7s %8s %7s %7s %7s %7s %7s %7s %6s %6s %6s %6s' % (
+             '%-18s %8s %7s %8s %7s %7s %7s %7s %7s %7s %6s %6s %6s %6s %6s %8s' % (
                  'kernel', 'avg_us', 'waves', 'TFLOP/s', 'mfmaU', 'mfmaBz', 'valuBz', 'VALU/w', 'MFMA/w', 'VMEM/w',
-                 'wait', 'stall', 'activ', 'ldsCf')]
+                 'wait', 'stall', 'activ', 'ldsCf', 'l2hit', 'l2reqM')]
     for k in order:
         e = res[k]
         f = lambda x, fmt='%7.3f': (fmt % x) if isinstance(x, (int, float)) else '%7s' % '-'   # noqa: E731
-        lines.append('%-18s %8s %7d %8s %7s %7s %7s %7s %7s %7s %6s %6s %6s %6s' % (
+        lines.append('%-18s %8s %7d %8s %7s %7s %7s %7s %7s %7s %6s %6s %6s %6s %6s %8s' % (
             k[:18], f(e['avg_us'], '%8.2f'), e['waves'], f(e.get('mfma_tflops'), '%8.1f'), f(e.get('mfma_util')),
             f(e.get('mfma_busy')), f(e.get('valu_busy')), f(e.get('valu_per_wave'), '%7.0f'),
             f(e.get('mfma_per_wave'), '%7.0f'), f(e.get('vmem_rd_per_wave'), '%7.0f'), f(e.get('wait_frac'), '%6.2f'),
-            f(e.get('issue_stall_frac'), '%6.2f'), f(e.get('active_frac'), '%6.2f'), f(e.get('lds_conflict'), '%6.3f')))
+            f(e.get('issue_stall_frac'), '%6.2f'), f(e.get('active_frac'), '%6.2f'), f(e.get('lds_conflict'), '%6.3f'),
+            f(e.get('l2_hit'), '%6.3f'), f(e['l2_req_per_dispatch'] / 1e6 if e.get('l2_req_per_dispatch') else None, '%8.2f')))
     open('profiles/%s_counters_%s.txt' % (tag, cfg), 'w').write('\n'.join(lines) + '\n')
     print('\n'.join(lines))
 
