@@ -17,6 +17,7 @@
 // MEP_RFW_DEPTH fragments ahead of their MFMAs.
 #include <atomic>
 #include <algorithm>
+#include <cstdlib>
 
 #include "common.h"
 #include "split.h"
@@ -563,7 +564,7 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(WPE))) v
         for (int i = 0; i < NI; ++i)
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                pw2[i][r] = gu[i][r] * xh[i][r];
+                pw2[i][r] = mul_rn(gu[i][r], xh[i][r]);   // rounded: a product fused into the column sum's first add would depend on the schedule
                 df[i][r] = sb * dz2[i][r];
                 db_s += dz2[i][r] * fv[i][r];
             }
@@ -626,7 +627,7 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(WPE))) v
         for (int i = 0; i < NI; ++i)
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                pw[i][r] = dh[i][r] * xh[i][r];
+                pw[i][r] = mul_rn(dh[i][r], xh[i][r]);
                 dxp[i][r] = sa * dz1[i][r];
                 da_s += dz1[i][r] * xpv[i][r];
             }
@@ -656,6 +657,498 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(WPE))) v
         split_ops<NP>(ds, dxp);
         g3.run(acc, ds);
         if (ok) store_mine<NI, W>(bd.dx, tok, acc, wave);
+    }
+}
+
+// ---------------------------------------------------------------- weight-stationary large launches
+// (round 6, MEP_RFS) The State_Transfer epilogue launches (>= MEP_RFW_BIG_TILES tiles, D = 96):
+// k_rfw_fwd / k_rfw_bwd stream every weight fragment from L2 once per 16-token tile (10,800 tiles
+// per launch, ~44 M L2 requests, MFMA busy 0.05-0.08).  Here one 8-wave workgroup per CU walks
+// jobs of 8 tiles (128 tokens) of one descriptor: each wave owns one tile for the whole chain
+// (every output tile of every product, so the LayerNorms run in-wave and nothing is exchanged),
+// and the workgroup copies each product's 2-part weight fragments into one of two 72-KiB LDS
+// buffers by LDS-DMA while it multiplies the previous product from the other -- a fragment leaves
+// L2 once per 8 tiles.  Per step: barrier -> the previous step's stores -> the next product's DMA
+// and the rows this step's epilogue needs -> MFMAs from LDS -> epilogue -> vmcnt(0) + barrier; the
+// rows the next job's first product multiplies are loaded one step ahead.  The products are
+// k_rfw_*<..., NW = 2>'s in the same order per accumulator, and every epilogue the same
+// arithmetic: results bit-identical to those kernels (test_gpu_rfw.py).
+#ifndef MEP_RFS_FWD_W
+#define MEP_RFS_FWD_W 8   // waves (16-token tiles) per workgroup: 2 per SIMD (186 VGPRs)
+#endif
+#ifndef MEP_RFS_BWD_W
+#define MEP_RFS_BWD_W 4   // 1 per SIMD: the backward's live rows need 256 VGPRs + AGPRs
+#endif
+constexpr int RFS_IMG = 1024;            // one part image of a fragment: 64 lanes x 16 B
+constexpr int RFS_BUF = 72 * RFS_IMG;    // the largest product's fragments: 12 x 3 or 6 x 6 pairs, 2 parts
+typedef __attribute__((address_space(3))) unsigned char lbyte_t;
+typedef __attribute__((address_space(3))) void lvoid_t;
+typedef __attribute__((address_space(3))) const bf16x8 lcbf8_t;
+
+// every wave's LDS-DMA and loads / stores retired, then the workgroup barrier
+MEP_DEV void rfs_sync() { asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// parts 0 and 1 of a product's fragments (NO output tiles x NPK k pairs of mep_wsplit parts with R
+// rows) -> an LDS buffer: image f = (i * NPK + p) * 2 + t holds lane l's 16-byte unit at 16 l (one
+// conflict-free ds_read_b128 per part), the W waves taking every W-th image
+template <int NO, int NPK, int R, int W>
+MEP_DEV void rfs_stage(lbyte_t* buf, uint64_t w, int wave, int lane) {
+    constexpr int NIMG = NO * NPK * 2;
+    static_assert(NIMG * RFS_IMG <= RFS_BUF, "rfs buffer");
+    const auto rs = __builtin_amdgcn_make_buffer_rsrc((void*)w, 0, MEP_WSPLIT_BYTES(R, 32 * NPK), 0x00020000);
+    const int c = lane & 15, g = lane >> 4;
+    for (int f = wave; f < NIMG; f += W) {
+        const int t = f & 1, ip = f >> 1, i = ip / NPK, p = ip - i * NPK;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lvoid_t*)(buf + f * RFS_IMG), 16,
+                                                 16 * (((t * R + 16 * i + c) * NPK + p) * 4 + g), 0, 0, 0);
+    }
+}
+
+// acc[i] = sum over the k pairs, in order, of W'(16 i + c, pair p) . X for every output tile i:
+// pair-major (each pair's activation operand split once, as split_ops, its NO fragments' MFMAs on
+// independent accumulators), the fragments read from LDS through a ring RFS_DEPTH steps ahead
+// (a scheduling barrier per step: left alone, the compiler hoists every read of the product and
+// spills)
+#ifndef MEP_RFS_DEPTH
+#define MEP_RFS_DEPTH 3
+#endif
+template <int NO, int NPK>
+MEP_DEV void rfs_mul(f32x4 (&acc)[NO], const lbyte_t* buf, const f32x4* v, int lane) {
+    constexpr int NS = NO * NPK, DEP = MEP_RFS_DEPTH < NS ? MEP_RFS_DEPTH : NS;
+    const lbyte_t* b = buf + 16 * lane;
+    auto ld = [&](int s) {
+        const int p = s / NO, i = s - p * NO;
+        OpN<2> a;
+        a.p[0] = *(lcbf8_t*)(b + ((i * NPK + p) * 2) * RFS_IMG);
+        a.p[1] = *(lcbf8_t*)(b + ((i * NPK + p) * 2 + 1) * RFS_IMG);
+        return a;
+    };
+    OpN<2> ring[DEP];
+#pragma unroll
+    for (int s = 0; s < DEP; ++s) ring[s] = ld(s);
+#pragma unroll
+    for (int i = 0; i < NO; ++i) acc[i] = zero_f4();
+    OpN<3> x;
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+        const int p = s / NO, i = s - p * NO;
+        if (i == 0) x = opn<3>(v[2 * p], v[2 * p + 1]);
+        const OpN<2> a = ring[s % DEP];
+        if (s + DEP < NS) ring[s % DEP] = ld(s + DEP);
+        acc[i] = mma_nm<2, 3>(a, x, acc[i]);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+}
+
+// a tile's 16-token column sums of NB blocks, packed: lane (c, g) keeps block c's sums of
+// features 16 c + 4 g .. +3 (row16_sum leaves the same sum in every lane of a row); stored by the
+// lanes c < NB at the partial row (4-byte aligned: scalar stores)
+template <int NB>
+MEP_DEV f32x4 rfs_colsum(const f32x4 (&v)[NB], int c) {
+    f32x4 k = zero_f4();
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+        f32x4 s;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) s[r] = row16_sum(v[i][r]);
+        if (c == i) k = s;
+    }
+    return k;
+}
+MEP_DEV void rfs_colsum_store(gfloat* dst, const f32x4& k, int nb, int c, int g) {
+    if (c < nb) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) dst[16 * c + 4 * g + r] = k[r];
+    }
+}
+
+// the jobs (descriptor, batch of W tiles) a workgroup walks: blockIdx.x, + gridDim.x, ...,
+// skipping batches past a descriptor's tokens (uniform over the workgroup)
+MEP_DEV int rfs_ntok(const mep_rf_epi_desc& d) { return d.ntok; }
+MEP_DEV int rfs_ntok(const mep_rf_epi_bwd_desc& d) { return d.f.ntok; }
+template <typename Desc, int W>
+struct RfsJobs {
+    const Desc* descs;
+    int njobs, nbat;
+    MEP_DEV int ntok(int j) const { return rfs_ntok(descs[j / nbat]); }
+    MEP_DEV bool valid(int j) const { return j < njobs && (j % nbat) * (16 * W) < ntok(j); }
+    // (readfirstlane: the job index is workgroup-uniform; without it the compiler keeps it in a
+    // VGPR and reads every descriptor field with vector loads and vmcnt(0) waits)
+    MEP_DEV int next(int j) const {
+        do { j += gridDim.x; } while (j < njobs && !valid(j));
+        return __builtin_amdgcn_readfirstlane(j);
+    }
+    MEP_DEV int first() const { return valid(blockIdx.x) ? (int)blockIdx.x : next(blockIdx.x); }
+};
+
+// a job's LayerNorm / bias parameters [n0 | n1 | ...] -> the job's LDS parameter slot: loaded into
+// registers at the start of the previous job's last step (before its DMA, so the wait for them,
+// at the end of that step, is for loads issued a step earlier), written to LDS there, published by
+// the step's barrier
+template <int TOTAL, int NSEG, int W>
+struct RfsParams {
+    static constexpr int PER = (TOTAL + 64 * W - 1) / (64 * W);
+    float v[PER];
+    MEP_DEV void load(const uint64_t (&src)[NSEG], const int (&len)[NSEG]) {
+#pragma unroll
+        for (int k = 0; k < PER; ++k) {
+            const int idx = threadIdx.x + 64 * W * k;
+            int off = idx, sg = 0;
+#pragma unroll
+            for (int q = 0; q < NSEG - 1; ++q)
+                if (sg == q && off >= len[q]) { off -= len[q]; sg = q + 1; }
+            v[k] = idx < TOTAL ? G<const float>(src[sg])[off] : 0.f;
+        }
+    }
+    MEP_DEV void write(lds_f* dst) const {
+#pragma unroll
+        for (int k = 0; k < PER; ++k)
+            if (threadIdx.x + 64 * W * k < TOTAL) dst[threadIdx.x + 64 * W * k] = v[k];
+    }
+};
+
+template <int D, int FD, int W>
+__global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(W / 4, W / 4))) void k_rfs_fwd(const mep_rf_epi_desc* __restrict__ descs, int n_desc, int nbat) {
+    constexpr int NI = D / 16, NF = FD / 16, NP = D / 32, NPF = FD / 32;
+    constexpr int NPRM = 5 * D + FD;   // ln1_w | ln1_b | ln2_w | ln2_b | b2 | b1 (k_rfw_fwd's order)
+    // two weight buffers as separate LDS objects, each product's buffer fixed at compile time
+    // (job bodies instantiated per first-buffer parity): the compiler then sees that a ds_read of
+    // one buffer does not alias the DMA in flight into the other, and does not wait for it
+    __shared__ __attribute__((aligned(16))) unsigned char sm0[RFS_BUF], sm1[RFS_BUF];
+    __shared__ __attribute__((aligned(16))) float prm[2 * NPRM];
+    lbyte_t* const LB[2] = {(lbyte_t*)sm0, (lbyte_t*)sm1};
+    lds_f* const PS = (lds_f*)prm;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63, c = lane & 15, g = lane >> 4;
+    const RfsJobs<mep_rf_epi_desc, W> jobs{descs, n_desc * nbat, nbat};
+    auto woff = [](const mep_rf_epi_desc& d, int k) { return d.wparts + MEP_RFW_PART_OFFSET(D, FD, k); };
+    auto tok_of = [&](int j) { return ((j % nbat) * W + wave) * 16 + c; };
+    auto prm_load = [&](RfsParams<NPRM, 6, W>& pr, const mep_rf_epi_desc& d) {
+        const uint64_t src[6] = {d.ln1_w, d.ln1_b, d.ln2_w, d.ln2_b, d.b2, d.b1};
+        const int len[6] = {D, D, D, D, D, FD};
+        pr.load(src, len);
+    };
+    int job = jobs.first();
+    if (job >= jobs.njobs) return;   // whole workgroup
+    int ps = 0;
+    f32x4 xv[NI];                     // the job's x rows (Wp's operand), loaded a step ahead
+    {
+        const mep_rf_epi_desc& d = descs[job / nbat];
+        RfsParams<NPRM, 6, W> pr;
+        prm_load(pr, d);
+        rfs_stage<NI, NP, D, W>(LB[0], woff(d, 0), wave, lane);
+        load_rows<NI>(xv, d.x, min(tok_of(job), d.ntok - 1));
+        pr.write(PS);
+        rfs_sync();
+    }
+    // one job; P: the buffer of its first product, Q: the next layer's query projection fused.
+    // Returns the next job's first buffer
+    auto body = [&](auto pc, auto qc) -> int {
+        constexpr int P = decltype(pc)::value;
+        constexpr bool Q = decltype(qc)::value;
+        job = __builtin_amdgcn_readfirstlane(job);
+        const int nj = jobs.next(job);
+        const mep_rf_epi_desc& d = descs[job / nbat];
+        const mep_rf_epi_desc* dn = nj < jobs.njobs ? &descs[nj / nbat] : nullptr;
+        const int ntok = d.ntok, tok = tok_of(job), tc = min(tok, ntok - 1);
+        const bool ok = tok < ntok;
+        const float sa = *G<const float>(d.a), sb = *G<const float>(d.b);
+        const lds_f* PR = PS + ps * NPRM;
+        // ---- xp = Wp x;  h = LN1(q + a xp)
+        rfs_stage<NF, NP, FD, W>(LB[P ^ 1], woff(d, 1), wave, lane);
+        f32x4 qv[NI];
+        load_rows<NI>(qv, d.q, tc);
+        f32x4 xp[NI], h[NI];
+        float mean1, rstd1;
+        rfs_mul<NI, NP>(xp, LB[P], xv, lane);
+        {
+            f32x4 z[NI];
+#pragma unroll
+            for (int i = 0; i < NI; ++i)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) z[i][r] = add_rn(qv[i][r], mul_rn(sa, xp[i][r]));
+            layer_norm_l<NI>(z, h, PR, PR + D, mean1, rstd1);
+        }
+        rfs_sync();
+        // ---- f1 = relu(W1 h + b1)
+        if (ok) {
+            store_rows<NI>(d.xp, tok, xp);
+            store_rows<NI>(d.h, tok, h);
+        }
+        rfs_stage<NI, NPF, D, W>(LB[P], woff(d, 2), wave, lane);
+        f32x4 f1[NF];
+        rfs_mul<NF, NP>(f1, LB[P ^ 1], h, lane);
+#pragma unroll
+        for (int j = 0; j < NF; ++j) {
+            const f32x4 bb = ld4w(PR + 5 * D + 16 * j + 4 * g);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) f1[j][r] = fmaxf(f1[j][r] + bb[r], 0.f);
+        }
+        rfs_sync();
+        // ---- f = W2 f1 + b2;  out = LN2(h + b f)
+        if (ok) store_rows<NF>(d.f1, tok, f1);
+        RfsParams<NPRM, 6, W> pr;   // the next job's parameters (its slot is free: the job before used it)
+        if (!Q && dn) prm_load(pr, *dn);
+        if constexpr (Q) rfs_stage<NI, NP, D, W>(LB[P ^ 1], d.wq_next, wave, lane);
+        else if (dn) rfs_stage<NI, NP, D, W>(LB[P ^ 1], woff(*dn, 0), wave, lane);
+        f32x4 f[NI], out[NI];
+        float mean2, rstd2;
+        rfs_mul<NI, NPF>(f, LB[P], f1, lane);
+#pragma unroll
+        for (int j = 0; j < NI; ++j) {
+            const f32x4 bb = ld4w(PR + 4 * D + 16 * j + 4 * g);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) f[j][r] = f[j][r] + bb[r];
+        }
+        {
+            f32x4 z[NI];
+#pragma unroll
+            for (int i = 0; i < NI; ++i)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) z[i][r] = add_rn(h[i][r], mul_rn(sb, f[i][r]));
+            layer_norm_l<NI>(z, out, PR + 2 * D, PR + 3 * D, mean2, rstd2);
+        }
+        if (!Q && dn) {
+            load_rows<NI>(xv, dn->x, min(tok_of(nj), dn->ntok - 1));
+            pr.write(PS + (ps ^ 1) * NPRM);
+        }
+        rfs_sync();
+        if (ok) {
+            store_rows<NI>(d.f, tok, f);
+            store_rows<NI>(d.out, tok, out);
+            if (g == 0)
+                *reinterpret_cast<MEP_G f32x4*>(G<float>(d.stats) + 4 * (int64_t)tok) = f32x4{mean1, rstd1, mean2, rstd2};
+            if (d.zero.ptr) {   // the backward's accumulated rows of these tokens, cleared for this step
+                f32x4 zr[NI];
+#pragma unroll
+                for (int i = 0; i < NI; ++i) zr[i] = zero_f4();
+                store_rows<NI>(d.zero, tok, zr);
+            }
+        }
+        if constexpr (Q) {   // ---- the next layer's query projection, qp_next = out Wq_next^T
+            if (dn) {
+                prm_load(pr, *dn);
+                rfs_stage<NI, NP, D, W>(LB[P], woff(*dn, 0), wave, lane);
+                load_rows<NI>(xv, dn->x, min(tok_of(nj), dn->ntok - 1));
+            }
+            f32x4 qp[NI];
+            rfs_mul<NI, NP>(qp, LB[P ^ 1], out, lane);
+            if (dn) pr.write(PS + (ps ^ 1) * NPRM);
+            rfs_sync();
+            if (ok) store_rows<NI>(d.qp_next, tok, qp);
+        }
+        ps ^= 1;
+        job = nj;
+        return Q ? P : P ^ 1;
+    };
+    int par = 0;
+    while (job < jobs.njobs) {
+        job = __builtin_amdgcn_readfirstlane(job);
+        const bool q = descs[job / nbat].wq_next != 0;
+        if (par) par = q ? body(std::integral_constant<int, 1>{}, std::true_type{}) : body(std::integral_constant<int, 1>{}, std::false_type{});
+        else par = q ? body(std::integral_constant<int, 0>{}, std::true_type{}) : body(std::integral_constant<int, 0>{}, std::false_type{});
+    }
+}
+
+template <int D, int FD, int W>
+__global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(W / 4, W / 4))) void k_rfs_bwd(const mep_rf_epi_bwd_desc* __restrict__ descs, int n_desc, int nbat) {
+    constexpr int NI = D / 16, NF = FD / 16, NP = D / 32, NPF = FD / 32;
+    constexpr int NPRM = 2 * D;        // ln1_w | ln2_w
+    __shared__ __attribute__((aligned(16))) unsigned char sm0[RFS_BUF], sm1[RFS_BUF];   // (as k_rfs_fwd)
+    __shared__ __attribute__((aligned(16))) float prm[2 * NPRM];
+    lbyte_t* const LB[2] = {(lbyte_t*)sm0, (lbyte_t*)sm1};
+    lds_f* const PS = (lds_f*)prm;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63, c = lane & 15, g = lane >> 4;
+    const RfsJobs<mep_rf_epi_bwd_desc, W> jobs{descs, n_desc * nbat, nbat};
+    auto woff = [](const mep_rf_epi_desc& d, int k) { return d.wparts + MEP_RFW_PART_OFFSET(D, FD, k); };
+    auto tok_of = [&](int j) { return ((j % nbat) * W + wave) * 16 + c; };
+    auto prm_load = [&](RfsParams<NPRM, 2, W>& pr, const mep_rf_epi_desc& d) {
+        const uint64_t src[2] = {d.ln1_w, d.ln2_w};
+        const int len[2] = {D, D};
+        pr.load(src, len);
+    };
+    // the job's first product (Wq_in: dqp_in Wq, else W2^T) staged, and its rows loaded a step ahead:
+    // dout, h, f, the stats and (Wq_in) dqp_in
+    f32x4 gu[NI], hv[NI], fv[NI], dv[NI], st;
+    auto stage_first = [&](const mep_rf_epi_bwd_desc& b, lbyte_t* buf) {
+        if (b.wq_in) rfs_stage<NI, NP, D, W>(buf, b.wq_in, wave, lane);
+        else rfs_stage<NF, NP, FD, W>(buf, woff(b.f, 5), wave, lane);
+    };
+    int job = jobs.first();
+    if (job >= jobs.njobs) return;   // whole workgroup
+    int ps = 0;
+    {
+        const mep_rf_epi_bwd_desc& b = descs[job / nbat];
+        RfsParams<NPRM, 2, W> pr;
+        prm_load(pr, b.f);
+        stage_first(b, LB[0]);
+        const int t = min(tok_of(job), b.f.ntok - 1);
+        st = ld4w(G<const float>(b.f.stats) + 4 * (int64_t)t);
+        load_rows<NI>(gu, b.dout, t);
+        load_rows<NI>(hv, b.f.h, t);
+        load_rows<NI>(fv, b.f.f, t);
+        if (b.wq_in) load_rows<NI>(dv, b.dqp_in, t);
+        pr.write(PS);
+        rfs_sync();
+    }
+    // one job; P: the buffer of its first product, Q: the next layer's query-projection input
+    // gradient fused (Wq_in first).  Returns the next job's first buffer
+    auto body = [&](auto pc, auto qc) -> int {
+        constexpr int P = decltype(pc)::value;
+        constexpr bool Q = decltype(qc)::value;
+        constexpr int C1 = Q ? P ^ 1 : P;   // W2^T's buffer
+        job = __builtin_amdgcn_readfirstlane(job);
+        const int nj = jobs.next(job);
+        const mep_rf_epi_bwd_desc& bd = descs[job / nbat];
+        const mep_rf_epi_desc& d = bd.f;
+        const mep_rf_epi_bwd_desc* bn = nj < jobs.njobs ? &descs[nj / nbat] : nullptr;
+        const int ntok = d.ntok, tok = tok_of(job), tc = min(tok, ntok - 1);
+        const int tile = (job % nbat) * W + wave;
+        const bool ok = tok < ntok, part_ok = tile * 16 < ntok;
+        const float sa = *G<const float>(d.a), sb = *G<const float>(d.b);
+        const lds_f* PR = PS + ps * NPRM;
+        gfloat* part = G<float>(bd.partial) + (int64_t)tile * MEP_RF_PARTIAL_STRIDE(D, FD);
+        if (bd.dout2.ptr) {
+            f32x4 g2[NI];
+            load_rows<NI>(g2, bd.dout2, tc);
+#pragma unroll
+            for (int i = 0; i < NI; ++i) gu[i] += g2[i];
+        }
+        if constexpr (Q) {   // ---- dout += dqp_in Wq: the next layer's query-projection input gradient
+            rfs_stage<NF, NP, FD, W>(LB[P ^ 1], woff(d, 5), wave, lane);
+            f32x4 acc[NI];
+            rfs_mul<NI, NP>(acc, LB[P], dv, lane);
+#pragma unroll
+            for (int i = 0; i < NI; ++i) gu[i] += acc[i];
+        }
+#pragma unroll
+        for (int i = 0; i < NI; ++i)
+            if (!ok) gu[i] = zero_f4();
+        // LN2 backward -> dz2; df = b dz2
+        f32x4 dz2[NI], df[NI], k_w2, k_b2, k_db2;
+        float db_s = 0.f;
+        {
+            f32x4 xh[NI], pw2[NI], w2v[NI];
+#pragma unroll
+            for (int i = 0; i < NI; ++i) {
+                w2v[i] = ld4w(PR + D + 16 * i + 4 * g);
+#pragma unroll
+                for (int r = 0; r < 4; ++r) xh[i][r] = (add_rn(hv[i][r], mul_rn(sb, fv[i][r])) - st[2]) * st[3];
+            }
+            ln_bwd<NI>(dz2, gu, xh, w2v, st[3]);
+#pragma unroll
+            for (int i = 0; i < NI; ++i)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    pw2[i][r] = mul_rn(gu[i][r], xh[i][r]);   // rounded: a product fused into the column sum's first add would depend on the schedule
+                    df[i][r] = sb * dz2[i][r];
+                    db_s += dz2[i][r] * fv[i][r];
+                }
+            k_w2 = rfs_colsum<NI>(pw2, c);   // dLN2.w
+            k_b2 = rfs_colsum<NI>(gu, c);    // dLN2.b
+            k_db2 = rfs_colsum<NI>(df, c);   // db2
+        }
+        const float st0 = st[0], st1 = st[1];
+        if constexpr (Q) rfs_sync();
+        // ---- df1 = relu'(f1) (W2^T df)
+        if (part_ok) {
+            rfs_colsum_store(part, k_w2, NI, c, g);
+            rfs_colsum_store(part + D, k_b2, NI, c, g);
+            rfs_colsum_store(part + 4 * D, k_db2, NI, c, g);
+        }
+        if (ok) store_rows<NI>(bd.df, tok, df);
+        rfs_stage<NI, NPF, D, W>(LB[C1 ^ 1], woff(d, 4), wave, lane);
+        f32x4 f1v[NF];
+        load_rows<NF>(f1v, d.f1, tc);
+        f32x4 df1[NF];
+        rfs_mul<NF, NP>(df1, LB[C1], df, lane);
+#pragma unroll
+        for (int j = 0; j < NF; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) df1[j][r] = (ok && f1v[j][r] > 0.f) ? df1[j][r] : 0.f;
+        const f32x4 k_db1 = rfs_colsum<NF>(df1, c);
+        rfs_sync();
+        // ---- dh = dz2 + W1^T df1;  LN1 backward -> dz1;  dq (+)= dz1;  dxp = a dz1
+        if (part_ok) rfs_colsum_store(part + 5 * D, k_db1, NF, c, g);
+        if (ok) store_rows<NF>(bd.df1, tok, df1);
+        rfs_stage<NI, NP, D, W>(LB[C1], woff(d, 3), wave, lane);
+        f32x4 qv[NI], xpv[NI];
+        load_rows<NI>(qv, d.q, tc);
+        load_rows<NI>(xpv, d.xp, tc);
+        f32x4 dh[NI];
+        rfs_mul<NI, NPF>(dh, LB[C1 ^ 1], df1, lane);
+#pragma unroll
+        for (int i = 0; i < NI; ++i) dh[i] += dz2[i];
+        f32x4 dxp[NI], dq[NI], k_w1, k_b1;
+        float da_s = 0.f;
+        {
+            f32x4 xh[NI], dz1[NI], pw[NI], w1v[NI];
+#pragma unroll
+            for (int i = 0; i < NI; ++i) {
+                w1v[i] = ld4w(PR + 16 * i + 4 * g);
+#pragma unroll
+                for (int r = 0; r < 4; ++r) xh[i][r] = (add_rn(qv[i][r], mul_rn(sa, xpv[i][r])) - st0) * st1;
+            }
+            ln_bwd<NI>(dz1, dh, xh, w1v, st1);
+#pragma unroll
+            for (int i = 0; i < NI; ++i)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    pw[i][r] = mul_rn(dh[i][r], xh[i][r]);
+                    dxp[i][r] = sa * dz1[i][r];
+                    da_s += dz1[i][r] * xpv[i][r];
+                }
+            k_w1 = rfs_colsum<NI>(pw, c);   // dLN1.w
+            k_b1 = rfs_colsum<NI>(dh, c);   // dLN1.b
+            if (bd.dq_accumulate) {   // the old dq rows, loaded here (the plans never accumulate)
+                f32x4 dqo[NI];
+                load_rows<NI>(dqo, bd.dq, tc);
+#pragma unroll
+                for (int i = 0; i < NI; ++i) dq[i] = dqo[i] + dz1[i];
+            } else {
+#pragma unroll
+                for (int i = 0; i < NI; ++i) dq[i] = dz1[i];
+            }
+        }
+        const float da = wave_sum(da_s), db = wave_sum(db_s);
+        rfs_sync();
+        // ---- dx = Wp^T dxp
+        if (part_ok) {
+            rfs_colsum_store(part + 2 * D, k_w1, NI, c, g);
+            rfs_colsum_store(part + 3 * D, k_b1, NI, c, g);
+            if (lane == 0) { part[5 * D + FD] = da; part[5 * D + FD + 1] = db; }
+        }
+        if (ok) {
+            store_rows<NI>(bd.dq, tok, dq);
+            store_rows<NI>(bd.dxp, tok, dxp);
+        }
+        RfsParams<NPRM, 2, W> pr;
+        if (bn) {   // the next job's parameters, first product and rows
+            prm_load(pr, bn->f);
+            stage_first(*bn, LB[C1 ^ 1]);
+            const int t = min(tok_of(nj), bn->f.ntok - 1);
+            st = ld4w(G<const float>(bn->f.stats) + 4 * (int64_t)t);
+            load_rows<NI>(gu, bn->dout, t);
+            load_rows<NI>(hv, bn->f.h, t);
+            load_rows<NI>(fv, bn->f.f, t);
+            if (bn->wq_in) load_rows<NI>(dv, bn->dqp_in, t);
+        }
+        f32x4 dx[NI];
+        rfs_mul<NI, NP>(dx, LB[C1], dxp, lane);
+        if (bn) pr.write(PS + (ps ^ 1) * NPRM);
+        rfs_sync();
+        if (ok) store_rows<NI>(bd.dx, tok, dx);
+        ps ^= 1;
+        job = nj;
+        return C1 ^ 1;
+    };
+    int par = 0;
+    while (job < jobs.njobs) {
+        job = __builtin_amdgcn_readfirstlane(job);
+        const bool q = descs[job / nbat].wq_in != 0;
+        if (par) par = q ? body(std::integral_constant<int, 1>{}, std::true_type{}) : body(std::integral_constant<int, 1>{}, std::false_type{});
+        else par = q ? body(std::integral_constant<int, 0>{}, std::true_type{}) : body(std::integral_constant<int, 0>{}, std::false_type{});
     }
 }
 
@@ -1256,12 +1749,34 @@ extern "C" int mep_rfw_front(const mep_rf_front_desc* descs, int n_desc, int max
     return mep_check_launch("mep_rfw_front");
 }
 
+// the weight-stationary kernels for the large launches: on unless MEP_RFS=0 in the environment
+// (read per call: the A/B switch of the tests and benches); one resident workgroup per CU
+static bool rfs_on() {
+    const char* e = getenv("MEP_RFS");
+    return !(e && e[0] == '0');
+}
+static int rfs_grid(int njobs) {
+    int dev = 0, n_cu = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        n_cu <= 0)
+        n_cu = 256;
+    return std::max(1, std::min(njobs, n_cu));
+}
+
 extern "C" int mep_rfw_epi_fwd(const mep_rf_epi_desc* descs, int n_desc, int max_tiles, int D, int FD,
                                mep_stream_t stream) {
     if (n_desc <= 0 || max_tiles <= 0) return 0;
     const bool big = (int64_t)max_tiles * n_desc >= MEP_RFW_BIG_TILES;
     const int rc = dispatch_rfw(D, FD, [&](auto dc, auto fc) {
         constexpr int DD = decltype(dc)::value, FF = decltype(fc)::value;
+        if constexpr (DD == 96 && FF == 192) {
+            if (big && rfs_on()) {
+                const int nbat = (max_tiles + MEP_RFS_FWD_W - 1) / MEP_RFS_FWD_W;
+                hipLaunchKernelGGL((k_rfs_fwd<DD, FF, MEP_RFS_FWD_W>), dim3(rfs_grid(n_desc * nbat)), dim3(64 * MEP_RFS_FWD_W), 0,
+                                   (hipStream_t)stream, descs, n_desc, nbat);
+                return;
+            }
+        }
         if (DD == 96 && big)
             hipLaunchKernelGGL((k_rfw_fwd<DD, FF, rfw_waves<DD>(), MEP_RFW_BIG_WPE, MEP_RFW_BIG_DEPTH, MEP_RFW_BIG_WPARTS>), dim3(max_tiles, n_desc),
                                dim3(64 * rfw_waves<DD>()), 0, (hipStream_t)stream, descs);
@@ -1279,6 +1794,14 @@ extern "C" int mep_rfw_epi_bwd(const mep_rf_epi_bwd_desc* descs, int n_desc, int
     const bool big = (int64_t)max_tiles * n_desc >= MEP_RFW_BIG_TILES;
     const int rc = dispatch_rfw(D, FD, [&](auto dc, auto fc) {
         constexpr int DD = decltype(dc)::value, FF = decltype(fc)::value;
+        if constexpr (DD == 96 && FF == 192) {
+            if (big && rfs_on()) {
+                const int nbat = (max_tiles + MEP_RFS_BWD_W - 1) / MEP_RFS_BWD_W;
+                hipLaunchKernelGGL((k_rfs_bwd<DD, FF, MEP_RFS_BWD_W>), dim3(rfs_grid(n_desc * nbat)), dim3(64 * MEP_RFS_BWD_W), 0,
+                                   (hipStream_t)stream, descs, n_desc, nbat);
+                return;
+            }
+        }
         if (DD == 96 && big)
             hipLaunchKernelGGL((k_rfw_bwd<DD, FF, rfw_waves<DD>(), 1, MEP_RFW_DEPTH, MEP_RFW_BIG_WPARTS>), dim3(max_tiles, n_desc),
                                dim3(64 * rfw_waves<DD>()), 0, (hipStream_t)stream, descs);

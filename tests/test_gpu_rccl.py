@@ -101,9 +101,10 @@ def test_norm_fold_matches_optimizer_norm_pass(cuda):
         assert float((p1 - p0).abs().max()) <= 1e-6, k
 
 
-def _fold_pair(build, steps=4):
+def _fold_pair(build, steps=4, ptol=1e-6):
     """(engine, model, losses, gnorms) with the norm pass folded and with the optimizer's own pass;
-    build(fold_norm) -> (engine, model, step function)"""
+    build(fold_norm) -> (engine, model, step function); ptol: the parameters' absolute agreement
+    after the steps"""
     out = []
     for fold in (True, False):
         eng, model, step = build(fold)
@@ -119,7 +120,7 @@ def _fold_pair(build, steps=4):
     assert float((l1 - l0).abs().max()) <= 1e-6 * float(l0.abs().max()), (l1, l0)
     for (k, p1), (_, p0) in zip(m1.named_parameters(), m0.named_parameters()):
         e = (p1 - p0).abs()
-        assert float(e.max()) <= 1e-6, (k, float(e.max()), int((e > 1e-6).sum()), e.numel(), g1, g0)
+        assert float(e.max()) <= ptol, (k, float(e.max()), int((e > ptol).sum()), e.numel(), g1, g0)
 
 
 def test_norm_fold_matches_optimizer_norm_pass_ren_dropout(cuda):
@@ -144,7 +145,10 @@ def test_norm_fold_matches_optimizer_norm_pass_ren_dropout(cuda):
 
 def test_norm_fold_matches_optimizer_norm_pass_realformer(cuda):
     """realformer State_Transfer (Adam, position-embedding column sums, the batch-loss column sum
-    that is not a gradient): folded norm vs the optimizer's own norm pass over 4 steps."""
+    that is not a gradient): folded norm vs the optimizer's own norm pass over 4 steps.  Adam
+    divides each update by its own running magnitude, so the norm's summation-order difference
+    (1e-7 relative in the clip coefficient) moves a near-zero-gradient element by up to a few
+    1e-6 after 4 steps at lr 1e-3 (1.9e-6 measured on 1 of 1,024 w_qkv elements): 4e-6 here."""
     from mep_amd.engine import TrainEngine
     from mep_amd.optim import FusedAdam
     from tests.test_gpu_realformer import _batch, _state
@@ -155,4 +159,4 @@ def test_norm_fold_matches_optimizer_norm_pass_realformer(cuda):
         model = _state(meta, cuda)
         eng = TrainEngine(model, FusedAdam(model, lr=1e-3), clip=1.0, graph=True, fold_norm=fold)
         return eng, model, lambda e: e.step(*batch)
-    _fold_pair(build)
+    _fold_pair(build, ptol=4e-6)

@@ -343,3 +343,38 @@ def test_rfw_wgemm_sum_plan_gradients(cuda):
         torch.cuda.synchronize()
         grads.append(runner.flat.grad.clone())
     assert torch.equal(grads[0], grads[1]), 'max |diff| %.3g' % (grads[0] - grads[1]).abs().max().item()
+
+
+@pytest.mark.parametrize('B,P', [(16, 6), (13, 5)])
+def test_rfs_matches_per_tile_epilogues(B, P, cuda, monkeypatch):
+    """The weight-stationary State_Transfer epilogue launches (k_rfs_fwd / k_rfs_bwd, on by default
+    for >= MEP_RFW_BIG_TILES tiles) write the logits, every block output and every gradient
+    (and the epilogue rows h / f1 / f / out / the fused next-layer q of every block) bit-identical
+    to the per-tile kernels they replace (MEP_RFS=0): same products in the same
+    order, same epilogue arithmetic.  13 x 5 x 50 tokens per block: a ragged last tile and a
+    last job with idle waves."""
+    from mep_amd import realformer as rf
+    from mep_amd import rf_plan
+    torch.manual_seed(B * P)
+    T = 50
+    st = rf.State_Transfer(300, 35, 74, 96, T, T, T, 6, 2, 2).to(cuda)
+    runner = st.mep_runner(cuda)
+    feats = tuple(torch.randn(B, P, T, d, device=cuda) for d in (300, 35, 74))
+    masks = tuple((torch.rand(B, P, T, device=cuda) > 0.2).float() for _ in range(3))
+    dout = torch.randn(B, P, 6, device=cuda)
+    res = []
+    for on in ('1', '0'):
+        monkeypatch.setenv('MEP_RFS', on)
+        plan = rf_plan.RealformerPlan(runner.spec, runner.flat, B, P, cuda)
+        for i in range(plan.spec.nl):   # every epilogue launch takes the large-launch path
+            assert plan.t_epif[i] * plan.d_epi[i].n >= 1024
+        plan.set_inputs(*feats, *masks)
+        plan.forward(grad=True)
+        runner.flat.grad.zero_()
+        plan.backward(ext_dout=dout)
+        torch.cuda.synchronize()
+        res.append([plan.out.clone(), runner.flat.grad.clone()] +
+                   [b[k].clone() for b in plan.blocks for k in ('H', 'F1', 'F', 'OUT', 'QP') if k in b])
+    assert torch.isfinite(res[0][0]).all() and torch.isfinite(res[0][1]).all()
+    for i, (a, b) in enumerate(zip(*res)):
+        assert torch.equal(a, b), 'tensor %d: max |diff| %.3g' % (i, (a - b).abs().max().item())
