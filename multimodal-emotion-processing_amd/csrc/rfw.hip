@@ -762,23 +762,39 @@ MEP_DEV void rfs_colsum_store(gfloat* dst, const f32x4& k, int nb, int c, int g)
     }
 }
 
-// the jobs (descriptor, batch of W tiles) a workgroup walks: blockIdx.x, + gridDim.x, ...,
-// skipping batches past a descriptor's tokens (uniform over the workgroup)
+// the jobs (descriptor, batch of W tiles) a workgroup walks, skipping batches past a descriptor's
+// tokens (uniform over the workgroup).  XCD-chunked: workgroup b runs on XCD b % 8 (round-robin
+// dispatch), and each XCD takes one contiguous eighth of the job list (descriptor-major), its
+// workgroups striding through it -- the 32 CUs of an XCD work on one or two descriptors at a
+// time, so their weight fragments stay in that XCD's L2 (the plain stride spread every
+// descriptor over every XCD: L2 hit rate 0.57 on the weight DMA)
 MEP_DEV int rfs_ntok(const mep_rf_epi_desc& d) { return d.ntok; }
 MEP_DEV int rfs_ntok(const mep_rf_epi_bwd_desc& d) { return d.f.ntok; }
 template <typename Desc, int W>
 struct RfsJobs {
     const Desc* descs;
-    int njobs, nbat;
+    int njobs, nbat, lo, hi, stride;
+    MEP_DEV RfsJobs(const Desc* d, int nj, int nb) : descs(d), njobs(nj), nbat(nb) {
+        const int G = gridDim.x, b = blockIdx.x;
+        if (G % 8 == 0) {
+            lo = (int)((int64_t)nj * (b % 8) / 8) + b / 8;
+            hi = (int)((int64_t)nj * (b % 8 + 1) / 8);
+            stride = G / 8;
+        } else {
+            lo = b;
+            hi = nj;
+            stride = G;
+        }
+    }
     MEP_DEV int ntok(int j) const { return rfs_ntok(descs[j / nbat]); }
-    MEP_DEV bool valid(int j) const { return j < njobs && (j % nbat) * (16 * W) < ntok(j); }
+    MEP_DEV bool valid(int j) const { return j < hi && (j % nbat) * (16 * W) < ntok(j); }
     // (readfirstlane: the job index is workgroup-uniform; without it the compiler keeps it in a
     // VGPR and reads every descriptor field with vector loads and vmcnt(0) waits)
     MEP_DEV int next(int j) const {
-        do { j += gridDim.x; } while (j < njobs && !valid(j));
-        return __builtin_amdgcn_readfirstlane(j);
+        do { j += stride; } while (j < hi && !valid(j));
+        return __builtin_amdgcn_readfirstlane(j < hi ? j : njobs);
     }
-    MEP_DEV int first() const { return valid(blockIdx.x) ? (int)blockIdx.x : next(blockIdx.x); }
+    MEP_DEV int first() const { return valid(lo) ? lo : next(lo); }
 };
 
 // a job's LayerNorm / bias parameters [n0 | n1 | ...] -> the job's LDS parameter slot: loaded into
@@ -820,7 +836,7 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(W / 4, W
     lds_f* const PS = (lds_f*)prm;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63, c = lane & 15, g = lane >> 4;
-    const RfsJobs<mep_rf_epi_desc, W> jobs{descs, n_desc * nbat, nbat};
+    const RfsJobs<mep_rf_epi_desc, W> jobs(descs, n_desc * nbat, nbat);
     auto woff = [](const mep_rf_epi_desc& d, int k) { return d.wparts + MEP_RFW_PART_OFFSET(D, FD, k); };
     auto tok_of = [&](int j) { return ((j % nbat) * W + wave) * 16 + c; };
     auto prm_load = [&](RfsParams<NPRM, 6, W>& pr, const mep_rf_epi_desc& d) {
@@ -960,7 +976,7 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(W / 4, W
     lds_f* const PS = (lds_f*)prm;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63, c = lane & 15, g = lane >> 4;
-    const RfsJobs<mep_rf_epi_bwd_desc, W> jobs{descs, n_desc * nbat, nbat};
+    const RfsJobs<mep_rf_epi_bwd_desc, W> jobs(descs, n_desc * nbat, nbat);
     auto woff = [](const mep_rf_epi_desc& d, int k) { return d.wparts + MEP_RFW_PART_OFFSET(D, FD, k); };
     auto tok_of = [&](int j) { return ((j % nbat) * W + wave) * 16 + c; };
     auto prm_load = [&](RfsParams<NPRM, 2, W>& pr, const mep_rf_epi_desc& d) {
