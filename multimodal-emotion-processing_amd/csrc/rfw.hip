@@ -674,10 +674,10 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(WPE))) v
 // k_rfw_*<..., NW = 2>'s in the same order per accumulator, and every epilogue the same
 // arithmetic: results bit-identical to those kernels (test_gpu_rfw.py).
 #ifndef MEP_RFS_FWD_W
-#define MEP_RFS_FWD_W 8   // waves (16-token tiles) per workgroup: 2 per SIMD (186 VGPRs)
+#define MEP_RFS_FWD_W 8   // waves (16-token tiles) per workgroup: 2 per SIMD (190 VGPRs)
 #endif
 #ifndef MEP_RFS_BWD_W
-#define MEP_RFS_BWD_W 4   // 1 per SIMD: the backward's live rows need 256 VGPRs + AGPRs
+#define MEP_RFS_BWD_W 8   // (4: one wave per SIMD with the rows AGPR-spilled, 276 vs 234 us per launch)
 #endif
 constexpr int RFS_IMG = 1024;            // one part image of a fragment: 64 lanes x 16 B
 constexpr int RFS_BUF = 72 * RFS_IMG;    // the largest product's fragments: 12 x 3 or 6 x 6 pairs, 2 parts
@@ -709,6 +709,9 @@ MEP_DEV void rfs_stage(lbyte_t* buf, uint64_t w, int wave, int lane) {
 // independent accumulators), the fragments read from LDS through a ring RFS_DEPTH steps ahead
 // (a scheduling barrier per step: left alone, the compiler hoists every read of the product and
 // spills)
+#ifndef MEP_RFS_BWD_PRE
+#define MEP_RFS_BWD_PRE 0   // 1: the backward's next-job rows loaded a step ahead (measured slower: 306 vs 279 us, the rows held across the step cost 100 AGPR moves)
+#endif
 #ifndef MEP_RFS_DEPTH
 #define MEP_RFS_DEPTH 3
 #endif
@@ -1025,6 +1028,13 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(W / 4, W
         const float sa = *G<const float>(d.a), sb = *G<const float>(d.b);
         const lds_f* PR = PS + ps * NPRM;
         gfloat* part = G<float>(bd.partial) + (int64_t)tile * MEP_RF_PARTIAL_STRIDE(D, FD);
+        if (!MEP_RFS_BWD_PRE) {   // (the A/B of the step-ahead rows: loaded here, waited for at once)
+            st = ld4w(G<const float>(d.stats) + 4 * (int64_t)tc);
+            load_rows<NI>(gu, bd.dout, tc);
+            load_rows<NI>(hv, d.h, tc);
+            load_rows<NI>(fv, d.f, tc);
+            if (Q) load_rows<NI>(dv, bd.dqp_in, tc);
+        }
         if (bd.dout2.ptr) {
             f32x4 g2[NI];
             load_rows<NI>(g2, bd.dout2, tc);
@@ -1143,12 +1153,14 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(W / 4, W
         if (bn) {   // the next job's parameters, first product and rows
             prm_load(pr, bn->f);
             stage_first(*bn, LB[C1 ^ 1]);
-            const int t = min(tok_of(nj), bn->f.ntok - 1);
-            st = ld4w(G<const float>(bn->f.stats) + 4 * (int64_t)t);
-            load_rows<NI>(gu, bn->dout, t);
-            load_rows<NI>(hv, bn->f.h, t);
-            load_rows<NI>(fv, bn->f.f, t);
-            if (bn->wq_in) load_rows<NI>(dv, bn->dqp_in, t);
+            if (MEP_RFS_BWD_PRE) {
+                const int t = min(tok_of(nj), bn->f.ntok - 1);
+                st = ld4w(G<const float>(bn->f.stats) + 4 * (int64_t)t);
+                load_rows<NI>(gu, bn->dout, t);
+                load_rows<NI>(hv, bn->f.h, t);
+                load_rows<NI>(fv, bn->f.f, t);
+                if (bn->wq_in) load_rows<NI>(dv, bn->dqp_in, t);
+            }
         }
         f32x4 dx[NI];
         rfs_mul<NI, NP>(dx, LB[C1], dxp, lane);
