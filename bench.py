@@ -188,13 +188,15 @@ def hbm_probe(dev, gib=2):
     return out
 
 
-# launch name -> kernel symbol prefix in the rocprofv3 summaries (scripts/parse_prof.py)
+# launch name -> kernel symbol prefix (or prefixes) in the rocprofv3 summaries (scripts/parse_prof.py);
+# mep_rfw_epi_* runs k_rfs_* on the large launches (State_Transfer) and k_rfw_* on the small ones
 KERNEL_OF = {'mep_attn_bwd': 'k_attn_bwd', 'mep_attn_fwd': 'k_attn_fwd', 'mep_block_epi_fwd': 'k_epi_fwd',
              'mep_block_epi_bwd': 'k_epi_bwd', 'mep_wgrad': 'k_wgrad', 'mep_unify': 'k_unify',
              'mep_pool_fwd': 'k_pool_fwd', 'mep_pool_bwd': 'k_pool_bwd', 'mep_gemm': 'k_gemm', 'mep_tgemm': 'k_tgemm',
              'mep_rf_epi_fwd': 'k_rf_epi_fwd', 'mep_rf_epi_bwd': 'k_rf_epi_bwd', 'mep_sum_rows': 'k_sum_rows',
              'mep_wgemm': 'k_wgemm', 'mep_wgemm_ws': 'k_wgemm_ws', 'mep_wgemm_sum': 'k_wgemm_sum',
-             'mep_rfw_front': 'k_rfw_front', 'mep_rfw_epi_fwd': 'k_rfw_fwd', 'mep_rfw_epi_bwd': 'k_rfw_bwd',
+             'mep_rfw_front': 'k_rfw_front', 'mep_rfw_epi_fwd': ('k_rfs_fwd', 'k_rfw_fwd'),
+             'mep_rfw_epi_bwd': ('k_rfs_bwd', 'k_rfw_bwd'),
              'mep_wsplit': 'k_wsplit', 'mep_reduce_grads': 'k_reduce_grads', 'mep_head_fwd_bwd': 'k_head',
              'mep_clip_adam_ext': 'k_clip_adam', 'mep_rf_head': 'k_rf_head'}
 
@@ -230,12 +232,14 @@ def pmc_valu(launch, tag='cfg3'):
     prefix = KERNEL_OF.get(launch)
     if prefix is None:
         return None, None
-    longer = [p for p in set(KERNEL_OF.values()) if p != prefix and p.startswith(prefix)]
+    flat = {q for p in KERNEL_OF.values() for q in (p if isinstance(p, tuple) else (p,))}
+    mine = prefix if isinstance(prefix, tuple) else (prefix,)
+    longer = tuple(p for p in flat if p not in mine and p.startswith(mine))
     files = glob.glob(os.path.join(ROOT, 'profiles', 'r*_counters_%s.json' % tag))
     for f in sorted(files, key=lambda f: [int(x) for x in re.findall(r'\d+', os.path.basename(f))], reverse=True):
         tot = 0.0
         for k, v in json.load(open(f)).items():
-            if k.startswith(prefix) and not any(k.startswith(p) for p in longer) and isinstance(v, dict):
+            if k.startswith(prefix) and not (longer and k.startswith(longer)) and isinstance(v, dict):
                 tot += float(v.get('raw', {}).get('SQ_INSTS_VALU', 0.0))
         if tot > 0:
             return tot, os.path.relpath(f, ROOT)
