@@ -31,6 +31,9 @@ def switches_from_env():
 
 # MEP_LIB: development override (A/B experiments with variant builds); never set in normal use
 LIB_PATH = switch('MEP_LIB', '') or os.path.join(PKG_DIR, 'libmep_hip.so')
+# MEP_RFS: read by the library itself at each mep_rfw_epi_* call (csrc/rfw.hip rfs_on: 0 = the per-tile
+# State_Transfer epilogues instead of the weight-stationary ones); recorded here for the bench line
+switch('MEP_RFS', '1')
 
 u64, i64, i32, f32 = ctypes.c_uint64, ctypes.c_int64, ctypes.c_int32, ctypes.c_float
 
