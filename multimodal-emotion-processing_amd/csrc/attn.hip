@@ -664,6 +664,10 @@ MEP_DEV void wave_lds_sync() {
 // layer's post-mask S output; BF: the bf16 path (one bf16 product per contraction); KV: k is v
 // and dk is dv (MEP_ATTN_KV: one register set for the K / V rows and ONE accumulator per key tile
 // for dK + dV, with Q pre-scaled by the exact 1/sqrt(hd) = 1/4 -- about 32 registers fewer).
+#ifndef MEP_BWD_SSTAGE
+#define MEP_BWD_SSTAGE 1   // short backward, LDS-DMA path: bit 0 stages S_prev (rfstate layer-1 launch 433 -> ~345 us), bit 1 dS_next (its addressing spills the fp32 DSN kernel: 6 -> 22 registers, slower)
+#endif
+constexpr bool SST_P = MEP_BWD_SSTAGE & 1, SST_D = (MEP_BWD_SSTAGE >> 1) & 1;
 template <bool PREV, bool DSN, bool BF, bool KV = false>
 struct Bwd {
     // per query tile: A of S (Q rows), A of dP (dO rows), B of dV / dK (dO / Q columns), O
@@ -681,7 +685,7 @@ struct Bwd {
     const gfloat *sprev, *dsn, *mask;
     gfloat* dsp;
     BRowT<BF> Qb, Kb, Vb, Ob, Gb, dQb;   // BF: bf16 rows
-    __amdgpu_buffer_rsrc_t rsStat, rsRp;
+    __amdgpu_buffer_rsrc_t rsStat, rsRp, rsSp, rsDn;
     bool same_kv;
     int k_lo;
     S2 kb[NT], vb[NT], kq[NT];
@@ -713,6 +717,8 @@ struct Bwd {
         sbase = (b * d.H + h) * Tq;
         rsStat = uniform_rsrc(d.stats + 8ull * (uint64_t)sbase, 8 * (int64_t)Tq);
         if (PREV) rsRp = uniform_rsrc(d.stats + 4ull * (uint64_t)(2 * d.B * d.H * Tq + sbase), 4 * (int64_t)Tq);
+        if (PREV) rsSp = uniform_rsrc(d.s_prev + 4ull * (uint64_t)sbase * Tk, 4 * (int64_t)Tq * Tk);
+        if (DSN) rsDn = uniform_rsrc(bd.ds_next + 4ull * (uint64_t)sbase * Tk, 4 * (int64_t)Tq * Tk);
     }
 
     MEP_DEV void load_chunk(int kc) {
@@ -769,7 +775,14 @@ struct Bwd {
     // wave's start and later holds finite rows of earlier tiles, whose products are masked).
     // BF (bf16 rows): 16 rows x 32 B per operand, lanes 0-31 (lane L = row L / 2, 16-byte piece
     // L % 2) into [16][16] bf16 images at the same float offsets (half of each slot used)
-    static constexpr int STG = 4 * 256 + 48;   // floats: Q, dO, O, dQ [16][16], stats [16][2], PREV's rp [16]
+    // PREV / DSN: the tile's S_prev / dS_next rows [16 queries][64 keys] too, one 4-byte DMA
+    // wave-instruction per query row (lane = key), rows SSTR floats apart (4 SSTR = 16 mod 32: the
+    // score reads of lane groups g and g + 1 fall in different banks), read per score from LDS
+    // instead of a dependent global load inside the tile's math (keys past Tk and rows past Tq fall
+    // outside the range: whatever finite value the slot holds meets P = 0 there)
+    static constexpr int SSTR = 68, SOPS = 16 * SSTR;
+    static constexpr int SPO = 4 * 256 + 48, DNO = SPO + (PREV && SST_P ? SOPS : 0);
+    static constexpr int STG = DNO + (DSN && SST_D ? SOPS : 0);   // floats: Q, dO, O, dQ [16][16], stats [16][2], PREV's rp [16], S_prev, dS_next
     MEP_DEV static bool dma_view(const mep_rows& v) {   // 16-byte aligned pieces of every row
         return BF ? ((v.ptr & 15) == 0 && v.sB % 8 == 0 && v.sT % 8 == 0) : aligned16(v);
     }
@@ -778,6 +791,16 @@ struct Bwd {
     }
     MEP_DEV void stage(int qt, float* S) const {
         typedef __attribute__((address_space(3))) void lvoid;
+        if ((PREV && SST_P) || (DSN && SST_D)) {
+            const int oor = 4 * Tq * Tk;
+#pragma unroll
+            for (int j = 0; j < 16; ++j) {
+                const int q = qt * 16 + j;
+                const int off = (lane < Tk && q < Tq) ? 4 * (q * Tk + lane) : oor;
+                if (PREV && SST_P) __builtin_amdgcn_raw_ptr_buffer_load_lds(rsSp, (lvoid*)(S + SPO + SSTR * j), 4, off, 0, 0, 0);
+                if (DSN && SST_D) __builtin_amdgcn_raw_ptr_buffer_load_lds(rsDn, (lvoid*)(S + DNO + SSTR * j), 4, off, 0, 0, 0);
+            }
+        }
         if (BF) {
             if (lane < 32) {
                 const int row = qt * 16 + (lane >> 1), col = hc + 8 * (lane & 1);
@@ -848,7 +871,8 @@ struct Bwd {
     // one 16-query tile against the chunk's 64 keys: accumulates dK / dV, returns this chunk's
     // dQ contribution (C[query 4g+r][dim c], before the 1/sqrt(hd) scale).  Tr: the wave's
     // transpose scratch in LDS (TFL floats: the bf16 hi and lo parts of dS, 16 x TLD2 each).
-    MEP_DEV floatx4 tile(const QIn& in, int qt, float* Tr) {
+    // SS: the staged tile (LDS-DMA path: S_prev / dS_next read from it), or nullptr (global loads)
+    MEP_DEV floatx4 tile(const QIn& in, int qt, float* Tr, const float* SS = nullptr) {
         const int q0 = qt * 16;
         constexpr float LOG2E = 1.4426950408889634f;
         float mm[4], li[4], del[4];
@@ -923,7 +947,7 @@ struct Bwd {
                 int si = 0;
                 if (PREV || DSN) {
                     si = (sbase + min(qq, Tq - 1)) * Tk + min(kk, Tk - 1);
-                    if (PREV) spv = sprev[si];
+                    if (PREV) spv = SST_P && SS ? ((const __attribute__((address_space(3))) float*)SS)[SPO + SSTR * (4 * g + r) + kt * 16 + c] : sprev[si];
                 }
                 float pv;
                 if constexpr (PREV) {
@@ -941,7 +965,8 @@ struct Bwd {
                 float gsv = pv * dp[r];
                 if (DSN || PREV) {
                     const bool ok = (qq < Tq) && (kk < Tk);
-                    const float gn = DSN && ok ? dsn[si] : 0.f;
+                    const float gn = DSN && ok ? (SST_D && SS ? ((const __attribute__((address_space(3))) float*)SS)[DNO + SSTR * (4 * g + r) + kt * 16 + c]
+                                                     : dsn[si]) : 0.f;
                     // dc = sum dS S_prev.  The softmax part P (dP - delta) sums to 0 over a row, so
                     // its S_prev is taken relative to the row's P-weighted mean rp (exact in real
                     // arithmetic): where c <= -1 puts the row's weight on masked keys, S_prev there is
@@ -1061,7 +1086,7 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(bwd_sho
             if (qt > 0) u.store_dq_rows(dqo_prev, qt - 1, dq_prev);   // after the wait: stores stay in flight
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // S read before it is refilled
             if (qt + 1 < nqt) u.stage(qt + 1, S);
-            dq_prev = u.tile(in, qt, Tr[wave]);
+            dq_prev = u.tile(in, qt, Tr[wave], S);
 #pragma unroll
             for (int r = 0; r < 4; ++r) dqo_prev[r] = in.dqo[r];
         }
