@@ -665,7 +665,7 @@ MEP_DEV void wave_lds_sync() {
 // and dk is dv (MEP_ATTN_KV: one register set for the K / V rows and ONE accumulator per key tile
 // for dK + dV, with Q pre-scaled by the exact 1/sqrt(hd) = 1/4 -- about 32 registers fewer).
 #ifndef MEP_BWD_SSTAGE
-#define MEP_BWD_SSTAGE 1   // short backward, LDS-DMA path: bit 0 stages S_prev (rfstate layer-1 launch 433 -> ~345 us), bit 1 dS_next (its addressing spills the fp32 DSN kernel: 6 -> 22 registers, slower)
+#define MEP_BWD_SSTAGE 3   // short backward, LDS-DMA path: bit 0 stages S_prev (rfstate layer-1 launch 433 -> ~345 us), bit 1 dS_next (with the DSN kernel at 2 waves per SIMD: at 3 its addressing spilled 22 registers and ran slower; 2 waves: ~10 us faster than unstaged)
 #endif
 constexpr bool SST_P = MEP_BWD_SSTAGE & 1, SST_D = (MEP_BWD_SSTAGE >> 1) & 1;
 template <bool PREV, bool DSN, bool BF, bool KV = false>
@@ -779,10 +779,13 @@ struct Bwd {
     // wave-instruction per query row (lane = key), rows SSTR floats apart (4 SSTR = 16 mod 32: the
     // score reads of lane groups g and g + 1 fall in different banks), read per score from LDS
     // instead of a dependent global load inside the tile's math (keys past Tk and rows past Tq fall
-    // outside the range: whatever finite value the slot holds meets P = 0 there)
+    // outside the range: whatever finite value the slot holds meets P = 0 there).  Two regions per
+    // operand by tile parity: tile() reads tile qt's rows while tile qt + 1's are being staged.
+    // dS_next is staged only without PREV (both would take the workgroup past half the LDS)
+    static constexpr bool STP = PREV && SST_P, STD = DSN && SST_D && !PREV;
     static constexpr int SSTR = 68, SOPS = 16 * SSTR;
-    static constexpr int SPO = 4 * 256 + 48, DNO = SPO + (PREV && SST_P ? SOPS : 0);
-    static constexpr int STG = DNO + (DSN && SST_D ? SOPS : 0);   // floats: Q, dO, O, dQ [16][16], stats [16][2], PREV's rp [16], S_prev, dS_next
+    static constexpr int SPO = 4 * 256 + 48, DNO = SPO + (STP ? 2 * SOPS : 0);
+    static constexpr int STG = DNO + (STD ? 2 * SOPS : 0);   // floats: Q, dO, O, dQ [16][16], stats [16][2], PREV's rp [16], S_prev, dS_next
     MEP_DEV static bool dma_view(const mep_rows& v) {   // 16-byte aligned pieces of every row
         return BF ? ((v.ptr & 15) == 0 && v.sB % 8 == 0 && v.sT % 8 == 0) : aligned16(v);
     }
@@ -791,14 +794,14 @@ struct Bwd {
     }
     MEP_DEV void stage(int qt, float* S) const {
         typedef __attribute__((address_space(3))) void lvoid;
-        if ((PREV && SST_P) || (DSN && SST_D)) {
-            const int oor = 4 * Tq * Tk;
+        if (STP || STD) {
+            const int oor = 4 * Tq * Tk, par = (qt & 1) * SOPS;
 #pragma unroll
             for (int j = 0; j < 16; ++j) {
                 const int q = qt * 16 + j;
                 const int off = (lane < Tk && q < Tq) ? 4 * (q * Tk + lane) : oor;
-                if (PREV && SST_P) __builtin_amdgcn_raw_ptr_buffer_load_lds(rsSp, (lvoid*)(S + SPO + SSTR * j), 4, off, 0, 0, 0);
-                if (DSN && SST_D) __builtin_amdgcn_raw_ptr_buffer_load_lds(rsDn, (lvoid*)(S + DNO + SSTR * j), 4, off, 0, 0, 0);
+                if (STP) __builtin_amdgcn_raw_ptr_buffer_load_lds(rsSp, (lvoid*)(S + SPO + par + SSTR * j), 4, off, 0, 0, 0);
+                if (STD) __builtin_amdgcn_raw_ptr_buffer_load_lds(rsDn, (lvoid*)(S + DNO + par + SSTR * j), 4, off, 0, 0, 0);
             }
         }
         if (BF) {
@@ -947,7 +950,7 @@ struct Bwd {
                 int si = 0;
                 if (PREV || DSN) {
                     si = (sbase + min(qq, Tq - 1)) * Tk + min(kk, Tk - 1);
-                    if (PREV) spv = SST_P && SS ? ((const __attribute__((address_space(3))) float*)SS)[SPO + SSTR * (4 * g + r) + kt * 16 + c] : sprev[si];
+                    if (PREV) spv = STP && SS ? ((const __attribute__((address_space(3))) float*)SS)[SPO + (qt & 1) * SOPS + SSTR * (4 * g + r) + kt * 16 + c] : sprev[si];
                 }
                 float pv;
                 if constexpr (PREV) {
@@ -965,7 +968,7 @@ struct Bwd {
                 float gsv = pv * dp[r];
                 if (DSN || PREV) {
                     const bool ok = (qq < Tq) && (kk < Tk);
-                    const float gn = DSN && ok ? (SST_D && SS ? ((const __attribute__((address_space(3))) float*)SS)[DNO + SSTR * (4 * g + r) + kt * 16 + c]
+                    const float gn = DSN && ok ? (STD && SS ? ((const __attribute__((address_space(3))) float*)SS)[DNO + (qt & 1) * SOPS + SSTR * (4 * g + r) + kt * 16 + c]
                                                      : dsn[si]) : 0.f;
                     // dc = sum dS S_prev.  The softmax part P (dP - delta) sums to 0 over a row, so
                     // its S_prev is taken relative to the row's P-weighted mean rp (exact in real
@@ -1047,7 +1050,7 @@ struct Bwd {
 // waves per SIMD of the short backward by register need (scripts/resusage.py, fp32 path; the bf16
 // instances need fewer): KV frees the V rows and the dV accumulators
 template <bool PREV, bool DSN, bool KV>
-constexpr int bwd_short_waves() { return PREV ? 2 : (KV && !DSN) ? MEP_BWD_WAVES_KV : MEP_BWD_WAVES; }
+constexpr int bwd_short_waves() { return PREV || (DSN && SST_D) ? 2 : (KV && !DSN) ? MEP_BWD_WAVES_KV : MEP_BWD_WAVES; }
 
 
 template <bool PREV, bool DSN, bool BF, bool KV>
