@@ -291,6 +291,9 @@ MEP_DEV BRowT<HS> brow(const mep_rows& v, int b, int n, int D) {
 }
 
 // ================================================================== forward
+#ifndef MEP_FWD_SOUT2
+#define MEP_FWD_SOUT2 1   // single-chunk forward: score rows out / S_prev in as 8-byte pairs (Tk even)
+#endif
 // One forward task: batch row b, head h, 64 queries.  PREV: residual scores in; SOUT: post-mask
 // scores out; SINGLE: Tk <= 64 (one key chunk: exact two-pass softmax, each query tile is
 // finalised right after its P.V, so no running O/max/sum state stays live).  BF: the bf16 path
@@ -306,6 +309,12 @@ MEP_DEV void attn_fwd_task(const mep_attn_desc& d, int qc, int h, int b, int lan
     const float cres = PREV ? *G<const float>(d.c) : 0.f;
     const gfloat* sprev = G<const float>(d.s_prev);
     gfloat* sout = G<float>(d.s_out);
+    // SOUT with Tk even and an 8-byte aligned score tensor: every row starts 8-byte aligned, so the
+    // lane's 4 keys go out as two 8-byte stores (not four scattered 4-byte ones)
+    const bool sout2 = MEP_FWD_SOUT2 && SOUT && (Tk % 2 == 0) && ((d.s_out & 7) == 0);
+    // PREV likewise: the lane's 4 S_prev values of a key tile as two 8-byte loads (keys past Tk read
+    // the row's last pair, finite; their scores are -inf either way)
+    const bool sprev2 = MEP_FWD_SOUT2 && PREV && (Tk % 2 == 0) && ((d.s_prev & 7) == 0);
     const gfloat* mask = G<const float>(d.mask) + (int64_t)b * d.mask_sB;
     const uint64_t mrow = d.mask + 4ull * (uint64_t)((int64_t)b * d.mask_sB);
     const auto rsMask = uniform_rsrc(mrow, 4 * (int64_t)Tk);
@@ -509,16 +518,22 @@ MEP_DEV void attn_fwd_task(const mep_attn_desc& d, int qc, int h, int b, int lan
                                 : zero4();                                 // C[key 4g+r][query c]
 #pragma unroll
                 for (int hb = 0; hb < NHB; ++hb) st = dot_score<true, BF>(ks[kt][hb], qs[hb], st);
+                f32x2 spa = f32x2{0.f, 0.f}, spb = spa;
+                if (PREV && sprev2) {
+                    const int k2 = k_lo + kt * 16 + 4 * g;
+                    spa = *reinterpret_cast<const MEP_G f32x2*>(sprev + srow + min(k2, Tk - 2));
+                    spb = *reinterpret_cast<const MEP_G f32x2*>(sprev + srow + min(k2 + 2, Tk - 2));
+                }
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     float spv = 0.f;
                     const int kk = k_lo + kt * 16 + 4 * g + r;
                     if (PREV || SOUT) {
                         const int si = srow + min(kk, Tk - 1);
-                        if (PREV) spv = sprev[si];
+                        if (PREV) spv = sprev2 ? (r < 2 ? spa[r] : spb[r - 2]) : sprev[si];
                         const float v = score<PREV, HDIM>(st[r], cres, spv, mt[kt][r]);
                         if (PREV) spm = v > mx ? spv : spm;   // mx below: the running max before v
-                        if (SOUT && kk < Tk && q < Tq) sout[si] = v;
+                        if (SOUT && !sout2 && kk < Tk && q < Tq) sout[si] = v;
                         sv[kt][r] = v;
                     } else if (MI) {
                         sv[kt][r] = st[r];                                 // 4 x the score (dot - 4 mask)
@@ -526,6 +541,13 @@ MEP_DEV void attn_fwd_task(const mep_attn_desc& d, int qc, int h, int b, int lan
                         sv[kt][r] = score<false, HDIM>(st[r], 0.f, 0.f, mt[kt][r]);
                     }
                     mx = fmaxf(mx, sv[kt][r]);
+                }
+                if (SOUT && sout2) {   // keys 4g .. 4g + 3 of the row as two 8-byte stores (Tk even: a pair is whole or past Tk)
+                    const int k2 = k_lo + kt * 16 + 4 * g;
+                    if (q < Tq) {
+                        if (k2 < Tk) *reinterpret_cast<MEP_G f32x2*>(sout + srow + k2) = f32x2{sv[kt][0], sv[kt][1]};
+                        if (k2 + 2 < Tk) *reinterpret_cast<MEP_G f32x2*>(sout + srow + k2 + 2) = f32x2{sv[kt][2], sv[kt][3]};
+                    }
                 }
             }
             if (PREV) {
