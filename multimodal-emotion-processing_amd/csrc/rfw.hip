@@ -670,7 +670,8 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(WPE))) v
 // buffers by LDS-DMA while it multiplies the previous product from the other -- a fragment leaves
 // L2 once per 8 tiles.  Per step: barrier -> the previous step's stores -> the next product's DMA
 // and the rows this step's epilogue needs -> MFMAs from LDS -> epilogue -> vmcnt(0) + barrier; the
-// rows the next job's first product multiplies are loaded one step ahead.  The products are
+// forward loads the next job's x rows one step ahead (the backward its first rows at the job's
+// start: held across a step they cost more registers than the wait).  The products are
 // k_rfw_*<..., NW = 2>'s in the same order per accumulator, and every epilogue the same
 // arithmetic: results bit-identical to those kernels (test_gpu_rfw.py).
 #ifndef MEP_RFS_FWD_W
@@ -987,7 +988,7 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(W / 4, W
         const int len[2] = {D, D};
         pr.load(src, len);
     };
-    // the job's first product (Wq_in: dqp_in Wq, else W2^T) staged, and its rows loaded a step ahead:
+    // the job's first product (Wq_in: dqp_in Wq, else W2^T) staged a step ahead, and its rows (MEP_RFS_BWD_PRE: a step ahead too):
     // dout, h, f, the stats and (Wq_in) dqp_in
     f32x4 gu[NI], hv[NI], fv[NI], dv[NI], st;
     auto stage_first = [&](const mep_rf_epi_bwd_desc& b, lbyte_t* buf) {
