@@ -581,13 +581,13 @@ def tgemm_ok(items):
     return tgemm_mode(items) is not None
 
 
-def gemm(name, descs, max_tiles, stream=None, prec=0):
+def gemm(name, descs, max_tiles, stream=None, prec=0, tgemm=True):
     """A token-GEMM launch (mep_gemm_desc array): the tiled split-bf16 kernel (mep_tgemm) when
-    the descriptors allow it, else the named launcher (mep_unify / mep_gemm).  prec: MEP_PREC_BF16
-    for the bf16 path (mep_unify reads the per-descriptor bf16 field instead)."""
+    the descriptors allow it (and tgemm), else the named launcher (mep_unify / mep_gemm).  prec:
+    MEP_PREC_BF16 for the bf16 path (mep_unify reads the per-descriptor bf16 field instead)."""
     if descs.n == 0:
         return
-    mode = tgemm_mode(descs.items)
+    mode = tgemm_mode(descs.items) if tgemm else None
     if mode is not None:
         flags = (prec & PREC_BF16) | (0 if descs.items[0].w_nt else TGEMM_WT)
         if any(d.bf16 for d in descs.items):
@@ -600,6 +600,6 @@ def gemm(name, descs, max_tiles, stream=None, prec=0):
     launch(name, descs, max_tiles, stream)
 
 
-def gemm_launcher(name, descs):
+def gemm_launcher(name, descs, tgemm=True):
     """Launch name a gemm() call is timed under (bench.py / roofline.py)."""
-    return 'mep_tgemm' if tgemm_ok(descs.items) else name
+    return 'mep_tgemm' if tgemm and tgemm_ok(descs.items) else name

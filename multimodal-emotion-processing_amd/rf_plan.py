@@ -596,7 +596,9 @@ class RealformerPlan:
         self._dq_clean = self.rfw
         if sp.head:
             launch('mep_pool_fwd', self.d_pool, self.t_pool, stream)
-            _lib.gemm('mep_gemm', self.d_fc, self.t_fc, stream)
+            # the head's fully_connected (B x P rows, K = 2C = 576): on mep_tgemm's 128-row workgroups
+            # it is 3 workgroups walking 18 K chunks (45 us at State_Transfer); mep_gemm spreads it
+            _lib.gemm('mep_gemm', self.d_fc, self.t_fc, stream, tgemm=False)
             self.head.compute_grad = int(grad)
             self.head.ext_dout = 0
             _lib.call('mep_rf_head', ctypes.byref(self.head), stream=stream)
