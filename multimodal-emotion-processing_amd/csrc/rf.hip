@@ -369,13 +369,27 @@ __global__ __launch_bounds__(64) void k_rf_head(mep_rf_head_desc d) {
     const bool c0 = lane < D, c1 = lane + 64 < D;
     const float w0 = c0 ? lnw[lane] : 0.f, w1 = c1 ? lnw[lane + 64] : 0.f;
     const float b0 = c0 ? lnb[lane] : 0.f, b1 = c1 ? lnb[lane + 64] : 0.f;
+    // the classifier rows (12 x D) in registers for both directions, and each utterance's fc row
+    // loaded one utterance ahead: the recurrence is one wave per batch row, so every load the loop
+    // waited on was a dependent L2 round trip (72 per direction at P = 6)
+    float wc0[2 * RF_NC], wc1[2 * RF_NC];
+#pragma unroll
+    for (int j = 0; j < 2 * RF_NC; ++j) {
+        wc0[j] = c0 ? wc[j * D + lane] : 0.f;
+        wc1[j] = c1 ? wc[j * D + lane + 64] : 0.f;
+    }
     float loss = 0.f;
+    float nx0 = c0 ? fc[(int64_t)(b * P) * D + lane] : 0.f, nx1 = c1 ? fc[(int64_t)(b * P) * D + lane + 64] : 0.f;
 
     for (int i = 0; i < P; ++i) {
         const int r = b * P + i;
-        const gfloat* fr = fc + (int64_t)r * D;
         // h = relu(LN(fc))   (realformer.py:263)
-        const float x0 = c0 ? fr[lane] : 0.f, x1 = c1 ? fr[lane + 64] : 0.f;
+        const float x0 = nx0, x1 = nx1;
+        if (i + 1 < P) {
+            const gfloat* fn = fc + (int64_t)(r + 1) * D;
+            nx0 = c0 ? fn[lane] : 0.f;
+            nx1 = c1 ? fn[lane + 64] : 0.f;
+        }
         const float mean = wave_sum(x0 + x1) / (float)D;
         const float d0 = c0 ? x0 - mean : 0.f, d1 = c1 ? x1 - mean : 0.f;
         const float rstd = 1.0f / sqrtf(wave_sum(d0 * d0 + d1 * d1) / (float)D + LN_EPS);
@@ -388,8 +402,7 @@ __global__ __launch_bounds__(64) void k_rf_head(mep_rf_head_desc d) {
         float z[2 * RF_NC];
 #pragma unroll
         for (int j = 0; j < 2 * RF_NC; ++j) {
-            const gfloat* wr = wc + j * D;
-            float s = (c0 ? wr[lane] * h0 : 0.f) + (c1 ? wr[lane + 64] * h1 : 0.f);
+            float s = (c0 ? wc0[j] * h0 : 0.f) + (c1 ? wc1[j] * h1 : 0.f);
             z[j] = wave_sum(s) + bc[j];
         }
         // gate (realformer.py:278-281), lanes 0..5 own one class each
@@ -471,9 +484,8 @@ __global__ __launch_bounds__(64) void k_rf_head(mep_rf_head_desc d) {
 #pragma unroll
         for (int j = 0; j < 2 * RF_NC; ++j) {
             const float dz = s_d12[j];
-            const gfloat* wr = wc + j * D;
-            if (c0) dh0 = fmaf(dz, wr[lane], dh0);
-            if (c1) dh1 = fmaf(dz, wr[lane + 64], dh1);
+            if (c0) dh0 = fmaf(dz, wc0[j], dh0);
+            if (c1) dh1 = fmaf(dz, wc1[j], dh1);
         }
         const float g0 = (c0 && s_h[i][lane] > 0.f) ? dh0 : 0.f;
         const float g1 = (c1 && s_h[i][lane + 64] > 0.f) ? dh1 : 0.f;
